@@ -1,0 +1,1260 @@
+// tas_oracle.cpp — CPU restatement of Kueue's TAS evaluation path.
+//
+// TEST INFRASTRUCTURE ONLY.  This file is the parity oracle (the checker) and
+// the CPU baseline ("port") for bench.py.  Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may load it.  The product path
+// (kueue_oss_amd/, libkueue_tas.so) never links, loads or calls it.
+//
+// It restates, line by line and with the reference's own data structures
+// (pointer tree, string-keyed ordered maps), the Go code of
+//   /root/reference/pkg/cache/scheduler/tas_flavor_snapshot.go   (TASFlavorSnapshot)
+//   /root/reference/pkg/cache/scheduler/tas_flavor.go            (snapshot construction)
+//   /root/reference/pkg/cache/scheduler/tas_nodes_cache.go       (node filtering)
+//   /root/reference/pkg/cache/scheduler/tas_non_tas_pod_cache.go (non-TAS usage)
+//   /root/reference/pkg/resources/requests.go                    (CountIn arithmetic)
+//   /root/reference/vendor/k8s.io/api/core/v1/toleration.go, taint.go
+//   /root/reference/vendor/k8s.io/component-helpers/scheduling/corev1/helpers.go
+// Each function cites the reference file:line it follows.
+//
+// Parity pinning: tests/test_oracle_goldens.py checks this oracle against every
+// in-scope golden case transcribed from the reference's own table test
+// (pkg/cache/scheduler/tas_cache_test.go TestFindTopologyAssignments) by
+// tools/extract_goldens.py.  The Go reference itself cannot run here (no Go
+// toolchain).
+//
+// Deterministic choices where Go is not deterministic:
+//   * CountInWithLimitingResource with >=2 missing requested keys returns the
+//     first missing key in Go map order (random); we return the smallest name.
+//   * Requests maps iterate in sorted key order (std::map).
+// Out of scope (returns an error reason "unsupported: ..."):
+//   TASBalancedPlacement, elastic workloads, node replacement, node affinity,
+//   nodeSelector validation errors.
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mini_json.h"
+
+namespace oracle {
+
+using Requests = std::map<std::string, int64_t>;
+static const char* kHostname = "kubernetes.io/hostname";
+
+// ---- Go integer semantics -------------------------------------------------
+static inline int32_t w_add(int32_t a, int32_t b) { return int32_t(uint32_t(a) + uint32_t(b)); }
+static inline int32_t w_sub(int32_t a, int32_t b) { return int32_t(uint32_t(a) - uint32_t(b)); }
+static inline int32_t w_mul(int32_t a, int32_t b) { return int32_t(uint32_t(a) * uint32_t(b)); }
+static inline int64_t w_add64(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
+static inline int64_t w_sub64(int64_t a, int64_t b) { return int64_t(uint64_t(a) - uint64_t(b)); }
+static inline int64_t w_mul64(int64_t a, int64_t b) { return int64_t(uint64_t(a) * uint64_t(b)); }
+struct GoPanic : std::runtime_error { using std::runtime_error::runtime_error; };
+static inline int32_t go_div32(int32_t a, int32_t b) {
+  if (b == 0) throw GoPanic("integer divide by zero");
+  if (a == INT32_MIN && b == -1) return INT32_MIN;
+  return a / b;
+}
+static inline int64_t go_div64(int64_t a, int64_t b) {
+  if (b == 0) throw GoPanic("integer divide by zero");
+  if (a == INT64_MIN && b == -1) return INT64_MIN;
+  return a / b;
+}
+
+// resources.Requests.Add / Sub (requests.go:84-94): keys of the operand are
+// created in the receiver.
+static void req_add(Requests& r, const Requests& o) { for (auto& kv : o) r[kv.first] = w_add64(r[kv.first], kv.second); }
+static void req_sub(Requests& r, const Requests& o) { for (auto& kv : o) r[kv.first] = w_sub64(r[kv.first], kv.second); }
+static Requests req_scaled_up(const Requests& r, int64_t f) {  // requests.go:53-57, :78-82
+  Requests out = r;
+  for (auto& kv : out) kv.second = w_mul64(kv.second, f);
+  return out;
+}
+
+// Requests.CountInWithLimitingResource (requests.go:183-217).
+static std::pair<int32_t, std::string> count_in_with_limiting(const Requests& r, const Requests& cap) {
+  bool has = false;
+  int32_t result = 0;
+  std::string lim;
+  for (auto& kv : r) {
+    const std::string& name = kv.first;
+    int64_t rv = kv.second;
+    auto it = cap.find(name);
+    if (it == cap.end() && rv != 0) return {0, name};
+    int64_t capv = it == cap.end() ? 0 : it->second;
+    int32_t count;
+    if (rv == 0) {
+      count = INT32_MAX;
+    } else {
+      int64_t q = go_div64(capv, rv);
+      count = std::max(int32_t(uint32_t(uint64_t(q))), int32_t(0));
+    }
+    if (!has || count < result || (count == result && name < lim)) {
+      result = count;
+      lim = name;
+      has = true;
+    }
+  }
+  return {has ? result : 0, lim};
+}
+static int32_t count_in(const Requests& r, const Requests& cap) { return count_in_with_limiting(r, cap).first; }
+
+// ---- k8s core types (subset) ----------------------------------------------
+struct Taint { std::string key, value, effect; };
+struct Toleration { std::string key, op, value, effect; };
+
+// Taint.ToString (vendor/k8s.io/api/core/v1/taint.go:28-39)
+static std::string taint_to_string(const Taint& t) {
+  if (t.effect.empty()) {
+    if (t.value.empty()) return t.key;
+    return t.key + "=" + t.value + ":";
+  }
+  if (t.value.empty()) return t.key + ":" + t.effect;
+  return t.key + "=" + t.value + ":" + t.effect;
+}
+
+// content.IsDecimalInteger + strconv.ParseInt (validate/content/decimal_int.go:30-62)
+static bool parse_decimal_int(const std::string& v, int64_t* out) {
+  size_t n = v.size();
+  if (n == 0) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (v[0] == '-') {
+    if (n == 1) return false;
+    i = 1;
+    neg = true;
+  }
+  if (v[i] == '0') {
+    if (n == 1 && i == 0) { *out = 0; return true; }
+    return false;
+  }
+  if (v[i] < '1' || v[i] > '9') return false;
+  for (size_t j = i + 1; j < n; j++)
+    if (v[j] < '0' || v[j] > '9') return false;
+  // ParseInt range check
+  unsigned __int128 acc = 0;
+  for (size_t j = i; j < n; j++) {
+    acc = acc * 10 + unsigned(v[j] - '0');
+    if (acc > (unsigned __int128)INT64_MAX + 1) return false;
+  }
+  if (!neg && acc > (unsigned __int128)INT64_MAX) return false;
+  *out = neg ? int64_t(uint64_t(0) - uint64_t(acc)) : int64_t(acc);
+  return true;
+}
+
+// Toleration.ToleratesTaint (vendor/k8s.io/api/core/v1/toleration.go:52-112)
+static bool tolerates_taint(const Toleration& t, const Taint& taint, bool enable_cmp) {
+  if (!t.effect.empty() && t.effect != taint.effect) return false;
+  if (!t.key.empty() && t.key != taint.key) return false;
+  if (t.op.empty() || t.op == "Equal") return t.value == taint.value;
+  if (t.op == "Exists") return true;
+  if (t.op == "Lt" || t.op == "Gt") {
+    if (!enable_cmp) return false;
+    int64_t tv, nv;
+    if (!parse_decimal_int(t.value, &tv)) return false;
+    if (!parse_decimal_int(taint.value, &nv)) return false;
+    return t.op == "Lt" ? nv < tv : nv > tv;
+  }
+  return false;
+}
+
+// corev1helpers.FindMatchingUntoleratedTaint with the NoSchedule/NoExecute filter
+// (component-helpers/scheduling/corev1/helpers.go:79-102; tas_flavor_snapshot.go:1584-1586)
+static const Taint* find_untolerated(const std::vector<Taint>& taints, const std::vector<Toleration>& tols) {
+  for (auto& taint : taints) {
+    if (!(taint.effect == "NoSchedule" || taint.effect == "NoExecute")) continue;
+    bool tolerated = false;
+    for (auto& tol : tols)
+      if (tolerates_taint(tol, taint, true)) { tolerated = true; break; }
+    if (!tolerated) return &taint;
+  }
+  return nullptr;
+}
+
+struct NodeInfo {  // tas_flavor.go:173-190
+  std::string name;
+  std::map<std::string, std::string> labels;
+  std::vector<Taint> taints;
+  Requests allocatable;
+};
+
+// ---- API types --------------------------------------------------------------
+struct SliceConstraint { std::string topology; int32_t size; };
+struct TopologyRequest {  // apis/kueue/v1beta2/workload_types.go:165-249
+  std::optional<std::string> required, preferred, sliceRequiredTopology;
+  std::optional<bool> unconstrained;
+  std::optional<int32_t> sliceSize;
+  std::vector<SliceConstraint> constraints;
+};
+struct PodSetRequest {  // TASPodSetRequests (tas_flavor_snapshot.go:356-367)
+  std::string name;
+  std::optional<TopologyRequest> topologyRequest;
+  Requests singlePodRequests;
+  int32_t count = 0;
+  bool implied = false;
+  std::optional<std::string> podSetGroupName;
+  std::vector<Toleration> tolerations;
+  std::optional<std::map<std::string, std::string>> nodeSelector;
+};
+struct DomainAssignment { std::vector<std::string> values; int32_t count; };
+struct TopologyAssignment { std::vector<std::string> levels; std::vector<DomainAssignment> domains; };
+struct PodSetResult { std::string name; std::optional<TopologyAssignment> assignment; std::string reason; };
+
+struct Gates {  // pkg/features/kube_features.go:445-448 (TASProfileMixed Beta, default on)
+  bool profileMixed = true;
+  bool multiLayer = false;
+  bool balanced = false;
+  bool elastic = false;
+};
+
+// ---- snapshot ---------------------------------------------------------------
+struct Domain {  // tas_flavor_snapshot.go:51-104 (domain + leafDomain)
+  std::string id;
+  Domain* parent = nullptr;
+  std::vector<Domain*> children;
+  int32_t state = 0, sliceState = 0, stateWithLeader = 0, sliceStateWithLeader = 0, leaderState = 0;
+  std::vector<std::string> levelValues;
+  bool isLeaf = false;
+  Requests freeCapacity;
+  Requests tasUsage;
+  const NodeInfo* node = nullptr;
+};
+
+struct ExclusionStats {  // tas_flavor_snapshot.go:423-499
+  std::map<std::string, int> taints;
+  int nodeSelector = 0, affinity = 0, topologyDomain = 0;
+  std::map<std::string, int> resources;
+  int totalNodes = 0;
+  bool has_exclusions() const {
+    return nodeSelector > 0 || affinity > 0 || topologyDomain > 0 || !taints.empty() || !resources.empty();
+  }
+  std::string format_reasons() const;
+};
+
+// Go %q for the ASCII strings that occur here (strconv.Quote).
+static std::string go_quote(const std::string& s) {
+  std::string out = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') { out += '\\'; out += char(c); }
+    else if (c == '\n') out += "\\n";
+    else if (c == '\t') out += "\\t";
+    else if (c == '\r') out += "\\r";
+    else if (c < 0x20 || c == 0x7f) { char b[8]; snprintf(b, sizeof b, "\\x%02x", c); out += b; }
+    else out += char(c);
+  }
+  return out + "\"";
+}
+
+std::string ExclusionStats::format_reasons() const {
+  std::vector<std::string> reasons;
+  if (nodeSelector > 0) reasons.push_back("nodeSelector: " + std::to_string(nodeSelector));
+  if (affinity > 0) reasons.push_back("affinity: " + std::to_string(affinity));
+  if (topologyDomain > 0) reasons.push_back("topologyDomain: " + std::to_string(topologyDomain));
+  for (auto& kv : taints) reasons.push_back("taint " + go_quote(kv.first) + ": " + std::to_string(kv.second));
+  for (auto& kv : resources) reasons.push_back("resource " + go_quote(kv.first) + ": " + std::to_string(kv.second));
+  std::sort(reasons.begin(), reasons.end());
+  std::string out;
+  for (size_t i = 0; i < reasons.size(); i++) {
+    if (i) out += ", ";
+    out += reasons[i];
+  }
+  return out;
+}
+
+struct Params {  // topologyAssignmentParameters + state (tas_flavor_snapshot.go:447-464)
+  std::map<int, int32_t> sliceSizeAtLevel;
+  int32_t sliceSize = 1, count = 0, leaderCount = 0;
+  int requestedLevelIdx = 0, sliceLevelIdx = 0;
+  bool required = false, unconstrained = false;
+  std::vector<SliceConstraint> multiLayerConstraints;
+  ExclusionStats stats;
+};
+
+struct Requirements {  // topologyAssignmentPodRequirements :434-443
+  Requests requests;
+  std::optional<Requests> leaderRequests;
+  std::map<std::string, Requests>* assumedUsage = nullptr;
+  std::vector<Toleration> tolerations;
+  std::map<std::string, std::string> selector;  // empty = Everything
+  bool simulateEmpty = false;
+};
+
+static std::string domain_id(const std::vector<std::string>& v) {  // util/tas/tas.go:29-31
+  std::string out;
+  for (size_t i = 0; i < v.size(); i++) {
+    if (i) out += ",";
+    out += v[i];
+  }
+  return out;
+}
+
+static int compare_values(const std::vector<std::string>& a, const std::vector<std::string>& b) {  // slices.Compare
+  size_t n = std::min(a.size(), b.size());
+  for (size_t i = 0; i < n; i++) {
+    int c = a[i].compare(b[i]);
+    if (c != 0) return c < 0 ? -1 : 1;
+  }
+  if (a.size() == b.size()) return 0;
+  return a.size() < b.size() ? -1 : 1;
+}
+static inline int cmp32(int32_t a, int32_t b) { return a < b ? -1 : (a > b ? 1 : 0); }
+
+class Snapshot {
+ public:
+  std::string topologyName = "default";
+  std::vector<std::string> levelKeys;
+  std::map<std::string, Domain*> leaves, roots, domains;
+  std::vector<std::map<std::string, Domain*>> domainsPerLevel;
+  std::vector<Toleration> tolerations;
+  bool isLowestLevelNode = false;
+  Gates gates;
+  std::deque<Domain> storage;
+  std::deque<NodeInfo> nodes;
+
+  Snapshot(const std::vector<std::string>& levels, const std::vector<Toleration>& tols) {  // :139-158
+    levelKeys = levels;
+    tolerations = tols;
+    domainsPerLevel.resize(levels.size());
+    isLowestLevelNode = !levels.empty() && levels.back() == kHostname;
+  }
+
+  static std::vector<std::string> level_values(const std::vector<std::string>& keys,
+                                               const std::map<std::string, std::string>& labels) {
+    std::vector<std::string> out;  // util/tas/tas.go:66-72
+    for (auto& k : keys) {
+      auto it = labels.find(k);
+      out.push_back(it == labels.end() ? "" : it->second);
+    }
+    return out;
+  }
+
+  std::string add_node(const NodeInfo* node) {  // :160-195
+    std::vector<std::string> levelValues;
+    std::string id;
+    bool found;
+    if (isLowestLevelNode) {
+      auto it = node->labels.find(kHostname);
+      id = it == node->labels.end() ? "" : it->second;
+      found = leaves.count(id) > 0;
+      if (!found) levelValues = level_values(levelKeys, node->labels);
+    } else {
+      levelValues = level_values(levelKeys, node->labels);
+      id = domain_id(levelValues);
+      found = leaves.count(id) > 0;
+    }
+    if (!found) {
+      storage.emplace_back();
+      Domain* d = &storage.back();
+      d->id = id;
+      d->levelValues = levelValues;
+      d->isLeaf = true;
+      if (isLowestLevelNode) d->node = node;
+      leaves[id] = d;
+    }
+    req_add(leaves[id]->freeCapacity, node->allocatable);  // addCapacity :243-248
+    return id;
+  }
+
+  void initialize() {  // :210-217
+    for (auto& kv : leaves) {
+      Domain* d = kv.second;
+      domains[d->id] = d;
+      domainsPerLevel[d->levelValues.size() - 1][d->id] = d;
+      initialize_helper(d);
+    }
+  }
+  void initialize_helper(Domain* dom) {  // :220-241
+    if (dom->levelValues.size() == 1) {
+      roots[dom->id] = dom;
+      return;
+    }
+    std::vector<std::string> parentValues(dom->levelValues.begin(), dom->levelValues.end() - 1);
+    std::string parentID = domain_id(parentValues);
+    Domain* parent;
+    auto it = domains.find(parentID);
+    if (it == domains.end()) {
+      storage.emplace_back();
+      parent = &storage.back();
+      parent->id = parentID;
+      parent->levelValues = parentValues;
+      domainsPerLevel[parentValues.size() - 1][parentID] = parent;
+      domains[parentID] = parent;
+      initialize_helper(parent);
+    } else {
+      parent = it->second;
+    }
+    dom->parent = parent;
+    parent->children.push_back(dom);
+  }
+  void add_non_tas_usage(const std::string& id, const Requests& usage) { req_sub(leaves[id]->freeCapacity, usage); }  // :250-255
+  void add_tas_usage(const std::string& id, const Requests& usage) {  // :267-279
+    auto it = leaves.find(id);
+    if (it == leaves.end()) return;
+    req_add(it->second->tasUsage, usage);
+  }
+  void update_tas_usage(const std::string& id, const Requests& usage, bool add, int32_t count) {  // :257-265
+    Requests u = usage;
+    req_add(u, Requests{{"pods", int64_t(count)}});
+    auto it = leaves.find(id);
+    if (it == leaves.end()) return;
+    if (add) req_add(it->second->tasUsage, u);
+    else req_sub(it->second->tasUsage, u);
+  }
+
+  std::string lowest_level() const { return levelKeys.back(); }
+  std::string highest_level() const { return levelKeys.front(); }
+  bool use_lfc(bool unconstrained) const { return unconstrained && gates.profileMixed; }  // :1328-1331
+  bool use_bf(bool unconstrained) const { return !use_lfc(unconstrained); }               // :1323-1326
+
+  int resolve_level_idx(const std::string& key) const {  // :1104-1110
+    for (size_t i = 0; i < levelKeys.size(); i++)
+      if (levelKeys[i] == key) return int(i);
+    return -1;
+  }
+  static bool is_slice_topology_only(const std::optional<TopologyRequest>& tr) {  // :1148-1153
+    if (!tr || tr->required || tr->preferred) return false;
+    return tr->sliceRequiredTopology.has_value() || !tr->constraints.empty();
+  }
+  std::optional<std::string> level_key(const std::optional<TopologyRequest>& tr) const {  // :1122-1138
+    if (!tr) return std::nullopt;
+    if (tr->required) return tr->required;
+    if (tr->preferred) return tr->preferred;
+    if (is_slice_topology_only(tr)) return highest_level();
+    if (tr->unconstrained.value_or(false)) return lowest_level();
+    return std::nullopt;
+  }
+  std::optional<std::string> level_key_with_implied_fallback(const PodSetRequest& r) const {  // :1112-1120
+    if (auto k = level_key(r.topologyRequest)) return k;
+    if (r.implied) return lowest_level();
+    return std::nullopt;
+  }
+  std::string slice_level_key_with_default(const std::optional<TopologyRequest>& tr, const std::string& def) const {  // :1092-1102
+    if (tr) {
+      if (tr->sliceRequiredTopology) return *tr->sliceRequiredTopology;
+      if (!tr->constraints.empty()) return tr->constraints[0].topology;
+    }
+    return def;
+  }
+  static std::pair<int32_t, std::string> slice_size_with_single_pod_default(const std::optional<TopologyRequest>& tr) {  // :1162-1180
+    if (!tr) return {1, ""};
+    if (!tr->constraints.empty()) return {tr->constraints[0].size, ""};
+    if (!tr->sliceRequiredTopology) return {1, ""};
+    if (!tr->sliceSize) return {0, "slice topology requested, but slice size not provided"};
+    return {*tr->sliceSize, ""};
+  }
+
+  std::string build_slice_size_at_level(const PodSetRequest& w, int32_t sliceSize, int sliceLevelIdx,
+                                        std::map<int, int32_t>& out) const {  // :1018-1063
+    out.clear();
+    if (!gates.multiLayer || !w.topologyRequest) return "";
+    int32_t prevSize = sliceSize;
+    int prevLevelIdx = sliceLevelIdx;
+    const auto& cs = w.topologyRequest->constraints;
+    for (size_t i = 1; i < cs.size(); i++) {
+      const auto& layer = cs[i];
+      int inner = resolve_level_idx(layer.topology);
+      if (inner < 0) return "no requested topology level for additional slice layer: " + layer.topology;
+      if (inner <= prevLevelIdx)
+        return "additional slice layer topology " + layer.topology + " must be at a lower level than " + levelKeys[prevLevelIdx];
+      if (layer.size == 0) throw GoPanic("integer divide by zero");
+      if (prevSize % layer.size != 0)
+        return "additional slice layer size " + std::to_string(layer.size) + " must evenly divide parent layer size " +
+               std::to_string(prevSize);
+      for (int lvl = prevLevelIdx + 1; lvl <= inner; lvl++) out[lvl] = layer.size;
+      prevSize = layer.size;
+      prevLevelIdx = inner;
+    }
+    return "";
+  }
+
+  // ---- phase 1 ----
+  void fill_in_counts(const Requirements& rq, Params& st) {  // :1568-1647
+    for (auto& kv : domains) {
+      Domain* d = kv.second;
+      d->state = d->stateWithLeader = d->sliceState = d->sliceStateWithLeader = d->leaderState = 0;
+    }
+    for (auto& kv : leaves) {
+      Domain* leaf = kv.second;
+      st.stats.totalNodes++;
+      if (isLowestLevelNode) {
+        const Taint* t = find_untolerated(leaf->node->taints, rq.tolerations);
+        if (t) {
+          st.stats.taints[taint_to_string(*t)]++;
+          continue;
+        }
+        bool match = true;
+        for (auto& sel : rq.selector) {
+          auto it = leaf->node->labels.find(sel.first);
+          if (it == leaf->node->labels.end() || it->second != sel.second) { match = false; break; }
+        }
+        if (!match) {
+          st.stats.nodeSelector++;
+          continue;
+        }
+        // affinity: not supported (see header)
+      }
+      // requiredReplacementDomain is always "" on this path (node replacement is out of scope)
+      Requests remaining = leaf->freeCapacity;
+      if (!rq.simulateEmpty) req_sub(remaining, leaf->tasUsage);
+      if (rq.assumedUsage) {
+        auto it = rq.assumedUsage->find(leaf->id);
+        if (it != rq.assumedUsage->end()) req_sub(remaining, it->second);
+      }
+      auto cl = count_in_with_limiting(rq.requests, remaining);
+      leaf->state = cl.first;
+      if (leaf->state == 0 && !cl.second.empty()) st.stats.resources[cl.second]++;
+      leaf->leaderState = 0;
+      if (rq.leaderRequests && count_in(*rq.leaderRequests, remaining) > 0) {
+        leaf->leaderState = 1;
+        req_sub(remaining, *rq.leaderRequests);
+      }
+      leaf->stateWithLeader = count_in(rq.requests, remaining);
+    }
+    for (auto& kv : roots) fill_in_counts_helper(kv.second, st.sliceSize, st.sliceLevelIdx, 0, st.sliceSizeAtLevel, st.leaderCount > 0);
+  }
+
+  void fill_in_counts_helper(Domain* d, int32_t sliceSize, int sliceLevelIdx, int level,
+                             const std::map<int, int32_t>& sizeAt, bool leaderRequired) {  // :1658-1719
+    if (d->children.empty()) {
+      if (level == sliceLevelIdx) {
+        d->sliceState = go_div32(d->state, sliceSize);
+        d->sliceStateWithLeader = go_div32(d->stateWithLeader, sliceSize);
+      }
+      return;
+    }
+    int32_t childrenCapacity = 0, sliceCapacity = 0;
+    bool hasContributor = false;
+    int32_t minDiff = INT32_MAX, minSliceDiff = INT32_MAX, leaderState = 0;
+    int childLevel = level + 1;
+    auto it = sizeAt.find(childLevel);
+    bool hasInner = it != sizeAt.end();
+    int32_t innerSize = hasInner ? it->second : 0;
+    for (Domain* c : d->children) {
+      fill_in_counts_helper(c, sliceSize, sliceLevelIdx, childLevel, sizeAt, leaderRequired);
+      int32_t cs = c->state, csw = c->stateWithLeader;
+      if (hasInner) {
+        cs = w_mul(go_div32(c->state, innerSize), innerSize);
+        csw = w_mul(go_div32(c->stateWithLeader, innerSize), innerSize);
+      }
+      childrenCapacity = w_add(childrenCapacity, cs);
+      sliceCapacity = w_add(sliceCapacity, c->sliceState);
+      if (!leaderRequired || c->leaderState > 0) {
+        hasContributor = true;
+        minDiff = std::min(w_sub(cs, csw), minDiff);
+        minSliceDiff = std::min(w_sub(c->sliceState, c->sliceStateWithLeader), minSliceDiff);
+      }
+      leaderState = std::max(c->leaderState, leaderState);
+    }
+    d->state = childrenCapacity;
+    int32_t sswl = 0;
+    if (hasContributor) {
+      d->stateWithLeader = w_sub(childrenCapacity, minDiff);
+      sswl = w_sub(sliceCapacity, minSliceDiff);
+    } else {
+      d->stateWithLeader = 0;
+    }
+    d->leaderState = leaderState;
+    if (level == sliceLevelIdx) {
+      sliceCapacity = go_div32(d->state, sliceSize);
+      sswl = go_div32(d->stateWithLeader, sliceSize);
+    }
+    d->sliceState = sliceCapacity;
+    d->sliceStateWithLeader = sswl;
+  }
+
+  // ---- phase 2 helpers ----
+  std::vector<Domain*> sorted_domains_with_leader(std::vector<Domain*> v, bool unconstrained) const {  // :1511-1535
+    bool lfc = use_lfc(unconstrained);
+    std::sort(v.begin(), v.end(), [&](Domain* a, Domain* b) {
+      int c;
+      if (a->leaderState != b->leaderState) c = cmp32(b->leaderState, a->leaderState);
+      else if (a->sliceStateWithLeader != b->sliceStateWithLeader)
+        c = lfc ? cmp32(a->sliceStateWithLeader, b->sliceStateWithLeader) : cmp32(b->sliceStateWithLeader, a->sliceStateWithLeader);
+      else if (a->stateWithLeader != b->stateWithLeader) c = cmp32(a->stateWithLeader, b->stateWithLeader);
+      else c = compare_values(a->levelValues, b->levelValues);
+      return c < 0;
+    });
+    return v;
+  }
+  std::vector<Domain*> sorted_domains(std::vector<Domain*> v, bool unconstrained) const {  // :1544-1564
+    bool lfc = use_lfc(unconstrained);
+    std::sort(v.begin(), v.end(), [&](Domain* a, Domain* b) {
+      int c;
+      if (a->sliceState != b->sliceState) c = lfc ? cmp32(a->sliceState, b->sliceState) : cmp32(b->sliceState, a->sliceState);
+      else if (a->state != b->state) c = cmp32(a->state, b->state);
+      else c = compare_values(a->levelValues, b->levelValues);
+      return c < 0;
+    });
+    return v;
+  }
+  template <typename F>
+  static Domain* find_best_fit_by(const std::vector<Domain*>& ds, size_t from, int32_t needed, F state) {  // :1216-1231
+    Domain* best = ds[from];
+    int32_t bestState = state(best);
+    for (size_t i = from; i < ds.size(); i++) {
+      int32_t s = state(ds[i]);
+      if (s >= needed && s < bestState) {
+        best = ds[i];
+        bestState = state(best);
+      }
+    }
+    return best;
+  }
+  static Domain* find_best_fit(const std::vector<Domain*>& ds, size_t from, int32_t count, int32_t leaderCount) {  // :1186-1196
+    if (leaderCount > 0) return find_best_fit_by(ds, from, count, [](Domain* d) { return d->stateWithLeader; });
+    return find_best_fit_by(ds, from, count, [](Domain* d) { return d->state; });
+  }
+  static Domain* find_best_fit_for_slices(const std::vector<Domain*>& ds, size_t from, int32_t n, int32_t leaderCount) {  // :1202-1212
+    if (leaderCount > 0) return find_best_fit_by(ds, from, n, [](Domain* d) { return d->sliceStateWithLeader; });
+    return find_best_fit_by(ds, from, n, [](Domain* d) { return d->sliceState; });
+  }
+
+  std::string not_fit_message(int32_t fit, int32_t total, int32_t sliceSize, const ExclusionStats& stats) const {  // :1721-1741
+    std::string unit = sliceSize == 1 ? "pod" : "slice";
+    std::string out;
+    if (fit == 0)
+      out = "topology " + go_quote(topologyName) + " doesn't allow to fit any of " + std::to_string(total) + " " + unit + "(s)";
+    else
+      out = "topology " + go_quote(topologyName) + " allows to fit only " + std::to_string(fit) + " out of " +
+            std::to_string(total) + " " + unit + "(s)";
+    if (stats.has_exclusions())
+      out += ". Total nodes: " + std::to_string(stats.totalNodes) + "; excluded: " + stats.format_reasons();
+    return out;
+  }
+  static int32_t count_slices_in_subtree(Domain* d, int cur, int target, int32_t sliceSize) {  // :1743-1752
+    if (cur == target) return go_div32(d->state, sliceSize);
+    int32_t total = 0;
+    for (Domain* c : d->children) total = w_add(total, count_slices_in_subtree(c, cur + 1, target, sliceSize));
+    return total;
+  }
+  std::string multi_layer_not_fit_message(int reqLevel, int32_t count, const std::vector<SliceConstraint>& cs,
+                                          const ExclusionStats& stats) const {  // :1754-1793
+    std::string out = "topology " + go_quote(topologyName) + " doesn't allow to fit";
+    Domain* best = nullptr;
+    for (auto& kv : domainsPerLevel[reqLevel]) {
+      Domain* d = kv.second;
+      if (!best || d->sliceState > best->sliceState || (d->sliceState == best->sliceState && d->id < best->id)) best = d;
+    }
+    if (!best) return out;
+    for (auto& c : cs) {
+      int t = resolve_level_idx(c.topology);
+      if (t < 0) continue;
+      int32_t needed = go_div32(count, c.size);
+      int32_t fit = count_slices_in_subtree(best, reqLevel, t, c.size);
+      out += "; " + std::to_string(fit) + "/" + std::to_string(needed) + " slice(s) fit on level " + c.topology;
+    }
+    if (stats.has_exclusions())
+      out += ". Total nodes: " + std::to_string(stats.totalNodes) + "; excluded: " + stats.format_reasons();
+    return out;
+  }
+
+  // findLevelWithFitDomains (:1236-1321)
+  std::string find_level_with_fit_domains(int searchLevelIdx, Params& st, int* fitLevel, std::vector<Domain*>* out) {
+    auto& doms = domainsPerLevel[searchLevelIdx];
+    if (doms.empty()) return "no topology domains at level: " + levelKeys[searchLevelIdx];
+    std::vector<Domain*> levelDomains;
+    for (auto& kv : doms) levelDomains.push_back(kv.second);
+    std::vector<Domain*> sorted = sorted_domains_with_leader(levelDomains, st.unconstrained);
+    Domain* top = sorted[0];
+    int32_t sliceCount = go_div32(st.count, st.sliceSize);
+    if (use_bf(st.unconstrained) && top->sliceStateWithLeader >= sliceCount && top->leaderState >= st.leaderCount)
+      top = find_best_fit_for_slices(sorted, 0, sliceCount, st.leaderCount);
+    auto notFit = [&](int32_t fit, int32_t total) {
+      if (!st.multiLayerConstraints.empty())
+        return multi_layer_not_fit_message(searchLevelIdx, st.count, st.multiLayerConstraints, st.stats);
+      return not_fit_message(fit, total, st.sliceSize, st.stats);
+    };
+    if (use_lfc(st.unconstrained)) {
+      for (Domain* c : sorted)
+        if (c->sliceState >= sliceCount) {
+          *fitLevel = searchLevelIdx;
+          *out = {c};
+          return "";
+        }
+      if (st.required) return notFit(sorted.back()->state, sliceCount);
+    }
+    if (top->sliceStateWithLeader < sliceCount || top->leaderState < st.leaderCount) {
+      if (st.required) return notFit(top->sliceState, sliceCount);
+      if (searchLevelIdx > 0 && !st.unconstrained) return find_level_with_fit_domains(searchLevelIdx - 1, st, fitLevel, out);
+      std::vector<Domain*> results;
+      int32_t remSlices = sliceCount, remLeaders = st.leaderCount;
+      size_t idx = 0;
+      for (; remLeaders > 0 && idx < sorted.size() && sorted[idx]->leaderState > 0; idx++) {
+        Domain* d = sorted[idx];
+        if (use_bf(st.unconstrained) && sorted[idx]->sliceStateWithLeader >= remSlices)
+          d = find_best_fit_for_slices(sorted, idx, remSlices, remLeaders);
+        results.push_back(d);
+        remLeaders = w_sub(remLeaders, d->leaderState);
+        remSlices = w_sub(remSlices, d->sliceStateWithLeader);
+      }
+      if (remLeaders > 0) return notFit(w_sub(st.leaderCount, remLeaders), sliceCount);
+      std::vector<Domain*> rest(sorted.begin() + idx, sorted.end());
+      sorted = sorted_domains(rest, st.unconstrained);
+      for (size_t i = 0; remSlices > 0 && i < sorted.size(); i++) {
+        Domain* d = sorted[i];
+        if (use_bf(st.unconstrained) && sorted[i]->sliceState >= remSlices) d = find_best_fit_for_slices(sorted, i, remSlices, 0);
+        results.push_back(d);
+        remSlices = w_sub(remSlices, d->sliceState);
+      }
+      if (remSlices > 0) return notFit(w_sub(sliceCount, remSlices), sliceCount);
+      *fitLevel = searchLevelIdx;
+      *out = results;
+      return "";
+    }
+    *fitLevel = searchLevelIdx;
+    *out = {top};
+    return "";
+  }
+
+  // consumeWithLeadersGeneric (:1348-1403).  `wl`/`pr` select the fields.
+  enum Field { F_STATE, F_SLICE, F_SWL, F_SSWL };
+  static int32_t& fld(Domain* d, Field f) {
+    switch (f) {
+      case F_STATE: return d->state;
+      case F_SLICE: return d->sliceState;
+      case F_SWL: return d->stateWithLeader;
+      default: return d->sliceStateWithLeader;
+    }
+  }
+  Domain* consume_with_leaders(Domain* domain, const std::vector<Domain*>& ds, size_t from, int32_t* remPrimary,
+                               int32_t* remLeaders, bool unconstrained, Field wl, Field pr, int32_t sliceSize,
+                               bool slices, bool* completed) {
+    if (use_bf(unconstrained) && fld(domain, wl) >= *remPrimary && domain->leaderState >= *remLeaders) {
+      if (slices) {
+        domain = find_best_fit_for_slices(ds, from, *remPrimary, *remLeaders);
+        wl = F_SSWL;
+        pr = F_SLICE;
+      } else {
+        domain = find_best_fit(ds, from, *remPrimary, *remLeaders);
+        wl = F_SWL;
+        pr = F_STATE;
+      }
+    }
+    if (fld(domain, wl) >= *remPrimary && domain->leaderState >= *remLeaders) {
+      fld(domain, pr) = *remPrimary;
+      domain->leaderState = *remLeaders;
+      domain->state = w_mul(*remPrimary, sliceSize);
+      *completed = true;
+      return domain;
+    }
+    if (slices) {
+      if (fld(domain, wl) > *remPrimary) fld(domain, wl) = *remPrimary;
+      if (domain->leaderState > *remLeaders) domain->leaderState = *remLeaders;
+      domain->state = w_mul(fld(domain, wl), sliceSize);
+      *remLeaders = w_sub(*remLeaders, domain->leaderState);
+      *remPrimary = w_sub(*remPrimary, fld(domain, wl));
+      *completed = false;
+      return domain;
+    }
+    *remPrimary = w_sub(*remPrimary, fld(domain, wl));
+    *remLeaders = w_sub(*remLeaders, domain->leaderState);
+    if (fld(domain, wl) > *remPrimary) fld(domain, wl) = *remPrimary;
+    if (domain->leaderState > *remLeaders) domain->leaderState = *remLeaders;
+    *completed = false;
+    return domain;
+  }
+
+  // updateCountsToMinimumGeneric (:1405-1469).  Returns false on the
+  // "code assumptions violated" path (Go returns nil).
+  bool update_counts_to_minimum(const std::vector<Domain*>& ds, int32_t count, int32_t leaderCount, int32_t sliceSize,
+                                bool unconstrained, bool slices, std::vector<Domain*>* result) {
+    result->clear();
+    int32_t remPrimary = slices ? go_div32(count, sliceSize) : count;
+    int32_t remLeaders = leaderCount;
+    for (size_t i = 0; i < ds.size(); i++) {
+      Domain* dom = ds[i];
+      if (remLeaders > 0) {
+        bool completed = false;
+        Domain* d = slices ? consume_with_leaders(dom, ds, i, &remPrimary, &remLeaders, unconstrained, F_SSWL, F_SLICE,
+                                                  sliceSize, true, &completed)
+                           : consume_with_leaders(dom, ds, i, &remPrimary, &remLeaders, unconstrained, F_SWL, F_STATE, 1,
+                                                  false, &completed);
+        result->push_back(d);
+        if (completed) return true;
+        continue;
+      }
+      if (slices) {
+        if (use_bf(unconstrained) && dom->sliceState >= remPrimary) dom = find_best_fit_for_slices(ds, i, remPrimary, 0);
+        dom->leaderState = 0;
+        if (dom->sliceState >= remPrimary) {
+          dom->state = w_mul(remPrimary, sliceSize);
+          dom->sliceState = remPrimary;
+          result->push_back(dom);
+          return true;
+        }
+        dom->state = w_mul(dom->sliceState, sliceSize);
+        remPrimary = w_sub(remPrimary, dom->sliceState);
+        result->push_back(dom);
+        continue;
+      }
+      if (use_bf(unconstrained) && dom->state >= remPrimary) dom = find_best_fit(ds, i, remPrimary, 0);
+      dom->leaderState = 0;
+      if (dom->state >= remPrimary) {
+        dom->state = remPrimary;
+        result->push_back(dom);
+        return true;
+      }
+      remPrimary = w_sub(remPrimary, dom->state);
+      result->push_back(dom);
+    }
+    result->clear();
+    return false;
+  }
+
+  TopologyAssignment build_assignment(std::vector<Domain*> ds) const {  // :1490-1501 + :1472-1488
+    std::stable_sort(ds.begin(), ds.end(), [](Domain* a, Domain* b) { return compare_values(a->levelValues, b->levelValues) < 0; });
+    size_t levelIdx = isLowestLevelNode ? levelKeys.size() - 1 : 0;
+    TopologyAssignment ta;
+    ta.levels.assign(levelKeys.begin() + levelIdx, levelKeys.end());
+    for (Domain* d : ds) {
+      if (d->state == 0) continue;
+      ta.domains.push_back({std::vector<std::string>(d->levelValues.begin() + levelIdx, d->levelValues.end()), d->state});
+    }
+    return ta;
+  }
+
+  static std::vector<Domain*> lower_level_domains(const std::vector<Domain*>& ds) {  // :1503-1509
+    std::vector<Domain*> out;
+    for (Domain* d : ds) out.insert(out.end(), d->children.begin(), d->children.end());
+    return out;
+  }
+
+  // findTopologyAssignment (:804-999)
+  std::string find_topology_assignment(const PodSetRequest& workers, const PodSetRequest* leader,
+                                       std::map<std::string, Requests>& assumed, bool simulateEmpty,
+                                       std::map<std::string, TopologyAssignment>* assignments) {
+    Requirements rq;
+    rq.assumedUsage = &assumed;
+    rq.simulateEmpty = simulateEmpty;
+    Params st;
+    st.count = workers.count;
+    rq.requests = workers.singlePodRequests;
+    req_add(rq.requests, Requests{{"pods", 1}});
+    if (leader) {
+      Requests lr = leader->singlePodRequests;
+      req_add(lr, Requests{{"pods", 1}});
+      rq.leaderRequests = lr;
+      st.leaderCount = 1;
+    }
+    auto ss = slice_size_with_single_pod_default(workers.topologyRequest);
+    if (!ss.second.empty()) return ss.second;
+    st.sliceSize = ss.first;
+    st.required = workers.topologyRequest && workers.topologyRequest->required.has_value();
+    st.unconstrained = (workers.topologyRequest && workers.topologyRequest->unconstrained.value_or(false)) ||
+                       workers.implied || is_slice_topology_only(workers.topologyRequest);
+    auto key = level_key_with_implied_fallback(workers);
+    if (!key) return "topology level not specified";
+    int req = resolve_level_idx(*key);
+    if (req < 0) return "no requested topology level: " + *key;
+    st.requestedLevelIdx = req;
+    std::string sliceKey = slice_level_key_with_default(workers.topologyRequest, lowest_level());
+    int sl = resolve_level_idx(sliceKey);
+    if (sl < 0) return "no requested topology level for slices: " + sliceKey;
+    st.sliceLevelIdx = sl;
+    if (st.requestedLevelIdx > st.sliceLevelIdx)
+      return "podset slice topology " + sliceKey + " is above the podset topology " + *key;
+    std::string r = build_slice_size_at_level(workers, st.sliceSize, st.sliceLevelIdx, st.sliceSizeAtLevel);
+    if (!r.empty()) return r;
+    if (gates.multiLayer && !st.sliceSizeAtLevel.empty()) st.multiLayerConstraints = workers.topologyRequest->constraints;
+    rq.tolerations = workers.tolerations;
+    rq.tolerations.insert(rq.tolerations.end(), tolerations.begin(), tolerations.end());
+    if (isLowestLevelNode && workers.nodeSelector) rq.selector = *workers.nodeSelector;
+
+    fill_in_counts(rq, st);
+
+    if (gates.balanced && !st.required && !st.unconstrained) return "unsupported: TASBalancedPlacement";
+    int fitLevelIdx = 0;
+    std::vector<Domain*> cur;
+    r = find_level_with_fit_domains(st.requestedLevelIdx, st, &fitLevelIdx, &cur);
+    if (!r.empty()) return r;
+    std::vector<Domain*> next;
+    if (!update_counts_to_minimum(cur, st.count, st.leaderCount, st.sliceSize, st.unconstrained, true, &next)) next.clear();
+    cur = next;
+    int level = fitLevelIdx;
+    int L = int(domainsPerLevel.size());
+    for (; level < std::min(L - 1, st.sliceLevelIdx); level++) {
+      auto lower = sorted_domains(lower_level_domains(cur), st.unconstrained);
+      if (!update_counts_to_minimum(lower, st.count, st.leaderCount, st.sliceSize, st.unconstrained, true, &next)) next.clear();
+      cur = next;
+    }
+    for (; level < L - 1; level++) {
+      int32_t sliceOnLevel = st.sliceSize;
+      if (level >= st.sliceLevelIdx) {
+        sliceOnLevel = 1;
+        auto it = st.sliceSizeAtLevel.find(level + 1);
+        if (it != st.sliceSizeAtLevel.end()) sliceOnLevel = it->second;
+      }
+      std::vector<Domain*> newCur;
+      for (Domain* d : cur) {
+        auto lower = sorted_domains(d->children, st.unconstrained);
+        if (sliceOnLevel > 1)
+          for (Domain* c : lower) {
+            c->sliceState = go_div32(c->state, sliceOnLevel);
+            c->sliceStateWithLeader = go_div32(c->stateWithLeader, sliceOnLevel);
+          }
+        std::vector<Domain*> add;
+        if (!update_counts_to_minimum(lower, d->state, d->leaderState, sliceOnLevel, st.unconstrained, sliceOnLevel > 1, &add))
+          add.clear();
+        newCur.insert(newCur.end(), add.begin(), add.end());
+      }
+      cur = newCur;
+    }
+    if (leader) {
+      std::vector<Domain*> leaderFit, workerFit;
+      std::deque<Domain> copies;  // `copiedDomain := *domain` (:981-983)
+      for (Domain* d : cur) {
+        if (d->leaderState > 0) {
+          copies.push_back(*d);
+          copies.back().state = copies.back().leaderState;
+          leaderFit.push_back(&copies.back());
+        }
+        if (d->state > 0) workerFit.push_back(d);
+      }
+      (*assignments)[leader->name] = build_assignment(leaderFit);
+      cur = workerFit;
+    }
+    (*assignments)[workers.name] = build_assignment(cur);
+    return "";
+  }
+
+  // FindTopologyAssignmentsForFlavor (:519-594) — normal (non-replacement,
+  // non-elastic) branch.
+  std::vector<PodSetResult> find_topology_assignments_for_flavor(const std::vector<PodSetRequest>& reqs, bool simulateEmpty) {
+    std::vector<PodSetResult> result;
+    std::map<std::string, Requests> assumed;
+    std::vector<std::string> order;
+    std::map<std::string, std::vector<const PodSetRequest*>> grouped;
+    for (size_t idx = 0; idx < reqs.size(); idx++) {
+      std::string key = reqs[idx].podSetGroupName ? *reqs[idx].podSetGroupName : std::to_string(idx);
+      if (std::find(order.begin(), order.end(), key) == order.end()) order.push_back(key);
+      grouped[key].push_back(&reqs[idx]);
+    }
+    auto set_result = [&](const std::string& name, std::optional<TopologyAssignment> a, const std::string& reason) {
+      for (auto& r : result)
+        if (r.name == name) { r.assignment = std::move(a); r.reason = reason; return; }
+      result.push_back({name, std::move(a), reason});
+    };
+    for (auto& key : order) {
+      auto& trs = grouped[key];
+      // findLeaderAndWorkers (:596-609)
+      const PodSetRequest* leader = nullptr;
+      const PodSetRequest* workers = trs[0];
+      if (trs.size() > 1) {
+        leader = trs[1];
+        if (leader->count > workers->count) { leader = trs[0]; workers = trs[1]; }
+      }
+      if (gates.elastic) {
+        set_result(workers->name, std::nullopt, "unsupported: ElasticJobsViaWorkloadSlicesWithTAS");
+        return result;
+      }
+      std::map<std::string, TopologyAssignment> assignments;
+      std::string reason;
+      try {
+        reason = find_topology_assignment(*workers, leader, assumed, simulateEmpty, &assignments);
+      } catch (const GoPanic& e) {
+        reason = std::string("panic: ") + e.what();
+      }
+      for (auto* tr : trs) {
+        auto it = assignments.find(tr->name);
+        if (it == assignments.end()) set_result(tr->name, std::nullopt, reason);
+        else set_result(tr->name, it->second, reason);
+      }
+      if (!reason.empty()) return result;
+      for (auto* tr : trs) {  // addAssumedUsage (:658-666)
+        auto it = assignments.find(tr->name);
+        if (it == assignments.end()) continue;
+        for (auto& d : it->second.domains) {
+          Requests& a = assumed[domain_id(d.values)];
+          req_add(a, req_scaled_up(tr->singlePodRequests, d.count));
+        }
+      }
+    }
+    return result;
+  }
+};
+
+// ---- JSON plumbing -------------------------------------------------------------
+static Requests parse_requests(const ojson::Value& v) {
+  Requests r;
+  if (v.kind == ojson::Value::Obj)
+    for (auto& kv : v.o) r[kv.first] = kv.second.as_int();
+  return r;
+}
+static std::vector<Toleration> parse_tolerations(const ojson::Value& v) {
+  std::vector<Toleration> out;
+  for (auto& t : v.a) out.push_back({t.at("key").as_str(), t.at("operator").as_str(), t.at("value").as_str(), t.at("effect").as_str()});
+  return out;
+}
+static Gates parse_gates(const ojson::Value& v) {
+  Gates g;
+  if (auto p = v.get("TASProfileMixed")) g.profileMixed = p->as_bool();
+  if (auto p = v.get("TASMultiLayerTopology")) g.multiLayer = p->as_bool();
+  if (auto p = v.get("TASBalancedPlacement")) g.balanced = p->as_bool();
+  if (auto p = v.get("ElasticJobsViaWorkloadSlicesWithTAS")) g.elastic = p->as_bool();
+  return g;
+}
+
+static std::vector<PodSetRequest> parse_podsets(const ojson::Value& arr) {
+  std::vector<PodSetRequest> out;
+  for (auto& ps : arr.a) {
+    PodSetRequest r;
+    r.name = ps.at("name").as_str();
+    const ojson::Value& tr = ps.at("topologyRequest");
+    if (!tr.is_null()) {
+      TopologyRequest t;
+      if (!tr.at("required").is_null()) t.required = tr.at("required").as_str();
+      if (!tr.at("preferred").is_null()) t.preferred = tr.at("preferred").as_str();
+      if (!tr.at("unconstrained").is_null()) t.unconstrained = tr.at("unconstrained").as_bool();
+      if (!tr.at("podSetSliceRequiredTopology").is_null()) t.sliceRequiredTopology = tr.at("podSetSliceRequiredTopology").as_str();
+      if (!tr.at("podSetSliceSize").is_null()) t.sliceSize = int32_t(tr.at("podSetSliceSize").as_int());
+      for (auto& c : tr.at("podsetSliceRequiredTopologyConstraints").a)
+        t.constraints.push_back({c.at("topology").as_str(), int32_t(c.at("size").as_int())});
+      r.topologyRequest = t;
+    }
+    r.implied = tr.is_null();  // harness: tas_cache_test.go:6322-6324
+    if (auto im = ps.get("implied")) r.implied = im->as_bool();
+    r.singlePodRequests = parse_requests(ps.at("requests"));
+    r.count = int32_t(ps.at("count").as_int());
+    if (!ps.at("podSetGroupName").is_null()) r.podSetGroupName = ps.at("podSetGroupName").as_str();
+    r.tolerations = parse_tolerations(ps.at("tolerations"));
+    const ojson::Value& ns = ps.at("nodeSelector");
+    if (ns.kind == ojson::Value::Obj) {
+      std::map<std::string, std::string> m;
+      for (auto& kv : ns.o) m[kv.first] = kv.second.as_str();
+      r.nodeSelector = m;
+    }
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+
+// Build the snapshot exactly like the reference test harness
+// (tas_cache_test.go:6270-6300): nodesCache.sync + find, nonTasUsageCache.update,
+// TASFlavorCache.snapshot (tas_flavor.go:118-138).
+static std::unique_ptr<Snapshot> build_snapshot(const ojson::Value& c) {
+  std::vector<std::string> levels;
+  for (auto& l : c.at("levels").a) levels.push_back(l.as_str());
+  if (levels.empty()) throw std::runtime_error("no levels");
+  auto snap = std::make_unique<Snapshot>(levels, parse_tolerations(c.at("flavorTolerations")));
+  snap->gates = parse_gates(c.at("featureGates"));
+  if (!c.at("topologyName").is_null()) snap->topologyName = c.at("topologyName").as_str();
+  std::map<std::string, std::string> flavorLabels;
+  for (auto& kv : c.at("nodeLabels").o) flavorLabels[kv.first] = kv.second.as_str();
+  std::map<std::string, std::string> nodeToDomain;
+  std::set<std::string> seenNames;
+  std::vector<const ojson::Value*> kept;
+  // nodesCache keyed by name: a later sync of the same name replaces the earlier one.
+  std::map<std::string, const ojson::Value*> byName;
+  std::vector<std::string> nameOrder;
+  for (auto& n : c.at("nodes").a) {
+    std::string name = n.at("name").as_str();
+    bool ready = false;
+    for (auto& cond : n.at("conditions").a)
+      if (cond.at("type").as_str() == "Ready") { ready = cond.at("status").as_str() == "True"; break; }
+    bool ok = !n.at("unschedulable").as_bool() && ready;  // tas_nodes_cache.go:38-50
+    if (ok) {
+      if (!byName.count(name)) nameOrder.push_back(name);
+      byName[name] = &n;
+    } else if (byName.count(name)) {
+      byName.erase(name);
+      nameOrder.erase(std::find(nameOrder.begin(), nameOrder.end(), name));
+    }
+  }
+  for (auto& name : nameOrder) {
+    const ojson::Value& n = *byName[name];
+    std::map<std::string, std::string> labels;
+    for (auto& kv : n.at("labels").o) labels[kv.first] = kv.second.as_str();
+    bool match = true;  // NodeMatchesFlavor (util/tas/node.go:21-33)
+    for (auto& kv : flavorLabels) {
+      auto it = labels.find(kv.first);
+      if ((it == labels.end() ? std::string() : it->second) != kv.second) { match = false; break; }
+    }
+    for (auto& l : levels)
+      if (!labels.count(l)) { match = false; break; }
+    if (!match) continue;
+    snap->nodes.emplace_back();
+    NodeInfo& ni = snap->nodes.back();
+    ni.name = name;
+    ni.labels = labels;
+    for (auto& t : n.at("taints").a) ni.taints.push_back({t.at("key").as_str(), t.at("value").as_str(), t.at("effect").as_str()});
+    ni.allocatable = parse_requests(n.at("allocatable"));
+    nodeToDomain[name] = snap->add_node(&ni);
+  }
+  snap->initialize();
+  // TAS usage (TASFlavorCache.updateUsage, tas_flavor.go:154-171)
+  std::map<std::string, Requests> usage;
+  for (auto& u : c.at("tasUsage").a) {
+    std::vector<std::string> values;
+    for (auto& v : u.at("values").a) values.push_back(v.as_str());
+    int64_t cnt = u.at("count").as_int();
+    Requests& dst = usage[domain_id(values)];
+    req_add(dst, req_scaled_up(parse_requests(u.at("singlePodRequests")), cnt));
+    req_add(dst, Requests{{"pods", cnt}});
+  }
+  for (auto& kv : usage) snap->add_tas_usage(kv.first, kv.second);
+  // non-TAS pods (tas_non_tas_pod_cache.go:46-120)
+  std::map<std::string, std::pair<std::string, Requests>> podUsage;
+  std::map<std::string, Requests> nodeUsage;
+  auto remove_node_usage = [&](const std::string& node, const Requests& u) {
+    auto it = nodeUsage.find(node);
+    if (it == nodeUsage.end()) return;
+    req_sub(it->second, u);
+    it->second["pods"] = w_sub64(it->second["pods"], 1);
+    if (it->second["pods"] <= 0) nodeUsage.erase(it);
+  };
+  for (auto& p : c.at("pods").a) {
+    std::string key = p.at("namespace").as_str() + "/" + p.at("name").as_str();
+    std::string phase = p.at("phase").as_str();
+    auto old = podUsage.find(key);
+    if (phase == "Succeeded" || phase == "Failed") {
+      if (old != podUsage.end()) remove_node_usage(old->second.first, old->second.second);
+      podUsage.erase(key);
+      continue;
+    }
+    if (old != podUsage.end()) remove_node_usage(old->second.first, old->second.second);
+    Requests r = parse_requests(p.at("requests"));
+    std::string node = p.at("nodeName").as_str();
+    podUsage[key] = {node, r};
+    Requests& nu = nodeUsage[node];
+    req_add(nu, r);
+    nu["pods"] = w_add64(nu["pods"], 1);
+  }
+  for (auto& kv : nodeUsage) {
+    auto it = nodeToDomain.find(kv.first);
+    if (it != nodeToDomain.end()) snap->add_non_tas_usage(it->second, kv.second);
+  }
+  return snap;
+}
+
+static void emit_results(std::string& out, const std::vector<PodSetResult>& rs) {
+  out += "[";
+  for (size_t i = 0; i < rs.size(); i++) {
+    if (i) out += ",";
+    out += "{\"name\":";
+    ojson::quote(out, rs[i].name);
+    out += ",\"assignment\":";
+    if (!rs[i].assignment) {
+      out += "null";
+    } else {
+      out += "{\"levels\":[";
+      auto& a = *rs[i].assignment;
+      for (size_t j = 0; j < a.levels.size(); j++) {
+        if (j) out += ",";
+        ojson::quote(out, a.levels[j]);
+      }
+      out += "],\"domains\":[";
+      for (size_t j = 0; j < a.domains.size(); j++) {
+        if (j) out += ",";
+        out += "{\"values\":[";
+        for (size_t k = 0; k < a.domains[j].values.size(); k++) {
+          if (k) out += ",";
+          ojson::quote(out, a.domains[j].values[k]);
+        }
+        out += "],\"count\":" + std::to_string(a.domains[j].count) + "}";
+      }
+      out += "]}";
+    }
+    out += ",\"reason\":";
+    ojson::quote(out, rs[i].reason);
+    out += "}";
+  }
+  out += "]";
+}
+
+static char* dup_out(const std::string& s) {
+  char* p = static_cast<char*>(malloc(s.size() + 1));
+  memcpy(p, s.data(), s.size() + 1);
+  return p;
+}
+
+}  // namespace oracle
+
+extern "C" {
+
+// Runs one fixture case (schema: tools/extract_goldens.py) and returns
+// {"results":[{"name","assignment","reason"}...]} or {"error": "..."}.
+int tas_oracle_run_case(const char* case_json, char** out_json) {
+  using namespace oracle;
+  std::string out;
+  try {
+    ojson::Value c = ojson::parse(case_json);
+    auto snap = build_snapshot(c);
+    auto reqs = parse_podsets(c.at("podSets"));
+    auto rs = snap->find_topology_assignments_for_flavor(reqs, c.at("simulateEmpty").as_bool());
+    out = "{\"results\":";
+    emit_results(out, rs);
+    out += "}";
+  } catch (const std::exception& e) {
+    out = "{\"error\":";
+    ojson::quote(out, e.what());
+    out += "}";
+    *out_json = dup_out(out);
+    return -1;
+  }
+  *out_json = dup_out(out);
+  return 0;
+}
+
+// Batched evaluation for the CPU baseline: builds the snapshot once from
+// `snapshot_json` (same schema, podSets ignored) and evaluates every workload
+// of `workloads_json` ({"workloads": [[podset...], ...]}) independently against
+// it, as Scheduler.nominate does (pkg/scheduler/scheduler.go:583-619).  Only
+// the evaluation loop is timed (*seconds).  `threads` > 1 gives each thread its
+// own snapshot copy (the Go snapshot's scratch counters are not reentrant).
+int tas_oracle_eval_workloads(const char* snapshot_json, const char* workloads_json, int threads, int emit,
+                              double* seconds, char** out_json) {
+  using namespace oracle;
+  try {
+    ojson::Value c = ojson::parse(snapshot_json);
+    ojson::Value w = ojson::parse(workloads_json);
+    std::vector<std::vector<PodSetRequest>> wls;
+    for (auto& wl : w.at("workloads").a) wls.push_back(parse_podsets(wl));
+    if (threads < 1) threads = 1;
+    std::vector<std::unique_ptr<Snapshot>> snaps;
+    for (int t = 0; t < threads; t++) snaps.push_back(build_snapshot(c));
+    std::vector<std::vector<PodSetResult>> results(wls.size());
+    auto t0 = std::chrono::steady_clock::now();
+    if (threads == 1) {
+      for (size_t i = 0; i < wls.size(); i++) results[i] = snaps[0]->find_topology_assignments_for_flavor(wls[i], false);
+    } else {
+      std::vector<std::thread> pool;
+      for (int t = 0; t < threads; t++)
+        pool.emplace_back([&, t] {
+          for (size_t i = t; i < wls.size(); i += threads)
+            results[i] = snaps[t]->find_topology_assignments_for_flavor(wls[i], false);
+        });
+      for (auto& th : pool) th.join();
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    *seconds = std::chrono::duration<double>(t1 - t0).count();
+    std::string out = "{\"results\":[";
+    if (emit) {
+      for (size_t i = 0; i < results.size(); i++) {
+        if (i) out += ",";
+        emit_results(out, results[i]);
+      }
+    }
+    out += "]}";
+    *out_json = dup_out(out);
+    return 0;
+  } catch (const std::exception& e) {
+    std::string out = "{\"error\":";
+    ojson::quote(out, e.what());
+    out += "}";
+    *out_json = dup_out(out);
+    return -1;
+  }
+}
+
+void tas_oracle_free(char* p) { free(p); }
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+"""ctypes loader for the CPU oracle (oracle/_build/libtas_oracle.so).
+
+Test infrastructure: imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libtas_oracle.so")
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    lib = ctypes.CDLL(ORACLE_SO)
+    lib.tas_oracle_run_case.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    lib.tas_oracle_run_case.restype = ctypes.c_int
+    lib.tas_oracle_eval_workloads.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_void_p)]
+    lib.tas_oracle_eval_workloads.restype = ctypes.c_int
+    lib.tas_oracle_free.argtypes = [ctypes.c_void_p]
+    _lib = lib
+    return lib
+
+
+def _take(lib, p):
+    s = ctypes.cast(p, ctypes.c_char_p).value.decode()
+    lib.tas_oracle_free(p)
+    return json.loads(s)
+
+
+def run_case(case: dict) -> dict:
+    """Returns {"results": [...]} or raises on oracle error."""
+    lib = load()
+    out = ctypes.c_void_p()
+    rc = lib.tas_oracle_run_case(json.dumps(case).encode(), ctypes.byref(out))
+    doc = _take(lib, out)
+    if rc != 0:
+        raise RuntimeError(doc.get("error"))
+    return doc
+
+
+def eval_workloads(snapshot_case: dict, workloads: list, threads: int = 1, emit: bool = True):
+    """Evaluates each workload independently; returns (results, seconds)."""
+    lib = load()
+    out = ctypes.c_void_p()
+    secs = ctypes.c_double()
+    rc = lib.tas_oracle_eval_workloads(json.dumps(snapshot_case).encode(),
+                                       json.dumps({"workloads": workloads}).encode(),
+                                       threads, 1 if emit else 0, ctypes.byref(secs), ctypes.byref(out))
+    doc = _take(lib, out)
+    if rc != 0:
+        raise RuntimeError(doc.get("error"))
+    return doc["results"], secs.value
