@@ -1,0 +1,218 @@
+/*
+ * kueue_tas.h — C-ABI of the MI355X-native TAS evaluation path.
+ *
+ * This is the drop-in boundary for Kueue's Topology-Aware Scheduling
+ * evaluation (reference: /root/reference/pkg/cache/scheduler/).  A Go cgo shim
+ * in the reference's pkg/cache/scheduler binds exactly these
+ * entry points; everything here is plain C: fixed-width integers, plain
+ * pointers and sizes, caller-owned buffers, 0 = OK / negative = error.
+ *
+ * Two layers are exported by libkueue_tas.so:
+ *
+ *  (1) Device layer (kueue_tas_ctx_*, kueue_tas_snapshot_*, kueue_tas_eval_*):
+ *      a device-resident TAS snapshot in HBM plus batched evaluation of
+ *      compiled PodSet-group requests.  Replaces, per call:
+ *        TASFlavorSnapshot.findTopologyAssignment   tas_flavor_snapshot.go:804-999
+ *          fillInCounts / fillInCountsHelper        :1568-1719
+ *          findLevelWithFitDomains                  :1236-1321
+ *          updateCountsToMinimumGeneric (+consume)  :1348-1469
+ *          buildAssignment                          :1490-1501
+ *        snapshot construction (domain tree)        :160-241, tas_flavor.go:118-138
+ *        updateTASUsage (snapshot delta)            :257-293
+ *
+ *  (2) Host layer (kueue_tas_host_*): the C++ mirror of the Go API
+ *      (TASFlavorSnapshot, TASPodSetRequests, TASAssignmentsResult,
+ *      FindTopologyAssignmentsForFlavor :519-594 with PodSet groups,
+ *      leader/worker split :596-609 and assumedUsage chaining :658-666,
+ *      failure strings :1721-1793) driven by JSON documents.  It is what a
+ *      Go shim would otherwise do in Go; tests drive it with the fixtures
+ *      transcribed from the reference's own table tests.
+ *
+ * Threading: one ctx per TAS flavor snapshot; calls on one ctx are
+ * serialized by the caller (the reference evaluates on the single scheduler
+ * goroutine, pkg/scheduler/scheduler.go:286-365).
+ */
+#ifndef KUEUE_TAS_H_
+#define KUEUE_TAS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KUEUE_TAS_ABI_VERSION 1
+#define KUEUE_TAS_MAX_LEVELS 16    /* topology_types.go:114 (<=16 levels) */
+#define KUEUE_TAS_MAX_COLS 32      /* resource columns per snapshot */
+#define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs per request */
+#define KUEUE_TAS_MAX_LAYERS 4     /* podsetSliceRequiredTopologyConstraints */
+
+/* error codes */
+#define KUEUE_TAS_OK 0
+#define KUEUE_TAS_EINVAL -1
+#define KUEUE_TAS_ENOMEM -2
+#define KUEUE_TAS_EDEVICE -3
+#define KUEUE_TAS_ENOSNAPSHOT -4
+#define KUEUE_TAS_EOVERFLOW -5
+
+typedef struct kueue_tas_ctx kueue_tas_ctx;
+
+/* ---- snapshot -------------------------------------------------------------
+ * Domains of every level are numbered in bytewise-lexicographic order of their
+ * levelValues (the tie-break of sortedDomains*, tas_flavor_snapshot.go:1532,
+ * :1561, and the output order of buildAssignment :1492).  Children of a domain
+ * are therefore contiguous in the next level (CSR).
+ */
+typedef struct {
+  int32_t num_levels;             /* L */
+  const int32_t* level_sizes;     /* [L] D_l */
+  const int32_t* child_offsets;   /* for l in 0..L-2: D_l+1 offsets into level l+1, concatenated */
+  int32_t num_cols;               /* R resource columns, numbered in sorted resource-name order */
+  const int64_t* free_capacity;   /* [R][N] allocatable - non-TAS usage (leafDomain.freeCapacity) */
+  const int64_t* tas_usage;       /* [R][N] leafDomain.tasUsage (incl. "pods") */
+  const uint32_t* free_present;   /* [N] bit c set: column c is a key of freeCapacity */
+  const uint32_t* usage_present;  /* [N] bit c set: column c is a key of tasUsage */
+  int32_t lowest_is_hostname;     /* isLowestLevelNode (:155): taint/selector filters apply */
+  const int32_t* taint_profile;   /* [N] taint-profile id (0..P-1) or NULL */
+  int32_t num_label_cols;         /* K dictionary-encoded label columns */
+  const int32_t* label_values;    /* [K][N] value id, 0 = label absent; NULL if K == 0 */
+  const int32_t* domain_id_rank;  /* [sum D_l] rank of the DomainID string within its level
+                                     (multiLayerNotFitMessage tie-break :1768-1769); NULL = index order */
+} kueue_tas_snapshot_desc;
+
+/* One snapshot delta record (updateTASUsage :257-265 / Sub on removal). */
+typedef struct {
+  int32_t leaf;                   /* leaf index */
+  int32_t col;                    /* resource column */
+  int64_t delta;                  /* added to tas_usage[col][leaf] */
+} kueue_tas_delta;
+
+/* ---- one PodSet-group evaluation (findTopologyAssignment) ---------------- */
+#define KUEUE_TAS_F_REQUIRED 1u       /* isRequired :1140 */
+#define KUEUE_TAS_F_UNCONSTRAINED 2u  /* isUnconstrained :1144 */
+#define KUEUE_TAS_F_LFC 4u            /* useLeastFreeCapacityAlgorithm :1328 */
+#define KUEUE_TAS_F_SIMULATE_EMPTY 8u /* WithSimulateEmpty :505 */
+#define KUEUE_TAS_F_LEADER 16u        /* leaderTasPodSetRequests != nil */
+#define KUEUE_TAS_F_MULTILAYER 32u    /* len(multiLayerConstraints) > 0 :873-875 */
+
+typedef struct {
+  uint32_t flags;
+  int32_t count;                  /* workers Count */
+  int32_t slice_size;             /* getSliceSizeWithSinglePodAsDefault :1162 */
+  int32_t requested_level;        /* requestedLevelIdx */
+  int32_t slice_level;            /* sliceLevelIdx */
+  int32_t num_req;                /* worker request columns (incl. pods+1), ascending column order */
+  int32_t num_leader_req;         /* leader request columns (incl. pods+1) */
+  int32_t num_selectors;
+  int32_t req_col[KUEUE_TAS_MAX_COLS];
+  int64_t req_val[KUEUE_TAS_MAX_COLS];
+  int32_t leader_col[KUEUE_TAS_MAX_COLS];
+  int64_t leader_val[KUEUE_TAS_MAX_COLS];
+  int32_t slice_size_at_level[KUEUE_TAS_MAX_LEVELS]; /* buildSliceSizeAtLevel :1018; 0 = absent */
+  int32_t sel_col[KUEUE_TAS_MAX_SELECTORS];          /* label column */
+  int32_t sel_val[KUEUE_TAS_MAX_SELECTORS];          /* required value id (-1: value never present) */
+  int32_t num_layers;                                /* multi-layer constraints (for the failure message) */
+  int32_t layer_level[KUEUE_TAS_MAX_LAYERS];
+  int32_t layer_size[KUEUE_TAS_MAX_LAYERS];
+  int32_t taint_table;            /* offset into the batch taint table: P entries, excluded taint id or -1 */
+  int32_t assumed_begin;          /* [begin,end) into the batch assumed-usage records (sorted by leaf) */
+  int32_t assumed_end;
+} kueue_tas_eval_req;
+
+/* assumedUsage overlay record (addAssumedUsage :658-666), subtracted from the
+ * remaining capacity of `leaf`; creates the key (presence) like Requests.Sub. */
+typedef struct {
+  int32_t leaf;
+  int32_t col;
+  int64_t value;
+} kueue_tas_assumed;
+
+#define KUEUE_TAS_ST_OK 0
+#define KUEUE_TAS_ST_NO_DOMAINS 1      /* "no topology domains at level: %s" (:1242); a = level */
+#define KUEUE_TAS_ST_NOT_FIT 2         /* notFitMessage(a, b, slice_size) (:1721) */
+#define KUEUE_TAS_ST_MULTILAYER 3      /* multiLayerNotFitMessage (:1754); ml_fit[] */
+#define KUEUE_TAS_ST_INTERNAL 4        /* device-side capacity limit hit (lists/output) */
+
+typedef struct {
+  int32_t status;
+  int32_t a, b;                   /* message numbers (see status) */
+  int32_t fit_level;              /* fitLevelIdx */
+  int32_t num_workers;            /* worker (leaf, count) entries written */
+  int32_t num_leaders;            /* leader (leaf, count) entries written after the workers */
+  int32_t assignment_nil;         /* 1: updateCountsToMinimumGeneric returned nil (:1462) */
+  int32_t total_nodes;            /* ExclusionStats (:423-430) */
+  int32_t excl_selector;
+  int32_t excl_affinity;
+  int32_t excl_topology;
+  int32_t ml_fit[KUEUE_TAS_MAX_LAYERS];
+  int32_t ml_need[KUEUE_TAS_MAX_LAYERS];
+  int32_t reserved[2];
+} kueue_tas_eval_out;
+
+typedef struct {
+  int32_t list_cap;               /* LDS sort capacity per wave (test knob; 0 = default) */
+  int32_t max_batch;              /* evaluations per device batch (0 = default 1024) */
+  int32_t device;                 /* HIP device ordinal */
+  int32_t reserved;
+} kueue_tas_config;
+
+/* ---- device layer -------------------------------------------------------- */
+int kueue_tas_abi_version(void);
+kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg);
+void kueue_tas_ctx_destroy(kueue_tas_ctx* ctx);
+const char* kueue_tas_last_error(kueue_tas_ctx* ctx);
+
+/* Upload (replace) the resident snapshot. */
+int kueue_tas_snapshot_load(kueue_tas_ctx* ctx, const kueue_tas_snapshot_desc* desc);
+/* Apply a delta list to tas_usage on the device (rank-local replica). */
+int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* ctx, const kueue_tas_delta* deltas, size_t n,
+                                    const uint32_t* usage_present_or_null);
+
+/* Evaluate n requests against the resident snapshot.
+ *  taint_table: int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
+ *  assumed:     overlay records referenced by reqs[i].assumed_begin/end
+ *  out:         [n] result headers
+ *  entries:     [n * entry_cap * 2] (leaf, count) int32 pairs per request; workers then leaders
+ *  taint_counts:[n * num_taints] per-request taint exclusion counts (may be NULL)
+ *  res_counts:  [n * num_cols]   per-request resource exclusion counts (may be NULL)
+ * Returns KUEUE_TAS_OK, or an error; a request whose assignment does not fit
+ * into entry_cap entries gets status KUEUE_TAS_ST_INTERNAL. */
+int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
+                         size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
+                         size_t num_assumed, kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap,
+                         int32_t* taint_counts, int32_t* res_counts);
+
+/* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
+ * events on the ctx stream): [0] fill, [1] roll-up, [2] select/descend, [3] total. */
+int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
+
+/* ---- host layer (C++ mirror of the Go API, JSON-driven) ------------------ */
+typedef struct kueue_tas_host kueue_tas_host;
+
+/* Build a TASFlavorSnapshot from a JSON case document (nodes, pods, levels,
+ * nodeLabels, flavorTolerations, tasUsage, featureGates; schema in
+ * tools/extract_goldens.py) and load it to the device. */
+kueue_tas_host* kueue_tas_host_create(const char* snapshot_json, const kueue_tas_config* cfg);
+void kueue_tas_host_destroy(kueue_tas_host* h);
+const char* kueue_tas_host_last_error(kueue_tas_host* h);
+
+/* FindTopologyAssignmentsForFlavor for one workload (podSets JSON array);
+ * *out_json = {"results":[{"name","assignment","reason"}]} (free with kueue_tas_free). */
+int kueue_tas_host_find(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json);
+
+/* Batched nominate: evaluate every workload of {"workloads":[[podset..],..]}
+ * independently against the same snapshot (scheduler.go:583-619). */
+int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, char** out_json);
+
+/* Compile the workloads once; then time repeated device evaluation
+ * (kueue_tas_host_run_compiled) without JSON on the timed path. */
+int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json);
+int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
+
+void kueue_tas_free(char* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KUEUE_TAS_H_ */

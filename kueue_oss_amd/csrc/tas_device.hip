@@ -1,0 +1,486 @@
+// tas_device.cpp — device layer of libkueue_tas.so: HBM-resident snapshot,
+// batch staging and kernel launches behind the C-ABI of include/kueue_tas.h.
+//
+// Data layout in HBM (per context):
+//   snapshot  free_cap[R][N], tas_usage[R][N] (int64 SoA), presence bitmasks
+//             [N], taint-profile ids [N], label-value ids [K][N], CSR child
+//             offsets per level, DomainID ranks [sum D_l]
+//   per batch counters[n][5][sum D_l] int32 (state, sliceState, stateWithLeader,
+//             sliceStateWithLeader, leaderState), exclusion counters, phase-2
+//             scratch lists, result headers and (leaf, count) entries
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tas_internal.h"
+#include "tas_kernels.hip"
+
+using namespace ktas;
+
+namespace {
+
+constexpr int kEvalsPerFillBlock = kEvalsPerBlock;
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) n = std::max<size_t>(count, 1);
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+template <typename T>
+struct HostBuf {  // pinned host staging
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc(&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) n = std::max<size_t>(count, 1);
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+// libdivide-style u64 magic for exact division by an invariant divisor d >= 1.
+void compute_magic(uint64_t d, DevTerm* t) {
+  t->magic = 0;
+  t->shift = 0;
+  t->add = 0;
+  t->pow2 = 0;
+  int fl = 63 - __builtin_clzll(d);
+  if ((d & (d - 1)) == 0) {
+    t->pow2 = 1;
+    t->shift = uint8_t(fl);
+    return;
+  }
+  unsigned __int128 num = (unsigned __int128)1 << (64 + fl);
+  uint64_t proposed = uint64_t(num / d);
+  uint64_t rem = uint64_t(num % d);
+  uint64_t e = d - rem;
+  if (e < (uint64_t(1) << fl)) {
+    t->shift = uint8_t(fl);
+  } else {
+    proposed += proposed;
+    uint64_t twice = rem + rem;
+    if (twice >= d || twice < rem) proposed += 1;
+    t->shift = uint8_t(fl);
+    t->add = 1;
+  }
+  t->magic = proposed + 1;
+}
+
+}  // namespace
+
+struct kueue_tas_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::string err;
+  int list_cap = 1024;
+  int max_batch = 1024;
+  // snapshot
+  bool loaded = false;
+  DevSnap snap{};
+  int maxD = 0;
+  std::vector<int32_t> h_level_sizes;
+  DevBuf<int32_t> d_child_off, d_id_rank, d_taint_profile, d_labels;
+  DevBuf<int64_t> d_free, d_usage;
+  DevBuf<uint32_t> d_free_present, d_usage_present;
+  // batch
+  DevBuf<DevEval> d_evals;
+  DevBuf<DevTerm> d_terms;
+  DevBuf<int32_t> d_taint_table;
+  DevBuf<kueue_tas_assumed> d_assumed;
+  DevBuf<int32_t> d_counters;
+  DevBuf<int32_t> d_stats;  // taint counts | res counts | sel counts
+  DevBuf<kueue_tas_eval_out> d_out;
+  DevBuf<int32_t> d_entries;
+  DevBuf<uint64_t> d_scratch;
+  DevBuf<kueue_tas_delta> d_deltas;
+  HostBuf<DevEval> h_evals;
+  HostBuf<DevTerm> h_terms;
+  float last_ms[4] = {0, 0, 0, 0};
+};
+
+static int fail(kueue_tas_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(c, x)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(c, KUEUE_TAS_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+extern "C" {
+
+int kueue_tas_abi_version(void) { return KUEUE_TAS_ABI_VERSION; }
+
+kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
+  auto* c = new kueue_tas_ctx();
+  if (cfg) {
+    c->device = cfg->device;
+    if (cfg->list_cap > 0) {
+      int lc = 64;
+      while (lc < cfg->list_cap && lc < 2048) lc <<= 1;
+      c->list_cap = lc;
+    }
+    if (cfg->max_batch > 0) c->max_batch = cfg->max_batch;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= c->device) {
+    c->err = "no HIP device available";
+    delete c;
+    return nullptr;
+  }
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  return c;
+}
+
+void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->d_child_off.release();
+  c->d_id_rank.release();
+  c->d_taint_profile.release();
+  c->d_labels.release();
+  c->d_free.release();
+  c->d_usage.release();
+  c->d_free_present.release();
+  c->d_usage_present.release();
+  c->d_evals.release();
+  c->d_terms.release();
+  c->d_taint_table.release();
+  c->d_assumed.release();
+  c->d_counters.release();
+  c->d_stats.release();
+  c->d_out.release();
+  c->d_entries.release();
+  c->d_scratch.release();
+  c->d_deltas.release();
+  c->h_evals.release();
+  c->h_terms.release();
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* kueue_tas_last_error(kueue_tas_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) {
+  if (!c || !d) return KUEUE_TAS_EINVAL;
+  if (d->num_levels < 1 || d->num_levels > KUEUE_TAS_MAX_LEVELS) return fail(c, KUEUE_TAS_EINVAL, "num_levels");
+  if (d->num_cols < 0 || d->num_cols > KUEUE_TAS_MAX_COLS) return fail(c, KUEUE_TAS_EINVAL, "num_cols");
+  HIPCHK(c, hipSetDevice(c->device));
+  DevSnap s{};
+  s.L = d->num_levels;
+  s.R = d->num_cols;
+  s.K = d->num_label_cols;
+  s.lowest_is_hostname = d->lowest_is_hostname;
+  int64_t off = 0;
+  int maxD = 0;
+  c->h_level_sizes.assign(d->level_sizes, d->level_sizes + s.L);
+  for (int l = 0; l < s.L; l++) {
+    s.level_size[l] = d->level_sizes[l];
+    s.level_off[l] = int32_t(off);
+    off += d->level_sizes[l];
+    maxD = std::max(maxD, d->level_sizes[l]);
+  }
+  s.level_off[s.L] = int32_t(off);
+  s.SD = int32_t(off);
+  s.N = d->level_sizes[s.L - 1];
+  const size_t N = size_t(s.N);
+  // CSR offsets
+  size_t nco = 0;
+  for (int l = 0; l + 1 < s.L; l++) {
+    s.child_base[l] = int32_t(nco);
+    nco += size_t(d->level_sizes[l]) + 1;
+  }
+  HIPCHK(c, c->d_child_off.ensure(nco));
+  if (nco) HIPCHK(c, hipMemcpyAsync(c->d_child_off.p, d->child_offsets, nco * 4, hipMemcpyHostToDevice, c->stream));
+  s.child_off = c->d_child_off.p;
+  HIPCHK(c, c->d_free.ensure(size_t(s.R) * N));
+  HIPCHK(c, c->d_usage.ensure(size_t(s.R) * N));
+  if (s.R && N) {
+    HIPCHK(c, hipMemcpyAsync(c->d_free.p, d->free_capacity, size_t(s.R) * N * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_usage.p, d->tas_usage, size_t(s.R) * N * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(c, c->d_free_present.ensure(N));
+  HIPCHK(c, c->d_usage_present.ensure(N));
+  if (N) {
+    HIPCHK(c, hipMemcpyAsync(c->d_free_present.p, d->free_present, N * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, d->usage_present, N * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  s.free_cap = c->d_free.p;
+  s.tas_usage = c->d_usage.p;
+  s.free_present = c->d_free_present.p;
+  s.usage_present = c->d_usage_present.p;
+  s.taint_profile = nullptr;
+  if (d->taint_profile && N) {
+    HIPCHK(c, c->d_taint_profile.ensure(N));
+    HIPCHK(c, hipMemcpyAsync(c->d_taint_profile.p, d->taint_profile, N * 4, hipMemcpyHostToDevice, c->stream));
+    s.taint_profile = c->d_taint_profile.p;
+  }
+  s.label_values = nullptr;
+  if (s.K > 0 && d->label_values && N) {
+    HIPCHK(c, c->d_labels.ensure(size_t(s.K) * N));
+    HIPCHK(c, hipMemcpyAsync(c->d_labels.p, d->label_values, size_t(s.K) * N * 4, hipMemcpyHostToDevice, c->stream));
+    s.label_values = c->d_labels.p;
+  }
+  s.id_rank = nullptr;
+  if (d->domain_id_rank && off) {
+    HIPCHK(c, c->d_id_rank.ensure(size_t(off)));
+    HIPCHK(c, hipMemcpyAsync(c->d_id_rank.p, d->domain_id_rank, size_t(off) * 4, hipMemcpyHostToDevice, c->stream));
+    s.id_rank = c->d_id_rank.p;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->snap = s;
+  c->maxD = maxD;
+  c->loaded = true;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n,
+                                    const uint32_t* usage_present_or_null) {
+  if (!c || !c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
+  HIPCHK(c, hipSetDevice(c->device));
+  for (size_t i = 0; i < n; i++)
+    if (deltas[i].leaf < 0 || deltas[i].leaf >= c->snap.N || deltas[i].col < 0 || deltas[i].col >= c->snap.R)
+      return fail(c, KUEUE_TAS_EINVAL, "delta out of range");
+  if (n) {
+    HIPCHK(c, c->d_deltas.ensure(n));
+    HIPCHK(c, hipMemcpyAsync(c->d_deltas.p, deltas, n * sizeof(kueue_tas_delta), hipMemcpyHostToDevice, c->stream));
+    int blocks = int((n + 255) / 256);
+    hipLaunchKernelGGL(apply_deltas_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_usage.p, c->d_usage_present.p,
+                       c->snap.N, c->d_deltas.p, int(n));
+    HIPCHK(c, hipGetLastError());
+  }
+  if (usage_present_or_null)
+    HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, usage_present_or_null, size_t(c->snap.N) * 4, hipMemcpyHostToDevice,
+                             c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
+static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
+                      size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
+                      kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap, int32_t* taint_counts,
+                      int32_t* res_counts, float* ms) {
+  const DevSnap& s = c->snap;
+  // ---- compile requests to device form (magic numbers) ----
+  HIPCHK(c, c->h_evals.ensure(n));
+  size_t nterms = 0;
+  int maxt = 1;
+  for (size_t i = 0; i < n; i++) {
+    const auto& r = reqs[i];
+    if (r.num_req < 0 || r.num_req > KUEUE_TAS_MAX_COLS || r.num_leader_req < 0 || r.num_leader_req > KUEUE_TAS_MAX_COLS)
+      return fail(c, KUEUE_TAS_EINVAL, "num_req");
+    if (r.slice_size == 0) return fail(c, KUEUE_TAS_EINVAL, "slice_size == 0 (integer divide by zero)");
+    if (r.requested_level < 0 || r.requested_level >= s.L || r.slice_level < 0 || r.slice_level >= s.L)
+      return fail(c, KUEUE_TAS_EINVAL, "level out of range");
+    if (r.num_selectors < 0 || r.num_selectors > KUEUE_TAS_MAX_SELECTORS) return fail(c, KUEUE_TAS_EINVAL, "num_selectors");
+    if (r.num_selectors > 0 && s.K == 0) return fail(c, KUEUE_TAS_EINVAL, "selectors without label columns");
+    nterms += size_t(r.num_req + r.num_leader_req);
+    maxt = std::max(maxt, std::max(r.num_req, r.num_leader_req));
+  }
+  HIPCHK(c, c->h_terms.ensure(std::max<size_t>(nterms, 1)));
+  size_t tp = 0;
+  for (size_t i = 0; i < n; i++) {
+    const auto& r = reqs[i];
+    DevEval& e = c->h_evals.p[i];
+    memset(&e, 0, sizeof e);
+    e.flags = r.flags;
+    e.count = r.count;
+    e.slice_size = r.slice_size;
+    e.requested_level = r.requested_level;
+    e.slice_level = r.slice_level;
+    e.nsel = r.num_selectors;
+    e.taint_table = r.taint_table;
+    e.assumed_begin = r.assumed_begin;
+    e.assumed_end = r.assumed_end;
+    e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
+    for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
+      e.layer_level[k] = r.layer_level[k];
+      e.layer_size[k] = r.layer_size[k] == 0 ? 1 : r.layer_size[k];
+    }
+    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) e.ssal[l] = r.slice_size_at_level[l];
+    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+      e.sel_col[k] = r.sel_col[k];
+      e.sel_val[k] = r.sel_val[k];
+    }
+    auto add_terms = [&](const int32_t* cols, const int64_t* vals, int cnt, uint32_t* mask) -> int {
+      int prev = -1;
+      for (int k = 0; k < cnt; k++) {
+        if (cols[k] < 0 || cols[k] >= s.R || cols[k] <= prev) return -1;
+        prev = cols[k];
+        DevTerm& t = c->h_terms.p[tp++];
+        memset(&t, 0, sizeof t);
+        t.col = cols[k];
+        t.val = vals[k];
+        t.neg = vals[k] < 0;
+        uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
+        if (mag) compute_magic(mag, &t);
+        *mask |= 1u << cols[k];
+      }
+      return 0;
+    };
+    e.term_begin = int32_t(tp);
+    e.nreq = r.num_req;
+    if (add_terms(r.req_col, r.req_val, r.num_req, &e.req_mask)) return fail(c, KUEUE_TAS_EINVAL, "req columns");
+    e.lead_begin = int32_t(tp);
+    e.nlead = (r.flags & KUEUE_TAS_F_LEADER) ? r.num_leader_req : 0;
+    if (add_terms(r.leader_col, r.leader_val, e.nlead, &e.lead_mask)) return fail(c, KUEUE_TAS_EINVAL, "leader columns");
+  }
+  // ---- device buffers ----
+  const int64_t SD = s.SD;
+  const int64_t ctr_stride = 5 * SD;
+  int64_t lcap = int64_t(c->maxD) * 2 + 64;
+  const int64_t scratch_stride = 6 * lcap;
+  HIPCHK(c, c->d_evals.ensure(n));
+  HIPCHK(c, c->d_terms.ensure(std::max<size_t>(nterms, 1)));
+  HIPCHK(c, c->d_taint_table.ensure(std::max<size_t>(taint_table_len, 1)));
+  HIPCHK(c, c->d_assumed.ensure(std::max<size_t>(num_assumed, 1)));
+  HIPCHK(c, c->d_counters.ensure(size_t(n) * size_t(ctr_stride)));
+  const size_t nt = size_t(std::max(num_taints, 0));
+  const size_t stats_len = n * nt + n * size_t(s.R) + n;
+  HIPCHK(c, c->d_stats.ensure(stats_len));
+  HIPCHK(c, c->d_out.ensure(n));
+  HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));
+  HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
+
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_evals.p, c->h_evals.p, n * sizeof(DevEval), hipMemcpyHostToDevice, c->stream));
+  if (nterms)
+    HIPCHK(c, hipMemcpyAsync(c->d_terms.p, c->h_terms.p, nterms * sizeof(DevTerm), hipMemcpyHostToDevice, c->stream));
+  if (taint_table_len)
+    HIPCHK(c, hipMemcpyAsync(c->d_taint_table.p, taint_table, taint_table_len * 4, hipMemcpyHostToDevice, c->stream));
+  if (num_assumed)
+    HIPCHK(c, hipMemcpyAsync(c->d_assumed.p, assumed, num_assumed * sizeof(kueue_tas_assumed), hipMemcpyHostToDevice,
+                             c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, stats_len * 4, c->stream));
+
+  DevBatch b{};
+  b.evals = c->d_evals.p;
+  b.terms = c->d_terms.p;
+  b.taint_table = c->d_taint_table.p;
+  b.assumed = c->d_assumed.p;
+  b.n = int32_t(n);
+  b.num_taints = int32_t(nt);
+  b.ctr_stride = ctr_stride;
+  b.counters = c->d_counters.p;
+  b.taint_counts = c->d_stats.p;
+  b.res_counts = c->d_stats.p + n * nt;
+  b.sel_counts = c->d_stats.p + n * nt + n * size_t(s.R);
+  b.out = c->d_out.p;
+  b.entries = c->d_entries.p;
+  b.entry_cap = entry_cap;
+  b.scratch_stride = scratch_stride;
+  b.scratch = c->d_scratch.p;
+  b.list_cap = c->list_cap;
+
+  // K1
+  if (s.N > 0) {
+    dim3 grid((s.N + 255) / 256, unsigned((n + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
+    if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
+    else if (maxt <= 8) hipLaunchKernelGGL(fill_leaves_kernel<8>, grid, dim3(256), 0, c->stream, s, b);
+    else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
+    else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  // K2
+  for (int l = s.L - 2; l >= 0; l--) {
+    dim3 grid((s.level_size[l] + 255) / 256, unsigned(n));
+    if (s.level_size[l] > 0) hipLaunchKernelGGL(rollup_level_kernel, grid, dim3(256), 0, c->stream, s, b, l);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  // K3
+  {
+    const int waves = 4;
+    size_t lds = size_t(waves) * size_t(c->list_cap) * 16;
+    dim3 grid(unsigned((n + waves - 1) / waves));
+    hipLaunchKernelGGL(select_kernel, grid, dim3(64 * waves), lds, c->stream, s, b);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_out.p, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(entries, c->d_entries.p, n * size_t(entry_cap) * 2 * 4, hipMemcpyDeviceToHost, c->stream));
+  if (taint_counts && nt)
+    HIPCHK(c, hipMemcpyAsync(taint_counts, b.taint_counts, n * nt * 4, hipMemcpyDeviceToHost, c->stream));
+  if (res_counts && s.R)
+    HIPCHK(c, hipMemcpyAsync(res_counts, b.res_counts, n * size_t(s.R) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+  (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
+  (void)hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
+  ms[0] += t01;
+  ms[1] += t12;
+  ms[2] += t23;
+  ms[3] += t03;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
+                         size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
+                         size_t num_assumed, kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap,
+                         int32_t* taint_counts, int32_t* res_counts) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (entry_cap < 1) return fail(c, KUEUE_TAS_EINVAL, "entry_cap");
+  HIPCHK(c, hipSetDevice(c->device));
+  float ms[4] = {0, 0, 0, 0};
+  const size_t chunk = size_t(c->max_batch);
+  for (size_t i0 = 0; i0 < n; i0 += chunk) {
+    size_t m = std::min(chunk, n - i0);
+    int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
+                        entries + i0 * size_t(entry_cap) * 2, entry_cap,
+                        taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
+                        res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms);
+    if (rc) return rc;
+  }
+  memcpy(c->last_ms, ms, sizeof ms);
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_timings(kueue_tas_ctx* c, float* ms4) {
+  if (!c || !ms4) return KUEUE_TAS_EINVAL;
+  memcpy(ms4, c->last_ms, sizeof c->last_ms);
+  return KUEUE_TAS_OK;
+}
+
+}  // extern "C"

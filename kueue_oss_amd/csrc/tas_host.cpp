@@ -1,0 +1,1177 @@
+// tas_host.cpp — host layer of libkueue_tas.so: the C++ mirror of the Go API
+// of Kueue's TAS evaluation path on top of the device layer.
+//
+// Mirrors (reference /root/reference/pkg/cache/scheduler/):
+//   TASFlavorCache.snapshot + caches       tas_flavor.go:118-171, tas_nodes_cache.go:38-72,
+//                                          tas_non_tas_pod_cache.go:46-120
+//   TASFlavorSnapshot.addNode/initialize   tas_flavor_snapshot.go:160-241
+//   FindTopologyAssignmentsForFlavor       :519-594 (groups, leader/workers :596-609,
+//                                          assumedUsage :658-666, stop at first failure)
+//   findTopologyAssignment prelude         :804-897 (requests + pods:1, slice size/levels,
+//                                          validation reasons, tolerations, selector)
+//   notFitMessage / multiLayerNotFitMessage / ExclusionStats.formatReasons
+//                                          :1721-1793, :480-499
+// Everything between the prelude and buildAssignment runs on the GPU
+// (tas_kernels.hip).  This layer never evaluates a placement on the CPU: if the
+// device library or a GPU is unavailable, creation fails loudly.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kueue_tas.h"
+#include "json_reader.h"
+
+namespace kueue_tas {
+
+using Requests = std::map<std::string, int64_t>;
+static const char* kHostname = "kubernetes.io/hostname";
+
+static int64_t add64(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
+static int64_t sub64(int64_t a, int64_t b) { return int64_t(uint64_t(a) - uint64_t(b)); }
+static int64_t mul64(int64_t a, int64_t b) { return int64_t(uint64_t(a) * uint64_t(b)); }
+static void req_add(Requests& r, const Requests& o) {
+  for (auto& kv : o) r[kv.first] = add64(r[kv.first], kv.second);
+}
+static void req_sub(Requests& r, const Requests& o) {
+  for (auto& kv : o) r[kv.first] = sub64(r[kv.first], kv.second);
+}
+static int32_t go_div32(int32_t a, int32_t b) {
+  if (b == -1) return int32_t(0u - uint32_t(a));
+  return a / b;
+}
+
+struct Taint {
+  std::string key, value, effect;
+  bool operator==(const Taint& o) const { return key == o.key && value == o.value && effect == o.effect; }
+  bool operator<(const Taint& o) const {
+    return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect);
+  }
+};
+struct Toleration {
+  std::string key, op, value, effect;
+  bool operator<(const Toleration& o) const {
+    return std::tie(key, op, value, effect) < std::tie(o.key, o.op, o.value, o.effect);
+  }
+};
+
+// Taint.ToString (vendor/k8s.io/api/core/v1/taint.go:28-39)
+static std::string taint_string(const Taint& t) {
+  if (t.effect.empty()) return t.value.empty() ? t.key : t.key + "=" + t.value + ":";
+  return t.value.empty() ? t.key + ":" + t.effect : t.key + "=" + t.value + ":" + t.effect;
+}
+
+// content.IsDecimalInteger + strconv.ParseInt (validate/content/decimal_int.go:30-62)
+static bool decimal_int(const std::string& v, int64_t* out) {
+  if (v.empty()) return false;
+  size_t i = v[0] == '-' ? 1 : 0;
+  if (i == 1 && v.size() == 1) return false;
+  if (v[i] == '0') {
+    if (v.size() == 1) {
+      *out = 0;
+      return true;
+    }
+    return false;
+  }
+  unsigned __int128 acc = 0;
+  for (size_t j = i; j < v.size(); j++) {
+    if (v[j] < '0' || v[j] > '9') return false;
+    acc = acc * 10 + unsigned(v[j] - '0');
+    if (acc > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (i == 0 && acc == ((unsigned __int128)1 << 63)) return false;
+  *out = i ? int64_t(uint64_t(0) - uint64_t(acc)) : int64_t(acc);
+  return true;
+}
+
+// Toleration.ToleratesTaint with enableComparisonOperators=true
+// (vendor/k8s.io/api/core/v1/toleration.go:52-112; tas_flavor_snapshot.go:1586)
+static bool tolerates(const Toleration& t, const Taint& x) {
+  if (!t.effect.empty() && t.effect != x.effect) return false;
+  if (!t.key.empty() && t.key != x.key) return false;
+  if (t.op.empty() || t.op == "Equal") return t.value == x.value;
+  if (t.op == "Exists") return true;
+  if (t.op == "Lt" || t.op == "Gt") {
+    int64_t a, b;
+    if (!decimal_int(t.value, &a) || !decimal_int(x.value, &b)) return false;
+    return t.op == "Lt" ? b < a : b > a;
+  }
+  return false;
+}
+
+static std::string go_quote(const std::string& s) {  // strconv.Quote for ASCII input
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += char(c);
+    } else if (c == '\n') o += "\\n";
+    else if (c == '\t') o += "\\t";
+    else if (c == '\r') o += "\\r";
+    else if (c < 0x20 || c == 0x7f) {
+      char b[8];
+      snprintf(b, sizeof b, "\\x%02x", c);
+      o += b;
+    } else o += char(c);
+  }
+  return o + "\"";
+}
+
+struct NodeInfo {
+  std::string name;
+  std::map<std::string, std::string> labels;
+  std::vector<Taint> taints;
+  Requests allocatable;
+};
+
+struct SliceConstraint {
+  std::string topology;
+  int32_t size;
+};
+struct TopologyRequest {  // kueue.PodSetTopologyRequest (apis/kueue/v1beta2/workload_types.go:165-249)
+  std::optional<std::string> required, preferred, sliceRequiredTopology;
+  std::optional<bool> unconstrained;
+  std::optional<int32_t> sliceSize;
+  std::vector<SliceConstraint> constraints;
+};
+struct TASPodSetRequests {  // tas_flavor_snapshot.go:356-367
+  std::string name;
+  std::optional<TopologyRequest> topologyRequest;
+  Requests singlePodRequests;
+  int32_t count = 0;
+  bool implied = false;
+  std::optional<std::string> podSetGroupName;
+  std::vector<Toleration> tolerations;
+  std::optional<std::map<std::string, std::string>> nodeSelector;
+};
+struct DomainAssignment {
+  int32_t leaf;
+  int32_t count;
+};
+struct PodSetResult {
+  std::string name;
+  bool has_assignment = false;
+  std::vector<DomainAssignment> domains;  // leaf indices (lexicographic order)
+  std::string reason;
+};
+
+struct Gates {  // pkg/features/kube_features.go (TASProfileMixed: Beta, default true)
+  bool profileMixed = true, multiLayer = false, balanced = false, elastic = false;
+};
+
+// One findTopologyAssignment call compiled for the device.
+struct GroupEval {
+  bool compiled = false;
+  const TASPodSetRequests* workers = nullptr;
+  const TASPodSetRequests* leader = nullptr;
+  std::vector<const TASPodSetRequests*> members;  // all PodSets of the group (result order)
+  std::string early_reason;                        // host-side validation failure
+  kueue_tas_eval_req req{};
+  int32_t slice_size = 1;
+  std::vector<std::string> layer_names;            // multi-layer message labels
+  std::vector<int32_t> taint_row;                  // per taint profile
+};
+
+struct Workload {
+  std::vector<TASPodSetRequests> podsets;
+  std::vector<GroupEval> groups;
+};
+
+class FlavorSnapshot {
+ public:
+  std::string topologyName = "default";
+  std::vector<std::string> levelKeys;
+  std::vector<Toleration> flavorTolerations;
+  bool lowestIsHostname = false;
+  Gates gates;
+
+  // tree (levels sorted lexicographically by levelValues)
+  std::vector<std::vector<std::vector<std::string>>> values;  // [l][i]
+  std::vector<std::vector<int32_t>> childOff;                 // [l][D_l + 1]
+  std::vector<std::string> leafId;
+  std::unordered_map<std::string, int32_t> leafById;
+  std::vector<const NodeInfo*> leafNode;
+  std::vector<Requests> freeCap, tasUsage;
+  std::vector<std::vector<int32_t>> idRank;  // [l][i]
+  // columns / profiles / labels
+  std::vector<std::string> cols;
+  std::map<std::string, int32_t> colByName;
+  std::vector<std::vector<Taint>> profiles;
+  std::vector<int32_t> leafProfile;
+  std::vector<std::string> taintStrings;
+  std::map<std::string, int32_t> taintIdByString;
+  std::vector<std::string> labelKeys;
+  std::map<std::string, int32_t> labelCol;
+  std::vector<std::map<std::string, int32_t>> labelDict;
+  std::vector<int32_t> labelValues;  // [K][N]
+  std::vector<NodeInfo> nodes;
+
+  kueue_tas_ctx* ctx = nullptr;
+  bool dirty = true;
+  std::string err;
+  kueue_tas_config cfg{};
+
+  ~FlavorSnapshot() {
+    if (ctx) kueue_tas_ctx_destroy(ctx);
+  }
+
+  int N() const { return values.empty() ? 0 : int(values.back().size()); }
+  int L() const { return int(levelKeys.size()); }
+
+  // ---- construction (harness semantics: tas_cache_test.go:6270-6300) ----
+  void build(const kjson::Node& c) {
+    for (auto& l : c["levels"].items) levelKeys.push_back(l.s());
+    if (levelKeys.empty()) throw std::runtime_error("no topology levels");
+    if (int(levelKeys.size()) > KUEUE_TAS_MAX_LEVELS) throw std::runtime_error("too many topology levels");
+    lowestIsHostname = levelKeys.back() == kHostname;
+    if (!c["topologyName"].null()) topologyName = c["topologyName"].s();
+    for (auto& t : c["flavorTolerations"].items)
+      flavorTolerations.push_back({t["key"].s(), t["operator"].s(), t["value"].s(), t["effect"].s()});
+    const kjson::Node& fg = c["featureGates"];
+    if (auto p = fg.find("TASProfileMixed")) gates.profileMixed = p->b();
+    if (auto p = fg.find("TASMultiLayerTopology")) gates.multiLayer = p->b();
+    if (auto p = fg.find("TASBalancedPlacement")) gates.balanced = p->b();
+    if (auto p = fg.find("ElasticJobsViaWorkloadSlicesWithTAS")) gates.elastic = p->b();
+    std::map<std::string, std::string> flavorLabels;
+    for (auto& kv : c["nodeLabels"].fields) flavorLabels[kv.first] = kv.second.s();
+
+    // nodesCache.sync (Ready && !Unschedulable) keyed by name, then find (NodeMatchesFlavor)
+    std::vector<std::string> order;
+    std::map<std::string, const kjson::Node*> byName;
+    for (auto& n : c["nodes"].items) {
+      const std::string& name = n["name"].s();
+      bool ready = false;
+      for (auto& cond : n["conditions"].items)
+        if (cond["type"].s() == "Ready") {
+          ready = cond["status"].s() == "True";
+          break;
+        }
+      if (!n["unschedulable"].b() && ready) {
+        if (!byName.count(name)) order.push_back(name);
+        byName[name] = &n;
+      } else if (byName.count(name)) {
+        byName.erase(name);
+        order.erase(std::find(order.begin(), order.end(), name));
+      }
+    }
+    nodes.reserve(order.size());
+    for (auto& name : order) {
+      const kjson::Node& n = *byName[name];
+      NodeInfo ni;
+      ni.name = name;
+      for (auto& kv : n["labels"].fields) ni.labels[kv.first] = kv.second.s();
+      bool match = true;
+      for (auto& kv : flavorLabels) {
+        auto it = ni.labels.find(kv.first);
+        if ((it == ni.labels.end() ? std::string() : it->second) != kv.second) match = false;
+      }
+      for (auto& l : levelKeys)
+        if (!ni.labels.count(l)) match = false;
+      if (!match) continue;
+      for (auto& t : n["taints"].items) ni.taints.push_back({t["key"].s(), t["value"].s(), t["effect"].s()});
+      for (auto& kv : n["allocatable"].fields) ni.allocatable[kv.first] = kv.second.i64();
+      nodes.push_back(std::move(ni));
+    }
+    // addNode (:160-195): leaves keyed by hostname or DomainID(levelValues)
+    struct LeafTmp {
+      std::vector<std::string> lv;
+      const NodeInfo* node;
+      Requests cap;
+    };
+    std::vector<LeafTmp> tmp;
+    std::unordered_map<std::string, int32_t> tmpById;
+    std::unordered_map<std::string, std::string> nodeToLeaf;
+    for (auto& ni : nodes) {
+      std::vector<std::string> lv;
+      for (auto& k : levelKeys) {
+        auto it = ni.labels.find(k);
+        lv.push_back(it == ni.labels.end() ? "" : it->second);
+      }
+      std::string id;
+      if (lowestIsHostname) {
+        auto it = ni.labels.find(kHostname);
+        id = it == ni.labels.end() ? "" : it->second;
+      } else {
+        for (size_t i = 0; i < lv.size(); i++) id += (i ? "," : "") + lv[i];
+      }
+      auto it = tmpById.find(id);
+      if (it == tmpById.end()) {
+        tmpById[id] = int32_t(tmp.size());
+        tmp.push_back({lv, lowestIsHostname ? &ni : nullptr, {}});
+        it = tmpById.find(id);
+      }
+      req_add(tmp[it->second].cap, ni.allocatable);
+      nodeToLeaf[ni.name] = id;
+    }
+    // sort leaves by levelValues; build levels + CSR
+    std::vector<int32_t> perm(tmp.size());
+    for (size_t i = 0; i < perm.size(); i++) perm[i] = int32_t(i);
+    std::sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return tmp[a].lv < tmp[b].lv; });
+    const int L = this->L();
+    values.assign(L, {});
+    childOff.assign(L > 1 ? L - 1 : 0, {});
+    std::vector<std::vector<std::string>> sortedLeaves;
+    for (int32_t p : perm) sortedLeaves.push_back(tmp[p].lv);
+    for (int l = 0; l < L; l++) {
+      auto& lvl = values[l];
+      for (auto& lv : sortedLeaves) {
+        std::vector<std::string> pre(lv.begin(), lv.begin() + l + 1);
+        if (lvl.empty() || lvl.back() != pre) lvl.push_back(std::move(pre));
+      }
+    }
+    for (int l = 0; l + 1 < L; l++) {
+      auto& off = childOff[l];
+      off.assign(values[l].size() + 1, 0);
+      size_t j = 0;
+      for (size_t i = 0; i < values[l].size(); i++) {
+        off[i] = int32_t(j);
+        while (j < values[l + 1].size() &&
+               std::equal(values[l][i].begin(), values[l][i].end(), values[l + 1][j].begin()))
+          j++;
+      }
+      off[values[l].size()] = int32_t(j);
+    }
+    const int N = this->N();
+    leafId.resize(N);
+    leafNode.resize(N);
+    freeCap.resize(N);
+    tasUsage.resize(N);
+    for (int i = 0; i < N; i++) {
+      const LeafTmp& t = tmp[perm[i]];
+      std::string id;
+      if (lowestIsHostname) {
+        auto it = t.node->labels.find(kHostname);
+        id = it == t.node->labels.end() ? "" : it->second;
+      } else {
+        for (size_t k = 0; k < t.lv.size(); k++) id += (k ? "," : "") + t.lv[k];
+      }
+      leafId[i] = id;
+      leafById[id] = i;
+      leafNode[i] = t.node;
+      freeCap[i] = t.cap;
+    }
+    // DomainID ranks per level (multiLayerNotFitMessage tie-break)
+    idRank.assign(L, {});
+    for (int l = 0; l < L; l++) {
+      size_t D = values[l].size();
+      std::vector<std::string> ids(D);
+      for (size_t i = 0; i < D; i++) {
+        if (l == L - 1) {
+          ids[i] = leafId[i];
+        } else {
+          for (size_t k = 0; k < values[l][i].size(); k++) ids[i] += (k ? "," : "") + values[l][i][k];
+        }
+      }
+      std::vector<int32_t> ord(D);
+      for (size_t i = 0; i < D; i++) ord[i] = int32_t(i);
+      std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return ids[a] < ids[b]; });
+      idRank[l].assign(D, 0);
+      for (size_t r = 0; r < D; r++) idRank[l][ord[r]] = int32_t(r);
+    }
+    // TAS usage (TASFlavorCache.updateUsage, tas_flavor.go:154-171)
+    std::map<std::string, Requests> usage;
+    for (auto& u : c["tasUsage"].items) {
+      std::string id;
+      for (size_t k = 0; k < u["values"].items.size(); k++) id += (k ? "," : "") + u["values"].items[k].s();
+      int64_t cnt = u["count"].i64();
+      Requests& dst = usage[id];
+      for (auto& kv : u["singlePodRequests"].fields) dst[kv.first] = add64(dst[kv.first], mul64(kv.second.i64(), cnt));
+      dst["pods"] = add64(dst["pods"], cnt);
+    }
+    for (auto& kv : usage) {
+      auto it = leafById.find(kv.first);
+      if (it != leafById.end()) req_add(tasUsage[it->second], kv.second);
+    }
+    // non-TAS pods (tas_non_tas_pod_cache.go:46-120)
+    std::map<std::string, std::pair<std::string, Requests>> podUsage;
+    std::map<std::string, Requests> nodeUsage;
+    auto remove_usage = [&](const std::string& node, const Requests& u) {
+      auto it = nodeUsage.find(node);
+      if (it == nodeUsage.end()) return;
+      req_sub(it->second, u);
+      it->second["pods"] = sub64(it->second["pods"], 1);
+      if (it->second["pods"] <= 0) nodeUsage.erase(it);
+    };
+    for (auto& p : c["pods"].items) {
+      std::string key = p["namespace"].s() + "/" + p["name"].s();
+      const std::string& phase = p["phase"].s();
+      auto old = podUsage.find(key);
+      if (old != podUsage.end()) remove_usage(old->second.first, old->second.second);
+      if (phase == "Succeeded" || phase == "Failed") {
+        podUsage.erase(key);
+        continue;
+      }
+      Requests r;
+      for (auto& kv : p["requests"].fields) r[kv.first] = kv.second.i64();
+      const std::string& node = p["nodeName"].s();
+      podUsage[key] = {node, r};
+      Requests& nu = nodeUsage[node];
+      req_add(nu, r);
+      nu["pods"] = add64(nu["pods"], 1);
+    }
+    for (auto& kv : nodeUsage) {
+      auto it = nodeToLeaf.find(kv.first);
+      if (it != nodeToLeaf.end()) req_sub(freeCap[leafById[it->second]], kv.second);
+    }
+    // resource columns
+    std::set<std::string> names;
+    for (int i = 0; i < N; i++) {
+      for (auto& kv : freeCap[i]) names.insert(kv.first);
+      for (auto& kv : tasUsage[i]) names.insert(kv.first);
+    }
+    names.insert("pods");
+    set_columns(names);
+    // taint profiles + label dictionaries (filters apply only with hostname leaves)
+    leafProfile.assign(N, 0);
+    if (lowestIsHostname) {
+      std::map<std::vector<Taint>, int32_t> pid;
+      for (int i = 0; i < N; i++) {
+        std::vector<Taint> ts;
+        for (auto& t : leafNode[i]->taints)
+          if (t.effect == "NoSchedule" || t.effect == "NoExecute") ts.push_back(t);
+        auto it = pid.find(ts);
+        if (it == pid.end()) {
+          it = pid.emplace(ts, int32_t(profiles.size())).first;
+          profiles.push_back(ts);
+        }
+        leafProfile[i] = it->second;
+        for (auto& t : ts) {
+          std::string s = taint_string(t);
+          if (!taintIdByString.count(s)) {
+            taintIdByString[s] = int32_t(taintStrings.size());
+            taintStrings.push_back(s);
+          }
+        }
+      }
+      std::set<std::string> keys;
+      for (int i = 0; i < N; i++)
+        for (auto& kv : leafNode[i]->labels) keys.insert(kv.first);
+      for (auto& k : keys) {
+        labelCol[k] = int32_t(labelKeys.size());
+        labelKeys.push_back(k);
+      }
+      labelDict.assign(labelKeys.size(), {});
+      labelValues.assign(labelKeys.size() * size_t(N), 0);
+      for (size_t k = 0; k < labelKeys.size(); k++) {
+        for (int i = 0; i < N; i++) {
+          auto it = leafNode[i]->labels.find(labelKeys[k]);
+          if (it == leafNode[i]->labels.end()) continue;
+          auto& dict = labelDict[k];
+          auto d = dict.find(it->second);
+          if (d == dict.end()) d = dict.emplace(it->second, int32_t(dict.size()) + 1).first;
+          labelValues[k * size_t(N) + i] = d->second;
+        }
+      }
+    }
+    if (profiles.empty()) profiles.push_back({});
+  }
+
+  void set_columns(const std::set<std::string>& names) {
+    cols.assign(names.begin(), names.end());
+    colByName.clear();
+    for (size_t i = 0; i < cols.size(); i++) colByName[cols[i]] = int32_t(i);
+    if (cols.size() > KUEUE_TAS_MAX_COLS) throw std::runtime_error("too many resource columns");
+    dirty = true;
+  }
+  // Requests may name resources no node has: they become all-absent columns.
+  // Returns true when the column set changed (compiled requests are stale).
+  bool ensure_columns_for(const std::vector<TASPodSetRequests>& podsets) {
+    std::set<std::string> names(cols.begin(), cols.end());
+    size_t before = names.size();
+    for (auto& p : podsets)
+      for (auto& kv : p.singlePodRequests) names.insert(kv.first);
+    if (names.size() == before) return false;
+    set_columns(names);
+    return true;
+  }
+
+  int upload() {
+    if (!dirty) return 0;
+    if (!ctx) {
+      ctx = kueue_tas_ctx_create(&cfg);
+      if (!ctx) {
+        err = "kueue_tas_ctx_create failed: no usable HIP device (the TAS path has no CPU fallback)";
+        return KUEUE_TAS_EDEVICE;
+      }
+    }
+    const int L = this->L(), N = this->N(), R = int(cols.size());
+    std::vector<int32_t> sizes(L), co;
+    for (int l = 0; l < L; l++) sizes[l] = int32_t(values[l].size());
+    for (int l = 0; l + 1 < L; l++) co.insert(co.end(), childOff[l].begin(), childOff[l].end());
+    std::vector<int64_t> fr(size_t(R) * N, 0), us(size_t(R) * N, 0);
+    std::vector<uint32_t> fp(N, 0), up(N, 0);
+    for (int i = 0; i < N; i++) {
+      for (auto& kv : freeCap[i]) {
+        int c = colByName[kv.first];
+        fr[size_t(c) * N + i] = kv.second;
+        fp[i] |= 1u << c;
+      }
+      for (auto& kv : tasUsage[i]) {
+        int c = colByName[kv.first];
+        us[size_t(c) * N + i] = kv.second;
+        up[i] |= 1u << c;
+      }
+    }
+    std::vector<int32_t> ranks;
+    for (int l = 0; l < L; l++) ranks.insert(ranks.end(), idRank[l].begin(), idRank[l].end());
+    kueue_tas_snapshot_desc d{};
+    d.num_levels = L;
+    d.level_sizes = sizes.data();
+    d.child_offsets = co.data();
+    d.num_cols = R;
+    d.free_capacity = fr.data();
+    d.tas_usage = us.data();
+    d.free_present = fp.data();
+    d.usage_present = up.data();
+    d.lowest_is_hostname = lowestIsHostname ? 1 : 0;
+    d.taint_profile = leafProfile.data();
+    d.num_label_cols = int32_t(labelKeys.size());
+    d.label_values = labelValues.empty() ? nullptr : labelValues.data();
+    d.domain_id_rank = ranks.data();
+    int rc = kueue_tas_snapshot_load(ctx, &d);
+    if (rc) {
+      err = std::string("snapshot load: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    dirty = false;
+    return 0;
+  }
+
+  // ---- request compilation: findTopologyAssignment prelude (:804-897) ----
+  int resolve(const std::string& key) const {
+    for (size_t i = 0; i < levelKeys.size(); i++)
+      if (levelKeys[i] == key) return int(i);
+    return -1;
+  }
+  static bool slice_only(const std::optional<TopologyRequest>& tr) {  // :1148-1153
+    if (!tr || tr->required || tr->preferred) return false;
+    return tr->sliceRequiredTopology.has_value() || !tr->constraints.empty();
+  }
+  std::optional<std::string> level_key(const TASPodSetRequests& r) const {  // :1112-1138
+    const auto& tr = r.topologyRequest;
+    if (tr) {
+      if (tr->required) return tr->required;
+      if (tr->preferred) return tr->preferred;
+      if (slice_only(tr)) return levelKeys.front();
+      if (tr->unconstrained.value_or(false)) return levelKeys.back();
+    }
+    if (r.implied) return levelKeys.back();
+    return std::nullopt;
+  }
+
+  void compile_group(GroupEval& g, bool simulateEmpty) {
+    const TASPodSetRequests& w = *g.workers;
+    kueue_tas_eval_req& q = g.req;
+    memset(&q, 0, sizeof q);
+    g.compiled = true;
+    g.early_reason.clear();
+    g.layer_names.clear();
+    // requests + pods:1 (:820-826); columns were ensured by ensure_columns_for()
+    Requests req = w.singlePodRequests;
+    req["pods"] = add64(req["pods"], 1);
+    Requests lreq;
+    if (g.leader) {
+      lreq = g.leader->singlePodRequests;
+      lreq["pods"] = add64(lreq["pods"], 1);
+    }
+    const auto& tr = w.topologyRequest;
+    // getSliceSizeWithSinglePodAsDefault (:1162-1180)
+    int32_t sliceSize = 1;
+    if (tr) {
+      if (!tr->constraints.empty()) sliceSize = tr->constraints[0].size;
+      else if (tr->sliceRequiredTopology) {
+        if (!tr->sliceSize) {
+          g.early_reason = "slice topology requested, but slice size not provided";
+          return;
+        }
+        sliceSize = *tr->sliceSize;
+      }
+    }
+    if (sliceSize == 0) {
+      g.early_reason = "panic: integer divide by zero";
+      return;
+    }
+    g.slice_size = sliceSize;
+    bool required = tr && tr->required.has_value();
+    bool unconstrained = (tr && tr->unconstrained.value_or(false)) || w.implied || slice_only(tr);
+    auto key = level_key(w);
+    if (!key) {
+      g.early_reason = "topology level not specified";
+      return;
+    }
+    int reqLevel = resolve(*key);
+    if (reqLevel < 0) {
+      g.early_reason = "no requested topology level: " + *key;
+      return;
+    }
+    std::string sliceKey = levelKeys.back();
+    if (tr) {
+      if (tr->sliceRequiredTopology) sliceKey = *tr->sliceRequiredTopology;
+      else if (!tr->constraints.empty()) sliceKey = tr->constraints[0].topology;
+    }
+    int sliceLevel = resolve(sliceKey);
+    if (sliceLevel < 0) {
+      g.early_reason = "no requested topology level for slices: " + sliceKey;
+      return;
+    }
+    if (reqLevel > sliceLevel) {
+      g.early_reason = "podset slice topology " + sliceKey + " is above the podset topology " + *key;
+      return;
+    }
+    // buildSliceSizeAtLevel (:1018-1063)
+    std::map<int, int32_t> ssal;
+    if (gates.multiLayer && tr) {
+      int32_t prevSize = sliceSize;
+      int prevLevel = sliceLevel;
+      for (size_t i = 1; i < tr->constraints.size(); i++) {
+        const auto& layer = tr->constraints[i];
+        int inner = resolve(layer.topology);
+        if (inner < 0) {
+          g.early_reason = "no requested topology level for additional slice layer: " + layer.topology;
+          return;
+        }
+        if (inner <= prevLevel) {
+          g.early_reason = "additional slice layer topology " + layer.topology + " must be at a lower level than " +
+                           levelKeys[prevLevel];
+          return;
+        }
+        if (layer.size == 0) {
+          g.early_reason = "panic: integer divide by zero";
+          return;
+        }
+        if (prevSize % layer.size != 0) {
+          g.early_reason = "additional slice layer size " + std::to_string(layer.size) +
+                           " must evenly divide parent layer size " + std::to_string(prevSize);
+          return;
+        }
+        for (int lvl = prevLevel + 1; lvl <= inner; lvl++) ssal[lvl] = layer.size;
+        prevSize = layer.size;
+        prevLevel = inner;
+      }
+    }
+    bool multilayer = gates.multiLayer && !ssal.empty();
+    if (gates.balanced && !required && !unconstrained) {
+      g.early_reason = "unsupported: TASBalancedPlacement (alpha) is not implemented on this path";
+      return;
+    }
+    q.flags = (required ? KUEUE_TAS_F_REQUIRED : 0u) | (unconstrained ? KUEUE_TAS_F_UNCONSTRAINED : 0u) |
+              ((unconstrained && gates.profileMixed) ? KUEUE_TAS_F_LFC : 0u) |
+              (simulateEmpty ? KUEUE_TAS_F_SIMULATE_EMPTY : 0u) | (g.leader ? KUEUE_TAS_F_LEADER : 0u) |
+              (multilayer ? KUEUE_TAS_F_MULTILAYER : 0u);
+    q.count = w.count;
+    q.slice_size = sliceSize;
+    q.requested_level = reqLevel;
+    q.slice_level = sliceLevel;
+    for (auto& kv : ssal) q.slice_size_at_level[kv.first] = kv.second;
+    if (multilayer) {
+      for (auto& c : tr->constraints) {
+        int t = resolve(c.topology);
+        if (t < 0) continue;  // multiLayerNotFitMessage skips unresolved layers (:1778-1781)
+        if (q.num_layers >= KUEUE_TAS_MAX_LAYERS) break;
+        if (c.size == 0) {
+          g.early_reason = "panic: integer divide by zero";
+          return;
+        }
+        q.layer_level[q.num_layers] = t;
+        q.layer_size[q.num_layers] = c.size;
+        g.layer_names.push_back(c.topology);
+        q.num_layers++;
+      }
+    }
+    for (auto& kv : req) {  // std::map order == column order (sorted names)
+      q.req_col[q.num_req] = colByName[kv.first];
+      q.req_val[q.num_req] = kv.second;
+      q.num_req++;
+    }
+    for (auto& kv : lreq) {
+      q.leader_col[q.num_leader_req] = colByName[kv.first];
+      q.leader_val[q.num_leader_req] = kv.second;
+      q.num_leader_req++;
+    }
+    // tolerations = podset + flavor (:877); first untolerated NoSchedule/NoExecute taint per profile
+    std::vector<Toleration> tols = w.tolerations;
+    tols.insert(tols.end(), flavorTolerations.begin(), flavorTolerations.end());
+    g.taint_row.assign(profiles.size(), -1);
+    if (lowestIsHostname) {
+      for (size_t p = 0; p < profiles.size(); p++) {
+        for (auto& t : profiles[p]) {
+          bool ok = false;
+          for (auto& tol : tols)
+            if (tolerates(tol, t)) {
+              ok = true;
+              break;
+            }
+          if (!ok) {
+            g.taint_row[p] = taintIdByString[taint_string(t)];
+            break;
+          }
+        }
+      }
+      // nodeSelector: labels.ValidatedSelectorFromSet (only with hostname leaves, :879-887)
+      if (w.nodeSelector && !w.nodeSelector->empty()) {
+        if (w.nodeSelector->size() > KUEUE_TAS_MAX_SELECTORS) {
+          g.early_reason = "unsupported: more than 8 nodeSelector terms";
+          return;
+        }
+        for (auto& kv : *w.nodeSelector) {
+          auto it = labelCol.find(kv.first);
+          int col = it == labelCol.end() ? 0 : it->second;
+          int val = -1;
+          if (it != labelCol.end()) {
+            auto d = labelDict[col].find(kv.second);
+            if (d != labelDict[col].end()) val = d->second;
+          }
+          q.sel_col[q.num_selectors] = col;
+          q.sel_val[q.num_selectors] = val;
+          q.num_selectors++;
+        }
+      }
+    }
+  }
+
+  // ---- failure strings ----
+  std::string format_stats(const kueue_tas_eval_out& o, const int32_t* taints, const int32_t* res) const {
+    bool has = o.excl_selector > 0 || o.excl_affinity > 0 || o.excl_topology > 0;
+    std::vector<std::string> reasons;
+    if (o.excl_selector > 0) reasons.push_back("nodeSelector: " + std::to_string(o.excl_selector));
+    if (o.excl_affinity > 0) reasons.push_back("affinity: " + std::to_string(o.excl_affinity));
+    if (o.excl_topology > 0) reasons.push_back("topologyDomain: " + std::to_string(o.excl_topology));
+    for (size_t t = 0; t < taintStrings.size(); t++)
+      if (taints[t] > 0) {
+        has = true;
+        reasons.push_back("taint " + go_quote(taintStrings[t]) + ": " + std::to_string(taints[t]));
+      }
+    for (size_t c = 0; c < cols.size(); c++)
+      if (res[c] > 0) {
+        has = true;
+        reasons.push_back("resource " + go_quote(cols[c]) + ": " + std::to_string(res[c]));
+      }
+    if (!has) return "";
+    std::sort(reasons.begin(), reasons.end());
+    std::string out = ". Total nodes: " + std::to_string(o.total_nodes) + "; excluded: ";
+    for (size_t i = 0; i < reasons.size(); i++) out += (i ? ", " : "") + reasons[i];
+    return out;
+  }
+  std::string failure_reason(const GroupEval& g, const kueue_tas_eval_out& o, const int32_t* taints,
+                             const int32_t* res) const {
+    const std::string topo = go_quote(topologyName);
+    switch (o.status) {
+      case KUEUE_TAS_ST_NO_DOMAINS:
+        return "no topology domains at level: " + levelKeys[o.a];
+      case KUEUE_TAS_ST_NOT_FIT: {
+        std::string unit = g.slice_size == 1 ? "pod" : "slice";
+        std::string m = o.a == 0 ? "topology " + topo + " doesn't allow to fit any of " + std::to_string(o.b) + " " + unit + "(s)"
+                                 : "topology " + topo + " allows to fit only " + std::to_string(o.a) + " out of " +
+                                       std::to_string(o.b) + " " + unit + "(s)";
+        return m + format_stats(o, taints, res);
+      }
+      case KUEUE_TAS_ST_MULTILAYER: {
+        std::string m = "topology " + topo + " doesn't allow to fit";
+        if (values[o.a].empty()) return m;
+        for (int c = 0; c < g.req.num_layers; c++)
+          m += "; " + std::to_string(o.ml_fit[c]) + "/" + std::to_string(o.ml_need[c]) + " slice(s) fit on level " +
+               g.layer_names[c];
+        return m + format_stats(o, taints, res);
+      }
+      default:
+        return "internal: device evaluation exceeded its list/output capacity";
+    }
+  }
+};
+
+// FindTopologyAssignmentsForFlavor (:519-594): groups in first-seen order
+static void make_groups(Workload& wl) {
+  std::vector<std::string> order;
+  std::map<std::string, std::vector<const TASPodSetRequests*>> grouped;
+  for (size_t i = 0; i < wl.podsets.size(); i++) {
+    const auto& p = wl.podsets[i];
+    std::string key = p.podSetGroupName ? *p.podSetGroupName : std::to_string(i);
+    if (std::find(order.begin(), order.end(), key) == order.end()) order.push_back(key);
+    grouped[key].push_back(&p);
+  }
+  wl.groups.clear();
+  for (auto& k : order) {
+    auto& trs = grouped[k];
+    GroupEval g;
+    g.members = trs;
+    g.workers = trs[0];
+    if (trs.size() > 1) {  // findLeaderAndWorkers (:596-609)
+      g.leader = trs[1];
+      if (g.leader->count > g.workers->count) {
+        g.leader = trs[0];
+        g.workers = trs[1];
+      }
+    }
+    wl.groups.push_back(std::move(g));
+  }
+}
+
+static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
+  std::vector<TASPodSetRequests> out;
+  for (auto& ps : arr.items) {
+    TASPodSetRequests r;
+    r.name = ps["name"].s();
+    const kjson::Node& tr = ps["topologyRequest"];
+    if (!tr.null()) {
+      TopologyRequest t;
+      if (!tr["required"].null()) t.required = tr["required"].s();
+      if (!tr["preferred"].null()) t.preferred = tr["preferred"].s();
+      if (!tr["unconstrained"].null()) t.unconstrained = tr["unconstrained"].b();
+      if (!tr["podSetSliceRequiredTopology"].null()) t.sliceRequiredTopology = tr["podSetSliceRequiredTopology"].s();
+      if (!tr["podSetSliceSize"].null()) t.sliceSize = int32_t(tr["podSetSliceSize"].i64());
+      for (auto& c : tr["podsetSliceRequiredTopologyConstraints"].items)
+        t.constraints.push_back({c["topology"].s(), int32_t(c["size"].i64())});
+      r.topologyRequest = t;
+    }
+    r.implied = tr.null();
+    if (auto im = ps.find("implied")) r.implied = im->b();
+    for (auto& kv : ps["requests"].fields) r.singlePodRequests[kv.first] = kv.second.i64();
+    r.count = int32_t(ps["count"].i64());
+    if (!ps["podSetGroupName"].null()) r.podSetGroupName = ps["podSetGroupName"].s();
+    for (auto& t : ps["tolerations"].items)
+      r.tolerations.push_back({t["key"].s(), t["operator"].s(), t["value"].s(), t["effect"].s()});
+    if (ps["nodeSelector"].type == kjson::Node::kObject) {
+      std::map<std::string, std::string> m;
+      for (auto& kv : ps["nodeSelector"].fields) m[kv.first] = kv.second.s();
+      r.nodeSelector = m;
+    }
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+
+// Batched driver: pass p evaluates group p of every workload still running
+// (groups of one workload are sequential through assumedUsage, :543-591).
+struct Evaluator {
+  FlavorSnapshot* snap;
+  int32_t entry_cap = 4096;
+  std::vector<kueue_tas_eval_req> reqs;
+  std::vector<int32_t> taint_table;
+  std::vector<kueue_tas_assumed> assumed;
+  std::vector<kueue_tas_eval_out> outs;
+  std::vector<int32_t> entries, taint_counts, res_counts;
+
+  static void set_result(std::vector<PodSetResult>& rs, const std::string& name, bool has, std::vector<DomainAssignment> d,
+                         const std::string& reason) {
+    for (auto& r : rs)
+      if (r.name == name) {
+        r.has_assignment = has;
+        r.domains = std::move(d);
+        r.reason = reason;
+        return;
+      }
+    PodSetResult r;
+    r.name = name;
+    r.has_assignment = has;
+    r.domains = std::move(d);
+    r.reason = reason;
+    rs.push_back(std::move(r));
+  }
+
+  int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results) {
+    results->assign(wls.size(), {});
+    bool changed = false;
+    for (auto& wl : wls) {
+      if (wl.groups.empty()) make_groups(wl);
+      changed |= snap->ensure_columns_for(wl.podsets);
+    }
+    for (auto& wl : wls)
+      for (auto& g : wl.groups)
+        if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
+    int rc = snap->upload();  // (re)load when columns were added
+    if (rc) return rc;
+    std::vector<char> done(wls.size(), 0);
+    std::vector<std::map<int32_t, std::map<int32_t, int64_t>>> assumedBy(wls.size());
+    size_t maxGroups = 0;
+    for (auto& wl : wls) maxGroups = std::max(maxGroups, wl.groups.size());
+    const size_t P = snap->profiles.size();
+    const size_t T = snap->taintStrings.size();
+    const size_t R = snap->cols.size();
+    for (size_t pass = 0; pass < maxGroups; pass++) {
+      std::vector<std::pair<size_t, GroupEval*>> batch;
+      reqs.clear();
+      taint_table.clear();
+      assumed.clear();
+      std::map<std::vector<int32_t>, int32_t> rowOff;
+      for (size_t w = 0; w < wls.size(); w++) {
+        if (done[w] || pass >= wls[w].groups.size()) continue;
+        GroupEval& g = wls[w].groups[pass];
+        if (!g.early_reason.empty()) {
+          for (auto* m : g.members) set_result((*results)[w], m->name, false, {}, g.early_reason);
+          done[w] = 1;
+          continue;
+        }
+        kueue_tas_eval_req q = g.req;
+        auto it = rowOff.find(g.taint_row);
+        if (it == rowOff.end()) {
+          it = rowOff.emplace(g.taint_row, int32_t(taint_table.size())).first;
+          taint_table.insert(taint_table.end(), g.taint_row.begin(), g.taint_row.end());
+        }
+        q.taint_table = it->second;
+        q.assumed_begin = int32_t(assumed.size());
+        for (auto& lv : assumedBy[w])
+          for (auto& cv : lv.second) assumed.push_back({lv.first, cv.first, cv.second});
+        q.assumed_end = int32_t(assumed.size());
+        reqs.push_back(q);
+        batch.emplace_back(w, &g);
+      }
+      if (batch.empty()) continue;
+      const size_t n = batch.size();
+      outs.resize(n);
+      int32_t cap = entry_cap;
+      for (;;) {
+        entries.resize(n * size_t(cap) * 2);
+        taint_counts.assign(n * std::max<size_t>(T, 1), 0);
+        res_counts.assign(n * R, 0);
+        rc = kueue_tas_eval_batch(snap->ctx, reqs.data(), n, taint_table.data(), taint_table.size(), int32_t(T),
+                                  assumed.data(), assumed.size(), outs.data(), entries.data(), cap,
+                                  taint_counts.data(), res_counts.data());
+        if (rc) {
+          snap->err = std::string("eval: ") + kueue_tas_last_error(snap->ctx);
+          return rc;
+        }
+        bool retry = false;
+        for (size_t i = 0; i < n; i++)
+          if (outs[i].status == KUEUE_TAS_ST_INTERNAL && outs[i].num_workers + outs[i].num_leaders > cap) retry = true;
+        if (!retry || cap >= (1 << 22)) break;
+        cap *= 4;
+      }
+      (void)P;
+      for (size_t i = 0; i < n; i++) {
+        size_t w = batch[i].first;
+        GroupEval& g = *batch[i].second;
+        const kueue_tas_eval_out& o = outs[i];
+        if (o.status != KUEUE_TAS_ST_OK) {
+          std::string reason = snap->failure_reason(g, o, taint_counts.data() + i * std::max<size_t>(T, 1),
+                                                    res_counts.data() + i * R);
+          for (auto* m : g.members) set_result((*results)[w], m->name, false, {}, reason);
+          done[w] = 1;
+          continue;
+        }
+        const int32_t* e = entries.data() + i * size_t(cap) * 2;
+        std::vector<DomainAssignment> wk, ld;
+        for (int k = 0; k < o.num_workers; k++) wk.push_back({e[2 * k], e[2 * k + 1]});
+        for (int k = 0; k < o.num_leaders; k++) ld.push_back({e[2 * (o.num_workers + k)], e[2 * (o.num_workers + k) + 1]});
+        for (auto* m : g.members) {
+          if (m == g.workers) set_result((*results)[w], m->name, true, wk, "");
+          else if (m == g.leader) set_result((*results)[w], m->name, true, ld, "");
+          else set_result((*results)[w], m->name, false, {}, "");
+        }
+        // addAssumedUsage (:658-666): SinglePodRequests x count (no pods term)
+        auto add = [&](const TASPodSetRequests* tr, const std::vector<DomainAssignment>& ds) {
+          for (auto& d : ds)
+            for (auto& kv : tr->singlePodRequests) {
+              int64_t& slot = assumedBy[w][d.leaf][snap->colByName[kv.first]];
+              slot = add64(slot, mul64(kv.second, d.count));
+            }
+        };
+        add(g.workers, wk);
+        if (g.leader) add(g.leader, ld);
+      }
+    }
+    return 0;
+  }
+};
+
+static void emit_results(std::string& out, const FlavorSnapshot& s, const std::vector<PodSetResult>& rs) {
+  out += "[";
+  const int L = s.L();
+  const size_t levelIdx = s.lowestIsHostname ? size_t(L - 1) : 0;
+  for (size_t i = 0; i < rs.size(); i++) {
+    if (i) out += ",";
+    out += "{\"name\":";
+    kjson::write_string(out, rs[i].name);
+    out += ",\"assignment\":";
+    if (!rs[i].has_assignment) {
+      out += "null";
+    } else {
+      out += "{\"levels\":[";
+      for (size_t l = levelIdx; l < size_t(L); l++) {
+        if (l > levelIdx) out += ",";
+        kjson::write_string(out, s.levelKeys[l]);
+      }
+      out += "],\"domains\":[";
+      for (size_t k = 0; k < rs[i].domains.size(); k++) {
+        if (k) out += ",";
+        out += "{\"values\":[";
+        const auto& lv = s.values[L - 1][rs[i].domains[k].leaf];
+        for (size_t l = levelIdx; l < lv.size(); l++) {
+          if (l > levelIdx) out += ",";
+          kjson::write_string(out, l == size_t(L - 1) && s.lowestIsHostname ? s.leafId[rs[i].domains[k].leaf] : lv[l]);
+        }
+        out += "],\"count\":" + std::to_string(rs[i].domains[k].count) + "}";
+      }
+      out += "]}";
+    }
+    out += ",\"reason\":";
+    kjson::write_string(out, rs[i].reason);
+    out += "}";
+  }
+  out += "]";
+}
+
+static char* dup(const std::string& s) {
+  char* p = static_cast<char*>(malloc(s.size() + 1));
+  memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+}  // namespace kueue_tas
+
+using namespace kueue_tas;
+
+struct kueue_tas_host {
+  std::unique_ptr<FlavorSnapshot> snap;
+  std::string err;
+  std::vector<Workload> compiled;
+};
+
+extern "C" {
+
+kueue_tas_host* kueue_tas_host_create(const char* snapshot_json, const kueue_tas_config* cfg) {
+  auto* h = new kueue_tas_host();
+  try {
+    h->snap = std::make_unique<FlavorSnapshot>();
+    if (cfg) h->snap->cfg = *cfg;
+    kjson::Node c = kjson::parse(snapshot_json);
+    h->snap->build(c);
+    if (h->snap->upload()) {
+      h->err = h->snap->err;
+      return h;
+    }
+  } catch (const std::exception& e) {
+    h->err = e.what();
+  }
+  return h;
+}
+
+void kueue_tas_host_destroy(kueue_tas_host* h) { delete h; }
+
+const char* kueue_tas_host_last_error(kueue_tas_host* h) { return h ? h->err.c_str() : "null host"; }
+
+static int run_workloads(kueue_tas_host* h, std::vector<Workload>& wls, bool sim, std::string* out, bool nested) {
+  Evaluator ev{h->snap.get()};
+  std::vector<std::vector<PodSetResult>> results;
+  int rc = ev.run(wls, sim, &results);
+  if (rc) {
+    h->err = h->snap->err;
+    return rc;
+  }
+  *out = "{\"results\":";
+  if (nested) {
+    *out += "[";
+    for (size_t i = 0; i < results.size(); i++) {
+      if (i) *out += ",";
+      emit_results(*out, *h->snap, results[i]);
+    }
+    *out += "]";
+  } else {
+    emit_results(*out, *h->snap, results[0]);
+  }
+  *out += "}";
+  return 0;
+}
+
+int kueue_tas_host_find(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    std::vector<Workload> wls(1);
+    wls[0].podsets = parse_podsets(kjson::parse(podsets_json));
+    if (h->snap->gates.elastic) {
+      std::string out = "{\"results\":[{\"name\":";
+      kjson::write_string(out, wls[0].podsets.empty() ? "" : wls[0].podsets[0].name);
+      out += ",\"assignment\":null,\"reason\":\"unsupported: ElasticJobsViaWorkloadSlicesWithTAS\"}]}";
+      *out_json = dup(out);
+      return 0;
+    }
+    std::string out;
+    int rc = run_workloads(h, wls, simulate_empty != 0, &out, false);
+    if (rc) return rc;
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, char** out_json) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    kjson::Node doc = kjson::parse(workloads_json);
+    std::vector<Workload> wls(doc["workloads"].items.size());
+    for (size_t i = 0; i < wls.size(); i++) wls[i].podsets = parse_podsets(doc["workloads"].items[i]);
+    std::string out;
+    int rc = run_workloads(h, wls, false, &out, true);
+    if (rc) return rc;
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    kjson::Node doc = kjson::parse(workloads_json);
+    h->compiled.assign(doc["workloads"].items.size(), Workload{});
+    for (size_t i = 0; i < h->compiled.size(); i++) {
+      h->compiled[i].podsets = parse_podsets(doc["workloads"].items[i]);
+      make_groups(h->compiled[i]);
+      h->snap->ensure_columns_for(h->compiled[i].podsets);
+    }
+    for (auto& wl : h->compiled)
+      for (auto& g : wl.groups) h->snap->compile_group(g, false);
+    return h->snap->upload();
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+// One timed "step": every compiled workload evaluated against the resident
+// snapshot, results decoded to (leaf, count) lists; FNV-1a over all results.
+int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
+  if (!h || !h->snap) return KUEUE_TAS_EINVAL;
+  Evaluator ev{h->snap.get()};
+  std::vector<std::vector<PodSetResult>> results;
+  int rc = ev.run(h->compiled, false, &results);
+  if (rc) {
+    h->err = h->snap->err;
+    return rc;
+  }
+  if (result_hash) {
+    uint64_t x = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) {
+      for (int i = 0; i < 8; i++) {
+        x ^= (v >> (8 * i)) & 0xff;
+        x *= 1099511628211ull;
+      }
+    };
+    for (auto& rs : results)
+      for (auto& r : rs) {
+        mix(r.has_assignment);
+        mix(r.domains.size());
+        for (auto& d : r.domains) {
+          mix(uint64_t(uint32_t(d.leaf)));
+          mix(uint64_t(uint32_t(d.count)));
+        }
+        mix(std::hash<std::string>()(r.reason));
+      }
+    *result_hash = x;
+  }
+  return 0;
+}
+
+void kueue_tas_free(char* p) { free(p); }
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// tas_internal.h — device-side data structures shared by the HIP kernels and
+// the C-ABI glue in tas_device.hip.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/kueue_tas.h"
+
+namespace ktas {
+
+constexpr int kWave = 64;
+constexpr int kMaxLevels = KUEUE_TAS_MAX_LEVELS;
+constexpr int kMaxCols = KUEUE_TAS_MAX_COLS;
+
+// One request term: requested column with its value and the exact
+// unsigned-division magic for |value| (Granlund–Montgomery / libdivide u64).
+struct DevTerm {
+  int64_t val;       // request value (Go int64)
+  uint64_t magic;    // multiplier (0 when power of two)
+  int32_t col;       // resource column
+  uint8_t shift;     // post shift
+  uint8_t add;       // 1: "add" variant of the decode
+  uint8_t pow2;      // 1: |val| is a power of two
+  uint8_t neg;       // 1: val < 0
+};
+
+// Compiled evaluation (device copy of kueue_tas_eval_req).
+struct DevEval {
+  uint32_t flags;
+  int32_t count;
+  int32_t slice_size;
+  int32_t requested_level;
+  int32_t slice_level;
+  int32_t term_begin;     // worker terms [term_begin, term_begin + nreq)
+  int32_t nreq;
+  int32_t lead_begin;     // leader terms
+  int32_t nlead;
+  int32_t nsel;
+  uint32_t req_mask;
+  uint32_t lead_mask;
+  int32_t taint_table;
+  int32_t assumed_begin;
+  int32_t assumed_end;
+  int32_t num_layers;
+  int32_t layer_level[KUEUE_TAS_MAX_LAYERS];
+  int32_t layer_size[KUEUE_TAS_MAX_LAYERS];
+  int32_t ssal[kMaxLevels];
+  int32_t sel_col[KUEUE_TAS_MAX_SELECTORS];
+  int32_t sel_val[KUEUE_TAS_MAX_SELECTORS];
+};
+
+// Device-resident snapshot (pointers into HBM).
+struct DevSnap {
+  int32_t L;
+  int32_t N;               // leaves
+  int32_t R;               // resource columns
+  int32_t SD;              // total domains
+  int32_t lowest_is_hostname;
+  int32_t K;               // label columns
+  int32_t level_size[kMaxLevels];
+  int32_t level_off[kMaxLevels + 1];   // global domain id offsets
+  int32_t child_base[kMaxLevels];      // offset of level l's child_offsets in child_off[]
+  const int32_t* child_off;
+  const int32_t* id_rank;              // [SD] rank of DomainID string within its level
+  const int64_t* free_cap;             // [R][N]
+  const int64_t* tas_usage;            // [R][N]
+  const uint32_t* free_present;        // [N]
+  const uint32_t* usage_present;       // [N]
+  const int32_t* taint_profile;        // [N] or null
+  const int32_t* label_values;         // [K][N] or null
+};
+
+// Per-batch device buffers.
+struct DevBatch {
+  const DevEval* evals;
+  const DevTerm* terms;
+  const int32_t* taint_table;
+  const kueue_tas_assumed* assumed;
+  int32_t n;
+  int32_t num_taints;
+  int64_t ctr_stride;      // int32 elements per eval (5 * SD)
+  int32_t* counters;       // [n][5][SD]
+  int32_t* taint_counts;   // [n][num_taints]
+  int32_t* res_counts;     // [n][R]
+  int32_t* sel_counts;     // [n]
+  kueue_tas_eval_out* out; // [n]
+  int32_t* entries;        // [n][entry_cap][2]
+  int32_t entry_cap;
+  int64_t scratch_stride;  // uint64 elements of scratch per eval
+  uint64_t* scratch;       // [n][scratch_stride]
+  int32_t list_cap;        // LDS sort capacity per wave
+};
+
+}  // namespace ktas

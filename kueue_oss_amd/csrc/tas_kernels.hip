@@ -1,0 +1,1359 @@
+// tas_kernels.hip — CDNA4 (gfx950) kernels for Kueue's TAS evaluation path.
+//
+// Three stages per batch of PodSet-group evaluations ("evals"), all integer,
+// all HBM/latency bound (no MFMA: there is no matrix-shaped work here):
+//
+//  K1 fill_leaves   — fillInCounts leaf loop (tas_flavor_snapshot.go:1578-1643):
+//                     per (leaf, eval) taint/selector masks, remaining capacity
+//                     and Requests.CountInWithLimitingResource (requests.go:183-217)
+//                     with exact int64 magic-number division, leader split,
+//                     wave-aggregated ExclusionStats.  One block = 256 leaves x
+//                     kEvalsPerBlock evals so the SoA snapshot columns are read
+//                     from HBM once per block and re-served from L1/L2.
+//  K2 rollup_level  — fillInCountsHelper (:1658-1719) bottom-up, one launch per
+//                     level, one thread per parent domain over its CSR children.
+//  K3 select        — phase 2 (findLevelWithFitDomains :1236-1321,
+//                     updateCountsToMinimumGeneric :1405-1469, the descent
+//                     :925-971, buildAssignment :1490-1501): one 64-lane wave per
+//                     eval executing the reference's sequential greedy with
+//                     wave-parallel primitives (arg-min reductions, LDS bitonic
+//                     sort, lazy sorted iteration, histogram threshold select).
+//
+// Every scalar of the greedy is held redundantly by all 64 lanes and every
+// mutation of a domain counter is stored by all lanes (so each lane reads back
+// its own store: no cross-lane global-memory hazards).  LDS traffic between
+// lanes is ordered with wave_sync().
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tas_internal.h"
+
+namespace ktas {
+
+// ----------------------------------------------------------------------------
+// Go integer helpers
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ int32_t w_add(int32_t a, int32_t b) { return int32_t(uint32_t(a) + uint32_t(b)); }
+__device__ __forceinline__ int32_t w_sub(int32_t a, int32_t b) { return int32_t(uint32_t(a) - uint32_t(b)); }
+__device__ __forceinline__ int32_t w_mul(int32_t a, int32_t b) { return int32_t(uint32_t(a) * uint32_t(b)); }
+// Go int32 division (truncating; MinInt32 / -1 == MinInt32).  b == 0 is
+// rejected on the host (Go panics).
+__device__ __forceinline__ int32_t go_div32(int32_t a, int32_t b) {
+  if (b == -1) return int32_t(0u - uint32_t(a));
+  return b == 0 ? 0 : a / b;
+}
+
+// Exact unsigned 64-bit division by an invariant divisor (host-computed magic).
+__device__ __forceinline__ uint64_t udiv_magic(uint64_t n, const DevTerm& t) {
+  if (t.pow2) return n >> t.shift;
+  uint64_t q = __umul64hi(t.magic, n);
+  if (t.add) {
+    uint64_t x = ((n - q) >> 1) + q;
+    return x >> t.shift;
+  }
+  return q >> t.shift;
+}
+
+// max(int32(cap / val), 0) with Go's truncating int64 division (val != 0).
+__device__ __forceinline__ int32_t count_term(int64_t cap, const DevTerm& t) {
+  uint64_t ucap = cap < 0 ? (0ull - uint64_t(cap)) : uint64_t(cap);
+  uint64_t q = udiv_magic(ucap, t);
+  bool negq = (cap < 0) != (t.neg != 0);
+  uint64_t sq = negq ? (0ull - q) : q;
+  int32_t c = int32_t(uint32_t(sq));
+  return c > 0 ? c : 0;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  lo = __shfl_xor(lo, m, 64);
+  hi = __shfl_xor(hi, m, 64);
+  return (uint64_t(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  lo = __shfl(lo, src, 64);
+  hi = __shfl(hi, src, 64);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+// 128-bit lexicographic key; lo's low 32 bits hold the domain index in its level.
+struct Key {
+  uint64_t hi, lo;
+};
+__device__ __forceinline__ bool key_lt(const Key& a, const Key& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+__device__ __forceinline__ bool key_le(const Key& a, const Key& b) { return !key_lt(b, a); }
+__device__ __forceinline__ Key key_max() { return Key{~0ull, ~0ull}; }
+__device__ __forceinline__ Key wave_min_key(Key k) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    Key o{shfl_xor_u64(k.hi, m), shfl_xor_u64(k.lo, m)};
+    if (key_lt(o, k)) k = o;
+  }
+  return k;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    uint64_t o = shfl_xor_u64(v, m);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += int64_t(shfl_xor_u64(uint64_t(v), m));
+  return v;
+}
+__device__ __forceinline__ int32_t wave_sum_wrap32(int32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = w_add(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t s_asc(int32_t x) { return uint32_t(x) ^ 0x80000000u; }
+__device__ __forceinline__ uint32_t s_desc(int32_t x) { return ~(uint32_t(x) ^ 0x80000000u); }
+
+// sortedDomains comparator (:1544-1564): sliceState desc (asc if LFC), state asc, levelValues asc.
+__device__ __forceinline__ Key key_plain(bool lfc, int32_t ss, int32_t s, int32_t idx) {
+  uint64_t k0 = lfc ? s_asc(ss) : s_desc(ss);
+  return Key{(k0 << 32) | s_asc(s), uint64_t(uint32_t(idx))};
+}
+// sortedDomainsWithLeader comparator (:1511-1535): leaderState desc,
+// sliceStateWithLeader desc (asc if LFC), stateWithLeader asc, levelValues asc.
+__device__ __forceinline__ Key key_wl(bool lfc, int32_t ls, int32_t sswl, int32_t swl, int32_t idx) {
+  uint64_t k1 = lfc ? s_asc(sswl) : s_desc(sswl);
+  return Key{(uint64_t(s_desc(ls)) << 32) | k1, (uint64_t(s_asc(swl)) << 32) | uint32_t(idx)};
+}
+
+// ----------------------------------------------------------------------------
+// K1: fillInCounts leaf loop
+// ----------------------------------------------------------------------------
+constexpr int kFillThreads = 256;
+constexpr int kEvalsPerBlock = 8;
+
+enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3 };
+
+// Requests.CountIn / CountInWithLimitingResource over up to MAXT terms held in
+// registers (fully unrolled: no runtime-indexed private arrays).  Terms are in
+// ascending column (= resource name) order, so the first missing key and the
+// first minimum are Go's limiting resource with the alphabetical tie-break.
+template <int MAXT>
+__device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, uint32_t pres, const int64_t (&caps)[MAXT],
+                                                 int* lim_out) {
+  int32_t result = 0;
+  bool any = false, done = false;
+  int lim = -1;
+#pragma unroll
+  for (int i = 0; i < MAXT; i++) {
+    if (i < nt && !done) {
+      const DevTerm& t = terms[i];
+      if (!((pres >> t.col) & 1u) && t.val != 0) {
+        lim = t.col;
+        result = 0;
+        any = true;
+        done = true;
+      } else {
+        int32_t c = t.val == 0 ? 0x7fffffff : count_term(caps[i], t);
+        if (!any || c < result) {
+          result = c;
+          lim = t.col;
+          any = true;
+        }
+      }
+    }
+  }
+  *lim_out = lim;
+  return any ? result : 0;
+}
+
+template <int MAXT>
+__global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, DevBatch b) {
+  __shared__ DevEval sh_ev[kEvalsPerBlock];
+  __shared__ DevTerm sh_terms[kEvalsPerBlock][2 * MAXT];
+  __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
+
+  const int e0 = blockIdx.y * kEvalsPerBlock;
+  const int ne = min(kEvalsPerBlock, b.n - e0);
+  if (threadIdx.x < ne) sh_ev[threadIdx.x] = b.evals[e0 + threadIdx.x];
+  __syncthreads();
+  for (int e = 0; e < ne; e++) {
+    const DevEval& ev = sh_ev[e];
+    if (threadIdx.x < ev.nreq) sh_terms[e][threadIdx.x] = b.terms[ev.term_begin + threadIdx.x];
+    if (threadIdx.x < ev.nlead) sh_terms[e][MAXT + threadIdx.x] = b.terms[ev.lead_begin + threadIdx.x];
+  }
+  __syncthreads();
+  for (int e = 0; e < ne; e++) {
+    const DevEval& ev = sh_ev[e];
+    if (threadIdx.x < ev.nreq) {
+      int col = sh_terms[e][threadIdx.x].col;
+      int64_t v = 0;
+      for (int j = 0; j < ev.nlead; j++)
+        if (sh_terms[e][MAXT + j].col == col) v = sh_terms[e][MAXT + j].val;
+      sh_wlead[e][threadIdx.x] = v;
+    }
+  }
+  __syncthreads();
+
+  const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
+  const bool valid = leaf < s.N;
+  const int N = s.N;
+  const int gleaf = s.level_off[s.L - 1] + leaf;
+  const uint32_t fp = valid ? s.free_present[leaf] : 0u;
+  const uint32_t up = valid ? s.usage_present[leaf] : 0u;
+  const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
+  const int lane = lane_id();
+
+  for (int e = 0; e < ne; e++) {
+    const DevEval& ev = sh_ev[e];
+    const int eid = e0 + e;
+    const DevTerm* wt = sh_terms[e];
+    const DevTerm* lt = sh_terms[e] + MAXT;
+    const bool leader = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+    int32_t state = 0, swl = 0, ls = 0;
+    int kind = EX_NONE, id = -1;
+    if (valid) {
+      if (s.lowest_is_hostname) {
+        if (s.taint_profile) {
+          int t = b.taint_table[ev.taint_table + prof];
+          if (t >= 0) {
+            kind = EX_TAINT;
+            id = t;
+          }
+        }
+        if (kind == EX_NONE) {
+          for (int k = 0; k < ev.nsel; k++) {
+            if (s.label_values[int64_t(ev.sel_col[k]) * N + leaf] != ev.sel_val[k]) {
+              kind = EX_SELECTOR;
+              break;
+            }
+          }
+        }
+      }
+      if (kind == EX_NONE) {
+        const bool sim = (ev.flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
+        uint32_t pres = fp | (sim ? 0u : up);
+        int a_lo = 0, a_hi = 0;
+        if (ev.assumed_end > ev.assumed_begin) {
+          int lo = ev.assumed_begin, hi = ev.assumed_end;
+          while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (b.assumed[mid].leaf < leaf) lo = mid + 1;
+            else hi = mid;
+          }
+          a_lo = lo;
+          a_hi = lo;
+          while (a_hi < ev.assumed_end && b.assumed[a_hi].leaf == leaf) {
+            pres |= 1u << b.assumed[a_hi].col;
+            a_hi++;
+          }
+        }
+        // remaining capacity: free - used - assumed (Requests.Sub, requests.go:90-94)
+        int64_t wcap[MAXT], lcap[MAXT];
+#pragma unroll
+        for (int i = 0; i < MAXT; i++) {
+          wcap[i] = 0;
+          lcap[i] = 0;
+          if (i < ev.nreq) {
+            const int col = wt[i].col;
+            int64_t c = s.free_cap[int64_t(col) * N + leaf];
+            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
+            for (int a = a_lo; a < a_hi; a++)
+              if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+            wcap[i] = c;
+          }
+          if (leader && i < ev.nlead) {
+            const int col = lt[i].col;
+            int64_t c = s.free_cap[int64_t(col) * N + leaf];
+            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
+            for (int a = a_lo; a < a_hi; a++)
+              if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+            lcap[i] = c;
+          }
+        }
+        int lim = -1;
+        state = count_in_regs<MAXT>(wt, ev.nreq, pres, wcap, &lim);
+        if (state == 0 && lim >= 0) {
+          kind = EX_RESOURCE;
+          id = lim;
+        }
+        swl = state;
+        if (leader) {
+          int dummy;
+          int32_t lc = count_in_regs<MAXT>(lt, ev.nlead, pres, lcap, &dummy);
+          if (lc > 0) {
+            ls = 1;
+#pragma unroll
+            for (int i = 0; i < MAXT; i++) wcap[i] = int64_t(uint64_t(wcap[i]) - uint64_t(sh_wlead[e][i]));
+            swl = count_in_regs<MAXT>(wt, ev.nreq, pres | ev.lead_mask, wcap, &dummy);
+          }
+        }
+      }
+    }
+    if (valid) {
+      int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+      const int64_t SD = s.SD;
+      int32_t ss = 0, sswl = 0;
+      if (s.L - 1 == ev.slice_level) {
+        ss = go_div32(state, ev.slice_size);
+        sswl = go_div32(swl, ev.slice_size);
+      }
+      base[gleaf] = state;
+      base[SD + gleaf] = ss;
+      if (leader) {
+        base[2 * SD + gleaf] = swl;
+        base[3 * SD + gleaf] = sswl;
+        base[4 * SD + gleaf] = ls;
+      }
+    }
+    // ExclusionStats (:1579-1634), aggregated per wave before the atomics.
+    uint64_t selm = ballot(kind == EX_SELECTOR);
+    if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    uint64_t tm = ballot(kind == EX_TAINT);
+    while (tm) {
+      int src = __ffsll((unsigned long long)tm) - 1;
+      int tid = __shfl(id, src, 64);
+      uint64_t mm = ballot(kind == EX_TAINT && id == tid);
+      if (lane == 0) atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
+      tm &= ~mm;
+    }
+    uint64_t rm = ballot(kind == EX_RESOURCE);
+    while (rm) {
+      int src = __ffsll((unsigned long long)rm) - 1;
+      int rid = __shfl(id, src, 64);
+      uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
+      if (lane == 0) atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
+      rm &= ~mm;
+    }
+  }
+}
+
+
+
+
+
+
+// ----------------------------------------------------------------------------
+// K2: fillInCountsHelper, one level (parents at `level`)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b, int level) {
+  const int eid = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (eid >= b.n || p >= s.level_size[level]) return;
+  const DevEval& ev = b.evals[eid];
+  const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+  const int cl = level + 1;
+  const int32_t inner = ev.ssal[cl];
+  const bool hasInner = inner != 0;
+  const int cb = s.child_off[s.child_base[level] + p];
+  const int ce = s.child_off[s.child_base[level] + p + 1];
+  int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+  const int64_t SD = s.SD;
+  const int coff = s.level_off[cl];
+  int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0;
+  bool has = false;
+  for (int c = cb; c < ce; c++) {
+    const int g = coff + c;
+    int32_t cs = base[g];
+    int32_t css = base[SD + g];
+    int32_t csw = cs, csswl = css, cls = 0;
+    if (leaderReq) {
+      csw = base[2 * SD + g];
+      csswl = base[3 * SD + g];
+      cls = base[4 * SD + g];
+    }
+    if (hasInner) {
+      cs = w_mul(go_div32(cs, inner), inner);
+      csw = w_mul(go_div32(csw, inner), inner);
+    }
+    cap = w_add(cap, cs);
+    slc = w_add(slc, css);
+    if (!leaderReq || cls > 0) {
+      has = true;
+      minD = min(w_sub(cs, csw), minD);
+      minSD = min(w_sub(css, csswl), minSD);
+    }
+    lead = max(cls, lead);
+  }
+  int32_t state = cap;
+  int32_t swl = has ? w_sub(cap, minD) : 0;
+  int32_t sswl = has ? w_sub(slc, minSD) : 0;
+  if (level == ev.slice_level) {
+    slc = go_div32(state, ev.slice_size);
+    sswl = go_div32(swl, ev.slice_size);
+  }
+  const int g = s.level_off[level] + p;
+  base[g] = state;
+  base[SD + g] = slc;
+  if (leaderReq) {
+    base[2 * SD + g] = swl;
+    base[3 * SD + g] = sswl;
+    base[4 * SD + g] = lead;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K3: phase 2, one wave per eval
+// ----------------------------------------------------------------------------
+enum Field : int { F_STATE = 0, F_SLICE = 1, F_SWL = 2, F_SSWL = 3, F_LS = 4 };
+
+struct Wave {
+  const DevSnap* s;
+  const DevEval* ev;
+  int eid;
+  int lane;
+  bool leader, lfc, bf, unconstrained;
+  int32_t* ctr;    // counters of this eval
+  int64_t SD;
+  Key* lds;        // per-wave LDS buffer (list_cap keys)
+  int cap;
+  int32_t* listA;  // global scratch lists (lcap entries each)
+  int32_t* listB;
+  int32_t* listC;
+  int32_t* listD;
+  Key* gkeys;      // global scratch keys (lcap entries)
+  Key* gkeys2;
+  int lcap;
+  bool overflow;
+
+  __device__ int32_t get(Field f, int g) const {
+    if (!leader) {
+      if (f == F_LS) return 0;
+      if (f == F_SWL) f = F_STATE;
+      if (f == F_SSWL) f = F_SLICE;
+    }
+    return ctr[int64_t(f) * SD + g];
+  }
+  // Stored by every lane (see file header).
+  __device__ void set(Field f, int g, int32_t v) {
+    if (!leader) {
+      if (f == F_LS || f == F_SWL || f == F_SSWL) return;
+    }
+    ctr[int64_t(f) * SD + g] = v;
+  }
+  __device__ Key kplain(int g) const {
+    int idx = g - s->level_off[level_of(g)];
+    return key_plain(lfc, get(F_SLICE, g), get(F_STATE, g), idx);
+  }
+  __device__ int level_of(int g) const {
+    int l = 0;
+    while (l + 1 < s->L && g >= s->level_off[l + 1]) l++;
+    return l;
+  }
+};
+
+// ---- LDS bitonic sort of m keys (one wave) ----
+__device__ void lds_sort(Key* k, int n, int lane) {
+  int m = 1;
+  while (m < n) m <<= 1;
+  for (int i = n + lane; i < m; i += kWave) k[i] = key_max();
+  wave_sync();
+  for (int size = 2; size <= m; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < m; i += kWave) {
+        int j = i ^ stride;
+        if (j > i) {
+          bool asc = (i & size) == 0;
+          Key a = k[i], c = k[j];
+          if (key_lt(c, a) == asc) {
+            k[i] = c;
+            k[j] = a;
+          }
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// ---- global merge sort of n keys in `a` (tmp same size); result in a ----
+__device__ void global_sort(Wave& w, Key* a, Key* tmp, int n) {
+  const int lane = w.lane;
+  const int run = w.cap;
+  // sort runs of `run` in LDS
+  for (int r0 = 0; r0 < n; r0 += run) {
+    int m = min(run, n - r0);
+    for (int i = lane; i < m; i += kWave) w.lds[i] = a[r0 + i];
+    wave_sync();
+    lds_sort(w.lds, m, lane);
+    for (int i = lane; i < m; i += kWave) a[r0 + i] = w.lds[i];
+    wave_sync();
+  }
+  Key* src = a;
+  Key* dst = tmp;
+  for (int width = run; width < n; width <<= 1) {
+    for (int r0 = 0; r0 < n; r0 += 2 * width) {
+      int aN = min(width, n - r0);
+      int bN = min(width, max(0, n - r0 - width));
+      const Key* A = src + r0;
+      const Key* B = src + r0 + aN;
+      for (int i = lane; i < aN; i += kWave) {  // rank in B: lower_bound
+        int lo = 0, hi = bN;
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if (key_lt(B[mid], A[i])) lo = mid + 1;
+          else hi = mid;
+        }
+        dst[r0 + i + lo] = A[i];
+      }
+      for (int j = lane; j < bN; j += kWave) {  // rank in A: upper_bound
+        int lo = 0, hi = aN;
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if (key_le(A[mid], B[j])) lo = mid + 1;
+          else hi = mid;
+        }
+        dst[r0 + j + lo] = B[j];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    Key* t = src;
+    src = dst;
+    dst = t;
+  }
+  if (src != a) {
+    for (int i = lane; i < n; i += kWave) a[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
+}
+
+// ---- sequences walked by updateCountsToMinimumGeneric ----
+// Explicit order: domain gids at positions [0, n) (LDS keys or a global list).
+struct SeqLds {
+  Wave* w;
+  int n, level_off, pos;
+  __device__ int size() const { return n; }
+  __device__ bool done() const { return pos >= n; }
+  __device__ int cur() const { return level_off + int(uint32_t(w->lds[pos].lo)); }
+  __device__ void next() { pos++; }
+  __device__ int at(int p) const { return level_off + int(uint32_t(w->lds[p].lo)); }
+  // findBestFitDomainBy over domains[pos:] (:1216-1231)
+  __device__ int bestfit(int32_t needed, Field f) const {
+    int g0 = cur();
+    if (w->get(f, g0) < needed) return g0;
+    uint64_t best = ~0ull;
+    for (int p = pos + w->lane; p < n; p += kWave) {
+      int32_t st = w->get(f, at(p));
+      if (st >= needed) {
+        uint64_t k = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
+        best = k < best ? k : best;
+      }
+    }
+    best = wave_min_u64(best);
+    return at(int(uint32_t(best)));
+  }
+};
+
+struct SeqList {
+  Wave* w;
+  const int32_t* g;
+  int n, pos;
+  __device__ int size() const { return n; }
+  __device__ bool done() const { return pos >= n; }
+  __device__ int cur() const { return g[pos]; }
+  __device__ void next() { pos++; }
+  __device__ int bestfit(int32_t needed, Field f) const {
+    int g0 = cur();
+    if (w->get(f, g0) < needed) return g0;
+    uint64_t best = ~0ull;
+    for (int p = pos + w->lane; p < n; p += kWave) {
+      int32_t st = w->get(f, g[p]);
+      if (st >= needed) {
+        uint64_t k = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
+        best = k < best ? k : best;
+      }
+    }
+    best = wave_min_u64(best);
+    return g[int(uint32_t(best))];
+  }
+};
+
+// Lazy sorted iteration over n materialized (unsorted) keys of one level.
+struct SeqLazy {
+  Wave* w;
+  const Key* k;
+  int n, level_off;
+  Key curk;
+  bool valid;
+  __device__ void find_next(bool first) {
+    Key best = key_max();
+    for (int i = w->lane; i < n; i += kWave) {
+      Key x = k[i];
+      if ((first || key_lt(curk, x)) && key_lt(x, best)) best = x;
+    }
+    best = wave_min_key(best);
+    valid = !(best.hi == ~0ull && best.lo == ~0ull);
+    curk = best;
+  }
+  __device__ void start() { find_next(true); }
+  __device__ bool done() const { return !valid; }
+  __device__ int cur() const { return level_off + int(uint32_t(curk.lo)); }
+  __device__ void next() { find_next(false); }
+  __device__ int bestfit(int32_t needed, Field f) const {
+    int g0 = cur();
+    if (w->get(f, g0) < needed) return g0;
+    uint32_t bst = ~0u;
+    for (int i = w->lane; i < n; i += kWave) {
+      Key x = k[i];
+      if (key_le(curk, x)) {
+        int32_t st = w->get(f, level_off + int(uint32_t(x.lo)));
+        if (st >= needed && s_asc(st) < bst) bst = s_asc(st);
+      }
+    }
+    bst = uint32_t(wave_min_u64(uint64_t(bst)));
+    Key best = key_max();
+    for (int i = w->lane; i < n; i += kWave) {
+      Key x = k[i];
+      if (key_le(curk, x) && key_lt(x, best)) {
+        int32_t st = w->get(f, level_off + int(uint32_t(x.lo)));
+        if (st >= needed && s_asc(st) == bst) best = x;
+      }
+    }
+    best = wave_min_key(best);
+    return level_off + int(uint32_t(best.lo));
+  }
+};
+
+// consumeWithLeadersGeneric (:1348-1403)
+template <class Seq>
+__device__ int consume_with_leaders(Wave& w, Seq& seq, int domain, int32_t* remP, int32_t* remL, Field wl, Field pr,
+                                    int32_t sliceSize, bool slices, bool* completed) {
+  if (w.bf && w.get(wl, domain) >= *remP && w.get(F_LS, domain) >= *remL) {
+    if (slices) {
+      domain = seq.bestfit(*remP, *remL > 0 ? F_SSWL : F_SLICE);
+      wl = F_SSWL;
+      pr = F_SLICE;
+    } else {
+      domain = seq.bestfit(*remP, *remL > 0 ? F_SWL : F_STATE);
+      wl = F_SWL;
+      pr = F_STATE;
+    }
+  }
+  if (w.get(wl, domain) >= *remP && w.get(F_LS, domain) >= *remL) {
+    w.set(pr, domain, *remP);
+    w.set(F_LS, domain, *remL);
+    w.set(F_STATE, domain, w_mul(*remP, sliceSize));
+    *completed = true;
+    return domain;
+  }
+  if (slices) {
+    if (w.get(wl, domain) > *remP) w.set(wl, domain, *remP);
+    if (w.get(F_LS, domain) > *remL) w.set(F_LS, domain, *remL);
+    w.set(F_STATE, domain, w_mul(w.get(wl, domain), sliceSize));
+    *remL = w_sub(*remL, w.get(F_LS, domain));
+    *remP = w_sub(*remP, w.get(wl, domain));
+    *completed = false;
+    return domain;
+  }
+  *remP = w_sub(*remP, w.get(wl, domain));
+  *remL = w_sub(*remL, w.get(F_LS, domain));
+  if (w.get(wl, domain) > *remP) w.set(wl, domain, *remP);
+  if (w.get(F_LS, domain) > *remL) w.set(F_LS, domain, *remL);
+  *completed = false;
+  return domain;
+}
+
+// updateCountsToMinimumGeneric (:1405-1469).  Appends to out[*np..].  Returns
+// false on the "code assumptions violated" path (Go returns nil): the appended
+// entries are then dropped.
+template <class Seq>
+__device__ bool update_counts(Wave& w, Seq& seq, int32_t count, int32_t leaderCount, int32_t sliceSize, bool slices,
+                              int32_t* out, int* np) {
+  const int start = *np;
+  int32_t remP = slices ? go_div32(count, sliceSize) : count;
+  int32_t remL = leaderCount;
+  auto push = [&](int g) {
+    if (*np < w.lcap) out[*np] = g;
+    else w.overflow = true;
+    (*np)++;
+  };
+  for (; !seq.done(); seq.next()) {
+    int dom = seq.cur();
+    if (remL > 0) {
+      bool completed = false;
+      int d = slices ? consume_with_leaders(w, seq, dom, &remP, &remL, F_SSWL, F_SLICE, sliceSize, true, &completed)
+                     : consume_with_leaders(w, seq, dom, &remP, &remL, F_SWL, F_STATE, 1, false, &completed);
+      push(d);
+      if (completed) return true;
+      continue;
+    }
+    if (slices) {
+      if (w.bf && w.get(F_SLICE, dom) >= remP) dom = seq.bestfit(remP, F_SLICE);
+      w.set(F_LS, dom, 0);
+      int32_t sl = w.get(F_SLICE, dom);
+      if (sl >= remP) {
+        w.set(F_STATE, dom, w_mul(remP, sliceSize));
+        w.set(F_SLICE, dom, remP);
+        push(dom);
+        return true;
+      }
+      w.set(F_STATE, dom, w_mul(sl, sliceSize));
+      remP = w_sub(remP, sl);
+      push(dom);
+      continue;
+    }
+    if (w.bf && w.get(F_STATE, dom) >= remP) dom = seq.bestfit(remP, F_STATE);
+    w.set(F_LS, dom, 0);
+    int32_t st = w.get(F_STATE, dom);
+    if (st >= remP) {
+      w.set(F_STATE, dom, remP);
+      push(dom);
+      return true;
+    }
+    remP = w_sub(remP, st);
+    push(dom);
+  }
+  *np = start;
+  return false;
+}
+
+// Walk an explicit list of gids of one level in the order given by `plain`
+// sortedDomains: LDS sort when it fits, lazy iteration otherwise.
+__device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t leaderCount,
+                            int32_t sliceSize, bool slices, int32_t sliceRecompute, int32_t* out, int* np) {
+  const int loff = w.s->level_off[level];
+  if (n <= w.cap) {
+    for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain(gids[i]);
+    wave_sync();
+    lds_sort(w.lds, n, w.lane);
+    if (sliceRecompute > 1) {  // multi-layer: recompute sliceState after sorting (:956-965)
+      for (int i = 0; i < n; i++) {
+        int g = loff + int(uint32_t(w.lds[i].lo));
+        w.set(F_SLICE, g, go_div32(w.get(F_STATE, g), sliceRecompute));
+        w.set(F_SSWL, g, go_div32(w.get(F_SWL, g), sliceRecompute));
+      }
+    }
+    SeqLds seq{&w, n, loff, 0};
+    bool ok = update_counts(w, seq, count, leaderCount, sliceSize, slices, out, np);
+    wave_sync();
+    return ok;
+  }
+  if (n > w.lcap) {
+    w.overflow = true;
+    return false;
+  }
+  for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = w.kplain(gids[i]);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  if (sliceRecompute > 1) {
+    for (int i = 0; i < n; i++) {
+      int g = gids[i];
+      w.set(F_SLICE, g, go_div32(w.get(F_STATE, g), sliceRecompute));
+      w.set(F_SSWL, g, go_div32(w.get(F_SWL, g), sliceRecompute));
+    }
+  }
+  SeqLazy seq{&w, w.gkeys, n, loff, Key{0, 0}, false};
+  seq.start();
+  return update_counts(w, seq, count, leaderCount, sliceSize, slices, out, np);
+}
+
+// Children (CSR) of `n` domains at `level` appended to out (lowerLevelDomains :1503-1509).
+__device__ int gather_children(Wave& w, const int32_t* parents, int n, int level, int32_t* out) {
+  const DevSnap& s = *w.s;
+  const int poff = s.level_off[level];
+  const int coff = s.level_off[level + 1];
+  int np = 0;
+  for (int i = 0; i < n; i++) {
+    int p = parents[i] - poff;
+    int cb = s.child_off[s.child_base[level] + p];
+    int ce = s.child_off[s.child_base[level] + p + 1];
+    int cnt = ce - cb;
+    if (np + cnt > w.lcap) {
+      w.overflow = true;
+      return np;
+    }
+    for (int j = w.lane; j < cnt; j += kWave) out[np + j] = coff + cb + j;
+    np += cnt;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  return np;
+}
+
+// multiLayerNotFitMessage numbers (:1754-1793)
+__device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
+  const DevSnap& s = *w.s;
+  const int D = s.level_size[level];
+  const int loff = s.level_off[level];
+  uint64_t best = ~0ull;
+  for (int i = w.lane; i < D; i += kWave) {
+    int g = loff + i;
+    uint32_t rank = s.id_rank ? uint32_t(s.id_rank[g]) : uint32_t(i);
+    // highest sliceState, ties: smaller DomainID string
+    uint64_t k = (uint64_t(s_desc(w.get(F_SLICE, g))) << 32) | rank;
+    best = k < best ? k : best;
+  }
+  best = wave_min_u64(best);
+  // recover the index of the domain with that rank
+  int bidx = -1;
+  uint32_t brank = uint32_t(best);
+  for (int i = w.lane; i < D; i += kWave) {
+    uint32_t rank = s.id_rank ? uint32_t(s.id_rank[loff + i]) : uint32_t(i);
+    if (rank == brank) bidx = i;
+  }
+  for (int m = 32; m >= 1; m >>= 1) bidx = max(bidx, __shfl_xor(bidx, m, 64));
+  for (int c = 0; c < w.ev->num_layers && c < KUEUE_TAS_MAX_LAYERS; c++) {
+    int t = w.ev->layer_level[c];
+    int32_t size = w.ev->layer_size[c];
+    o.ml_need[c] = go_div32(w.ev->count, size);
+    int32_t fit = 0;
+    if (t == level) {
+      fit = go_div32(w.get(F_STATE, loff + bidx), size);
+    } else if (t > level) {
+      int lo = bidx, hi = bidx + 1;
+      for (int l = level; l < t; l++) {
+        lo = s.child_off[s.child_base[l] + lo];
+        hi = s.child_off[s.child_base[l] + hi];
+      }
+      int32_t acc = 0;
+      for (int i = lo + w.lane; i < hi; i += kWave) acc = w_add(acc, go_div32(w.get(F_STATE, s.level_off[t] + i), size));
+      fit = wave_sum_wrap32(acc);
+    }
+    o.ml_fit[c] = fit;
+  }
+}
+
+// notFitReason (:1253-1258)
+__device__ void not_fit(Wave& w, int level, int32_t fit, int32_t total, kueue_tas_eval_out& o) {
+  if (w.ev->flags & KUEUE_TAS_F_MULTILAYER) {
+    o.status = KUEUE_TAS_ST_MULTILAYER;
+    o.a = level;
+    multilayer_message(w, level, o);
+  } else {
+    o.status = KUEUE_TAS_ST_NOT_FIT;
+    o.a = fit;
+    o.b = total;
+  }
+}
+
+// Write (leaf, count) entries sorted by leaf index (buildAssignment :1490-1501).
+__device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, bool positive_only, int32_t* ent, int ent_cap,
+                           int base) {
+  const int loff = w.s->level_off[w.s->L - 1];
+  Key* arr;
+  if (n <= w.cap) {
+    for (int i = w.lane; i < n; i += kWave) w.lds[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
+    wave_sync();
+    lds_sort(w.lds, n, w.lane);
+    arr = w.lds;
+  } else {
+    for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    global_sort(w, w.gkeys, w.gkeys2, n);
+    arr = w.gkeys;
+  }
+  int cnt = base;
+  for (int i0 = 0; i0 < n; i0 += kWave) {
+    int i = i0 + w.lane;
+    int32_t leaf = 0, v = 0;
+    bool keep = false;
+    if (i < n) {
+      leaf = int32_t(uint32_t(arr[i].lo));
+      v = use_ls ? w.get(F_LS, loff + leaf) : w.get(F_STATE, loff + leaf);
+      keep = positive_only ? v > 0 : v != 0;
+    }
+    uint64_t m = ballot(keep);
+    int rank = __popcll(m & ((1ull << w.lane) - 1ull));
+    if (keep) {
+      int pos = cnt + rank;
+      if (pos < ent_cap) {
+        ent[2 * pos] = leaf;
+        ent[2 * pos + 1] = v;
+      }
+    }
+    cnt += __popcll(m);
+  }
+  wave_sync();
+  return cnt - base;
+}
+
+// LeastFreeCapacity greedy over all leaves without leaders (the
+// findLevelWithFitDomains greedy :1278-1318 followed by
+// updateCountsToMinimumGeneric, LFC order) for n > LDS capacity: histogram
+// threshold select on sliceState instead of a full sort.  Requires every
+// leaf sliceState >= 0.  Returns 1 done, 0 needs the generic path.
+__device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& o, int32_t* ent, int ent_cap) {
+  const DevSnap& s = *w.s;
+  const int D = s.N;
+  const int loff = s.level_off[s.L - 1];
+  const int32_t ss = w.ev->slice_size;
+  constexpr int kBins = 256;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B (host: list_cap >= 64)
+  for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
+  wave_sync();
+  int64_t over = 0;
+  for (int i = w.lane; i < D; i += kWave) {
+    int32_t v = w.get(F_SLICE, loff + i);
+    if (v > 0) {
+      if (v < kBins) {
+        atomicAdd(&hist[v], 1u);
+      } else {
+        over += v;
+      }
+    }
+  }
+  wave_sync();
+  over = wave_sum_i64(over);
+  // find the threshold value t (ascending)
+  int64_t need = sliceCount;
+  int64_t before = 0;
+  int t = -1;
+  for (int v = 1; v < kBins; v++) {
+    int64_t add = int64_t(hist[v]) * v;
+    if (before + add >= need) {
+      t = v;
+      break;
+    }
+    before += add;
+  }
+  if (t < 0) {
+    if (before + over >= need) return 0;  // threshold in the overflow range: generic path
+    // not enough capacity: greedy fails with remaining = need - total (:1315-1316)
+    int64_t total = before + over;
+    not_fit(w, s.L - 1, int32_t(total), sliceCount, o);
+    return 1;
+  }
+  int64_t m = (need - before + t - 1) / t;  // elements of value t taken (last one is the crossing)
+  int32_t rem_last = int32_t(need - before - (m - 1) * t);
+  // order inside value t: state asc, then index asc
+  int32_t u = t * ss;  // state threshold
+  int64_t mp = m;      // rank among (value t, state u) in index order
+  if (ss > 1) {
+    if (ss > kBins) return 0;
+    for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = w.lane; i < D; i += kWave) {
+      int g = loff + i;
+      if (w.get(F_SLICE, g) == t) atomicAdd(&hist[w.get(F_STATE, g) - t * ss], 1u);
+    }
+    wave_sync();
+    int64_t acc = 0;
+    int j = 0;
+    for (; j < ss; j++) {
+      if (acc + hist[j] >= m) break;
+      acc += hist[j];
+    }
+    u = t * ss + j;
+    mp = m - acc;
+  }
+  // emit in index order: v < t (v > 0), or v == t && state < u, or (state == u && rank < mp)
+  int64_t seen = 0;
+  int cnt = 0;
+  for (int i0 = 0; i0 < D; i0 += kWave) {
+    int i = i0 + w.lane;
+    int32_t v = 0, st = 0;
+    if (i < D) {
+      v = w.get(F_SLICE, loff + i);
+      st = w.get(F_STATE, loff + i);
+    }
+    bool tie = i < D && v == t && st == u;
+    uint64_t tm = ballot(tie);
+    int64_t r = seen + __popcll(tm & ((1ull << w.lane) - 1ull));
+    bool keep = i < D && ((v > 0 && v < t) || (v == t && st < u) || (tie && r < mp));
+    bool crossing = tie && r == mp - 1;
+    int32_t val = crossing ? w_mul(rem_last, ss) : w_mul(v, ss);
+    uint64_t km = ballot(keep);
+    int rank = __popcll(km & ((1ull << w.lane) - 1ull));
+    if (keep) {
+      int pos = cnt + rank;
+      if (pos < ent_cap) {
+        ent[2 * pos] = i;
+        ent[2 * pos + 1] = val;
+      }
+    }
+    cnt += __popcll(km);
+    seen += __popcll(tm);
+  }
+  o.status = KUEUE_TAS_ST_OK;
+  o.fit_level = s.L - 1;
+  o.num_workers = cnt;
+  if (cnt > ent_cap) o.status = KUEUE_TAS_ST_INTERNAL;
+  return 1;
+}
+
+// findLevelWithFitDomains (:1236-1321).  Returns: 0 ok (results in listA,
+// *nres), 1 failure (o filled), 2 finished by the LFC fast path (o filled).
+__device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, kueue_tas_eval_out& o, int32_t* ent,
+                          int ent_cap) {
+  const DevSnap& s = *w.s;
+  const DevEval& ev = *w.ev;
+  const bool required = (ev.flags & KUEUE_TAS_F_REQUIRED) != 0;
+  const int32_t leaderCount = w.leader ? 1 : 0;
+  const int32_t sliceCount = go_div32(ev.count, ev.slice_size);
+  int level = ev.requested_level;
+  for (;;) {
+    const int D = s.level_size[level];
+    const int loff = s.level_off[level];
+    if (D == 0) {
+      o.status = KUEUE_TAS_ST_NO_DOMAINS;
+      o.a = level;
+      return 1;
+    }
+    // sortedDomainsWithLeader: first (top), last, LFC first fit, BF best fit
+    Key top = key_max(), lfcfit = key_max(), last = Key{0, 0};
+    bool has_last = false;
+    int32_t minss = 0x7fffffff;
+    for (int i = w.lane; i < D; i += kWave) {
+      int g = loff + i;
+      int32_t ls = w.get(F_LS, g), sswl = w.get(F_SSWL, g), swl = w.get(F_SWL, g), ss = w.get(F_SLICE, g);
+      Key k = key_wl(w.lfc, ls, sswl, swl, i);
+      if (key_lt(k, top)) top = k;
+      if (!has_last || key_lt(last, k)) {
+        last = k;
+        has_last = true;
+      }
+      if (ss >= sliceCount && key_lt(k, lfcfit)) lfcfit = k;
+      minss = min(minss, ss);
+    }
+    top = wave_min_key(top);
+    lfcfit = wave_min_key(lfcfit);
+    {  // max key
+      Key inv{~last.hi, ~last.lo};
+      if (!has_last) inv = key_max();
+      inv = wave_min_key(inv);
+      last = Key{~inv.hi, ~inv.lo};
+    }
+    for (int m = 32; m >= 1; m >>= 1) minss = min(minss, __shfl_xor(minss, m, 64));
+    int topg = loff + int(uint32_t(top.lo));
+    if (w.bf && w.get(F_SSWL, topg) >= sliceCount && w.get(F_LS, topg) >= leaderCount) {
+      // findBestFitDomainForSlices(sorted, sliceCount, leaderCount)
+      Field f = leaderCount > 0 ? F_SSWL : F_SLICE;
+      if (w.get(f, topg) >= sliceCount) {
+        uint32_t bst = ~0u;
+        for (int i = w.lane; i < D; i += kWave) {
+          int32_t st = w.get(f, loff + i);
+          if (st >= sliceCount && s_asc(st) < bst) bst = s_asc(st);
+        }
+        bst = uint32_t(wave_min_u64(uint64_t(bst)));
+        Key b = key_max();
+        for (int i = w.lane; i < D; i += kWave) {
+          int g = loff + i;
+          if (s_asc(w.get(f, g)) == bst) {
+            Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+            if (key_lt(k, b)) b = k;
+          }
+        }
+        b = wave_min_key(b);
+        topg = loff + int(uint32_t(b.lo));
+      }
+    }
+    if (w.lfc) {
+      if (!(lfcfit.hi == ~0ull && lfcfit.lo == ~0ull)) {
+        results[0] = loff + int(uint32_t(lfcfit.lo));
+        *nres = 1;
+        *fitLevel = level;
+        return 0;
+      }
+      if (required) {
+        not_fit(w, level, w.get(F_STATE, loff + int(uint32_t(last.lo))), sliceCount, o);
+        return 1;
+      }
+    }
+    if (w.get(F_SSWL, topg) < sliceCount || w.get(F_LS, topg) < leaderCount) {
+      if (required) {
+        not_fit(w, level, w.get(F_SLICE, topg), sliceCount, o);
+        return 1;
+      }
+      if (level > 0 && !w.unconstrained) {
+        level--;
+        continue;
+      }
+      // ---- greedy over several domains (:1278-1318) ----
+      int32_t remS = sliceCount, remL = leaderCount;
+      int nr = 0;
+      if (D <= w.cap) {
+        for (int i = w.lane; i < D; i += kWave) {
+          int g = loff + i;
+          w.lds[i] = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+        }
+        wave_sync();
+        lds_sort(w.lds, D, w.lane);
+        SeqLds seq{&w, D, loff, 0};
+        int idx = 0;
+        for (; remL > 0 && idx < D && w.get(F_LS, seq.at(idx)) > 0; idx++) {
+          seq.pos = idx;
+          int d = seq.at(idx);
+          if (w.bf && w.get(F_SSWL, d) >= remS) d = seq.bestfit(remS, remL > 0 ? F_SSWL : F_SLICE);
+          results[nr++] = d;
+          remL = w_sub(remL, w.get(F_LS, d));
+          remS = w_sub(remS, w.get(F_SSWL, d));
+        }
+        if (remL > 0) {
+          not_fit(w, level, w_sub(leaderCount, remL), sliceCount, o);
+          wave_sync();
+          return 1;
+        }
+        // re-sort the remainder sortedDomainsWithLeader[idx:] with sortedDomains
+        const int nrem = D - idx;
+        for (int i = w.lane; i < nrem; i += kWave) w.gkeys[i] = w.lds[idx + i];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        wave_sync();
+        for (int i = w.lane; i < nrem; i += kWave) w.lds[i] = w.kplain(loff + int(uint32_t(w.gkeys[i].lo)));
+        wave_sync();
+        lds_sort(w.lds, nrem, w.lane);
+        SeqLds seq2{&w, nrem, loff, 0};
+        for (int i = 0; remS > 0 && i < nrem; i++) {
+          seq2.pos = i;
+          int d = seq2.at(i);
+          if (w.bf && w.get(F_SLICE, d) >= remS) d = seq2.bestfit(remS, F_SLICE);
+          results[nr++] = d;
+          remS = w_sub(remS, w.get(F_SLICE, d));
+        }
+        wave_sync();
+      } else {
+        if (w.lfc && !w.leader && level == s.L - 1 && minss >= 0) {
+          if (lfc_leaf_greedy(w, sliceCount, o, ent, ent_cap)) return 2;
+        }
+        // lazy iteration with live keys (no counter mutation inside findLevelWithFitDomains)
+        Key lastwl{0, 0};
+        bool consumed = false;
+        Key cur = top;  // first in WL order
+        bool valid = true;
+        while (remL > 0 && valid && w.get(F_LS, loff + int(uint32_t(cur.lo))) > 0) {
+          int d = loff + int(uint32_t(cur.lo));
+          if (w.bf && w.get(F_SSWL, d) >= remS) {
+            Field f = remL > 0 ? F_SSWL : F_SLICE;
+            if (w.get(f, d) >= remS) {
+              uint32_t bst = ~0u;
+              for (int i = w.lane; i < D; i += kWave) {
+                int g = loff + i;
+                Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+                int32_t st = w.get(f, g);
+                if (key_le(cur, k) && st >= remS && s_asc(st) < bst) bst = s_asc(st);
+              }
+              bst = uint32_t(wave_min_u64(uint64_t(bst)));
+              Key b = key_max();
+              for (int i = w.lane; i < D; i += kWave) {
+                int g = loff + i;
+                Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+                if (key_le(cur, k) && s_asc(w.get(f, g)) == bst && key_lt(k, b)) b = k;
+              }
+              b = wave_min_key(b);
+              d = loff + int(uint32_t(b.lo));
+            }
+          }
+          if (nr < w.lcap) results[nr] = d;
+          else w.overflow = true;
+          nr++;
+          remL = w_sub(remL, w.get(F_LS, d));
+          remS = w_sub(remS, w.get(F_SSWL, d));
+          lastwl = cur;
+          consumed = true;
+          // next in WL order
+          Key nb = key_max();
+          for (int i = w.lane; i < D; i += kWave) {
+            int g = loff + i;
+            Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+            if (key_lt(cur, k) && key_lt(k, nb)) nb = k;
+          }
+          nb = wave_min_key(nb);
+          valid = !(nb.hi == ~0ull && nb.lo == ~0ull);
+          cur = nb;
+        }
+        if (remL > 0) {
+          not_fit(w, level, w_sub(leaderCount, remL), sliceCount, o);
+          return 1;
+        }
+        // remainder (WL key > lastwl) in sortedDomains order
+        Key pc = key_max();
+        bool first = true;
+        for (;;) {
+          if (remS <= 0) break;
+          Key nb = key_max();
+          for (int i = w.lane; i < D; i += kWave) {
+            int g = loff + i;
+            if (consumed) {
+              Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+              if (!key_lt(lastwl, kw)) continue;
+            }
+            Key kp = w.kplain(g);
+            if ((first || key_lt(pc, kp)) && key_lt(kp, nb)) nb = kp;
+          }
+          nb = wave_min_key(nb);
+          if (nb.hi == ~0ull && nb.lo == ~0ull) break;
+          first = false;
+          pc = nb;
+          int d = loff + int(uint32_t(nb.lo));
+          if (w.bf && w.get(F_SLICE, d) >= remS) {
+            uint32_t bst = ~0u;
+            for (int i = w.lane; i < D; i += kWave) {
+              int g = loff + i;
+              if (consumed) {
+                Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+                if (!key_lt(lastwl, kw)) continue;
+              }
+              Key kp = w.kplain(g);
+              int32_t st = w.get(F_SLICE, g);
+              if (key_le(pc, kp) && st >= remS && s_asc(st) < bst) bst = s_asc(st);
+            }
+            bst = uint32_t(wave_min_u64(uint64_t(bst)));
+            Key b = key_max();
+            for (int i = w.lane; i < D; i += kWave) {
+              int g = loff + i;
+              if (consumed) {
+                Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+                if (!key_lt(lastwl, kw)) continue;
+              }
+              Key kp = w.kplain(g);
+              if (key_le(pc, kp) && s_asc(w.get(F_SLICE, g)) == bst && key_lt(kp, b)) b = kp;
+            }
+            b = wave_min_key(b);
+            d = loff + int(uint32_t(b.lo));
+          }
+          if (nr < w.lcap) results[nr] = d;
+          else w.overflow = true;
+          nr++;
+          remS = w_sub(remS, w.get(F_SLICE, d));
+        }
+      }
+      if (remS > 0) {
+        not_fit(w, level, w_sub(sliceCount, remS), sliceCount, o);
+        return 1;
+      }
+      *nres = nr;
+      *fitLevel = level;
+      return 0;
+    }
+    results[0] = topg;
+    *nres = 1;
+    *fitLevel = level;
+    return 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
+  extern __shared__ Key lds_all[];
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int eid = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (eid >= b.n) return;
+  const DevEval& ev = b.evals[eid];
+  Wave w;
+  w.s = &s;
+  w.ev = &ev;
+  w.eid = eid;
+  w.lane = lane;
+  w.leader = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+  w.lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
+  w.bf = !w.lfc;
+  w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
+  w.ctr = b.counters + int64_t(eid) * b.ctr_stride;
+  w.SD = s.SD;
+  w.lds = lds_all + int64_t(wave) * b.list_cap;
+  w.cap = b.list_cap;
+  int64_t lcap = b.scratch_stride / 6;  // 4 int32 lists (2 per u64) + 2 key arrays (2 u64 per key)
+  uint64_t* sc = b.scratch + int64_t(eid) * b.scratch_stride;
+  w.lcap = int(lcap);
+  w.listA = reinterpret_cast<int32_t*>(sc);
+  w.listB = w.listA + lcap;
+  w.listC = w.listB + lcap;
+  w.listD = w.listC + lcap;
+  w.gkeys = reinterpret_cast<Key*>(sc + 2 * lcap);
+  w.gkeys2 = w.gkeys + lcap;
+  w.overflow = false;
+  int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
+  const int ecap = b.entry_cap;
+
+  kueue_tas_eval_out o;
+  o.status = KUEUE_TAS_ST_OK;
+  o.a = o.b = 0;
+  o.fit_level = 0;
+  o.num_workers = o.num_leaders = 0;
+  o.assignment_nil = 0;
+  o.total_nodes = s.N;
+  o.excl_selector = b.sel_counts[eid];
+  o.excl_affinity = 0;
+  o.excl_topology = 0;
+  for (int c = 0; c < KUEUE_TAS_MAX_LAYERS; c++) o.ml_fit[c] = o.ml_need[c] = 0;
+  o.reserved[0] = o.reserved[1] = 0;
+
+  int nres = 0, fitLevel = 0;
+  int r = find_level(w, w.listA, &nres, &fitLevel, o, ent, ecap);
+  if (r == 0) {
+    const int L = s.L;
+    const int32_t leaderCount = w.leader ? 1 : 0;
+    int32_t* cur = w.listB;
+    int ncur = 0;
+    // currFitDomain = updateCountsToMinimumGeneric(currFitDomain, ...) (:928)
+    SeqList seq0{&w, w.listA, nres, 0};
+    bool ok = update_counts(w, seq0, ev.count, leaderCount, ev.slice_size, true, cur, &ncur);
+    if (!ok) o.assignment_nil = 1;
+    int level = fitLevel;
+    int32_t* spare = w.listA;
+    for (; level < min(L - 1, ev.slice_level); level++) {  // above the slice level (:930-935)
+      int nch = gather_children(w, cur, ncur, level, w.listC);
+      int nn = 0;
+      bool ok2 = walk_sorted(w, w.listC, nch, level + 1, ev.count, leaderCount, ev.slice_size, true, 0, spare, &nn);
+      if (!ok2) o.assignment_nil = 1;
+      int32_t* t = cur;
+      cur = spare;
+      spare = t;
+      ncur = nn;
+    }
+    for (; level < L - 1; level++) {  // at/below the slice level (:937-971)
+      int32_t sol = ev.slice_size;
+      if (level >= ev.slice_level) {
+        sol = 1;
+        if (ev.ssal[level + 1] != 0) sol = ev.ssal[level + 1];
+      }
+      int nn = 0;
+      const int poff = s.level_off[level];
+      for (int i = 0; i < ncur; i++) {
+        int d = cur[i];
+        int p = d - poff;
+        int cb = s.child_off[s.child_base[level] + p];
+        int ce = s.child_off[s.child_base[level] + p + 1];
+        int nch = ce - cb;
+        if (nch > w.lcap) {
+          w.overflow = true;
+          break;
+        }
+        for (int j = lane; j < nch; j += kWave) w.listC[j] = s.level_off[level + 1] + cb + j;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        bool ok3 = walk_sorted(w, w.listC, nch, level + 1, w.get(F_STATE, d), w.get(F_LS, d), sol, sol > 1, sol, spare,
+                               &nn);
+        if (!ok3) o.assignment_nil = 1;
+      }
+      int32_t* t = cur;
+      cur = spare;
+      spare = t;
+      ncur = nn;
+    }
+    o.fit_level = fitLevel;
+    if (w.leader) {
+      // leaders: copies with state = leaderState (:975-994)
+      int nl = 0, nw = 0;
+      for (int i = 0; i < ncur; i++) {
+        if (w.get(F_LS, cur[i]) > 0) spare[nl++] = cur[i];
+        if (w.get(F_STATE, cur[i]) > 0) w.listD[nw++] = cur[i];
+      }
+      o.num_workers = emit_sorted(w, w.listD, nw, false, false, ent, ecap, 0);
+      o.num_leaders = emit_sorted(w, spare, nl, true, true, ent, ecap, o.num_workers);
+    } else {
+      o.num_workers = emit_sorted(w, cur, ncur, false, false, ent, ecap, 0);
+    }
+    if (o.num_workers + o.num_leaders > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
+  }
+  if (w.overflow) o.status = KUEUE_TAS_ST_INTERNAL;
+  if (lane == 0) b.out[eid] = o;
+}
+
+// Snapshot delta: tas_usage[col][leaf] += delta (updateTASUsage :257-293)
+__global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present, int N, const kueue_tas_delta* d,
+                                    int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  kueue_tas_delta x = d[i];
+  atomicAdd(reinterpret_cast<unsigned long long*>(&tas_usage[int64_t(x.col) * N + x.leaf]),
+            (unsigned long long)(uint64_t(x.delta)));
+  atomicOr(&usage_present[x.leaf], 1u << x.col);
+}
+
+}  // namespace ktas

@@ -1,0 +1,156 @@
+"""ctypes binding of libkueue_tas.so (include/kueue_tas.h).
+
+This is the product path: every evaluation runs the HIP kernels of
+``csrc/tas_kernels.hip``.  There is no CPU fallback — if the shared library or
+a HIP device is missing, construction raises ``NativeLibraryMissing``.
+
+``TASFlavorSnapshot`` mirrors the reference's Go type of the same name
+(pkg/cache/scheduler/tas_flavor_snapshot.go:109-137) at the granularity the
+host layer exposes: build from a snapshot document (nodes, pods, levels,
+flavor node labels/tolerations, TAS usage, feature gates), then
+``find_topology_assignments_for_flavor`` (:519) or the batched
+``find_topology_assignments_for_workloads`` (the nominate batch of
+pkg/scheduler/scheduler.go:583-619).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_CSRC = os.path.join(_PKG, "csrc")
+_BUILD = os.path.join(_PKG, "_build")
+_LIB = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    """libkueue_tas.so could not be loaded or no HIP device is usable."""
+
+
+def library_path() -> str:
+    return os.path.join(_BUILD, "libkueue_tas.so")
+
+
+def build_native(jobs: int = 4) -> str:
+    """Compile libkueue_tas.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", _CSRC], check=True)
+    return library_path()
+
+
+class KueueTasConfig(ctypes.Structure):
+    _fields_ = [("list_cap", ctypes.c_int32), ("max_batch", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+EXPORTED_SYMBOLS = [
+    "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
+    "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch",
+    "kueue_tas_last_timings", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
+    "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_free",
+]
+
+
+def load_library():
+    """Load the in-tree libkueue_tas.so (raises NativeLibraryMissing)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = library_path()
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(f"{path} not built (run __graft_entry__.build())")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:  # pragma: no cover - environment specific
+        raise NativeLibraryMissing(str(e)) from e
+    c = ctypes
+    lib.kueue_tas_abi_version.restype = c.c_int
+    lib.kueue_tas_host_create.argtypes = [c.c_char_p, c.POINTER(KueueTasConfig)]
+    lib.kueue_tas_host_create.restype = c.c_void_p
+    lib.kueue_tas_host_destroy.argtypes = [c.c_void_p]
+    lib.kueue_tas_host_last_error.argtypes = [c.c_void_p]
+    lib.kueue_tas_host_last_error.restype = c.c_char_p
+    lib.kueue_tas_host_find.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_find.restype = c.c_int
+    lib.kueue_tas_host_find_batch.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_find_batch.restype = c.c_int
+    lib.kueue_tas_host_compile.argtypes = [c.c_void_p, c.c_char_p]
+    lib.kueue_tas_host_compile.restype = c.c_int
+    lib.kueue_tas_host_run_compiled.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
+    lib.kueue_tas_host_run_compiled.restype = c.c_int
+    lib.kueue_tas_free.argtypes = [c.c_void_p]
+    _LIB = lib
+    return lib
+
+
+def _take(lib, p) -> dict:
+    s = ctypes.cast(p, ctypes.c_char_p).value.decode()
+    lib.kueue_tas_free(p)
+    return json.loads(s)
+
+
+class TASFlavorSnapshot:
+    """Device-resident TAS snapshot of one ResourceFlavor (reference
+    tas_flavor_snapshot.go:109).  ``snapshot`` follows the fixture schema of
+    tools/extract_goldens.py (podSets ignored)."""
+
+    def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0):
+        self._lib = load_library()
+        cfg = KueueTasConfig(list_cap, max_batch, device, 0)
+        doc = {k: v for k, v in snapshot.items() if k != "podSets"}
+        h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
+        if not h:
+            raise NativeLibraryMissing("kueue_tas_host_create returned NULL")
+        err = self._lib.kueue_tas_host_last_error(h).decode()
+        if err:
+            self._lib.kueue_tas_host_destroy(h)
+            raise NativeLibraryMissing(err)
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.kueue_tas_host_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _err(self):
+        return self._lib.kueue_tas_host_last_error(self._h).decode()
+
+    def find_topology_assignments_for_flavor(self, podsets: list, simulate_empty: bool = False) -> list:
+        """FindTopologyAssignmentsForFlavor (:519-594) for one workload's
+        PodSets; returns [{"name", "assignment", "reason"}] in result order."""
+        out = ctypes.c_void_p()
+        rc = self._lib.kueue_tas_host_find(self._h, json.dumps(podsets).encode(), 1 if simulate_empty else 0,
+                                           ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError(f"kueue_tas_host_find failed ({rc}): {self._err()}")
+        return _take(self._lib, out)["results"]
+
+    def find_topology_assignments_for_workloads(self, workloads: list) -> list:
+        """Evaluate many workloads independently against this snapshot in one
+        device batch (Scheduler.nominate, scheduler.go:583-619)."""
+        out = ctypes.c_void_p()
+        rc = self._lib.kueue_tas_host_find_batch(self._h, json.dumps({"workloads": workloads}).encode(),
+                                                 ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError(f"kueue_tas_host_find_batch failed ({rc}): {self._err()}")
+        return _take(self._lib, out)["results"]
+
+    def compile(self, workloads: list):
+        rc = self._lib.kueue_tas_host_compile(self._h, json.dumps({"workloads": workloads}).encode())
+        if rc != 0:
+            raise RuntimeError(f"kueue_tas_host_compile failed ({rc}): {self._err()}")
+
+    def run_compiled(self) -> int:
+        h = ctypes.c_uint64()
+        rc = self._lib.kueue_tas_host_run_compiled(self._h, ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"kueue_tas_host_run_compiled failed ({rc}): {self._err()}")
+        return h.value

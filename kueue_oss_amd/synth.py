@@ -1,0 +1,366 @@
+"""Seeded synthetic TAS inputs.
+
+* ``bench_config(name)`` — the BASELINE.json configs:
+  C1 1,024 nodes / C2 16,384 / C3 131,072 / C4 65,536 JobSet / C5 1,048,576,
+  modelled on the reference's perf generator (test/performance/scheduler/
+  generator/topology_generator.go:64-157: zone/block/rack/hostname labels,
+  unpadded names, 96 cpu / 256Gi / 110 pods per node).
+* ``random_case(rng)`` — small randomized cases for differential tests
+  against the CPU oracle: taints (Equal/Exists/Lt/Gt tolerations), node
+  selectors, non-TAS pods (incl. over-subscription), TAS usage, leaders,
+  slices, multi-layer constraints, implied/unconstrained/preferred/required
+  requests, both TASProfileMixed settings.
+
+Documents follow the fixture schema of tools/extract_goldens.py.
+"""
+from __future__ import annotations
+
+import random
+
+HOST = "kubernetes.io/hostname"
+ZONE = "cloud.provider.com/topology-zone"
+BLOCK = "cloud.provider.com/topology-block"
+RACK = "cloud.provider.com/topology-rack"
+GI = 1 << 30
+
+
+def _node(name, labels, alloc, taints=(), ready=True):
+    return {"name": name, "labels": labels, "allocatable": alloc, "taints": list(taints),
+            "unschedulable": False, "conditions": [{"type": "Ready", "status": "True" if ready else "False"}]}
+
+
+def _ps(name, count, requests, required=None, preferred=None, unconstrained=None, slice_topo=None,
+        slice_size=None, constraints=None, group=None, tolerations=None, selector=None, implied=False):
+    tr = None
+    if any(v is not None for v in (required, preferred, unconstrained, slice_topo)) or constraints:
+        tr = {"required": required, "preferred": preferred, "unconstrained": unconstrained,
+              "podSetSliceRequiredTopology": slice_topo, "podSetSliceSize": slice_size,
+              "podsetSliceRequiredTopologyConstraints": constraints or []}
+    d = {"name": name, "topologyRequest": tr, "requests": requests, "count": count,
+         "tolerations": tolerations or [], "nodeSelector": selector, "podSetGroupName": group}
+    if tr is None and not implied:
+        d["implied"] = False
+    return d
+
+
+# ----------------------------------------------------------------------------
+# Benchmark configurations
+# ----------------------------------------------------------------------------
+def _tree_nodes(shape, labels_for, alloc_for, taints_for=None):
+    nodes = []
+    idx = 0
+    import itertools
+    for path in itertools.product(*[range(n) for n in shape]):
+        nodes.append(_node(f"node-{'-'.join(map(str, path))}", labels_for(path), alloc_for(idx, path),
+                           taints_for(idx, path) if taints_for else ()))
+        idx += 1
+    return nodes
+
+
+def config_c1(seed=42):
+    """C1: block/rack/hostname 4x16x16 = 1,024 nodes; one PodSet of 64 pods,
+    cpu 8 + memory 32Gi, required rack; TAS usage u~U{0..6} pods per node."""
+    rng = random.Random(seed)
+    levels = [BLOCK, RACK, HOST]
+    usage = []
+
+    def labels(p):
+        return {BLOCK: f"block-{p[0]}", RACK: f"rack-{p[0]}-{p[1]}", HOST: f"node-b{p[0]}-r{p[1]}-n{p[2]}"}
+
+    nodes = _tree_nodes((4, 16, 16), labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
+    for n in nodes:
+        u = rng.randint(0, 6)
+        if u:
+            usage.append({"values": [n["labels"][HOST]], "singlePodRequests": {"cpu": 8000, "memory": 32 * GI},
+                          "count": u})
+    snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": usage, "nodeLabels": {}, "featureGates": {}}
+    wl = [[_ps("main", 64, {"cpu": 8000, "memory": 32 * GI}, required=RACK)]]
+    return snap, wl
+
+
+def _mixed_workloads(rng, n, levels_req, lowest, highest):
+    wls = []
+    for i in range(n):
+        r = rng.random()
+        cpu = rng.choice([1, 2, 4, 8])
+        req = {"cpu": cpu * 1000, "memory": 4 * GI * cpu}
+        count = max(1, int(round(2 ** rng.uniform(0, 8))))
+        if r < 0.4:
+            lvl = levels_req[0] if rng.random() < 0.7 else levels_req[1]
+            wls.append([_ps(f"ps{i}", count, req, required=lvl)])
+        elif r < 0.8:
+            lvl = rng.choice(levels_req)
+            wls.append([_ps(f"ps{i}", count, req, preferred=lvl)])
+        elif r < 0.9:
+            wls.append([_ps(f"ps{i}", count, req, unconstrained=True)])
+        else:
+            # slice-only ("balanced" class of the perf generator): LFC at the highest level
+            ss = rng.choice([1, 2, 4])
+            count = max(ss, count - count % ss)
+            wls.append([_ps(f"ps{i}", count, req, slice_topo=lowest, slice_size=ss)])
+    return wls
+
+
+def config_c2(seed=1234, n_workloads=1000):
+    """C2: zone/block/rack/hostname 2x8x32x32 = 16,384 nodes; 1k workloads:
+    40% required (70% rack / 30% block), 40% preferred, 20% unconstrained or
+    slice-only; pod count log-uniform [1,256]; cpu in {1,2,4,8}, memory 4Gi/cpu."""
+    rng = random.Random(seed)
+    levels = [ZONE, BLOCK, RACK, HOST]
+
+    def labels(p):
+        return {ZONE: f"zone-{p[0]}", BLOCK: f"block-{p[0]}-{p[1]}", RACK: f"rack-{p[0]}-{p[1]}-{p[2]}",
+                HOST: f"node-z{p[0]}-b{p[1]}-r{p[2]}-n{p[3]}"}
+
+    nodes = _tree_nodes((2, 8, 32, 32), labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
+    usage = []
+    for n in nodes:
+        u = rng.randint(0, 8)
+        if u:
+            usage.append({"values": [n["labels"][HOST]], "singlePodRequests": {"cpu": 8000, "memory": 16 * GI},
+                          "count": u})
+    snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": usage, "nodeLabels": {}, "featureGates": {}}
+    return snap, _mixed_workloads(rng, n_workloads, [RACK, BLOCK], HOST, ZONE)
+
+
+def config_c3(seed=7, n_workloads=1000, shape=(4, 16, 64, 32)):
+    """C3: 4x16x64x32 = 131,072 nodes with cpu/memory/amd.com/gpu/ephemeral-storage,
+    non-TAS usage on every node, TAS GPU usage g~U{0..8}, 10% gpu-maint NoSchedule
+    + 2% NoExecute taints, gpu-type label; 50% required/preferred (BestFit),
+    50% unconstrained (LeastFreeCapacity); 30% with nodeSelector, 20% tolerating."""
+    rng = random.Random(seed)
+    levels = [ZONE, BLOCK, RACK, HOST]
+
+    def labels(p):
+        return {ZONE: f"zone-{p[0]}", BLOCK: f"block-{p[0]}-{p[1]}", RACK: f"rack-{p[0]}-{p[1]}-{p[2]}",
+                HOST: f"node-z{p[0]}-b{p[1]}-r{p[2]}-n{p[3]}",
+                "cloud.provider.com/gpu-type": "abcd"[(p[2] * 7 + p[3]) % 4]}
+
+    def taints(i, p):
+        r = rng.random()
+        if r < 0.10:
+            return [{"key": "gpu-maint", "value": "true", "effect": "NoSchedule"}]
+        if r < 0.12:
+            return [{"key": "gpu-maint", "value": "true", "effect": "NoExecute"}]
+        return []
+
+    alloc = {"cpu": 192000, "memory": 1536 * GI, "amd.com/gpu": 8, "ephemeral-storage": 3500 * GI, "pods": 110}
+    nodes = _tree_nodes(shape, labels, lambda i, p: dict(alloc), taints)
+    pods = []
+    usage = []
+    for n in nodes:
+        pods.append({"name": f"ds-{n['name']}", "namespace": "kube-system", "nodeName": n["name"],
+                     "phase": "Running", "requests": {"cpu": 2000, "memory": 4 * GI}})
+        g = rng.randint(0, 8)
+        if g:
+            usage.append({"values": [n["labels"][HOST]],
+                          "singlePodRequests": {"cpu": 24000, "memory": 192 * GI, "amd.com/gpu": 1,
+                                                "ephemeral-storage": 100 * GI}, "count": g})
+    snap = {"levels": levels, "nodes": nodes, "pods": pods, "tasUsage": usage, "nodeLabels": {}, "featureGates": {}}
+    wls = []
+    for i in range(n_workloads):
+        gpus = rng.randint(1, 8)
+        req = {"cpu": 24000 * gpus, "memory": 192 * GI * gpus, "amd.com/gpu": gpus, "ephemeral-storage": 100 * GI * gpus}
+        count = max(1, int(round(2 ** rng.uniform(0, 10))))
+        sel = {"cloud.provider.com/gpu-type": rng.choice("abcd")} if rng.random() < 0.3 else None
+        tol = [{"key": "gpu-maint", "operator": "Exists", "value": "", "effect": ""}] if rng.random() < 0.2 else []
+        if rng.random() < 0.5:
+            lvl = rng.choice([RACK, BLOCK])
+            if rng.random() < 0.5:
+                wls.append([_ps(f"ps{i}", count, req, required=lvl, selector=sel, tolerations=tol)])
+            else:
+                wls.append([_ps(f"ps{i}", count, req, preferred=lvl, selector=sel, tolerations=tol)])
+        else:
+            wls.append([_ps(f"ps{i}", count, req, unconstrained=True, selector=sel, tolerations=tol)])
+    return snap, wls
+
+
+def config_c4(seed=11, n_workloads=256, shape=(2, 16, 64, 32)):
+    """C4: 2x16x64x32 = 65,536 nodes; JobSet-like workloads: a PodSet group
+    {leader 1 pod cpu-only, workers 16-512 required block with 16-pod rack
+    slices} plus an independent second PodSet (assumedUsage chaining)."""
+    rng = random.Random(seed)
+    levels = [ZONE, BLOCK, RACK, HOST]
+
+    def labels(p):
+        return {ZONE: f"zone-{p[0]}", BLOCK: f"block-{p[0]}-{p[1]}", RACK: f"rack-{p[0]}-{p[1]}-{p[2]}",
+                HOST: f"node-z{p[0]}-b{p[1]}-r{p[2]}-n{p[3]}"}
+
+    nodes = _tree_nodes(shape, labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
+    usage = []
+    for n in nodes:
+        u = rng.randint(0, 10)
+        if u:
+            usage.append({"values": [n["labels"][HOST]], "singlePodRequests": {"cpu": 8000, "memory": 16 * GI},
+                          "count": u})
+    snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": usage, "nodeLabels": {}, "featureGates": {}}
+    wls = []
+    for i in range(n_workloads):
+        workers = 16 * rng.randint(1, 32)
+        wls.append([
+            _ps("leader", 1, {"cpu": 1000}, required=BLOCK, group="g", slice_topo=RACK, slice_size=1),
+            _ps("workers", workers, {"cpu": 4000, "memory": 8 * GI}, required=BLOCK, group="g",
+                slice_topo=RACK, slice_size=16),
+            _ps("aux", rng.randint(1, 64), {"cpu": 2000, "memory": 4 * GI}, preferred=RACK),
+        ])
+    return snap, wls
+
+
+def config_c5(seed=5, n_workloads=100000, shape=(8, 32, 128, 32)):
+    """C5: 8x32x128x32 = 1,048,576 nodes; 100k workloads with the C2 mix."""
+    rng = random.Random(seed)
+    levels = [ZONE, BLOCK, RACK, HOST]
+
+    def labels(p):
+        return {ZONE: f"zone-{p[0]}", BLOCK: f"block-{p[0]}-{p[1]}", RACK: f"rack-{p[0]}-{p[1]}-{p[2]}",
+                HOST: f"node-z{p[0]}-b{p[1]}-r{p[2]}-n{p[3]}"}
+
+    nodes = _tree_nodes(shape, labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
+    snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": [], "nodeLabels": {}, "featureGates": {}}
+    return snap, _mixed_workloads(rng, n_workloads, [RACK, BLOCK], HOST, ZONE)
+
+
+CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C4": config_c4, "C5": config_c5}
+
+
+# ----------------------------------------------------------------------------
+# Randomized differential cases
+# ----------------------------------------------------------------------------
+_TAINTS = [
+    {"key": "gpu", "value": "present", "effect": "NoSchedule"},
+    {"key": "maint", "value": "", "effect": "NoExecute"},
+    {"key": "soft", "value": "x", "effect": "PreferNoSchedule"},
+    {"key": "level", "value": "5", "effect": "NoSchedule"},
+    {"key": "level", "value": "12", "effect": "NoExecute"},
+]
+_TOLS = [
+    {"key": "gpu", "operator": "Equal", "value": "present", "effect": ""},
+    {"key": "gpu", "operator": "Exists", "value": "", "effect": "NoSchedule"},
+    {"key": "maint", "operator": "Exists", "value": "", "effect": ""},
+    {"key": "", "operator": "Exists", "value": "", "effect": "NoExecute"},
+    {"key": "level", "operator": "Gt", "value": "4", "effect": ""},
+    {"key": "level", "operator": "Lt", "value": "10", "effect": ""},
+    {"key": "level", "operator": "Lt", "value": "007", "effect": ""},
+]
+
+
+def random_case(rng: random.Random, max_nodes: int = 60, profile_mixed=None) -> dict:
+    nlev = rng.choice([1, 2, 3, 3, 4])
+    hostname = rng.random() < 0.75
+    keys = ["dc", "block", "rack", "sub"]
+    levels = keys[: nlev - 1 if hostname else nlev] + ([HOST] if hostname else [])
+    if not levels:
+        levels = [HOST]
+    nn = rng.randint(0, max_nodes)
+    fan = [rng.randint(1, 4) for _ in levels]
+    res_names = ["cpu", "memory", "pods", "example.com/gpu"]
+    nodes = []
+    for i in range(nn):
+        labels = {}
+        for k in levels:
+            if k == HOST:
+                labels[k] = f"x{i}" if rng.random() < 0.97 else f"x{rng.randint(0, nn)}"
+            else:
+                labels[k] = f"{k[0]}{rng.randint(1, fan[levels.index(k)] * 3)}"
+        if rng.random() < 0.05 and levels[0] != HOST:
+            labels.pop(levels[0])  # missing level label: filtered by NodeMatchesFlavor
+        if rng.random() < 0.5:
+            labels["zone"] = rng.choice(["a", "b"])
+        if rng.random() < 0.3:
+            labels["gpu-type"] = rng.choice(["t1", "t2", "t3"])
+        alloc = {}
+        for r in res_names:
+            if rng.random() < 0.85:
+                if r == "cpu":
+                    alloc[r] = rng.choice([0, 500, 1000, 2000, 4000, 8000, 16000])
+                elif r == "memory":
+                    alloc[r] = rng.choice([0, GI, 2 * GI, 8 * GI, 64 * GI])
+                elif r == "pods":
+                    alloc[r] = rng.choice([0, 1, 3, 10, 110])
+                else:
+                    alloc[r] = rng.choice([0, 1, 2, 4, 8])
+        taints = [dict(t) for t in rng.sample(_TAINTS, rng.randint(0, 2))] if rng.random() < 0.3 else []
+        n = _node(f"node{i}", labels, alloc, taints, ready=rng.random() < 0.95)
+        n["unschedulable"] = rng.random() < 0.03
+        nodes.append(n)
+    pods = []
+    for j in range(rng.randint(0, nn // 2 + 1)):
+        if not nodes:
+            break
+        target = rng.choice(nodes)["name"] if rng.random() < 0.9 else ""
+        pods.append({"name": f"p{j}", "namespace": "ns", "nodeName": target,
+                     "phase": rng.choice(["Running", "Running", "Pending", "Succeeded", "Failed"]),
+                     "requests": {r: rng.choice([0, 250, 1000, 3000]) if r == "cpu" else rng.choice([0, GI // 2, GI])
+                                  for r in rng.sample(["cpu", "memory"], rng.randint(0, 2))}})
+    usage = []
+    for n in nodes:
+        if rng.random() < 0.3:
+            vals = [n["labels"].get(HOST, "")] if hostname else [n["labels"].get(k, "") for k in levels]
+            usage.append({"values": vals, "singlePodRequests": {"cpu": rng.choice([0, 500, 1000]),
+                                                                 "memory": rng.choice([0, GI // 4])},
+                          "count": rng.randint(1, 4)})
+    gates = {}
+    if profile_mixed is not None:
+        gates["TASProfileMixed"] = profile_mixed
+    elif rng.random() < 0.3:
+        gates["TASProfileMixed"] = False
+    if rng.random() < 0.3:
+        gates["TASMultiLayerTopology"] = True
+    nodeLabels = {"zone": "a"} if rng.random() < 0.1 else {}
+    flavor_tols = [dict(rng.choice(_TOLS))] if rng.random() < 0.1 else []
+    podsets = []
+    nps = rng.choice([1, 1, 1, 2, 2, 3])
+    group_mode = nps >= 2 and rng.random() < 0.5
+    for k in range(nps):
+        req = {}
+        for r in ["cpu", "memory", "example.com/gpu", "example.com/fpga"]:
+            if rng.random() < (0.8 if r == "cpu" else 0.25):
+                if r == "cpu":
+                    req[r] = rng.choice([0, 100, 500, 1000, 2000])
+                elif r == "memory":
+                    req[r] = rng.choice([0, GI // 2, GI])
+                else:
+                    req[r] = rng.choice([0, 1, 2])
+        if rng.random() < 0.05:
+            req["pods"] = rng.choice([0, 1])
+        kind = rng.random()
+        lvl = rng.choice(levels)
+        low_idx = rng.randrange(levels.index(lvl), len(levels))
+        slice_lvl = levels[low_idx]
+        ss = rng.choice([1, 1, 2, 3, 4])
+        count = rng.choice([0, 1, 1, 2, 3, 4, 5, 8, 12, 20, 40])
+        if ss > 1 and rng.random() < 0.8:
+            count = ss * max(1, count // ss)
+        kw = {}
+        if kind < 0.3:
+            kw["required"] = lvl
+        elif kind < 0.55:
+            kw["preferred"] = lvl
+        elif kind < 0.7:
+            kw["unconstrained"] = True
+        elif kind < 0.8:
+            pass  # implied (topologyRequest nil)
+        else:
+            kw["slice_topo"] = slice_lvl
+            kw["slice_size"] = ss
+        if kw and "slice_topo" not in kw and rng.random() < 0.35:
+            kw["slice_topo"] = slice_lvl
+            kw["slice_size"] = ss if rng.random() < 0.95 else None
+        if kw and rng.random() < 0.15 and low_idx + 1 < len(levels):
+            inner = levels[rng.randrange(low_idx + 1, len(levels))]
+            inner_sz = rng.choice([d for d in range(1, ss + 1) if ss % d == 0])
+            kw["constraints"] = [{"topology": slice_lvl, "size": ss}, {"topology": inner, "size": inner_sz}]
+            kw.pop("slice_topo", None)
+            kw.pop("slice_size", None)
+        tol = [dict(t) for t in rng.sample(_TOLS, rng.randint(0, 2))] if rng.random() < 0.4 else []
+        sel = None
+        if rng.random() < 0.25:
+            sel = {rng.choice(["zone", "gpu-type", "missing"]): rng.choice(["a", "b", "t1", "t2", "zz"])}
+        elif rng.random() < 0.05:
+            sel = {}
+        group = "grp" if group_mode and k < 2 else None
+        name = f"ps{k}"
+        podsets.append(_ps(name, count, req, tolerations=tol, selector=sel, group=group,
+                           implied=not kw, **kw))
+    return {"name": "random", "levels": levels, "nodes": nodes, "pods": pods, "tasUsage": usage,
+            "nodeLabels": nodeLabels, "flavorTolerations": flavor_tols, "featureGates": gates, "podSets": podsets}

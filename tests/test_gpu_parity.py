@@ -1,0 +1,74 @@
+"""GPU parity: the HIP path (libkueue_tas.so) against the golden fixtures and,
+on seeded random inputs, against the CPU oracle — bit-exact (same domains,
+same per-leaf pod counts, same failure strings)."""
+import random
+
+import pytest
+
+import oracle_lib
+from golden_util import diff_against_golden, load_cases
+from kueue_oss_amd import TASFlavorSnapshot, synth
+
+pytestmark = pytest.mark.gpu
+CASES = load_cases()
+
+
+@pytest.mark.parametrize("list_cap", [0, 64])
+def test_goldens_on_gpu(list_cap):
+    bad = []
+    for case in CASES:
+        snap = TASFlavorSnapshot(case, list_cap=list_cap)
+        res = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        p = diff_against_golden(case, res)
+        if p:
+            bad.append((case["line"], case["name"], p))
+    assert bad == []
+
+
+def _random_parity(seed, n, list_cap, max_nodes=60, profile_mixed=None):
+    rng = random.Random(seed)
+    bad = []
+    for i in range(n):
+        case = synth.random_case(rng, max_nodes=max_nodes, profile_mixed=profile_mixed)
+        want = oracle_lib.run_case(case)["results"]
+        snap = TASFlavorSnapshot(case, list_cap=list_cap)
+        got = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        if got != want:
+            bad.append((i, case, got, want))
+            if len(bad) >= 3:
+                break
+    return bad
+
+
+@pytest.mark.parametrize("seed,list_cap", [(1, 0), (2, 64), (3, 0)])
+def test_random_small_topologies(seed, list_cap):
+    bad = _random_parity(seed, 400, list_cap)
+    assert not bad, (bad[0][2], bad[0][3])
+
+
+def test_random_larger_topologies_small_lds():
+    # list_cap 64 forces the lazy / global-sort / histogram paths on lists > 64
+    bad = _random_parity(7, 60, 64, max_nodes=600)
+    assert not bad, (bad[0][2], bad[0][3])
+
+
+def test_batched_workloads_match_oracle_c2_sample():
+    snap_doc, wls = synth.config_c2(n_workloads=120)
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    mism = [i for i in range(len(wls)) if got[i] != want[i]]
+    assert mism == [], (mism[:5], got[mism[0]] if mism else None, want[mism[0]] if mism else None)
+
+
+def test_batched_workloads_match_oracle_c4_jobset():
+    snap_doc, wls = synth.config_c4(n_workloads=40, shape=(2, 4, 16, 32))
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    mism = [i for i in range(len(wls)) if got[i] != want[i]]
+    assert mism == [], (mism[:5], got[mism[0]] if mism else None, want[mism[0]] if mism else None)

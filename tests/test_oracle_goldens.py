@@ -1,0 +1,23 @@
+"""The CPU oracle reproduces every in-scope golden case transcribed from the
+reference's TestFindTopologyAssignments (pkg/cache/scheduler/tas_cache_test.go)."""
+import pytest
+
+import oracle_lib
+from golden_util import diff_against_golden, load_cases
+
+CASES = load_cases()
+
+
+def test_fixture_inventory():
+    from golden_util import load_cases as lc
+    allc = lc(scope_in=False)
+    assert len(allc) == 104  # 104 named cases in the reference table (:383-6266)
+    assert len(CASES) == 82
+    out = [c for c in allc if c["scope"] != "in"]
+    assert all(c["scope"].startswith("out:") for c in out)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"L{c['line']}" for c in CASES])
+def test_oracle_matches_golden(case):
+    res = oracle_lib.run_case(case)["results"]
+    assert diff_against_golden(case, res) == []
