@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""TAS placements/sec on MI355X (BASELINE.json metric) — C3: 131,072 nodes.
+
+A step = one nominate batch (pkg/scheduler/scheduler.go:583-619): every rank
+evaluates its shard of pending workloads (FindTopologyAssignmentsForWorkload,
+pkg/cache/scheduler/clusterqueue_snapshot.go:191) against its replica of the
+snapshot resident in HBM, through the C-ABI host layer (request H2D, three
+kernel stages, result D2H and decode), then the per-workload result records
+are all-gathered over RCCL (N > 1).  Weak scaling: per-rank batch fixed.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Rank 0 prints ONE JSON line.  See DESIGN.md §Measurement for the roofline
+bytes and the CPU baseline (the C++ oracle, "port", timed on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--batch", type=int, default=1024, help="pending workloads per rank per step")
+    ap.add_argument("--cpu-sample", type=int, default=24, help="workloads timed on the CPU oracle (rank 0)")
+    ap.add_argument("--parity-sample", type=int, default=24)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def fill_algorithmic_bytes(N, n_evals, n_leader, R_used, label_cols, evals_per_block=8):
+    """Minimum HBM bytes of one fill launch: the SoA snapshot columns the
+    batch requests (free + used int64, presence words, taint profile, label
+    ids) once per launch, plus the per-eval leaf counters written
+    (state + sliceState int32; stateWithLeader, sliceStateWithLeader,
+    leaderState for leader evals)."""
+    snap = N * (16 * R_used + 8 + 4 + 4 * label_cols)
+    writes = N * (8 * n_evals + 12 * n_leader)
+    return snap + writes
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = dist_mod
+
+    from kueue_oss_amd import TASFlavorSnapshot, synth
+    from kueue_oss_amd.sharding import shard_workloads
+
+    gen = synth.CONFIGS[a.config]
+    t0 = time.time()
+    snap_doc, all_wls = gen(n_workloads=a.batch * world) if a.config != "C1" else gen()
+    mine = shard_workloads(all_wls, world, rank)
+    gen_s = time.time() - t0
+
+    t0 = time.time()
+    snap = TASFlavorSnapshot(snap_doc, device=local_rank if world > 1 else 0)
+    snap.compile(mine)
+    load_s = time.time() - t0
+    N = len(snap_doc["nodes"])
+
+    # ---- parity (untimed): product vs CPU oracle on a sample; CPU baseline timing ----
+    parity = None
+    cpu = None
+    if rank == 0 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+
+        sample = mine[: max(a.parity_sample, a.cpu_sample)]
+        got = snap.find_topology_assignments_for_workloads(sample)
+        want, secs = oracle_lib.eval_workloads(snap_doc, sample[: a.cpu_sample])
+        parity = all(got[i] == want[i] for i in range(len(want)))
+        cpu = {"value": round(len(want) / secs, 3), "unit": "placements/s", "cores": 1, "kind": "port",
+               "sample": f"{len(want)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
+                         f"(C++ restatement of the Go path; Go toolchain absent)",
+               "seconds": round(secs, 3)}
+        if not parity:
+            bad = [i for i in range(len(want)) if got[i] != want[i]]
+            print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
+
+    import torch
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize() if torch.cuda.is_available() else None
+
+    rec = None
+    gathered = None
+
+    def step():
+        nonlocal rec, gathered
+        h = snap.run_compiled()
+        if dist is not None:
+            r = torch.tensor(snap.last_records(len(mine)), dtype=torch.int32, device=f"cuda:{local_rank}")
+            out = [torch.empty_like(r) for _ in range(world)]
+            dist.all_gather(out, r)  # RCCL all-gather of assignment records over xGMI
+            gathered = out
+        return h
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    fill_ms = rollup_ms = select_ms = dev_ms = 0.0
+    counts = None
+    for _ in range(a.steps):
+        step()
+        ms, counts = snap.last_timings()
+        fill_ms += ms[0]
+        rollup_ms += ms[1]
+        select_ms += ms[2]
+        dev_ms += ms[3]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    placements = len(mine) * world * a.steps
+    value = placements / dt
+
+    batches, evals, leader_evals = counts
+    per_launch_fill_ms = fill_ms / (a.steps * batches)
+    R_used = len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
+    label_cols = 1 if any(p.get("nodeSelector") for w in mine for p in w) else 0
+    fill_bytes = fill_algorithmic_bytes(N, evals / batches, leader_evals / batches, R_used, label_cols)
+    achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
+    stages = {"fill_ms": round(fill_ms / a.steps, 3), "rollup_ms": round(rollup_ms / a.steps, 3),
+              "select_ms": round(select_ms / a.steps, 3), "device_ms": round(dev_ms / a.steps, 3)}
+    if rank == 0:
+        line = {
+            "metric": "TAS placements/sec at 128k nodes (1/2/4/8 GPU); % HBM roofline",
+            "value": round(value, 1),
+            "unit": "placements/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (seeded generator modelled on test/performance/scheduler/generator)",
+            "config": {"workload": f"{a.config}: {N} nodes, {a.batch} pending workloads per GPU per step "
+                                   "(50% BestFit required/preferred, 50% LeastFreeCapacity unconstrained; "
+                                   "taints + nodeSelector)",
+                       "nodes": N, "batch_per_gpu": a.batch, "parallelism": f"dp{world} (replicated snapshot)"},
+            "roofline": {"kernel": "fill_leaves_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_launch": int(fill_bytes),
+                         "avg_launch_ms": round(per_launch_fill_ms, 4)},
+            "stages": stages,
+            "cpu_baseline": cpu,
+            "parity_sample_ok": parity,
+            "setup_s": {"generate": round(gen_s, 2), "snapshot_load_and_compile": round(load_s, 2)},
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    snap.close()
+
+
+if __name__ == "__main__":
+    main()

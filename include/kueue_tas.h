@@ -209,6 +209,14 @@ int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, cha
  * (kueue_tas_host_run_compiled) without JSON on the timed path. */
 int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json);
 int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
+/* Device stage times of the last run (summed over its batches, ms):
+ * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
+ * counts[1] = evaluations, counts[2] = evaluations with a leader. */
+int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
+/* Per-workload compact results of the last run_compiled into buf (int32):
+ * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
+ * 4 int32 per workload (used for the cross-rank all-gather). */
+int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n_workloads);
 
 void kueue_tas_free(char* p);
 

@@ -148,7 +148,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->device = cfg->device;
     if (cfg->list_cap > 0) {
       int lc = 64;
-      while (lc < cfg->list_cap && lc < 2048) lc <<= 1;
+      while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
       c->list_cap = lc;
     }
     if (cfg->max_batch > 0) c->max_batch = cfg->max_batch;

@@ -658,7 +658,7 @@ class FlavorSnapshot {
     }
     bool multilayer = gates.multiLayer && !ssal.empty();
     if (gates.balanced && !required && !unconstrained) {
-      g.early_reason = "unsupported: TASBalancedPlacement (alpha) is not implemented on this path";
+      g.early_reason = "unsupported: TASBalancedPlacement";
       return;
     }
     q.flags = (required ? KUEUE_TAS_F_REQUIRED : 0u) | (unconstrained ? KUEUE_TAS_F_UNCONSTRAINED : 0u) |
@@ -715,7 +715,7 @@ class FlavorSnapshot {
         }
       }
       // nodeSelector: labels.ValidatedSelectorFromSet (only with hostname leaves, :879-887)
-      if (w.nodeSelector && !w.nodeSelector->empty()) {
+      if (w.nodeSelector && !w.nodeSelector->empty() && !labelKeys.empty()) {
         if (w.nodeSelector->size() > KUEUE_TAS_MAX_SELECTORS) {
           g.early_reason = "unsupported: more than 8 nodeSelector terms";
           return;
@@ -852,6 +852,8 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
 struct Evaluator {
   FlavorSnapshot* snap;
   int32_t entry_cap = 4096;
+  float ms[4] = {0, 0, 0, 0};
+  int64_t counts[3] = {0, 0, 0};
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
@@ -943,6 +945,12 @@ struct Evaluator {
         if (!retry || cap >= (1 << 22)) break;
         cap *= 4;
       }
+      float t4[4];
+      kueue_tas_last_timings(snap->ctx, t4);
+      for (int k = 0; k < 4; k++) ms[k] += t4[k];
+      counts[0]++;
+      counts[1] += int64_t(n);
+      for (auto& q : reqs) counts[2] += (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
       (void)P;
       for (size_t i = 0; i < n; i++) {
         size_t w = batch[i].first;
@@ -1031,6 +1039,9 @@ struct kueue_tas_host {
   std::unique_ptr<FlavorSnapshot> snap;
   std::string err;
   std::vector<Workload> compiled;
+  std::vector<std::vector<PodSetResult>> last;
+  float ms[4] = {0, 0, 0, 0};
+  int64_t counts[3] = {0, 0, 0};
 };
 
 extern "C" {
@@ -1143,12 +1154,14 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
 int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
   if (!h || !h->snap) return KUEUE_TAS_EINVAL;
   Evaluator ev{h->snap.get()};
-  std::vector<std::vector<PodSetResult>> results;
+  std::vector<std::vector<PodSetResult>>& results = h->last;
   int rc = ev.run(h->compiled, false, &results);
   if (rc) {
     h->err = h->snap->err;
     return rc;
   }
+  memcpy(h->ms, ev.ms, sizeof h->ms);
+  memcpy(h->counts, ev.counts, sizeof h->counts);
   if (result_hash) {
     uint64_t x = 1469598103934665603ull;
     auto mix = [&](uint64_t v) {
@@ -1168,6 +1181,35 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
         mix(std::hash<std::string>()(r.reason));
       }
     *result_hash = x;
+  }
+  return 0;
+}
+
+int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3) {
+  if (!h) return KUEUE_TAS_EINVAL;
+  if (ms4) memcpy(ms4, h->ms, sizeof h->ms);
+  if (counts3) memcpy(counts3, h->counts, sizeof h->counts);
+  return 0;
+}
+
+int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n) {
+  if (!h || !buf) return KUEUE_TAS_EINVAL;
+  for (size_t i = 0; i < n; i++) {
+    int32_t* r = buf + 4 * i;
+    r[0] = r[1] = r[2] = r[3] = 0;
+    if (i >= h->last.size()) continue;
+    bool fail = false;
+    int32_t ent = 0;
+    for (auto& p : h->last[i]) {
+      if (!p.reason.empty()) fail = true;
+      ent += int32_t(p.domains.size());
+      if (r[2] == 0 && !p.domains.empty()) {
+        r[2] = p.domains[0].leaf;
+        r[3] = p.domains[0].count;
+      }
+    }
+    r[0] = fail ? 1 : 0;
+    r[1] = ent;
   }
   return 0;
 }

@@ -49,7 +49,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch",
     "kueue_tas_last_timings", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
-    "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_free",
+    "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
+    "kueue_tas_host_last_records", "kueue_tas_free",
 ]
 
 
@@ -80,6 +81,8 @@ def load_library():
     lib.kueue_tas_host_compile.restype = c.c_int
     lib.kueue_tas_host_run_compiled.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     lib.kueue_tas_host_run_compiled.restype = c.c_int
+    lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
+    lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_free.argtypes = [c.c_void_p]
     _LIB = lib
     return lib
@@ -147,6 +150,19 @@ class TASFlavorSnapshot:
         rc = self._lib.kueue_tas_host_compile(self._h, json.dumps({"workloads": workloads}).encode())
         if rc != 0:
             raise RuntimeError(f"kueue_tas_host_compile failed ({rc}): {self._err()}")
+
+    def last_timings(self):
+        """(fill_ms, rollup_ms, select_ms, total_ms), (batches, evals, leader_evals) of the last run."""
+        ms = (ctypes.c_float * 4)()
+        cnt = (ctypes.c_int64 * 3)()
+        self._lib.kueue_tas_host_last_timings(self._h, ms, cnt)
+        return tuple(ms), tuple(cnt)
+
+    def last_records(self, n: int):
+        """[n][4] int32 compact per-workload results of the last run_compiled."""
+        buf = (ctypes.c_int32 * (4 * n))()
+        self._lib.kueue_tas_host_last_records(self._h, buf, n)
+        return list(buf)
 
     def run_compiled(self) -> int:
         h = ctypes.c_uint64()
