@@ -54,18 +54,28 @@ EXPORTED_SYMBOLS = [
 ]
 
 
-def load_library():
-    """Load the in-tree libkueue_tas.so (raises NativeLibraryMissing)."""
+def load_library(path: str | None = None):
+    """Load the in-tree libkueue_tas.so (raises NativeLibraryMissing).
+
+    ``path`` loads another build of the same C-ABI instead (tests use the
+    CPU-emulated build of tests/emu to check kernel logic without a GPU)."""
     global _LIB
-    if _LIB is not None:
+    if path is None and _LIB is not None:
         return _LIB
-    path = library_path()
-    if not os.path.exists(path):
-        raise NativeLibraryMissing(f"{path} not built (run __graft_entry__.build())")
+    p = path or library_path()
+    if not os.path.exists(p):
+        raise NativeLibraryMissing(f"{p} not built (run __graft_entry__.build())")
     try:
-        lib = ctypes.CDLL(path)
+        lib = ctypes.CDLL(p)
     except OSError as e:  # pragma: no cover - environment specific
         raise NativeLibraryMissing(str(e)) from e
+    _bind(lib)
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def _bind(lib):
     c = ctypes
     lib.kueue_tas_abi_version.restype = c.c_int
     lib.kueue_tas_host_create.argtypes = [c.c_char_p, c.POINTER(KueueTasConfig)]
@@ -84,8 +94,6 @@ def load_library():
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_free.argtypes = [c.c_void_p]
-    _LIB = lib
-    return lib
 
 
 def _take(lib, p) -> dict:
@@ -99,8 +107,8 @@ class TASFlavorSnapshot:
     tas_flavor_snapshot.go:109).  ``snapshot`` follows the fixture schema of
     tools/extract_goldens.py (podSets ignored)."""
 
-    def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0):
-        self._lib = load_library()
+    def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None):
+        self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, 0)
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))

@@ -1,0 +1,28 @@
+#!/bin/bash
+# TEST INFRASTRUCTURE: build libkueue_tas_emu.so — the unmodified product
+# sources (kernels + device layer + host layer) compiled with g++ against the
+# CPU SIMT emulator in tests/emu/hip/hip_runtime.h.  Output: tests/emu/_build/.
+set -euo pipefail
+HERE="$(cd "$(dirname "$0")" && pwd)"
+ROOT="$(cd "$HERE/../.." && pwd)"
+OUT="$HERE/_build"
+mkdir -p "$OUT/src"
+CSRC="$ROOT/kueue_oss_amd/csrc"
+# dynamic LDS: `extern __shared__ T name[];` has no static-local equivalent
+# - dynamic LDS: `extern __shared__ T name[];` has no static-local equivalent
+# - lockstep: on hardware the 64 lanes of a wave execute the (wave-uniform)
+#   counter stores of phase 2 in lockstep; fibers do not, so every store of a
+#   domain counter becomes a wave-synchronization point here.
+sed -e 's/extern __shared__ Key lds_all\[\];/Key* lds_all = static_cast<Key*>(emu::dynamic_lds());/' \
+    -e 's/^    ctr\[int64_t(f) \* SD + g\] = v;/    emu::wave_barrier(); ctr[int64_t(f) * SD + g] = v; emu::wave_barrier();/' \
+  "$CSRC/tas_kernels.hip" > "$OUT/src/tas_kernels.hip"
+grep -q 'emu::wave_barrier(); ctr' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
+cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$OUT/src/"
+sed 's#"../../include/kueue_tas.h"#"kueue_tas.h"#' "$CSRC/tas_internal.h" > "$OUT/src/tas_internal.h"
+cp "$ROOT/include/kueue_tas.h" "$OUT/src/"
+cp "$CSRC/tas_device.hip" "$OUT/src/tas_device.cpp"
+sed 's#"../../include/kueue_tas.h"#"kueue_tas.h"#' "$CSRC/tas_host.cpp" > "$OUT/src/tas_host.cpp"
+CXXFLAGS="${CXXFLAGS:--O1 -g}"
+g++ -std=c++17 $CXXFLAGS -fPIC -shared -I"$HERE" -I"$OUT/src" \
+  "$OUT/src/tas_device.cpp" "$OUT/src/tas_host.cpp" "$HERE/hip_emu.cpp" -o "$OUT/libkueue_tas_emu.so"
+echo "$OUT/libkueue_tas_emu.so"

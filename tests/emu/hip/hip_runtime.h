@@ -1,0 +1,133 @@
+// TEST INFRASTRUCTURE: a CPU SIMT emulator standing in for <hip/hip_runtime.h>
+// so that the UNMODIFIED kernel sources (kueue_oss_amd/csrc/tas_kernels.hip,
+// tas_device.hip) can be compiled with g++ and parity-tested on a machine
+// without a GPU (tests/emu/build_emu.sh).  Never linked into the product.
+//
+// Model: every GPU thread is a fiber (ucontext); a block's fibers run on one
+// OS thread, round-robin; blocks run sequentially.  Wave-level primitives
+// (__shfl*, __ballot, wave barriers, fences) synchronize the 64 lanes of a
+// wave; __syncthreads synchronizes the block.  __shared__ locals become
+// function statics (one block runs at a time).
+#pragma once
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+
+struct dim3 {
+  unsigned x, y, z;
+  dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+
+namespace emu {
+struct Ctx {
+  dim3 tid, bid, bdim, gdim;
+};
+Ctx* cur();
+void wave_barrier();
+void block_barrier();
+uint64_t wave_exchange(uint64_t v, int src);       // value of lane `src`
+uint64_t wave_ballot(bool p);
+void* dynamic_lds();
+void launch(dim3 grid, dim3 block, size_t shmem, const std::function<void()>& fn);
+}  // namespace emu
+
+#define threadIdx (emu::cur()->tid)
+#define blockIdx (emu::cur()->bid)
+#define blockDim (emu::cur()->bdim)
+#define gridDim (emu::cur()->gdim)
+
+inline void __syncthreads() { emu::block_barrier(); }
+#define __builtin_amdgcn_fence(order, scope) emu::wave_barrier()
+#define __builtin_amdgcn_wave_barrier() emu::wave_barrier()
+
+inline int __lane_of_cur() { return int(emu::cur()->tid.x & 63u); }
+template <typename T>
+inline T __shfl(T v, int src, int width = 64) {
+  (void)width;
+  uint64_t bits = 0;
+  memcpy(&bits, &v, sizeof(T));
+  uint64_t r = emu::wave_exchange(bits, src & 63);
+  T out;
+  memcpy(&out, &r, sizeof(T));
+  return out;
+}
+template <typename T>
+inline T __shfl_xor(T v, int mask, int width = 64) {
+  (void)width;
+  return __shfl(v, __lane_of_cur() ^ mask, 64);
+}
+inline unsigned long long __ballot(int p) { return emu::wave_ballot(p != 0); }
+inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+inline int __ffsll(long long x) { return __builtin_ffsll(x); }
+inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return uint64_t(((unsigned __int128)a * b) >> 64); }
+// fibers of one block share one OS thread: plain read-modify-write is atomic
+inline int atomicAdd(int* p, int v) { int o = *p; *p = o + v; return o; }
+inline unsigned atomicAdd(unsigned* p, unsigned v) { unsigned o = *p; *p = o + v; return o; }
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+  unsigned long long o = *p;
+  *p = o + v;
+  return o;
+}
+inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v; return o; }
+using std::max;
+using std::min;
+
+// ---- runtime API subset ----
+typedef int hipError_t;
+constexpr hipError_t hipSuccess = 0;
+typedef struct emu_stream* hipStream_t;
+typedef struct emu_event* hipEvent_t;
+enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
+constexpr unsigned hipStreamNonBlocking = 1;
+constexpr unsigned hipHostMallocDefault = 0;
+inline const char* hipGetErrorString(hipError_t) { return "emu error"; }
+inline hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
+inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
+template <typename T>
+inline hipError_t hipMalloc(T** p, size_t bytes) {
+  *p = static_cast<T*>(calloc(1, bytes));
+  return *p ? hipSuccess : 2;
+}
+inline hipError_t hipFree(void* p) { free(p); return hipSuccess; }
+template <typename T>
+inline hipError_t hipHostMalloc(T** p, size_t bytes, unsigned) {
+  *p = static_cast<T*>(calloc(1, bytes));
+  return *p ? hipSuccess : 2;
+}
+inline hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+  if (n) memmove(d, s, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
+  memset(d, v, n);
+  return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) {
+  *s = reinterpret_cast<hipStream_t>(new char[1]);
+  return hipSuccess;
+}
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamDestroy(hipStream_t s) { delete[] reinterpret_cast<char*>(s); return hipSuccess; }
+inline hipError_t hipEventCreate(hipEvent_t* e) {
+  *e = reinterpret_cast<hipEvent_t>(new char[1]);
+  return hipSuccess;
+}
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char*>(e); return hipSuccess; }
+
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
+  emu::launch(dim3(grid), dim3(block), size_t(shmem), [&]() { kernel(__VA_ARGS__); })
