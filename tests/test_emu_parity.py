@@ -1,0 +1,59 @@
+"""Kernel logic on CPU: the unmodified HIP sources compiled against the
+test-only SIMT emulator (tests/emu) must match the golden fixtures and the
+oracle.  This is not the product path (that is tests/test_gpu_parity.py on an
+MI355X); it checks the wave-level algorithm where no GPU is available."""
+import os
+import random
+import subprocess
+
+import pytest
+
+import oracle_lib
+from golden_util import diff_against_golden, load_cases
+from kueue_oss_amd import TASFlavorSnapshot, native, synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EMU_SO = os.path.join(HERE, "emu", "_build", "libkueue_tas_emu.so")
+
+
+@pytest.fixture(scope="module")
+def emu_lib():
+    srcs = [os.path.join(HERE, "..", "kueue_oss_amd", "csrc", f) for f in
+            ("tas_kernels.hip", "tas_device.hip", "tas_host.cpp", "tas_internal.h", "json_reader.h")]
+    srcs += [os.path.join(HERE, "emu", f) for f in ("hip_emu.cpp", "build_emu.sh", "hip/hip_runtime.h")]
+    if not os.path.exists(EMU_SO) or os.path.getmtime(EMU_SO) < max(os.path.getmtime(s) for s in srcs):
+        subprocess.run([os.path.join(HERE, "emu", "build_emu.sh")], check=True, capture_output=True)
+    return native.load_library(EMU_SO)
+
+
+@pytest.mark.parametrize("list_cap", [0, 64])
+def test_emulated_kernels_match_goldens(emu_lib, list_cap):
+    bad = []
+    for case in load_cases():
+        snap = TASFlavorSnapshot(case, list_cap=list_cap, lib=emu_lib)
+        res = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        if diff_against_golden(case, res):
+            bad.append(case["line"])
+    assert bad == []
+
+
+@pytest.mark.parametrize("seed,list_cap,max_nodes,n", [(11, 0, 60, 250), (12, 64, 60, 250), (13, 64, 400, 60)])
+def test_emulated_kernels_match_oracle_random(emu_lib, seed, list_cap, max_nodes, n):
+    rng = random.Random(seed)
+    for i in range(n):
+        case = synth.random_case(rng, max_nodes=max_nodes)
+        want = oracle_lib.run_case(case)["results"]
+        snap = TASFlavorSnapshot(case, list_cap=list_cap, lib=emu_lib)
+        got = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        assert got == want, (i, got, want)
+
+
+def test_emulated_kernels_match_oracle_c3_small(emu_lib):
+    snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 4, 16, 32))
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc, list_cap=64, lib=emu_lib)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    assert got == want
