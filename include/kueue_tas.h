@@ -170,18 +170,23 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* ctx, const kueue_tas_delta* d
                                     const uint32_t* usage_present_or_null);
 
 /* Evaluate n requests against the resident snapshot.
- *  taint_table: int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
- *  assumed:     overlay records referenced by reqs[i].assumed_begin/end
- *  out:         [n] result headers
- *  entries:     [n * entry_cap * 2] (leaf, count) int32 pairs per request; workers then leaders
- *  taint_counts:[n * num_taints] per-request taint exclusion counts (may be NULL)
- *  res_counts:  [n * num_cols]   per-request resource exclusion counts (may be NULL)
- * Returns KUEUE_TAS_OK, or an error; a request whose assignment does not fit
- * into entry_cap entries gets status KUEUE_TAS_ST_INTERNAL. */
+ *  taint_table:   int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
+ *  assumed:       overlay records referenced by reqs[i].assumed_begin/end
+ *  out:           [n] result headers
+ *  entry_offsets: [n+1] the (leaf, count) int32 pairs of request i are
+ *                 entries[2*off[i] .. 2*off[i+1]): workers, then leaders
+ *  entries:       packed pairs, capacity `entries_capacity` pairs
+ *  taint_counts:  [n * num_taints] per-request taint exclusion counts (may be NULL)
+ *  res_counts:    [n * num_cols]   per-request resource exclusion counts (may be NULL)
+ * Returns KUEUE_TAS_OK; KUEUE_TAS_EOVERFLOW when the packed entries exceed
+ * entries_capacity (out/entry_offsets are valid: grow the buffer and call
+ * kueue_tas_fetch_entries); or another error. */
 int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                          size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
-                         size_t num_assumed, kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap,
-                         int32_t* taint_counts, int32_t* res_counts);
+                         size_t num_assumed, kueue_tas_eval_out* out, int64_t* entry_offsets, int32_t* entries,
+                         size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts);
+/* Copy the packed entries of the last kueue_tas_eval_batch (after EOVERFLOW). */
+int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries_capacity);
 
 /* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
  * events on the ctx stream): [0] fill, [1] roll-up, [2] select/descend, [3] total. */

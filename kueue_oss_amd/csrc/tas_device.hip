@@ -103,6 +103,7 @@ struct kueue_tas_ctx {
   std::string err;
   int list_cap = 1024;
   int max_batch = 1024;
+  int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
   bool loaded = false;
   DevSnap snap{};
@@ -122,8 +123,15 @@ struct kueue_tas_ctx {
   DevBuf<int32_t> d_entries;
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
+  DevBuf<int64_t> d_offsets;
+  DevBuf<int32_t> d_packed;
+  DevBuf<LeafPartial> d_partials;
   HostBuf<DevEval> h_evals;
   HostBuf<DevTerm> h_terms;
+  HostBuf<kueue_tas_eval_out> h_out;
+  HostBuf<int64_t> h_offsets;
+  HostBuf<int32_t> h_stats;
+  std::vector<int32_t> last_entries;  // packed (leaf, count) pairs of the last batch
   float last_ms[4] = {0, 0, 0, 0};
 };
 
@@ -189,8 +197,14 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_entries.release();
   c->d_scratch.release();
   c->d_deltas.release();
+  c->d_offsets.release();
+  c->d_packed.release();
+  c->d_partials.release();
   c->h_evals.release();
   c->h_terms.release();
+  c->h_out.release();
+  c->h_offsets.release();
+  c->h_stats.release();
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -212,10 +226,10 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   int64_t off = 0;
   int maxD = 0;
   c->h_level_sizes.assign(d->level_sizes, d->level_sizes + s.L);
-  for (int l = 0; l < s.L; l++) {
+  for (int l = 0; l < s.L; l++) {  // level starts 16-byte aligned (vectorized leaf scans)
     s.level_size[l] = d->level_sizes[l];
     s.level_off[l] = int32_t(off);
-    off += d->level_sizes[l];
+    off += (int64_t(d->level_sizes[l]) + 3) / 4 * 4;
     maxD = std::max(maxD, d->level_sizes[l]);
   }
   s.level_off[s.L] = int32_t(off);
@@ -260,9 +274,13 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
     s.label_values = c->d_labels.p;
   }
   s.id_rank = nullptr;
-  if (d->domain_id_rank && off) {
+  if (d->domain_id_rank && off) {  // re-laid out on the padded level offsets
+    std::vector<int32_t> ranks(size_t(off), 0);
+    int64_t src = 0;
+    for (int l = 0; l < s.L; l++)
+      for (int i = 0; i < d->level_sizes[l]; i++) ranks[size_t(s.level_off[l] + i)] = d->domain_id_rank[src++];
     HIPCHK(c, c->d_id_rank.ensure(size_t(off)));
-    HIPCHK(c, hipMemcpyAsync(c->d_id_rank.p, d->domain_id_rank, size_t(off) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpy(c->d_id_rank.p, ranks.data(), size_t(off) * 4, hipMemcpyHostToDevice));
     s.id_rank = c->d_id_rank.p;
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -296,8 +314,9 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
 
 static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
-                      kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap, int32_t* taint_counts,
-                      int32_t* res_counts, float* ms) {
+                      kueue_tas_eval_out* out, int64_t* offsets, int32_t* taint_counts, int32_t* res_counts,
+                      float* ms) {
+  const int32_t entry_cap = c->entry_cap;
   const DevSnap& s = c->snap;
   // ---- compile requests to device form (magic numbers) ----
   HIPCHK(c, c->h_evals.ensure(n));
@@ -377,7 +396,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t stats_len = n * nt + n * size_t(s.R) + n;
   HIPCHK(c, c->d_stats.ensure(stats_len));
   HIPCHK(c, c->d_out.ensure(n));
-  HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));
+  HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));  // per-eval regions, packed after select
   HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
 
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
@@ -409,6 +428,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.scratch_stride = scratch_stride;
   b.scratch = c->d_scratch.p;
   b.list_cap = c->list_cap;
+  b.nblk = (s.N + 255) / 256;
+  HIPCHK(c, c->d_partials.ensure(n * size_t(std::max(b.nblk, 1))));
+  b.partials = c->d_partials.p;
 
   // K1
   if (s.N > 0) {
@@ -422,8 +444,16 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   // K2
   for (int l = s.L - 2; l >= 0; l--) {
-    dim3 grid((s.level_size[l] + 255) / 256, unsigned(n));
-    if (s.level_size[l] > 0) hipLaunchKernelGGL(rollup_level_kernel, grid, dim3(256), 0, c->stream, s, b, l);
+    if (s.level_size[l] <= 0) continue;
+    const int fanout = s.level_size[l + 1] / s.level_size[l];
+    if (fanout >= 8) {  // wave per parent: coalesced child reads
+      const int per_block = 4 * kParentsPerWave;
+      dim3 grid((s.level_size[l] + per_block - 1) / per_block, unsigned(n));
+      hipLaunchKernelGGL(rollup_level_wave_kernel, grid, dim3(256), 0, c->stream, s, b, l);
+    } else {
+      dim3 grid((s.level_size[l] + 255) / 256, unsigned(n));
+      hipLaunchKernelGGL(rollup_level_kernel, grid, dim3(256), 0, c->stream, s, b, l);
+    }
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -435,14 +465,38 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(select_kernel, grid, dim3(64 * waves), lds, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
+  // pack the per-eval entries: offsets (scan) + compaction, then one D2H of exactly the used pairs
+  HIPCHK(c, c->d_offsets.ensure(n + 1));
+  hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_out.p, int(n), entry_cap,
+                     c->d_offsets.p);
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  HIPCHK(c, hipMemcpyAsync(out, c->d_out.p, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(entries, c->d_entries.p, n * size_t(entry_cap) * 2 * 4, hipMemcpyDeviceToHost, c->stream));
-  if (taint_counts && nt)
-    HIPCHK(c, hipMemcpyAsync(taint_counts, b.taint_counts, n * nt * 4, hipMemcpyDeviceToHost, c->stream));
-  if (res_counts && s.R)
-    HIPCHK(c, hipMemcpyAsync(res_counts, b.res_counts, n * size_t(s.R) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, c->h_out.ensure(n));
+  HIPCHK(c, c->h_offsets.ensure(n + 1));
+  HIPCHK(c, c->h_stats.ensure(stats_len));
+  HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_offsets.p, c->d_offsets.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_stats.p, c->d_stats.p, stats_len * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  int32_t need = 0;
+  for (size_t i = 0; i < n; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
+  if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
+  const int64_t total = c->h_offsets.p[n];
+  HIPCHK(c, c->d_packed.ensure(size_t(std::max<int64_t>(total, 1)) * 2));
+  if (total > 0) {
+    hipLaunchKernelGGL(pack_entries_kernel, dim3(unsigned(n)), dim3(256), 0, c->stream, c->d_entries.p, entry_cap,
+                       c->d_offsets.p, c->d_packed.p, int(n));
+    HIPCHK(c, hipGetLastError());
+    size_t base = c->last_entries.size();
+    c->last_entries.resize(base + size_t(total) * 2);
+    HIPCHK(c, hipMemcpyAsync(c->last_entries.data() + base, c->d_packed.p, size_t(total) * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
+  for (size_t i = 0; i <= n; i++) offsets[i] = c->h_offsets.p[i];
+  if (taint_counts && nt) memcpy(taint_counts, c->h_stats.p, n * nt * 4);
+  if (res_counts && s.R) memcpy(res_counts, c->h_stats.p + n * nt, n * size_t(s.R) * 4);
   float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
   (void)hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
@@ -457,23 +511,51 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
 
 int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                          size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
-                         size_t num_assumed, kueue_tas_eval_out* out, int32_t* entries, int32_t entry_cap,
-                         int32_t* taint_counts, int32_t* res_counts) {
+                         size_t num_assumed, kueue_tas_eval_out* out, int64_t* entry_offsets, int32_t* entries,
+                         size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts) {
   if (!c) return KUEUE_TAS_EINVAL;
   if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
-  if (entry_cap < 1) return fail(c, KUEUE_TAS_EINVAL, "entry_cap");
   HIPCHK(c, hipSetDevice(c->device));
   float ms[4] = {0, 0, 0, 0};
+  c->last_entries.clear();
   const size_t chunk = size_t(c->max_batch);
+  std::vector<int64_t> off;
+  entry_offsets[0] = 0;
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t m = std::min(chunk, n - i0);
-    int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
-                        entries + i0 * size_t(entry_cap) * 2, entry_cap,
-                        taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
-                        res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms);
-    if (rc) return rc;
+    off.assign(m + 1, 0);
+    for (;;) {
+      size_t keep = c->last_entries.size();
+      int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
+                          off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
+                          res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms);
+      if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
+        c->last_entries.resize(keep);
+        int32_t need = 0;
+        for (size_t i = 0; i < m; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
+        int cap = c->entry_cap;
+        while (cap < need) cap *= 2;
+        c->entry_cap = cap;
+        continue;
+      }
+      if (rc) return rc;
+      break;
+    }
+    const int64_t base = entry_offsets[i0];
+    for (size_t i = 1; i <= m; i++) entry_offsets[i0 + i] = base + off[i];
   }
   memcpy(c->last_ms, ms, sizeof ms);
+  const size_t total = c->last_entries.size() / 2;
+  if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
+  if (total) memcpy(entries, c->last_entries.data(), total * 8);
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_capacity) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  const size_t total = c->last_entries.size() / 2;
+  if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
+  if (total) memcpy(entries, c->last_entries.data(), total * 8);
   return KUEUE_TAS_OK;
 }
 

@@ -851,13 +851,13 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
 // (groups of one workload are sequential through assumedUsage, :543-591).
 struct Evaluator {
   FlavorSnapshot* snap;
-  int32_t entry_cap = 4096;
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
   std::vector<kueue_tas_eval_out> outs;
+  std::vector<int64_t> offsets;
   std::vector<int32_t> entries, taint_counts, res_counts;
 
   static void set_result(std::vector<PodSetResult>& rs, const std::string& name, bool has, std::vector<DomainAssignment> d,
@@ -877,16 +877,22 @@ struct Evaluator {
     rs.push_back(std::move(r));
   }
 
-  int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results) {
-    results->assign(wls.size(), {});
-    bool changed = false;
-    for (auto& wl : wls) {
-      if (wl.groups.empty()) make_groups(wl);
-      changed |= snap->ensure_columns_for(wl.podsets);
+  int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results,
+          bool precompiled = false) {
+    ms[0] = ms[1] = ms[2] = ms[3] = 0;
+    counts[0] = counts[1] = counts[2] = 0;
+    results->resize(wls.size());
+    for (auto& r : *results) r.clear();
+    if (!precompiled) {
+      bool changed = false;
+      for (auto& wl : wls) {
+        if (wl.groups.empty()) make_groups(wl);
+        changed |= snap->ensure_columns_for(wl.podsets);
+      }
+      for (auto& wl : wls)
+        for (auto& g : wl.groups)
+          if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
     }
-    for (auto& wl : wls)
-      for (auto& g : wl.groups)
-        if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
     std::vector<char> done(wls.size(), 0);
@@ -927,23 +933,20 @@ struct Evaluator {
       if (batch.empty()) continue;
       const size_t n = batch.size();
       outs.resize(n);
-      int32_t cap = entry_cap;
-      for (;;) {
-        entries.resize(n * size_t(cap) * 2);
-        taint_counts.assign(n * std::max<size_t>(T, 1), 0);
-        res_counts.assign(n * R, 0);
-        rc = kueue_tas_eval_batch(snap->ctx, reqs.data(), n, taint_table.data(), taint_table.size(), int32_t(T),
-                                  assumed.data(), assumed.size(), outs.data(), entries.data(), cap,
-                                  taint_counts.data(), res_counts.data());
-        if (rc) {
-          snap->err = std::string("eval: ") + kueue_tas_last_error(snap->ctx);
-          return rc;
-        }
-        bool retry = false;
-        for (size_t i = 0; i < n; i++)
-          if (outs[i].status == KUEUE_TAS_ST_INTERNAL && outs[i].num_workers + outs[i].num_leaders > cap) retry = true;
-        if (!retry || cap >= (1 << 22)) break;
-        cap *= 4;
+      offsets.resize(n + 1);
+      if (entries.size() < 2 * 64 * n) entries.resize(2 * 64 * n);
+      taint_counts.resize(n * std::max<size_t>(T, 1));
+      res_counts.resize(n * R);
+      rc = kueue_tas_eval_batch(snap->ctx, reqs.data(), n, taint_table.data(), taint_table.size(), int32_t(T),
+                                assumed.data(), assumed.size(), outs.data(), offsets.data(), entries.data(),
+                                entries.size() / 2, taint_counts.data(), res_counts.data());
+      if (rc == KUEUE_TAS_EOVERFLOW) {
+        entries.resize(size_t(offsets[n]) * 2 + 2);
+        rc = kueue_tas_fetch_entries(snap->ctx, entries.data(), entries.size() / 2);
+      }
+      if (rc) {
+        snap->err = std::string("eval: ") + kueue_tas_last_error(snap->ctx);
+        return rc;
       }
       float t4[4];
       kueue_tas_last_timings(snap->ctx, t4);
@@ -963,7 +966,7 @@ struct Evaluator {
           done[w] = 1;
           continue;
         }
-        const int32_t* e = entries.data() + i * size_t(cap) * 2;
+        const int32_t* e = entries.data() + size_t(offsets[i]) * 2;
         std::vector<DomainAssignment> wk, ld;
         for (int k = 0; k < o.num_workers; k++) wk.push_back({e[2 * k], e[2 * k + 1]});
         for (int k = 0; k < o.num_leaders; k++) ld.push_back({e[2 * (o.num_workers + k)], e[2 * (o.num_workers + k) + 1]});
@@ -1039,6 +1042,7 @@ struct kueue_tas_host {
   std::unique_ptr<FlavorSnapshot> snap;
   std::string err;
   std::vector<Workload> compiled;
+  std::unique_ptr<Evaluator> ev;
   std::vector<std::vector<PodSetResult>> last;
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
@@ -1153,9 +1157,10 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
 // snapshot, results decoded to (leaf, count) lists; FNV-1a over all results.
 int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
   if (!h || !h->snap) return KUEUE_TAS_EINVAL;
-  Evaluator ev{h->snap.get()};
+  if (!h->ev) h->ev = std::make_unique<Evaluator>(Evaluator{h->snap.get()});
+  Evaluator& ev = *h->ev;
   std::vector<std::vector<PodSetResult>>& results = h->last;
-  int rc = ev.run(h->compiled, false, &results);
+  int rc = ev.run(h->compiled, false, &results, /*precompiled=*/true);
   if (rc) {
     h->err = h->snap->err;
     return rc;

@@ -70,6 +70,24 @@ struct DevSnap {
   const int32_t* label_values;         // [K][N] or null
 };
 
+// 128-bit lexicographic sort key; lo's low 32 bits hold the domain index in its level.
+struct Key {
+  uint64_t hi, lo;
+};
+
+// Per-(eval, fill block) reductions over the block's leaves, for evals whose
+// requested level is the leaf level: findLevelWithFitDomains (:1244-1270) then
+// reduces gridDim.x partials instead of every leaf.
+struct LeafPartial {
+  Key top;      // min sortedDomainsWithLeader key
+  Key last;     // max key
+  Key lfcfit;   // min key with sliceState >= sliceCount
+  Key bfkey;    // min key among st == bfst
+  uint32_t bfst;   // min sortable(st) with st >= sliceCount (st: sliceState, or sliceStateWithLeader with a leader)
+  int32_t minss;   // min sliceState
+  int32_t pad[2];
+};
+
 // Per-batch device buffers.
 struct DevBatch {
   const DevEval* evals;
@@ -89,6 +107,8 @@ struct DevBatch {
   int64_t scratch_stride;  // uint64 elements of scratch per eval
   uint64_t* scratch;       // [n][scratch_stride]
   int32_t list_cap;        // LDS sort capacity per wave
+  LeafPartial* partials;   // [n][nblk]
+  int32_t nblk;            // fill blocks per eval (partials per eval)
 };
 
 }  // namespace ktas

@@ -86,10 +86,6 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   return (uint64_t(hi) << 32) | lo;
 }
 
-// 128-bit lexicographic key; lo's low 32 bits hold the domain index in its level.
-struct Key {
-  uint64_t hi, lo;
-};
 __device__ __forceinline__ bool key_lt(const Key& a, const Key& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
 __device__ __forceinline__ bool key_le(const Key& a, const Key& b) { return !key_lt(b, a); }
 __device__ __forceinline__ Key key_max() { return Key{~0ull, ~0ull}; }
@@ -176,8 +172,13 @@ __device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, u
   return any ? result : 0;
 }
 
+__device__ __forceinline__ Key key_min2(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
+__device__ __forceinline__ Key key_max2(const Key& a, const Key& b) { return key_lt(a, b) ? b : a; }
+
 template <int MAXT>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, DevBatch b) {
+  __shared__ Key sh_k[4][4];
+  __shared__ uint32_t sh_u[4][2];
   __shared__ DevEval sh_ev[kEvalsPerBlock];
   __shared__ DevTerm sh_terms[kEvalsPerBlock][2 * MAXT];
   __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
@@ -315,6 +316,56 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         base[4 * SD + gleaf] = ls;
       }
     }
+    // Leaf-level selection partials (findLevelWithFitDomains at the leaf level).
+    if (ev.requested_level == s.L - 1) {
+      const bool lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
+      const int32_t sliceCount = go_div32(ev.count, ev.slice_size);
+      int32_t ss = 0, sswl = 0;
+      if (s.L - 1 == ev.slice_level) {
+        ss = go_div32(state, ev.slice_size);
+        sswl = go_div32(swl, ev.slice_size);
+      }
+      Key k = key_wl(lfc, ls, sswl, swl, leaf);
+      Key top = valid ? k : key_max();
+      Key inv = valid ? Key{~k.hi, ~k.lo} : key_max();
+      Key lf = (valid && ss >= sliceCount) ? k : key_max();
+      const int32_t st = leader ? sswl : ss;
+      uint32_t bst = (valid && st >= sliceCount) ? s_asc(st) : ~0u;
+      uint32_t mss = valid ? s_asc(ss) : ~0u;
+      top = wave_min_key(top);
+      inv = wave_min_key(inv);
+      lf = wave_min_key(lf);
+      bst = uint32_t(wave_min_u64(bst));
+      mss = uint32_t(wave_min_u64(mss));
+      const int wv = threadIdx.x >> 6;
+      if (lane == 0) {
+        sh_k[wv][0] = top;
+        sh_k[wv][1] = inv;
+        sh_k[wv][2] = lf;
+        sh_u[wv][0] = bst;
+        sh_u[wv][1] = mss;
+      }
+      __syncthreads();
+      uint32_t bbst = min(min(sh_u[0][0], sh_u[1][0]), min(sh_u[2][0], sh_u[3][0]));
+      Key bk = (valid && st >= sliceCount && s_asc(st) == bbst) ? k : key_max();
+      bk = wave_min_key(bk);
+      if (lane == 0) sh_k[wv][3] = bk;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        LeafPartial pt;
+        pt.top = key_min2(key_min2(sh_k[0][0], sh_k[1][0]), key_min2(sh_k[2][0], sh_k[3][0]));
+        Key mi = key_min2(key_min2(sh_k[0][1], sh_k[1][1]), key_min2(sh_k[2][1], sh_k[3][1]));
+        pt.last = Key{~mi.hi, ~mi.lo};
+        pt.lfcfit = key_min2(key_min2(sh_k[0][2], sh_k[1][2]), key_min2(sh_k[2][2], sh_k[3][2]));
+        pt.bfkey = key_min2(key_min2(sh_k[0][3], sh_k[1][3]), key_min2(sh_k[2][3], sh_k[3][3]));
+        pt.bfst = bbst;
+        uint32_t m = min(min(sh_u[0][1], sh_u[1][1]), min(sh_u[2][1], sh_u[3][1]));
+        pt.minss = int32_t(m ^ 0x80000000u);
+        pt.pad[0] = pt.pad[1] = 0;
+        b.partials[int64_t(eid) * b.nblk + blockIdx.x] = pt;
+      }
+      __syncthreads();
+    }
     // ExclusionStats (:1579-1634), aggregated per wave before the atomics.
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
@@ -401,6 +452,82 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
   }
 }
 
+// Same reduction with one wave per parent: lanes stride over the CSR children
+// (coalesced reads), then a wave reduction.  Used when the mean fan-out is
+// large (e.g. leaves -> racks).  kParentsPerWave parents per wave.
+constexpr int kParentsPerWave = 4;
+__global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBatch b, int level) {
+  const int eid = blockIdx.y;
+  if (eid >= b.n) return;
+  const DevEval& ev = b.evals[eid];
+  const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+  const int cl = level + 1;
+  const int32_t inner = ev.ssal[cl];
+  const bool hasInner = inner != 0;
+  int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+  const int64_t SD = s.SD;
+  const int coff = s.level_off[cl];
+  const int lane = lane_id();
+  const int p0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kParentsPerWave;
+  for (int j = 0; j < kParentsPerWave; j++) {
+    const int p = p0 + j;
+    if (p >= s.level_size[level]) return;
+    const int cb = s.child_off[s.child_base[level] + p];
+    const int ce = s.child_off[s.child_base[level] + p + 1];
+    int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0;
+    int has = 0;
+    for (int c = cb + lane; c < ce; c += kWave) {
+      const int g = coff + c;
+      int32_t cs = base[g];
+      int32_t css = base[SD + g];
+      int32_t csw = cs, csswl = css, cls = 0;
+      if (leaderReq) {
+        csw = base[2 * SD + g];
+        csswl = base[3 * SD + g];
+        cls = base[4 * SD + g];
+      }
+      if (hasInner) {
+        cs = w_mul(go_div32(cs, inner), inner);
+        csw = w_mul(go_div32(csw, inner), inner);
+      }
+      cap = w_add(cap, cs);
+      slc = w_add(slc, css);
+      if (!leaderReq || cls > 0) {
+        has = 1;
+        minD = min(w_sub(cs, csw), minD);
+        minSD = min(w_sub(css, csswl), minSD);
+      }
+      lead = max(cls, lead);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      cap = w_add(cap, __shfl_xor(cap, m, 64));
+      slc = w_add(slc, __shfl_xor(slc, m, 64));
+      minD = min(minD, __shfl_xor(minD, m, 64));
+      minSD = min(minSD, __shfl_xor(minSD, m, 64));
+      lead = max(lead, __shfl_xor(lead, m, 64));
+      has |= __shfl_xor(has, m, 64);
+    }
+    if (lane == 0) {
+      int32_t state = cap;
+      int32_t swl = has ? w_sub(cap, minD) : 0;
+      int32_t sswl = has ? w_sub(slc, minSD) : 0;
+      if (level == ev.slice_level) {
+        slc = go_div32(state, ev.slice_size);
+        sswl = go_div32(swl, ev.slice_size);
+      }
+      const int g = s.level_off[level] + p;
+      base[g] = state;
+      base[SD + g] = slc;
+      if (leaderReq) {
+        base[2 * SD + g] = swl;
+        base[3 * SD + g] = sswl;
+        base[4 * SD + g] = lead;
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------
 // K3: phase 2, one wave per eval
 // ----------------------------------------------------------------------------
@@ -424,6 +551,8 @@ struct Wave {
   Key* gkeys2;
   int lcap;
   bool overflow;
+  const LeafPartial* partials;  // leaf-level partial reductions of this eval (or null)
+  int nblk;
 
   __device__ int32_t get(Field f, int g) const {
     if (!leader) {
@@ -874,44 +1003,94 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
   return cnt - base;
 }
 
+// Wave-wide exclusive prefix sum of per-lane counts.
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = lane_id();
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl(x, max(lane - d, 0), 64);
+    if (lane >= d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
 // LeastFreeCapacity greedy over all leaves without leaders (the
 // findLevelWithFitDomains greedy :1278-1318 followed by
 // updateCountsToMinimumGeneric, LFC order) for n > LDS capacity: histogram
 // threshold select on sliceState instead of a full sort.  Requires every
-// leaf sliceState >= 0.  Returns 1 done, 0 needs the generic path.
+// leaf sliceState >= 0 (then zero-capacity leaves are output-invisible).
+// Leaf counters are read 4 at a time (16-byte aligned level start).
+// Returns 1 done, 0 needs the generic path.
 __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& o, int32_t* ent, int ent_cap) {
   const DevSnap& s = *w.s;
   const int D = s.N;
   const int loff = s.level_off[s.L - 1];
   const int32_t ss = w.ev->slice_size;
+  const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
+  const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
+  const int nq = (D + 3) / 4;
   constexpr int kBins = 256;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B (host: list_cap >= 64)
   for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
   wave_sync();
   int64_t over = 0;
-  for (int i = w.lane; i < D; i += kWave) {
-    int32_t v = w.get(F_SLICE, loff + i);
-    if (v > 0) {
-      if (v < kBins) {
-        atomicAdd(&hist[v], 1u);
-      } else {
-        over += v;
+  for (int q = w.lane; q < nq; q += kWave) {
+    int4 v4 = SS4[q];
+    int vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int32_t v = vv[k];
+      if (4 * q + k < D && v > 0) {
+        if (v < kBins) atomicAdd(&hist[v], 1u);
+        else over += v;
       }
     }
   }
   wave_sync();
   over = wave_sum_i64(over);
-  // find the threshold value t (ascending)
+  // threshold value t (ascending): per-lane chunk sums of bins, then a scan
   int64_t need = sliceCount;
   int64_t before = 0;
   int t = -1;
-  for (int v = 1; v < kBins; v++) {
-    int64_t add = int64_t(hist[v]) * v;
-    if (before + add >= need) {
-      t = v;
-      break;
+  {
+    // each lane owns 4 consecutive bins
+    int64_t local[4];
+    int64_t lsum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int v = 4 * w.lane + k;
+      local[k] = v >= 1 ? int64_t(hist[v]) * v : 0;
+      lsum += local[k];
     }
-    before += add;
+    int64_t x = lsum;
+    for (int d = 1; d < 64; d <<= 1) {
+      int64_t y = int64_t(shfl_u64(uint64_t(x), max(w.lane - d, 0)));
+      if (w.lane >= d) x += y;
+    }
+    int64_t excl = x - lsum;
+    // first lane whose inclusive sum reaches need
+    uint64_t m = ballot(x >= need);
+    if (m) {
+      int src = __ffsll((unsigned long long)m) - 1;
+      int64_t e = int64_t(shfl_u64(uint64_t(excl), src));
+      int tt = -1;
+      int64_t bb = e;
+      if (w.lane == src) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (tt < 0) {
+            if (bb + local[k] >= need) tt = 4 * w.lane + k;
+            else bb += local[k];
+          }
+        }
+      }
+      t = __shfl(tt, src, 64);
+      before = int64_t(shfl_u64(uint64_t(bb), src));
+    } else {
+      before = int64_t(shfl_u64(uint64_t(x), 63));
+    }
   }
   if (t < 0) {
     if (before + over >= need) return 0;  // threshold in the overflow range: generic path
@@ -927,11 +1106,15 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   int64_t mp = m;      // rank among (value t, state u) in index order
   if (ss > 1) {
     if (ss > kBins) return 0;
+    wave_sync();
     for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
     wave_sync();
-    for (int i = w.lane; i < D; i += kWave) {
-      int g = loff + i;
-      if (w.get(F_SLICE, g) == t) atomicAdd(&hist[w.get(F_STATE, g) - t * ss], 1u);
+    for (int q = w.lane; q < nq; q += kWave) {
+      int4 v4 = SS4[q], s4 = S4[q];
+      int vv[4] = {v4.x, v4.y, v4.z, v4.w}, st[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (4 * q + k < D && vv[k] == t) atomicAdd(&hist[st[k] - t * ss], 1u);
     }
     wave_sync();
     int64_t acc = 0;
@@ -946,31 +1129,52 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   // emit in index order: v < t (v > 0), or v == t && state < u, or (state == u && rank < mp)
   int64_t seen = 0;
   int cnt = 0;
-  for (int i0 = 0; i0 < D; i0 += kWave) {
-    int i = i0 + w.lane;
-    int32_t v = 0, st = 0;
-    if (i < D) {
-      v = w.get(F_SLICE, loff + i);
-      st = w.get(F_STATE, loff + i);
+  for (int q0 = 0; q0 < nq; q0 += kWave) {
+    const int q = q0 + w.lane;
+    int vv[4] = {0, 0, 0, 0}, st[4] = {0, 0, 0, 0};
+    if (q < nq) {
+      int4 v4 = SS4[q], s4 = S4[q];
+      vv[0] = v4.x; vv[1] = v4.y; vv[2] = v4.z; vv[3] = v4.w;
+      st[0] = s4.x; st[1] = s4.y; st[2] = s4.z; st[3] = s4.w;
     }
-    bool tie = i < D && v == t && st == u;
-    uint64_t tm = ballot(tie);
-    int64_t r = seen + __popcll(tm & ((1ull << w.lane) - 1ull));
-    bool keep = i < D && ((v > 0 && v < t) || (v == t && st < u) || (tie && r < mp));
-    bool crossing = tie && r == mp - 1;
-    int32_t val = crossing ? w_mul(rem_last, ss) : w_mul(v, ss);
-    uint64_t km = ballot(keep);
-    int rank = __popcll(km & ((1ull << w.lane) - 1ull));
-    if (keep) {
-      int pos = cnt + rank;
-      if (pos < ent_cap) {
-        ent[2 * pos] = i;
-        ent[2 * pos + 1] = val;
+    int ntie = 0;
+    bool tie[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      tie[k] = (4 * q + k < D) && vv[k] == t && st[k] == u;
+      ntie += tie[k] ? 1 : 0;
+    }
+    int tie_total;
+    int tie_excl = wave_excl_scan(ntie, &tie_total);
+    int64_t r = seen + tie_excl;
+    bool keep[4];
+    int32_t val[4];
+    int nkeep = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool in = 4 * q + k < D;
+      keep[k] = in && ((vv[k] > 0 && vv[k] < t) || (vv[k] == t && st[k] < u) || (tie[k] && r < mp));
+      const bool crossing = tie[k] && r == mp - 1;
+      val[k] = crossing ? w_mul(rem_last, ss) : w_mul(vv[k], ss);
+      if (tie[k]) r++;
+      nkeep += keep[k] ? 1 : 0;
+    }
+    int keep_total;
+    int pos = cnt + wave_excl_scan(nkeep, &keep_total);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (keep[k]) {
+        if (pos < ent_cap) {
+          ent[2 * pos] = 4 * q + k;
+          ent[2 * pos + 1] = val[k];
+        }
+        pos++;
       }
     }
-    cnt += __popcll(km);
-    seen += __popcll(tm);
+    cnt += keep_total;
+    seen += tie_total;
   }
+  wave_sync();
   o.status = KUEUE_TAS_ST_OK;
   o.fit_level = s.L - 1;
   o.num_workers = cnt;
@@ -998,23 +1202,44 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
     }
     // sortedDomainsWithLeader: first (top), last, LFC first fit, BF best fit
     Key top = key_max(), lfcfit = key_max(), last = Key{0, 0};
-    bool has_last = false;
     int32_t minss = 0x7fffffff;
-    for (int i = w.lane; i < D; i += kWave) {
-      int g = loff + i;
-      int32_t ls = w.get(F_LS, g), sswl = w.get(F_SSWL, g), swl = w.get(F_SWL, g), ss = w.get(F_SLICE, g);
-      Key k = key_wl(w.lfc, ls, sswl, swl, i);
-      if (key_lt(k, top)) top = k;
-      if (!has_last || key_lt(last, k)) {
-        last = k;
-        has_last = true;
+    const bool use_partials = level == s.L - 1 && w.partials != nullptr;
+    uint32_t pbst = ~0u;
+    Key pbk = key_max();
+    if (use_partials) {  // reductions precomputed per fill block
+      Key inv = key_max();
+      for (int i = w.lane; i < w.nblk; i += kWave) {
+        const LeafPartial& p = w.partials[i];
+        top = key_min2(top, p.top);
+        inv = key_min2(inv, Key{~p.last.hi, ~p.last.lo});
+        lfcfit = key_min2(lfcfit, p.lfcfit);
+        minss = min(minss, p.minss);
+        pbst = min(pbst, p.bfst);
       }
-      if (ss >= sliceCount && key_lt(k, lfcfit)) lfcfit = k;
-      minss = min(minss, ss);
-    }
-    top = wave_min_key(top);
-    lfcfit = wave_min_key(lfcfit);
-    {  // max key
+      top = wave_min_key(top);
+      lfcfit = wave_min_key(lfcfit);
+      inv = wave_min_key(inv);
+      last = Key{~inv.hi, ~inv.lo};
+      pbst = uint32_t(wave_min_u64(pbst));
+      for (int i = w.lane; i < w.nblk; i += kWave)
+        if (w.partials[i].bfst == pbst) pbk = key_min2(pbk, w.partials[i].bfkey);
+      pbk = wave_min_key(pbk);
+    } else {
+      bool has_last = false;
+      for (int i = w.lane; i < D; i += kWave) {
+        int g = loff + i;
+        int32_t ls = w.get(F_LS, g), sswl = w.get(F_SSWL, g), swl = w.get(F_SWL, g), ss = w.get(F_SLICE, g);
+        Key k = key_wl(w.lfc, ls, sswl, swl, i);
+        if (key_lt(k, top)) top = k;
+        if (!has_last || key_lt(last, k)) {
+          last = k;
+          has_last = true;
+        }
+        if (ss >= sliceCount && key_lt(k, lfcfit)) lfcfit = k;
+        minss = min(minss, ss);
+      }
+      top = wave_min_key(top);
+      lfcfit = wave_min_key(lfcfit);
       Key inv{~last.hi, ~last.lo};
       if (!has_last) inv = key_max();
       inv = wave_min_key(inv);
@@ -1026,22 +1251,26 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       // findBestFitDomainForSlices(sorted, sliceCount, leaderCount)
       Field f = leaderCount > 0 ? F_SSWL : F_SLICE;
       if (w.get(f, topg) >= sliceCount) {
-        uint32_t bst = ~0u;
-        for (int i = w.lane; i < D; i += kWave) {
-          int32_t st = w.get(f, loff + i);
-          if (st >= sliceCount && s_asc(st) < bst) bst = s_asc(st);
-        }
-        bst = uint32_t(wave_min_u64(uint64_t(bst)));
-        Key b = key_max();
-        for (int i = w.lane; i < D; i += kWave) {
-          int g = loff + i;
-          if (s_asc(w.get(f, g)) == bst) {
-            Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
-            if (key_lt(k, b)) b = k;
+        if (use_partials) {
+          topg = loff + int(uint32_t(pbk.lo));
+        } else {
+          uint32_t bst = ~0u;
+          for (int i = w.lane; i < D; i += kWave) {
+            int32_t st = w.get(f, loff + i);
+            if (st >= sliceCount && s_asc(st) < bst) bst = s_asc(st);
           }
+          bst = uint32_t(wave_min_u64(uint64_t(bst)));
+          Key b = key_max();
+          for (int i = w.lane; i < D; i += kWave) {
+            int g = loff + i;
+            if (s_asc(w.get(f, g)) == bst) {
+              Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
+              if (key_lt(k, b)) b = k;
+            }
+          }
+          b = wave_min_key(b);
+          topg = loff + int(uint32_t(b.lo));
         }
-        b = wave_min_key(b);
-        topg = loff + int(uint32_t(b.lo));
       }
     }
     if (w.lfc) {
@@ -1258,6 +1487,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.gkeys = reinterpret_cast<Key*>(sc + 2 * lcap);
   w.gkeys2 = w.gkeys + lcap;
   w.overflow = false;
+  w.partials = (b.partials && ev.requested_level == s.L - 1) ? b.partials + int64_t(eid) * b.nblk : nullptr;
+  w.nblk = b.nblk;
   int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
   const int ecap = b.entry_cap;
 
@@ -1343,6 +1574,46 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   }
   if (w.overflow) o.status = KUEUE_TAS_ST_INTERNAL;
   if (lane == 0) b.out[eid] = o;
+}
+
+// Packed result entries: offsets[i] = sum_{j<i} min(count_j, cap) (single block).
+__global__ __launch_bounds__(1024) void entry_offsets_kernel(const kueue_tas_eval_out* out, int n, int cap,
+                                                             int64_t* offsets) {
+  __shared__ int64_t warp_sums[16];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    int i = base + int(threadIdx.x);
+    int64_t v = 0;
+    if (i < n) v = min(out[i].num_workers + out[i].num_leaders, cap);
+    // inclusive wave scan
+    int64_t x = v;
+    const int lane = lane_id();
+    for (int d = 1; d < 64; d <<= 1) {
+      int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane - d, 0)));
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) warp_sums[threadIdx.x >> 6] = x;
+    __syncthreads();
+    int64_t wpre = 0;
+    for (int k = 0; k < int(threadIdx.x >> 6); k++) wpre += warp_sums[k];
+    if (i < n) offsets[i] = carry + wpre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += wpre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offsets[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void pack_entries_kernel(const int32_t* entries, int cap, const int64_t* offsets,
+                                                           int32_t* packed, int n) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const int64_t o = offsets[i];
+  const int cnt = int(offsets[i + 1] - o);
+  const int32_t* src = entries + int64_t(i) * cap * 2;
+  for (int k = threadIdx.x; k < 2 * cnt; k += blockDim.x) packed[2 * o + k] = src[k];
 }
 
 // Snapshot delta: tas_usage[col][leaf] += delta (updateTASUsage :257-293)

@@ -111,6 +111,13 @@ inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind
   if (n) memmove(d, s, n);
   return hipSuccess;
 }
+inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+  if (n) memmove(d, s, n);
+  return hipSuccess;
+}
+struct int4 {
+  int x, y, z, w;
+};
 inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
   memset(d, v, n);
   return hipSuccess;

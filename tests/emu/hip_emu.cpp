@@ -112,9 +112,9 @@ void launch(dim3 grid, dim3 block, size_t shmem, const std::function<void()>& fn
   }
   g_fn = &fn;
   g_lds.assign(shmem + 16, 0);
-  g_fibers.resize(T);
-  for (auto& f : g_fibers)
-    if (f.stack.size() != (512u << 10)) f.stack.assign(512u << 10, 0);
+  if (int(g_fibers.size()) < T) g_fibers.resize(T);  // never shrink: stacks are reused across launches
+  for (int t = 0; t < T; t++)
+    if (g_fibers[t].stack.size() != (256u << 10)) g_fibers[t].stack.assign(256u << 10, 0);
   for (unsigned bz = 0; bz < grid.z; bz++)
     for (unsigned by = 0; by < grid.y; by++)
       for (unsigned bx = 0; bx < grid.x; bx++) {
