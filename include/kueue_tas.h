@@ -218,6 +218,9 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
  * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
  * counts[1] = evaluations, counts[2] = evaluations with a leader. */
 int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
+/* Host wall time of the last run_compiled (ms): [0] request staging,
+ * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
+int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
 /* Per-workload compact results of the last run_compiled into buf (int32):
  * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
  * 4 int32 per workload (used for the cross-rank all-gather). */

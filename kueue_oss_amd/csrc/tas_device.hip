@@ -428,7 +428,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.scratch_stride = scratch_stride;
   b.scratch = c->d_scratch.p;
   b.list_cap = c->list_cap;
-  b.nblk = (s.N + 255) / 256;
+  b.nblk = (s.N + 255) / 256 * 4;  // one partial per 64-leaf wave
   HIPCHK(c, c->d_partials.ensure(n * size_t(std::max(b.nblk, 1))));
   b.partials = c->d_partials.p;
 

@@ -15,6 +15,7 @@
 // (tas_kernels.hip).  This layer never evaluates a placement on the CPU: if the
 // device library or a GPU is unavailable, creation fails loudly.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -849,9 +850,14 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
 
 // Batched driver: pass p evaluates group p of every workload still running
 // (groups of one workload are sequential through assumedUsage, :543-591).
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
+  double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   int64_t counts[3] = {0, 0, 0};
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
@@ -881,6 +887,8 @@ struct Evaluator {
           bool precompiled = false) {
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     counts[0] = counts[1] = counts[2] = 0;
+    host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
+    const double t_start = now_ms();
     results->resize(wls.size());
     for (auto& r : *results) r.clear();
     if (!precompiled) {
@@ -931,6 +939,8 @@ struct Evaluator {
         batch.emplace_back(w, &g);
       }
       if (batch.empty()) continue;
+      const double t_call = now_ms();
+      host_ms[0] += t_call - t_start;
       const size_t n = batch.size();
       outs.resize(n);
       offsets.resize(n + 1);
@@ -948,6 +958,8 @@ struct Evaluator {
         snap->err = std::string("eval: ") + kueue_tas_last_error(snap->ctx);
         return rc;
       }
+      const double t_decode = now_ms();
+      host_ms[1] += t_decode - t_call;
       float t4[4];
       kueue_tas_last_timings(snap->ctx, t4);
       for (int k = 0; k < 4; k++) ms[k] += t4[k];
@@ -966,15 +978,11 @@ struct Evaluator {
           done[w] = 1;
           continue;
         }
-        const int32_t* e = entries.data() + size_t(offsets[i]) * 2;
-        std::vector<DomainAssignment> wk, ld;
-        for (int k = 0; k < o.num_workers; k++) wk.push_back({e[2 * k], e[2 * k + 1]});
-        for (int k = 0; k < o.num_leaders; k++) ld.push_back({e[2 * (o.num_workers + k)], e[2 * (o.num_workers + k) + 1]});
-        for (auto* m : g.members) {
-          if (m == g.workers) set_result((*results)[w], m->name, true, wk, "");
-          else if (m == g.leader) set_result((*results)[w], m->name, true, ld, "");
-          else set_result((*results)[w], m->name, false, {}, "");
-        }
+        const DomainAssignment* e = reinterpret_cast<const DomainAssignment*>(entries.data() + size_t(offsets[i]) * 2);
+        std::vector<DomainAssignment> wk(e, e + o.num_workers), ld(e + o.num_workers, e + o.num_workers + o.num_leaders);
+        // addAssumedUsage only matters for the workload's later groups
+        const bool more = pass + 1 < wls[w].groups.size();
+        if (more) {
         // addAssumedUsage (:658-666): SinglePodRequests x count (no pods term)
         auto add = [&](const TASPodSetRequests* tr, const std::vector<DomainAssignment>& ds) {
           for (auto& d : ds)
@@ -985,8 +993,16 @@ struct Evaluator {
         };
         add(g.workers, wk);
         if (g.leader) add(g.leader, ld);
+        }
+        for (auto* m : g.members) {
+          if (m == g.workers) set_result((*results)[w], m->name, true, std::move(wk), "");
+          else if (m == g.leader) set_result((*results)[w], m->name, true, std::move(ld), "");
+          else set_result((*results)[w], m->name, false, {}, "");
+        }
       }
+      host_ms[2] += now_ms() - t_decode;
     }
+    host_ms[3] = now_ms() - t_start;
     return 0;
   }
 };
@@ -1187,6 +1203,12 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
       }
     *result_hash = x;
   }
+  return 0;
+}
+
+int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4) {
+  if (!h || !h->ev) return KUEUE_TAS_EINVAL;
+  memcpy(ms4, h->ev->host_ms, sizeof h->ev->host_ms);
   return 0;
 }
 

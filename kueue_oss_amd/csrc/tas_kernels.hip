@@ -175,10 +175,15 @@ __device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, u
 __device__ __forceinline__ Key key_min2(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
 __device__ __forceinline__ Key key_max2(const Key& a, const Key& b) { return key_lt(a, b) ? b : a; }
 
+constexpr int kStageCols = 8;  // snapshot columns staged in LDS per block
+
 template <int MAXT>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, DevBatch b) {
-  __shared__ Key sh_k[4][4];
-  __shared__ uint32_t sh_u[4][2];
+  __shared__ int64_t sh_free[kStageCols][kFillThreads];
+  __shared__ int64_t sh_used[kStageCols][kFillThreads];
+  __shared__ int sh_slot[kMaxCols];
+  __shared__ int sh_stage_col[kStageCols];
+  __shared__ int sh_nstage;
   __shared__ DevEval sh_ev[kEvalsPerBlock];
   __shared__ DevTerm sh_terms[kEvalsPerBlock][2 * MAXT];
   __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
@@ -209,6 +214,28 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
   const bool valid = leaf < s.N;
   const int N = s.N;
   const int gleaf = s.level_off[s.L - 1] + leaf;
+  // Stage the columns the block's evals request: each snapshot word is read
+  // from HBM once per block and served from LDS to all its evals.
+  if (threadIdx.x == 0) {
+    uint32_t m = 0;
+    for (int e = 0; e < ne; e++) m |= sh_ev[e].req_mask | sh_ev[e].lead_mask;
+    int k = 0;
+    for (int c = 0; c < kMaxCols; c++) {
+      sh_slot[c] = -1;
+      if (((m >> c) & 1u) && k < kStageCols) {
+        sh_slot[c] = k;
+        sh_stage_col[k++] = c;
+      }
+    }
+    sh_nstage = k;
+  }
+  __syncthreads();
+  for (int k = 0; k < sh_nstage; k++) {
+    const int col = sh_stage_col[k];
+    sh_free[k][threadIdx.x] = valid ? s.free_cap[int64_t(col) * N + leaf] : 0;
+    sh_used[k][threadIdx.x] = valid ? s.tas_usage[int64_t(col) * N + leaf] : 0;
+  }
+  __syncthreads();
   const uint32_t fp = valid ? s.free_present[leaf] : 0u;
   const uint32_t up = valid ? s.usage_present[leaf] : 0u;
   const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
@@ -266,16 +293,22 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
           lcap[i] = 0;
           if (i < ev.nreq) {
             const int col = wt[i].col;
-            int64_t c = s.free_cap[int64_t(col) * N + leaf];
-            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
+            const int sl = sh_slot[col];
+            int64_t c = sl >= 0 ? sh_free[sl][threadIdx.x] : s.free_cap[int64_t(col) * N + leaf];
+            if (!sim)
+              c = int64_t(uint64_t(c) -
+                          uint64_t(sl >= 0 ? sh_used[sl][threadIdx.x] : s.tas_usage[int64_t(col) * N + leaf]));
             for (int a = a_lo; a < a_hi; a++)
               if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
             wcap[i] = c;
           }
           if (leader && i < ev.nlead) {
             const int col = lt[i].col;
-            int64_t c = s.free_cap[int64_t(col) * N + leaf];
-            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
+            const int sl = sh_slot[col];
+            int64_t c = sl >= 0 ? sh_free[sl][threadIdx.x] : s.free_cap[int64_t(col) * N + leaf];
+            if (!sim)
+              c = int64_t(uint64_t(c) -
+                          uint64_t(sl >= 0 ? sh_used[sl][threadIdx.x] : s.tas_usage[int64_t(col) * N + leaf]));
             for (int a = a_lo; a < a_hi; a++)
               if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
             lcap[i] = c;
@@ -337,34 +370,19 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
       lf = wave_min_key(lf);
       bst = uint32_t(wave_min_u64(bst));
       mss = uint32_t(wave_min_u64(mss));
-      const int wv = threadIdx.x >> 6;
-      if (lane == 0) {
-        sh_k[wv][0] = top;
-        sh_k[wv][1] = inv;
-        sh_k[wv][2] = lf;
-        sh_u[wv][0] = bst;
-        sh_u[wv][1] = mss;
-      }
-      __syncthreads();
-      uint32_t bbst = min(min(sh_u[0][0], sh_u[1][0]), min(sh_u[2][0], sh_u[3][0]));
-      Key bk = (valid && st >= sliceCount && s_asc(st) == bbst) ? k : key_max();
+      Key bk = (valid && st >= sliceCount && s_asc(st) == bst) ? k : key_max();
       bk = wave_min_key(bk);
-      if (lane == 0) sh_k[wv][3] = bk;
-      __syncthreads();
-      if (threadIdx.x == 0) {
+      if (lane == 0) {  // one partial per wave (64 leaves)
         LeafPartial pt;
-        pt.top = key_min2(key_min2(sh_k[0][0], sh_k[1][0]), key_min2(sh_k[2][0], sh_k[3][0]));
-        Key mi = key_min2(key_min2(sh_k[0][1], sh_k[1][1]), key_min2(sh_k[2][1], sh_k[3][1]));
-        pt.last = Key{~mi.hi, ~mi.lo};
-        pt.lfcfit = key_min2(key_min2(sh_k[0][2], sh_k[1][2]), key_min2(sh_k[2][2], sh_k[3][2]));
-        pt.bfkey = key_min2(key_min2(sh_k[0][3], sh_k[1][3]), key_min2(sh_k[2][3], sh_k[3][3]));
-        pt.bfst = bbst;
-        uint32_t m = min(min(sh_u[0][1], sh_u[1][1]), min(sh_u[2][1], sh_u[3][1]));
-        pt.minss = int32_t(m ^ 0x80000000u);
+        pt.top = top;
+        pt.last = Key{~inv.hi, ~inv.lo};
+        pt.lfcfit = lf;
+        pt.bfkey = bk;
+        pt.bfst = bst;
+        pt.minss = int32_t(mss ^ 0x80000000u);
         pt.pad[0] = pt.pad[1] = 0;
-        b.partials[int64_t(eid) * b.nblk + blockIdx.x] = pt;
+        b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
       }
-      __syncthreads();
     }
     // ExclusionStats (:1579-1634), aggregated per wave before the atomics.
     uint64_t selm = ballot(kind == EX_SELECTOR);
@@ -706,6 +724,31 @@ struct SeqList {
   }
 };
 
+// Explicit order from keys sorted in global memory (lists longer than the LDS).
+struct SeqKeys {
+  Wave* w;
+  const Key* k;
+  int n, level_off, pos;
+  __device__ bool done() const { return pos >= n; }
+  __device__ int at(int p) const { return level_off + int(uint32_t(k[p].lo)); }
+  __device__ int cur() const { return at(pos); }
+  __device__ void next() { pos++; }
+  __device__ int bestfit(int32_t needed, Field f) const {
+    int g0 = cur();
+    if (w->get(f, g0) < needed) return g0;
+    uint64_t best = ~0ull;
+    for (int p = pos + w->lane; p < n; p += kWave) {
+      int32_t st = w->get(f, at(p));
+      if (st >= needed) {
+        uint64_t kk = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
+        best = kk < best ? kk : best;
+      }
+    }
+    best = wave_min_u64(best);
+    return at(int(uint32_t(best)));
+  }
+};
+
 // Lazy sorted iteration over n materialized (unsorted) keys of one level.
 struct SeqLazy {
   Wave* w;
@@ -870,17 +913,19 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
     w.overflow = true;
     return false;
   }
+  // longer than the LDS: merge-sort the keys in global memory once (O(n log n)),
+  // then walk them in order
   for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = w.kplain(gids[i]);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  global_sort(w, w.gkeys, w.gkeys2, n);
   if (sliceRecompute > 1) {
     for (int i = 0; i < n; i++) {
-      int g = gids[i];
+      int g = loff + int(uint32_t(w.gkeys[i].lo));
       w.set(F_SLICE, g, go_div32(w.get(F_STATE, g), sliceRecompute));
       w.set(F_SSWL, g, go_div32(w.get(F_SWL, g), sliceRecompute));
     }
   }
-  SeqLazy seq{&w, w.gkeys, n, loff, Key{0, 0}, false};
-  seq.start();
+  SeqKeys seq{&w, w.gkeys, n, loff, 0};
   return update_counts(w, seq, count, leaderCount, sliceSize, slices, out, np);
 }
 

@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_last_timings", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_free",
+    "kueue_tas_host_last_records", "kueue_tas_host_last_profile", "kueue_tas_free",
 ]
 
 
@@ -93,6 +93,7 @@ def _bind(lib):
     lib.kueue_tas_host_run_compiled.restype = c.c_int
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
+    lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_free.argtypes = [c.c_void_p]
 
 
@@ -165,6 +166,12 @@ class TASFlavorSnapshot:
         cnt = (ctypes.c_int64 * 3)()
         self._lib.kueue_tas_host_last_timings(self._h, ms, cnt)
         return tuple(ms), tuple(cnt)
+
+    def last_profile(self):
+        """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""
+        ms = (ctypes.c_double * 4)()
+        self._lib.kueue_tas_host_last_profile(self._h, ms)
+        return tuple(ms)
 
     def last_records(self, n: int):
         """[n][4] int32 compact per-workload results of the last run_compiled."""
