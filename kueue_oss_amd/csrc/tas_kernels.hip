@@ -139,6 +139,25 @@ constexpr int kEvalsPerBlock = 8;
 
 enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3 };
 
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(uint64_t(v)));
+  uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(uint64_t(v) >> 32));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+// A request term with every field in scalar registers (wave-uniform).
+__device__ __forceinline__ DevTerm uni_term(const DevTerm& t) {
+  DevTerm u;
+  u.val = uni64(t.val);
+  u.magic = uint64_t(uni64(int64_t(t.magic)));
+  u.col = uni(t.col);
+  u.shift = uint8_t(uni(t.shift));
+  u.add = uint8_t(uni(t.add));
+  u.pow2 = uint8_t(uni(t.pow2));
+  u.neg = uint8_t(uni(t.neg));
+  return u;
+}
+
 // Requests.CountIn / CountInWithLimitingResource over up to MAXT terms held in
 // registers (fully unrolled: no runtime-indexed private arrays).  Terms are in
 // ascending column (= resource name) order, so the first missing key and the
@@ -152,7 +171,7 @@ __device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, u
 #pragma unroll
   for (int i = 0; i < MAXT; i++) {
     if (i < nt && !done) {
-      const DevTerm& t = terms[i];
+      const DevTerm t = uni_term(terms[i]);
       if (!((pres >> t.col) & 1u) && t.val != 0) {
         lim = t.col;
         result = 0;
@@ -175,15 +194,9 @@ __device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, u
 __device__ __forceinline__ Key key_min2(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
 __device__ __forceinline__ Key key_max2(const Key& a, const Key& b) { return key_lt(a, b) ? b : a; }
 
-constexpr int kStageCols = 8;  // snapshot columns staged in LDS per block
-
 template <int MAXT>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, DevBatch b) {
-  __shared__ int64_t sh_free[kStageCols][kFillThreads];
-  __shared__ int64_t sh_used[kStageCols][kFillThreads];
-  __shared__ int sh_slot[kMaxCols];
-  __shared__ int sh_stage_col[kStageCols];
-  __shared__ int sh_nstage;
+
   __shared__ DevEval sh_ev[kEvalsPerBlock];
   __shared__ DevTerm sh_terms[kEvalsPerBlock][2 * MAXT];
   __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
@@ -214,28 +227,6 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
   const bool valid = leaf < s.N;
   const int N = s.N;
   const int gleaf = s.level_off[s.L - 1] + leaf;
-  // Stage the columns the block's evals request: each snapshot word is read
-  // from HBM once per block and served from LDS to all its evals.
-  if (threadIdx.x == 0) {
-    uint32_t m = 0;
-    for (int e = 0; e < ne; e++) m |= sh_ev[e].req_mask | sh_ev[e].lead_mask;
-    int k = 0;
-    for (int c = 0; c < kMaxCols; c++) {
-      sh_slot[c] = -1;
-      if (((m >> c) & 1u) && k < kStageCols) {
-        sh_slot[c] = k;
-        sh_stage_col[k++] = c;
-      }
-    }
-    sh_nstage = k;
-  }
-  __syncthreads();
-  for (int k = 0; k < sh_nstage; k++) {
-    const int col = sh_stage_col[k];
-    sh_free[k][threadIdx.x] = valid ? s.free_cap[int64_t(col) * N + leaf] : 0;
-    sh_used[k][threadIdx.x] = valid ? s.tas_usage[int64_t(col) * N + leaf] : 0;
-  }
-  __syncthreads();
   const uint32_t fp = valid ? s.free_present[leaf] : 0u;
   const uint32_t up = valid ? s.usage_present[leaf] : 0u;
   const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
@@ -246,7 +237,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     const int eid = e0 + e;
     const DevTerm* wt = sh_terms[e];
     const DevTerm* lt = sh_terms[e] + MAXT;
-    const bool leader = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+    // wave-uniform copies (scalar registers: uniform branches below)
+    const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
+    const int nreq = uni(ev.nreq), nlead = uni(ev.nlead), nsel = uni(ev.nsel);
+    const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
+    const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     int32_t state = 0, swl = 0, ls = 0;
     int kind = EX_NONE, id = -1;
     if (valid) {
@@ -259,7 +254,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
           }
         }
         if (kind == EX_NONE) {
-          for (int k = 0; k < ev.nsel; k++) {
+          for (int k = 0; k < nsel; k++) {
             if (s.label_values[int64_t(ev.sel_col[k]) * N + leaf] != ev.sel_val[k]) {
               kind = EX_SELECTOR;
               break;
@@ -268,11 +263,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         }
       }
       if (kind == EX_NONE) {
-        const bool sim = (ev.flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
+        const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
         uint32_t pres = fp | (sim ? 0u : up);
         int a_lo = 0, a_hi = 0;
-        if (ev.assumed_end > ev.assumed_begin) {
-          int lo = ev.assumed_begin, hi = ev.assumed_end;
+        if (aend > abeg) {
+          int lo = abeg, hi = aend;
           while (lo < hi) {
             int mid = (lo + hi) >> 1;
             if (b.assumed[mid].leaf < leaf) lo = mid + 1;
@@ -280,7 +275,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
           }
           a_lo = lo;
           a_hi = lo;
-          while (a_hi < ev.assumed_end && b.assumed[a_hi].leaf == leaf) {
+          while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
             pres |= 1u << b.assumed[a_hi].col;
             a_hi++;
           }
@@ -291,31 +286,25 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         for (int i = 0; i < MAXT; i++) {
           wcap[i] = 0;
           lcap[i] = 0;
-          if (i < ev.nreq) {
+          if (i < nreq) {
             const int col = wt[i].col;
-            const int sl = sh_slot[col];
-            int64_t c = sl >= 0 ? sh_free[sl][threadIdx.x] : s.free_cap[int64_t(col) * N + leaf];
-            if (!sim)
-              c = int64_t(uint64_t(c) -
-                          uint64_t(sl >= 0 ? sh_used[sl][threadIdx.x] : s.tas_usage[int64_t(col) * N + leaf]));
+            int64_t c = s.free_cap[int64_t(col) * N + leaf];
+            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
             for (int a = a_lo; a < a_hi; a++)
               if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
             wcap[i] = c;
           }
-          if (leader && i < ev.nlead) {
+          if (leader && i < nlead) {
             const int col = lt[i].col;
-            const int sl = sh_slot[col];
-            int64_t c = sl >= 0 ? sh_free[sl][threadIdx.x] : s.free_cap[int64_t(col) * N + leaf];
-            if (!sim)
-              c = int64_t(uint64_t(c) -
-                          uint64_t(sl >= 0 ? sh_used[sl][threadIdx.x] : s.tas_usage[int64_t(col) * N + leaf]));
+            int64_t c = s.free_cap[int64_t(col) * N + leaf];
+            if (!sim) c = int64_t(uint64_t(c) - uint64_t(s.tas_usage[int64_t(col) * N + leaf]));
             for (int a = a_lo; a < a_hi; a++)
               if (b.assumed[a].col == col) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
             lcap[i] = c;
           }
         }
         int lim = -1;
-        state = count_in_regs<MAXT>(wt, ev.nreq, pres, wcap, &lim);
+        state = count_in_regs<MAXT>(wt, nreq, pres, wcap, &lim);
         if (state == 0 && lim >= 0) {
           kind = EX_RESOURCE;
           id = lim;
@@ -323,12 +312,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         swl = state;
         if (leader) {
           int dummy;
-          int32_t lc = count_in_regs<MAXT>(lt, ev.nlead, pres, lcap, &dummy);
+          int32_t lc = count_in_regs<MAXT>(lt, nlead, pres, lcap, &dummy);
           if (lc > 0) {
             ls = 1;
 #pragma unroll
             for (int i = 0; i < MAXT; i++) wcap[i] = int64_t(uint64_t(wcap[i]) - uint64_t(sh_wlead[e][i]));
-            swl = count_in_regs<MAXT>(wt, ev.nreq, pres | ev.lead_mask, wcap, &dummy);
+            swl = count_in_regs<MAXT>(wt, nreq, pres | uint32_t(uni(int32_t(ev.lead_mask))), wcap, &dummy);
           }
         }
       }

@@ -138,3 +138,6 @@ inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char
 
 #define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
   emu::launch(dim3(grid), dim3(block), size_t(shmem), [&]() { kernel(__VA_ARGS__); })
+
+// every lane holds the same value where the kernels use it (wave-uniform data)
+#define __builtin_amdgcn_readfirstlane(v) (v)
