@@ -435,7 +435,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   // K1
   if (s.N > 0) {
     dim3 grid((s.N + 255) / 256, unsigned((n + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
-    if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
+    uint32_t umask = 0;
+    for (size_t i = 0; i < n; i++) umask |= c->h_evals.p[i].req_mask | c->h_evals.p[i].lead_mask;
+    const int ucols = __builtin_popcount(umask);
+    if (ucols <= 4) hipLaunchKernelGGL(fill_leaves_staged_kernel<4>, grid, dim3(256), 0, c->stream, s, b, umask);
+    else if (ucols <= 8) hipLaunchKernelGGL(fill_leaves_staged_kernel<8>, grid, dim3(256), 0, c->stream, s, b, umask);
+    else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 8) hipLaunchKernelGGL(fill_leaves_kernel<8>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);

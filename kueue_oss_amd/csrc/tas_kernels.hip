@@ -400,6 +400,213 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 
 
 
+// Staged variant (the batch requests at most NS distinct resource columns):
+// every thread loads its leaf's free/used words of those columns ONCE into
+// registers (static slots, ascending column order) and reuses them for all
+// kEvalsPerBlock evals; per-eval request terms are read with uniform
+// (scalar) loads.  Semantics identical to fill_leaves_kernel.
+template <int NS>
+__global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
+  const int e0 = blockIdx.y * kEvalsPerBlock;
+  const int ne = min(kEvalsPerBlock, b.n - e0);
+  const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
+  const bool valid = leaf < s.N;
+  const int N = s.N;
+  const int gleaf = s.level_off[s.L - 1] + leaf;
+  const int lane = lane_id();
+  int scol[NS];
+  int64_t fr[NS], us[NS];
+  {
+    uint32_t m = stage_mask;
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      scol[k] = m ? __builtin_ctz(m) : -1;
+      if (m) m &= m - 1;
+      fr[k] = 0;
+      us[k] = 0;
+      if (valid && scol[k] >= 0) {
+        fr[k] = s.free_cap[int64_t(scol[k]) * N + leaf];
+        us[k] = s.tas_usage[int64_t(scol[k]) * N + leaf];
+      }
+    }
+  }
+  const uint32_t fp = valid ? s.free_present[leaf] : 0u;
+  const uint32_t up = valid ? s.usage_present[leaf] : 0u;
+  const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
+
+  for (int e = 0; e < ne; e++) {
+    const int eid = e0 + e;
+    const DevEval& ev = b.evals[eid];
+    const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
+    const uint32_t rmask = uint32_t(uni(int32_t(ev.req_mask)));
+    const uint32_t lmask = uint32_t(uni(int32_t(ev.lead_mask)));
+    const int tb = uni(ev.term_begin), lb = uni(ev.lead_begin);
+    const int nsel = uni(ev.nsel);
+    const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
+    const int32_t slice_size = uni(ev.slice_size), slice_level = uni(ev.slice_level);
+    const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
+    const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
+    int32_t state = 0, swl = 0, ls = 0;
+    int kind = EX_NONE, id = -1;
+    if (valid) {
+      if (s.lowest_is_hostname) {
+        if (s.taint_profile) {
+          int t = b.taint_table[uni(ev.taint_table) + prof];
+          if (t >= 0) {
+            kind = EX_TAINT;
+            id = t;
+          }
+        }
+        if (kind == EX_NONE) {
+          for (int k = 0; k < nsel; k++) {
+            if (s.label_values[int64_t(uni(ev.sel_col[k])) * N + leaf] != uni(ev.sel_val[k])) {
+              kind = EX_SELECTOR;
+              break;
+            }
+          }
+        }
+      }
+      if (kind == EX_NONE) {
+        uint32_t pres = fp | (sim ? 0u : up);
+        int a_lo = 0, a_hi = 0;
+        if (aend > abeg) {
+          int lo = abeg, hi = aend;
+          while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (b.assumed[mid].leaf < leaf) lo = mid + 1;
+            else hi = mid;
+          }
+          a_lo = lo;
+          a_hi = lo;
+          while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
+            pres |= 1u << b.assumed[a_hi].col;
+            a_hi++;
+          }
+        }
+        int64_t cap[NS];
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+          int64_t c = sim ? fr[k] : int64_t(uint64_t(fr[k]) - uint64_t(us[k]));
+          for (int a = a_lo; a < a_hi; a++)
+            if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+          cap[k] = c;
+        }
+        // CountInWithLimitingResource over the worker terms, ascending column order
+        auto count_slots = [&](uint32_t mask, int tbase, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
+          int32_t result = 0;
+          bool any = false, done = false;
+          int lim = -1;
+#pragma unroll
+          for (int k = 0; k < NS; k++) {
+            const int col = scol[k];
+            if (col >= 0 && ((mask >> col) & 1u) && !done) {
+              const DevTerm t = uni_term(b.terms[tbase + __popc(mask & ((1u << col) - 1u))]);
+              if (!((presm >> col) & 1u) && t.val != 0) {
+                lim = col;
+                result = 0;
+                any = true;
+                done = true;
+              } else {
+                int64_t c = cap[k];
+                if (sub_leader && ((lmask >> col) & 1u)) {
+                  const DevTerm lt = uni_term(b.terms[lb + __popc(lmask & ((1u << col) - 1u))]);
+                  c = int64_t(uint64_t(c) - uint64_t(lt.val));
+                }
+                int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
+                if (!any || cnt < result) {
+                  result = cnt;
+                  lim = col;
+                  any = true;
+                }
+              }
+            }
+          }
+          *lim_out = lim;
+          return any ? result : 0;
+        };
+        int lim = -1;
+        state = count_slots(rmask, tb, pres, false, &lim);
+        if (state == 0 && lim >= 0) {
+          kind = EX_RESOURCE;
+          id = lim;
+        }
+        swl = state;
+        if (leader) {
+          int dummy;
+          int32_t lc = count_slots(lmask, lb, pres, false, &dummy);
+          if (lc > 0) {
+            ls = 1;
+            swl = count_slots(rmask, tb, pres | lmask, true, &dummy);
+          }
+        }
+      }
+    }
+    int32_t ss = 0, sswl = 0;
+    if (s.L - 1 == slice_level) {
+      ss = go_div32(state, slice_size);
+      sswl = go_div32(swl, slice_size);
+    }
+    if (valid) {
+      int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+      const int64_t SD = s.SD;
+      base[gleaf] = state;
+      base[SD + gleaf] = ss;
+      if (leader) {
+        base[2 * SD + gleaf] = swl;
+        base[3 * SD + gleaf] = sswl;
+        base[4 * SD + gleaf] = ls;
+      }
+    }
+    if (uni(ev.requested_level) == s.L - 1) {
+      const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
+      const int32_t sliceCount = go_div32(uni(ev.count), slice_size);
+      Key k = key_wl(lfc, ls, sswl, swl, leaf);
+      Key top = valid ? k : key_max();
+      Key inv = valid ? Key{~k.hi, ~k.lo} : key_max();
+      Key lf = (valid && ss >= sliceCount) ? k : key_max();
+      const int32_t st = leader ? sswl : ss;
+      uint32_t bst = (valid && st >= sliceCount) ? s_asc(st) : ~0u;
+      uint32_t mss = valid ? s_asc(ss) : ~0u;
+      top = wave_min_key(top);
+      inv = wave_min_key(inv);
+      lf = wave_min_key(lf);
+      bst = uint32_t(wave_min_u64(bst));
+      mss = uint32_t(wave_min_u64(mss));
+      Key bk = (valid && st >= sliceCount && s_asc(st) == bst) ? k : key_max();
+      bk = wave_min_key(bk);
+      if (lane == 0) {
+        LeafPartial pt;
+        pt.top = top;
+        pt.last = Key{~inv.hi, ~inv.lo};
+        pt.lfcfit = lf;
+        pt.bfkey = bk;
+        pt.bfst = bst;
+        pt.minss = int32_t(mss ^ 0x80000000u);
+        pt.pad[0] = pt.pad[1] = 0;
+        b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
+      }
+    }
+    uint64_t selm = ballot(kind == EX_SELECTOR);
+    if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    uint64_t tm = ballot(kind == EX_TAINT);
+    while (tm) {
+      int src = __ffsll((unsigned long long)tm) - 1;
+      int tid = __shfl(id, src, 64);
+      uint64_t mm = ballot(kind == EX_TAINT && id == tid);
+      if (lane == 0) atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
+      tm &= ~mm;
+    }
+    uint64_t rm = ballot(kind == EX_RESOURCE);
+    while (rm) {
+      int src = __ffsll((unsigned long long)rm) - 1;
+      int rid = __shfl(id, src, 64);
+      uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
+      if (lane == 0) atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
+      rm &= ~mm;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------
 // K2: fillInCountsHelper, one level (parents at `level`)
 // ----------------------------------------------------------------------------

@@ -141,3 +141,4 @@ inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char
 
 // every lane holds the same value where the kernels use it (wave-uniform data)
 #define __builtin_amdgcn_readfirstlane(v) (v)
+inline int __popc(unsigned x) { return __builtin_popcount(x); }
