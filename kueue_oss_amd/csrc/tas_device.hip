@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "tas_internal.h"
@@ -126,6 +127,10 @@ struct kueue_tas_ctx {
   DevBuf<int64_t> d_offsets;
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
+  DevBuf<int32_t> d_fill_ids, d_pairs;
+  std::vector<int32_t> h_fill_ids, h_pairs;
+  int num_profiles = 1;
+  int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
   HostBuf<DevEval> h_evals;
   HostBuf<DevTerm> h_terms;
   HostBuf<kueue_tas_eval_out> h_out;
@@ -200,6 +205,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_offsets.release();
   c->d_packed.release();
   c->d_partials.release();
+  c->d_fill_ids.release();
+  c->d_pairs.release();
   c->h_evals.release();
   c->h_terms.release();
   c->h_out.release();
@@ -262,7 +269,9 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   s.free_present = c->d_free_present.p;
   s.usage_present = c->d_usage_present.p;
   s.taint_profile = nullptr;
+  c->num_profiles = 1;
   if (d->taint_profile && N) {
+    for (size_t i = 0; i < N; i++) c->num_profiles = std::max(c->num_profiles, d->taint_profile[i] + 1);
     HIPCHK(c, c->d_taint_profile.ensure(N));
     HIPCHK(c, hipMemcpyAsync(c->d_taint_profile.p, d->taint_profile, N * 4, hipMemcpyHostToDevice, c->stream));
     s.taint_profile = c->d_taint_profile.p;
@@ -432,9 +441,62 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, c->d_partials.ensure(n * size_t(std::max(b.nblk, 1))));
   b.partials = c->d_partials.p;
 
+  // Phase-1 classes: evals with identical phase-1 inputs (request terms,
+  // masks, overlay, slice parameters, partial parameters) get identical
+  // counters; phase 1 runs once per class and is replicated.
+  c->h_fill_ids.clear();
+  c->h_pairs.clear();
+  {
+    std::unordered_map<std::string, int32_t> rep;
+    rep.reserve(n * 2);
+    std::string key;
+    for (size_t i = 0; i < n; i++) {
+      const DevEval& e = c->h_evals.p[i];
+      const bool leafsel = e.requested_level == s.L - 1;
+      key.clear();
+      auto put = [&](const void* p, size_t len) { key.append(static_cast<const char*>(p), len); };
+      uint32_t f = e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY | (leafsel ? KUEUE_TAS_F_LFC : 0u));
+      put(&f, 4);
+      int32_t hdr[4] = {leafsel ? 1 : 0, leafsel ? e.count : 0, e.slice_size, e.slice_level};
+      put(hdr, sizeof hdr);
+      put(e.ssal, sizeof e.ssal);
+      put(&e.nsel, 4);
+      put(e.sel_col, 4 * size_t(e.nsel));
+      put(e.sel_val, 4 * size_t(e.nsel));
+      if (taint_table && size_t(e.taint_table) + size_t(c->num_profiles) <= taint_table_len)
+        put(taint_table + e.taint_table, 4 * size_t(c->num_profiles));
+      int32_t nt2[2] = {e.nreq, e.nlead};
+      put(nt2, sizeof nt2);
+      for (int k = 0; k < e.nreq + e.nlead; k++) {
+        const DevTerm& t = c->h_terms.p[(k < e.nreq ? e.term_begin + k : e.lead_begin + (k - e.nreq))];
+        put(&t.col, 4);
+        put(&t.val, 8);
+      }
+      for (int a = e.assumed_begin; a < e.assumed_end; a++) put(&assumed[a], sizeof(kueue_tas_assumed));
+      auto it = rep.find(key);
+      if (it == rep.end()) {
+        rep.emplace(key, int32_t(i));
+        c->h_fill_ids.push_back(int32_t(i));
+      } else {
+        c->h_pairs.push_back(it->second);
+        c->h_pairs.push_back(int32_t(i));
+      }
+    }
+  }
+  const int nfill = int(c->h_fill_ids.size());
+  const int npairs = int(c->h_pairs.size() / 2);
+  c->stat_fills += nfill;
+  c->stat_evals += int64_t(n);
+  HIPCHK(c, c->d_fill_ids.ensure(size_t(std::max(nfill, 1))));
+  HIPCHK(c, c->d_pairs.ensure(size_t(std::max(2 * npairs, 1))));
+  HIPCHK(c, hipMemcpyAsync(c->d_fill_ids.p, c->h_fill_ids.data(), size_t(nfill) * 4, hipMemcpyHostToDevice, c->stream));
+  if (npairs)
+    HIPCHK(c, hipMemcpyAsync(c->d_pairs.p, c->h_pairs.data(), size_t(npairs) * 8, hipMemcpyHostToDevice, c->stream));
+  b.fill_ids = c->d_fill_ids.p;
+  b.nfill = nfill;
   // K1
   if (s.N > 0) {
-    dim3 grid((s.N + 255) / 256, unsigned((n + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
+    dim3 grid((s.N + 255) / 256, unsigned((nfill + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
     uint32_t umask = 0;
     for (size_t i = 0; i < n; i++) umask |= c->h_evals.p[i].req_mask | c->h_evals.p[i].lead_mask;
     const int ucols = __builtin_popcount(umask);
@@ -453,12 +515,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int fanout = s.level_size[l + 1] / s.level_size[l];
     if (fanout >= 8) {  // wave per parent: coalesced child reads
       const int per_block = 4 * kParentsPerWave;
-      dim3 grid((s.level_size[l] + per_block - 1) / per_block, unsigned(n));
+      dim3 grid((s.level_size[l] + per_block - 1) / per_block, unsigned(nfill));
       hipLaunchKernelGGL(rollup_level_wave_kernel, grid, dim3(256), 0, c->stream, s, b, l);
     } else {
-      dim3 grid((s.level_size[l] + 255) / 256, unsigned(n));
+      dim3 grid((s.level_size[l] + 255) / 256, unsigned(nfill));
       hipLaunchKernelGGL(rollup_level_kernel, grid, dim3(256), 0, c->stream, s, b, l);
     }
+    HIPCHK(c, hipGetLastError());
+  }
+  if (npairs) {  // replicate phase-1 results to the duplicates
+    dim3 grid(unsigned(std::min<int64_t>((2 * int64_t(s.SD) / 4 + 255) / 256, 256)), unsigned(npairs));
+    hipLaunchKernelGGL(replicate_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_pairs.p, npairs);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));

@@ -109,6 +109,8 @@ struct DevBatch {
   int32_t list_cap;        // LDS sort capacity per wave
   LeafPartial* partials;   // [n][nblk]
   int32_t nblk;            // fill blocks per eval (partials per eval)
+  const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
+  int32_t nfill;
 };
 
 }  // namespace ktas

@@ -202,8 +202,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
   __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
 
   const int e0 = blockIdx.y * kEvalsPerBlock;
-  const int ne = min(kEvalsPerBlock, b.n - e0);
-  if (threadIdx.x < ne) sh_ev[threadIdx.x] = b.evals[e0 + threadIdx.x];
+  const int ne = min(kEvalsPerBlock, b.nfill - e0);
+  if (threadIdx.x < ne) sh_ev[threadIdx.x] = b.evals[b.fill_ids[e0 + threadIdx.x]];
   __syncthreads();
   for (int e = 0; e < ne; e++) {
     const DevEval& ev = sh_ev[e];
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 
   for (int e = 0; e < ne; e++) {
     const DevEval& ev = sh_ev[e];
-    const int eid = e0 + e;
+    const int eid = b.fill_ids[e0 + e];
     const DevTerm* wt = sh_terms[e];
     const DevTerm* lt = sh_terms[e] + MAXT;
     // wave-uniform copies (scalar registers: uniform branches below)
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 template <int NS>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
   const int e0 = blockIdx.y * kEvalsPerBlock;
-  const int ne = min(kEvalsPerBlock, b.n - e0);
+  const int ne = min(kEvalsPerBlock, b.nfill - e0);
   const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
   const int N = s.N;
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
 
   for (int e = 0; e < ne; e++) {
-    const int eid = e0 + e;
+    const int eid = uni(b.fill_ids[e0 + e]);
     const DevEval& ev = b.evals[eid];
     const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
     const uint32_t rmask = uint32_t(uni(int32_t(ev.req_mask)));
@@ -611,9 +611,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 // K2: fillInCountsHelper, one level (parents at `level`)
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b, int level) {
-  const int eid = blockIdx.y;
+  if (int(blockIdx.y) >= b.nfill) return;
+  const int eid = b.fill_ids[blockIdx.y];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (eid >= b.n || p >= s.level_size[level]) return;
+  if (p >= s.level_size[level]) return;
   const DevEval& ev = b.evals[eid];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   const int cl = level + 1;
@@ -671,8 +672,8 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
 // large (e.g. leaves -> racks).  kParentsPerWave parents per wave.
 constexpr int kParentsPerWave = 4;
 __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBatch b, int level) {
-  const int eid = blockIdx.y;
-  if (eid >= b.n) return;
+  if (int(blockIdx.y) >= b.nfill) return;
+  const int eid = b.fill_ids[blockIdx.y];
   const DevEval& ev = b.evals[eid];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   const int cl = level + 1;
@@ -739,6 +740,30 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
         base[4 * SD + g] = lead;
       }
     }
+  }
+}
+
+// Replicate phase-1 results (counters, leaf partials, exclusion stats) from a
+// representative eval to an eval with identical phase-1 inputs.
+__global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, const int32_t* pairs, int npairs) {
+  const int pi = blockIdx.y;
+  if (pi >= npairs) return;
+  const int src = pairs[2 * pi], dst = pairs[2 * pi + 1];
+  const bool leader = (b.evals[dst].flags & KUEUE_TAS_F_LEADER) != 0;
+  const int64_t words = int64_t(leader ? 5 : 2) * s.SD;  // SD is a multiple of 4
+  const int4* a = reinterpret_cast<const int4*>(b.counters + int64_t(src) * b.ctr_stride);
+  int4* d = reinterpret_cast<int4*>(b.counters + int64_t(dst) * b.ctr_stride);
+  const int64_t q = words / 4;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < q; i += int64_t(gridDim.x) * blockDim.x) d[i] = a[i];
+  if (blockIdx.x == 0) {
+    if (b.evals[dst].requested_level == s.L - 1)
+      for (int i = threadIdx.x; i < b.nblk; i += blockDim.x)
+        b.partials[int64_t(dst) * b.nblk + i] = b.partials[int64_t(src) * b.nblk + i];
+    for (int i = threadIdx.x; i < b.num_taints; i += blockDim.x)
+      b.taint_counts[int64_t(dst) * b.num_taints + i] = b.taint_counts[int64_t(src) * b.num_taints + i];
+    for (int i = threadIdx.x; i < s.R; i += blockDim.x)
+      b.res_counts[int64_t(dst) * s.R + i] = b.res_counts[int64_t(src) * s.R + i];
+    if (threadIdx.x == 0) b.sel_counts[dst] = b.sel_counts[src];
   }
 }
 
