@@ -127,8 +127,8 @@ struct kueue_tas_ctx {
   DevBuf<int64_t> d_offsets;
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
-  DevBuf<int32_t> d_fill_ids, d_pairs;
-  std::vector<int32_t> h_fill_ids, h_pairs;
+  DevBuf<int32_t> d_fill_ids, d_pairs, d_leafsel;
+  std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
   HostBuf<DevEval> h_evals;
@@ -206,6 +206,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_packed.release();
   c->d_partials.release();
   c->d_fill_ids.release();
+  c->d_leafsel.release();
   c->d_pairs.release();
   c->h_evals.release();
   c->h_terms.release();
@@ -452,12 +453,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     std::string key;
     for (size_t i = 0; i < n; i++) {
       const DevEval& e = c->h_evals.p[i];
-      const bool leafsel = e.requested_level == s.L - 1;
       key.clear();
       auto put = [&](const void* p, size_t len) { key.append(static_cast<const char*>(p), len); };
-      uint32_t f = e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY | (leafsel ? KUEUE_TAS_F_LFC : 0u));
+      uint32_t f = e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY);
       put(&f, 4);
-      int32_t hdr[4] = {leafsel ? 1 : 0, leafsel ? e.count : 0, e.slice_size, e.slice_level};
+      int32_t hdr[2] = {e.slice_size, e.slice_level};
       put(hdr, sizeof hdr);
       put(e.ssal, sizeof e.ssal);
       put(&e.nsel, 4);
@@ -526,6 +526,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   if (npairs) {  // replicate phase-1 results to the duplicates
     dim3 grid(unsigned(std::min<int64_t>((2 * int64_t(s.SD) / 4 + 255) / 256, 256)), unsigned(npairs));
     hipLaunchKernelGGL(replicate_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_pairs.p, npairs);
+    HIPCHK(c, hipGetLastError());
+  }
+  // leaf-level selection partials (evals whose requested level is the leaf level)
+  c->h_leafsel.clear();
+  for (size_t i = 0; i < n; i++)
+    if (c->h_evals.p[i].requested_level == s.L - 1) c->h_leafsel.push_back(int32_t(i));
+  if (!c->h_leafsel.empty() && s.N > 0) {
+    const int nl = int(c->h_leafsel.size());
+    HIPCHK(c, c->d_leafsel.ensure(size_t(nl)));
+    HIPCHK(c, hipMemcpyAsync(c->d_leafsel.p, c->h_leafsel.data(), size_t(nl) * 4, hipMemcpyHostToDevice, c->stream));
+    dim3 grid((s.N + 255) / 256, unsigned((nl + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
+    hipLaunchKernelGGL(leaf_partials_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_leafsel.p, nl);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));

@@ -338,41 +338,6 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         base[4 * SD + gleaf] = ls;
       }
     }
-    // Leaf-level selection partials (findLevelWithFitDomains at the leaf level).
-    if (ev.requested_level == s.L - 1) {
-      const bool lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
-      const int32_t sliceCount = go_div32(ev.count, ev.slice_size);
-      int32_t ss = 0, sswl = 0;
-      if (s.L - 1 == ev.slice_level) {
-        ss = go_div32(state, ev.slice_size);
-        sswl = go_div32(swl, ev.slice_size);
-      }
-      Key k = key_wl(lfc, ls, sswl, swl, leaf);
-      Key top = valid ? k : key_max();
-      Key inv = valid ? Key{~k.hi, ~k.lo} : key_max();
-      Key lf = (valid && ss >= sliceCount) ? k : key_max();
-      const int32_t st = leader ? sswl : ss;
-      uint32_t bst = (valid && st >= sliceCount) ? s_asc(st) : ~0u;
-      uint32_t mss = valid ? s_asc(ss) : ~0u;
-      top = wave_min_key(top);
-      inv = wave_min_key(inv);
-      lf = wave_min_key(lf);
-      bst = uint32_t(wave_min_u64(bst));
-      mss = uint32_t(wave_min_u64(mss));
-      Key bk = (valid && st >= sliceCount && s_asc(st) == bst) ? k : key_max();
-      bk = wave_min_key(bk);
-      if (lane == 0) {  // one partial per wave (64 leaves)
-        LeafPartial pt;
-        pt.top = top;
-        pt.last = Key{~inv.hi, ~inv.lo};
-        pt.lfcfit = lf;
-        pt.bfkey = bk;
-        pt.bfst = bst;
-        pt.minss = int32_t(mss ^ 0x80000000u);
-        pt.pad[0] = pt.pad[1] = 0;
-        b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
-      }
-    }
     // ExclusionStats (:1579-1634), aggregated per wave before the atomics.
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
@@ -557,35 +522,6 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         base[4 * SD + gleaf] = ls;
       }
     }
-    if (uni(ev.requested_level) == s.L - 1) {
-      const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
-      const int32_t sliceCount = go_div32(uni(ev.count), slice_size);
-      Key k = key_wl(lfc, ls, sswl, swl, leaf);
-      Key top = valid ? k : key_max();
-      Key inv = valid ? Key{~k.hi, ~k.lo} : key_max();
-      Key lf = (valid && ss >= sliceCount) ? k : key_max();
-      const int32_t st = leader ? sswl : ss;
-      uint32_t bst = (valid && st >= sliceCount) ? s_asc(st) : ~0u;
-      uint32_t mss = valid ? s_asc(ss) : ~0u;
-      top = wave_min_key(top);
-      inv = wave_min_key(inv);
-      lf = wave_min_key(lf);
-      bst = uint32_t(wave_min_u64(bst));
-      mss = uint32_t(wave_min_u64(mss));
-      Key bk = (valid && st >= sliceCount && s_asc(st) == bst) ? k : key_max();
-      bk = wave_min_key(bk);
-      if (lane == 0) {
-        LeafPartial pt;
-        pt.top = top;
-        pt.last = Key{~inv.hi, ~inv.lo};
-        pt.lfcfit = lf;
-        pt.bfkey = bk;
-        pt.bfst = bst;
-        pt.minss = int32_t(mss ^ 0x80000000u);
-        pt.pad[0] = pt.pad[1] = 0;
-        b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
-      }
-    }
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
     uint64_t tm = ballot(kind == EX_TAINT);
@@ -743,7 +679,68 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
   }
 }
 
-// Replicate phase-1 results (counters, leaf partials, exclusion stats) from a
+// Leaf-level selection partials for evals whose requested level is the leaf
+// level: per 64-leaf wave, the reductions findLevelWithFitDomains needs
+// (:1244-1270): first/last sortedDomainsWithLeader key, LFC first fit,
+// BestFit best fit and the minimum sliceState.  Reads the leaf counters.
+__global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, DevBatch b, const int32_t* ids,
+                                                                    int nids) {
+  const int e0 = blockIdx.y * kEvalsPerBlock;
+  const int ne = min(kEvalsPerBlock, nids - e0);
+  const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
+  const bool valid = leaf < s.N;
+  const int gleaf = s.level_off[s.L - 1] + leaf;
+  const int lane = lane_id();
+  const int64_t SD = s.SD;
+  for (int e = 0; e < ne; e++) {
+    const int eid = uni(ids[e0 + e]);
+    const DevEval& ev = b.evals[eid];
+    const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
+    const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
+    const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
+    const int32_t sliceCount = go_div32(uni(ev.count), uni(ev.slice_size));
+    const int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    int32_t state = 0, ss = 0, swl = 0, sswl = 0, ls = 0;
+    if (valid) {
+      state = base[gleaf];
+      ss = base[SD + gleaf];
+      swl = state;
+      sswl = ss;
+      if (leader) {
+        swl = base[2 * SD + gleaf];
+        sswl = base[3 * SD + gleaf];
+        ls = base[4 * SD + gleaf];
+      }
+    }
+    Key k = key_wl(lfc, ls, sswl, swl, leaf);
+    Key top = valid ? k : key_max();
+    Key inv = valid ? Key{~k.hi, ~k.lo} : key_max();
+    Key lf = (valid && ss >= sliceCount) ? k : key_max();
+    const int32_t st = leader ? sswl : ss;
+    uint32_t bst = (valid && st >= sliceCount) ? s_asc(st) : ~0u;
+    uint32_t mss = valid ? s_asc(ss) : ~0u;
+    top = wave_min_key(top);
+    inv = wave_min_key(inv);
+    lf = wave_min_key(lf);
+    bst = uint32_t(wave_min_u64(bst));
+    mss = uint32_t(wave_min_u64(mss));
+    Key bk = (valid && st >= sliceCount && s_asc(st) == bst) ? k : key_max();
+    bk = wave_min_key(bk);
+    if (lane == 0) {
+      LeafPartial pt;
+      pt.top = top;
+      pt.last = Key{~inv.hi, ~inv.lo};
+      pt.lfcfit = lf;
+      pt.bfkey = bk;
+      pt.bfst = bst;
+      pt.minss = int32_t(mss ^ 0x80000000u);
+      pt.pad[0] = pt.pad[1] = 0;
+      b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
+    }
+  }
+}
+
+// Replicate phase-1 results (counters, exclusion stats) from a
 // representative eval to an eval with identical phase-1 inputs.
 __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, const int32_t* pairs, int npairs) {
   const int pi = blockIdx.y;
@@ -756,9 +753,6 @@ __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, c
   const int64_t q = words / 4;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < q; i += int64_t(gridDim.x) * blockDim.x) d[i] = a[i];
   if (blockIdx.x == 0) {
-    if (b.evals[dst].requested_level == s.L - 1)
-      for (int i = threadIdx.x; i < b.nblk; i += blockDim.x)
-        b.partials[int64_t(dst) * b.nblk + i] = b.partials[int64_t(src) * b.nblk + i];
     for (int i = threadIdx.x; i < b.num_taints; i += blockDim.x)
       b.taint_counts[int64_t(dst) * b.num_taints + i] = b.taint_counts[int64_t(src) * b.num_taints + i];
     for (int i = threadIdx.x; i < s.R; i += blockDim.x)
