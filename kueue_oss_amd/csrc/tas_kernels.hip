@@ -110,6 +110,18 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
   for (int m = 32; m >= 1; m >>= 1) v += int64_t(shfl_xor_u64(uint64_t(v), m));
   return v;
 }
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = lane_id();
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl(x, max(lane - d, 0), 64);
+    if (lane >= d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
 __device__ __forceinline__ int32_t wave_sum_wrap32(int32_t v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = w_add(v, __shfl_xor(v, m, 64));
@@ -802,6 +814,12 @@ struct Wave {
     }
     ctr[int64_t(f) * SD + g] = v;
   }
+  // Stored by one lane for a domain only it handles in a lane-parallel pass;
+  // readers on other lanes come after a fence.
+  __device__ void set_lane(Field f, int g, int32_t v) {
+    if (!leader && (f == F_LS || f == F_SWL || f == F_SSWL)) return;
+    ctr[g + int64_t(f) * SD] = v;  // lane-private
+  }
   __device__ Key kplain(int g) const {
     int idx = g - s->level_off[level_of(g)];
     return key_plain(lfc, get(F_SLICE, g), get(F_STATE, g), idx);
@@ -1103,15 +1121,333 @@ __device__ bool update_counts(Wave& w, Seq& seq, int32_t count, int32_t leaderCo
   return false;
 }
 
+// ---- threshold walk: updateCountsToMinimumGeneric without leaders, no sort ----
+// Without leaders the walk (:1434-1468) takes the sorted list's elements in
+// order until the running sum of their weight w (sliceState with slices,
+// state without) reaches rem; the element at that crossing is replaced by
+// BestFit's best fit over the rest of the list (:1435, :1453), everything
+// before it is taken whole.  Every descent consumer of the result is
+// order-independent (lowerLevelDomains is re-sorted, per-parent walks are
+// independent, buildAssignment sorts), so only WHICH elements are taken and
+// their final counters matter.  With w >= 0 the crossing is found with
+// weighted histograms over the sort key's components (sliceState, then state,
+// then the domain index within one (sliceState, state) class) in a few
+// coalesced passes instead of an O(n log n) sort plus an O(k) dependent walk.
+
+// Decode the components of a key_plain key.
+__device__ __forceinline__ int32_t kp_ss(bool lfc, const Key& k) {
+  uint32_t k0 = uint32_t(k.hi >> 32);
+  return int32_t((lfc ? k0 : ~k0) ^ 0x80000000u);
+}
+__device__ __forceinline__ int32_t kp_st(const Key& k) { return int32_t(uint32_t(k.hi) ^ 0x80000000u); }
+
+// First position p (in scan order: bin i = p, or kBins-1-p when desc) whose
+// inclusive weighted sum reaches need.  Returns the bin (or -1: total < need,
+// *before = total) and the sum before it.
+constexpr int kThrBins = 256;
+__device__ int bins_threshold(const uint64_t* hist, bool desc, int64_t need, int64_t* before) {
+  const int lane = lane_id();
+  int64_t local[4];
+  int64_t lsum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int p = 4 * lane + k;
+    local[k] = int64_t(hist[desc ? kThrBins - 1 - p : p]);
+    lsum += local[k];
+  }
+  int64_t x = lsum;
+  for (int d = 1; d < 64; d <<= 1) {
+    int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane - d, 0)));
+    if (lane >= d) x += y;
+  }
+  const int64_t excl = x - lsum;
+  const uint64_t m = ballot(x >= need);
+  if (!m) {
+    *before = int64_t(shfl_u64(uint64_t(x), 63));
+    return -1;
+  }
+  const int src = __ffsll((unsigned long long)m) - 1;
+  int pp = -1;
+  int64_t bb = excl;
+  if (lane == src) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (pp < 0) {
+        if (bb + local[k] >= need) pp = 4 * lane + k;
+        else bb += local[k];
+      }
+    }
+  }
+  pp = __shfl(pp, src, 64);
+  *before = int64_t(shfl_u64(uint64_t(bb), src));
+  return desc ? kThrBins - 1 - pp : pp;
+}
+
+// Returns 1 (taken elements appended to out), 0 (Go returns nil: the list
+// cannot hold rem; mutations of a discarded list are unobservable) or -1
+// (preconditions unmet: caller sorts).  Keys are materialized in w.gkeys.
+__device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t sliceSize,
+                              bool slices, int32_t* out, int* np) {
+  if (w.cap * int(sizeof(Key)) < kThrBins * int(sizeof(uint64_t))) return -1;
+  const int loff = w.s->level_off[level];
+  const bool lfc = w.lfc;
+  const int32_t rem = slices ? go_div32(count, sliceSize) : count;
+  Key* keys = w.gkeys;
+  // pass A: keys, range of the primary component, minimum weight
+  int32_t vmin = 0x7fffffff, vmax = int32_t(0x80000000u), wmin = 0x7fffffff;
+  int64_t wsum = 0;
+  for (int i = w.lane; i < n; i += kWave) {
+    const int g = gids[i];
+    const int32_t ss = w.get(F_SLICE, g), st = w.get(F_STATE, g);
+    keys[i] = key_plain(lfc, ss, st, g - loff);
+    vmin = min(vmin, ss);
+    vmax = max(vmax, ss);
+    wmin = min(wmin, slices ? ss : st);
+    wsum += slices ? ss : st;
+  }
+  wsum = wave_sum_i64(wsum);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    vmin = min(vmin, __shfl_xor(vmin, m, 64));
+    vmax = max(vmax, __shfl_xor(vmax, m, 64));
+    wmin = min(wmin, __shfl_xor(wmin, m, 64));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  if (wmin < 0 || wsum >= (int64_t(1) << 31)) return -1;  // int32 rem arithmetic never wraps
+  uint64_t* hist = reinterpret_cast<uint64_t*>(w.lds);
+  Key ck;          // key of the crossing element
+  int32_t remc;    // rem left when the walk reaches it
+  if (rem <= 0) {  // the first element already satisfies rem
+    Key k = key_max();
+    for (int i = w.lane; i < n; i += kWave) k = key_min2(k, keys[i]);
+    ck = wave_min_key(k);
+    remc = rem;
+  } else {
+    if (int64_t(vmax) - int64_t(vmin) >= kThrBins) return -1;
+    // pass B: weight per sliceState value
+    for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = w.lane; i < n; i += kWave) {
+      const Key k = keys[i];
+      const int32_t ss = kp_ss(lfc, k);
+      const int32_t wt = slices ? ss : kp_st(k);
+      if (wt > 0) atomicAdd((unsigned long long*)&hist[ss - vmin], (unsigned long long)wt);
+    }
+    wave_sync();
+    int64_t before1;
+    const int b1 = bins_threshold(hist, !lfc, rem, &before1);
+    if (b1 < 0) return 0;  // the list cannot hold rem (:1469)
+    const int32_t t = vmin + b1;
+    const int64_t rem1 = rem - before1;
+    // pass C: state range inside class t
+    int32_t umin = 0x7fffffff, umax = int32_t(0x80000000u);
+    for (int i = w.lane; i < n; i += kWave) {
+      const Key k = keys[i];
+      if (kp_ss(lfc, k) == t) {
+        umin = min(umin, kp_st(k));
+        umax = max(umax, kp_st(k));
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      umin = min(umin, __shfl_xor(umin, m, 64));
+      umax = max(umax, __shfl_xor(umax, m, 64));
+    }
+    if (int64_t(umax) - int64_t(umin) >= kThrBins) return -1;
+    // pass D: weight per state value inside class t
+    wave_sync();
+    for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = w.lane; i < n; i += kWave) {
+      const Key k = keys[i];
+      if (kp_ss(lfc, k) == t) {
+        const int32_t wt = slices ? t : kp_st(k);
+        if (wt > 0) atomicAdd((unsigned long long*)&hist[kp_st(k) - umin], (unsigned long long)wt);
+      }
+    }
+    wave_sync();
+    int64_t before2;
+    const int b2 = bins_threshold(hist, false, rem1, &before2);
+    if (b2 < 0) return -1;  // unreachable: class t holds rem1
+    const int32_t u = umin + b2;
+    const int64_t rem2 = rem1 - before2;
+    const int64_t wt = slices ? t : u;  // > 0: the class added weight
+    const int64_t m = (rem2 + wt - 1) / wt;
+    remc = int32_t(rem2 - (m - 1) * wt);
+    // pass E: the m-th smallest index of class (t, u)
+    wave_sync();
+    int cnt = 0;
+    for (int i0 = 0; i0 < n; i0 += kWave) {
+      const int i = i0 + w.lane;
+      bool in = false;
+      Key k{0, 0};
+      if (i < n) {
+        k = keys[i];
+        in = kp_ss(lfc, k) == t && kp_st(k) == u;
+      }
+      int tot;
+      const int pos = cnt + wave_excl_scan(in ? 1 : 0, &tot);
+      if (in && pos < w.cap) w.lds[pos] = Key{0, k.lo};
+      cnt += tot;
+    }
+    if (cnt > w.cap) return -1;
+    wave_sync();
+    lds_sort(w.lds, cnt, w.lane);
+    ck = key_plain(lfc, t, u, int32_t(uint32_t(w.lds[m - 1].lo)));
+    wave_sync();
+  }
+  int chosen = loff + int(uint32_t(ck.lo));
+  if (w.bf) {  // findBestFitDomainBy over the crossing and everything after it (:1216-1231)
+    uint32_t bst = ~0u;
+    for (int i = w.lane; i < n; i += kWave) {
+      const Key k = keys[i];
+      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
+      if (key_le(ck, k) && wt >= remc) bst = min(bst, s_asc(wt));
+    }
+    bst = uint32_t(wave_min_u64(bst));
+    Key best = key_max();
+    for (int i = w.lane; i < n; i += kWave) {
+      const Key k = keys[i];
+      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
+      if (key_le(ck, k) && s_asc(wt) == bst) best = key_min2(best, k);
+    }
+    best = wave_min_key(best);
+    chosen = loff + int(uint32_t(best.lo));
+  }
+  // pass F: emit the whole elements before the crossing (lane-private stores)
+  int cnt = *np;
+  for (int i0 = 0; i0 < n; i0 += kWave) {
+    const int i = i0 + w.lane;
+    bool take = false;
+    Key k{0, 0};
+    if (i < n) {
+      k = keys[i];
+      take = key_lt(k, ck);
+    }
+    int tot;
+    const int pos = cnt + wave_excl_scan(take ? 1 : 0, &tot);
+    if (take) {
+      const int g = loff + int(uint32_t(k.lo));
+      if (slices) w.set_lane(F_STATE, g, w_mul(kp_ss(lfc, k), sliceSize));
+      w.set_lane(F_LS, g, 0);
+      if (pos < w.lcap) out[pos] = g;
+    }
+    cnt += tot;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  // the crossing element (or its best fit) takes the remainder
+  w.set(F_LS, chosen, 0);
+  if (slices) {
+    w.set(F_STATE, chosen, w_mul(remc, sliceSize));
+    w.set(F_SLICE, chosen, remc);
+  } else {
+    w.set(F_STATE, chosen, remc);
+  }
+  if (cnt < w.lcap) out[cnt] = chosen;
+  cnt++;
+  if (cnt > w.lcap) w.overflow = true;
+  *np = cnt;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  return 1;
+}
+
+// The same leaderless walk over a list already sorted in LDS: the crossing
+// is the first position whose inclusive weight sum reaches rem (the
+// walk's `w_i >= rem_i` test, :1444/:1459, is exactly S_i >= rem while no int32
+// arithmetic wraps), found with a wave scan; elements before it are emitted in
+// parallel.  Returns 1 / 0 (nil) / -1 (would wrap: caller walks).
+__device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t sliceSize, bool slices, int32_t* out,
+                               int* np) {
+  const bool lfc = w.lfc;
+  const int32_t rem = slices ? go_div32(count, sliceSize) : count;
+  int64_t absum = 0;
+  for (int i = w.lane; i < n; i += kWave) {
+    const Key k = w.lds[i];
+    const int64_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
+    absum += wt < 0 ? -wt : wt;
+  }
+  absum = wave_sum_i64(absum);
+  if (absum + (rem < 0 ? -int64_t(rem) : int64_t(rem)) >= (int64_t(1) << 31)) return -1;
+  int64_t run = 0;
+  int cross = -1;
+  int64_t before = 0;
+  for (int i0 = 0; i0 < n; i0 += kWave) {
+    const int i = i0 + w.lane;
+    int64_t wt = 0;
+    if (i < n) {
+      const Key k = w.lds[i];
+      wt = slices ? kp_ss(lfc, k) : kp_st(k);
+    }
+    int64_t x = wt;
+    for (int d = 1; d < 64; d <<= 1) {
+      int64_t y = int64_t(shfl_u64(uint64_t(x), max(w.lane - d, 0)));
+      if (w.lane >= d) x += y;
+    }
+    const uint64_t m = ballot(i < n && run + x >= rem);
+    if (m) {
+      const int src = __ffsll((unsigned long long)m) - 1;
+      cross = i0 + src;
+      before = run + int64_t(shfl_u64(uint64_t(x - wt), src));
+      break;
+    }
+    run += int64_t(shfl_u64(uint64_t(x), 63));
+  }
+  if (cross < 0) return 0;
+  const int32_t remc = int32_t(rem - before);
+  int pick = cross;
+  if (w.bf) {  // findBestFitDomainBy over [cross, n) (:1216-1231)
+    uint64_t best = ~0ull;
+    for (int i = cross + w.lane; i < n; i += kWave) {
+      const Key k = w.lds[i];
+      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
+      if (wt >= remc) best = min(best, (uint64_t(s_asc(wt)) << 32) | uint32_t(i));
+    }
+    pick = int(uint32_t(wave_min_u64(best)));
+  }
+  int cnt = *np;
+  for (int i = w.lane; i < cross; i += kWave) {
+    const Key k = w.lds[i];
+    const int g = loff + int(uint32_t(k.lo));
+    if (slices) w.set_lane(F_STATE, g, w_mul(kp_ss(lfc, k), sliceSize));
+    w.set_lane(F_LS, g, 0);
+    if (cnt + i < w.lcap) out[cnt + i] = g;
+  }
+  cnt += cross;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  const int chosen = loff + int(uint32_t(w.lds[pick].lo));
+  w.set(F_LS, chosen, 0);
+  if (slices) {
+    w.set(F_STATE, chosen, w_mul(remc, sliceSize));
+    w.set(F_SLICE, chosen, remc);
+  } else {
+    w.set(F_STATE, chosen, remc);
+  }
+  if (cnt < w.lcap) out[cnt] = chosen;
+  cnt++;
+  if (cnt > w.lcap) w.overflow = true;
+  *np = cnt;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  return 1;
+}
+
 // Walk an explicit list of gids of one level in the order given by `plain`
 // sortedDomains: LDS sort when it fits, lazy iteration otherwise.
 __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t leaderCount,
                             int32_t sliceSize, bool slices, int32_t sliceRecompute, int32_t* out, int* np) {
   const int loff = w.s->level_off[level];
+  // leaderless walks need no sequential pass (see threshold_walk)
+  const bool leaderless = !w.leader && leaderCount <= 0 && sliceRecompute <= 1;
   if (n <= w.cap) {
     for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain(gids[i]);
     wave_sync();
     lds_sort(w.lds, n, w.lane);
+    if (leaderless) {
+      const int r = lds_prefix_walk(w, n, loff, count, sliceSize, slices, out, np);
+      if (r >= 0) {
+        wave_sync();
+        return r == 1;
+      }
+    }
     if (sliceRecompute > 1) {  // multi-layer: recompute sliceState after sorting (:956-965)
       for (int i = 0; i < n; i++) {
         int g = loff + int(uint32_t(w.lds[i].lo));
@@ -1127,6 +1463,10 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   if (n > w.lcap) {
     w.overflow = true;
     return false;
+  }
+  if (leaderless) {
+    const int r = threshold_walk(w, gids, n, level, count, sliceSize, slices, out, np);
+    if (r >= 0) return r == 1;
   }
   // longer than the LDS: merge-sort the keys in global memory once (O(n log n)),
   // then walk them in order
@@ -1264,18 +1604,6 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
 }
 
 // Wave-wide exclusive prefix sum of per-lane counts.
-__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
-  const int lane = lane_id();
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl(x, max(lane - d, 0), 64);
-    if (lane >= d) x += y;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
-}
-
 // LeastFreeCapacity greedy over all leaves without leaders (the
 // findLevelWithFitDomains greedy :1278-1318 followed by
 // updateCountsToMinimumGeneric, LFC order) for n > LDS capacity: histogram

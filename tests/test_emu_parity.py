@@ -38,7 +38,7 @@ def test_emulated_kernels_match_goldens(emu_lib, list_cap):
     assert bad == []
 
 
-@pytest.mark.parametrize("seed,list_cap,max_nodes,n", [(11, 0, 60, 250), (12, 64, 60, 250), (13, 64, 400, 60)])
+@pytest.mark.parametrize("seed,list_cap,max_nodes,n", [(11, 0, 60, 250), (12, 64, 60, 250), (13, 64, 400, 60), (21, 128, 600, 60)])
 def test_emulated_kernels_match_oracle_random(emu_lib, seed, list_cap, max_nodes, n):
     rng = random.Random(seed)
     for i in range(n):
@@ -50,10 +50,12 @@ def test_emulated_kernels_match_oracle_random(emu_lib, seed, list_cap, max_nodes
         assert got == want, (i, got, want)
 
 
-def test_emulated_kernels_match_oracle_c3_small(emu_lib):
-    snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 4, 16, 32))
+@pytest.mark.parametrize("list_cap,n", [(64, 24), (128, 40)])
+def test_emulated_kernels_match_oracle_c3_small(emu_lib, list_cap, n):
+    # list_cap 128: descents longer than the LDS take the histogram threshold walk
+    snap_doc, wls = synth.config_c3(n_workloads=n, shape=(2, 4, 16, 32))
     want, _ = oracle_lib.eval_workloads(snap_doc, wls)
-    snap = TASFlavorSnapshot(snap_doc, list_cap=64, lib=emu_lib)
+    snap = TASFlavorSnapshot(snap_doc, list_cap=list_cap, lib=emu_lib)
     got = snap.find_topology_assignments_for_workloads(wls)
     snap.close()
     assert got == want
