@@ -40,15 +40,29 @@ def parse():
     return ap.parse_args()
 
 
-def fill_algorithmic_bytes(N, n_evals, n_leader, R_used, label_cols, evals_per_block=8):
+def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols):
     """Minimum HBM bytes of one fill launch: the SoA snapshot columns the
-    batch requests (free + used int64, presence words, taint profile, label
-    ids) once per launch, plus the per-eval leaf counters written
-    (state + sliceState int32; stateWithLeader, sliceStateWithLeader,
+    batch requests (free + used int64 per requested column, the two presence
+    words, taint profile, label ids) once per launch, plus the leaf counters
+    written for every eval whose phase 1 runs (one per distinct phase-1 input:
+    state + sliceState int32; stateWithLeader, sliceStateWithLeader,
     leaderState for leader evals)."""
     snap = N * (16 * R_used + 8 + 4 + 4 * label_cols)
-    writes = N * (8 * n_evals + 12 * n_leader)
+    writes = N * (8 * n_fill + 12 * n_leader)
     return snap + writes
+
+
+def load_traffic(path, config, n_fill):
+    """HBM bytes per fill launch from a committed PMC measurement of the same
+    workload (tools/pmc.sh -> profiles/), scaled per launch; None if absent."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config:
+        return None
+    return d.get("fill_bytes_per_launch")
 
 
 def main():
@@ -143,11 +157,15 @@ def main():
     value = placements / dt
 
     batches, evals, leader_evals = counts
-    per_launch_fill_ms = fill_ms / (a.steps * batches)
-    R_used = len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
+    st = snap.last_stats()
+    launches = max(st["fill_launches"], 1)
+    per_launch_fill_ms = fill_ms / (a.steps * launches)
+    R_used = st["staged_cols"] or len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
     label_cols = 1 if any(p.get("nodeSelector") for w in mine for p in w) else 0
-    fill_bytes = fill_algorithmic_bytes(N, evals / batches, leader_evals / batches, R_used, label_cols)
+    fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(leader_evals, st["fill_evals"]) / launches,
+                                        R_used, label_cols)
     achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
+    traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config, st["fill_evals"])
     stages = {"fill_ms": round(fill_ms / a.steps, 3), "rollup_ms": round(rollup_ms / a.steps, 3),
               "select_ms": round(select_ms / a.steps, 3), "device_ms": round(dev_ms / a.steps, 3)}
     if rank == 0:
@@ -170,9 +188,12 @@ def main():
                        "nodes": N, "batch_per_gpu": a.batch, "parallelism": f"dp{world} (replicated snapshot)"},
             "roofline": {"kernel": "fill_leaves_kernel", "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_launch": int(fill_bytes),
-                         "avg_launch_ms": round(per_launch_fill_ms, 4)},
+                         "traffic": traffic, "bytes_per_launch": int(fill_bytes),
+                         "avg_launch_ms": round(per_launch_fill_ms, 4),
+                         "per_launch": f"{N} leaves x {st['fill_evals'] // launches} phase-1 evals "
+                                       f"({evals // max(batches, 1)} evals, deduplicated), {R_used} columns"},
             "stages": stages,
+            "work": st,
             "cpu_baseline": cpu,
             "parity_sample_ok": parity,
             "setup_s": {"generate": round(gen_s, 2), "snapshot_load_and_compile": round(load_s, 2)},

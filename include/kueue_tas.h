@@ -189,8 +189,16 @@ int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, siz
 int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries_capacity);
 
 /* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
- * events on the ctx stream): [0] fill, [1] roll-up, [2] select/descend, [3] total. */
+ * events on the ctx stream): [0] the fill kernel alone, [1] roll-up +
+ * replication + leaf partials, [2] select/descend + entry offsets, [3] total
+ * from the request upload to the entry offsets. */
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
+
+/* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
+ * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
+ * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
+ * fill staged (0: generic kernel). */
+int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 
 /* ---- host layer (C++ mirror of the Go API, JSON-driven) ------------------ */
 typedef struct kueue_tas_host kueue_tas_host;
@@ -224,6 +232,10 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
 /* Per-workload compact results of the last run_compiled into buf (int32):
  * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
  * 4 int32 per workload (used for the cross-rank all-gather). */
+/* Work counters of the last find/run: [0] device batches, [1] evals,
+ * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
+int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
+
 int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n_workloads);
 
 void kueue_tas_free(char* p);

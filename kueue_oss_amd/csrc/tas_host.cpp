@@ -859,6 +859,7 @@ struct Evaluator {
   float ms[4] = {0, 0, 0, 0};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   int64_t counts[3] = {0, 0, 0};
+  int64_t stats[4] = {0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
@@ -887,6 +888,7 @@ struct Evaluator {
           bool precompiled = false) {
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     counts[0] = counts[1] = counts[2] = 0;
+    stats[0] = stats[1] = stats[2] = stats[3] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
     const double t_start = now_ms();
     results->resize(wls.size());
@@ -963,6 +965,10 @@ struct Evaluator {
       float t4[4];
       kueue_tas_last_timings(snap->ctx, t4);
       for (int k = 0; k < 4; k++) ms[k] += t4[k];
+      int64_t st4[4];
+      kueue_tas_last_stats(snap->ctx, st4);
+      for (int k = 0; k < 3; k++) stats[k] += st4[k];
+      stats[3] = std::max(stats[3], st4[3]);
       counts[0]++;
       counts[1] += int64_t(n);
       for (auto& q : reqs) counts[2] += (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
@@ -1062,6 +1068,7 @@ struct kueue_tas_host {
   std::vector<std::vector<PodSetResult>> last;
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
+  int64_t stats[4] = {0, 0, 0, 0};
 };
 
 extern "C" {
@@ -1183,6 +1190,7 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
   }
   memcpy(h->ms, ev.ms, sizeof h->ms);
   memcpy(h->counts, ev.counts, sizeof h->counts);
+  memcpy(h->stats, ev.stats, sizeof h->stats);
   if (result_hash) {
     uint64_t x = 1469598103934665603ull;
     auto mix = [&](uint64_t v) {
@@ -1216,6 +1224,16 @@ int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3)
   if (!h) return KUEUE_TAS_EINVAL;
   if (ms4) memcpy(ms4, h->ms, sizeof h->ms);
   if (counts3) memcpy(counts3, h->counts, sizeof h->counts);
+  return 0;
+}
+
+int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8) {
+  if (!h || !stats8) return KUEUE_TAS_EINVAL;
+  stats8[0] = h->counts[0];
+  stats8[1] = h->counts[1];
+  stats8[2] = h->counts[2];
+  for (int k = 0; k < 4; k++) stats8[3 + k] = h->stats[k];
+  stats8[7] = 0;
   return 0;
 }
 

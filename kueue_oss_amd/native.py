@@ -47,10 +47,10 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_host_last_profile", "kueue_tas_free",
+    "kueue_tas_host_last_records", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
 ]
 
 
@@ -94,6 +94,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
     lib.kueue_tas_free.argtypes = [c.c_void_p]
 
 
@@ -166,6 +167,14 @@ class TASFlavorSnapshot:
         cnt = (ctypes.c_int64 * 3)()
         self._lib.kueue_tas_host_last_timings(self._h, ms, cnt)
         return tuple(ms), tuple(cnt)
+
+    def last_stats(self):
+        """Work counters of the last run: dict(batches, evals, leader_evals,
+        fill_evals, leaf_partial_evals, fill_launches, staged_cols)."""
+        st = (ctypes.c_int64 * 8)()
+        self._lib.kueue_tas_host_last_stats(self._h, st)
+        keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols")
+        return dict(zip(keys, list(st)[:7]))
 
     def last_profile(self):
         """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""
