@@ -138,15 +138,15 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    fill_ms = rollup_ms = select_ms = dev_ms = 0.0
+    stage_sum = {}
+    host_sum = [0.0] * 4
     counts = None
     for _ in range(a.steps):
         step()
-        ms, counts = snap.last_timings()
-        fill_ms += ms[0]
-        rollup_ms += ms[1]
-        select_ms += ms[2]
-        dev_ms += ms[3]
+        _, counts = snap.last_timings()
+        for k, v in snap.last_stage_times().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+        host_sum = [x + y for x, y in zip(host_sum, snap.last_profile())]
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -159,15 +159,15 @@ def main():
     batches, evals, leader_evals = counts
     st = snap.last_stats()
     launches = max(st["fill_launches"], 1)
-    per_launch_fill_ms = fill_ms / (a.steps * launches)
+    per_launch_fill_ms = stage_sum["fill"] / (a.steps * launches)
     R_used = st["staged_cols"] or len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
     label_cols = 1 if any(p.get("nodeSelector") for w in mine for p in w) else 0
     fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(leader_evals, st["fill_evals"]) / launches,
                                         R_used, label_cols)
     achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
     traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config, st["fill_evals"])
-    stages = {"fill_ms": round(fill_ms / a.steps, 3), "rollup_ms": round(rollup_ms / a.steps, 3),
-              "select_ms": round(select_ms / a.steps, 3), "device_ms": round(dev_ms / a.steps, 3)}
+    stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}
+    host = dict(zip(("staging_ms", "eval_calls_ms", "decode_ms", "total_ms"), (round(x / a.steps, 3) for x in host_sum)))
     if rank == 0:
         line = {
             "metric": "TAS placements/sec at 128k nodes (1/2/4/8 GPU); % HBM roofline",
@@ -193,6 +193,7 @@ def main():
                          "per_launch": f"{N} leaves x {st['fill_evals'] // launches} phase-1 evals "
                                        f"({evals // max(batches, 1)} evals, deduplicated), {R_used} columns"},
             "stages": stages,
+            "host": host,
             "work": st,
             "cpu_baseline": cpu,
             "parity_sample_ok": parity,

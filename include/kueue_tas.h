@@ -194,6 +194,18 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries
  * from the request upload to the entry offsets. */
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 
+/* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
+ * events on the ctx stream, summed over its chunks): [0] fill, [1] roll-up
+ * (all levels), [2] phase-1 replication to duplicate evals, [3] leaf-level
+ * selection partials, [4] select/descend, [5] entry offsets, [6] total from
+ * the request upload to the entry offsets.  Copies min(n, 7) values. */
+#define KUEUE_TAS_NUM_STAGES 7
+int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
+
+/* Diagnostics: wall-clock time each eval of the last kueue_tas_eval_batch
+ * spent in the select kernel (100 MHz ticks), request order. */
+int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
+
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
  * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
@@ -226,6 +238,10 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
  * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
  * counts[1] = evaluations, counts[2] = evaluations with a leader. */
 int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
+/* kueue_tas_last_stage_times summed over the last run's batches. */
+int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n);
+/* kueue_tas_last_eval_ticks of the last device batch (diagnostics). */
+int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* Host wall time of the last run_compiled (ms): [0] request staging,
  * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);

@@ -100,7 +100,7 @@ void compute_magic(uint64_t d, DevTerm* t) {
 struct kueue_tas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
   std::string err;
   int list_cap = 1024;
   int max_batch = 1024;
@@ -129,6 +129,12 @@ struct kueue_tas_ctx {
   DevBuf<LeafPartial> d_partials;
   DevBuf<int32_t> d_fill_ids, d_pairs, d_leafsel;
   std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel;
+  // fast-LFC leaf tables (LfcJob, tas_internal.h)
+  DevBuf<int32_t> d_rep_of, d_lfc_slot, d_lfc_rep, d_fast;
+  DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
+  DevBuf<uint64_t> d_lfc_ovs, d_lfc_ovtot;
+  DevBuf<LfcJob> d_lfc_jobs;
+  std::vector<int32_t> h_rep_of, h_lfc_slot, h_lfc_rep, h_fast;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
   HostBuf<DevEval> h_evals;
@@ -136,8 +142,10 @@ struct kueue_tas_ctx {
   HostBuf<kueue_tas_eval_out> h_out;
   HostBuf<int64_t> h_offsets;
   HostBuf<int32_t> h_stats;
+  std::vector<int32_t> last_ticks;    // per-eval select time (100 MHz ticks) of the last batch
   std::vector<int32_t> last_entries;  // packed (leaf, count) pairs of the last batch
   float last_ms[4] = {0, 0, 0, 0};
+  float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
 };
 
@@ -209,6 +217,16 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_fill_ids.release();
   c->d_leafsel.release();
   c->d_pairs.release();
+  c->d_rep_of.release();
+  c->d_lfc_slot.release();
+  c->d_lfc_rep.release();
+  c->d_fast.release();
+  c->d_lfc_ch.release();
+  c->d_lfc_cp.release();
+  c->d_lfc_tot.release();
+  c->d_lfc_ovs.release();
+  c->d_lfc_ovtot.release();
+  c->d_lfc_jobs.release();
   c->h_evals.release();
   c->h_terms.release();
   c->h_out.release();
@@ -326,7 +344,7 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
 static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
                       kueue_tas_eval_out* out, int64_t* offsets, int32_t* taint_counts, int32_t* res_counts,
-                      float* ms) {
+                      float* ms, float* stage_ms) {
   const int32_t entry_cap = c->entry_cap;
   const DevSnap& s = c->snap;
   // ---- compile requests to device form (magic numbers) ----
@@ -445,12 +463,27 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
 
   // Phase-1 classes: evals with identical phase-1 inputs (request terms,
   // masks, overlay, slice parameters, partial parameters) get identical
-  // counters; phase 1 runs once per class and is replicated.
+  // counters; phase 1 runs once per class.  Fast-LFC members (LfcJob,
+  // tas_internal.h) read the class rep's counters in place (the rep is a
+  // fast-LFC member when the class has one, so its counters are never
+  // mutated); other duplicates get a replicated private copy.
   c->h_fill_ids.clear();
   c->h_pairs.clear();
+  c->h_rep_of.assign(n, 0);
+  c->h_lfc_slot.assign(n, -1);
+  c->h_lfc_rep.clear();
+  c->h_fast.clear();
+  int ncopy = 0;
   {
-    std::unordered_map<std::string, int32_t> rep;
-    rep.reserve(n * 2);
+    auto fast_lfc = [&](const DevEval& e) {
+      return (e.flags & KUEUE_TAS_F_LFC) != 0 &&
+             (e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_REQUIRED | KUEUE_TAS_F_MULTILAYER)) == 0 &&
+             e.requested_level == s.L - 1 && e.slice_level == s.L - 1 && e.slice_size == 1 && e.count >= 0 &&
+             s.N > 0;
+    };
+    std::unordered_map<std::string, int32_t> cls;
+    cls.reserve(n * 2);
+    std::vector<std::vector<int32_t>> members;
     std::string key;
     for (size_t i = 0; i < n; i++) {
       const DevEval& e = c->h_evals.p[i];
@@ -474,16 +507,71 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
         put(&t.val, 8);
       }
       for (int a = e.assumed_begin; a < e.assumed_end; a++) put(&assumed[a], sizeof(kueue_tas_assumed));
-      auto it = rep.find(key);
-      if (it == rep.end()) {
-        rep.emplace(key, int32_t(i));
-        c->h_fill_ids.push_back(int32_t(i));
+      auto it = cls.find(key);
+      if (it == cls.end()) {
+        cls.emplace(key, int32_t(members.size()));
+        members.push_back({int32_t(i)});
       } else {
-        c->h_pairs.push_back(it->second);
-        c->h_pairs.push_back(int32_t(i));
+        members[size_t(it->second)].push_back(int32_t(i));
       }
     }
+    std::vector<int32_t> stats_pairs;
+    for (const auto& mem : members) {
+      int32_t rep = mem[0];
+      for (int32_t m : mem)
+        if (fast_lfc(c->h_evals.p[m])) {
+          rep = m;
+          break;
+        }
+      c->h_fill_ids.push_back(rep);
+      const bool has_fast = fast_lfc(c->h_evals.p[rep]);
+      const int32_t slot = has_fast ? int32_t(c->h_lfc_rep.size()) : -1;
+      if (has_fast) c->h_lfc_rep.push_back(rep);
+      for (int32_t m : mem) {
+        const bool fast = has_fast && fast_lfc(c->h_evals.p[m]);
+        c->h_rep_of[size_t(m)] = fast ? rep : m;
+        c->h_lfc_slot[size_t(m)] = fast ? slot : -1;
+        if (fast) c->h_fast.push_back(m);
+        if (m != rep) {
+          auto& dst = fast ? stats_pairs : c->h_pairs;
+          dst.push_back(rep);
+          dst.push_back(fast ? ~m : m);  // ~m: exclusion stats only
+        }
+      }
+    }
+    ncopy = int(c->h_pairs.size() / 2);  // pairs [0, ncopy) copy counters, the rest stats only
+    c->h_pairs.insert(c->h_pairs.end(), stats_pairs.begin(), stats_pairs.end());
   }
+  const int nslots = int(c->h_lfc_rep.size());
+  const int nfast = int(c->h_fast.size());
+  const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
+  HIPCHK(c, c->d_rep_of.ensure(n));
+  HIPCHK(c, c->d_lfc_slot.ensure(n));
+  HIPCHK(c, c->d_lfc_jobs.ensure(n));
+  HIPCHK(c, c->d_lfc_rep.ensure(size_t(std::max(nslots, 1))));
+  HIPCHK(c, c->d_fast.ensure(size_t(std::max(nfast, 1))));
+  HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_cp.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_ovs.ensure(size_t(std::max(nslots * nchunks, 1))));
+  HIPCHK(c, c->d_lfc_ovtot.ensure(size_t(std::max(nslots, 1))));
+  HIPCHK(c, hipMemcpyAsync(c->d_rep_of.p, c->h_rep_of.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_lfc_slot.p, c->h_lfc_slot.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  if (nslots)
+    HIPCHK(c, hipMemcpyAsync(c->d_lfc_rep.p, c->h_lfc_rep.data(), size_t(nslots) * 4, hipMemcpyHostToDevice, c->stream));
+  if (nfast)
+    HIPCHK(c, hipMemcpyAsync(c->d_fast.p, c->h_fast.data(), size_t(nfast) * 4, hipMemcpyHostToDevice, c->stream));
+  b.rep_of = c->d_rep_of.p;
+  b.lfc_slot = c->d_lfc_slot.p;
+  b.lfc_rep = c->d_lfc_rep.p;
+  b.lfc_nslots = nslots;
+  b.lfc_nchunks = nchunks;
+  b.lfc_ch = c->d_lfc_ch.p;
+  b.lfc_cp = c->d_lfc_cp.p;
+  b.lfc_tot = c->d_lfc_tot.p;
+  b.lfc_ovs = c->d_lfc_ovs.p;
+  b.lfc_ovtot = c->d_lfc_ovtot.p;
+  b.lfc_jobs = c->d_lfc_jobs.p;
   const int nfill = int(c->h_fill_ids.size());
   const int npairs = int(c->h_pairs.size() / 2);
   c->stat_fills += nfill;
@@ -496,7 +584,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.fill_ids = c->d_fill_ids.p;
   b.nfill = nfill;
   // K1
-  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   c->last_stats[0] += nfill;
   if (s.N > 0) {
     dim3 grid((s.N + 255) / 256, unsigned((nfill + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
@@ -513,7 +601,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   // K2
   for (int l = s.L - 2; l >= 0; l--) {
     if (s.level_size[l] <= 0) continue;
@@ -528,15 +616,28 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
     HIPCHK(c, hipGetLastError());
   }
-  if (npairs) {  // replicate phase-1 results to the duplicates
-    dim3 grid(unsigned(std::min<int64_t>((2 * int64_t(s.SD) / 4 + 255) / 256, 256)), unsigned(npairs));
-    hipLaunchKernelGGL(replicate_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_pairs.p, npairs);
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  if (ncopy) {  // replicate phase-1 results to the duplicates
+    dim3 grid(unsigned(std::min<int64_t>((2 * int64_t(s.SD) / 4 + 255) / 256, 256)), unsigned(ncopy));
+    hipLaunchKernelGGL(replicate_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_pairs.p, ncopy);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (npairs > ncopy) {  // exclusion stats only (fast-LFC duplicates)
+    hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs - ncopy)), dim3(256), 0, c->stream, s, b,
+                       c->d_pairs.p + 2 * ncopy, npairs - ncopy);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  if (nslots) {  // fast-LFC leaf tables: chunk histograms, then per-bin chunk prefixes
+    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream, s, b);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream, b);
     HIPCHK(c, hipGetLastError());
   }
   // leaf-level selection partials (evals whose requested level is the leaf level)
   c->h_leafsel.clear();
   for (size_t i = 0; i < n; i++)
-    if (c->h_evals.p[i].requested_level == s.L - 1) c->h_leafsel.push_back(int32_t(i));
+    if (c->h_evals.p[i].requested_level == s.L - 1 && c->h_lfc_slot[i] < 0) c->h_leafsel.push_back(int32_t(i));
   if (!c->h_leafsel.empty() && s.N > 0) {
     const int nl = int(c->h_leafsel.size());
     c->last_stats[1] += nl;
@@ -546,7 +647,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(leaf_partials_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_leafsel.p, nl);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   // K3
   {
     const int waves = 4;
@@ -555,12 +656,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(select_kernel, grid, dim3(64 * waves), lds, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
+  if (nfast) {  // expand fast-LFC greedy results into entries
+    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(nchunks), unsigned(nfast)), dim3(256), 0, c->stream, s, b,
+                       c->d_fast.p);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   // pack the per-eval entries: offsets (scan) + compaction, then one D2H of exactly the used pairs
   HIPCHK(c, c->d_offsets.ensure(n + 1));
   hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_out.p, int(n), entry_cap,
                      c->d_offsets.p);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, c->h_out.ensure(n));
   HIPCHK(c, c->h_offsets.ensure(n + 1));
   HIPCHK(c, c->h_stats.ensure(stats_len));
@@ -584,18 +691,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
+  for (size_t i = 0; i < n; i++) c->last_ticks.push_back(c->h_out.p[i].reserved[0]);
   for (size_t i = 0; i <= n; i++) offsets[i] = c->h_offsets.p[i];
   if (taint_counts && nt) memcpy(taint_counts, c->h_stats.p, n * nt * 4);
   if (res_counts && s.R) memcpy(res_counts, c->h_stats.p + n * nt, n * size_t(s.R) * 4);
-  float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
-  (void)hipEventElapsedTime(&t01, c->ev[4], c->ev[1]);  // the fill kernel alone
-  (void)hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
-  (void)hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
-  ms[0] += t01;
-  ms[1] += t12;
-  ms[2] += t23;
-  ms[3] += t03;
+  float st[KUEUE_TAS_NUM_STAGES] = {};
+  for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&st[k], c->ev[k + 1], c->ev[k + 2]);
+  (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
+  for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
+  ms[0] += st[0];                  // the fill kernel alone
+  ms[1] += st[1] + st[2] + st[3];  // roll-up + replication + leaf partials
+  ms[2] += st[4] + st[5];          // select + entry offsets
+  ms[3] += st[6];
   return KUEUE_TAS_OK;
 }
 
@@ -607,7 +714,9 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
   HIPCHK(c, hipSetDevice(c->device));
   float ms[4] = {0, 0, 0, 0};
+  float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   c->last_entries.clear();
+  c->last_ticks.clear();
   for (auto& v : c->last_stats) v = 0;
   const size_t chunk = size_t(c->max_batch);
   std::vector<int64_t> off;
@@ -619,9 +728,10 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
       size_t keep = c->last_entries.size();
       int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
                           off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
-                          res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms);
+                          res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
         c->last_entries.resize(keep);
+        c->last_ticks.resize(i0);
         int32_t need = 0;
         for (size_t i = 0; i < m; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
         int cap = c->entry_cap;
@@ -636,6 +746,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
     for (size_t i = 1; i <= m; i++) entry_offsets[i0 + i] = base + off[i];
   }
   memcpy(c->last_ms, ms, sizeof ms);
+  memcpy(c->last_stage_ms, stage_ms, sizeof stage_ms);
   const size_t total = c->last_entries.size() / 2;
   if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
   if (total) memcpy(entries, c->last_entries.data(), total * 8);
@@ -653,6 +764,18 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_c
 int kueue_tas_last_timings(kueue_tas_ctx* c, float* ms4) {
   if (!c || !ms4) return KUEUE_TAS_EINVAL;
   memcpy(ms4, c->last_ms, sizeof c->last_ms);
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_stage_times(kueue_tas_ctx* c, float* ms, int n) {
+  if (!c || !ms || n < 0) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < KUEUE_TAS_NUM_STAGES; k++) ms[k] = c->last_stage_ms[k];
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_eval_ticks(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
+  if (!c || !ticks) return KUEUE_TAS_EINVAL;
+  for (size_t i = 0; i < n; i++) ticks[i] = i < c->last_ticks.size() ? c->last_ticks[i] : 0;
   return KUEUE_TAS_OK;
 }
 

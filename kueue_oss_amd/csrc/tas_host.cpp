@@ -857,6 +857,7 @@ static double now_ms() {
 struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
+  float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[4] = {0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches
@@ -887,6 +888,7 @@ struct Evaluator {
   int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results,
           bool precompiled = false) {
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
+    for (auto& v : stage_ms) v = 0;
     counts[0] = counts[1] = counts[2] = 0;
     stats[0] = stats[1] = stats[2] = stats[3] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
@@ -965,6 +967,9 @@ struct Evaluator {
       float t4[4];
       kueue_tas_last_timings(snap->ctx, t4);
       for (int k = 0; k < 4; k++) ms[k] += t4[k];
+      float st[KUEUE_TAS_NUM_STAGES];
+      kueue_tas_last_stage_times(snap->ctx, st, KUEUE_TAS_NUM_STAGES);
+      for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
       int64_t st4[4];
       kueue_tas_last_stats(snap->ctx, st4);
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
@@ -1212,6 +1217,17 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
     *result_hash = x;
   }
   return 0;
+}
+
+int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n) {
+  if (!h || !h->ev || !ms || n < 0) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < KUEUE_TAS_NUM_STAGES; k++) ms[k] = h->ev->stage_ms[k];
+  return 0;
+}
+
+int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n) {
+  if (!h || !h->snap) return KUEUE_TAS_EINVAL;
+  return kueue_tas_last_eval_ticks(h->snap->ctx, ticks, n);
 }
 
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4) {

@@ -88,6 +88,22 @@ struct LeafPartial {
   int32_t pad[2];
 };
 
+// LeastFreeCapacity leaf tables (one per phase-1 class that has "fast LFC"
+// evals: unconstrained, TASProfileMixed, no leader, slice size 1 at the leaf
+// level, requested level = leaves).  For those evals sliceState == state at
+// the leaves and the sortedDomains order (:1544-1564, LFC) is (value asc,
+// leaf index asc), so findLevelWithFitDomains + updateCountsToMinimumGeneric
+// reduce to bin counts: chunk histograms of the leaf values.
+constexpr int kLfcBins = 128;    // values 0..126 exact; bin 127 counts values >= 127
+constexpr int kLfcChunk = 2048;  // leaves per histogram chunk
+
+// Phase-2 result of a fast-LFC greedy eval that the emit kernel expands:
+// every leaf with 0 < value < t, then the first m leaves with value t (index
+// order), the m-th of which gets rem_last.  t == 0: nothing to expand.
+struct LfcJob {
+  int32_t t, m, rem_last, pad;
+};
+
 // Per-batch device buffers.
 struct DevBatch {
   const DevEval* evals;
@@ -111,6 +127,17 @@ struct DevBatch {
   int32_t nblk;            // fill blocks per eval (partials per eval)
   const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
   int32_t nfill;
+  const int32_t* rep_of;   // [n] eval whose counters select reads (itself, or the class rep for fast LFC)
+  const int32_t* lfc_slot; // [n] fast-LFC table slot, -1 if the eval is not fast LFC
+  const int32_t* lfc_rep;  // [lfc_nslots] eval whose leaf counters the table summarizes
+  int32_t lfc_nslots;
+  int32_t lfc_nchunks;
+  uint32_t* lfc_ch;        // [nslots][nchunks][kLfcBins] per-chunk value counts
+  uint32_t* lfc_cp;        // [nslots][nchunks][kLfcBins] exclusive prefix over chunks
+  uint32_t* lfc_tot;       // [nslots][kLfcBins]
+  uint64_t* lfc_ovs;       // [nslots][nchunks] sum of the values >= kLfcBins - 1
+  uint64_t* lfc_ovtot;     // [nslots]
+  LfcJob* lfc_jobs;        // [n]
 };
 
 }  // namespace ktas

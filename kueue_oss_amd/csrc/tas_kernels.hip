@@ -757,9 +757,11 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
 __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, const int32_t* pairs, int npairs) {
   const int pi = blockIdx.y;
   if (pi >= npairs) return;
-  const int src = pairs[2 * pi], dst = pairs[2 * pi + 1];
+  const int src = pairs[2 * pi], dst_raw = pairs[2 * pi + 1];
+  const bool stats_only = dst_raw < 0;  // fast-LFC duplicates read the rep's counters in place
+  const int dst = stats_only ? ~dst_raw : dst_raw;
   const bool leader = (b.evals[dst].flags & KUEUE_TAS_F_LEADER) != 0;
-  const int64_t words = int64_t(leader ? 5 : 2) * s.SD;  // SD is a multiple of 4
+  const int64_t words = stats_only ? 0 : int64_t(leader ? 5 : 2) * s.SD;  // SD is a multiple of 4
   const int4* a = reinterpret_cast<const int4*>(b.counters + int64_t(src) * b.ctr_stride);
   int4* d = reinterpret_cast<int4*>(b.counters + int64_t(dst) * b.ctr_stride);
   const int64_t q = words / 4;
@@ -770,6 +772,57 @@ __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, c
     for (int i = threadIdx.x; i < s.R; i += blockDim.x)
       b.res_counts[int64_t(dst) * s.R + i] = b.res_counts[int64_t(src) * s.R + i];
     if (threadIdx.x == 0) b.sel_counts[dst] = b.sel_counts[src];
+  }
+}
+
+
+// ----------------------------------------------------------------------------
+// LeastFreeCapacity leaf tables (see LfcJob in tas_internal.h)
+// ----------------------------------------------------------------------------
+// Per (class slot, chunk of kLfcChunk leaves): counts of each leaf value
+// (sliceState == state for fast-LFC classes) and the sum of the values that
+// land in the overflow bin.
+__global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
+  __shared__ uint32_t h[kLfcBins];
+  __shared__ unsigned long long ovs;
+  const int slot = blockIdx.y, chunk = blockIdx.x;
+  for (int i = threadIdx.x; i < kLfcBins; i += blockDim.x) h[i] = 0;
+  if (threadIdx.x == 0) ovs = 0;
+  __syncthreads();
+  const int32_t* v = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
+  const int lo = chunk * kLfcChunk, hi = min(s.N, lo + kLfcChunk);
+  uint64_t mysum = 0;
+  for (int i = lo + int(threadIdx.x); i < hi; i += blockDim.x) {
+    const int32_t x = v[i];
+    if (x >= kLfcBins - 1 || x < 0) {  // x < 0 cannot occur at a leaf (CountIn clamps at 0)
+      atomicAdd(&h[kLfcBins - 1], 1u);
+      mysum += uint64_t(int64_t(x));
+    } else {
+      atomicAdd(&h[x], 1u);
+    }
+  }
+  mysum = uint64_t(wave_sum_i64(int64_t(mysum)));
+  if (lane_id() == 0 && mysum) atomicAdd(&ovs, (unsigned long long)mysum);
+  __syncthreads();
+  uint32_t* out = b.lfc_ch + (int64_t(slot) * b.lfc_nchunks + chunk) * kLfcBins;
+  for (int i = threadIdx.x; i < kLfcBins; i += blockDim.x) out[i] = h[i];
+  if (threadIdx.x == 0) b.lfc_ovs[int64_t(slot) * b.lfc_nchunks + chunk] = ovs;
+}
+
+// Per slot: exclusive prefix of every bin over the chunks, totals, overflow sum.
+__global__ __launch_bounds__(kLfcBins) void lfc_total_kernel(DevBatch b) {
+  const int slot = blockIdx.x, bin = threadIdx.x;
+  const int64_t base = int64_t(slot) * b.lfc_nchunks;
+  uint32_t acc = 0;
+  for (int c = 0; c < b.lfc_nchunks; c++) {
+    b.lfc_cp[(base + c) * kLfcBins + bin] = acc;
+    acc += b.lfc_ch[(base + c) * kLfcBins + bin];
+  }
+  b.lfc_tot[int64_t(slot) * kLfcBins + bin] = acc;
+  if (bin == 0) {
+    uint64_t o = 0;
+    for (int c = 0; c < b.lfc_nchunks; c++) o += b.lfc_ovs[base + c];
+    b.lfc_ovtot[slot] = o;
   }
 }
 
@@ -1770,6 +1823,214 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   return 1;
 }
 
+// ---- fast LeastFreeCapacity leaf path (LfcJob, tas_internal.h) ----
+// For an unconstrained eval under TASProfileMixed without leader, with slice
+// size 1 at the leaf level, findLevelWithFitDomains (:1236-1318) at the leaf
+// level sorts leaves by (value asc, index asc) (sortedDomainsWithLeader /
+// sortedDomains, LFC; value = sliceState = state).  Then:
+//  * first fit (:1260-1265): the smallest value >= sliceCount, smallest index;
+//    updateCountsToMinimumGeneric gives it state = count;
+//  * otherwise the greedy (:1278-1318) takes leaves in that order until the
+//    value mass reaches sliceCount: all leaves below a threshold value t and
+//    the first m leaves of value t, the last one getting the remainder
+//    (updateCountsToMinimumGeneric, slices, :1437-1450); zero-value leaves
+//    end with state 0 and are dropped by buildAssignment (:1476-1480).
+// Both only need the class's value histogram (lfc_total_kernel); the greedy
+// output is expanded by lfc_emit_kernel.  Reads the class rep's counters in
+// place and never writes counters, so evals of one class share them.
+
+// Smallest leaf index whose value is v (tot[v] > 0): first chunk with a count, then a scan of it.
+__device__ int lfc_first_leaf(const Wave& w, const DevBatch& b, int slot, const int32_t* V, int v) {
+  const uint32_t* ch = b.lfc_ch + int64_t(slot) * b.lfc_nchunks * kLfcBins;
+  int chunk = -1;
+  for (int c0 = 0; c0 < b.lfc_nchunks && chunk < 0; c0 += kWave) {
+    const int c = c0 + w.lane;
+    const uint64_t m = ballot(c < b.lfc_nchunks && ch[int64_t(c) * kLfcBins + v] > 0);
+    if (m) chunk = c0 + __ffsll((unsigned long long)m) - 1;
+  }
+  if (chunk < 0) return -1;
+  const int lo = chunk * kLfcChunk, hi = min(w.s->N, lo + kLfcChunk);
+  for (int i0 = lo; i0 < hi; i0 += kWave) {
+    const int i = i0 + w.lane;
+    const uint64_t m = ballot(i < hi && V[i] == v);
+    if (m) return i0 + __ffsll((unsigned long long)m) - 1;
+  }
+  return -1;
+}
+
+// Greedy whose threshold lies among the overflow values (>= kLfcBins - 1):
+// exact single-wave version (value windows over all leaves, then emission in
+// index order).  Rare: leaf values that large need tiny requests.
+__device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before, int64_t below,
+                         kueue_tas_eval_out& o, int32_t* ent, int ecap) {
+  const DevSnap& s = *w.s;
+  const int N = s.N;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B
+  constexpr int kW = 256;
+  int32_t lo = kLfcBins - 1;
+  int32_t t = -1;
+  for (;;) {
+    // skip the gap to the next present value
+    int32_t vmin = 0x7fffffff;
+    for (int i = w.lane; i < N; i += kWave) {
+      const int32_t x = V[i];
+      if (x >= lo && x < vmin) vmin = x;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) vmin = min(vmin, __shfl_xor(vmin, m, 64));
+    if (vmin == 0x7fffffff) break;
+    lo = vmin;
+    for (int i = w.lane; i < kW; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = w.lane; i < N; i += kWave) {
+      const int32_t x = V[i];
+      if (x >= lo && int64_t(x) < int64_t(lo) + kW) atomicAdd(&hist[x - lo], 1u);
+    }
+    wave_sync();
+    int64_t acc = before, cnt = below;
+    for (int k = 0; k < kW; k++) {  // wave-uniform walk over the window
+      const uint32_t c = hist[k];
+      if (!c) continue;
+      const int64_t v = int64_t(lo) + k;
+      if (acc + v * int64_t(c) >= need) {
+        t = int32_t(v);
+        break;
+      }
+      acc += v * int64_t(c);
+      cnt += c;
+    }
+    before = acc;
+    below = cnt;
+    wave_sync();
+    if (t >= 0 || int64_t(lo) + kW > 0x7fffffffLL) break;
+    lo += kW;
+  }
+  if (t < 0) {  // cannot happen (the caller checked the total); keep the reference's failure shape
+    not_fit(w, s.L - 1, int32_t(before), need, o);
+    return;
+  }
+  const int64_t mt = (int64_t(need) - before + t - 1) / t;
+  const int32_t rem_last = int32_t(int64_t(need) - before - (mt - 1) * t);
+  int64_t seen = 0;
+  int cnt = 0;
+  for (int i0 = 0; i0 < N; i0 += kWave) {
+    const int i = i0 + w.lane;
+    const int32_t x = i < N ? V[i] : 0;
+    const bool tie = i < N && x == t;
+    const uint64_t tm = ballot(tie);
+    const int64_t r = seen + __popcll(tm & ((1ull << w.lane) - 1ull));
+    const bool keep = (x > 0 && x < t) || (tie && r < mt);
+    const uint64_t km = ballot(keep);
+    if (keep) {
+      const int pos = cnt + __popcll(km & ((1ull << w.lane) - 1ull));
+      if (pos < ecap) {
+        ent[2 * pos] = i;
+        ent[2 * pos + 1] = (tie && r == mt - 1) ? rem_last : x;
+      }
+    }
+    cnt += __popcll(km);
+    seen += __popcll(tm);
+  }
+  wave_sync();
+  o.status = KUEUE_TAS_ST_OK;
+  o.fit_level = s.L - 1;
+  o.num_workers = cnt;
+  if (cnt > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
+}
+
+__device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_out& o, int32_t* ent, int ecap) {
+  const DevSnap& s = *w.s;
+  const int L1 = s.L - 1;
+  const int lane = w.lane;
+  const int32_t* V = w.ctr + w.SD + s.level_off[L1];
+  const int32_t need = w.ev->count;  // sliceCount = count / 1 (host: count >= 0)
+  const uint32_t* tot = b.lfc_tot + int64_t(slot) * kLfcBins;
+  LfcJob job{0, 0, 0, 0};
+  static_assert(kLfcBins == 128, "two bins per lane");
+  const uint32_t h0 = tot[lane], h1 = tot[lane + 64];
+  const uint32_t nover = __shfl(h1, 63, 64);
+  // LFC first fit (:1260-1265)
+  int fit_leaf = -1;
+  if (need <= kLfcBins - 2) {
+    const uint64_t m0 = ballot(lane >= need && h0 > 0);
+    const uint64_t m1 = ballot(lane + 64 >= need && lane + 64 < kLfcBins - 1 && h1 > 0);
+    const int v = m0 ? __ffsll((unsigned long long)m0) - 1 : (m1 ? 64 + __ffsll((unsigned long long)m1) - 1 : -1);
+    if (v >= 0) fit_leaf = lfc_first_leaf(w, b, slot, V, v);
+  }
+  if (fit_leaf < 0 && nover > 0) {  // the fit is among the overflow values: min (value, index) scan
+    const int32_t lo = max(need, int32_t(kLfcBins - 1));
+    uint64_t best = ~0ull;
+    for (int i = lane; i < s.N; i += kWave) {
+      const int32_t x = V[i];
+      if (x >= lo) {
+        const uint64_t k = (uint64_t(uint32_t(x)) << 32) | uint32_t(i);
+        best = k < best ? k : best;
+      }
+    }
+    best = wave_min_u64(best);
+    if (best != ~0ull) fit_leaf = int(uint32_t(best));
+  }
+  if (fit_leaf >= 0) {
+    o.status = KUEUE_TAS_ST_OK;
+    o.fit_level = L1;
+    if (need != 0) {
+      if (lane == 0 && ecap > 0) {
+        ent[0] = fit_leaf;
+        ent[1] = need;
+      }
+      o.num_workers = 1;
+    }
+    return job;
+  }
+  // greedy (:1278-1318): value mass over bins 1..126, lane owns bins 2*lane, 2*lane+1
+  const int b0 = 2 * lane, b1 = 2 * lane + 1;
+  const int64_t c0 = (b0 >= 1 && b0 <= kLfcBins - 2) ? int64_t(tot[b0]) : 0;
+  const int64_t c1 = (b1 <= kLfcBins - 2) ? int64_t(tot[b1]) : 0;
+  const int64_t l0 = c0 * b0, l1 = c1 * b1;
+  int64_t x = l0 + l1, y = c0 + c1;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t xs = int64_t(shfl_u64(uint64_t(x), max(lane - d, 0)));
+    const int64_t ys = int64_t(shfl_u64(uint64_t(y), max(lane - d, 0)));
+    if (lane >= d) {
+      x += xs;
+      y += ys;
+    }
+  }
+  const uint64_t hit = ballot(x >= need);
+  if (hit) {
+    const int src = __ffsll((unsigned long long)hit) - 1;
+    const int64_t ex = x - (l0 + l1), ey = y - (c0 + c1);
+    int64_t before = ex, below = ey;
+    int t = b0;
+    if (ex + l0 < need) {
+      t = b1;
+      before = ex + l0;
+      below = ey + c0;
+    }
+    t = __shfl(t, src, 64);
+    before = int64_t(shfl_u64(uint64_t(before), src));
+    below = int64_t(shfl_u64(uint64_t(below), src));
+    const int64_t mt = (int64_t(need) - before + t - 1) / t;
+    job.t = t;
+    job.m = int32_t(mt);
+    job.rem_last = int32_t(int64_t(need) - before - (mt - 1) * t);
+    o.status = KUEUE_TAS_ST_OK;
+    o.fit_level = L1;
+    o.num_workers = int32_t(below + mt);
+    if (o.num_workers > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
+    return job;
+  }
+  const int64_t bins_mass = int64_t(shfl_u64(uint64_t(x), 63));
+  const int64_t bins_cnt = int64_t(shfl_u64(uint64_t(y), 63));
+  const int64_t total = bins_mass + int64_t(b.lfc_ovtot[slot]);
+  if (total < need) {  // not enough capacity: remaining = need - total (:1315-1316)
+    not_fit(w, L1, int32_t(total), need, o);
+    return job;
+  }
+  lfc_wide(w, need, V, bins_mass, bins_cnt, o, ent, ecap);
+  return job;
+}
+
 // findLevelWithFitDomains (:1236-1321).  Returns: 0 ok (results in listA,
 // *nres), 1 failure (o filled), 2 finished by the LFC fast path (o filled).
 __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, kueue_tas_eval_out& o, int32_t* ent,
@@ -2051,6 +2312,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   const int lane = lane_id();
   const int eid = blockIdx.x * (blockDim.x >> 6) + wave;
   if (eid >= b.n) return;
+  const uint64_t t_begin = wall_clock64();
   const DevEval& ev = b.evals[eid];
   Wave w;
   w.s = &s;
@@ -2061,7 +2323,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
   w.bf = !w.lfc;
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
-  w.ctr = b.counters + int64_t(eid) * b.ctr_stride;
+  w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
   w.SD = s.SD;
   w.lds = lds_all + int64_t(wave) * b.list_cap;
   w.cap = b.list_cap;
@@ -2094,7 +2356,15 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   o.reserved[0] = o.reserved[1] = 0;
 
   int nres = 0, fitLevel = 0;
-  int r = find_level(w, w.listA, &nres, &fitLevel, o, ent, ecap);
+  int r;
+  const int lslot = b.lfc_slot[eid];
+  if (lslot >= 0) {
+    const LfcJob job = lfc_fast(w, b, lslot, o, ent, ecap);
+    if (lane == 0) b.lfc_jobs[eid] = job;
+    r = 2;
+  } else {
+    r = find_level(w, w.listA, &nres, &fitLevel, o, ent, ecap);
+  }
   if (r == 0) {
     const int L = s.L;
     const int32_t leaderCount = w.leader ? 1 : 0;
@@ -2161,7 +2431,87 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
     if (o.num_workers + o.num_leaders > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
   }
   if (w.overflow) o.status = KUEUE_TAS_ST_INTERNAL;
+  o.reserved[0] = int32_t(wall_clock64() - t_begin);  // diagnostics: 100 MHz ticks in select
   if (lane == 0) b.out[eid] = o;
+}
+
+// Expand fast-LFC greedy results (LfcJob) into (leaf, count) entries in leaf
+// index order.  Grid (chunks, fast evals), one kLfcChunk-leaf chunk per block;
+// the chunk's output offset and tie ranks come from the chunk prefix counts.
+__global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b, const int32_t* fast_ids) {
+  __shared__ int64_t sh_base, sh_nkeep, sh_tie0;
+  __shared__ int32_t sh_wt[4], sh_wk[4];
+  const int eid = fast_ids[blockIdx.y];
+  const LfcJob job = b.lfc_jobs[eid];
+  if (job.t <= 0) return;
+  const int slot = b.lfc_slot[eid];
+  const int chunk = blockIdx.x;
+  const int t = job.t;
+  const int64_t mt = job.m;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  if (wv == 0) {
+    const int64_t off = (int64_t(slot) * b.lfc_nchunks + chunk) * kLfcBins;
+    int64_t a = 0, c = 0;
+    for (int v = 1 + lane; v < t; v += kWave) {
+      a += b.lfc_cp[off + v];
+      c += b.lfc_ch[off + v];
+    }
+    a = wave_sum_i64(a);
+    c = wave_sum_i64(c);
+    if (lane == 0) {
+      const int64_t tb = b.lfc_cp[off + t], tin = b.lfc_ch[off + t];
+      int64_t take = mt - tb;
+      take = take < 0 ? 0 : (take > tin ? tin : take);
+      sh_base = a + (tb < mt ? tb : mt);
+      sh_nkeep = c + take;
+      sh_tie0 = tb;
+    }
+  }
+  __syncthreads();
+  if (sh_nkeep == 0) return;
+  const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
+  const int lo = chunk * kLfcChunk + int(threadIdx.x) * 8;
+  int32_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? V[lo + k] : 0;
+  int nt = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) nt += x[k] == t ? 1 : 0;
+  int wt_total;
+  const int tex = wave_excl_scan(nt, &wt_total);
+  if (lane == 0) sh_wt[wv] = wt_total;
+  __syncthreads();
+  int64_t r = sh_tie0 + tex;
+  for (int k = 0; k < wv; k++) r += sh_wt[k];
+  bool keep[8];
+  int nk = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const bool tie = x[k] == t;
+    keep[k] = (x[k] > 0 && x[k] < t) || (tie && r < mt);
+    if (tie) {
+      if (r == mt - 1) x[k] = job.rem_last;
+      r++;
+    }
+    nk += keep[k] ? 1 : 0;
+  }
+  int wk_total;
+  const int kex = wave_excl_scan(nk, &wk_total);
+  if (lane == 0) sh_wk[wv] = wk_total;
+  __syncthreads();
+  int64_t pos = sh_base + kex;
+  for (int k = 0; k < wv; k++) pos += sh_wk[k];
+  int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (keep[k]) {
+      if (pos < b.entry_cap) {
+        ent[2 * pos] = lo + k;
+        ent[2 * pos + 1] = x[k];
+      }
+      pos++;
+    }
+  }
 }
 
 // Packed result entries: offsets[i] = sum_{j<i} min(count_j, cap) (single block).

@@ -47,10 +47,10 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
+    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
 ]
 
 
@@ -93,6 +93,8 @@ def _bind(lib):
     lib.kueue_tas_host_run_compiled.restype = c.c_int
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
+    lib.kueue_tas_host_last_stage_times.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int]
+    lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
     lib.kueue_tas_free.argtypes = [c.c_void_p]
@@ -175,6 +177,20 @@ class TASFlavorSnapshot:
         self._lib.kueue_tas_host_last_stats(self._h, st)
         keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols")
         return dict(zip(keys, list(st)[:7]))
+
+    STAGES = ("fill", "rollup", "replicate", "leaf_partials", "select", "entry_offsets", "device_total")
+
+    def last_stage_times(self):
+        """Device ms per stage of the last run (HIP events on the ctx stream), dict keyed by STAGES."""
+        ms = (ctypes.c_float * len(self.STAGES))()
+        self._lib.kueue_tas_host_last_stage_times(self._h, ms, len(self.STAGES))
+        return dict(zip(self.STAGES, list(ms)))
+
+    def last_eval_ticks(self, n: int):
+        """Per-eval select-kernel time (100 MHz ticks) of the last device batch (diagnostics)."""
+        buf = (ctypes.c_int32 * n)()
+        self._lib.kueue_tas_host_last_eval_ticks(self._h, buf, n)
+        return list(buf)
 
     def last_profile(self):
         """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""

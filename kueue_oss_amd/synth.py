@@ -364,3 +364,42 @@ def random_case(rng: random.Random, max_nodes: int = 60, profile_mixed=None) -> 
                            implied=not kw, **kw))
     return {"name": "random", "levels": levels, "nodes": nodes, "pods": pods, "tasUsage": usage,
             "nodeLabels": nodeLabels, "flavorTolerations": flavor_tols, "featureGates": gates, "podSets": podsets}
+
+
+def lfc_stress_case(rng: random.Random, n_nodes: int = 5000, n_workloads: int = 40, big: bool = True):
+    """LeastFreeCapacity leaf-level stress: rack/hostname nodes whose free
+    slot counts (cpu / 1 cpu request) span the exact histogram bins and, with
+    ``big``, the overflow range (>= 127), over several 2,048-leaf chunks;
+    unconstrained workloads sized to hit the single-leaf first fit, the
+    greedy threshold inside the bins, inside the overflow range, and the
+    not-fit failure.  Workloads share phase-1 classes (same request)."""
+    levels = [RACK, HOST]
+    nodes = []
+    for i in range(n_nodes):
+        r = rng.random()
+        if big and r < 0.02:
+            slots = rng.randint(127, 900)
+        elif r < 0.25:
+            slots = 0
+        else:
+            slots = rng.choice([1, 1, 1, 2, 2, 3, 5, 8, 40, 126])
+        nodes.append(_node(f"n{i}", {RACK: f"r{i // 64}", HOST: f"n{i}"},
+                           {"cpu": slots * 1000, "memory": 4096 * GI, "pods": 5000}))
+    total = 0
+    for n in nodes:
+        total += n["allocatable"]["cpu"] // 1000
+    wls = []
+    for k in range(n_workloads):
+        kind = rng.random()
+        if kind < 0.2:
+            count = rng.randint(0, 130)
+        elif kind < 0.5:
+            count = rng.randint(100, 3000)
+        elif kind < 0.8:
+            count = rng.randint(max(1, total - 3000), total)
+        else:
+            count = total + rng.randint(1, 50)
+        ps = _ps("main", count, {"cpu": 1000}, unconstrained=True)
+        wls.append([ps])
+    snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": [], "nodeLabels": {}, "featureGates": {}}
+    return snap, wls

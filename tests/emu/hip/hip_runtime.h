@@ -142,4 +142,5 @@ inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char
 
 // every lane holds the same value where the kernels use it (wave-uniform data)
 #define __builtin_amdgcn_readfirstlane(v) (v)
+inline uint64_t wall_clock64() { return 0; }
 inline int __popc(unsigned x) { return __builtin_popcount(x); }

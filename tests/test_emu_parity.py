@@ -59,3 +59,15 @@ def test_emulated_kernels_match_oracle_c3_small(emu_lib, list_cap, n):
     got = snap.find_topology_assignments_for_workloads(wls)
     snap.close()
     assert got == want
+
+
+@pytest.mark.parametrize("seed,big", [(31, True), (32, False)])
+def test_emulated_fast_lfc_stress(emu_lib, seed, big):
+    # fast LeastFreeCapacity leaf path: several histogram chunks, overflow values, all outcomes
+    snap_doc, wls = synth.lfc_stress_case(random.Random(seed), n_nodes=4500, n_workloads=24, big=big)
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc, lib=emu_lib)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    mism = [i for i in range(len(wls)) if got[i] != want[i]]
+    assert mism == [], (mism[:5], wls[mism[0]][0]["count"] if mism else None)

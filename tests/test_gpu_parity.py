@@ -72,3 +72,28 @@ def test_batched_workloads_match_oracle_c4_jobset():
     snap.close()
     mism = [i for i in range(len(wls)) if got[i] != want[i]]
     assert mism == [], (mism[:5], got[mism[0]] if mism else None, want[mism[0]] if mism else None)
+
+
+@pytest.mark.parametrize("seed,big,n_nodes", [(31, True, 4500), (32, False, 20000), (33, True, 40000)])
+def test_fast_lfc_stress(seed, big, n_nodes):
+    # fast LeastFreeCapacity leaf path: many 2,048-leaf chunks, overflow values, every outcome
+    snap_doc, wls = synth.lfc_stress_case(random.Random(seed), n_nodes=n_nodes, n_workloads=40, big=big)
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    mism = [i for i in range(len(wls)) if got[i] != want[i]]
+    assert mism == [], (mism[:5], wls[mism[0]][0]["count"] if mism else None)
+
+
+def test_c3_sample_full_size():
+    # the bench workload at full size (131,072 nodes) against the oracle on a sample
+    snap_doc, wls = synth.config_c3(n_workloads=1024)
+    sample = wls[:32] + [w for w in wls if w[0]["topologyRequest"] and w[0]["topologyRequest"].get("unconstrained")][:32]
+    want, _ = oracle_lib.eval_workloads(snap_doc, sample)
+    snap = TASFlavorSnapshot(snap_doc)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    idx = {id(w): i for i, w in enumerate(wls)}
+    mism = [k for k, w in enumerate(sample) if got[idx[id(w)]] != want[k]]
+    assert mism == [], mism[:5]

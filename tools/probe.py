@@ -18,4 +18,5 @@ for name, g in groups.items():
     t = time.perf_counter(); snap.run_compiled(); wall = (time.perf_counter() - t) * 1e3
     ms, cnt = snap.last_timings()
     print(json.dumps({"class": name, "n": len(g), "wall_ms": round(wall, 2), "device_ms": [round(x, 2) for x in ms],
-                      "host_ms": [round(x, 2) for x in snap.last_profile()]}))
+                      "host_ms": [round(x, 2) for x in snap.last_profile()],
+                      "stages": {k: round(v, 3) for k, v in snap.last_stage_times().items()}}))
