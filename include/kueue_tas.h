@@ -203,7 +203,8 @@ int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
 
 /* Diagnostics: wall-clock time each eval of the last kueue_tas_eval_batch
- * spent in the select kernel (100 MHz ticks), request order. */
+ * spent in the select kernel (100 MHz ticks), request order: ticks[2i] total,
+ * ticks[2i+1] the findLevelWithFitDomains part.  ticks holds 2n values. */
 int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1

@@ -691,7 +691,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
-  for (size_t i = 0; i < n; i++) c->last_ticks.push_back(c->h_out.p[i].reserved[0]);
+  for (size_t i = 0; i < n; i++) {
+    c->last_ticks.push_back(c->h_out.p[i].reserved[0]);
+    c->last_ticks.push_back(c->h_out.p[i].reserved[1]);
+  }
   for (size_t i = 0; i <= n; i++) offsets[i] = c->h_offsets.p[i];
   if (taint_counts && nt) memcpy(taint_counts, c->h_stats.p, n * nt * 4);
   if (res_counts && s.R) memcpy(res_counts, c->h_stats.p + n * nt, n * size_t(s.R) * 4);
@@ -731,7 +734,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
         c->last_entries.resize(keep);
-        c->last_ticks.resize(i0);
+        c->last_ticks.resize(2 * i0);
         int32_t need = 0;
         for (size_t i = 0; i < m; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
         int cap = c->entry_cap;
@@ -775,7 +778,7 @@ int kueue_tas_last_stage_times(kueue_tas_ctx* c, float* ms, int n) {
 
 int kueue_tas_last_eval_ticks(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   if (!c || !ticks) return KUEUE_TAS_EINVAL;
-  for (size_t i = 0; i < n; i++) ticks[i] = i < c->last_ticks.size() ? c->last_ticks[i] : 0;
+  for (size_t i = 0; i < 2 * n; i++) ticks[i] = i < c->last_ticks.size() ? c->last_ticks[i] : 0;
   return KUEUE_TAS_OK;
 }
 

@@ -1198,11 +1198,10 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
   memcpy(h->stats, ev.stats, sizeof h->stats);
   if (result_hash) {
     uint64_t x = 1469598103934665603ull;
-    auto mix = [&](uint64_t v) {
-      for (int i = 0; i < 8; i++) {
-        x ^= (v >> (8 * i)) & 0xff;
-        x *= 1099511628211ull;
-      }
+    auto mix = [&](uint64_t v) {  // word-wise FNV-1a variant
+      x ^= v;
+      x *= 1099511628211ull;
+      x ^= x >> 29;
     };
     for (auto& rs : results)
       for (auto& r : rs) {

@@ -1194,6 +1194,43 @@ __device__ __forceinline__ int32_t kp_ss(bool lfc, const Key& k) {
 }
 __device__ __forceinline__ int32_t kp_st(const Key& k) { return int32_t(uint32_t(k.hi) ^ 0x80000000u); }
 
+// Strided wave loops with kU independent loads in flight per lane: the loads
+// of kU strided indices are issued first (clamped index, so unconditional),
+// then the body runs for them in index order.  wave_for: body(i, v) only for
+// i < n; wave_for_all: every lane runs body(i, v, valid) (bodies with wave
+// collectives).  Single-wave passes over long lists are latency bound; this
+// keeps kU requests per lane outstanding instead of one.
+constexpr int kU = 8;
+template <class T, class Load, class Body>
+__device__ __forceinline__ void wave_for(int n, Load load, Body body) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += kU * kWave) {
+    T v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) v[u] = load(min(base + u * kWave + lane, n - 1));
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = base + u * kWave + lane;
+      if (i < n) body(i, v[u]);
+    }
+  }
+}
+template <class T, class Load, class Body>
+__device__ __forceinline__ void wave_for_all(int n, Load load, Body body) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += kU * kWave) {
+    T v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) v[u] = load(min(base + u * kWave + lane, n - 1));
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = base + u * kWave + lane;
+      body(i, v[u], i < n);
+    }
+  }
+}
+
+
 // First position p (in scan order: bin i = p, or kBins-1-p when desc) whose
 // inclusive weighted sum reaches need.  Returns the bin (or -1: total < need,
 // *before = total) and the sum before it.
@@ -1249,14 +1286,27 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   // pass A: keys, range of the primary component, minimum weight
   int32_t vmin = 0x7fffffff, vmax = int32_t(0x80000000u), wmin = 0x7fffffff;
   int64_t wsum = 0;
-  for (int i = w.lane; i < n; i += kWave) {
-    const int g = gids[i];
-    const int32_t ss = w.get(F_SLICE, g), st = w.get(F_STATE, g);
-    keys[i] = key_plain(lfc, ss, st, g - loff);
-    vmin = min(vmin, ss);
-    vmax = max(vmax, ss);
-    wmin = min(wmin, slices ? ss : st);
-    wsum += slices ? ss : st;
+  for (int base = 0; base < n; base += kU * kWave) {
+    int g[kU];
+    int32_t ss[kU], st[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      ss[u] = w.get(F_SLICE, g[u]);
+      st[u] = w.get(F_STATE, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = base + u * kWave + w.lane;
+      if (i < n) {
+        keys[i] = key_plain(lfc, ss[u], st[u], g[u] - loff);
+        vmin = min(vmin, ss[u]);
+        vmax = max(vmax, ss[u]);
+        wmin = min(wmin, slices ? ss[u] : st[u]);
+        wsum += slices ? ss[u] : st[u];
+      }
+    }
   }
   wsum = wave_sum_i64(wsum);
 #pragma unroll
@@ -1272,7 +1322,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   int32_t remc;    // rem left when the walk reaches it
   if (rem <= 0) {  // the first element already satisfies rem
     Key k = key_max();
-    for (int i = w.lane; i < n; i += kWave) k = key_min2(k, keys[i]);
+    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& x) { k = key_min2(k, x); });
     ck = wave_min_key(k);
     remc = rem;
   } else {
@@ -1280,12 +1330,11 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     // pass B: weight per sliceState value
     for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
     wave_sync();
-    for (int i = w.lane; i < n; i += kWave) {
-      const Key k = keys[i];
+    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
       const int32_t ss = kp_ss(lfc, k);
       const int32_t wt = slices ? ss : kp_st(k);
       if (wt > 0) atomicAdd((unsigned long long*)&hist[ss - vmin], (unsigned long long)wt);
-    }
+    });
     wave_sync();
     int64_t before1;
     const int b1 = bins_threshold(hist, !lfc, rem, &before1);
@@ -1294,13 +1343,12 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     const int64_t rem1 = rem - before1;
     // pass C: state range inside class t
     int32_t umin = 0x7fffffff, umax = int32_t(0x80000000u);
-    for (int i = w.lane; i < n; i += kWave) {
-      const Key k = keys[i];
+    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
       if (kp_ss(lfc, k) == t) {
         umin = min(umin, kp_st(k));
         umax = max(umax, kp_st(k));
       }
-    }
+    });
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       umin = min(umin, __shfl_xor(umin, m, 64));
@@ -1311,13 +1359,12 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     wave_sync();
     for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
     wave_sync();
-    for (int i = w.lane; i < n; i += kWave) {
-      const Key k = keys[i];
+    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
       if (kp_ss(lfc, k) == t) {
         const int32_t wt = slices ? t : kp_st(k);
         if (wt > 0) atomicAdd((unsigned long long*)&hist[kp_st(k) - umin], (unsigned long long)wt);
       }
-    }
+    });
     wave_sync();
     int64_t before2;
     const int b2 = bins_threshold(hist, false, rem1, &before2);
@@ -1330,19 +1377,13 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     // pass E: the m-th smallest index of class (t, u)
     wave_sync();
     int cnt = 0;
-    for (int i0 = 0; i0 < n; i0 += kWave) {
-      const int i = i0 + w.lane;
-      bool in = false;
-      Key k{0, 0};
-      if (i < n) {
-        k = keys[i];
-        in = kp_ss(lfc, k) == t && kp_st(k) == u;
-      }
-      int tot;
-      const int pos = cnt + wave_excl_scan(in ? 1 : 0, &tot);
+    wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
+      const bool in = valid && kp_ss(lfc, k) == t && kp_st(k) == u;
+      const uint64_t bm = ballot(in);
+      const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
       if (in && pos < w.cap) w.lds[pos] = Key{0, k.lo};
-      cnt += tot;
-    }
+      cnt += __popcll(bm);
+    });
     if (cnt > w.cap) return -1;
     wave_sync();
     lds_sort(w.lds, cnt, w.lane);
@@ -1351,42 +1392,37 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   }
   int chosen = loff + int(uint32_t(ck.lo));
   if (w.bf) {  // findBestFitDomainBy over the crossing and everything after it (:1216-1231)
+    // one pass: per lane the best (weight, key) pair, then a wave arg-min
     uint32_t bst = ~0u;
-    for (int i = w.lane; i < n; i += kWave) {
-      const Key k = keys[i];
-      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
-      if (key_le(ck, k) && wt >= remc) bst = min(bst, s_asc(wt));
-    }
-    bst = uint32_t(wave_min_u64(bst));
     Key best = key_max();
-    for (int i = w.lane; i < n; i += kWave) {
-      const Key k = keys[i];
+    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
       const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
-      if (key_le(ck, k) && s_asc(wt) == bst) best = key_min2(best, k);
-    }
-    best = wave_min_key(best);
+      if (key_le(ck, k) && wt >= remc) {
+        const uint32_t sw = s_asc(wt);
+        if (sw < bst || (sw == bst && key_lt(k, best))) {
+          bst = sw;
+          best = k;
+        }
+      }
+    });
+    const uint32_t wbst = uint32_t(wave_min_u64(bst));
+    best = wave_min_key(bst == wbst ? best : key_max());
     chosen = loff + int(uint32_t(best.lo));
   }
   // pass F: emit the whole elements before the crossing (lane-private stores)
   int cnt = *np;
-  for (int i0 = 0; i0 < n; i0 += kWave) {
-    const int i = i0 + w.lane;
-    bool take = false;
-    Key k{0, 0};
-    if (i < n) {
-      k = keys[i];
-      take = key_lt(k, ck);
-    }
-    int tot;
-    const int pos = cnt + wave_excl_scan(take ? 1 : 0, &tot);
+  wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
+    const bool take = valid && key_lt(k, ck);
+    const uint64_t bm = ballot(take);
+    const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
     if (take) {
       const int g = loff + int(uint32_t(k.lo));
       if (slices) w.set_lane(F_STATE, g, w_mul(kp_ss(lfc, k), sliceSize));
       w.set_lane(F_LS, g, 0);
       if (pos < w.lcap) out[pos] = g;
     }
-    cnt += tot;
-  }
+    cnt += __popcll(bm);
+  });
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   // the crossing element (or its best fit) takes the remainder
   w.set(F_LS, chosen, 0);
@@ -1542,18 +1578,24 @@ __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level
   const DevSnap& s = *w.s;
   const int poff = s.level_off[level];
   const int coff = s.level_off[level + 1];
+  const int32_t* co = s.child_off + s.child_base[level];
   int np = 0;
-  for (int i = 0; i < n; i++) {
-    int p = parents[i] - poff;
-    int cb = s.child_off[s.child_base[level] + p];
-    int ce = s.child_off[s.child_base[level] + p + 1];
-    int cnt = ce - cb;
-    if (np + cnt > w.lcap) {
+  for (int i0 = 0; i0 < n; i0 += kWave) {  // 64 parents per step: ranges, then a scan for the offsets
+    const int i = i0 + w.lane;
+    int cb = 0, cnt = 0;
+    if (i < n) {
+      const int p = parents[i] - poff;
+      cb = co[p];
+      cnt = co[p + 1] - cb;
+    }
+    int tot;
+    const int ex = wave_excl_scan(cnt, &tot);
+    if (np + tot > w.lcap) {
       w.overflow = true;
       return np;
     }
-    for (int j = w.lane; j < cnt; j += kWave) out[np + j] = coff + cb + j;
-    np += cnt;
+    for (int j = 0; j < cnt; j++) out[np + ex + j] = coff + cb + j;
+    np += tot;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   return np;
@@ -2365,6 +2407,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   } else {
     r = find_level(w, w.listA, &nres, &fitLevel, o, ent, ecap);
   }
+  const uint64_t t_found = wall_clock64();
   if (r == 0) {
     const int L = s.L;
     const int32_t leaderCount = w.leader ? 1 : 0;
@@ -2431,7 +2474,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
     if (o.num_workers + o.num_leaders > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
   }
   if (w.overflow) o.status = KUEUE_TAS_ST_INTERNAL;
-  o.reserved[0] = int32_t(wall_clock64() - t_begin);  // diagnostics: 100 MHz ticks in select
+  o.reserved[0] = int32_t(wall_clock64() - t_begin);  // diagnostics: 100 MHz ticks in select,
+  o.reserved[1] = int32_t(t_found - t_begin);         // of which findLevelWithFitDomains
   if (lane == 0) b.out[eid] = o;
 }
 

@@ -187,10 +187,11 @@ class TASFlavorSnapshot:
         return dict(zip(self.STAGES, list(ms)))
 
     def last_eval_ticks(self, n: int):
-        """Per-eval select-kernel time (100 MHz ticks) of the last device batch (diagnostics)."""
-        buf = (ctypes.c_int32 * n)()
+        """Per-eval select-kernel time (100 MHz ticks) of the last device batch
+        (diagnostics): [(total, findLevelWithFitDomains part)] * n."""
+        buf = (ctypes.c_int32 * (2 * n))()
         self._lib.kueue_tas_host_last_eval_ticks(self._h, buf, n)
-        return list(buf)
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
     def last_profile(self):
         """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""
@@ -204,9 +205,10 @@ class TASFlavorSnapshot:
         self._lib.kueue_tas_host_last_records(self._h, buf, n)
         return list(buf)
 
-    def run_compiled(self) -> int:
+    def run_compiled(self, want_hash: bool = False):
+        """One timed step over the compiled workloads; returns the result hash if asked."""
         h = ctypes.c_uint64()
-        rc = self._lib.kueue_tas_host_run_compiled(self._h, ctypes.byref(h))
+        rc = self._lib.kueue_tas_host_run_compiled(self._h, ctypes.byref(h) if want_hash else None)
         if rc != 0:
             raise RuntimeError(f"kueue_tas_host_run_compiled failed ({rc}): {self._err()}")
-        return h.value
+        return h.value if want_hash else None

@@ -28,7 +28,7 @@ rows = []
 for i, w in enumerate(wls):
     r = res[i][0]
     nd = len(r["assignment"]["domains"]) if r.get("assignment") else 0
-    rows.append({"i": i, "us": ticks[i] / 100.0, "cls": cls(w), "count": w[0]["count"],
+    rows.append({"i": i, "us": ticks[i][0] / 100.0, "find_us": ticks[i][1] / 100.0, "cls": cls(w), "count": w[0]["count"],
                  "req": w[0]["requests"], "sel": bool(w[0].get("nodeSelector")), "tol": bool(w[0].get("tolerations")),
                  "domains": nd, "fail": (r.get("reason") or "")[:60]})
 rows.sort(key=lambda r: -r["us"])
