@@ -207,6 +207,12 @@ int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
  * ticks[2i+1] the findLevelWithFitDomains part.  ticks holds 2n values. */
 int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
+/* Diagnostics (profiling build libkueue_tas_prof.so; zeros otherwise): 8
+ * inclusive select-phase tick counters per eval of the last batch (LDS sort,
+ * threshold walk, child gather, emit, sorted walk, global sort, count
+ * update, findLevelWithFitDomains).  ticks holds 8n values. */
+int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
+
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
  * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
@@ -241,6 +247,8 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
 int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
 /* kueue_tas_last_stage_times summed over the last run's batches. */
 int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n);
+/* kueue_tas_last_eval_profile of the last device batch (diagnostics). */
+int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* kueue_tas_last_eval_ticks of the last device batch (diagnostics). */
 int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* Host wall time of the last run_compiled (ms): [0] request staging,

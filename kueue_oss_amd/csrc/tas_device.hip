@@ -134,6 +134,8 @@ struct kueue_tas_ctx {
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
   DevBuf<uint64_t> d_lfc_ovs, d_lfc_ovtot;
   DevBuf<LfcJob> d_lfc_jobs;
+  DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
+  std::vector<int32_t> last_prof;
   std::vector<int32_t> h_rep_of, h_lfc_slot, h_lfc_rep, h_fast;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
@@ -227,6 +229,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_ovs.release();
   c->d_lfc_ovtot.release();
   c->d_lfc_jobs.release();
+  c->d_prof.release();
   c->h_evals.release();
   c->h_terms.release();
   c->h_out.release();
@@ -572,6 +575,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.lfc_ovs = c->d_lfc_ovs.p;
   b.lfc_ovtot = c->d_lfc_ovtot.p;
   b.lfc_jobs = c->d_lfc_jobs.p;
+  b.prof = nullptr;
+  if (KTAS_PROFILE) {
+    HIPCHK(c, c->d_prof.ensure(n * P_NCAT));
+    HIPCHK(c, hipMemsetAsync(c->d_prof.p, 0, n * P_NCAT * 4, c->stream));
+    b.prof = c->d_prof.p;
+  }
   const int nfill = int(c->h_fill_ids.size());
   const int npairs = int(c->h_pairs.size() / 2);
   c->stat_fills += nfill;
@@ -691,6 +700,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
+  if (KTAS_PROFILE) {
+    const size_t base = c->last_prof.size();
+    c->last_prof.resize(base + n * P_NCAT);
+    HIPCHK(c, hipMemcpy(c->last_prof.data() + base, c->d_prof.p, n * P_NCAT * 4, hipMemcpyDeviceToHost));
+  }
   for (size_t i = 0; i < n; i++) {
     c->last_ticks.push_back(c->h_out.p[i].reserved[0]);
     c->last_ticks.push_back(c->h_out.p[i].reserved[1]);
@@ -720,6 +734,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   c->last_entries.clear();
   c->last_ticks.clear();
+  c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
   const size_t chunk = size_t(c->max_batch);
   std::vector<int64_t> off;
@@ -735,6 +750,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
         c->last_entries.resize(keep);
         c->last_ticks.resize(2 * i0);
+        c->last_prof.resize(KTAS_PROFILE ? i0 * P_NCAT : 0);
         int32_t need = 0;
         for (size_t i = 0; i < m; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
         int cap = c->entry_cap;
@@ -779,6 +795,12 @@ int kueue_tas_last_stage_times(kueue_tas_ctx* c, float* ms, int n) {
 int kueue_tas_last_eval_ticks(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   if (!c || !ticks) return KUEUE_TAS_EINVAL;
   for (size_t i = 0; i < 2 * n; i++) ticks[i] = i < c->last_ticks.size() ? c->last_ticks[i] : 0;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
+  if (!c || !ticks) return KUEUE_TAS_EINVAL;
+  for (size_t i = 0; i < n * P_NCAT; i++) ticks[i] = i < c->last_prof.size() ? c->last_prof[i] : 0;
   return KUEUE_TAS_OK;
 }
 

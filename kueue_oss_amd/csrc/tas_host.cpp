@@ -1229,6 +1229,11 @@ int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n) 
   return kueue_tas_last_eval_ticks(h->snap->ctx, ticks, n);
 }
 
+int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n) {
+  if (!h || !h->snap) return KUEUE_TAS_EINVAL;
+  return kueue_tas_last_eval_profile(h->snap->ctx, ticks, n);
+}
+
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4) {
   if (!h || !h->ev) return KUEUE_TAS_EINVAL;
   memcpy(ms4, h->ev->host_ms, sizeof h->ev->host_ms);

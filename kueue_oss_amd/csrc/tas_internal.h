@@ -138,6 +138,7 @@ struct DevBatch {
   uint64_t* lfc_ovs;       // [nslots][nchunks] sum of the values >= kLfcBins - 1
   uint64_t* lfc_ovtot;     // [nslots]
   LfcJob* lfc_jobs;        // [n]
+  int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
 };
 
 }  // namespace ktas

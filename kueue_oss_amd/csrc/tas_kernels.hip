@@ -831,6 +831,13 @@ __global__ __launch_bounds__(kLfcBins) void lfc_total_kernel(DevBatch b) {
 // ----------------------------------------------------------------------------
 enum Field : int { F_STATE = 0, F_SLICE = 1, F_SWL = 2, F_SSWL = 3, F_LS = 4 };
 
+// Profiling build (-DKTAS_PROFILE=1, libkueue_tas_prof.so): per-eval ticks
+// of the select kernel's phases into DevBatch::prof (diagnostics only).
+#ifndef KTAS_PROFILE
+#define KTAS_PROFILE 0
+#endif
+enum ProfCat : int { P_LDS_SORT = 0, P_THRESHOLD, P_GATHER, P_EMIT, P_WALK, P_GLOBAL_SORT, P_UPDATE, P_FIND, P_NCAT };
+
 struct Wave {
   const DevSnap* s;
   const DevEval* ev;
@@ -851,6 +858,7 @@ struct Wave {
   bool overflow;
   const LeafPartial* partials;  // leaf-level partial reductions of this eval (or null)
   int nblk;
+  uint64_t prof[P_NCAT];
 
   __device__ int32_t get(Field f, int g) const {
     if (!leader) {
@@ -884,22 +892,49 @@ struct Wave {
   }
 };
 
+struct ProfScope {
+#if KTAS_PROFILE
+  uint64_t* slot;
+  uint64_t t0;
+  __device__ ProfScope(Wave& w, int cat) : slot(&w.prof[cat]), t0(wall_clock64()) {}
+  __device__ ~ProfScope() { *slot += wall_clock64() - t0; }
+#else
+  __device__ ProfScope(Wave&, int) {}
+#endif
+};
+
 // ---- LDS bitonic sort of m keys (one wave) ----
+// Each stage visits the m/2 compare-exchange pairs (lane p handles pair p:
+// i = p with a zero bit inserted at `stride`, j = i | stride), kSortU pairs
+// per lane in flight, so the LDS round trips of one stage overlap.
+constexpr int kSortU = 4;
 __device__ void lds_sort(Key* k, int n, int lane) {
   int m = 1;
   while (m < n) m <<= 1;
   for (int i = n + lane; i < m; i += kWave) k[i] = key_max();
   wave_sync();
+  const int half = m >> 1;
   for (int size = 2; size <= m; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = lane; i < m; i += kWave) {
-        int j = i ^ stride;
-        if (j > i) {
-          bool asc = (i & size) == 0;
-          Key a = k[i], c = k[j];
-          if (key_lt(c, a) == asc) {
-            k[i] = c;
-            k[j] = a;
+      for (int p0 = 0; p0 < half; p0 += kSortU * kWave) {
+        Key a[kSortU], c[kSortU];
+        int ii[kSortU];
+#pragma unroll
+        for (int u = 0; u < kSortU; u++) {
+          const int p = min(p0 + u * kWave + lane, half - 1);
+          const int i = ((p & ~(stride - 1)) << 1) | (p & (stride - 1));
+          ii[u] = i;
+          a[u] = k[i];
+          c[u] = k[i | stride];
+        }
+#pragma unroll
+        for (int u = 0; u < kSortU; u++) {
+          const int p = p0 + u * kWave + lane;
+          const int i = ii[u];
+          const bool asc = (i & size) == 0;
+          if (p < half && key_lt(c[u], a[u]) == asc) {
+            k[i] = c[u];
+            k[i | stride] = a[u];
           }
         }
       }
@@ -910,6 +945,7 @@ __device__ void lds_sort(Key* k, int n, int lane) {
 
 // ---- global merge sort of n keys in `a` (tmp same size); result in a ----
 __device__ void global_sort(Wave& w, Key* a, Key* tmp, int n) {
+  ProfScope prof_scope_(w, P_GLOBAL_SORT);
   const int lane = w.lane;
   const int run = w.cap;
   // sort runs of `run` in LDS
@@ -917,7 +953,10 @@ __device__ void global_sort(Wave& w, Key* a, Key* tmp, int n) {
     int m = min(run, n - r0);
     for (int i = lane; i < m; i += kWave) w.lds[i] = a[r0 + i];
     wave_sync();
-    lds_sort(w.lds, m, lane);
+    {
+      ProfScope ps_(w, P_LDS_SORT);
+      lds_sort(w.lds, m, lane);
+    }
     for (int i = lane; i < m; i += kWave) a[r0 + i] = w.lds[i];
     wave_sync();
   }
@@ -1126,6 +1165,7 @@ __device__ int consume_with_leaders(Wave& w, Seq& seq, int domain, int32_t* remP
 template <class Seq>
 __device__ bool update_counts(Wave& w, Seq& seq, int32_t count, int32_t leaderCount, int32_t sliceSize, bool slices,
                               int32_t* out, int* np) {
+  ProfScope prof_scope_(w, P_UPDATE);
   const int start = *np;
   int32_t remP = slices ? go_div32(count, sliceSize) : count;
   int32_t remL = leaderCount;
@@ -1278,6 +1318,7 @@ __device__ int bins_threshold(const uint64_t* hist, bool desc, int64_t need, int
 // (preconditions unmet: caller sorts).  Keys are materialized in w.gkeys.
 __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t sliceSize,
                               bool slices, int32_t* out, int* np) {
+  ProfScope prof_scope_(w, P_THRESHOLD);
   if (w.cap * int(sizeof(Key)) < kThrBins * int(sizeof(uint64_t))) return -1;
   const int loff = w.s->level_off[level];
   const bool lfc = w.lfc;
@@ -1386,7 +1427,10 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     });
     if (cnt > w.cap) return -1;
     wave_sync();
-    lds_sort(w.lds, cnt, w.lane);
+    {
+      ProfScope ps_(w, P_LDS_SORT);
+      lds_sort(w.lds, cnt, w.lane);
+    }
     ck = key_plain(lfc, t, u, int32_t(uint32_t(w.lds[m - 1].lo)));
     wave_sync();
   }
@@ -1523,13 +1567,42 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
 // sortedDomains: LDS sort when it fits, lazy iteration otherwise.
 __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t leaderCount,
                             int32_t sliceSize, bool slices, int32_t sliceRecompute, int32_t* out, int* np) {
+  ProfScope prof_scope_(w, P_WALK);
   const int loff = w.s->level_off[level];
   // leaderless walks need no sequential pass (see threshold_walk)
   const bool leaderless = !w.leader && leaderCount <= 0 && sliceRecompute <= 1;
+  if (leaderless && w.bf && slices && n > w.cap && gids != w.listD && go_div32(count, sliceSize) > 0) {
+    // BestFit slice walk with rem > 0: elements with sliceState <= 0 sort after
+    // every positive one (sliceState desc), cannot move the running sum up to
+    // rem, and cannot be the best fit (weight >= remc > 0), so they are never
+    // taken (:1452-1467): walk the positive ones only.
+    int m = 0;
+    for (int base = 0; base < n; base += kU * kWave) {
+      int g[kU];
+      int32_t v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
+#pragma unroll
+      for (int u = 0; u < kU; u++) v[u] = w.get(F_SLICE, g[u]);
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const bool keep = base + u * kWave + w.lane < n && v[u] > 0;
+        const uint64_t bm = ballot(keep);
+        if (keep) w.listD[m + __popcll(bm & ((1ull << w.lane) - 1ull))] = g[u];
+        m += __popcll(bm);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    gids = w.listD;
+    n = m;
+  }
   if (n <= w.cap) {
     for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain(gids[i]);
     wave_sync();
-    lds_sort(w.lds, n, w.lane);
+    {
+      ProfScope ps_(w, P_LDS_SORT);
+      lds_sort(w.lds, n, w.lane);
+    }
     if (leaderless) {
       const int r = lds_prefix_walk(w, n, loff, count, sliceSize, slices, out, np);
       if (r >= 0) {
@@ -1575,6 +1648,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
 
 // Children (CSR) of `n` domains at `level` appended to out (lowerLevelDomains :1503-1509).
 __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level, int32_t* out) {
+  ProfScope prof_scope_(w, P_GATHER);
   const DevSnap& s = *w.s;
   const int poff = s.level_off[level];
   const int coff = s.level_off[level + 1];
@@ -1660,12 +1734,16 @@ __device__ void not_fit(Wave& w, int level, int32_t fit, int32_t total, kueue_ta
 // Write (leaf, count) entries sorted by leaf index (buildAssignment :1490-1501).
 __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, bool positive_only, int32_t* ent, int ent_cap,
                            int base) {
+  ProfScope prof_scope_(w, P_EMIT);
   const int loff = w.s->level_off[w.s->L - 1];
   Key* arr;
   if (n <= w.cap) {
     for (int i = w.lane; i < n; i += kWave) w.lds[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
     wave_sync();
-    lds_sort(w.lds, n, w.lane);
+    {
+      ProfScope ps_(w, P_LDS_SORT);
+      lds_sort(w.lds, n, w.lane);
+    }
     arr = w.lds;
   } else {
     for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
@@ -2077,6 +2155,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
 // *nres), 1 failure (o filled), 2 finished by the LFC fast path (o filled).
 __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, kueue_tas_eval_out& o, int32_t* ent,
                           int ent_cap) {
+  ProfScope prof_scope_(w, P_FIND);
   const DevSnap& s = *w.s;
   const DevEval& ev = *w.ev;
   const bool required = (ev.flags & KUEUE_TAS_F_REQUIRED) != 0;
@@ -2194,7 +2273,10 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
           w.lds[i] = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
         }
         wave_sync();
-        lds_sort(w.lds, D, w.lane);
+        {
+          ProfScope ps_(w, P_LDS_SORT);
+          lds_sort(w.lds, D, w.lane);
+        }
         SeqLds seq{&w, D, loff, 0};
         int idx = 0;
         for (; remL > 0 && idx < D && w.get(F_LS, seq.at(idx)) > 0; idx++) {
@@ -2217,7 +2299,10 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         wave_sync();
         for (int i = w.lane; i < nrem; i += kWave) w.lds[i] = w.kplain(loff + int(uint32_t(w.gkeys[i].lo)));
         wave_sync();
-        lds_sort(w.lds, nrem, w.lane);
+        {
+          ProfScope ps_(w, P_LDS_SORT);
+          lds_sort(w.lds, nrem, w.lane);
+        }
         SeqLds seq2{&w, nrem, loff, 0};
         for (int i = 0; remS > 0 && i < nrem; i++) {
           seq2.pos = i;
@@ -2379,6 +2464,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.gkeys = reinterpret_cast<Key*>(sc + 2 * lcap);
   w.gkeys2 = w.gkeys + lcap;
   w.overflow = false;
+  for (auto& x : w.prof) x = 0;
   w.partials = (b.partials && ev.requested_level == s.L - 1) ? b.partials + int64_t(eid) * b.nblk : nullptr;
   w.nblk = b.nblk;
   int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
@@ -2477,6 +2563,10 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   o.reserved[0] = int32_t(wall_clock64() - t_begin);  // diagnostics: 100 MHz ticks in select,
   o.reserved[1] = int32_t(t_found - t_begin);         // of which findLevelWithFitDomains
   if (lane == 0) b.out[eid] = o;
+#if KTAS_PROFILE
+  if (lane == 0 && b.prof)
+    for (int k = 0; k < P_NCAT; k++) b.prof[int64_t(eid) * P_NCAT + k] = int32_t(w.prof[k]);
+#endif
 }
 
 // Expand fast-LFC greedy results (LfcJob) into (leaf, count) entries in leaf

@@ -47,10 +47,10 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
+    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
 ]
 
 
@@ -94,6 +94,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_stage_times.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int]
+    lib.kueue_tas_host_last_eval_profile.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
@@ -192,6 +193,14 @@ class TASFlavorSnapshot:
         buf = (ctypes.c_int32 * (2 * n))()
         self._lib.kueue_tas_host_last_eval_ticks(self._h, buf, n)
         return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
+
+    PROF = ("lds_sort", "threshold_walk", "gather", "emit", "walk_sorted", "global_sort", "update_counts", "find_level")
+
+    def last_eval_profile(self, n: int):
+        """Profiling build only: inclusive select-phase ticks per eval, dicts keyed by PROF."""
+        buf = (ctypes.c_int32 * (8 * n))()
+        self._lib.kueue_tas_host_last_eval_profile(self._h, buf, n)
+        return [dict(zip(self.PROF, buf[8 * i: 8 * i + 8])) for i in range(n)]
 
     def last_profile(self):
         """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""

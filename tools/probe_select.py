@@ -6,15 +6,19 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from kueue_oss_amd import TASFlavorSnapshot, synth
+from kueue_oss_amd import TASFlavorSnapshot, native, synth
+
+PROF = "--prof" in sys.argv
+lib = native.load_library(os.path.join(os.path.dirname(native.library_path()), "libkueue_tas_prof.so")) if PROF else None
 
 snap_doc, wls = synth.config_c3(n_workloads=int(os.environ.get("N_WL", "1024")))
-snap = TASFlavorSnapshot(snap_doc)
+snap = TASFlavorSnapshot(snap_doc, lib=lib)
 res = snap.find_topology_assignments_for_workloads(wls)
 snap.compile(wls)
 for _ in range(3):
     snap.run_compiled()
 ticks = snap.last_eval_ticks(len(wls))
+prof = snap.last_eval_profile(len(wls)) if PROF else None
 
 
 def cls(w):
@@ -31,6 +35,8 @@ for i, w in enumerate(wls):
     rows.append({"i": i, "us": ticks[i][0] / 100.0, "find_us": ticks[i][1] / 100.0, "cls": cls(w), "count": w[0]["count"],
                  "req": w[0]["requests"], "sel": bool(w[0].get("nodeSelector")), "tol": bool(w[0].get("tolerations")),
                  "domains": nd, "fail": (r.get("reason") or "")[:60]})
+    if PROF:
+        rows[-1]["prof_us"] = {k: v / 100.0 for k, v in prof[i].items() if v}
 rows.sort(key=lambda r: -r["us"])
 for r in rows[:25]:
     print(json.dumps(r))
