@@ -128,7 +128,8 @@ struct kueue_tas_ctx {
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
   DevBuf<int32_t> d_fill_ids, d_pairs, d_leafsel;
-  std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel;
+  std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel, h_fill_chunks;
+  DevBuf<int32_t> d_fill_chunks, d_fill_stats;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
   DevBuf<int32_t> d_rep_of, d_lfc_slot, d_lfc_rep, d_fast;
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
@@ -217,6 +218,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_packed.release();
   c->d_partials.release();
   c->d_fill_ids.release();
+  c->d_fill_chunks.release();
+  c->d_fill_stats.release();
   c->d_leafsel.release();
   c->d_pairs.release();
   c->d_rep_of.release();
@@ -449,6 +452,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.assumed = c->d_assumed.p;
   b.n = int32_t(n);
   b.num_taints = int32_t(nt);
+  b.num_profiles = c->num_profiles;
+  b.nstat = 0;
+  b.nstat_R = s.R;
+  b.fill_stats = nullptr;
   b.ctr_stride = ctr_stride;
   b.counters = c->d_counters.p;
   b.taint_counts = c->d_stats.p;
@@ -484,10 +491,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
              e.requested_level == s.L - 1 && e.slice_level == s.L - 1 && e.slice_size == 1 && e.count >= 0 &&
              s.N > 0;
     };
-    std::unordered_map<std::string, int32_t> cls;
+    std::unordered_map<std::string, int32_t> cls, sigs;
     cls.reserve(n * 2);
     std::vector<std::vector<int32_t>> members;
-    std::string key;
+    std::vector<int32_t> class_sig;  // request signature of each class (fill chunks share counts)
+    std::string key, sig;
     for (size_t i = 0; i < n; i++) {
       const DevEval& e = c->h_evals.p[i];
       key.clear();
@@ -502,6 +510,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       put(e.sel_val, 4 * size_t(e.nsel));
       if (taint_table && size_t(e.taint_table) + size_t(c->num_profiles) <= taint_table_len)
         put(taint_table + e.taint_table, 4 * size_t(c->num_profiles));
+      const size_t sig_begin = key.size();
+      put(&f, 4);
       int32_t nt2[2] = {e.nreq, e.nlead};
       put(nt2, sizeof nt2);
       for (int k = 0; k < e.nreq + e.nlead; k++) {
@@ -514,6 +524,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (it == cls.end()) {
         cls.emplace(key, int32_t(members.size()));
         members.push_back({int32_t(i)});
+        sig.assign(key, sig_begin, std::string::npos);
+        auto si = sigs.find(sig);
+        if (si == sigs.end()) si = sigs.emplace(sig, int32_t(sigs.size())).first;
+        class_sig.push_back(si->second);
       } else {
         members[size_t(it->second)].push_back(int32_t(i));
       }
@@ -541,6 +555,26 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
           dst.push_back(fast ? ~m : m);  // ~m: exclusion stats only
         }
       }
+    }
+    // fill chunks: classes ordered by request signature, <= kEvalsPerFillBlock per chunk, one signature each
+    {
+      std::vector<int32_t> order(members.size());
+      for (size_t k = 0; k < order.size(); k++) order[k] = int32_t(k);
+      std::stable_sort(order.begin(), order.end(),
+                       [&](int32_t a, int32_t b2) { return class_sig[size_t(a)] < class_sig[size_t(b2)]; });
+      std::vector<int32_t> sorted_ids(order.size());
+      for (size_t k = 0; k < order.size(); k++) sorted_ids[k] = c->h_fill_ids[size_t(order[k])];
+      c->h_fill_chunks.clear();
+      for (size_t k = 0; k < order.size();) {
+        size_t e = k + 1;
+        while (e < order.size() && e - k < size_t(kEvalsPerFillBlock) &&
+               class_sig[size_t(order[e])] == class_sig[size_t(order[k])])
+          e++;
+        c->h_fill_chunks.push_back(int32_t(k));
+        c->h_fill_chunks.push_back(int32_t(e - k));
+        k = e;
+      }
+      c->h_fill_ids.swap(sorted_ids);
     }
     ncopy = int(c->h_pairs.size() / 2);  // pairs [0, ncopy) copy counters, the rest stats only
     c->h_pairs.insert(c->h_pairs.end(), stats_pairs.begin(), stats_pairs.end());
@@ -590,18 +624,31 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, hipMemcpyAsync(c->d_fill_ids.p, c->h_fill_ids.data(), size_t(nfill) * 4, hipMemcpyHostToDevice, c->stream));
   if (npairs)
     HIPCHK(c, hipMemcpyAsync(c->d_pairs.p, c->h_pairs.data(), size_t(npairs) * 8, hipMemcpyHostToDevice, c->stream));
+  const int nfchunks = int(c->h_fill_chunks.size() / 2);
+  HIPCHK(c, c->d_fill_chunks.ensure(size_t(std::max(2 * nfchunks, 1))));
+  if (nfchunks)
+    HIPCHK(c, hipMemcpyAsync(c->d_fill_chunks.p, c->h_fill_chunks.data(), size_t(nfchunks) * 8, hipMemcpyHostToDevice,
+                             c->stream));
   b.fill_ids = c->d_fill_ids.p;
   b.nfill = nfill;
+  b.fill_chunks = c->d_fill_chunks.p;
   // K1
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   c->last_stats[0] += nfill;
-  if (s.N > 0) {
-    dim3 grid((s.N + 255) / 256, unsigned((nfill + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
+  if (s.N > 0 && nfchunks > 0) {
+    dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
     uint32_t umask = 0;
     for (size_t i = 0; i < n; i++) umask |= c->h_evals.p[i].req_mask | c->h_evals.p[i].lead_mask;
     const int ucols = __builtin_popcount(umask);
     c->last_stats[2] += 1;
     c->last_stats[3] = ucols;
+    const int nstat = 1 + int(nt) + s.R;
+    b.nstat = (ucols <= 8 && nstat <= kMaxFillStats) ? nstat : 0;
+    b.nstat_R = s.R;
+    if (b.nstat) {
+      HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
+      b.fill_stats = c->d_fill_stats.p;
+    }
     if (ucols <= 4) hipLaunchKernelGGL(fill_leaves_staged_kernel<4>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (ucols <= 8) hipLaunchKernelGGL(fill_leaves_staged_kernel<8>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
@@ -609,6 +656,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
+    if (b.nstat) {
+      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(64), 0, c->stream, b, int(grid.x));
+      HIPCHK(c, hipGetLastError());
+    }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   // K2

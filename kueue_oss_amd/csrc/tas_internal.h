@@ -112,6 +112,10 @@ struct DevBatch {
   const kueue_tas_assumed* assumed;
   int32_t n;
   int32_t num_taints;
+  int32_t num_profiles;    // taint-profile rows per eval in taint_table
+  int32_t nstat;           // 1 + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
+  int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
+  int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int64_t ctr_stride;      // int32 elements per eval (5 * SD)
   int32_t* counters;       // [n][5][SD]
   int32_t* taint_counts;   // [n][num_taints]
@@ -127,6 +131,7 @@ struct DevBatch {
   int32_t nblk;            // fill blocks per eval (partials per eval)
   const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
   int32_t nfill;
+  const int32_t* fill_chunks; // [nchunks][2] (start, len) into fill_ids: <= kEvalsPerBlock classes, one request signature
   const int32_t* rep_of;   // [n] eval whose counters select reads (itself, or the class rep for fast LFC)
   const int32_t* lfc_slot; // [n] fast-LFC table slot, -1 if the eval is not fast LFC
   const int32_t* lfc_rep;  // [lfc_nslots] eval whose leaf counters the table summarizes

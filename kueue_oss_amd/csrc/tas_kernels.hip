@@ -213,8 +213,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
   __shared__ DevTerm sh_terms[kEvalsPerBlock][2 * MAXT];
   __shared__ int64_t sh_wlead[kEvalsPerBlock][MAXT];  // leader value on each worker term's column
 
-  const int e0 = blockIdx.y * kEvalsPerBlock;
-  const int ne = min(kEvalsPerBlock, b.nfill - e0);
+  const int e0 = b.fill_chunks[2 * blockIdx.y];
+  const int ne = b.fill_chunks[2 * blockIdx.y + 1];
   if (threadIdx.x < ne) sh_ev[threadIdx.x] = b.evals[b.fill_ids[e0 + threadIdx.x]];
   __syncthreads();
   for (int e = 0; e < ne; e++) {
@@ -379,13 +379,59 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 
 // Staged variant (the batch requests at most NS distinct resource columns):
 // every thread loads its leaf's free/used words of those columns ONCE into
-// registers (static slots, ascending column order) and reuses them for all
-// kEvalsPerBlock evals; per-eval request terms are read with uniform
-// (scalar) loads.  Semantics identical to fill_leaves_kernel.
+// registers (static slots, ascending column order).  A block handles one
+// fill chunk: up to kEvalsPerBlock phase-1 classes with the same request
+// signature (worker/leader terms, overlay, simulateEmpty; the host groups
+// them), so CountInWithLimitingResource runs once per leaf and only the
+// per-eval masks (taints, nodeSelector) and slice parameters differ.
+// Semantics identical to fill_leaves_kernel.
+// Per-eval parameters of a fill chunk, staged in LDS once per block so the
+// per-eval loop has no dependent global loads (eval record -> taint row).
+struct FillEvalParams {
+  int32_t eid, taint_off, nsel, slice_size, slice_level, pad[3];
+  int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
+};
+constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
+constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
+
+// ExclusionStats of a fill block are counted in LDS and written as per-block
+// partials (DevBatch::fill_stats), summed by fill_stats_reduce_kernel: no
+// global atomics on a handful of hot addresses from every wave of the grid
+// (device-scope atomics from all XCDs serialize at the memory side).
+constexpr int kMaxFillStats = 64;  // 1 (nodeSelector) + taints + resource columns; more: global atomics
+
 template <int NS>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
-  const int e0 = blockIdx.y * kEvalsPerBlock;
-  const int ne = min(kEvalsPerBlock, b.nfill - e0);
+  __shared__ FillEvalParams sh_p[kEvalsPerBlock];
+  __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
+  __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  const bool lds_stats = b.nstat > 0;
+  for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
+  const int e0 = b.fill_chunks[2 * blockIdx.y];
+  const int ne = b.fill_chunks[2 * blockIdx.y + 1];
+  const bool stage_taints = b.num_profiles <= kStagedProfiles;
+  if (int(threadIdx.x) < ne) {
+    const int eid = b.fill_ids[e0 + threadIdx.x];
+    const DevEval& ev = b.evals[eid];
+    FillEvalParams& P = sh_p[threadIdx.x];
+    P.eid = eid;
+    P.taint_off = ev.taint_table;
+    P.nsel = ev.nsel;
+    P.slice_size = ev.slice_size;
+    P.slice_level = ev.slice_level;
+    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+      P.sel_col[k] = ev.sel_col[k];
+      P.sel_val[k] = ev.sel_val[k];
+    }
+  }
+  __syncthreads();
+  if (s.taint_profile && stage_taints) {
+    for (int i = threadIdx.x; i < ne * kStagedProfiles; i += kFillThreads) {
+      const int e = i / kStagedProfiles, p = i % kStagedProfiles;
+      sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_p[e].taint_off + p] : -1;
+    }
+  }
+  __syncthreads();
   const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
   const int N = s.N;
@@ -410,25 +456,105 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   const uint32_t fp = valid ? s.free_present[leaf] : 0u;
   const uint32_t up = valid ? s.usage_present[leaf] : 0u;
   const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
+  int32_t lab[kStagedLabels];
+#pragma unroll
+  for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
 
-  for (int e = 0; e < ne; e++) {
-    const int eid = uni(b.fill_ids[e0 + e]);
-    const DevEval& ev = b.evals[eid];
+  // ---- the chunk's request signature (first member): counts once per leaf ----
+  int32_t state0 = 0, swl0 = 0, ls0 = 0;
+  int lim0 = -1;
+  bool leader;
+  {
+    const DevEval& ev = b.evals[uni(b.fill_ids[e0])];
     const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
     const uint32_t rmask = uint32_t(uni(int32_t(ev.req_mask)));
     const uint32_t lmask = uint32_t(uni(int32_t(ev.lead_mask)));
     const int tb = uni(ev.term_begin), lb = uni(ev.lead_begin);
-    const int nsel = uni(ev.nsel);
     const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
-    const int32_t slice_size = uni(ev.slice_size), slice_level = uni(ev.slice_level);
-    const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
+    leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
+    if (valid) {
+      uint32_t pres = fp | (sim ? 0u : up);
+      int a_lo = 0, a_hi = 0;
+      if (aend > abeg) {
+        int lo = abeg, hi = aend;
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if (b.assumed[mid].leaf < leaf) lo = mid + 1;
+          else hi = mid;
+        }
+        a_lo = lo;
+        a_hi = lo;
+        while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
+          pres |= 1u << b.assumed[a_hi].col;
+          a_hi++;
+        }
+      }
+      int64_t cap[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        int64_t c = sim ? fr[k] : int64_t(uint64_t(fr[k]) - uint64_t(us[k]));
+        for (int a = a_lo; a < a_hi; a++)
+          if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+        cap[k] = c;
+      }
+      // CountInWithLimitingResource over the worker terms, ascending column order
+      auto count_slots = [&](uint32_t mask, int tbase, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
+        int32_t result = 0;
+        bool any = false, done = false;
+        int lim = -1;
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+          const int col = scol[k];
+          if (col >= 0 && ((mask >> col) & 1u) && !done) {
+            const DevTerm t = uni_term(b.terms[tbase + __popc(mask & ((1u << col) - 1u))]);
+            if (!((presm >> col) & 1u) && t.val != 0) {
+              lim = col;
+              result = 0;
+              any = true;
+              done = true;
+            } else {
+              int64_t c = cap[k];
+              if (sub_leader && ((lmask >> col) & 1u)) {
+                const DevTerm lt = uni_term(b.terms[lb + __popc(lmask & ((1u << col) - 1u))]);
+                c = int64_t(uint64_t(c) - uint64_t(lt.val));
+              }
+              int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
+              if (!any || cnt < result) {
+                result = cnt;
+                lim = col;
+                any = true;
+              }
+            }
+          }
+        }
+        *lim_out = lim;
+        return any ? result : 0;
+      };
+      state0 = count_slots(rmask, tb, pres, false, &lim0);
+      swl0 = state0;
+      if (leader) {
+        int dummy;
+        int32_t lc = count_slots(lmask, lb, pres, false, &dummy);
+        if (lc > 0) {
+          ls0 = 1;
+          swl0 = count_slots(rmask, tb, pres | lmask, true, &dummy);
+        }
+      }
+    }
+  }
+
+  for (int e = 0; e < ne; e++) {
+    const FillEvalParams& P = sh_p[e];
+    const int eid = uni(P.eid);
+    const int nsel = uni(P.nsel);
+    const int32_t slice_size = uni(P.slice_size), slice_level = uni(P.slice_level);
     int32_t state = 0, swl = 0, ls = 0;
     int kind = EX_NONE, id = -1;
     if (valid) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
-          int t = b.taint_table[uni(ev.taint_table) + prof];
+          int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(P.taint_off) + prof];
           if (t >= 0) {
             kind = EX_TAINT;
             id = t;
@@ -436,7 +562,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         }
         if (kind == EX_NONE) {
           for (int k = 0; k < nsel; k++) {
-            if (s.label_values[int64_t(uni(ev.sel_col[k])) * N + leaf] != uni(ev.sel_val[k])) {
+            const int col = uni(P.sel_col[k]);
+            int32_t v;
+            if (col < kStagedLabels) {
+              v = lab[0];
+#pragma unroll
+              for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+            } else {
+              v = s.label_values[int64_t(col) * N + leaf];
+            }
+            if (v != uni(P.sel_val[k])) {
               kind = EX_SELECTOR;
               break;
             }
@@ -444,77 +579,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         }
       }
       if (kind == EX_NONE) {
-        uint32_t pres = fp | (sim ? 0u : up);
-        int a_lo = 0, a_hi = 0;
-        if (aend > abeg) {
-          int lo = abeg, hi = aend;
-          while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (b.assumed[mid].leaf < leaf) lo = mid + 1;
-            else hi = mid;
-          }
-          a_lo = lo;
-          a_hi = lo;
-          while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
-            pres |= 1u << b.assumed[a_hi].col;
-            a_hi++;
-          }
-        }
-        int64_t cap[NS];
-#pragma unroll
-        for (int k = 0; k < NS; k++) {
-          int64_t c = sim ? fr[k] : int64_t(uint64_t(fr[k]) - uint64_t(us[k]));
-          for (int a = a_lo; a < a_hi; a++)
-            if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
-          cap[k] = c;
-        }
-        // CountInWithLimitingResource over the worker terms, ascending column order
-        auto count_slots = [&](uint32_t mask, int tbase, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
-          int32_t result = 0;
-          bool any = false, done = false;
-          int lim = -1;
-#pragma unroll
-          for (int k = 0; k < NS; k++) {
-            const int col = scol[k];
-            if (col >= 0 && ((mask >> col) & 1u) && !done) {
-              const DevTerm t = uni_term(b.terms[tbase + __popc(mask & ((1u << col) - 1u))]);
-              if (!((presm >> col) & 1u) && t.val != 0) {
-                lim = col;
-                result = 0;
-                any = true;
-                done = true;
-              } else {
-                int64_t c = cap[k];
-                if (sub_leader && ((lmask >> col) & 1u)) {
-                  const DevTerm lt = uni_term(b.terms[lb + __popc(lmask & ((1u << col) - 1u))]);
-                  c = int64_t(uint64_t(c) - uint64_t(lt.val));
-                }
-                int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
-                if (!any || cnt < result) {
-                  result = cnt;
-                  lim = col;
-                  any = true;
-                }
-              }
-            }
-          }
-          *lim_out = lim;
-          return any ? result : 0;
-        };
-        int lim = -1;
-        state = count_slots(rmask, tb, pres, false, &lim);
-        if (state == 0 && lim >= 0) {
+        state = state0;
+        swl = swl0;
+        ls = ls0;
+        if (state == 0 && lim0 >= 0) {
           kind = EX_RESOURCE;
-          id = lim;
-        }
-        swl = state;
-        if (leader) {
-          int dummy;
-          int32_t lc = count_slots(lmask, lb, pres, false, &dummy);
-          if (lc > 0) {
-            ls = 1;
-            swl = count_slots(rmask, tb, pres | lmask, true, &dummy);
-          }
+          id = lim0;
         }
       }
     }
@@ -535,13 +605,19 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       }
     }
     uint64_t selm = ballot(kind == EX_SELECTOR);
-    if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    if (lane == 0 && selm) {
+      if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
+      else atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    }
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
       int tid = __shfl(id, src, 64);
       uint64_t mm = ballot(kind == EX_TAINT && id == tid);
-      if (lane == 0) atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
+      if (lane == 0) {
+        if (lds_stats) atomicAdd(&sh_stats[e][1 + tid], __popcll(mm));
+        else atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
+      }
       tm &= ~mm;
     }
     uint64_t rm = ballot(kind == EX_RESOURCE);
@@ -549,9 +625,33 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       int src = __ffsll((unsigned long long)rm) - 1;
       int rid = __shfl(id, src, 64);
       uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
-      if (lane == 0) atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
+      if (lane == 0) {
+        if (lds_stats) atomicAdd(&sh_stats[e][1 + b.num_taints + rid], __popcll(mm));
+        else atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
+      }
       rm &= ~mm;
     }
+  }
+  if (lds_stats) {  // per-block partials [fill position][block][stat]
+    __syncthreads();
+    for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
+      const int e = i / b.nstat, k = i % b.nstat;
+      b.fill_stats[(int64_t(e0 + e) * gridDim.x + blockIdx.x) * b.nstat + k] = sh_stats[e][k];
+    }
+  }
+}
+
+// Sum the per-block ExclusionStats partials of every phase-1 class.
+__global__ __launch_bounds__(64) void fill_stats_reduce_kernel(DevBatch b, int nblk) {
+  const int f = blockIdx.x;
+  const int eid = b.fill_ids[f];
+  for (int k = threadIdx.x; k < b.nstat; k += blockDim.x) {
+    int32_t acc = 0;
+    const int32_t* p = b.fill_stats + int64_t(f) * nblk * b.nstat + k;
+    for (int j = 0; j < nblk; j++) acc += p[int64_t(j) * b.nstat];
+    if (k == 0) b.sel_counts[eid] = acc;
+    else if (k <= b.num_taints) b.taint_counts[int64_t(eid) * b.num_taints + (k - 1)] = acc;
+    else b.res_counts[int64_t(eid) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
   }
 }
 
