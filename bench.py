@@ -140,6 +140,7 @@ def main():
     t0 = time.perf_counter()
     stage_sum = {}
     host_sum = [0.0] * 4
+    dev_host_sum = {}
     counts = None
     for _ in range(a.steps):
         step()
@@ -147,6 +148,8 @@ def main():
         for k, v in snap.last_stage_times().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
         host_sum = [x + y for x, y in zip(host_sum, snap.last_profile())]
+        for k, v in snap.last_device_host_times().items():
+            dev_host_sum[k] = dev_host_sum.get(k, 0.0) + v
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -168,6 +171,7 @@ def main():
     traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config, st["fill_evals"])
     stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}
     host = dict(zip(("staging_ms", "eval_calls_ms", "decode_ms", "total_ms"), (round(x / a.steps, 3) for x in host_sum)))
+    host["eval_call_detail_ms"] = {k: round(v / a.steps, 3) for k, v in dev_host_sum.items()}
     if rank == 0:
         line = {
             "metric": "TAS placements/sec at 128k nodes (1/2/4/8 GPU); % HBM roofline",

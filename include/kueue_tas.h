@@ -213,6 +213,11 @@ int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
  * update, findLevelWithFitDomains).  ticks holds 8n values. */
 int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
+/* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request
+ * compile, [1] phase-1 classes, [2] uploads + launches, [3] wait for the
+ * select results, [4] entry packing + D2H, [5] copy-out.  Copies min(n, 6). */
+int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
+
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
  * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
@@ -247,6 +252,8 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
 int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
 /* kueue_tas_last_stage_times summed over the last run's batches. */
 int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n);
+/* kueue_tas_last_host_times summed over the last run's batches. */
+int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n);
 /* kueue_tas_last_eval_profile of the last device batch (diagnostics). */
 int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* kueue_tas_last_eval_ticks of the last device batch (diagnostics). */

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -130,6 +131,8 @@ struct kueue_tas_ctx {
   DevBuf<int32_t> d_fill_ids, d_pairs, d_leafsel;
   std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel, h_fill_chunks;
   DevBuf<int32_t> d_fill_chunks, d_fill_stats;
+  DevBuf<int32_t> d_overlay, d_tags;  // select's copy-on-write counters and ownership tags
+  int32_t tag_epoch = 0;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
   DevBuf<int32_t> d_rep_of, d_lfc_slot, d_lfc_rep, d_fast;
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
@@ -149,6 +152,7 @@ struct kueue_tas_ctx {
   std::vector<int32_t> last_entries;  // packed (leaf, count) pairs of the last batch
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
+  double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
 };
 
@@ -220,6 +224,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_fill_ids.release();
   c->d_fill_chunks.release();
   c->d_fill_stats.release();
+  c->d_overlay.release();
+  c->d_tags.release();
   c->d_leafsel.release();
   c->d_pairs.release();
   c->d_rep_of.release();
@@ -347,12 +353,22 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
   return KUEUE_TAS_OK;
 }
 
+static double wall_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
                       kueue_tas_eval_out* out, int64_t* offsets, int32_t* taint_counts, int32_t* res_counts,
                       float* ms, float* stage_ms) {
   const int32_t entry_cap = c->entry_cap;
   const DevSnap& s = c->snap;
+  double tm = wall_ms();
+  auto lap = [&](int k) {
+    const double t = wall_ms();
+    c->host_ms[k] += t - tm;
+    tm = t;
+  };
   // ---- compile requests to device form (magic numbers) ----
   HIPCHK(c, c->h_evals.ensure(n));
   size_t nterms = 0;
@@ -417,6 +433,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     e.nlead = (r.flags & KUEUE_TAS_F_LEADER) ? r.num_leader_req : 0;
     if (add_terms(r.leader_col, r.leader_val, e.nlead, &e.lead_mask)) return fail(c, KUEUE_TAS_EINVAL, "leader columns");
   }
+  lap(0);
   // ---- device buffers ----
   const int64_t SD = s.SD;
   const int64_t ctr_stride = 5 * SD;
@@ -427,6 +444,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, c->d_taint_table.ensure(std::max<size_t>(taint_table_len, 1)));
   HIPCHK(c, c->d_assumed.ensure(std::max<size_t>(num_assumed, 1)));
   HIPCHK(c, c->d_counters.ensure(size_t(n) * size_t(ctr_stride)));
+  HIPCHK(c, c->d_overlay.ensure(size_t(n) * size_t(ctr_stride)));
+  if (c->d_tags.n < size_t(n) * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
+    HIPCHK(c, c->d_tags.ensure(size_t(n) * size_t(SD)));
+    HIPCHK(c, hipMemsetAsync(c->d_tags.p, 0, c->d_tags.n * 4, c->stream));
+    c->tag_epoch = 0;
+  }
+  c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
   const size_t stats_len = n * nt + n * size_t(s.R) + n;
   HIPCHK(c, c->d_stats.ensure(stats_len));
@@ -458,6 +482,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.fill_stats = nullptr;
   b.ctr_stride = ctr_stride;
   b.counters = c->d_counters.p;
+  b.overlay = c->d_overlay.p;
+  b.tags = c->d_tags.p;
+  b.tag_epoch = c->tag_epoch;
   b.taint_counts = c->d_stats.p;
   b.res_counts = c->d_stats.p + n * nt;
   b.sel_counts = c->d_stats.p + n * nt + n * size_t(s.R);
@@ -546,13 +573,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (has_fast) c->h_lfc_rep.push_back(rep);
       for (int32_t m : mem) {
         const bool fast = has_fast && fast_lfc(c->h_evals.p[m]);
-        c->h_rep_of[size_t(m)] = fast ? rep : m;
+        c->h_rep_of[size_t(m)] = rep;  // select reads the class counters; mutations go to the eval's overlay
         c->h_lfc_slot[size_t(m)] = fast ? slot : -1;
         if (fast) c->h_fast.push_back(m);
         if (m != rep) {
-          auto& dst = fast ? stats_pairs : c->h_pairs;
-          dst.push_back(rep);
-          dst.push_back(fast ? ~m : m);  // ~m: exclusion stats only
+          stats_pairs.push_back(rep);
+          stats_pairs.push_back(~m);  // ~m: exclusion stats only
         }
       }
     }
@@ -579,6 +605,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     ncopy = int(c->h_pairs.size() / 2);  // pairs [0, ncopy) copy counters, the rest stats only
     c->h_pairs.insert(c->h_pairs.end(), stats_pairs.begin(), stats_pairs.end());
   }
+  lap(1);
   const int nslots = int(c->h_lfc_rep.size());
   const int nfast = int(c->h_fast.size());
   const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
@@ -734,7 +761,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_offsets.p, c->d_offsets.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_stats.p, c->d_stats.p, stats_len * 4, hipMemcpyDeviceToHost, c->stream));
+  lap(2);
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  lap(3);
   int32_t need = 0;
   for (size_t i = 0; i < n; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
   if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
@@ -750,6 +779,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  lap(4);
   memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
   if (KTAS_PROFILE) {
     const size_t base = c->last_prof.size();
@@ -771,6 +801,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   ms[1] += st[1] + st[2] + st[3];  // roll-up + replication + leaf partials
   ms[2] += st[4] + st[5];          // select + entry offsets
   ms[3] += st[6];
+  lap(5);
   return KUEUE_TAS_OK;
 }
 
@@ -787,6 +818,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   c->last_ticks.clear();
   c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
+  for (auto& v : c->host_ms) v = 0;
   const size_t chunk = size_t(c->max_batch);
   std::vector<int64_t> off;
   entry_offsets[0] = 0;
@@ -852,6 +884,12 @@ int kueue_tas_last_eval_ticks(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
 int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   if (!c || !ticks) return KUEUE_TAS_EINVAL;
   for (size_t i = 0; i < n * P_NCAT; i++) ticks[i] = i < c->last_prof.size() ? c->last_prof[i] : 0;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_host_times(kueue_tas_ctx* c, double* ms, int n) {
+  if (!c || !ms || n < 0) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < 6; k++) ms[k] = c->host_ms[k];
   return KUEUE_TAS_OK;
 }
 

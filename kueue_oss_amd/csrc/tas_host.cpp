@@ -858,6 +858,7 @@ struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
+  double dev_host_ms[6] = {};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[4] = {0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches
@@ -889,6 +890,7 @@ struct Evaluator {
           bool precompiled = false) {
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     for (auto& v : stage_ms) v = 0;
+    for (auto& v : dev_host_ms) v = 0;
     counts[0] = counts[1] = counts[2] = 0;
     stats[0] = stats[1] = stats[2] = stats[3] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
@@ -970,6 +972,9 @@ struct Evaluator {
       float st[KUEUE_TAS_NUM_STAGES];
       kueue_tas_last_stage_times(snap->ctx, st, KUEUE_TAS_NUM_STAGES);
       for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
+      double ht[6];
+      kueue_tas_last_host_times(snap->ctx, ht, 6);
+      for (int k = 0; k < 6; k++) dev_host_ms[k] += ht[k];
       int64_t st4[4];
       kueue_tas_last_stats(snap->ctx, st4);
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
@@ -1215,6 +1220,12 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
       }
     *result_hash = x;
   }
+  return 0;
+}
+
+int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n) {
+  if (!h || !h->ev || !ms || n < 0) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < 6; k++) ms[k] = h->ev->dev_host_ms[k];
   return 0;
 }
 

@@ -132,7 +132,7 @@ struct DevBatch {
   const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
   int32_t nfill;
   const int32_t* fill_chunks; // [nchunks][2] (start, len) into fill_ids: <= kEvalsPerBlock classes, one request signature
-  const int32_t* rep_of;   // [n] eval whose counters select reads (itself, or the class rep for fast LFC)
+  const int32_t* rep_of;   // [n] class rep whose phase-1 counters the eval reads
   const int32_t* lfc_slot; // [n] fast-LFC table slot, -1 if the eval is not fast LFC
   const int32_t* lfc_rep;  // [lfc_nslots] eval whose leaf counters the table summarizes
   int32_t lfc_nslots;
@@ -143,6 +143,9 @@ struct DevBatch {
   uint64_t* lfc_ovs;       // [nslots][nchunks] sum of the values >= kLfcBins - 1
   uint64_t* lfc_ovtot;     // [nslots]
   LfcJob* lfc_jobs;        // [n]
+  int32_t* overlay;        // [n][5][SD] phase-2 copy-on-write counters (select)
+  int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
+  int32_t tag_epoch;
   int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
 };
 

@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
     const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
     const int32_t sliceCount = go_div32(uni(ev.count), uni(ev.slice_size));
-    const int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    const int32_t* base = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
     int32_t state = 0, ss = 0, swl = 0, sswl = 0, ls = 0;
     if (valid) {
       state = base[gleaf];
@@ -944,7 +944,11 @@ struct Wave {
   int eid;
   int lane;
   bool leader, lfc, bf, unconstrained;
-  int32_t* ctr;    // counters of this eval
+  const int32_t* ctr;  // phase-1 counters of this eval's class (shared, read-only here)
+  int32_t* ov;         // private overlay [5][SD]
+  int32_t* tag;        // [SD] overlay ownership tags
+  int32_t my_tag;
+  bool dirty;
   int64_t SD;
   Key* lds;        // per-wave LDS buffer (list_cap keys)
   int cap;
@@ -960,7 +964,49 @@ struct Wave {
   int nblk;
   uint64_t prof[P_NCAT];
 
+  // Phase-2 mutations go to a private copy-on-write overlay (ov, tag ==
+  // my_tag marks the domains it holds) so evals of one phase-1 class share
+  // the class counters `ctr` read-only: no per-eval replication.  Until the
+  // first mutation (`dirty`, wave-uniform: findLevelWithFitDomains never
+  // mutates) reads go straight to ctr.
   __device__ int32_t get(Field f, int g) const {
+    if (!leader) {
+      if (f == F_LS) return 0;
+      if (f == F_SWL) f = F_STATE;
+      if (f == F_SSWL) f = F_SLICE;
+    }
+    const int64_t o = int64_t(f) * SD + g;
+    if (!dirty) return ctr[o];
+    const int32_t shared = ctr[o], own = ov[o];
+    return tag[g] == my_tag ? own : shared;
+  }
+  // first write of a domain: copy its counters into the overlay
+  __device__ void own(int g) {
+    if (tag[g] != my_tag) {
+      const int nf = leader ? 5 : 2;
+      for (int f = 0; f < nf; f++) ov[int64_t(f) * SD + g] = ctr[int64_t(f) * SD + g];
+      tag[g] = my_tag;
+    }
+  }
+  // Stored by every lane (see file header).
+  __device__ void set(Field f, int g, int32_t v) {
+    if (!leader) {
+      if (f == F_LS || f == F_SWL || f == F_SSWL) return;
+    }
+    dirty = true;
+    own(g);
+    ov[int64_t(f) * SD + g] = v;
+  }
+  // Stored by one lane for a domain only it handles in a lane-parallel pass;
+  // readers on other lanes come after a fence (callers have set dirty).
+  __device__ void set_lane(Field f, int g, int32_t v) {
+    if (!leader && (f == F_LS || f == F_SWL || f == F_SSWL)) return;
+    this->own(g);
+    ov[g + int64_t(f) * SD] = v;  // lane-private
+  }
+  // Reads of domains this eval has not mutated (the children a walk is
+  // about to sort: every domain has one parent and is walked once).
+  __device__ int32_t get_clean(Field f, int g) const {
     if (!leader) {
       if (f == F_LS) return 0;
       if (f == F_SWL) f = F_STATE;
@@ -968,18 +1014,9 @@ struct Wave {
     }
     return ctr[int64_t(f) * SD + g];
   }
-  // Stored by every lane (see file header).
-  __device__ void set(Field f, int g, int32_t v) {
-    if (!leader) {
-      if (f == F_LS || f == F_SWL || f == F_SSWL) return;
-    }
-    ctr[int64_t(f) * SD + g] = v;
-  }
-  // Stored by one lane for a domain only it handles in a lane-parallel pass;
-  // readers on other lanes come after a fence.
-  __device__ void set_lane(Field f, int g, int32_t v) {
-    if (!leader && (f == F_LS || f == F_SWL || f == F_SSWL)) return;
-    ctr[g + int64_t(f) * SD] = v;  // lane-private
+  __device__ Key kplain_clean(int g) const {
+    int idx = g - s->level_off[level_of(g)];
+    return key_plain(lfc, get_clean(F_SLICE, g), get_clean(F_STATE, g), idx);
   }
   __device__ Key kplain(int g) const {
     int idx = g - s->level_off[level_of(g)];
@@ -1434,8 +1471,8 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      ss[u] = w.get(F_SLICE, g[u]);
-      st[u] = w.get(F_STATE, g[u]);
+      ss[u] = w.get_clean(F_SLICE, g[u]);
+      st[u] = w.get_clean(F_STATE, g[u]);
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
@@ -1683,7 +1720,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
 #pragma unroll
       for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
 #pragma unroll
-      for (int u = 0; u < kU; u++) v[u] = w.get(F_SLICE, g[u]);
+      for (int u = 0; u < kU; u++) v[u] = w.get_clean(F_SLICE, g[u]);
 #pragma unroll
       for (int u = 0; u < kU; u++) {
         const bool keep = base + u * kWave + w.lane < n && v[u] > 0;
@@ -1697,7 +1734,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
     n = m;
   }
   if (n <= w.cap) {
-    for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain(gids[i]);
+    for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain_clean(gids[i]);
     wave_sync();
     {
       ProfScope ps_(w, P_LDS_SORT);
@@ -1732,7 +1769,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   }
   // longer than the LDS: merge-sort the keys in global memory once (O(n log n)),
   // then walk them in order
-  for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = w.kplain(gids[i]);
+  for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = w.kplain_clean(gids[i]);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   global_sort(w, w.gkeys, w.gkeys2, n);
   if (sliceRecompute > 1) {
@@ -2551,6 +2588,10 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.bf = !w.lfc;
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
   w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
+  w.ov = b.overlay + int64_t(eid) * b.ctr_stride;
+  w.tag = b.tags + int64_t(eid) * s.SD;
+  w.my_tag = b.tag_epoch;
+  w.dirty = false;
   w.SD = s.SD;
   w.lds = lds_all + int64_t(wave) * b.list_cap;
   w.cap = b.list_cap;
@@ -2594,6 +2635,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
     r = find_level(w, w.listA, &nres, &fitLevel, o, ent, ecap);
   }
   const uint64_t t_found = wall_clock64();
+  w.dirty = true;  // the descent mutates (overlay)
   if (r == 0) {
     const int L = s.L;
     const int32_t leaderCount = w.leader ? 1 : 0;

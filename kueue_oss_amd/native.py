@@ -47,10 +47,10 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
+    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
 ]
 
 
@@ -95,6 +95,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_stage_times.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int]
     lib.kueue_tas_host_last_eval_profile.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
+    lib.kueue_tas_host_last_device_host_times.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
@@ -201,6 +202,14 @@ class TASFlavorSnapshot:
         buf = (ctypes.c_int32 * (8 * n))()
         self._lib.kueue_tas_host_last_eval_profile(self._h, buf, n)
         return [dict(zip(self.PROF, buf[8 * i: 8 * i + 8])) for i in range(n)]
+
+    DEVICE_HOST = ("compile", "classes", "enqueue", "wait", "pack_d2h", "copy_out")
+
+    def last_device_host_times(self):
+        """Host ms inside the device layer over the last run, dict keyed by DEVICE_HOST."""
+        ms = (ctypes.c_double * 6)()
+        self._lib.kueue_tas_host_last_device_host_times(self._h, ms, 6)
+        return dict(zip(self.DEVICE_HOST, list(ms)))
 
     def last_profile(self):
         """Host wall ms of the last run_compiled: (staging, eval calls, decode, total)."""

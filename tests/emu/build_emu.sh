@@ -14,9 +14,11 @@ CSRC="$ROOT/kueue_oss_amd/csrc"
 #   counter stores of phase 2 in lockstep; fibers do not, so every store of a
 #   domain counter becomes a wave-synchronization point here.
 sed -e 's/extern __shared__ Key lds_all\[\];/Key* lds_all = static_cast<Key*>(emu::dynamic_lds());/' \
-    -e 's/^    ctr\[int64_t(f) \* SD + g\] = v;/    emu::wave_barrier(); ctr[int64_t(f) * SD + g] = v; emu::wave_barrier();/' \
+    -e 's/^    own(g);$/    emu::wave_barrier(); own(g);/' \
+    -e 's/^    ov\[int64_t(f) \* SD + g\] = v;/    ov[int64_t(f) * SD + g] = v; emu::wave_barrier();/' \
   "$CSRC/tas_kernels.hip" > "$OUT/src/tas_kernels.hip"
-grep -q 'emu::wave_barrier(); ctr' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
+grep -q 'emu::wave_barrier(); own(g);' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
+grep -q '= v; emu::wave_barrier();' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
 cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$OUT/src/"
 sed 's#"../../include/kueue_tas.h"#"kueue_tas.h"#' "$CSRC/tas_internal.h" > "$OUT/src/tas_internal.h"
 cp "$ROOT/include/kueue_tas.h" "$OUT/src/"
