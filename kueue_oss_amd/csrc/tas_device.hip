@@ -110,15 +110,12 @@ struct kueue_tas_ctx {
   bool loaded = false;
   DevSnap snap{};
   int maxD = 0;
+  int rack_fanout = 0;  // see kueue_tas_snapshot_load
   std::vector<int32_t> h_level_sizes;
   DevBuf<int32_t> d_child_off, d_id_rank, d_taint_profile, d_labels;
   DevBuf<int64_t> d_free, d_usage;
   DevBuf<uint32_t> d_free_present, d_usage_present;
   // batch
-  DevBuf<DevEval> d_evals;
-  DevBuf<DevTerm> d_terms;
-  DevBuf<int32_t> d_taint_table;
-  DevBuf<kueue_tas_assumed> d_assumed;
   DevBuf<int32_t> d_counters;
   DevBuf<int32_t> d_stats;  // taint counts | res counts | sel counts
   DevBuf<kueue_tas_eval_out> d_out;
@@ -128,23 +125,22 @@ struct kueue_tas_ctx {
   DevBuf<int64_t> d_offsets;
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
-  DevBuf<int32_t> d_fill_ids, d_pairs, d_leafsel;
-  std::vector<int32_t> h_fill_ids, h_pairs, h_leafsel, h_fill_chunks;
-  DevBuf<int32_t> d_fill_chunks, d_fill_stats;
+  DevBuf<int32_t> d_fill_stats;
+  HostBuf<uint8_t> h_stage;  // one pinned upload per batch: evals, terms, tables, index lists
+  DevBuf<uint8_t> d_stage;
+  // phase-1 class computation scratch (kept to avoid reallocation)
+  std::vector<int32_t> cls_rep, cls_sig, cls_of, sig_rep, cls_next, sig_next, cls_fastrep, cls_slot, cls_order;
+  std::unordered_map<uint64_t, int32_t> cls_head, sig_head;
   DevBuf<int32_t> d_overlay, d_tags;  // select's copy-on-write counters and ownership tags
   int32_t tag_epoch = 0;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
-  DevBuf<int32_t> d_rep_of, d_lfc_slot, d_lfc_rep, d_fast;
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
   DevBuf<uint64_t> d_lfc_ovs, d_lfc_ovtot;
   DevBuf<LfcJob> d_lfc_jobs;
   DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
   std::vector<int32_t> last_prof;
-  std::vector<int32_t> h_rep_of, h_lfc_slot, h_lfc_rep, h_fast;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
-  HostBuf<DevEval> h_evals;
-  HostBuf<DevTerm> h_terms;
   HostBuf<kueue_tas_eval_out> h_out;
   HostBuf<int64_t> h_offsets;
   HostBuf<int32_t> h_stats;
@@ -208,10 +204,6 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_usage.release();
   c->d_free_present.release();
   c->d_usage_present.release();
-  c->d_evals.release();
-  c->d_terms.release();
-  c->d_taint_table.release();
-  c->d_assumed.release();
   c->d_counters.release();
   c->d_stats.release();
   c->d_out.release();
@@ -221,17 +213,11 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_offsets.release();
   c->d_packed.release();
   c->d_partials.release();
-  c->d_fill_ids.release();
-  c->d_fill_chunks.release();
   c->d_fill_stats.release();
+  c->h_stage.release();
+  c->d_stage.release();
   c->d_overlay.release();
   c->d_tags.release();
-  c->d_leafsel.release();
-  c->d_pairs.release();
-  c->d_rep_of.release();
-  c->d_lfc_slot.release();
-  c->d_lfc_rep.release();
-  c->d_fast.release();
   c->d_lfc_ch.release();
   c->d_lfc_cp.release();
   c->d_lfc_tot.release();
@@ -239,8 +225,6 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_ovtot.release();
   c->d_lfc_jobs.release();
   c->d_prof.release();
-  c->h_evals.release();
-  c->h_terms.release();
   c->h_out.release();
   c->h_offsets.release();
   c->h_stats.release();
@@ -324,6 +308,19 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
     HIPCHK(c, hipMemcpy(c->d_id_rank.p, ranks.data(), size_t(off) * 4, hipMemcpyHostToDevice));
     s.id_rank = c->d_id_rank.p;
   }
+  // leaves' parents with a uniform power-of-two fan-out F <= 64 in leaf order:
+  // the staged fill rolls them up itself (one wave holds whole parents)
+  c->rack_fanout = 0;
+  if (s.L >= 2 && d->level_sizes[s.L - 2] > 0 && d->child_offsets) {
+    const int P = d->level_sizes[s.L - 2];
+    const int F = s.N / P;
+    if (F > 0 && F <= kWave && (F & (F - 1)) == 0 && int64_t(F) * P == s.N) {
+      const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
+      bool ok = true;
+      for (int p = 0; p <= P && ok; p++) ok = co[p] == p * F;
+      if (ok) c->rack_fanout = F;
+    }
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap = s;
   c->maxD = maxD;
@@ -369,8 +366,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     c->host_ms[k] += t - tm;
     tm = t;
   };
-  // ---- compile requests to device form (magic numbers) ----
-  HIPCHK(c, c->h_evals.ensure(n));
+  // ---- layout of the single pinned upload (evals, terms, tables, index lists) ----
   size_t nterms = 0;
   int maxt = 1;
   for (size_t i = 0; i < n; i++) {
@@ -385,11 +381,27 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     nterms += size_t(r.num_req + r.num_leader_req);
     maxt = std::max(maxt, std::max(r.num_req, r.num_leader_req));
   }
-  HIPCHK(c, c->h_terms.ensure(std::max<size_t>(nterms, 1)));
+  size_t stage_bytes = 0;
+  auto seg = [&](size_t bytes) {
+    const size_t o = stage_bytes;
+    stage_bytes += (bytes + 255) / 256 * 256;
+    return o;
+  };
+  const size_t o_evals = seg(n * sizeof(DevEval)), o_terms = seg(nterms * sizeof(DevTerm));
+  const size_t o_taint = seg(taint_table_len * 4), o_assumed = seg(num_assumed * sizeof(kueue_tas_assumed));
+  const size_t o_fill = seg(n * 4), o_fchunks = seg(n * 8), o_pairs = seg(n * 8), o_rep = seg(n * 4);
+  const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
+  const size_t o_pidx = seg(n * 4);
+  HIPCHK(c, c->h_stage.ensure(stage_bytes));
+  HIPCHK(c, c->d_stage.ensure(stage_bytes));
+  uint8_t* hs = c->h_stage.p;
+  DevEval* hev = reinterpret_cast<DevEval*>(hs + o_evals);
+  DevTerm* hterms = reinterpret_cast<DevTerm*>(hs + o_terms);
+  // ---- compile requests to device form (magic numbers) ----
   size_t tp = 0;
   for (size_t i = 0; i < n; i++) {
     const auto& r = reqs[i];
-    DevEval& e = c->h_evals.p[i];
+    DevEval& e = hev[i];
     memset(&e, 0, sizeof e);
     e.flags = r.flags;
     e.count = r.count;
@@ -415,7 +427,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       for (int k = 0; k < cnt; k++) {
         if (cols[k] < 0 || cols[k] >= s.R || cols[k] <= prev) return -1;
         prev = cols[k];
-        DevTerm& t = c->h_terms.p[tp++];
+        DevTerm& t = hterms[tp++];
         memset(&t, 0, sizeof t);
         t.col = cols[k];
         t.val = vals[k];
@@ -433,16 +445,212 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     e.nlead = (r.flags & KUEUE_TAS_F_LEADER) ? r.num_leader_req : 0;
     if (add_terms(r.leader_col, r.leader_val, e.nlead, &e.lead_mask)) return fail(c, KUEUE_TAS_EINVAL, "leader columns");
   }
+  if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
+  if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
   lap(0);
+
+  // Phase-1 classes: evals with identical phase-1 inputs (request terms,
+  // masks, overlay, slice parameters) get identical counters; phase 1 runs
+  // once per class (its representative).  Every member's select reads the
+  // class counters and keeps its mutations in a private overlay; duplicates
+  // only get the rep's exclusion stats.  A class's request signature (terms,
+  // overlay, simulateEmpty, leader) decides which classes share a fill chunk.
+  const int32_t P = c->num_profiles;
+  auto taint_row = [&](const DevEval& e) -> const int32_t* {
+    return (taint_table && size_t(e.taint_table) + size_t(P) <= taint_table_len) ? taint_table + e.taint_table
+                                                                                  : nullptr;
+  };
+  auto sig_hash = [&](const DevEval& e) {
+    uint64_t h = 1469598103934665603ull;
+    auto add = [&](uint64_t v) {
+      h ^= v;
+      h *= 1099511628211ull;
+      h ^= h >> 31;
+    };
+    add(e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY));
+    add(uint64_t(uint32_t(e.nreq)) | (uint64_t(uint32_t(e.nlead)) << 32));
+    for (int k = 0; k < e.nreq + e.nlead; k++) {
+      const DevTerm& t = hterms[k < e.nreq ? e.term_begin + k : e.lead_begin + (k - e.nreq)];
+      add(uint64_t(uint32_t(t.col)));
+      add(uint64_t(t.val));
+    }
+    for (int a = e.assumed_begin; a < e.assumed_end; a++) {
+      add(uint64_t(uint32_t(assumed[a].leaf)) | (uint64_t(uint32_t(assumed[a].col)) << 32));
+      add(uint64_t(assumed[a].value));
+    }
+    return h;
+  };
+  auto same_sig = [&](const DevEval& x, const DevEval& y) {
+    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
+    if (x.nreq != y.nreq || x.nlead != y.nlead) return false;
+    for (int k = 0; k < x.nreq + x.nlead; k++) {
+      const DevTerm& a = hterms[k < x.nreq ? x.term_begin + k : x.lead_begin + (k - x.nreq)];
+      const DevTerm& b2 = hterms[k < y.nreq ? y.term_begin + k : y.lead_begin + (k - y.nreq)];
+      if (a.col != b2.col || a.val != b2.val) return false;
+    }
+    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
+    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
+      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
+      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
+      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
+    }
+    return true;
+  };
+  auto mask_hash = [&](const DevEval& e) {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    auto add = [&](uint64_t v) {
+      h ^= v;
+      h *= 1099511628211ull;
+      h ^= h >> 29;
+    };
+    add(uint64_t(uint32_t(e.slice_size)) | (uint64_t(uint32_t(e.slice_level)) << 32));
+    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) add(uint64_t(uint32_t(e.ssal[l])));
+    add(uint64_t(uint32_t(e.nsel)));
+    for (int k = 0; k < e.nsel; k++) add(uint64_t(uint32_t(e.sel_col[k])) | (uint64_t(uint32_t(e.sel_val[k])) << 32));
+    if (const int32_t* row = taint_row(e))
+      for (int p = 0; p < P; p++) add(uint64_t(uint32_t(row[p])));
+    return h;
+  };
+  auto same_mask = [&](const DevEval& x, const DevEval& y) {
+    if (x.slice_size != y.slice_size || x.slice_level != y.slice_level || x.nsel != y.nsel) return false;
+    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++)
+      if (x.ssal[l] != y.ssal[l]) return false;
+    for (int k = 0; k < x.nsel; k++)
+      if (x.sel_col[k] != y.sel_col[k] || x.sel_val[k] != y.sel_val[k]) return false;
+    const int32_t *rx = taint_row(x), *ry = taint_row(y);
+    if ((rx == nullptr) != (ry == nullptr)) return false;
+    return rx == nullptr || rx == ry || memcmp(rx, ry, size_t(P) * 4) == 0;
+  };
+  auto fast_lfc = [&](const DevEval& e) {
+    return (e.flags & KUEUE_TAS_F_LFC) != 0 &&
+           (e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_REQUIRED | KUEUE_TAS_F_MULTILAYER)) == 0 &&
+           e.requested_level == s.L - 1 && e.slice_level == s.L - 1 && e.slice_size == 1 && e.count >= 0 && s.N > 0;
+  };
+  int32_t* h_fill = reinterpret_cast<int32_t*>(hs + o_fill);
+  int32_t* h_fchunks = reinterpret_cast<int32_t*>(hs + o_fchunks);
+  int32_t* h_pairs = reinterpret_cast<int32_t*>(hs + o_pairs);
+  int32_t* h_rep = reinterpret_cast<int32_t*>(hs + o_rep);
+  int32_t* h_slot = reinterpret_cast<int32_t*>(hs + o_slot);
+  int32_t* h_lrep = reinterpret_cast<int32_t*>(hs + o_lrep);
+  int32_t* h_fast = reinterpret_cast<int32_t*>(hs + o_fast);
+  int32_t* h_leafsel = reinterpret_cast<int32_t*>(hs + o_leafsel);
+  int32_t* h_pidx = reinterpret_cast<int32_t*>(hs + o_pidx);  // eval -> row of its leaf partials, -1
+  int nfill = 0, npairs = 0, nslots = 0, nfast = 0, nfchunks = 0, nleafsel = 0;
+  {
+    // classes: open hash chains on the 64-bit (signature, mask) hash, exact compare on the rep
+    std::vector<int32_t>& cls_rep = c->cls_rep;    // first member of each class
+    std::vector<int32_t>& cls_sig = c->cls_sig;    // signature id of each class
+    std::vector<int32_t>& cls_of = c->cls_of;      // class of each eval
+    std::vector<int32_t>& sig_rep = c->sig_rep;    // first eval of each signature
+    cls_rep.clear();
+    cls_sig.clear();
+    sig_rep.clear();
+    cls_of.assign(n, -1);
+    std::unordered_map<uint64_t, int32_t>& cls_head = c->cls_head;
+    std::unordered_map<uint64_t, int32_t>& sig_head = c->sig_head;
+    cls_head.clear();
+    sig_head.clear();
+    std::vector<int32_t>& cls_next = c->cls_next;  // chain of classes with the same hash
+    std::vector<int32_t>& sig_next = c->sig_next;
+    cls_next.clear();
+    sig_next.clear();
+    for (size_t i = 0; i < n; i++) {
+      const DevEval& e = hev[i];
+      const uint64_t hs1 = sig_hash(e);
+      const uint64_t hc = hs1 ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
+      int32_t k = -1;
+      auto it = cls_head.find(hc);
+      if (it != cls_head.end())
+        for (int32_t q = it->second; q >= 0; q = cls_next[size_t(q)]) {
+          const DevEval& r = hev[cls_rep[size_t(q)]];
+          if (same_sig(e, r) && same_mask(e, r)) {
+            k = q;
+            break;
+          }
+        }
+      if (k < 0) {
+        k = int32_t(cls_rep.size());
+        cls_rep.push_back(int32_t(i));
+        cls_next.push_back(it != cls_head.end() ? it->second : -1);
+        cls_head[hc] = k;
+        int32_t sg = -1;
+        auto si = sig_head.find(hs1);
+        if (si != sig_head.end())
+          for (int32_t q = si->second; q >= 0; q = sig_next[size_t(q)])
+            if (same_sig(e, hev[sig_rep[size_t(q)]])) {
+              sg = q;
+              break;
+            }
+        if (sg < 0) {
+          sg = int32_t(sig_rep.size());
+          sig_rep.push_back(int32_t(i));
+          sig_next.push_back(si != sig_head.end() ? si->second : -1);
+          sig_head[hs1] = sg;
+        }
+        cls_sig.push_back(sg);
+      }
+      cls_of[i] = k;
+    }
+    const int ncls = int(cls_rep.size());
+    // representative: the first fast-LFC member if any (its class gets an LFC table slot)
+    std::vector<int32_t>& rep = c->cls_fastrep;
+    rep.assign(size_t(ncls), -1);
+    for (size_t i = 0; i < n; i++) {
+      const int32_t k = cls_of[i];
+      if (rep[size_t(k)] < 0 && fast_lfc(hev[i])) rep[size_t(k)] = int32_t(i);
+    }
+    std::vector<int32_t>& slot_of = c->cls_slot;
+    slot_of.assign(size_t(ncls), -1);
+    for (int k = 0; k < ncls; k++) {
+      if (rep[size_t(k)] >= 0) {
+        slot_of[size_t(k)] = nslots;
+        h_lrep[nslots++] = rep[size_t(k)];
+      } else {
+        rep[size_t(k)] = cls_rep[size_t(k)];
+      }
+    }
+    for (size_t i = 0; i < n; i++) {
+      const int32_t k = cls_of[i], r = rep[size_t(k)];
+      const bool fast = slot_of[size_t(k)] >= 0 && fast_lfc(hev[i]);
+      h_rep[i] = r;
+      h_slot[i] = fast ? slot_of[size_t(k)] : -1;
+      if (fast) h_fast[nfast++] = int32_t(i);
+      if (int32_t(i) != r) {
+        h_pairs[2 * npairs] = r;
+        h_pairs[2 * npairs + 1] = ~int32_t(i);  // exclusion stats only
+        npairs++;
+      }
+      h_pidx[i] = -1;
+      if (hev[i].requested_level == s.L - 1 && !fast) {
+        h_pidx[i] = nleafsel;
+        h_leafsel[nleafsel++] = int32_t(i);
+      }
+    }
+    // fill chunks: classes ordered by signature, <= kEvalsPerFillBlock per chunk, one signature each
+    std::vector<int32_t>& order = c->cls_order;
+    order.resize(size_t(ncls));
+    for (int k = 0; k < ncls; k++) order[size_t(k)] = k;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b2) { return cls_sig[size_t(a)] < cls_sig[size_t(b2)]; });
+    for (int k = 0; k < ncls; k++) h_fill[k] = rep[size_t(order[size_t(k)])];
+    nfill = ncls;
+    for (int k = 0; k < ncls;) {
+      int e = k + 1;
+      while (e < ncls && e - k < kEvalsPerFillBlock && cls_sig[size_t(order[size_t(e)])] == cls_sig[size_t(order[size_t(k)])])
+        e++;
+      h_fchunks[2 * nfchunks] = k;
+      h_fchunks[2 * nfchunks + 1] = e - k;
+      nfchunks++;
+      k = e;
+    }
+  }
+  lap(1);
   // ---- device buffers ----
   const int64_t SD = s.SD;
   const int64_t ctr_stride = 5 * SD;
   int64_t lcap = int64_t(c->maxD) * 2 + 64;
   const int64_t scratch_stride = 6 * lcap;
-  HIPCHK(c, c->d_evals.ensure(n));
-  HIPCHK(c, c->d_terms.ensure(std::max<size_t>(nterms, 1)));
-  HIPCHK(c, c->d_taint_table.ensure(std::max<size_t>(taint_table_len, 1)));
-  HIPCHK(c, c->d_assumed.ensure(std::max<size_t>(num_assumed, 1)));
+  const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
   HIPCHK(c, c->d_counters.ensure(size_t(n) * size_t(ctr_stride)));
   HIPCHK(c, c->d_overlay.ensure(size_t(n) * size_t(ctr_stride)));
   if (c->d_tags.n < size_t(n) * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
@@ -457,29 +665,31 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, c->d_out.ensure(n));
   HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));  // per-eval regions, packed after select
   HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
+  HIPCHK(c, c->d_lfc_jobs.ensure(n));
+  HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_cp.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
+  HIPCHK(c, c->d_lfc_ovs.ensure(size_t(std::max(nslots * nchunks, 1))));
+  HIPCHK(c, c->d_lfc_ovtot.ensure(size_t(std::max(nslots, 1))));
+  const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
+  HIPCHK(c, c->d_partials.ensure(size_t(std::max(nleafsel, 1)) * size_t(std::max(nblk, 1))));
 
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_evals.p, c->h_evals.p, n * sizeof(DevEval), hipMemcpyHostToDevice, c->stream));
-  if (nterms)
-    HIPCHK(c, hipMemcpyAsync(c->d_terms.p, c->h_terms.p, nterms * sizeof(DevTerm), hipMemcpyHostToDevice, c->stream));
-  if (taint_table_len)
-    HIPCHK(c, hipMemcpyAsync(c->d_taint_table.p, taint_table, taint_table_len * 4, hipMemcpyHostToDevice, c->stream));
-  if (num_assumed)
-    HIPCHK(c, hipMemcpyAsync(c->d_assumed.p, assumed, num_assumed * sizeof(kueue_tas_assumed), hipMemcpyHostToDevice,
-                             c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, stage_bytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, stats_len * 4, c->stream));
-
+  uint8_t* ds = c->d_stage.p;
   DevBatch b{};
-  b.evals = c->d_evals.p;
-  b.terms = c->d_terms.p;
-  b.taint_table = c->d_taint_table.p;
-  b.assumed = c->d_assumed.p;
+  b.evals = reinterpret_cast<const DevEval*>(ds + o_evals);
+  b.terms = reinterpret_cast<const DevTerm*>(ds + o_terms);
+  b.taint_table = reinterpret_cast<const int32_t*>(ds + o_taint);
+  b.assumed = reinterpret_cast<const kueue_tas_assumed*>(ds + o_assumed);
   b.n = int32_t(n);
   b.num_taints = int32_t(nt);
   b.num_profiles = c->num_profiles;
   b.nstat = 0;
   b.nstat_R = s.R;
   b.fill_stats = nullptr;
+  b.rack_fanout = 0;
   b.ctr_stride = ctr_stride;
   b.counters = c->d_counters.p;
   b.overlay = c->d_overlay.p;
@@ -494,140 +704,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.scratch_stride = scratch_stride;
   b.scratch = c->d_scratch.p;
   b.list_cap = c->list_cap;
-  b.nblk = (s.N + 255) / 256 * 4;  // one partial per 64-leaf wave
-  HIPCHK(c, c->d_partials.ensure(n * size_t(std::max(b.nblk, 1))));
+  b.nblk = nblk;
   b.partials = c->d_partials.p;
-
-  // Phase-1 classes: evals with identical phase-1 inputs (request terms,
-  // masks, overlay, slice parameters, partial parameters) get identical
-  // counters; phase 1 runs once per class.  Fast-LFC members (LfcJob,
-  // tas_internal.h) read the class rep's counters in place (the rep is a
-  // fast-LFC member when the class has one, so its counters are never
-  // mutated); other duplicates get a replicated private copy.
-  c->h_fill_ids.clear();
-  c->h_pairs.clear();
-  c->h_rep_of.assign(n, 0);
-  c->h_lfc_slot.assign(n, -1);
-  c->h_lfc_rep.clear();
-  c->h_fast.clear();
-  int ncopy = 0;
-  {
-    auto fast_lfc = [&](const DevEval& e) {
-      return (e.flags & KUEUE_TAS_F_LFC) != 0 &&
-             (e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_REQUIRED | KUEUE_TAS_F_MULTILAYER)) == 0 &&
-             e.requested_level == s.L - 1 && e.slice_level == s.L - 1 && e.slice_size == 1 && e.count >= 0 &&
-             s.N > 0;
-    };
-    std::unordered_map<std::string, int32_t> cls, sigs;
-    cls.reserve(n * 2);
-    std::vector<std::vector<int32_t>> members;
-    std::vector<int32_t> class_sig;  // request signature of each class (fill chunks share counts)
-    std::string key, sig;
-    for (size_t i = 0; i < n; i++) {
-      const DevEval& e = c->h_evals.p[i];
-      key.clear();
-      auto put = [&](const void* p, size_t len) { key.append(static_cast<const char*>(p), len); };
-      uint32_t f = e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY);
-      put(&f, 4);
-      int32_t hdr[2] = {e.slice_size, e.slice_level};
-      put(hdr, sizeof hdr);
-      put(e.ssal, sizeof e.ssal);
-      put(&e.nsel, 4);
-      put(e.sel_col, 4 * size_t(e.nsel));
-      put(e.sel_val, 4 * size_t(e.nsel));
-      if (taint_table && size_t(e.taint_table) + size_t(c->num_profiles) <= taint_table_len)
-        put(taint_table + e.taint_table, 4 * size_t(c->num_profiles));
-      const size_t sig_begin = key.size();
-      put(&f, 4);
-      int32_t nt2[2] = {e.nreq, e.nlead};
-      put(nt2, sizeof nt2);
-      for (int k = 0; k < e.nreq + e.nlead; k++) {
-        const DevTerm& t = c->h_terms.p[(k < e.nreq ? e.term_begin + k : e.lead_begin + (k - e.nreq))];
-        put(&t.col, 4);
-        put(&t.val, 8);
-      }
-      for (int a = e.assumed_begin; a < e.assumed_end; a++) put(&assumed[a], sizeof(kueue_tas_assumed));
-      auto it = cls.find(key);
-      if (it == cls.end()) {
-        cls.emplace(key, int32_t(members.size()));
-        members.push_back({int32_t(i)});
-        sig.assign(key, sig_begin, std::string::npos);
-        auto si = sigs.find(sig);
-        if (si == sigs.end()) si = sigs.emplace(sig, int32_t(sigs.size())).first;
-        class_sig.push_back(si->second);
-      } else {
-        members[size_t(it->second)].push_back(int32_t(i));
-      }
-    }
-    std::vector<int32_t> stats_pairs;
-    for (const auto& mem : members) {
-      int32_t rep = mem[0];
-      for (int32_t m : mem)
-        if (fast_lfc(c->h_evals.p[m])) {
-          rep = m;
-          break;
-        }
-      c->h_fill_ids.push_back(rep);
-      const bool has_fast = fast_lfc(c->h_evals.p[rep]);
-      const int32_t slot = has_fast ? int32_t(c->h_lfc_rep.size()) : -1;
-      if (has_fast) c->h_lfc_rep.push_back(rep);
-      for (int32_t m : mem) {
-        const bool fast = has_fast && fast_lfc(c->h_evals.p[m]);
-        c->h_rep_of[size_t(m)] = rep;  // select reads the class counters; mutations go to the eval's overlay
-        c->h_lfc_slot[size_t(m)] = fast ? slot : -1;
-        if (fast) c->h_fast.push_back(m);
-        if (m != rep) {
-          stats_pairs.push_back(rep);
-          stats_pairs.push_back(~m);  // ~m: exclusion stats only
-        }
-      }
-    }
-    // fill chunks: classes ordered by request signature, <= kEvalsPerFillBlock per chunk, one signature each
-    {
-      std::vector<int32_t> order(members.size());
-      for (size_t k = 0; k < order.size(); k++) order[k] = int32_t(k);
-      std::stable_sort(order.begin(), order.end(),
-                       [&](int32_t a, int32_t b2) { return class_sig[size_t(a)] < class_sig[size_t(b2)]; });
-      std::vector<int32_t> sorted_ids(order.size());
-      for (size_t k = 0; k < order.size(); k++) sorted_ids[k] = c->h_fill_ids[size_t(order[k])];
-      c->h_fill_chunks.clear();
-      for (size_t k = 0; k < order.size();) {
-        size_t e = k + 1;
-        while (e < order.size() && e - k < size_t(kEvalsPerFillBlock) &&
-               class_sig[size_t(order[e])] == class_sig[size_t(order[k])])
-          e++;
-        c->h_fill_chunks.push_back(int32_t(k));
-        c->h_fill_chunks.push_back(int32_t(e - k));
-        k = e;
-      }
-      c->h_fill_ids.swap(sorted_ids);
-    }
-    ncopy = int(c->h_pairs.size() / 2);  // pairs [0, ncopy) copy counters, the rest stats only
-    c->h_pairs.insert(c->h_pairs.end(), stats_pairs.begin(), stats_pairs.end());
-  }
-  lap(1);
-  const int nslots = int(c->h_lfc_rep.size());
-  const int nfast = int(c->h_fast.size());
-  const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
-  HIPCHK(c, c->d_rep_of.ensure(n));
-  HIPCHK(c, c->d_lfc_slot.ensure(n));
-  HIPCHK(c, c->d_lfc_jobs.ensure(n));
-  HIPCHK(c, c->d_lfc_rep.ensure(size_t(std::max(nslots, 1))));
-  HIPCHK(c, c->d_fast.ensure(size_t(std::max(nfast, 1))));
-  HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
-  HIPCHK(c, c->d_lfc_cp.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
-  HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
-  HIPCHK(c, c->d_lfc_ovs.ensure(size_t(std::max(nslots * nchunks, 1))));
-  HIPCHK(c, c->d_lfc_ovtot.ensure(size_t(std::max(nslots, 1))));
-  HIPCHK(c, hipMemcpyAsync(c->d_rep_of.p, c->h_rep_of.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_lfc_slot.p, c->h_lfc_slot.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-  if (nslots)
-    HIPCHK(c, hipMemcpyAsync(c->d_lfc_rep.p, c->h_lfc_rep.data(), size_t(nslots) * 4, hipMemcpyHostToDevice, c->stream));
-  if (nfast)
-    HIPCHK(c, hipMemcpyAsync(c->d_fast.p, c->h_fast.data(), size_t(nfast) * 4, hipMemcpyHostToDevice, c->stream));
-  b.rep_of = c->d_rep_of.p;
-  b.lfc_slot = c->d_lfc_slot.p;
-  b.lfc_rep = c->d_lfc_rep.p;
+  b.partial_idx = reinterpret_cast<const int32_t*>(ds + o_pidx);
+  b.rep_of = reinterpret_cast<const int32_t*>(ds + o_rep);
+  b.lfc_slot = reinterpret_cast<const int32_t*>(ds + o_slot);
+  b.lfc_rep = reinterpret_cast<const int32_t*>(ds + o_lrep);
   b.lfc_nslots = nslots;
   b.lfc_nchunks = nchunks;
   b.lfc_ch = c->d_lfc_ch.p;
@@ -642,30 +724,21 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipMemsetAsync(c->d_prof.p, 0, n * P_NCAT * 4, c->stream));
     b.prof = c->d_prof.p;
   }
-  const int nfill = int(c->h_fill_ids.size());
-  const int npairs = int(c->h_pairs.size() / 2);
   c->stat_fills += nfill;
   c->stat_evals += int64_t(n);
-  HIPCHK(c, c->d_fill_ids.ensure(size_t(std::max(nfill, 1))));
-  HIPCHK(c, c->d_pairs.ensure(size_t(std::max(2 * npairs, 1))));
-  HIPCHK(c, hipMemcpyAsync(c->d_fill_ids.p, c->h_fill_ids.data(), size_t(nfill) * 4, hipMemcpyHostToDevice, c->stream));
-  if (npairs)
-    HIPCHK(c, hipMemcpyAsync(c->d_pairs.p, c->h_pairs.data(), size_t(npairs) * 8, hipMemcpyHostToDevice, c->stream));
-  const int nfchunks = int(c->h_fill_chunks.size() / 2);
-  HIPCHK(c, c->d_fill_chunks.ensure(size_t(std::max(2 * nfchunks, 1))));
-  if (nfchunks)
-    HIPCHK(c, hipMemcpyAsync(c->d_fill_chunks.p, c->h_fill_chunks.data(), size_t(nfchunks) * 8, hipMemcpyHostToDevice,
-                             c->stream));
-  b.fill_ids = c->d_fill_ids.p;
+  const int32_t* d_pairs = reinterpret_cast<const int32_t*>(ds + o_pairs);
+  const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
+  const int32_t* d_leafsel = reinterpret_cast<const int32_t*>(ds + o_leafsel);
+  b.fill_ids = reinterpret_cast<const int32_t*>(ds + o_fill);
   b.nfill = nfill;
-  b.fill_chunks = c->d_fill_chunks.p;
+  b.fill_chunks = reinterpret_cast<const int32_t*>(ds + o_fchunks);
   // K1
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   c->last_stats[0] += nfill;
   if (s.N > 0 && nfchunks > 0) {
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
     uint32_t umask = 0;
-    for (size_t i = 0; i < n; i++) umask |= c->h_evals.p[i].req_mask | c->h_evals.p[i].lead_mask;
+    for (size_t i = 0; i < n; i++) umask |= hev[i].req_mask | hev[i].lead_mask;
     const int ucols = __builtin_popcount(umask);
     c->last_stats[2] += 1;
     c->last_stats[3] = ucols;
@@ -676,6 +749,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
     }
+    b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (ucols <= 4) hipLaunchKernelGGL(fill_leaves_staged_kernel<4>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (ucols <= 8) hipLaunchKernelGGL(fill_leaves_staged_kernel<8>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
@@ -690,7 +764,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   // K2
-  for (int l = s.L - 2; l >= 0; l--) {
+  for (int l = s.L - 2 - (b.rack_fanout ? 1 : 0); l >= 0; l--) {
     if (s.level_size[l] <= 0) continue;
     const int fanout = s.level_size[l + 1] / s.level_size[l];
     if (fanout >= 8) {  // wave per parent: coalesced child reads
@@ -704,14 +778,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  if (ncopy) {  // replicate phase-1 results to the duplicates
-    dim3 grid(unsigned(std::min<int64_t>((2 * int64_t(s.SD) / 4 + 255) / 256, 256)), unsigned(ncopy));
-    hipLaunchKernelGGL(replicate_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_pairs.p, ncopy);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (npairs > ncopy) {  // exclusion stats only (fast-LFC duplicates)
-    hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs - ncopy)), dim3(256), 0, c->stream, s, b,
-                       c->d_pairs.p + 2 * ncopy, npairs - ncopy);
+  if (npairs) {  // exclusion stats of the class rep to the other members
+    hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
@@ -721,17 +789,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream, b);
     HIPCHK(c, hipGetLastError());
   }
-  // leaf-level selection partials (evals whose requested level is the leaf level)
-  c->h_leafsel.clear();
-  for (size_t i = 0; i < n; i++)
-    if (c->h_evals.p[i].requested_level == s.L - 1 && c->h_lfc_slot[i] < 0) c->h_leafsel.push_back(int32_t(i));
-  if (!c->h_leafsel.empty() && s.N > 0) {
-    const int nl = int(c->h_leafsel.size());
-    c->last_stats[1] += nl;
-    HIPCHK(c, c->d_leafsel.ensure(size_t(nl)));
-    HIPCHK(c, hipMemcpyAsync(c->d_leafsel.p, c->h_leafsel.data(), size_t(nl) * 4, hipMemcpyHostToDevice, c->stream));
-    dim3 grid((s.N + 255) / 256, unsigned((nl + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
-    hipLaunchKernelGGL(leaf_partials_kernel, grid, dim3(256), 0, c->stream, s, b, c->d_leafsel.p, nl);
+  // leaf-level selection partials (non-fast evals whose requested level is the leaf level)
+  if (nleafsel && s.N > 0) {
+    c->last_stats[1] += nleafsel;
+    dim3 grid((s.N + 255) / 256, unsigned((nleafsel + kEvalsPerFillBlock - 1) / kEvalsPerFillBlock));
+    hipLaunchKernelGGL(leaf_partials_kernel, grid, dim3(256), 0, c->stream, s, b, d_leafsel, nleafsel);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -745,7 +807,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   if (nfast) {  // expand fast-LFC greedy results into entries
     hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(nchunks), unsigned(nfast)), dim3(256), 0, c->stream, s, b,
-                       c->d_fast.p);
+                       d_fast);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));

@@ -116,6 +116,7 @@ struct DevBatch {
   int32_t nstat;           // 1 + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
+  int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)
   int64_t ctr_stride;      // int32 elements per eval (5 * SD)
   int32_t* counters;       // [n][5][SD]
   int32_t* taint_counts;   // [n][num_taints]
@@ -127,7 +128,8 @@ struct DevBatch {
   int64_t scratch_stride;  // uint64 elements of scratch per eval
   uint64_t* scratch;       // [n][scratch_stride]
   int32_t list_cap;        // LDS sort capacity per wave
-  LeafPartial* partials;   // [n][nblk]
+  LeafPartial* partials;   // [leaf-level evals][nblk]
+  const int32_t* partial_idx; // [n] row of the eval's partials, -1 if none
   int32_t nblk;            // fill blocks per eval (partials per eval)
   const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
   int32_t nfill;

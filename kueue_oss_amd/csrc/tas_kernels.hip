@@ -388,7 +388,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 // Per-eval parameters of a fill chunk, staged in LDS once per block so the
 // per-eval loop has no dependent global loads (eval record -> taint row).
 struct FillEvalParams {
-  int32_t eid, taint_off, nsel, slice_size, slice_level, pad[3];
+  int32_t eid, taint_off, nsel, slice_size, slice_level, inner, pad[2];  // inner: ssal of the leaf level
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
@@ -419,6 +419,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     P.nsel = ev.nsel;
     P.slice_size = ev.slice_size;
     P.slice_level = ev.slice_level;
+    P.inner = ev.ssal[s.L - 1];
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       P.sel_col[k] = ev.sel_col[k];
       P.sel_val[k] = ev.sel_val[k];
@@ -593,15 +594,59 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       ss = go_div32(state, slice_size);
       sswl = go_div32(swl, slice_size);
     }
+    int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    const int64_t SD = s.SD;
     if (valid) {
-      int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
-      const int64_t SD = s.SD;
       base[gleaf] = state;
       base[SD + gleaf] = ss;
       if (leader) {
         base[2 * SD + gleaf] = swl;
         base[3 * SD + gleaf] = sswl;
         base[4 * SD + gleaf] = ls;
+      }
+    }
+    if (b.rack_fanout) {
+      // fused fillInCountsHelper (:1658-1719) of the leaves' parents: uniform
+      // power-of-two fan-out F <= 64, parent p owns leaves [p*F, (p+1)*F), so
+      // a parent's children are F aligned lanes of one wave (xor reductions).
+      const int F = b.rack_fanout;
+      const int32_t inner = uni(P.inner);
+      int32_t cs = state, csw = swl;
+      if (inner != 0) {
+        cs = w_mul(go_div32(cs, inner), inner);
+        csw = w_mul(go_div32(csw, inner), inner);
+      }
+      int32_t cap = cs, slc = ss, lead = ls, minD = 0x7fffffff, minSD = 0x7fffffff;
+      int has = 0;
+      if (!leader || ls > 0) {
+        has = 1;
+        minD = w_sub(cs, csw);
+        minSD = w_sub(ss, sswl);
+      }
+      for (int m = 1; m < F; m <<= 1) {
+        cap = w_add(cap, __shfl_xor(cap, m, 64));
+        slc = w_add(slc, __shfl_xor(slc, m, 64));
+        minD = min(minD, __shfl_xor(minD, m, 64));
+        minSD = min(minSD, __shfl_xor(minSD, m, 64));
+        lead = max(lead, __shfl_xor(lead, m, 64));
+        has |= __shfl_xor(has, m, 64);
+      }
+      const int parent = leaf / F;
+      if ((lane & (F - 1)) == 0 && parent < s.level_size[s.L - 2]) {
+        const int32_t pswl = has ? w_sub(cap, minD) : 0;
+        int32_t psswl = has ? w_sub(slc, minSD) : 0;
+        if (s.L - 2 == slice_level) {
+          slc = go_div32(cap, slice_size);
+          psswl = go_div32(pswl, slice_size);
+        }
+        const int g = s.level_off[s.L - 2] + parent;
+        base[g] = cap;
+        base[SD + g] = slc;
+        if (leader) {
+          base[2 * SD + g] = pswl;
+          base[3 * SD + g] = psswl;
+          base[4 * SD + g] = lead;
+        }
       }
     }
     uint64_t selm = ballot(kind == EX_SELECTOR);
@@ -847,7 +892,7 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
       pt.bfst = bst;
       pt.minss = int32_t(mss ^ 0x80000000u);
       pt.pad[0] = pt.pad[1] = 0;
-      b.partials[int64_t(eid) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
+      b.partials[int64_t(e0 + e) * b.nblk + blockIdx.x * (kFillThreads / kWave) + (threadIdx.x >> 6)] = pt;
     }
   }
 }
@@ -892,17 +937,26 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
   const int32_t* v = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
   const int lo = chunk * kLfcChunk, hi = min(s.N, lo + kLfcChunk);
   uint64_t mysum = 0;
-  for (int i = lo + int(threadIdx.x); i < hi; i += blockDim.x) {
-    const int32_t x = v[i];
-    if (x >= kLfcBins - 1 || x < 0) {  // x < 0 cannot occur at a leaf (CountIn clamps at 0)
-      atomicAdd(&h[kLfcBins - 1], 1u);
-      mysum += uint64_t(int64_t(x));
-    } else {
-      atomicAdd(&h[x], 1u);
+  const int lane = lane_id();
+  for (int base = lo; base < hi; base += blockDim.x) {  // wave-uniform trip count
+    const int i = base + int(threadIdx.x);
+    const bool act = i < hi;
+    const int32_t x = act ? v[i] : 0;
+    const bool over = x >= kLfcBins - 1 || x < 0;  // x < 0 cannot occur at a leaf (CountIn clamps at 0)
+    if (act && over) mysum += uint64_t(int64_t(x));
+    const int bin = over ? kLfcBins - 1 : x;
+    // one LDS atomic per distinct bin of the wave (leaf values are few and repetitive)
+    uint64_t pending = ballot(act);
+    while (pending) {
+      const int src = __ffsll((unsigned long long)pending) - 1;
+      const int b0 = __shfl(bin, src, 64);
+      const uint64_t m = ballot(act && bin == b0);
+      if (lane == src) atomicAdd(&h[b0], uint32_t(__popcll(m)));
+      pending &= ~m;
     }
   }
   mysum = uint64_t(wave_sum_i64(int64_t(mysum)));
-  if (lane_id() == 0 && mysum) atomicAdd(&ovs, (unsigned long long)mysum);
+  if (lane == 0 && mysum) atomicAdd(&ovs, (unsigned long long)mysum);
   __syncthreads();
   uint32_t* out = b.lfc_ch + (int64_t(slot) * b.lfc_nchunks + chunk) * kLfcBins;
   for (int i = threadIdx.x; i < kLfcBins; i += blockDim.x) out[i] = h[i];
@@ -2606,7 +2660,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.gkeys2 = w.gkeys + lcap;
   w.overflow = false;
   for (auto& x : w.prof) x = 0;
-  w.partials = (b.partials && ev.requested_level == s.L - 1) ? b.partials + int64_t(eid) * b.nblk : nullptr;
+  w.partials = (ev.requested_level == s.L - 1 && b.partial_idx[eid] >= 0)
+                   ? b.partials + int64_t(b.partial_idx[eid]) * b.nblk : nullptr;
   w.nblk = b.nblk;
   int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
   const int ecap = b.entry_cap;

@@ -71,3 +71,14 @@ def test_emulated_fast_lfc_stress(emu_lib, seed, big):
     snap.close()
     mism = [i for i in range(len(wls)) if got[i] != want[i]]
     assert mism == [], (mism[:5], wls[mism[0]][0]["count"] if mism else None)
+
+
+def test_emulated_kernels_match_oracle_c4_jobset(emu_lib):
+    # leader/worker groups with slice topology on a uniform fan-out tree (fused parent roll-up in fill)
+    snap_doc, wls = synth.config_c4(n_workloads=16, shape=(2, 2, 8, 16))
+    want, _ = oracle_lib.eval_workloads(snap_doc, wls)
+    snap = TASFlavorSnapshot(snap_doc, list_cap=64, lib=emu_lib)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    mism = [i for i in range(len(wls)) if got[i] != want[i]]
+    assert mism == [], (mism[:5], got[mism[0]] if mism else None, want[mism[0]] if mism else None)
