@@ -137,6 +137,7 @@ struct kueue_tas_ctx {
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
   DevBuf<uint64_t> d_lfc_ovs, d_lfc_ovtot;
   DevBuf<LfcJob> d_lfc_jobs;
+  DevBuf<LfcItem> d_lfc_items;  // [0]: item count, then the items
   DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
   std::vector<int32_t> last_prof;
   int num_profiles = 1;
@@ -224,6 +225,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_ovs.release();
   c->d_lfc_ovtot.release();
   c->d_lfc_jobs.release();
+  c->d_lfc_items.release();
   c->d_prof.release();
   c->h_out.release();
   c->h_offsets.release();
@@ -666,6 +668,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));  // per-eval regions, packed after select
   HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
+  HIPCHK(c, c->d_lfc_items.ensure(size_t(std::max(nfast, 1)) * size_t(std::max(nchunks, 1)) + 1));
   HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
   HIPCHK(c, c->d_lfc_cp.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
   HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
@@ -718,6 +721,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.lfc_ovs = c->d_lfc_ovs.p;
   b.lfc_ovtot = c->d_lfc_ovtot.p;
   b.lfc_jobs = c->d_lfc_jobs.p;
+  b.lfc_nitems = reinterpret_cast<int32_t*>(c->d_lfc_items.p);  // item 0's slot holds the count
+  b.lfc_items = c->d_lfc_items.p + 1;
+  HIPCHK(c, hipMemsetAsync(b.lfc_nitems, 0, sizeof(LfcItem), c->stream));
   b.prof = nullptr;
   if (KTAS_PROFILE) {
     HIPCHK(c, c->d_prof.ensure(n * P_NCAT));
@@ -727,7 +733,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->stat_fills += nfill;
   c->stat_evals += int64_t(n);
   const int32_t* d_pairs = reinterpret_cast<const int32_t*>(ds + o_pairs);
-  const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
   const int32_t* d_leafsel = reinterpret_cast<const int32_t*>(ds + o_leafsel);
   b.fill_ids = reinterpret_cast<const int32_t*>(ds + o_fill);
   b.nfill = nfill;
@@ -758,7 +763,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
     if (b.nstat) {
-      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(64), 0, c->stream, b, int(grid.x));
+      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(grid.x));
       HIPCHK(c, hipGetLastError());
     }
   }
@@ -805,9 +810,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(select_kernel, grid, dim3(64 * waves), lds, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
-  if (nfast) {  // expand fast-LFC greedy results into entries
-    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(nchunks), unsigned(nfast)), dim3(256), 0, c->stream, s, b,
-                       d_fast);
+  if (nfast) {  // expand fast-LFC greedy results into entries (items appended by select)
+    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
+    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));

@@ -104,6 +104,12 @@ struct LfcJob {
   int32_t t, m, rem_last, pad;
 };
 
+// One (eval, chunk) piece of fast-LFC greedy output: base = output position
+// of the chunk's first kept leaf, tie0 = rank of its first value-t leaf.
+struct LfcItem {
+  int32_t eid, chunk, base, tie0;
+};
+
 // Per-batch device buffers.
 struct DevBatch {
   const DevEval* evals;
@@ -145,6 +151,8 @@ struct DevBatch {
   uint64_t* lfc_ovs;       // [nslots][nchunks] sum of the values >= kLfcBins - 1
   uint64_t* lfc_ovtot;     // [nslots]
   LfcJob* lfc_jobs;        // [n]
+  LfcItem* lfc_items;      // [nfast * nchunks] chunks with greedy output (appended by select)
+  int32_t* lfc_nitems;     // [1] number of lfc_items
   int32_t* overlay;        // [n][5][SD] phase-2 copy-on-write counters (select)
   int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
   int32_t tag_epoch;

@@ -687,16 +687,21 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 }
 
 // Sum the per-block ExclusionStats partials of every phase-1 class.
-__global__ __launch_bounds__(64) void fill_stats_reduce_kernel(DevBatch b, int nblk) {
+__global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int nblk) {
   const int f = blockIdx.x;
   const int eid = b.fill_ids[f];
-  for (int k = threadIdx.x; k < b.nstat; k += blockDim.x) {
-    int32_t acc = 0;
+  const int wv = threadIdx.x >> 6, lane = lane_id();
+  for (int k = wv; k < b.nstat; k += 4) {  // one wave per statistic, lanes over the fill blocks
     const int32_t* p = b.fill_stats + int64_t(f) * nblk * b.nstat + k;
-    for (int j = 0; j < nblk; j++) acc += p[int64_t(j) * b.nstat];
-    if (k == 0) b.sel_counts[eid] = acc;
-    else if (k <= b.num_taints) b.taint_counts[int64_t(eid) * b.num_taints + (k - 1)] = acc;
-    else b.res_counts[int64_t(eid) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
+    int32_t acc = 0;
+#pragma unroll 8
+    for (int j = lane; j < nblk; j += kWave) acc += p[int64_t(j) * b.nstat];
+    acc = wave_sum_wrap32(acc);
+    if (lane == 0) {
+      if (k == 0) b.sel_counts[eid] = acc;
+      else if (k <= b.num_taints) b.taint_counts[int64_t(eid) * b.num_taints + (k - 1)] = acc;
+      else b.res_counts[int64_t(eid) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
+    }
   }
 }
 
@@ -967,16 +972,24 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
 __global__ __launch_bounds__(kLfcBins) void lfc_total_kernel(DevBatch b) {
   const int slot = blockIdx.x, bin = threadIdx.x;
   const int64_t base = int64_t(slot) * b.lfc_nchunks;
+  constexpr int U = 16;  // chunk counts loaded ahead of the running prefix
   uint32_t acc = 0;
-  for (int c = 0; c < b.lfc_nchunks; c++) {
-    b.lfc_cp[(base + c) * kLfcBins + bin] = acc;
-    acc += b.lfc_ch[(base + c) * kLfcBins + bin];
+  for (int c0 = 0; c0 < b.lfc_nchunks; c0 += U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = c0 + u < b.lfc_nchunks ? b.lfc_ch[(base + c0 + u) * kLfcBins + bin] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (c0 + u < b.lfc_nchunks) b.lfc_cp[(base + c0 + u) * kLfcBins + bin] = acc;
+      acc += v[u];
+    }
   }
   b.lfc_tot[int64_t(slot) * kLfcBins + bin] = acc;
-  if (bin == 0) {
+  if (bin < kWave) {
     uint64_t o = 0;
-    for (int c = 0; c < b.lfc_nchunks; c++) o += b.lfc_ovs[base + c];
-    b.lfc_ovtot[slot] = o;
+    for (int c = bin; c < b.lfc_nchunks; c += kWave) o += b.lfc_ovs[base + c];
+    o = uint64_t(wave_sum_i64(int64_t(o)));
+    if (bin == 0) b.lfc_ovtot[slot] = o;
   }
 }
 
@@ -2329,6 +2342,40 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
     o.fit_level = L1;
     o.num_workers = int32_t(below + mt);
     if (o.num_workers > ecap) o.status = KUEUE_TAS_ST_INTERNAL;
+    // work items for lfc_emit_kernel: the chunks holding output, with their
+    // output offset (kept leaves in earlier chunks) and first tie rank
+    for (int c0 = 0; c0 < b.lfc_nchunks; c0 += kWave) {
+      const int ci = c0 + lane;
+      int64_t base = 0, nkeep = 0, tb = 0;
+      if (ci < b.lfc_nchunks) {
+        const int64_t off = (int64_t(slot) * b.lfc_nchunks + ci) * kLfcBins;
+        int64_t a = 0, cc = 0;
+        for (int v = 1; v < t; v++) {
+          a += b.lfc_cp[off + v];
+          cc += b.lfc_ch[off + v];
+        }
+        tb = b.lfc_cp[off + t];
+        const int64_t tin = b.lfc_ch[off + t];
+        int64_t take = mt - tb;
+        take = take < 0 ? 0 : (take > tin ? tin : take);
+        base = a + (tb < mt ? tb : mt);
+        nkeep = cc + take;
+      }
+      const uint64_t has = ballot(nkeep > 0);
+      if (has) {
+        int first = 0;
+        if (lane == 0) first = atomicAdd(b.lfc_nitems, __popcll(has));
+        first = __shfl(first, 0, 64);
+        if (nkeep > 0) {
+          LfcItem it;
+          it.eid = w.eid;
+          it.chunk = ci;
+          it.base = int32_t(base);
+          it.tie0 = int32_t(tb);
+          b.lfc_items[first + __popcll(has & ((1ull << lane) - 1ull))] = it;
+        }
+      }
+    }
     return job;
   }
   const int64_t bins_mass = int64_t(shfl_u64(uint64_t(x), 63));
@@ -2767,81 +2814,64 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
 }
 
 // Expand fast-LFC greedy results (LfcJob) into (leaf, count) entries in leaf
-// index order.  Grid (chunks, fast evals), one kLfcChunk-leaf chunk per block;
-// the chunk's output offset and tie ranks come from the chunk prefix counts.
-__global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b, const int32_t* fast_ids) {
-  __shared__ int64_t sh_base, sh_nkeep, sh_tie0;
+// index order.  Persistent grid over the (eval, chunk) items select appended:
+// one kLfcChunk-leaf chunk per item; its output offset and first tie rank
+// come with the item, in-chunk positions from block scans.
+__global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t sh_wt[4], sh_wk[4];
-  const int eid = fast_ids[blockIdx.y];
-  const LfcJob job = b.lfc_jobs[eid];
-  if (job.t <= 0) return;
-  const int slot = b.lfc_slot[eid];
-  const int chunk = blockIdx.x;
-  const int t = job.t;
-  const int64_t mt = job.m;
+  const int nitems = *b.lfc_nitems;
   const int lane = lane_id(), wv = threadIdx.x >> 6;
-  if (wv == 0) {
-    const int64_t off = (int64_t(slot) * b.lfc_nchunks + chunk) * kLfcBins;
-    int64_t a = 0, c = 0;
-    for (int v = 1 + lane; v < t; v += kWave) {
-      a += b.lfc_cp[off + v];
-      c += b.lfc_ch[off + v];
-    }
-    a = wave_sum_i64(a);
-    c = wave_sum_i64(c);
-    if (lane == 0) {
-      const int64_t tb = b.lfc_cp[off + t], tin = b.lfc_ch[off + t];
-      int64_t take = mt - tb;
-      take = take < 0 ? 0 : (take > tin ? tin : take);
-      sh_base = a + (tb < mt ? tb : mt);
-      sh_nkeep = c + take;
-      sh_tie0 = tb;
-    }
-  }
-  __syncthreads();
-  if (sh_nkeep == 0) return;
-  const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
-  const int lo = chunk * kLfcChunk + int(threadIdx.x) * 8;
-  int32_t x[8];
+  for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {
+    const LfcItem item = b.lfc_items[itx];
+    const int eid = item.eid;
+    const LfcJob job = b.lfc_jobs[eid];
+    const int slot = b.lfc_slot[eid];
+    const int t = job.t;
+    const int64_t mt = job.m;
+    const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
+    const int lo = item.chunk * kLfcChunk + int(threadIdx.x) * 8;
+    int32_t x[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? V[lo + k] : 0;
-  int nt = 0;
+    for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? V[lo + k] : 0;
+    int nt = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) nt += x[k] == t ? 1 : 0;
-  int wt_total;
-  const int tex = wave_excl_scan(nt, &wt_total);
-  if (lane == 0) sh_wt[wv] = wt_total;
-  __syncthreads();
-  int64_t r = sh_tie0 + tex;
-  for (int k = 0; k < wv; k++) r += sh_wt[k];
-  bool keep[8];
-  int nk = 0;
+    for (int k = 0; k < 8; k++) nt += x[k] == t ? 1 : 0;
+    int wt_total;
+    const int tex = wave_excl_scan(nt, &wt_total);
+    if (lane == 0) sh_wt[wv] = wt_total;
+    __syncthreads();
+    int64_t r = int64_t(item.tie0) + tex;
+    for (int k = 0; k < wv; k++) r += sh_wt[k];
+    bool keep[8];
+    int nk = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const bool tie = x[k] == t;
-    keep[k] = (x[k] > 0 && x[k] < t) || (tie && r < mt);
-    if (tie) {
-      if (r == mt - 1) x[k] = job.rem_last;
-      r++;
-    }
-    nk += keep[k] ? 1 : 0;
-  }
-  int wk_total;
-  const int kex = wave_excl_scan(nk, &wk_total);
-  if (lane == 0) sh_wk[wv] = wk_total;
-  __syncthreads();
-  int64_t pos = sh_base + kex;
-  for (int k = 0; k < wv; k++) pos += sh_wk[k];
-  int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    if (keep[k]) {
-      if (pos < b.entry_cap) {
-        ent[2 * pos] = lo + k;
-        ent[2 * pos + 1] = x[k];
+    for (int k = 0; k < 8; k++) {
+      const bool tie = x[k] == t;
+      keep[k] = (x[k] > 0 && x[k] < t) || (tie && r < mt);
+      if (tie) {
+        if (r == mt - 1) x[k] = job.rem_last;
+        r++;
       }
-      pos++;
+      nk += keep[k] ? 1 : 0;
     }
+    int wk_total;
+    const int kex = wave_excl_scan(nk, &wk_total);
+    if (lane == 0) sh_wk[wv] = wk_total;
+    __syncthreads();
+    int64_t pos = int64_t(item.base) + kex;
+    for (int k = 0; k < wv; k++) pos += sh_wk[k];
+    int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (keep[k]) {
+        if (pos < b.entry_cap) {
+          ent[2 * pos] = lo + k;
+          ent[2 * pos + 1] = x[k];
+        }
+        pos++;
+      }
+    }
+    __syncthreads();  // sh_wt / sh_wk reused by the next item
   }
 }
 
