@@ -187,6 +187,10 @@ int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, siz
                          size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts);
 /* Copy the packed entries of the last kueue_tas_eval_batch (after EOVERFLOW). */
 int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries_capacity);
+/* Zero-copy view of the packed entries of the last kueue_tas_eval_batch
+ * (pinned host memory the device wrote; valid until the next call on ctx).
+ * Pass entries = NULL to kueue_tas_eval_batch to skip its copy. */
+const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 
 /* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
  * events on the ctx stream): [0] the fill kernel alone, [1] roll-up +

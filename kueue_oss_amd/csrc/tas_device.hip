@@ -146,7 +146,12 @@ struct kueue_tas_ctx {
   HostBuf<int64_t> h_offsets;
   HostBuf<int32_t> h_stats;
   std::vector<int32_t> last_ticks;    // per-eval select time (100 MHz ticks) of the last batch
-  std::vector<int32_t> last_entries;  // packed (leaf, count) pairs of the last batch
+  // packed (leaf, count) pairs of the last batch: pinned, device-mapped host
+  // memory the pack kernel writes directly (no separate D2H copy or sync)
+  int32_t* ent_host = nullptr;
+  int32_t* ent_dev = nullptr;
+  size_t ent_cap = 0;   // int32 capacity
+  size_t ent_used = 0;  // int32 used by the last batch
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
@@ -228,6 +233,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_items.release();
   c->d_prof.release();
   c->h_out.release();
+  if (c->ent_host) (void)hipHostFree(c->ent_host);
+  c->ent_host = c->ent_dev = nullptr;
   c->h_offsets.release();
   c->h_stats.release();
   for (auto& e : c->ev)
@@ -821,6 +828,24 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_out.p, int(n), entry_cap,
                      c->d_offsets.p);
   HIPCHK(c, hipGetLastError());
+  // pack the entries straight into the mapped host buffer (worst case n * entry_cap pairs)
+  {
+    const size_t need_ints = c->ent_used + size_t(n) * size_t(entry_cap) * 2;
+    if (need_ints > c->ent_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      size_t cap = std::max<size_t>(need_ints, 2 * c->ent_cap);
+      int32_t* p = nullptr;
+      HIPCHK(c, hipHostMalloc(&p, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+      if (c->ent_used) memcpy(p, c->ent_host, c->ent_used * 4);
+      if (c->ent_host) (void)hipHostFree(c->ent_host);
+      c->ent_host = p;
+      c->ent_cap = cap;
+      HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
+    }
+    hipLaunchKernelGGL(pack_entries_kernel, dim3(unsigned(n)), dim3(256), 0, c->stream, c->d_entries.p, entry_cap,
+                       c->d_offsets.p, c->ent_dev + c->ent_used, int(n));
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, c->h_out.ensure(n));
   HIPCHK(c, c->h_offsets.ensure(n + 1));
@@ -835,17 +860,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   for (size_t i = 0; i < n; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
   if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
   const int64_t total = c->h_offsets.p[n];
-  HIPCHK(c, c->d_packed.ensure(size_t(std::max<int64_t>(total, 1)) * 2));
-  if (total > 0) {
-    hipLaunchKernelGGL(pack_entries_kernel, dim3(unsigned(n)), dim3(256), 0, c->stream, c->d_entries.p, entry_cap,
-                       c->d_offsets.p, c->d_packed.p, int(n));
-    HIPCHK(c, hipGetLastError());
-    size_t base = c->last_entries.size();
-    c->last_entries.resize(base + size_t(total) * 2);
-    HIPCHK(c, hipMemcpyAsync(c->last_entries.data() + base, c->d_packed.p, size_t(total) * 8, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
+  c->ent_used += size_t(total) * 2;
   lap(4);
   memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
   if (KTAS_PROFILE) {
@@ -881,7 +896,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   HIPCHK(c, hipSetDevice(c->device));
   float ms[4] = {0, 0, 0, 0};
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
-  c->last_entries.clear();
+  c->ent_used = 0;
   c->last_ticks.clear();
   c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
@@ -893,12 +908,12 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
     size_t m = std::min(chunk, n - i0);
     off.assign(m + 1, 0);
     for (;;) {
-      size_t keep = c->last_entries.size();
+      size_t keep = c->ent_used;
       int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
                           off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
-        c->last_entries.resize(keep);
+        c->ent_used = keep;
         c->last_ticks.resize(2 * i0);
         c->last_prof.resize(KTAS_PROFILE ? i0 * P_NCAT : 0);
         int32_t need = 0;
@@ -916,17 +931,24 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   }
   memcpy(c->last_ms, ms, sizeof ms);
   memcpy(c->last_stage_ms, stage_ms, sizeof stage_ms);
-  const size_t total = c->last_entries.size() / 2;
+  const size_t total = c->ent_used / 2;
+  if (!entries) return KUEUE_TAS_OK;  // caller reads kueue_tas_last_entries()
   if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
-  if (total) memcpy(entries, c->last_entries.data(), total * 8);
+  if (total) memcpy(entries, c->ent_host, total * 8);
   return KUEUE_TAS_OK;
+}
+
+const int32_t* kueue_tas_last_entries(kueue_tas_ctx* c, size_t* num_pairs) {
+  if (!c) return nullptr;
+  if (num_pairs) *num_pairs = c->ent_used / 2;
+  return c->ent_host;
 }
 
 int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_capacity) {
   if (!c) return KUEUE_TAS_EINVAL;
-  const size_t total = c->last_entries.size() / 2;
+  const size_t total = c->ent_used / 2;
   if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
-  if (total) memcpy(entries, c->last_entries.data(), total * 8);
+  if (total) memcpy(entries, c->ent_host, total * 8);
   return KUEUE_TAS_OK;
 }
 

@@ -92,6 +92,8 @@ typedef struct emu_event* hipEvent_t;
 enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
 constexpr unsigned hipStreamNonBlocking = 1;
 constexpr unsigned hipHostMallocDefault = 0;
+constexpr unsigned hipHostMallocMapped = 2;
+constexpr unsigned hipHostMallocCoherent = 0x40000000;
 inline const char* hipGetErrorString(hipError_t) { return "emu error"; }
 inline hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
 inline hipError_t hipSetDevice(int) { return hipSuccess; }
@@ -108,6 +110,7 @@ inline hipError_t hipHostMalloc(T** p, size_t bytes, unsigned) {
   return *p ? hipSuccess : 2;
 }
 inline hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
 inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
   if (n) memmove(d, s, n);
   return hipSuccess;
