@@ -741,27 +741,46 @@ class FlavorSnapshot {
   }
 
   // ---- failure strings ----
-  std::string format_stats(const kueue_tas_eval_out& o, const int32_t* taints, const int32_t* res) const {
-    bool has = o.excl_selector > 0 || o.excl_affinity > 0 || o.excl_topology > 0;
-    std::vector<std::string> reasons;
-    if (o.excl_selector > 0) reasons.push_back("nodeSelector: " + std::to_string(o.excl_selector));
-    if (o.excl_affinity > 0) reasons.push_back("affinity: " + std::to_string(o.excl_affinity));
-    if (o.excl_topology > 0) reasons.push_back("topologyDomain: " + std::to_string(o.excl_topology));
+  // ExclusionStats reasons (:480-499) in sorted order.  Every reason is
+  // "<prefix><count>" with a distinct prefix ending in ": ", so sorting the
+  // full strings is sorting the prefixes: that order is computed once per
+  // (taints, columns) set, not per failure.
+  mutable std::vector<std::pair<std::string, int32_t>> reasonOrder;  // (prefix, kind: -3..-1 fixed, t, T + c)
+  mutable size_t reasonFor = size_t(-1);
+  void reason_order() const {
+    const size_t key = taintStrings.size() * 1000003u + cols.size() * 7919u + compile_gen;
+    if (reasonFor == key) return;
+    reasonOrder.clear();
+    reasonOrder.emplace_back("nodeSelector: ", -1);
+    reasonOrder.emplace_back("affinity: ", -2);
+    reasonOrder.emplace_back("topologyDomain: ", -3);
     for (size_t t = 0; t < taintStrings.size(); t++)
-      if (taints[t] > 0) {
-        has = true;
-        reasons.push_back("taint " + go_quote(taintStrings[t]) + ": " + std::to_string(taints[t]));
-      }
+      reasonOrder.emplace_back("taint " + go_quote(taintStrings[t]) + ": ", int32_t(t));
     for (size_t c = 0; c < cols.size(); c++)
-      if (res[c] > 0) {
-        has = true;
-        reasons.push_back("resource " + go_quote(cols[c]) + ": " + std::to_string(res[c]));
+      reasonOrder.emplace_back("resource " + go_quote(cols[c]) + ": ", int32_t(taintStrings.size() + c));
+    std::sort(reasonOrder.begin(), reasonOrder.end());
+    reasonFor = key;
+  }
+  void format_stats(std::string& out, const kueue_tas_eval_out& o, const int32_t* taints, const int32_t* res) const {
+    reason_order();
+    const int32_t T = int32_t(taintStrings.size());
+    bool first = true;
+    for (const auto& r : reasonOrder) {
+      const int32_t k = r.second;
+      const int32_t v = k == -1 ? o.excl_selector : k == -2 ? o.excl_affinity : k == -3 ? o.excl_topology
+                                                         : k < T ? taints[k] : res[k - T];
+      if (v <= 0) continue;
+      if (first) {
+        out += ". Total nodes: ";
+        out += std::to_string(o.total_nodes);
+        out += "; excluded: ";
+        first = false;
+      } else {
+        out += ", ";
       }
-    if (!has) return "";
-    std::sort(reasons.begin(), reasons.end());
-    std::string out = ". Total nodes: " + std::to_string(o.total_nodes) + "; excluded: ";
-    for (size_t i = 0; i < reasons.size(); i++) out += (i ? ", " : "") + reasons[i];
-    return out;
+      out += r.first;
+      out += std::to_string(v);
+    }
   }
   std::string failure_reason(const GroupEval& g, const kueue_tas_eval_out& o, const int32_t* taints,
                              const int32_t* res) const {
@@ -774,7 +793,8 @@ class FlavorSnapshot {
         std::string m = o.a == 0 ? "topology " + topo + " doesn't allow to fit any of " + std::to_string(o.b) + " " + unit + "(s)"
                                  : "topology " + topo + " allows to fit only " + std::to_string(o.a) + " out of " +
                                        std::to_string(o.b) + " " + unit + "(s)";
-        return m + format_stats(o, taints, res);
+        format_stats(m, o, taints, res);
+        return m;
       }
       case KUEUE_TAS_ST_MULTILAYER: {
         std::string m = "topology " + topo + " doesn't allow to fit";
@@ -782,7 +802,8 @@ class FlavorSnapshot {
         for (int c = 0; c < g.req.num_layers; c++)
           m += "; " + std::to_string(o.ml_fit[c]) + "/" + std::to_string(o.ml_need[c]) + " slice(s) fit on level " +
                g.layer_names[c];
-        return m + format_stats(o, taints, res);
+        format_stats(m, o, taints, res);
+        return m;
       }
       default:
         return "internal: device evaluation exceeded its list/output capacity";
