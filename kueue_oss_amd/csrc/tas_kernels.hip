@@ -1475,6 +1475,50 @@ __device__ __forceinline__ void wave_for_all(int n, Load load, Body body) {
 }
 
 
+// m-th smallest (1-based) of cnt uint32 values in LDS (one wave): MSB-first
+// radix select with 8-bit digits (4 histogram rounds, no sort).
+__device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* hist, int lane) {
+  uint32_t prefix = 0, pmask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = lane; i < 256; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = lane; i < cnt; i += kWave) {
+      const uint32_t x = v[i];
+      if ((x & pmask) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+    }
+    wave_sync();
+    uint32_t c[4];
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = hist[4 * lane + k];
+      lsum += c[k];
+    }
+    uint32_t x = lsum;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl(x, max(lane - d, 0), 64);
+      if (lane >= d) x += y;
+    }
+    const uint64_t hit = ballot(x >= uint32_t(m));
+    const int src = __ffsll((unsigned long long)hit) - 1;  // exists: m <= matching count
+    int digit = 0;
+    uint32_t before = x - lsum;
+    if (lane == src) {
+      int k = 0;
+      while (k < 3 && before + c[k] < uint32_t(m)) before += c[k++];
+      digit = 4 * lane + k;
+    }
+    digit = __shfl(digit, src, 64);
+    before = __shfl(before, src, 64);
+    m -= int(before);
+    prefix |= uint32_t(digit) << shift;
+    pmask |= 255u << shift;
+    wave_sync();
+  }
+  return prefix;
+}
+
+
 // First position p (in scan order: bin i = p, or kBins-1-p when desc) whose
 // inclusive weighted sum reaches need.  Returns the bin (or -1: total < need,
 // *before = total) and the sum before it.
@@ -1619,23 +1663,22 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     const int64_t wt = slices ? t : u;  // > 0: the class added weight
     const int64_t m = (rem2 + wt - 1) / wt;
     remc = int32_t(rem2 - (m - 1) * wt);
-    // pass E: the m-th smallest index of class (t, u)
+    // pass E: the m-th smallest index of class (t, u) (radix select in LDS)
     wave_sync();
+    uint32_t* cand = reinterpret_cast<uint32_t*>(w.lds);
+    const int ccap = w.cap * 4 - 256;  // uint32 slots; the last 256 hold the digit histogram
     int cnt = 0;
     wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
       const bool in = valid && kp_ss(lfc, k) == t && kp_st(k) == u;
       const uint64_t bm = ballot(in);
       const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
-      if (in && pos < w.cap) w.lds[pos] = Key{0, k.lo};
+      if (in && pos < ccap) cand[pos] = uint32_t(k.lo);
       cnt += __popcll(bm);
     });
-    if (cnt > w.cap) return -1;
+    if (cnt > ccap) return -1;
     wave_sync();
-    {
-      ProfScope ps_(w, P_LDS_SORT);
-      lds_sort(w.lds, cnt, w.lane);
-    }
-    ck = key_plain(lfc, t, u, int32_t(uint32_t(w.lds[m - 1].lo)));
+    const uint32_t kth = lds_select_kth(cand, cnt, int(m), cand + ccap, w.lane);
+    ck = key_plain(lfc, t, u, int32_t(kth));
     wave_sync();
   }
   int chosen = loff + int(uint32_t(ck.lo));
@@ -1940,6 +1983,59 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
                            int base) {
   ProfScope prof_scope_(w, P_EMIT);
   const int loff = w.s->level_off[w.s->L - 1];
+  if (n > 0) {
+    // Leaf-index range of the output: when its bitmap fits the wave's LDS,
+    // mark the leaves and emit them in index order without sorting.
+    int32_t mn = 0x7fffffff, mx = -1;
+    wave_for<int32_t>(n, [&](int i) { return gids[i]; }, [&](int, int32_t g) {
+      mn = min(mn, g - loff);
+      mx = max(mx, g - loff);
+    });
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      mn = min(mn, __shfl_xor(mn, m, 64));
+      mx = max(mx, __shfl_xor(mx, m, 64));
+    }
+    const int64_t words = (int64_t(mx) - mn + 32) / 32;
+    if (words * 4 <= int64_t(w.cap) * int64_t(sizeof(Key))) {
+      uint32_t* bm = reinterpret_cast<uint32_t*>(w.lds);
+      wave_sync();
+      for (int j = w.lane; j < words; j += kWave) bm[j] = 0;
+      wave_sync();
+      wave_for<int32_t>(n, [&](int i) { return gids[i]; }, [&](int, int32_t g) {
+        const int off = g - loff - mn;
+        atomicOr(&bm[off >> 5], 1u << (off & 31));
+      });
+      wave_sync();
+      int cnt = base;
+      for (int64_t j0 = 0; j0 < words; j0 += kWave) {
+        const int64_t j = j0 + w.lane;
+        const uint32_t word = j < words ? bm[j] : 0u;
+        int nk = 0;
+        for (uint32_t x = word; x; x &= x - 1) {
+          const int32_t leaf = mn + int32_t(j) * 32 + __builtin_ctz(x);
+          const int32_t v = use_ls ? w.get(F_LS, loff + leaf) : w.get(F_STATE, loff + leaf);
+          nk += (positive_only ? v > 0 : v != 0) ? 1 : 0;
+        }
+        int tot;
+        int pos = cnt + wave_excl_scan(nk, &tot);
+        for (uint32_t x = word; x; x &= x - 1) {
+          const int32_t leaf = mn + int32_t(j) * 32 + __builtin_ctz(x);
+          const int32_t v = use_ls ? w.get(F_LS, loff + leaf) : w.get(F_STATE, loff + leaf);
+          if (positive_only ? v > 0 : v != 0) {
+            if (pos < ent_cap) {
+              ent[2 * pos] = leaf;
+              ent[2 * pos + 1] = v;
+            }
+            pos++;
+          }
+        }
+        cnt += tot;
+      }
+      wave_sync();
+      return cnt - base;
+    }
+  }
   Key* arr;
   if (n <= w.cap) {
     for (int i = w.lane; i < n; i += kWave) w.lds[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
