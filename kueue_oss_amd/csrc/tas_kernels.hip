@@ -1818,7 +1818,8 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   const int loff = w.s->level_off[level];
   // leaderless walks need no sequential pass (see threshold_walk)
   const bool leaderless = !w.leader && leaderCount <= 0 && sliceRecompute <= 1;
-  if (leaderless && w.bf && slices && n > w.cap && gids != w.listD && go_div32(count, sliceSize) > 0) {
+  constexpr int kSmallWalk = 64;  // shorter lists: sort + prefix walk
+  if (leaderless && w.bf && slices && n > kSmallWalk && gids != w.listD && go_div32(count, sliceSize) > 0) {
     // BestFit slice walk with rem > 0: elements with sliceState <= 0 sort after
     // every positive one (sliceState desc), cannot move the running sum up to
     // rem, and cannot be the best fit (weight >= remc > 0), so they are never
@@ -1842,6 +1843,10 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     gids = w.listD;
     n = m;
+  }
+  if (leaderless && n > kSmallWalk && n <= w.lcap) {  // sort-free histogram walk
+    const int r = threshold_walk(w, gids, n, level, count, sliceSize, slices, out, np);
+    if (r >= 0) return r == 1;
   }
   if (n <= w.cap) {
     for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain_clean(gids[i]);
