@@ -1064,6 +1064,13 @@ struct Wave {
     own(g);
     ov[int64_t(f) * SD + g] = v;
   }
+  // Lane-private first write of a domain a leaderless walk has just read clean
+  // (non-leader evals hold two fields): stores only, no ownership check.
+  __device__ void set_walked(int g, int32_t state, int32_t slice) {
+    ov[int64_t(F_STATE) * SD + g] = state;
+    ov[int64_t(F_SLICE) * SD + g] = slice;
+    tag[g] = my_tag;
+  }
   // Stored by one lane for a domain only it handles in a lane-parallel pass;
   // readers on other lanes come after a fence (callers have set dirty).
   __device__ void set_lane(Field f, int g, int32_t v) {
@@ -1708,8 +1715,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
     if (take) {
       const int g = loff + int(uint32_t(k.lo));
-      if (slices) w.set_lane(F_STATE, g, w_mul(kp_ss(lfc, k), sliceSize));
-      w.set_lane(F_LS, g, 0);
+      if (slices) w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));  // !leader: no F_LS
       if (pos < w.lcap) out[pos] = g;
     }
     cnt += __popcll(bm);
@@ -1788,8 +1794,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   for (int i = w.lane; i < cross; i += kWave) {
     const Key k = w.lds[i];
     const int g = loff + int(uint32_t(k.lo));
-    if (slices) w.set_lane(F_STATE, g, w_mul(kp_ss(lfc, k), sliceSize));
-    w.set_lane(F_LS, g, 0);
+    if (slices) w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));  // !leader: no F_LS
     if (cnt + i < w.lcap) out[cnt + i] = g;
   }
   cnt += cross;
@@ -1927,6 +1932,79 @@ __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level
   return np;
 }
 
+// gather_children restricted to children with sliceState > 0 (clean reads):
+// the BestFit slice walk only ever takes those (see walk_sorted), so the
+// filtered list is walked directly.  64 parents per step; their children are
+// visited as one flattened range, kU loads in flight per lane.
+__device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, int level, int32_t* out) {
+  ProfScope prof_scope_(w, P_GATHER);
+  const DevSnap& s = *w.s;
+  const int poff = s.level_off[level];
+  const int coff = s.level_off[level + 1];
+  const int32_t* co = s.child_off + s.child_base[level];
+  int32_t* sh_ex = reinterpret_cast<int32_t*>(w.lds);  // [64] exclusive child offsets of the step's parents
+  int32_t* sh_cb = sh_ex + kWave;                        // [64] first child of each
+  int np = 0;
+  for (int i0 = 0; i0 < n; i0 += kWave) {
+    const int i = i0 + w.lane;
+    int cb = 0, cnt = 0;
+    if (i < n) {
+      const int p = parents[i] - poff;
+      cb = co[p];
+      cnt = co[p + 1] - cb;
+    }
+    int tot;
+    const int ex = wave_excl_scan(cnt, &tot);
+    wave_sync();
+    sh_ex[w.lane] = ex;
+    sh_cb[w.lane] = cb;
+    wave_sync();
+    const int nparents = min(kWave, n - i0);
+    // uniform power-of-two fan-out in this step: element e belongs to parent e >> sh
+    const int f0 = __shfl(cnt, 0, 64);
+    const bool uniform = f0 > 0 && (f0 & (f0 - 1)) == 0 && ballot(i < n && cnt != f0) == 0;
+    const int sh = uniform ? __builtin_ctz(f0) : 0;
+    for (int b0 = 0; b0 < tot; b0 += kU * kWave) {
+      int g[kU];
+      int32_t v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int e = min(b0 + u * kWave + w.lane, tot - 1);
+        if (uniform) {
+          g[u] = coff + __shfl(cb, e >> sh, 64) + (e & (f0 - 1));
+        } else {
+          int lo = 0, hi = nparents - 1;  // last parent with ex <= e
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (sh_ex[mid] <= e) lo = mid;
+            else hi = mid - 1;
+          }
+          g[u] = coff + sh_cb[lo] + (e - sh_ex[lo]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) v[u] = w.get_clean(F_SLICE, g[u]);
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const bool keep = b0 + u * kWave + w.lane < tot && v[u] > 0;
+        const uint64_t km = ballot(keep);
+        if (keep) {
+          const int pos = np + __popcll(km & ((1ull << w.lane) - 1ull));
+          if (pos < w.lcap) out[pos] = g[u];
+        }
+        np += __popcll(km);
+      }
+    }
+    if (np > w.lcap) {
+      w.overflow = true;
+      return np;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_sync();
+  return np;
+}
+
 // multiLayerNotFitMessage numbers (:1754-1793)
 __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
   const DevSnap& s = *w.s;
@@ -2012,30 +2090,39 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
         atomicOr(&bm[off >> 5], 1u << (off & 31));
       });
       wave_sync();
-      int cnt = base;
+      // marked leaves in index order -> scratch list (stores only) ...
+      int32_t* sorted = reinterpret_cast<int32_t*>(w.gkeys);
+      int ns = 0;
       for (int64_t j0 = 0; j0 < words; j0 += kWave) {
         const int64_t j = j0 + w.lane;
         const uint32_t word = j < words ? bm[j] : 0u;
-        int nk = 0;
-        for (uint32_t x = word; x; x &= x - 1) {
-          const int32_t leaf = mn + int32_t(j) * 32 + __builtin_ctz(x);
-          const int32_t v = use_ls ? w.get(F_LS, loff + leaf) : w.get(F_STATE, loff + leaf);
-          nk += (positive_only ? v > 0 : v != 0) ? 1 : 0;
-        }
         int tot;
-        int pos = cnt + wave_excl_scan(nk, &tot);
-        for (uint32_t x = word; x; x &= x - 1) {
-          const int32_t leaf = mn + int32_t(j) * 32 + __builtin_ctz(x);
-          const int32_t v = use_ls ? w.get(F_LS, loff + leaf) : w.get(F_STATE, loff + leaf);
-          if (positive_only ? v > 0 : v != 0) {
+        int pos = ns + wave_excl_scan(__popc(word), &tot);
+        for (uint32_t x = word; x; x &= x - 1) sorted[pos++] = mn + int32_t(j) * 32 + __builtin_ctz(x);
+        ns += tot;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      // ... then their counts with kU loads in flight, kept ones compacted in order
+      int cnt = base;
+      for (int b0 = 0; b0 < ns; b0 += kU * kWave) {
+        int32_t lf[kU], v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) lf[u] = sorted[min(b0 + u * kWave + w.lane, ns - 1)];
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = use_ls ? w.get(F_LS, loff + lf[u]) : w.get(F_STATE, loff + lf[u]);
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const bool keep = b0 + u * kWave + w.lane < ns && (positive_only ? v[u] > 0 : v[u] != 0);
+          const uint64_t km = ballot(keep);
+          if (keep) {
+            const int pos = cnt + __popcll(km & ((1ull << w.lane) - 1ull));
             if (pos < ent_cap) {
-              ent[2 * pos] = leaf;
-              ent[2 * pos + 1] = v;
+              ent[2 * pos] = lf[u];
+              ent[2 * pos + 1] = v[u];
             }
-            pos++;
           }
+          cnt += __popcll(km);
         }
-        cnt += tot;
       }
       wave_sync();
       return cnt - base;
@@ -2851,9 +2938,12 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
     int level = fitLevel;
     int32_t* spare = w.listA;
     for (; level < min(L - 1, ev.slice_level); level++) {  // above the slice level (:930-935)
-      int nch = gather_children(w, cur, ncur, level, w.listC);
+      // leaderless BestFit slice walk with rem > 0: only positive children can be taken
+      const bool positive = !w.leader && w.bf && go_div32(ev.count, ev.slice_size) > 0;
+      int32_t* kids = positive ? w.listD : w.listC;
+      int nch = positive ? gather_children_positive(w, cur, ncur, level, kids) : gather_children(w, cur, ncur, level, kids);
       int nn = 0;
-      bool ok2 = walk_sorted(w, w.listC, nch, level + 1, ev.count, leaderCount, ev.slice_size, true, 0, spare, &nn);
+      bool ok2 = walk_sorted(w, kids, nch, level + 1, ev.count, leaderCount, ev.slice_size, true, 0, spare, &nn);
       if (!ok2) o.assignment_nil = 1;
       int32_t* t = cur;
       cur = spare;
