@@ -131,7 +131,8 @@ struct kueue_tas_ctx {
   // phase-1 class computation scratch (kept to avoid reallocation)
   std::vector<int32_t> cls_rep, cls_sig, cls_of, sig_rep, cls_next, sig_next, cls_fastrep, cls_slot, cls_order;
   std::unordered_map<uint64_t, int32_t> cls_head, sig_head;
-  DevBuf<int32_t> d_overlay, d_tags;  // select's copy-on-write counters and ownership tags
+  DevBuf<int32_t> d_overlay, d_tags;
+  DevBuf<uint64_t> d_rack_pos;  // positive-child masks of the leaves' parents (fused fill)  // select's copy-on-write counters and ownership tags
   int32_t tag_epoch = 0;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
@@ -223,6 +224,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->h_stage.release();
   c->d_stage.release();
   c->d_overlay.release();
+  c->d_rack_pos.release();
   c->d_tags.release();
   c->d_lfc_ch.release();
   c->d_lfc_cp.release();
@@ -700,6 +702,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.nstat_R = s.R;
   b.fill_stats = nullptr;
   b.rack_fanout = 0;
+  b.rack_pos = nullptr;
   b.ctr_stride = ctr_stride;
   b.counters = c->d_counters.p;
   b.overlay = c->d_overlay.p;
@@ -762,6 +765,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.fill_stats = c->d_fill_stats.p;
     }
     b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
+    if (b.rack_fanout) {
+      HIPCHK(c, c->d_rack_pos.ensure(n * size_t(s.level_size[s.L - 2])));
+      b.rack_pos = c->d_rack_pos.p;
+    }
     if (ucols <= 4) hipLaunchKernelGGL(fill_leaves_staged_kernel<4>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (ucols <= 8) hipLaunchKernelGGL(fill_leaves_staged_kernel<8>, grid, dim3(256), 0, c->stream, s, b, umask);
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);

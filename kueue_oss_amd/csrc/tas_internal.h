@@ -123,6 +123,7 @@ struct DevBatch {
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)
+  uint64_t* rack_pos;      // [n][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rep rows)
   int64_t ctr_stride;      // int32 elements per eval (5 * SD)
   int32_t* counters;       // [n][5][SD]
   int32_t* taint_counts;   // [n][num_taints]

@@ -632,7 +632,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         has |= __shfl_xor(has, m, 64);
       }
       const int parent = leaf / F;
+      const uint64_t posm = ballot(valid && ss > 0);  // positive children, for the BestFit descent
       if ((lane & (F - 1)) == 0 && parent < s.level_size[s.L - 2]) {
+        const uint64_t seg = F == kWave ? posm : (posm >> lane) & ((1ull << F) - 1ull);
+        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + parent] = seg;
         const int32_t pswl = has ? w_sub(cap, minD) : 0;
         int32_t psswl = has ? w_sub(slc, minSD) : 0;
         if (s.L - 2 == slice_level) {
@@ -1012,6 +1015,7 @@ struct Wave {
   int lane;
   bool leader, lfc, bf, unconstrained;
   const int32_t* ctr;  // phase-1 counters of this eval's class (shared, read-only here)
+  const uint64_t* rack_pos;  // the class's positive-child masks of level L-2 (or null)
   int32_t* ov;         // private overlay [5][SD]
   int32_t* tag;        // [SD] overlay ownership tags
   int32_t my_tag;
@@ -1945,6 +1949,28 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
   int32_t* sh_ex = reinterpret_cast<int32_t*>(w.lds);  // [64] exclusive child offsets of the step's parents
   int32_t* sh_cb = sh_ex + kWave;                        // [64] first child of each
   int np = 0;
+  if (w.rack_pos && level == s.L - 2) {
+    // children are leaves: the fill's per-parent positive masks give them without loads
+    for (int i0 = 0; i0 < n; i0 += kWave) {
+      const int i = i0 + w.lane;
+      uint64_t m = 0;
+      int cb = 0;
+      if (i < n) {
+        const int p = parents[i] - poff;
+        m = w.rack_pos[p];
+        cb = co[p];
+      }
+      int tot;
+      int pos = np + wave_excl_scan(__popcll(m), &tot);
+      for (; m; m &= m - 1)
+        if (pos < w.lcap) out[pos++] = coff + cb + __builtin_ctzll(m);
+        else pos++;
+      np += tot;
+    }
+    if (np > w.lcap) w.overflow = true;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    return np;
+  }
   for (int i0 = 0; i0 < n; i0 += kWave) {
     const int i = i0 + w.lane;
     int cb = 0, cnt = 0;
@@ -2877,6 +2903,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   w.bf = !w.lfc;
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
   w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
+  w.rack_pos = b.rack_fanout ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
   w.ov = b.overlay + int64_t(eid) * b.ctr_stride;
   w.tag = b.tags + int64_t(eid) * s.SD;
   w.my_tag = b.tag_epoch;
