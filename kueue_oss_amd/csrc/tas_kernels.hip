@@ -2646,6 +2646,45 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       for (int i = w.lane; i < w.nblk; i += kWave)
         if (w.partials[i].bfst == pbst) pbk = key_min2(pbk, w.partials[i].bfkey);
       pbk = wave_min_key(pbk);
+    } else if (!w.leader) {
+      // no leader: keys (sliceState, state, index); the level's counters are
+      // read 4 domains per lane per load (levels start 16-byte aligned), 4
+      // loads per array in flight.  findLevelWithFitDomains never mutates.
+      const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
+      const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
+      const int nq = (D + 3) / 4;
+      Key inv = key_max();
+      constexpr int QU = 4;
+      for (int q0 = 0; q0 < nq; q0 += QU * kWave) {
+        int4 sa[QU], ssa[QU];
+#pragma unroll
+        for (int u = 0; u < QU; u++) {
+          const int q = min(q0 + u * kWave + w.lane, nq - 1);
+          sa[u] = S4[q];
+          ssa[u] = SS4[q];
+        }
+#pragma unroll
+        for (int u = 0; u < QU; u++) {
+          const int q = q0 + u * kWave + w.lane;
+          const int32_t st4[4] = {sa[u].x, sa[u].y, sa[u].z, sa[u].w};
+          const int32_t ss4[4] = {ssa[u].x, ssa[u].y, ssa[u].z, ssa[u].w};
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int i = 4 * q + k;
+            if (q < nq && i < D) {
+              const Key kk = key_wl(w.lfc, 0, ss4[k], st4[k], i);
+              top = key_min2(top, kk);
+              inv = key_min2(inv, Key{~kk.hi, ~kk.lo});
+              if (ss4[k] >= sliceCount) lfcfit = key_min2(lfcfit, kk);
+              minss = min(minss, ss4[k]);
+            }
+          }
+        }
+      }
+      top = wave_min_key(top);
+      lfcfit = wave_min_key(lfcfit);
+      inv = wave_min_key(inv);
+      last = Key{~inv.hi, ~inv.lo};
     } else {
       bool has_last = false;
       for (int i = w.lane; i < D; i += kWave) {
@@ -2675,6 +2714,44 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       if (w.get(f, topg) >= sliceCount) {
         if (use_partials) {
           topg = loff + int(uint32_t(pbk.lo));
+        } else if (!w.leader) {
+          // one vectorized pass: per lane the smallest (sliceState >= sliceCount, key), then a wave arg-min
+          const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
+          const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
+          const int nq = (D + 3) / 4;
+          uint32_t bst = ~0u;
+          Key bk = key_max();
+          constexpr int QU = 4;
+          for (int q0 = 0; q0 < nq; q0 += QU * kWave) {
+            int4 sa[QU], ssa[QU];
+#pragma unroll
+            for (int u = 0; u < QU; u++) {
+              const int q = min(q0 + u * kWave + w.lane, nq - 1);
+              sa[u] = S4[q];
+              ssa[u] = SS4[q];
+            }
+#pragma unroll
+            for (int u = 0; u < QU; u++) {
+              const int q = q0 + u * kWave + w.lane;
+              const int32_t st4[4] = {sa[u].x, sa[u].y, sa[u].z, sa[u].w};
+              const int32_t ss4[4] = {ssa[u].x, ssa[u].y, ssa[u].z, ssa[u].w};
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                const int i = 4 * q + k;
+                if (q < nq && i < D && ss4[k] >= sliceCount) {
+                  const uint32_t sw = s_asc(ss4[k]);
+                  const Key kk = key_wl(w.lfc, 0, ss4[k], st4[k], i);
+                  if (sw < bst || (sw == bst && key_lt(kk, bk))) {
+                    bst = sw;
+                    bk = kk;
+                  }
+                }
+              }
+            }
+          }
+          const uint32_t wbst = uint32_t(wave_min_u64(uint64_t(bst)));
+          bk = wave_min_key(bst == wbst ? bk : key_max());
+          topg = loff + int(uint32_t(bk.lo));
         } else {
           uint32_t bst = ~0u;
           for (int i = w.lane; i < D; i += kWave) {
