@@ -147,7 +147,7 @@ __device__ __forceinline__ Key key_wl(bool lfc, int32_t ls, int32_t sswl, int32_
 // K1: fillInCounts leaf loop
 // ----------------------------------------------------------------------------
 constexpr int kFillThreads = 256;
-constexpr int kEvalsPerBlock = 8;
+constexpr int kEvalsPerBlock = 16;
 
 enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3 };
 
