@@ -591,8 +591,13 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     }
     int32_t ss = 0, sswl = 0;
     if (s.L - 1 == slice_level) {
-      ss = go_div32(state, slice_size);
-      sswl = go_div32(swl, slice_size);
+      if (slice_size == 1) {  // wave-uniform: no integer division
+        ss = state;
+        sswl = swl;
+      } else {
+        ss = go_div32(state, slice_size);
+        sswl = leader ? go_div32(swl, slice_size) : ss;
+      }
     }
     int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
     const int64_t SD = s.SD;
@@ -626,10 +631,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       for (int m = 1; m < F; m <<= 1) {
         cap = w_add(cap, __shfl_xor(cap, m, 64));
         slc = w_add(slc, __shfl_xor(slc, m, 64));
-        minD = min(minD, __shfl_xor(minD, m, 64));
-        minSD = min(minSD, __shfl_xor(minSD, m, 64));
-        lead = max(lead, __shfl_xor(lead, m, 64));
-        has |= __shfl_xor(has, m, 64);
+      }
+      if (leader) {  // leader fields only matter for leader evals (parents of others keep state, sliceState)
+        for (int m = 1; m < F; m <<= 1) {
+          minD = min(minD, __shfl_xor(minD, m, 64));
+          minSD = min(minSD, __shfl_xor(minSD, m, 64));
+          lead = max(lead, __shfl_xor(lead, m, 64));
+          has |= __shfl_xor(has, m, 64);
+        }
       }
       const int parent = leaf / F;
       const uint64_t posm = ballot(valid && ss > 0);  // positive children, for the BestFit descent
