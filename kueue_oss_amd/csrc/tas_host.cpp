@@ -156,11 +156,29 @@ struct DomainAssignment {
   int32_t leaf;
   int32_t count;
 };
+// (leaf, count) pairs of one assignment: a view into the device layer's
+// packed entries (valid until its next batch) or into `own`.
+struct DomainSpan {
+  const DomainAssignment* p = nullptr;
+  size_t n = 0;
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const DomainAssignment& operator[](size_t i) const { return p[i]; }
+  const DomainAssignment* begin() const { return p; }
+  const DomainAssignment* end() const { return p + n; }
+};
 struct PodSetResult {
   std::string name;
   bool has_assignment = false;
-  std::vector<DomainAssignment> domains;  // leaf indices (lexicographic order)
+  DomainSpan domains;                  // leaf indices (lexicographic order)
+  std::vector<DomainAssignment> own;   // storage once the view is materialized
   std::string reason;
+  void materialize() {
+    if (domains.n && domains.p != own.data()) {
+      own.assign(domains.p, domains.p + domains.n);
+      domains.p = own.data();
+    }
+  }
 };
 
 struct Gates {  // pkg/features/kube_features.go (TASProfileMixed: Beta, default true)
@@ -909,7 +927,7 @@ struct Evaluator {
     for (size_t k = 0; k < n; k++)
       if (rs[k].name == name) {
         rs[k].has_assignment = has;
-        rs[k].domains.assign(d, d + nd);
+        rs[k].domains = DomainSpan{d, nd};
         rs[k].reason = reason;
         return;
       }
@@ -917,7 +935,7 @@ struct Evaluator {
     PodSetResult& r = rs[n++];
     r.name = name;
     r.has_assignment = has;
-    r.domains.assign(d, d + nd);
+    r.domains = DomainSpan{d, nd};  // zero-copy view of the batch's entries
     r.reason = reason;
   }
 
@@ -1010,6 +1028,9 @@ struct Evaluator {
         done[we.first] = 1;
       }
       if (bt->empty()) continue;
+      if (pass > 0)  // the next batch reuses the entries buffer the earlier views point into
+        for (size_t w = 0; w < wls.size(); w++)
+          for (size_t k = 0; k < used[w]; k++) (*results)[w][k].materialize();
       const double t_call = now_ms();
       host_ms[0] += t_call - t_start;
       const size_t n = bt->size();
