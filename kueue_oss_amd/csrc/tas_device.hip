@@ -68,6 +68,39 @@ struct HostBuf {  // pinned host staging
   }
 };
 
+// Open-addressing uint64 -> int32 map (linear probing), reset per batch
+// without freeing: the phase-1 class lookup of every eval.
+struct FlatMap {
+  std::vector<uint64_t> keys;
+  std::vector<int32_t> vals;  // -1: empty
+  size_t mask = 0;
+  void reset(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    if (keys.size() != cap) {
+      keys.assign(cap, 0);
+      vals.assign(cap, -1);
+    } else {
+      std::fill(vals.begin(), vals.end(), -1);
+    }
+    mask = cap - 1;
+  }
+  static size_t mix(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return size_t(k);
+  }
+  int32_t* find(uint64_t k) {  // the slot's value (-1 if absent)
+    for (size_t i = mix(k) & mask;; i = (i + 1) & mask) {
+      if (vals[i] < 0 || keys[i] == k) {
+        keys[i] = k;
+        return &vals[i];
+      }
+    }
+  }
+};
+
 // libdivide-style u64 magic for exact division by an invariant divisor d >= 1.
 void compute_magic(uint64_t d, DevTerm* t) {
   t->magic = 0;
@@ -117,12 +150,15 @@ struct kueue_tas_ctx {
   DevBuf<uint32_t> d_free_present, d_usage_present;
   // batch
   DevBuf<int32_t> d_counters;
-  DevBuf<int32_t> d_stats;  // taint counts | res counts | sel counts
-  DevBuf<kueue_tas_eval_out> d_out;
+  // results of a batch, one D2H: out[n] | offsets[n + 1] | stats (taint | res | sel counts)
+  DevBuf<uint8_t> d_res;
+  HostBuf<uint8_t> h_res;
+  kueue_tas_eval_out* res_out_h = nullptr;
+  int64_t* res_off_h = nullptr;
+  int32_t* res_stats_h = nullptr;
   DevBuf<int32_t> d_entries;
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
-  DevBuf<int64_t> d_offsets;
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
   DevBuf<int32_t> d_fill_stats;
@@ -130,7 +166,7 @@ struct kueue_tas_ctx {
   DevBuf<uint8_t> d_stage;
   // phase-1 class computation scratch (kept to avoid reallocation)
   std::vector<int32_t> cls_rep, cls_sig, cls_of, sig_rep, cls_next, sig_next, cls_fastrep, cls_slot, cls_order;
-  std::unordered_map<uint64_t, int32_t> cls_head, sig_head;
+  FlatMap cls_head, sig_head;
   DevBuf<int32_t> d_overlay, d_tags;
   DevBuf<uint64_t> d_rack_pos;  // positive-child masks of the leaves' parents (fused fill)  // select's copy-on-write counters and ownership tags
   int32_t tag_epoch = 0;
@@ -143,9 +179,6 @@ struct kueue_tas_ctx {
   std::vector<int32_t> last_prof;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
-  HostBuf<kueue_tas_eval_out> h_out;
-  HostBuf<int64_t> h_offsets;
-  HostBuf<int32_t> h_stats;
   std::vector<int32_t> last_ticks;    // per-eval select time (100 MHz ticks) of the last batch
   // packed (leaf, count) pairs of the last batch: pinned, device-mapped host
   // memory the pack kernel writes directly (no separate D2H copy or sync)
@@ -212,12 +245,11 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_free_present.release();
   c->d_usage_present.release();
   c->d_counters.release();
-  c->d_stats.release();
-  c->d_out.release();
+  c->d_res.release();
+  c->h_res.release();
   c->d_entries.release();
   c->d_scratch.release();
   c->d_deltas.release();
-  c->d_offsets.release();
   c->d_packed.release();
   c->d_partials.release();
   c->d_fill_stats.release();
@@ -234,11 +266,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_jobs.release();
   c->d_lfc_items.release();
   c->d_prof.release();
-  c->h_out.release();
   if (c->ent_host) (void)hipHostFree(c->ent_host);
   c->ent_host = c->ent_dev = nullptr;
-  c->h_offsets.release();
-  c->h_stats.release();
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -557,10 +586,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     cls_sig.clear();
     sig_rep.clear();
     cls_of.assign(n, -1);
-    std::unordered_map<uint64_t, int32_t>& cls_head = c->cls_head;
-    std::unordered_map<uint64_t, int32_t>& sig_head = c->sig_head;
-    cls_head.clear();
-    sig_head.clear();
+    FlatMap& cls_head = c->cls_head;
+    FlatMap& sig_head = c->sig_head;
+    cls_head.reset(n);
+    sig_head.reset(n);
     std::vector<int32_t>& cls_next = c->cls_next;  // chain of classes with the same hash
     std::vector<int32_t>& sig_next = c->sig_next;
     cls_next.clear();
@@ -570,33 +599,31 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       const uint64_t hs1 = sig_hash(e);
       const uint64_t hc = hs1 ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
       int32_t k = -1;
-      auto it = cls_head.find(hc);
-      if (it != cls_head.end())
-        for (int32_t q = it->second; q >= 0; q = cls_next[size_t(q)]) {
-          const DevEval& r = hev[cls_rep[size_t(q)]];
-          if (same_sig(e, r) && same_mask(e, r)) {
-            k = q;
-            break;
-          }
+      int32_t* head = cls_head.find(hc);
+      for (int32_t q = *head; q >= 0; q = cls_next[size_t(q)]) {
+        const DevEval& r = hev[cls_rep[size_t(q)]];
+        if (same_sig(e, r) && same_mask(e, r)) {
+          k = q;
+          break;
         }
+      }
       if (k < 0) {
         k = int32_t(cls_rep.size());
         cls_rep.push_back(int32_t(i));
-        cls_next.push_back(it != cls_head.end() ? it->second : -1);
-        cls_head[hc] = k;
+        cls_next.push_back(*head);
+        *head = k;
         int32_t sg = -1;
-        auto si = sig_head.find(hs1);
-        if (si != sig_head.end())
-          for (int32_t q = si->second; q >= 0; q = sig_next[size_t(q)])
-            if (same_sig(e, hev[sig_rep[size_t(q)]])) {
-              sg = q;
-              break;
-            }
+        int32_t* shead = sig_head.find(hs1);
+        for (int32_t q = *shead; q >= 0; q = sig_next[size_t(q)])
+          if (same_sig(e, hev[sig_rep[size_t(q)]])) {
+            sg = q;
+            break;
+          }
         if (sg < 0) {
           sg = int32_t(sig_rep.size());
           sig_rep.push_back(int32_t(i));
-          sig_next.push_back(si != sig_head.end() ? si->second : -1);
-          sig_head[hs1] = sg;
+          sig_next.push_back(*shead);
+          *shead = sg;
         }
         cls_sig.push_back(sg);
       }
@@ -672,8 +699,24 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
   const size_t stats_len = n * nt + n * size_t(s.R) + n;
-  HIPCHK(c, c->d_stats.ensure(stats_len));
-  HIPCHK(c, c->d_out.ensure(n));
+  const size_t res_off_offsets = (n * sizeof(kueue_tas_eval_out) + 15) / 16 * 16;
+  const size_t res_off_stats = res_off_offsets + ((n + 1) * 8 + 15) / 16 * 16;
+  const size_t res_bytes = res_off_stats + stats_len * 4;
+  HIPCHK(c, c->d_res.ensure(res_bytes));
+  HIPCHK(c, c->h_res.ensure(res_bytes));
+  kueue_tas_eval_out* d_out = reinterpret_cast<kueue_tas_eval_out*>(c->d_res.p);
+  int64_t* d_offsets = reinterpret_cast<int64_t*>(c->d_res.p + res_off_offsets);
+  int32_t* d_stats = reinterpret_cast<int32_t*>(c->d_res.p + res_off_stats);
+  c->res_out_h = reinterpret_cast<kueue_tas_eval_out*>(c->h_res.p);
+  c->res_off_h = reinterpret_cast<int64_t*>(c->h_res.p + res_off_offsets);
+  c->res_stats_h = reinterpret_cast<int32_t*>(c->h_res.p + res_off_stats);
+  // ExclusionStats are fully written by the fill's reduce (class reps) and the
+  // replication (other members) when the staged fill counts them in LDS
+  uint32_t umask = 0;
+  for (size_t i = 0; i < n; i++) umask |= hev[i].req_mask | hev[i].lead_mask;
+  const int ucols = __builtin_popcount(umask);
+  const int nstat_all = 1 + int(nt) + s.R;
+  const bool lds_stats = s.N > 0 && nfchunks > 0 && ucols <= 8 && nstat_all <= kMaxFillStats;
   HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));  // per-eval regions, packed after select
   HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
@@ -688,7 +731,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
 
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, stage_bytes, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, stats_len * 4, c->stream));
+  if (!lds_stats) HIPCHK(c, hipMemsetAsync(d_stats, 0, stats_len * 4, c->stream));
   uint8_t* ds = c->d_stage.p;
   DevBatch b{};
   b.evals = reinterpret_cast<const DevEval*>(ds + o_evals);
@@ -708,10 +751,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.overlay = c->d_overlay.p;
   b.tags = c->d_tags.p;
   b.tag_epoch = c->tag_epoch;
-  b.taint_counts = c->d_stats.p;
-  b.res_counts = c->d_stats.p + n * nt;
-  b.sel_counts = c->d_stats.p + n * nt + n * size_t(s.R);
-  b.out = c->d_out.p;
+  b.taint_counts = d_stats;
+  b.res_counts = d_stats + n * nt;
+  b.sel_counts = d_stats + n * nt + n * size_t(s.R);
+  b.out = d_out;
   b.entries = c->d_entries.p;
   b.entry_cap = entry_cap;
   b.scratch_stride = scratch_stride;
@@ -733,7 +776,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.lfc_jobs = c->d_lfc_jobs.p;
   b.lfc_nitems = reinterpret_cast<int32_t*>(c->d_lfc_items.p);  // item 0's slot holds the count
   b.lfc_items = c->d_lfc_items.p + 1;
-  HIPCHK(c, hipMemsetAsync(b.lfc_nitems, 0, sizeof(LfcItem), c->stream));
   b.prof = nullptr;
   if (KTAS_PROFILE) {
     HIPCHK(c, c->d_prof.ensure(n * P_NCAT));
@@ -752,13 +794,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->last_stats[0] += nfill;
   if (s.N > 0 && nfchunks > 0) {
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
-    uint32_t umask = 0;
-    for (size_t i = 0; i < n; i++) umask |= hev[i].req_mask | hev[i].lead_mask;
-    const int ucols = __builtin_popcount(umask);
     c->last_stats[2] += 1;
     c->last_stats[3] = ucols;
-    const int nstat = 1 + int(nt) + s.R;
-    b.nstat = (ucols <= 8 && nstat <= kMaxFillStats) ? nstat : 0;
+    const int nstat = nstat_all;
+    b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
     if (b.nstat) {
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
@@ -831,9 +870,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   // pack the per-eval entries: offsets (scan) + compaction, then one D2H of exactly the used pairs
-  HIPCHK(c, c->d_offsets.ensure(n + 1));
-  hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_out.p, int(n), entry_cap,
-                     c->d_offsets.p);
+  hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, d_out, int(n), entry_cap, d_offsets);
   HIPCHK(c, hipGetLastError());
   // pack the entries straight into the mapped host buffer (worst case n * entry_cap pairs)
   {
@@ -850,38 +887,33 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
     }
     hipLaunchKernelGGL(pack_entries_kernel, dim3(unsigned(n)), dim3(256), 0, c->stream, c->d_entries.p, entry_cap,
-                       c->d_offsets.p, c->ent_dev + c->ent_used, int(n));
+                       d_offsets, c->ent_dev + c->ent_used, int(n));
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
-  HIPCHK(c, c->h_out.ensure(n));
-  HIPCHK(c, c->h_offsets.ensure(n + 1));
-  HIPCHK(c, c->h_stats.ensure(stats_len));
-  HIPCHK(c, hipMemcpyAsync(c->h_out.p, c->d_out.p, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_offsets.p, c->d_offsets.p, (n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_stats.p, c->d_stats.p, stats_len * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   lap(3);
   int32_t need = 0;
-  for (size_t i = 0; i < n; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
+  for (size_t i = 0; i < n; i++) need = std::max(need, c->res_out_h[i].num_workers + c->res_out_h[i].num_leaders);
   if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
-  const int64_t total = c->h_offsets.p[n];
+  const int64_t total = c->res_off_h[n];
   c->ent_used += size_t(total) * 2;
   lap(4);
-  memcpy(out, c->h_out.p, n * sizeof(kueue_tas_eval_out));
+  memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
   if (KTAS_PROFILE) {
     const size_t base = c->last_prof.size();
     c->last_prof.resize(base + n * P_NCAT);
     HIPCHK(c, hipMemcpy(c->last_prof.data() + base, c->d_prof.p, n * P_NCAT * 4, hipMemcpyDeviceToHost));
   }
   for (size_t i = 0; i < n; i++) {
-    c->last_ticks.push_back(c->h_out.p[i].reserved[0]);
-    c->last_ticks.push_back(c->h_out.p[i].reserved[1]);
+    c->last_ticks.push_back(c->res_out_h[i].reserved[0]);
+    c->last_ticks.push_back(c->res_out_h[i].reserved[1]);
   }
-  for (size_t i = 0; i <= n; i++) offsets[i] = c->h_offsets.p[i];
-  if (taint_counts && nt) memcpy(taint_counts, c->h_stats.p, n * nt * 4);
-  if (res_counts && s.R) memcpy(res_counts, c->h_stats.p + n * nt, n * size_t(s.R) * 4);
+  for (size_t i = 0; i <= n; i++) offsets[i] = c->res_off_h[i];
+  if (taint_counts && nt) memcpy(taint_counts, c->res_stats_h, n * nt * 4);
+  if (res_counts && s.R) memcpy(res_counts, c->res_stats_h + n * nt, n * size_t(s.R) * 4);
   float st[KUEUE_TAS_NUM_STAGES] = {};
   for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&st[k], c->ev[k + 1], c->ev[k + 2]);
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
@@ -924,7 +956,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
         c->last_ticks.resize(2 * i0);
         c->last_prof.resize(KTAS_PROFILE ? i0 * P_NCAT : 0);
         int32_t need = 0;
-        for (size_t i = 0; i < m; i++) need = std::max(need, c->h_out.p[i].num_workers + c->h_out.p[i].num_leaders);
+        for (size_t i = 0; i < m; i++) need = std::max(need, c->res_out_h[i].num_workers + c->res_out_h[i].num_leaders);
         int cap = c->entry_cap;
         while (cap < need) cap *= 2;
         c->entry_cap = cap;

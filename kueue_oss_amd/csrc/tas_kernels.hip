@@ -983,6 +983,7 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
 // Per slot: exclusive prefix of every bin over the chunks, totals, overflow sum.
 __global__ __launch_bounds__(kLfcBins) void lfc_total_kernel(DevBatch b) {
   const int slot = blockIdx.x, bin = threadIdx.x;
+  if (slot == 0 && bin == 0) *b.lfc_nitems = 0;  // select appends the emit work items after this kernel
   const int64_t base = int64_t(slot) * b.lfc_nchunks;
   constexpr int U = 16;  // chunk counts loaded ahead of the running prefix
   uint32_t acc = 0;
