@@ -1593,9 +1593,15 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   const bool lfc = w.lfc;
   const int32_t rem = slices ? go_div32(count, sliceSize) : count;
   Key* keys = w.gkeys;
-  // pass A: keys, range of the primary component, minimum weight
+  uint64_t* hist = reinterpret_cast<uint64_t*>(w.lds);
+  for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+  wave_sync();
+  // pass A: keys, range of the primary component, minimum weight, and the
+  // weight per sliceState value for values in [0, kThrBins) (pass B when the
+  // values fall outside); all_eq: sliceState == state everywhere
   int32_t vmin = 0x7fffffff, vmax = int32_t(0x80000000u), wmin = 0x7fffffff;
   int64_t wsum = 0;
+  bool neq = false;
   for (int base = 0; base < n; base += kU * kWave) {
     int g[kU];
     int32_t ss[kU], st[kU];
@@ -1613,8 +1619,12 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
         keys[i] = key_plain(lfc, ss[u], st[u], g[u] - loff);
         vmin = min(vmin, ss[u]);
         vmax = max(vmax, ss[u]);
-        wmin = min(wmin, slices ? ss[u] : st[u]);
-        wsum += slices ? ss[u] : st[u];
+        const int32_t wt = slices ? ss[u] : st[u];
+        wmin = min(wmin, wt);
+        wsum += wt;
+        neq |= ss[u] != st[u];
+        if (wt > 0 && ss[u] >= 0 && ss[u] < kThrBins)
+          atomicAdd((unsigned long long*)&hist[ss[u]], (unsigned long long)wt);
       }
     }
   }
@@ -1625,9 +1635,10 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     vmax = max(vmax, __shfl_xor(vmax, m, 64));
     wmin = min(wmin, __shfl_xor(wmin, m, 64));
   }
+  const bool all_eq = ballot(neq) == 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_sync();
   if (wmin < 0 || wsum >= (int64_t(1) << 31)) return -1;  // int32 rem arithmetic never wraps
-  uint64_t* hist = reinterpret_cast<uint64_t*>(w.lds);
   Key ck;          // key of the crossing element
   int32_t remc;    // rem left when the walk reaches it
   if (rem <= 0) {  // the first element already satisfies rem
@@ -1637,20 +1648,30 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     remc = rem;
   } else {
     if (int64_t(vmax) - int64_t(vmin) >= kThrBins) return -1;
-    // pass B: weight per sliceState value
-    for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
-    wave_sync();
-    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
-      const int32_t ss = kp_ss(lfc, k);
-      const int32_t wt = slices ? ss : kp_st(k);
-      if (wt > 0) atomicAdd((unsigned long long*)&hist[ss - vmin], (unsigned long long)wt);
-    });
-    wave_sync();
+    int32_t hbase = 0;  // value of bin 0
+    if (vmin < 0 || vmax >= kThrBins) {
+      // pass B: weight per sliceState value, bins from vmin
+      hbase = vmin;
+      for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+      wave_sync();
+      wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
+        const int32_t ss = kp_ss(lfc, k);
+        const int32_t wt = slices ? ss : kp_st(k);
+        if (wt > 0) atomicAdd((unsigned long long*)&hist[ss - vmin], (unsigned long long)wt);
+      });
+      wave_sync();
+    }
     int64_t before1;
     const int b1 = bins_threshold(hist, !lfc, rem, &before1);
     if (b1 < 0) return 0;  // the list cannot hold rem (:1469)
-    const int32_t t = vmin + b1;
+    const int32_t t = hbase + b1;
     const int64_t rem1 = rem - before1;
+    int32_t u;
+    int64_t rem2;
+    if (all_eq) {  // class t holds state t only
+      u = t;
+      rem2 = rem1;
+    } else {
     // pass C: state range inside class t
     int32_t umin = 0x7fffffff, umax = int32_t(0x80000000u);
     wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
@@ -1679,8 +1700,9 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     int64_t before2;
     const int b2 = bins_threshold(hist, false, rem1, &before2);
     if (b2 < 0) return -1;  // unreachable: class t holds rem1
-    const int32_t u = umin + b2;
-    const int64_t rem2 = rem1 - before2;
+    u = umin + b2;
+    rem2 = rem1 - before2;
+    }
     const int64_t wt = slices ? t : u;  // > 0: the class added weight
     const int64_t m = (rem2 + wt - 1) / wt;
     remc = int32_t(rem2 - (m - 1) * wt);
@@ -1702,26 +1724,12 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     ck = key_plain(lfc, t, u, int32_t(kth));
     wave_sync();
   }
-  int chosen = loff + int(uint32_t(ck.lo));
-  if (w.bf) {  // findBestFitDomainBy over the crossing and everything after it (:1216-1231)
-    // one pass: per lane the best (weight, key) pair, then a wave arg-min
-    uint32_t bst = ~0u;
-    Key best = key_max();
-    wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
-      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
-      if (key_le(ck, k) && wt >= remc) {
-        const uint32_t sw = s_asc(wt);
-        if (sw < bst || (sw == bst && key_lt(k, best))) {
-          bst = sw;
-          best = k;
-        }
-      }
-    });
-    const uint32_t wbst = uint32_t(wave_min_u64(bst));
-    best = wave_min_key(bst == wbst ? best : key_max());
-    chosen = loff + int(uint32_t(best.lo));
-  }
-  // pass F: emit the whole elements before the crossing (lane-private stores)
+  // one pass: emit the whole elements before the crossing (lane-private
+  // stores) and, BestFit, find the best fit over the crossing and everything
+  // after it (findBestFitDomainBy :1216-1231: per lane (weight, key), then a
+  // wave arg-min)
+  uint32_t bst = ~0u;
+  Key best = key_max();
   int cnt = *np;
   wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
     const bool take = valid && key_lt(k, ck);
@@ -1731,9 +1739,24 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
       const int g = loff + int(uint32_t(k.lo));
       if (slices) w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));  // !leader: no F_LS
       if (pos < w.lcap) out[pos] = g;
+    } else if (valid && w.bf) {
+      const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
+      if (wt >= remc) {
+        const uint32_t sw = s_asc(wt);
+        if (sw < bst || (sw == bst && key_lt(k, best))) {
+          bst = sw;
+          best = k;
+        }
+      }
     }
     cnt += __popcll(bm);
   });
+  int chosen = loff + int(uint32_t(ck.lo));
+  if (w.bf) {
+    const uint32_t wbst = uint32_t(wave_min_u64(bst));
+    best = wave_min_key(bst == wbst ? best : key_max());
+    chosen = loff + int(uint32_t(best.lo));
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   // the crossing element (or its best fit) takes the remainder
   w.set(F_LS, chosen, 0);
