@@ -211,10 +211,11 @@ int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
  * ticks[2i+1] the findLevelWithFitDomains part.  ticks holds 2n values. */
 int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
-/* Diagnostics (profiling build libkueue_tas_prof.so; zeros otherwise): 8
+/* Diagnostics (profiling build libkueue_tas_prof.so; zeros otherwise): 12
  * inclusive select-phase tick counters per eval of the last batch (LDS sort,
  * threshold walk, child gather, emit, sorted walk, global sort, count
- * update, findLevelWithFitDomains).  ticks holds 8n values. */
+ * update, findLevelWithFitDomains, threshold-walk keys / k-th select / emit,
+ * setup).  ticks holds 12n values. */
 int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
 /* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request

@@ -1016,7 +1016,10 @@ enum Field : int { F_STATE = 0, F_SLICE = 1, F_SWL = 2, F_SSWL = 3, F_LS = 4 };
 #ifndef KTAS_PROFILE
 #define KTAS_PROFILE 0
 #endif
-enum ProfCat : int { P_LDS_SORT = 0, P_THRESHOLD, P_GATHER, P_EMIT, P_WALK, P_GLOBAL_SORT, P_UPDATE, P_FIND, P_NCAT };
+enum ProfCat : int {
+  P_LDS_SORT = 0, P_THRESHOLD, P_GATHER, P_EMIT, P_WALK, P_GLOBAL_SORT, P_UPDATE, P_FIND,
+  P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_NCAT
+};
 
 struct Wave {
   const DevSnap* s;
@@ -1496,23 +1499,38 @@ __device__ __forceinline__ void wave_for_all(int n, Load load, Body body) {
 }
 
 
-// m-th smallest (1-based) of cnt uint32 values in LDS (one wave): MSB-first
-// radix select with 8-bit digits (4 histogram rounds, no sort).
-__device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* hist, int lane) {
+// m-th smallest (1-based) of cnt uint32 values < 2^bits in LDS (one wave):
+// MSB-first radix select with 9-bit digits (hist: 512 LDS words), no sort.
+__device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* hist, int lane, int bits,
+                                   int digit_bits) {
+  if (m == cnt || m == 1) {  // the maximum / minimum: one reduction
+    uint32_t r = m == 1 ? ~0u : 0u;
+    for (int i = lane; i < cnt; i += kWave) r = m == 1 ? min(r, v[i]) : max(r, v[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t o = __shfl_xor(r, d, 64);
+      r = m == 1 ? min(r, o) : max(r, o);
+    }
+    return r;
+  }
+  const int NB = 1 << digit_bits;  // 256 or 512
   uint32_t prefix = 0, pmask = 0;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = lane; i < 256; i += kWave) hist[i] = 0;
+  const int rounds = (bits + digit_bits - 1) / digit_bits;
+  for (int rd = rounds - 1; rd >= 0; rd--) {
+    const int shift = rd * digit_bits;
+    for (int i = lane; i < NB; i += kWave) hist[i] = 0;
     wave_sync();
     for (int i = lane; i < cnt; i += kWave) {
       const uint32_t x = v[i];
-      if ((x & pmask) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+      if ((x & pmask) == prefix) atomicAdd(&hist[(x >> shift) & uint32_t(NB - 1)], 1u);
     }
     wave_sync();
-    uint32_t c[4];
+    const int PER = NB / kWave;  // bins per lane (4 or 8)
+    uint32_t c[8];
     uint32_t lsum = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      c[k] = hist[4 * lane + k];
+    for (int k = 0; k < 8; k++) {
+      c[k] = k < PER ? hist[PER * lane + k] : 0u;
       lsum += c[k];
     }
     uint32_t x = lsum;
@@ -1526,14 +1544,14 @@ __device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* 
     uint32_t before = x - lsum;
     if (lane == src) {
       int k = 0;
-      while (k < 3 && before + c[k] < uint32_t(m)) before += c[k++];
-      digit = 4 * lane + k;
+      while (k < PER - 1 && before + c[k] < uint32_t(m)) before += c[k++];
+      digit = PER * lane + k;
     }
     digit = __shfl(digit, src, 64);
     before = __shfl(before, src, 64);
     m -= int(before);
     prefix |= uint32_t(digit) << shift;
-    pmask |= 255u << shift;
+    pmask |= uint32_t(NB - 1) << shift;
     wave_sync();
   }
   return prefix;
@@ -1602,6 +1620,8 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   int32_t vmin = 0x7fffffff, vmax = int32_t(0x80000000u), wmin = 0x7fffffff;
   int64_t wsum = 0;
   bool neq = false;
+  {
+  ProfScope ps_keys(w, P_TW_KEYS);
   for (int base = 0; base < n; base += kU * kWave) {
     int g[kU];
     int32_t ss[kU], st[kU];
@@ -1627,6 +1647,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
           atomicAdd((unsigned long long*)&hist[ss[u]], (unsigned long long)wt);
       }
     }
+  }
   }
   wsum = wave_sum_i64(wsum);
 #pragma unroll
@@ -1709,7 +1730,8 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     // pass E: the m-th smallest index of class (t, u) (radix select in LDS)
     wave_sync();
     uint32_t* cand = reinterpret_cast<uint32_t*>(w.lds);
-    const int ccap = w.cap * 4 - 256;  // uint32 slots; the last 256 hold the digit histogram
+    const int dbits = w.cap >= 512 ? 9 : 8;         // radix-select digit width (histogram 2^dbits words)
+    const int ccap = w.cap * 4 - (1 << dbits);      // uint32 candidate slots before the histogram
     int cnt = 0;
     wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
       const bool in = valid && kp_ss(lfc, k) == t && kp_st(k) == u;
@@ -1720,7 +1742,12 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     });
     if (cnt > ccap) return -1;
     wave_sync();
-    const uint32_t kth = lds_select_kth(cand, cnt, int(m), cand + ccap, w.lane);
+    uint32_t kth;
+    {
+      ProfScope ps_sel(w, P_TW_SELECT);
+      const int nbits = 32 - __builtin_clz(uint32_t(max(w.s->level_size[level] - 1, 1)));  // indices < level size
+      kth = lds_select_kth(cand, cnt, int(m), cand + ccap, w.lane, nbits, dbits);
+    }
     ck = key_plain(lfc, t, u, int32_t(kth));
     wave_sync();
   }
@@ -1731,13 +1758,16 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   uint32_t bst = ~0u;
   Key best = key_max();
   int cnt = *np;
+  ProfScope ps_emit(w, P_TW_EMIT);
   wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
     const bool take = valid && key_lt(k, ck);
     const uint64_t bm = ballot(take);
     const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
     if (take) {
       const int g = loff + int(uint32_t(k.lo));
-      if (slices) w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));  // !leader: no F_LS
+      // !leader: no F_LS; the value only changes if sliceSize * sliceState != state
+      if (slices && w_mul(kp_ss(lfc, k), sliceSize) != kp_st(k))
+        w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));
       if (pos < w.lcap) out[pos] = g;
     } else if (valid && w.bf) {
       const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
@@ -1831,7 +1861,8 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   for (int i = w.lane; i < cross; i += kWave) {
     const Key k = w.lds[i];
     const int g = loff + int(uint32_t(k.lo));
-    if (slices) w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));  // !leader: no F_LS
+    if (slices && w_mul(kp_ss(lfc, k), sliceSize) != kp_st(k))  // !leader: no F_LS; only real changes
+      w.set_walked(g, w_mul(kp_ss(lfc, k), sliceSize), kp_ss(lfc, k));
     if (cnt + i < w.lcap) out[cnt + i] = g;
   }
   cnt += cross;
@@ -3051,6 +3082,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
   for (int c = 0; c < KUEUE_TAS_MAX_LAYERS; c++) o.ml_fit[c] = o.ml_need[c] = 0;
   o.reserved[0] = o.reserved[1] = 0;
 
+  if (KTAS_PROFILE) w.prof[P_SETUP] = wall_clock64() - t_begin;
   int nres = 0, fitLevel = 0;
   int r;
   const int lslot = b.lfc_slot[eid];

@@ -195,13 +195,15 @@ class TASFlavorSnapshot:
         self._lib.kueue_tas_host_last_eval_ticks(self._h, buf, n)
         return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
-    PROF = ("lds_sort", "threshold_walk", "gather", "emit", "walk_sorted", "global_sort", "update_counts", "find_level")
+    PROF = ("lds_sort", "threshold_walk", "gather", "emit", "walk_sorted", "global_sort", "update_counts", "find_level",
+            "tw_keys", "tw_select", "tw_emit", "setup")
 
     def last_eval_profile(self, n: int):
         """Profiling build only: inclusive select-phase ticks per eval, dicts keyed by PROF."""
-        buf = (ctypes.c_int32 * (8 * n))()
+        k = len(self.PROF)
+        buf = (ctypes.c_int32 * (k * n))()
         self._lib.kueue_tas_host_last_eval_profile(self._h, buf, n)
-        return [dict(zip(self.PROF, buf[8 * i: 8 * i + 8])) for i in range(n)]
+        return [dict(zip(self.PROF, buf[k * i: k * i + k])) for i in range(n)]
 
     DEVICE_HOST = ("compile", "classes", "enqueue", "wait", "pack_d2h", "copy_out")
 
