@@ -81,7 +81,7 @@ def main():
         dist = dist_mod
 
     from kueue_oss_amd import TASFlavorSnapshot, synth
-    from kueue_oss_amd.sharding import shard_workloads
+    from kueue_oss_amd.sharding import gather_records, shard_workloads
 
     gen = synth.CONFIGS[a.config]
     t0 = time.time()
@@ -128,10 +128,8 @@ def main():
         nonlocal rec, gathered
         h = snap.run_compiled()
         if dist is not None:
-            r = torch.tensor(snap.last_records(len(mine)), dtype=torch.int32, device=f"cuda:{local_rank}")
-            out = [torch.empty_like(r) for _ in range(world)]
-            dist.all_gather(out, r)  # RCCL all-gather of assignment records over xGMI
-            gathered = out
+            # RCCL all-gather of the per-workload result records over xGMI (shards differ in size: padded)
+            gathered = gather_records(snap.last_records(len(mine)), world, dist, device=f"cuda:{local_rank}")
         return h
 
     for _ in range(a.warmup):
@@ -156,7 +154,7 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    placements = len(mine) * world * a.steps
+    placements = len(all_wls) * a.steps  # every rank's shard, all steps
     value = placements / dt
 
     batches, evals, leader_evals = counts

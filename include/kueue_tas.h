@@ -154,8 +154,11 @@ typedef struct {
   int32_t list_cap;               /* LDS sort capacity per wave (test knob; 0 = default) */
   int32_t max_batch;              /* evaluations per device batch (0 = default 1024) */
   int32_t device;                 /* HIP device ordinal */
-  int32_t reserved;
+  int32_t flags;                  /* KUEUE_TAS_CFG_* */
 } kueue_tas_config;
+/* host layer: copy the entries through kueue_tas_eval_batch's packed buffer
+ * instead of reading the zero-copy view (exercises both ABI paths) */
+#define KUEUE_TAS_CFG_PACKED_ENTRIES 1
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);
@@ -175,7 +178,11 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* ctx, const kueue_tas_delta* d
  *  out:           [n] result headers
  *  entry_offsets: [n+1] the (leaf, count) int32 pairs of request i are
  *                 entries[2*off[i] .. 2*off[i+1]): workers, then leaders
- *  entries:       packed pairs, capacity `entries_capacity` pairs
+ *  entries:       packed pairs, capacity `entries_capacity` pairs; NULL: no
+ *                 copy — entry_offsets then index (in pairs) the zero-copy
+ *                 buffer of kueue_tas_last_entries(), where each request owns
+ *                 a region and off[i+1] - off[i] is its capacity, not its
+ *                 count (count = out[i].num_workers + out[i].num_leaders)
  *  taint_counts:  [n * num_taints] per-request taint exclusion counts (may be NULL)
  *  res_counts:    [n * num_cols]   per-request resource exclusion counts (may be NULL)
  * Returns KUEUE_TAS_OK; KUEUE_TAS_EOVERFLOW when the packed entries exceed
@@ -199,10 +206,11 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 
 /* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
- * events on the ctx stream, summed over its chunks): [0] fill, [1] roll-up
- * (all levels), [2] phase-1 replication to duplicate evals, [3] leaf-level
- * selection partials, [4] select/descend, [5] entry offsets, [6] total from
- * the request upload to the entry offsets.  Copies min(n, 7) values. */
+ * events on the ctx stream, summed over its chunks): [0] fill (+ exclusion
+ * stats reduce), [1] roll-up of the remaining levels, [2] exclusion-stats
+ * replication to duplicate evals, [3] leaf-level tables (LFC histograms,
+ * selection partials), [4] select/descend + LFC emit, [5] reserved (0), [6]
+ * total from the request upload to the end of select.  Copies min(n, 7). */
 #define KUEUE_TAS_NUM_STAGES 7
 int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
 

@@ -150,13 +150,11 @@ struct kueue_tas_ctx {
   DevBuf<uint32_t> d_free_present, d_usage_present;
   // batch
   DevBuf<int32_t> d_counters;
-  // results of a batch, one D2H: out[n] | offsets[n + 1] | stats (taint | res | sel counts)
+  // results of a batch, one D2H: out[n] | stats (taint | res | sel counts)
   DevBuf<uint8_t> d_res;
   HostBuf<uint8_t> h_res;
   kueue_tas_eval_out* res_out_h = nullptr;
-  int64_t* res_off_h = nullptr;
   int32_t* res_stats_h = nullptr;
-  DevBuf<int32_t> d_entries;
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
   DevBuf<int32_t> d_packed;
@@ -186,6 +184,9 @@ struct kueue_tas_ctx {
   int32_t* ent_dev = nullptr;
   size_t ent_cap = 0;   // int32 capacity
   size_t ent_used = 0;  // int32 used by the last batch
+  int32_t ent_stride = 0;              // pairs per eval region of the last chunk
+  std::vector<int32_t> ent_count;      // pairs written per eval of the last batch (request order)
+  std::vector<int64_t> ent_strided_off;  // their region offsets (pairs) in ent_host
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
@@ -247,7 +248,6 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_counters.release();
   c->d_res.release();
   c->h_res.release();
-  c->d_entries.release();
   c->d_scratch.release();
   c->d_deltas.release();
   c->d_packed.release();
@@ -699,16 +699,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
   const size_t stats_len = n * nt + n * size_t(s.R) + n;
-  const size_t res_off_offsets = (n * sizeof(kueue_tas_eval_out) + 15) / 16 * 16;
-  const size_t res_off_stats = res_off_offsets + ((n + 1) * 8 + 15) / 16 * 16;
+  const size_t res_off_stats = (n * sizeof(kueue_tas_eval_out) + 15) / 16 * 16;
   const size_t res_bytes = res_off_stats + stats_len * 4;
   HIPCHK(c, c->d_res.ensure(res_bytes));
   HIPCHK(c, c->h_res.ensure(res_bytes));
   kueue_tas_eval_out* d_out = reinterpret_cast<kueue_tas_eval_out*>(c->d_res.p);
-  int64_t* d_offsets = reinterpret_cast<int64_t*>(c->d_res.p + res_off_offsets);
   int32_t* d_stats = reinterpret_cast<int32_t*>(c->d_res.p + res_off_stats);
   c->res_out_h = reinterpret_cast<kueue_tas_eval_out*>(c->h_res.p);
-  c->res_off_h = reinterpret_cast<int64_t*>(c->h_res.p + res_off_offsets);
   c->res_stats_h = reinterpret_cast<int32_t*>(c->h_res.p + res_off_stats);
   // ExclusionStats are fully written by the fill's reduce (class reps) and the
   // replication (other members) when the staged fill counts them in LDS
@@ -717,7 +714,23 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int ucols = __builtin_popcount(umask);
   const int nstat_all = 1 + int(nt) + s.R;
   const bool lds_stats = s.N > 0 && nfchunks > 0 && ucols <= 8 && nstat_all <= kMaxFillStats;
-  HIPCHK(c, c->d_entries.ensure(n * size_t(entry_cap) * 2));  // per-eval regions, packed after select
+  // per-eval entry regions [n][entry_cap] pairs in pinned, device-mapped host
+  // memory: select / lfc_emit write the (leaf, count) pairs the host reads
+  // after the batch's one sync (no offsets/pack kernels, no entries D2H)
+  {
+    const size_t need_ints = c->ent_used + size_t(n) * size_t(entry_cap) * 2;
+    if (need_ints > c->ent_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      size_t cap = std::max<size_t>(need_ints, 2 * c->ent_cap);
+      int32_t* p = nullptr;
+      HIPCHK(c, hipHostMalloc(&p, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
+      if (c->ent_used) memcpy(p, c->ent_host, c->ent_used * 4);
+      if (c->ent_host) (void)hipHostFree(c->ent_host);
+      c->ent_host = p;
+      c->ent_cap = cap;
+      HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
+    }
+  }
   HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
   HIPCHK(c, c->d_lfc_items.ensure(size_t(std::max(nfast, 1)) * size_t(std::max(nchunks, 1)) + 1));
@@ -755,7 +768,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.res_counts = d_stats + n * nt;
   b.sel_counts = d_stats + n * nt + n * size_t(s.R);
   b.out = d_out;
-  b.entries = c->d_entries.p;
+  b.entries = c->ent_dev + c->ent_used;
   b.entry_cap = entry_cap;
   b.scratch_stride = scratch_stride;
   b.scratch = c->d_scratch.p;
@@ -869,27 +882,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
-  // pack the per-eval entries: offsets (scan) + compaction, then one D2H of exactly the used pairs
-  hipLaunchKernelGGL(entry_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, d_out, int(n), entry_cap, d_offsets);
-  HIPCHK(c, hipGetLastError());
-  // pack the entries straight into the mapped host buffer (worst case n * entry_cap pairs)
-  {
-    const size_t need_ints = c->ent_used + size_t(n) * size_t(entry_cap) * 2;
-    if (need_ints > c->ent_cap) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      size_t cap = std::max<size_t>(need_ints, 2 * c->ent_cap);
-      int32_t* p = nullptr;
-      HIPCHK(c, hipHostMalloc(&p, cap * 4, hipHostMallocMapped | hipHostMallocCoherent));
-      if (c->ent_used) memcpy(p, c->ent_host, c->ent_used * 4);
-      if (c->ent_host) (void)hipHostFree(c->ent_host);
-      c->ent_host = p;
-      c->ent_cap = cap;
-      HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
-    }
-    hipLaunchKernelGGL(pack_entries_kernel, dim3(unsigned(n)), dim3(256), 0, c->stream, c->d_entries.p, entry_cap,
-                       d_offsets, c->ent_dev + c->ent_used, int(n));
-    HIPCHK(c, hipGetLastError());
-  }
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
@@ -898,8 +890,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   int32_t need = 0;
   for (size_t i = 0; i < n; i++) need = std::max(need, c->res_out_h[i].num_workers + c->res_out_h[i].num_leaders);
   if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
-  const int64_t total = c->res_off_h[n];
-  c->ent_used += size_t(total) * 2;
+  const int64_t base_pairs = int64_t(c->ent_used / 2);
+  for (size_t i = 0; i <= n; i++) offsets[i] = base_pairs + int64_t(i) * entry_cap;  // strided regions
+  for (size_t i = 0; i < n; i++)
+    c->ent_count.push_back(std::min(c->res_out_h[i].num_workers + c->res_out_h[i].num_leaders, entry_cap));
+  c->ent_used += size_t(n) * size_t(entry_cap) * 2;
+  c->ent_stride = entry_cap;
   lap(4);
   memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
   if (KTAS_PROFILE) {
@@ -911,7 +907,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     c->last_ticks.push_back(c->res_out_h[i].reserved[0]);
     c->last_ticks.push_back(c->res_out_h[i].reserved[1]);
   }
-  for (size_t i = 0; i <= n; i++) offsets[i] = c->res_off_h[i];
   if (taint_counts && nt) memcpy(taint_counts, c->res_stats_h, n * nt * 4);
   if (res_counts && s.R) memcpy(res_counts, c->res_stats_h + n * nt, n * size_t(s.R) * 4);
   float st[KUEUE_TAS_NUM_STAGES] = {};
@@ -936,6 +931,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   float ms[4] = {0, 0, 0, 0};
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   c->ent_used = 0;
+  c->ent_count.clear();
   c->last_ticks.clear();
   c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
@@ -953,6 +949,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
         c->ent_used = keep;
+        c->ent_count.resize(i0);
         c->last_ticks.resize(2 * i0);
         c->last_prof.resize(KTAS_PROFILE ? i0 * P_NCAT : 0);
         int32_t need = 0;
@@ -965,16 +962,21 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
       if (rc) return rc;
       break;
     }
-    const int64_t base = entry_offsets[i0];
-    for (size_t i = 1; i <= m; i++) entry_offsets[i0 + i] = base + off[i];
+    for (size_t i = 0; i <= m; i++) entry_offsets[i0 + i] = off[i];
   }
   memcpy(c->last_ms, ms, sizeof ms);
   memcpy(c->last_stage_ms, stage_ms, sizeof stage_ms);
-  const size_t total = c->ent_used / 2;
-  if (!entries) return KUEUE_TAS_OK;  // caller reads kueue_tas_last_entries()
-  if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
-  if (total) memcpy(entries, c->ent_host, total * 8);
-  return KUEUE_TAS_OK;
+  c->ent_strided_off.assign(entry_offsets, entry_offsets + n + 1);
+  if (!entries) return KUEUE_TAS_OK;  // strided offsets into kueue_tas_last_entries()
+  // packed layout for the caller
+  int64_t total = 0;
+  for (size_t i = 0; i < n; i++) {
+    entry_offsets[i] = total;
+    total += c->ent_count[i];
+  }
+  entry_offsets[n] = total;
+  if (size_t(total) > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
+  return kueue_tas_fetch_entries(c, entries, entries_capacity);
 }
 
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* c, size_t* num_pairs) {
@@ -985,9 +987,15 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* c, size_t* num_pairs) {
 
 int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_capacity) {
   if (!c) return KUEUE_TAS_EINVAL;
-  const size_t total = c->ent_used / 2;
+  size_t total = 0;
+  for (int32_t k : c->ent_count) total += size_t(k);
   if (total > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
-  if (total) memcpy(entries, c->ent_host, total * 8);
+  size_t pos = 0;
+  for (size_t i = 0; i < c->ent_count.size(); i++) {
+    const size_t k = size_t(c->ent_count[i]);
+    if (k) memcpy(entries + 2 * pos, c->ent_host + 2 * size_t(c->ent_strided_off[i]), k * 8);
+    pos += k;
+  }
   return KUEUE_TAS_OK;
 }
 

@@ -1038,14 +1038,21 @@ struct Evaluator {
       offsets.resize(n + 1);
       taint_counts.resize(n * std::max<size_t>(T, 1));
       res_counts.resize(n * R);
+      const bool packed = (snap->cfg.flags & KUEUE_TAS_CFG_PACKED_ENTRIES) != 0;
+      if (packed && entries.size() < 2 * 64 * n) entries.resize(2 * 64 * n);
       rc = kueue_tas_eval_batch(snap->ctx, rq->data(), n, tt->data(), tt->size(), int32_t(T), assumed.data(),
-                                assumed.size(), outs.data(), offsets.data(), nullptr, 0, taint_counts.data(),
-                                res_counts.data());
+                                assumed.size(), outs.data(), offsets.data(), packed ? entries.data() : nullptr,
+                                packed ? entries.size() / 2 : 0, taint_counts.data(), res_counts.data());
+      if (rc == KUEUE_TAS_EOVERFLOW && packed) {
+        entries.resize(size_t(offsets[n]) * 2 + 2);
+        rc = kueue_tas_fetch_entries(snap->ctx, entries.data(), entries.size() / 2);
+      }
       if (rc) {
         snap->err = std::string("eval: ") + kueue_tas_last_error(snap->ctx);
         return rc;
       }
-      const int32_t* ent_view = kueue_tas_last_entries(snap->ctx, nullptr);  // zero-copy (pinned)
+      // zero-copy view (pinned, strided regions) or the packed copy
+      const int32_t* ent_view = packed ? entries.data() : kueue_tas_last_entries(snap->ctx, nullptr);
       const double t_decode = now_ms();
       host_ms[1] += t_decode - t_call;
       float t4[4];

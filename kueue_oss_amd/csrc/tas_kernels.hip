@@ -3235,46 +3235,6 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
   }
 }
 
-// Packed result entries: offsets[i] = sum_{j<i} min(count_j, cap) (single block).
-__global__ __launch_bounds__(1024) void entry_offsets_kernel(const kueue_tas_eval_out* out, int n, int cap,
-                                                             int64_t* offsets) {
-  __shared__ int64_t warp_sums[16];
-  __shared__ int64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int base = 0; base < n; base += 1024) {
-    int i = base + int(threadIdx.x);
-    int64_t v = 0;
-    if (i < n) v = min(out[i].num_workers + out[i].num_leaders, cap);
-    // inclusive wave scan
-    int64_t x = v;
-    const int lane = lane_id();
-    for (int d = 1; d < 64; d <<= 1) {
-      int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane - d, 0)));
-      if (lane >= d) x += y;
-    }
-    if (lane == 63) warp_sums[threadIdx.x >> 6] = x;
-    __syncthreads();
-    int64_t wpre = 0;
-    for (int k = 0; k < int(threadIdx.x >> 6); k++) wpre += warp_sums[k];
-    if (i < n) offsets[i] = carry + wpre + x - v;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry += wpre + x;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) offsets[n] = carry;
-}
-
-__global__ __launch_bounds__(256) void pack_entries_kernel(const int32_t* entries, int cap, const int64_t* offsets,
-                                                           int32_t* packed, int n) {
-  const int i = blockIdx.x;
-  if (i >= n) return;
-  const int64_t o = offsets[i];
-  const int cnt = int(offsets[i + 1] - o);
-  const int32_t* src = entries + int64_t(i) * cap * 2;
-  for (int k = threadIdx.x; k < 2 * cnt; k += blockDim.x) packed[2 * o + k] = src[k];
-}
-
 // Snapshot delta: tas_usage[col][leaf] += delta (updateTASUsage :257-293)
 __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present, int N, const kueue_tas_delta* d,
                                     int n) {

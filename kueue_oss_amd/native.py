@@ -41,7 +41,7 @@ def build_native(jobs: int = 4) -> str:
 
 class KueueTasConfig(ctypes.Structure):
     _fields_ = [("list_cap", ctypes.c_int32), ("max_batch", ctypes.c_int32),
-                ("device", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 EXPORTED_SYMBOLS = [
@@ -113,9 +113,10 @@ class TASFlavorSnapshot:
     tas_flavor_snapshot.go:109).  ``snapshot`` follows the fixture schema of
     tools/extract_goldens.py (podSets ignored)."""
 
-    def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None):
+    def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
+                 packed_entries: bool = False):
         self._lib = lib if lib is not None else load_library()
-        cfg = KueueTasConfig(list_cap, max_batch, device, 0)
+        cfg = KueueTasConfig(list_cap, max_batch, device, 1 if packed_entries else 0)
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:

@@ -97,3 +97,15 @@ def test_c3_sample_full_size():
     idx = {id(w): i for i, w in enumerate(wls)}
     mism = [k for k, w in enumerate(sample) if got[idx[id(w)]] != want[k]]
     assert mism == [], mism[:5]
+
+
+def test_packed_entries_path_matches_view_path():
+    # kueue_tas_eval_batch's packed copy (caller buffer, EOVERFLOW + fetch) vs the zero-copy view
+    snap_doc, wls = synth.config_c2(n_workloads=200)
+    a = TASFlavorSnapshot(snap_doc)
+    b = TASFlavorSnapshot(snap_doc, packed_entries=True)
+    got_a = a.find_topology_assignments_for_workloads(wls)
+    got_b = b.find_topology_assignments_for_workloads(wls)
+    a.close()
+    b.close()
+    assert got_a == got_b
