@@ -206,11 +206,12 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 
 /* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
- * events on the ctx stream, summed over its chunks): [0] fill (+ exclusion
- * stats reduce), [1] roll-up of the remaining levels, [2] exclusion-stats
- * replication to duplicate evals, [3] leaf-level tables (LFC histograms,
- * selection partials), [4] select/descend + LFC emit, [5] reserved (0), [6]
- * total from the request upload to the end of select.  Copies min(n, 7). */
+ * events, summed over its chunks): [0] fill (+ exclusion stats reduce), [1]
+ * roll-up of the remaining levels, [2] exclusion-stats replication, [3] the
+ * fast-LFC branch on the second stream (leaf tables, select, emit; runs
+ * concurrently with [1], [2], [4]), [4] select of the other evals, [5] wait
+ * for the fast-LFC branch, [6] total from the request upload to the join.
+ * Copies min(n, 7). */
 #define KUEUE_TAS_NUM_STAGES 7
 int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
 

@@ -134,7 +134,9 @@ void compute_magic(uint64_t d, DevTerm* t) {
 struct kueue_tas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // fast-LFC branch (tables, select, emit) beside the BestFit select
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
+  hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
   std::string err;
   int list_cap = 1024;
   int max_batch = 1024;
@@ -225,11 +227,13 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     delete c;
     return nullptr;
   }
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->evl) (void)hipEventCreate(&e);
   return c;
 }
 
@@ -237,6 +241,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   c->d_child_off.release();
   c->d_id_rank.release();
   c->d_taint_profile.release();
@@ -270,6 +275,9 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->ent_host = c->ent_dev = nullptr;
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->evl)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -431,7 +439,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t o_taint = seg(taint_table_len * 4), o_assumed = seg(num_assumed * sizeof(kueue_tas_assumed));
   const size_t o_fill = seg(n * 4), o_fchunks = seg(n * 8), o_pairs = seg(n * 8), o_rep = seg(n * 4);
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
-  const size_t o_pidx = seg(n * 4);
+  const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
   HIPCHK(c, c->h_stage.ensure(stage_bytes));
   HIPCHK(c, c->d_stage.ensure(stage_bytes));
   uint8_t* hs = c->h_stage.p;
@@ -575,6 +583,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   int32_t* h_fast = reinterpret_cast<int32_t*>(hs + o_fast);
   int32_t* h_leafsel = reinterpret_cast<int32_t*>(hs + o_leafsel);
   int32_t* h_pidx = reinterpret_cast<int32_t*>(hs + o_pidx);  // eval -> row of its leaf partials, -1
+  int32_t* h_bf = reinterpret_cast<int32_t*>(hs + o_bf);      // evals selected on the main stream
+  int nbf = 0;
   int nfill = 0, npairs = 0, nslots = 0, nfast = 0, nfchunks = 0, nleafsel = 0;
   {
     // classes: open hash chains on the 64-bit (signature, mask) hash, exact compare on the rep
@@ -653,6 +663,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       h_rep[i] = r;
       h_slot[i] = fast ? slot_of[size_t(k)] : -1;
       if (fast) h_fast[nfast++] = int32_t(i);
+      else h_bf[nbf++] = int32_t(i);
       if (int32_t(i) != r) {
         h_pairs[2 * npairs] = r;
         h_pairs[2 * npairs + 1] = ~int32_t(i);  // exclusion stats only
@@ -854,11 +865,27 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-  if (nslots) {  // fast-LFC leaf tables: chunk histograms, then per-bin chunk prefixes
-    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream, s, b);
+  const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
+  const int32_t* d_bf = reinterpret_cast<const int32_t*>(ds + o_bf);
+  const int waves = 4;
+  const size_t sel_lds = size_t(waves) * size_t(c->list_cap) * 16;
+  // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
+  // (after the stats replication); the main stream runs the BestFit side
+  if (nfast) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[2], 0));  // fill done
+    HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
+    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream, b);
+    hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[4], 0));  // stats replicated
+    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves), sel_lds,
+                       c->stream2, s, b, d_fast, nfast);
+    HIPCHK(c, hipGetLastError());
+    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
+    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->evl[1], c->stream2));
   }
   // leaf-level selection partials (non-fast evals whose requested level is the leaf level)
   if (nleafsel && s.N > 0) {
@@ -868,20 +895,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
-  // K3
-  {
-    const int waves = 4;
-    size_t lds = size_t(waves) * size_t(c->list_cap) * 16;
-    dim3 grid(unsigned((n + waves - 1) / waves));
-    hipLaunchKernelGGL(select_kernel, grid, dim3(64 * waves), lds, c->stream, s, b);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (nfast) {  // expand fast-LFC greedy results into entries (items appended by select)
-    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
-    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream, s, b);
+  // K3 (BestFit side and every other non-fast eval)
+  if (nbf) {
+    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nbf + waves - 1) / waves)), dim3(64 * waves), sel_lds, c->stream,
+                       s, b, d_bf, nbf);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+  if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
@@ -911,6 +932,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   if (res_counts && s.R) memcpy(res_counts, c->res_stats_h + n * nt, n * size_t(s.R) * 4);
   float st[KUEUE_TAS_NUM_STAGES] = {};
   for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&st[k], c->ev[k + 1], c->ev[k + 2]);
+  st[3] = 0.f;  // ev4 -> ev5 is the partials launch; report the concurrent fast-LFC branch instead
+  if (nfast) (void)hipEventElapsedTime(&st[3], c->evl[0], c->evl[1]);
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
   for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
   ms[0] += st[0];                  // the fill kernel alone

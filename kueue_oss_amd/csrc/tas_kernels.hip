@@ -3026,12 +3026,15 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
   }
 }
 
-__global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b) {
+// One wave per eval of `ids` (the BestFit-side and the fast-LFC evals are
+// launched separately, on two streams).
+__global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, const int32_t* ids, int nids) {
   extern __shared__ Key lds_all[];
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
-  const int eid = blockIdx.x * (blockDim.x >> 6) + wave;
-  if (eid >= b.n) return;
+  const int slot = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (slot >= nids) return;
+  const int eid = ids[slot];
   const uint64_t t_begin = wall_clock64();
   const DevEval& ev = b.evals[eid];
   Wave w;

@@ -137,6 +137,7 @@ inline hipError_t hipEventCreate(hipEvent_t* e) {
   return hipSuccess;
 }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char*>(e); return hipSuccess; }
 
