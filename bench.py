@@ -40,16 +40,35 @@ def parse():
     return ap.parse_args()
 
 
-def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols):
+def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols, parents=0):
     """Minimum HBM bytes of one fill launch: the SoA snapshot columns the
     batch requests (free + used int64 per requested column, the two presence
     words, taint profile, label ids) once per launch, plus the leaf counters
     written for every eval whose phase 1 runs (one per distinct phase-1 input:
     state + sliceState int32; stateWithLeader, sliceStateWithLeader,
-    leaderState for leader evals)."""
+    leaderState for leader evals).  With the fused parent roll-up (`parents`
+    leaf parents of uniform power-of-two fan-out) each phase-1 eval also
+    writes the parents' state + sliceState and a 64-bit positive-children
+    mask (+ the three leader fields)."""
     snap = N * (16 * R_used + 8 + 4 + 4 * label_cols)
-    writes = N * (8 * n_fill + 12 * n_leader)
+    writes = N * (8 * n_fill + 12 * n_leader) + parents * (16 * n_fill + 12 * n_leader)
     return snap + writes
+
+
+def fused_parents(doc):
+    """Number of leaf parents the fill rolls up itself (tas_device.hip
+    kueue_tas_snapshot_load: uniform power-of-two fan-out <= 64, contiguous in
+    leaf order, which the CSR layout gives), 0 when the snapshot does not qualify."""
+    levels = doc["levels"]
+    if len(levels) < 2:
+        return 0
+    from collections import Counter
+
+    sizes = set(Counter(tuple(n["labels"].get(l) for l in levels[:-1]) for n in doc["nodes"]).values())
+    if len(sizes) != 1:
+        return 0
+    F = sizes.pop()
+    return len(doc["nodes"]) // F if F <= 64 and F & (F - 1) == 0 else 0
 
 
 def load_traffic(path, config, n_fill):
@@ -164,7 +183,7 @@ def main():
     R_used = st["staged_cols"] or len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
     label_cols = 1 if any(p.get("nodeSelector") for w in mine for p in w) else 0
     fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(leader_evals, st["fill_evals"]) / launches,
-                                        R_used, label_cols)
+                                        R_used, label_cols, fused_parents(snap_doc))
     achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
     traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config, st["fill_evals"])
     stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}

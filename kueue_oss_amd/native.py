@@ -181,10 +181,10 @@ class TASFlavorSnapshot:
         keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols")
         return dict(zip(keys, list(st)[:7]))
 
-    STAGES = ("fill", "rollup", "replicate", "leaf_partials", "select", "entry_offsets", "device_total")
+    STAGES = ("fill", "rollup", "replicate", "lfc_branch", "select", "join_wait", "device_total")
 
     def last_stage_times(self):
-        """Device ms per stage of the last run (HIP events on the ctx stream), dict keyed by STAGES."""
+        """Device ms per stage of the last run (HIP events; lfc_branch runs on the second stream concurrently with rollup..select), dict keyed by STAGES."""
         ms = (ctypes.c_float * len(self.STAGES))()
         self._lib.kueue_tas_host_last_stage_times(self._h, ms, len(self.STAGES))
         return dict(zip(self.STAGES, list(ms)))
