@@ -200,9 +200,9 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 
 /* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
- * events on the ctx stream): [0] the fill kernel alone, [1] roll-up +
- * replication + leaf partials, [2] select/descend + entry offsets, [3] total
- * from the request upload to the entry offsets. */
+ * events on the ctx stream): [0] fill (+ exclusion stats reduce), [1] roll-up
+ * + exclusion-stats replication, [2] leaf partials + select/descend + join
+ * with the fast-LFC branch, [3] total from the request upload to the join. */
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 
 /* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP

@@ -932,13 +932,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   if (res_counts && s.R) memcpy(res_counts, c->res_stats_h + n * nt, n * size_t(s.R) * 4);
   float st[KUEUE_TAS_NUM_STAGES] = {};
   for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&st[k], c->ev[k + 1], c->ev[k + 2]);
-  st[3] = 0.f;  // ev4 -> ev5 is the partials launch; report the concurrent fast-LFC branch instead
+  const float partials = st[3];  // ev4 -> ev5: leaf partials; stage [3] reports the concurrent fast-LFC branch
+  st[3] = 0.f;
   if (nfast) (void)hipEventElapsedTime(&st[3], c->evl[0], c->evl[1]);
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
   for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
-  ms[0] += st[0];                  // the fill kernel alone
-  ms[1] += st[1] + st[2] + st[3];  // roll-up + replication + leaf partials
-  ms[2] += st[4] + st[5];          // select + entry offsets
+  ms[0] += st[0];                    // fill (+ exclusion stats reduce)
+  ms[1] += st[1] + st[2];            // roll-up + replication
+  ms[2] += partials + st[4] + st[5]; // leaf partials + select + join with the fast-LFC branch
   ms[3] += st[6];
   lap(5);
   return KUEUE_TAS_OK;

@@ -403,3 +403,42 @@ def lfc_stress_case(rng: random.Random, n_nodes: int = 5000, n_workloads: int = 
         wls.append([ps])
     snap = {"levels": levels, "nodes": nodes, "pods": [], "tasUsage": [], "nodeLabels": {}, "featureGates": {}}
     return snap, wls
+
+
+_EXTREME_CAP = [0, 1, 2, 3, 7, 1000, (1 << 31) - 1, 1 << 31, (1 << 32) + 5, (1 << 33) - 1, 3 << 40,
+                10 ** 18 + 7, 1 << 62, (1 << 63) - 1]
+_EXTREME_REQ = [1, 2, 3, 5, 7, 10 ** 9 + 7, 1 << 20, (1 << 20) + 1, (1 << 31) + 3, 1 << 40, 3 << 40,
+                (1 << 62) + 3, (1 << 63) - 1]
+
+
+def arith_stress_case(rng: random.Random, max_nodes: int = 40) -> dict:
+    """random_case with adversarial int64 quantities: capacities up to
+    2^63-1, requests with non-power-of-two and huge divisors, usage above
+    allocatable (negative free), so CountInWithLimitingResource
+    (pkg/resources/requests.go:183-217: int64 Go division, int32 truncation,
+    clamp at 0) and the per-pod usage products (requests.go:53-57) wrap the
+    way Go does.  The kernels divide with host-computed multiply-high magic."""
+    case = random_case(rng, max_nodes=max_nodes)
+    big = "example.com/big"
+
+    def pick(vals):
+        return rng.choice(vals) if rng.random() < 0.8 else rng.randrange(1, 1 << 63)
+
+    for n in case["nodes"]:
+        if rng.random() < 0.9:
+            n["allocatable"][big] = pick(_EXTREME_CAP)
+        if "cpu" in n["allocatable"] and rng.random() < 0.5:
+            n["allocatable"]["cpu"] = pick(_EXTREME_CAP)
+    for p in case["pods"]:
+        if rng.random() < 0.5:
+            p["requests"][big] = rng.choice(_EXTREME_REQ + [0])
+    for u in case["tasUsage"]:
+        if rng.random() < 0.5:
+            u["singlePodRequests"][big] = rng.choice(_EXTREME_REQ)
+    for ps in case["podSets"]:
+        if rng.random() < 0.7:
+            ps["requests"][big] = pick(_EXTREME_REQ)
+        if "cpu" in ps["requests"] and rng.random() < 0.3:
+            ps["requests"]["cpu"] = pick(_EXTREME_REQ)
+    case["name"] = "arith-stress"
+    return case

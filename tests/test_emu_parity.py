@@ -82,3 +82,16 @@ def test_emulated_kernels_match_oracle_c4_jobset(emu_lib):
     snap.close()
     mism = [i for i in range(len(wls)) if got[i] != want[i]]
     assert mism == [], (mism[:5], got[mism[0]] if mism else None, want[mism[0]] if mism else None)
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_emulated_int64_arithmetic_stress(emu_lib, seed):
+    # Go int64 wrap, truncating division by huge / odd divisors, int32 truncation and clamp
+    rng = random.Random(seed)
+    for i in range(150):
+        case = synth.arith_stress_case(rng)
+        want = oracle_lib.run_case(case)["results"]
+        snap = TASFlavorSnapshot(case, lib=emu_lib)
+        got = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        assert got == want, (i, got, want)

@@ -26,11 +26,11 @@ def test_goldens_on_gpu(list_cap):
     assert bad == []
 
 
-def _random_parity(seed, n, list_cap, max_nodes=60, profile_mixed=None):
+def _random_parity(seed, n, list_cap, max_nodes=60, profile_mixed=None, gen=None):
     rng = random.Random(seed)
     bad = []
     for i in range(n):
-        case = synth.random_case(rng, max_nodes=max_nodes, profile_mixed=profile_mixed)
+        case = gen(rng) if gen else synth.random_case(rng, max_nodes=max_nodes, profile_mixed=profile_mixed)
         want = oracle_lib.run_case(case)["results"]
         snap = TASFlavorSnapshot(case, list_cap=list_cap)
         got = snap.find_topology_assignments_for_flavor(case["podSets"])
@@ -45,6 +45,12 @@ def _random_parity(seed, n, list_cap, max_nodes=60, profile_mixed=None):
 @pytest.mark.parametrize("seed,list_cap", [(1, 0), (2, 64), (3, 0)])
 def test_random_small_topologies(seed, list_cap):
     bad = _random_parity(seed, 400, list_cap)
+    assert not bad, (bad[0][2], bad[0][3])
+
+
+def test_int64_arithmetic_stress():
+    # Go int64 wrap, truncating division by huge / odd divisors, int32 truncation and clamp
+    bad = _random_parity(43, 400, 0, gen=synth.arith_stress_case)
     assert not bad, (bad[0][2], bad[0][3])
 
 
