@@ -238,6 +238,26 @@ int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
  * fill staged (0: generic kernel). */
 int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 
+/* ---- admission re-check: TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415) ----
+ * One record per workload.TopologyDomainRequests (pkg/workload/workload.go:260-269). */
+typedef struct {
+  int32_t leaf;        /* leaf index; -1: DomainID(values) is not a leaf of the snapshot */
+  int32_t count;       /* pods placed in the domain (TopologyDomainRequests.Count) */
+  int32_t term_begin;  /* single-pod requests: terms[term_begin, term_begin + num_terms) */
+  int32_t num_terms;
+} kueue_tas_fits_req;
+typedef struct {
+  int64_t value;       /* single-pod request value (Go int64) */
+  int32_t col;         /* resource column; -1: a resource no leaf has (always absent) */
+  int32_t pad;
+} kueue_tas_fits_term;
+/* fits[i] = 1 when reqs[i].leaf >= 0 and
+ * SinglePodRequests.CountIn(freeCapacity - tasUsage of that leaf) >= count
+ * (requests.go:174-217, no pods:1 added), else 0.  The reference's Fits is
+ * the AND over a workload's records. */
+int kueue_tas_fits(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
+                   size_t num_terms, int32_t* fits);
+
 /* ---- host layer (C++ mirror of the Go API, JSON-driven) ------------------ */
 typedef struct kueue_tas_host kueue_tas_host;
 
@@ -275,14 +295,25 @@ int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* Host wall time of the last run_compiled (ms): [0] request staging,
  * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
-/* Per-workload compact results of the last run_compiled into buf (int32):
- * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
- * 4 int32 per workload (used for the cross-rank all-gather). */
 /* Work counters of the last find/run: [0] device batches, [1] evals,
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
 
+/* Per-workload compact results of the last run_compiled into buf (int32):
+ * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
+ * 4 int32 per workload (used for the cross-rank all-gather). */
 int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n_workloads);
+
+/* Snapshot usage updates and the admission re-check, JSON records
+ * [{"values": [...], "singlePodRequests": {...}, "count": n}, ...]
+ * (workload.TASFlavorUsage, pkg/workload/usage.go:24):
+ *  update_usage: ClusterQueueSnapshot.AddUsage (add = 1) / RemoveUsage
+ *    (add = 0) -> updateTASUsage (clusterqueue_snapshot.go:94-119,
+ *    tas_flavor_snapshot.go:257-293): single x count + pods:count per leaf,
+ *    applied on the device (records for unknown domains are skipped);
+ *  fits: TASFlavorSnapshot.Fits (:401-415), *fits = 0 / 1. */
+int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32_t add);
+int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits);
 
 void kueue_tas_free(char* p);
 

@@ -159,6 +159,7 @@ struct kueue_tas_ctx {
   int32_t* res_stats_h = nullptr;
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
+  DevBuf<uint8_t> d_fits;  // kueue_tas_fits: requests | terms | results
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
   DevBuf<int32_t> d_fill_stats;
@@ -255,6 +256,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->h_res.release();
   c->d_scratch.release();
   c->d_deltas.release();
+  c->d_fits.release();
   c->d_packed.release();
   c->d_partials.release();
   c->d_fill_stats.release();
@@ -394,6 +396,38 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
   if (usage_present_or_null)
     HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, usage_present_or_null, size_t(c->snap.N) * 4, hipMemcpyHostToDevice,
                              c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_fits(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
+                   size_t num_terms, int32_t* fits) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (n == 0) return KUEUE_TAS_OK;
+  if (!reqs || !fits || (num_terms && !terms)) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  for (size_t i = 0; i < n; i++) {
+    const kueue_tas_fits_req& r = reqs[i];
+    if (r.leaf >= c->snap.N || r.num_terms < 0 || r.term_begin < 0 ||
+        size_t(r.term_begin) + size_t(r.num_terms) > num_terms)
+      return fail(c, KUEUE_TAS_EINVAL, "fits request out of range");
+    for (int k = 0; k < r.num_terms; k++)
+      if (terms[r.term_begin + k].col >= c->snap.R) return fail(c, KUEUE_TAS_EINVAL, "fits term column out of range");
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t bytes = n * sizeof(kueue_tas_fits_req) + num_terms * sizeof(kueue_tas_fits_term) + n * 4;
+  HIPCHK(c, c->d_fits.ensure(bytes));
+  uint8_t* d = c->d_fits.p;
+  auto* d_reqs = reinterpret_cast<kueue_tas_fits_req*>(d);
+  auto* d_terms = reinterpret_cast<kueue_tas_fits_term*>(d + n * sizeof(kueue_tas_fits_req));
+  auto* d_out = reinterpret_cast<int32_t*>(d + n * sizeof(kueue_tas_fits_req) + num_terms * sizeof(kueue_tas_fits_term));
+  HIPCHK(c, hipMemcpyAsync(d_reqs, reqs, n * sizeof(kueue_tas_fits_req), hipMemcpyHostToDevice, c->stream));
+  if (num_terms)
+    HIPCHK(c, hipMemcpyAsync(d_terms, terms, num_terms * sizeof(kueue_tas_fits_term), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(fits_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->snap, d_reqs, int(n),
+                     d_terms, d_out);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(fits, d_out, n * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KUEUE_TAS_OK;
 }

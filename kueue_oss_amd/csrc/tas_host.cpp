@@ -564,6 +564,89 @@ class FlavorSnapshot {
     return 0;
   }
 
+  // ---- usage updates and the admission re-check ----
+  // One workload.TopologyDomainRequests (pkg/workload/workload.go:260-269).
+  struct DomainUsage {
+    std::string id;  // utiltas.DomainID(Values) (util/tas/tas.go:29-31)
+    Requests single;
+    int32_t count = 0;
+  };
+  static std::vector<DomainUsage> parse_usage(const kjson::Node& arr) {
+    std::vector<DomainUsage> us;
+    for (auto& u : arr.items) {
+      DomainUsage d;
+      for (size_t k = 0; k < u["values"].items.size(); k++) d.id += (k ? "," : "") + u["values"].items[k].s();
+      for (auto& kv : u["singlePodRequests"].fields) d.single[kv.first] = kv.second.i64();
+      d.count = int32_t(u["count"].i64());
+      us.push_back(std::move(d));
+    }
+    return us;
+  }
+  // ClusterQueueSnapshot.AddUsage/RemoveUsage -> updateTASUsage
+  // (clusterqueue_snapshot.go:94-119; tas_flavor_snapshot.go:257-293): the
+  // leaf's tasUsage gains (or loses) SinglePodRequests.ScaledUp(count) plus
+  // pods:count; domains that are not leaves are skipped.  The device replica
+  // is updated in place by a delta launch; a resource no column holds yet
+  // changes the column set, and then the next evaluation reloads the snapshot.
+  int update_usage(const std::vector<DomainUsage>& us, bool add) {
+    std::vector<kueue_tas_delta> deltas;
+    bool new_col = false;
+    for (auto& u : us) {
+      auto it = leafById.find(u.id);
+      if (it == leafById.end()) continue;
+      const int32_t leaf = it->second;
+      Requests tot;
+      for (auto& kv : u.single) tot[kv.first] = mul64(kv.second, u.count);
+      tot["pods"] = add64(tot["pods"], u.count);
+      for (auto& kv : tot) {
+        Requests& mine = tasUsage[leaf];
+        mine[kv.first] = add ? add64(mine[kv.first], kv.second) : sub64(mine[kv.first], kv.second);
+        auto c = colByName.find(kv.first);
+        if (c == colByName.end()) {
+          new_col = true;
+          continue;
+        }
+        deltas.push_back({leaf, c->second, add ? kv.second : sub64(0, kv.second)});
+      }
+    }
+    if (new_col) {
+      std::set<std::string> names(cols.begin(), cols.end());
+      for (auto& u : us)
+        for (auto& kv : u.single) names.insert(kv.first);
+      set_columns(names);  // dirty: the next upload() takes the host mirror
+      return 0;
+    }
+    if (dirty || !ctx || deltas.empty()) return 0;
+    int rc = kueue_tas_snapshot_apply_deltas(ctx, deltas.data(), deltas.size(), nullptr);
+    if (rc) err = std::string("apply deltas: ") + kueue_tas_last_error(ctx);
+    return rc;
+  }
+  // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), on the device.
+  int fits(const std::vector<DomainUsage>& us, bool* out) {
+    int rc = upload();
+    if (rc) return rc;
+    std::vector<kueue_tas_fits_req> reqs;
+    std::vector<kueue_tas_fits_term> terms;
+    for (auto& u : us) {
+      auto it = leafById.find(u.id);
+      kueue_tas_fits_req r{it == leafById.end() ? -1 : it->second, u.count, int32_t(terms.size()), 0};
+      for (auto& kv : u.single) {
+        auto c = colByName.find(kv.first);
+        terms.push_back({kv.second, c == colByName.end() ? -1 : c->second, 0});
+        r.num_terms++;
+      }
+      reqs.push_back(r);
+    }
+    std::vector<int32_t> f(reqs.size(), 0);
+    rc = kueue_tas_fits(ctx, reqs.data(), reqs.size(), terms.data(), terms.size(), f.data());
+    if (rc) {
+      err = std::string("fits: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    *out = std::all_of(f.begin(), f.end(), [](int32_t x) { return x != 0; });
+    return 0;
+  }
+
   // ---- request compilation: findTopologyAssignment prelude (:804-897) ----
   int resolve(const std::string& key) const {
     for (size_t i = 0; i < levelKeys.size(); i++)
@@ -1249,6 +1332,35 @@ int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, cha
     int rc = run_workloads(h, wls, false, &out, true);
     if (rc) return rc;
     *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32_t add) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    int rc = h->snap->update_usage(FlavorSnapshot::parse_usage(kjson::parse(usage_json)), add != 0);
+    if (rc) h->err = h->snap->err;
+    return rc;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits) {
+  if (!h || !h->snap || !h->err.empty() || !fits) return KUEUE_TAS_EINVAL;
+  try {
+    bool f = false;
+    int rc = h->snap->fits(FlavorSnapshot::parse_usage(kjson::parse(usage_json)), &f);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    *fits = f ? 1 : 0;
     return 0;
   } catch (const std::exception& e) {
     h->err = e.what();

@@ -3249,4 +3249,45 @@ __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present,
   atomicOr(&usage_present[x.leaf], 1u << x.col);
 }
 
+// TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), one thread per
+// TopologyDomainRequests record: remaining = freeCapacity - tasUsage (keys of
+// either map present, requests.go:84-94), then SinglePodRequests.CountIn
+// (requests.go:174-217: a missing key with a non-zero request gives 0, a zero
+// request MaxInt32, else max(int32(cap / req), 0); no keys gives 0).  Admission
+// re-checks are a handful of records per call: plain int64 division.
+__global__ void fits_kernel(DevSnap s, const kueue_tas_fits_req* reqs, int n, const kueue_tas_fits_term* terms,
+                            int32_t* fits) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const kueue_tas_fits_req r = reqs[i];
+  if (r.leaf < 0 || r.leaf >= s.N) {
+    fits[i] = 0;
+    return;
+  }
+  const uint32_t pres = s.free_present[r.leaf] | s.usage_present[r.leaf];
+  int32_t result = 0;
+  bool any = false;
+  for (int k = 0; k < r.num_terms; k++) {
+    const kueue_tas_fits_term t = terms[r.term_begin + k];
+    const bool present = t.col >= 0 && ((pres >> t.col) & 1u);
+    int32_t c;
+    if (!present && t.value != 0) {
+      result = 0;
+      any = true;
+      break;
+    }
+    if (t.value == 0) {
+      c = 0x7fffffff;
+    } else {
+      const int64_t cap = int64_t(uint64_t(s.free_cap[int64_t(t.col) * s.N + r.leaf]) -
+                                  uint64_t(s.tas_usage[int64_t(t.col) * s.N + r.leaf]));
+      const int64_t q = (cap == INT64_MIN && t.value == -1) ? INT64_MIN : cap / t.value;
+      c = max(int32_t(uint32_t(uint64_t(q))), 0);
+    }
+    if (!any || c < result) result = c;
+    any = true;
+  }
+  fits[i] = (any ? result : 0) >= r.count ? 1 : 0;
+}
+
 }  // namespace ktas

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
+    "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits",
 ]
 
 
@@ -99,6 +100,10 @@ def _bind(lib):
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
+    lib.kueue_tas_host_update_usage.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
+    lib.kueue_tas_host_update_usage.restype = c.c_int
+    lib.kueue_tas_host_fits.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
+    lib.kueue_tas_host_fits.restype = c.c_int
     lib.kueue_tas_free.argtypes = [c.c_void_p]
 
 
@@ -150,6 +155,25 @@ class TASFlavorSnapshot:
         if rc != 0:
             raise RuntimeError(f"kueue_tas_host_find failed ({rc}): {self._err()}")
         return _take(self._lib, out)["results"]
+
+    # ---- snapshot usage and the admission re-check (records: workload.TopologyDomainRequests,
+    # [{"values": [...], "singlePodRequests": {...}, "count": n}]) ----
+    def add_usage(self, records: list):
+        """ClusterQueueSnapshot.AddUsage -> updateTASUsage (clusterqueue_snapshot.go:94-119)."""
+        if self._lib.kueue_tas_host_update_usage(self._h, json.dumps(records).encode(), 1):
+            raise RuntimeError(self._err())
+
+    def remove_usage(self, records: list):
+        """ClusterQueueSnapshot.RemoveUsage -> updateTASUsage (clusterqueue_snapshot.go:100-119)."""
+        if self._lib.kueue_tas_host_update_usage(self._h, json.dumps(records).encode(), 0):
+            raise RuntimeError(self._err())
+
+    def fits(self, records: list) -> bool:
+        """TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), evaluated on the device."""
+        f = ctypes.c_int32()
+        if self._lib.kueue_tas_host_fits(self._h, json.dumps(records).encode(), ctypes.byref(f)):
+            raise RuntimeError(self._err())
+        return bool(f.value)
 
     def find_topology_assignments_for_workloads(self, workloads: list) -> list:
         """Evaluate many workloads independently against this snapshot in one

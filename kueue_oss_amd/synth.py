@@ -442,3 +442,75 @@ def arith_stress_case(rng: random.Random, max_nodes: int = 40) -> dict:
             ps["requests"]["cpu"] = pick(_EXTREME_REQ)
     case["name"] = "arith-stress"
     return case
+
+
+def usage_records(podsets: list, results: list) -> list:
+    """workload.TopologyDomainRequests records of the admitted assignments in
+    `results` (ComputeTASNetUsage, flavorassigner.go:94-130: per domain, the
+    PodSet's single-pod requests and the domain's pod count)."""
+    by_name = {p["name"].lower(): p for p in podsets}
+    recs = []
+    for r in results:
+        a = r.get("assignment")
+        if not a:
+            continue
+        req = by_name.get(r["name"], {}).get("requests", {})
+        for d in a["domains"]:
+            recs.append({"values": d["values"], "singlePodRequests": dict(req), "count": d["count"]})
+    return recs
+
+
+def admission_ops(rng: random.Random, case: dict, first_results: list) -> list:
+    """An admission-loop script for one snapshot (pkg/scheduler/scheduler.go:
+    426-435: Fits re-check, AddUsage; preemption's SimulateUsageRemoval,
+    clusterqueue_snapshot.go:85-92), interleaved with evaluations: find / fits /
+    add / remove ops as run by tests on the oracle and the device."""
+    ps = case["podSets"]
+    u = usage_records(ps, first_results)
+    half = u[: len(u) // 2]
+    grown = [dict(r, count=r["count"] + rng.choice([1, 3, 1000])) for r in u]
+    leaf_vals = [d["values"] for r in first_results if r.get("assignment") for d in r["assignment"]["domains"]]
+    junk = [{"values": ["no-such-domain"], "singlePodRequests": {"cpu": 1}, "count": 1}]
+    if leaf_vals:
+        junk.append({"values": rng.choice(leaf_vals), "singlePodRequests": {"example.com/new": 2, "cpu": 0},
+                     "count": 2})
+        junk.append({"values": rng.choice(leaf_vals), "singlePodRequests": {}, "count": rng.choice([0, 1])})
+    return [
+        {"op": "find", "podSets": ps},
+        {"op": "fits", "usage": u},
+        {"op": "fits", "usage": grown},
+        {"op": "add", "usage": u},
+        {"op": "find", "podSets": ps},
+        {"op": "fits", "usage": u},
+        {"op": "remove", "usage": half},
+        {"op": "find", "podSets": ps},
+        {"op": "fits", "usage": junk[:1]},
+        {"op": "fits", "usage": junk[1:]},
+        {"op": "add", "usage": junk},
+        {"op": "find", "podSets": ps},
+        {"op": "remove", "usage": u},
+        {"op": "add", "usage": half},
+        {"op": "find", "podSets": ps, "simulateEmpty": True},
+        {"op": "find", "podSets": ps},
+        {"op": "fits", "usage": u},
+    ]
+
+
+def run_session(snap, ops: list) -> list:
+    """Runs admission_ops on a TASFlavorSnapshot (the device path)."""
+    out = []
+    for op in ops:
+        k = op["op"]
+        if k == "find":
+            out.append(snap.find_topology_assignments_for_flavor(op["podSets"], op.get("simulateEmpty", False)))
+        elif k == "fits":
+            out.append(snap.fits(op["usage"]))
+        elif k == "add":
+            snap.add_usage(op["usage"])
+            out.append(None)
+        elif k == "remove":
+            snap.remove_usage(op["usage"])
+            out.append(None)
+        else:
+            raise ValueError(k)
+    return out

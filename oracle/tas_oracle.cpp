@@ -410,6 +410,30 @@ class Snapshot {
     else req_sub(it->second->tasUsage, u);
   }
 
+  // One workload.TopologyDomainRequests record (pkg/workload/workload.go:260-269).
+  struct DomainUsage {
+    std::vector<std::string> values;
+    Requests single;
+    int32_t count = 0;
+  };
+  // ClusterQueueSnapshot.AddUsage / RemoveUsage -> updateTASUsage
+  // (clusterqueue_snapshot.go:94-119): TotalRequests = single.ScaledUp(count)
+  // (workload.go:267-269), then :257-265 adds pods:count.
+  void update_usage(const std::vector<DomainUsage>& us, bool add) {
+    for (auto& u : us) update_tas_usage(domain_id(u.values), req_scaled_up(u.single, u.count), add, u.count);
+  }
+  // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415): no pods:1 here.
+  bool fits(const std::vector<DomainUsage>& us) const {
+    for (auto& u : us) {
+      auto it = leaves.find(domain_id(u.values));
+      if (it == leaves.end()) return false;
+      Requests remaining = it->second->freeCapacity;
+      req_sub(remaining, it->second->tasUsage);
+      if (count_in(u.single, remaining) < u.count) return false;
+    }
+    return true;
+  }
+
   std::string lowest_level() const { return levelKeys.back(); }
   std::string highest_level() const { return levelKeys.front(); }
   bool use_lfc(bool unconstrained) const { return unconstrained && gates.profileMixed; }  // :1328-1331
@@ -1253,6 +1277,60 @@ int tas_oracle_eval_workloads(const char* snapshot_json, const char* workloads_j
     *out_json = dup_out(out);
     return -1;
   }
+}
+
+// A scheduling session on one snapshot (the scheduler's admission loop,
+// pkg/scheduler/scheduler.go:426-435): `ops_json` = {"ops": [...]} with
+//   {"op": "find", "podSets": [...], "simulateEmpty": bool} -> results list
+//   {"op": "fits", "usage": [{values, singlePodRequests, count}...]} -> bool
+//   {"op": "add" | "remove", "usage": [...]}                         -> null
+// applied in order; returns {"results": [one entry per op]}.
+int tas_oracle_session(const char* snapshot_json, const char* ops_json, char** out_json) {
+  using namespace oracle;
+  std::string out = "{\"results\":[";
+  try {
+    ojson::Value c = ojson::parse(snapshot_json);
+    ojson::Value o = ojson::parse(ops_json);
+    auto snap = build_snapshot(c);
+    auto parse_usage = [](const ojson::Value& arr) {
+      std::vector<Snapshot::DomainUsage> us;
+      for (auto& u : arr.a) {
+        Snapshot::DomainUsage d;
+        for (auto& v : u.at("values").a) d.values.push_back(v.as_str());
+        d.single = parse_requests(u.at("singlePodRequests"));
+        d.count = int32_t(u.at("count").as_int());
+        us.push_back(std::move(d));
+      }
+      return us;
+    };
+    bool first = true;
+    for (auto& op : o.at("ops").a) {
+      if (!first) out += ",";
+      first = false;
+      const std::string kind = op.at("op").as_str();
+      if (kind == "find") {
+        auto sim = op.get("simulateEmpty");
+        emit_results(out, snap->find_topology_assignments_for_flavor(parse_podsets(op.at("podSets")),
+                                                                     sim && sim->as_bool()));
+      } else if (kind == "fits") {
+        out += snap->fits(parse_usage(op.at("usage"))) ? "true" : "false";
+      } else if (kind == "add" || kind == "remove") {
+        snap->update_usage(parse_usage(op.at("usage")), kind == "add");
+        out += "null";
+      } else {
+        throw std::runtime_error("unknown op " + kind);
+      }
+    }
+    out += "]}";
+  } catch (const std::exception& e) {
+    out = "{\"error\":";
+    ojson::quote(out, e.what());
+    out += "}";
+    *out_json = dup_out(out);
+    return -1;
+  }
+  *out_json = dup_out(out);
+  return 0;
 }
 
 void tas_oracle_free(char* p) { free(p); }

@@ -29,6 +29,8 @@ def load():
     lib.tas_oracle_eval_workloads.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_void_p)]
     lib.tas_oracle_eval_workloads.restype = ctypes.c_int
+    lib.tas_oracle_session.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    lib.tas_oracle_session.restype = ctypes.c_int
     lib.tas_oracle_free.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
@@ -63,3 +65,15 @@ def eval_workloads(snapshot_case: dict, workloads: list, threads: int = 1, emit:
     if rc != 0:
         raise RuntimeError(doc.get("error"))
     return doc["results"], secs.value
+
+
+def session(snapshot_case: dict, ops: list) -> list:
+    """Applies find / fits / add / remove ops in order on one snapshot; one result per op."""
+    lib = load()
+    out = ctypes.c_void_p()
+    rc = lib.tas_oracle_session(json.dumps(snapshot_case).encode(), json.dumps({"ops": ops}).encode(),
+                                ctypes.byref(out))
+    doc = _take(lib, out)
+    if rc != 0:
+        raise RuntimeError(doc.get("error"))
+    return doc["results"]

@@ -1,0 +1,60 @@
+"""Snapshot usage updates (ClusterQueueSnapshot.AddUsage/RemoveUsage ->
+updateTASUsage, clusterqueue_snapshot.go:94-119) and the admission re-check
+(TASFlavorSnapshot.Fits, tas_flavor_snapshot.go:401-415), interleaved with
+evaluations, against the oracle's restatement of the same session.  The
+reference's tests hold no golden vector for Fits/updateTASUsage alone; the
+usage arithmetic is the one the find goldens pin through `tasUsage`."""
+import random
+
+import pytest
+
+import oracle_lib
+from kueue_oss_amd import TASFlavorSnapshot, synth
+from test_emu_parity import emu_lib  # noqa: F401  (fixture)
+
+
+def _sessions(seed, n, lib=None, gen=None):
+    rng = random.Random(seed)
+    for i in range(n):
+        case = (gen or synth.random_case)(rng)
+        first = oracle_lib.run_case(case)["results"]
+        ops = synth.admission_ops(rng, case, first)
+        want = oracle_lib.session(case, ops)
+        snap = TASFlavorSnapshot(case, lib=lib) if lib else TASFlavorSnapshot(case)
+        got = synth.run_session(snap, ops)
+        snap.close()
+        for k, (g, w) in enumerate(zip(got, want)):
+            assert g == w, (i, k, ops[k]["op"], g, w)
+
+
+def test_oracle_session_replays_usage():
+    # add then remove of the same records restores every evaluation
+    rng = random.Random(3)
+    for _ in range(20):
+        case = synth.random_case(rng)
+        first = oracle_lib.run_case(case)["results"]
+        u = synth.usage_records(case["podSets"], first)
+        ops = [{"op": "find", "podSets": case["podSets"]}, {"op": "add", "usage": u},
+               {"op": "remove", "usage": u}, {"op": "find", "podSets": case["podSets"]}]
+        r = oracle_lib.session(case, ops)
+        assert r[0] == r[3] == first
+
+
+@pytest.mark.parametrize("seed", [51, 52])
+def test_emulated_admission_session(emu_lib, seed):  # noqa: F811
+    _sessions(seed, 60, lib=emu_lib)
+
+
+def test_emulated_admission_session_arith(emu_lib):  # noqa: F811
+    _sessions(53, 40, lib=emu_lib, gen=synth.arith_stress_case)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [61, 62])
+def test_admission_session_on_gpu(seed):
+    _sessions(seed, 150)
+
+
+@pytest.mark.gpu
+def test_admission_session_arith_on_gpu():
+    _sessions(63, 150, gen=synth.arith_stress_case)
