@@ -31,6 +31,8 @@ def load():
     lib.tas_oracle_eval_workloads.restype = ctypes.c_int
     lib.tas_oracle_session.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
     lib.tas_oracle_session.restype = ctypes.c_int
+    lib.tas_oracle_encoding.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    lib.tas_oracle_encoding.restype = ctypes.c_int
     lib.tas_oracle_free.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
@@ -77,3 +79,23 @@ def session(snapshot_case: dict, ops: list) -> list:
     if rc != 0:
         raise RuntimeError(doc.get("error"))
     return doc["results"]
+
+
+def _encoding(doc: dict, direction: int) -> dict:
+    lib = load()
+    out = ctypes.c_void_p()
+    rc = lib.tas_oracle_encoding(json.dumps(doc).encode(), direction, ctypes.byref(out))
+    res = _take(lib, out)
+    if rc != 0:
+        raise RuntimeError(res.get("error"))
+    return res
+
+
+def v1beta2_from(internal: dict) -> dict:
+    """V1Beta2From (pkg/util/tas/tas_assignment.go:251-259)."""
+    return _encoding(internal, 0)
+
+
+def internal_from(v1beta2: dict) -> dict:
+    """InternalFrom (pkg/util/tas/tas_assignment.go:124-133)."""
+    return _encoding(v1beta2, 1)
