@@ -176,6 +176,29 @@ def main():
     placements = len(all_wls) * a.steps  # every rank's shard, all steps
     value = placements / dt
 
+    # ---- widened rows, after the timed region: v1beta2 encoding of the last
+    # batch's assignments and the admission re-check + usage update ----
+    extras = {}
+    if rank == 0:
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            snap.last_v1beta2(materialize=False)
+        enc_ms = (time.perf_counter() - t0) / reps * 1e3
+        got = snap.find_topology_assignments_for_workloads(mine[:64])
+        recs = [r for w, res in zip(mine[:64], got) for r in synth.usage_records(w, res)]
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            snap.fits(recs[:8])
+        fits_ms = (time.perf_counter() - t0) / reps * 1e3
+        t0 = time.perf_counter()
+        snap.add_usage(recs[:8])
+        snap.remove_usage(recs[:8])
+        upd_ms = (time.perf_counter() - t0) / 2 * 1e3
+        extras = {"v1beta2_encode_ms_per_batch": round(enc_ms, 3),
+                  "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
+                  "usage_update_ms_per_call": round(upd_ms, 3)}
+
     batches, evals, leader_evals = counts
     st = snap.last_stats()
     launches = max(st["fill_launches"], 1)
@@ -218,6 +241,7 @@ def main():
             "work": st,
             "cpu_baseline": cpu,
             "parity_sample_ok": parity,
+            "extras": extras,
             "setup_s": {"generate": round(gen_s, 2), "snapshot_load_and_compile": round(load_s, 2)},
         }
         print(json.dumps(line), flush=True)

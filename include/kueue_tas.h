@@ -258,6 +258,43 @@ typedef struct {
 int kueue_tas_fits(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
                    size_t num_terms, int32_t* fits);
 
+/* ---- v1beta2 compact TopologyAssignment encoding -------------------------
+ * V1Beta2From / singleCompactSliceEncoding (pkg/util/tas/tas_assignment.go:
+ * 135-259): one slice per assignment; per level either Universal (all values
+ * equal) or Individual {Prefix, Suffix, Roots} with the longest common prefix
+ * and suffix of the level's values (prefix cut so the two do not overlap);
+ * PodCounts Universal when every count is equal.  The device computes the
+ * per-level lengths; Roots[j] = value_j[prefix_len : len_j - suffix_len]. */
+typedef struct {
+  int32_t universal;   /* 1: every value equals value 0 (Universal) */
+  int32_t prefix_len;  /* Individual.Prefix = value0[:prefix_len]; 0: unset */
+  int32_t suffix_len;  /* Individual.Suffix = value0[len0 - suffix_len:]; 0: unset */
+  int32_t first;       /* string id of value 0 (-1: no domains) */
+} kueue_tas_level_enc;
+
+/* Explicit strings: assignment a owns domains [off[a], off[a+1]); domain j's
+ * value at level k is string ids[j * num_levels + k] of the table
+ * bytes[str_off[id] .. str_off[id+1]); counts[j] its pod count.
+ * out[a * num_levels + k] is level k's encoding, same_counts[a] = 1 when
+ * every count of assignment a is equal (0 for an empty assignment). */
+int kueue_tas_encode_v1beta2(kueue_tas_ctx* ctx, const char* bytes, size_t nbytes, const int64_t* str_off,
+                             size_t num_strings, const int32_t* ids, const int32_t* counts, const int64_t* off,
+                             size_t n_assign, int32_t num_levels, kueue_tas_level_enc* out, int32_t* same_counts);
+
+/* Resident domain names for the leaf-mode encoder: the own label value of
+ * every domain, level by level in domain-index order (level 0 first), as
+ * bytes[offsets[i] .. offsets[i+1]), i < sum(level_sizes).  Replaced by the
+ * next kueue_tas_snapshot_load (call again after it). */
+int kueue_tas_snapshot_load_names(kueue_tas_ctx* ctx, const char* bytes, size_t nbytes, const int64_t* offsets);
+
+/* Leaf mode: assignments as (leaf, count) pairs (kueue_tas_eval_batch's
+ * entries layout, pairs[2j], pairs[2j+1]); assignment a owns pairs
+ * [off[a], off[a+1]).  Encoding level k is snapshot level first_level + k
+ * (the leaf's ancestor there), num_levels = L - first_level; out and
+ * same_counts as above, `first` indexing the resident names. */
+int kueue_tas_encode_v1beta2_leaves(kueue_tas_ctx* ctx, const int32_t* pairs, const int64_t* off, size_t n_assign,
+                                    int32_t first_level, kueue_tas_level_enc* out, int32_t* same_counts);
+
 /* ---- host layer (C++ mirror of the Go API, JSON-driven) ------------------ */
 typedef struct kueue_tas_host kueue_tas_host;
 
@@ -313,6 +350,22 @@ int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n_worklo
  *    applied on the device (records for unknown domains are skipped);
  *  fits: TASFlavorSnapshot.Fits (:401-415), *fits = 0 / 1. */
 int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32_t add);
+
+/* v1beta2 wire format (apis/kueue/v1beta2 TopologyAssignment; JSON shapes in
+ * oracle/tas_encoding_oracle.cpp):
+ *  v1beta2_from: V1Beta2From (tas_assignment.go:251-259) of a JSON array of
+ *    internal assignments ({"levels","domains":[{"values","count"}]} or null),
+ *    prefix/suffix lengths computed on the device;
+ *  internal_from: InternalFrom (:124-133) of a JSON array of v1beta2 values;
+ *  find_v1beta2: kueue_tas_host_find whose results carry
+ *    "topologyAssignment" in the v1beta2 form (Assignment.ToAPI,
+ *    flavorassigner.go:355), encoded from the resident domain names;
+ *  v1beta2_last: the v1beta2 form of every result of the last run_compiled
+ *    ([[...] per workload]; out_json may be NULL to encode only). */
+int kueue_tas_host_v1beta2_from(kueue_tas_host* h, const char* assignments_json, char** out_json);
+int kueue_tas_host_internal_from(kueue_tas_host* h, const char* v1beta2_json, char** out_json);
+int kueue_tas_host_find_v1beta2(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json);
+int kueue_tas_host_v1beta2_last(kueue_tas_host* h, char** out_json);
 int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits);
 
 void kueue_tas_free(char* p);

@@ -160,6 +160,15 @@ struct kueue_tas_ctx {
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
   DevBuf<uint8_t> d_fits;  // kueue_tas_fits: requests | terms | results
+  // v1beta2 encoder: parent map (leaf mode), resident names, per-call buffers
+  DevBuf<int32_t> d_parent;
+  DevBuf<char> d_names;
+  DevBuf<int64_t> d_name_off;
+  bool names_loaded = false;
+  DevBuf<char> d_enc_bytes;
+  DevBuf<int64_t> d_enc_stroff, d_enc_off;
+  DevBuf<int32_t> d_enc_ids, d_enc_counts, d_enc_same;
+  DevBuf<kueue_tas_level_enc> d_enc_out;
   DevBuf<int32_t> d_packed;
   DevBuf<LeafPartial> d_partials;
   DevBuf<int32_t> d_fill_stats;
@@ -257,6 +266,16 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_scratch.release();
   c->d_deltas.release();
   c->d_fits.release();
+  c->d_parent.release();
+  c->d_names.release();
+  c->d_name_off.release();
+  c->d_enc_bytes.release();
+  c->d_enc_stroff.release();
+  c->d_enc_off.release();
+  c->d_enc_ids.release();
+  c->d_enc_counts.release();
+  c->d_enc_same.release();
+  c->d_enc_out.release();
   c->d_packed.release();
   c->d_partials.release();
   c->d_fill_stats.release();
@@ -371,11 +390,140 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
       if (ok) c->rack_fanout = F;
     }
   }
+  // parent global domain id of every domain (v1beta2 leaf-mode encoder)
+  {
+    std::vector<int32_t> parent(size_t(std::max<int64_t>(off, 1)), -1);
+    for (int l = 0; l + 1 < s.L; l++) {
+      const int32_t* co = d->child_offsets + s.child_base[l];
+      for (int p = 0; p < d->level_sizes[l]; p++)
+        for (int j = co[p]; j < co[p + 1]; j++) parent[size_t(s.level_off[l + 1] + j)] = s.level_off[l] + p;
+    }
+    HIPCHK(c, c->d_parent.ensure(parent.size()));
+    HIPCHK(c, hipMemcpy(c->d_parent.p, parent.data(), parent.size() * 4, hipMemcpyHostToDevice));
+  }
+  c->names_loaded = false;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap = s;
   c->maxD = maxD;
   c->loaded = true;
   return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_load_names(kueue_tas_ctx* c, const char* bytes, size_t nbytes, const int64_t* offsets) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (!offsets || (nbytes && !bytes)) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  size_t total = 0;
+  for (int l = 0; l < c->snap.L; l++) total += size_t(c->snap.level_size[l]);
+  if (offsets[0] != 0 || size_t(offsets[total]) != nbytes) return fail(c, KUEUE_TAS_EINVAL, "name offsets");
+  for (size_t i = 0; i < total; i++)
+    if (offsets[i + 1] < offsets[i]) return fail(c, KUEUE_TAS_EINVAL, "name offsets not monotone");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, c->d_names.ensure(nbytes));
+  HIPCHK(c, c->d_name_off.ensure(total + 1));
+  if (nbytes) HIPCHK(c, hipMemcpy(c->d_names.p, bytes, nbytes, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_name_off.p, offsets, (total + 1) * 8, hipMemcpyHostToDevice));
+  c->names_loaded = true;
+  return KUEUE_TAS_OK;
+}
+
+static int run_encode(kueue_tas_ctx* c, EncodeArgs& a, size_t n_assign, kueue_tas_level_enc* out, int32_t* same) {
+  const size_t nout = n_assign * size_t(a.num_levels);
+  HIPCHK(c, c->d_enc_out.ensure(nout));
+  HIPCHK(c, c->d_enc_same.ensure(n_assign));
+  a.out = c->d_enc_out.p;
+  a.same = c->d_enc_same.p;
+  a.n_assign = int32_t(n_assign);
+  hipLaunchKernelGGL(encode_v1beta2_kernel, dim3(unsigned(n_assign), unsigned(a.num_levels)), dim3(256), 0, c->stream,
+                     a);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, a.out, nout * sizeof(kueue_tas_level_enc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(same, a.same, n_assign * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_encode_v1beta2(kueue_tas_ctx* c, const char* bytes, size_t nbytes, const int64_t* str_off,
+                             size_t num_strings, const int32_t* ids, const int32_t* counts, const int64_t* off,
+                             size_t n_assign, int32_t num_levels, kueue_tas_level_enc* out, int32_t* same_counts) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (n_assign == 0) return KUEUE_TAS_OK;
+  if (num_levels < 1 || num_levels > 65535 || !str_off || !off || !out || !same_counts || (nbytes && !bytes))
+    return fail(c, KUEUE_TAS_EINVAL, "encode arguments");
+  if (n_assign > 0x7fffffff) return fail(c, KUEUE_TAS_EINVAL, "too many assignments");
+  // host-side shape checks: every id and offset the kernel will touch
+  if (off[0] < 0) return fail(c, KUEUE_TAS_EINVAL, "assignment offsets");
+  for (size_t i = 0; i < n_assign; i++)
+    if (off[i + 1] < off[i]) return fail(c, KUEUE_TAS_EINVAL, "assignment offsets not monotone");
+  const size_t ndom = size_t(off[n_assign]);
+  if (ndom && (!ids || !counts)) return fail(c, KUEUE_TAS_EINVAL, "null ids/counts");
+  if (str_off[0] < 0 || size_t(str_off[num_strings]) > nbytes) return fail(c, KUEUE_TAS_EINVAL, "string offsets");
+  for (size_t i = 0; i < num_strings; i++)
+    if (str_off[i + 1] < str_off[i]) return fail(c, KUEUE_TAS_EINVAL, "string offsets not monotone");
+  for (size_t i = 0; i < ndom * size_t(num_levels); i++)
+    if (ids[i] < 0 || size_t(ids[i]) >= num_strings) return fail(c, KUEUE_TAS_EINVAL, "string id out of range");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, c->d_enc_bytes.ensure(nbytes));
+  HIPCHK(c, c->d_enc_stroff.ensure(num_strings + 1));
+  HIPCHK(c, c->d_enc_off.ensure(n_assign + 1));
+  HIPCHK(c, c->d_enc_ids.ensure(ndom * size_t(num_levels)));
+  HIPCHK(c, c->d_enc_counts.ensure(ndom));
+  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->d_enc_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_enc_stroff.p, str_off, (num_strings + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_enc_off.p, off, (n_assign + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (ndom) {
+    HIPCHK(c, hipMemcpyAsync(c->d_enc_ids.p, ids, ndom * size_t(num_levels) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_enc_counts.p, counts, ndom * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  EncodeArgs a{};
+  a.bytes = c->d_enc_bytes.p;
+  a.str_off = c->d_enc_stroff.p;
+  a.ids = c->d_enc_ids.p;
+  a.counts = c->d_enc_counts.p;
+  a.off = c->d_enc_off.p;
+  a.num_levels = num_levels;
+  return run_encode(c, a, n_assign, out, same_counts);
+}
+
+int kueue_tas_encode_v1beta2_leaves(kueue_tas_ctx* c, const int32_t* pairs, const int64_t* off, size_t n_assign,
+                                    int32_t first_level, kueue_tas_level_enc* out, int32_t* same_counts) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (!c->names_loaded) return fail(c, KUEUE_TAS_EINVAL, "no names loaded (kueue_tas_snapshot_load_names)");
+  if (n_assign == 0) return KUEUE_TAS_OK;
+  const DevSnap& s = c->snap;
+  if (first_level < 0 || first_level >= s.L || !off || !out || !same_counts)
+    return fail(c, KUEUE_TAS_EINVAL, "encode arguments");
+  if (n_assign > 0x7fffffff) return fail(c, KUEUE_TAS_EINVAL, "too many assignments");
+  if (off[0] < 0) return fail(c, KUEUE_TAS_EINVAL, "assignment offsets");
+  for (size_t i = 0; i < n_assign; i++)
+    if (off[i + 1] < off[i]) return fail(c, KUEUE_TAS_EINVAL, "assignment offsets not monotone");
+  const size_t npairs = size_t(off[n_assign]);
+  if (npairs && !pairs) return fail(c, KUEUE_TAS_EINVAL, "null pairs");
+  for (size_t j = size_t(off[0]); j < npairs; j++)
+    if (pairs[2 * j] < 0 || pairs[2 * j] >= s.N) return fail(c, KUEUE_TAS_EINVAL, "leaf out of range");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, c->d_enc_counts.ensure(2 * npairs));  // the pairs
+  HIPCHK(c, c->d_enc_off.ensure(n_assign + 1));
+  if (npairs)
+    HIPCHK(c, hipMemcpyAsync(c->d_enc_counts.p, pairs, npairs * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_enc_off.p, off, (n_assign + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  EncodeArgs a{};
+  a.bytes = c->d_names.p;
+  a.str_off = c->d_name_off.p;
+  a.pairs = c->d_enc_counts.p;
+  a.parent = c->d_parent.p;
+  a.off = c->d_enc_off.p;
+  a.num_levels = s.L - first_level;
+  a.first_level = first_level;
+  a.L = s.L;
+  int64_t base = 0;
+  for (int l = 0; l < s.L; l++) {
+    a.level_off[l] = s.level_off[l];
+    a.name_base[l] = base;
+    base += s.level_size[l];
+  }
+  return run_encode(c, a, n_assign, out, same_counts);
 }
 
 int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n,

@@ -24,6 +24,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -558,6 +559,19 @@ class FlavorSnapshot {
     int rc = kueue_tas_snapshot_load(ctx, &d);
     if (rc) {
       err = std::string("snapshot load: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    // own label value of every domain, for the v1beta2 encoder's leaf mode
+    std::string names;
+    std::vector<int64_t> name_off(1, 0);
+    for (int l = 0; l < L; l++)
+      for (auto& v : values[l]) {
+        names += v.back();
+        name_off.push_back(int64_t(names.size()));
+      }
+    rc = kueue_tas_snapshot_load_names(ctx, names.data(), names.size(), name_off.data());
+    if (rc) {
+      err = std::string("snapshot names: ") + kueue_tas_last_error(ctx);
       return rc;
     }
     dirty = false;
@@ -1232,6 +1246,261 @@ static void emit_results(std::string& out, const FlavorSnapshot& s, const std::v
   out += "]";
 }
 
+// ---- v1beta2 TopologyAssignment (apis/kueue/v1beta2; tas_assignment.go:135-259) ----
+// One single-slice encoding from the device's per-level lengths; value(j, k)
+// is domain j's value at encoding level k.
+template <class ValueAt, class CountAt>
+static void write_v1beta2(std::string& out, const std::vector<std::string>& levels, size_t n,
+                          const kueue_tas_level_enc* enc, int32_t same, ValueAt value, CountAt count) {
+  out += "{\"levels\":[";
+  for (size_t l = 0; l < levels.size(); l++) {
+    if (l) out += ",";
+    kjson::write_string(out, levels[l]);
+  }
+  out += "],\"slices\":[";
+  if (n == 0) {
+    out += "]}";
+    return;
+  }
+  out += "{\"domainCount\":" + std::to_string(n) + ",\"podCounts\":";
+  if (same) {
+    out += "{\"universal\":" + std::to_string(count(0)) + "}";
+  } else {
+    out += "{\"individual\":[";
+    for (size_t j = 0; j < n; j++) out += (j ? "," : "") + std::to_string(count(j));
+    out += "]}";
+  }
+  out += ",\"valuesPerLevel\":[";
+  for (size_t k = 0; k < levels.size(); k++) {
+    if (k) out += ",";
+    const kueue_tas_level_enc& e = enc[k];
+    const std::string_view v0 = value(0, k);
+    if (e.universal) {
+      out += "{\"universal\":";
+      kjson::write_string(out, std::string(v0));
+      out += "}";
+      continue;
+    }
+    out += "{\"individual\":{";
+    if (e.prefix_len > 0) {
+      out += "\"prefix\":";
+      kjson::write_string(out, std::string(v0.substr(0, size_t(e.prefix_len))));
+      out += ",";
+    }
+    if (e.suffix_len > 0) {
+      out += "\"suffix\":";
+      kjson::write_string(out, std::string(v0.substr(v0.size() - size_t(e.suffix_len))));
+      out += ",";
+    }
+    out += "\"roots\":[";
+    for (size_t j = 0; j < n; j++) {
+      if (j) out += ",";
+      const std::string_view vj = value(j, k);
+      kjson::write_string(out, std::string(vj.substr(size_t(e.prefix_len), vj.size() - size_t(e.prefix_len) -
+                                                                              size_t(e.suffix_len))));
+    }
+    out += "]}}";
+  }
+  out += "]}]}";
+}
+
+// V1Beta2From of the snapshot's results (leaf mode, resident names): one
+// device launch for every assignment of `rs`; writes [v1beta2 | null] per result.
+static int encode_results(FlavorSnapshot& s, const std::vector<const PodSetResult*>& rs, std::vector<std::string>* out) {
+  const int L = s.L();
+  const int first = s.lowestIsHostname ? L - 1 : 0;
+  std::vector<int32_t> pairs;
+  std::vector<int64_t> off(1, 0);
+  std::vector<size_t> which;
+  for (size_t i = 0; i < rs.size(); i++) {
+    if (!rs[i]->has_assignment) continue;
+    for (auto& d : rs[i]->domains) {
+      pairs.push_back(d.leaf);
+      pairs.push_back(d.count);
+    }
+    off.push_back(int64_t(pairs.size() / 2));
+    which.push_back(i);
+  }
+  const int nl = L - first;
+  std::vector<kueue_tas_level_enc> enc(which.size() * size_t(nl));
+  std::vector<int32_t> same(which.size());
+  if (!which.empty()) {
+    int rc = kueue_tas_encode_v1beta2_leaves(s.ctx, pairs.data(), off.data(), which.size(), first, enc.data(),
+                                             same.data());
+    if (rc) {
+      s.err = std::string("encode: ") + kueue_tas_last_error(s.ctx);
+      return rc;
+    }
+  }
+  std::vector<std::string> levels(s.levelKeys.begin() + first, s.levelKeys.end());
+  out->assign(rs.size(), "null");
+  // ancestors of a leaf per level: walk the CSR bounds (levels are few)
+  for (size_t a = 0; a < which.size(); a++) {
+    const DomainSpan& d = rs[which[a]]->domains;
+    std::string& o = (*out)[which[a]];
+    o.clear();
+    write_v1beta2(
+        o, levels, d.size(), enc.data() + a * size_t(nl), same[a],
+        [&](size_t j, size_t k) -> std::string_view {
+          const auto& lv = s.values[L - 1][size_t(d[j].leaf)];
+          return lv[size_t(first) + k];
+        },
+        [&](size_t j) { return d[j].count; });
+  }
+  return 0;
+}
+
+// V1Beta2From over explicit internal assignments (explicit-string mode).
+static int v1beta2_from_json(kueue_tas_ctx* ctx, const kjson::Node& arr, std::string* out, std::string* err) {
+  std::string bytes;
+  std::vector<int64_t> str_off(1, 0);
+  std::vector<int32_t> ids, counts;
+  std::vector<int64_t> off(1, 0);
+  struct Item {
+    bool null;
+    std::vector<std::string> levels;
+    size_t first_dom, first_id, n;  // string ids of domain j, level k: first_id + j * levels + k
+  };
+  std::vector<Item> items;
+  std::vector<int32_t> nlev;
+  size_t ndom = 0;
+  for (auto& ta : arr.items) {
+    Item it{ta.null(), {}, ndom, ids.size(), 0};
+    if (!it.null) {
+      for (auto& l : ta["levels"].items) it.levels.push_back(l.s());
+      for (auto& d : ta["domains"].items) {
+        if (d["values"].items.size() != it.levels.size()) throw std::runtime_error("values/levels length mismatch");
+        for (auto& v : d["values"].items) {
+          ids.push_back(int32_t(str_off.size() - 1));
+          bytes += v.s();
+          str_off.push_back(int64_t(bytes.size()));
+        }
+        counts.push_back(int32_t(d["count"].i64()));
+        it.n++;
+      }
+    }
+    ndom += it.n;
+    items.push_back(std::move(it));
+  }
+  // one launch per distinct level count (assignments of one batch share it)
+  std::vector<std::vector<kueue_tas_level_enc>> enc(items.size());
+  std::vector<int32_t> same(items.size(), 0);
+  std::map<size_t, std::vector<size_t>> by_levels;
+  for (size_t i = 0; i < items.size(); i++)
+    if (!items[i].null && !items[i].levels.empty()) by_levels[items[i].levels.size()].push_back(i);
+  for (auto& kv : by_levels) {
+    const size_t nl = kv.first;
+    std::vector<int32_t> gids, gcounts;
+    std::vector<int64_t> goff(1, 0);
+    for (size_t i : kv.second) {
+      const Item& it = items[i];
+      gids.insert(gids.end(), ids.begin() + int64_t(it.first_id), ids.begin() + int64_t(it.first_id + it.n * nl));
+      gcounts.insert(gcounts.end(), counts.begin() + int64_t(it.first_dom), counts.begin() + int64_t(it.first_dom + it.n));
+      goff.push_back(int64_t(gcounts.size()));
+    }
+    std::vector<kueue_tas_level_enc> e(kv.second.size() * nl);
+    std::vector<int32_t> sm(kv.second.size());
+    int rc = kueue_tas_encode_v1beta2(ctx, bytes.data(), bytes.size(), str_off.data(), str_off.size() - 1, gids.data(),
+                                      gcounts.data(), goff.data(), kv.second.size(), int32_t(nl), e.data(), sm.data());
+    if (rc) {
+      *err = std::string("encode: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    for (size_t q = 0; q < kv.second.size(); q++) {
+      enc[kv.second[q]].assign(e.begin() + int64_t(q * nl), e.begin() + int64_t((q + 1) * nl));
+      same[kv.second[q]] = sm[q];
+    }
+  }
+  *out = "[";
+  for (size_t i = 0; i < items.size(); i++) {
+    if (i) *out += ",";
+    const Item& it = items[i];
+    if (it.null) {
+      *out += "null";
+      continue;
+    }
+    const size_t nl = it.levels.size();
+    if (nl == 0) {  // no levels: only the slice shape and pod counts remain
+      *out += "{\"levels\":[],\"slices\":[";
+      if (it.n) {
+        bool eq = true;
+        for (size_t j = 1; j < it.n; j++) eq = eq && counts[it.first_dom + j] == counts[it.first_dom];
+        *out += "{\"domainCount\":" + std::to_string(it.n) + ",\"podCounts\":";
+        if (eq) {
+          *out += "{\"universal\":" + std::to_string(counts[it.first_dom]) + "}";
+        } else {
+          *out += "{\"individual\":[";
+          for (size_t j = 0; j < it.n; j++) *out += (j ? "," : "") + std::to_string(counts[it.first_dom + j]);
+          *out += "]}";
+        }
+        *out += ",\"valuesPerLevel\":[]}";
+      }
+      *out += "]}";
+      continue;
+    }
+    write_v1beta2(
+        *out, it.levels, it.n, enc[i].data(), same[i],
+        [&](size_t j, size_t k) -> std::string_view {
+          const size_t sid = it.first_id + j * nl + k;
+          return std::string_view(bytes.data() + str_off[sid], size_t(str_off[sid + 1] - str_off[sid]));
+        },
+        [&](size_t j) { return counts[it.first_dom + j]; });
+  }
+  *out += "]";
+  return 0;
+}
+
+// InternalFrom / InternalSeqFrom (tas_assignment.go:103-133): wire format ->
+// internal assignment (string expansion only; runs where the JSON is).
+static void internal_from_json(const kjson::Node& arr, std::string* out) {
+  *out = "[";
+  bool first_item = true;
+  for (auto& ta : arr.items) {
+    if (!first_item) *out += ",";
+    first_item = false;
+    if (ta.null()) {
+      *out += "null";
+      continue;
+    }
+    const auto& levels = ta["levels"].items;
+    *out += "{\"levels\":[";
+    for (size_t l = 0; l < levels.size(); l++) {
+      if (l) *out += ",";
+      kjson::write_string(*out, levels[l].s());
+    }
+    *out += "],\"domains\":[";
+    bool first = true;
+    for (auto& sl : ta["slices"].items) {
+      const int64_t dc = sl["domainCount"].i64();
+      const kjson::Node& pc = sl["podCounts"];
+      const kjson::Node* uc = pc.find("universal");
+      for (int64_t i = 0; i < dc; i++) {
+        if (!first) *out += ",";
+        first = false;
+        *out += "{\"values\":[";
+        for (size_t l = 0; l < levels.size(); l++) {
+          const kjson::Node& v = sl["valuesPerLevel"].items.at(l);
+          std::string val;
+          if (const kjson::Node* u = v.find("universal")) {  // valueAtIndex (:40-48)
+            val = u->s();
+          } else {
+            const kjson::Node& ind = v["individual"];
+            const kjson::Node* p = ind.find("prefix");
+            const kjson::Node* x = ind.find("suffix");
+            val = (p ? p->s() : std::string()) + ind["roots"].items.at(size_t(i)).s() + (x ? x->s() : std::string());
+          }
+          if (l) *out += ",";
+          kjson::write_string(*out, val);
+        }
+        const int64_t c = uc ? uc->i64() : pc["individual"].items.at(size_t(i)).i64();  // countAtIndex (:50-55)
+        *out += "],\"count\":" + std::to_string(c) + "}";
+      }
+    }
+    *out += "]}";
+  }
+  *out += "]";
+}
+
 static char* dup(const std::string& s) {
   char* p = static_cast<char*>(malloc(s.size() + 1));
   memcpy(p, s.c_str(), s.size() + 1);
@@ -1331,6 +1600,108 @@ int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, cha
     std::string out;
     int rc = run_workloads(h, wls, false, &out, true);
     if (rc) return rc;
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_v1beta2_from(kueue_tas_host* h, const char* assignments_json, char** out_json) {
+  if (!h || !h->snap || !h->err.empty() || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    int rc = h->snap->upload();  // the device context
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    std::string out;
+    rc = v1beta2_from_json(h->snap->ctx, kjson::parse(assignments_json), &out, &h->err);
+    if (rc) return rc;
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_internal_from(kueue_tas_host* h, const char* v1beta2_json, char** out_json) {
+  if (!h || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    std::string out;
+    internal_from_json(kjson::parse(v1beta2_json), &out);
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_find_v1beta2(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json) {
+  if (!h || !h->snap || !h->err.empty() || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    std::vector<Workload> wls(1);
+    wls[0].podsets = parse_podsets(kjson::parse(podsets_json));
+    Evaluator ev{h->snap.get()};
+    std::vector<std::vector<PodSetResult>> results;
+    int rc = ev.run(wls, simulate_empty != 0, &results);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    std::vector<const PodSetResult*> rs;
+    for (auto& r : results[0]) rs.push_back(&r);
+    std::vector<std::string> enc;
+    rc = encode_results(*h->snap, rs, &enc);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    std::string out = "{\"results\":[";
+    for (size_t i = 0; i < rs.size(); i++) {
+      if (i) out += ",";
+      out += "{\"name\":";
+      kjson::write_string(out, rs[i]->name);
+      out += ",\"topologyAssignment\":" + enc[i] + ",\"reason\":";
+      kjson::write_string(out, rs[i]->reason);
+      out += "}";
+    }
+    out += "]}";
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_v1beta2_last(kueue_tas_host* h, char** out_json) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    std::vector<const PodSetResult*> rs;
+    std::vector<size_t> per;
+    for (auto& w : h->last) {
+      per.push_back(w.size());
+      for (auto& r : w) rs.push_back(&r);
+    }
+    std::vector<std::string> enc;
+    int rc = encode_results(*h->snap, rs, &enc);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    if (!out_json) return 0;
+    std::string out = "[";
+    size_t q = 0;
+    for (size_t w = 0; w < per.size(); w++) {
+      out += w ? ",[" : "[";
+      for (size_t i = 0; i < per[w]; i++, q++) out += (i ? "," : "") + enc[q];
+      out += "]";
+    }
+    out += "]";
     *out_json = dup(out);
     return 0;
   } catch (const std::exception& e) {

@@ -3249,6 +3249,110 @@ __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present,
   atomicOr(&usage_present[x.leaf], 1u << x.col);
 }
 
+// ---- v1beta2 compact encoding (pkg/util/tas/tas_assignment.go:135-259) ----
+// fillSingleCompactSliceValues walks the values keeping a running prefix and
+// suffix of value 0; by induction the prefix after value i is value0's prefix
+// of length min_{j<=i} lcp(value0, value_j) (each step cuts it to the first
+// mismatch or to len(value_i) <= which lcp is bounded), and likewise for the
+// suffix.  So the walk is a min-reduction of per-value lcp / lcs lengths,
+// done by one block per (assignment, level) over its domains.
+struct EncodeArgs {
+  const char* bytes;
+  const int64_t* str_off;
+  const int32_t* ids;     // explicit mode: [domain][num_levels] string ids (null: leaf mode)
+  const int32_t* counts;  // explicit mode counts
+  const int32_t* pairs;   // leaf mode: (leaf, count)
+  const int32_t* parent;  // leaf mode: parent global domain id, [SD]
+  const int64_t* off;     // [n_assign + 1]
+  int32_t n_assign;
+  int32_t num_levels;
+  int32_t first_level;
+  int32_t L;
+  int32_t level_off[kMaxLevels];
+  int64_t name_base[kMaxLevels];  // string id of level l's domain 0
+  kueue_tas_level_enc* out;
+  int32_t* same;
+};
+
+__device__ __forceinline__ int64_t enc_string_id(const EncodeArgs& a, int64_t j, int k) {
+  if (a.ids) return a.ids[j * a.num_levels + k];
+  const int lvl = a.first_level + k;
+  int32_t g = a.level_off[a.L - 1] + a.pairs[2 * j];
+  for (int l = a.L - 1; l > lvl; l--) g = a.parent[g];
+  return a.name_base[lvl] + (g - a.level_off[lvl]);
+}
+
+__global__ __launch_bounds__(256) void encode_v1beta2_kernel(EncodeArgs a) {
+  __shared__ int32_t red[4][4];
+  __shared__ int32_t same_red[4];
+  const int asg = blockIdx.x, k = blockIdx.y;
+  const int64_t j0 = a.off[asg], j1 = a.off[asg + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (j1 <= j0) {
+    if (threadIdx.x == 0) {
+      a.out[int64_t(asg) * a.num_levels + k] = kueue_tas_level_enc{0, 0, 0, -1};
+      if (k == 0) a.same[asg] = 0;
+    }
+    return;
+  }
+  const int64_t id0 = enc_string_id(a, j0, k);
+  const char* s0 = a.bytes + a.str_off[id0];
+  const int32_t len0 = int32_t(a.str_off[id0 + 1] - a.str_off[id0]);
+  const int32_t c0 = a.ids ? a.counts[j0] : a.pairs[2 * j0 + 1];
+  int32_t P = len0, S = len0, mn = len0, mx = len0, same = 1;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+    const int64_t id = enc_string_id(a, j, k);
+    const char* sj = a.bytes + a.str_off[id];
+    const int32_t lj = int32_t(a.str_off[id + 1] - a.str_off[id]);
+    mn = min(mn, lj);
+    mx = max(mx, lj);
+    const int32_t m = min(min(len0, lj), P);  // lcp beyond the running minimum cannot lower it
+    int32_t p = 0;
+    while (p < m && sj[p] == s0[p]) p++;
+    P = min(P, p);
+    const int32_t ms = min(min(len0, lj), S);
+    int32_t q = 0;
+    while (q < ms && sj[lj - 1 - q] == s0[len0 - 1 - q]) q++;
+    S = min(S, q);
+    if (k == 0) same &= (a.ids ? a.counts[j] : a.pairs[2 * j + 1]) == c0;
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    P = min(P, __shfl_xor(P, d, 64));
+    S = min(S, __shfl_xor(S, d, 64));
+    mn = min(mn, __shfl_xor(mn, d, 64));
+    mx = max(mx, __shfl_xor(mx, d, 64));
+    same &= __shfl_xor(same, d, 64);
+  }
+  if (lane == 0) {
+    red[wave][0] = P;
+    red[wave][1] = S;
+    red[wave][2] = mn;
+    red[wave][3] = mx;
+    same_red[wave] = same;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int w = 1; w < nw; w++) {
+      P = min(P, red[w][0]);
+      S = min(S, red[w][1]);
+      mn = min(mn, red[w][2]);
+      mx = max(mx, red[w][3]);
+      same &= same_red[w];
+    }
+    kueue_tas_level_enc e{0, 0, 0, int32_t(id0)};
+    if (P == mx) {  // all values equal (:174-178)
+      e.universal = 1;
+    } else {
+      if (P + S > mn) P = mn - S;  // no prefix/suffix overlap (:180-184)
+      e.prefix_len = P;
+      e.suffix_len = S;
+    }
+    a.out[int64_t(asg) * a.num_levels + k] = e;
+    if (k == 0) a.same[asg] = same;
+  }
+}
+
 // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), one thread per
 // TopologyDomainRequests record: remaining = freeCapacity - tasUsage (keys of
 // either map present, requests.go:84-94), then SinglePodRequests.CountIn

@@ -52,6 +52,9 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
     "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits",
+    "kueue_tas_encode_v1beta2", "kueue_tas_snapshot_load_names", "kueue_tas_encode_v1beta2_leaves",
+    "kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from", "kueue_tas_host_find_v1beta2",
+    "kueue_tas_host_v1beta2_last",
 ]
 
 
@@ -104,6 +107,13 @@ def _bind(lib):
     lib.kueue_tas_host_update_usage.restype = c.c_int
     lib.kueue_tas_host_fits.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
     lib.kueue_tas_host_fits.restype = c.c_int
+    for name in ("kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from"):
+        getattr(lib, name).argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_void_p)]
+        getattr(lib, name).restype = c.c_int
+    lib.kueue_tas_host_find_v1beta2.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_find_v1beta2.restype = c.c_int
+    lib.kueue_tas_host_v1beta2_last.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_v1beta2_last.restype = c.c_int
     lib.kueue_tas_free.argtypes = [c.c_void_p]
 
 
@@ -174,6 +184,38 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_fits(self._h, json.dumps(records).encode(), ctypes.byref(f)):
             raise RuntimeError(self._err())
         return bool(f.value)
+
+    # ---- v1beta2 wire format (pkg/util/tas/tas_assignment.go) ----
+    def _json_call(self, fn, payload, *extra):
+        out = ctypes.c_void_p()
+        rc = fn(self._h, json.dumps(payload).encode(), *extra, ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError(f"{fn.__name__} failed ({rc}): {self._err()}")
+        return _take(self._lib, out)
+
+    def v1beta2_from(self, assignments: list) -> list:
+        """V1Beta2From (tas_assignment.go:251-259) of internal assignments (None allowed), on the device."""
+        return self._json_call(self._lib.kueue_tas_host_v1beta2_from, assignments)
+
+    def internal_from(self, assignments: list) -> list:
+        """InternalFrom (tas_assignment.go:124-133) of v1beta2 assignments."""
+        return self._json_call(self._lib.kueue_tas_host_internal_from, assignments)
+
+    def find_topology_assignments_v1beta2(self, podsets: list, simulate_empty: bool = False) -> list:
+        """find_topology_assignments_for_flavor with the assignment in the v1beta2
+        form ("topologyAssignment"), encoded on the device from the resident names."""
+        return self._json_call(self._lib.kueue_tas_host_find_v1beta2, podsets, 1 if simulate_empty else 0)["results"]
+
+    def last_v1beta2(self, materialize: bool = True):
+        """v1beta2 form of every result of the last run_compiled ([[...] per workload])."""
+        if not materialize:
+            if self._lib.kueue_tas_host_v1beta2_last(self._h, None):
+                raise RuntimeError(self._err())
+            return None
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_v1beta2_last(self._h, ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        return _take(self._lib, out)
 
     def find_topology_assignments_for_workloads(self, workloads: list) -> list:
         """Evaluate many workloads independently against this snapshot in one

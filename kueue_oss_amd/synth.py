@@ -514,3 +514,39 @@ def run_session(snap, ops: list) -> list:
         else:
             raise ValueError(k)
     return out
+
+
+def random_internal_assignment(rng: random.Random):
+    """An internal TopologyAssignment (pkg/util/tas/tas_assignment.go:30-38)
+    whose level values share prefixes/suffixes, overlap ("ababa"/"aba"),
+    repeat, or are empty — the cases fillSingleCompactSliceValues
+    (tas_assignment.go:135-197) distinguishes.  None sometimes."""
+    if rng.random() < 0.03:
+        return None
+    nl = rng.choice([1, 1, 2, 3, 4])
+    levels = [f"l{k}" for k in range(nl)]
+    n = rng.choice([0, 1, 2, 2, 3, 5, 8, 30, 200])
+    alpha = rng.choice(["ab", "abc", "a.", "xyz-0123"])
+
+    def word(m):
+        return "".join(rng.choice(alpha) for _ in range(m))
+
+    per_level = []
+    for _ in range(nl):
+        mode = rng.random()
+        pre, suf = word(rng.randint(0, 4)), word(rng.randint(0, 4))
+        base = word(rng.randint(0, 6))
+        vals = []
+        for _ in range(n):
+            if mode < 0.2:
+                vals.append(base)  # universal
+            elif mode < 0.35:
+                vals.append(rng.choice([base, base + word(1), base[: max(0, len(base) - 1)]]))
+            else:
+                vals.append(pre + word(rng.randint(0, 3)) + suf)
+        per_level.append(vals)
+    same = rng.random() < 0.5
+    c0 = rng.randint(1, 9)
+    domains = [{"values": [per_level[k][j] for k in range(nl)], "count": c0 if same else rng.randint(1, 9)}
+               for j in range(n)]
+    return {"levels": levels, "domains": domains}
