@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
@@ -197,22 +198,26 @@ class Reader {
 
 inline Node parse(const char* text) { return Reader(text).read(); }
 
-inline void write_string(std::string& out, const std::string& s) {
+inline void write_string(std::string& out, std::string_view s) {
   out += '"';
-  for (unsigned char ch : s) {
+  size_t run = 0;  // start of the pending run of characters that need no escape
+  for (size_t i = 0; i < s.size(); i++) {
+    const unsigned char ch = static_cast<unsigned char>(s[i]);
+    if (ch >= 0x20 && ch != '"' && ch != '\\') continue;
+    out.append(s.data() + run, i - run);
+    run = i + 1;
     if (ch == '"') out += "\\\"";
     else if (ch == '\\') out += "\\\\";
     else if (ch == '\n') out += "\\n";
     else if (ch == '\t') out += "\\t";
     else if (ch == '\r') out += "\\r";
-    else if (ch < 0x20) {
+    else {
       char buf[8];
       snprintf(buf, sizeof buf, "\\u%04x", ch);
       out += buf;
-    } else {
-      out += char(ch);
     }
   }
+  out.append(s.data() + run, s.size() - run);
   out += '"';
 }
 

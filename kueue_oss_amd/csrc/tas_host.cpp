@@ -1277,27 +1277,26 @@ static void write_v1beta2(std::string& out, const std::vector<std::string>& leve
     const std::string_view v0 = value(0, k);
     if (e.universal) {
       out += "{\"universal\":";
-      kjson::write_string(out, std::string(v0));
+      kjson::write_string(out, v0);
       out += "}";
       continue;
     }
     out += "{\"individual\":{";
     if (e.prefix_len > 0) {
       out += "\"prefix\":";
-      kjson::write_string(out, std::string(v0.substr(0, size_t(e.prefix_len))));
+      kjson::write_string(out, v0.substr(0, size_t(e.prefix_len)));
       out += ",";
     }
     if (e.suffix_len > 0) {
       out += "\"suffix\":";
-      kjson::write_string(out, std::string(v0.substr(v0.size() - size_t(e.suffix_len))));
+      kjson::write_string(out, v0.substr(v0.size() - size_t(e.suffix_len)));
       out += ",";
     }
     out += "\"roots\":[";
     for (size_t j = 0; j < n; j++) {
       if (j) out += ",";
       const std::string_view vj = value(j, k);
-      kjson::write_string(out, std::string(vj.substr(size_t(e.prefix_len), vj.size() - size_t(e.prefix_len) -
-                                                                              size_t(e.suffix_len))));
+      kjson::write_string(out, vj.substr(size_t(e.prefix_len), vj.size() - size_t(e.prefix_len) - size_t(e.suffix_len)));
     }
     out += "]}}";
   }
