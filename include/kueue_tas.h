@@ -206,8 +206,9 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
 
 /* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
- * events, summed over its chunks): [0] fill (+ exclusion stats reduce), [1]
- * roll-up of the remaining levels, [2] exclusion-stats replication, [3] the
+ * events, summed over its chunks): [0] fill, [1] roll-up of the remaining
+ * levels, [2] ExclusionStats (staged fill: the third-stream branch of counts
+ * + reduce, concurrent with [1] and [4]; else the replication), [3] the
  * fast-LFC branch on the second stream (leaf tables, select, emit; runs
  * concurrently with [1], [2], [4]), [4] select of the other evals, [5] wait
  * for the fast-LFC branch, [6] total from the request upload to the join.

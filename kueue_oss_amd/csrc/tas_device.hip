@@ -135,6 +135,10 @@ struct kueue_tas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // fast-LFC branch (tables, select, emit) beside the BestFit select
+  hipStream_t stream3 = nullptr;  // ExclusionStats branch (staged fill): counts + reduce beside the roll-up/select
+  hipEvent_t evs[2] = {};         // ExclusionStats branch: start, end (also the join)
+  DevBuf<int8_t> d_fill_lim;
+  std::vector<int32_t> cls_pos, cls_cur;
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
   std::string err;
@@ -238,12 +242,14 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     return nullptr;
   }
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->evl) (void)hipEventCreate(&e);
+  for (auto& e : c->evs) (void)hipEventCreate(&e);
   return c;
 }
 
@@ -252,6 +258,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   c->d_child_off.release();
   c->d_id_rank.release();
   c->d_taint_profile.release();
@@ -266,6 +273,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_scratch.release();
   c->d_deltas.release();
   c->d_fits.release();
+  c->d_fill_lim.release();
   c->d_parent.release();
   c->d_names.release();
   c->d_name_off.release();
@@ -298,6 +306,9 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evl)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->evs)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -622,6 +633,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t o_fill = seg(n * 4), o_fchunks = seg(n * 8), o_pairs = seg(n * 8), o_rep = seg(n * 4);
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
   const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
+  const size_t o_moff = seg((n + 1) * 4), o_mem = seg(n * 4);  // class members in fill order (CSR)
   HIPCHK(c, c->h_stage.ensure(stage_bytes));
   HIPCHK(c, c->d_stage.ensure(stage_bytes));
   uint8_t* hs = c->h_stage.p;
@@ -865,6 +877,21 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
                      [&](int32_t a, int32_t b2) { return cls_sig[size_t(a)] < cls_sig[size_t(b2)]; });
     for (int k = 0; k < ncls; k++) h_fill[k] = rep[size_t(order[size_t(k)])];
     nfill = ncls;
+    {  // members other than the rep, grouped by fill position (stats written by the reduce)
+      int32_t* h_moff = reinterpret_cast<int32_t*>(hs + o_moff);
+      int32_t* h_mem = reinterpret_cast<int32_t*>(hs + o_mem);
+      std::vector<int32_t>& pos = c->cls_pos;
+      pos.resize(size_t(ncls));
+      for (int k = 0; k < ncls; k++) pos[size_t(order[size_t(k)])] = k;
+      for (int k = 0; k <= ncls; k++) h_moff[k] = 0;
+      for (size_t i = 0; i < n; i++)
+        if (int32_t(i) != rep[size_t(cls_of[i])]) h_moff[pos[size_t(cls_of[i])] + 1]++;
+      for (int k = 0; k < ncls; k++) h_moff[k + 1] += h_moff[k];
+      std::vector<int32_t>& cur = c->cls_cur;
+      cur.assign(h_moff, h_moff + ncls);
+      for (size_t i = 0; i < n; i++)
+        if (int32_t(i) != rep[size_t(cls_of[i])]) h_mem[cur[size_t(pos[size_t(cls_of[i])])]++] = int32_t(i);
+    }
     for (int k = 0; k < ncls;) {
       int e = k + 1;
       while (e < ncls && e - k < kEvalsPerFillBlock && cls_sig[size_t(order[size_t(e)])] == cls_sig[size_t(order[size_t(k)])])
@@ -950,6 +977,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.nstat = 0;
   b.nstat_R = s.R;
   b.fill_stats = nullptr;
+  b.stats_split = 0;
+  b.fill_lim = nullptr;
+  b.cls_member_off = nullptr;
+  b.cls_members = nullptr;
   b.rack_fanout = 0;
   b.rack_pos = nullptr;
   b.ctr_stride = ctr_stride;
@@ -1005,9 +1036,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
-    if (b.nstat) {
+    if (b.nstat) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
+      HIPCHK(c, c->d_fill_lim.ensure(size_t(nfchunks) * size_t(s.N)));
+      b.stats_split = 1;
+      b.fill_lim = c->d_fill_lim.p;
+      b.cls_member_off = reinterpret_cast<const int32_t*>(ds + o_moff);
+      b.cls_members = reinterpret_cast<const int32_t*>(ds + o_mem);
     }
     b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (b.rack_fanout) {
@@ -1021,12 +1057,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
-    if (b.nstat) {
-      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(grid.x));
-      HIPCHK(c, hipGetLastError());
-    }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  if (b.stats_split) {  // counts, reduce and member stores beside the roll-up / select
+    HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
+    HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
+    dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
+    hipLaunchKernelGGL(fill_exclusion_kernel, grid, dim3(256), 0, c->stream3, s, b);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(grid.x));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->evs[1], c->stream3));
+  }
   // K2
   for (int l = s.L - 2 - (b.rack_fanout ? 1 : 0); l >= 0; l--) {
     if (s.level_size[l] <= 0) continue;
@@ -1042,7 +1084,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  if (npairs) {  // exclusion stats of the class rep to the other members
+  if (npairs && !b.stats_split) {  // exclusion stats of the class rep to the other members
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
     HIPCHK(c, hipGetLastError());
   }
@@ -1085,6 +1127,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
+  if (b.stats_split) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
@@ -1117,6 +1160,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const float partials = st[3];  // ev4 -> ev5: leaf partials; stage [3] reports the concurrent fast-LFC branch
   st[3] = 0.f;
   if (nfast) (void)hipEventElapsedTime(&st[3], c->evl[0], c->evl[1]);
+  if (b.stats_split) (void)hipEventElapsedTime(&st[2], c->evs[0], c->evs[1]);  // the concurrent stats branch
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
   for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
   ms[0] += st[0];                    // fill (+ exclusion stats reduce)

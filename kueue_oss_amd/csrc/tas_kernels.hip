@@ -97,6 +97,30 @@ __device__ __forceinline__ Key wave_min_key(Key k) {
   }
   return k;
 }
+// Wave arg-min / arg-max over (value, index) pairs: ties keep the smaller
+// (arg-min) or larger (arg-max) index.
+__device__ __forceinline__ void wave_argmin(uint64_t& v, int32_t& i) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t ov = shfl_xor_u64(v, m);
+    const int32_t oi = __shfl_xor(i, m, 64);
+    if (ov < v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+__device__ __forceinline__ void wave_argmax(uint64_t& v, int32_t& i) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t ov = shfl_xor_u64(v, m);
+    const int32_t oi = __shfl_xor(i, m, 64);
+    if (ov > v || (ov == v && oi > i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
@@ -405,8 +429,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   __shared__ FillEvalParams sh_p[kEvalsPerBlock];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
-  const bool lds_stats = b.nstat > 0;
-  for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
+  const bool split = b.stats_split != 0;  // ExclusionStats counted by fill_exclusion_kernel
+  const bool lds_stats = !split && b.nstat > 0;
+  if (lds_stats)
+    for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   const int e0 = b.fill_chunks[2 * blockIdx.y];
   const int ne = b.fill_chunks[2 * blockIdx.y + 1];
   const bool stage_taints = b.num_profiles <= kStagedProfiles;
@@ -533,6 +559,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         return any ? result : 0;
       };
       state0 = count_slots(rmask, tb, pres, false, &lim0);
+      if (split) b.fill_lim[int64_t(blockIdx.y) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
       swl0 = state0;
       if (leader) {
         int dummy;
@@ -661,6 +688,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         }
       }
     }
+    if (split) continue;
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) {
       if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
@@ -698,8 +726,111 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   }
 }
 
-// Sum the per-block ExclusionStats partials of every phase-1 class.
+// ExclusionStats of the staged fill's classes (fillInCounts :1578-1634:
+// first untolerated taint, then nodeSelector, then a resource giving state 0)
+// in a kernel of their own, off the fill's critical path: it runs on a
+// third stream beside the roll-up and select.  Same grid and masks as the
+// fill; the resource case reads the limiting resource the fill recorded per
+// (chunk, leaf) where the chunk's signature gives state 0.
+__global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
+  __shared__ int32_t sh_toff[kEvalsPerBlock];
+  __shared__ int32_t sh_nsel[kEvalsPerBlock];
+  __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
+  __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
+  __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
+  const int e0 = b.fill_chunks[2 * blockIdx.y];
+  const int ne = b.fill_chunks[2 * blockIdx.y + 1];
+  const bool stage_taints = b.num_profiles <= kStagedProfiles;
+  if (int(threadIdx.x) < ne) {
+    const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
+    sh_toff[threadIdx.x] = ev.taint_table;
+    sh_nsel[threadIdx.x] = ev.nsel;
+    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+      sh_sel[threadIdx.x][2 * k] = ev.sel_col[k];
+      sh_sel[threadIdx.x][2 * k + 1] = ev.sel_val[k];
+    }
+  }
+  __syncthreads();
+  if (s.taint_profile && stage_taints) {
+    for (int i = threadIdx.x; i < ne * kStagedProfiles; i += kFillThreads) {
+      const int e = i / kStagedProfiles, p = i % kStagedProfiles;
+      sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_toff[e] + p] : -1;
+    }
+  }
+  __syncthreads();
+  const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
+  const bool valid = leaf < s.N;
+  const int N = s.N;
+  const int lane = lane_id();
+  const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
+  const int lim = valid ? int(b.fill_lim[int64_t(blockIdx.y) * N + leaf]) : -1;
+  int32_t lab[kStagedLabels];
+#pragma unroll
+  for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
+  for (int e = 0; e < ne; e++) {
+    int kind = EX_NONE, id = -1;
+    if (valid) {
+      if (s.lowest_is_hostname) {
+        if (s.taint_profile) {
+          const int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(sh_toff[e]) + prof];
+          if (t >= 0) {
+            kind = EX_TAINT;
+            id = t;
+          }
+        }
+        if (kind == EX_NONE) {
+          const int nsel = uni(sh_nsel[e]);
+          for (int k = 0; k < nsel; k++) {
+            const int col = uni(sh_sel[e][2 * k]);
+            int32_t v;
+            if (col < kStagedLabels) {
+              v = lab[0];
+#pragma unroll
+              for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+            } else {
+              v = s.label_values[int64_t(col) * N + leaf];
+            }
+            if (v != uni(sh_sel[e][2 * k + 1])) {
+              kind = EX_SELECTOR;
+              break;
+            }
+          }
+        }
+      }
+      if (kind == EX_NONE && lim >= 0) {
+        kind = EX_RESOURCE;
+        id = lim;
+      }
+    }
+    const uint64_t selm = ballot(kind == EX_SELECTOR);
+    if (lane == 0 && selm) atomicAdd(&sh_stats[e][0], __popcll(selm));
+    uint64_t tm = ballot(kind == EX_TAINT);
+    while (tm) {
+      const int tid = __shfl(id, __ffsll((unsigned long long)tm) - 1, 64);
+      const uint64_t mm = ballot(kind == EX_TAINT && id == tid);
+      if (lane == 0) atomicAdd(&sh_stats[e][1 + tid], __popcll(mm));
+      tm &= ~mm;
+    }
+    uint64_t rm = ballot(kind == EX_RESOURCE);
+    while (rm) {
+      const int rid = __shfl(id, __ffsll((unsigned long long)rm) - 1, 64);
+      const uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
+      if (lane == 0) atomicAdd(&sh_stats[e][1 + b.num_taints + rid], __popcll(mm));
+      rm &= ~mm;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
+    const int e = i / b.nstat, k = i % b.nstat;
+    b.fill_stats[(int64_t(e0 + e) * gridDim.x + blockIdx.x) * b.nstat + k] = sh_stats[e][k];
+  }
+}
+
+// Sum the per-block ExclusionStats partials of every phase-1 class; with
+// class member lists, also store them for every other member of the class.
 __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int nblk) {
+
   const int f = blockIdx.x;
   const int eid = b.fill_ids[f];
   const int wv = threadIdx.x >> 6, lane = lane_id();
@@ -709,10 +840,13 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
 #pragma unroll 8
     for (int j = lane; j < nblk; j += kWave) acc += p[int64_t(j) * b.nstat];
     acc = wave_sum_wrap32(acc);
-    if (lane == 0) {
-      if (k == 0) b.sel_counts[eid] = acc;
-      else if (k <= b.num_taints) b.taint_counts[int64_t(eid) * b.num_taints + (k - 1)] = acc;
-      else b.res_counts[int64_t(eid) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
+    const int m0 = b.cls_member_off ? b.cls_member_off[f] : 0;
+    const int m1 = b.cls_member_off ? b.cls_member_off[f + 1] : 0;
+    for (int m = m0 - 1 + lane; m < m1; m += kWave) {  // m0 - 1: the rep itself
+      const int d = m < m0 ? eid : b.cls_members[m];
+      if (k == 0) b.sel_counts[d] = acc;
+      else if (k <= b.num_taints) b.taint_counts[int64_t(d) * b.num_taints + (k - 1)] = acc;
+      else b.res_counts[int64_t(d) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
     }
   }
 }
@@ -2711,13 +2845,21 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         if (w.partials[i].bfst == pbst) pbk = key_min2(pbk, w.partials[i].bfkey);
       pbk = wave_min_key(pbk);
     } else if (!w.leader) {
-      // no leader: keys (sliceState, state, index); the level's counters are
-      // read 4 domains per lane per load (levels start 16-byte aligned), 4
-      // loads per array in flight.  findLevelWithFitDomains never mutates.
+      // no leader: the sortedDomainsWithLeader key is (k1(sliceState),
+      // s_asc(state), index) under a constant leader part, so lanes compare
+      // the packed 64-bit (k1 << 32 | s_asc(state)) and keep the first index
+      // (each lane walks its indices in increasing order); the wave then
+      // reduces (value, index) pairs.  The level's counters are read 4
+      // domains per lane per load (levels start 16-byte aligned), 4 loads per
+      // array in flight.  BestFit evals also track findBestFitDomainBy's
+      // candidate (:1216-1231: min sliceState >= sliceCount, ties by key) in
+      // the same pass; LFC evals the first fit, the last key and the minimum.
       const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
       const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
       const int nq = (D + 3) / 4;
-      Key inv = key_max();
+      const bool lfc = w.lfc, bf = w.bf;
+      uint64_t tv = ~0ull, fv = ~0ull, lv = 0, bv = ~0ull;
+      int32_t ti = 0x7fffffff, fi = 0x7fffffff, li = -1, bi = 0x7fffffff;
       constexpr int QU = 4;
       for (int q0 = 0; q0 < nq; q0 += QU * kWave) {
         int4 sa[QU], ssa[QU];
@@ -2736,19 +2878,51 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
           for (int k = 0; k < 4; k++) {
             const int i = 4 * q + k;
             if (q < nq && i < D) {
-              const Key kk = key_wl(w.lfc, 0, ss4[k], st4[k], i);
-              top = key_min2(top, kk);
-              inv = key_min2(inv, Key{~kk.hi, ~kk.lo});
-              if (ss4[k] >= sliceCount) lfcfit = key_min2(lfcfit, kk);
-              minss = min(minss, ss4[k]);
+              const uint32_t lo = s_asc(st4[k]);
+              const uint64_t v = (uint64_t(lfc ? s_asc(ss4[k]) : s_desc(ss4[k])) << 32) | lo;
+              if (v < tv) {
+                tv = v;
+                ti = i;
+              }
+              const bool fits = ss4[k] >= sliceCount;
+              if (lfc) {
+                if (v >= lv) {
+                  lv = v;
+                  li = i;
+                }
+                if (fits && v < fv) {
+                  fv = v;
+                  fi = i;
+                }
+                minss = min(minss, ss4[k]);
+              }
+              if (bf) {
+                const uint64_t b = (uint64_t(s_asc(ss4[k])) << 32) | lo;
+                if (fits && b < bv) {
+                  bv = b;
+                  bi = i;
+                }
+              }
             }
           }
         }
       }
-      top = wave_min_key(top);
-      lfcfit = wave_min_key(lfcfit);
-      inv = wave_min_key(inv);
-      last = Key{~inv.hi, ~inv.lo};
+      wave_argmin(tv, ti);
+      const uint64_t lead_hi = uint64_t(s_desc(0)) << 32;
+      auto unpack = [&](uint64_t v, int32_t i) {
+        return Key{lead_hi | (v >> 32), ((v & 0xffffffffull) << 32) | uint32_t(i)};
+      };
+      top = unpack(tv, ti);
+      if (lfc) {
+        wave_argmin(fv, fi);
+        wave_argmax(lv, li);
+        if (fi != 0x7fffffff) lfcfit = unpack(fv, fi);
+        last = unpack(lv, li);
+      }
+      if (bf) {
+        wave_argmin(bv, bi);
+        if (bi != 0x7fffffff) pbk = Key{0, uint32_t(bi)};  // best-fit domain index (used below)
+      }
     } else {
       bool has_last = false;
       for (int i = w.lane; i < D; i += kWave) {
@@ -2779,43 +2953,8 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         if (use_partials) {
           topg = loff + int(uint32_t(pbk.lo));
         } else if (!w.leader) {
-          // one vectorized pass: per lane the smallest (sliceState >= sliceCount, key), then a wave arg-min
-          const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
-          const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
-          const int nq = (D + 3) / 4;
-          uint32_t bst = ~0u;
-          Key bk = key_max();
-          constexpr int QU = 4;
-          for (int q0 = 0; q0 < nq; q0 += QU * kWave) {
-            int4 sa[QU], ssa[QU];
-#pragma unroll
-            for (int u = 0; u < QU; u++) {
-              const int q = min(q0 + u * kWave + w.lane, nq - 1);
-              sa[u] = S4[q];
-              ssa[u] = SS4[q];
-            }
-#pragma unroll
-            for (int u = 0; u < QU; u++) {
-              const int q = q0 + u * kWave + w.lane;
-              const int32_t st4[4] = {sa[u].x, sa[u].y, sa[u].z, sa[u].w};
-              const int32_t ss4[4] = {ssa[u].x, ssa[u].y, ssa[u].z, ssa[u].w};
-#pragma unroll
-              for (int k = 0; k < 4; k++) {
-                const int i = 4 * q + k;
-                if (q < nq && i < D && ss4[k] >= sliceCount) {
-                  const uint32_t sw = s_asc(ss4[k]);
-                  const Key kk = key_wl(w.lfc, 0, ss4[k], st4[k], i);
-                  if (sw < bst || (sw == bst && key_lt(kk, bk))) {
-                    bst = sw;
-                    bk = kk;
-                  }
-                }
-              }
-            }
-          }
-          const uint32_t wbst = uint32_t(wave_min_u64(uint64_t(bst)));
-          bk = wave_min_key(bst == wbst ? bk : key_max());
-          topg = loff + int(uint32_t(bk.lo));
+          // found by the scan above (top fits, so a candidate exists)
+          topg = loff + int(uint32_t(pbk.lo));
         } else {
           uint32_t bst = ~0u;
           for (int i = w.lane; i < D; i += kWave) {
