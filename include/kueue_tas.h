@@ -159,6 +159,9 @@ typedef struct {
 /* host layer: copy the entries through kueue_tas_eval_batch's packed buffer
  * instead of reading the zero-copy view (exercises both ABI paths) */
 #define KUEUE_TAS_CFG_PACKED_ENTRIES 1
+/* count ExclusionStats inside the fill instead of the concurrent
+ * fill_exclusion_kernel branch (test knob: both paths must agree) */
+#define KUEUE_TAS_CFG_INLINE_STATS 2
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

@@ -143,6 +143,7 @@ struct kueue_tas_ctx {
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
   std::string err;
   int list_cap = 1024;
+  bool inline_stats = false;  // KUEUE_TAS_CFG_INLINE_STATS
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
@@ -228,6 +229,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
   auto* c = new kueue_tas_ctx();
   if (cfg) {
     c->device = cfg->device;
+    c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -1036,9 +1038,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
-    if (b.nstat) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
+    if (b.nstat) {
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
+    }
+    if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
       HIPCHK(c, c->d_fill_lim.ensure(size_t(nfchunks) * size_t(s.N)));
       b.stats_split = 1;
       b.fill_lim = c->d_fill_lim.p;
@@ -1057,6 +1061,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
+    if (b.nstat && !b.stats_split) {  // ExclusionStats counted inside the fill
+      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(grid.x));
+      HIPCHK(c, hipGetLastError());
+    }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   if (b.stats_split) {  // counts, reduce and member stores beside the roll-up / select
@@ -1144,6 +1152,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->ent_stride = entry_cap;
   lap(4);
   memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
+  {  // nodeSelector exclusions: counted beside select (stream3), read from the stats region after the join
+    const int32_t* sel = c->res_stats_h + n * nt + n * size_t(s.R);
+    for (size_t i = 0; i < n; i++) out[i].excl_selector = sel[i];
+  }
   if (KTAS_PROFILE) {
     const size_t base = c->last_prof.size();
     c->last_prof.resize(base + n * P_NCAT);

@@ -2880,7 +2880,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
             if (q < nq && i < D) {
               const uint32_t lo = s_asc(st4[k]);
               const uint64_t v = (uint64_t(lfc ? s_asc(ss4[k]) : s_desc(ss4[k])) << 32) | lo;
-              if (v < tv) {
+              if (v < tv || (v == tv && i < ti)) {  // the index test only matters for the sentinel
                 tv = v;
                 ti = i;
               }
@@ -2890,7 +2890,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
                   lv = v;
                   li = i;
                 }
-                if (fits && v < fv) {
+                if (fits && (v < fv || (v == fv && i < fi))) {
                   fv = v;
                   fi = i;
                 }
@@ -2898,7 +2898,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
               }
               if (bf) {
                 const uint64_t b = (uint64_t(s_asc(ss4[k])) << 32) | lo;
-                if (fits && b < bv) {
+                if (fits && (b < bv || (b == bv && i < bi))) {
                   bv = b;
                   bi = i;
                 }
@@ -3218,7 +3218,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   o.num_workers = o.num_leaders = 0;
   o.assignment_nil = 0;
   o.total_nodes = s.N;
-  o.excl_selector = b.sel_counts[eid];
+  o.excl_selector = 0;  // set by the host from the stats region (counted concurrently, stream3)
   o.excl_affinity = 0;
   o.excl_topology = 0;
   for (int c = 0; c < KUEUE_TAS_MAX_LAYERS; c++) o.ml_fit[c] = o.ml_need[c] = 0;

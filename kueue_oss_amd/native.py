@@ -129,9 +129,9 @@ class TASFlavorSnapshot:
     tools/extract_goldens.py (podSets ignored)."""
 
     def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
-                 packed_entries: bool = False):
+                 packed_entries: bool = False, inline_stats: bool = False):
         self._lib = lib if lib is not None else load_library()
-        cfg = KueueTasConfig(list_cap, max_batch, device, 1 if packed_entries else 0)
+        cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <cstdio>
 #include <functional>
+#include <vector>
 
 #define __global__
 #define __device__
@@ -40,6 +41,41 @@ uint64_t wave_exchange(uint64_t v, int src);       // value of lane `src`
 uint64_t wave_ballot(bool p);
 void* dynamic_lds();
 void launch(dim3 grid, dim3 block, size_t shmem, const std::function<void()>& fn);
+
+// Streams are DEFERRED queues: nothing a stream holds runs until something
+// needs it — hipStreamSynchronize of that stream, a hipStreamWaitEvent
+// executed by another stream (which drains the recording stream up to the
+// event), or a synchronous API (hipMemcpy, hipFree, ...: all streams).  So a
+// side stream's work runs as late as its dependencies allow, and a missing
+// event dependency shows up as a wrong result instead of passing by luck.
+struct Stream;
+struct Event {
+  Stream* stream = nullptr;
+  size_t pos = 0;  // ops of `stream` that precede the record
+};
+struct Stream {
+  std::vector<std::function<void()>> ops;
+  size_t done = 0;
+  void run_until(size_t n) {
+    while (done < n && done < ops.size()) {
+      auto op = std::move(ops[done]);
+      done++;  // before running: a wait inside may re-enter this stream's drain
+      op();
+    }
+  }
+  void drain() { run_until(ops.size()); }
+};
+std::vector<Stream*>& streams();
+inline void drain_all() {
+  for (bool again = true; again;) {
+    again = false;
+    for (Stream* s : streams())
+      if (s->done < s->ops.size()) {
+        s->drain();
+        again = true;
+      }
+  }
+}
 }  // namespace emu
 
 #define threadIdx (emu::cur()->tid)
@@ -87,8 +123,8 @@ using std::min;
 // ---- runtime API subset ----
 typedef int hipError_t;
 constexpr hipError_t hipSuccess = 0;
-typedef struct emu_stream* hipStream_t;
-typedef struct emu_event* hipEvent_t;
+typedef emu::Stream* hipStream_t;
+typedef emu::Event* hipEvent_t;
 enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
 constexpr unsigned hipStreamNonBlocking = 1;
 constexpr unsigned hipHostMallocDefault = 0;
@@ -103,46 +139,79 @@ inline hipError_t hipMalloc(T** p, size_t bytes) {
   *p = static_cast<T*>(calloc(1, bytes));
   return *p ? hipSuccess : 2;
 }
-inline hipError_t hipFree(void* p) { free(p); return hipSuccess; }
+inline hipError_t hipFree(void* p) {
+  emu::drain_all();
+  free(p);
+  return hipSuccess;
+}
 template <typename T>
 inline hipError_t hipHostMalloc(T** p, size_t bytes, unsigned) {
   *p = static_cast<T*>(calloc(1, bytes));
   return *p ? hipSuccess : 2;
 }
-inline hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+inline hipError_t hipHostFree(void* p) {
+  emu::drain_all();
+  free(p);
+  return hipSuccess;
+}
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
-inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
-  if (n) memmove(d, s, n);
+inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t st) {
+  if (n) st->ops.push_back([=]() { memmove(d, s, n); });
   return hipSuccess;
 }
 inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+  emu::drain_all();
   if (n) memmove(d, s, n);
   return hipSuccess;
 }
 struct int4 {
   int x, y, z, w;
 };
-inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
-  memset(d, v, n);
+inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t st) {
+  st->ops.push_back([=]() { memset(d, v, n); });
   return hipSuccess;
 }
 inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) {
-  *s = reinterpret_cast<hipStream_t>(new char[1]);
+  *s = new emu::Stream();
+  emu::streams().push_back(*s);
   return hipSuccess;
 }
-inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
-inline hipError_t hipStreamDestroy(hipStream_t s) { delete[] reinterpret_cast<char*>(s); return hipSuccess; }
+inline hipError_t hipStreamSynchronize(hipStream_t s) {
+  s->drain();
+  return hipSuccess;
+}
+inline hipError_t hipStreamDestroy(hipStream_t s) {
+  emu::drain_all();
+  auto& v = emu::streams();
+  v.erase(std::find(v.begin(), v.end(), s));
+  delete s;
+  return hipSuccess;
+}
 inline hipError_t hipEventCreate(hipEvent_t* e) {
-  *e = reinterpret_cast<hipEvent_t>(new char[1]);
+  *e = new emu::Event();
   return hipSuccess;
 }
-inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
-inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
+inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+  e->stream = s;
+  e->pos = s->ops.size();
+  return hipSuccess;
+}
+inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
+  emu::Stream* src = e->stream;
+  const size_t pos = e->pos;
+  if (src && src != s) s->ops.push_back([=]() { src->run_until(pos); });
+  return hipSuccess;
+}
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
-inline hipError_t hipEventDestroy(hipEvent_t e) { delete[] reinterpret_cast<char*>(e); return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t e) { delete e; return hipSuccess; }
 
-#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...) \
-  emu::launch(dim3(grid), dim3(block), size_t(shmem), [&]() { kernel(__VA_ARGS__); })
+// kernel arguments are captured by value: the launch may run after the caller's locals are gone
+#define hipLaunchKernelGGL(kernel, grid, block, shmem, stream, ...)                                              \
+  do {                                                                                                            \
+    const dim3 emu_g_ = dim3(grid), emu_b_ = dim3(block);                                                         \
+    const size_t emu_sh_ = size_t(shmem);                                                                         \
+    (stream)->ops.push_back([=]() { emu::launch(emu_g_, emu_b_, emu_sh_, [=]() { kernel(__VA_ARGS__); }); });    \
+  } while (0)
 
 // every lane holds the same value where the kernels use it (wave-uniform data)
 #define __builtin_amdgcn_readfirstlane(v) (v)

@@ -7,6 +7,10 @@
 #include "hip/hip_runtime.h"
 
 namespace emu {
+std::vector<Stream*>& streams() {
+  static std::vector<Stream*> v;
+  return v;
+}
 namespace {
 enum Wait { kNone = 0, kWave = 1, kBlock = 2 };
 struct Fiber {

@@ -95,3 +95,15 @@ def test_emulated_int64_arithmetic_stress(emu_lib, seed):
         got = snap.find_topology_assignments_for_flavor(case["podSets"])
         snap.close()
         assert got == want, (i, got, want)
+
+
+def test_emulated_inline_stats_path_matches_oracle(emu_lib):
+    # KUEUE_TAS_CFG_INLINE_STATS: ExclusionStats counted inside the fill (no third-stream branch)
+    rng = random.Random(14)
+    for i in range(120):
+        case = synth.random_case(rng)
+        want = oracle_lib.run_case(case)["results"]
+        snap = TASFlavorSnapshot(case, lib=emu_lib, inline_stats=True)
+        got = snap.find_topology_assignments_for_flavor(case["podSets"])
+        snap.close()
+        assert got == want, (i, got, want)
