@@ -372,6 +372,19 @@ int kueue_tas_host_find_v1beta2(kueue_tas_host* h, const char* podsets_json, int
 int kueue_tas_host_v1beta2_last(kueue_tas_host* h, char** out_json);
 int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits);
 
+/* Batched preemption search: the TAS part of preemption's `minimal`
+ * (pkg/scheduler/preemption/preemption.go:307-345; workloadFits :614-625 with
+ * the quota checks left to the caller).  candidates_json = [[usage records of
+ * candidate 0], ...] in candidate order (records as in update_usage; the
+ * candidates' usage is in the snapshot).  Every prefix {0..i} is evaluated in
+ * ONE device batch as the workload under RemoveUsage of the prefix (a removal
+ * overlay, the snapshot itself is not modified); then fillBackWorkloads runs
+ * on the first fitting prefix.  *out_json = {"prefixFits":[bool per prefix],
+ * "firstFit": i or -1, "targets": [candidate indices in the reference's final
+ * order] or null, "fillBackEvals": n}. */
+int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json, const char* candidates_json,
+                                     char** out_json);
+
 void kueue_tas_free(char* p);
 
 #ifdef __cplusplus

@@ -635,6 +635,36 @@ class FlavorSnapshot {
     if (rc) err = std::string("apply deltas: ") + kueue_tas_last_error(ctx);
     return rc;
   }
+  // Columns for every resource of a usage list (a removal overlay needs one).
+  bool ensure_columns_for_usage(const std::vector<DomainUsage>& us) {
+    std::set<std::string> names(cols.begin(), cols.end());
+    const size_t before = names.size();
+    names.insert("pods");
+    for (auto& u : us)
+      for (auto& kv : u.single) names.insert(kv.first);
+    if (names.size() == before) return false;
+    set_columns(names);
+    return true;
+  }
+  // RemoveUsage(us) as an evaluation overlay: the leaf's tasUsage loses
+  // SinglePodRequests x count + pods:count (updateTASUsage :257-293), so the
+  // remaining capacity gains it; fillInCounts computes
+  // free - (used - x) - assumed == free - used - (assumed - x) in Go's
+  // wrapping int64, and both Subs create the key (requests.go:90-94).
+  // Unknown domains are skipped like removeTASUsage does.
+  void add_removal(const std::vector<DomainUsage>& us, std::map<int32_t, std::map<int32_t, int64_t>>& o) const {
+    for (auto& u : us) {
+      auto it = leafById.find(u.id);
+      if (it == leafById.end()) continue;
+      auto& row = o[it->second];
+      for (auto& kv : u.single) {
+        int64_t& slot = row[colByName.at(kv.first)];
+        slot = sub64(slot, mul64(kv.second, u.count));
+      }
+      int64_t& pods = row[colByName.at("pods")];
+      pods = sub64(pods, u.count);
+    }
+  }
   // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), on the device.
   int fits(const std::vector<DomainUsage>& us, bool* out) {
     int rc = upload();
@@ -1070,8 +1100,12 @@ struct Evaluator {
     }
   }
 
+  // base: optional per-workload starting overlay (leaf -> column -> value
+  // subtracted from the remaining capacity), e.g. the negated usage of the
+  // workloads a preemption candidate set removes (SimulateUsageRemoval).
+  using Overlay = std::map<int32_t, std::map<int32_t, int64_t>>;
   int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results,
-          bool precompiled = false) {
+          bool precompiled = false, const std::vector<Overlay>* base = nullptr) {
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     for (auto& v : stage_ms) v = 0;
     for (auto& v : dev_host_ms) v = 0;
@@ -1094,7 +1128,7 @@ struct Evaluator {
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
     std::vector<char> done(wls.size(), 0);
-    std::vector<std::map<int32_t, std::map<int32_t, int64_t>>> assumedBy(wls.size());
+    std::vector<Overlay> assumedBy = base ? *base : std::vector<Overlay>(wls.size());
     size_t maxGroups = 0;
     for (auto& wl : wls) maxGroups = std::max(maxGroups, wl.groups.size());
     const size_t T = snap->taintStrings.size();
@@ -1105,7 +1139,7 @@ struct Evaluator {
       const std::vector<int32_t>* tt = &taint_table;
       const std::vector<std::pair<size_t, GroupEval*>>* bt = &batch;
       const std::vector<std::pair<size_t, GroupEval*>>* ea = &early;
-      if (pass == 0 && precompiled) {  // no assumed usage yet: reuse the compiled first pass
+      if (pass == 0 && precompiled && !base) {  // no assumed usage yet: reuse the compiled first pass
         if (p0_for != &wls || p0_gen != snap->compile_gen) {
           build_pass(wls, 0, done, assumedBy, p0_reqs, p0_taint, assumed, p0_batch, p0_early);
           p0_for = &wls;
@@ -1731,6 +1765,108 @@ int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits
       return rc;
     }
     *fits = f ? 1 : 0;
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+// Batched preemption search: the TAS part of `minimal` (pkg/scheduler/
+// preemption/preemption.go:307-341) with workloadFits (:614-625) reduced to
+// FindTopologyAssignmentsForWorkload(...).Failure() == nil.  Every candidate
+// prefix is one evaluation of the same workload under a removal overlay, so
+// the prefix scan is ONE device batch; fillBackWorkloads (:330-345) then runs
+// its reverse add-back loop one evaluation per step (each step depends on the
+// previous decision), keeping the reference's O(1) swap-delete target order.
+static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, const kjson::Node& cands,
+                             std::string* out) {
+  FlavorSnapshot& s = *h->snap;
+  std::vector<std::vector<FlavorSnapshot::DomainUsage>> cu;
+  for (auto& c : cands.items) {
+    cu.push_back(FlavorSnapshot::parse_usage(c));
+    s.ensure_columns_for_usage(cu.back());  // a re-columned snapshot reloads inside Evaluator::run
+  }
+  const size_t k = cu.size();
+  using Overlay = Evaluator::Overlay;
+  auto fits_all = [](const std::vector<PodSetResult>& rs) {
+    for (auto& r : rs)
+      if (!r.reason.empty()) return false;  // TASAssignmentsResult.Failure() (:384-391)
+    return true;
+  };
+  // one evaluation per removal set; every Workload parses its own PodSets
+  auto eval_sets = [&](const std::vector<std::vector<size_t>>& sets, std::vector<char>* fit) -> int {
+    std::vector<Workload> wls(sets.size());
+    std::vector<Overlay> base(sets.size());
+    for (size_t i = 0; i < sets.size(); i++) wls[i].podsets = parse_podsets(podsets);
+    // settle the column set first: the overlays index columns
+    for (auto& w : wls) s.ensure_columns_for(w.podsets);
+    for (size_t i = 0; i < sets.size(); i++)
+      for (size_t c : sets[i]) s.add_removal(cu[c], base[i]);
+    Evaluator ev{&s};
+    std::vector<std::vector<PodSetResult>> results;
+    int rc = ev.run(wls, false, &results, false, &base);
+    if (rc) return rc;
+    fit->resize(sets.size());
+    for (size_t i = 0; i < sets.size(); i++) (*fit)[i] = fits_all(results[i]) ? 1 : 0;
+    return 0;
+  };
+  std::vector<std::vector<size_t>> prefixes(k);
+  for (size_t i = 0; i < k; i++)
+    for (size_t c = 0; c <= i; c++) prefixes[i].push_back(c);
+  std::vector<char> pfit;
+  int rc = k ? eval_sets(prefixes, &pfit) : 0;
+  if (rc) return rc;
+  long first = -1;
+  for (size_t i = 0; i < k; i++)
+    if (pfit[i]) {
+      first = long(i);
+      break;
+    }
+  std::vector<size_t> targets;
+  int64_t fill_evals = 0;
+  if (first >= 0) {
+    targets = prefixes[size_t(first)];
+    for (long i = long(targets.size()) - 2; i >= 0; i--) {
+      // AddWorkload(targets[i]): the removal set is every other target
+      std::vector<size_t> set;
+      for (size_t j = 0; j < targets.size(); j++)
+        if (long(j) != i) set.push_back(targets[j]);
+      std::vector<char> f;
+      rc = eval_sets({set}, &f);
+      if (rc) return rc;
+      fill_evals++;
+      if (f[0]) {
+        targets[size_t(i)] = targets.back();
+        targets.pop_back();
+      }
+    }
+  }
+  *out = "{\"prefixFits\":[";
+  for (size_t i = 0; i < k; i++) *out += std::string(i ? "," : "") + (pfit[i] ? "true" : "false");
+  *out += "],\"firstFit\":" + std::to_string(first) + ",\"targets\":";
+  if (first < 0) {
+    *out += "null";
+  } else {
+    *out += "[";
+    for (size_t j = 0; j < targets.size(); j++) *out += (j ? "," : "") + std::to_string(targets[j]);
+    *out += "]";
+  }
+  *out += ",\"fillBackEvals\":" + std::to_string(fill_evals) + "}";
+  return 0;
+}
+
+int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json, const char* candidates_json,
+                                     char** out_json) {
+  if (!h || !h->snap || !h->err.empty() || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    std::string out;
+    int rc = preemption_search(h, kjson::parse(podsets_json), kjson::parse(candidates_json), &out);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    *out_json = dup(out);
     return 0;
   } catch (const std::exception& e) {
     h->err = e.what();

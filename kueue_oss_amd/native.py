@@ -114,6 +114,8 @@ def _bind(lib):
     lib.kueue_tas_host_find_v1beta2.restype = c.c_int
     lib.kueue_tas_host_v1beta2_last.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_v1beta2_last.restype = c.c_int
+    lib.kueue_tas_host_preemption_search.argtypes = [c.c_void_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_preemption_search.restype = c.c_int
     lib.kueue_tas_free.argtypes = [c.c_void_p]
 
 
@@ -184,6 +186,14 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_fits(self._h, json.dumps(records).encode(), ctypes.byref(f)):
             raise RuntimeError(self._err())
         return bool(f.value)
+
+    def preemption_search(self, podsets: list, candidates: list) -> dict:
+        """TAS part of preemption's `minimal` (pkg/scheduler/preemption/
+        preemption.go:307-345): every candidate prefix evaluated in one device
+        batch under a removal overlay, then fillBackWorkloads.  ``candidates``
+        is a list of usage-record lists (the candidates' admitted usage)."""
+        return self._json_call(self._lib.kueue_tas_host_preemption_search, podsets,
+                               json.dumps(candidates).encode())
 
     # ---- v1beta2 wire format (pkg/util/tas/tas_assignment.go) ----
     def _json_call(self, fn, payload, *extra):

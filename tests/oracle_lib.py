@@ -99,3 +99,33 @@ def v1beta2_from(internal: dict) -> dict:
 def internal_from(v1beta2: dict) -> dict:
     """InternalFrom (pkg/util/tas/tas_assignment.go:124-133)."""
     return _encoding(v1beta2, 1)
+
+
+def preemption_search(snapshot_case: dict, setup: list, podsets: list, candidates: list) -> dict:
+    """Oracle restatement of the TAS part of preemption's `minimal`
+    (pkg/scheduler/preemption/preemption.go:307-345, workloadFits :614-625
+    reduced to FindTopologyAssignmentsForWorkload(...).Failure() == nil):
+    candidates are removed one by one (snapshot.RemoveWorkload ->
+    RemoveUsage -> updateTASUsage on the oracle snapshot) and the workload is
+    re-evaluated after each; on the first fit, fillBackWorkloads adds the
+    targets back in reverse order with the reference's swap-delete.  Every
+    evaluation replays `setup` (ops that put the candidates' usage in) on a
+    fresh oracle snapshot.  Evaluates every prefix, like the device batch."""
+    def fits(removed):
+        ops = list(setup) + [{"op": "remove", "usage": candidates[c]} for c in removed]
+        ops.append({"op": "find", "podSets": podsets})
+        res = session(snapshot_case, ops)[-1]
+        return all(not r["reason"] for r in res)
+
+    pfits = [fits(list(range(i + 1))) for i in range(len(candidates))]
+    first = next((i for i, f in enumerate(pfits) if f), -1)
+    targets = None
+    fill = 0
+    if first >= 0:
+        targets = list(range(first + 1))
+        for i in range(len(targets) - 2, -1, -1):
+            fill += 1
+            if fits([t for j, t in enumerate(targets) if j != i]):
+                targets[i] = targets[-1]
+                targets.pop()
+    return {"prefixFits": pfits, "firstFit": first, "targets": targets, "fillBackEvals": fill}
