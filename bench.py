@@ -195,7 +195,21 @@ def main():
         snap.add_usage(recs[:8])
         snap.remove_usage(recs[:8])
         upd_ms = (time.perf_counter() - t0) / 2 * 1e3
-        extras = {"v1beta2_encode_ms_per_batch": round(enc_ms, 3),
+        # batched preemption search (preemption.go:307-345): 16 admitted
+        # workloads as candidates, one batch over their prefixes + fill-back
+        cands = [synth.usage_records(w, res) for w, res in zip(mine[:64], got)]
+        cands = [c for c in cands if c][:16]
+        for c in cands:
+            snap.add_usage(c)
+        pre = [dict(p, count=p.get("count", 1) * 4) for p in mine[0]]
+        t0 = time.perf_counter()
+        pr = snap.preemption_search(pre, cands)
+        pre_ms = (time.perf_counter() - t0) * 1e3
+        for c in cands:
+            snap.remove_usage(c)
+        extras = {"preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),
+                  "preemption_first_fit": pr["firstFit"], "preemption_fill_back_evals": pr["fillBackEvals"],
+                  "v1beta2_encode_ms_per_batch": round(enc_ms, 3),
                   "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
                   "usage_update_ms_per_call": round(upd_ms, 3)}
 

@@ -25,6 +25,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1367,19 +1368,41 @@ static int encode_results(FlavorSnapshot& s, const std::vector<const PodSetResul
   }
   std::vector<std::string> levels(s.levelKeys.begin() + first, s.levelKeys.end());
   out->assign(rs.size(), "null");
-  // ancestors of a leaf per level: walk the CSR bounds (levels are few)
-  for (size_t a = 0; a < which.size(); a++) {
-    const DomainSpan& d = rs[which[a]]->domains;
-    std::string& o = (*out)[which[a]];
-    o.clear();
-    write_v1beta2(
-        o, levels, d.size(), enc.data() + a * size_t(nl), same[a],
-        [&](size_t j, size_t k) -> std::string_view {
-          const auto& lv = s.values[L - 1][size_t(d[j].leaf)];
-          return lv[size_t(first) + k];
-        },
-        [&](size_t j) { return d[j].count; });
+  // The strings are the host's share (Go would allocate them too): independent
+  // per assignment, so large batches are split over threads by domain count.
+  auto write_range = [&](size_t a0, size_t a1) {
+    for (size_t a = a0; a < a1; a++) {
+      const DomainSpan& d = rs[which[a]]->domains;
+      std::string& o = (*out)[which[a]];
+      o.clear();
+      o.reserve(d.size() * (levels.size() * 24 + 8) + 64);
+      write_v1beta2(
+          o, levels, d.size(), enc.data() + a * size_t(nl), same[a],
+          [&](size_t j, size_t k) -> std::string_view {
+            const auto& lv = s.values[L - 1][size_t(d[j].leaf)];
+            return lv[size_t(first) + k];
+          },
+          [&](size_t j) { return d[j].count; });
+    }
+  };
+  const size_t total = size_t(off.back());
+  const size_t nthreads = std::min<size_t>({8, std::max<unsigned>(1, std::thread::hardware_concurrency()),
+                                            total / 8192 + 1, which.size()});
+  if (nthreads <= 1) {
+    write_range(0, which.size());
+    return 0;
   }
+  std::vector<std::thread> pool;
+  size_t a0 = 0;
+  for (size_t t = 0; t < nthreads && a0 < which.size(); t++) {
+    const size_t goal = total * (t + 1) / nthreads;  // domain-balanced cut
+    size_t a1 = a0 + 1;
+    while (a1 < which.size() && size_t(off[a1]) < goal) a1++;
+    if (t + 1 == nthreads) a1 = which.size();
+    pool.emplace_back(write_range, a0, a1);
+    a0 = a1;
+  }
+  for (auto& th : pool) th.join();
   return 0;
 }
 

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
-    "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits",
+    "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits", "kueue_tas_host_preemption_search",
     "kueue_tas_encode_v1beta2", "kueue_tas_snapshot_load_names", "kueue_tas_encode_v1beta2_leaves",
     "kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from", "kueue_tas_host_find_v1beta2",
     "kueue_tas_host_v1beta2_last",

@@ -25,6 +25,6 @@ cp "$ROOT/include/kueue_tas.h" "$OUT/src/"
 cp "$CSRC/tas_device.hip" "$OUT/src/tas_device.cpp"
 sed 's#"../../include/kueue_tas.h"#"kueue_tas.h"#' "$CSRC/tas_host.cpp" > "$OUT/src/tas_host.cpp"
 CXXFLAGS="${CXXFLAGS:--O1 -g}"
-g++ -std=c++17 $CXXFLAGS -fPIC -shared -I"$HERE" -I"$OUT/src" \
+g++ -std=c++17 $CXXFLAGS -fPIC -shared -pthread -I"$HERE" -I"$OUT/src" \
   "$OUT/src/tas_device.cpp" "$OUT/src/tas_host.cpp" "$HERE/hip_emu.cpp" -o "$OUT/libkueue_tas_emu.so"
 echo "$OUT/libkueue_tas_emu.so"
