@@ -175,6 +175,15 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* ctx, const kueue_tas_snapshot_desc* d
 int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* ctx, const kueue_tas_delta* deltas, size_t n,
                                     const uint32_t* usage_present_or_null);
 
+/* Replace the free-capacity rows of n leaves (rows [n][R] int64 in column
+ * order, free_present [n] presence bitmasks): the device side of a non-TAS
+ * pod event (nonTasUsageCache.update/delete, tas_non_tas_pod_cache.go:46-87),
+ * whose leaf the host recomputes as allocatable - non-TAS usage
+ * (TASFlavorCache.snapshot, tas_flavor.go:124-137) instead of rebuilding the
+ * snapshot.  Leaves must be distinct. */
+int kueue_tas_snapshot_set_free(kueue_tas_ctx* ctx, const int32_t* leaves, size_t n, const int64_t* rows,
+                                const uint32_t* free_present);
+
 /* Evaluate n requests against the resident snapshot.
  *  taint_table:   int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
  *  assumed:       overlay records referenced by reqs[i].assumed_begin/end
@@ -371,6 +380,14 @@ int kueue_tas_host_internal_from(kueue_tas_host* h, const char* v1beta2_json, ch
 int kueue_tas_host_find_v1beta2(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json);
 int kueue_tas_host_v1beta2_last(kueue_tas_host* h, char** out_json);
 int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits);
+
+/* Non-TAS pod events on the resident snapshot, in order: JSON array of pods
+ * as in the snapshot document ({"namespace","name","nodeName","phase",
+ * "requests"}; phase Succeeded/Failed or "delete": true removes the pod),
+ * nonTasUsageCache.update/delete (tas_non_tas_pod_cache.go:46-116).  Only
+ * the touched leaves are recomputed and replaced on the device
+ * (kueue_tas_snapshot_set_free) — no snapshot rebuild. */
+int kueue_tas_host_update_pods(kueue_tas_host* h, const char* pods_json);
 
 /* Batched preemption search: the TAS part of preemption's `minimal`
  * (pkg/scheduler/preemption/preemption.go:307-345; workloadFits :614-625 with

@@ -164,6 +164,7 @@ struct kueue_tas_ctx {
   int32_t* res_stats_h = nullptr;
   DevBuf<uint64_t> d_scratch;
   DevBuf<kueue_tas_delta> d_deltas;
+  DevBuf<uint8_t> d_setfree;  // set_free: leaves | rows | presence
   DevBuf<uint8_t> d_fits;  // kueue_tas_fits: requests | terms | results
   // v1beta2 encoder: parent map (leaf mode), resident names, per-call buffers
   DevBuf<int32_t> d_parent;
@@ -274,6 +275,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->h_res.release();
   c->d_scratch.release();
   c->d_deltas.release();
+  c->d_setfree.release();
   c->d_fits.release();
   c->d_fill_lim.release();
   c->d_parent.release();
@@ -557,6 +559,32 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
   if (usage_present_or_null)
     HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, usage_present_or_null, size_t(c->snap.N) * 4, hipMemcpyHostToDevice,
                              c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_set_free(kueue_tas_ctx* c, const int32_t* leaves, size_t n, const int64_t* rows,
+                                const uint32_t* free_present) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (n == 0) return KUEUE_TAS_OK;
+  if (!leaves || !rows || !free_present) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "set_free leaf out of range");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t R = size_t(c->snap.R);
+  const size_t rows_off = (n * 4 + 7) / 8 * 8;
+  const size_t pres_off = rows_off + n * R * 8;
+  HIPCHK(c, c->d_setfree.ensure(pres_off + n * 4));
+  uint8_t* d = c->d_setfree.p;
+  HIPCHK(c, hipMemcpyAsync(d, leaves, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d + rows_off, rows, n * R * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d + pres_off, free_present, n * 4, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(set_free_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->d_free.p,
+                     c->d_free_present.p, c->snap.N, c->snap.R, reinterpret_cast<const int32_t*>(d),
+                     reinterpret_cast<const int64_t*>(d + rows_off), reinterpret_cast<const uint32_t*>(d + pres_off),
+                     int(n));
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KUEUE_TAS_OK;
 }

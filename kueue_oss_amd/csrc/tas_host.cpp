@@ -220,6 +220,13 @@ class FlavorSnapshot {
   std::unordered_map<std::string, int32_t> leafById;
   std::vector<const NodeInfo*> leafNode;
   std::vector<Requests> freeCap, tasUsage;
+  // non-TAS pod cache mirror (tas_non_tas_pod_cache.go:30-120), kept so pod
+  // events update leaves in place: allocatable sum and member nodes per leaf
+  std::vector<Requests> leafAlloc;
+  std::vector<std::vector<std::string>> leafNodeNames;
+  std::unordered_map<std::string, std::string> nodeToLeaf;
+  std::map<std::string, std::pair<std::string, Requests>> podUsage;
+  std::map<std::string, Requests> nodeUsage;
   std::vector<std::vector<int32_t>> idRank;  // [l][i]
   // columns / profiles / labels
   std::vector<std::string> cols;
@@ -308,7 +315,7 @@ class FlavorSnapshot {
     };
     std::vector<LeafTmp> tmp;
     std::unordered_map<std::string, int32_t> tmpById;
-    std::unordered_map<std::string, std::string> nodeToLeaf;
+    nodeToLeaf.clear();
     for (auto& ni : nodes) {
       std::vector<std::string> lv;
       for (auto& k : levelKeys) {
@@ -378,6 +385,9 @@ class FlavorSnapshot {
       leafNode[i] = t.node;
       freeCap[i] = t.cap;
     }
+    leafAlloc = freeCap;
+    leafNodeNames.assign(N, {});
+    for (auto& kv : nodeToLeaf) leafNodeNames[leafById[kv.second]].push_back(kv.first);
     // DomainID ranks per level (multiLayerNotFitMessage tie-break)
     idRank.assign(L, {});
     for (int l = 0; l < L; l++) {
@@ -411,32 +421,9 @@ class FlavorSnapshot {
       if (it != leafById.end()) req_add(tasUsage[it->second], kv.second);
     }
     // non-TAS pods (tas_non_tas_pod_cache.go:46-120)
-    std::map<std::string, std::pair<std::string, Requests>> podUsage;
-    std::map<std::string, Requests> nodeUsage;
-    auto remove_usage = [&](const std::string& node, const Requests& u) {
-      auto it = nodeUsage.find(node);
-      if (it == nodeUsage.end()) return;
-      req_sub(it->second, u);
-      it->second["pods"] = sub64(it->second["pods"], 1);
-      if (it->second["pods"] <= 0) nodeUsage.erase(it);
-    };
-    for (auto& p : c["pods"].items) {
-      std::string key = p["namespace"].s() + "/" + p["name"].s();
-      const std::string& phase = p["phase"].s();
-      auto old = podUsage.find(key);
-      if (old != podUsage.end()) remove_usage(old->second.first, old->second.second);
-      if (phase == "Succeeded" || phase == "Failed") {
-        podUsage.erase(key);
-        continue;
-      }
-      Requests r;
-      for (auto& kv : p["requests"].fields) r[kv.first] = kv.second.i64();
-      const std::string& node = p["nodeName"].s();
-      podUsage[key] = {node, r};
-      Requests& nu = nodeUsage[node];
-      req_add(nu, r);
-      nu["pods"] = add64(nu["pods"], 1);
-    }
+    podUsage.clear();
+    nodeUsage.clear();
+    for (auto& p : c["pods"].items) apply_pod(p, nullptr);
     for (auto& kv : nodeUsage) {
       auto it = nodeToLeaf.find(kv.first);
       if (it != nodeToLeaf.end()) req_sub(freeCap[leafById[it->second]], kv.second);
@@ -492,6 +479,82 @@ class FlavorSnapshot {
       }
     }
     if (profiles.empty()) profiles.push_back({});
+  }
+
+  // nonTasUsageCache.update (tas_non_tas_pod_cache.go:46-73): a terminated
+  // pod leaves the cache, any other replaces its previous entry; per-node
+  // totals gain pods:1 per pod and are dropped at pods <= 0 (removeNodeUsage
+  // :101-116), keeping zero-valued keys otherwise (Requests.Sub).
+  // {"delete": true} is nonTasUsageCache.delete (:76-83).
+  void apply_pod(const kjson::Node& p, std::set<std::string>* touched) {
+    const std::string key = p["namespace"].s() + "/" + p["name"].s();
+    const std::string& phase = p["phase"].s();
+    auto remove_usage = [&](const std::string& node, const Requests& u) {
+      if (touched) touched->insert(node);
+      auto it = nodeUsage.find(node);
+      if (it == nodeUsage.end()) return;
+      req_sub(it->second, u);
+      it->second["pods"] = sub64(it->second["pods"], 1);
+      if (it->second["pods"] <= 0) nodeUsage.erase(it);
+    };
+    auto old = podUsage.find(key);
+    if (old != podUsage.end()) remove_usage(old->second.first, old->second.second);
+    if (phase == "Succeeded" || phase == "Failed" || p["delete"].b()) {
+      podUsage.erase(key);
+      return;
+    }
+    Requests r;
+    for (auto& kv : p["requests"].fields) r[kv.first] = kv.second.i64();
+    const std::string& node = p["nodeName"].s();
+    podUsage[key] = {node, r};
+    Requests& nu = nodeUsage[node];
+    req_add(nu, r);
+    nu["pods"] = add64(nu["pods"], 1);
+    if (touched) touched->insert(node);
+  }
+  // Pod events on a built snapshot: the touched leaves' freeCapacity is
+  // recomputed as allocatable - Σ non-TAS usage of their nodes
+  // (TASFlavorCache.snapshot :124-137) and replaced on the device; a resource
+  // with no column yet re-columns (the next evaluation reloads).
+  int update_pods(const kjson::Node& arr) {
+    std::set<std::string> touched;
+    for (auto& p : arr.items) apply_pod(p, &touched);
+    std::set<int32_t> leaves;
+    for (auto& n : touched) {
+      auto it = nodeToLeaf.find(n);
+      if (it != nodeToLeaf.end()) leaves.insert(leafById[it->second]);
+    }
+    bool new_col = false;
+    for (int32_t l : leaves) {
+      Requests f = leafAlloc[size_t(l)];
+      for (auto& n : leafNodeNames[size_t(l)]) {
+        auto u = nodeUsage.find(n);
+        if (u != nodeUsage.end()) req_sub(f, u->second);
+      }
+      for (auto& kv : f) new_col |= !colByName.count(kv.first);
+      freeCap[size_t(l)] = std::move(f);
+    }
+    if (new_col) {
+      std::set<std::string> names(cols.begin(), cols.end());
+      for (int32_t l : leaves)
+        for (auto& kv : freeCap[size_t(l)]) names.insert(kv.first);
+      set_columns(names);
+      return 0;
+    }
+    if (dirty || !ctx || leaves.empty()) return 0;
+    const size_t R = cols.size();
+    std::vector<int32_t> ls(leaves.begin(), leaves.end());
+    std::vector<int64_t> rows(ls.size() * R, 0);
+    std::vector<uint32_t> pres(ls.size(), 0);
+    for (size_t i = 0; i < ls.size(); i++)
+      for (auto& kv : freeCap[size_t(ls[i])]) {
+        const int c = colByName[kv.first];
+        rows[i * R + size_t(c)] = kv.second;
+        pres[i] |= 1u << c;
+      }
+    int rc = kueue_tas_snapshot_set_free(ctx, ls.data(), ls.size(), rows.data(), pres.data());
+    if (rc) err = std::string("set free: ") + kueue_tas_last_error(ctx);
+    return rc;
   }
 
   void set_columns(const std::set<std::string>& names) {
@@ -1770,6 +1833,18 @@ int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
     int rc = h->snap->update_usage(FlavorSnapshot::parse_usage(kjson::parse(usage_json)), add != 0);
+    if (rc) h->err = h->snap->err;
+    return rc;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_update_pods(kueue_tas_host* h, const char* pods_json) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    int rc = h->snap->update_pods(kjson::parse(pods_json));
     if (rc) h->err = h->snap->err;
     return rc;
   } catch (const std::exception& e) {

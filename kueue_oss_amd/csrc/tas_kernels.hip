@@ -3388,6 +3388,19 @@ __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present,
   atomicOr(&usage_present[x.leaf], 1u << x.col);
 }
 
+// Leaf free-capacity rows replaced after non-TAS pod events
+// (nonTasUsageCache.update/delete, tas_non_tas_pod_cache.go:46-87, folded in by
+// TASFlavorCache.snapshot, tas_flavor.go:133-137): one thread per (leaf, column),
+// column-major stores so a wave writes one column of 64 leaves.
+__global__ void set_free_kernel(int64_t* free_cap, uint32_t* free_present, int N, int R, const int32_t* leaves,
+                                const int64_t* rows, const uint32_t* present, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int leaf = leaves[i];
+  for (int col = 0; col < R; col++) free_cap[int64_t(col) * N + leaf] = rows[int64_t(i) * R + col];
+  free_present[leaf] = present[i];
+}
+
 // ---- v1beta2 compact encoding (pkg/util/tas/tas_assignment.go:135-259) ----
 // fillSingleCompactSliceValues walks the values keeping a running prefix and
 // suffix of value 0; by induction the prefix after value i is value0's prefix
