@@ -716,18 +716,22 @@ class FlavorSnapshot {
   // free - (used - x) - assumed == free - used - (assumed - x) in Go's
   // wrapping int64, and both Subs create the key (requests.go:90-94).
   // Unknown domains are skipped like removeTASUsage does.
-  void add_removal(const std::vector<DomainUsage>& us, std::map<int32_t, std::map<int32_t, int64_t>>& o) const {
+  std::vector<kueue_tas_assumed> removal(const std::vector<DomainUsage>& us) const {
+    std::map<std::pair<int32_t, int32_t>, int64_t> o;
     for (auto& u : us) {
       auto it = leafById.find(u.id);
       if (it == leafById.end()) continue;
-      auto& row = o[it->second];
       for (auto& kv : u.single) {
-        int64_t& slot = row[colByName.at(kv.first)];
+        int64_t& slot = o[{it->second, colByName.at(kv.first)}];
         slot = sub64(slot, mul64(kv.second, u.count));
       }
-      int64_t& pods = row[colByName.at("pods")];
+      int64_t& pods = o[{it->second, colByName.at("pods")}];
       pods = sub64(pods, u.count);
     }
+    std::vector<kueue_tas_assumed> r;
+    r.reserve(o.size());
+    for (auto& kv : o) r.push_back({kv.first.first, kv.first.second, kv.second});
+    return r;
   }
   // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), on the device.
   int fits(const std::vector<DomainUsage>& us, bool* out) {
@@ -1157,19 +1161,37 @@ struct Evaluator {
       }
       q.taint_table = it->second;
       q.assumed_begin = int32_t(as.size());
-      for (auto& lv : assumedBy[w])
-        for (auto& cv : lv.second) as.push_back({lv.first, cv.first, cv.second});
+      if (base && !(*base)[w].empty()) {  // merge the base overlay with the group's assumed usage
+        const Overlay& b = (*base)[w];
+        size_t k = 0;
+        for (auto& lv : assumedBy[w])
+          for (auto& cv : lv.second) {
+            while (k < b.size() && (b[k].leaf < lv.first || (b[k].leaf == lv.first && b[k].col < cv.first)))
+              as.push_back(b[k++]);
+            if (k < b.size() && b[k].leaf == lv.first && b[k].col == cv.first)
+              as.push_back({lv.first, cv.first, add64(b[k++].value, cv.second)});
+            else
+              as.push_back({lv.first, cv.first, cv.second});
+          }
+        as.insert(as.end(), b.begin() + int64_t(k), b.end());
+      } else {
+        for (auto& lv : assumedBy[w])
+          for (auto& cv : lv.second) as.push_back({lv.first, cv.first, cv.second});
+      }
       q.assumed_end = int32_t(as.size());
       bt.emplace_back(w, &g);
     }
   }
 
-  // base: optional per-workload starting overlay (leaf -> column -> value
-  // subtracted from the remaining capacity), e.g. the negated usage of the
-  // workloads a preemption candidate set removes (SimulateUsageRemoval).
-  using Overlay = std::map<int32_t, std::map<int32_t, int64_t>>;
+  // base: optional per-workload starting overlay, records sorted by (leaf,
+  // column) with distinct keys, subtracted from the remaining capacity: the
+  // negated usage of the workloads a preemption candidate set removes
+  // (SimulateUsageRemoval).
+  using Overlay = std::vector<kueue_tas_assumed>;
+  const std::vector<Overlay>* base = nullptr;
   int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results,
-          bool precompiled = false, const std::vector<Overlay>* base = nullptr) {
+          bool precompiled = false, const std::vector<Overlay>* base_overlay = nullptr) {
+    base = base_overlay;
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     for (auto& v : stage_ms) v = 0;
     for (auto& v : dev_host_ms) v = 0;
@@ -1192,7 +1214,7 @@ struct Evaluator {
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
     std::vector<char> done(wls.size(), 0);
-    std::vector<Overlay> assumedBy = base ? *base : std::vector<Overlay>(wls.size());
+    std::vector<std::map<int32_t, std::map<int32_t, int64_t>>> assumedBy(wls.size());
     size_t maxGroups = 0;
     for (auto& wl : wls) maxGroups = std::max(maxGroups, wl.groups.size());
     const size_t T = snap->taintStrings.size();
@@ -1892,29 +1914,48 @@ static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, cons
       if (!r.reason.empty()) return false;  // TASAssignmentsResult.Failure() (:384-391)
     return true;
   };
-  // one evaluation per removal set; every Workload parses its own PodSets
-  auto eval_sets = [&](const std::vector<std::vector<size_t>>& sets, std::vector<char>* fit) -> int {
-    std::vector<Workload> wls(sets.size());
-    std::vector<Overlay> base(sets.size());
-    for (size_t i = 0; i < sets.size(); i++) wls[i].podsets = parse_podsets(podsets);
-    // settle the column set first: the overlays index columns
-    for (auto& w : wls) s.ensure_columns_for(w.podsets);
-    for (size_t i = 0; i < sets.size(); i++)
-      for (size_t c : sets[i]) s.add_removal(cu[c], base[i]);
+  // settle the column set first (PodSets may add columns): overlays index columns
+  {
+    std::vector<Workload> probe(1);
+    probe[0].podsets = parse_podsets(podsets);
+    s.ensure_columns_for(probe[0].podsets);
+  }
+  std::vector<Overlay> rem(k);
+  for (size_t c = 0; c < k; c++) rem[c] = s.removal(cu[c]);
+  auto merge = [](const Overlay& x, const Overlay& y) {  // sorted (leaf, col) union, values added
+    Overlay r;
+    r.reserve(x.size() + y.size());
+    size_t i = 0, j = 0;
+    while (i < x.size() || j < y.size()) {
+      if (j == y.size() || (i < x.size() && (x[i].leaf < y[j].leaf || (x[i].leaf == y[j].leaf && x[i].col < y[j].col)))) {
+        r.push_back(x[i++]);
+      } else if (i == x.size() || y[j].leaf < x[i].leaf || (y[j].leaf == x[i].leaf && y[j].col < x[i].col)) {
+        r.push_back(y[j++]);
+      } else {
+        r.push_back({x[i].leaf, x[i].col, add64(x[i].value, y[j].value)});
+        i++, j++;
+      }
+    }
+    return r;
+  };
+  // one evaluation per overlay; every Workload parses its own PodSets
+  auto eval_overlays = [&](const std::vector<Overlay>& base, std::vector<char>* fit) -> int {
+    std::vector<Workload> wls(base.size());
+    for (auto& w : wls) w.podsets = parse_podsets(podsets);
     Evaluator ev{&s};
     std::vector<std::vector<PodSetResult>> results;
     int rc = ev.run(wls, false, &results, false, &base);
     if (rc) return rc;
-    fit->resize(sets.size());
-    for (size_t i = 0; i < sets.size(); i++) (*fit)[i] = fits_all(results[i]) ? 1 : 0;
+    fit->resize(base.size());
+    for (size_t i = 0; i < base.size(); i++) (*fit)[i] = fits_all(results[i]) ? 1 : 0;
     return 0;
   };
-  std::vector<std::vector<size_t>> prefixes(k);
-  for (size_t i = 0; i < k; i++)
-    for (size_t c = 0; c <= i; c++) prefixes[i].push_back(c);
+  std::vector<Overlay> prefixes(k);
+  for (size_t i = 0; i < k; i++) prefixes[i] = i ? merge(prefixes[i - 1], rem[i]) : rem[0];
   std::vector<char> pfit;
-  int rc = k ? eval_sets(prefixes, &pfit) : 0;
+  int rc = k ? eval_overlays(prefixes, &pfit) : 0;
   if (rc) return rc;
+  prefixes.clear();
   long first = -1;
   for (size_t i = 0; i < k; i++)
     if (pfit[i]) {
@@ -1924,14 +1965,14 @@ static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, cons
   std::vector<size_t> targets;
   int64_t fill_evals = 0;
   if (first >= 0) {
-    targets = prefixes[size_t(first)];
+    for (size_t c = 0; c <= size_t(first); c++) targets.push_back(c);
     for (long i = long(targets.size()) - 2; i >= 0; i--) {
       // AddWorkload(targets[i]): the removal set is every other target
-      std::vector<size_t> set;
+      Overlay set;
       for (size_t j = 0; j < targets.size(); j++)
-        if (long(j) != i) set.push_back(targets[j]);
+        if (long(j) != i) set = merge(set, rem[targets[j]]);
       std::vector<char> f;
-      rc = eval_sets({set}, &f);
+      rc = eval_overlays({set}, &f);
       if (rc) return rc;
       fill_evals++;
       if (f[0]) {
