@@ -1938,6 +1938,8 @@ static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, cons
     }
     return r;
   };
+  double eval_ms[4] = {}, dev_ms[6] = {};
+  const double t0 = now_ms();
   // one evaluation per overlay; every Workload parses its own PodSets
   auto eval_overlays = [&](const std::vector<Overlay>& base, std::vector<char>* fit) -> int {
     std::vector<Workload> wls(base.size());
@@ -1946,6 +1948,8 @@ static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, cons
     std::vector<std::vector<PodSetResult>> results;
     int rc = ev.run(wls, false, &results, false, &base);
     if (rc) return rc;
+    for (int q = 0; q < 4; q++) eval_ms[q] += ev.host_ms[q];
+    for (int q = 0; q < 6; q++) dev_ms[q] += ev.dev_host_ms[q];
     fit->resize(base.size());
     for (size_t i = 0; i < base.size(); i++) (*fit)[i] = fits_all(results[i]) ? 1 : 0;
     return 0;
@@ -1991,7 +1995,14 @@ static int preemption_search(kueue_tas_host* h, const kjson::Node& podsets, cons
     for (size_t j = 0; j < targets.size(); j++) *out += (j ? "," : "") + std::to_string(targets[j]);
     *out += "]";
   }
-  *out += ",\"fillBackEvals\":" + std::to_string(fill_evals) + "}";
+  *out += ",\"fillBackEvals\":" + std::to_string(fill_evals);
+  // host profile: [prepare, eval calls, decode, total] of the Evaluator runs,
+  // the device layer's [compile, classes, enqueue, wait, pack, copy], and the whole search
+  *out += ",\"profileMs\":{\"evaluator\":[";
+  for (int q = 0; q < 4; q++) *out += (q ? "," : "") + std::to_string(eval_ms[q]);
+  *out += "],\"device\":[";
+  for (int q = 0; q < 6; q++) *out += (q ? "," : "") + std::to_string(dev_ms[q]);
+  *out += "],\"search\":" + std::to_string(now_ms() - t0) + "}}";
   return 0;
 }
 

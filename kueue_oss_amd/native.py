@@ -200,9 +200,10 @@ class TASFlavorSnapshot:
         """TAS part of preemption's `minimal` (pkg/scheduler/preemption/
         preemption.go:307-345): every candidate prefix evaluated in one device
         batch under a removal overlay, then fillBackWorkloads.  ``candidates``
-        is a list of usage-record lists (the candidates' admitted usage)."""
-        return self._json_call(self._lib.kueue_tas_host_preemption_search, podsets,
-                               json.dumps(candidates).encode())
+        is a list of usage-record lists (the candidates' admitted usage), or
+        that list already JSON-encoded (bytes)."""
+        enc = candidates if isinstance(candidates, bytes) else json.dumps(candidates).encode()
+        return self._json_call(self._lib.kueue_tas_host_preemption_search, podsets, enc)
 
     # ---- v1beta2 wire format (pkg/util/tas/tas_assignment.go) ----
     def _json_call(self, fn, payload, *extra):
