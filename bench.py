@@ -217,7 +217,17 @@ def main():
         snap.update_pods(evs)
         snap.update_pods([dict(e, delete=True) for e in evs])
         pod_ms = (time.perf_counter() - t0) / 2 * 1e3
+        # 64 in-place node updates (allocatable change), then restored
+        import copy
+        upd = [copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)]
+        for nd in upd:
+            nd["allocatable"]["cpu"] = nd["allocatable"].get("cpu", 0) - 1000
+        t0 = time.perf_counter()
+        rebuilt = snap.update_nodes(upd)
+        node_ms = (time.perf_counter() - t0) * 1e3
+        snap.update_nodes([copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)])
         extras = {"pod_events_ms_per_64": round(pod_ms, 3),
+                  "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,
                   "preemption_search_profile_ms": pr["profileMs"],
                   "preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),
                   "preemption_first_fit": pr["firstFit"], "preemption_fill_back_evals": pr["fillBackEvals"],

@@ -184,6 +184,13 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* ctx, const kueue_tas_delta* d
 int kueue_tas_snapshot_set_free(kueue_tas_ctx* ctx, const int32_t* leaves, size_t n, const int64_t* rows,
                                 const uint32_t* free_present);
 
+/* Replace the taint profile (profiles [n]) and selector label ids
+ * (labels [n][K], NULL when the snapshot has no label columns) of n distinct
+ * hostname leaves: the device side of an in-place node update
+ * (nodesCache.sync, tas_nodes_cache.go:38-50). */
+int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* ctx, const int32_t* leaves, size_t n, const int32_t* profiles,
+                                      const int32_t* labels);
+
 /* Evaluate n requests against the resident snapshot.
  *  taint_table:   int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
  *  assumed:       overlay records referenced by reqs[i].assumed_begin/end
@@ -388,6 +395,16 @@ int kueue_tas_host_fits(kueue_tas_host* h, const char* usage_json, int32_t* fits
  * the touched leaves are recomputed and replaced on the device
  * (kueue_tas_snapshot_set_free) — no snapshot rebuild. */
 int kueue_tas_host_update_pods(kueue_tas_host* h, const char* pods_json);
+
+/* Node events, in order: JSON array of node objects as in the snapshot
+ * document (a node with the same name replaces it; not Ready or
+ * unschedulable removes it; nodesCache.sync, tas_nodes_cache.go:38-72).
+ * Updates that keep a node in place in the topology with an existing taint
+ * profile and existing label values (allocatable, taints, labels) are
+ * applied to the touched leaves only (kueue_tas_snapshot_set_free +
+ * kueue_tas_snapshot_set_leaf_attrs); any other event rebuilds the snapshot
+ * from the document and every event since (*rebuilt = 1; may be NULL). */
+int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32_t* rebuilt);
 
 /* Batched preemption search: the TAS part of preemption's `minimal`
  * (pkg/scheduler/preemption/preemption.go:307-345; workloadFits :614-625 with

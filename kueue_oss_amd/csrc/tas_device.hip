@@ -589,6 +589,36 @@ int kueue_tas_snapshot_set_free(kueue_tas_ctx* c, const int32_t* leaves, size_t 
   return KUEUE_TAS_OK;
 }
 
+int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* c, const int32_t* leaves, size_t n, const int32_t* profiles,
+                                      const int32_t* labels) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (n == 0) return KUEUE_TAS_OK;
+  if (!leaves || !profiles) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  const size_t K = size_t(c->snap.K);
+  if (K && !labels) return fail(c, KUEUE_TAS_EINVAL, "labels required (snapshot has label columns)");
+  if (!c->snap.taint_profile) return fail(c, KUEUE_TAS_EINVAL, "snapshot has no taint profiles");
+  for (size_t i = 0; i < n; i++) {
+    if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "leaf out of range");
+    if (profiles[i] < 0) return fail(c, KUEUE_TAS_EINVAL, "negative taint profile");
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  for (size_t i = 0; i < n; i++) c->num_profiles = std::max(c->num_profiles, profiles[i] + 1);
+  const size_t prof_off = n * 4, lab_off = 2 * n * 4;
+  HIPCHK(c, c->d_setfree.ensure(lab_off + n * K * 4));
+  uint8_t* d = c->d_setfree.p;
+  HIPCHK(c, hipMemcpyAsync(d, leaves, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d + prof_off, profiles, n * 4, hipMemcpyHostToDevice, c->stream));
+  if (K) HIPCHK(c, hipMemcpyAsync(d + lab_off, labels, n * K * 4, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(set_leaf_attrs_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream,
+                     c->d_taint_profile.p, K ? c->d_labels.p : nullptr, c->snap.N, c->snap.K,
+                     reinterpret_cast<const int32_t*>(d), reinterpret_cast<const int32_t*>(d + prof_off),
+                     reinterpret_cast<const int32_t*>(d + lab_off), int(n));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
 int kueue_tas_fits(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
                    size_t num_terms, int32_t* fits) {
   if (!c) return KUEUE_TAS_EINVAL;

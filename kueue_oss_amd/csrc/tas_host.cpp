@@ -240,6 +240,8 @@ class FlavorSnapshot {
   std::vector<std::map<std::string, int32_t>> labelDict;
   std::vector<int32_t> labelValues;  // [K][N]
   std::vector<NodeInfo> nodes;
+  std::map<std::string, std::string> flavorLabels;
+  std::unordered_map<std::string, size_t> nodeIdx;  // node name -> nodes[]
 
   kueue_tas_ctx* ctx = nullptr;
   bool dirty = true;
@@ -267,7 +269,6 @@ class FlavorSnapshot {
     if (auto p = fg.find("TASMultiLayerTopology")) gates.multiLayer = p->b();
     if (auto p = fg.find("TASBalancedPlacement")) gates.balanced = p->b();
     if (auto p = fg.find("ElasticJobsViaWorkloadSlicesWithTAS")) gates.elastic = p->b();
-    std::map<std::string, std::string> flavorLabels;
     for (auto& kv : c["nodeLabels"].fields) flavorLabels[kv.first] = kv.second.s();
 
     // nodesCache.sync (Ready && !Unschedulable) keyed by name, then find (NodeMatchesFlavor)
@@ -386,6 +387,8 @@ class FlavorSnapshot {
       freeCap[i] = t.cap;
     }
     leafAlloc = freeCap;
+    nodeIdx.clear();
+    for (size_t i = 0; i < nodes.size(); i++) nodeIdx[nodes[i].name] = i;
     leafNodeNames.assign(N, {});
     for (auto& kv : nodeToLeaf) leafNodeNames[leafById[kv.second]].push_back(kv.first);
     // DomainID ranks per level (multiLayerNotFitMessage tie-break)
@@ -524,6 +527,76 @@ class FlavorSnapshot {
       auto it = nodeToLeaf.find(n);
       if (it != nodeToLeaf.end()) leaves.insert(leafById[it->second]);
     }
+    return push_leaves(leaves, false);
+  }
+
+  // ---- node events (nodesCache.sync, tas_nodes_cache.go:38-72) ----
+  // An update of a node already in the snapshot that keeps it Ready,
+  // schedulable, matching the flavor and at the same topology position, whose
+  // taint list is an existing profile and whose labels use existing label
+  // keys and values, changes only leaf attributes: allocatable (freeCapacity,
+  // addCapacity :243-248), the taint profile and the selector label columns.
+  // Those are applied in place; anything else returns false (the caller
+  // rebuilds the snapshot, as the reference does every cycle).
+  bool node_event_in_place(const kjson::Node& n, std::set<int32_t>* touched) {
+    auto ix = nodeIdx.find(n["name"].s());
+    if (ix == nodeIdx.end()) return false;
+    bool ready = false;
+    for (auto& cond : n["conditions"].items)
+      if (cond["type"].s() == "Ready") {
+        ready = cond["status"].s() == "True";
+        break;
+      }
+    if (!ready || n["unschedulable"].b()) return false;
+    NodeInfo ni;
+    ni.name = n["name"].s();
+    for (auto& kv : n["labels"].fields) ni.labels[kv.first] = kv.second.s();
+    for (auto& kv : flavorLabels) {
+      auto it = ni.labels.find(kv.first);
+      if ((it == ni.labels.end() ? std::string() : it->second) != kv.second) return false;
+    }
+    NodeInfo& cur = nodes[ix->second];
+    for (auto& l : levelKeys) {
+      auto a = ni.labels.find(l), b = cur.labels.find(l);
+      if (a == ni.labels.end() || b == cur.labels.end() || a->second != b->second) return false;
+    }
+    for (auto& t : n["taints"].items) ni.taints.push_back({t["key"].s(), t["value"].s(), t["effect"].s()});
+    for (auto& kv : n["allocatable"].fields) ni.allocatable[kv.first] = kv.second.i64();
+    const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
+    int32_t prof = leafProfile[size_t(leaf)];
+    if (lowestIsHostname) {
+      std::vector<Taint> ts;
+      for (auto& t : ni.taints)
+        if (t.effect == "NoSchedule" || t.effect == "NoExecute") ts.push_back(t);
+      auto pit = std::find(profiles.begin(), profiles.end(), ts);
+      if (pit == profiles.end()) return false;
+      prof = int32_t(pit - profiles.begin());
+      for (auto& kv : ni.labels) {
+        auto c = labelCol.find(kv.first);
+        if (c == labelCol.end() || !labelDict[size_t(c->second)].count(kv.second)) return false;
+      }
+    }
+    // in place
+    cur.labels = std::move(ni.labels);
+    cur.taints = std::move(ni.taints);
+    cur.allocatable = std::move(ni.allocatable);
+    leafProfile[size_t(leaf)] = prof;
+    if (lowestIsHostname) {
+      const size_t N = size_t(this->N());
+      for (size_t k = 0; k < labelKeys.size(); k++) {
+        auto it = cur.labels.find(labelKeys[k]);
+        labelValues[k * N + size_t(leaf)] = it == cur.labels.end() ? 0 : labelDict[k].at(it->second);
+      }
+    }
+    Requests alloc;
+    for (auto& nm : leafNodeNames[size_t(leaf)]) req_add(alloc, nodes[nodeIdx.at(nm)].allocatable);
+    leafAlloc[size_t(leaf)] = std::move(alloc);
+    touched->insert(leaf);
+    return true;
+  }
+  // Pushes touched leaves to the device: free-capacity rows (allocatable -
+  // non-TAS usage) and, with hostname leaves, taint profile + label columns.
+  int push_leaves(const std::set<int32_t>& leaves, bool attrs) {
     bool new_col = false;
     for (int32_t l : leaves) {
       Requests f = leafAlloc[size_t(l)];
@@ -553,7 +626,19 @@ class FlavorSnapshot {
         pres[i] |= 1u << c;
       }
     int rc = kueue_tas_snapshot_set_free(ctx, ls.data(), ls.size(), rows.data(), pres.data());
-    if (rc) err = std::string("set free: ") + kueue_tas_last_error(ctx);
+    if (rc) {
+      err = std::string("set free: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    if (!attrs || !lowestIsHostname) return 0;
+    const size_t K = labelKeys.size(), N = size_t(this->N());
+    std::vector<int32_t> prof(ls.size()), lab(ls.size() * K);
+    for (size_t i = 0; i < ls.size(); i++) {
+      prof[i] = leafProfile[size_t(ls[i])];
+      for (size_t k = 0; k < K; k++) lab[i * K + k] = labelValues[k * N + size_t(ls[i])];
+    }
+    rc = kueue_tas_snapshot_set_leaf_attrs(ctx, ls.data(), ls.size(), prof.data(), K ? lab.data() : nullptr);
+    if (rc) err = std::string("set leaf attrs: ") + kueue_tas_last_error(ctx);
     return rc;
   }
 
@@ -1661,6 +1746,12 @@ struct kueue_tas_host {
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[4] = {0, 0, 0, 0};
+  // what a rebuild replays: the snapshot document, node and pod event
+  // batches (appended to its node and pod lists, which build() consumes as
+  // event streams) and the usage updates applied since
+  std::string doc;
+  std::vector<std::string> node_batches, pod_batches;
+  std::vector<std::pair<std::vector<FlavorSnapshot::DomainUsage>, bool>> usage_log;
 };
 
 extern "C" {
@@ -1670,6 +1761,7 @@ kueue_tas_host* kueue_tas_host_create(const char* snapshot_json, const kueue_tas
   try {
     h->snap = std::make_unique<FlavorSnapshot>();
     if (cfg) h->snap->cfg = *cfg;
+    h->doc = snapshot_json;
     kjson::Node c = kjson::parse(snapshot_json);
     h->snap->build(c);
     if (h->snap->upload()) {
@@ -1854,7 +1946,68 @@ int kueue_tas_host_v1beta2_last(kueue_tas_host* h, char** out_json) {
 int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32_t add) {
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
-    int rc = h->snap->update_usage(FlavorSnapshot::parse_usage(kjson::parse(usage_json)), add != 0);
+    auto us = FlavorSnapshot::parse_usage(kjson::parse(usage_json));
+    int rc = h->snap->update_usage(us, add != 0);
+    if (rc) h->err = h->snap->err;
+    else h->usage_log.emplace_back(std::move(us), add != 0);
+    return rc;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+// Rebuild after a structural node event (a node added, removed, NotReady,
+// cordoned, moved in the topology, or with a new taint profile / label):
+// the reference rebuilds its snapshot every cycle (Cache.Snapshot,
+// snapshot.go:186-191); here the host mirror is rebuilt from the document
+// plus every event since, the usage updates are replayed, the device context
+// is kept and the compiled workloads are recompiled against the new columns.
+static int rebuild(kueue_tas_host* h) {
+  kjson::Node doc = kjson::parse(h->doc.c_str());
+  auto list = [&](const char* key) -> std::vector<kjson::Node>& {
+    for (auto& f : doc.fields)
+      if (f.first == key) {
+        f.second.type = kjson::Node::kArray;
+        return f.second.items;
+      }
+    doc.fields.emplace_back(key, kjson::Node{});
+    doc.fields.back().second.type = kjson::Node::kArray;
+    return doc.fields.back().second.items;
+  };
+  for (auto& b : h->node_batches)
+    for (auto& n : kjson::parse(b.c_str()).items) list("nodes").push_back(n);
+  for (auto& b : h->pod_batches)
+    for (auto& p : kjson::parse(b.c_str()).items) list("pods").push_back(p);
+  auto ns = std::make_unique<FlavorSnapshot>();
+  ns->cfg = h->snap->cfg;
+  ns->build(doc);
+  ns->ctx = h->snap->ctx;  // keep the device context (and its buffers)
+  h->snap->ctx = nullptr;
+  for (auto& u : h->usage_log) ns->update_usage(u.first, u.second);  // host mirror: ns is dirty
+  h->snap = std::move(ns);
+  h->ev.reset();
+  h->last.clear();
+  for (auto& wl : h->compiled) h->snap->ensure_columns_for(wl.podsets);
+  for (auto& wl : h->compiled)
+    for (auto& g : wl.groups) h->snap->compile_group(g, false);
+  return h->snap->upload();
+}
+
+int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32_t* rebuilt) {
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  try {
+    kjson::Node arr = kjson::parse(nodes_json);
+    h->node_batches.emplace_back(nodes_json);
+    std::set<int32_t> touched;
+    bool structural = false;
+    for (auto& n : arr.items)
+      if (!h->snap->node_event_in_place(n, &touched)) {
+        structural = true;
+        break;
+      }
+    if (rebuilt) *rebuilt = structural ? 1 : 0;
+    int rc = structural ? rebuild(h) : h->snap->push_leaves(touched, true);
     if (rc) h->err = h->snap->err;
     return rc;
   } catch (const std::exception& e) {
@@ -1868,6 +2021,7 @@ int kueue_tas_host_update_pods(kueue_tas_host* h, const char* pods_json) {
   try {
     int rc = h->snap->update_pods(kjson::parse(pods_json));
     if (rc) h->err = h->snap->err;
+    else h->pod_batches.emplace_back(pods_json);
     return rc;
   } catch (const std::exception& e) {
     h->err = e.what();

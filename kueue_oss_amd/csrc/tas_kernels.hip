@@ -3401,6 +3401,18 @@ __global__ void set_free_kernel(int64_t* free_cap, uint32_t* free_present, int N
   free_present[leaf] = present[i];
 }
 
+// Leaf taint profile and selector label columns replaced after in-place node
+// updates (nodesCache.sync, tas_nodes_cache.go:38-50).
+__global__ void set_leaf_attrs_kernel(int32_t* taint_profile, int32_t* label_values, int N, int K,
+                                      const int32_t* leaves, const int32_t* profiles, const int32_t* labels, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int leaf = leaves[i];
+  if (taint_profile) taint_profile[leaf] = profiles[i];
+  if (label_values)
+    for (int k = 0; k < K; k++) label_values[int64_t(k) * N + leaf] = labels[int64_t(i) * K + k];
+}
+
 // ---- v1beta2 compact encoding (pkg/util/tas/tas_assignment.go:135-259) ----
 // fillSingleCompactSliceValues walks the values keeping a running prefix and
 // suffix of value 0; by induction the prefix after value i is value0's prefix

@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
     "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits", "kueue_tas_host_preemption_search", "kueue_tas_host_update_pods",
-    "kueue_tas_snapshot_set_free",
+    "kueue_tas_snapshot_set_free", "kueue_tas_snapshot_set_leaf_attrs", "kueue_tas_host_update_nodes",
     "kueue_tas_encode_v1beta2", "kueue_tas_snapshot_load_names", "kueue_tas_encode_v1beta2_leaves",
     "kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from", "kueue_tas_host_find_v1beta2",
     "kueue_tas_host_v1beta2_last",
@@ -117,6 +117,8 @@ def _bind(lib):
     lib.kueue_tas_host_v1beta2_last.restype = c.c_int
     lib.kueue_tas_host_preemption_search.argtypes = [c.c_void_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_preemption_search.restype = c.c_int
+    lib.kueue_tas_host_update_nodes.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
+    lib.kueue_tas_host_update_nodes.restype = c.c_int
     lib.kueue_tas_host_update_pods.argtypes = [c.c_void_p, c.c_char_p]
     lib.kueue_tas_host_update_pods.restype = c.c_int
     lib.kueue_tas_free.argtypes = [c.c_void_p]
@@ -182,6 +184,15 @@ class TASFlavorSnapshot:
         """ClusterQueueSnapshot.RemoveUsage -> updateTASUsage (clusterqueue_snapshot.go:100-119)."""
         if self._lib.kueue_tas_host_update_usage(self._h, json.dumps(records).encode(), 0):
             raise RuntimeError(self._err())
+
+    def update_nodes(self, nodes: list) -> bool:
+        """Node events (nodesCache.sync, tas_nodes_cache.go:38-72): in place when the
+        nodes keep their topology position and existing taint profiles / label values,
+        else a rebuild.  Returns True when the snapshot was rebuilt."""
+        r = ctypes.c_int32()
+        if self._lib.kueue_tas_host_update_nodes(self._h, json.dumps(nodes).encode(), ctypes.byref(r)):
+            raise RuntimeError(self._err())
+        return bool(r.value)
 
     def update_pods(self, pods: list):
         """Non-TAS pod events (nonTasUsageCache.update/delete, tas_non_tas_pod_cache.go:46-116)

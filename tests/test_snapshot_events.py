@@ -1,5 +1,6 @@
-"""Device-resident snapshot maintenance: non-TAS pod
-events applied to a built snapshot in place (nonTasUsageCache.update/delete,
+"""Device-resident snapshot maintenance: node events
+(nodesCache.sync, tas_nodes_cache.go:38-72: in place for attribute updates,
+a rebuild otherwise) and non-TAS pod events applied to a built snapshot in place (nonTasUsageCache.update/delete,
 pkg/cache/scheduler/tas_non_tas_pod_cache.go:46-116, folded into the leaves'
 freeCapacity as TASFlavorCache.snapshot does, tas_flavor.go:124-137) must give
 the same evaluations as the reference's per-cycle rebuild — the oracle built
@@ -42,6 +43,58 @@ def pod_events(rng, case, n):
     return evs
 
 
+def node_events(rng, ref, n):
+    """Random node events against the latest state of every node: allocatable
+    changes (sometimes a new resource), taints copied from another node or
+    new, label value changes, NotReady / cordon, new nodes, topology moves."""
+    latest = {}
+    for nd in ref["nodes"]:
+        latest[nd["name"]] = nd
+    names = list(latest)
+    levels = ref["levels"]
+    evs = []
+    for k in range(n):
+        if not names:
+            break
+        nd = copy.deepcopy(latest[rng.choice(names)])
+        r = rng.random()
+        if r < 0.3:
+            for res in list(nd["allocatable"]):
+                if rng.random() < 0.6:
+                    nd["allocatable"][res] = max(0, nd["allocatable"][res] + rng.choice([-1, 1, 2]) *
+                                                 (1000 if res == "cpu" else GI if res == "memory" else 1))
+            if rng.random() < 0.1:
+                nd["allocatable"]["example.com/new"] = rng.choice([0, 3])
+        elif r < 0.5:
+            other = latest[rng.choice(names)]
+            nd["taints"] = copy.deepcopy(other.get("taints", [])) if rng.random() < 0.8 else \
+                [{"key": f"t{k}", "value": "v", "effect": "NoSchedule"}]
+        elif r < 0.7:
+            key = rng.choice(["zone", "gpu-type"])
+            if rng.random() < 0.2:
+                nd["labels"].pop(key, None)
+            else:
+                nd["labels"][key] = rng.choice(["a", "b", "t1", "t2"]) if rng.random() < 0.9 else f"new{k}"
+        elif r < 0.8:
+            if rng.random() < 0.5:
+                nd["conditions"] = [{"type": "Ready", "status": "False"}]
+            else:
+                nd["unschedulable"] = True
+        elif r < 0.9:
+            nd["name"] = f"new-node-{k}-{rng.randint(0, 1 << 20)}"
+            if "kubernetes.io/hostname" in nd["labels"]:
+                nd["labels"]["kubernetes.io/hostname"] = nd["name"]
+        else:
+            lvl = rng.choice(levels)
+            nd["labels"][lvl] = nd["labels"].get(lvl, "") + "x"
+        nd["conditions"] = nd.get("conditions") or [{"type": "Ready", "status": "True"}]
+        latest[nd["name"]] = nd
+        if nd["name"] not in names:
+            names.append(nd["name"])
+        evs.append(nd)
+    return evs
+
+
 def _oracle_pods(evs):
     return [dict(e, phase="Succeeded") if e.get("delete") else e for e in evs]
 
@@ -61,6 +114,53 @@ def _check(seed, n, lib=None, gen=None):
             want = oracle_lib.run_case(ref)["results"]
             assert got == want, (i, step, evs, got, want)
         snap.close()
+
+
+def _check_nodes(seed, n, lib=None, gen=None):
+    """Node events interleaved with pod events and admitted usage; the oracle
+    rebuilds from the document with every event appended and replays the
+    usage updates (a session) — the reference's per-cycle rebuild."""
+    rng = random.Random(seed)
+    rebuilt = inplace = 0
+    for i in range(n):
+        case = (gen or synth.random_case)(rng)
+        snap = TASFlavorSnapshot(case, lib=lib) if lib else TASFlavorSnapshot(case)
+        ref = copy.deepcopy(case)
+        ref.setdefault("pods", [])
+        adds = []
+        for step in range(4):
+            kind = rng.random()
+            if kind < 0.6:
+                evs = node_events(rng, ref, rng.randint(1, 4))
+                if snap.update_nodes(evs):
+                    rebuilt += 1
+                else:
+                    inplace += 1
+                ref["nodes"] = ref["nodes"] + evs
+            elif kind < 0.8:
+                evs = pod_events(rng, ref, rng.randint(1, 4))
+                snap.update_pods(evs)
+                ref["pods"] += _oracle_pods(evs)
+            else:
+                res = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+                u = synth.usage_records(case["podSets"], res)
+                if u:
+                    snap.add_usage(u)
+                    adds.append({"op": "add", "usage": u})
+            got = snap.find_topology_assignments_for_flavor(case["podSets"])
+            want = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+            assert got == want, (i, step, got, want)
+        snap.close()
+    assert rebuilt > 0 and inplace > 0, (rebuilt, inplace)
+
+
+def test_emulated_node_events(emu_lib):  # noqa: F811
+    _check_nodes(94, 60, lib=emu_lib)
+
+
+@pytest.mark.gpu
+def test_node_events_on_gpu():
+    _check_nodes(95, 200)
 
 
 def test_emulated_pod_events(emu_lib):  # noqa: F811
