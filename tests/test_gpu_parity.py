@@ -105,6 +105,26 @@ def test_c3_sample_full_size():
     assert mism == [], mism[:5]
 
 
+@pytest.mark.timeout(900)
+def test_c5_sample_max_size():
+    # the largest config (C5: 8x32x128x32 = 1,048,576 nodes) on one GPU with a
+    # 256-evaluation device batch; the oracle checks a BestFit + LFC sample
+    snap_doc, wls = synth.config_c5(n_workloads=256)
+    bf = [w for w in wls if w[0]["topologyRequest"] and not w[0]["topologyRequest"].get("unconstrained")]
+    lfc = [w for w in wls if w not in bf]
+    sample = bf[:4] + lfc[:4]
+    want, _ = oracle_lib.eval_workloads(snap_doc, sample, threads=8)
+    snap = TASFlavorSnapshot(snap_doc, max_batch=256)
+    del snap_doc
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    idx = {id(w): i for i, w in enumerate(wls)}
+    mism = [k for k, w in enumerate(sample) if got[idx[id(w)]] != want[k]]
+    assert mism == [], mism[:5]
+    assert any(r[0]["assignment"] for r in got) and sum(len(r[0]["assignment"]["domains"]) for r in got
+                                                         if r[0]["assignment"]) > 100
+
+
 def test_packed_entries_path_matches_view_path():
     # kueue_tas_eval_batch's packed copy (caller buffer, EOVERFLOW + fetch) vs the zero-copy view
     snap_doc, wls = synth.config_c2(n_workloads=200)
