@@ -105,6 +105,23 @@ def test_c3_sample_full_size():
     assert mism == [], mism[:5]
 
 
+def test_c4_sample_full_size():
+    # JobSet-like groups (leader + sliced workers, assumed-usage chaining) at
+    # the full C4 size (2x16x64x32 = 65,536 nodes) against the oracle on a sample.
+    # Reference quirk reproduced here: when the host that takes the leader does
+    # not complete the group, consumeWithLeadersGeneric's pods branch subtracts
+    # before clamping (tas_flavor_snapshot.go:1392-1402), zeroing that host's
+    # leaderState: the leader assignment comes out empty and the workers get
+    # count + 1 pods.  The restatement and the device both follow the code.
+    snap_doc, wls = synth.config_c4(n_workloads=256)
+    sample = wls[:12]
+    want, _ = oracle_lib.eval_workloads(snap_doc, sample, threads=8)
+    snap = TASFlavorSnapshot(snap_doc)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    assert got[:12] == want
+
+
 @pytest.mark.timeout(900)
 def test_c5_sample_max_size():
     # the largest config (C5: 8x32x128x32 = 1,048,576 nodes) on one GPU with a
