@@ -129,6 +129,20 @@ def main():
                "sample": f"{len(want)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
                          f"(C++ restatement of the Go path; Go toolchain absent)",
                "seconds": round(secs, 3)}
+        # mode (ii) of BASELINE.md: the batch's independent workloads over host threads
+        thr = int(os.environ.get("KTAS_CPU_THREADS", "16"))
+        tsample = mine[: 4 * thr]
+        _, tsecs = oracle_lib.eval_workloads(snap_doc, tsample, threads=thr)
+        model = ""
+        try:
+            with open("/proc/cpuinfo") as fh:
+                model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+        except OSError:
+            pass
+        cpu["threaded"] = {"value": round(len(tsample) / tsecs, 3), "threads": thr,
+                           "sample": f"{len(tsample)} workloads", "seconds": round(tsecs, 3)}
+        cpu["cpu_model"] = model
+        cpu["gomaxprocs"] = "n/a (Go toolchain absent)"
         if not parity:
             bad = [i for i in range(len(want)) if got[i] != want[i]]
             print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
