@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -1024,6 +1025,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
 
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, stage_bytes, hipMemcpyHostToDevice, c->stream));
+  // the select path's descriptor (g_select_snap), ordered before both select
+  // launches: stream2 joins after events recorded later on this stream
+  HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_select_snap), &c->snap, sizeof(DevSnap), 0, hipMemcpyHostToDevice,
+                                   c->stream));
   if (!lds_stats) HIPCHK(c, hipMemsetAsync(d_stats, 0, stats_len * 4, c->stream));
   uint8_t* ds = c->d_stage.p;
   DevBatch b{};
@@ -1245,6 +1250,9 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
                          size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
                          size_t num_assumed, kueue_tas_eval_out* out, int64_t* entry_offsets, int32_t* entries,
                          size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts) {
+  // g_select_snap is one per device: batches of different contexts must not interleave
+  static std::mutex select_snap_mu;
+  std::lock_guard<std::mutex> select_snap_lock(select_snap_mu);
   if (!c) return KUEUE_TAS_EINVAL;
   if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
   HIPCHK(c, hipSetDevice(c->device));

@@ -1155,8 +1155,16 @@ enum ProfCat : int {
   P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_NCAT
 };
 
+// The select path's snapshot descriptor, in the constant address space: the
+// walk's helpers (not inlined) read its fields with scalar loads from a known
+// address.  A pointer to the by-value kernel argument instead made the
+// compiler copy the argument into scratch and chase two dependent scratch
+// loads (Wave -> descriptor -> field) per access.  Written by the host on the
+// batch's stream before the select launches (kueue_tas_eval_batch holds a
+// process-wide lock, so contexts do not interleave their descriptors).
+__constant__ DevSnap g_select_snap;
+
 struct Wave {
-  const DevSnap* s;
   const DevEval* ev;
   int eid;
   int lane;
@@ -1240,16 +1248,16 @@ struct Wave {
     return ctr[int64_t(f) * SD + g];
   }
   __device__ Key kplain_clean(int g) const {
-    int idx = g - s->level_off[level_of(g)];
+    int idx = g - g_select_snap.level_off[level_of(g)];
     return key_plain(lfc, get_clean(F_SLICE, g), get_clean(F_STATE, g), idx);
   }
   __device__ Key kplain(int g) const {
-    int idx = g - s->level_off[level_of(g)];
+    int idx = g - g_select_snap.level_off[level_of(g)];
     return key_plain(lfc, get(F_SLICE, g), get(F_STATE, g), idx);
   }
   __device__ int level_of(int g) const {
     int l = 0;
-    while (l + 1 < s->L && g >= s->level_off[l + 1]) l++;
+    while (l + 1 < g_select_snap.L && g >= g_select_snap.level_off[l + 1]) l++;
     return l;
   }
 };
@@ -1741,7 +1749,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
                               bool slices, int32_t* out, int* np) {
   ProfScope prof_scope_(w, P_THRESHOLD);
   if (w.cap * int(sizeof(Key)) < kThrBins * int(sizeof(uint64_t))) return -1;
-  const int loff = w.s->level_off[level];
+  const int loff = g_select_snap.level_off[level];
   const bool lfc = w.lfc;
   const int32_t rem = slices ? go_div32(count, sliceSize) : count;
   Key* keys = w.gkeys;
@@ -1879,7 +1887,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     uint32_t kth;
     {
       ProfScope ps_sel(w, P_TW_SELECT);
-      const int nbits = 32 - __builtin_clz(uint32_t(max(w.s->level_size[level] - 1, 1)));  // indices < level size
+      const int nbits = 32 - __builtin_clz(uint32_t(max(g_select_snap.level_size[level] - 1, 1)));  // indices < level size
       kth = lds_select_kth(cand, cnt, int(m), cand + ccap, w.lane, nbits, dbits);
     }
     ck = key_plain(lfc, t, u, int32_t(kth));
@@ -2022,7 +2030,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
 __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int32_t count, int32_t leaderCount,
                             int32_t sliceSize, bool slices, int32_t sliceRecompute, int32_t* out, int* np) {
   ProfScope prof_scope_(w, P_WALK);
-  const int loff = w.s->level_off[level];
+  const int loff = g_select_snap.level_off[level];
   // leaderless walks need no sequential pass (see threshold_walk)
   const bool leaderless = !w.leader && leaderCount <= 0 && sliceRecompute <= 1;
   constexpr int kSmallWalk = 64;  // shorter lists: sort + prefix walk
@@ -2108,7 +2116,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
 // Children (CSR) of `n` domains at `level` appended to out (lowerLevelDomains :1503-1509).
 __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level, int32_t* out) {
   ProfScope prof_scope_(w, P_GATHER);
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int poff = s.level_off[level];
   const int coff = s.level_off[level + 1];
   const int32_t* co = s.child_off + s.child_base[level];
@@ -2140,7 +2148,7 @@ __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level
 // visited as one flattened range, kU loads in flight per lane.
 __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, int level, int32_t* out) {
   ProfScope prof_scope_(w, P_GATHER);
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int poff = s.level_off[level];
   const int coff = s.level_off[level + 1];
   const int32_t* co = s.child_off + s.child_base[level];
@@ -2231,7 +2239,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
 
 // multiLayerNotFitMessage numbers (:1754-1793)
 __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int D = s.level_size[level];
   const int loff = s.level_off[level];
   uint64_t best = ~0ull;
@@ -2289,7 +2297,7 @@ __device__ void not_fit(Wave& w, int level, int32_t fit, int32_t total, kueue_ta
 __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, bool positive_only, int32_t* ent, int ent_cap,
                            int base) {
   ProfScope prof_scope_(w, P_EMIT);
-  const int loff = w.s->level_off[w.s->L - 1];
+  const int loff = g_select_snap.level_off[g_select_snap.L - 1];
   if (n > 0) {
     // Leaf-index range of the output: when its bitmap fits the wave's LDS,
     // mark the leaves and emit them in index order without sorting.
@@ -2401,7 +2409,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
 // Leaf counters are read 4 at a time (16-byte aligned level start).
 // Returns 1 done, 0 needs the generic path.
 __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& o, int32_t* ent, int ent_cap) {
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int D = s.N;
   const int loff = s.level_off[s.L - 1];
   const int32_t ss = w.ev->slice_size;
@@ -2585,7 +2593,7 @@ __device__ int lfc_first_leaf(const Wave& w, const DevBatch& b, int slot, const 
     if (m) chunk = c0 + __ffsll((unsigned long long)m) - 1;
   }
   if (chunk < 0) return -1;
-  const int lo = chunk * kLfcChunk, hi = min(w.s->N, lo + kLfcChunk);
+  const int lo = chunk * kLfcChunk, hi = min(g_select_snap.N, lo + kLfcChunk);
   for (int i0 = lo; i0 < hi; i0 += kWave) {
     const int i = i0 + w.lane;
     const uint64_t m = ballot(i < hi && V[i] == v);
@@ -2599,7 +2607,7 @@ __device__ int lfc_first_leaf(const Wave& w, const DevBatch& b, int slot, const 
 // index order).  Rare: leaf values that large need tiny requests.
 __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before, int64_t below,
                          kueue_tas_eval_out& o, int32_t* ent, int ecap) {
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int N = s.N;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B
   constexpr int kW = 256;
@@ -2675,7 +2683,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
 }
 
 __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_out& o, int32_t* ent, int ecap) {
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const int L1 = s.L - 1;
   const int lane = w.lane;
   const int32_t* V = w.ctr + w.SD + s.level_off[L1];
@@ -2806,7 +2814,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
 __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, kueue_tas_eval_out& o, int32_t* ent,
                           int ent_cap) {
   ProfScope prof_scope_(w, P_FIND);
-  const DevSnap& s = *w.s;
+  const DevSnap& s = g_select_snap;
   const DevEval& ev = *w.ev;
   const bool required = (ev.flags & KUEUE_TAS_F_REQUIRED) != 0;
   const int32_t leaderCount = w.leader ? 1 : 0;
@@ -3177,7 +3185,6 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   const uint64_t t_begin = wall_clock64();
   const DevEval& ev = b.evals[eid];
   Wave w;
-  w.s = &s;
   w.ev = &ev;
   w.eid = eid;
   w.lane = lane;

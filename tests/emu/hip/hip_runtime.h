@@ -24,6 +24,8 @@
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define __shared__ static
+#define __constant__
+#define HIP_SYMBOL(x) (&(x))
 
 struct dim3 {
   unsigned x, y, z;
@@ -158,6 +160,10 @@ inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h;
 inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t st) {
   if (n) st->ops.push_back([=]() { memmove(d, s, n); });
   return hipSuccess;
+}
+inline hipError_t hipMemcpyToSymbolAsync(const void* sym, const void* s, size_t n, size_t off, hipMemcpyKind k,
+                                         hipStream_t st) {
+  return hipMemcpyAsync(static_cast<char*>(const_cast<void*>(sym)) + off, s, n, k, st);
 }
 inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
   emu::drain_all();
