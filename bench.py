@@ -16,6 +16,7 @@ bytes and the CPU baseline (the C++ oracle, "port", timed on a bounded sample).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -34,7 +35,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=1024, help="pending workloads per rank per step")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="workloads timed on the CPU oracle (rank 0)")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="workloads timed on the CPU oracle (rank 0)")
     ap.add_argument("--parity-sample", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -114,38 +115,41 @@ def main():
     load_s = time.time() - t0
     N = len(snap_doc["nodes"])
 
-    # ---- parity (untimed): product vs CPU oracle on a sample; CPU baseline timing ----
-    parity = None
-    cpu = None
-    if rank == 0 and not a.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib
+    # ---- parity (untimed, after the timed region so the CPU burn cannot
+    # disturb it): product vs CPU oracle on a sample; CPU baseline timing ----
+    def cpu_leg():
+        parity = None
+        cpu = None
+        if rank == 0 and not a.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib
 
-        sample = mine[: max(a.parity_sample, a.cpu_sample)]
-        got = snap.find_topology_assignments_for_workloads(sample)
-        want, secs = oracle_lib.eval_workloads(snap_doc, sample[: a.cpu_sample])
-        parity = all(got[i] == want[i] for i in range(len(want)))
-        cpu = {"value": round(len(want) / secs, 3), "unit": "placements/s", "cores": 1, "kind": "port",
-               "sample": f"{len(want)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
-                         f"(C++ restatement of the Go path; Go toolchain absent)",
-               "seconds": round(secs, 3)}
-        # mode (ii) of BASELINE.md: the batch's independent workloads over host threads
-        thr = int(os.environ.get("KTAS_CPU_THREADS", "16"))
-        tsample = mine[: 4 * thr]
-        _, tsecs = oracle_lib.eval_workloads(snap_doc, tsample, threads=thr)
-        model = ""
-        try:
-            with open("/proc/cpuinfo") as fh:
-                model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
-        except OSError:
-            pass
-        cpu["threaded"] = {"value": round(len(tsample) / tsecs, 3), "threads": thr,
-                           "sample": f"{len(tsample)} workloads", "seconds": round(tsecs, 3)}
-        cpu["cpu_model"] = model
-        cpu["gomaxprocs"] = "n/a (Go toolchain absent)"
-        if not parity:
-            bad = [i for i in range(len(want)) if got[i] != want[i]]
-            print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
+            sample = mine[: max(a.parity_sample, a.cpu_sample)]
+            got = snap.find_topology_assignments_for_workloads(sample)
+            want, secs = oracle_lib.eval_workloads(snap_doc, sample[: a.cpu_sample])
+            parity = all(got[i] == want[i] for i in range(len(want)))
+            cpu = {"value": round(len(want) / secs, 3), "unit": "placements/s", "cores": 1, "kind": "port",
+                   "sample": f"{len(want)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
+                             f"(C++ restatement of the Go path; Go toolchain absent)",
+                   "seconds": round(secs, 3)}
+            # mode (ii) of BASELINE.md: the batch's independent workloads over host threads
+            thr = int(os.environ.get("KTAS_CPU_THREADS", "16"))
+            tsample = mine[: 4 * thr]
+            _, tsecs = oracle_lib.eval_workloads(snap_doc, tsample, threads=thr)
+            model = ""
+            try:
+                with open("/proc/cpuinfo") as fh:
+                    model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+            except OSError:
+                pass
+            cpu["threaded"] = {"value": round(len(tsample) / tsecs, 3), "threads": thr,
+                               "sample": f"{len(tsample)} workloads", "seconds": round(tsecs, 3)}
+            cpu["cpu_model"] = model
+            cpu["gomaxprocs"] = "n/a (Go toolchain absent)"
+            if not parity:
+                bad = [i for i in range(len(want)) if got[i] != want[i]]
+                print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
+        return parity, cpu
 
     import torch
 
@@ -165,6 +169,10 @@ def main():
             gathered = gather_records(snap.last_records(len(mine)), world, dist, device=f"cuda:{local_rank}")
         return h
 
+    # the snapshot document and generated workloads are long-lived: keep them
+    # out of the collector's scans during the timed loop
+    gc.collect()
+    gc.freeze()
     for _ in range(a.warmup):
         step()
     barrier()
@@ -189,6 +197,7 @@ def main():
         dt = float(tt.item())
     placements = len(all_wls) * a.steps  # every rank's shard, all steps
     value = placements / dt
+    parity, cpu = cpu_leg()
 
     # ---- widened rows, after the timed region: v1beta2 encoding of the last
     # batch's assignments and the admission re-check + usage update ----
