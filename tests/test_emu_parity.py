@@ -107,3 +107,19 @@ def test_emulated_inline_stats_path_matches_oracle(emu_lib):
         got = snap.find_topology_assignments_for_flavor(case["podSets"])
         snap.close()
         assert got == want, (i, got, want)
+
+
+def test_emulated_two_resident_flavors_interleaved(emu_lib):
+    # alternating batches of two resident contexts share the device's select
+    # descriptor, re-uploaded only when the context changes
+    doc_a, wls_a = synth.config_c3(n_workloads=8, shape=(2, 2, 8, 16))
+    doc_b, wls_b = synth.config_c4(n_workloads=4, shape=(2, 2, 4, 16))
+    want_a, _ = oracle_lib.eval_workloads(doc_a, wls_a)
+    want_b, _ = oracle_lib.eval_workloads(doc_b, wls_b)
+    a = TASFlavorSnapshot(doc_a, lib=emu_lib)
+    b = TASFlavorSnapshot(doc_b, lib=emu_lib)
+    for _ in range(2):
+        assert a.find_topology_assignments_for_workloads(wls_a) == want_a
+        assert b.find_topology_assignments_for_workloads(wls_b) == want_b
+    a.close()
+    b.close()

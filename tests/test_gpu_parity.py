@@ -152,3 +152,20 @@ def test_packed_entries_path_matches_view_path():
     a.close()
     b.close()
     assert got_a == got_b
+
+
+def test_two_resident_flavors_interleaved():
+    # two flavor snapshots resident on one device, batches alternating between
+    # them: the select path's constant-memory descriptor is shared per device
+    # and re-uploaded only when the context changes (tas_device.hip eval_chunk)
+    doc_a, wls_a = synth.config_c2(n_workloads=40)
+    doc_b, wls_b = synth.config_c4(n_workloads=12, shape=(2, 4, 16, 32))
+    want_a, _ = oracle_lib.eval_workloads(doc_a, wls_a)
+    want_b, _ = oracle_lib.eval_workloads(doc_b, wls_b)
+    a = TASFlavorSnapshot(doc_a)
+    b = TASFlavorSnapshot(doc_b)
+    for _ in range(2):
+        assert a.find_topology_assignments_for_workloads(wls_a) == want_a
+        assert b.find_topology_assignments_for_workloads(wls_b) == want_b
+    a.close()
+    b.close()
