@@ -433,8 +433,20 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   const bool lds_stats = !split && b.nstat > 0;
   if (lds_stats)
     for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
-  const int e0 = b.fill_chunks[2 * blockIdx.y];
-  const int ne = b.fill_chunks[2 * blockIdx.y + 1];
+  // XCD-aware (tile, chunk) order: consecutive workgroups go round-robin to
+  // the 8 XCDs, so the chunks of one leaf tile are laid out 8 workgroups apart
+  // and land on the same XCD back to back, where the tile's snapshot columns
+  // are still in that XCD's L2 (each chunk re-reads them).  A bijection of
+  // the 2-D grid; identity when the tile count is not a multiple of 8.
+  int tile = blockIdx.x, chunk = blockIdx.y;
+  if ((gridDim.x & 7u) == 0 && gridDim.y > 1) {
+    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t g = lin >> 3;
+    chunk = int(g % gridDim.y);
+    tile = int((g / gridDim.y) * 8u + (lin & 7u));
+  }
+  const int e0 = b.fill_chunks[2 * chunk];
+  const int ne = b.fill_chunks[2 * chunk + 1];
   const bool stage_taints = b.num_profiles <= kStagedProfiles;
   if (int(threadIdx.x) < ne) {
     const int eid = b.fill_ids[e0 + threadIdx.x];
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     }
   }
   __syncthreads();
-  const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
+  const int leaf = tile * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
   const int N = s.N;
   const int gleaf = s.level_off[s.L - 1] + leaf;
@@ -559,7 +571,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         return any ? result : 0;
       };
       state0 = count_slots(rmask, tb, pres, false, &lim0);
-      if (split) b.fill_lim[int64_t(blockIdx.y) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
+      if (split) b.fill_lim[int64_t(chunk) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
       swl0 = state0;
       if (leader) {
         int dummy;
@@ -721,7 +733,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     __syncthreads();
     for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
       const int e = i / b.nstat, k = i % b.nstat;
-      b.fill_stats[(int64_t(e0 + e) * gridDim.x + blockIdx.x) * b.nstat + k] = sh_stats[e][k];
+      b.fill_stats[(int64_t(e0 + e) * gridDim.x + tile) * b.nstat + k] = sh_stats[e][k];
     }
   }
 }
