@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KUEUE_TAS_ABI_VERSION 1
+#define KUEUE_TAS_ABI_VERSION 2
 #define KUEUE_TAS_MAX_LEVELS 16    /* topology_types.go:114 (<=16 levels) */
 #define KUEUE_TAS_MAX_COLS 32      /* resource columns per snapshot */
 #define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs per request */
@@ -95,6 +95,7 @@ typedef struct {
 #define KUEUE_TAS_F_SIMULATE_EMPTY 8u /* WithSimulateEmpty :505 */
 #define KUEUE_TAS_F_LEADER 16u        /* leaderTasPodSetRequests != nil */
 #define KUEUE_TAS_F_MULTILAYER 32u    /* len(multiLayerConstraints) > 0 :873-875 */
+#define KUEUE_TAS_F_AFFINITY 64u      /* requirements.affinitySelector != nil :889-897 (hostname leaves) */
 
 typedef struct {
   uint32_t flags;
@@ -118,7 +119,28 @@ typedef struct {
   int32_t taint_table;            /* offset into the batch taint table: P entries, excluded taint id or -1 */
   int32_t assumed_begin;          /* [begin,end) into the batch assumed-usage records (sorted by leaf) */
   int32_t assumed_end;
+  int32_t affinity_begin;         /* with KUEUE_TAS_F_AFFINITY: [begin,end) into the batch affinity */
+  int32_t affinity_end;           /*   requirements; an empty range matches no leaf */
 } kueue_tas_eval_req;
+
+/* One compiled requirement of required node affinity
+ * (nodeaffinity.NodeSelector, vendor/k8s.io/component-helpers/scheduling/
+ * corev1/nodeaffinity/nodeaffinity.go:75-201; labels.Requirement.Matches,
+ * vendor/k8s.io/apimachinery/pkg/labels/selector.go:247-294).  A leaf matches
+ * the requirement when its id is in values[begin, begin + len) (sorted
+ * ascending) XOR negate; the id is the leaf's label value id in column `col`
+ * (0 = label absent), or with col == KUEUE_TAS_AFFINITY_LEAF the leaf index
+ * itself (matchFields on metadata.name).  Requirements of one
+ * nodeSelectorTerm share `term` (ascending within a request): a leaf passes
+ * when every requirement of some term matches. */
+#define KUEUE_TAS_AFFINITY_LEAF (-1)
+typedef struct {
+  int32_t term;
+  int32_t col;
+  int32_t negate;
+  int32_t begin;
+  int32_t len;
+} kueue_tas_affinity_req;
 
 /* assumedUsage overlay record (addAssumedUsage :658-666), subtracted from the
  * remaining capacity of `leaf`; creates the key (presence) like Requests.Sub. */
@@ -194,6 +216,9 @@ int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* ctx, const int32_t* leaves,
 /* Evaluate n requests against the resident snapshot.
  *  taint_table:   int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
  *  assumed:       overlay records referenced by reqs[i].assumed_begin/end
+ *  affinity:      requirements referenced by reqs[i].affinity_begin/end, their
+ *                 value ids in affinity_values (both may be NULL when no
+ *                 request sets KUEUE_TAS_F_AFFINITY)
  *  out:           [n] result headers
  *  entry_offsets: [n+1] the (leaf, count) int32 pairs of request i are
  *                 entries[2*off[i] .. 2*off[i+1]): workers, then leaders
@@ -209,8 +234,10 @@ int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* ctx, const int32_t* leaves,
  * kueue_tas_fetch_entries); or another error. */
 int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                          size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
-                         size_t num_assumed, kueue_tas_eval_out* out, int64_t* entry_offsets, int32_t* entries,
-                         size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts);
+                         size_t num_assumed, const kueue_tas_affinity_req* affinity, size_t num_affinity,
+                         const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
+                         int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
+                         int32_t* res_counts);
 /* Copy the packed entries of the last kueue_tas_eval_batch (after EOVERFLOW). */
 int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries_capacity);
 /* Zero-copy view of the packed entries of the last kueue_tas_eval_batch

@@ -658,6 +658,7 @@ static double wall_ms() {
 
 static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
+                      const kueue_tas_affinity_req* aff, size_t num_aff, const int32_t* aff_vals, size_t num_aff_vals,
                       kueue_tas_eval_out* out, int64_t* offsets, int32_t* taint_counts, int32_t* res_counts,
                       float* ms, float* stage_ms) {
   const int32_t entry_cap = c->entry_cap;
@@ -680,6 +681,20 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       return fail(c, KUEUE_TAS_EINVAL, "level out of range");
     if (r.num_selectors < 0 || r.num_selectors > KUEUE_TAS_MAX_SELECTORS) return fail(c, KUEUE_TAS_EINVAL, "num_selectors");
     if (r.num_selectors > 0 && s.K == 0) return fail(c, KUEUE_TAS_EINVAL, "selectors without label columns");
+    if (r.flags & KUEUE_TAS_F_AFFINITY) {  // host-side shape check of everything the fill will read
+      if (r.affinity_begin < 0 || r.affinity_end < r.affinity_begin || size_t(r.affinity_end) > num_aff ||
+          (r.affinity_end > r.affinity_begin && (!aff || !aff_vals)))
+        return fail(c, KUEUE_TAS_EINVAL, "affinity range");
+      for (int32_t k = r.affinity_begin; k < r.affinity_end; k++) {
+        const kueue_tas_affinity_req& q = aff[k];
+        if (q.col < KUEUE_TAS_AFFINITY_LEAF || q.col >= s.K || q.begin < 0 || q.len < 0 ||
+            size_t(q.begin) + size_t(q.len) > num_aff_vals || (k > r.affinity_begin && q.term < aff[k - 1].term))
+          return fail(c, KUEUE_TAS_EINVAL, "affinity requirement");
+        for (int32_t j = 1; j < q.len; j++)
+          if (aff_vals[q.begin + j] <= aff_vals[q.begin + j - 1])
+            return fail(c, KUEUE_TAS_EINVAL, "affinity values not sorted");
+      }
+    }
     nterms += size_t(r.num_req + r.num_leader_req);
     maxt = std::max(maxt, std::max(r.num_req, r.num_leader_req));
   }
@@ -691,6 +706,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   };
   const size_t o_evals = seg(n * sizeof(DevEval)), o_terms = seg(nterms * sizeof(DevTerm));
   const size_t o_taint = seg(taint_table_len * 4), o_assumed = seg(num_assumed * sizeof(kueue_tas_assumed));
+  const size_t o_aff = seg(num_aff * sizeof(kueue_tas_affinity_req)), o_affv = seg(num_aff_vals * 4);
   const size_t o_fill = seg(n * 4), o_fchunks = seg(n * 8), o_pairs = seg(n * 8), o_rep = seg(n * 4);
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
   const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
@@ -715,6 +731,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     e.taint_table = r.taint_table;
     e.assumed_begin = r.assumed_begin;
     e.assumed_end = r.assumed_end;
+    e.aff_begin = r.affinity_begin;
+    e.aff_end = r.affinity_end;
     e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
     for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
       e.layer_level[k] = r.layer_level[k];
@@ -750,6 +768,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
   if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
+  if (num_aff) memcpy(hs + o_aff, aff, num_aff * sizeof(kueue_tas_affinity_req));
+  if (num_aff_vals) memcpy(hs + o_affv, aff_vals, num_aff_vals * 4);
   lap(0);
 
   // Phase-1 classes: evals with identical phase-1 inputs (request terms,
@@ -812,6 +832,15 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     for (int k = 0; k < e.nsel; k++) add(uint64_t(uint32_t(e.sel_col[k])) | (uint64_t(uint32_t(e.sel_val[k])) << 32));
     if (const int32_t* row = taint_row(e))
       for (int p = 0; p < P; p++) add(uint64_t(uint32_t(row[p])));
+    if (e.flags & KUEUE_TAS_F_AFFINITY) {
+      add(0xaff1u);
+      for (int k = e.aff_begin; k < e.aff_end; k++) {
+        const kueue_tas_affinity_req& q = aff[k];
+        add(uint64_t(uint32_t(q.term)) | (uint64_t(uint32_t(q.col)) << 32));
+        add(uint64_t(uint32_t(q.negate)) | (uint64_t(uint32_t(q.len)) << 32));
+        for (int j = 0; j < q.len; j++) add(uint64_t(uint32_t(aff_vals[q.begin + j])));
+      }
+    }
     return h;
   };
   auto same_mask = [&](const DevEval& x, const DevEval& y) {
@@ -822,7 +851,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (x.sel_col[k] != y.sel_col[k] || x.sel_val[k] != y.sel_val[k]) return false;
     const int32_t *rx = taint_row(x), *ry = taint_row(y);
     if ((rx == nullptr) != (ry == nullptr)) return false;
-    return rx == nullptr || rx == ry || memcmp(rx, ry, size_t(P) * 4) == 0;
+    if (!(rx == nullptr || rx == ry || memcmp(rx, ry, size_t(P) * 4) == 0)) return false;
+    const bool ax = (x.flags & KUEUE_TAS_F_AFFINITY) != 0, ay = (y.flags & KUEUE_TAS_F_AFFINITY) != 0;
+    if (ax != ay) return false;
+    if (!ax) return true;
+    if (x.aff_end - x.aff_begin != y.aff_end - y.aff_begin) return false;
+    for (int k = 0; k < x.aff_end - x.aff_begin; k++) {
+      const kueue_tas_affinity_req& p = aff[x.aff_begin + k];
+      const kueue_tas_affinity_req& q = aff[y.aff_begin + k];
+      if (p.term != q.term || p.col != q.col || p.negate != q.negate || p.len != q.len) return false;
+      if (p.begin != q.begin && memcmp(aff_vals + p.begin, aff_vals + q.begin, size_t(p.len) * 4) != 0) return false;
+    }
+    return true;
   };
   auto fast_lfc = [&](const DevEval& e) {
     return (e.flags & KUEUE_TAS_F_LFC) != 0 &&
@@ -979,7 +1019,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
-  const size_t stats_len = n * nt + n * size_t(s.R) + n;
+  const size_t stats_len = n * nt + n * size_t(s.R) + 2 * n;  // taints | resources | nodeSelector | affinity
   const size_t res_off_stats = (n * sizeof(kueue_tas_eval_out) + 15) / 16 * 16;
   const size_t res_bytes = res_off_stats + stats_len * 4;
   HIPCHK(c, c->d_res.ensure(res_bytes));
@@ -993,7 +1033,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   uint32_t umask = 0;
   for (size_t i = 0; i < n; i++) umask |= hev[i].req_mask | hev[i].lead_mask;
   const int ucols = __builtin_popcount(umask);
-  const int nstat_all = 1 + int(nt) + s.R;
+  const int nstat_all = kStatFixed + int(nt) + s.R;
   const bool lds_stats = s.N > 0 && nfchunks > 0 && ucols <= 8 && nstat_all <= kMaxFillStats;
   // per-eval entry regions [n][entry_cap] pairs in pinned, device-mapped host
   // memory: select / lfc_emit write the (leaf, count) pairs the host reads
@@ -1050,6 +1090,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.terms = reinterpret_cast<const DevTerm*>(ds + o_terms);
   b.taint_table = reinterpret_cast<const int32_t*>(ds + o_taint);
   b.assumed = reinterpret_cast<const kueue_tas_assumed*>(ds + o_assumed);
+  b.aff = reinterpret_cast<const kueue_tas_affinity_req*>(ds + o_aff);
+  b.aff_vals = reinterpret_cast<const int32_t*>(ds + o_affv);
   b.n = int32_t(n);
   b.num_taints = int32_t(nt);
   b.num_profiles = c->num_profiles;
@@ -1070,6 +1112,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.taint_counts = d_stats;
   b.res_counts = d_stats + n * nt;
   b.sel_counts = d_stats + n * nt + n * size_t(s.R);
+  b.aff_counts = b.sel_counts + n;
   b.out = d_out;
   b.entries = c->ent_dev + c->ent_used;
   b.entry_cap = entry_cap;
@@ -1229,9 +1272,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->ent_stride = entry_cap;
   lap(4);
   memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
-  {  // nodeSelector exclusions: counted beside select (stream3), read from the stats region after the join
+  {  // nodeSelector / affinity exclusions: counted beside select (stream3), read from the stats region after the join
     const int32_t* sel = c->res_stats_h + n * nt + n * size_t(s.R);
-    for (size_t i = 0; i < n; i++) out[i].excl_selector = sel[i];
+    for (size_t i = 0; i < n; i++) {
+      out[i].excl_selector = sel[i];
+      out[i].excl_affinity = sel[n + i];
+    }
   }
   if (KTAS_PROFILE) {
     const size_t base = c->last_prof.size();
@@ -1262,8 +1308,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
 
 int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
                          size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed,
-                         size_t num_assumed, kueue_tas_eval_out* out, int64_t* entry_offsets, int32_t* entries,
-                         size_t entries_capacity, int32_t* taint_counts, int32_t* res_counts) {
+                         size_t num_assumed, const kueue_tas_affinity_req* affinity, size_t num_affinity,
+                         const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
+                         int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
+                         int32_t* res_counts) {
   // g_select_snap is one per device: batches of different contexts must not interleave
   static std::mutex select_snap_mu;
   std::lock_guard<std::mutex> select_snap_lock(select_snap_mu);
@@ -1286,7 +1334,8 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
     off.assign(m + 1, 0);
     for (;;) {
       size_t keep = c->ent_used;
-      int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, out + i0,
+      int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, affinity,
+                          num_affinity, affinity_values, num_affinity_values, out + i0,
                           off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run

@@ -8,7 +8,8 @@
 //   FindTopologyAssignmentsForFlavor       :519-594 (groups, leader/workers :596-609,
 //                                          assumedUsage :658-666, stop at first failure)
 //   findTopologyAssignment prelude         :804-897 (requests + pods:1, slice size/levels,
-//                                          validation reasons, tolerations, selector)
+//                                          validation reasons, tolerations, nodeSelector,
+//                                          required node affinity compiled to label-id sets)
 //   notFitMessage / multiLayerNotFitMessage / ExclusionStats.formatReasons
 //                                          :1721-1793, :480-499
 // Everything between the prelude and buildAssignment runs on the GPU
@@ -31,6 +32,7 @@
 
 #include "../../include/kueue_tas.h"
 #include "json_reader.h"
+#include "label_selectors.h"
 
 namespace kueue_tas {
 
@@ -153,6 +155,8 @@ struct TASPodSetRequests {  // tas_flavor_snapshot.go:356-367
   std::optional<std::string> podSetGroupName;
   std::vector<Toleration> tolerations;
   std::optional<std::map<std::string, std::string>> nodeSelector;
+  // PodSpec affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution (podset.go:104-144)
+  std::optional<labelsel::RequiredAffinity> affinity;
 };
 struct DomainAssignment {
   int32_t leaf;
@@ -198,6 +202,10 @@ struct GroupEval {
   int32_t slice_size = 1;
   std::vector<std::string> layer_names;            // multi-layer message labels
   std::vector<int32_t> taint_row;                  // per taint profile
+  // required node affinity (KUEUE_TAS_F_AFFINITY): requirements with `begin`
+  // relative to aff_vals; build_pass rebases them into the batch tables
+  std::vector<kueue_tas_affinity_req> aff;
+  std::vector<int32_t> aff_vals;
 };
 
 struct Workload {
@@ -242,6 +250,10 @@ class FlavorSnapshot {
   std::vector<NodeInfo> nodes;
   std::map<std::string, std::string> flavorLabels;
   std::unordered_map<std::string, size_t> nodeIdx;  // node name -> nodes[]
+  // hostname leaves by their node's name (matchFields metadata.name) and the
+  // leaves whose node has no name (nodeaffinity ignores matchFields there)
+  std::unordered_map<std::string, int32_t> leafByNodeName;
+  std::vector<int32_t> unnamedLeaves;
 
   kueue_tas_ctx* ctx = nullptr;
   bool dirty = true;
@@ -482,6 +494,13 @@ class FlavorSnapshot {
       }
     }
     if (profiles.empty()) profiles.push_back({});
+    leafByNodeName.clear();
+    unnamedLeaves.clear();
+    if (lowestIsHostname)
+      for (int i = 0; i < N; i++) {
+        if (leafNode[i]->name.empty()) unnamedLeaves.push_back(i);
+        else leafByNodeName.emplace(leafNode[i]->name, i);
+      }
   }
 
   // nonTasUsageCache.update (tas_non_tas_pod_cache.go:46-73): a terminated
@@ -959,10 +978,6 @@ class FlavorSnapshot {
       }
     }
     bool multilayer = gates.multiLayer && !ssal.empty();
-    if (gates.balanced && !required && !unconstrained) {
-      g.early_reason = "unsupported: TASBalancedPlacement";
-      return;
-    }
     q.flags = (required ? KUEUE_TAS_F_REQUIRED : 0u) | (unconstrained ? KUEUE_TAS_F_UNCONSTRAINED : 0u) |
               ((unconstrained && gates.profileMixed) ? KUEUE_TAS_F_LFC : 0u) |
               (simulateEmpty ? KUEUE_TAS_F_SIMULATE_EMPTY : 0u) | (g.leader ? KUEUE_TAS_F_LEADER : 0u) |
@@ -1017,6 +1032,13 @@ class FlavorSnapshot {
         }
       }
       // nodeSelector: labels.ValidatedSelectorFromSet (only with hostname leaves, :879-887)
+      if (w.nodeSelector) {
+        const std::string e = labelsel::node_selector_failure(*w.nodeSelector);
+        if (!e.empty()) {
+          g.early_reason = e;
+          return;
+        }
+      }
       if (w.nodeSelector && !w.nodeSelector->empty() && !labelKeys.empty()) {
         if (w.nodeSelector->size() > KUEUE_TAS_MAX_SELECTORS) {
           g.early_reason = "unsupported: more than 8 nodeSelector terms";
@@ -1036,6 +1058,110 @@ class FlavorSnapshot {
         }
       }
     }
+    // required node affinity: validated always, filters only hostname leaves (:889-897, :1605-1610)
+    g.aff.clear();
+    g.aff_vals.clear();
+    if (w.affinity) {
+      const std::string e = labelsel::affinity_failure(*w.affinity);
+      if (!e.empty()) {
+        g.early_reason = e;
+        return;
+      }
+      if (lowestIsHostname) compile_affinity(*w.affinity, g);
+    }
+    // TASBalancedPlacement branches after fillInCounts (:907-917): not supported
+    if (gates.balanced && !required && !unconstrained) {
+      g.early_reason = "unsupported: TASBalancedPlacement";
+      return;
+    }
+  }
+
+  // Required node affinity compiled against the snapshot's label
+  // dictionaries (nodeaffinity.NodeSelector.Match, nodeaffinity.go:84-201;
+  // labels.Requirement.Matches, selector.go:247-294): every requirement
+  // becomes a sorted set of label-value ids of one column (0 = label absent)
+  // XOR negate, or a set of leaf indices for matchFields on metadata.name;
+  // requirements with the same outcome on every leaf fold away.  Sets
+  // KUEUE_TAS_F_AFFINITY unless every leaf matches; no remaining term means
+  // no leaf matches.  Matching runs in the fill kernels (affinity_match).
+  void compile_affinity(const labelsel::RequiredAffinity& terms, GroupEval& g) {
+    int32_t term_id = 0;
+    auto add = [&](int32_t col, std::vector<int32_t> ids, bool negate) {
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      g.aff.push_back({term_id, col, negate ? 1 : 0, int32_t(g.aff_vals.size()), int32_t(ids.size())});
+      g.aff_vals.insert(g.aff_vals.end(), ids.begin(), ids.end());
+    };
+    for (const labelsel::Term& t : terms) {
+      if (t.empty()) continue;  // an empty term is dropped by NewLazyErrorNodeSelector (:60-64)
+      const size_t mark_r = g.aff.size(), mark_v = g.aff_vals.size();
+      bool never = false;
+      for (const labelsel::Expr& e : t.exprs) {
+        const auto c = labelCol.find(e.key);
+        if (c == labelCol.end()) {  // no leaf has the key: constant outcome
+          never |= !(e.op == "NotIn" || e.op == "DoesNotExist");
+          continue;
+        }
+        const auto& dict = labelDict[size_t(c->second)];
+        std::vector<int32_t> ids;
+        if (e.op == "In" || e.op == "NotIn") {
+          for (auto& v : *e.values) {
+            auto d = dict.find(v);
+            if (d != dict.end()) ids.push_back(d->second);
+          }
+          if (ids.empty()) {  // no leaf carries any of the values
+            never |= e.op == "In";
+            continue;
+          }
+          add(c->second, std::move(ids), e.op == "NotIn");
+        } else if (e.op == "Exists" || e.op == "DoesNotExist") {
+          add(c->second, {0}, e.op == "Exists");
+        } else {  // Gt / Lt over the column's distinct values that parse as int64
+          int64_t rv = 0, lv = 0;
+          labelsel::parse_int((*e.values)[0], &rv);
+          for (auto& kv : dict)
+            if (labelsel::parse_int(kv.first, &lv) && (e.op == "Gt" ? lv > rv : lv < rv)) ids.push_back(kv.second);
+          if (ids.empty()) {
+            never = true;
+            continue;
+          }
+          add(c->second, std::move(ids), false);
+        }
+      }
+      // matchFields: field value is the node name for metadata.name, "" for
+      // any other key; ignored on a node without a name (:197)
+      for (const labelsel::Expr& e : t.fields) {
+        const std::string& v = (*e.values)[0];
+        const bool in = e.op == "In";
+        std::vector<int32_t> ids;
+        if (e.key == "metadata.name") {
+          auto it = leafByNodeName.find(v);
+          if (in) {
+            if (it != leafByNodeName.end()) ids.push_back(it->second);
+            ids.insert(ids.end(), unnamedLeaves.begin(), unnamedLeaves.end());
+            if (ids.empty()) never = true;
+            else add(KUEUE_TAS_AFFINITY_LEAF, std::move(ids), false);
+          } else if (it != leafByNodeName.end()) {
+            add(KUEUE_TAS_AFFINITY_LEAF, {it->second}, true);
+          }
+        } else if (in != v.empty()) {  // In "x" / NotIn "": only unnamed leaves pass
+          if (unnamedLeaves.empty()) never = true;
+          else add(KUEUE_TAS_AFFINITY_LEAF, unnamedLeaves, false);
+        }
+      }
+      if (never) {  // the term matches no leaf
+        g.aff.resize(mark_r);
+        g.aff_vals.resize(mark_v);
+        continue;
+      }
+      if (g.aff.size() == mark_r) {  // the term matches every leaf, so does the selector
+        g.aff.clear();
+        g.aff_vals.clear();
+        return;
+      }
+      term_id++;
+    }
+    g.req.flags |= KUEUE_TAS_F_AFFINITY;
   }
 
   // ---- failure strings ----
@@ -1136,6 +1262,33 @@ static void make_groups(Workload& wl) {
   }
 }
 
+// PodSpec.Affinity.NodeAffinity.RequiredDuringSchedulingIgnoredDuringExecution
+// in its Kubernetes JSON shape; nullopt when any step is absent or null.
+static std::optional<labelsel::RequiredAffinity> parse_required_affinity(const kjson::Node& aff) {
+  if (aff.type != kjson::Node::kObject) return std::nullopt;
+  const kjson::Node& na = aff["nodeAffinity"];
+  if (na.type != kjson::Node::kObject) return std::nullopt;
+  const kjson::Node& req = na["requiredDuringSchedulingIgnoredDuringExecution"];
+  if (req.type != kjson::Node::kObject) return std::nullopt;
+  auto exprs = [](const kjson::Node& arr) {
+    std::vector<labelsel::Expr> out;
+    for (auto& r : arr.items) {
+      labelsel::Expr e;
+      e.key = r["key"].s();
+      e.op = r["operator"].s();
+      if (r["values"].type == kjson::Node::kArray) {
+        e.values.emplace();
+        for (auto& v : r["values"].items) e.values->push_back(v.s());
+      }
+      out.push_back(std::move(e));
+    }
+    return out;
+  };
+  labelsel::RequiredAffinity terms;
+  for (auto& t : req["nodeSelectorTerms"].items) terms.push_back({exprs(t["matchExpressions"]), exprs(t["matchFields"])});
+  return terms;
+}
+
 static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
   std::vector<TASPodSetRequests> out;
   for (auto& ps : arr.items) {
@@ -1165,6 +1318,7 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
       for (auto& kv : ps["nodeSelector"].fields) m[kv.first] = kv.second.s();
       r.nodeSelector = m;
     }
+    r.affinity = parse_required_affinity(ps["affinity"]);
     out.push_back(std::move(r));
   }
   return out;
@@ -1187,6 +1341,8 @@ struct Evaluator {
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
+  std::vector<kueue_tas_affinity_req> aff;
+  std::vector<int32_t> affv;
   std::vector<kueue_tas_eval_out> outs;
   std::vector<int64_t> offsets;
   std::vector<int32_t> entries, taint_counts, res_counts;
@@ -1197,6 +1353,8 @@ struct Evaluator {
   uint64_t p0_gen = 0;
   std::vector<kueue_tas_eval_req> p0_reqs;
   std::vector<int32_t> p0_taint;
+  std::vector<kueue_tas_affinity_req> p0_aff;
+  std::vector<int32_t> p0_affv;
   std::vector<std::pair<size_t, GroupEval*>> p0_batch, p0_early;
   std::vector<size_t> used;  // results set per workload in this run
 
@@ -1223,10 +1381,13 @@ struct Evaluator {
   void build_pass(std::vector<Workload>& wls, size_t pass, const std::vector<char>& done,
                   const std::vector<std::map<int32_t, std::map<int32_t, int64_t>>>& assumedBy,
                   std::vector<kueue_tas_eval_req>& rq, std::vector<int32_t>& tt, std::vector<kueue_tas_assumed>& as,
+                  std::vector<kueue_tas_affinity_req>& af, std::vector<int32_t>& afv,
                   std::vector<std::pair<size_t, GroupEval*>>& bt, std::vector<std::pair<size_t, GroupEval*>>& early) {
     rq.clear();
     tt.clear();
     as.clear();
+    af.clear();
+    afv.clear();
     bt.clear();
     early.clear();
     std::map<std::vector<int32_t>, int32_t> rowOff;
@@ -1245,6 +1406,16 @@ struct Evaluator {
         tt.insert(tt.end(), g.taint_row.begin(), g.taint_row.end());
       }
       q.taint_table = it->second;
+      q.affinity_begin = int32_t(af.size());
+      if (q.flags & KUEUE_TAS_F_AFFINITY) {  // rebase the group's requirements into the batch tables
+        const int32_t vb = int32_t(afv.size());
+        for (auto r : g.aff) {
+          r.begin += vb;
+          af.push_back(r);
+        }
+        afv.insert(afv.end(), g.aff_vals.begin(), g.aff_vals.end());
+      }
+      q.affinity_end = int32_t(af.size());
       q.assumed_begin = int32_t(as.size());
       if (base && !(*base)[w].empty()) {  // merge the base overlay with the group's assumed usage
         const Overlay& b = (*base)[w];
@@ -1308,21 +1479,25 @@ struct Evaluator {
     for (size_t pass = 0; pass < maxGroups; pass++) {
       const std::vector<kueue_tas_eval_req>* rq = &reqs;
       const std::vector<int32_t>* tt = &taint_table;
+      const std::vector<kueue_tas_affinity_req>* af = &aff;
+      const std::vector<int32_t>* afv = &affv;
       const std::vector<std::pair<size_t, GroupEval*>>* bt = &batch;
       const std::vector<std::pair<size_t, GroupEval*>>* ea = &early;
       if (pass == 0 && precompiled && !base) {  // no assumed usage yet: reuse the compiled first pass
         if (p0_for != &wls || p0_gen != snap->compile_gen) {
-          build_pass(wls, 0, done, assumedBy, p0_reqs, p0_taint, assumed, p0_batch, p0_early);
+          build_pass(wls, 0, done, assumedBy, p0_reqs, p0_taint, assumed, p0_aff, p0_affv, p0_batch, p0_early);
           p0_for = &wls;
           p0_gen = snap->compile_gen;
         }
         rq = &p0_reqs;
         tt = &p0_taint;
+        af = &p0_aff;
+        afv = &p0_affv;
         bt = &p0_batch;
         ea = &p0_early;
         assumed.clear();
       } else {
-        build_pass(wls, pass, done, assumedBy, reqs, taint_table, assumed, batch, early);
+        build_pass(wls, pass, done, assumedBy, reqs, taint_table, assumed, aff, affv, batch, early);
       }
       for (auto& we : *ea) {
         for (auto* m : we.second->members)
@@ -1343,7 +1518,7 @@ struct Evaluator {
       const bool packed = (snap->cfg.flags & KUEUE_TAS_CFG_PACKED_ENTRIES) != 0;
       if (packed && entries.size() < 2 * 64 * n) entries.resize(2 * 64 * n);
       rc = kueue_tas_eval_batch(snap->ctx, rq->data(), n, tt->data(), tt->size(), int32_t(T), assumed.data(),
-                                assumed.size(), outs.data(), offsets.data(), packed ? entries.data() : nullptr,
+                                assumed.size(), af->data(), af->size(), afv->data(), afv->size(), outs.data(), offsets.data(), packed ? entries.data() : nullptr,
                                 packed ? entries.size() / 2 : 0, taint_counts.data(), res_counts.data());
       if (rc == KUEUE_TAS_EOVERFLOW && packed) {
         entries.resize(size_t(offsets[n]) * 2 + 2);

@@ -41,6 +41,8 @@ struct DevEval {
   int32_t taint_table;
   int32_t assumed_begin;
   int32_t assumed_end;
+  int32_t aff_begin;      // required node affinity requirements [aff_begin, aff_end) (KUEUE_TAS_F_AFFINITY)
+  int32_t aff_end;
   int32_t num_layers;
   int32_t layer_level[KUEUE_TAS_MAX_LAYERS];
   int32_t layer_size[KUEUE_TAS_MAX_LAYERS];
@@ -116,10 +118,12 @@ struct DevBatch {
   const DevTerm* terms;
   const int32_t* taint_table;
   const kueue_tas_assumed* assumed;
+  const kueue_tas_affinity_req* aff;  // compiled required node affinity (kueue_tas.h)
+  const int32_t* aff_vals;            // their sorted value ids
   int32_t n;
   int32_t num_taints;
   int32_t num_profiles;    // taint-profile rows per eval in taint_table
-  int32_t nstat;           // 1 + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
+  int32_t nstat;           // kStatFixed + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_lim)
@@ -133,6 +137,7 @@ struct DevBatch {
   int32_t* taint_counts;   // [n][num_taints]
   int32_t* res_counts;     // [n][R]
   int32_t* sel_counts;     // [n]
+  int32_t* aff_counts;     // [n]
   kueue_tas_eval_out* out; // [n]
   int32_t* entries;        // [n][entry_cap][2]
   int32_t entry_cap;

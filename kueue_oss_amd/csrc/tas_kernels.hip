@@ -173,7 +173,10 @@ __device__ __forceinline__ Key key_wl(bool lfc, int32_t ls, int32_t sswl, int32_
 constexpr int kFillThreads = 256;
 constexpr int kEvalsPerBlock = 16;
 
-enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3 };
+enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3, EX_AFFINITY = 4 };
+// ExclusionStats slots of the LDS / per-block partials: [0] nodeSelector,
+// [1] affinity, then one per taint string, then one per resource column.
+constexpr int kStatFixed = 2;
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -192,6 +195,45 @@ __device__ __forceinline__ DevTerm uni_term(const DevTerm& t) {
   u.pow2 = uint8_t(uni(t.pow2));
   u.neg = uint8_t(uni(t.neg));
   return u;
+}
+
+// Sorted-set membership of a per-lane id in a wave-uniform id list.
+__device__ __forceinline__ bool sorted_contains(const int32_t* v, int len, int32_t x) {
+  int lo = 0, hi = len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < len && v[lo] == x;
+}
+
+// Required node affinity of one leaf (fillInCounts :1605-1610):
+// nodeaffinity.NodeSelector.Match (nodeaffinity.go:84-103, :190-201) with
+// the terms ORed and each term's requirements ANDed; a compiled requirement
+// (host: labels.Requirement / fields selector folded against the snapshot's
+// label dictionaries) is "the leaf's id is in a sorted set" XOR negate.
+// [rb, re) is wave-uniform; an empty range matches no leaf (no terms).
+template <class LabelAt>
+__device__ __forceinline__ bool affinity_match(const DevBatch& b, int rb, int re, int leaf, LabelAt label_at) {
+  if (rb >= re) return false;
+  bool any = false, cur = true;
+  int term = uni(b.aff[rb].term);
+  for (int r = rb; r < re; r++) {
+    const int t = uni(b.aff[r].term);
+    if (t != term) {
+      any = any || cur;
+      cur = true;
+      term = t;
+    }
+    if (cur) {
+      const int col = uni(b.aff[r].col);
+      const int32_t v = col < 0 ? int32_t(leaf) : label_at(col);
+      const bool in = sorted_contains(b.aff_vals + uni(b.aff[r].begin), uni(b.aff[r].len), v);
+      cur = in != (uni(b.aff[r].negate) != 0);
+    }
+  }
+  return any || cur;
 }
 
 // Requests.CountIn / CountInWithLimitingResource over up to MAXT terms held in
@@ -297,6 +339,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
             }
           }
         }
+        if (kind == EX_NONE && (flags & KUEUE_TAS_F_AFFINITY) &&
+            !affinity_match(b, uni(ev.aff_begin), uni(ev.aff_end), leaf,
+                            [&](int col) { return s.label_values[int64_t(col) * N + leaf]; }))
+          kind = EX_AFFINITY;
       }
       if (kind == EX_NONE) {
         const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
@@ -377,6 +423,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     // ExclusionStats (:1579-1634), aggregated per wave before the atomics.
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    const uint64_t affm = ballot(kind == EX_AFFINITY);
+    if (lane == 0 && affm) atomicAdd(&b.aff_counts[eid], __popcll(affm));
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
@@ -412,7 +460,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 // Per-eval parameters of a fill chunk, staged in LDS once per block so the
 // per-eval loop has no dependent global loads (eval record -> taint row).
 struct FillEvalParams {
-  int32_t eid, taint_off, nsel, slice_size, slice_level, inner, pad[2];  // inner: ssal of the leaf level
+  int32_t eid, taint_off, nsel, slice_size, slice_level, inner;  // inner: ssal of the leaf level
+  int32_t aff_begin, aff_end;  // required node affinity requirements; aff_begin < 0: none
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
@@ -422,7 +471,7 @@ constexpr int kStagedLabels = 4;     // label columns held in registers (more: r
 // partials (DevBatch::fill_stats), summed by fill_stats_reduce_kernel: no
 // global atomics on a handful of hot addresses from every wave of the grid
 // (device-scope atomics from all XCDs serialize at the memory side).
-constexpr int kMaxFillStats = 64;  // 1 (nodeSelector) + taints + resource columns; more: global atomics
+constexpr int kMaxFillStats = 64;  // kStatFixed + taints + resource columns; more: global atomics
 
 template <int NS>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
@@ -458,6 +507,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     P.slice_size = ev.slice_size;
     P.slice_level = ev.slice_level;
     P.inner = ev.ssal[s.L - 1];
+    const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
+    P.aff_begin = aff ? ev.aff_begin : -1;
+    P.aff_end = aff ? ev.aff_end : -1;
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       P.sel_col[k] = ev.sel_col[k];
       P.sel_val[k] = ev.sel_val[k];
@@ -498,6 +550,15 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   int32_t lab[kStagedLabels];
 #pragma unroll
   for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
+  auto label_at = [&](int col) -> int32_t {  // col is wave-uniform
+    if (col < kStagedLabels) {
+      int32_t v = lab[0];
+#pragma unroll
+      for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+      return v;
+    }
+    return s.label_values[int64_t(col) * N + leaf];
+  };
 
   // ---- the chunk's request signature (first member): counts once per leaf ----
   int32_t state0 = 0, swl0 = 0, ls0 = 0;
@@ -617,6 +678,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
             }
           }
         }
+        const int ab = uni(P.aff_begin);
+        if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(P.aff_end), leaf, label_at)) kind = EX_AFFINITY;
       }
       if (kind == EX_NONE) {
         state = state0;
@@ -706,13 +769,18 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
       else atomicAdd(&b.sel_counts[eid], __popcll(selm));
     }
+    const uint64_t affm = ballot(kind == EX_AFFINITY);
+    if (lane == 0 && affm) {
+      if (lds_stats) atomicAdd(&sh_stats[e][1], __popcll(affm));
+      else atomicAdd(&b.aff_counts[eid], __popcll(affm));
+    }
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
       int tid = __shfl(id, src, 64);
       uint64_t mm = ballot(kind == EX_TAINT && id == tid);
       if (lane == 0) {
-        if (lds_stats) atomicAdd(&sh_stats[e][1 + tid], __popcll(mm));
+        if (lds_stats) atomicAdd(&sh_stats[e][kStatFixed + tid], __popcll(mm));
         else atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
       }
       tm &= ~mm;
@@ -723,7 +791,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       int rid = __shfl(id, src, 64);
       uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
       if (lane == 0) {
-        if (lds_stats) atomicAdd(&sh_stats[e][1 + b.num_taints + rid], __popcll(mm));
+        if (lds_stats) atomicAdd(&sh_stats[e][kStatFixed + b.num_taints + rid], __popcll(mm));
         else atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
       }
       rm &= ~mm;
@@ -747,6 +815,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t sh_toff[kEvalsPerBlock];
   __shared__ int32_t sh_nsel[kEvalsPerBlock];
+  __shared__ int32_t sh_aff[kEvalsPerBlock][2];
   __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
@@ -758,6 +827,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
     sh_toff[threadIdx.x] = ev.taint_table;
     sh_nsel[threadIdx.x] = ev.nsel;
+    const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
+    sh_aff[threadIdx.x][0] = aff ? ev.aff_begin : -1;
+    sh_aff[threadIdx.x][1] = aff ? ev.aff_end : -1;
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       sh_sel[threadIdx.x][2 * k] = ev.sel_col[k];
       sh_sel[threadIdx.x][2 * k + 1] = ev.sel_val[k];
@@ -780,6 +852,15 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   int32_t lab[kStagedLabels];
 #pragma unroll
   for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
+  auto label_at = [&](int col) -> int32_t {  // col is wave-uniform
+    if (col < kStagedLabels) {
+      int32_t v = lab[0];
+#pragma unroll
+      for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+      return v;
+    }
+    return s.label_values[int64_t(col) * N + leaf];
+  };
   for (int e = 0; e < ne; e++) {
     int kind = EX_NONE, id = -1;
     if (valid) {
@@ -809,6 +890,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
             }
           }
         }
+        const int ab = uni(sh_aff[e][0]);
+        if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(sh_aff[e][1]), leaf, label_at)) kind = EX_AFFINITY;
       }
       if (kind == EX_NONE && lim >= 0) {
         kind = EX_RESOURCE;
@@ -817,18 +900,20 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     }
     const uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) atomicAdd(&sh_stats[e][0], __popcll(selm));
+    const uint64_t affm = ballot(kind == EX_AFFINITY);
+    if (lane == 0 && affm) atomicAdd(&sh_stats[e][1], __popcll(affm));
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       const int tid = __shfl(id, __ffsll((unsigned long long)tm) - 1, 64);
       const uint64_t mm = ballot(kind == EX_TAINT && id == tid);
-      if (lane == 0) atomicAdd(&sh_stats[e][1 + tid], __popcll(mm));
+      if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + tid], __popcll(mm));
       tm &= ~mm;
     }
     uint64_t rm = ballot(kind == EX_RESOURCE);
     while (rm) {
       const int rid = __shfl(id, __ffsll((unsigned long long)rm) - 1, 64);
       const uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
-      if (lane == 0) atomicAdd(&sh_stats[e][1 + b.num_taints + rid], __popcll(mm));
+      if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + b.num_taints + rid], __popcll(mm));
       rm &= ~mm;
     }
   }
@@ -857,8 +942,9 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
     for (int m = m0 - 1 + lane; m < m1; m += kWave) {  // m0 - 1: the rep itself
       const int d = m < m0 ? eid : b.cls_members[m];
       if (k == 0) b.sel_counts[d] = acc;
-      else if (k <= b.num_taints) b.taint_counts[int64_t(d) * b.num_taints + (k - 1)] = acc;
-      else b.res_counts[int64_t(d) * b.nstat_R + (k - 1 - b.num_taints)] = acc;
+      else if (k == 1) b.aff_counts[d] = acc;
+      else if (k < kStatFixed + b.num_taints) b.taint_counts[int64_t(d) * b.num_taints + (k - kStatFixed)] = acc;
+      else b.res_counts[int64_t(d) * b.nstat_R + (k - kStatFixed - b.num_taints)] = acc;
     }
   }
 }
@@ -1079,7 +1165,10 @@ __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, c
       b.taint_counts[int64_t(dst) * b.num_taints + i] = b.taint_counts[int64_t(src) * b.num_taints + i];
     for (int i = threadIdx.x; i < s.R; i += blockDim.x)
       b.res_counts[int64_t(dst) * s.R + i] = b.res_counts[int64_t(src) * s.R + i];
-    if (threadIdx.x == 0) b.sel_counts[dst] = b.sel_counts[src];
+    if (threadIdx.x == 0) {
+      b.sel_counts[dst] = b.sel_counts[src];
+      b.aff_counts[dst] = b.aff_counts[src];
+    }
   }
 }
 

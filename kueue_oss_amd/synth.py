@@ -550,3 +550,95 @@ def random_internal_assignment(rng: random.Random):
     domains = [{"values": [per_level[k][j] for k in range(nl)], "count": c0 if same else rng.randint(1, 9)}
                for j in range(n)]
     return {"levels": levels, "domains": domains}
+
+
+_AFF_KEYS = ["zone", "gpu-type", "num", HOST, "rack", "missing"]
+
+
+def _aff_expr(rng, node_names, valid=True):
+    key = rng.choice(_AFF_KEYS)
+    op = rng.choice(["In", "In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"])
+    pool = {"zone": ["a", "b", "c"], "gpu-type": ["t1", "t2", "t9"], "num": ["1", "5", "12", "007", "x"],
+            HOST: node_names[:6] + ["nope"], "rack": ["r1", "r2", "r3"], "missing": ["a"]}[key]
+    if op in ("In", "NotIn"):
+        values = rng.sample(pool, rng.randint(1, min(3, len(pool))))
+    elif op in ("Exists", "DoesNotExist"):
+        values = None if rng.random() < 0.5 else []
+    else:
+        values = [rng.choice(["0", "3", "6", "10", "-1", "+4", "9223372036854775807"])]
+    if not valid:
+        k = rng.random()
+        if k < 0.3:
+            op = rng.choice(["Foo", "", "in"])
+        elif k < 0.5:
+            key = rng.choice(["-bad", "a/b/c", "UPPER/x", "/x", "x" * 70, "ok.io/"])
+        elif k < 0.7:
+            values = [] if op in ("In", "NotIn") else ["a", "b"]
+        elif k < 0.85:
+            values = ["bad value!", "<x>"] if op in ("In", "NotIn") else ["1.5"]
+        else:
+            values = ["y" * 64]
+    return {"key": key, "operator": op, "values": values}
+
+
+def _aff_field(rng, node_names, valid=True):
+    op = rng.choice(["In", "NotIn"])
+    key = "metadata.name" if rng.random() < 0.85 else "spec.other"
+    v = rng.choice(node_names + ["", "ghost"]) if node_names else rng.choice(["", "ghost"])
+    values = [v]
+    if not valid:
+        if rng.random() < 0.5:
+            op = rng.choice(["Exists", "Gt"])
+        else:
+            values = [v, "other"] if rng.random() < 0.5 else []
+    return {"key": key, "operator": op, "values": values}
+
+
+def random_affinity(rng: random.Random, node_names: list, invalid_p: float = 0.1):
+    """PodSpec affinity with required node affinity (nodeSelectorTerms ORed,
+    matchExpressions / matchFields ANDed; nodeaffinity.go:84-201): label
+    operators In/NotIn/Exists/DoesNotExist/Gt/Lt on present, absent and
+    numeric labels, metadata.name fields, empty terms, an empty term list,
+    and (with probability invalid_p) one malformed requirement whose
+    validation error becomes the failure reason (tas_flavor_snapshot.go:889-897)."""
+    terms = []
+    for _ in range(rng.choice([0, 1, 1, 1, 2, 2, 3])):
+        r = rng.random()
+        t = {}
+        if r < 0.08:
+            pass  # empty term: skipped
+        else:
+            if r < 0.85:
+                t["matchExpressions"] = [_aff_expr(rng, node_names) for _ in range(rng.randint(1, 3))]
+            if r >= 0.6:
+                t["matchFields"] = [_aff_field(rng, node_names) for _ in range(rng.randint(1, 2))]
+        terms.append(t)
+    if terms and rng.random() < invalid_p:
+        t = rng.choice(terms)
+        if rng.random() < 0.7:
+            t.setdefault("matchExpressions", []).append(_aff_expr(rng, node_names, valid=False))
+        else:
+            t.setdefault("matchFields", []).append(_aff_field(rng, node_names, valid=False))
+    return {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": terms}}}
+
+
+def affinity_case(rng: random.Random, max_nodes: int = 60, invalid_p: float = 0.1) -> dict:
+    """random_case whose nodes carry a numeric label ("num") and whose PodSets
+    set required node affinity (and sometimes an invalid nodeSelector)."""
+    case = random_case(rng, max_nodes=max_nodes)
+    for n in case["nodes"]:
+        if rng.random() < 0.6:
+            n["labels"]["num"] = rng.choice(["0", "2", "5", "11", "-3", "+7", "08", "abc"])
+        if rng.random() < 0.03:
+            n["name"] = ""
+    names = [n["name"] for n in case["nodes"] if n["name"]]
+    for ps in case["podSets"]:
+        r = rng.random()
+        if r < 0.8:
+            ps["affinity"] = random_affinity(rng, names, invalid_p)
+        elif r < 0.85:
+            ps["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": None}}
+        if rng.random() < invalid_p / 2:
+            ps["nodeSelector"] = {rng.choice(["-bad", "ok", "a/b/c"]): rng.choice(["v!", "fine", ""])}
+    case["name"] = "affinity"
+    return case

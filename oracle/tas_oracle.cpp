@@ -14,6 +14,7 @@
 //   /root/reference/pkg/resources/requests.go                    (CountIn arithmetic)
 //   /root/reference/vendor/k8s.io/api/core/v1/toleration.go, taint.go
 //   /root/reference/vendor/k8s.io/component-helpers/scheduling/corev1/helpers.go
+//   label selectors and required node affinity: k8s_selectors.h
 // Each function cites the reference file:line it follows.
 //
 // Parity pinning: tests/test_oracle_goldens.py checks this oracle against every
@@ -26,9 +27,10 @@
 //   * CountInWithLimitingResource with >=2 missing requested keys returns the
 //     first missing key in Go map order (random); we return the smallest name.
 //   * Requests maps iterate in sorted key order (std::map).
+//   * ValidatedSelectorFromSet with >=2 invalid entries reports the first in
+//     Go map order (random); we report the smallest key's (k8s_selectors.h).
 // Out of scope (returns an error reason "unsupported: ..."):
-//   TASBalancedPlacement, elastic workloads, node replacement, node affinity,
-//   nodeSelector validation errors.
+//   TASBalancedPlacement, elastic workloads, node replacement.
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -44,6 +46,7 @@
 #include <thread>
 #include <vector>
 
+#include "k8s_selectors.h"
 #include "mini_json.h"
 
 namespace oracle {
@@ -204,6 +207,8 @@ struct PodSetRequest {  // TASPodSetRequests (tas_flavor_snapshot.go:356-367)
   std::optional<std::string> podSetGroupName;
   std::vector<Toleration> tolerations;
   std::optional<std::map<std::string, std::string>> nodeSelector;
+  // affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution (podset.go:104-144)
+  std::optional<k8s::NodeSelector> requiredAffinity;
 };
 struct DomainAssignment { std::vector<std::string> values; int32_t count; };
 struct TopologyAssignment { std::vector<std::string> levels; std::vector<DomainAssignment> domains; };
@@ -285,6 +290,7 @@ struct Requirements {  // topologyAssignmentPodRequirements :434-443
   std::map<std::string, Requests>* assumedUsage = nullptr;
   std::vector<Toleration> tolerations;
   std::map<std::string, std::string> selector;  // empty = Everything
+  std::optional<k8s::ParsedNodeSelector> affinitySelector;
   bool simulateEmpty = false;
 };
 
@@ -524,7 +530,11 @@ class Snapshot {
           st.stats.nodeSelector++;
           continue;
         }
-        // affinity: not supported (see header)
+        // required node affinity against leaf.node.toNode() (:1605-1610; tas_flavor.go:196-209)
+        if (rq.affinitySelector && !rq.affinitySelector->match(leaf->node->labels, leaf->node->name)) {
+          st.stats.affinity++;
+          continue;
+        }
       }
       // requiredReplacementDomain is always "" on this path (node replacement is out of scope)
       Requests remaining = leaf->freeCapacity;
@@ -891,7 +901,18 @@ class Snapshot {
     if (gates.multiLayer && !st.sliceSizeAtLevel.empty()) st.multiLayerConstraints = workers.topologyRequest->constraints;
     rq.tolerations = workers.tolerations;
     rq.tolerations.insert(rq.tolerations.end(), tolerations.begin(), tolerations.end());
-    if (isLowestLevelNode && workers.nodeSelector) rq.selector = *workers.nodeSelector;
+    if (isLowestLevelNode && workers.nodeSelector) {  // :879-887
+      std::string e = k8s::validated_selector_from_set(*workers.nodeSelector);
+      if (!e.empty()) return "invalid node selectors: " + k8s::go_map_string(*workers.nodeSelector) + ", reason: " + e;
+      rq.selector = *workers.nodeSelector;
+    }
+    if (workers.requiredAffinity) {  // :889-897
+      k8s::ParsedNodeSelector ns;
+      std::string e = k8s::new_node_selector(*workers.requiredAffinity, &ns);
+      if (!e.empty())
+        return "invalid affinity node selectors: " + k8s::node_selector_string(*workers.requiredAffinity) + ", reason: " + e;
+      rq.affinitySelector = std::move(ns);
+    }
 
     fill_in_counts(rq, st);
 
@@ -1027,6 +1048,35 @@ static Gates parse_gates(const ojson::Value& v) {
   return g;
 }
 
+// PodSpec.Affinity.NodeAffinity.RequiredDuringSchedulingIgnoredDuringExecution
+// (k8s JSON shape); absent / null at any step -> no required affinity.
+static std::optional<k8s::NodeSelector> parse_required_affinity(const ojson::Value& aff) {
+  if (aff.kind != ojson::Value::Obj) return std::nullopt;
+  const ojson::Value* na = aff.get("nodeAffinity");
+  if (!na || na->kind != ojson::Value::Obj) return std::nullopt;
+  const ojson::Value* req = na->get("requiredDuringSchedulingIgnoredDuringExecution");
+  if (!req || req->kind != ojson::Value::Obj) return std::nullopt;
+  k8s::NodeSelector ns;
+  auto reqs = [](const ojson::Value* arr) {
+    std::vector<k8s::NodeSelectorRequirement> out;
+    if (!arr || arr->kind != ojson::Value::Arr) return out;
+    for (auto& r : arr->a) {
+      k8s::NodeSelectorRequirement q;
+      if (auto k = r.get("key")) q.key = k->as_str();
+      if (auto o = r.get("operator")) q.op = o->as_str();
+      if (auto v = r.get("values"); v && v->kind == ojson::Value::Arr) {
+        q.values.emplace();
+        for (auto& x : v->a) q.values->push_back(x.as_str());
+      }
+      out.push_back(std::move(q));
+    }
+    return out;
+  };
+  if (auto terms = req->get("nodeSelectorTerms"); terms && terms->kind == ojson::Value::Arr)
+    for (auto& t : terms->a) ns.terms.push_back({reqs(t.get("matchExpressions")), reqs(t.get("matchFields"))});
+  return ns;
+}
+
 static std::vector<PodSetRequest> parse_podsets(const ojson::Value& arr) {
   std::vector<PodSetRequest> out;
   for (auto& ps : arr.a) {
@@ -1056,6 +1106,7 @@ static std::vector<PodSetRequest> parse_podsets(const ojson::Value& arr) {
       for (auto& kv : ns.o) m[kv.first] = kv.second.as_str();
       r.nodeSelector = m;
     }
+    if (auto aff = ps.get("affinity")) r.requiredAffinity = parse_required_affinity(*aff);
     out.push_back(std::move(r));
   }
   return out;

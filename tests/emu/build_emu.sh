@@ -19,7 +19,7 @@ sed -e 's/extern __shared__ Key lds_all\[\];/Key* lds_all = static_cast<Key*>(em
   "$CSRC/tas_kernels.hip" > "$OUT/src/tas_kernels.hip"
 grep -q 'emu::wave_barrier(); own(g);' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
 grep -q '= v; emu::wave_barrier();' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
-cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$OUT/src/"
+cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$CSRC/label_selectors.h" "$OUT/src/"
 sed 's#"../../include/kueue_tas.h"#"kueue_tas.h"#' "$CSRC/tas_internal.h" > "$OUT/src/tas_internal.h"
 cp "$ROOT/include/kueue_tas.h" "$OUT/src/"
 cp "$CSRC/tas_device.hip" "$OUT/src/tas_device.cpp"

@@ -10,7 +10,6 @@ import pytest
 
 import oracle_lib
 from kueue_oss_amd import TASFlavorSnapshot, synth
-from test_emu_parity import emu_lib  # noqa: F401  (fixture)
 
 
 def _sessions(seed, n, lib=None, gen=None):

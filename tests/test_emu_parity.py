@@ -16,16 +16,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 EMU_SO = os.path.join(HERE, "emu", "_build", "libkueue_tas_emu.so")
 
 
-@pytest.fixture(scope="module")
-def emu_lib():
-    srcs = [os.path.join(HERE, "..", "kueue_oss_amd", "csrc", f) for f in
-            ("tas_kernels.hip", "tas_device.hip", "tas_host.cpp", "tas_internal.h", "json_reader.h")]
-    srcs += [os.path.join(HERE, "emu", f) for f in ("hip_emu.cpp", "build_emu.sh", "hip/hip_runtime.h")]
-    if not os.path.exists(EMU_SO) or os.path.getmtime(EMU_SO) < max(os.path.getmtime(s) for s in srcs):
-        subprocess.run([os.path.join(HERE, "emu", "build_emu.sh")], check=True, capture_output=True)
-    return native.load_library(EMU_SO)
-
-
 @pytest.mark.parametrize("list_cap", [0, 64])
 def test_emulated_kernels_match_goldens(emu_lib, list_cap):
     bad = []

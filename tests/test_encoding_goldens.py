@@ -33,7 +33,6 @@ def test_oracle_internal_from(case):
 
 # ---- the device encoder (explicit strings) and the host decoder ----
 from kueue_oss_amd import TASFlavorSnapshot, synth  # noqa: E402
-from test_emu_parity import emu_lib  # noqa: E402,F401  (fixture)
 
 _TINY = {"name": "enc", "levels": ["kubernetes.io/hostname"],
          "nodes": [{"name": "n0", "labels": {"kubernetes.io/hostname": "n0"}, "allocatable": {"cpu": 1},

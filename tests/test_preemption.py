@@ -13,7 +13,6 @@ import pytest
 
 import oracle_lib
 from kueue_oss_amd import TASFlavorSnapshot, synth
-from test_emu_parity import emu_lib  # noqa: F401  (fixture)
 
 
 def preemption_case(rng, gen=None):

@@ -14,7 +14,6 @@ import pytest
 
 import oracle_lib
 from kueue_oss_amd import TASFlavorSnapshot, synth
-from test_emu_parity import emu_lib  # noqa: F401  (fixture)
 
 GI = 1 << 30
 
