@@ -383,6 +383,10 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
 
+/* Every result of the last run_compiled as {"results": [[{"name",
+ * "assignment","reason"}...] per compiled workload]} (kueue_tas_free). */
+int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json);
+
 /* Per-workload compact results of the last run_compiled into buf (int32):
  * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
  * 4 int32 per workload (used for the cross-rank all-gather). */

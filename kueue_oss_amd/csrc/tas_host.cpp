@@ -16,6 +16,7 @@
 // (tas_kernels.hip).  This layer never evaluates a placement on the CPU: if the
 // device library or a GPU is unavailable, creation fails loudly.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -268,6 +269,17 @@ class FlavorSnapshot {
   int L() const { return int(levelKeys.size()); }
 
   // ---- construction (harness semantics: tas_cache_test.go:6270-6300) ----
+  // The snapshot is assembled from the caches' state, which events keep
+  // current: nodesCache (Ready && !Unschedulable nodes by name, first-seen
+  // order; tas_nodes_cache.go:38-50), nonTasUsageCache (podUsage/nodeUsage,
+  // tas_non_tas_pod_cache.go:46-120) and the TAS usage per domain
+  // (TASFlavorCache.updateUsage, tas_flavor.go:154-171, plus the
+  // AddUsage/RemoveUsage updates since).  A rebuild re-assembles from that
+  // state: nothing is re-parsed and no event log is kept.
+  std::vector<std::string> nodeCacheOrder;
+  std::unordered_map<std::string, NodeInfo> nodeCache;
+  std::map<std::string, Requests> usageByDomain;
+
   void build(const kjson::Node& c) {
     for (auto& l : c["levels"].items) levelKeys.push_back(l.s());
     if (levelKeys.empty()) throw std::runtime_error("no topology levels");
@@ -282,32 +294,74 @@ class FlavorSnapshot {
     if (auto p = fg.find("TASBalancedPlacement")) gates.balanced = p->b();
     if (auto p = fg.find("ElasticJobsViaWorkloadSlicesWithTAS")) gates.elastic = p->b();
     for (auto& kv : c["nodeLabels"].fields) flavorLabels[kv.first] = kv.second.s();
-
-    // nodesCache.sync (Ready && !Unschedulable) keyed by name, then find (NodeMatchesFlavor)
-    std::vector<std::string> order;
-    std::map<std::string, const kjson::Node*> byName;
-    for (auto& n : c["nodes"].items) {
-      const std::string& name = n["name"].s();
-      bool ready = false;
-      for (auto& cond : n["conditions"].items)
-        if (cond["type"].s() == "Ready") {
-          ready = cond["status"].s() == "True";
-          break;
-        }
-      if (!n["unschedulable"].b() && ready) {
-        if (!byName.count(name)) order.push_back(name);
-        byName[name] = &n;
-      } else if (byName.count(name)) {
-        byName.erase(name);
-        order.erase(std::find(order.begin(), order.end(), name));
-      }
+    for (auto& n : c["nodes"].items) sync_node(n);
+    for (auto& u : c["tasUsage"].items) {
+      std::string id;
+      for (size_t k = 0; k < u["values"].items.size(); k++) id += (k ? "," : "") + u["values"].items[k].s();
+      const int64_t cnt = u["count"].i64();
+      Requests& dst = usageByDomain[id];
+      for (auto& kv : u["singlePodRequests"].fields) dst[kv.first] = add64(dst[kv.first], mul64(kv.second.i64(), cnt));
+      dst["pods"] = add64(dst["pods"], cnt);
     }
-    nodes.reserve(order.size());
-    for (auto& name : order) {
-      const kjson::Node& n = *byName[name];
-      NodeInfo ni;
-      ni.name = name;
-      for (auto& kv : n["labels"].fields) ni.labels[kv.first] = kv.second.s();
+    podUsage.clear();
+    nodeUsage.clear();
+    for (auto& p : c["pods"].items) apply_pod(p, nullptr);
+    assemble();
+  }
+
+  // nodesCache.sync (tas_nodes_cache.go:38-50): a Ready, schedulable node is
+  // (re)placed under its name, any other node leaves the cache.
+  static NodeInfo parse_node(const kjson::Node& n, bool* ready, bool* unschedulable) {
+    NodeInfo ni;
+    ni.name = n["name"].s();
+    *ready = false;
+    for (auto& cond : n["conditions"].items)
+      if (cond["type"].s() == "Ready") {
+        *ready = cond["status"].s() == "True";
+        break;
+      }
+    *unschedulable = n["unschedulable"].b();
+    for (auto& kv : n["labels"].fields) ni.labels[kv.first] = kv.second.s();
+    for (auto& t : n["taints"].items) ni.taints.push_back({t["key"].s(), t["value"].s(), t["effect"].s()});
+    for (auto& kv : n["allocatable"].fields) ni.allocatable[kv.first] = kv.second.i64();
+    return ni;
+  }
+  void sync_node(const kjson::Node& n) {
+    bool ready, unsched;
+    NodeInfo ni = parse_node(n, &ready, &unsched);
+    auto it = nodeCache.find(ni.name);
+    if (ready && !unsched) {
+      if (it == nodeCache.end()) nodeCacheOrder.push_back(ni.name);
+      nodeCache[ni.name] = std::move(ni);
+    } else if (it != nodeCache.end()) {
+      nodeCacheOrder.erase(std::find(nodeCacheOrder.begin(), nodeCacheOrder.end(), ni.name));
+      nodeCache.erase(it);
+    }
+  }
+  // A new snapshot with this one's settings and cache state (for a rebuild).
+  std::unique_ptr<FlavorSnapshot> fork_state() const {
+    auto ns = std::make_unique<FlavorSnapshot>();
+    ns->topologyName = topologyName;
+    ns->levelKeys = levelKeys;
+    ns->flavorTolerations = flavorTolerations;
+    ns->lowestIsHostname = lowestIsHostname;
+    ns->gates = gates;
+    ns->flavorLabels = flavorLabels;
+    ns->cfg = cfg;
+    ns->nodeCacheOrder = nodeCacheOrder;
+    ns->nodeCache = nodeCache;
+    ns->usageByDomain = usageByDomain;
+    ns->podUsage = podUsage;
+    ns->nodeUsage = nodeUsage;
+    return ns;
+  }
+
+  // TASFlavorCache.snapshot (tas_flavor.go:118-138) over the cache state.
+  void assemble() {
+    nodes.clear();
+    nodes.reserve(nodeCacheOrder.size());
+    for (auto& name : nodeCacheOrder) {  // nodesCache.find: NodeMatchesFlavor (util/tas/node.go:21-33)
+      const NodeInfo& ni = nodeCache.at(name);
       bool match = true;
       for (auto& kv : flavorLabels) {
         auto it = ni.labels.find(kv.first);
@@ -315,10 +369,7 @@ class FlavorSnapshot {
       }
       for (auto& l : levelKeys)
         if (!ni.labels.count(l)) match = false;
-      if (!match) continue;
-      for (auto& t : n["taints"].items) ni.taints.push_back({t["key"].s(), t["value"].s(), t["effect"].s()});
-      for (auto& kv : n["allocatable"].fields) ni.allocatable[kv.first] = kv.second.i64();
-      nodes.push_back(std::move(ni));
+      if (match) nodes.push_back(ni);
     }
     // addNode (:160-195): leaves keyed by hostname or DomainID(levelValues)
     struct LeafTmp {
@@ -421,24 +472,12 @@ class FlavorSnapshot {
       idRank[l].assign(D, 0);
       for (size_t r = 0; r < D; r++) idRank[l][ord[r]] = int32_t(r);
     }
-    // TAS usage (TASFlavorCache.updateUsage, tas_flavor.go:154-171)
-    std::map<std::string, Requests> usage;
-    for (auto& u : c["tasUsage"].items) {
-      std::string id;
-      for (size_t k = 0; k < u["values"].items.size(); k++) id += (k ? "," : "") + u["values"].items[k].s();
-      int64_t cnt = u["count"].i64();
-      Requests& dst = usage[id];
-      for (auto& kv : u["singlePodRequests"].fields) dst[kv.first] = add64(dst[kv.first], mul64(kv.second.i64(), cnt));
-      dst["pods"] = add64(dst["pods"], cnt);
-    }
-    for (auto& kv : usage) {
+    // TAS usage per domain (TASFlavorCache.updateUsage, tas_flavor.go:154-171): leaves only
+    for (auto& kv : usageByDomain) {
       auto it = leafById.find(kv.first);
       if (it != leafById.end()) req_add(tasUsage[it->second], kv.second);
     }
     // non-TAS pods (tas_non_tas_pod_cache.go:46-120)
-    podUsage.clear();
-    nodeUsage.clear();
-    for (auto& p : c["pods"].items) apply_pod(p, nullptr);
     for (auto& kv : nodeUsage) {
       auto it = nodeToLeaf.find(kv.first);
       if (it != nodeToLeaf.end()) req_sub(freeCap[leafById[it->second]], kv.second);
@@ -560,16 +599,9 @@ class FlavorSnapshot {
   bool node_event_in_place(const kjson::Node& n, std::set<int32_t>* touched) {
     auto ix = nodeIdx.find(n["name"].s());
     if (ix == nodeIdx.end()) return false;
-    bool ready = false;
-    for (auto& cond : n["conditions"].items)
-      if (cond["type"].s() == "Ready") {
-        ready = cond["status"].s() == "True";
-        break;
-      }
-    if (!ready || n["unschedulable"].b()) return false;
-    NodeInfo ni;
-    ni.name = n["name"].s();
-    for (auto& kv : n["labels"].fields) ni.labels[kv.first] = kv.second.s();
+    bool ready, unsched;
+    NodeInfo ni = parse_node(n, &ready, &unsched);
+    if (!ready || unsched) return false;
     for (auto& kv : flavorLabels) {
       auto it = ni.labels.find(kv.first);
       if ((it == ni.labels.end() ? std::string() : it->second) != kv.second) return false;
@@ -579,8 +611,6 @@ class FlavorSnapshot {
       auto a = ni.labels.find(l), b = cur.labels.find(l);
       if (a == ni.labels.end() || b == cur.labels.end() || a->second != b->second) return false;
     }
-    for (auto& t : n["taints"].items) ni.taints.push_back({t["key"].s(), t["value"].s(), t["effect"].s()});
-    for (auto& kv : n["allocatable"].fields) ni.allocatable[kv.first] = kv.second.i64();
     const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
     int32_t prof = leafProfile[size_t(leaf)];
     if (lowestIsHostname) {
@@ -595,7 +625,8 @@ class FlavorSnapshot {
         if (c == labelCol.end() || !labelDict[size_t(c->second)].count(kv.second)) return false;
       }
     }
-    // in place
+    // in place (the nodesCache record too, for later rebuilds)
+    nodeCache[ni.name] = ni;
     cur.labels = std::move(ni.labels);
     cur.taints = std::move(ni.taints);
     cur.allocatable = std::move(ni.allocatable);
@@ -661,7 +692,12 @@ class FlavorSnapshot {
     return rc;
   }
 
+  // Column sets are numbered process-wide: compiled requests hold column
+  // indices, so a request compiled against an older set must be recompiled.
+  uint64_t col_gen = 0;
   void set_columns(const std::set<std::string>& names) {
+    static std::atomic<uint64_t> gen_counter{0};
+    col_gen = ++gen_counter;
     cols.assign(names.begin(), names.end());
     colByName.clear();
     for (size_t i = 0; i < cols.size(); i++) colByName[cols[i]] = int32_t(i);
@@ -774,12 +810,16 @@ class FlavorSnapshot {
     std::vector<kueue_tas_delta> deltas;
     bool new_col = false;
     for (auto& u : us) {
-      auto it = leafById.find(u.id);
-      if (it == leafById.end()) continue;
-      const int32_t leaf = it->second;
       Requests tot;
       for (auto& kv : u.single) tot[kv.first] = mul64(kv.second, u.count);
       tot["pods"] = add64(tot["pods"], u.count);
+      {  // the cache's usage per domain, kept for domains that are not leaves (yet)
+        Requests& d = usageByDomain[u.id];
+        for (auto& kv : tot) d[kv.first] = add ? add64(d[kv.first], kv.second) : sub64(d[kv.first], kv.second);
+      }
+      auto it = leafById.find(u.id);
+      if (it == leafById.end()) continue;
+      const int32_t leaf = it->second;
       for (auto& kv : tot) {
         Requests& mine = tasUsage[leaf];
         mine[kv.first] = add ? add64(mine[kv.first], kv.second) : sub64(mine[kv.first], kv.second);
@@ -1921,12 +1961,7 @@ struct kueue_tas_host {
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[4] = {0, 0, 0, 0};
-  // what a rebuild replays: the snapshot document, node and pod event
-  // batches (appended to its node and pod lists, which build() consumes as
-  // event streams) and the usage updates applied since
-  std::string doc;
-  std::vector<std::string> node_batches, pod_batches;
-  std::vector<std::pair<std::vector<FlavorSnapshot::DomainUsage>, bool>> usage_log;
+  uint64_t compiled_cols = 0;  // FlavorSnapshot::col_gen the compiled workloads were compiled against
 };
 
 extern "C" {
@@ -1936,7 +1971,6 @@ kueue_tas_host* kueue_tas_host_create(const char* snapshot_json, const kueue_tas
   try {
     h->snap = std::make_unique<FlavorSnapshot>();
     if (cfg) h->snap->cfg = *cfg;
-    h->doc = snapshot_json;
     kjson::Node c = kjson::parse(snapshot_json);
     h->snap->build(c);
     if (h->snap->upload()) {
@@ -2124,7 +2158,6 @@ int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32
     auto us = FlavorSnapshot::parse_usage(kjson::parse(usage_json));
     int rc = h->snap->update_usage(us, add != 0);
     if (rc) h->err = h->snap->err;
-    else h->usage_log.emplace_back(std::move(us), add != 0);
     return rc;
   } catch (const std::exception& e) {
     h->err = e.what();
@@ -2135,37 +2168,23 @@ int kueue_tas_host_update_usage(kueue_tas_host* h, const char* usage_json, int32
 // Rebuild after a structural node event (a node added, removed, NotReady,
 // cordoned, moved in the topology, or with a new taint profile / label):
 // the reference rebuilds its snapshot every cycle (Cache.Snapshot,
-// snapshot.go:186-191); here the host mirror is rebuilt from the document
-// plus every event since, the usage updates are replayed, the device context
-// is kept and the compiled workloads are recompiled against the new columns.
-static int rebuild(kueue_tas_host* h) {
-  kjson::Node doc = kjson::parse(h->doc.c_str());
-  auto list = [&](const char* key) -> std::vector<kjson::Node>& {
-    for (auto& f : doc.fields)
-      if (f.first == key) {
-        f.second.type = kjson::Node::kArray;
-        return f.second.items;
-      }
-    doc.fields.emplace_back(key, kjson::Node{});
-    doc.fields.back().second.type = kjson::Node::kArray;
-    return doc.fields.back().second.items;
-  };
-  for (auto& b : h->node_batches)
-    for (auto& n : kjson::parse(b.c_str()).items) list("nodes").push_back(n);
-  for (auto& b : h->pod_batches)
-    for (auto& p : kjson::parse(b.c_str()).items) list("pods").push_back(p);
-  auto ns = std::make_unique<FlavorSnapshot>();
-  ns->cfg = h->snap->cfg;
-  ns->build(doc);
+// snapshot.go:186-191); here a new host mirror is assembled from the current
+// cache state (nodesCache with the batch's events applied, non-TAS pods, TAS
+// usage per domain), the device context is kept, and the compiled
+// workloads are recompiled against the new columns.
+static int rebuild(kueue_tas_host* h, const kjson::Node& node_events) {
+  auto ns = h->snap->fork_state();
+  for (auto& n : node_events.items) ns->sync_node(n);
+  ns->assemble();
   ns->ctx = h->snap->ctx;  // keep the device context (and its buffers)
   h->snap->ctx = nullptr;
-  for (auto& u : h->usage_log) ns->update_usage(u.first, u.second);  // host mirror: ns is dirty
   h->snap = std::move(ns);
   h->ev.reset();
   h->last.clear();
   for (auto& wl : h->compiled) h->snap->ensure_columns_for(wl.podsets);
   for (auto& wl : h->compiled)
     for (auto& g : wl.groups) h->snap->compile_group(g, false);
+  h->compiled_cols = h->snap->col_gen;
   return h->snap->upload();
 }
 
@@ -2173,7 +2192,6 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
     kjson::Node arr = kjson::parse(nodes_json);
-    h->node_batches.emplace_back(nodes_json);
     std::set<int32_t> touched;
     bool structural = false;
     for (auto& n : arr.items)
@@ -2182,7 +2200,7 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
         break;
       }
     if (rebuilt) *rebuilt = structural ? 1 : 0;
-    int rc = structural ? rebuild(h) : h->snap->push_leaves(touched, true);
+    int rc = structural ? rebuild(h, arr) : h->snap->push_leaves(touched, true);
     if (rc) h->err = h->snap->err;
     return rc;
   } catch (const std::exception& e) {
@@ -2196,7 +2214,6 @@ int kueue_tas_host_update_pods(kueue_tas_host* h, const char* pods_json) {
   try {
     int rc = h->snap->update_pods(kjson::parse(pods_json));
     if (rc) h->err = h->snap->err;
-    else h->pod_batches.emplace_back(pods_json);
     return rc;
   } catch (const std::exception& e) {
     h->err = e.what();
@@ -2365,6 +2382,7 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
     }
     for (auto& wl : h->compiled)
       for (auto& g : wl.groups) h->snap->compile_group(g, false);
+    h->compiled_cols = h->snap->col_gen;
     return h->snap->upload();
   } catch (const std::exception& e) {
     h->err = e.what();
@@ -2375,7 +2393,18 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
 // One timed "step": every compiled workload evaluated against the resident
 // snapshot, results decoded to (leaf, count) lists; FNV-1a over all results.
 int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
-  if (!h || !h->snap) return KUEUE_TAS_EINVAL;
+  if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
+  if (h->compiled_cols != h->snap->col_gen) {  // a pod / usage event re-columned the snapshot since compile
+    try {
+      for (auto& wl : h->compiled) h->snap->ensure_columns_for(wl.podsets);
+      for (auto& wl : h->compiled)
+        for (auto& g : wl.groups) h->snap->compile_group(g, false);
+      h->compiled_cols = h->snap->col_gen;
+    } catch (const std::exception& e) {
+      h->err = e.what();
+      return KUEUE_TAS_EINVAL;
+    }
+  }
   if (!h->ev) h->ev = std::make_unique<Evaluator>(Evaluator{h->snap.get()});
   Evaluator& ev = *h->ev;
   std::vector<std::vector<PodSetResult>>& results = h->last;
@@ -2452,6 +2481,23 @@ int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8) {
   for (int k = 0; k < 4; k++) stats8[3 + k] = h->stats[k];
   stats8[7] = 0;
   return 0;
+}
+
+int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json) {
+  if (!h || !h->snap || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    std::string out = "{\"results\":[";
+    for (size_t i = 0; i < h->last.size(); i++) {
+      if (i) out += ",";
+      emit_results(out, *h->snap, h->last[i]);
+    }
+    out += "]}";
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
 }
 
 int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n) {

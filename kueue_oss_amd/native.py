@@ -55,7 +55,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_snapshot_set_free", "kueue_tas_snapshot_set_leaf_attrs", "kueue_tas_host_update_nodes",
     "kueue_tas_encode_v1beta2", "kueue_tas_snapshot_load_names", "kueue_tas_encode_v1beta2_leaves",
     "kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from", "kueue_tas_host_find_v1beta2",
-    "kueue_tas_host_v1beta2_last",
+    "kueue_tas_host_v1beta2_last", "kueue_tas_host_last_results",
 ]
 
 
@@ -114,6 +114,8 @@ def _bind(lib):
     lib.kueue_tas_host_find_v1beta2.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_find_v1beta2.restype = c.c_int
     lib.kueue_tas_host_v1beta2_last.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_last_results.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_last_results.restype = c.c_int
     lib.kueue_tas_host_v1beta2_last.restype = c.c_int
     lib.kueue_tas_host_preemption_search.argtypes = [c.c_void_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_preemption_search.restype = c.c_int
@@ -316,6 +318,13 @@ class TASFlavorSnapshot:
         ms = (ctypes.c_double * 4)()
         self._lib.kueue_tas_host_last_profile(self._h, ms)
         return tuple(ms)
+
+    def last_results(self) -> list:
+        """Results of the last run_compiled, one result list per compiled workload."""
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_last_results(self._h, ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        return _take(self._lib, out)["results"]
 
     def last_records(self, n: int):
         """[n][4] int32 compact per-workload results of the last run_compiled."""

@@ -174,3 +174,39 @@ def test_pod_events_on_gpu():
 @pytest.mark.gpu
 def test_pod_events_arith_on_gpu():
     _check(93, 100, gen=synth.arith_stress_case)
+
+
+def _check_recolumn(lib=None):
+    """Compiled workloads (kueue_tas_host_compile / run_compiled) stay correct
+    when events change the snapshot's resource columns after compile: a pod
+    with a resource no leaf had (sorting before "cpu", so existing column
+    indices shift) and a usage update with another new resource."""
+    snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 2, 4, 8))
+    snap = TASFlavorSnapshot(snap_doc, lib=lib) if lib else TASFlavorSnapshot(snap_doc)
+    snap.compile(wls)
+    ref = copy.deepcopy(snap_doc)
+    snap.run_compiled()
+    assert snap.last_results() == oracle_lib.eval_workloads(ref, wls)[0]
+    node = ref["nodes"][3]["name"]
+    ev = [{"namespace": "x", "name": "p-new", "nodeName": node, "phase": "Running",
+           "requests": {"aaa.io/new": 1, "cpu": 1000}}]
+    snap.update_pods(ev)
+    ref["pods"] = ref["pods"] + ev
+    snap.run_compiled()
+    assert snap.last_results() == oracle_lib.eval_workloads(ref, wls)[0]
+    host = ref["nodes"][5]["labels"]["kubernetes.io/hostname"]
+    u = [{"values": [host], "singlePodRequests": {"aab.io/other": 2, "memory": 1 << 30}, "count": 1}]
+    snap.add_usage(u)
+    snap.run_compiled()
+    want = [oracle_lib.session(ref, [{"op": "add", "usage": u}, {"op": "find", "podSets": w}])[-1] for w in wls]
+    assert snap.last_results() == want
+    snap.close()
+
+
+def test_emulated_recolumn_after_compile(emu_lib):
+    _check_recolumn(emu_lib)
+
+
+@pytest.mark.gpu
+def test_recolumn_after_compile_on_gpu():
+    _check_recolumn()
