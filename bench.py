@@ -4,14 +4,20 @@
 A step = one nominate batch (pkg/scheduler/scheduler.go:583-619): every rank
 evaluates its shard of pending workloads (FindTopologyAssignmentsForWorkload,
 pkg/cache/scheduler/clusterqueue_snapshot.go:191) against its replica of the
-snapshot resident in HBM, through the C-ABI host layer (request H2D, three
-kernel stages, result D2H and decode), then the per-workload result records
-are all-gathered over RCCL (N > 1).  Weak scaling: per-rank batch fixed.
+snapshot resident in HBM, starting from the workloads' TASPodSetRequests:
+grouping and the findTopologyAssignment prelude run inside the step
+(KUEUE_TAS_RUN_COMPILE), then request H2D, the kernel stages, result D2H and
+the TopologyAssignment of every result (Values, Count; KUEUE_TAS_RUN_VALUES).
+With N > 1 ranks the full assignments are then all-gathered over RCCL.
+Weak scaling: per-rank batch fixed.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
 
-Rank 0 prints ONE JSON line.  See DESIGN.md §Measurement for the roofline
-bytes and the CPU baseline (the C++ oracle, "port", timed on a bounded sample).
+Rank 0 prints ONE JSON line.  After the timed region (untimed): the
+precompiled-request rate, the admission loop (gather, Fits + AddUsage in
+order on rank 0, delta broadcast, replicas apply), the whole timed batch
+checked against the CPU oracle, the oracle's CPU baseline, the adversarial
+C3J variant, and the widened rows.  See DESIGN.md §5.
 """
 from __future__ import annotations
 
@@ -35,9 +41,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=1024, help="pending workloads per rank per step")
-    ap.add_argument("--cpu-sample", type=int, default=64, help="workloads timed on the CPU oracle (rank 0)")
-    ap.add_argument("--parity-sample", type=int, default=24)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="workloads timed on the single-thread CPU oracle")
+    ap.add_argument("--parity-threads", type=int, default=16, help="oracle threads for the whole-batch check")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the whole-batch oracle check")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C3J variant and the widened rows")
     return ap.parse_args()
 
 
@@ -72,9 +79,9 @@ def fused_parents(doc):
     return len(doc["nodes"]) // F if F <= 64 and F & (F - 1) == 0 else 0
 
 
-def load_traffic(path, config, n_fill):
+def load_traffic(path, config):
     """HBM bytes per fill launch from a committed PMC measurement of the same
-    workload (tools/pmc.sh -> profiles/), scaled per launch; None if absent."""
+    workload (tools/pmc.sh -> profiles/), None if absent."""
     try:
         with open(path) as f:
             d = json.load(f)
@@ -85,12 +92,31 @@ def load_traffic(path, config, n_fill):
     return d.get("fill_bytes_per_launch")
 
 
+def pct(xs, q):
+    s = sorted(xs)
+    return s[min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))]
+
+
+def roofline_of(snap, doc, wls, steps, stage_sum):
+    st = snap.last_stats()
+    launches = max(st["fill_launches"], 1)
+    per_launch_fill_ms = stage_sum["fill"] / (steps * launches)
+    N = len(doc["nodes"])
+    R_used = st["staged_cols"] or len({r for w in wls for p in w for r in p["requests"]} | {"pods"})
+    label_cols = 1 if any(p.get("nodeSelector") for w in wls for p in w) else 0
+    fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(st["leader_evals"], st["fill_evals"]) / launches,
+                                        R_used, label_cols, fused_parents(doc))
+    achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
+    return st, fill_bytes, per_launch_fill_ms, achieved, R_used
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = None
     if world > 1:
         import torch
         import torch.distributed as dist_mod
@@ -99,75 +125,41 @@ def main():
         torch.cuda.set_device(local_rank)
         dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = dist_mod
+        device = f"cuda:{local_rank}"
+
+    import numpy as np
+    import torch
 
     from kueue_oss_amd import TASFlavorSnapshot, synth
-    from kueue_oss_amd.sharding import gather_records, shard_workloads
+    from kueue_oss_amd.sharding import admit_round, gather_assignments, shard_ids
 
     gen = synth.CONFIGS[a.config]
     t0 = time.time()
     snap_doc, all_wls = gen(n_workloads=a.batch * world) if a.config != "C1" else gen()
-    mine = shard_workloads(all_wls, world, rank)
+    ids = shard_ids(all_wls, world, rank)
+    mine = [all_wls[i] for i in ids]
     gen_s = time.time() - t0
 
     t0 = time.time()
     snap = TASFlavorSnapshot(snap_doc, device=local_rank if world > 1 else 0)
-    snap.compile(mine)
+    snap.compile(all_wls)  # identical resource columns on every replica
+    if world > 1:
+        snap.set_shard(ids)
     load_s = time.time() - t0
     N = len(snap_doc["nodes"])
-
-    # ---- parity (untimed, after the timed region so the CPU burn cannot
-    # disturb it): product vs CPU oracle on a sample; CPU baseline timing ----
-    def cpu_leg():
-        parity = None
-        cpu = None
-        if rank == 0 and not a.no_cpu:
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            import oracle_lib
-
-            sample = mine[: max(a.parity_sample, a.cpu_sample)]
-            got = snap.find_topology_assignments_for_workloads(sample)
-            want, secs = oracle_lib.eval_workloads(snap_doc, sample[: a.cpu_sample])
-            parity = all(got[i] == want[i] for i in range(len(want)))
-            cpu = {"value": round(len(want) / secs, 3), "unit": "placements/s", "cores": 1, "kind": "port",
-                   "sample": f"{len(want)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
-                             f"(C++ restatement of the Go path; Go toolchain absent)",
-                   "seconds": round(secs, 3)}
-            # mode (ii) of BASELINE.md: the batch's independent workloads over host threads
-            thr = int(os.environ.get("KTAS_CPU_THREADS", "16"))
-            tsample = mine[: 4 * thr]
-            _, tsecs = oracle_lib.eval_workloads(snap_doc, tsample, threads=thr)
-            model = ""
-            try:
-                with open("/proc/cpuinfo") as fh:
-                    model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
-            except OSError:
-                pass
-            cpu["threaded"] = {"value": round(len(tsample) / tsecs, 3), "threads": thr,
-                               "sample": f"{len(tsample)} workloads", "seconds": round(tsecs, 3)}
-            cpu["cpu_model"] = model
-            cpu["gomaxprocs"] = "n/a (Go toolchain absent)"
-            if not parity:
-                bad = [i for i in range(len(want)) if got[i] != want[i]]
-                print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
-        return parity, cpu
-
-    import torch
+    FULL = TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES
 
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize() if torch.cuda.is_available() else None
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
 
-    rec = None
-    gathered = None
-
-    def step():
-        nonlocal rec, gathered
-        h = snap.run_compiled()
-        if dist is not None:
-            # RCCL all-gather of the per-workload result records over xGMI (shards differ in size: padded)
-            gathered = gather_records(snap.last_records(len(mine)), world, dist, device=f"cuda:{local_rank}")
-        return h
+    def step(flags=FULL, gather=True):
+        snap.run_compiled(flags=flags)
+        if dist is not None and gather:
+            # RCCL all-gather of every rank's full assignments (quads) over xGMI
+            gather_assignments(snap.last_assignments(), world, dist, device)
 
     # the snapshot document and generated workloads are long-lived: keep them
     # out of the collector's scans during the timed loop
@@ -176,14 +168,14 @@ def main():
     for _ in range(a.warmup):
         step()
     barrier()
-    t0 = time.perf_counter()
-    stage_sum = {}
+    stage_sum, dev_host_sum = {}, {}
     host_sum = [0.0] * 4
-    dev_host_sum = {}
-    counts = None
+    per_step = []
+    t0 = time.perf_counter()
     for _ in range(a.steps):
+        ts = time.perf_counter()
         step()
-        _, counts = snap.last_timings()
+        per_step.append((time.perf_counter() - ts) * 1e3)
         for k, v in snap.last_stage_times().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
         host_sum = [x + y for x, y in zip(host_sum, snap.last_profile())]
@@ -192,85 +184,83 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     placements = len(all_wls) * a.steps  # every rank's shard, all steps
     value = placements / dt
-    parity, cpu = cpu_leg()
+    st, fill_bytes, per_launch_fill_ms, achieved, R_used = roofline_of(snap, snap_doc, mine, a.steps, stage_sum)
+    timed_results = snap.last_results() if rank == 0 and not a.no_cpu else None
 
-    # ---- widened rows, after the timed region: v1beta2 encoding of the last
-    # batch's assignments and the admission re-check + usage update ----
+    # ---- precompiled-request rate (round-1 definition of the step) ----
+    pre_steps = max(10, a.steps // 2)
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(pre_steps):
+        step(flags=0, gather=False)
+    barrier()
+    pre_rate = len(mine) * pre_steps / (time.perf_counter() - t1)
+
+    # ---- admission loop: evaluate, gather, rank 0 admits in order and
+    # broadcasts its deltas, replicas apply; then the negated deltas (the
+    # workloads finish) restore the snapshot for the next round ----
+    rounds = 5
+    adm_ms, admitted_n, deltas_n = [], 0, 0
+    for _ in range(rounds):
+        barrier()
+        ta = time.perf_counter()
+        snap.run_compiled(flags=FULL)
+        if dist is not None:
+            _, admitted, deltas = admit_round(snap, world, rank, dist, device)
+        else:
+            admitted, deltas = snap.admit(snap.last_assignments())
+        barrier()
+        adm_ms.append((time.perf_counter() - ta) * 1e3)
+        if admitted is not None:
+            admitted_n = int(admitted[:, 1].sum())
+        deltas_n = len(deltas)
+        neg = deltas.copy()
+        neg["delta"] = -neg["delta"]
+        snap.apply_deltas(neg)
+
+    # ---- whole timed batch vs the CPU oracle; CPU baseline ----
+    parity = cpu = None
+    if rank == 0 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+
+        thr = a.parity_threads
+        want, psecs = oracle_lib.eval_workloads(snap_doc, mine, threads=thr)
+        bad = [i for i in range(len(want)) if timed_results[i] != want[i]]
+        parity = {"ok": not bad, "workloads": len(want), "mismatches": bad[:8], "oracle_threads": thr,
+                  "oracle_seconds": round(psecs, 2)}
+        if bad:
+            print(f"PARITY MISMATCH on workloads {bad[:8]}", file=sys.stderr)
+        sample = mine[: a.cpu_sample]
+        _, secs = oracle_lib.eval_workloads(snap_doc, sample)
+        model = ""
+        try:
+            with open("/proc/cpuinfo") as fh:
+                model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+        except OSError:
+            pass
+        cpu = {"value": round(len(sample) / secs, 3), "unit": "placements/s", "cores": 1, "kind": "port",
+               "sample": f"{len(sample)} {a.config} workloads x {N} nodes, oracle/tas_oracle.cpp single thread "
+                         f"(C++ restatement of the Go path; Go toolchain absent)",
+               "seconds": round(secs, 3),
+               "threaded": {"value": round(len(want) / psecs, 3), "threads": thr,
+                            "sample": f"the whole {len(want)}-workload batch", "seconds": round(psecs, 3)},
+               "cpu_model": model, "gomaxprocs": "n/a (Go toolchain absent)"}
+
     extras = {}
-    if rank == 0:
-        reps = 5
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            snap.last_v1beta2(materialize=False)
-        enc_ms = (time.perf_counter() - t0) / reps * 1e3
-        got = snap.find_topology_assignments_for_workloads(mine[:64])
-        recs = [r for w, res in zip(mine[:64], got) for r in synth.usage_records(w, res)]
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            snap.fits(recs[:8])
-        fits_ms = (time.perf_counter() - t0) / reps * 1e3
-        t0 = time.perf_counter()
-        snap.add_usage(recs[:8])
-        snap.remove_usage(recs[:8])
-        upd_ms = (time.perf_counter() - t0) / 2 * 1e3
-        # batched preemption search (preemption.go:307-345): 16 admitted
-        # workloads as candidates, one batch over their prefixes + fill-back
-        cands = [synth.usage_records(w, res) for w, res in zip(mine[:64], got)]
-        cands = [c for c in cands if c][:16]
-        for c in cands:
-            snap.add_usage(c)
-        pre = [dict(p, count=p.get("count", 1) * 4) for p in mine[0]]
-        enc = json.dumps(cands).encode()  # the caller's records, serialized outside the timed call
-        snap.preemption_search(pre, enc)
-        t0 = time.perf_counter()
-        pr = snap.preemption_search(pre, enc)
-        pre_ms = (time.perf_counter() - t0) * 1e3
-        for c in cands:
-            snap.remove_usage(c)
-        # device-resident maintenance: 64 non-TAS pod events (add, then delete)
-        # replace only the touched leaves instead of rebuilding the snapshot
-        evs = [{"namespace": "bench", "name": f"np{k}", "nodeName": f"node-{k % 4}-{k % 16}-{k % 64}-{k % 32}",
-                "phase": "Running", "requests": {"cpu": 1000, "memory": 1 << 30}} for k in range(64)]
-        t0 = time.perf_counter()
-        snap.update_pods(evs)
-        snap.update_pods([dict(e, delete=True) for e in evs])
-        pod_ms = (time.perf_counter() - t0) / 2 * 1e3
-        # 64 in-place node updates (allocatable change), then restored
-        import copy
-        upd = [copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)]
-        for nd in upd:
-            nd["allocatable"]["cpu"] = nd["allocatable"].get("cpu", 0) - 1000
-        t0 = time.perf_counter()
-        rebuilt = snap.update_nodes(upd)
-        node_ms = (time.perf_counter() - t0) * 1e3
-        snap.update_nodes([copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)])
-        extras = {"pod_events_ms_per_64": round(pod_ms, 3),
-                  "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,
-                  "preemption_search_profile_ms": pr["profileMs"],
-                  "preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),
-                  "preemption_first_fit": pr["firstFit"], "preemption_fill_back_evals": pr["fillBackEvals"],
-                  "v1beta2_encode_ms_per_batch": round(enc_ms, 3),
-                  "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
-                  "usage_update_ms_per_call": round(upd_ms, 3)}
+    if rank == 0 and world == 1 and not a.no_extras:
+        extras = widened_rows(a, snap, snap_doc, mine, synth)
+        extras["c3j"] = c3j_variant(a, synth, TASFlavorSnapshot, FULL)
 
-    batches, evals, leader_evals = counts
-    st = snap.last_stats()
-    launches = max(st["fill_launches"], 1)
-    per_launch_fill_ms = stage_sum["fill"] / (a.steps * launches)
-    R_used = st["staged_cols"] or len({r for w in mine for p in w for r in p["requests"]} | {"pods"})
-    label_cols = 1 if any(p.get("nodeSelector") for w in mine for p in w) else 0
-    fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(leader_evals, st["fill_evals"]) / launches,
-                                        R_used, label_cols, fused_parents(snap_doc))
-    achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
-    traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config, st["fill_evals"])
     stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}
     host = dict(zip(("staging_ms", "eval_calls_ms", "decode_ms", "total_ms"), (round(x / a.steps, 3) for x in host_sum)))
     host["eval_call_detail_ms"] = {k: round(v / a.steps, 3) for k, v in dev_host_sum.items()}
+    traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config)
     if rank == 0:
         line = {
             "metric": "TAS placements/sec at 128k nodes (1/2/4/8 GPU); % HBM roofline",
@@ -280,26 +270,36 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "step_ms": {"median": round(pct(per_step, 0.5), 3), "p10": round(pct(per_step, 0.1), 3),
+                        "p90": round(pct(per_step, 0.9), 3)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded generator modelled on test/performance/scheduler/generator)",
-            "config": {"workload": f"{a.config}: {N} nodes, {a.batch} pending workloads per GPU per step "
-                                   "(50% BestFit required/preferred, 50% LeastFreeCapacity unconstrained; "
-                                   "taints + nodeSelector)",
+            "config": {"workload": f"{a.config}: {N} nodes, {a.batch} pending workloads per GPU per step from "
+                                   "TASPodSetRequests (grouping + request compile + evaluation + TopologyAssignment "
+                                   "values in the step; 50% BestFit required/preferred, 50% LeastFreeCapacity "
+                                   "unconstrained; taints + nodeSelector)",
                        "nodes": N, "batch_per_gpu": a.batch, "parallelism": f"dp{world} (replicated snapshot)"},
-            "roofline": {"kernel": "fill_leaves_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+            "roofline": {"kernel": "fill_leaves_staged_kernel", "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": int(fill_bytes),
                          "avg_launch_ms": round(per_launch_fill_ms, 4),
-                         "per_launch": f"{N} leaves x {st['fill_evals'] // launches} phase-1 evals "
-                                       f"({evals // max(batches, 1)} evals, deduplicated), {R_used} columns"},
+                         "per_launch": f"{N} leaves x {st['fill_evals'] // max(st['fill_launches'], 1)} phase-1 evals "
+                                       f"({st['evals'] // max(st['batches'], 1)} evals, deduplicated), {R_used} columns"},
+            "precompiled_rate": {"value": round(pre_rate * world, 1), "unit": "placements/s",
+                                 "note": "requests compiled once before timing, no TopologyAssignment values "
+                                         "(round-1 step definition), no gather"},
+            "admission": {"round_ms_median": round(pct(adm_ms, 0.5), 3), "rounds": rounds,
+                          "admitted": admitted_n, "deltas": deltas_n,
+                          "round": "evaluate + all-gather assignments + rank-0 Fits/AddUsage in workload order "
+                                   "(admit_kernel) + delta broadcast + replicas apply"},
             "stages": stages,
             "host": host,
             "work": st,
             "cpu_baseline": cpu,
-            "parity_sample_ok": parity,
+            "parity_full_batch": parity,
             "extras": extras,
             "setup_s": {"generate": round(gen_s, 2), "snapshot_load_and_compile": round(load_s, 2)},
         }
@@ -307,6 +307,95 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     snap.close()
+
+
+def widened_rows(a, snap, snap_doc, mine, synth):
+    """§8f rows on the bench snapshot (after the timed region)."""
+    import copy
+
+    N = len(snap_doc["nodes"])
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        snap.last_v1beta2(materialize=False)
+    enc_ms = (time.perf_counter() - t0) / reps * 1e3
+    got = snap.find_topology_assignments_for_workloads(mine[:64])
+    recs = [r for w, res in zip(mine[:64], got) for r in synth.usage_records(w, res)]
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        snap.fits(recs[:8])
+    fits_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    snap.add_usage(recs[:8])
+    snap.remove_usage(recs[:8])
+    upd_ms = (time.perf_counter() - t0) / 2 * 1e3
+    # batched preemption search (preemption.go:307-345): 16 admitted
+    # workloads as candidates, one batch over their prefixes + fill-back
+    cands = [synth.usage_records(w, res) for w, res in zip(mine[:64], got)]
+    cands = [c for c in cands if c][:16]
+    for c in cands:
+        snap.add_usage(c)
+    pre = [dict(p, count=p.get("count", 1) * 4) for p in mine[0]]
+    enc = json.dumps(cands).encode()
+    snap.preemption_search(pre, enc)
+    t0 = time.perf_counter()
+    pr = snap.preemption_search(pre, enc)
+    pre_ms = (time.perf_counter() - t0) * 1e3
+    for c in cands:
+        snap.remove_usage(c)
+    evs = [{"namespace": "bench", "name": f"np{k}", "nodeName": snap_doc["nodes"][k * 977 % N]["name"],
+            "phase": "Running", "requests": {"cpu": 1000, "memory": 1 << 30}} for k in range(64)]
+    t0 = time.perf_counter()
+    snap.update_pods(evs)
+    snap.update_pods([dict(e, delete=True) for e in evs])
+    pod_ms = (time.perf_counter() - t0) / 2 * 1e3
+    upd = [copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)]
+    for nd in upd:
+        nd["allocatable"]["cpu"] = nd["allocatable"].get("cpu", 0) - 1000
+    t0 = time.perf_counter()
+    rebuilt = snap.update_nodes(upd)
+    node_ms = (time.perf_counter() - t0) * 1e3
+    snap.update_nodes([copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)])
+    return {"pod_events_ms_per_64": round(pod_ms, 3),
+            "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,
+            "preemption_search_profile_ms": pr["profileMs"],
+            "preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),
+            "preemption_first_fit": pr["firstFit"], "preemption_fill_back_evals": pr["fillBackEvals"],
+            "v1beta2_encode_ms_per_batch": round(enc_ms, 3),
+            "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
+            "usage_update_ms_per_call": round(upd_ms, 3)}
+
+
+def c3j_variant(a, synth, TASFlavorSnapshot, flags, steps=20, sample=32):
+    """The adversarial C3 variant: ragged racks and one request signature per
+    workload (config_c3j), same step definition; parity on a sample."""
+    doc, wls = synth.config_c3j(n_workloads=a.batch)
+    snap = TASFlavorSnapshot(doc)
+    snap.compile(wls)
+    for _ in range(3):
+        snap.run_compiled(flags=flags)
+    stage_sum = {}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        snap.run_compiled(flags=flags)
+        for k, v in snap.last_stage_times().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    dt = time.perf_counter() - t0
+    st, fill_bytes, fill_ms, achieved, _ = roofline_of(snap, doc, wls, steps, stage_sum)
+    res = snap.last_results()
+    ok = None
+    if not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+
+        want, _ = oracle_lib.eval_workloads(doc, wls[:sample], threads=a.parity_threads)
+        ok = res[:sample] == want
+    snap.close()
+    return {"nodes": len(doc["nodes"]), "workloads": len(wls), "value": round(len(wls) * steps / dt, 1),
+            "ms_per_step": round(dt / steps * 1e3, 3), "phase1_classes": st["fill_evals"] // max(st["batches"], 1),
+            "fill_frac": round(achieved / HBM_PEAK_GBS, 4), "fill_avg_launch_ms": round(fill_ms, 4),
+            "stages_ms": {k: round(v / steps, 3) for k, v in stage_sum.items()},
+            "parity_sample_ok": ok, "parity_sample": sample}
 
 
 if __name__ == "__main__":

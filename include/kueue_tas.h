@@ -305,6 +305,17 @@ typedef struct {
 int kueue_tas_fits(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
                    size_t num_terms, int32_t* fits);
 
+/* ---- admission: the TAS half of Scheduler.processEntry ----------------------
+ * (pkg/scheduler/scheduler.go:371-435).  Workload w owns the records
+ * reqs[wl_off[w] .. wl_off[w+1]) (its TopologyDomainRequests, terms without
+ * pods).  In order, w is admitted (admitted[w] = 1) when every record fits
+ * (TASFlavorSnapshot.Fits :401-415) against the snapshot plus the usage of
+ * the workloads admitted before it; its usage is then added on the device
+ * (updateTASUsage :257-265: single x count per term + pods:count in
+ * pods_col; -1: no pods column).  Every term's col must be >= 0. */
+int kueue_tas_admit(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
+                    size_t num_terms, const int64_t* wl_off, size_t n_workloads, int32_t pods_col, int32_t* admitted);
+
 /* ---- v1beta2 compact TopologyAssignment encoding -------------------------
  * V1Beta2From / singleCompactSliceEncoding (pkg/util/tas/tas_assignment.go:
  * 135-259): one slice per assignment; per level either Universal (all values
@@ -364,6 +375,14 @@ int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, cha
  * (kueue_tas_host_run_compiled) without JSON on the timed path. */
 int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json);
 int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
+/* run_compiled with options: KUEUE_TAS_RUN_COMPILE groups and compiles every
+ * workload's TASPodSetRequests inside the call (FindTopologyAssignmentsForFlavor
+ * :528-541 + the findTopologyAssignment prelude :809-897, no cached pass);
+ * KUEUE_TAS_RUN_VALUES builds each result's TopologyAssignment domains
+ * (Values = the leaf's levelValues[levelIdx:], Count; buildAssignment :1472-1501). */
+#define KUEUE_TAS_RUN_COMPILE 1u
+#define KUEUE_TAS_RUN_VALUES 2u
+int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash);
 /* Device stage times of the last run (summed over its batches, ms):
  * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
  * counts[1] = evaluations, counts[2] = evaluations with a leader. */
@@ -383,14 +402,34 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
 
+/* Data-parallel batches (one rank per GPU, each with a replica of the
+ * snapshot).  Every rank compiles the same global workload list
+ * (kueue_tas_host_compile: identical resource columns everywhere) and
+ * evaluates only its shard:
+ *  set_shard: run_compiled evaluates compiled workloads ids[0..n) (global
+ *    indices) in that order;
+ *  last_assignments: the results of the last run_compiled as int32 quads,
+ *    per workload a header (id, -1, failed 0/1, number of domain quads) then
+ *    one (id, podset index, leaf, count) per assigned domain;
+ *    *len = quads x 4; KUEUE_TAS_EOVERFLOW when cap is too small;
+ *  admit: the TAS half of processEntry over the gathered quads of every rank
+ *    (workloads in ascending id): kueue_tas_admit on this replica, the host
+ *    mirror updated; admitted = (id, 0/1) pairs (capacity checked first:
+ *    KUEUE_TAS_EOVERFLOW before anything is admitted, *n_workloads set);
+ *    *n_deltas = length of the applied delta list (updateTASUsage per domain
+ *    record), copied out by last_deltas for the other replicas;
+ *  apply_deltas: a replica applies those deltas (host mirror + device). */
+int kueue_tas_host_set_shard(kueue_tas_host* h, const int32_t* ids, size_t n);
+int kueue_tas_host_last_assignments(kueue_tas_host* h, int32_t* buf, size_t cap, size_t* len);
+int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* quads, size_t len, int32_t* admitted, size_t admitted_cap,
+                         size_t* n_workloads, size_t* n_deltas);
+int kueue_tas_host_last_deltas(kueue_tas_host* h, kueue_tas_delta* buf, size_t cap);
+int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* deltas, size_t n);
+
 /* Every result of the last run_compiled as {"results": [[{"name",
  * "assignment","reason"}...] per compiled workload]} (kueue_tas_free). */
 int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json);
 
-/* Per-workload compact results of the last run_compiled into buf (int32):
- * for workload i: [status(0 ok/1 fail), entries, first leaf, first count],
- * 4 int32 per workload (used for the cross-rank all-gather). */
-int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n_workloads);
 
 /* Snapshot usage updates and the admission re-check, JSON records
  * [{"values": [...], "singlePodRequests": {...}, "count": n}, ...]
@@ -451,6 +490,11 @@ int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json
                                      char** out_json);
 
 void kueue_tas_free(char* p);
+
+/* Content hash of the sources the library was built from (first 16 hex
+ * digits of sha256 over kueue_oss_amd/csrc's sources and this header, in the
+ * Makefile's order); "unversioned" for builds outside that Makefile. */
+const char* kueue_tas_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -652,6 +652,43 @@ int kueue_tas_fits(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, c
   return KUEUE_TAS_OK;
 }
 
+int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
+                    size_t num_terms, const int64_t* wl_off, size_t n_wl, int32_t pods_col, int32_t* admitted) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (n_wl == 0) return KUEUE_TAS_OK;
+  if (!wl_off || !admitted || (n && !reqs) || (num_terms && !terms)) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  if (pods_col < -1 || pods_col >= c->snap.R) return fail(c, KUEUE_TAS_EINVAL, "pods column out of range");
+  if (wl_off[0] != 0 || size_t(wl_off[n_wl]) != n) return fail(c, KUEUE_TAS_EINVAL, "workload offsets");
+  for (size_t w = 0; w < n_wl; w++)
+    if (wl_off[w + 1] < wl_off[w]) return fail(c, KUEUE_TAS_EINVAL, "workload offsets not monotone");
+  for (size_t i = 0; i < n; i++) {
+    const kueue_tas_fits_req& r = reqs[i];
+    if (r.leaf >= c->snap.N || r.num_terms < 0 || r.term_begin < 0 || size_t(r.term_begin) + size_t(r.num_terms) > num_terms)
+      return fail(c, KUEUE_TAS_EINVAL, "admit record out of range");
+    for (int k = 0; k < r.num_terms; k++)
+      if (terms[r.term_begin + k].col < 0 || terms[r.term_begin + k].col >= c->snap.R)
+        return fail(c, KUEUE_TAS_EINVAL, "admit term column out of range");
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t o_terms = (n * sizeof(kueue_tas_fits_req) + 255) / 256 * 256;
+  const size_t o_off = o_terms + (num_terms * sizeof(kueue_tas_fits_term) + 255) / 256 * 256;
+  const size_t o_out = o_off + ((n_wl + 1) * 8 + 255) / 256 * 256;
+  HIPCHK(c, c->d_fits.ensure(o_out + n_wl * 4));
+  uint8_t* d = c->d_fits.p;
+  if (n) HIPCHK(c, hipMemcpyAsync(d, reqs, n * sizeof(kueue_tas_fits_req), hipMemcpyHostToDevice, c->stream));
+  if (num_terms)
+    HIPCHK(c, hipMemcpyAsync(d + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d + o_off, wl_off, (n_wl + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), 0, c->stream, c->snap, c->d_usage.p, c->d_usage_present.p,
+                     reinterpret_cast<const kueue_tas_fits_req*>(d), reinterpret_cast<const kueue_tas_fits_term*>(d + o_terms),
+                     reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col, reinterpret_cast<int32_t*>(d + o_out));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(admitted, d + o_out, n_wl * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
 static double wall_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }

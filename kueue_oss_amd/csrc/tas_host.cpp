@@ -16,6 +16,7 @@
 // (tas_kernels.hip).  This layer never evaluates a placement on the CPU: if the
 // device library or a GPU is unavailable, creation fails loudly.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -174,11 +175,20 @@ struct DomainSpan {
   const DomainAssignment* begin() const { return p; }
   const DomainAssignment* end() const { return p + n; }
 };
+// One domain of utiltas.TopologyAssignment (tas_assignment.go:30-38):
+// Values = the leaf's levelValues[levelIdx:] (buildAssignment :1472-1501
+// slices the domain's own values, no string copies), Count.
+struct DomainValues {
+  const std::string* values;
+  int32_t n;
+  int32_t count;
+};
 struct PodSetResult {
   std::string name;
   bool has_assignment = false;
   DomainSpan domains;                  // leaf indices (lexicographic order)
   std::vector<DomainAssignment> own;   // storage once the view is materialized
+  std::vector<DomainValues> values;    // with KUEUE_TAS_RUN_VALUES: the TopologyAssignment domains
   std::string reason;
   void materialize() {
     if (domains.n && domains.p != own.data()) {
@@ -806,7 +816,7 @@ class FlavorSnapshot {
   // pods:count; domains that are not leaves are skipped.  The device replica
   // is updated in place by a delta launch; a resource no column holds yet
   // changes the column set, and then the next evaluation reloads the snapshot.
-  int update_usage(const std::vector<DomainUsage>& us, bool add) {
+  int update_usage(const std::vector<DomainUsage>& us, bool add, bool device = true) {
     std::vector<kueue_tas_delta> deltas;
     bool new_col = false;
     for (auto& u : us) {
@@ -838,7 +848,7 @@ class FlavorSnapshot {
       set_columns(names);  // dirty: the next upload() takes the host mirror
       return 0;
     }
-    if (dirty || !ctx || deltas.empty()) return 0;
+    if (!device || dirty || !ctx || deltas.empty()) return 0;
     int rc = kueue_tas_snapshot_apply_deltas(ctx, deltas.data(), deltas.size(), nullptr);
     if (rc) err = std::string("apply deltas: ") + kueue_tas_last_error(ctx);
     return rc;
@@ -1406,6 +1416,7 @@ struct Evaluator {
       if (rs[k].name == name) {
         rs[k].has_assignment = has;
         rs[k].domains = DomainSpan{d, nd};
+        rs[k].values.clear();
         rs[k].reason = reason;
         return;
       }
@@ -1414,6 +1425,7 @@ struct Evaluator {
     r.name = name;
     r.has_assignment = has;
     r.domains = DomainSpan{d, nd};  // zero-copy view of the batch's entries
+    r.values.clear();
     r.reason = reason;
   }
 
@@ -1486,7 +1498,7 @@ struct Evaluator {
   using Overlay = std::vector<kueue_tas_assumed>;
   const std::vector<Overlay>* base = nullptr;
   int run(std::vector<Workload>& wls, bool simulateEmpty, std::vector<std::vector<PodSetResult>>* results,
-          bool precompiled = false, const std::vector<Overlay>* base_overlay = nullptr) {
+          bool precompiled = false, const std::vector<Overlay>* base_overlay = nullptr, bool regroup = false) {
     base = base_overlay;
     ms[0] = ms[1] = ms[2] = ms[3] = 0;
     for (auto& v : stage_ms) v = 0;
@@ -1500,7 +1512,7 @@ struct Evaluator {
     if (!precompiled) {
       bool changed = false;
       for (auto& wl : wls) {
-        if (wl.groups.empty()) make_groups(wl);
+        if (wl.groups.empty() || regroup) make_groups(wl);
         changed |= snap->ensure_columns_for(wl.podsets);
       }
       for (auto& wl : wls)
@@ -1962,6 +1974,19 @@ struct kueue_tas_host {
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[4] = {0, 0, 0, 0};
   uint64_t compiled_cols = 0;  // FlavorSnapshot::col_gen the compiled workloads were compiled against
+  // this rank's shard of the compiled workloads (indices into `compiled`)
+  // and its own compiled copies; empty: run_compiled evaluates them all
+  std::vector<int32_t> shard_ids;
+  std::vector<Workload> shard;
+  std::vector<Workload>& active() { return shard_ids.empty() ? compiled : shard; }
+  std::vector<kueue_tas_delta> last_deltas;  // usage deltas the last kueue_tas_host_admit applied
+  void recompile_all() {
+    for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
+    for (auto* v : {&compiled, &shard})
+      for (auto& wl : *v)
+        for (auto& g : wl.groups) snap->compile_group(g, false);
+    compiled_cols = snap->col_gen;
+  }
 };
 
 extern "C" {
@@ -2181,10 +2206,7 @@ static int rebuild(kueue_tas_host* h, const kjson::Node& node_events) {
   h->snap = std::move(ns);
   h->ev.reset();
   h->last.clear();
-  for (auto& wl : h->compiled) h->snap->ensure_columns_for(wl.podsets);
-  for (auto& wl : h->compiled)
-    for (auto& g : wl.groups) h->snap->compile_group(g, false);
-  h->compiled_cols = h->snap->col_gen;
+  h->recompile_all();
   return h->snap->upload();
 }
 
@@ -2374,6 +2396,8 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
     kjson::Node doc = kjson::parse(workloads_json);
+    h->shard_ids.clear();
+    h->shard.clear();
     h->compiled.assign(doc["workloads"].items.size(), Workload{});
     for (size_t i = 0; i < h->compiled.size(); i++) {
       h->compiled[i].podsets = parse_podsets(doc["workloads"].items[i]);
@@ -2392,14 +2416,15 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
 
 // One timed "step": every compiled workload evaluated against the resident
 // snapshot, results decoded to (leaf, count) lists; FNV-1a over all results.
-int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
+// KUEUE_TAS_RUN_COMPILE redoes FindTopologyAssignmentsForFlavor's grouping
+// and findTopologyAssignment's prelude (make_groups, compile_group) for every
+// workload inside the call, from its TASPodSetRequests; KUEUE_TAS_RUN_VALUES
+// builds every result's TopologyAssignment domains (Values, Count).
+int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash) {
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   if (h->compiled_cols != h->snap->col_gen) {  // a pod / usage event re-columned the snapshot since compile
     try {
-      for (auto& wl : h->compiled) h->snap->ensure_columns_for(wl.podsets);
-      for (auto& wl : h->compiled)
-        for (auto& g : wl.groups) h->snap->compile_group(g, false);
-      h->compiled_cols = h->snap->col_gen;
+      h->recompile_all();
     } catch (const std::exception& e) {
       h->err = e.what();
       return KUEUE_TAS_EINVAL;
@@ -2408,10 +2433,27 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
   if (!h->ev) h->ev = std::make_unique<Evaluator>(Evaluator{h->snap.get()});
   Evaluator& ev = *h->ev;
   std::vector<std::vector<PodSetResult>>& results = h->last;
-  int rc = ev.run(h->compiled, false, &results, /*precompiled=*/true);
+  const bool compile = (flags & KUEUE_TAS_RUN_COMPILE) != 0;
+  int rc = ev.run(h->active(), false, &results, /*precompiled=*/!compile, nullptr, /*regroup=*/compile);
   if (rc) {
     h->err = h->snap->err;
     return rc;
+  }
+  if (flags & KUEUE_TAS_RUN_VALUES) {
+    const double t0 = now_ms();
+    const FlavorSnapshot& s = *h->snap;
+    const int L = s.L();
+    const int32_t lvl = s.lowestIsHostname ? L - 1 : 0;
+    for (auto& rs : results)
+      for (auto& r : rs) {
+        r.values.resize(r.domains.size());
+        for (size_t k = 0; k < r.domains.size(); k++) {
+          const auto& lv = s.values[size_t(L - 1)][size_t(r.domains[k].leaf)];
+          r.values[k] = {lv.data() + lvl, int32_t(L - lvl), r.domains[k].count};
+        }
+      }
+    ev.host_ms[2] += now_ms() - t0;
+    ev.host_ms[3] += now_ms() - t0;
   }
   memcpy(h->ms, ev.ms, sizeof h->ms);
   memcpy(h->counts, ev.counts, sizeof h->counts);
@@ -2431,12 +2473,16 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) {
           mix(uint64_t(uint32_t(d.leaf)));
           mix(uint64_t(uint32_t(d.count)));
         }
+        for (auto& v : r.values)
+          for (int32_t k = 0; k < v.n; k++) mix(std::hash<std::string>()(v.values[k]));
         mix(std::hash<std::string>()(r.reason));
       }
     *result_hash = x;
   }
   return 0;
 }
+
+int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) { return kueue_tas_host_run(h, 0, result_hash); }
 
 int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n) {
   if (!h || !h->ev || !ms || n < 0) return KUEUE_TAS_EINVAL;
@@ -2483,6 +2529,202 @@ int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8) {
   return 0;
 }
 
+int kueue_tas_host_set_shard(kueue_tas_host* h, const int32_t* ids, size_t n) {
+  if (!h || !h->snap || !h->err.empty() || (n && !ids)) return KUEUE_TAS_EINVAL;
+  try {
+    h->shard_ids.assign(ids, ids + n);
+    h->shard.assign(n, Workload{});
+    for (size_t k = 0; k < n; k++) {
+      if (ids[k] < 0 || size_t(ids[k]) >= h->compiled.size()) throw std::runtime_error("shard index out of range");
+      h->shard[k].podsets = h->compiled[size_t(ids[k])].podsets;
+      make_groups(h->shard[k]);
+      for (auto& g : h->shard[k].groups) h->snap->compile_group(g, false);
+    }
+    h->ev.reset();
+    h->last.clear();
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_last_assignments(kueue_tas_host* h, int32_t* buf, size_t cap, size_t* len) {
+  if (!h || !h->snap || !len) return KUEUE_TAS_EINVAL;
+  std::vector<Workload>& wls = h->active();
+  size_t need = 0;
+  for (size_t i = 0; i < h->last.size(); i++) {
+    need += 4;
+    for (auto& r : h->last[i]) need += 4 * r.domains.size();
+  }
+  *len = need;
+  if (need > cap || (need && !buf)) return KUEUE_TAS_EOVERFLOW;
+  size_t o = 0;
+  for (size_t i = 0; i < h->last.size() && i < wls.size(); i++) {
+    const int32_t g = h->shard_ids.empty() ? int32_t(i) : h->shard_ids[i];
+    bool fail = false;
+    int32_t nd = 0;
+    for (auto& r : h->last[i]) {
+      fail |= !r.reason.empty();
+      nd += int32_t(r.domains.size());
+    }
+    int32_t* hd = buf + o;
+    hd[0] = g;
+    hd[1] = -1;
+    hd[2] = fail ? 1 : 0;
+    hd[3] = nd;
+    o += 4;
+    for (auto& r : h->last[i]) {
+      int32_t p = 0;
+      while (size_t(p) < wls[i].podsets.size() && wls[i].podsets[size_t(p)].name != r.name) p++;
+      for (auto& d : r.domains) {
+        buf[o] = g;
+        buf[o + 1] = p;
+        buf[o + 2] = d.leaf;
+        buf[o + 3] = d.count;
+        o += 4;
+      }
+    }
+  }
+  return 0;
+}
+
+// Admission over the gathered records of a nominate batch: workloads in
+// ascending id order (the iteration order of processEntry,
+// pkg/scheduler/scheduler.go:337-339), each admitted when its assignments
+// all exist and Fits, then AddUsage -> updateTASUsage (usage records as
+// ComputeTASNetUsage builds them, flavorassigner.go:94-130: per assigned
+// domain, the PodSet's single-pod requests and the domain's count).  The
+// device applies the usage (kueue_tas_admit); the host mirror follows.
+int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int32_t* admitted, size_t admitted_cap,
+                         size_t* n_workloads, size_t* n_deltas) {
+  if (!h || !h->snap || !h->err.empty() || (len && !recs) || len % 4 || !n_workloads) return KUEUE_TAS_EINVAL;
+  try {
+    {  // capacity first: nothing is admitted when the caller's buffer is short
+      std::set<int32_t> heads;
+      for (size_t o = 0; o < len; o += 4) heads.insert(recs[o]);
+      *n_workloads = heads.size();
+      if (!admitted || admitted_cap < 2 * heads.size()) return KUEUE_TAS_EOVERFLOW;
+    }
+    h->last_deltas.clear();
+    FlavorSnapshot& s = *h->snap;
+    int rc = s.upload();
+    if (rc) {
+      h->err = s.err;
+      return rc;
+    }
+    struct Wl {
+      bool fail = false;
+      std::vector<std::array<int32_t, 3>> doms;  // podset, leaf, count
+    };
+    std::map<int32_t, Wl> byId;
+    for (size_t o = 0; o < len; o += 4) {
+      const int32_t g = recs[o];
+      if (g < 0 || size_t(g) >= h->compiled.size()) throw std::runtime_error("admit: workload id out of range");
+      Wl& w = byId[g];
+      if (recs[o + 1] < 0) {
+        w.fail |= recs[o + 2] != 0;
+      } else {
+        if (size_t(recs[o + 1]) >= h->compiled[size_t(g)].podsets.size() || recs[o + 2] < 0 || recs[o + 2] >= s.N())
+          throw std::runtime_error("admit: record out of range");
+        w.doms.push_back({recs[o + 1], recs[o + 2], recs[o + 3]});
+      }
+    }
+    *n_workloads = byId.size();
+    std::vector<kueue_tas_fits_req> fr;
+    std::vector<kueue_tas_fits_term> terms;
+    std::vector<int64_t> off(1, 0);
+    std::vector<int32_t> ids;
+    for (auto& kv : byId) {
+      ids.push_back(kv.first);
+      if (!kv.second.fail) {
+        const Workload& wl = h->compiled[size_t(kv.first)];
+        for (auto& d : kv.second.doms) {
+          const TASPodSetRequests& ps = wl.podsets[size_t(d[0])];
+          kueue_tas_fits_req r{d[1], d[2], int32_t(terms.size()), 0};
+          for (auto& t : ps.singlePodRequests) {
+            terms.push_back({t.second, s.colByName.at(t.first), 0});
+            r.num_terms++;
+          }
+          fr.push_back(r);
+        }
+      } else {  // a failed evaluation is never admitted: one record that cannot fit
+        fr.push_back({-1, 0, int32_t(terms.size()), 0});
+      }
+      off.push_back(int64_t(fr.size()));
+    }
+    std::vector<int32_t> adm(ids.size(), 0);
+    const auto pods = s.colByName.find("pods");
+    const int32_t pods_col = pods == s.colByName.end() ? -1 : pods->second;
+    rc = kueue_tas_admit(s.ctx, fr.data(), fr.size(), terms.data(), terms.size(), off.data(), ids.size(), pods_col,
+                         adm.data());
+    if (rc) {
+      h->err = std::string("admit: ") + kueue_tas_last_error(s.ctx);
+      return rc;
+    }
+    // host mirror + the delta list the replicas apply (updateTASUsage per record)
+    std::vector<FlavorSnapshot::DomainUsage> us;
+    std::vector<kueue_tas_delta>& deltas = h->last_deltas;
+    for (size_t k = 0; k < ids.size(); k++) {
+      admitted[2 * k] = ids[k];
+      admitted[2 * k + 1] = adm[k];
+      if (!adm[k]) continue;
+      for (int64_t i = off[k]; i < off[k + 1]; i++) {
+        const kueue_tas_fits_req& r = fr[size_t(i)];
+        FlavorSnapshot::DomainUsage u;
+        u.id = s.leafId[size_t(r.leaf)];
+        u.count = r.count;
+        for (int q = 0; q < r.num_terms; q++) {
+          const kueue_tas_fits_term& t = terms[size_t(r.term_begin + q)];
+          u.single[s.cols[size_t(t.col)]] = t.value;
+          deltas.push_back({r.leaf, t.col, mul64(t.value, r.count)});
+        }
+        if (pods_col >= 0) deltas.push_back({r.leaf, pods_col, int64_t(r.count)});
+        us.push_back(std::move(u));
+      }
+    }
+    if (n_deltas) *n_deltas = deltas.size();
+    rc = s.update_usage(us, true, /*device=*/false);  // already applied on the device
+    if (rc) h->err = s.err;
+    return rc;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_last_deltas(kueue_tas_host* h, kueue_tas_delta* buf, size_t cap) {
+  if (!h || (cap && !buf)) return KUEUE_TAS_EINVAL;
+  if (cap < h->last_deltas.size()) return KUEUE_TAS_EOVERFLOW;
+  std::copy(h->last_deltas.begin(), h->last_deltas.end(), buf);
+  return 0;
+}
+
+// A replica applies the delta list another rank's admission produced
+// (updateTASUsage on its own copy of the snapshot).
+int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* d, size_t n) {
+  if (!h || !h->snap || !h->err.empty() || (n && !d)) return KUEUE_TAS_EINVAL;
+  try {
+    FlavorSnapshot& s = *h->snap;
+    for (size_t i = 0; i < n; i++) {
+      if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
+        throw std::runtime_error("delta out of range");
+      const std::string& res = s.cols[size_t(d[i].col)];
+      int64_t& v = s.tasUsage[size_t(d[i].leaf)][res];
+      v = add64(v, d[i].delta);
+      int64_t& u = s.usageByDomain[s.leafId[size_t(d[i].leaf)]][res];
+      u = add64(u, d[i].delta);
+    }
+    if (s.dirty || !s.ctx) return s.upload();
+    int rc = n ? kueue_tas_snapshot_apply_deltas(s.ctx, d, n, nullptr) : 0;
+    if (rc) h->err = std::string("apply deltas: ") + kueue_tas_last_error(s.ctx);
+    return rc;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
 int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json) {
   if (!h || !h->snap || !out_json) return KUEUE_TAS_EINVAL;
   try {
@@ -2500,27 +2742,10 @@ int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json) {
   }
 }
 
-int kueue_tas_host_last_records(kueue_tas_host* h, int32_t* buf, size_t n) {
-  if (!h || !buf) return KUEUE_TAS_EINVAL;
-  for (size_t i = 0; i < n; i++) {
-    int32_t* r = buf + 4 * i;
-    r[0] = r[1] = r[2] = r[3] = 0;
-    if (i >= h->last.size()) continue;
-    bool fail = false;
-    int32_t ent = 0;
-    for (auto& p : h->last[i]) {
-      if (!p.reason.empty()) fail = true;
-      ent += int32_t(p.domains.size());
-      if (r[2] == 0 && !p.domains.empty()) {
-        r[2] = p.domains[0].leaf;
-        r[3] = p.domains[0].count;
-      }
-    }
-    r[0] = fail ? 1 : 0;
-    r[1] = ent;
-  }
-  return 0;
-}
+#ifndef KTAS_SOURCE_HASH
+#define KTAS_SOURCE_HASH "unversioned"
+#endif
+const char* kueue_tas_build_id(void) { return KTAS_SOURCE_HASH; }
 
 void kueue_tas_free(char* p) { free(p); }
 

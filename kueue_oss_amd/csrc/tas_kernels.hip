@@ -3666,4 +3666,85 @@ __global__ void fits_kernel(DevSnap s, const kueue_tas_fits_req* reqs, int n, co
   fits[i] = (any ? result : 0) >= r.count ? 1 : 0;
 }
 
+// Sequential admission over a batch of nominated workloads: the TAS half of
+// Scheduler.processEntry (pkg/scheduler/scheduler.go:371-435) per workload in
+// order: ClusterQueueSnapshot.Fits -> TASFlavorSnapshot.Fits
+// (tas_flavor_snapshot.go:401-415: every record's SinglePodRequests.CountIn
+// of free - tasUsage >= Count, no pods:1) against the usage of the workloads
+// admitted before it, then AddUsage -> updateTASUsage (:257-265: per record
+// single x count plus pods:count added to the leaf's tasUsage, keys created).
+// One wave walks the workloads in order (the dependency chain); its lanes
+// split a workload's records.  tas_usage / usage_present are read with
+// L1-bypassing loads because this wave's own atomics updated them.
+__device__ __forceinline__ int64_t load_l2(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t load_l2(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage, uint32_t* usage_present,
+                                                   const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
+                                                   const int64_t* wl_off, int n_wl, int pods_col, int32_t* admitted) {
+  const int lane = lane_id();
+  for (int w = 0; w < n_wl; w++) {
+    const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
+    bool all_fit = true;
+    for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
+      const int64_t i = base + lane;
+      bool fit = true;
+      if (i < r1) {
+        const kueue_tas_fits_req r = reqs[i];
+        if (r.leaf < 0 || r.leaf >= s.N) {
+          fit = false;
+        } else {
+          const uint32_t pres = s.free_present[r.leaf] | load_l2(usage_present + r.leaf);
+          int32_t result = 0;
+          bool any = false;
+          for (int k = 0; k < r.num_terms; k++) {
+            const kueue_tas_fits_term t = terms[r.term_begin + k];
+            const bool present = t.col >= 0 && ((pres >> t.col) & 1u);
+            if (!present && t.value != 0) {
+              result = 0;
+              any = true;
+              break;
+            }
+            int32_t c = 0x7fffffff;
+            if (t.value != 0) {
+              const int64_t cap = int64_t(uint64_t(s.free_cap[int64_t(t.col) * s.N + r.leaf]) -
+                                          uint64_t(load_l2(tas_usage + int64_t(t.col) * s.N + r.leaf)));
+              const int64_t q = (cap == INT64_MIN && t.value == -1) ? INT64_MIN : cap / t.value;
+              c = max(int32_t(uint32_t(uint64_t(q))), 0);
+            }
+            if (!any || c < result) result = c;
+            any = true;
+          }
+          fit = (any ? result : 0) >= r.count;
+        }
+      }
+      all_fit = ballot(!fit) == 0;
+    }
+    if (lane == 0) admitted[w] = all_fit ? 1 : 0;
+    if (!all_fit) continue;
+    for (int64_t i = r0 + lane; i < r1; i += kWave) {
+      const kueue_tas_fits_req r = reqs[i];
+      uint32_t bits = 0;
+      for (int k = 0; k < r.num_terms; k++) {
+        const kueue_tas_fits_term t = terms[r.term_begin + k];
+        if (t.col < 0) continue;  // the host gives every usage resource a column first
+        atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
+                  (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
+        bits |= 1u << t.col;
+      }
+      if (pods_col >= 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                  (unsigned long long)int64_t(r.count));
+        bits |= 1u << pods_col;
+      }
+      atomicOr(usage_present + r.leaf, bits);
+    }
+    __threadfence();
+    wave_sync();
+  }
+}
+
 }  // namespace ktas

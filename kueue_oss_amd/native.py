@@ -50,13 +50,37 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_entries", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
-    "kueue_tas_host_last_records", "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
+    "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
     "kueue_tas_fits", "kueue_tas_host_update_usage", "kueue_tas_host_fits", "kueue_tas_host_preemption_search", "kueue_tas_host_update_pods",
     "kueue_tas_snapshot_set_free", "kueue_tas_snapshot_set_leaf_attrs", "kueue_tas_host_update_nodes",
     "kueue_tas_encode_v1beta2", "kueue_tas_snapshot_load_names", "kueue_tas_encode_v1beta2_leaves",
     "kueue_tas_host_v1beta2_from", "kueue_tas_host_internal_from", "kueue_tas_host_find_v1beta2",
-    "kueue_tas_host_v1beta2_last", "kueue_tas_host_last_results",
+    "kueue_tas_host_v1beta2_last", "kueue_tas_host_last_results", "kueue_tas_admit", "kueue_tas_host_set_shard",
+    "kueue_tas_host_last_assignments", "kueue_tas_host_admit", "kueue_tas_host_apply_deltas",
+    "kueue_tas_host_last_deltas", "kueue_tas_host_run", "kueue_tas_build_id",
 ]
+
+# the Makefile's SRC_HASH inputs, in order
+_HASHED_SOURCES = ("tas_device.hip", "tas_host.cpp", "tas_internal.h", "tas_kernels.hip", "json_reader.h",
+                   "label_selectors.h", os.path.join("..", "..", "include", "kueue_tas.h"))
+
+
+def source_hash() -> str | None:
+    """The build id a library built from this tree's sources reports (None when
+    the sources are not shipped next to the package)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in _HASHED_SOURCES:
+        p = os.path.join(_CSRC, f)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+# kueue_tas_delta {int32 leaf, int32 col, int64 delta} as a numpy record
+DELTA_DTYPE = [("leaf", "<i4"), ("col", "<i4"), ("delta", "<i8")]
 
 
 def load_library(path: str | None = None):
@@ -76,6 +100,11 @@ def load_library(path: str | None = None):
         raise NativeLibraryMissing(str(e)) from e
     _bind(lib)
     if path is None:
+        want = source_hash()
+        got = lib.kueue_tas_build_id().decode()
+        if want is not None and got != want:
+            raise NativeLibraryMissing(f"{p} was built from other sources (build id {got}, tree {want}): "
+                                       "run __graft_entry__.build()")
         _LIB = lib
     return lib
 
@@ -83,6 +112,7 @@ def load_library(path: str | None = None):
 def _bind(lib):
     c = ctypes
     lib.kueue_tas_abi_version.restype = c.c_int
+    lib.kueue_tas_build_id.restype = c.c_char_p
     lib.kueue_tas_host_create.argtypes = [c.c_char_p, c.POINTER(KueueTasConfig)]
     lib.kueue_tas_host_create.restype = c.c_void_p
     lib.kueue_tas_host_destroy.argtypes = [c.c_void_p]
@@ -96,8 +126,9 @@ def _bind(lib):
     lib.kueue_tas_host_compile.restype = c.c_int
     lib.kueue_tas_host_run_compiled.argtypes = [c.c_void_p, c.POINTER(c.c_uint64)]
     lib.kueue_tas_host_run_compiled.restype = c.c_int
+    lib.kueue_tas_host_run.argtypes = [c.c_void_p, c.c_uint32, c.POINTER(c.c_uint64)]
+    lib.kueue_tas_host_run.restype = c.c_int
     lib.kueue_tas_host_last_timings.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.POINTER(c.c_int64)]
-    lib.kueue_tas_host_last_records.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_stage_times.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int]
     lib.kueue_tas_host_last_eval_profile.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_device_host_times.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
@@ -115,6 +146,17 @@ def _bind(lib):
     lib.kueue_tas_host_find_v1beta2.restype = c.c_int
     lib.kueue_tas_host_v1beta2_last.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_last_results.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_set_shard.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.kueue_tas_host_set_shard.restype = c.c_int
+    lib.kueue_tas_host_last_assignments.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t)]
+    lib.kueue_tas_host_last_assignments.restype = c.c_int
+    lib.kueue_tas_host_admit.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
+                                         c.POINTER(c.c_size_t), c.POINTER(c.c_size_t)]
+    lib.kueue_tas_host_last_deltas.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.kueue_tas_host_last_deltas.restype = c.c_int
+    lib.kueue_tas_host_admit.restype = c.c_int
+    lib.kueue_tas_host_apply_deltas.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.kueue_tas_host_apply_deltas.restype = c.c_int
     lib.kueue_tas_host_last_results.restype = c.c_int
     lib.kueue_tas_host_v1beta2_last.restype = c.c_int
     lib.kueue_tas_host_preemption_search.argtypes = [c.c_void_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
@@ -326,16 +368,58 @@ class TASFlavorSnapshot:
             raise RuntimeError(self._err())
         return _take(self._lib, out)["results"]
 
-    def last_records(self, n: int):
-        """[n][4] int32 compact per-workload results of the last run_compiled."""
-        buf = (ctypes.c_int32 * (4 * n))()
-        self._lib.kueue_tas_host_last_records(self._h, buf, n)
-        return list(buf)
+    # ---- data-parallel batches (kueue_tas.h "Data-parallel batches") ----
+    def set_shard(self, ids):
+        """run_compiled evaluates only the compiled workloads `ids` (global indices)."""
+        import numpy as np
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        if self._lib.kueue_tas_host_set_shard(self._h, a.ctypes.data, a.size):
+            raise RuntimeError(self._err())
 
-    def run_compiled(self, want_hash: bool = False):
+    def last_assignments(self):
+        """int32 quads of the last run_compiled: per workload (id, -1, failed, n)
+        then (id, podset, leaf, count) per assigned domain."""
+        import numpy as np
+        n = ctypes.c_size_t()
+        rc = self._lib.kueue_tas_host_last_assignments(self._h, None, 0, ctypes.byref(n))
+        if rc not in (0, -5):
+            raise RuntimeError(self._err())
+        buf = np.empty(n.value, dtype=np.int32)
+        if self._lib.kueue_tas_host_last_assignments(self._h, buf.ctypes.data, buf.size, ctypes.byref(n)):
+            raise RuntimeError(self._err())
+        return buf
+
+    def admit(self, quads):
+        """Admission (Fits + AddUsage, in workload order) over gathered quads on this
+        replica; returns (admitted (id, 0/1) pairs [n, 2], deltas numpy DELTA_DTYPE)."""
+        import numpy as np
+        q = np.ascontiguousarray(quads, dtype=np.int32)
+        heads = int(np.unique(q[0::4]).size) if q.size else 0
+        adm = np.zeros((heads, 2), dtype=np.int32)
+        nw = ctypes.c_size_t()
+        nd = ctypes.c_size_t()
+        if self._lib.kueue_tas_host_admit(self._h, q.ctypes.data, q.size, adm.ctypes.data, adm.size,
+                                          ctypes.byref(nw), ctypes.byref(nd)):
+            raise RuntimeError(self._err())
+        deltas = np.zeros(nd.value, dtype=DELTA_DTYPE)
+        if self._lib.kueue_tas_host_last_deltas(self._h, deltas.ctypes.data, deltas.size):
+            raise RuntimeError(self._err())
+        return adm[: nw.value], deltas
+
+    def apply_deltas(self, deltas):
+        """Apply another replica's admission deltas (numpy DELTA_DTYPE)."""
+        import numpy as np
+        d = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
+        if self._lib.kueue_tas_host_apply_deltas(self._h, d.ctypes.data, d.size):
+            raise RuntimeError(self._err())
+
+    RUN_COMPILE = 1  # KUEUE_TAS_RUN_COMPILE: group + compile every TASPodSetRequests in the call
+    RUN_VALUES = 2   # KUEUE_TAS_RUN_VALUES: build the TopologyAssignment domains (Values, Count)
+
+    def run_compiled(self, want_hash: bool = False, flags: int = 0):
         """One timed step over the compiled workloads; returns the result hash if asked."""
         h = ctypes.c_uint64()
-        rc = self._lib.kueue_tas_host_run_compiled(self._h, ctypes.byref(h) if want_hash else None)
+        rc = self._lib.kueue_tas_host_run(self._h, flags, ctypes.byref(h) if want_hash else None)
         if rc != 0:
             raise RuntimeError(f"kueue_tas_host_run_compiled failed ({rc}): {self._err()}")
         return h.value if want_hash else None

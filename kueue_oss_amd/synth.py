@@ -101,7 +101,7 @@ def _mixed_workloads(rng, n, levels_req, lowest, highest):
     return wls
 
 
-def config_c2(seed=1234, n_workloads=1000):
+def config_c2(seed=1234, n_workloads=1000, shape=(2, 8, 32, 32)):
     """C2: zone/block/rack/hostname 2x8x32x32 = 16,384 nodes; 1k workloads:
     40% required (70% rack / 30% block), 40% preferred, 20% unconstrained or
     slice-only; pod count log-uniform [1,256]; cpu in {1,2,4,8}, memory 4Gi/cpu."""
@@ -112,7 +112,7 @@ def config_c2(seed=1234, n_workloads=1000):
         return {ZONE: f"zone-{p[0]}", BLOCK: f"block-{p[0]}-{p[1]}", RACK: f"rack-{p[0]}-{p[1]}-{p[2]}",
                 HOST: f"node-z{p[0]}-b{p[1]}-r{p[2]}-n{p[3]}"}
 
-    nodes = _tree_nodes((2, 8, 32, 32), labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
+    nodes = _tree_nodes(shape, labels, lambda i, p: {"cpu": 96000, "memory": 256 * GI, "pods": 110})
     usage = []
     for n in nodes:
         u = rng.randint(0, 8)
@@ -175,6 +175,51 @@ def config_c3(seed=7, n_workloads=1000, shape=(4, 16, 64, 32)):
     return snap, wls
 
 
+def config_c3j(seed=8, n_workloads=1000, shape=(4, 16, 64), rack_sizes=(20, 44)):
+    """C3 made adversarial: ragged racks (uniform in rack_sizes, mean 32, so
+    ~131k nodes and no uniform fan-out) and per-workload jittered cpu/memory
+    requests (every workload its own request signature and phase-1 class).
+    Same node resources, usage, taints, labels and request mix as C3."""
+    rng = random.Random(seed)
+    levels = [ZONE, BLOCK, RACK, HOST]
+    alloc = {"cpu": 192000, "memory": 1536 * GI, "amd.com/gpu": 8, "ephemeral-storage": 3500 * GI, "pods": 110}
+    nodes, pods, usage = [], [], []
+    for z in range(shape[0]):
+        for b in range(shape[1]):
+            for r in range(shape[2]):
+                for n in range(rng.randint(*rack_sizes)):
+                    name = f"node-{z}-{b}-{r}-{n}"
+                    t = rng.random()
+                    taints = ([{"key": "gpu-maint", "value": "true", "effect": "NoSchedule"}] if t < 0.10 else
+                              [{"key": "gpu-maint", "value": "true", "effect": "NoExecute"}] if t < 0.12 else [])
+                    labels = {ZONE: f"zone-{z}", BLOCK: f"block-{z}-{b}", RACK: f"rack-{z}-{b}-{r}",
+                              HOST: f"node-z{z}-b{b}-r{r}-n{n}", "cloud.provider.com/gpu-type": "abcd"[(r * 7 + n) % 4]}
+                    nodes.append(_node(name, labels, dict(alloc), taints))
+                    pods.append({"name": f"ds-{name}", "namespace": "kube-system", "nodeName": name,
+                                 "phase": "Running", "requests": {"cpu": 2000, "memory": 4 * GI}})
+                    g = rng.randint(0, 8)
+                    if g:
+                        usage.append({"values": [labels[HOST]],
+                                      "singlePodRequests": {"cpu": 24000, "memory": 192 * GI, "amd.com/gpu": 1,
+                                                            "ephemeral-storage": 100 * GI}, "count": g})
+    snap = {"levels": levels, "nodes": nodes, "pods": pods, "tasUsage": usage, "nodeLabels": {}, "featureGates": {}}
+    wls = []
+    for i in range(n_workloads):
+        gpus = rng.randint(1, 8)
+        req = {"cpu": 24000 * gpus - 250 * rng.randint(0, 40), "memory": 192 * GI * gpus - (1 << 26) * rng.randint(0, 63),
+               "amd.com/gpu": gpus, "ephemeral-storage": 100 * GI * gpus}
+        count = max(1, int(round(2 ** rng.uniform(0, 10))))
+        sel = {"cloud.provider.com/gpu-type": rng.choice("abcd")} if rng.random() < 0.3 else None
+        tol = [{"key": "gpu-maint", "operator": "Exists", "value": "", "effect": ""}] if rng.random() < 0.2 else []
+        if rng.random() < 0.5:
+            lvl = rng.choice([RACK, BLOCK])
+            kw = {"required": lvl} if rng.random() < 0.5 else {"preferred": lvl}
+            wls.append([_ps(f"ps{i}", count, req, selector=sel, tolerations=tol, **kw)])
+        else:
+            wls.append([_ps(f"ps{i}", count, req, unconstrained=True, selector=sel, tolerations=tol)])
+    return snap, wls
+
+
 def config_c4(seed=11, n_workloads=256, shape=(2, 16, 64, 32)):
     """C4: 2x16x64x32 = 65,536 nodes; JobSet-like workloads: a PodSet group
     {leader 1 pod cpu-only, workers 16-512 required block with 16-pod rack
@@ -220,7 +265,7 @@ def config_c5(seed=5, n_workloads=100000, shape=(8, 32, 128, 32)):
     return snap, _mixed_workloads(rng, n_workloads, [RACK, BLOCK], HOST, ZONE)
 
 
-CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C4": config_c4, "C5": config_c5}
+CONFIGS = {"C1": config_c1, "C2": config_c2, "C3": config_c3, "C3J": config_c3j, "C4": config_c4, "C5": config_c5}
 
 
 # ----------------------------------------------------------------------------

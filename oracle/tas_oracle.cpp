@@ -1335,6 +1335,7 @@ int tas_oracle_eval_workloads(const char* snapshot_json, const char* workloads_j
 //   {"op": "find", "podSets": [...], "simulateEmpty": bool} -> results list
 //   {"op": "fits", "usage": [{values, singlePodRequests, count}...]} -> bool
 //   {"op": "add" | "remove", "usage": [...]}                         -> null
+//   {"op": "admit", "usage": [...]}: fits, then add when it fits     -> bool
 // applied in order; returns {"results": [one entry per op]}.
 int tas_oracle_session(const char* snapshot_json, const char* ops_json, char** out_json) {
   using namespace oracle;
@@ -1365,6 +1366,11 @@ int tas_oracle_session(const char* snapshot_json, const char* ops_json, char** o
                                                                      sim && sim->as_bool()));
       } else if (kind == "fits") {
         out += snap->fits(parse_usage(op.at("usage"))) ? "true" : "false";
+      } else if (kind == "admit") {  // processEntry's TAS half: Fits, then AddUsage (scheduler.go:426-435)
+        auto us = parse_usage(op.at("usage"));
+        const bool ok = snap->fits(us);
+        if (ok) snap->update_usage(us, true);
+        out += ok ? "true" : "false";
       } else if (kind == "add" || kind == "remove") {
         snap->update_usage(parse_usage(op.at("usage")), kind == "add");
         out += "null";

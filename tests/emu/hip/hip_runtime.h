@@ -119,6 +119,11 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
   return o;
 }
 inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v; return o; }
+inline void __threadfence() {}
+// device-scope loads that bypass L1 on hardware; plain loads here
+#define __HIP_MEMORY_SCOPE_AGENT 3
+template <class T>
+inline T __hip_atomic_load(const T* p, int, int) { return *p; }
 using std::max;
 using std::min;
 

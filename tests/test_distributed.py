@@ -1,15 +1,24 @@
-"""Multi-rank path on CPU (gloo, world_size 2): cost-balanced sharding keeps
-every workload on exactly one rank, result records all-gather, and the
-admission delta list broadcasts identically to every replica."""
+"""Multi-rank path on CPU (gloo, world_size 2).
+
+Each rank holds a replica of the snapshot (here the emulated build of the
+product library, tests/emu), compiles the same global workload list and
+evaluates its cost-balanced shard; the full assignments are all-gathered,
+rank 0 admits in workload order (Fits + AddUsage: the TAS half of
+processEntry, pkg/scheduler/scheduler.go:371-435) and broadcasts the delta
+list it applied, the other replica applies it; a second batch then runs on
+the updated replicas.  Every assignment and admission decision must equal the
+oracle session: find every workload, admit them in order, find again."""
 import os
 import socket
 
+import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from kueue_oss_amd import sharding, synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
@@ -20,42 +29,85 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _workload(n=40):
+    return synth.config_c2(n_workloads=n, shape=(2, 2, 8, 16))
+
+
+def _worker(rank, world, port, q, lib_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    _, wls = synth.config_c2(n_workloads=50)
-    mine = sharding.shard_workloads(wls, world, rank)
-    # per-workload records: [global index, #podsets, 0, 0]
-    idx = {id(w): i for i, w in enumerate(wls)}
-    recs = []
-    for w in mine:
-        recs += [idx[id(w)], len(w), 0, 0]
-    got = sharding.gather_records(recs, world, dist)
-    deltas = [(3, 1, 1000), (7, 0, -5)] if rank == 0 else None
-    bd = sharding.broadcast_deltas(deltas, dist, src=0)
-    q.put((rank, got, bd))
-    dist.destroy_process_group()
+    try:
+        from kueue_oss_amd import TASFlavorSnapshot, native
+
+        lib = native.load_library(lib_path)
+        snap_doc, wls = _workload()
+        ids = sharding.shard_ids(wls, world, rank)
+        snap = TASFlavorSnapshot(snap_doc, lib=lib)
+        snap.compile(wls)
+        snap.set_shard(ids)
+        out = {"ids": ids}
+        snap.run_compiled()
+        out["batch1"] = snap.last_results()
+        quads, admitted, deltas = sharding.admit_round(snap, world, rank, dist)
+        out["quads"] = quads.tolist()
+        out["admitted"] = admitted.tolist() if admitted is not None else None
+        out["deltas"] = deltas.tolist()
+        snap.run_compiled()
+        out["batch2"] = snap.last_results()
+        snap.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2])
-def test_gloo_shard_gather_broadcast(world):
+def test_gloo_shard_gather_admit_broadcast(world, emu_lib):
+    import oracle_lib
+
+    lib_path = os.path.join(HERE, "emu", "_build", "libkueue_tas_emu.so")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, lib_path)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=120) for _ in range(world)]
+    outs = dict(q.get(timeout=600) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    out.sort()
-    gathered = out[0][1]
-    assert gathered == out[1][1]
-    seen = sorted(r[i] for r in gathered for i in range(0, len(r), 4))
-    assert seen == list(range(50))  # each workload on exactly one rank
-    assert out[0][2] == out[1][2] == [(3, 1, 1000), (7, 0, -5)]
+    snap_doc, wls = _workload()
+    n = len(wls)
+    # every workload on exactly one rank
+    assert sorted(i for r in range(world) for i in outs[r]["ids"]) == list(range(n))
+    # identical gathered assignments and deltas everywhere
+    assert outs[0]["quads"] == outs[1]["quads"]
+    assert outs[0]["deltas"] == outs[1]["deltas"]
+
+    def by_id(key):
+        res = {}
+        for r in range(world):
+            for i, rs in zip(outs[r]["ids"], outs[r][key]):
+                res[i] = rs
+        return [res[i] for i in range(n)]
+
+    b1, b2 = by_id("batch1"), by_id("batch2")
+    # the oracle session: find all, admit in order the ones without failure, find all again
+    ops = [{"op": "find", "podSets": w} for w in wls]
+    admit_idx = []
+    for i, w in enumerate(wls):
+        if all(not r["reason"] for r in b1[i]):
+            ops.append({"op": "admit", "usage": synth.usage_records(w, b1[i])})
+            admit_idx.append(i)
+    ops += [{"op": "find", "podSets": w} for w in wls]
+    res = oracle_lib.session(snap_doc, ops)
+    assert b1 == res[:n]
+    want_admit = dict(zip(admit_idx, res[n:n + len(admit_idx)]))
+    got_admit = {int(i): bool(a) for i, a in outs[0]["admitted"]}
+    assert {i: got_admit[i] for i in want_admit} == want_admit
+    assert all(not got_admit[i] for i in range(n) if i not in want_admit)
+    assert any(want_admit.values()) and not all(want_admit.values())
+    assert b2 == res[n + len(admit_idx):]
 
 
 def test_shard_is_cost_balanced():
@@ -64,3 +116,17 @@ def test_shard_is_cost_balanced():
     assert sum(len(s) for s in shards) == 400
     loads = [sum(sharding.workload_cost(w) for w in s) for s in shards]
     assert max(loads) - min(loads) <= 4.0
+    ids = [sharding.shard_ids(wls, 4, r) for r in range(4)]
+    assert sorted(i for s in ids for i in s) == list(range(400))
+    assert [[wls[i] for i in s] for s in ids] == shards
+
+
+def test_delta_records_roundtrip():
+    from kueue_oss_amd.native import DELTA_DTYPE
+
+    d = np.zeros(3, dtype=DELTA_DTYPE)
+    d["leaf"] = [1, 2, 3]
+    d["col"] = [0, 4, 2]
+    d["delta"] = [-5, 1 << 40, 7]
+    words = d.view(np.int64).reshape(3, 2)
+    assert words.reshape(-1).view(DELTA_DTYPE).tolist() == d.tolist()
