@@ -674,7 +674,7 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_terms = (n * sizeof(kueue_tas_fits_req) + 255) / 256 * 256;
   const size_t o_off = o_terms + (num_terms * sizeof(kueue_tas_fits_term) + 255) / 256 * 256;
   const size_t o_out = o_off + ((n_wl + 1) * 8 + 255) / 256 * 256;
-  HIPCHK(c, c->d_fits.ensure(o_out + n_wl * 4));
+  HIPCHK(c, c->d_fits.ensure(o_out + (n_wl + 1) * 4));  // + the kernel's sink word
   uint8_t* d = c->d_fits.p;
   if (n) HIPCHK(c, hipMemcpyAsync(d, reqs, n * sizeof(kueue_tas_fits_req), hipMemcpyHostToDevice, c->stream));
   if (num_terms)

@@ -214,6 +214,16 @@ __device__ __forceinline__ bool sorted_contains(const int32_t* v, int len, int32
 // (host: labels.Requirement / fields selector folded against the snapshot's
 // label dictionaries) is "the leaf's id is in a sorted set" XOR negate.
 // [rb, re) is wave-uniform; an empty range matches no leaf (no terms).
+// Label value id of `leaf` in column `col` (wave-uniform): one of the first
+// kStagedLabels columns held in registers (l0..l3), else a load.
+__device__ __forceinline__ int32_t staged_label(const DevSnap& s, int leaf, int col, int32_t l0, int32_t l1, int32_t l2,
+                                                int32_t l3) {
+  if (col == 0) return l0;
+  if (col == 1) return l1;
+  if (col == 2) return l2;
+  if (col == 3) return l3;
+  return s.label_values[int64_t(col) * s.N + leaf];
+}
 template <class LabelAt>
 __device__ __forceinline__ bool affinity_match(const DevBatch& b, int rb, int re, int leaf, LabelAt label_at) {
   if (rb >= re) return false;
@@ -550,14 +560,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   int32_t lab[kStagedLabels];
 #pragma unroll
   for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
-  auto label_at = [&](int col) -> int32_t {  // col is wave-uniform
-    if (col < kStagedLabels) {
-      int32_t v = lab[0];
-#pragma unroll
-      for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
-      return v;
-    }
-    return s.label_values[int64_t(col) * N + leaf];
+  static_assert(kStagedLabels == 4, "staged_label takes four staged columns");
+  const int32_t lab0 = lab[0], lab1 = lab[1], lab2 = lab[2], lab3 = lab[3];
+  auto label_at = [s, leaf, lab0, lab1, lab2, lab3](int col) {  // by value: nothing escapes to scratch
+    return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
   };
 
   // ---- the chunk's request signature (first member): counts once per leaf ----
@@ -852,14 +858,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   int32_t lab[kStagedLabels];
 #pragma unroll
   for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
-  auto label_at = [&](int col) -> int32_t {  // col is wave-uniform
-    if (col < kStagedLabels) {
-      int32_t v = lab[0];
-#pragma unroll
-      for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
-      return v;
-    }
-    return s.label_values[int64_t(col) * N + leaf];
+  static_assert(kStagedLabels == 4, "staged_label takes four staged columns");
+  const int32_t lab0 = lab[0], lab1 = lab[1], lab2 = lab[2], lab3 = lab[3];
+  auto label_at = [s, leaf, lab0, lab1, lab2, lab3](int col) {  // by value: nothing escapes to scratch
+    return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
   };
   for (int e = 0; e < ne; e++) {
     int kind = EX_NONE, id = -1;
@@ -3675,7 +3677,10 @@ __global__ void fits_kernel(DevSnap s, const kueue_tas_fits_req* reqs, int n, co
 // single x count plus pods:count added to the leaf's tasUsage, keys created).
 // One wave walks the workloads in order (the dependency chain); its lanes
 // split a workload's records.  tas_usage / usage_present are read with
-// L1-bypassing loads because this wave's own atomics updated them.
+// L1-bypassing loads because this wave's own atomics updated them, and the
+// atomics return values the wave consumes, so each admitted workload's
+// updates have completed before the next workload's loads issue (no
+// __threadfence: that costs microseconds per call on gfx950).
 __device__ __forceinline__ int64_t load_l2(const int64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -3686,6 +3691,7 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
                                                    const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
                                                    const int64_t* wl_off, int n_wl, int pods_col, int32_t* admitted) {
   const int lane = lane_id();
+  unsigned long long sink = 0;
   for (int w = 0; w < n_wl; w++) {
     const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
     bool all_fit = true;
@@ -3731,20 +3737,20 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
       for (int k = 0; k < r.num_terms; k++) {
         const kueue_tas_fits_term t = terms[r.term_begin + k];
         if (t.col < 0) continue;  // the host gives every usage resource a column first
-        atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
-                  (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
+        sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
+                          (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
         bits |= 1u << t.col;
       }
       if (pods_col >= 0) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
-                  (unsigned long long)int64_t(r.count));
+        sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                          (unsigned long long)int64_t(r.count));
         bits |= 1u << pods_col;
       }
-      atomicOr(usage_present + r.leaf, bits);
+      sink += atomicOr(usage_present + r.leaf, bits);
     }
-    __threadfence();
     wave_sync();
   }
+  if (lane == 0) admitted[n_wl] = int32_t(uint32_t(sink));  // consumes the returned values (see above)
 }
 
 }  // namespace ktas
