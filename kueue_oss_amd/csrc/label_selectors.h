@@ -28,6 +28,7 @@
 #include <optional>
 #include <set>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace kueue_tas {
@@ -136,23 +137,23 @@ inline std::string regex_msg(std::string msg, const char* re, std::initializer_l
 }
 inline bool alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
 // ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]
-inline bool qualified_name_ok(const std::string& s) {
+inline bool qualified_name_ok(std::string_view s) {
   if (s.empty() || !alnum(s.front()) || !alnum(s.back())) return false;
   for (char c : s)
     if (!alnum(c) && c != '-' && c != '_' && c != '.') return false;
   return true;
 }
 // [a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*
-inline bool dns_subdomain_ok(const std::string& s) {
+inline bool dns_subdomain_ok(std::string_view s) {
   auto lc = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
   size_t b = 0;
   for (;;) {
     const size_t e = s.find('.', b);
-    const size_t len = (e == std::string::npos ? s.size() : e) - b;
+    const size_t len = (e == std::string_view::npos ? s.size() : e) - b;
     if (len == 0 || !lc(s[b]) || !lc(s[b + len - 1])) return false;
     for (size_t k = b; k < b + len; k++)
       if (!lc(s[k]) && s[k] != '-') return false;
-    if (e == std::string::npos) return true;
+    if (e == std::string_view::npos) return true;
     b = e + 1;
   }
 }
@@ -201,6 +202,38 @@ inline std::string label_value_problems(const std::string& v) {
                    "(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?", {"MyValue", "my_value", "12345"});
   }
   return o;
+}
+
+// Allocation-free equivalents of label_key_problems(k).empty() and
+// label_value_problems(v).empty(): the common (valid) case of every compile.
+inline bool label_key_ok(std::string_view k) {
+  std::string_view name = k;
+  const size_t slash = k.find('/');
+  if (slash != std::string_view::npos) {
+    if (k.find('/', slash + 1) != std::string_view::npos) return false;
+    const std::string_view prefix = k.substr(0, slash);
+    if (prefix.empty() || prefix.size() > 253 || !dns_subdomain_ok(prefix)) return false;
+    name = k.substr(slash + 1);
+  }
+  return !name.empty() && name.size() <= 63 && qualified_name_ok(name);
+}
+inline bool label_value_ok(std::string_view v) { return v.size() <= 63 && (v.empty() || qualified_name_ok(v)); }
+// labels.NewRequirement succeeds (requirement_errors would add nothing)
+inline bool requirement_ok(const std::string& key, const std::string& op, const std::optional<std::vector<std::string>>& vals) {
+  if (!label_key_ok(key)) return false;
+  const size_t n = vals ? vals->size() : 0;
+  if (op == "In" || op == "NotIn") {
+    if (n == 0) return false;
+  } else if (op == "=") {
+    if (n != 1) return false;
+  } else if (op == "Exists" || op == "DoesNotExist") {
+    if (n != 0) return false;
+  } else {
+    if (n != 1 || !parse_int((*vals)[0], nullptr)) return false;
+  }
+  for (size_t i = 0; i < n; i++)
+    if (!label_value_ok((*vals)[i])) return false;
+  return true;
 }
 
 // ---- error collection --------------------------------------------------------
@@ -258,6 +291,7 @@ inline std::string aggregate(const std::vector<std::string>& msgs) {
 // here the smallest invalid key is reported (deterministic).
 inline std::string node_selector_failure(const std::map<std::string, std::string>& sel) {
   for (auto& kv : sel) {
+    if (label_key_ok(kv.first) && label_value_ok(kv.second)) continue;
     std::vector<std::string> errs;
     requirement_errors("", kv.first, "=", std::vector<std::string>{kv.second}, &errs);
     if (errs.empty()) continue;
@@ -291,7 +325,20 @@ inline std::string node_selector_string(const RequiredAffinity& terms) {
 
 // "invalid affinity node selectors: ..." reason, or "" when every non-empty
 // term parses (nodeaffinity.NewNodeSelector).
+inline bool affinity_ok(const RequiredAffinity& terms) {
+  for (const Term& t : terms) {
+    for (const Expr& e : t.exprs) {
+      const bool known = e.op == "In" || e.op == "NotIn" || e.op == "Exists" || e.op == "DoesNotExist" ||
+                         e.op == "Gt" || e.op == "Lt";
+      if (!known || !requirement_ok(e.key, e.op, e.values)) return false;
+    }
+    for (const Expr& e : t.fields)
+      if (!(e.op == "In" || e.op == "NotIn") || !e.values || e.values->size() != 1) return false;
+  }
+  return true;
+}
 inline std::string affinity_failure(const RequiredAffinity& terms) {
+  if (affinity_ok(terms)) return "";
   std::vector<std::string> errs;
   for (size_t i = 0; i < terms.size(); i++) {
     const Term& t = terms[i];

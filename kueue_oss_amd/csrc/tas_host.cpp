@@ -23,6 +23,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <stdexcept>
@@ -53,6 +54,15 @@ static void req_sub(Requests& r, const Requests& o) {
 static int32_t go_div32(int32_t a, int32_t b) {
   if (b == -1) return int32_t(0u - uint32_t(a));
   return a / b;
+}
+
+// Resource names interned process-wide (ids never change): a compiled request
+// maps each name to its snapshot column through one array lookup.
+static int32_t intern_resource(const std::string& name) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, int32_t> ids;
+  std::lock_guard<std::mutex> lock(mu);
+  return ids.emplace(name, int32_t(ids.size())).first->second;
 }
 
 struct Taint {
@@ -113,6 +123,20 @@ static bool tolerates(const Toleration& t, const Taint& x) {
   return false;
 }
 
+// decimal text of v appended to out (strconv.FormatInt; no locale, no allocation)
+static void append_int(std::string& out, int64_t v) {
+  char b[24];
+  char* e = b + sizeof b;
+  char* p = e;
+  uint64_t u = v < 0 ? uint64_t(0) - uint64_t(v) : uint64_t(v);
+  do {
+    *--p = char('0' + u % 10);
+    u /= 10;
+  } while (u);
+  if (v < 0) *--p = '-';
+  out.append(p, size_t(e - p));
+}
+
 static std::string go_quote(const std::string& s) {  // strconv.Quote for ASCII input
   std::string o = "\"";
   for (unsigned char c : s) {
@@ -152,6 +176,7 @@ struct TASPodSetRequests {  // tas_flavor_snapshot.go:356-367
   std::string name;
   std::optional<TopologyRequest> topologyRequest;
   Requests singlePodRequests;
+  std::vector<std::pair<int32_t, int64_t>> requestIds;  // singlePodRequests by interned name, same order
   int32_t count = 0;
   bool implied = false;
   std::optional<std::string> podSetGroupName;
@@ -227,6 +252,14 @@ struct Workload {
 class FlavorSnapshot {
  public:
   std::string topologyName = "default";
+  mutable std::string topoQuoted, topoQuotedFor;
+  const std::string& topology_quoted() const {  // strconv.Quote(topologyName), kept between failures
+    if (topoQuoted.empty() || topoQuotedFor != topologyName) {
+      topoQuoted = go_quote(topologyName);
+      topoQuotedFor = topologyName;
+    }
+    return topoQuoted;
+  }
   std::vector<std::string> levelKeys;
   std::vector<Toleration> flavorTolerations;
   bool lowestIsHostname = false;
@@ -251,6 +284,7 @@ class FlavorSnapshot {
   std::vector<std::string> cols;
   std::map<std::string, int32_t> colByName;
   std::vector<std::vector<Taint>> profiles;
+  std::vector<std::vector<int32_t>> profileTaintIds;  // taintIdByString[taint_string(t)] per profile taint
   std::vector<int32_t> leafProfile;
   std::vector<std::string> taintStrings;
   std::map<std::string, int32_t> taintIdByString;
@@ -543,6 +577,9 @@ class FlavorSnapshot {
       }
     }
     if (profiles.empty()) profiles.push_back({});
+    profileTaintIds.assign(profiles.size(), {});
+    for (size_t p = 0; p < profiles.size(); p++)
+      for (auto& t : profiles[p]) profileTaintIds[p].push_back(taintIdByString.at(taint_string(t)));
     leafByNodeName.clear();
     unnamedLeaves.clear();
     if (lowestIsHostname)
@@ -710,14 +747,29 @@ class FlavorSnapshot {
     col_gen = ++gen_counter;
     cols.assign(names.begin(), names.end());
     colByName.clear();
-    for (size_t i = 0; i < cols.size(); i++) colByName[cols[i]] = int32_t(i);
+    colOfId.clear();
+    for (size_t i = 0; i < cols.size(); i++) {
+      colByName[cols[i]] = int32_t(i);
+      const size_t id = size_t(intern_resource(cols[i]));
+      if (colOfId.size() <= id) colOfId.resize(id + 1, -1);
+      colOfId[id] = int32_t(i);
+    }
+    auto pc = colByName.find("pods");
+    podsCol = pc == colByName.end() ? -1 : pc->second;
     if (cols.size() > KUEUE_TAS_MAX_COLS) throw std::runtime_error("too many resource columns");
     dirty = true;
     compile_gen++;
   }
   // Requests may name resources no node has: they become all-absent columns.
   // Returns true when the column set changed (compiled requests are stale).
+  std::vector<int32_t> colOfId;  // interned resource id -> column, -1 when none
+  int32_t podsCol = -1;
+  int32_t col_of(int32_t id) const { return size_t(id) < colOfId.size() ? colOfId[size_t(id)] : -1; }
   bool ensure_columns_for(const std::vector<TASPodSetRequests>& podsets) {
+    bool known = true;
+    for (auto& p : podsets)
+      for (auto& kv : p.requestIds) known = known && col_of(kv.first) >= 0;
+    if (known) return false;
     std::set<std::string> names(cols.begin(), cols.end());
     size_t before = names.size();
     for (auto& p : podsets)
@@ -923,16 +975,44 @@ class FlavorSnapshot {
     if (!tr || tr->required || tr->preferred) return false;
     return tr->sliceRequiredTopology.has_value() || !tr->constraints.empty();
   }
-  std::optional<std::string> level_key(const TASPodSetRequests& r) const {  // :1112-1138
+  const std::string* level_key(const TASPodSetRequests& r) const {  // :1112-1138
     const auto& tr = r.topologyRequest;
     if (tr) {
-      if (tr->required) return tr->required;
-      if (tr->preferred) return tr->preferred;
-      if (slice_only(tr)) return levelKeys.front();
-      if (tr->unconstrained.value_or(false)) return levelKeys.back();
+      if (tr->required) return &*tr->required;
+      if (tr->preferred) return &*tr->preferred;
+      if (slice_only(tr)) return &levelKeys.front();
+      if (tr->unconstrained.value_or(false)) return &levelKeys.back();
     }
-    if (r.implied) return levelKeys.back();
-    return std::nullopt;
+    if (r.implied) return &levelKeys.back();
+    return nullptr;
+  }
+  // requests + pods:1 (:820-826) written as (column, value) in column order
+  // (std::map order == column order: columns are the sorted names)
+  int32_t emit_requests(const std::vector<std::pair<int32_t, int64_t>>& r, int32_t* col, int64_t* val) const {
+    if (podsCol < 0) throw std::runtime_error("internal: no pods column");
+    int32_t n = 0;
+    bool pods = false;
+    for (auto& kv : r) {
+      const int32_t c = col_of(kv.first);
+      if (c < 0) throw std::runtime_error("internal: request resource without a column");
+      if (!pods && c >= podsCol) {
+        pods = true;
+        if (c == podsCol) {
+          col[n] = c;
+          val[n++] = add64(kv.second, 1);
+          continue;
+        }
+        col[n] = podsCol;
+        val[n++] = 1;
+      }
+      col[n] = c;
+      val[n++] = kv.second;
+    }
+    if (!pods) {
+      col[n] = podsCol;
+      val[n++] = 1;
+    }
+    return n;
   }
 
   uint64_t compile_gen = 1;  // bumped whenever compiled requests may change
@@ -944,14 +1024,6 @@ class FlavorSnapshot {
     g.compiled = true;
     g.early_reason.clear();
     g.layer_names.clear();
-    // requests + pods:1 (:820-826); columns were ensured by ensure_columns_for()
-    Requests req = w.singlePodRequests;
-    req["pods"] = add64(req["pods"], 1);
-    Requests lreq;
-    if (g.leader) {
-      lreq = g.leader->singlePodRequests;
-      lreq["pods"] = add64(lreq["pods"], 1);
-    }
     const auto& tr = w.topologyRequest;
     // getSliceSizeWithSinglePodAsDefault (:1162-1180)
     int32_t sliceSize = 1;
@@ -972,7 +1044,7 @@ class FlavorSnapshot {
     g.slice_size = sliceSize;
     bool required = tr && tr->required.has_value();
     bool unconstrained = (tr && tr->unconstrained.value_or(false)) || w.implied || slice_only(tr);
-    auto key = level_key(w);
+    const std::string* key = level_key(w);
     if (!key) {
       g.early_reason = "topology level not specified";
       return;
@@ -982,11 +1054,12 @@ class FlavorSnapshot {
       g.early_reason = "no requested topology level: " + *key;
       return;
     }
-    std::string sliceKey = levelKeys.back();
+    const std::string* sliceKeyP = &levelKeys.back();
     if (tr) {
-      if (tr->sliceRequiredTopology) sliceKey = *tr->sliceRequiredTopology;
-      else if (!tr->constraints.empty()) sliceKey = tr->constraints[0].topology;
+      if (tr->sliceRequiredTopology) sliceKeyP = &*tr->sliceRequiredTopology;
+      else if (!tr->constraints.empty()) sliceKeyP = &tr->constraints[0].topology;
     }
+    const std::string& sliceKey = *sliceKeyP;
     int sliceLevel = resolve(sliceKey);
     if (sliceLevel < 0) {
       g.early_reason = "no requested topology level for slices: " + sliceKey;
@@ -1052,31 +1125,20 @@ class FlavorSnapshot {
         q.num_layers++;
       }
     }
-    for (auto& kv : req) {  // std::map order == column order (sorted names)
-      q.req_col[q.num_req] = colByName[kv.first];
-      q.req_val[q.num_req] = kv.second;
-      q.num_req++;
-    }
-    for (auto& kv : lreq) {
-      q.leader_col[q.num_leader_req] = colByName[kv.first];
-      q.leader_val[q.num_leader_req] = kv.second;
-      q.num_leader_req++;
-    }
+    // columns were ensured by ensure_columns_for()
+    q.num_req = emit_requests(w.requestIds, q.req_col, q.req_val);
+    if (g.leader) q.num_leader_req = emit_requests(g.leader->requestIds, q.leader_col, q.leader_val);
     // tolerations = podset + flavor (:877); first untolerated NoSchedule/NoExecute taint per profile
-    std::vector<Toleration> tols = w.tolerations;
-    tols.insert(tols.end(), flavorTolerations.begin(), flavorTolerations.end());
     g.taint_row.assign(profiles.size(), -1);
     if (lowestIsHostname) {
       for (size_t p = 0; p < profiles.size(); p++) {
-        for (auto& t : profiles[p]) {
+        for (size_t k = 0; k < profiles[p].size(); k++) {
+          const Taint& t = profiles[p][k];
           bool ok = false;
-          for (auto& tol : tols)
-            if (tolerates(tol, t)) {
-              ok = true;
-              break;
-            }
+          for (auto& tol : w.tolerations) ok = ok || tolerates(tol, t);
+          for (auto& tol : flavorTolerations) ok = ok || tolerates(tol, t);
           if (!ok) {
-            g.taint_row[p] = taintIdByString[taint_string(t)];
+            g.taint_row[p] = profileTaintIds[p][k];
             break;
           }
         }
@@ -1246,47 +1308,86 @@ class FlavorSnapshot {
       if (v <= 0) continue;
       if (first) {
         out += ". Total nodes: ";
-        out += std::to_string(o.total_nodes);
+        append_int(out, o.total_nodes);
         out += "; excluded: ";
         first = false;
       } else {
         out += ", ";
       }
       out += r.first;
-      out += std::to_string(v);
+      append_int(out, v);
+    }
+  }
+  // notFitMessage / multiLayerNotFitMessage text written into m (cleared
+  // first; its storage is reused from one failure to the next)
+  void failure_reason(std::string& m, const GroupEval& g, const kueue_tas_eval_out& o, const int32_t* taints,
+                      const int32_t* res) const {
+    m.clear();
+    auto put = [&](int64_t v) { append_int(m, v); };
+    switch (o.status) {
+      case KUEUE_TAS_ST_NO_DOMAINS:
+        m += "no topology domains at level: ";
+        m += levelKeys[o.a];
+        return;
+      case KUEUE_TAS_ST_NOT_FIT: {
+        m += "topology ";
+        m += topology_quoted();
+        if (o.a == 0) {
+          m += " doesn't allow to fit any of ";
+        } else {
+          m += " allows to fit only ";
+          put(o.a);
+          m += " out of ";
+        }
+        put(o.b);
+        m += g.slice_size == 1 ? " pod(s)" : " slice(s)";
+        format_stats(m, o, taints, res);
+        return;
+      }
+      case KUEUE_TAS_ST_MULTILAYER: {
+        m += "topology ";
+        m += topology_quoted();
+        m += " doesn't allow to fit";
+        if (values[o.a].empty()) return;
+        for (int c = 0; c < g.req.num_layers; c++) {
+          m += "; ";
+          put(o.ml_fit[c]);
+          m += "/";
+          put(o.ml_need[c]);
+          m += " slice(s) fit on level ";
+          m += g.layer_names[c];
+        }
+        format_stats(m, o, taints, res);
+        return;
+      }
+      default:
+        m += "internal: device evaluation exceeded its list/output capacity";
     }
   }
   std::string failure_reason(const GroupEval& g, const kueue_tas_eval_out& o, const int32_t* taints,
                              const int32_t* res) const {
-    const std::string topo = go_quote(topologyName);
-    switch (o.status) {
-      case KUEUE_TAS_ST_NO_DOMAINS:
-        return "no topology domains at level: " + levelKeys[o.a];
-      case KUEUE_TAS_ST_NOT_FIT: {
-        std::string unit = g.slice_size == 1 ? "pod" : "slice";
-        std::string m = o.a == 0 ? "topology " + topo + " doesn't allow to fit any of " + std::to_string(o.b) + " " + unit + "(s)"
-                                 : "topology " + topo + " allows to fit only " + std::to_string(o.a) + " out of " +
-                                       std::to_string(o.b) + " " + unit + "(s)";
-        format_stats(m, o, taints, res);
-        return m;
-      }
-      case KUEUE_TAS_ST_MULTILAYER: {
-        std::string m = "topology " + topo + " doesn't allow to fit";
-        if (values[o.a].empty()) return m;
-        for (int c = 0; c < g.req.num_layers; c++)
-          m += "; " + std::to_string(o.ml_fit[c]) + "/" + std::to_string(o.ml_need[c]) + " slice(s) fit on level " +
-               g.layer_names[c];
-        format_stats(m, o, taints, res);
-        return m;
-      }
-      default:
-        return "internal: device evaluation exceeded its list/output capacity";
-    }
+    std::string m;
+    failure_reason(m, g, o, taints, res);
+    return m;
   }
 };
 
 // FindTopologyAssignmentsForFlavor (:519-594): groups in first-seen order
+// (GroupEval storage is reused across calls: a regroup keeps the vectors' capacity)
 static void make_groups(Workload& wl) {
+  bool named = false;
+  for (auto& p : wl.podsets) named |= p.podSetGroupName.has_value();
+  if (!named) {  // every PodSet is its own group
+    wl.groups.resize(wl.podsets.size());
+    for (size_t i = 0; i < wl.podsets.size(); i++) {
+      GroupEval& g = wl.groups[i];
+      g.compiled = false;
+      g.members.assign(1, &wl.podsets[i]);
+      g.workers = &wl.podsets[i];
+      g.leader = nullptr;
+    }
+    return;
+  }
   std::vector<std::string> order;
   std::map<std::string, std::vector<const TASPodSetRequests*>> grouped;
   for (size_t i = 0; i < wl.podsets.size(); i++) {
@@ -1359,6 +1460,7 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
     r.implied = tr.null();
     if (auto im = ps.find("implied")) r.implied = im->b();
     for (auto& kv : ps["requests"].fields) r.singlePodRequests[kv.first] = kv.second.i64();
+    for (auto& kv : r.singlePodRequests) r.requestIds.emplace_back(intern_resource(kv.first), kv.second);
     r.count = int32_t(ps["count"].i64());
     if (!ps["podSetGroupName"].null()) r.podSetGroupName = ps["podSetGroupName"].s();
     for (auto& t : ps["tolerations"].items)
@@ -1407,6 +1509,7 @@ struct Evaluator {
   std::vector<int32_t> p0_affv;
   std::vector<std::pair<size_t, GroupEval*>> p0_batch, p0_early;
   std::vector<size_t> used;  // results set per workload in this run
+  std::string reasonBuf;
 
   // Results are updated in place (member order = first set in this run), so
   // repeated runs reuse the strings' and vectors' storage.
@@ -1443,6 +1546,8 @@ struct Evaluator {
     bt.clear();
     early.clear();
     std::map<std::vector<int32_t>, int32_t> rowOff;
+    const std::vector<int32_t>* lastRow = nullptr;
+    int32_t lastOff = 0;
     for (size_t w = 0; w < wls.size(); w++) {
       if (done[w] || pass >= wls[w].groups.size()) continue;
       GroupEval& g = wls[w].groups[pass];
@@ -1452,12 +1557,16 @@ struct Evaluator {
       }
       rq.push_back(g.req);
       kueue_tas_eval_req& q = rq.back();
-      auto it = rowOff.find(g.taint_row);
-      if (it == rowOff.end()) {
-        it = rowOff.emplace(g.taint_row, int32_t(tt.size())).first;
-        tt.insert(tt.end(), g.taint_row.begin(), g.taint_row.end());
+      if (!lastRow || *lastRow != g.taint_row) {  // consecutive requests mostly share a row
+        auto it = rowOff.find(g.taint_row);
+        if (it == rowOff.end()) {
+          it = rowOff.emplace(g.taint_row, int32_t(tt.size())).first;
+          tt.insert(tt.end(), g.taint_row.begin(), g.taint_row.end());
+        }
+        lastRow = &g.taint_row;
+        lastOff = it->second;
       }
-      q.taint_table = it->second;
+      q.taint_table = lastOff;
       q.affinity_begin = int32_t(af.size());
       if (q.flags & KUEUE_TAS_F_AFFINITY) {  // rebase the group's requirements into the batch tables
         const int32_t vb = int32_t(afv.size());
@@ -1605,9 +1714,8 @@ struct Evaluator {
         GroupEval& g = *(*bt)[i].second;
         const kueue_tas_eval_out& o = outs[i];
         if (o.status != KUEUE_TAS_ST_OK) {
-          std::string reason = snap->failure_reason(g, o, taint_counts.data() + i * std::max<size_t>(T, 1),
-                                                    res_counts.data() + i * R);
-          for (auto* m : g.members) set_result((*results)[w], used[w], m->name, false, nullptr, 0, reason);
+          snap->failure_reason(reasonBuf, g, o, taint_counts.data() + i * std::max<size_t>(T, 1), res_counts.data() + i * R);
+          for (auto* m : g.members) set_result((*results)[w], used[w], m->name, false, nullptr, 0, reasonBuf);
           done[w] = 1;
           continue;
         }
@@ -1618,8 +1726,8 @@ struct Evaluator {
         if (pass + 1 < wls[w].groups.size()) {
           auto add = [&](const TASPodSetRequests* tr, const DomainAssignment* ds, int32_t nd) {
             for (int32_t k = 0; k < nd; k++)
-              for (auto& kv : tr->singlePodRequests) {
-                int64_t& slot = assumedBy[w][ds[k].leaf][snap->colByName[kv.first]];
+              for (auto& kv : tr->requestIds) {
+                int64_t& slot = assumedBy[w][ds[k].leaf][snap->col_of(kv.first)];
                 slot = add64(slot, mul64(kv.second, ds[k].count));
               }
           };
