@@ -383,7 +383,29 @@ class FlavorSnapshot {
     }
   }
   // A new snapshot with this one's settings and cache state (for a rebuild).
-  std::unique_ptr<FlavorSnapshot> fork_state() const {
+  // Usage deltas already applied on the device whose host-mirror update
+  // (tasUsage, usageByDomain: updateTASUsage, tas_flavor_snapshot.go:257-293)
+  // waits until a reader needs the mirror (upload, a column change, a
+  // rebuild): an admission round touches thousands of (leaf, column) pairs and
+  // the device copy is the one evaluations read.  Wrapping adds commute, so
+  // the deferred records may be folded in any order.
+  std::vector<kueue_tas_delta> mirrorPending;
+  void defer_mirror(const kueue_tas_delta* d, size_t n) {
+    mirrorPending.insert(mirrorPending.end(), d, d + n);
+    if (mirrorPending.size() > (size_t(1) << 22)) flush_mirror();
+  }
+  void flush_mirror() {
+    for (auto& d : mirrorPending) {
+      const std::string& res = cols[size_t(d.col)];
+      int64_t& v = tasUsage[size_t(d.leaf)][res];
+      v = add64(v, d.delta);
+      int64_t& u = usageByDomain[leafId[size_t(d.leaf)]][res];
+      u = add64(u, d.delta);
+    }
+    mirrorPending.clear();
+  }
+  std::unique_ptr<FlavorSnapshot> fork_state() {
+    flush_mirror();
     auto ns = std::make_unique<FlavorSnapshot>();
     ns->topologyName = topologyName;
     ns->levelKeys = levelKeys;
@@ -743,6 +765,7 @@ class FlavorSnapshot {
   // indices, so a request compiled against an older set must be recompiled.
   uint64_t col_gen = 0;
   void set_columns(const std::set<std::string>& names) {
+    flush_mirror();  // pending records name columns of the old set
     static std::atomic<uint64_t> gen_counter{0};
     col_gen = ++gen_counter;
     cols.assign(names.begin(), names.end());
@@ -781,6 +804,7 @@ class FlavorSnapshot {
 
   int upload() {
     if (!dirty) return 0;
+    flush_mirror();
     if (!ctx) {
       ctx = kueue_tas_ctx_create(&cfg);
       if (!ctx) {
@@ -2750,8 +2774,10 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
         for (auto& d : kv.second.doms) {
           const TASPodSetRequests& ps = wl.podsets[size_t(d[0])];
           kueue_tas_fits_req r{d[1], d[2], int32_t(terms.size()), 0};
-          for (auto& t : ps.singlePodRequests) {
-            terms.push_back({t.second, s.colByName.at(t.first), 0});
+          for (auto& t : ps.requestIds) {
+            const int32_t c = s.col_of(t.first);
+            if (c < 0) throw std::runtime_error("admit: request resource without a column");
+            terms.push_back({t.second, c, 0});
             r.num_terms++;
           }
           fr.push_back(r);
@@ -2770,8 +2796,8 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       h->err = std::string("admit: ") + kueue_tas_last_error(s.ctx);
       return rc;
     }
-    // host mirror + the delta list the replicas apply (updateTASUsage per record)
-    std::vector<FlavorSnapshot::DomainUsage> us;
+    // the delta list the replicas apply (updateTASUsage per record); the
+    // host mirror takes it deferred (already applied on the device)
     std::vector<kueue_tas_delta>& deltas = h->last_deltas;
     for (size_t k = 0; k < ids.size(); k++) {
       admitted[2 * k] = ids[k];
@@ -2779,22 +2805,16 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       if (!adm[k]) continue;
       for (int64_t i = off[k]; i < off[k + 1]; i++) {
         const kueue_tas_fits_req& r = fr[size_t(i)];
-        FlavorSnapshot::DomainUsage u;
-        u.id = s.leafId[size_t(r.leaf)];
-        u.count = r.count;
         for (int q = 0; q < r.num_terms; q++) {
           const kueue_tas_fits_term& t = terms[size_t(r.term_begin + q)];
-          u.single[s.cols[size_t(t.col)]] = t.value;
           deltas.push_back({r.leaf, t.col, mul64(t.value, r.count)});
         }
         if (pods_col >= 0) deltas.push_back({r.leaf, pods_col, int64_t(r.count)});
-        us.push_back(std::move(u));
       }
     }
     if (n_deltas) *n_deltas = deltas.size();
-    rc = s.update_usage(us, true, /*device=*/false);  // already applied on the device
-    if (rc) h->err = s.err;
-    return rc;
+    s.defer_mirror(deltas.data(), deltas.size());
+    return 0;
   } catch (const std::exception& e) {
     h->err = e.what();
     return KUEUE_TAS_EINVAL;
@@ -2814,15 +2834,10 @@ int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* d, siz
   if (!h || !h->snap || !h->err.empty() || (n && !d)) return KUEUE_TAS_EINVAL;
   try {
     FlavorSnapshot& s = *h->snap;
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < n; i++)
       if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
         throw std::runtime_error("delta out of range");
-      const std::string& res = s.cols[size_t(d[i].col)];
-      int64_t& v = s.tasUsage[size_t(d[i].leaf)][res];
-      v = add64(v, d[i].delta);
-      int64_t& u = s.usageByDomain[s.leafId[size_t(d[i].leaf)]][res];
-      u = add64(u, d[i].delta);
-    }
+    s.defer_mirror(d, n);
     if (s.dirty || !s.ctx) return s.upload();
     int rc = n ? kueue_tas_snapshot_apply_deltas(s.ctx, d, n, nullptr) : 0;
     if (rc) h->err = std::string("apply deltas: ") + kueue_tas_last_error(s.ctx);

@@ -57,3 +57,44 @@ def test_admission_session_on_gpu(seed):
 @pytest.mark.gpu
 def test_admission_session_arith_on_gpu():
     _sessions(63, 150, gen=synth.arith_stress_case)
+
+
+def _admit_then_rebuild(make_snap):
+    """kueue_tas_host_admit applies usage on the device and defers the host
+    mirror; a node event that forces a rebuild must see every admitted
+    record (the oracle rebuilt from a document holding that usage)."""
+    import copy
+
+    snap_doc, wls = synth.config_c2(n_workloads=24, shape=(2, 2, 4, 8))
+    snap = make_snap(snap_doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    res = snap.last_results()
+    admitted, deltas = snap.admit(snap.last_assignments())
+    assert len(deltas) and admitted[:, 1].any()
+    want_doc = copy.deepcopy(snap_doc)
+    for i, ok in admitted.tolist():
+        if ok:
+            want_doc.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
+    # a node with a new rack: not an in-place update, the snapshot is rebuilt
+    extra = copy.deepcopy(snap_doc["nodes"][0])
+    extra["name"] = "added-node"
+    for k in list(extra["labels"]):
+        if k != "kubernetes.io/hostname":
+            extra["labels"][k] = extra["labels"][k] + "-x"
+    extra["labels"]["kubernetes.io/hostname"] = "added-node"
+    want_doc["nodes"].append(extra)
+    assert snap.update_nodes([extra]) is True  # rebuilt
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    want, _ = oracle_lib.eval_workloads(want_doc, wls, threads=4)
+    assert got == want
+
+
+def test_emulated_admit_then_rebuild(emu_lib):  # noqa: F811
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+
+
+@pytest.mark.gpu
+def test_admit_then_rebuild_on_gpu():
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d))
