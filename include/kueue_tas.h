@@ -245,45 +245,6 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries
  * Pass entries = NULL to kueue_tas_eval_batch to skip its copy. */
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 
-/* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
- * events on the ctx stream): [0] fill (+ exclusion stats reduce), [1] roll-up
- * + exclusion-stats replication, [2] leaf partials + select/descend + join
- * with the fast-LFC branch, [3] total from the request upload to the join. */
-int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
-
-/* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
- * events, summed over its chunks): [0] fill, [1] roll-up of the remaining
- * levels, [2] ExclusionStats (staged fill: the third-stream branch of counts
- * + reduce, concurrent with [1] and [4]; else the replication), [3] the
- * fast-LFC branch on the second stream (leaf tables, select, emit; runs
- * concurrently with [1], [2], [4]), [4] select of the other evals, [5] wait
- * for the fast-LFC branch, [6] total from the request upload to the join.
- * Copies min(n, 7). */
-#define KUEUE_TAS_NUM_STAGES 7
-int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
-
-/* Diagnostics: wall-clock time each eval of the last kueue_tas_eval_batch
- * spent in the select kernel (100 MHz ticks), request order: ticks[2i] total,
- * ticks[2i+1] the findLevelWithFitDomains part.  ticks holds 2n values. */
-int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
-
-/* Diagnostics (profiling build libkueue_tas_prof.so; zeros otherwise): 12
- * inclusive select-phase tick counters per eval of the last batch (LDS sort,
- * threshold walk, child gather, emit, sorted walk, global sort, count
- * update, findLevelWithFitDomains, threshold-walk keys / k-th select / emit,
- * setup).  ticks holds 12n values. */
-int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
-
-/* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request
- * compile, [1] phase-1 classes, [2] uploads + launches, [3] wait for the
- * select results, [4] entry packing + D2H, [5] copy-out.  Copies min(n, 6). */
-int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
-
-/* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
- * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
- * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
- * fill staged (0: generic kernel). */
-int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 
 /* ---- admission re-check: TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415) ----
  * One record per workload.TopologyDomainRequests (pkg/workload/workload.go:260-269). */
@@ -383,24 +344,6 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash);
 #define KUEUE_TAS_RUN_COMPILE 1u
 #define KUEUE_TAS_RUN_VALUES 2u
 int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash);
-/* Device stage times of the last run (summed over its batches, ms):
- * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
- * counts[1] = evaluations, counts[2] = evaluations with a leader. */
-int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
-/* kueue_tas_last_stage_times summed over the last run's batches. */
-int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n);
-/* kueue_tas_last_host_times summed over the last run's batches. */
-int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n);
-/* kueue_tas_last_eval_profile of the last device batch (diagnostics). */
-int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n);
-/* kueue_tas_last_eval_ticks of the last device batch (diagnostics). */
-int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
-/* Host wall time of the last run_compiled (ms): [0] request staging,
- * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
-int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
-/* Work counters of the last find/run: [0] device batches, [1] evals,
- * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
-int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
 
 /* Data-parallel batches (one rank per GPU, each with a replica of the
  * snapshot).  Every rank compiles the same global workload list
@@ -488,6 +431,58 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
  * order] or null, "fillBackEvals": n}. */
 int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json, const char* candidates_json,
                                      char** out_json);
+
+/* ---- the snapshot queries of the scheduler's other callers ---------------
+ *  has_level: TASFlavorSnapshot.HasLevel (tas_flavor_snapshot.go:1065-1088;
+ *    caller tas_flavorassigner.go:195) for a kueue.PodSetTopologyRequest in
+ *    its JSON shape (null -> 0): the level key and the slice level key (and,
+ *    with TASMultiLayerTopology, every layer's topology) are levels of the
+ *    snapshot;
+ *  assignment_stale: IsTopologyAssignmentStale (:733-743; callers :621 and
+ *    tas_elastic_workloads.go:47) for an internal TopologyAssignment
+ *    {"levels","domains":[{"values","count"}]}: *stale = 1 when some
+ *    domain's DomainID(values) is not a domain of the snapshot, *domain
+ *    (kueue_tas_free; may be NULL) = that domain's values[0], else "";
+ *  free_capacity_json: SerializeFreeCapacityPerDomain (:320-355; caller
+ *    snapshot.go:113): {leaf DomainID: {"freeCapacity": {resource: quantity},
+ *    "tasUsage": {...}}} with keys sorted, as json.Marshal writes it. */
+int kueue_tas_host_has_level(kueue_tas_host* h, const char* topology_request_json, int32_t* out);
+int kueue_tas_host_assignment_stale(kueue_tas_host* h, const char* assignment_json, int32_t* stale, char** domain);
+int kueue_tas_host_free_capacity_json(kueue_tas_host* h, char** out_json);
+/* resources.ResourceQuantityString (pkg/resources/requests.go:147-150): the
+ * resource.Quantity text of value v of resource `name` (cpu in milli units,
+ * memory / ephemeral-storage / hugepages-* BinarySI-canonical, else
+ * DecimalSI), NUL-terminated into buf; *len = its length without the NUL;
+ * KUEUE_TAS_EOVERFLOW when cap < *len + 1. */
+int kueue_tas_resource_quantity_string(const char* name, int64_t value, char* buf, size_t cap, size_t* len);
+
+/* ---- the device layer under a host snapshot ----------------------------------
+ * For a binding that keeps its own batching but not its own request compiler:
+ *  host_ctx: the device context holding the host snapshot (valid until the
+ *    next call that rebuilds it; NULL on error);
+ *  leaf_ids: JSON array of the leaves' DomainIDs by leaf index (decodes the
+ *    (leaf, count) entries of kueue_tas_eval_batch);
+ *  compile_workload: findTopologyAssignment's prelude (:804-897) for every
+ *    PodSet group of one workload (podSets JSON array; groups and
+ *    leader/workers as FindTopologyAssignmentsForFlavor :528-609 forms them):
+ *    reqs[g] is group g's request for kueue_tas_eval_batch with its taint
+ *    row at taint_table[g * P ..] (P = *taint_len / *n_groups profiles,
+ *    num_taints for eval_batch in *num_taints, may be NULL), its affinity
+ *    requirements rebased into affinity / affinity_values, and no assumed
+ *    usage (the caller chains groups: addAssumedUsage :658-666);
+ *    early_reasons_json (kueue_tas_free; may be NULL) = per group "" or the
+ *    failure text of the prelude (the group is not evaluated then).  Sizes
+ *    are always set; KUEUE_TAS_EOVERFLOW when a capacity is short.  A
+ *    request naming a resource no column holds re-columns (and reloads) the
+ *    device snapshot first. */
+kueue_tas_ctx* kueue_tas_host_ctx(kueue_tas_host* h);
+int kueue_tas_host_leaf_ids(kueue_tas_host* h, char** out_json);
+int kueue_tas_host_compile_workload(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty,
+                                    kueue_tas_eval_req* reqs, size_t reqs_cap, size_t* n_groups, int32_t* taint_table,
+                                    size_t taint_cap, size_t* taint_len, int32_t* num_taints,
+                                    kueue_tas_affinity_req* affinity, size_t affinity_cap, size_t* n_affinity,
+                                    int32_t* affinity_values, size_t values_cap, size_t* n_values,
+                                    char** early_reasons_json);
 
 void kueue_tas_free(char* p);
 

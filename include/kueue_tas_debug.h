@@ -1,0 +1,80 @@
+/*
+ * kueue_tas_debug.h — diagnostics of libkueue_tas.so: device stage times,
+ * per-eval select ticks and work counters of the last evaluation.  Not part
+ * of the drop-in boundary (kueue_tas.h): the bench and the profiling tools
+ * read them; a Go binding does not need them.
+ */
+#ifndef KUEUE_TAS_DEBUG_H_
+#define KUEUE_TAS_DEBUG_H_
+
+#include "kueue_tas.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- device layer -------------------------------------------------------- */
+/* Per-stage device time of the last kueue_tas_eval_batch (milliseconds, HIP
+ * events on the ctx stream): [0] fill (+ exclusion stats reduce), [1] roll-up
+ * + exclusion-stats replication, [2] leaf partials + select/descend + join
+ * with the fast-LFC branch, [3] total from the request upload to the join. */
+int kueue_tas_last_timings(kueue_tas_ctx* ctx, float* ms4);
+
+/* Finer per-stage device time of the last kueue_tas_eval_batch (ms, HIP
+ * events, summed over its chunks): [0] fill, [1] roll-up of the remaining
+ * levels, [2] ExclusionStats (staged fill: the third-stream branch of counts
+ * + reduce, concurrent with [1] and [4]; else the replication), [3] the
+ * fast-LFC branch on the second stream (leaf tables, select, emit; runs
+ * concurrently with [1], [2], [4]), [4] select of the other evals, [5] wait
+ * for the fast-LFC branch, [6] total from the request upload to the join.
+ * Copies min(n, 7). */
+#define KUEUE_TAS_NUM_STAGES 7
+int kueue_tas_last_stage_times(kueue_tas_ctx* ctx, float* ms, int n);
+
+/* Diagnostics: wall-clock time each eval of the last kueue_tas_eval_batch
+ * spent in the select kernel (100 MHz ticks), request order: ticks[2i] total,
+ * ticks[2i+1] the findLevelWithFitDomains part.  ticks holds 2n values. */
+int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
+
+/* Diagnostics (profiling build libkueue_tas_prof.so; zeros otherwise): 12
+ * inclusive select-phase tick counters per eval of the last batch (LDS sort,
+ * threshold walk, child gather, emit, sorted walk, global sort, count
+ * update, findLevelWithFitDomains, threshold-walk keys / k-th select / emit,
+ * setup).  ticks holds 12n values. */
+int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
+
+/* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request
+ * compile, [1] phase-1 classes, [2] uploads + launches, [3] wait for the
+ * select results, [4] entry packing + D2H, [5] copy-out.  Copies min(n, 6). */
+int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
+
+/* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
+ * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
+ * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
+ * fill staged (0: generic kernel). */
+int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
+
+/* ---- host layer ---------------------------------------------------------- */
+/* Device stage times of the last run (summed over its batches, ms):
+ * [0] fill, [1] roll-up, [2] select, [3] total; counts[0] = device batches,
+ * counts[1] = evaluations, counts[2] = evaluations with a leader. */
+int kueue_tas_host_last_timings(kueue_tas_host* h, float* ms4, int64_t* counts3);
+/* kueue_tas_last_stage_times summed over the last run's batches. */
+int kueue_tas_host_last_stage_times(kueue_tas_host* h, float* ms, int n);
+/* kueue_tas_last_host_times summed over the last run's batches. */
+int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n);
+/* kueue_tas_last_eval_profile of the last device batch (diagnostics). */
+int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n);
+/* kueue_tas_last_eval_ticks of the last device batch (diagnostics). */
+int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
+/* Host wall time of the last run_compiled (ms): [0] request staging,
+ * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
+int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
+/* Work counters of the last find/run: [0] device batches, [1] evals,
+ * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
+int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KUEUE_TAS_DEBUG_H_ */

@@ -33,7 +33,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/kueue_tas.h"
+#include "../../include/kueue_tas_debug.h"
 #include "json_reader.h"
 #include "label_selectors.h"
 
@@ -153,6 +153,67 @@ static std::string go_quote(const std::string& s) {  // strconv.Quote for ASCII 
     } else o += char(c);
   }
   return o + "\"";
+}
+
+// resources.ResourceQuantityString (pkg/resources/requests.go:113-150) as
+// resource.Quantity.String renders it (vendor/k8s.io/apimachinery/pkg/api/
+// resource/quantity.go:425-467 CanonicalizeBytes, amount.go:257-293,
+// suffix.go): cpu is a DecimalSI milli-quantity; memory, ephemeral-storage
+// and hugepages-* are newCanonicalQuantity(v, BinarySI) (the BinarySI string
+// re-parsed: a value that is no multiple of 1024 prints as DecimalSI);
+// anything else is a DecimalSI quantity.  Exact for every int64.
+static std::string decimal_si(int64_t v, int exp) {  // AsCanonicalBytes + decimal suffix
+  if (v == 0) return "0";
+  const bool neg = v < 0;
+  unsigned __int128 a = neg ? (unsigned __int128)(uint64_t(0) - uint64_t(v)) : (unsigned __int128)uint64_t(v);
+  while (a >= 10 && a % 10 == 0) {
+    a /= 10;
+    exp++;
+  }
+  switch (exp % 3) {  // Go's % keeps the dividend's sign, as C++'s does
+    case 1: case -2: a *= 10; exp -= 1; break;
+    case 2: case -1: a *= 100; exp -= 2; break;
+    default: break;
+  }
+  char b[48];
+  char* e = b + sizeof b;
+  char* p = e;
+  do {
+    *--p = char('0' + int(a % 10));
+    a /= 10;
+  } while (a);
+  if (neg) *--p = '-';
+  std::string s(p, size_t(e - p));
+  switch (exp) {
+    case -9: return s + "n";
+    case -6: return s + "u";
+    case -3: return s + "m";
+    case 3: return s + "k";
+    case 6: return s + "M";
+    case 9: return s + "G";
+    case 12: return s + "T";
+    case 15: return s + "P";
+    case 18: return s + "E";
+    default: return s;  // 0 (and no other exponent arises from an int64)
+  }
+}
+static std::string resource_quantity_string(const std::string& name, int64_t v) {
+  if (name == "cpu") return decimal_si(v, -3);
+  const bool binary = name == "memory" || name == "ephemeral-storage" || name.rfind("hugepages-", 0) == 0;
+  if (!binary) return decimal_si(v, 0);
+  if (v == 0) return "0";
+  if (v > -1024 && v < 1024) return decimal_si(v, 0);
+  const bool neg = v < 0;
+  uint64_t a = neg ? uint64_t(0) - uint64_t(v) : uint64_t(v);
+  int e = 0;
+  while (a >= 1024 && a % 1024 == 0) {
+    a /= 1024;
+    e++;
+  }
+  if (e == 0) return decimal_si(v, 0);  // no suffix: re-parsed as DecimalSI
+  static const char* kBin[] = {"", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
+  std::string s = std::to_string(a);
+  return (neg ? "-" : "") + s + kBin[e];
 }
 
 struct NodeInfo {
@@ -1300,6 +1361,94 @@ class FlavorSnapshot {
     g.req.flags |= KUEUE_TAS_F_AFFINITY;
   }
 
+  // ---- snapshot queries of the scheduler's callers ----
+  // HasLevel (tas_flavor_snapshot.go:1065-1088): the request's level key
+  // (levelKey :1120-1138, no implied fallback) and its slice level key
+  // (sliceLevelKeyWithDefault :1090-1100, default the lowest level) resolve;
+  // with TASMultiLayerTopology every additional layer's topology too.
+  bool has_level(const std::optional<TopologyRequest>& tr) const {
+    if (!tr) return false;
+    const std::string* key = nullptr;
+    if (tr->required) key = &*tr->required;
+    else if (tr->preferred) key = &*tr->preferred;
+    else if (slice_only(tr)) key = &levelKeys.front();
+    else if (tr->unconstrained.value_or(false)) key = &levelKeys.back();
+    if (!key) return false;
+    const std::string& sliceKey = tr->sliceRequiredTopology ? *tr->sliceRequiredTopology
+                                  : !tr->constraints.empty() ? tr->constraints[0].topology
+                                                              : levelKeys.back();
+    if (resolve(*key) < 0 || resolve(sliceKey) < 0) return false;
+    if (gates.multiLayer)
+      for (auto& c : tr->constraints)
+        if (resolve(c.topology) < 0) return false;
+    return true;
+  }
+  // DomainID -> present, for every level (TASFlavorSnapshot.domains)
+  // (the tree of a snapshot object never changes: node events that move a
+  // node rebuild it into a new object)
+  mutable std::unordered_map<std::string, int32_t> upperDomainIds;  // levels 0..L-2, built on first use
+  mutable bool upperBuilt = false;
+  bool has_domain(const std::string& id) const {
+    if (leafById.count(id)) return true;
+    if (!upperBuilt) {
+      upperDomainIds.clear();
+      for (int l = 0; l + 1 < L(); l++)
+        for (size_t i = 0; i < values[size_t(l)].size(); i++) {
+          std::string d;
+          for (size_t k = 0; k < values[size_t(l)][i].size(); k++) d += (k ? "," : "") + values[size_t(l)][i][k];
+          upperDomainIds.emplace(std::move(d), l);
+        }
+      upperBuilt = true;
+    }
+    return upperDomainIds.count(id) != 0;
+  }
+  // IsTopologyAssignmentStale (:733-743): the first domain whose
+  // DomainID(Values) is not a domain of the snapshot -> (true, Values[0]).
+  bool assignment_stale(const kjson::Node& ta, std::string* domain) const {
+    for (auto& d : ta["domains"].items) {
+      std::string id;
+      const auto& vs = d["values"].items;
+      for (size_t k = 0; k < vs.size(); k++) id += (k ? "," : "") + vs[k].s();
+      if (!has_domain(id)) {
+        *domain = vs.empty() ? std::string() : vs[0].s();
+        return true;
+      }
+    }
+    return false;
+  }
+  // SerializeFreeCapacityPerDomain (:320-355): every leaf's freeCapacity and
+  // tasUsage as resources.ResourceQuantityString values, json.Marshal of the
+  // maps (keys sorted).
+  std::string free_capacity_json() {
+    flush_mirror();
+    std::vector<int32_t> ord(static_cast<size_t>(N()));
+    for (int i = 0; i < N(); i++) ord[size_t(i)] = i;
+    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return leafId[size_t(a)] < leafId[size_t(b)]; });
+    std::string out = "{";
+    auto reqs = [&](const Requests& r) {
+      out += "{";
+      bool first = true;
+      for (auto& kv : r) {
+        if (!first) out += ",";
+        first = false;
+        labelsel::json_escape(out, kv.first);
+        out += ":";
+        labelsel::json_escape(out, resource_quantity_string(kv.first, kv.second));
+      }
+      out += "}";
+    };
+    for (size_t k = 0; k < ord.size(); k++) {
+      if (k) out += ",";
+      labelsel::json_escape(out, leafId[size_t(ord[k])]);
+      out += ":{\"freeCapacity\":";
+      reqs(freeCap[size_t(ord[k])]);
+      out += ",\"tasUsage\":";
+      reqs(tasUsage[size_t(ord[k])]);
+      out += "}";
+    }
+    return out + "}";
+  }
+
   // ---- failure strings ----
   // ExclusionStats reasons (:480-499) in sorted order.  Every reason is
   // "<prefix><count>" with a distinct prefix ending in ": ", so sorting the
@@ -1464,23 +1613,27 @@ static std::optional<labelsel::RequiredAffinity> parse_required_affinity(const k
   return terms;
 }
 
+// kueue.PodSetTopologyRequest in its JSON shape (nullopt for null)
+static std::optional<TopologyRequest> parse_topology_request(const kjson::Node& tr) {
+  if (tr.null()) return std::nullopt;
+  TopologyRequest t;
+  if (!tr["required"].null()) t.required = tr["required"].s();
+  if (!tr["preferred"].null()) t.preferred = tr["preferred"].s();
+  if (!tr["unconstrained"].null()) t.unconstrained = tr["unconstrained"].b();
+  if (!tr["podSetSliceRequiredTopology"].null()) t.sliceRequiredTopology = tr["podSetSliceRequiredTopology"].s();
+  if (!tr["podSetSliceSize"].null()) t.sliceSize = int32_t(tr["podSetSliceSize"].i64());
+  for (auto& c : tr["podsetSliceRequiredTopologyConstraints"].items)
+    t.constraints.push_back({c["topology"].s(), int32_t(c["size"].i64())});
+  return t;
+}
+
 static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
   std::vector<TASPodSetRequests> out;
   for (auto& ps : arr.items) {
     TASPodSetRequests r;
     r.name = ps["name"].s();
     const kjson::Node& tr = ps["topologyRequest"];
-    if (!tr.null()) {
-      TopologyRequest t;
-      if (!tr["required"].null()) t.required = tr["required"].s();
-      if (!tr["preferred"].null()) t.preferred = tr["preferred"].s();
-      if (!tr["unconstrained"].null()) t.unconstrained = tr["unconstrained"].b();
-      if (!tr["podSetSliceRequiredTopology"].null()) t.sliceRequiredTopology = tr["podSetSliceRequiredTopology"].s();
-      if (!tr["podSetSliceSize"].null()) t.sliceSize = int32_t(tr["podSetSliceSize"].i64());
-      for (auto& c : tr["podsetSliceRequiredTopologyConstraints"].items)
-        t.constraints.push_back({c["topology"].s(), int32_t(c["size"].i64())});
-      r.topologyRequest = t;
-    }
+    r.topologyRequest = parse_topology_request(tr);
     r.implied = tr.null();
     if (auto im = ps.find("implied")) r.implied = im->b();
     for (auto& kv : ps["requests"].fields) r.singlePodRequests[kv.first] = kv.second.i64();
@@ -2868,6 +3021,128 @@ int kueue_tas_host_last_results(kueue_tas_host* h, char** out_json) {
 #ifndef KTAS_SOURCE_HASH
 #define KTAS_SOURCE_HASH "unversioned"
 #endif
+int kueue_tas_resource_quantity_string(const char* name, int64_t value, char* buf, size_t cap, size_t* len) {
+  if (!name || !len || (cap && !buf)) return KUEUE_TAS_EINVAL;
+  const std::string q = resource_quantity_string(name, value);
+  *len = q.size();
+  if (cap < q.size() + 1) return KUEUE_TAS_EOVERFLOW;
+  memcpy(buf, q.c_str(), q.size() + 1);
+  return 0;
+}
+
+int kueue_tas_host_has_level(kueue_tas_host* h, const char* topology_request_json, int32_t* out) {
+  if (!h || !h->snap || !topology_request_json || !out) return KUEUE_TAS_EINVAL;
+  try {
+    *out = h->snap->has_level(parse_topology_request(kjson::parse(topology_request_json))) ? 1 : 0;
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_assignment_stale(kueue_tas_host* h, const char* assignment_json, int32_t* stale, char** domain) {
+  if (!h || !h->snap || !assignment_json || !stale) return KUEUE_TAS_EINVAL;
+  try {
+    std::string d;
+    *stale = h->snap->assignment_stale(kjson::parse(assignment_json), &d) ? 1 : 0;
+    if (domain) *domain = dup(d);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_free_capacity_json(kueue_tas_host* h, char** out_json) {
+  if (!h || !h->snap || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    *out_json = dup(h->snap->free_capacity_json());
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+kueue_tas_ctx* kueue_tas_host_ctx(kueue_tas_host* h) {
+  if (!h || !h->snap || !h->err.empty()) return nullptr;
+  return h->snap->upload() ? nullptr : h->snap->ctx;
+}
+
+int kueue_tas_host_leaf_ids(kueue_tas_host* h, char** out_json) {
+  if (!h || !h->snap || !out_json) return KUEUE_TAS_EINVAL;
+  std::string o = "[";
+  for (size_t i = 0; i < h->snap->leafId.size(); i++) {
+    if (i) o += ",";
+    kjson::write_string(o, h->snap->leafId[i]);
+  }
+  *out_json = dup(o + "]");
+  return 0;
+}
+
+int kueue_tas_host_compile_workload(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty,
+                                    kueue_tas_eval_req* reqs, size_t reqs_cap, size_t* n_groups, int32_t* taint_table,
+                                    size_t taint_cap, size_t* taint_len, int32_t* num_taints,
+                                    kueue_tas_affinity_req* affinity, size_t affinity_cap, size_t* n_affinity,
+                                    int32_t* affinity_values, size_t values_cap, size_t* n_values,
+                                    char** early_reasons_json) {
+  if (!h || !h->snap || !h->err.empty() || !podsets_json || !n_groups || !taint_len || !n_affinity || !n_values)
+    return KUEUE_TAS_EINVAL;
+  try {
+    FlavorSnapshot& s = *h->snap;
+    Workload wl;
+    wl.podsets = parse_podsets(kjson::parse(podsets_json));
+    make_groups(wl);
+    s.ensure_columns_for(wl.podsets);
+    for (auto& g : wl.groups) s.compile_group(g, simulate_empty != 0);
+    int rc = s.upload();  // a new request resource re-columns the device snapshot
+    if (rc) {
+      h->err = s.err;
+      return rc;
+    }
+    size_t na = 0, nv = 0;
+    for (auto& g : wl.groups) {
+      na += g.aff.size();
+      nv += g.aff_vals.size();
+    }
+    const size_t P = s.profiles.size();
+    *n_groups = wl.groups.size();
+    *taint_len = P * wl.groups.size();
+    *n_affinity = na;
+    *n_values = nv;
+    if (num_taints) *num_taints = int32_t(s.taintStrings.size());
+    if (reqs_cap < wl.groups.size() || taint_cap < *taint_len || affinity_cap < na || values_cap < nv ||
+        (wl.groups.size() && (!reqs || (P && !taint_table))) || (na && !affinity) || (nv && !affinity_values))
+      return KUEUE_TAS_EOVERFLOW;
+    std::string reasons = "[";
+    size_t ka = 0, kv = 0;
+    for (size_t i = 0; i < wl.groups.size(); i++) {
+      const GroupEval& g = wl.groups[i];
+      kueue_tas_eval_req q = g.req;
+      q.taint_table = int32_t(i * P);
+      std::copy(g.taint_row.begin(), g.taint_row.end(), taint_table + i * P);
+      q.assumed_begin = q.assumed_end = 0;
+      q.affinity_begin = int32_t(ka);
+      for (auto r : g.aff) {
+        r.begin += int32_t(kv);
+        affinity[ka++] = r;
+      }
+      q.affinity_end = int32_t(ka);
+      std::copy(g.aff_vals.begin(), g.aff_vals.end(), affinity_values + kv);
+      kv += g.aff_vals.size();
+      reqs[i] = q;
+      if (i) reasons += ",";
+      kjson::write_string(reasons, g.early_reason);
+    }
+    if (early_reasons_json) *early_reasons_json = dup(reasons + "]");
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
 const char* kueue_tas_build_id(void) { return KTAS_SOURCE_HASH; }
 
 void kueue_tas_free(char* p) { free(p); }

@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/kueue_tas.h"
+#include "../../include/kueue_tas_debug.h"
 
 namespace ktas {
 

@@ -58,11 +58,15 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_v1beta2_last", "kueue_tas_host_last_results", "kueue_tas_admit", "kueue_tas_host_set_shard",
     "kueue_tas_host_last_assignments", "kueue_tas_host_admit", "kueue_tas_host_apply_deltas",
     "kueue_tas_host_last_deltas", "kueue_tas_host_run", "kueue_tas_build_id",
+    "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
+    "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
+    "kueue_tas_host_compile_workload",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
 _HASHED_SOURCES = ("tas_device.hip", "tas_host.cpp", "tas_internal.h", "tas_kernels.hip", "json_reader.h",
-                   "label_selectors.h", os.path.join("..", "..", "include", "kueue_tas.h"))
+                   "label_selectors.h", os.path.join("..", "..", "include", "kueue_tas.h"),
+                   os.path.join("..", "..", "include", "kueue_tas_debug.h"))
 
 
 def source_hash() -> str | None:
@@ -166,6 +170,36 @@ def _bind(lib):
     lib.kueue_tas_host_update_pods.argtypes = [c.c_void_p, c.c_char_p]
     lib.kueue_tas_host_update_pods.restype = c.c_int
     lib.kueue_tas_free.argtypes = [c.c_void_p]
+    lib.kueue_tas_host_has_level.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
+    lib.kueue_tas_host_has_level.restype = c.c_int
+    lib.kueue_tas_host_assignment_stale.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32), c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_assignment_stale.restype = c.c_int
+    lib.kueue_tas_host_free_capacity_json.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_free_capacity_json.restype = c.c_int
+    lib.kueue_tas_resource_quantity_string.argtypes = [c.c_char_p, c.c_int64, c.c_char_p, c.c_size_t,
+                                                       c.POINTER(c.c_size_t)]
+    lib.kueue_tas_resource_quantity_string.restype = c.c_int
+    lib.kueue_tas_host_ctx.argtypes = [c.c_void_p]
+    lib.kueue_tas_host_ctx.restype = c.c_void_p
+    lib.kueue_tas_host_leaf_ids.argtypes = [c.c_void_p, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_leaf_ids.restype = c.c_int
+    lib.kueue_tas_host_compile_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32,
+                                                    c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t),
+                                                    c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.POINTER(c.c_int32),
+                                                    c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t),
+                                                    c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t),
+                                                    c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_compile_workload.restype = c.c_int
+
+
+def resource_quantity_string(name: str, value: int, lib=None) -> str:
+    """resources.ResourceQuantityString (pkg/resources/requests.go:147) via the library."""
+    lib = lib if lib is not None else load_library()
+    buf = ctypes.create_string_buffer(64)
+    n = ctypes.c_size_t()
+    if lib.kueue_tas_resource_quantity_string(name.encode(), value, buf, 64, ctypes.byref(n)):
+        raise RuntimeError("kueue_tas_resource_quantity_string failed")
+    return buf.value.decode()
 
 
 def _take(lib, p) -> dict:
@@ -412,6 +446,75 @@ class TASFlavorSnapshot:
         d = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
         if self._lib.kueue_tas_host_apply_deltas(self._h, d.ctypes.data, d.size):
             raise RuntimeError(self._err())
+
+    # ---- snapshot queries of the scheduler's other callers ----
+    def has_level(self, topology_request) -> bool:
+        """TASFlavorSnapshot.HasLevel (tas_flavor_snapshot.go:1065) of a
+        PodSetTopologyRequest dict (or None)."""
+        r = ctypes.c_int32()
+        if self._lib.kueue_tas_host_has_level(self._h, json.dumps(topology_request).encode(), ctypes.byref(r)):
+            raise RuntimeError(self._err())
+        return bool(r.value)
+
+    def is_topology_assignment_stale(self, assignment: dict):
+        """IsTopologyAssignmentStale (:736) of an internal TopologyAssignment:
+        (stale, values[0] of the first unknown domain or "")."""
+        st = ctypes.c_int32()
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_assignment_stale(self._h, json.dumps(assignment).encode(), ctypes.byref(st),
+                                                     ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        d = ctypes.cast(out, ctypes.c_char_p).value.decode()
+        self._lib.kueue_tas_free(out)
+        return bool(st.value), d
+
+    def serialize_free_capacity_per_domain(self) -> str:
+        """SerializeFreeCapacityPerDomain (:320): the JSON text itself."""
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_free_capacity_json(self._h, ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        s = ctypes.cast(out, ctypes.c_char_p).value.decode()
+        self._lib.kueue_tas_free(out)
+        return s
+
+    def leaf_ids(self) -> list:
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_leaf_ids(self._h, ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        return _take(self._lib, out)
+
+    def device_ctx(self):
+        """The kueue_tas_ctx* under this snapshot (for direct device-layer calls)."""
+        p = self._lib.kueue_tas_host_ctx(self._h)
+        if not p:
+            raise RuntimeError(self._err())
+        return p
+
+    def compile_workload(self, podsets: list, simulate_empty: bool = False):
+        """kueue_tas_host_compile_workload: (reqs buffer, taint table int32 array,
+        num_taints, affinity buffer, affinity values int32 array, early reasons)."""
+        import numpy as np
+        c = ctypes
+        ng, tl, na, nv = c.c_size_t(), c.c_size_t(), c.c_size_t(), c.c_size_t()
+        nt = c.c_int32()
+        doc = json.dumps(podsets).encode()
+        rc = self._lib.kueue_tas_host_compile_workload(self._h, doc, int(simulate_empty), None, 0, c.byref(ng), None, 0,
+                                                       c.byref(tl), c.byref(nt), None, 0, c.byref(na), None, 0,
+                                                       c.byref(nv), None)
+        if rc not in (0, -5):
+            raise RuntimeError(self._err())
+        from . import abi
+        reqs = (abi.EvalReq * max(ng.value, 1))()
+        taints = np.zeros(max(tl.value, 1), dtype=np.int32)
+        aff = (abi.AffinityReq * max(na.value, 1))()
+        vals = np.zeros(max(nv.value, 1), dtype=np.int32)
+        out = c.c_void_p()
+        if self._lib.kueue_tas_host_compile_workload(self._h, doc, int(simulate_empty), reqs, ng.value, c.byref(ng),
+                                                     taints.ctypes.data, taints.size, c.byref(tl), c.byref(nt),
+                                                     aff, na.value, c.byref(na), vals.ctypes.data,
+                                                     vals.size, c.byref(nv), c.byref(out)):
+            raise RuntimeError(self._err())
+        return reqs, ng.value, taints[: tl.value], nt.value, aff, na.value, vals[: nv.value], _take(self._lib, out)
 
     RUN_COMPILE = 1  # KUEUE_TAS_RUN_COMPILE: group + compile every TASPodSetRequests in the call
     RUN_VALUES = 2   # KUEUE_TAS_RUN_VALUES: build the TopologyAssignment domains (Values, Count)

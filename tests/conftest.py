@@ -30,6 +30,7 @@ def emu_lib():
     srcs = [os.path.join(ROOT, "kueue_oss_amd", "csrc", f) for f in _EMU_SRCS]
     srcs += [os.path.join(here, "emu", f) for f in ("hip_emu.cpp", "build_emu.sh", "hip/hip_runtime.h")]
     srcs.append(os.path.join(ROOT, "include", "kueue_tas.h"))
+    srcs.append(os.path.join(ROOT, "include", "kueue_tas_debug.h"))
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in srcs):
         subprocess.run([os.path.join(here, "emu", "build_emu.sh")], check=True, capture_output=True)
     return native.load_library(so)

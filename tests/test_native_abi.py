@@ -9,12 +9,15 @@ import pytest
 import kueue_oss_amd
 from kueue_oss_amd import native
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "kueue_tas.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADERS = [os.path.join(INCLUDE, "kueue_tas.h"), os.path.join(INCLUDE, "kueue_tas_debug.h")]
 
 
 def header_functions():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(kueue_tas_[a-z_0-9]+)\s*\(", text)))
+    found = set()
+    for h in HEADERS:
+        found |= set(re.findall(r"\b(kueue_tas_[a-z_0-9]+)\s*\(", open(h).read()))
+    return sorted(found)
 
 
 def test_header_declares_exported_set():
