@@ -206,16 +206,19 @@ def main():
     # workloads finish) restore the snapshot for the next round ----
     rounds = 5
     adm_ms, admitted_n, deltas_n = [], 0, 0
+    adm_parts = []
     for _ in range(rounds):
         barrier()
         ta = time.perf_counter()
         snap.run_compiled(flags=FULL)
+        tb = time.perf_counter()
         if dist is not None:
             _, admitted, deltas = admit_round(snap, world, rank, dist, device)
         else:
             admitted, deltas = snap.admit(snap.last_assignments())
         barrier()
         adm_ms.append((time.perf_counter() - ta) * 1e3)
+        adm_parts.append([(tb - ta) * 1e3, (time.perf_counter() - tb) * 1e3] + list(snap.last_admit_times()))
         if admitted is not None:
             admitted_n = int(admitted[:, 1].sum())
         deltas_n = len(deltas)
@@ -293,6 +296,10 @@ def main():
                                          "(round-1 step definition), no gather"},
             "admission": {"round_ms_median": round(pct(adm_ms, 0.5), 3), "rounds": rounds,
                           "admitted": admitted_n, "deltas": deltas_n,
+                          "parts_ms_median": dict(zip(["evaluate", "gather_admit_broadcast", "admit_host_prep",
+                                                       "admit_device", "admit_delta_list"],
+                                                      [round(pct([p[k] for p in adm_parts], 0.5), 3)
+                                                       for k in range(5)])),
                           "round": "evaluate + all-gather assignments + rank-0 Fits/AddUsage in workload order "
                                    "(admit_kernel) + delta broadcast + replicas apply"},
             "stages": stages,

@@ -73,6 +73,10 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
 /* Work counters of the last find/run: [0] device batches, [1] evals,
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
+/* Host wall time of the last kueue_tas_host_admit (ms): [0] record
+ * preparation, [1] kueue_tas_admit (uploads, admit_kernel, result copy),
+ * [2] delta list. */
+int kueue_tas_host_last_admit_times(kueue_tas_host* h, double* ms3);
 
 #ifdef __cplusplus
 }

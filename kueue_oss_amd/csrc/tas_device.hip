@@ -1256,7 +1256,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
   const int32_t* d_bf = reinterpret_cast<const int32_t*>(ds + o_bf);
-  const int waves = 4;
+  const int waves = kSelectWaves;  // the kernel's per-wave LDS state is sized for this
   const size_t sel_lds = size_t(waves) * size_t(c->list_cap) * 16;
   // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
   // (after the stats replication); the main stream runs the BestFit side

@@ -2265,6 +2265,7 @@ struct kueue_tas_host {
   std::vector<Workload> shard;
   std::vector<Workload>& active() { return shard_ids.empty() ? compiled : shard; }
   std::vector<kueue_tas_delta> last_deltas;  // usage deltas the last kueue_tas_host_admit applied
+  double admit_ms[3] = {0, 0, 0};            // last admit: host prep, kueue_tas_admit, delta list
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
     for (auto* v : {&compiled, &shard})
@@ -2892,6 +2893,7 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       if (!admitted || admitted_cap < 2 * heads.size()) return KUEUE_TAS_EOVERFLOW;
     }
     h->last_deltas.clear();
+    const double t0 = now_ms();
     FlavorSnapshot& s = *h->snap;
     int rc = s.upload();
     if (rc) {
@@ -2943,6 +2945,7 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     std::vector<int32_t> adm(ids.size(), 0);
     const auto pods = s.colByName.find("pods");
     const int32_t pods_col = pods == s.colByName.end() ? -1 : pods->second;
+    const double t1 = now_ms();
     rc = kueue_tas_admit(s.ctx, fr.data(), fr.size(), terms.data(), terms.size(), off.data(), ids.size(), pods_col,
                          adm.data());
     if (rc) {
@@ -2951,6 +2954,7 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     }
     // the delta list the replicas apply (updateTASUsage per record); the
     // host mirror takes it deferred (already applied on the device)
+    const double t2 = now_ms();
     std::vector<kueue_tas_delta>& deltas = h->last_deltas;
     for (size_t k = 0; k < ids.size(); k++) {
       admitted[2 * k] = ids[k];
@@ -2967,11 +2971,20 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     }
     if (n_deltas) *n_deltas = deltas.size();
     s.defer_mirror(deltas.data(), deltas.size());
+    h->admit_ms[0] = t1 - t0;
+    h->admit_ms[1] = t2 - t1;
+    h->admit_ms[2] = now_ms() - t2;
     return 0;
   } catch (const std::exception& e) {
     h->err = e.what();
     return KUEUE_TAS_EINVAL;
   }
+}
+
+int kueue_tas_host_last_admit_times(kueue_tas_host* h, double* ms3) {
+  if (!h || !ms3) return KUEUE_TAS_EINVAL;
+  memcpy(ms3, h->admit_ms, sizeof h->admit_ms);
+  return 0;
 }
 
 int kueue_tas_host_last_deltas(kueue_tas_host* h, kueue_tas_delta* buf, size_t cap) {

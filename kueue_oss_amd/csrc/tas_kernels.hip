@@ -1270,7 +1270,6 @@ __constant__ DevSnap g_select_snap;
 struct Wave {
   const DevEval* ev;
   int eid;
-  int lane;
   bool leader, lfc, bf, unconstrained;
   const int32_t* ctr;  // phase-1 counters of this eval's class (shared, read-only here)
   const uint64_t* rack_pos;  // the class's positive-child masks of level L-2 (or null)
@@ -1291,7 +1290,9 @@ struct Wave {
   bool overflow;
   const LeafPartial* partials;  // leaf-level partial reductions of this eval (or null)
   int nblk;
+#if KTAS_PROFILE
   uint64_t prof[P_NCAT];
+#endif
 
   // Phase-2 mutations go to a private copy-on-write overlay (ov, tag ==
   // my_tag marks the domains it holds) so evals of one phase-1 class share
@@ -1419,7 +1420,7 @@ __device__ void lds_sort(Key* k, int n, int lane) {
 // ---- global merge sort of n keys in `a` (tmp same size); result in a ----
 __device__ void global_sort(Wave& w, Key* a, Key* tmp, int n) {
   ProfScope prof_scope_(w, P_GLOBAL_SORT);
-  const int lane = w.lane;
+  const int lane = lane_id();
   const int run = w.cap;
   // sort runs of `run` in LDS
   for (int r0 = 0; r0 < n; r0 += run) {
@@ -1486,7 +1487,7 @@ struct SeqLds {
     int g0 = cur();
     if (w->get(f, g0) < needed) return g0;
     uint64_t best = ~0ull;
-    for (int p = pos + w->lane; p < n; p += kWave) {
+    for (int p = pos + lane_id(); p < n; p += kWave) {
       int32_t st = w->get(f, at(p));
       if (st >= needed) {
         uint64_t k = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
@@ -1510,7 +1511,7 @@ struct SeqList {
     int g0 = cur();
     if (w->get(f, g0) < needed) return g0;
     uint64_t best = ~0ull;
-    for (int p = pos + w->lane; p < n; p += kWave) {
+    for (int p = pos + lane_id(); p < n; p += kWave) {
       int32_t st = w->get(f, g[p]);
       if (st >= needed) {
         uint64_t k = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
@@ -1535,7 +1536,7 @@ struct SeqKeys {
     int g0 = cur();
     if (w->get(f, g0) < needed) return g0;
     uint64_t best = ~0ull;
-    for (int p = pos + w->lane; p < n; p += kWave) {
+    for (int p = pos + lane_id(); p < n; p += kWave) {
       int32_t st = w->get(f, at(p));
       if (st >= needed) {
         uint64_t kk = (uint64_t(s_asc(st)) << 32) | uint32_t(p);
@@ -1556,7 +1557,7 @@ struct SeqLazy {
   bool valid;
   __device__ void find_next(bool first) {
     Key best = key_max();
-    for (int i = w->lane; i < n; i += kWave) {
+    for (int i = lane_id(); i < n; i += kWave) {
       Key x = k[i];
       if ((first || key_lt(curk, x)) && key_lt(x, best)) best = x;
     }
@@ -1572,7 +1573,7 @@ struct SeqLazy {
     int g0 = cur();
     if (w->get(f, g0) < needed) return g0;
     uint32_t bst = ~0u;
-    for (int i = w->lane; i < n; i += kWave) {
+    for (int i = lane_id(); i < n; i += kWave) {
       Key x = k[i];
       if (key_le(curk, x)) {
         int32_t st = w->get(f, level_off + int(uint32_t(x.lo)));
@@ -1581,7 +1582,7 @@ struct SeqLazy {
     }
     bst = uint32_t(wave_min_u64(uint64_t(bst)));
     Key best = key_max();
-    for (int i = w->lane; i < n; i += kWave) {
+    for (int i = lane_id(); i < n; i += kWave) {
       Key x = k[i];
       if (key_le(curk, x) && key_lt(x, best)) {
         int32_t st = w->get(f, level_off + int(uint32_t(x.lo)));
@@ -1857,7 +1858,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   const int32_t rem = slices ? go_div32(count, sliceSize) : count;
   Key* keys = w.gkeys;
   uint64_t* hist = reinterpret_cast<uint64_t*>(w.lds);
-  for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+  for (int i = lane_id(); i < kThrBins; i += kWave) hist[i] = 0;
   wave_sync();
   // pass A: keys, range of the primary component, minimum weight, and the
   // weight per sliceState value for values in [0, kThrBins) (pass B when the
@@ -1871,7 +1872,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     int g[kU];
     int32_t ss[kU], st[kU];
 #pragma unroll
-    for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
+    for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + lane_id(), n - 1)];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       ss[u] = w.get_clean(F_SLICE, g[u]);
@@ -1879,7 +1880,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      const int i = base + u * kWave + w.lane;
+      const int i = base + u * kWave + lane_id();
       if (i < n) {
         keys[i] = key_plain(lfc, ss[u], st[u], g[u] - loff);
         vmin = min(vmin, ss[u]);
@@ -1918,7 +1919,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     if (vmin < 0 || vmax >= kThrBins) {
       // pass B: weight per sliceState value, bins from vmin
       hbase = vmin;
-      for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+      for (int i = lane_id(); i < kThrBins; i += kWave) hist[i] = 0;
       wave_sync();
       wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
         const int32_t ss = kp_ss(lfc, k);
@@ -1954,7 +1955,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     if (int64_t(umax) - int64_t(umin) >= kThrBins) return -1;
     // pass D: weight per state value inside class t
     wave_sync();
-    for (int i = w.lane; i < kThrBins; i += kWave) hist[i] = 0;
+    for (int i = lane_id(); i < kThrBins; i += kWave) hist[i] = 0;
     wave_sync();
     wave_for<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k) {
       if (kp_ss(lfc, k) == t) {
@@ -1981,7 +1982,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
       const bool in = valid && kp_ss(lfc, k) == t && kp_st(k) == u;
       const uint64_t bm = ballot(in);
-      const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
+      const int pos = cnt + __popcll(bm & ((1ull << lane_id()) - 1ull));
       if (in && pos < ccap) cand[pos] = uint32_t(k.lo);
       cnt += __popcll(bm);
     });
@@ -1991,7 +1992,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     {
       ProfScope ps_sel(w, P_TW_SELECT);
       const int nbits = 32 - __builtin_clz(uint32_t(max(g_select_snap.level_size[level] - 1, 1)));  // indices < level size
-      kth = lds_select_kth(cand, cnt, int(m), cand + ccap, w.lane, nbits, dbits);
+      kth = lds_select_kth(cand, cnt, int(m), cand + ccap, lane_id(), nbits, dbits);
     }
     ck = key_plain(lfc, t, u, int32_t(kth));
     wave_sync();
@@ -2007,7 +2008,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   wave_for_all<Key>(n, [&](int i) { return keys[i]; }, [&](int, const Key& k, bool valid) {
     const bool take = valid && key_lt(k, ck);
     const uint64_t bm = ballot(take);
-    const int pos = cnt + __popcll(bm & ((1ull << w.lane) - 1ull));
+    const int pos = cnt + __popcll(bm & ((1ull << lane_id()) - 1ull));
     if (take) {
       const int g = loff + int(uint32_t(k.lo));
       // !leader: no F_LS; the value only changes if sliceSize * sliceState != state
@@ -2059,7 +2060,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   const bool lfc = w.lfc;
   const int32_t rem = slices ? go_div32(count, sliceSize) : count;
   int64_t absum = 0;
-  for (int i = w.lane; i < n; i += kWave) {
+  for (int i = lane_id(); i < n; i += kWave) {
     const Key k = w.lds[i];
     const int64_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
     absum += wt < 0 ? -wt : wt;
@@ -2070,7 +2071,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   int cross = -1;
   int64_t before = 0;
   for (int i0 = 0; i0 < n; i0 += kWave) {
-    const int i = i0 + w.lane;
+    const int i = i0 + lane_id();
     int64_t wt = 0;
     if (i < n) {
       const Key k = w.lds[i];
@@ -2078,8 +2079,8 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
     }
     int64_t x = wt;
     for (int d = 1; d < 64; d <<= 1) {
-      int64_t y = int64_t(shfl_u64(uint64_t(x), max(w.lane - d, 0)));
-      if (w.lane >= d) x += y;
+      int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane_id() - d, 0)));
+      if (lane_id() >= d) x += y;
     }
     const uint64_t m = ballot(i < n && run + x >= rem);
     if (m) {
@@ -2095,7 +2096,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   int pick = cross;
   if (w.bf) {  // findBestFitDomainBy over [cross, n) (:1216-1231)
     uint64_t best = ~0ull;
-    for (int i = cross + w.lane; i < n; i += kWave) {
+    for (int i = cross + lane_id(); i < n; i += kWave) {
       const Key k = w.lds[i];
       const int32_t wt = slices ? kp_ss(lfc, k) : kp_st(k);
       if (wt >= remc) best = min(best, (uint64_t(s_asc(wt)) << 32) | uint32_t(i));
@@ -2103,7 +2104,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
     pick = int(uint32_t(wave_min_u64(best)));
   }
   int cnt = *np;
-  for (int i = w.lane; i < cross; i += kWave) {
+  for (int i = lane_id(); i < cross; i += kWave) {
     const Key k = w.lds[i];
     const int g = loff + int(uint32_t(k.lo));
     if (slices && w_mul(kp_ss(lfc, k), sliceSize) != kp_st(k))  // !leader: no F_LS; only real changes
@@ -2147,14 +2148,14 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
       int g[kU];
       int32_t v[kU];
 #pragma unroll
-      for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + w.lane, n - 1)];
+      for (int u = 0; u < kU; u++) g[u] = gids[min(base + u * kWave + lane_id(), n - 1)];
 #pragma unroll
       for (int u = 0; u < kU; u++) v[u] = w.get_clean(F_SLICE, g[u]);
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const bool keep = base + u * kWave + w.lane < n && v[u] > 0;
+        const bool keep = base + u * kWave + lane_id() < n && v[u] > 0;
         const uint64_t bm = ballot(keep);
-        if (keep) w.listD[m + __popcll(bm & ((1ull << w.lane) - 1ull))] = g[u];
+        if (keep) w.listD[m + __popcll(bm & ((1ull << lane_id()) - 1ull))] = g[u];
         m += __popcll(bm);
       }
     }
@@ -2167,11 +2168,11 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
     if (r >= 0) return r == 1;
   }
   if (n <= w.cap) {
-    for (int i = w.lane; i < n; i += kWave) w.lds[i] = w.kplain_clean(gids[i]);
+    for (int i = lane_id(); i < n; i += kWave) w.lds[i] = w.kplain_clean(gids[i]);
     wave_sync();
     {
       ProfScope ps_(w, P_LDS_SORT);
-      lds_sort(w.lds, n, w.lane);
+      lds_sort(w.lds, n, lane_id());
     }
     if (leaderless) {
       const int r = lds_prefix_walk(w, n, loff, count, sliceSize, slices, out, np);
@@ -2202,7 +2203,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   }
   // longer than the LDS: merge-sort the keys in global memory once (O(n log n)),
   // then walk them in order
-  for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = w.kplain_clean(gids[i]);
+  for (int i = lane_id(); i < n; i += kWave) w.gkeys[i] = w.kplain_clean(gids[i]);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   global_sort(w, w.gkeys, w.gkeys2, n);
   if (sliceRecompute > 1) {
@@ -2225,7 +2226,7 @@ __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level
   const int32_t* co = s.child_off + s.child_base[level];
   int np = 0;
   for (int i0 = 0; i0 < n; i0 += kWave) {  // 64 parents per step: ranges, then a scan for the offsets
-    const int i = i0 + w.lane;
+    const int i = i0 + lane_id();
     int cb = 0, cnt = 0;
     if (i < n) {
       const int p = parents[i] - poff;
@@ -2261,7 +2262,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
   if (w.rack_pos && level == s.L - 2) {
     // children are leaves: the fill's per-parent positive masks give them without loads
     for (int i0 = 0; i0 < n; i0 += kWave) {
-      const int i = i0 + w.lane;
+      const int i = i0 + lane_id();
       uint64_t m = 0;
       int cb = 0;
       if (i < n) {
@@ -2281,7 +2282,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
     return np;
   }
   for (int i0 = 0; i0 < n; i0 += kWave) {
-    const int i = i0 + w.lane;
+    const int i = i0 + lane_id();
     int cb = 0, cnt = 0;
     if (i < n) {
       const int p = parents[i] - poff;
@@ -2291,8 +2292,8 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
     int tot;
     const int ex = wave_excl_scan(cnt, &tot);
     wave_sync();
-    sh_ex[w.lane] = ex;
-    sh_cb[w.lane] = cb;
+    sh_ex[lane_id()] = ex;
+    sh_cb[lane_id()] = cb;
     wave_sync();
     const int nparents = min(kWave, n - i0);
     // uniform power-of-two fan-out in this step: element e belongs to parent e >> sh
@@ -2304,7 +2305,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
       int32_t v[kU];
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const int e = min(b0 + u * kWave + w.lane, tot - 1);
+        const int e = min(b0 + u * kWave + lane_id(), tot - 1);
         if (uniform) {
           g[u] = coff + __shfl(cb, e >> sh, 64) + (e & (f0 - 1));
         } else {
@@ -2321,10 +2322,10 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
       for (int u = 0; u < kU; u++) v[u] = w.get_clean(F_SLICE, g[u]);
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const bool keep = b0 + u * kWave + w.lane < tot && v[u] > 0;
+        const bool keep = b0 + u * kWave + lane_id() < tot && v[u] > 0;
         const uint64_t km = ballot(keep);
         if (keep) {
-          const int pos = np + __popcll(km & ((1ull << w.lane) - 1ull));
+          const int pos = np + __popcll(km & ((1ull << lane_id()) - 1ull));
           if (pos < w.lcap) out[pos] = g[u];
         }
         np += __popcll(km);
@@ -2346,7 +2347,7 @@ __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
   const int D = s.level_size[level];
   const int loff = s.level_off[level];
   uint64_t best = ~0ull;
-  for (int i = w.lane; i < D; i += kWave) {
+  for (int i = lane_id(); i < D; i += kWave) {
     int g = loff + i;
     uint32_t rank = s.id_rank ? uint32_t(s.id_rank[g]) : uint32_t(i);
     // highest sliceState, ties: smaller DomainID string
@@ -2357,7 +2358,7 @@ __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
   // recover the index of the domain with that rank
   int bidx = -1;
   uint32_t brank = uint32_t(best);
-  for (int i = w.lane; i < D; i += kWave) {
+  for (int i = lane_id(); i < D; i += kWave) {
     uint32_t rank = s.id_rank ? uint32_t(s.id_rank[loff + i]) : uint32_t(i);
     if (rank == brank) bidx = i;
   }
@@ -2376,7 +2377,7 @@ __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
         hi = s.child_off[s.child_base[l] + hi];
       }
       int32_t acc = 0;
-      for (int i = lo + w.lane; i < hi; i += kWave) acc = w_add(acc, go_div32(w.get(F_STATE, s.level_off[t] + i), size));
+      for (int i = lo + lane_id(); i < hi; i += kWave) acc = w_add(acc, go_div32(w.get(F_STATE, s.level_off[t] + i), size));
       fit = wave_sum_wrap32(acc);
     }
     o.ml_fit[c] = fit;
@@ -2418,7 +2419,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
     if (words * 4 <= int64_t(w.cap) * int64_t(sizeof(Key))) {
       uint32_t* bm = reinterpret_cast<uint32_t*>(w.lds);
       wave_sync();
-      for (int j = w.lane; j < words; j += kWave) bm[j] = 0;
+      for (int j = lane_id(); j < words; j += kWave) bm[j] = 0;
       wave_sync();
       wave_for<int32_t>(n, [&](int i) { return gids[i]; }, [&](int, int32_t g) {
         const int off = g - loff - mn;
@@ -2429,7 +2430,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
       int32_t* sorted = reinterpret_cast<int32_t*>(w.gkeys);
       int ns = 0;
       for (int64_t j0 = 0; j0 < words; j0 += kWave) {
-        const int64_t j = j0 + w.lane;
+        const int64_t j = j0 + lane_id();
         const uint32_t word = j < words ? bm[j] : 0u;
         int tot;
         int pos = ns + wave_excl_scan(__popc(word), &tot);
@@ -2442,15 +2443,15 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
       for (int b0 = 0; b0 < ns; b0 += kU * kWave) {
         int32_t lf[kU], v[kU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) lf[u] = sorted[min(b0 + u * kWave + w.lane, ns - 1)];
+        for (int u = 0; u < kU; u++) lf[u] = sorted[min(b0 + u * kWave + lane_id(), ns - 1)];
 #pragma unroll
         for (int u = 0; u < kU; u++) v[u] = use_ls ? w.get(F_LS, loff + lf[u]) : w.get(F_STATE, loff + lf[u]);
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-          const bool keep = b0 + u * kWave + w.lane < ns && (positive_only ? v[u] > 0 : v[u] != 0);
+          const bool keep = b0 + u * kWave + lane_id() < ns && (positive_only ? v[u] > 0 : v[u] != 0);
           const uint64_t km = ballot(keep);
           if (keep) {
-            const int pos = cnt + __popcll(km & ((1ull << w.lane) - 1ull));
+            const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
             if (pos < ent_cap) {
               ent[2 * pos] = lf[u];
               ent[2 * pos + 1] = v[u];
@@ -2465,22 +2466,22 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
   }
   Key* arr;
   if (n <= w.cap) {
-    for (int i = w.lane; i < n; i += kWave) w.lds[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
+    for (int i = lane_id(); i < n; i += kWave) w.lds[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
     wave_sync();
     {
       ProfScope ps_(w, P_LDS_SORT);
-      lds_sort(w.lds, n, w.lane);
+      lds_sort(w.lds, n, lane_id());
     }
     arr = w.lds;
   } else {
-    for (int i = w.lane; i < n; i += kWave) w.gkeys[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
+    for (int i = lane_id(); i < n; i += kWave) w.gkeys[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     global_sort(w, w.gkeys, w.gkeys2, n);
     arr = w.gkeys;
   }
   int cnt = base;
   for (int i0 = 0; i0 < n; i0 += kWave) {
-    int i = i0 + w.lane;
+    int i = i0 + lane_id();
     int32_t leaf = 0, v = 0;
     bool keep = false;
     if (i < n) {
@@ -2489,7 +2490,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
       keep = positive_only ? v > 0 : v != 0;
     }
     uint64_t m = ballot(keep);
-    int rank = __popcll(m & ((1ull << w.lane) - 1ull));
+    int rank = __popcll(m & ((1ull << lane_id()) - 1ull));
     if (keep) {
       int pos = cnt + rank;
       if (pos < ent_cap) {
@@ -2521,10 +2522,10 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   const int nq = (D + 3) / 4;
   constexpr int kBins = 256;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B (host: list_cap >= 64)
-  for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
+  for (int i = lane_id(); i < kBins; i += kWave) hist[i] = 0;
   wave_sync();
   int64_t over = 0;
-  for (int q = w.lane; q < nq; q += kWave) {
+  for (int q = lane_id(); q < nq; q += kWave) {
     int4 v4 = SS4[q];
     int vv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
@@ -2548,14 +2549,14 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
     int64_t lsum = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      int v = 4 * w.lane + k;
+      int v = 4 * lane_id() + k;
       local[k] = v >= 1 ? int64_t(hist[v]) * v : 0;
       lsum += local[k];
     }
     int64_t x = lsum;
     for (int d = 1; d < 64; d <<= 1) {
-      int64_t y = int64_t(shfl_u64(uint64_t(x), max(w.lane - d, 0)));
-      if (w.lane >= d) x += y;
+      int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane_id() - d, 0)));
+      if (lane_id() >= d) x += y;
     }
     int64_t excl = x - lsum;
     // first lane whose inclusive sum reaches need
@@ -2565,11 +2566,11 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
       int64_t e = int64_t(shfl_u64(uint64_t(excl), src));
       int tt = -1;
       int64_t bb = e;
-      if (w.lane == src) {
+      if (lane_id() == src) {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           if (tt < 0) {
-            if (bb + local[k] >= need) tt = 4 * w.lane + k;
+            if (bb + local[k] >= need) tt = 4 * lane_id() + k;
             else bb += local[k];
           }
         }
@@ -2595,9 +2596,9 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   if (ss > 1) {
     if (ss > kBins) return 0;
     wave_sync();
-    for (int i = w.lane; i < kBins; i += kWave) hist[i] = 0;
+    for (int i = lane_id(); i < kBins; i += kWave) hist[i] = 0;
     wave_sync();
-    for (int q = w.lane; q < nq; q += kWave) {
+    for (int q = lane_id(); q < nq; q += kWave) {
       int4 v4 = SS4[q], s4 = S4[q];
       int vv[4] = {v4.x, v4.y, v4.z, v4.w}, st[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
@@ -2618,7 +2619,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   int64_t seen = 0;
   int cnt = 0;
   for (int q0 = 0; q0 < nq; q0 += kWave) {
-    const int q = q0 + w.lane;
+    const int q = q0 + lane_id();
     int vv[4] = {0, 0, 0, 0}, st[4] = {0, 0, 0, 0};
     if (q < nq) {
       int4 v4 = SS4[q], s4 = S4[q];
@@ -2691,14 +2692,14 @@ __device__ int lfc_first_leaf(const Wave& w, const DevBatch& b, int slot, const 
   const uint32_t* ch = b.lfc_ch + int64_t(slot) * b.lfc_nchunks * kLfcBins;
   int chunk = -1;
   for (int c0 = 0; c0 < b.lfc_nchunks && chunk < 0; c0 += kWave) {
-    const int c = c0 + w.lane;
+    const int c = c0 + lane_id();
     const uint64_t m = ballot(c < b.lfc_nchunks && ch[int64_t(c) * kLfcBins + v] > 0);
     if (m) chunk = c0 + __ffsll((unsigned long long)m) - 1;
   }
   if (chunk < 0) return -1;
   const int lo = chunk * kLfcChunk, hi = min(g_select_snap.N, lo + kLfcChunk);
   for (int i0 = lo; i0 < hi; i0 += kWave) {
-    const int i = i0 + w.lane;
+    const int i = i0 + lane_id();
     const uint64_t m = ballot(i < hi && V[i] == v);
     if (m) return i0 + __ffsll((unsigned long long)m) - 1;
   }
@@ -2719,7 +2720,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
   for (;;) {
     // skip the gap to the next present value
     int32_t vmin = 0x7fffffff;
-    for (int i = w.lane; i < N; i += kWave) {
+    for (int i = lane_id(); i < N; i += kWave) {
       const int32_t x = V[i];
       if (x >= lo && x < vmin) vmin = x;
     }
@@ -2727,9 +2728,9 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
     for (int m = 32; m >= 1; m >>= 1) vmin = min(vmin, __shfl_xor(vmin, m, 64));
     if (vmin == 0x7fffffff) break;
     lo = vmin;
-    for (int i = w.lane; i < kW; i += kWave) hist[i] = 0;
+    for (int i = lane_id(); i < kW; i += kWave) hist[i] = 0;
     wave_sync();
-    for (int i = w.lane; i < N; i += kWave) {
+    for (int i = lane_id(); i < N; i += kWave) {
       const int32_t x = V[i];
       if (x >= lo && int64_t(x) < int64_t(lo) + kW) atomicAdd(&hist[x - lo], 1u);
     }
@@ -2761,15 +2762,15 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
   int64_t seen = 0;
   int cnt = 0;
   for (int i0 = 0; i0 < N; i0 += kWave) {
-    const int i = i0 + w.lane;
+    const int i = i0 + lane_id();
     const int32_t x = i < N ? V[i] : 0;
     const bool tie = i < N && x == t;
     const uint64_t tm = ballot(tie);
-    const int64_t r = seen + __popcll(tm & ((1ull << w.lane) - 1ull));
+    const int64_t r = seen + __popcll(tm & ((1ull << lane_id()) - 1ull));
     const bool keep = (x > 0 && x < t) || (tie && r < mt);
     const uint64_t km = ballot(keep);
     if (keep) {
-      const int pos = cnt + __popcll(km & ((1ull << w.lane) - 1ull));
+      const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
       if (pos < ecap) {
         ent[2 * pos] = i;
         ent[2 * pos + 1] = (tie && r == mt - 1) ? rem_last : x;
@@ -2788,7 +2789,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
 __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_out& o, int32_t* ent, int ecap) {
   const DevSnap& s = g_select_snap;
   const int L1 = s.L - 1;
-  const int lane = w.lane;
+  const int lane = lane_id();
   const int32_t* V = w.ctr + w.SD + s.level_off[L1];
   const int32_t need = w.ev->count;  // sliceCount = count / 1 (host: count >= 0)
   const uint32_t* tot = b.lfc_tot + int64_t(slot) * kLfcBins;
@@ -2939,7 +2940,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
     Key pbk = key_max();
     if (use_partials) {  // reductions precomputed per fill block
       Key inv = key_max();
-      for (int i = w.lane; i < w.nblk; i += kWave) {
+      for (int i = lane_id(); i < w.nblk; i += kWave) {
         const LeafPartial& p = w.partials[i];
         top = key_min2(top, p.top);
         inv = key_min2(inv, Key{~p.last.hi, ~p.last.lo});
@@ -2952,7 +2953,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       inv = wave_min_key(inv);
       last = Key{~inv.hi, ~inv.lo};
       pbst = uint32_t(wave_min_u64(pbst));
-      for (int i = w.lane; i < w.nblk; i += kWave)
+      for (int i = lane_id(); i < w.nblk; i += kWave)
         if (w.partials[i].bfst == pbst) pbk = key_min2(pbk, w.partials[i].bfkey);
       pbk = wave_min_key(pbk);
     } else if (!w.leader) {
@@ -2976,13 +2977,13 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         int4 sa[QU], ssa[QU];
 #pragma unroll
         for (int u = 0; u < QU; u++) {
-          const int q = min(q0 + u * kWave + w.lane, nq - 1);
+          const int q = min(q0 + u * kWave + lane_id(), nq - 1);
           sa[u] = S4[q];
           ssa[u] = SS4[q];
         }
 #pragma unroll
         for (int u = 0; u < QU; u++) {
-          const int q = q0 + u * kWave + w.lane;
+          const int q = q0 + u * kWave + lane_id();
           const int32_t st4[4] = {sa[u].x, sa[u].y, sa[u].z, sa[u].w};
           const int32_t ss4[4] = {ssa[u].x, ssa[u].y, ssa[u].z, ssa[u].w};
 #pragma unroll
@@ -3036,7 +3037,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       }
     } else {
       bool has_last = false;
-      for (int i = w.lane; i < D; i += kWave) {
+      for (int i = lane_id(); i < D; i += kWave) {
         int g = loff + i;
         int32_t ls = w.get(F_LS, g), sswl = w.get(F_SSWL, g), swl = w.get(F_SWL, g), ss = w.get(F_SLICE, g);
         Key k = key_wl(w.lfc, ls, sswl, swl, i);
@@ -3068,13 +3069,13 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
           topg = loff + int(uint32_t(pbk.lo));
         } else {
           uint32_t bst = ~0u;
-          for (int i = w.lane; i < D; i += kWave) {
+          for (int i = lane_id(); i < D; i += kWave) {
             int32_t st = w.get(f, loff + i);
             if (st >= sliceCount && s_asc(st) < bst) bst = s_asc(st);
           }
           bst = uint32_t(wave_min_u64(uint64_t(bst)));
           Key b = key_max();
-          for (int i = w.lane; i < D; i += kWave) {
+          for (int i = lane_id(); i < D; i += kWave) {
             int g = loff + i;
             if (s_asc(w.get(f, g)) == bst) {
               Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
@@ -3111,14 +3112,14 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       int32_t remS = sliceCount, remL = leaderCount;
       int nr = 0;
       if (D <= w.cap) {
-        for (int i = w.lane; i < D; i += kWave) {
+        for (int i = lane_id(); i < D; i += kWave) {
           int g = loff + i;
           w.lds[i] = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
         }
         wave_sync();
         {
           ProfScope ps_(w, P_LDS_SORT);
-          lds_sort(w.lds, D, w.lane);
+          lds_sort(w.lds, D, lane_id());
         }
         SeqLds seq{&w, D, loff, 0};
         int idx = 0;
@@ -3137,14 +3138,14 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         }
         // re-sort the remainder sortedDomainsWithLeader[idx:] with sortedDomains
         const int nrem = D - idx;
-        for (int i = w.lane; i < nrem; i += kWave) w.gkeys[i] = w.lds[idx + i];
+        for (int i = lane_id(); i < nrem; i += kWave) w.gkeys[i] = w.lds[idx + i];
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         wave_sync();
-        for (int i = w.lane; i < nrem; i += kWave) w.lds[i] = w.kplain(loff + int(uint32_t(w.gkeys[i].lo)));
+        for (int i = lane_id(); i < nrem; i += kWave) w.lds[i] = w.kplain(loff + int(uint32_t(w.gkeys[i].lo)));
         wave_sync();
         {
           ProfScope ps_(w, P_LDS_SORT);
-          lds_sort(w.lds, nrem, w.lane);
+          lds_sort(w.lds, nrem, lane_id());
         }
         SeqLds seq2{&w, nrem, loff, 0};
         for (int i = 0; remS > 0 && i < nrem; i++) {
@@ -3170,7 +3171,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
             Field f = remL > 0 ? F_SSWL : F_SLICE;
             if (w.get(f, d) >= remS) {
               uint32_t bst = ~0u;
-              for (int i = w.lane; i < D; i += kWave) {
+              for (int i = lane_id(); i < D; i += kWave) {
                 int g = loff + i;
                 Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
                 int32_t st = w.get(f, g);
@@ -3178,7 +3179,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
               }
               bst = uint32_t(wave_min_u64(uint64_t(bst)));
               Key b = key_max();
-              for (int i = w.lane; i < D; i += kWave) {
+              for (int i = lane_id(); i < D; i += kWave) {
                 int g = loff + i;
                 Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
                 if (key_le(cur, k) && s_asc(w.get(f, g)) == bst && key_lt(k, b)) b = k;
@@ -3196,7 +3197,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
           consumed = true;
           // next in WL order
           Key nb = key_max();
-          for (int i = w.lane; i < D; i += kWave) {
+          for (int i = lane_id(); i < D; i += kWave) {
             int g = loff + i;
             Key k = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
             if (key_lt(cur, k) && key_lt(k, nb)) nb = k;
@@ -3215,7 +3216,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         for (;;) {
           if (remS <= 0) break;
           Key nb = key_max();
-          for (int i = w.lane; i < D; i += kWave) {
+          for (int i = lane_id(); i < D; i += kWave) {
             int g = loff + i;
             if (consumed) {
               Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
@@ -3231,7 +3232,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
           int d = loff + int(uint32_t(nb.lo));
           if (w.bf && w.get(F_SLICE, d) >= remS) {
             uint32_t bst = ~0u;
-            for (int i = w.lane; i < D; i += kWave) {
+            for (int i = lane_id(); i < D; i += kWave) {
               int g = loff + i;
               if (consumed) {
                 Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
@@ -3243,7 +3244,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
             }
             bst = uint32_t(wave_min_u64(uint64_t(bst)));
             Key b = key_max();
-            for (int i = w.lane; i < D; i += kWave) {
+            for (int i = lane_id(); i < D; i += kWave) {
               int g = loff + i;
               if (consumed) {
                 Key kw = key_wl(w.lfc, w.get(F_LS, g), w.get(F_SSWL, g), w.get(F_SWL, g), i);
@@ -3278,6 +3279,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
 
 // One wave per eval of `ids` (the BestFit-side and the fast-LFC evals are
 // launched separately, on two streams).
+constexpr int kSelectWaves = 4;  // select_kernel's block = 4 waves (launch: 256 threads)
 __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, const int32_t* ids, int nids) {
   extern __shared__ Key lds_all[];
   const int wave = threadIdx.x >> 6;
@@ -3287,10 +3289,16 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   const int eid = ids[slot];
   const uint64_t t_begin = wall_clock64();
   const DevEval& ev = b.evals[eid];
-  Wave w;
+  // The wave's descriptor, result header and walk out-parameters live in LDS:
+  // the walk's helpers are not inlined and take them by reference, which put
+  // them in scratch (400 B/lane, a vector-memory round trip per field read).
+  // Every field is wave-uniform (written alike by all lanes).
+  __shared__ Wave sh_wave[kSelectWaves];
+  __shared__ kueue_tas_eval_out sh_out[kSelectWaves];
+  __shared__ int sh_ints[kSelectWaves][4];  // nres, fitLevel, nn
+  Wave& w = sh_wave[wave];
   w.ev = &ev;
   w.eid = eid;
-  w.lane = lane;
   w.leader = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   w.lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
   w.bf = !w.lfc;
@@ -3314,14 +3322,16 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.gkeys = reinterpret_cast<Key*>(sc + 2 * lcap);
   w.gkeys2 = w.gkeys + lcap;
   w.overflow = false;
+#if KTAS_PROFILE
   for (auto& x : w.prof) x = 0;
+#endif
   w.partials = (ev.requested_level == s.L - 1 && b.partial_idx[eid] >= 0)
                    ? b.partials + int64_t(b.partial_idx[eid]) * b.nblk : nullptr;
   w.nblk = b.nblk;
   int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
   const int ecap = b.entry_cap;
 
-  kueue_tas_eval_out o;
+  kueue_tas_eval_out& o = sh_out[wave];
   o.status = KUEUE_TAS_ST_OK;
   o.a = o.b = 0;
   o.fit_level = 0;
@@ -3334,8 +3344,13 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   for (int c = 0; c < KUEUE_TAS_MAX_LAYERS; c++) o.ml_fit[c] = o.ml_need[c] = 0;
   o.reserved[0] = o.reserved[1] = 0;
 
-  if (KTAS_PROFILE) w.prof[P_SETUP] = wall_clock64() - t_begin;
-  int nres = 0, fitLevel = 0;
+#if KTAS_PROFILE
+  w.prof[P_SETUP] = wall_clock64() - t_begin;
+#endif
+  int& nres = sh_ints[wave][0];
+  int& fitLevel = sh_ints[wave][1];
+  nres = 0;
+  fitLevel = 0;
   int r;
   const int lslot = b.lfc_slot[eid];
   if (lslot >= 0) {
@@ -3363,7 +3378,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
       const bool positive = !w.leader && w.bf && go_div32(ev.count, ev.slice_size) > 0;
       int32_t* kids = positive ? w.listD : w.listC;
       int nch = positive ? gather_children_positive(w, cur, ncur, level, kids) : gather_children(w, cur, ncur, level, kids);
-      int nn = 0;
+      int& nn = sh_ints[wave][2];
+      nn = 0;
       bool ok2 = walk_sorted(w, kids, nch, level + 1, ev.count, leaderCount, ev.slice_size, true, 0, spare, &nn);
       if (!ok2) o.assignment_nil = 1;
       int32_t* t = cur;
@@ -3377,7 +3393,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
         sol = 1;
         if (ev.ssal[level + 1] != 0) sol = ev.ssal[level + 1];
       }
-      int nn = 0;
+      int& nn = sh_ints[wave][2];
+      nn = 0;
       const int poff = s.level_off[level];
       for (int i = 0; i < ncur; i++) {
         int d = cur[i];
@@ -3687,6 +3704,56 @@ __device__ __forceinline__ int64_t load_l2(const int64_t* p) {
 __device__ __forceinline__ uint32_t load_l2(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// CountIn of one record against free - usage (requests.go:174-217, no pods:1):
+// terms are loaded first, then every capacity load issues at once (the loop
+// Go breaks out of is evaluated on registers), kAdmitTerms per pass.
+constexpr int kAdmitTerms = 8;
+__device__ __forceinline__ bool admit_record_fits(const DevSnap& s, const int64_t* tas_usage,
+                                                  const uint32_t* usage_present, const kueue_tas_fits_req& r,
+                                                  const kueue_tas_fits_term* terms) {
+  if (r.leaf < 0 || r.leaf >= s.N) return false;
+  const uint32_t pres = s.free_present[r.leaf] | load_l2(usage_present + r.leaf);
+  int32_t result = 0;
+  bool any = false;
+  for (int k0 = 0; k0 < r.num_terms; k0 += kAdmitTerms) {
+    int32_t col[kAdmitTerms];
+    int64_t val[kAdmitTerms], fc[kAdmitTerms], us[kAdmitTerms];
+#pragma unroll
+    for (int u = 0; u < kAdmitTerms; u++) {
+      col[u] = -1;
+      val[u] = 0;
+      if (k0 + u < r.num_terms) {
+        const kueue_tas_fits_term t = terms[r.term_begin + k0 + u];
+        col[u] = t.col;
+        val[u] = t.value;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kAdmitTerms; u++) {
+      fc[u] = us[u] = 0;
+      if (col[u] >= 0) {
+        fc[u] = s.free_cap[int64_t(col[u]) * s.N + r.leaf];
+        us[u] = load_l2(tas_usage + int64_t(col[u]) * s.N + r.leaf);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kAdmitTerms; u++) {
+      if (k0 + u >= r.num_terms) break;
+      const bool present = col[u] >= 0 && ((pres >> col[u]) & 1u);
+      if (!present && val[u] != 0) return 0 >= r.count;  // CountIn: a missing resource fits 0 (:200-203)
+      int32_t c = 0x7fffffff;
+      if (val[u] != 0) {
+        const int64_t cap = int64_t(uint64_t(fc[u]) - uint64_t(us[u]));
+        const int64_t q = (cap == INT64_MIN && val[u] == -1) ? INT64_MIN : cap / val[u];
+        c = max(int32_t(uint32_t(uint64_t(q))), 0);
+      }
+      if (!any || c < result) result = c;
+      any = true;
+    }
+  }
+  return (any ? result : 0) >= r.count;
+}
+
 __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage, uint32_t* usage_present,
                                                    const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
                                                    const int64_t* wl_off, int n_wl, int pods_col, int32_t* admitted) {
@@ -3698,35 +3765,7 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
     for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
       const int64_t i = base + lane;
       bool fit = true;
-      if (i < r1) {
-        const kueue_tas_fits_req r = reqs[i];
-        if (r.leaf < 0 || r.leaf >= s.N) {
-          fit = false;
-        } else {
-          const uint32_t pres = s.free_present[r.leaf] | load_l2(usage_present + r.leaf);
-          int32_t result = 0;
-          bool any = false;
-          for (int k = 0; k < r.num_terms; k++) {
-            const kueue_tas_fits_term t = terms[r.term_begin + k];
-            const bool present = t.col >= 0 && ((pres >> t.col) & 1u);
-            if (!present && t.value != 0) {
-              result = 0;
-              any = true;
-              break;
-            }
-            int32_t c = 0x7fffffff;
-            if (t.value != 0) {
-              const int64_t cap = int64_t(uint64_t(s.free_cap[int64_t(t.col) * s.N + r.leaf]) -
-                                          uint64_t(load_l2(tas_usage + int64_t(t.col) * s.N + r.leaf)));
-              const int64_t q = (cap == INT64_MIN && t.value == -1) ? INT64_MIN : cap / t.value;
-              c = max(int32_t(uint32_t(uint64_t(q))), 0);
-            }
-            if (!any || c < result) result = c;
-            any = true;
-          }
-          fit = (any ? result : 0) >= r.count;
-        }
-      }
+      if (i < r1) fit = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
       all_fit = ballot(!fit) == 0;
     }
     if (lane == 0) admitted[w] = all_fit ? 1 : 0;

@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_deltas", "kueue_tas_host_run", "kueue_tas_build_id",
     "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
-    "kueue_tas_host_compile_workload",
+    "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -138,6 +138,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_device_host_times.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
     lib.kueue_tas_host_update_usage.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
     lib.kueue_tas_host_update_usage.restype = c.c_int
@@ -439,6 +440,12 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_last_deltas(self._h, deltas.ctypes.data, deltas.size):
             raise RuntimeError(self._err())
         return adm[: nw.value], deltas
+
+    def last_admit_times(self):
+        """Host ms of the last admit: (record prep, kueue_tas_admit, delta list)."""
+        ms = (ctypes.c_double * 3)()
+        self._lib.kueue_tas_host_last_admit_times(self._h, ms)
+        return tuple(ms)
 
     def apply_deltas(self, deltas):
         """Apply another replica's admission deltas (numpy DELTA_DTYPE)."""

@@ -13,12 +13,18 @@ CSRC="$ROOT/kueue_oss_amd/csrc"
 # - lockstep: on hardware the 64 lanes of a wave execute the (wave-uniform)
 #   counter stores of phase 2 in lockstep; fibers do not, so every store of a
 #   domain counter becomes a wave-synchronization point here.
+# - per-wave state: select_kernel keeps the wave's descriptor / result header /
+#   out-parameters in LDS, stored alike by all (lockstep) lanes; fibers are
+#   not lockstep, so each lane keeps a private copy instead.
 sed -e 's/extern __shared__ Key lds_all\[\];/Key* lds_all = static_cast<Key*>(emu::dynamic_lds());/' \
+    -e 's/^  __shared__ \(Wave sh_wave\|kueue_tas_eval_out sh_out\|int sh_ints\)/  \1/' \
     -e 's/^    own(g);$/    emu::wave_barrier(); own(g);/' \
     -e 's/^    ov\[int64_t(f) \* SD + g\] = v;/    ov[int64_t(f) * SD + g] = v; emu::wave_barrier();/' \
   "$CSRC/tas_kernels.hip" > "$OUT/src/tas_kernels.hip"
 grep -q 'emu::wave_barrier(); own(g);' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
 grep -q '= v; emu::wave_barrier();' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
+grep -q '^  Wave sh_wave\[' "$OUT/src/tas_kernels.hip" || { echo "per-wave state patch failed"; exit 1; }
+grep -q '^  __shared__ \(Wave\|kueue_tas_eval_out\|int sh_ints\)' "$OUT/src/tas_kernels.hip" && { echo "per-wave state patch incomplete"; exit 1; }
 cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$CSRC/label_selectors.h" "$OUT/src/"
 sed "s#\"../../include/#\"#" "$CSRC/tas_internal.h" > "$OUT/src/tas_internal.h"
 cp "$ROOT/include/kueue_tas.h" "$ROOT/include/kueue_tas_debug.h" "$OUT/src/"

@@ -7,7 +7,7 @@
 // OS thread, round-robin; blocks run sequentially.  Wave-level primitives
 // (__shfl*, __ballot, wave barriers, fences) synchronize the 64 lanes of a
 // wave; __syncthreads synchronizes the block.  __shared__ locals become
-// function statics (one block runs at a time).
+// function statics, per OS thread (one block of a stream runs at a time).
 #pragma once
 #include <algorithm>
 #include <cstddef>
@@ -23,7 +23,7 @@
 #define __host__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
-#define __shared__ static
+#define __shared__ static thread_local
 #define __constant__
 #define HIP_SYMBOL(x) (&(x))
 
