@@ -670,19 +670,65 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
       if (terms[r.term_begin + k].col < 0 || terms[r.term_begin + k].col >= c->snap.R)
         return fail(c, KUEUE_TAS_EINVAL, "admit term column out of range");
   }
+  // monotone shortcut (admit_fit0_kernel) only for non-negative values and
+  // counts whose total usage this call could add stays below 2^61 (with
+  // every capacity and usage value below 2^61, checked on the device, no
+  // int64 arithmetic of the call wraps)
+  bool exact = false;
+  __int128 total = 0;
+  for (size_t i = 0; i < n && !exact; i++) {
+    const kueue_tas_fits_req& r = reqs[i];
+    exact = r.count < 0;
+    for (int k = 0; k < r.num_terms && !exact; k++) {
+      const int64_t v = terms[r.term_begin + k].value;
+      exact = v < 0;
+      total += __int128(v) * r.count;
+    }
+    total += r.count;  // pods
+    exact = exact || total >= (__int128(1) << 61);
+  }
   HIPCHK(c, hipSetDevice(c->device));
-  const size_t o_terms = (n * sizeof(kueue_tas_fits_req) + 255) / 256 * 256;
-  const size_t o_off = o_terms + (num_terms * sizeof(kueue_tas_fits_term) + 255) / 256 * 256;
-  const size_t o_out = o_off + ((n_wl + 1) * 8 + 255) / 256 * 256;
-  HIPCHK(c, c->d_fits.ensure(o_out + (n_wl + 1) * 4));  // + the kernel's sink word
+  // one pinned upload: records, terms, workload offsets, record -> workload,
+  // phase-1 flags (1 = fit) and the exact flag
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t o_terms = al(n * sizeof(kueue_tas_fits_req));
+  const size_t o_off = o_terms + al(num_terms * sizeof(kueue_tas_fits_term));
+  const size_t o_recwl = o_off + al((n_wl + 1) * 8);
+  const size_t o_fit0 = o_recwl + al(n * 4);
+  const size_t o_exact = o_fit0 + al(n_wl * 4);
+  const size_t up_bytes = o_exact + 4;
+  const size_t o_out = al(up_bytes);
+  const size_t nwords = (size_t(c->snap.N) + 31) / 32;
+  const bool lds_bits = nwords * 4 <= 64 * 1024;
+  const size_t o_bits = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
+  HIPCHK(c, c->d_fits.ensure(o_bits + (lds_bits ? 0 : nwords * 4)));
+  HIPCHK(c, c->h_stage.ensure(up_bytes));
+  uint8_t* h = c->h_stage.p;
+  if (n) memcpy(h, reqs, n * sizeof(kueue_tas_fits_req));
+  if (num_terms) memcpy(h + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term));
+  memcpy(h + o_off, wl_off, (n_wl + 1) * 8);
+  int32_t* rec_wl = reinterpret_cast<int32_t*>(h + o_recwl);
+  for (size_t w = 0; w < n_wl; w++)
+    for (int64_t i = wl_off[w]; i < wl_off[w + 1]; i++) rec_wl[i] = int32_t(w);
+  int32_t* fit0 = reinterpret_cast<int32_t*>(h + o_fit0);
+  for (size_t w = 0; w < n_wl; w++) fit0[w] = 1;
+  *reinterpret_cast<int32_t*>(h + o_exact) = exact ? 1 : 0;
   uint8_t* d = c->d_fits.p;
-  if (n) HIPCHK(c, hipMemcpyAsync(d, reqs, n * sizeof(kueue_tas_fits_req), hipMemcpyHostToDevice, c->stream));
-  if (num_terms)
-    HIPCHK(c, hipMemcpyAsync(d + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d + o_off, wl_off, (n_wl + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), 0, c->stream, c->snap, c->d_usage.p, c->d_usage_present.p,
-                     reinterpret_cast<const kueue_tas_fits_req*>(d), reinterpret_cast<const kueue_tas_fits_term*>(d + o_terms),
-                     reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col, reinterpret_cast<int32_t*>(d + o_out));
+  HIPCHK(c, hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, c->stream));
+  if (!lds_bits) HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
+  const auto* d_reqs = reinterpret_cast<const kueue_tas_fits_req*>(d);
+  const auto* d_terms = reinterpret_cast<const kueue_tas_fits_term*>(d + o_terms);
+  if (n) {
+    hipLaunchKernelGGL(admit_fit0_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->snap,
+                       c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
+                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), reinterpret_cast<int32_t*>(d + o_fit0),
+                       reinterpret_cast<int32_t*>(d + o_exact));
+    HIPCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
+                     c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
+                     pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
+                     reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(admitted, d + o_out, n_wl * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -2266,6 +2266,12 @@ struct kueue_tas_host {
   std::vector<Workload>& active() { return shard_ids.empty() ? compiled : shard; }
   std::vector<kueue_tas_delta> last_deltas;  // usage deltas the last kueue_tas_host_admit applied
   double admit_ms[3] = {0, 0, 0};            // last admit: host prep, kueue_tas_admit, delta list
+  // admit's working storage (kept between rounds)
+  std::vector<int32_t> admit_seen, admit_ids;
+  std::vector<int64_t> admit_start, admit_off;
+  std::vector<std::array<int32_t, 3>> admit_doms;
+  std::vector<kueue_tas_fits_req> admit_fr;
+  std::vector<kueue_tas_fits_term> admit_terms;
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
     for (auto* v : {&compiled, &shard})
@@ -2886,12 +2892,23 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
                          size_t* n_workloads, size_t* n_deltas) {
   if (!h || !h->snap || !h->err.empty() || (len && !recs) || len % 4 || !n_workloads) return KUEUE_TAS_EINVAL;
   try {
-    {  // capacity first: nothing is admitted when the caller's buffer is short
-      std::set<int32_t> heads;
-      for (size_t o = 0; o < len; o += 4) heads.insert(recs[o]);
-      *n_workloads = heads.size();
-      if (!admitted || admitted_cap < 2 * heads.size()) return KUEUE_TAS_EOVERFLOW;
+    // workloads in ascending id (the gathered quads of every rank; a
+    // workload's quads are contiguous per rank), capacity checked first:
+    // nothing is admitted when the caller's buffer is short
+    const size_t W = h->compiled.size();
+    std::vector<int32_t>& seen = h->admit_seen;  // per id: 0 absent, 1 present, 2 failed evaluation
+    seen.assign(W, 0);
+    size_t nwl = 0;
+    for (size_t o = 0; o < len; o += 4) {
+      const int32_t g = recs[o];
+      if (g < 0 || size_t(g) >= W) throw std::runtime_error("admit: workload id out of range");
+      if (!seen[size_t(g)]) {
+        seen[size_t(g)] = 1;
+        nwl++;
+      }
     }
+    *n_workloads = nwl;
+    if (!admitted || admitted_cap < 2 * nwl) return KUEUE_TAS_EOVERFLOW;
     h->last_deltas.clear();
     const double t0 = now_ms();
     FlavorSnapshot& s = *h->snap;
@@ -2900,33 +2917,42 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       h->err = s.err;
       return rc;
     }
-    struct Wl {
-      bool fail = false;
-      std::vector<std::array<int32_t, 3>> doms;  // podset, leaf, count
-    };
-    std::map<int32_t, Wl> byId;
+    // records of each workload, grouped by id with a counting sort
+    std::vector<int64_t>& start = h->admit_start;
+    start.assign(W + 1, 0);
     for (size_t o = 0; o < len; o += 4) {
       const int32_t g = recs[o];
-      if (g < 0 || size_t(g) >= h->compiled.size()) throw std::runtime_error("admit: workload id out of range");
-      Wl& w = byId[g];
       if (recs[o + 1] < 0) {
-        w.fail |= recs[o + 2] != 0;
+        if (recs[o + 2] != 0) seen[size_t(g)] = 2;
       } else {
         if (size_t(recs[o + 1]) >= h->compiled[size_t(g)].podsets.size() || recs[o + 2] < 0 || recs[o + 2] >= s.N())
           throw std::runtime_error("admit: record out of range");
-        w.doms.push_back({recs[o + 1], recs[o + 2], recs[o + 3]});
+        start[size_t(g) + 1]++;
       }
     }
-    *n_workloads = byId.size();
-    std::vector<kueue_tas_fits_req> fr;
-    std::vector<kueue_tas_fits_term> terms;
-    std::vector<int64_t> off(1, 0);
-    std::vector<int32_t> ids;
-    for (auto& kv : byId) {
-      ids.push_back(kv.first);
-      if (!kv.second.fail) {
-        const Workload& wl = h->compiled[size_t(kv.first)];
-        for (auto& d : kv.second.doms) {
+    for (size_t g = 0; g < W; g++) start[g + 1] += start[g];
+    std::vector<std::array<int32_t, 3>>& doms = h->admit_doms;  // podset, leaf, count
+    doms.resize(size_t(start[W]));
+    {
+      std::vector<int64_t> pos(start.begin(), start.end() - 1);
+      for (size_t o = 0; o < len; o += 4)
+        if (recs[o + 1] >= 0) doms[size_t(pos[size_t(recs[o])]++)] = {recs[o + 1], recs[o + 2], recs[o + 3]};
+    }
+    std::vector<kueue_tas_fits_req>& fr = h->admit_fr;
+    std::vector<kueue_tas_fits_term>& terms = h->admit_terms;
+    std::vector<int64_t>& off = h->admit_off;
+    std::vector<int32_t>& ids = h->admit_ids;
+    fr.clear();
+    terms.clear();
+    off.assign(1, 0);
+    ids.clear();
+    for (size_t g = 0; g < W; g++) {
+      if (!seen[g]) continue;
+      ids.push_back(int32_t(g));
+      if (seen[g] == 1) {
+        const Workload& wl = h->compiled[g];
+        for (int64_t k = start[g]; k < start[g + 1]; k++) {
+          const auto& d = doms[size_t(k)];
           const TASPodSetRequests& ps = wl.podsets[size_t(d[0])];
           kueue_tas_fits_req r{d[1], d[2], int32_t(terms.size()), 0};
           for (auto& t : ps.requestIds) {

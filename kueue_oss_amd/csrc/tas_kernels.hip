@@ -3754,42 +3754,127 @@ __device__ __forceinline__ bool admit_record_fits(const DevSnap& s, const int64_
   return (any ? result : 0) >= r.count;
 }
 
+// Phase 1 (parallel over every record of the call): the record's fit
+// against the usage at the start of the call; a workload with a record that
+// does not fit then cannot fit after more usage is added (CountIn is
+// monotone in the usage while nothing wraps: `exact` = 1 when a capacity or
+// usage value is large enough that it might, and the sequential pass then
+// re-checks everything).
+__global__ __launch_bounds__(256) void admit_fit0_kernel(DevSnap s, const int64_t* tas_usage,
+                                                         const uint32_t* usage_present, const kueue_tas_fits_req* reqs,
+                                                         const kueue_tas_fits_term* terms, const int32_t* rec_wl, int n,
+                                                         int32_t* wl_fit0, int32_t* exact) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const kueue_tas_fits_req r = reqs[i];
+  if (!admit_record_fits(s, tas_usage, usage_present, r, terms)) atomicAnd(wl_fit0 + rec_wl[i], 0);
+  if (r.leaf < 0 || r.leaf >= s.N) return;
+  constexpr int64_t kBig = int64_t(1) << 61;
+  bool big = false;
+  for (int k = 0; k < r.num_terms; k++) {
+    const int c = terms[r.term_begin + k].col;
+    if (c < 0) continue;
+    const int64_t f = s.free_cap[int64_t(c) * s.N + r.leaf], u = tas_usage[int64_t(c) * s.N + r.leaf];
+    big |= f >= kBig || f <= -kBig || u >= kBig || u <= -kBig;
+  }
+  if (big) atomicOr(exact, 1);
+}
+
+// Phase 2: one wave walks the workloads in order (the dependency chain), its
+// lanes splitting a workload's records.  A workload whose phase-1 fit failed
+// is rejected at once; one that fitted is re-checked against the current
+// usage only when an earlier workload of this call was admitted onto one of
+// its leaves (`touched`, one bit per leaf, in LDS when it fits).  Admission
+// adds the usage with returning atomics whose values the wave consumes, so
+// they have completed before a later re-check's L1-bypassing loads issue (no
+// __threadfence: that costs microseconds per call on gfx950).
 __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage, uint32_t* usage_present,
                                                    const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
-                                                   const int64_t* wl_off, int n_wl, int pods_col, int32_t* admitted) {
+                                                   const int64_t* wl_off, int n_wl, int pods_col,
+                                                   const int32_t* wl_fit0, const int32_t* exact_flag,
+                                                   uint32_t* touched_global, int touched_in_lds, int32_t* admitted) {
+  extern __shared__ uint32_t touched_lds[];
   const int lane = lane_id();
-  unsigned long long sink = 0;
-  for (int w = 0; w < n_wl; w++) {
-    const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
-    bool all_fit = true;
-    for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
-      const int64_t i = base + lane;
-      bool fit = true;
-      if (i < r1) fit = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
-      all_fit = ballot(!fit) == 0;
-    }
-    if (lane == 0) admitted[w] = all_fit ? 1 : 0;
-    if (!all_fit) continue;
-    for (int64_t i = r0 + lane; i < r1; i += kWave) {
-      const kueue_tas_fits_req r = reqs[i];
-      uint32_t bits = 0;
-      for (int k = 0; k < r.num_terms; k++) {
-        const kueue_tas_fits_term t = terms[r.term_begin + k];
-        if (t.col < 0) continue;  // the host gives every usage resource a column first
-        sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
-                          (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
-        bits |= 1u << t.col;
-      }
-      if (pods_col >= 0) {
-        sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
-                          (unsigned long long)int64_t(r.count));
-        bits |= 1u << pods_col;
-      }
-      sink += atomicOr(usage_present + r.leaf, bits);
-    }
+  if (touched_in_lds) {  // (the global bitmap is cleared by the host)
+    for (int k = lane; k < (s.N + 31) / 32; k += kWave) touched_lds[k] = 0;
     wave_sync();
   }
-  if (lane == 0) admitted[n_wl] = int32_t(uint32_t(sink));  // consumes the returned values (see above)
+  const bool exact = *exact_flag != 0;
+  unsigned long long sink = 0;
+  for (int w0 = 0; w0 < n_wl; w0 += kWave) {
+    // 64 workloads' phase-1 results and offsets per load
+    const int wl = min(w0 + lane, n_wl - 1);
+    const int32_t my_fit0 = wl_fit0[wl];
+    const int64_t my_r0 = wl_off[wl], my_r1 = wl_off[wl + 1];
+    const int wend = min(w0 + kWave, n_wl);
+    for (int w = w0; w < wend; w++) {
+      const int32_t fit0 = __shfl(my_fit0, w - w0, 64);
+      const int64_t r0 = int64_t(shfl_u64(uint64_t(my_r0), w - w0)), r1 = int64_t(shfl_u64(uint64_t(my_r1), w - w0));
+      if (!fit0 && !exact) {
+        if (lane == 0) admitted[w] = 0;
+        continue;
+      }
+      bool recheck = exact;
+      for (int64_t base = r0; base < r1 && !recheck; base += kWave) {
+        const int64_t i = base + lane;
+        bool hit = false;
+        if (i < r1) {
+          const int32_t leaf = reqs[i].leaf;
+          if (leaf >= 0 && leaf < s.N) {
+            const uint32_t word = touched_in_lds ? touched_lds[leaf >> 5] : load_l2(touched_global + (leaf >> 5));
+            hit = (word >> (leaf & 31)) & 1u;
+          }
+        }
+        recheck = ballot(hit) != 0;
+      }
+      bool all_fit = true;
+      if (recheck) {
+        for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
+          const int64_t i = base + lane;
+          bool fit = true;
+          if (i < r1) fit = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+          all_fit = ballot(!fit) == 0;
+        }
+      }
+      if (lane == 0) admitted[w] = all_fit ? 1 : 0;
+      if (!all_fit) continue;
+      for (int64_t i = r0 + lane; i < r1; i += kWave) {
+        const kueue_tas_fits_req r = reqs[i];
+        uint32_t bits = 0;
+        int32_t col[kAdmitTerms];
+        int64_t val[kAdmitTerms];
+        for (int k0 = 0; k0 < r.num_terms; k0 += kAdmitTerms) {
+#pragma unroll
+          for (int u = 0; u < kAdmitTerms; u++) {
+            col[u] = -1;
+            val[u] = 0;
+            if (k0 + u < r.num_terms) {
+              const kueue_tas_fits_term t = terms[r.term_begin + k0 + u];
+              col[u] = t.col;
+              val[u] = t.value;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kAdmitTerms; u++) {
+            if (col[u] < 0) continue;  // the host gives every usage resource a column first
+            sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(col[u]) * s.N + r.leaf),
+                              (unsigned long long)(uint64_t(val[u]) * uint64_t(int64_t(r.count))));
+            bits |= 1u << col[u];
+          }
+        }
+        if (pods_col >= 0) {
+          sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                            (unsigned long long)int64_t(r.count));
+          bits |= 1u << pods_col;
+        }
+        sink += atomicOr(usage_present + r.leaf, bits);
+        if (touched_in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+        else sink += atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+      }
+      wave_sync();
+    }
+  }
+  if (lane == 0) admitted[n_wl] = int32_t(uint32_t(sink));
 }
 
 }  // namespace ktas

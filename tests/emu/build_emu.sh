@@ -17,6 +17,7 @@ CSRC="$ROOT/kueue_oss_amd/csrc"
 #   out-parameters in LDS, stored alike by all (lockstep) lanes; fibers are
 #   not lockstep, so each lane keeps a private copy instead.
 sed -e 's/extern __shared__ Key lds_all\[\];/Key* lds_all = static_cast<Key*>(emu::dynamic_lds());/' \
+    -e 's/extern __shared__ uint32_t touched_lds\[\];/uint32_t* touched_lds = static_cast<uint32_t*>(emu::dynamic_lds());/' \
     -e 's/^  __shared__ \(Wave sh_wave\|kueue_tas_eval_out sh_out\|int sh_ints\)/  \1/' \
     -e 's/^    own(g);$/    emu::wave_barrier(); own(g);/' \
     -e 's/^    ov\[int64_t(f) \* SD + g\] = v;/    ov[int64_t(f) * SD + g] = v; emu::wave_barrier();/' \

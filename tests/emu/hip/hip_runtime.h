@@ -119,6 +119,9 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
   return o;
 }
 inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v; return o; }
+inline int atomicOr(int* p, int v) { int o = *p; *p = o | v; return o; }
+inline int atomicAnd(int* p, int v) { int o = *p; *p = o & v; return o; }
+inline unsigned atomicAnd(unsigned* p, unsigned v) { unsigned o = *p; *p = o & v; return o; }
 inline void __threadfence() {}
 // device-scope loads that bypass L1 on hardware; plain loads here
 #define __HIP_MEMORY_SCOPE_AGENT 3

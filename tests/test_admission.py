@@ -98,3 +98,40 @@ def test_emulated_admit_then_rebuild(emu_lib):  # noqa: F811
 @pytest.mark.gpu
 def test_admit_then_rebuild_on_gpu():
     _admit_then_rebuild(lambda d: TASFlavorSnapshot(d))
+
+
+def _admit_batch(make, n=64, shape=(2, 2, 4, 8)):
+    """kueue_tas_host_admit over one evaluated batch (admit_fit0_kernel +
+    admit_kernel: phase-1 rejections, re-checks of workloads whose leaves an
+    earlier admission touched) against the oracle session: find every
+    workload, admit in order the ones that found an assignment, find again."""
+    snap_doc, wls = synth.config_c2(n_workloads=n, shape=shape)
+    snap = make(snap_doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    b1 = snap.last_results()
+    admitted, deltas = snap.admit(snap.last_assignments())
+    snap.run_compiled()
+    b2 = snap.last_results()
+    snap.close()
+    ops = [{"op": "find", "podSets": w} for w in wls]
+    admit_idx = [i for i, w in enumerate(wls) if all(not r["reason"] for r in b1[i])]
+    ops += [{"op": "admit", "usage": synth.usage_records(wls[i], b1[i])} for i in admit_idx]
+    ops += [{"op": "find", "podSets": w} for w in wls]
+    res = oracle_lib.session(snap_doc, ops)
+    assert b1 == res[:n]
+    want = dict(zip(admit_idx, res[n:n + len(admit_idx)]))
+    got = {int(i): bool(a) for i, a in admitted.tolist()}
+    assert {i: got[i] for i in want} == want
+    assert all(not got[i] for i in range(n) if i not in want)
+    assert any(want.values()) and not all(want.values())
+    assert b2 == res[n + len(admit_idx):]
+
+
+def test_emulated_admit_batch(emu_lib):  # noqa: F811
+    _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+
+
+@pytest.mark.gpu
+def test_admit_batch_on_gpu():
+    _admit_batch(lambda d: TASFlavorSnapshot(d), n=256, shape=(2, 4, 8, 16))
