@@ -700,7 +700,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_out = al(up_bytes);
   const size_t nwords = (size_t(c->snap.N) + 31) / 32;
   const bool lds_bits = nwords * 4 <= 64 * 1024;
-  const size_t o_bits = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
+  const size_t o_recs = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
+  const size_t o_bits = o_recs + al(n * sizeof(AdmitRec));
   HIPCHK(c, c->d_fits.ensure(o_bits + (lds_bits ? 0 : nwords * 4)));
   HIPCHK(c, c->h_stage.ensure(up_bytes));
   uint8_t* h = c->h_stage.p;
@@ -721,12 +722,14 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   if (n) {
     hipLaunchKernelGGL(admit_fit0_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->snap,
                        c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
-                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), reinterpret_cast<int32_t*>(d + o_fit0),
+                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), exact ? int64_t(0) : int64_t(total),
+                       reinterpret_cast<int32_t*>(d + o_fit0), reinterpret_cast<AdmitRec*>(d + o_recs),
                        reinterpret_cast<int32_t*>(d + o_exact));
     HIPCHK(c, hipGetLastError());
   }
   hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
-                     c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
+                     c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
+                     reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
                      pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
                      reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   HIPCHK(c, hipGetLastError());

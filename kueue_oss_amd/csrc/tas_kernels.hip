@@ -3754,43 +3754,88 @@ __device__ __forceinline__ bool admit_record_fits(const DevSnap& s, const int64_
   return (any ? result : 0) >= r.count;
 }
 
+// One admission record as phase 1 leaves it for the in-order pass: the
+// record's terms with, per term, the largest tasUsage at which it still fits
+// (`lim` = free - count x value: CountIn(free - usage) >= count <=> usage <=
+// lim for every term once nothing wraps and no quotient leaves int32, which
+// phase 1 verifies for the whole call, else `exact`).
+struct AdmitRec {
+  int32_t leaf, count;
+  int32_t status;  // kAdmitCheck / kAdmitAlways / kAdmitNever / kAdmitWide
+  int32_t nt;
+  int32_t col[kAdmitTerms];
+  int64_t val[kAdmitTerms];
+  int64_t lim[kAdmitTerms];
+};
+constexpr int32_t kAdmitCheck = 0;   // fits now; re-check (usage <= lim) once its leaf is touched
+constexpr int32_t kAdmitAlways = 1;  // count <= 0: CountIn >= 0 >= count
+constexpr int32_t kAdmitNever = 2;   // does not fit now, so never later in the call (usage only grows)
+constexpr int32_t kAdmitWide = 3;    // more than kAdmitTerms terms: generic re-check
+
 // Phase 1 (parallel over every record of the call): the record's fit
 // against the usage at the start of the call; a workload with a record that
-// does not fit then cannot fit after more usage is added (CountIn is
-// monotone in the usage while nothing wraps: `exact` = 1 when a capacity or
-// usage value is large enough that it might, and the sequential pass then
-// re-checks everything).
+// does not fit cannot fit after more usage is added.  `exact` = 1 when the
+// shortcuts do not hold for some record (a capacity, usage or count x value
+// of 2^61 or more, a quotient outside int32 at the start or after the call's
+// total additions `total`); the in-order pass then re-checks everything.
 __global__ __launch_bounds__(256) void admit_fit0_kernel(DevSnap s, const int64_t* tas_usage,
                                                          const uint32_t* usage_present, const kueue_tas_fits_req* reqs,
                                                          const kueue_tas_fits_term* terms, const int32_t* rec_wl, int n,
-                                                         int32_t* wl_fit0, int32_t* exact) {
+                                                         int64_t total, int32_t* wl_fit0, AdmitRec* recs,
+                                                         int32_t* exact) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const kueue_tas_fits_req r = reqs[i];
-  if (!admit_record_fits(s, tas_usage, usage_present, r, terms)) atomicAnd(wl_fit0 + rec_wl[i], 0);
-  if (r.leaf < 0 || r.leaf >= s.N) return;
+  const bool fits = admit_record_fits(s, tas_usage, usage_present, r, terms);
+  if (!fits) atomicAnd(wl_fit0 + rec_wl[i], 0);
+  AdmitRec a;
+  a.leaf = r.leaf;
+  a.count = r.count;
+  a.nt = r.num_terms;
+  a.status = r.count <= 0 ? kAdmitAlways : !fits ? kAdmitNever : r.num_terms > kAdmitTerms ? kAdmitWide : kAdmitCheck;
+  bool bad = false;
   constexpr int64_t kBig = int64_t(1) << 61;
-  bool big = false;
-  for (int k = 0; k < r.num_terms; k++) {
-    const int c = terms[r.term_begin + k].col;
-    if (c < 0) continue;
-    const int64_t f = s.free_cap[int64_t(c) * s.N + r.leaf], u = tas_usage[int64_t(c) * s.N + r.leaf];
-    big |= f >= kBig || f <= -kBig || u >= kBig || u <= -kBig;
+#pragma unroll
+  for (int u = 0; u < kAdmitTerms; u++) {
+    a.col[u] = -1;
+    a.val[u] = 0;
+    a.lim[u] = 0;
+    if (u < r.num_terms && r.leaf >= 0 && r.leaf < s.N) {
+      const kueue_tas_fits_term t = terms[r.term_begin + u];
+      a.col[u] = t.col;
+      a.val[u] = t.value;
+      if (a.status == kAdmitCheck && t.col >= 0 && t.value > 0) {
+        const int64_t f = s.free_cap[int64_t(t.col) * s.N + r.leaf], us = tas_usage[int64_t(t.col) * s.N + r.leaf];
+        bad |= f >= kBig || f <= -kBig || us >= kBig || us <= -kBig || t.value > kBig / r.count;
+        if (!bad) {
+          const int64_t q0 = (f - us) / t.value, q1 = (f - us - total) / t.value;
+          bad |= q0 >= (int64_t(1) << 31) || q1 <= -(int64_t(1) << 31);
+          a.lim[u] = f - int64_t(r.count) * t.value;
+        }
+      }
+    }
   }
-  if (big) atomicOr(exact, 1);
+  recs[i] = a;
+  if (bad) atomicOr(exact, 1);
 }
 
 // Phase 2: one wave walks the workloads in order (the dependency chain), its
 // lanes splitting a workload's records.  A workload whose phase-1 fit failed
-// is rejected at once; one that fitted is re-checked against the current
-// usage only when an earlier workload of this call was admitted onto one of
-// its leaves (`touched`, one bit per leaf, in LDS when it fits).  Admission
-// adds the usage with returning atomics whose values the wave consumes, so
-// they have completed before a later re-check's L1-bypassing loads issue (no
-// __threadfence: that costs microseconds per call on gfx950).
+// is rejected at once; one that fitted is re-checked (usage <= lim, with
+// L1-bypassing loads) only on the leaves an earlier workload of this call was
+// admitted onto (`touched`, one bit per leaf, in LDS when it fits).  The
+// next candidate's first 64 records are fetched while the current one is
+// decided.  Admission adds the usage with returning atomics (all issued, then
+// consumed), so they have completed before a later re-check's loads issue
+// (no __threadfence: that costs microseconds per call on gfx950).
+__device__ __forceinline__ bool admit_touched(const uint32_t* lds, const uint32_t* glob, bool in_lds, int32_t leaf) {
+  const uint32_t word = in_lds ? lds[leaf >> 5] : load_l2(glob + (leaf >> 5));
+  return (word >> (leaf & 31)) & 1u;
+}
+
 __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage, uint32_t* usage_present,
                                                    const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
-                                                   const int64_t* wl_off, int n_wl, int pods_col,
+                                                   const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
                                                    const int32_t* wl_fit0, const int32_t* exact_flag,
                                                    uint32_t* touched_global, int touched_in_lds, int32_t* admitted) {
   extern __shared__ uint32_t touched_lds[];
@@ -3800,76 +3845,107 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
     wave_sync();
   }
   const bool exact = *exact_flag != 0;
+  const bool in_lds = touched_in_lds != 0;
   unsigned long long sink = 0;
+  AdmitRec nxt;
+  int nxt_w = -1;
   for (int w0 = 0; w0 < n_wl; w0 += kWave) {
     // 64 workloads' phase-1 results and offsets per load
     const int wl = min(w0 + lane, n_wl - 1);
-    const int32_t my_fit0 = wl_fit0[wl];
+    const bool my_cand = wl_fit0[wl] != 0 || exact;
     const int64_t my_r0 = wl_off[wl], my_r1 = wl_off[wl + 1];
+    const uint64_t cands = ballot(my_cand && w0 + lane < n_wl);
     const int wend = min(w0 + kWave, n_wl);
     for (int w = w0; w < wend; w++) {
-      const int32_t fit0 = __shfl(my_fit0, w - w0, 64);
-      const int64_t r0 = int64_t(shfl_u64(uint64_t(my_r0), w - w0)), r1 = int64_t(shfl_u64(uint64_t(my_r1), w - w0));
-      if (!fit0 && !exact) {
+      if (!((cands >> (w - w0)) & 1ull)) {
         if (lane == 0) admitted[w] = 0;
         continue;
       }
-      bool recheck = exact;
-      for (int64_t base = r0; base < r1 && !recheck; base += kWave) {
-        const int64_t i = base + lane;
-        bool hit = false;
-        if (i < r1) {
-          const int32_t leaf = reqs[i].leaf;
-          if (leaf >= 0 && leaf < s.N) {
-            const uint32_t word = touched_in_lds ? touched_lds[leaf >> 5] : load_l2(touched_global + (leaf >> 5));
-            hit = (word >> (leaf & 31)) & 1u;
-          }
-        }
-        recheck = ballot(hit) != 0;
+      const int64_t r0 = int64_t(shfl_u64(uint64_t(my_r0), w - w0)), r1 = int64_t(shfl_u64(uint64_t(my_r1), w - w0));
+      AdmitRec cur;
+      if (nxt_w == w) cur = nxt;
+      else if (r0 + lane < r1) cur = recs[r0 + lane];
+      // fetch the next candidate of this block while this one is decided
+      const uint64_t later = (w - w0 + 1 < kWave) ? cands & (~0ull << (w - w0 + 1)) : 0ull;
+      nxt_w = -1;
+      if (later) {
+        const int nw = w0 + __builtin_ctzll(later);
+        const int64_t n0 = int64_t(shfl_u64(uint64_t(my_r0), nw - w0)), n1 = int64_t(shfl_u64(uint64_t(my_r1), nw - w0));
+        if (n0 + lane < n1) nxt = recs[n0 + lane];
+        nxt_w = nw;
       }
       bool all_fit = true;
-      if (recheck) {
-        for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
-          const int64_t i = base + lane;
-          bool fit = true;
-          if (i < r1) fit = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
-          all_fit = ballot(!fit) == 0;
+      for (int64_t base = r0; base < r1 && all_fit; base += kWave) {
+        const int64_t i = base + lane;
+        bool fit = true;
+        if (i < r1) {
+          const AdmitRec a = base == r0 ? cur : recs[i];
+          if (exact || a.status == kAdmitWide) {
+            fit = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+          } else if (a.status == kAdmitNever) {
+            fit = false;
+          } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
+            int64_t us[kAdmitTerms];
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++)
+              us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++) fit &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
+          }
         }
+        all_fit = ballot(!fit) == 0;
       }
       if (lane == 0) admitted[w] = all_fit ? 1 : 0;
       if (!all_fit) continue;
-      for (int64_t i = r0 + lane; i < r1; i += kWave) {
+      for (int64_t base = r0; base < r1; base += kWave) {
+        const int64_t i = base + lane;
+        if (i >= r1) continue;
         const kueue_tas_fits_req r = reqs[i];
         uint32_t bits = 0;
-        int32_t col[kAdmitTerms];
-        int64_t val[kAdmitTerms];
         for (int k0 = 0; k0 < r.num_terms; k0 += kAdmitTerms) {
+          int32_t col[kAdmitTerms];
+          int64_t val[kAdmitTerms];
+          unsigned long long ret[kAdmitTerms];
+          if (k0 == 0 && base == r0 && !exact && cur.status != kAdmitWide) {
 #pragma unroll
-          for (int u = 0; u < kAdmitTerms; u++) {
-            col[u] = -1;
-            val[u] = 0;
-            if (k0 + u < r.num_terms) {
-              const kueue_tas_fits_term t = terms[r.term_begin + k0 + u];
-              col[u] = t.col;
-              val[u] = t.value;
+            for (int u = 0; u < kAdmitTerms; u++) {
+              col[u] = cur.col[u];
+              val[u] = cur.val[u];
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++) {
+              col[u] = -1;
+              val[u] = 0;
+              if (k0 + u < r.num_terms) {
+                const kueue_tas_fits_term t = terms[r.term_begin + k0 + u];
+                col[u] = t.col;
+                val[u] = t.value;
+              }
             }
           }
 #pragma unroll
           for (int u = 0; u < kAdmitTerms; u++) {
-            if (col[u] < 0) continue;  // the host gives every usage resource a column first
-            sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(col[u]) * s.N + r.leaf),
-                              (unsigned long long)(uint64_t(val[u]) * uint64_t(int64_t(r.count))));
-            bits |= 1u << col[u];
+            ret[u] = 0;
+            if (col[u] >= 0) {  // the host gives every usage resource a column first
+              ret[u] = atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(col[u]) * s.N + r.leaf),
+                                 (unsigned long long)(uint64_t(val[u]) * uint64_t(int64_t(r.count))));
+              bits |= 1u << col[u];
+            }
           }
+#pragma unroll
+          for (int u = 0; u < kAdmitTerms; u++) sink += ret[u];
         }
+        unsigned long long rp = 0, rb;
         if (pods_col >= 0) {
-          sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
-                            (unsigned long long)int64_t(r.count));
+          rp = atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                         (unsigned long long)int64_t(r.count));
           bits |= 1u << pods_col;
         }
-        sink += atomicOr(usage_present + r.leaf, bits);
-        if (touched_in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
-        else sink += atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+        rb = atomicOr(usage_present + r.leaf, bits);
+        if (in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+        else rb += atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+        sink += rp + rb;
       }
       wave_sync();
     }
