@@ -675,18 +675,18 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   // every capacity and usage value below 2^61, checked on the device, no
   // int64 arithmetic of the call wraps)
   bool exact = false;
-  __int128 total = 0;
+  __int128 total[KUEUE_TAS_MAX_COLS] = {};  // per column: the most usage this call can add
   for (size_t i = 0; i < n && !exact; i++) {
     const kueue_tas_fits_req& r = reqs[i];
     exact = r.count < 0;
     for (int k = 0; k < r.num_terms && !exact; k++) {
-      const int64_t v = terms[r.term_begin + k].value;
-      exact = v < 0;
-      total += __int128(v) * r.count;
+      const kueue_tas_fits_term& t = terms[r.term_begin + k];
+      exact = t.value < 0;
+      if (t.col >= 0 && t.col < KUEUE_TAS_MAX_COLS) total[t.col] += __int128(t.value) * r.count;
     }
-    total += r.count;  // pods
-    exact = exact || total >= (__int128(1) << 61);
+    if (pods_col >= 0) total[pods_col] += r.count;
   }
+  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++) exact = exact || total[k] >= (__int128(1) << 61);
   HIPCHK(c, hipSetDevice(c->device));
   // one pinned upload: records, terms, workload offsets, record -> workload,
   // phase-1 flags (1 = fit) and the exact flag
@@ -696,7 +696,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_recwl = o_off + al((n_wl + 1) * 8);
   const size_t o_fit0 = o_recwl + al(n * 4);
   const size_t o_exact = o_fit0 + al(n_wl * 4);
-  const size_t up_bytes = o_exact + 4;
+  const size_t o_total = o_exact + 256;
+  const size_t up_bytes = o_total + KUEUE_TAS_MAX_COLS * 8;
   const size_t o_out = al(up_bytes);
   const size_t nwords = (size_t(c->snap.N) + 31) / 32;
   const bool lds_bits = nwords * 4 <= 64 * 1024;
@@ -714,6 +715,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   int32_t* fit0 = reinterpret_cast<int32_t*>(h + o_fit0);
   for (size_t w = 0; w < n_wl; w++) fit0[w] = 1;
   *reinterpret_cast<int32_t*>(h + o_exact) = exact ? 1 : 0;
+  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++)
+    reinterpret_cast<int64_t*>(h + o_total)[k] = exact ? 0 : int64_t(total[k]);
   uint8_t* d = c->d_fits.p;
   HIPCHK(c, hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, c->stream));
   if (!lds_bits) HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
@@ -722,7 +725,7 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   if (n) {
     hipLaunchKernelGGL(admit_fit0_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->snap,
                        c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
-                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), exact ? int64_t(0) : int64_t(total),
+                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), reinterpret_cast<const int64_t*>(d + o_total),
                        reinterpret_cast<int32_t*>(d + o_fit0), reinterpret_cast<AdmitRec*>(d + o_recs),
                        reinterpret_cast<int32_t*>(d + o_exact));
     HIPCHK(c, hipGetLastError());

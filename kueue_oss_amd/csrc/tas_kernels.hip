@@ -3777,11 +3777,12 @@ constexpr int32_t kAdmitWide = 3;    // more than kAdmitTerms terms: generic re-
 // does not fit cannot fit after more usage is added.  `exact` = 1 when the
 // shortcuts do not hold for some record (a capacity, usage or count x value
 // of 2^61 or more, a quotient outside int32 at the start or after the call's
-// total additions `total`); the in-order pass then re-checks everything.
+// total additions `total[col]` to the column); the in-order pass then
+// re-checks everything.
 __global__ __launch_bounds__(256) void admit_fit0_kernel(DevSnap s, const int64_t* tas_usage,
                                                          const uint32_t* usage_present, const kueue_tas_fits_req* reqs,
                                                          const kueue_tas_fits_term* terms, const int32_t* rec_wl, int n,
-                                                         int64_t total, int32_t* wl_fit0, AdmitRec* recs,
+                                                         const int64_t* total, int32_t* wl_fit0, AdmitRec* recs,
                                                          int32_t* exact) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -3808,7 +3809,7 @@ __global__ __launch_bounds__(256) void admit_fit0_kernel(DevSnap s, const int64_
         const int64_t f = s.free_cap[int64_t(t.col) * s.N + r.leaf], us = tas_usage[int64_t(t.col) * s.N + r.leaf];
         bad |= f >= kBig || f <= -kBig || us >= kBig || us <= -kBig || t.value > kBig / r.count;
         if (!bad) {
-          const int64_t q0 = (f - us) / t.value, q1 = (f - us - total) / t.value;
+          const int64_t q0 = (f - us) / t.value, q1 = (f - us - total[t.col]) / t.value;
           bad |= q0 >= (int64_t(1) << 31) || q1 <= -(int64_t(1) << 31);
           a.lim[u] = f - int64_t(r.count) * t.value;
         }

@@ -100,16 +100,15 @@ def test_admit_then_rebuild_on_gpu():
     _admit_then_rebuild(lambda d: TASFlavorSnapshot(d))
 
 
-def _admit_batch(make, n=64, shape=(2, 2, 4, 8), tiny_request=False):
+def _admit_batch(make, n=64, shape=(2, 2, 4, 8), huge_memory=False):
     """kueue_tas_host_admit over one evaluated batch (admit_fit0_kernel +
     admit_kernel: phase-1 rejections, re-checks of workloads whose leaves an
     earlier admission touched) against the oracle session: find every
     workload, admit in order the ones that found an assignment, find again."""
     snap_doc, wls = synth.config_c2(n_workloads=n, shape=shape)
-    if tiny_request:  # 1m cpu: the call's total usage over the request leaves int32 (the exact pass)
-        for w in wls[::2]:
-            for ps in w:
-                ps["requests"]["cpu"] = 1
+    if huge_memory:  # capacities of 2^62: the limits' preconditions fail, the exact re-check pass runs
+        for nd in snap_doc["nodes"]:
+            nd["allocatable"]["memory"] = 1 << 62
     snap = make(snap_doc)
     snap.compile(wls)
     snap.run_compiled()
@@ -134,10 +133,10 @@ def _admit_batch(make, n=64, shape=(2, 2, 4, 8), tiny_request=False):
 
 @pytest.mark.parametrize("tiny", [False, True])
 def test_emulated_admit_batch(emu_lib, tiny):  # noqa: F811
-    _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib), tiny_request=tiny)
+    _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib), huge_memory=tiny)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiny", [False, True])
 def test_admit_batch_on_gpu(tiny):
-    _admit_batch(lambda d: TASFlavorSnapshot(d), n=256, shape=(2, 4, 8, 16), tiny_request=tiny)
+    _admit_batch(lambda d: TASFlavorSnapshot(d), n=256, shape=(2, 4, 8, 16), huge_memory=tiny)
