@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KUEUE_TAS_ABI_VERSION 2
+#define KUEUE_TAS_ABI_VERSION 3
 #define KUEUE_TAS_MAX_LEVELS 16    /* topology_types.go:114 (<=16 levels) */
 #define KUEUE_TAS_MAX_COLS 32      /* resource columns per snapshot */
 #define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs per request */
@@ -96,6 +96,7 @@ typedef struct {
 #define KUEUE_TAS_F_LEADER 16u        /* leaderTasPodSetRequests != nil */
 #define KUEUE_TAS_F_MULTILAYER 32u    /* len(multiLayerConstraints) > 0 :873-875 */
 #define KUEUE_TAS_F_AFFINITY 64u      /* requirements.affinitySelector != nil :889-897 (hostname leaves) */
+#define KUEUE_TAS_F_DOMAIN 128u       /* requiredReplacementDomain != "" (node replacement, :614-678) */
 
 typedef struct {
   uint32_t flags;
@@ -121,6 +122,9 @@ typedef struct {
   int32_t assumed_end;
   int32_t affinity_begin;         /* with KUEUE_TAS_F_AFFINITY: [begin,end) into the batch affinity */
   int32_t affinity_end;           /*   requirements; an empty range matches no leaf */
+  int32_t domain_begin;           /* with KUEUE_TAS_F_DOMAIN: only leaves [begin, end) take part */
+  int32_t domain_end;             /*   (belongsToRequiredDomain :1649-1656); the others count as
+                                     ExclusionStats.TopologyDomain (:1613-1617) */
 } kueue_tas_eval_req;
 
 /* One compiled requirement of required node affinity

@@ -784,6 +784,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
             return fail(c, KUEUE_TAS_EINVAL, "affinity values not sorted");
       }
     }
+    if ((r.flags & KUEUE_TAS_F_DOMAIN) &&
+        (r.domain_begin < 0 || r.domain_end < r.domain_begin || r.domain_end > s.N))
+      return fail(c, KUEUE_TAS_EINVAL, "required domain leaf range");
     nterms += size_t(r.num_req + r.num_leader_req);
     maxt = std::max(maxt, std::max(r.num_req, r.num_leader_req));
   }
@@ -822,6 +825,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     e.assumed_end = r.assumed_end;
     e.aff_begin = r.affinity_begin;
     e.aff_end = r.affinity_end;
+    e.dom_begin = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_begin : -1;
+    e.dom_end = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_end : -1;
     e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
     for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
       e.layer_level[k] = r.layer_level[k];
@@ -918,6 +923,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     add(uint64_t(uint32_t(e.slice_size)) | (uint64_t(uint32_t(e.slice_level)) << 32));
     for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) add(uint64_t(uint32_t(e.ssal[l])));
     add(uint64_t(uint32_t(e.nsel)));
+    add(uint64_t(uint32_t(e.dom_begin)) | (uint64_t(uint32_t(e.dom_end)) << 32));
     for (int k = 0; k < e.nsel; k++) add(uint64_t(uint32_t(e.sel_col[k])) | (uint64_t(uint32_t(e.sel_val[k])) << 32));
     if (const int32_t* row = taint_row(e))
       for (int p = 0; p < P; p++) add(uint64_t(uint32_t(row[p])));
@@ -934,6 +940,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   };
   auto same_mask = [&](const DevEval& x, const DevEval& y) {
     if (x.slice_size != y.slice_size || x.slice_level != y.slice_level || x.nsel != y.nsel) return false;
+    if (x.dom_begin != y.dom_begin || x.dom_end != y.dom_end) return false;
     for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++)
       if (x.ssal[l] != y.ssal[l]) return false;
     for (int k = 0; k < x.nsel; k++)
@@ -1108,7 +1115,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
-  const size_t stats_len = n * nt + n * size_t(s.R) + 2 * n;  // taints | resources | nodeSelector | affinity
+  const size_t stats_len = n * nt + n * size_t(s.R) + 3 * n;  // taints | resources | nodeSelector | affinity | topologyDomain
   const size_t res_off_stats = (n * sizeof(kueue_tas_eval_out) + 15) / 16 * 16;
   const size_t res_bytes = res_off_stats + stats_len * 4;
   HIPCHK(c, c->d_res.ensure(res_bytes));
@@ -1202,6 +1209,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.res_counts = d_stats + n * nt;
   b.sel_counts = d_stats + n * nt + n * size_t(s.R);
   b.aff_counts = b.sel_counts + n;
+  b.dom_counts = b.aff_counts + n;
   b.out = d_out;
   b.entries = c->ent_dev + c->ent_used;
   b.entry_cap = entry_cap;
@@ -1366,6 +1374,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     for (size_t i = 0; i < n; i++) {
       out[i].excl_selector = sel[i];
       out[i].excl_affinity = sel[n + i];
+      out[i].excl_topology = sel[2 * n + i];
     }
   }
   if (KTAS_PROFILE) {

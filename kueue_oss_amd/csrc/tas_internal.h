@@ -43,6 +43,8 @@ struct DevEval {
   int32_t assumed_end;
   int32_t aff_begin;      // required node affinity requirements [aff_begin, aff_end) (KUEUE_TAS_F_AFFINITY)
   int32_t aff_end;
+  int32_t dom_begin;      // required replacement domain: leaves [dom_begin, dom_end); dom_begin < 0: none
+  int32_t dom_end;
   int32_t num_layers;
   int32_t layer_level[KUEUE_TAS_MAX_LAYERS];
   int32_t layer_size[KUEUE_TAS_MAX_LAYERS];
@@ -138,6 +140,7 @@ struct DevBatch {
   int32_t* res_counts;     // [n][R]
   int32_t* sel_counts;     // [n]
   int32_t* aff_counts;     // [n]
+  int32_t* dom_counts;     // [n] ExclusionStats.TopologyDomain
   kueue_tas_eval_out* out; // [n]
   int32_t* entries;        // [n][entry_cap][2]
   int32_t entry_cap;

@@ -173,10 +173,15 @@ __device__ __forceinline__ Key key_wl(bool lfc, int32_t ls, int32_t sswl, int32_
 constexpr int kFillThreads = 256;
 constexpr int kEvalsPerBlock = 16;
 
-enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3, EX_AFFINITY = 4 };
+enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3, EX_AFFINITY = 4, EX_TOPOLOGY = 5 };
 // ExclusionStats slots of the LDS / per-block partials: [0] nodeSelector,
-// [1] affinity, then one per taint string, then one per resource column.
-constexpr int kStatFixed = 2;
+// [1] affinity, [2] topologyDomain, then one per taint string, then one per
+// resource column.
+constexpr int kStatFixed = 3;
+// belongsToRequiredDomain (:1649-1656) on every leaf, after the hostname-only
+// filters (:1613-1617): the host turns the required domain's DomainID prefix
+// into the leaf range [db, de) (db < 0: no required domain).
+__device__ __forceinline__ bool outside_domain(int db, int de, int leaf) { return db >= 0 && (leaf < db || leaf >= de); }
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -354,6 +359,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
                             [&](int col) { return s.label_values[int64_t(col) * N + leaf]; }))
           kind = EX_AFFINITY;
       }
+      if (kind == EX_NONE && outside_domain(uni(ev.dom_begin), uni(ev.dom_end), leaf)) kind = EX_TOPOLOGY;
       if (kind == EX_NONE) {
         const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
         uint32_t pres = fp | (sim ? 0u : up);
@@ -435,6 +441,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     if (lane == 0 && selm) atomicAdd(&b.sel_counts[eid], __popcll(selm));
     const uint64_t affm = ballot(kind == EX_AFFINITY);
     if (lane == 0 && affm) atomicAdd(&b.aff_counts[eid], __popcll(affm));
+    const uint64_t domm = ballot(kind == EX_TOPOLOGY);
+    if (lane == 0 && domm) atomicAdd(&b.dom_counts[eid], __popcll(domm));
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
@@ -472,6 +480,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 struct FillEvalParams {
   int32_t eid, taint_off, nsel, slice_size, slice_level, inner;  // inner: ssal of the leaf level
   int32_t aff_begin, aff_end;  // required node affinity requirements; aff_begin < 0: none
+  int32_t dom_begin, dom_end;  // required replacement domain leaf range; dom_begin < 0: none
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
@@ -520,6 +529,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
     P.aff_begin = aff ? ev.aff_begin : -1;
     P.aff_end = aff ? ev.aff_end : -1;
+    P.dom_begin = ev.dom_begin;
+    P.dom_end = ev.dom_end;
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       P.sel_col[k] = ev.sel_col[k];
       P.sel_val[k] = ev.sel_val[k];
@@ -687,6 +698,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         const int ab = uni(P.aff_begin);
         if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(P.aff_end), leaf, label_at)) kind = EX_AFFINITY;
       }
+      if (kind == EX_NONE && outside_domain(uni(P.dom_begin), uni(P.dom_end), leaf)) kind = EX_TOPOLOGY;
       if (kind == EX_NONE) {
         state = state0;
         swl = swl0;
@@ -780,6 +792,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       if (lds_stats) atomicAdd(&sh_stats[e][1], __popcll(affm));
       else atomicAdd(&b.aff_counts[eid], __popcll(affm));
     }
+    const uint64_t domm = ballot(kind == EX_TOPOLOGY);
+    if (lane == 0 && domm) {
+      if (lds_stats) atomicAdd(&sh_stats[e][2], __popcll(domm));
+      else atomicAdd(&b.dom_counts[eid], __popcll(domm));
+    }
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
@@ -821,7 +838,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t sh_toff[kEvalsPerBlock];
   __shared__ int32_t sh_nsel[kEvalsPerBlock];
-  __shared__ int32_t sh_aff[kEvalsPerBlock][2];
+  __shared__ int32_t sh_aff[kEvalsPerBlock][4];  // affinity range, required-domain leaf range
   __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
@@ -836,6 +853,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
     sh_aff[threadIdx.x][0] = aff ? ev.aff_begin : -1;
     sh_aff[threadIdx.x][1] = aff ? ev.aff_end : -1;
+    sh_aff[threadIdx.x][2] = ev.dom_begin;
+    sh_aff[threadIdx.x][3] = ev.dom_end;
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       sh_sel[threadIdx.x][2 * k] = ev.sel_col[k];
       sh_sel[threadIdx.x][2 * k + 1] = ev.sel_val[k];
@@ -895,6 +914,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
         const int ab = uni(sh_aff[e][0]);
         if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(sh_aff[e][1]), leaf, label_at)) kind = EX_AFFINITY;
       }
+      if (kind == EX_NONE && outside_domain(uni(sh_aff[e][2]), uni(sh_aff[e][3]), leaf)) kind = EX_TOPOLOGY;
       if (kind == EX_NONE && lim >= 0) {
         kind = EX_RESOURCE;
         id = lim;
@@ -904,6 +924,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     if (lane == 0 && selm) atomicAdd(&sh_stats[e][0], __popcll(selm));
     const uint64_t affm = ballot(kind == EX_AFFINITY);
     if (lane == 0 && affm) atomicAdd(&sh_stats[e][1], __popcll(affm));
+    const uint64_t domm = ballot(kind == EX_TOPOLOGY);
+    if (lane == 0 && domm) atomicAdd(&sh_stats[e][2], __popcll(domm));
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       const int tid = __shfl(id, __ffsll((unsigned long long)tm) - 1, 64);
@@ -945,6 +967,7 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
       const int d = m < m0 ? eid : b.cls_members[m];
       if (k == 0) b.sel_counts[d] = acc;
       else if (k == 1) b.aff_counts[d] = acc;
+      else if (k == 2) b.dom_counts[d] = acc;
       else if (k < kStatFixed + b.num_taints) b.taint_counts[int64_t(d) * b.num_taints + (k - kStatFixed)] = acc;
       else b.res_counts[int64_t(d) * b.nstat_R + (k - kStatFixed - b.num_taints)] = acc;
     }
@@ -1170,6 +1193,7 @@ __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, c
     if (threadIdx.x == 0) {
       b.sel_counts[dst] = b.sel_counts[src];
       b.aff_counts[dst] = b.aff_counts[src];
+      b.dom_counts[dst] = b.dom_counts[src];
     }
   }
 }
