@@ -332,6 +332,18 @@ const char* kueue_tas_host_last_error(kueue_tas_host* h);
  * *out_json = {"results":[{"name","assignment","reason"}]} (free with kueue_tas_free). */
 int kueue_tas_host_find(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty, char** out_json);
 
+/* FindTopologyAssignmentsForFlavor with WithWorkload (:511-515, :519-594):
+ * workload_json = {"podSets": [...], "unhealthyNodes": [node...],
+ * "podSetAssignments": [{"name", "topologyAssignment": internal
+ * {"levels","domains":[{"values","count"}]} or null}]}.  With unhealthy nodes
+ * every PodSet with an existing assignment is repaired around
+ * unhealthyNodes[0] (findReplacementAssignment :614-656: deleteDomain,
+ * IsTopologyAssignmentStale, requiredReplacementDomain as a required-domain
+ * leaf range (KUEUE_TAS_F_DOMAIN), the slice adjustment, mergeTopologyAssignments);
+ * results carry the merged assignment.  Without unhealthy nodes it is
+ * kueue_tas_host_find. */
+int kueue_tas_host_find_workload(kueue_tas_host* h, const char* workload_json, int32_t simulate_empty, char** out_json);
+
 /* Batched nominate: evaluate every workload of {"workloads":[[podset..],..]}
  * independently against the same snapshot (scheduler.go:583-619). */
 int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, char** out_json);

@@ -2304,6 +2304,294 @@ void kueue_tas_host_destroy(kueue_tas_host* h) { delete h; }
 
 const char* kueue_tas_host_last_error(kueue_tas_host* h) { return h ? h->err.c_str() : "null host"; }
 
+// ---- node replacement (tas_flavor_snapshot.go:546-562, :614-678) ----------
+// utiltas.TopologyAssignment with explicit values (the existing assignment of
+// an admitted workload comes from its status, not from this snapshot).
+struct ExplicitAssignment {
+  std::vector<std::string> levels;
+  std::vector<std::pair<std::vector<std::string>, int32_t>> domains;  // (values, count)
+};
+static std::string join_values(const std::vector<std::string>& v) {  // utiltas.DomainID
+  std::string id;
+  for (size_t k = 0; k < v.size(); k++) {
+    if (k) id += ",";
+    id += v[k];
+  }
+  return id;
+}
+static ExplicitAssignment parse_explicit(const kjson::Node& ta) {
+  ExplicitAssignment a;
+  for (auto& l : ta["levels"].items) a.levels.push_back(l.s());
+  for (auto& d : ta["domains"].items) {
+    std::vector<std::string> vals;
+    for (auto& x : d["values"].items) vals.push_back(x.s());
+    a.domains.emplace_back(std::move(vals), int32_t(d["count"].i64()));
+  }
+  return a;
+}
+struct Replacement {
+  const kueue_tas_host* h;
+  FlavorSnapshot& s;
+  static int32_t go_mod32(int32_t a, int32_t b) {
+    if (b == 0) throw std::runtime_error("panic: runtime error: integer divide by zero");
+    return b == -1 ? 0 : a % b;
+  }
+  static bool slices_requested(const std::optional<TopologyRequest>& tr) {  // :1155-1160
+    return tr && ((tr->sliceRequiredTopology && tr->sliceSize) || !tr->constraints.empty());
+  }
+  static int32_t slice_size(const std::optional<TopologyRequest>& tr) {  // getSliceSizeWithSinglePodAsDefault
+    if (!tr) return 1;
+    if (!tr->constraints.empty()) return tr->constraints[0].size;
+    if (!tr->sliceRequiredTopology) return 1;
+    return tr->sliceSize ? *tr->sliceSize : 0;
+  }
+  // the leaf behind DomainID(values) at the node level (domainsPerLevel[nodeLevel]), or -1
+  int32_t leaf_of(const std::vector<std::string>& values) const {
+    auto it = s.leafById.find(join_values(values));
+    return it == s.leafById.end() ? -1 : it->second;
+  }
+  // domain.id of the leaf's ancestor at `level` (the leaf's own id at the node level)
+  std::string ancestor_id(int32_t leaf, int level) const {
+    if (level == s.L() - 1) return s.leafId[size_t(leaf)];
+    const auto& lv = s.values[size_t(s.L() - 1)][size_t(leaf)];
+    return join_values(std::vector<std::string>(lv.begin(), lv.begin() + level + 1));
+  }
+  // findIncompleteSliceDomain (:760-792); the first qualifying domain in
+  // assignment order (Go ranges over a map: random among several)
+  std::string incomplete_slice_domain(const ExplicitAssignment& ta, int32_t missing, int32_t sliceSize,
+                                      const std::string& topologyKey) const {
+    const int sliceLevel = s.resolve(topologyKey);
+    if (sliceLevel < 0) return "";
+    std::vector<std::string> order;
+    std::map<std::string, int32_t> usage;
+    for (auto& d : ta.domains) {
+      const int32_t leaf = leaf_of(d.first);
+      if (leaf < 0) continue;
+      const std::string id = ancestor_id(leaf, sliceLevel);
+      if (!usage.count(id)) order.push_back(id);
+      usage[id] = int32_t(uint32_t(usage[id]) + uint32_t(d.second));
+    }
+    for (auto& id : order)
+      if (go_mod32(int32_t(uint32_t(usage[id]) + uint32_t(missing)), sliceSize) == 0) return id;
+    return "";
+  }
+  // requiredReplacementDomain (:680-731)
+  std::string required_domain(const TASPodSetRequests& tr, const ExplicitAssignment& ta) const {
+    const std::string* key = s.level_key(tr);
+    if (!key) return "";
+    const int levelIdx = s.resolve(*key);
+    if (levelIdx < 0 || ta.domains.empty()) return "";
+    const auto& req = tr.topologyRequest;
+    const int32_t ss = slice_size(req);
+    if (slices_requested(req) && go_mod32(tr.count, ss) != 0) {
+      const auto& cs = req->constraints;
+      if (cs.size() > 1)
+        for (size_t i = cs.size(); i-- > 0;)
+          if (go_mod32(tr.count, cs[i].size) != 0) return incomplete_slice_domain(ta, tr.count, cs[i].size, cs[i].topology);
+      const std::string sliceKey = req->sliceRequiredTopology ? *req->sliceRequiredTopology
+                                   : !req->constraints.empty() ? req->constraints[0].topology
+                                                               : s.levelKeys.back();
+      return incomplete_slice_domain(ta, tr.count, ss, sliceKey);
+    }
+    if (!(req && req->required)) return "";
+    if (ta.domains[0].first.empty()) return "";
+    const int32_t leaf = leaf_of(ta.domains[0].first);
+    return leaf < 0 ? "" : ancestor_id(leaf, levelIdx);
+  }
+  // belongsToRequiredDomain (:1649-1656) as a leaf index range: the leaves
+  // whose DomainID(levelValues) starts with `id` (lexicographic leaf order
+  // keeps them contiguous; checked)
+  void domain_range(const std::string& id, int32_t* begin, int32_t* end) const {
+    int32_t lo = -1, hi = -1;
+    for (int32_t i = 0; i < s.N(); i++) {
+      const std::string d = join_values(s.values[size_t(s.L() - 1)][size_t(i)]);
+      if (d.compare(0, id.size(), id) != 0) continue;
+      if (lo < 0) lo = i;
+      else if (hi != i) throw std::runtime_error("internal: required replacement domain is not one leaf range");
+      hi = i + 1;
+    }
+    *begin = lo < 0 ? 0 : lo;
+    *end = lo < 0 ? 0 : hi;
+  }
+  // mergeTopologyAssignments (:1796-1826)
+  ExplicitAssignment merge(const ExplicitAssignment& a, const ExplicitAssignment& b) const {
+    std::vector<std::pair<std::string, const std::pair<std::vector<std::string>, int32_t>*>> keyed;
+    for (auto* ta : {&a, &b})
+      for (auto& d : ta->domains) {
+        const int32_t leaf = leaf_of(d.first);
+        if (leaf < 0) throw std::runtime_error("panic: runtime error: invalid memory address or nil pointer dereference");
+        keyed.push_back({join_values(s.values[size_t(s.L() - 1)][size_t(leaf)]), &d});
+      }
+    std::stable_sort(keyed.begin(), keyed.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    ExplicitAssignment out;
+    out.levels = a.levels;
+    for (auto& kd : keyed) {
+      if (!out.domains.empty() && join_values(out.domains.back().first) == join_values(kd.second->first))
+        out.domains.back().second = int32_t(uint32_t(out.domains.back().second) + uint32_t(kd.second->second));
+      else
+        out.domains.push_back(*kd.second);
+    }
+    return out;
+  }
+};
+
+static void emit_explicit(std::string& out, const std::string& name, const std::optional<ExplicitAssignment>& a,
+                          const std::string& reason) {
+  out += "{\"name\":";
+  kjson::write_string(out, name);
+  out += ",\"assignment\":";
+  if (!a) {
+    out += "null";
+  } else {
+    out += "{\"levels\":[";
+    for (size_t l = 0; l < a->levels.size(); l++) {
+      if (l) out += ",";
+      kjson::write_string(out, a->levels[l]);
+    }
+    out += "],\"domains\":[";
+    for (size_t k = 0; k < a->domains.size(); k++) {
+      if (k) out += ",";
+      out += "{\"values\":[";
+      for (size_t j = 0; j < a->domains[k].first.size(); j++) {
+        if (j) out += ",";
+        kjson::write_string(out, a->domains[k].first[j]);
+      }
+      out += "],\"count\":" + std::to_string(a->domains[k].second) + "}";
+    }
+    out += "]}";
+  }
+  out += ",\"reason\":";
+  kjson::write_string(out, reason);
+  out += "}";
+}
+
+// FindTopologyAssignmentsForFlavor with a workload in node replacement
+// (HasUnhealthyNodes, :546-562): per group, per PodSet with an existing
+// assignment, findReplacementAssignment (:614-656) — deleteDomain,
+// IsTopologyAssignmentStale, requiredReplacementDomain, the slice
+// adjustment, one device evaluation of the replacement pods with the
+// required domain's leaf range and the replacements so far as assumed
+// usage, mergeTopologyAssignments.
+static int find_replacement(kueue_tas_host* h, std::vector<TASPodSetRequests>& podsets,
+                            const std::string& unhealthy, const std::map<std::string, ExplicitAssignment>& psa,
+                            std::string* out) {
+  FlavorSnapshot& s = *h->snap;
+  Replacement R{h, s};
+  Workload wl;
+  wl.podsets = podsets;
+  make_groups(wl);
+  std::map<std::pair<int32_t, int32_t>, int64_t> assumed;  // (leaf, column) -> addAssumedUsage
+  std::vector<std::string> results;
+  auto finish = [&]() {
+    *out = "{\"results\":[";
+    for (size_t i = 0; i < results.size(); i++) *out += (i ? "," : "") + results[i];
+    *out += "]}";
+    return 0;
+  };
+  for (auto& g : wl.groups) {
+    for (const TASPodSetRequests* m : g.members) {
+      auto p = psa.find(m->name);
+      if (p == psa.end()) continue;
+      ExplicitAssignment existing = p->second;
+      TASPodSetRequests tr = *m;
+      std::string reason;
+      std::optional<ExplicitAssignment> merged, replacement;
+      try {
+        // deleteDomain (:746-758)
+        int32_t affected = 0;
+        std::vector<std::pair<std::vector<std::string>, int32_t>> kept;
+        for (auto& d : existing.domains) {
+          if (!d.first.empty() && d.first.back() == unhealthy) affected = d.second;
+          else kept.push_back(d);
+        }
+        existing.domains = kept;
+        tr.count = affected;
+        for (auto& d : existing.domains)  // IsTopologyAssignmentStale (:733-743)
+          if (!s.has_domain(join_values(d.first))) {
+            reason = "Cannot replace the node, because the existing topologyAssignment is invalid, as it contains the "
+                     "stale domain " + (d.first.empty() ? std::string() : d.first[0]);
+            break;
+          }
+        if (reason.empty()) {
+          const std::string reqDomain = R.required_domain(tr, existing);
+          TASPodSetRequests trCopy = tr;
+          if (Replacement::slices_requested(tr.topologyRequest) && !reqDomain.empty() &&
+              Replacement::go_mod32(tr.count, Replacement::slice_size(tr.topologyRequest)) != 0) {
+            int32_t effSize = 1;
+            std::optional<std::string> effTopo;
+            const auto& cs = tr.topologyRequest->constraints;
+            for (size_t i = cs.size(); i-- > 0;)
+              if (Replacement::go_mod32(tr.count, cs[i].size) == 0) {
+                effSize = cs[i].size;
+                effTopo = cs[i].topology;
+                break;
+              }
+            trCopy.topologyRequest->constraints.clear();
+            trCopy.topologyRequest->sliceRequiredTopology = effTopo;
+            trCopy.topologyRequest->sliceSize = effSize;
+          }
+          // findTopologyAssignment(trCopy, nil, assumedUsage, false, requiredReplacementDomain)
+          std::vector<Workload> one(1);
+          one[0].podsets.push_back(trCopy);
+          make_groups(one[0]);
+          s.ensure_columns_for(one[0].podsets);
+          GroupEval& ge = one[0].groups[0];
+          s.compile_group(ge, false);
+          if (!reqDomain.empty() && ge.early_reason.empty()) {
+            ge.req.flags |= KUEUE_TAS_F_DOMAIN;
+            R.domain_range(reqDomain, &ge.req.domain_begin, &ge.req.domain_end);
+          }
+          std::vector<Evaluator::Overlay> base(1);
+          for (auto& kv : assumed) base[0].push_back({kv.first.first, kv.first.second, kv.second});
+          Evaluator ev{&s};
+          std::vector<std::vector<PodSetResult>> res;
+          int rc = ev.run(one, false, &res, /*precompiled=*/true, base[0].empty() ? nullptr : &base);
+          if (rc) {
+            h->err = s.err;
+            return rc;
+          }
+          const PodSetResult& r = res[0][0];
+          if (!r.reason.empty()) {
+            reason = r.reason;
+          } else if (!r.has_assignment || r.domains.empty()) {
+            reason = "cannot find replacement assignment for unhealthy node: " + unhealthy;
+          } else {
+            ExplicitAssignment rep;
+            const int L = s.L();
+            const size_t levelIdx = s.lowestIsHostname ? size_t(L - 1) : 0;
+            rep.levels.assign(s.levelKeys.begin() + int64_t(levelIdx), s.levelKeys.end());
+            for (auto& d : r.domains) {
+              const auto& lv = s.values[size_t(L - 1)][size_t(d.leaf)];
+              std::vector<std::string> vals(lv.begin() + int64_t(levelIdx), lv.end());
+              if (s.lowestIsHostname) vals.back() = s.leafId[size_t(d.leaf)];
+              rep.domains.emplace_back(std::move(vals), d.count);
+            }
+            merged = R.merge(rep, existing);
+            replacement = rep;
+          }
+        }
+      } catch (const std::runtime_error& e) {
+        const std::string w = e.what();
+        if (w.rfind("panic: ", 0) != 0) throw;
+        reason = w;
+      }
+      std::string one_out;
+      emit_explicit(one_out, m->name, reason.empty() ? merged : std::nullopt, reason);
+      results.push_back(one_out);
+      if (!reason.empty()) return finish();
+      for (auto& d : replacement->domains) {  // addAssumedUsage (:658-666): single x count, no pods
+        const int32_t leaf = R.leaf_of(d.first);
+        for (auto& kv : m->requestIds) {
+          const int32_t c = s.col_of(kv.first);
+          int64_t& slot = assumed[{leaf, c}];
+          slot = int64_t(uint64_t(slot) + uint64_t(kv.second) * uint64_t(int64_t(d.second)));
+        }
+      }
+    }
+  }
+  return finish();
+}
+
 static int run_workloads(kueue_tas_host* h, std::vector<Workload>& wls, bool sim, std::string* out, bool nested) {
   Evaluator ev{h->snap.get()};
   std::vector<std::vector<PodSetResult>> results;
@@ -2340,6 +2628,42 @@ int kueue_tas_host_find(kueue_tas_host* h, const char* podsets_json, int32_t sim
       return 0;
     }
     std::string out;
+    int rc = run_workloads(h, wls, simulate_empty != 0, &out, false);
+    if (rc) return rc;
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_find_workload(kueue_tas_host* h, const char* workload_json, int32_t simulate_empty, char** out_json) {
+  if (!h || !h->snap || !h->err.empty() || !workload_json || !out_json) return KUEUE_TAS_EINVAL;
+  try {
+    kjson::Node doc = kjson::parse(workload_json);
+    std::vector<TASPodSetRequests> podsets = parse_podsets(doc["podSets"]);
+    std::vector<std::string> unhealthy;
+    for (auto& n : doc["unhealthyNodes"].items) unhealthy.push_back(n.s());
+    std::string out;
+    if (!unhealthy.empty()) {
+      std::map<std::string, ExplicitAssignment> psa;
+      for (auto& p : doc["podSetAssignments"].items)
+        if (!p["topologyAssignment"].null()) psa[p["name"].s()] = parse_explicit(p["topologyAssignment"]);
+      int rc = find_replacement(h, podsets, unhealthy[0], psa, &out);
+      if (rc) return rc;
+      *out_json = dup(out);
+      return 0;
+    }
+    if (h->snap->gates.elastic) {
+      out = "{\"results\":[{\"name\":";
+      kjson::write_string(out, podsets.empty() ? "" : podsets[0].name);
+      out += ",\"assignment\":null,\"reason\":\"unsupported: ElasticJobsViaWorkloadSlicesWithTAS\"}]}";
+      *out_json = dup(out);
+      return 0;
+    }
+    std::vector<Workload> wls(1);
+    wls[0].podsets = std::move(podsets);
     int rc = run_workloads(h, wls, simulate_empty != 0, &out, false);
     if (rc) return rc;
     *out_json = dup(out);

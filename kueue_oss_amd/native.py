@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_deltas", "kueue_tas_host_run", "kueue_tas_build_id",
     "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
-    "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times",
+    "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -139,6 +139,8 @@ def _bind(lib):
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    lib.kueue_tas_host_find_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_find_workload.restype = c.c_int
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
     lib.kueue_tas_host_update_usage.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
     lib.kueue_tas_host_update_usage.restype = c.c_int
@@ -453,6 +455,18 @@ class TASFlavorSnapshot:
         d = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
         if self._lib.kueue_tas_host_apply_deltas(self._h, d.ctypes.data, d.size):
             raise RuntimeError(self._err())
+
+    def find_topology_assignments_for_workload(self, podsets: list, workload: dict = None,
+                                               simulate_empty: bool = False) -> list:
+        """FindTopologyAssignmentsForFlavor(..., WithWorkload(wl)) (tas_flavor_snapshot.go:519):
+        workload = {"unhealthyNodes": [...], "podSetAssignments": [{"name", "topologyAssignment"}]};
+        with unhealthy nodes the PodSets' existing assignments are repaired (node replacement)."""
+        doc = dict(workload or {}, podSets=podsets)
+        out = ctypes.c_void_p()
+        if self._lib.kueue_tas_host_find_workload(self._h, json.dumps(doc).encode(), int(simulate_empty),
+                                                  ctypes.byref(out)):
+            raise RuntimeError(self._err())
+        return _take(self._lib, out)["results"]
 
     # ---- snapshot queries of the scheduler's other callers ----
     def has_level(self, topology_request) -> bool:

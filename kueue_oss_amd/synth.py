@@ -687,3 +687,74 @@ def affinity_case(rng: random.Random, max_nodes: int = 60, invalid_p: float = 0.
             ps["nodeSelector"] = {rng.choice(["-bad", "ok", "a/b/c"]): rng.choice(["v!", "fine", ""])}
     case["name"] = "affinity"
     return case
+
+
+def replacement_case(rng: random.Random, oracle_run) -> dict:
+    """A node-replacement case (FindTopologyAssignmentsForFlavor with a
+    workload whose Status.UnhealthyNodes names a node of its admitted
+    assignment, tas_flavor_snapshot.go:546-562): the PodSets' existing
+    assignments come from evaluating them first (`oracle_run(case)` ->
+    results); the unhealthy node then usually leaves the snapshot
+    (NotReady), sometimes a second assigned node too (a stale assignment),
+    and the admitted usage is sometimes in the snapshot."""
+    four = rng.random() < 0.35
+    levels = ["block", "rack"] + (["switch"] if four else []) + [HOST]
+    nodes = []
+    for b in range(rng.randint(1, 3)):
+        for r in range(rng.randint(1, 3)):
+            for sw in range(rng.randint(1, 2) if four else 1):
+                for k in range(rng.randint(1, 4)):
+                    name = f"b{b}r{r}s{sw}x{k}"
+                    labels = {"block": f"b{b}", "rack": f"b{b}-r{r}", HOST: name}
+                    if four:
+                        labels["switch"] = f"b{b}-r{r}-s{sw}"
+                    nodes.append(_node(name, labels, {"cpu": rng.choice([1000, 2000, 4000, 8000]),
+                                                      "pods": rng.choice([10, 110])}))
+    gates = {"TASMultiLayerTopology": True} if rng.random() < 0.7 else {}
+    podsets = []
+    for k in range(rng.choice([1, 1, 2])):
+        kind = rng.random()
+        kw = {}
+        lvl = rng.choice(levels[:-1])
+        if kind < 0.45:
+            kw["required"] = lvl
+        elif kind < 0.7:
+            kw["preferred"] = lvl
+        elif kind < 0.8:
+            kw["unconstrained"] = True
+        count = rng.choice([1, 2, 3, 4, 6, 8])
+        if kw and rng.random() < 0.6:
+            inner = levels[levels.index(lvl) + 1:]
+            a = rng.choice([1, 2, 4])
+            cons = [{"topology": rng.choice(inner), "size": a}]
+            if len(inner) > 1 and rng.random() < 0.5:
+                li = levels.index(cons[0]["topology"])
+                if li + 1 < len(levels):
+                    cons.append({"topology": rng.choice(levels[li + 1:]), "size": rng.choice([d for d in (1, 2) if a % d == 0])})
+            count = a * rng.randint(1, 4)
+            if rng.random() < 0.5:
+                kw["constraints"] = cons
+            else:
+                kw["slice_topo"], kw["slice_size"] = cons[0]["topology"], a
+        podsets.append(_ps(f"ps{k}", count, {"cpu": rng.choice([500, 1000, 2000])}, implied=not kw, **kw))
+    case = {"name": "replacement", "levels": levels, "nodes": nodes, "pods": [], "tasUsage": [], "nodeLabels": {},
+            "flavorTolerations": [], "featureGates": gates, "podSets": podsets, "simulateEmpty": False}
+    first = oracle_run(case)
+    psa, assigned = [], []
+    for r in first:
+        if r["assignment"]:
+            psa.append({"name": r["name"], "topologyAssignment": r["assignment"]})
+            assigned += [d["values"][-1] for d in r["assignment"]["domains"]]
+    if not assigned:
+        return None
+    unhealthy = rng.choice(assigned) if rng.random() < 0.9 else rng.choice([n["name"] for n in nodes])
+    down = {unhealthy} if rng.random() < 0.85 else set()
+    if rng.random() < 0.1:
+        down.add(rng.choice(assigned))  # a second node gone: the assignment is stale
+    for n in nodes:
+        if n["labels"][HOST] in down:
+            n["conditions"] = [{"type": "Ready", "status": "False"}]
+    if rng.random() < 0.5:  # the admitted usage of the healthy domains is in the snapshot
+        case["tasUsage"] = [u for u in usage_records(podsets, first) if u["values"][-1] not in down]
+    case["workload"] = {"unhealthyNodes": [unhealthy], "podSetAssignments": psa}
+    return case

@@ -213,6 +213,14 @@ struct PodSetRequest {  // TASPodSetRequests (tas_flavor_snapshot.go:356-367)
 struct DomainAssignment { std::vector<std::string> values; int32_t count; };
 struct TopologyAssignment { std::vector<std::string> levels; std::vector<DomainAssignment> domains; };
 struct PodSetResult { std::string name; std::optional<TopologyAssignment> assignment; std::string reason; };
+// The parts of kueue.Workload the flavor search reads (WithWorkload,
+// tas_flavor_snapshot.go:511-515): Status.UnhealthyNodes and the
+// Admission's PodSetAssignments' TopologyAssignment (internal form,
+// utiltas.InternalFrom).
+struct WorkloadInfo {
+  std::vector<std::string> unhealthyNodes;
+  std::map<std::string, std::optional<TopologyAssignment>> psa;  // by PodSet name
+};
 
 struct Gates {  // pkg/features/kube_features.go:445-448 (TASProfileMixed Beta, default on)
   bool profileMixed = true;
@@ -292,6 +300,7 @@ struct Requirements {  // topologyAssignmentPodRequirements :434-443
   std::map<std::string, std::string> selector;  // empty = Everything
   std::optional<k8s::ParsedNodeSelector> affinitySelector;
   bool simulateEmpty = false;
+  std::string requiredReplacementDomain;  // :441
 };
 
 static std::string domain_id(const std::vector<std::string>& v) {  // util/tas/tas.go:29-31
@@ -536,7 +545,12 @@ class Snapshot {
           continue;
         }
       }
-      // requiredReplacementDomain is always "" on this path (node replacement is out of scope)
+      // belongsToRequiredDomain (:1613-1617, :1649-1656): DomainID(levelValues) string prefix
+      if (!rq.requiredReplacementDomain.empty() &&
+          domain_id(leaf->levelValues).compare(0, rq.requiredReplacementDomain.size(), rq.requiredReplacementDomain) != 0) {
+        st.stats.topologyDomain++;
+        continue;
+      }
       Requests remaining = leaf->freeCapacity;
       if (!rq.simulateEmpty) req_sub(remaining, leaf->tasUsage);
       if (rq.assumedUsage) {
@@ -865,10 +879,12 @@ class Snapshot {
   // findTopologyAssignment (:804-999)
   std::string find_topology_assignment(const PodSetRequest& workers, const PodSetRequest* leader,
                                        std::map<std::string, Requests>& assumed, bool simulateEmpty,
-                                       std::map<std::string, TopologyAssignment>* assignments) {
+                                       std::map<std::string, TopologyAssignment>* assignments,
+                                       const std::string& requiredReplacementDomain = "") {
     Requirements rq;
     rq.assumedUsage = &assumed;
     rq.simulateEmpty = simulateEmpty;
+    rq.requiredReplacementDomain = requiredReplacementDomain;
     Params st;
     st.count = workers.count;
     rq.requests = workers.singlePodRequests;
@@ -973,7 +989,145 @@ class Snapshot {
 
   // FindTopologyAssignmentsForFlavor (:519-594) — normal (non-replacement,
   // non-elastic) branch.
-  std::vector<PodSetResult> find_topology_assignments_for_flavor(const std::vector<PodSetRequest>& reqs, bool simulateEmpty) {
+  // ---- node replacement (:614-678, :680-727, :733-792, :1796-1826) ----
+  // IsTopologyAssignmentStale (:736-743)
+  std::pair<bool, std::string> is_topology_assignment_stale(const TopologyAssignment& ta) const {
+    for (auto& d : ta.domains)
+      if (!domains.count(domain_id(d.values))) return {true, d.values.empty() ? "" : d.values[0]};
+    return {false, ""};
+  }
+  // deleteDomain (:746-758): drops the unhealthy node's domains, returns the
+  // pods they held (the last match's count)
+  static int32_t delete_domain(TopologyAssignment& ta, const std::string& node) {
+    int32_t affected = 0;
+    std::vector<DomainAssignment> kept;
+    for (auto& d : ta.domains) {
+      if (!d.values.empty() && d.values.back() == node) affected = d.count;
+      else kept.push_back(d);
+    }
+    ta.domains = kept;
+    return affected;
+  }
+  static bool slices_requested(const std::optional<TopologyRequest>& tr) {  // :1155-1160
+    if (!tr) return false;
+    return (tr->sliceRequiredTopology && tr->sliceSize) || !tr->constraints.empty();
+  }
+  // findIncompleteSliceDomain (:760-792).  Go ranges over a map: with more
+  // than one qualifying domain its choice is random; here (and in the
+  // library) the first qualifying domain in assignment order is taken.
+  std::string find_incomplete_slice_domain(const TopologyAssignment& ta, int32_t missing, int32_t sliceSize,
+                                           const std::string& topologyKey) const {
+    const int sliceLevel = resolve_level_idx(topologyKey);
+    if (sliceLevel < 0) return "";
+    const int nodeLevel = int(levelKeys.size()) - 1;
+    std::vector<std::string> order;
+    std::map<std::string, int32_t> usage;
+    for (auto& d : ta.domains) {
+      auto it = domainsPerLevel[size_t(nodeLevel)].find(domain_id(d.values));
+      if (it == domainsPerLevel[size_t(nodeLevel)].end()) continue;
+      Domain* dom = it->second;
+      for (int i = nodeLevel; i > sliceLevel; i--) dom = dom->parent;
+      if (!usage.count(dom->id)) order.push_back(dom->id);
+      usage[dom->id] = w_add(usage[dom->id], d.count);
+    }
+    if (sliceSize == 0) throw GoPanic("runtime error: integer divide by zero");
+    for (auto& id : order)
+      if (go_mod32(w_add(usage[id], missing), sliceSize) == 0) return id;
+    return "";
+  }
+  static int32_t go_mod32(int32_t a, int32_t b) {
+    if (b == 0) throw GoPanic("runtime error: integer divide by zero");
+    if (b == -1) return 0;
+    return a % b;
+  }
+  // requiredReplacementDomain (:680-731)
+  std::string required_replacement_domain(const PodSetRequest& tr, const TopologyAssignment& ta) const {
+    auto key = level_key_with_implied_fallback(tr);
+    if (!key) return "";
+    const int levelIdx = resolve_level_idx(*key);
+    if (levelIdx < 0) return "";
+    if (ta.domains.empty()) return "";
+    const int32_t sliceSize = slice_size_with_single_pod_default(tr.topologyRequest).first;
+    if (slices_requested(tr.topologyRequest) && go_mod32(tr.count, sliceSize) != 0) {
+      const auto& cs = tr.topologyRequest->constraints;
+      if (cs.size() > 1)
+        for (size_t i = cs.size(); i-- > 0;)
+          if (go_mod32(tr.count, cs[i].size) != 0) return find_incomplete_slice_domain(ta, tr.count, cs[i].size, cs[i].topology);
+      return find_incomplete_slice_domain(ta, tr.count, sliceSize, slice_level_key_with_default(tr.topologyRequest, lowest_level()));
+    }
+    if (!(tr.topologyRequest && tr.topologyRequest->required)) return "";
+    const int nodeLevel = int(levelKeys.size()) - 1;
+    const auto& vals = ta.domains[0].values;
+    if (vals.empty()) return "";
+    auto it = domainsPerLevel[size_t(nodeLevel)].find(domain_id(vals));
+    if (it == domainsPerLevel[size_t(nodeLevel)].end()) return "";
+    Domain* dom = it->second;
+    for (int i = nodeLevel; i > levelIdx; i--) dom = dom->parent;
+    return dom->id;
+  }
+  // mergeTopologyAssignments (:1796-1826): sorted by DomainID of the leaves'
+  // levelValues, adjacent equal DomainIDs merged
+  TopologyAssignment merge_topology_assignments(const TopologyAssignment& a, const TopologyAssignment& b) const {
+    const int nodeLevel = int(levelKeys.size()) - 1;
+    std::vector<std::pair<std::string, const DomainAssignment*>> keyed;
+    for (auto* ta : {&a, &b})
+      for (auto& d : ta->domains) {
+        auto it = domainsPerLevel[size_t(nodeLevel)].find(domain_id(d.values));
+        if (it == domainsPerLevel[size_t(nodeLevel)].end())
+          throw GoPanic("runtime error: invalid memory address or nil pointer dereference");
+        keyed.push_back({domain_id(it->second->levelValues), &d});
+      }
+    std::stable_sort(keyed.begin(), keyed.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    TopologyAssignment out;
+    out.levels = a.levels;
+    for (auto& kd : keyed) {
+      if (!out.domains.empty() && domain_id(out.domains.back().values) == domain_id(kd.second->values))
+        out.domains.back().count = w_add(out.domains.back().count, kd.second->count);
+      else
+        out.domains.push_back(*kd.second);
+    }
+    return out;
+  }
+  // findReplacementAssignment (:614-656): (new assignment, replacement, reason)
+  std::string find_replacement_assignment(PodSetRequest tr, TopologyAssignment existing, const std::string& node,
+                                          std::map<std::string, Requests>& assumed, TopologyAssignment* merged,
+                                          TopologyAssignment* replacement) {
+    tr.count = delete_domain(existing, node);
+    auto stale = is_topology_assignment_stale(existing);
+    if (stale.first)
+      return "Cannot replace the node, because the existing topologyAssignment is invalid, as it contains the stale domain " +
+             stale.second;
+    const std::string reqDomain = required_replacement_domain(tr, existing);
+    PodSetRequest trCopy = tr;
+    const int32_t sliceSize = slice_size_with_single_pod_default(tr.topologyRequest).first;
+    if (slices_requested(tr.topologyRequest) && !reqDomain.empty() && go_mod32(tr.count, sliceSize) != 0) {
+      // the innermost constraint whose size divides the replacement pods
+      int32_t effSize = 1;
+      std::optional<std::string> effTopo;
+      const auto& cs = tr.topologyRequest->constraints;
+      for (size_t i = cs.size(); i-- > 0;)
+        if (go_mod32(tr.count, cs[i].size) == 0) {
+          effSize = cs[i].size;
+          effTopo = cs[i].topology;
+          break;
+        }
+      trCopy.topologyRequest->constraints.clear();
+      trCopy.topologyRequest->sliceRequiredTopology = effTopo;
+      trCopy.topologyRequest->sliceSize = effSize;
+    }
+    std::map<std::string, TopologyAssignment> as;
+    std::string reason = find_topology_assignment(trCopy, nullptr, assumed, false, &as, reqDomain);
+    if (!reason.empty()) return reason;
+    auto it = as.find(tr.name);
+    if (it == as.end() || it->second.domains.empty())
+      return "cannot find replacement assignment for unhealthy node: " + node;
+    *replacement = it->second;
+    *merged = merge_topology_assignments(it->second, existing);
+    return "";
+  }
+
+  std::vector<PodSetResult> find_topology_assignments_for_flavor(const std::vector<PodSetRequest>& reqs, bool simulateEmpty,
+                                                                 const WorkloadInfo* wl = nullptr) {
     std::vector<PodSetResult> result;
     std::map<std::string, Requests> assumed;
     std::vector<std::string> order;
@@ -990,6 +1144,29 @@ class Snapshot {
     };
     for (auto& key : order) {
       auto& trs = grouped[key];
+      if (wl && !wl->unhealthyNodes.empty()) {  // HasUnhealthyNodes: node replacement (:546-562)
+        for (auto* tr : trs) {
+          auto p = wl->psa.find(tr->name);
+          if (p == wl->psa.end() || !p->second) continue;
+          TopologyAssignment merged, replacement;
+          std::string reason;
+          try {
+            reason = find_replacement_assignment(*tr, *p->second, wl->unhealthyNodes[0], assumed, &merged, &replacement);
+          } catch (const GoPanic& e) {
+            reason = std::string("panic: ") + e.what();
+          }
+          if (!reason.empty()) {
+            set_result(tr->name, std::nullopt, reason);
+            return result;
+          }
+          set_result(tr->name, merged, "");
+          for (auto& d : replacement.domains) {  // addAssumedUsage (:658-666)
+            Requests& a = assumed[domain_id(d.values)];
+            req_add(a, req_scaled_up(tr->singlePodRequests, d.count));
+          }
+        }
+        continue;
+      }
       // findLeaderAndWorkers (:596-609)
       const PodSetRequest* leader = nullptr;
       const PodSetRequest* workers = trs[0];
@@ -1110,6 +1287,30 @@ static std::vector<PodSetRequest> parse_podsets(const ojson::Value& arr) {
     out.push_back(std::move(r));
   }
   return out;
+}
+
+static TopologyAssignment parse_assignment(const ojson::Value& v) {  // internal utiltas.TopologyAssignment
+  TopologyAssignment ta;
+  for (auto& l : v.at("levels").a) ta.levels.push_back(l.as_str());
+  for (auto& d : v.at("domains").a) {
+    DomainAssignment da;
+    for (auto& x : d.at("values").a) da.values.push_back(x.as_str());
+    da.count = int32_t(d.at("count").as_int());
+    ta.domains.push_back(std::move(da));
+  }
+  return ta;
+}
+// {"unhealthyNodes": [...], "podSetAssignments": [{"name", "topologyAssignment": internal | null}]}
+static WorkloadInfo parse_workload(const ojson::Value& w) {
+  WorkloadInfo wl;
+  if (auto u = w.get("unhealthyNodes"))
+    for (auto& n : u->a) wl.unhealthyNodes.push_back(n.as_str());
+  if (auto ps = w.get("podSetAssignments"))
+    for (auto& p : ps->a) {
+      const ojson::Value& ta = p.at("topologyAssignment");
+      wl.psa[p.at("name").as_str()] = ta.is_null() ? std::nullopt : std::optional<TopologyAssignment>(parse_assignment(ta));
+    }
+  return wl;
 }
 
 // Build the snapshot exactly like the reference test harness
@@ -1264,7 +1465,9 @@ int tas_oracle_run_case(const char* case_json, char** out_json) {
     ojson::Value c = ojson::parse(case_json);
     auto snap = build_snapshot(c);
     auto reqs = parse_podsets(c.at("podSets"));
-    auto rs = snap->find_topology_assignments_for_flavor(reqs, c.at("simulateEmpty").as_bool());
+    std::optional<WorkloadInfo> wl;
+    if (auto w = c.get("workload")) wl = parse_workload(*w);
+    auto rs = snap->find_topology_assignments_for_flavor(reqs, c.at("simulateEmpty").as_bool(), wl ? &*wl : nullptr);
     out = "{\"results\":";
     emit_results(out, rs);
     out += "}";
