@@ -233,6 +233,30 @@ struct TopologyRequest {  // kueue.PodSetTopologyRequest (apis/kueue/v1beta2/wor
   std::optional<int32_t> sliceSize;
   std::vector<SliceConstraint> constraints;
 };
+// utiltas.TopologyAssignment with explicit values (the existing assignment of
+// an admitted workload comes from its status, not from this snapshot).
+struct ExplicitAssignment {
+  std::vector<std::string> levels;
+  std::vector<std::pair<std::vector<std::string>, int32_t>> domains;  // (values, count)
+};
+static std::string join_values(const std::vector<std::string>& v) {  // utiltas.DomainID
+  std::string id;
+  for (size_t k = 0; k < v.size(); k++) {
+    if (k) id += ",";
+    id += v[k];
+  }
+  return id;
+}
+static ExplicitAssignment parse_explicit(const kjson::Node& ta) {
+  ExplicitAssignment a;
+  for (auto& l : ta["levels"].items) a.levels.push_back(l.s());
+  for (auto& d : ta["domains"].items) {
+    std::vector<std::string> vals;
+    for (auto& x : d["values"].items) vals.push_back(x.s());
+    a.domains.emplace_back(std::move(vals), int32_t(d["count"].i64()));
+  }
+  return a;
+}
 struct TASPodSetRequests {  // tas_flavor_snapshot.go:356-367
   std::string name;
   std::optional<TopologyRequest> topologyRequest;
@@ -245,6 +269,8 @@ struct TASPodSetRequests {  // tas_flavor_snapshot.go:356-367
   std::optional<std::map<std::string, std::string>> nodeSelector;
   // PodSpec affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution (podset.go:104-144)
   std::optional<labelsel::RequiredAffinity> affinity;
+  // PreviousAssignment of an elastic workload slice (:364-366), internal form
+  std::optional<ExplicitAssignment> previousAssignment;
 };
 struct DomainAssignment {
   int32_t leaf;
@@ -1648,6 +1674,8 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
       r.nodeSelector = m;
     }
     r.affinity = parse_required_affinity(ps["affinity"]);
+    if (auto pa = ps.find("previousAssignment"))
+      if (!pa->null()) r.previousAssignment = parse_explicit(*pa);
     out.push_back(std::move(r));
   }
   return out;
@@ -2305,30 +2333,6 @@ void kueue_tas_host_destroy(kueue_tas_host* h) { delete h; }
 const char* kueue_tas_host_last_error(kueue_tas_host* h) { return h ? h->err.c_str() : "null host"; }
 
 // ---- node replacement (tas_flavor_snapshot.go:546-562, :614-678) ----------
-// utiltas.TopologyAssignment with explicit values (the existing assignment of
-// an admitted workload comes from its status, not from this snapshot).
-struct ExplicitAssignment {
-  std::vector<std::string> levels;
-  std::vector<std::pair<std::vector<std::string>, int32_t>> domains;  // (values, count)
-};
-static std::string join_values(const std::vector<std::string>& v) {  // utiltas.DomainID
-  std::string id;
-  for (size_t k = 0; k < v.size(); k++) {
-    if (k) id += ",";
-    id += v[k];
-  }
-  return id;
-}
-static ExplicitAssignment parse_explicit(const kjson::Node& ta) {
-  ExplicitAssignment a;
-  for (auto& l : ta["levels"].items) a.levels.push_back(l.s());
-  for (auto& d : ta["domains"].items) {
-    std::vector<std::string> vals;
-    for (auto& x : d["values"].items) vals.push_back(x.s());
-    a.domains.emplace_back(std::move(vals), int32_t(d["count"].i64()));
-  }
-  return a;
-}
 struct Replacement {
   const kueue_tas_host* h;
   FlavorSnapshot& s;
@@ -2592,6 +2596,177 @@ static int find_replacement(kueue_tas_host* h, std::vector<TASPodSetRequests>& p
   return finish();
 }
 
+// FindTopologyAssignmentsForFlavor with ElasticJobsViaWorkloadSlicesWithTAS
+// (:563-577, tas_elastic_workloads.go:35-127): groups in order, one device
+// evaluation per group with the assumed usage so far as the overlay; a
+// workers PodSet with a (non-stale) previous assignment is placed delta-only
+// (scale up: the previous pods' usage incl. pods:count assumed, only the new
+// pods evaluated, merged with the previous assignment; scale down:
+// TruncateAssignment; same count: the previous assignment).
+static int find_sequential(kueue_tas_host* h, std::vector<TASPodSetRequests>& podsets, bool sim, std::string* out) {
+  FlavorSnapshot& s = *h->snap;
+  Replacement R{h, s};
+  Workload wl;
+  wl.podsets = podsets;
+  make_groups(wl);
+  std::map<std::pair<int32_t, int32_t>, int64_t> assumed;  // (leaf, column) -> usage
+  std::vector<std::pair<std::string, std::string>> results;  // (name, JSON) in set order
+  auto set_result = [&](const std::string& name, const std::optional<ExplicitAssignment>& a, const std::string& reason) {
+    std::string js;
+    emit_explicit(js, name, a, reason);
+    for (auto& r : results)
+      if (r.first == name) {
+        r.second = js;
+        return;
+      }
+    results.emplace_back(name, js);
+  };
+  auto finish = [&]() {
+    *out = "{\"results\":[";
+    for (size_t i = 0; i < results.size(); i++) *out += (i ? "," : "") + results[i].second;
+    *out += "]}";
+    return 0;
+  };
+  auto add_usage = [&](const ExplicitAssignment& a, const TASPodSetRequests& tr, bool pods) {
+    for (auto& d : a.domains) {
+      const int32_t leaf = R.leaf_of(d.first);  // assumed usage of other domains is never read (:1620)
+      if (leaf < 0) continue;
+      for (auto& kv : tr.requestIds) {
+        int64_t& slot = assumed[{leaf, s.col_of(kv.first)}];
+        slot = int64_t(uint64_t(slot) + uint64_t(kv.second) * uint64_t(int64_t(d.second)));
+      }
+      if (pods) {
+        int64_t& slot = assumed[{leaf, s.podsCol}];
+        slot = int64_t(uint64_t(slot) + uint64_t(int64_t(d.second)));
+      }
+    }
+  };
+  const int L = s.L();
+  const size_t levelIdx = s.lowestIsHostname ? size_t(L - 1) : 0;
+  auto explicit_of = [&](const PodSetResult& r) {
+    ExplicitAssignment a;
+    a.levels.assign(s.levelKeys.begin() + int64_t(levelIdx), s.levelKeys.end());
+    for (auto& d : r.domains) {
+      const auto& lv = s.values[size_t(L - 1)][size_t(d.leaf)];
+      std::vector<std::string> vals(lv.begin() + int64_t(levelIdx), lv.end());
+      if (s.lowestIsHostname) vals.back() = s.leafId[size_t(d.leaf)];
+      a.domains.emplace_back(std::move(vals), d.count);
+    }
+    return a;
+  };
+  // findTopologyAssignment(workers, leader, assumedUsage, simulateEmpty, "") on the device
+  auto evaluate = [&](const TASPodSetRequests& workers, const TASPodSetRequests* leader,
+                      std::vector<PodSetResult>* res) -> int {
+    std::vector<Workload> one(1);
+    one[0].podsets.push_back(workers);
+    if (leader) one[0].podsets.push_back(*leader);
+    s.ensure_columns_for(one[0].podsets);
+    one[0].groups.resize(1);
+    GroupEval& g = one[0].groups[0];
+    g.workers = &one[0].podsets[0];
+    g.leader = leader ? &one[0].podsets[1] : nullptr;
+    g.members = {g.workers};
+    if (leader) g.members.push_back(g.leader);
+    s.compile_group(g, sim);
+    std::vector<Evaluator::Overlay> base(1);
+    for (auto& kv : assumed) base[0].push_back({kv.first.first, kv.first.second, kv.second});
+    Evaluator ev{&s};
+    std::vector<std::vector<PodSetResult>> rs;
+    const int rc = ev.run(one, sim, &rs, /*precompiled=*/true, base[0].empty() ? nullptr : &base);
+    if (rc) {
+      h->err = s.err;
+      return rc;
+    }
+    *res = rs[0];
+    return 0;
+  };
+  auto find_in = [](const std::vector<PodSetResult>& rs, const std::string& name) -> const PodSetResult* {
+    for (auto& r : rs)
+      if (r.name == name) return &r;
+    return nullptr;
+  };
+  for (auto& g : wl.groups) {
+    const TASPodSetRequests& workers = *g.workers;
+    const TASPodSetRequests* leader = g.leader;
+    if (s.gates.elastic && workers.previousAssignment) {  // handleElasticWorkload (:35-69)
+      const ExplicitAssignment& prev = *workers.previousAssignment;
+      bool stale = false;
+      for (auto& d : prev.domains) stale = stale || !s.has_domain(join_values(d.first));
+      if (!stale) {
+        int32_t prevCount = 0;
+        for (auto& d : prev.domains) prevCount = int32_t(uint32_t(prevCount) + uint32_t(d.second));
+        if (workers.count > prevCount) {  // handleScaleUp (:72-112)
+          TASPodSetRequests delta = workers;
+          delta.count = int32_t(uint32_t(workers.count) - uint32_t(prevCount));
+          delta.previousAssignment.reset();
+          {  // ComputeUsagePerDomain: per DomainID the last domain's single x count + pods:count
+            std::map<std::string, std::pair<const std::vector<std::string>*, int32_t>> per;
+            for (auto& d : prev.domains) per[join_values(d.first)] = {&d.first, d.second};
+            for (auto& kv : per) {
+              ExplicitAssignment one;
+              one.domains.emplace_back(*kv.second.first, kv.second.second);
+              add_usage(one, workers, true);
+            }
+          }
+          std::vector<PodSetResult> rs;
+          if (int rc = evaluate(delta, leader, &rs)) return rc;
+          const PodSetResult* wr = find_in(rs, workers.name);
+          if (!wr->reason.empty()) {
+            set_result(workers.name, std::nullopt, wr->reason);
+            return finish();
+          }
+          try {
+            set_result(workers.name, R.merge(explicit_of(*wr), prev), "");
+          } catch (const std::runtime_error& e) {
+            set_result(workers.name, std::nullopt, e.what());
+            return finish();
+          }
+          if (leader) {
+            const ExplicitAssignment la = explicit_of(*find_in(rs, leader->name));
+            set_result(leader->name, la, "");
+            add_usage(la, *leader, false);
+          }
+          add_usage(explicit_of(*wr), workers, false);
+        } else if (workers.count < prevCount) {  // handleScaleDown: TruncateAssignment
+          ExplicitAssignment t;
+          t.levels = prev.levels;
+          int32_t remaining = workers.count;
+          for (auto& d : prev.domains) {
+            if (remaining <= 0) break;
+            if (d.second <= remaining) {
+              t.domains.push_back(d);
+              remaining -= d.second;
+            } else {
+              t.domains.emplace_back(d.first, remaining);
+              remaining = 0;
+            }
+          }
+          set_result(workers.name, t, "");
+          add_usage(t, workers, false);
+        } else {
+          set_result(workers.name, prev, "");
+          add_usage(prev, workers, false);
+        }
+        continue;
+      }
+    }
+    std::vector<PodSetResult> rs;
+    if (int rc = evaluate(workers, leader, &rs)) return rc;
+    const std::string reason = find_in(rs, workers.name)->reason;
+    for (const TASPodSetRequests* m : g.members) {
+      const PodSetResult* r = find_in(rs, m->name);
+      if (r && r->has_assignment) set_result(m->name, explicit_of(*r), reason);
+      else set_result(m->name, std::nullopt, reason);
+    }
+    if (!reason.empty()) return finish();
+    for (const TASPodSetRequests* m : g.members) {
+      const PodSetResult* r = find_in(rs, m->name);
+      if (r && r->has_assignment) add_usage(explicit_of(*r), *m, false);
+    }
+  }
+  return finish();
+}
+
 static int run_workloads(kueue_tas_host* h, std::vector<Workload>& wls, bool sim, std::string* out, bool nested) {
   Evaluator ev{h->snap.get()};
   std::vector<std::vector<PodSetResult>> results;
@@ -2620,15 +2795,9 @@ int kueue_tas_host_find(kueue_tas_host* h, const char* podsets_json, int32_t sim
   try {
     std::vector<Workload> wls(1);
     wls[0].podsets = parse_podsets(kjson::parse(podsets_json));
-    if (h->snap->gates.elastic) {
-      std::string out = "{\"results\":[{\"name\":";
-      kjson::write_string(out, wls[0].podsets.empty() ? "" : wls[0].podsets[0].name);
-      out += ",\"assignment\":null,\"reason\":\"unsupported: ElasticJobsViaWorkloadSlicesWithTAS\"}]}";
-      *out_json = dup(out);
-      return 0;
-    }
     std::string out;
-    int rc = run_workloads(h, wls, simulate_empty != 0, &out, false);
+    int rc = h->snap->gates.elastic ? find_sequential(h, wls[0].podsets, simulate_empty != 0, &out)
+                                    : run_workloads(h, wls, simulate_empty != 0, &out, false);
     if (rc) return rc;
     *out_json = dup(out);
     return 0;
@@ -2656,9 +2825,8 @@ int kueue_tas_host_find_workload(kueue_tas_host* h, const char* workload_json, i
       return 0;
     }
     if (h->snap->gates.elastic) {
-      out = "{\"results\":[{\"name\":";
-      kjson::write_string(out, podsets.empty() ? "" : podsets[0].name);
-      out += ",\"assignment\":null,\"reason\":\"unsupported: ElasticJobsViaWorkloadSlicesWithTAS\"}]}";
+      int rc = find_sequential(h, podsets, simulate_empty != 0, &out);
+      if (rc) return rc;
       *out_json = dup(out);
       return 0;
     }
@@ -2681,6 +2849,17 @@ int kueue_tas_host_find_batch(kueue_tas_host* h, const char* workloads_json, cha
     std::vector<Workload> wls(doc["workloads"].items.size());
     for (size_t i = 0; i < wls.size(); i++) wls[i].podsets = parse_podsets(doc["workloads"].items[i]);
     std::string out;
+    if (h->snap->gates.elastic) {  // delta placement per workload (find_sequential)
+      out = "{\"results\":[";
+      for (size_t i = 0; i < wls.size(); i++) {
+        std::string one;
+        if (int rc = find_sequential(h, wls[i].podsets, false, &one)) return rc;
+        // {"results":[...]} -> [...]
+        out += (i ? "," : "") + one.substr(11, one.size() - 12);
+      }
+      *out_json = dup(out + "]}");
+      return 0;
+    }
     int rc = run_workloads(h, wls, false, &out, true);
     if (rc) return rc;
     *out_json = dup(out);

@@ -758,3 +758,34 @@ def replacement_case(rng: random.Random, oracle_run) -> dict:
         case["tasUsage"] = [u for u in usage_records(podsets, first) if u["values"][-1] not in down]
     case["workload"] = {"unhealthyNodes": [unhealthy], "podSetAssignments": psa}
     return case
+
+
+def elastic_case(rng: random.Random, oracle_run) -> dict:
+    """An elastic workload-slice case (ElasticJobsViaWorkloadSlicesWithTAS,
+    tas_elastic_workloads.go:35-127): a random case whose PodSets were first
+    placed (`oracle_run(case)` with the gate off) and now ask for more, fewer
+    or the same pods with that placement as PreviousAssignment; sometimes a
+    node of it has left the snapshot (stale: fresh placement)."""
+    while True:
+        case = random_case(rng, max_nodes=40)
+        case["featureGates"] = dict(case["featureGates"])
+        case["featureGates"].pop("ElasticJobsViaWorkloadSlicesWithTAS", None)
+        first = oracle_run(case)
+        placed = {r["name"]: r["assignment"] for r in first if r["assignment"] and r["assignment"]["domains"]}
+        if placed:
+            break
+    for ps in case["podSets"]:
+        a = placed.get(ps["name"])
+        if a is None or rng.random() < 0.15:
+            continue
+        ps["previousAssignment"] = a
+        prev = sum(d["count"] for d in a["domains"])
+        ps["count"] = max(0, prev + rng.choice([-3, -1, 0, 0, 1, 2, 4, 8]))
+    if rng.random() < 0.1:  # a previously used node leaves: stale, fresh placement
+        used = {d["values"][-1] for a in placed.values() for d in a["domains"]}
+        for n in case["nodes"]:
+            if n["labels"].get(HOST) in used:
+                n["conditions"] = [{"type": "Ready", "status": "False"}]
+                break
+    case["featureGates"]["ElasticJobsViaWorkloadSlicesWithTAS"] = True
+    return case

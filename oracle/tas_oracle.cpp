@@ -29,8 +29,10 @@
 //   * Requests maps iterate in sorted key order (std::map).
 //   * ValidatedSelectorFromSet with >=2 invalid entries reports the first in
 //     Go map order (random); we report the smallest key's (k8s_selectors.h).
+//   * findIncompleteSliceDomain with >=2 qualifying domains returns the
+//     first in Go map order (random); we return the first in assignment order.
 // Out of scope (returns an error reason "unsupported: ..."):
-//   TASBalancedPlacement, elastic workloads, node replacement.
+//   TASBalancedPlacement.
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -212,6 +214,9 @@ struct PodSetRequest {  // TASPodSetRequests (tas_flavor_snapshot.go:356-367)
 };
 struct DomainAssignment { std::vector<std::string> values; int32_t count; };
 struct TopologyAssignment { std::vector<std::string> levels; std::vector<DomainAssignment> domains; };
+// TASPodSetRequests.PreviousAssignment (:364-366) of an elastic workload
+// slice, in internal form (utiltas.InternalFrom of the v1beta2 value)
+struct PreviousAssignments { std::map<std::string, TopologyAssignment> byName; };
 struct PodSetResult { std::string name; std::optional<TopologyAssignment> assignment; std::string reason; };
 // The parts of kueue.Workload the flavor search reads (WithWorkload,
 // tas_flavor_snapshot.go:511-515): Status.UnhealthyNodes and the
@@ -1126,8 +1131,95 @@ class Snapshot {
     return "";
   }
 
+  // ---- elastic workload slices (tas_elastic_workloads.go:35-127) ----
+  struct ElasticResult {
+    bool applied = false;
+    std::vector<PodSetResult> assignments;  // in the order the reference sets them
+  };
+  static int32_t count_pods(const TopologyAssignment& ta) {  // utiltas.CountPodsInAssignment
+    int32_t t = 0;
+    for (auto& d : ta.domains) t = w_add(t, d.count);
+    return t;
+  }
+  static TopologyAssignment truncate_assignment(const TopologyAssignment& ta, int32_t n) {  // TruncateAssignment
+    TopologyAssignment out;
+    out.levels = ta.levels;
+    if (n <= 0) return out;
+    int32_t remaining = n;
+    for (auto& d : ta.domains) {
+      if (remaining <= 0) break;
+      if (d.count <= remaining) {
+        out.domains.push_back(d);
+        remaining -= d.count;
+      } else {
+        out.domains.push_back({d.values, remaining});
+        remaining = 0;
+      }
+    }
+    return out;
+  }
+  static void add_assumed(std::map<std::string, Requests>& assumed, const TopologyAssignment& ta, const PodSetRequest& tr) {
+    for (auto& d : ta.domains) req_add(assumed[domain_id(d.values)], req_scaled_up(tr.singlePodRequests, d.count));
+  }
+  // handleElasticWorkload (:35-69), handleScaleUp (:72-112), handleScaleDown (:115-127)
+  ElasticResult handle_elastic(const PodSetRequest& workers, const PodSetRequest* leader,
+                               const TopologyAssignment* previous, std::map<std::string, Requests>& assumed,
+                               bool simulateEmpty) {
+    ElasticResult r;
+    if (!previous) return r;
+    const TopologyAssignment& prev = *previous;
+    if (is_topology_assignment_stale(prev).first) return r;  // fresh placement
+    r.applied = true;
+    const int32_t prevCount = count_pods(prev);
+    if (workers.count > prevCount) {
+      PodSetRequest delta = workers;
+      delta.count = w_sub(workers.count, prevCount);
+      // ComputeUsagePerDomain (util/tas/tas_assignment.go:305-314): single x count + pods:count, per domain (last wins)
+      std::map<std::string, Requests> prevUsage;
+      for (auto& d : prev.domains) {
+        Requests u = req_scaled_up(workers.singlePodRequests, d.count);
+        req_add(u, Requests{{"pods", int64_t(d.count)}});
+        prevUsage[domain_id(d.values)] = u;
+      }
+      for (auto& kv : prevUsage) req_add(assumed[kv.first], kv.second);
+      std::map<std::string, TopologyAssignment> as;
+      std::string reason;
+      try {
+        reason = find_topology_assignment(delta, leader, assumed, simulateEmpty, &as);
+      } catch (const GoPanic& e) {
+        reason = std::string("panic: ") + e.what();
+      }
+      if (!reason.empty()) {
+        r.assignments.push_back({workers.name, std::nullopt, reason});
+        return r;
+      }
+      TopologyAssignment merged;
+      try {
+        merged = merge_topology_assignments(as[workers.name], prev);
+      } catch (const GoPanic& e) {
+        r.assignments.push_back({workers.name, std::nullopt, std::string("panic: ") + e.what()});
+        return r;
+      }
+      r.assignments.push_back({workers.name, merged, ""});
+      if (leader) {
+        r.assignments.push_back({leader->name, as[leader->name], ""});
+        add_assumed(assumed, as[leader->name], *leader);
+      }
+      add_assumed(assumed, as[workers.name], workers);
+    } else if (workers.count < prevCount) {
+      TopologyAssignment t = truncate_assignment(prev, workers.count);
+      r.assignments.push_back({workers.name, t, ""});
+      add_assumed(assumed, t, workers);
+    } else {
+      r.assignments.push_back({workers.name, prev, ""});
+      add_assumed(assumed, prev, workers);
+    }
+    return r;
+  }
+
   std::vector<PodSetResult> find_topology_assignments_for_flavor(const std::vector<PodSetRequest>& reqs, bool simulateEmpty,
-                                                                 const WorkloadInfo* wl = nullptr) {
+                                                                 const WorkloadInfo* wl = nullptr,
+                                                                 const PreviousAssignments* prevs = nullptr) {
     std::vector<PodSetResult> result;
     std::map<std::string, Requests> assumed;
     std::vector<std::string> order;
@@ -1174,9 +1266,22 @@ class Snapshot {
         leader = trs[1];
         if (leader->count > workers->count) { leader = trs[0]; workers = trs[1]; }
       }
-      if (gates.elastic) {
-        set_result(workers->name, std::nullopt, "unsupported: ElasticJobsViaWorkloadSlicesWithTAS");
-        return result;
+      if (gates.elastic) {  // delta-only placement (:567-576)
+        const TopologyAssignment* prev = nullptr;
+        if (prevs) {
+          auto it = prevs->byName.find(workers->name);
+          if (it != prevs->byName.end()) prev = &it->second;
+        }
+        ElasticResult er = handle_elastic(*workers, leader, prev, assumed, simulateEmpty);
+        if (er.applied) {
+          std::string wreason;
+          for (auto& a : er.assignments) {
+            set_result(a.name, a.assignment, a.reason);
+            if (a.name == workers->name) wreason = a.reason;
+          }
+          if (!wreason.empty()) return result;
+          continue;
+        }
       }
       std::map<std::string, TopologyAssignment> assignments;
       std::string reason;
@@ -1467,7 +1572,12 @@ int tas_oracle_run_case(const char* case_json, char** out_json) {
     auto reqs = parse_podsets(c.at("podSets"));
     std::optional<WorkloadInfo> wl;
     if (auto w = c.get("workload")) wl = parse_workload(*w);
-    auto rs = snap->find_topology_assignments_for_flavor(reqs, c.at("simulateEmpty").as_bool(), wl ? &*wl : nullptr);
+    PreviousAssignments prevs;
+    for (auto& ps : c.at("podSets").a)
+      if (auto pa = ps.get("previousAssignment"))
+        if (!pa->is_null()) prevs.byName[ps.at("name").as_str()] = parse_assignment(*pa);
+    auto rs = snap->find_topology_assignments_for_flavor(reqs, c.at("simulateEmpty").as_bool(), wl ? &*wl : nullptr,
+                                                         &prevs);
     out = "{\"results\":";
     emit_results(out, rs);
     out += "}";

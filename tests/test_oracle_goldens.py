@@ -12,7 +12,7 @@ def test_fixture_inventory():
     from golden_util import load_cases as lc
     allc = lc(scope_in=False)
     assert len(allc) == 104  # 104 named cases in the reference table (:383-6266)
-    assert len(CASES) == 82
+    assert len(CASES) == 86  # + the 4 elastic workload-slice cases (:5524-5733)
     out = [c for c in allc if c["scope"] != "in"]
     assert all(c["scope"].startswith("out:") for c in out)
 

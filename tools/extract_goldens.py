@@ -464,6 +464,11 @@ class Evaluator:
             if fn in ("int32", "int64", "int", "string", "corev1.ResourceName", "kueue.PodSetReference",
                       "kueue.TopologyReference"):
                 return args[0]
+            if fn == "tas.V1Beta2From":
+                # previousAssignment (v1beta2); the fixture keeps the internal
+                # form: InternalFrom(V1Beta2From(x)) == x (pinned by the
+                # encoding goldens, tests/golden/tas_v1beta2_encoding.json)
+                return args[0]
             if fn == "resource.MustParse":
                 return Quantity(args[0])
             if fn == "testingnode.MakeNode":
@@ -519,6 +524,7 @@ FIELD_TYPES = {
         "[]kueue.PodsetSliceRequiredTopologyConstraint",
     ("tas.TopologyAssignment", "Domains"): "[]tas.TopologyDomainAssignment",
     ("PodSetTestCase", "wantAssignment"): "*tas.TopologyAssignment",
+    ("PodSetTestCase", "previousAssignment"): "*tas.TopologyAssignment",
 }
 
 
@@ -592,8 +598,11 @@ def normalise_case(name, line, raw):
             wa = {"levels": wa.get("Levels") or [],
                   "domains": [{"values": d.get("Values") or [], "count": d.get("Count", 0)}
                               for d in (wa.get("Domains") or [])]}
-        if ps.get("previousAssignment") is not None:
-            out["scope"] = "out:elastic (previousAssignment, gate ElasticJobsViaWorkloadSlicesWithTAS)"
+        pa = ps.get("previousAssignment")
+        if pa is not None:
+            pa = {"levels": pa.get("Levels") or [],
+                  "domains": [{"values": d.get("Values") or [], "count": d.get("Count", 0)}
+                              for d in (pa.get("Domains") or [])]}
         pss.append({
             "name": (ps.get("podSetName") or "").lower(),
             "topologyRequest": tr,
@@ -604,12 +613,11 @@ def normalise_case(name, line, raw):
             "podSetGroupName": ps.get("podSetGroupName"),
             "wantAssignment": wa,
             "wantReason": ps.get("wantReason") or "",
+            **({"previousAssignment": pa} if pa is not None else {}),
         })
     out["podSets"] = pss
     if fg.get("TASBalancedPlacement"):
         out["scope"] = "out:balanced placement (alpha gate TASBalancedPlacement; SURVEY §2 row 6)"
-    if fg.get("ElasticJobsViaWorkloadSlicesWithTAS") or fg.get("ElasticJobsViaWorkloadSlices"):
-        out["scope"] = "out:elastic (alpha gate ElasticJobsViaWorkloadSlicesWithTAS; SURVEY §2 row 7)"
     return out
 
 
