@@ -217,6 +217,17 @@ int kueue_tas_snapshot_set_free(kueue_tas_ctx* ctx, const int32_t* leaves, size_
 int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* ctx, const int32_t* leaves, size_t n, const int32_t* profiles,
                                       const int32_t* labels);
 
+/* Take n distinct leaves out of the snapshot (live[i] = 0) or put them back
+ * (live[i] = 1) without changing the tree: the device side of a node that
+ * leaves (NotReady, cordoned, deleted) or returns (nodesCache.sync,
+ * tas_nodes_cache.go:38-50) while its parent keeps another leaf.  A leaf out
+ * of the snapshot takes part in no evaluation (zero counts, no
+ * ExclusionStats, not in Total nodes) and fits nothing; it keeps its rows, so
+ * usage deltas applied meanwhile are there when it returns.  The caller
+ * keeps at least one live leaf under every domain (else it reloads);
+ * kueue_tas_snapshot_load puts every leaf in. */
+int kueue_tas_snapshot_set_leaf_live(kueue_tas_ctx* ctx, const int32_t* leaves, size_t n, const int32_t* live);
+
 /* Evaluate n requests against the resident snapshot.
  *  taint_table:   int32 entries referenced by reqs[i].taint_table (may be NULL if no profiles)
  *  assumed:       overlay records referenced by reqs[i].assumed_begin/end

@@ -154,6 +154,9 @@ struct kueue_tas_ctx {
   int rack_fanout = 0;  // see kueue_tas_snapshot_load
   std::vector<int32_t> h_level_sizes;
   DevBuf<int32_t> d_child_off, d_id_rank, d_taint_profile, d_labels;
+  DevBuf<uint8_t> d_dead;        // leaves out of the snapshot (kueue_tas_snapshot_set_leaf_live)
+  std::vector<uint8_t> h_dead;
+  int64_t n_dead = 0;
   DevBuf<int64_t> d_free, d_usage;
   DevBuf<uint32_t> d_free_present, d_usage_present;
   // batch
@@ -344,6 +347,10 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   s.SD = int32_t(off);
   s.N = d->level_sizes[s.L - 1];
   const size_t N = size_t(s.N);
+  s.leaf_dead = nullptr;  // a load describes live leaves only
+  s.n_live = s.N;
+  c->h_dead.assign(N, 0);
+  c->n_dead = 0;
   // CSR offsets
   size_t nco = 0;
   for (int l = 0; l + 1 < s.L; l++) {
@@ -587,6 +594,30 @@ int kueue_tas_snapshot_set_free(kueue_tas_ctx* c, const int32_t* leaves, size_t 
                      int(n));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_set_leaf_live(kueue_tas_ctx* c, const int32_t* leaves, size_t n, const int32_t* live) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (n == 0) return KUEUE_TAS_OK;
+  if (!leaves || !live) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "leaf out of range");
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t d = live[i] ? 0 : 1;
+    c->n_dead += int64_t(d) - int64_t(c->h_dead[size_t(leaves[i])]);
+    c->h_dead[size_t(leaves[i])] = d;
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  c->snap.n_live = int32_t(int64_t(c->snap.N) - c->n_dead);
+  if (c->n_dead == 0) {
+    c->snap.leaf_dead = nullptr;
+    return KUEUE_TAS_OK;
+  }
+  HIPCHK(c, c->d_dead.ensure(size_t(c->snap.N)));
+  HIPCHK(c, hipMemcpy(c->d_dead.p, c->h_dead.data(), size_t(c->snap.N), hipMemcpyHostToDevice));
+  c->snap.leaf_dead = c->d_dead.p;
   return KUEUE_TAS_OK;
 }
 

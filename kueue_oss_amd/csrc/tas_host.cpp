@@ -358,6 +358,17 @@ class FlavorSnapshot {
   std::vector<std::string> leafId;
   std::unordered_map<std::string, int32_t> leafById;
   std::vector<const NodeInfo*> leafNode;
+  // Leaves whose last node left in place (kueue_tas_snapshot_set_leaf_live):
+  // out of the snapshot until that node returns; every domain above keeps a
+  // live leaf (liveUnder per leaf parent, leaf level L-2; the whole leaf
+  // level for L == 1), so the tree itself never changes in place.
+  std::vector<uint8_t> leafDead;
+  std::vector<int32_t> leafParent, liveUnder;
+  std::unordered_map<std::string, std::pair<int32_t, size_t>> leftNodes;  // node name -> (leaf, nodes[] slot)
+  int32_t live_leaf(const std::string& id) const {
+    auto it = leafById.find(id);
+    return (it == leafById.end() || leafDead[size_t(it->second)]) ? -1 : it->second;
+  }
   std::vector<Requests> freeCap, tasUsage;
   // non-TAS pod cache mirror (tas_non_tas_pod_cache.go:30-120), kept so pod
   // events update leaves in place: allocatable sum and member nodes per leaf
@@ -607,6 +618,17 @@ class FlavorSnapshot {
     for (size_t i = 0; i < nodes.size(); i++) nodeIdx[nodes[i].name] = i;
     leafNodeNames.assign(N, {});
     for (auto& kv : nodeToLeaf) leafNodeNames[leafById[kv.second]].push_back(kv.first);
+    leafDead.assign(size_t(N), 0);
+    leftNodes.clear();
+    leafParent.assign(size_t(N), 0);
+    liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
+    for (int i = 0; i < N; i++) {
+      if (L >= 2) {
+        const auto& co = childOff[size_t(L - 2)];
+        leafParent[size_t(i)] = int32_t(std::upper_bound(co.begin(), co.end(), i) - co.begin()) - 1;
+      }
+      liveUnder[size_t(leafParent[size_t(i)])]++;
+    }
     // DomainID ranks per level (multiLayerNotFitMessage tie-break)
     idRank.assign(L, {});
     for (int l = 0; l < L; l++) {
@@ -745,43 +767,46 @@ class FlavorSnapshot {
   }
 
   // ---- node events (nodesCache.sync, tas_nodes_cache.go:38-72) ----
-  // An update of a node already in the snapshot that keeps it Ready,
-  // schedulable, matching the flavor and at the same topology position, whose
-  // taint list is an existing profile and whose labels use existing label
-  // keys and values, changes only leaf attributes: allocatable (freeCapacity,
-  // addCapacity :243-248), the taint profile and the selector label columns.
-  // Those are applied in place; anything else returns false (the caller
-  // rebuilds the snapshot, as the reference does every cycle).
-  bool node_event_in_place(const kjson::Node& n, std::set<int32_t>* touched) {
-    auto ix = nodeIdx.find(n["name"].s());
-    if (ix == nodeIdx.end()) return false;
-    bool ready, unsched;
-    NodeInfo ni = parse_node(n, &ready, &unsched);
+  // Applied in place when the tree does not change:
+  //  * an update of a node in the snapshot that keeps it a member (Ready,
+  //    schedulable, matching the flavor, every level label) at the same
+  //    topology position, whose taint list is an existing profile and whose
+  //    labels use existing label keys and values: leaf attributes only —
+  //    allocatable (freeCapacity, addCapacity :243-248), taint profile,
+  //    selector label columns;
+  //  * a node leaving the snapshot (NotReady, cordoned, no longer matching):
+  //    its leaf loses its capacity, or, as its last node, leaves the snapshot
+  //    (kueue_tas_snapshot_set_leaf_live) while its parent keeps a live leaf;
+  //  * such a node returning to the same position (the leaf comes back);
+  //  * an event for a node that is not and stays not in the snapshot.
+  // Anything else (a new node, a move, a new taint profile or label value, a
+  // domain losing its last leaf) returns false: the caller rebuilds the
+  // snapshot, as the reference does every cycle.
+  bool member_of(const NodeInfo& ni, bool ready, bool unsched) const {  // nodesCache.find (util/tas/node.go:21-33)
     if (!ready || unsched) return false;
     for (auto& kv : flavorLabels) {
       auto it = ni.labels.find(kv.first);
       if ((it == ni.labels.end() ? std::string() : it->second) != kv.second) return false;
     }
-    NodeInfo& cur = nodes[ix->second];
-    for (auto& l : levelKeys) {
-      auto a = ni.labels.find(l), b = cur.labels.find(l);
-      if (a == ni.labels.end() || b == cur.labels.end() || a->second != b->second) return false;
+    for (auto& l : levelKeys)
+      if (!ni.labels.count(l)) return false;
+    return true;
+  }
+  // taint profile and label ids of `ni` when they already exist (-1: rebuild)
+  int32_t known_attrs(const NodeInfo& ni) const {
+    if (!lowestIsHostname) return 0;
+    std::vector<Taint> ts;
+    for (auto& t : ni.taints)
+      if (t.effect == "NoSchedule" || t.effect == "NoExecute") ts.push_back(t);
+    auto pit = std::find(profiles.begin(), profiles.end(), ts);
+    if (pit == profiles.end()) return -1;
+    for (auto& kv : ni.labels) {
+      auto c = labelCol.find(kv.first);
+      if (c == labelCol.end() || !labelDict[size_t(c->second)].count(kv.second)) return -1;
     }
-    const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
-    int32_t prof = leafProfile[size_t(leaf)];
-    if (lowestIsHostname) {
-      std::vector<Taint> ts;
-      for (auto& t : ni.taints)
-        if (t.effect == "NoSchedule" || t.effect == "NoExecute") ts.push_back(t);
-      auto pit = std::find(profiles.begin(), profiles.end(), ts);
-      if (pit == profiles.end()) return false;
-      prof = int32_t(pit - profiles.begin());
-      for (auto& kv : ni.labels) {
-        auto c = labelCol.find(kv.first);
-        if (c == labelCol.end() || !labelDict[size_t(c->second)].count(kv.second)) return false;
-      }
-    }
-    // in place (the nodesCache record too, for later rebuilds)
+    return int32_t(pit - profiles.begin());
+  }
+  void set_attrs(NodeInfo& cur, NodeInfo&& ni, int32_t leaf, int32_t prof) {
     nodeCache[ni.name] = ni;
     cur.labels = std::move(ni.labels);
     cur.taints = std::move(ni.taints);
@@ -794,11 +819,87 @@ class FlavorSnapshot {
         labelValues[k * N + size_t(leaf)] = it == cur.labels.end() ? 0 : labelDict[k].at(it->second);
       }
     }
+  }
+  void realloc_leaf(int32_t leaf) {
     Requests alloc;
     for (auto& nm : leafNodeNames[size_t(leaf)]) req_add(alloc, nodes[nodeIdx.at(nm)].allocatable);
     leafAlloc[size_t(leaf)] = std::move(alloc);
+  }
+  bool node_event_in_place(const kjson::Node& n, std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
+    bool ready, unsched;
+    NodeInfo ni = parse_node(n, &ready, &unsched);
+    const bool member = member_of(ni, ready, unsched);
+    const int L = this->L();
+    auto ix = nodeIdx.find(ni.name);
+    if (ix == nodeIdx.end()) {
+      if (!member) {  // not in the snapshot before or after
+        sync_node(n);
+        return true;
+      }
+      auto left = leftNodes.find(ni.name);
+      if (left == leftNodes.end()) return false;  // a new node: the tree changes
+      const int32_t leaf = left->second.first;
+      const size_t slot = left->second.second;
+      std::vector<std::string> lv;
+      for (auto& k : levelKeys) lv.push_back(ni.labels.at(k));
+      if (lv != values[size_t(L - 1)][size_t(leaf)]) return false;  // moved
+      if (lowestIsHostname && ni.labels.at(kHostname) != leafId[size_t(leaf)]) return false;
+      const int32_t prof = known_attrs(ni);
+      if (prof < 0) return false;
+      // back in: the node's slot, its leaf (alive again when it was its last node)
+      sync_node(n);
+      nodeIdx[ni.name] = slot;
+      nodeToLeaf[ni.name] = leafId[size_t(leaf)];
+      leafNodeNames[size_t(leaf)].push_back(ni.name);
+      leftNodes.erase(left);
+      set_attrs(nodes[slot], std::move(ni), leaf, prof);
+      if (leafDead[size_t(leaf)]) {
+        leafDead[size_t(leaf)] = 0;
+        liveUnder[size_t(leafParent[size_t(leaf)])]++;
+        liveChanged->insert(leaf);
+      }
+      realloc_leaf(leaf);
+      touched->insert(leaf);
+      return true;
+    }
+    NodeInfo& cur = nodes[ix->second];
+    const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
+    if (!member) {  // leaves the snapshot
+      auto& names = leafNodeNames[size_t(leaf)];
+      if (names.size() == 1) {
+        if (liveUnder[size_t(leafParent[size_t(leaf)])] <= 1) return false;  // its domain would vanish
+        leafDead[size_t(leaf)] = 1;
+        liveUnder[size_t(leafParent[size_t(leaf)])]--;
+        liveChanged->insert(leaf);
+      }
+      names.erase(std::find(names.begin(), names.end(), ni.name));
+      leftNodes[ni.name] = {leaf, ix->second};
+      nodeToLeaf.erase(ni.name);
+      nodeIdx.erase(ix);
+      sync_node(n);
+      realloc_leaf(leaf);
+      touched->insert(leaf);
+      return true;
+    }
+    for (auto& l : levelKeys) {
+      auto a = ni.labels.find(l), b = cur.labels.find(l);
+      if (a == ni.labels.end() || b == cur.labels.end() || a->second != b->second) return false;
+    }
+    const int32_t prof = known_attrs(ni);
+    if (prof < 0) return false;
+    sync_node(n);
+    set_attrs(cur, std::move(ni), leaf, prof);
+    realloc_leaf(leaf);
     touched->insert(leaf);
     return true;
+  }
+  int push_liveness(const std::set<int32_t>& leaves) {
+    if (dirty || !ctx || leaves.empty()) return 0;  // a reload applies leafDead itself
+    std::vector<int32_t> ls(leaves.begin(), leaves.end()), live(ls.size());
+    for (size_t i = 0; i < ls.size(); i++) live[i] = leafDead[size_t(ls[i])] ? 0 : 1;
+    int rc = kueue_tas_snapshot_set_leaf_live(ctx, ls.data(), ls.size(), live.data());
+    if (rc) err = std::string("leaf liveness: ") + kueue_tas_last_error(ctx);
+    return rc;
   }
   // Pushes touched leaves to the device: free-capacity rows (allocatable -
   // non-TAS usage) and, with hostname leaves, taint profile + label columns.
@@ -951,6 +1052,17 @@ class FlavorSnapshot {
       err = std::string("snapshot names: ") + kueue_tas_last_error(ctx);
       return rc;
     }
+    {  // a load puts every leaf in: take the dead ones out again
+      std::vector<int32_t> dl, live;
+      for (int i = 0; i < N; i++)
+        if (leafDead[size_t(i)]) dl.push_back(i);
+      live.assign(dl.size(), 0);
+      rc = dl.empty() ? 0 : kueue_tas_snapshot_set_leaf_live(ctx, dl.data(), dl.size(), live.data());
+      if (rc) {
+        err = std::string("leaf liveness: ") + kueue_tas_last_error(ctx);
+        return rc;
+      }
+    }
     dirty = false;
     return 0;
   }
@@ -1037,7 +1149,7 @@ class FlavorSnapshot {
     std::map<std::pair<int32_t, int32_t>, int64_t> o;
     for (auto& u : us) {
       auto it = leafById.find(u.id);
-      if (it == leafById.end()) continue;
+      if (it == leafById.end() || leafDead[size_t(it->second)]) continue;
       for (auto& kv : u.single) {
         int64_t& slot = o[{it->second, colByName.at(kv.first)}];
         slot = sub64(slot, mul64(kv.second, u.count));
@@ -1057,8 +1169,7 @@ class FlavorSnapshot {
     std::vector<kueue_tas_fits_req> reqs;
     std::vector<kueue_tas_fits_term> terms;
     for (auto& u : us) {
-      auto it = leafById.find(u.id);
-      kueue_tas_fits_req r{it == leafById.end() ? -1 : it->second, u.count, int32_t(terms.size()), 0};
+      kueue_tas_fits_req r{live_leaf(u.id), u.count, int32_t(terms.size()), 0};
       for (auto& kv : u.single) {
         auto c = colByName.find(kv.first);
         terms.push_back({kv.second, c == colByName.end() ? -1 : c->second, 0});
@@ -1415,7 +1526,7 @@ class FlavorSnapshot {
   mutable std::unordered_map<std::string, int32_t> upperDomainIds;  // levels 0..L-2, built on first use
   mutable bool upperBuilt = false;
   bool has_domain(const std::string& id) const {
-    if (leafById.count(id)) return true;
+    if (live_leaf(id) >= 0) return true;
     if (!upperBuilt) {
       upperDomainIds.clear();
       for (int l = 0; l + 1 < L(); l++)
@@ -1463,8 +1574,11 @@ class FlavorSnapshot {
       }
       out += "}";
     };
+    bool firstLeaf = true;
     for (size_t k = 0; k < ord.size(); k++) {
-      if (k) out += ",";
+      if (leafDead[size_t(ord[k])]) continue;  // not a leaf of the snapshot
+      if (!firstLeaf) out += ",";
+      firstLeaf = false;
       labelsel::json_escape(out, leafId[size_t(ord[k])]);
       out += ":{\"freeCapacity\":";
       reqs(freeCap[size_t(ord[k])]);
@@ -2351,8 +2465,7 @@ struct Replacement {
   }
   // the leaf behind DomainID(values) at the node level (domainsPerLevel[nodeLevel]), or -1
   int32_t leaf_of(const std::vector<std::string>& values) const {
-    auto it = s.leafById.find(join_values(values));
-    return it == s.leafById.end() ? -1 : it->second;
+    return s.live_leaf(join_values(values));
   }
   // domain.id of the leaf's ancestor at `level` (the leaf's own id at the node level)
   std::string ancestor_id(int32_t leaf, int level) const {
@@ -3009,15 +3122,22 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
     kjson::Node arr = kjson::parse(nodes_json);
-    std::set<int32_t> touched;
-    bool structural = false;
-    for (auto& n : arr.items)
-      if (!h->snap->node_event_in_place(n, &touched)) {
-        structural = true;
-        break;
-      }
+    std::set<int32_t> touched, liveChanged;
+    size_t k = 0;
+    for (; k < arr.items.size(); k++)
+      if (!h->snap->node_event_in_place(arr.items[k], &touched, &liveChanged)) break;
+    const bool structural = k < arr.items.size();
     if (rebuilt) *rebuilt = structural ? 1 : 0;
-    int rc = structural ? rebuild(h, arr) : h->snap->push_leaves(touched, true);
+    int rc;
+    if (structural) {  // the events applied so far are in the cache state; the rest replay on it
+      kjson::Node rest;
+      rest.type = kjson::Node::kArray;
+      rest.items.assign(arr.items.begin() + int64_t(k), arr.items.end());
+      rc = rebuild(h, rest);
+    } else {
+      rc = h->snap->push_liveness(liveChanged);
+      if (!rc) rc = h->snap->push_leaves(touched, true);
+    }
     if (rc) h->err = h->snap->err;
     return rc;
   } catch (const std::exception& e) {

@@ -72,6 +72,8 @@ struct DevSnap {
   const uint32_t* usage_present;       // [N]
   const int32_t* taint_profile;        // [N] or null
   const int32_t* label_values;         // [K][N] or null
+  const uint8_t* leaf_dead;            // [N] 1: the leaf left the snapshot (kueue_tas_snapshot_set_leaf_live); null: none
+  int32_t n_live;                      // leaves in the snapshot (ExclusionStats.TotalNodes)
 };
 
 // 128-bit lexicographic sort key; lo's low 32 bits hold the domain index in its level.

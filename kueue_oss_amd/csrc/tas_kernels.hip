@@ -173,7 +173,9 @@ __device__ __forceinline__ Key key_wl(bool lfc, int32_t ls, int32_t sswl, int32_
 constexpr int kFillThreads = 256;
 constexpr int kEvalsPerBlock = 16;
 
-enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3, EX_AFFINITY = 4, EX_TOPOLOGY = 5 };
+enum ExclKind : int { EX_NONE = 0, EX_TAINT = 1, EX_SELECTOR = 2, EX_RESOURCE = 3, EX_AFFINITY = 4, EX_TOPOLOGY = 5,
+                      EX_DEAD = 6 };  // EX_DEAD: the leaf is out of the snapshot (counted nowhere)
+__device__ __forceinline__ bool leaf_out(const DevSnap& s, int leaf) { return s.leaf_dead && s.leaf_dead[leaf]; }
 // ExclusionStats slots of the LDS / per-block partials: [0] nodeSelector,
 // [1] affinity, [2] topologyDomain, then one per taint string, then one per
 // resource column.
@@ -336,8 +338,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
     const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     int32_t state = 0, swl = 0, ls = 0;
-    int kind = EX_NONE, id = -1;
-    if (valid) {
+    int kind = (valid && leaf_out(s, leaf)) ? EX_DEAD : EX_NONE, id = -1;
+    if (valid && kind == EX_NONE) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
           int t = b.taint_table[ev.taint_table + prof];
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
     leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
-    if (valid) {
+    if (valid && !leaf_out(s, leaf)) {
       uint32_t pres = fp | (sim ? 0u : up);
       int a_lo = 0, a_hi = 0;
       if (aend > abeg) {
@@ -668,8 +670,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     const int nsel = uni(P.nsel);
     const int32_t slice_size = uni(P.slice_size), slice_level = uni(P.slice_level);
     int32_t state = 0, swl = 0, ls = 0;
-    int kind = EX_NONE, id = -1;
-    if (valid) {
+    int kind = (valid && leaf_out(s, leaf)) ? EX_DEAD : EX_NONE, id = -1;
+    if (valid && kind == EX_NONE) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
           int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(P.taint_off) + prof];
@@ -882,9 +884,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   auto label_at = [s, leaf, lab0, lab1, lab2, lab3](int col) {  // by value: nothing escapes to scratch
     return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
   };
+  const bool dead = valid && leaf_out(s, leaf);
   for (int e = 0; e < ne; e++) {
     int kind = EX_NONE, id = -1;
-    if (valid) {
+    if (valid && !dead) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
           const int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(sh_toff[e]) + prof];
@@ -3361,7 +3364,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   o.fit_level = 0;
   o.num_workers = o.num_leaders = 0;
   o.assignment_nil = 0;
-  o.total_nodes = s.N;
+  o.total_nodes = s.n_live;
   o.excl_selector = 0;  // set by the host from the stats region (counted concurrently, stream3)
   o.excl_affinity = 0;
   o.excl_topology = 0;
@@ -3679,7 +3682,7 @@ __global__ void fits_kernel(DevSnap s, const kueue_tas_fits_req* reqs, int n, co
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const kueue_tas_fits_req r = reqs[i];
-  if (r.leaf < 0 || r.leaf >= s.N) {
+  if (r.leaf < 0 || r.leaf >= s.N || leaf_out(s, r.leaf)) {
     fits[i] = 0;
     return;
   }
@@ -3735,7 +3738,7 @@ constexpr int kAdmitTerms = 8;
 __device__ __forceinline__ bool admit_record_fits(const DevSnap& s, const int64_t* tas_usage,
                                                   const uint32_t* usage_present, const kueue_tas_fits_req& r,
                                                   const kueue_tas_fits_term* terms) {
-  if (r.leaf < 0 || r.leaf >= s.N) return false;
+  if (r.leaf < 0 || r.leaf >= s.N || leaf_out(s, r.leaf)) return false;
   const uint32_t pres = s.free_present[r.leaf] | load_l2(usage_present + r.leaf);
   int32_t result = 0;
   bool any = false;

@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
     "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
+    "kueue_tas_snapshot_set_leaf_live",
 ]
 
 # the Makefile's SRC_HASH inputs, in order

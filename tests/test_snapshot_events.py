@@ -210,3 +210,71 @@ def test_emulated_recolumn_after_compile(emu_lib):
 @pytest.mark.gpu
 def test_recolumn_after_compile_on_gpu():
     _check_recolumn()
+
+
+def _check_leave_return(seed, n, lib=None):
+    """Nodes leaving the snapshot (NotReady, cordoned) and coming back, while
+    their parent domain keeps another node: applied in place (the leaf leaves
+    and returns, kueue_tas_snapshot_set_leaf_live), never a rebuild; every
+    evaluation equals the oracle rebuilt from the document with the events,
+    with admitted usage added meanwhile (also on leaves that are out)."""
+    rng = random.Random(seed)
+    steps_total = 0
+    for i in range(n):
+        case = synth.random_case(rng)
+        if case["levels"][-1] != "kubernetes.io/hostname" or len(case["levels"]) < 2 or not case["nodes"]:
+            continue
+        snap = TASFlavorSnapshot(case, lib=lib) if lib else TASFlavorSnapshot(case)
+        ref = copy.deepcopy(case)
+        adds = []
+        out = {}  # node name -> its last Ready document
+        for step in range(6):
+            latest = {nd["name"]: nd for nd in ref["nodes"]}
+            live = [nd for nd in latest.values()  # in the snapshot: nodesCache.find (util/tas/node.go:21-33)
+                    if nd["conditions"] == [{"type": "Ready", "status": "True"}] and not nd["unschedulable"]
+                    and nd["name"] not in out and all(k in nd["labels"] for k in case["levels"])
+                    and all(nd["labels"].get(k, "") == v for k, v in case.get("nodeLabels", {}).items())]
+            r = rng.random()
+            ev = None
+            if out and r < 0.4:
+                name = rng.choice(sorted(out))
+                ev = out.pop(name)
+            elif r < 0.85 and live:
+                nd = rng.choice(live)
+                parent = [nd["labels"].get(k) for k in case["levels"][:-1]]
+                sib = [x for x in live if [x["labels"].get(k) for k in case["levels"][:-1]] == parent]
+                host = nd["labels"].get("kubernetes.io/hostname")
+                shared = sum(1 for x in case["nodes"] if x["labels"].get("kubernetes.io/hostname") == host) > 1
+                # (a hostname shared by two nodes: the leaf's level values come from one of
+                # them, so its return may re-position the leaf — a rebuild, not checked here)
+                if len(sib) >= 2 and not shared and all(k in nd["labels"] for k in case["levels"]):
+                    out[nd["name"]] = copy.deepcopy(nd)
+                    ev = copy.deepcopy(nd)
+                    if rng.random() < 0.5:
+                        ev["conditions"] = [{"type": "Ready", "status": "False"}]
+                    else:
+                        ev["unschedulable"] = True
+            if ev is not None:
+                assert snap.update_nodes([ev]) is False, (i, step, ev["name"])
+                ref["nodes"] = ref["nodes"] + [ev]
+            else:
+                res = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+                u = synth.usage_records(case["podSets"], res)
+                if u:
+                    snap.add_usage(u)
+                    adds.append({"op": "add", "usage": u})
+            got = snap.find_topology_assignments_for_flavor(case["podSets"])
+            want = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+            assert got == want, (i, step, got, want)
+            steps_total += 1
+        snap.close()
+    assert steps_total > 50
+
+
+def test_emulated_leave_return_in_place(emu_lib):  # noqa: F811
+    _check_leave_return(31, 60, lib=emu_lib)
+
+
+@pytest.mark.gpu
+def test_leave_return_in_place_on_gpu():
+    _check_leave_return(32, 200)
