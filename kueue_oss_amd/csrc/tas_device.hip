@@ -815,6 +815,15 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
             return fail(c, KUEUE_TAS_EINVAL, "affinity values not sorted");
       }
     }
+    if (r.assumed_begin < 0 || r.assumed_end < r.assumed_begin || size_t(r.assumed_end) > num_assumed ||
+        (r.assumed_end > r.assumed_begin && !assumed))
+      return fail(c, KUEUE_TAS_EINVAL, "assumed range");
+    for (int32_t a = r.assumed_begin; a < r.assumed_end; a++) {  // sorted by leaf (the fill's binary search)
+      const kueue_tas_assumed& x = assumed[a];
+      if (x.leaf < 0 || x.leaf >= s.N || x.col < 0 || x.col >= s.R || x.col >= KUEUE_TAS_MAX_COLS ||
+          (a > r.assumed_begin && x.leaf < assumed[a - 1].leaf))
+        return fail(c, KUEUE_TAS_EINVAL, "assumed record out of range or not sorted by leaf");
+    }
     if ((r.flags & KUEUE_TAS_F_DOMAIN) &&
         (r.domain_begin < 0 || r.domain_end < r.domain_begin || r.domain_end > s.N))
       return fail(c, KUEUE_TAS_EINVAL, "required domain leaf range");

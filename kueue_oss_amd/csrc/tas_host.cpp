@@ -2597,6 +2597,7 @@ static int find_replacement(kueue_tas_host* h, std::vector<TASPodSetRequests>& p
   Workload wl;
   wl.podsets = podsets;
   make_groups(wl);
+  s.ensure_columns_for(wl.podsets);  // assumed usage is kept per column
   std::map<std::pair<int32_t, int32_t>, int64_t> assumed;  // (leaf, column) -> addAssumedUsage
   std::vector<std::string> results;
   auto finish = [&]() {
@@ -2722,6 +2723,7 @@ static int find_sequential(kueue_tas_host* h, std::vector<TASPodSetRequests>& po
   Workload wl;
   wl.podsets = podsets;
   make_groups(wl);
+  s.ensure_columns_for(wl.podsets);  // assumed usage is kept per column
   std::map<std::pair<int32_t, int32_t>, int64_t> assumed;  // (leaf, column) -> usage
   std::vector<std::pair<std::string, std::string>> results;  // (name, JSON) in set order
   auto set_result = [&](const std::string& name, const std::optional<ExplicitAssignment>& a, const std::string& reason) {

@@ -31,6 +31,11 @@ def emu_lib():
     srcs += [os.path.join(here, "emu", f) for f in ("hip_emu.cpp", "build_emu.sh", "hip/hip_runtime.h")]
     srcs.append(os.path.join(ROOT, "include", "kueue_tas.h"))
     srcs.append(os.path.join(ROOT, "include", "kueue_tas_debug.h"))
-    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in srcs):
-        subprocess.run([os.path.join(here, "emu", "build_emu.sh")], check=True, capture_output=True)
+    import fcntl
+
+    os.makedirs(os.path.join(here, "emu", "_build"), exist_ok=True)
+    with open(os.path.join(here, "emu", "_build", ".lock"), "w") as lk:  # one builder across xdist workers
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in srcs):
+            subprocess.run([os.path.join(here, "emu", "build_emu.sh")], check=True, capture_output=True)
     return native.load_library(so)

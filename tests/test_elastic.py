@@ -35,7 +35,7 @@ def _random(make, seed, n):
 
 
 def test_emulated_random(emu_lib):
-    _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 21, 60)
+    _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 21, 150)
 
 
 @pytest.mark.gpu
