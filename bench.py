@@ -363,7 +363,41 @@ def widened_rows(a, snap, snap_doc, mine, synth):
     rebuilt = snap.update_nodes(upd)
     node_ms = (time.perf_counter() - t0) * 1e3
     snap.update_nodes([copy.deepcopy(snap_doc["nodes"][k * 997 % N]) for k in range(64)])
-    return {"pod_events_ms_per_64": round(pod_ms, 3),
+    # nodes leaving (NotReady) and returning, in place (kueue_tas_snapshot_set_leaf_live)
+    gone = [dict(copy.deepcopy(snap_doc["nodes"][k * 991 % N]), conditions=[{"type": "Ready", "status": "False"}])
+            for k in range(64)]
+    t0 = time.perf_counter()
+    left_rebuilt = snap.update_nodes(gone)
+    leave_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    back_rebuilt = snap.update_nodes([copy.deepcopy(snap_doc["nodes"][k * 991 % N]) for k in range(64)])
+    return_ms = (time.perf_counter() - t0) * 1e3
+    # node replacement (findReplacementAssignment) of one assigned node of a placed workload
+    rep_ms, rep_ok = None, None
+    for w, res in zip(mine[:64], got):
+        a0 = res[0].get("assignment")
+        if a0 and a0["domains"] and not w[0].get("podSetGroupName"):
+            wl = {"unhealthyNodes": [a0["domains"][0]["values"][-1]],
+                  "podSetAssignments": [{"name": res[0]["name"], "topologyAssignment": a0}]}
+            snap.find_topology_assignments_for_workload(w, wl)
+            t0 = time.perf_counter()
+            rr = snap.find_topology_assignments_for_workload(w, wl)
+            rep_ms = (time.perf_counter() - t0) * 1e3
+            rep_ok = not rr[0]["reason"]
+            break
+    # single-workload latency through the C-ABI (JSON in, JSON out) on the resident snapshot
+    lat = []
+    for w in mine[:40]:
+        t0 = time.perf_counter()
+        snap.find_topology_assignments_for_flavor(w)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    lat.sort()
+    return {"single_call_ms": {"median": round(lat[len(lat) // 2], 3), "p90": round(lat[int(len(lat) * 0.9)], 3),
+                               "calls": len(lat), "path": "kueue_tas_host_find (JSON) on the C3 snapshot"},
+            "node_leave_ms_per_64": round(leave_ms, 3), "node_return_ms_per_64": round(return_ms, 3),
+            "node_leave_return_rebuilt": bool(left_rebuilt or back_rebuilt),
+            "node_replacement_ms": None if rep_ms is None else round(rep_ms, 3), "node_replacement_ok": rep_ok,
+            "pod_events_ms_per_64": round(pod_ms, 3),
             "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,
             "preemption_search_profile_ms": pr["profileMs"],
             "preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),

@@ -241,10 +241,14 @@ def _check_leave_return(seed, n, lib=None):
                 ev = out.pop(name)
             elif r < 0.85 and live:
                 nd = rng.choice(live)
+                hosts = [x["labels"].get("kubernetes.io/hostname") for x in case["nodes"]]
                 parent = [nd["labels"].get(k) for k in case["levels"][:-1]]
-                sib = [x for x in live if [x["labels"].get(k) for k in case["levels"][:-1]] == parent]
+                # siblings: live nodes under the same parent that own their leaf (a hostname
+                # shared by two nodes makes one leaf whose level values come from one of them)
+                sib = [x for x in live if [x["labels"].get(k) for k in case["levels"][:-1]] == parent
+                       and hosts.count(x["labels"].get("kubernetes.io/hostname")) == 1]
                 host = nd["labels"].get("kubernetes.io/hostname")
-                shared = sum(1 for x in case["nodes"] if x["labels"].get("kubernetes.io/hostname") == host) > 1
+                shared = hosts.count(host) > 1
                 # (a hostname shared by two nodes: the leaf's level values come from one of
                 # them, so its return may re-position the leaf — a rebuild, not checked here)
                 if len(sib) >= 2 and not shared and all(k in nd["labels"] for k in case["levels"]):
