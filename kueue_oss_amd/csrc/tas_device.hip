@@ -611,12 +611,25 @@ int kueue_tas_snapshot_set_leaf_live(kueue_tas_ctx* c, const int32_t* leaves, si
   }
   HIPCHK(c, hipSetDevice(c->device));
   c->snap.n_live = int32_t(int64_t(c->snap.N) - c->n_dead);
+  const bool was_dense = c->snap.leaf_dead != nullptr;
   if (c->n_dead == 0) {
     c->snap.leaf_dead = nullptr;
     return KUEUE_TAS_OK;
   }
-  HIPCHK(c, c->d_dead.ensure(size_t(c->snap.N)));
-  HIPCHK(c, hipMemcpy(c->d_dead.p, c->h_dead.data(), size_t(c->snap.N), hipMemcpyHostToDevice));
+  std::vector<int32_t> lv;  // read by the async copy: lives until the synchronize below
+  if (!was_dense) {  // first dead leaf: the whole map (the device copy was dropped while all leaves lived)
+    HIPCHK(c, c->d_dead.ensure(size_t(c->snap.N)));
+    HIPCHK(c, hipMemcpyAsync(c->d_dead.p, c->h_dead.data(), size_t(c->snap.N), hipMemcpyHostToDevice, c->stream));
+  } else {  // scatter the changed leaves
+    lv.resize(2 * n);
+    for (size_t i = 0; i < n; i++) lv[2 * i] = leaves[i], lv[2 * i + 1] = live[i] ? 1 : 0;
+    HIPCHK(c, c->d_setfree.ensure(lv.size() * 4));
+    HIPCHK(c, hipMemcpyAsync(c->d_setfree.p, lv.data(), lv.size() * 4, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(set_leaf_dead_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->d_dead.p,
+                       reinterpret_cast<const int32_t*>(c->d_setfree.p), int(n));
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap.leaf_dead = c->d_dead.p;
   return KUEUE_TAS_OK;
 }

@@ -3567,6 +3567,12 @@ __global__ void set_leaf_attrs_kernel(int32_t* taint_profile, int32_t* label_val
     for (int k = 0; k < K; k++) label_values[int64_t(k) * N + leaf] = labels[int64_t(i) * K + k];
 }
 
+__global__ void set_leaf_dead_kernel(uint8_t* dead, const int32_t* leaves_live, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dead[leaves_live[2 * i]] = leaves_live[2 * i + 1] ? 0 : 1;
+}
+
 // ---- v1beta2 compact encoding (pkg/util/tas/tas_assignment.go:135-259) ----
 // fillSingleCompactSliceValues walks the values keeping a running prefix and
 // suffix of value 0; by induction the prefix after value i is value0's prefix

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <cstdio>
 #include <functional>
+#include <tuple>
 #include <vector>
 
 #define __global__
@@ -224,7 +225,9 @@ inline hipError_t hipEventDestroy(hipEvent_t e) { delete e; return hipSuccess; }
   do {                                                                                                            \
     const dim3 emu_g_ = dim3(grid), emu_b_ = dim3(block);                                                         \
     const size_t emu_sh_ = size_t(shmem);                                                                         \
-    (stream)->ops.push_back([=]() { emu::launch(emu_g_, emu_b_, emu_sh_, [=]() { kernel(__VA_ARGS__); }); });    \
+    auto emu_a_ = std::make_tuple(__VA_ARGS__); /* arguments bind at the launch, as on the device */            \
+    (stream)->ops.push_back(                                                                                      \
+        [=]() { emu::launch(emu_g_, emu_b_, emu_sh_, [=]() { std::apply(kernel, emu_a_); }); });                 \
   } while (0)
 
 // every lane holds the same value where the kernels use it (wave-uniform data)

@@ -3,7 +3,12 @@
 Per kernel: dispatches, mean FETCH_SIZE / WRITE_SIZE per dispatch (KB as
 rocprofv3 reports them) and HBM bytes per dispatch, corrected as
 MI355X_MICROARCH.md §HBM prescribes for gfx950 (FETCH_SIZE counts half of the
-bytes of a wide coalesced read: x2; WRITE_SIZE exact).  Writes the table to
+bytes of a wide coalesced read: x2; WRITE_SIZE exact).  From the SQ passes
+(pmc3: instruction mix + SQ_WAVE_CYCLES / SQ_BUSY_CYCLES; pmc4: the disjoint
+wait / issue-stall / active split) the per-dispatch means and the fractions
+of wave time parked on memory (SQ_WAIT_ANY), stalled at issue
+(SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY); SQ cycle counters count
+quad-cycles (MI355X_MICROARCH.md PMC table).  Writes the table to
 <out>/pmc_summary.json and the fill kernel's bytes per launch to
 profiles/fill_traffic.json, which bench.py reports as roofline.traffic.
 
@@ -39,6 +44,27 @@ def main():
         w = sum(write[k]) / len(write[k]) if write[k] else 0.0
         table[k] = {"dispatches": max(len(fetch[k]), len(write[k])), "fetch_kb": round(f, 1), "write_kb": round(w, 1),
                     "hbm_bytes": int((2 * f + w) * 1024)}
+    sq = {}
+    for sub, names in (("pmc3", ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                                  "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"]),
+                       ("pmc4", ["SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"])):
+        for cn in names:
+            for k, v in read(os.path.join(src, sub, "p_counter_collection.csv"), cn).items():
+                sq.setdefault(k, {})[cn] = sum(v) / len(v)
+    for k, d in sq.items():
+        row = table.setdefault(k, {})
+        row["sq"] = {cn: round(v, 1) for cn, v in d.items()}
+        waves = d.get("SQ_WAVES") or 0
+        if waves:
+            row["per_wave"] = {cn.replace("SQ_INSTS_", "").lower(): round(d[cn] / waves, 1)
+                               for cn in d if cn.startswith("SQ_INSTS_")}
+            if "SQ_WAVE_CYCLES" in d:
+                row["per_wave"]["wave_cycles"] = round(4 * d["SQ_WAVE_CYCLES"] / waves, 1)
+        tot = sum(d.get(c, 0) for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"))
+        if tot:
+            row["wave_time_split"] = {"wait_any": round(d.get("SQ_WAIT_ANY", 0) / tot, 3),
+                                      "wait_inst_any": round(d.get("SQ_WAIT_INST_ANY", 0) / tot, 3),
+                                      "active_inst_any": round(d.get("SQ_ACTIVE_INST_ANY", 0) / tot, 3)}
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "pmc_summary.json"), "w") as fh:
         json.dump(table, fh, indent=1)
