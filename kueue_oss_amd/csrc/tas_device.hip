@@ -1324,8 +1324,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       HIPCHK(c, c->d_rack_pos.ensure(n * size_t(s.level_size[s.L - 2])));
       b.rack_pos = c->d_rack_pos.p;
     }
-    if (ucols <= 4) hipLaunchKernelGGL(fill_leaves_staged_kernel<4>, grid, dim3(256), 0, c->stream, s, b, umask);
-    else if (ucols <= 8) hipLaunchKernelGGL(fill_leaves_staged_kernel<8>, grid, dim3(256), 0, c->stream, s, b, umask);
+    const bool ts = b.num_profiles <= kStagedProfiles;
+    if (ucols <= 4 && ts) hipLaunchKernelGGL((fill_leaves_staged_kernel<4, true>), grid, dim3(256), 0, c->stream, s, b, umask);
+    else if (ucols <= 4) hipLaunchKernelGGL((fill_leaves_staged_kernel<4, false>), grid, dim3(256), 0, c->stream, s, b, umask);
+    else if (ucols <= 8 && ts) hipLaunchKernelGGL((fill_leaves_staged_kernel<8, true>), grid, dim3(256), 0, c->stream, s, b, umask);
+    else if (ucols <= 8) hipLaunchKernelGGL((fill_leaves_staged_kernel<8, false>), grid, dim3(256), 0, c->stream, s, b, umask);
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 8) hipLaunchKernelGGL(fill_leaves_kernel<8>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
@@ -1341,7 +1344,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
     HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
-    hipLaunchKernelGGL(fill_exclusion_kernel, grid, dim3(256), 0, c->stream3, s, b);
+    if (b.num_profiles <= kStagedProfiles) hipLaunchKernelGGL(fill_exclusion_kernel<true>, grid, dim3(256), 0, c->stream3, s, b);
+    else hipLaunchKernelGGL(fill_exclusion_kernel<false>, grid, dim3(256), 0, c->stream3, s, b);
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(grid.x));
     HIPCHK(c, hipGetLastError());

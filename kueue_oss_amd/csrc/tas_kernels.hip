@@ -36,6 +36,32 @@ namespace ktas {
 __device__ __forceinline__ int32_t w_add(int32_t a, int32_t b) { return int32_t(uint32_t(a) + uint32_t(b)); }
 __device__ __forceinline__ int32_t w_sub(int32_t a, int32_t b) { return int32_t(uint32_t(a) - uint32_t(b)); }
 __device__ __forceinline__ int32_t w_mul(int32_t a, int32_t b) { return int32_t(uint32_t(a) * uint32_t(b)); }
+// Reductions over aligned groups of F lanes (F a power of two, 1..64; every
+// lane of a group gets the group's result): DPP for the steps inside a row of
+// 16 (one VALU each: quad_perm, half-row mirror, row mirror — after the
+// earlier steps every lane of a sub-group holds the same partial, so a mirror
+// reads the other sub-group's), ds_swizzle (xor 16) across the rows of a
+// 32-lane half, ds_bpermute across the halves.
+template <class Op>
+__device__ __forceinline__ int32_t group_reduce(int32_t v, int F, Op op) {
+  if (F >= 2) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  if (F >= 4) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  if (F >= 8) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  if (F >= 16) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));  // row_mirror
+  if (F >= 32) v = op(v, __builtin_amdgcn_ds_swizzle(v, 0x401F));  // bit mode: lane ^ 16
+  if (F >= 64) v = op(v, __shfl_xor(v, 32, 64));
+  return v;
+}
+struct OpWAdd {
+  __device__ int32_t operator()(int32_t a, int32_t b) const { return int32_t(uint32_t(a) + uint32_t(b)); }
+};
+struct OpMin {
+  __device__ int32_t operator()(int32_t a, int32_t b) const { return a < b ? a : b; }
+};
+struct OpMax {
+  __device__ int32_t operator()(int32_t a, int32_t b) const { return a > b ? a : b; }
+};
+
 // Go int32 division (truncating; MinInt32 / -1 == MinInt32).  b == 0 is
 // rejected on the host (Go panics).
 __device__ __forceinline__ int32_t go_div32(int32_t a, int32_t b) {
@@ -481,6 +507,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 // per-eval loop has no dependent global loads (eval record -> taint row).
 struct FillEvalParams {
   int32_t eid, taint_off, nsel, slice_size, slice_level, inner;  // inner: ssal of the leaf level
+  int32_t sel_far;  // a nodeSelector column beyond the kStagedLabels held in registers
   int32_t aff_begin, aff_end;  // required node affinity requirements; aff_begin < 0: none
   int32_t dom_begin, dom_end;  // required replacement domain leaf range; dom_begin < 0: none
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
@@ -494,7 +521,11 @@ constexpr int kStagedLabels = 4;     // label columns held in registers (more: r
 // (device-scope atomics from all XCDs serialize at the memory side).
 constexpr int kMaxFillStats = 64;  // kStatFixed + taints + resource columns; more: global atomics
 
-template <int NS>
+// TS: the batch's taint-profile rows fit LDS (b.num_profiles <= kStagedProfiles).
+// A template parameter, not a runtime select: a select between the LDS row and
+// the global table compiles to a flat load whose vmcnt wait also drains every
+// store the loop issued before it.
+template <int NS, bool TS>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
   __shared__ FillEvalParams sh_p[kEvalsPerBlock];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
@@ -517,7 +548,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   }
   const int e0 = b.fill_chunks[2 * chunk];
   const int ne = b.fill_chunks[2 * chunk + 1];
-  const bool stage_taints = b.num_profiles <= kStagedProfiles;
+  constexpr bool stage_taints = TS;
   if (int(threadIdx.x) < ne) {
     const int eid = b.fill_ids[e0 + threadIdx.x];
     const DevEval& ev = b.evals[eid];
@@ -533,9 +564,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     P.aff_end = aff ? ev.aff_end : -1;
     P.dom_begin = ev.dom_begin;
     P.dom_end = ev.dom_end;
+    P.sel_far = 0;
     for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
       P.sel_col[k] = ev.sel_col[k];
       P.sel_val[k] = ev.sel_val[k];
+      if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
     }
   }
   __syncthreads();
@@ -664,36 +697,47 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     }
   }
 
+  // loads the per-eval loop needs, hoisted: a global load inside the loop
+  // waits (vmcnt) for every store of the earlier evals
+  const bool dead = valid && leaf_out(s, leaf);
   for (int e = 0; e < ne; e++) {
     const FillEvalParams& P = sh_p[e];
     const int eid = uni(P.eid);
     const int nsel = uni(P.nsel);
     const int32_t slice_size = uni(P.slice_size), slice_level = uni(P.slice_level);
     int32_t state = 0, swl = 0, ls = 0;
-    int kind = (valid && leaf_out(s, leaf)) ? EX_DEAD : EX_NONE, id = -1;
+    int kind = dead ? EX_DEAD : EX_NONE, id = -1;
     if (valid && kind == EX_NONE) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
-          int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(P.taint_off) + prof];
+          int t;
+          if constexpr (TS) t = sh_taint[e][prof];
+          else t = b.taint_table[uni(P.taint_off) + prof];
           if (t >= 0) {
             kind = EX_TAINT;
             id = t;
           }
         }
-        if (kind == EX_NONE) {
-          for (int k = 0; k < nsel; k++) {
-            const int col = uni(P.sel_col[k]);
-            int32_t v;
-            if (col < kStagedLabels) {
-              v = lab[0];
+        if (kind == EX_NONE && nsel > 0) {
+          // two loops: with every column in registers the loop holds no global
+          // load, so no vmcnt wait (which would also drain the earlier stores)
+          if (!uni(P.sel_far)) {
+            for (int k = 0; k < nsel; k++) {
+              const int col = uni(P.sel_col[k]);
+              int32_t v = lab[0];
 #pragma unroll
               for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
-            } else {
-              v = s.label_values[int64_t(col) * N + leaf];
+              if (v != uni(P.sel_val[k])) {
+                kind = EX_SELECTOR;
+                break;
+              }
             }
-            if (v != uni(P.sel_val[k])) {
-              kind = EX_SELECTOR;
-              break;
+          } else {
+            for (int k = 0; k < nsel; k++) {
+              if (label_at(uni(P.sel_col[k])) != uni(P.sel_val[k])) {
+                kind = EX_SELECTOR;
+                break;
+              }
             }
           }
         }
@@ -739,7 +783,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       const int F = b.rack_fanout;
       const int32_t inner = uni(P.inner);
       int32_t cs = state, csw = swl;
-      if (inner != 0) {
+      if (inner != 0 && inner != 1) {  // wave-uniform; x / 1 * 1 == x
         cs = w_mul(go_div32(cs, inner), inner);
         csw = w_mul(go_div32(csw, inner), inner);
       }
@@ -750,17 +794,18 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         minD = w_sub(cs, csw);
         minSD = w_sub(ss, sswl);
       }
-      for (int m = 1; m < F; m <<= 1) {
-        cap = w_add(cap, __shfl_xor(cap, m, 64));
-        slc = w_add(slc, __shfl_xor(slc, m, 64));
+      cap = group_reduce(cap, F, OpWAdd());
+      if (s.L - 1 != slice_level) {  // wave-uniform: the leaves' sliceState is 0
+      } else if (inner == 1 && slice_size == 1) {  // wave-uniform: sliceState == state
+        slc = cap;
+      } else {
+        slc = group_reduce(slc, F, OpWAdd());
       }
       if (leader) {  // leader fields only matter for leader evals (parents of others keep state, sliceState)
-        for (int m = 1; m < F; m <<= 1) {
-          minD = min(minD, __shfl_xor(minD, m, 64));
-          minSD = min(minSD, __shfl_xor(minSD, m, 64));
-          lead = max(lead, __shfl_xor(lead, m, 64));
-          has |= __shfl_xor(has, m, 64);
-        }
+        minD = group_reduce(minD, F, OpMin());
+        minSD = group_reduce(minSD, F, OpMin());
+        lead = group_reduce(lead, F, OpMax());
+        has = group_reduce(has, F, OpMax());
       }
       const int parent = leaf / F;
       const uint64_t posm = ballot(valid && ss > 0);  // positive children, for the BestFit descent
@@ -837,6 +882,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 // third stream beside the roll-up and select.  Same grid and masks as the
 // fill; the resource case reads the limiting resource the fill recorded per
 // (chunk, leaf) where the chunk's signature gives state 0.
+template <bool TS>  // as fill_leaves_staged_kernel
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t sh_toff[kEvalsPerBlock];
   __shared__ int32_t sh_nsel[kEvalsPerBlock];
@@ -847,7 +893,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   const int e0 = b.fill_chunks[2 * blockIdx.y];
   const int ne = b.fill_chunks[2 * blockIdx.y + 1];
-  const bool stage_taints = b.num_profiles <= kStagedProfiles;
+  constexpr bool stage_taints = TS;
   if (int(threadIdx.x) < ne) {
     const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
     sh_toff[threadIdx.x] = ev.taint_table;
@@ -890,7 +936,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     if (valid && !dead) {
       if (s.lowest_is_hostname) {
         if (s.taint_profile) {
-          const int t = stage_taints ? sh_taint[e][prof] : b.taint_table[uni(sh_toff[e]) + prof];
+          int t;
+          if constexpr (TS) t = sh_taint[e][prof];
+          else t = b.taint_table[uni(sh_toff[e]) + prof];
           if (t >= 0) {
             kind = EX_TAINT;
             id = t;

@@ -101,6 +101,23 @@ inline T __shfl(T v, int src, int width = 64) {
   memcpy(&out, &r, sizeof(T));
   return out;
 }
+// DPP / swizzle lane permutations (the controls the kernels use)
+inline int __builtin_amdgcn_update_dpp(int, int v, int ctrl, int, int, bool) {
+  const int l = __lane_of_cur();
+  int src;
+  if (ctrl < 0x100) src = (l & ~3) | ((ctrl >> (2 * (l & 3))) & 3);  // quad_perm
+  else if (ctrl == 0x140) src = (l & ~15) | (15 - (l & 15));          // row_mirror
+  else if (ctrl == 0x141) src = (l & ~7) | (7 - (l & 7));             // row_half_mirror
+  else abort();
+  return int(emu::wave_exchange(uint64_t(uint32_t(v)), src));
+}
+inline int __builtin_amdgcn_ds_swizzle(int v, int pattern) {
+  if (pattern & 0x8000) abort();  // bit mode only
+  const int l = __lane_of_cur();
+  const int and_m = pattern & 31, or_m = (pattern >> 5) & 31, xor_m = (pattern >> 10) & 31;
+  const int src = (l & ~31) | ((((l & 31) & and_m) | or_m) ^ xor_m);
+  return int(emu::wave_exchange(uint64_t(uint32_t(v)), src));
+}
 template <typename T>
 inline T __shfl_xor(T v, int mask, int width = 64) {
   (void)width;
