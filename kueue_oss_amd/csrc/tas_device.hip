@@ -186,6 +186,7 @@ struct kueue_tas_ctx {
   DevBuf<uint8_t> d_stage;
   // phase-1 class computation scratch (kept to avoid reallocation)
   std::vector<int32_t> cls_rep, cls_sig, cls_of, sig_rep, cls_next, sig_next, cls_fastrep, cls_slot, cls_order;
+  std::vector<int32_t> sig_base, base_rep, cls_packed, sig_ncls;
   FlatMap cls_head, sig_head;
   DevBuf<int32_t> d_overlay, d_tags;
   DevBuf<uint64_t> d_rack_pos;  // positive-child masks of the leaves' parents (fused fill)  // select's copy-on-write counters and ownership tags
@@ -853,6 +854,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t o_taint = seg(taint_table_len * 4), o_assumed = seg(num_assumed * sizeof(kueue_tas_assumed));
   const size_t o_aff = seg(num_aff * sizeof(kueue_tas_affinity_req)), o_affv = seg(num_aff_vals * 4);
   const size_t o_fill = seg(n * 4), o_fchunks = seg(n * 8), o_pairs = seg(n * 8), o_rep = seg(n * 4);
+  const size_t o_frun = seg(n * 4);
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
   const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
   const size_t o_moff = seg((n + 1) * 4), o_mem = seg(n * 4);  // class members in fill order (CSR)
@@ -966,6 +968,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
     return true;
   };
+  // base signature: what the leaf's remaining capacity depends on (a fill chunk shares it)
+  auto same_base = [&](const DevEval& x, const DevEval& y) {
+    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
+    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
+    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
+      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
+      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
+      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
+    }
+    return true;
+  };
   auto mask_hash = [&](const DevEval& e) {
     uint64_t h = 0x9e3779b97f4a7c15ull;
     auto add = [&](uint64_t v) {
@@ -1029,7 +1042,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   int32_t* h_pidx = reinterpret_cast<int32_t*>(hs + o_pidx);  // eval -> row of its leaf partials, -1
   int32_t* h_bf = reinterpret_cast<int32_t*>(hs + o_bf);      // evals selected on the main stream
   int nbf = 0;
-  int nfill = 0, npairs = 0, nslots = 0, nfast = 0, nfchunks = 0, nleafsel = 0;
+  int nfill = 0, npairs = 0, nslots = 0, nfast = 0, nfchunks = 0, nleafsel = 0, nruns = 0, nsingle = 0;
   {
     // classes: open hash chains on the 64-bit (signature, mask) hash, exact compare on the rep
     std::vector<int32_t>& cls_rep = c->cls_rep;    // first member of each class
@@ -1119,12 +1132,43 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
         h_leafsel[nleafsel++] = int32_t(i);
       }
     }
-    // fill chunks: classes ordered by signature, <= kEvalsPerFillBlock per chunk, one signature each
+    // fill chunks: classes ordered by (base signature, signature), <= kEvalsPerFillBlock
+    // per chunk, one base signature each (the leaf's remaining capacity is
+    // shared); a run of one signature inside a chunk shares the CountIn
+    const int nsig = int(sig_rep.size());
+    std::vector<int32_t>& sig_base = c->sig_base;
+    sig_base.assign(size_t(nsig), -1);
+    {
+      std::vector<int32_t>& base_rep = c->base_rep;
+      base_rep.clear();
+      for (int g = 0; g < nsig; g++) {
+        const DevEval& e = hev[sig_rep[size_t(g)]];
+        for (size_t q = 0; q < base_rep.size() && sig_base[size_t(g)] < 0; q++)
+          if (same_base(e, hev[base_rep[q]])) sig_base[size_t(g)] = int32_t(q);
+        if (sig_base[size_t(g)] < 0) {
+          sig_base[size_t(g)] = int32_t(base_rep.size());
+          base_rep.push_back(sig_rep[size_t(g)]);
+        }
+        if (base_rep.size() > 64) {  // many distinct bases (assumed usage per eval): no sharing to look for
+          for (int h = g + 1; h < nsig; h++) sig_base[size_t(h)] = int32_t(base_rep.size()) + (h - g - 1);
+          break;
+        }
+      }
+    }
     std::vector<int32_t>& order = c->cls_order;
     order.resize(size_t(ncls));
     for (int k = 0; k < ncls; k++) order[size_t(k)] = k;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int32_t a, int32_t b2) { return cls_sig[size_t(a)] < cls_sig[size_t(b2)]; });
+    std::vector<int32_t>& sig_ncls = c->sig_ncls;  // classes per signature: small ones pack together
+    sig_ncls.assign(size_t(nsig), 0);
+    for (int k = 0; k < ncls; k++) sig_ncls[size_t(cls_sig[size_t(k)])]++;
+    auto small = [&](int32_t sg) { return sig_ncls[size_t(sg)] < kEvalsPerFillBlock / 2; };
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b2) {
+      const int32_t sa = cls_sig[size_t(a)], sb = cls_sig[size_t(b2)];
+      const int32_t ba = sig_base[size_t(sa)], bb = sig_base[size_t(sb)];
+      if (ba != bb) return ba < bb;
+      if (small(sa) != small(sb)) return !small(sa);
+      return sa < sb;
+    });
     for (int k = 0; k < ncls; k++) h_fill[k] = rep[size_t(order[size_t(k)])];
     nfill = ncls;
     {  // members other than the rep, grouped by fill position (stats written by the reduce)
@@ -1142,14 +1186,45 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       for (size_t i = 0; i < n; i++)
         if (int32_t(i) != rep[size_t(cls_of[i])]) h_mem[cur[size_t(pos[size_t(cls_of[i])])]++] = int32_t(i);
     }
+    int32_t* h_frun = reinterpret_cast<int32_t*>(hs + o_frun);
+    // a signature with at least half a chunk of classes gets chunks of its
+    // own (one run: CountIn before the eval loop); the smaller ones of a base
+    // share packed chunks (several runs).  Single-run chunks first.
+    std::vector<int32_t>& packed = c->cls_packed;  // [start, len) signature runs left for packing
+    packed.clear();
     for (int k = 0; k < ncls;) {
+      const int32_t sg = cls_sig[size_t(order[size_t(k)])];
       int e = k + 1;
-      while (e < ncls && e - k < kEvalsPerFillBlock && cls_sig[size_t(order[size_t(e)])] == cls_sig[size_t(order[size_t(k)])])
-        e++;
-      h_fchunks[2 * nfchunks] = k;
-      h_fchunks[2 * nfchunks + 1] = e - k;
-      nfchunks++;
+      while (e < ncls && cls_sig[size_t(order[size_t(e)])] == sg) e++;
+      if (e - k >= kEvalsPerFillBlock / 2) {
+        for (int q = k; q < e; q += kEvalsPerFillBlock) {
+          h_fchunks[2 * nfchunks] = q;
+          h_fchunks[2 * nfchunks + 1] = std::min(kEvalsPerFillBlock, e - q);
+          nfchunks++;
+          for (int r = q; r < q + h_fchunks[2 * nfchunks - 1]; r++) h_frun[r] = nruns;
+          nruns++;
+        }
+      } else {
+        packed.push_back(k);
+        packed.push_back(e - k);
+      }
       k = e;
+    }
+    nsingle = nfchunks;
+    for (size_t i = 0; i < packed.size();) {  // runs of one base, in order, up to a chunk each
+      const int32_t k0 = packed[i];
+      const int32_t base = sig_base[size_t(cls_sig[size_t(order[size_t(k0)])])];
+      int len = 0;
+      h_fchunks[2 * nfchunks] = k0;
+      while (i < packed.size() && len + packed[i + 1] <= kEvalsPerFillBlock && packed[i] == k0 + len &&
+             sig_base[size_t(cls_sig[size_t(order[size_t(packed[i])])])] == base) {
+        for (int r = packed[i]; r < packed[i] + packed[i + 1]; r++) h_frun[r] = nruns;
+        nruns++;
+        len += packed[i + 1];
+        i += 2;
+      }
+      h_fchunks[2 * nfchunks + 1] = len;
+      nfchunks++;
     }
   }
   lap(1);
@@ -1298,6 +1373,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.fill_ids = reinterpret_cast<const int32_t*>(ds + o_fill);
   b.nfill = nfill;
   b.fill_chunks = reinterpret_cast<const int32_t*>(ds + o_fchunks);
+  b.fill_run = reinterpret_cast<const int32_t*>(ds + o_frun);
   // K1
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   c->last_stats[0] += nfill;
@@ -1313,7 +1389,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.fill_stats = c->d_fill_stats.p;
     }
     if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
-      HIPCHK(c, c->d_fill_lim.ensure(size_t(nfchunks) * size_t(s.N)));
+      HIPCHK(c, c->d_fill_lim.ensure(size_t(nruns) * size_t(s.N)));
       b.stats_split = 1;
       b.fill_lim = c->d_fill_lim.p;
       b.cls_member_off = reinterpret_cast<const int32_t*>(ds + o_moff);
@@ -1325,10 +1401,22 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.rack_pos = c->d_rack_pos.p;
     }
     const bool ts = b.num_profiles <= kStagedProfiles;
-    if (ucols <= 4 && ts) hipLaunchKernelGGL((fill_leaves_staged_kernel<4, true>), grid, dim3(256), 0, c->stream, s, b, umask);
-    else if (ucols <= 4) hipLaunchKernelGGL((fill_leaves_staged_kernel<4, false>), grid, dim3(256), 0, c->stream, s, b, umask);
-    else if (ucols <= 8 && ts) hipLaunchKernelGGL((fill_leaves_staged_kernel<8, true>), grid, dim3(256), 0, c->stream, s, b, umask);
-    else if (ucols <= 8) hipLaunchKernelGGL((fill_leaves_staged_kernel<8, false>), grid, dim3(256), 0, c->stream, s, b, umask);
+    // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
+    auto staged = [&](auto ns, auto tsv, auto mr, int first, int count) {
+      if (count <= 0) return;
+      hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value>),
+                         dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+    };
+    auto staged2 = [&](auto ns, auto tsv) {
+      staged(ns, tsv, std::false_type(), 0, nsingle);
+      staged(ns, tsv, std::true_type(), nsingle, nfchunks - nsingle);
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    if (ucols <= 4 && ts) staged2(I4(), std::true_type());
+    else if (ucols <= 4) staged2(I4(), std::false_type());
+    else if (ucols <= 8 && ts) staged2(I8(), std::true_type());
+    else if (ucols <= 8) staged2(I8(), std::false_type());
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 8) hipLaunchKernelGGL(fill_leaves_kernel<8>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);

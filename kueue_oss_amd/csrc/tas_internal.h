@@ -131,7 +131,7 @@ struct DevBatch {
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_lim)
-  int8_t* fill_lim;        // [fill chunks][N] limiting resource where the chunk signature gives state 0, else -1
+  int8_t* fill_lim;        // [signature runs][N] limiting resource where the run's signature gives state 0, else -1
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)
   const int32_t* cls_members;     // eval ids
   int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)
@@ -154,7 +154,10 @@ struct DevBatch {
   int32_t nblk;            // fill blocks per eval (partials per eval)
   const int32_t* fill_ids; // [nfill] evals whose phase 1 is computed (one per distinct phase-1 input)
   int32_t nfill;
-  const int32_t* fill_chunks; // [nchunks][2] (start, len) into fill_ids: <= kEvalsPerBlock classes, one request signature
+  const int32_t* fill_chunks; // [nchunks][2] (start, len) into fill_ids: <= kEvalsPerBlock classes with one base
+                              // signature (leader / simulateEmpty flags, assumed usage), request terms may differ
+  const int32_t* fill_run;    // [nfill] signature run of each fill position: consecutive positions of a chunk
+                              // with the same request terms share a run (one CountIn per leaf)
   const int32_t* rep_of;   // [n] class rep whose phase-1 counters the eval reads
   const int32_t* lfc_slot; // [n] fast-LFC table slot, -1 if the eval is not fast LFC
   const int32_t* lfc_rep;  // [lfc_nslots] eval whose leaf counters the table summarizes

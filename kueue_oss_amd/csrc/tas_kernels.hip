@@ -508,6 +508,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 struct FillEvalParams {
   int32_t eid, taint_off, nsel, slice_size, slice_level, inner;  // inner: ssal of the leaf level
   int32_t sel_far;  // a nodeSelector column beyond the kStagedLabels held in registers
+  int32_t run, sig_new;  // signature run (DevBatch::fill_run); 1: first position of its run in the chunk
+  int32_t rmask, lmask;  // the run's worker / leader column masks
   int32_t aff_begin, aff_end;  // required node affinity requirements; aff_begin < 0: none
   int32_t dom_begin, dom_end;  // required replacement domain leaf range; dom_begin < 0: none
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
@@ -525,9 +527,14 @@ constexpr int kMaxFillStats = 64;  // kStatFixed + taints + resource columns; mo
 // A template parameter, not a runtime select: a select between the LDS row and
 // the global table compiles to a flat load whose vmcnt wait also drains every
 // store the loop issued before it.
-template <int NS, bool TS>
-__global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask) {
+// MR: the launch's chunks hold several signature runs (CountIn per run inside
+// the eval loop); otherwise one run per chunk, counted before the loop (fewer
+// live registers: higher occupancy).  chunk_base: first chunk of the launch.
+template <int NS, bool TS, bool MR>
+__global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
+                                                                          int chunk_base) {
   __shared__ FillEvalParams sh_p[kEvalsPerBlock];
+  __shared__ DevTerm sh_term[kEvalsPerBlock][2 * NS];  // a run's worker | leader terms (at its first position)
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
   const bool split = b.stats_split != 0;  // ExclusionStats counted by fill_exclusion_kernel
@@ -546,6 +553,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     chunk = int(g % gridDim.y);
     tile = int((g / gridDim.y) * 8u + (lin & 7u));
   }
+  chunk += chunk_base;
   const int e0 = b.fill_chunks[2 * chunk];
   const int ne = b.fill_chunks[2 * chunk + 1];
   constexpr bool stage_taints = TS;
@@ -570,6 +578,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       P.sel_val[k] = ev.sel_val[k];
       if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
     }
+    P.run = b.fill_run[e0 + threadIdx.x];
+    P.sig_new = threadIdx.x == 0 || b.fill_run[e0 + threadIdx.x - 1] != P.run;
+    P.rmask = int32_t(ev.req_mask);
+    P.lmask = int32_t(ev.lead_mask);
   }
   __syncthreads();
   if (s.taint_profile && stage_taints) {
@@ -577,6 +589,13 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       const int e = i / kStagedProfiles, p = i % kStagedProfiles;
       sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_p[e].taint_off + p] : -1;
     }
+  }
+  for (int i = threadIdx.x; i < ne * 2 * NS; i += kFillThreads) {
+    const int e = i / (2 * NS), j = i % (2 * NS);
+    if (!sh_p[e].sig_new) continue;
+    const DevEval& ev = b.evals[sh_p[e].eid];
+    if (j < NS && j < ev.nreq) sh_term[e][j] = b.terms[ev.term_begin + j];
+    if (j >= NS && j - NS < ev.nlead) sh_term[e][j] = b.terms[ev.lead_begin + (j - NS)];
   }
   __syncthreads();
   const int leaf = tile * kFillThreads + threadIdx.x;
@@ -612,96 +631,111 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
   };
 
-  // ---- the chunk's request signature (first member): counts once per leaf ----
-  int32_t state0 = 0, swl0 = 0, ls0 = 0;
-  int lim0 = -1;
-  bool leader;
+  // ---- the chunk's base signature (leader / simulateEmpty, assumed usage):
+  // the leaf's remaining capacity, once per leaf ----
+  bool leader, live;
+  uint32_t pres = 0;
+  int64_t cap[NS];
   {
     const DevEval& ev = b.evals[uni(b.fill_ids[e0])];
     const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
-    const uint32_t rmask = uint32_t(uni(int32_t(ev.req_mask)));
-    const uint32_t lmask = uint32_t(uni(int32_t(ev.lead_mask)));
-    const int tb = uni(ev.term_begin), lb = uni(ev.lead_begin);
     const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
     leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
-    if (valid && !leaf_out(s, leaf)) {
-      uint32_t pres = fp | (sim ? 0u : up);
-      int a_lo = 0, a_hi = 0;
-      if (aend > abeg) {
-        int lo = abeg, hi = aend;
-        while (lo < hi) {
-          int mid = (lo + hi) >> 1;
-          if (b.assumed[mid].leaf < leaf) lo = mid + 1;
-          else hi = mid;
-        }
-        a_lo = lo;
-        a_hi = lo;
-        while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
-          pres |= 1u << b.assumed[a_hi].col;
-          a_hi++;
-        }
+    live = valid && !leaf_out(s, leaf);
+    pres = fp | (sim ? 0u : up);
+    int a_lo = 0, a_hi = 0;
+    if (live && aend > abeg) {
+      int lo = abeg, hi = aend;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (b.assumed[mid].leaf < leaf) lo = mid + 1;
+        else hi = mid;
       }
-      int64_t cap[NS];
-#pragma unroll
-      for (int k = 0; k < NS; k++) {
-        int64_t c = sim ? fr[k] : int64_t(uint64_t(fr[k]) - uint64_t(us[k]));
-        for (int a = a_lo; a < a_hi; a++)
-          if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
-        cap[k] = c;
+      a_lo = lo;
+      a_hi = lo;
+      while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
+        pres |= 1u << b.assumed[a_hi].col;
+        a_hi++;
       }
-      // CountInWithLimitingResource over the worker terms, ascending column order
-      auto count_slots = [&](uint32_t mask, int tbase, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
-        int32_t result = 0;
-        bool any = false, done = false;
-        int lim = -1;
+    }
 #pragma unroll
-        for (int k = 0; k < NS; k++) {
-          const int col = scol[k];
-          if (col >= 0 && ((mask >> col) & 1u) && !done) {
-            const DevTerm t = uni_term(b.terms[tbase + __popc(mask & ((1u << col) - 1u))]);
-            if (!((presm >> col) & 1u) && t.val != 0) {
-              lim = col;
-              result = 0;
-              any = true;
-              done = true;
-            } else {
-              int64_t c = cap[k];
-              if (sub_leader && ((lmask >> col) & 1u)) {
-                const DevTerm lt = uni_term(b.terms[lb + __popc(lmask & ((1u << col) - 1u))]);
-                c = int64_t(uint64_t(c) - uint64_t(lt.val));
-              }
-              int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
-              if (!any || cnt < result) {
-                result = cnt;
-                lim = col;
-                any = true;
-              }
-            }
+    for (int k = 0; k < NS; k++) {
+      int64_t c = sim ? fr[k] : int64_t(uint64_t(fr[k]) - uint64_t(us[k]));
+      for (int a = a_lo; a < a_hi; a++)
+        if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+      cap[k] = c;
+    }
+  }
+  // CountInWithLimitingResource over a run's terms (LDS), ascending column order
+  auto count_slots = [&](const DevTerm* terms, uint32_t mask, const DevTerm* lterms, uint32_t lmask, uint32_t presm,
+                         bool sub_leader, int* lim_out) -> int32_t {
+    int32_t result = 0;
+    bool any = false, done = false;
+    int lim = -1;
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      const int col = scol[k];
+      if (col >= 0 && ((mask >> col) & 1u) && !done) {
+        const DevTerm t = uni_term(terms[__popc(mask & ((1u << col) - 1u))]);
+        if (!((presm >> col) & 1u) && t.val != 0) {
+          lim = col;
+          result = 0;
+          any = true;
+          done = true;
+        } else {
+          int64_t c = cap[k];
+          if (sub_leader && ((lmask >> col) & 1u)) {
+            const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
+            c = int64_t(uint64_t(c) - uint64_t(lt.val));
           }
-        }
-        *lim_out = lim;
-        return any ? result : 0;
-      };
-      state0 = count_slots(rmask, tb, pres, false, &lim0);
-      if (split) b.fill_lim[int64_t(chunk) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
-      swl0 = state0;
-      if (leader) {
-        int dummy;
-        int32_t lc = count_slots(lmask, lb, pres, false, &dummy);
-        if (lc > 0) {
-          ls0 = 1;
-          swl0 = count_slots(rmask, tb, pres | lmask, true, &dummy);
+          int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
+          if (!any || cnt < result) {
+            result = cnt;
+            lim = col;
+            any = true;
+          }
         }
       }
     }
-  }
+    *lim_out = lim;
+    return any ? result : 0;
+  };
+  int32_t state0 = 0, swl0 = 0, ls0 = 0;
+  int lim0 = -1;
+  auto count_run = [&](int e) {  // CountIn of the run starting at chunk position e
+    state0 = swl0 = ls0 = 0;
+    lim0 = -1;
+    const FillEvalParams& P = sh_p[e];
+    if (live) {
+      const uint32_t rmask = uint32_t(uni(P.rmask)), lmask = uint32_t(uni(P.lmask));
+      const DevTerm* wt = sh_term[e];
+      const DevTerm* lt = sh_term[e] + NS;
+      state0 = count_slots(wt, rmask, lt, lmask, pres, false, &lim0);
+      if (split) b.fill_lim[int64_t(uni(P.run)) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
+      swl0 = state0;
+      if (leader) {
+        int dummy;
+        int32_t lc = count_slots(lt, lmask, lt, lmask, pres, false, &dummy);
+        if (lc > 0) {
+          ls0 = 1;
+          swl0 = count_slots(wt, rmask, lt, lmask, pres | lmask, true, &dummy);
+        }
+      }
+    } else if (split && valid) {
+      b.fill_lim[int64_t(uni(P.run)) * N + leaf] = int8_t(-1);
+    }
+  };
+  if constexpr (!MR) count_run(0);
 
   // loads the per-eval loop needs, hoisted: a global load inside the loop
   // waits (vmcnt) for every store of the earlier evals
-  const bool dead = valid && leaf_out(s, leaf);
+  const bool dead = valid && !live;
   for (int e = 0; e < ne; e++) {
     const FillEvalParams& P = sh_p[e];
+    if constexpr (MR) {
+      if (uni(P.sig_new)) count_run(e);  // a new signature run: CountIn once per leaf for the run
+    }
     const int eid = uni(P.eid);
     const int nsel = uni(P.nsel);
     const int32_t slice_size = uni(P.slice_size), slice_level = uni(P.slice_level);
@@ -886,6 +920,7 @@ template <bool TS>  // as fill_leaves_staged_kernel
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t sh_toff[kEvalsPerBlock];
   __shared__ int32_t sh_nsel[kEvalsPerBlock];
+  __shared__ int32_t sh_run[kEvalsPerBlock];
   __shared__ int32_t sh_aff[kEvalsPerBlock][4];  // affinity range, required-domain leaf range
   __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
@@ -898,6 +933,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
     sh_toff[threadIdx.x] = ev.taint_table;
     sh_nsel[threadIdx.x] = ev.nsel;
+    sh_run[threadIdx.x] = b.fill_run[e0 + threadIdx.x];
     const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
     sh_aff[threadIdx.x][0] = aff ? ev.aff_begin : -1;
     sh_aff[threadIdx.x][1] = aff ? ev.aff_end : -1;
@@ -921,7 +957,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   const int N = s.N;
   const int lane = lane_id();
   const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
-  const int lim = valid ? int(b.fill_lim[int64_t(blockIdx.y) * N + leaf]) : -1;
+  int lim = -1;  // limiting resource of the position's signature run (the fill recorded it)
   int32_t lab[kStagedLabels];
 #pragma unroll
   for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
@@ -932,6 +968,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   };
   const bool dead = valid && leaf_out(s, leaf);
   for (int e = 0; e < ne; e++) {
+    const int run = uni(sh_run[e]);
+    if (e == 0 || run != uni(sh_run[e - 1])) lim = valid ? int(b.fill_lim[int64_t(run) * N + leaf]) : -1;
     int kind = EX_NONE, id = -1;
     if (valid && !dead) {
       if (s.lowest_is_hostname) {
