@@ -19,8 +19,11 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -354,6 +357,17 @@ class FlavorSnapshot {
 
   // tree (levels sorted lexicographically by levelValues)
   std::vector<std::vector<std::vector<std::string>>> values;  // [l][i]
+  // values[L-1][leaf].data() per leaf: the Values views of TopologyAssignment
+  // domains (one flat lookup per domain instead of a vector header each)
+  mutable std::vector<const std::string*> leafVals;
+  const std::string* const* leaf_values() const {
+    const auto& lv = values.back();
+    if (leafVals.size() != lv.size()) {
+      leafVals.resize(lv.size());
+      for (size_t i = 0; i < lv.size(); i++) leafVals[i] = lv[i].data();
+    }
+    return leafVals.data();
+  }
   std::vector<std::vector<int32_t>> childOff;                 // [l][D_l + 1]
   std::vector<std::string> leafId;
   std::unordered_map<std::string, int32_t> leafById;
@@ -572,6 +586,7 @@ class FlavorSnapshot {
     std::sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return tmp[a].lv < tmp[b].lv; });
     const int L = this->L();
     values.assign(L, {});
+    leafVals.clear();
     childOff.assign(L > 1 ? L - 1 : 0, {});
     std::vector<std::vector<std::string>> sortedLeaves;
     for (int32_t p : perm) sortedLeaves.push_back(tmp[p].lv);
@@ -1238,8 +1253,9 @@ class FlavorSnapshot {
   }
 
   uint64_t compile_gen = 1;  // bumped whenever compiled requests may change
-  void compile_group(GroupEval& g, bool simulateEmpty) {
-    compile_gen++;
+  // bump = false: the caller bumps compile_gen once for a parallel compile
+  void compile_group(GroupEval& g, bool simulateEmpty, bool bump = true) {
+    if (bump) compile_gen++;
     const TASPodSetRequests& w = *g.workers;
     kueue_tas_eval_req& q = g.req;
     memset(&q, 0, sizeof q);
@@ -1801,6 +1817,99 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Persistent host workers for the per-batch loops that are independent per
+// workload (the request compile of a step, TopologyAssignment values).  The
+// calling thread takes chunks too and only waits for chunks already taken,
+// so a worker still asleep never delays a call; idle workers spin briefly
+// for the next job (steps follow each other within a millisecond), then
+// sleep.  KUEUE_TAS_HOST_THREADS sets the worker count (0: inline).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool pool;
+    return pool;
+  }
+  size_t workers() const { return threads_.size(); }
+  // fn(begin, end) over [0, n) in chunks of `grain`; one job at a time
+  template <class F>
+  void run(size_t n, size_t grain, F&& fn) {
+    if (threads_.empty() || n <= grain) {
+      if (n) fn(size_t(0), n);
+      return;
+    }
+    std::lock_guard<std::mutex> one(callMu_);
+    std::function<void(size_t, size_t)> f(std::ref(fn));
+    auto job = std::make_shared<Job>();
+    job->fn = &f;
+    job->n = n;
+    job->grain = grain;
+    job->chunks = (n + grain - 1) / grain;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = job;
+      epoch_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    work(*job);
+    while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
+    std::lock_guard<std::mutex> lk(mu_);
+    job_.reset();  // late workers keep their reference; its chunks are exhausted
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      epoch_.fetch_add(1);
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+
+ private:
+  struct Job {
+    std::function<void(size_t, size_t)>* fn = nullptr;
+    size_t n = 0, grain = 1, chunks = 0;
+    std::atomic<size_t> next{0}, done{0};
+  };
+  HostPool() {
+    size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
+    if (const char* e = getenv("KUEUE_TAS_HOST_THREADS")) n = size_t(std::max(0, atoi(e)));
+    for (size_t i = 0; i < n; i++) threads_.emplace_back([this] { loop(); });
+  }
+  static void work(Job& j) {
+    for (;;) {
+      const size_t c = j.next.fetch_add(1, std::memory_order_relaxed);
+      if (c >= j.chunks) return;
+      const size_t b = c * j.grain;
+      (*j.fn)(b, std::min(j.n, b + j.grain));
+      j.done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void loop() {
+    uint64_t seen = epoch_.load();
+    for (;;) {
+      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(300);
+      while (epoch_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < spin_until)
+        std::this_thread::yield();
+      std::shared_ptr<Job> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || epoch_.load() != seen; });
+        if (stop_) return;
+        seen = epoch_.load();
+        job = job_;
+      }
+      if (job) work(*job);
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_, callMu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> epoch_{0};
+  std::shared_ptr<Job> job_;
+  bool stop_ = false;
+};
+
 struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
@@ -1938,14 +2047,22 @@ struct Evaluator {
     results->resize(wls.size());
     used.assign(wls.size(), 0);
     if (!precompiled) {
+      // grouping and the prelude are independent per workload: split over
+      // the host pool; only the column check touches the shared snapshot
+      HostPool& pool = HostPool::get();
+      constexpr size_t kGrain = 64;
+      pool.run(wls.size(), kGrain, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++)
+          if (wls[i].groups.empty() || regroup) make_groups(wls[i]);
+      });
       bool changed = false;
-      for (auto& wl : wls) {
-        if (wl.groups.empty() || regroup) make_groups(wl);
-        changed |= snap->ensure_columns_for(wl.podsets);
-      }
-      for (auto& wl : wls)
-        for (auto& g : wl.groups)
-          if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
+      for (auto& wl : wls) changed |= snap->ensure_columns_for(wl.podsets);
+      pool.run(wls.size(), kGrain, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++)
+          for (auto& g : wls[i].groups)
+            if (!g.compiled || changed) snap->compile_group(g, simulateEmpty, /*bump=*/false);
+      });
+      snap->compile_gen++;
     }
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
@@ -3361,14 +3478,17 @@ int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash)
     const FlavorSnapshot& s = *h->snap;
     const int L = s.L();
     const int32_t lvl = s.lowestIsHostname ? L - 1 : 0;
-    for (auto& rs : results)
-      for (auto& r : rs) {
-        r.values.resize(r.domains.size());
-        for (size_t k = 0; k < r.domains.size(); k++) {
-          const auto& lv = s.values[size_t(L - 1)][size_t(r.domains[k].leaf)];
-          r.values[k] = {lv.data() + lvl, int32_t(L - lvl), r.domains[k].count};
+    const std::string* const* lv = s.leaf_values();
+    HostPool::get().run(results.size(), 64, [&](size_t b, size_t e) {
+      for (size_t w = b; w < e; w++)
+        for (auto& r : results[w]) {
+          const size_t nd = r.domains.size();
+          r.values.resize(nd);
+          const DomainAssignment* d = r.domains.begin();
+          DomainValues* out = r.values.data();
+          for (size_t k = 0; k < nd; k++) out[k] = {lv[d[k].leaf] + lvl, int32_t(L - lvl), d[k].count};
         }
-      }
+    });
     ev.host_ms[2] += now_ms() - t0;
     ev.host_ms[3] += now_ms() - t0;
   }
