@@ -1253,9 +1253,8 @@ class FlavorSnapshot {
   }
 
   uint64_t compile_gen = 1;  // bumped whenever compiled requests may change
-  // bump = false: the caller bumps compile_gen once for a parallel compile
-  void compile_group(GroupEval& g, bool simulateEmpty, bool bump = true) {
-    if (bump) compile_gen++;
+  void compile_group(GroupEval& g, bool simulateEmpty) {
+    compile_gen++;
     const TASPodSetRequests& w = *g.workers;
     kueue_tas_eval_req& q = g.req;
     memset(&q, 0, sizeof q);
@@ -1817,12 +1816,12 @@ static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Persistent host workers for the per-batch loops that are independent per
-// workload (the request compile of a step, TopologyAssignment values).  The
+// Persistent host workers for per-batch loops that are independent per
+// workload (TopologyAssignment values of a step's results).  The
 // calling thread takes chunks too and only waits for chunks already taken,
 // so a worker still asleep never delays a call; idle workers spin briefly
 // for the next job (steps follow each other within a millisecond), then
-// sleep.  KUEUE_TAS_HOST_THREADS sets the worker count (0: inline).
+// sleep after 2 ms.  KUEUE_TAS_HOST_THREADS sets the worker count (0: inline).
 class HostPool {
  public:
   static HostPool& get() {
@@ -1888,7 +1887,7 @@ class HostPool {
   void loop() {
     uint64_t seen = epoch_.load();
     for (;;) {
-      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(300);
+      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(2000);
       while (epoch_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < spin_until)
         std::this_thread::yield();
       std::shared_ptr<Job> job;
@@ -2047,22 +2046,16 @@ struct Evaluator {
     results->resize(wls.size());
     used.assign(wls.size(), 0);
     if (!precompiled) {
-      // grouping and the prelude are independent per workload: split over
-      // the host pool; only the column check touches the shared snapshot
-      HostPool& pool = HostPool::get();
-      constexpr size_t kGrain = 64;
-      pool.run(wls.size(), kGrain, [&](size_t b, size_t e) {
-        for (size_t i = b; i < e; i++)
-          if (wls[i].groups.empty() || regroup) make_groups(wls[i]);
-      });
+      // serial: split over the host pool this got slower on the GPU box (the
+      // compiled records then sit in other cores' caches when build_pass reads them)
       bool changed = false;
-      for (auto& wl : wls) changed |= snap->ensure_columns_for(wl.podsets);
-      pool.run(wls.size(), kGrain, [&](size_t b, size_t e) {
-        for (size_t i = b; i < e; i++)
-          for (auto& g : wls[i].groups)
-            if (!g.compiled || changed) snap->compile_group(g, simulateEmpty, /*bump=*/false);
-      });
-      snap->compile_gen++;
+      for (auto& wl : wls) {
+        if (wl.groups.empty() || regroup) make_groups(wl);
+        changed |= snap->ensure_columns_for(wl.podsets);
+      }
+      for (auto& wl : wls)
+        for (auto& g : wl.groups)
+          if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
     }
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
