@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tas_internal.h"
 
 namespace ktas {
@@ -36,20 +38,65 @@ namespace ktas {
 __device__ __forceinline__ int32_t w_add(int32_t a, int32_t b) { return int32_t(uint32_t(a) + uint32_t(b)); }
 __device__ __forceinline__ int32_t w_sub(int32_t a, int32_t b) { return int32_t(uint32_t(a) - uint32_t(b)); }
 __device__ __forceinline__ int32_t w_mul(int32_t a, int32_t b) { return int32_t(uint32_t(a) * uint32_t(b)); }
-// Reductions over aligned groups of F lanes (F a power of two, 1..64; every
-// lane of a group gets the group's result): DPP for the steps inside a row of
-// 16 (one VALU each: quad_perm, half-row mirror, row mirror — after the
-// earlier steps every lane of a sub-group holds the same partial, so a mirror
-// reads the other sub-group's), ds_swizzle (xor 16) across the rows of a
-// 32-lane half, ds_bpermute across the halves.
+// ---- lane exchange without LDS ----
+// bfly<M>(v): the partner value of step M of an ASCENDING butterfly (M = 1,
+// 2, 4, ..., 32) in one VALU op: DPP quad_perm for 1 and 2, the half-row and
+// row mirrors for 4 and 8 (after the steps below M every lane of an aligned
+// M-group holds the same partial, so the mirror reads the partner group's),
+// and the gfx950 permlane swaps across rows for 16 and 32 (exact xor: the
+// swap returns the lane's own row value and its partner row's).  No ds_bpermute /
+// ds_swizzle, so no LDS round trip and no lgkmcnt wait per step.
+__device__ __forceinline__ int lane_id();
+template <int M>
+__device__ __forceinline__ uint32_t bfly(uint32_t v) {
+  if constexpr (M == 1) return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  else if constexpr (M == 2) return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  else if constexpr (M == 4) return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  else if constexpr (M == 8) return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  else if constexpr (M == 16) {  // {r0, r1} = {own, partner} in some order; equal values are interchangeable
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return uint32_t(r[0]) == v ? uint32_t(r[1]) : uint32_t(r[0]);
+  } else {
+    static_assert(M == 32, "butterfly steps are 1..32");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return uint32_t(r[0]) == v ? uint32_t(r[1]) : uint32_t(r[0]);
+  }
+}
+template <int M>
+__device__ __forceinline__ uint64_t bfly64(uint64_t v) {
+  return (uint64_t(bfly<M>(uint32_t(v >> 32))) << 32) | bfly<M>(uint32_t(v));
+}
+template <int M>
+__device__ __forceinline__ int32_t bfly_i(int32_t v) { return int32_t(bfly<M>(uint32_t(v))); }
+// Ascending butterfly over the aligned groups of F lanes (F = 1..64):
+// step(integral_constant<M>) folds the partner of step M into the lane's
+// partial; a commutative, associative fold leaves every lane of a group
+// holding the group's result.
+template <class Step>
+__device__ __forceinline__ void butterfly(int F, Step step) {
+  if (F >= 2) step(std::integral_constant<int, 1>());
+  if (F >= 4) step(std::integral_constant<int, 2>());
+  if (F >= 8) step(std::integral_constant<int, 4>());
+  if (F >= 16) step(std::integral_constant<int, 8>());
+  if (F >= 32) step(std::integral_constant<int, 16>());
+  if (F >= 64) step(std::integral_constant<int, 32>());
+}
+// step m of an ascending butterfly (m = 1, 2, 4, ..., 32; see bfly) for
+// reduction loops `for (m = 1; m <= 32; m <<= 1)` (unrolled: m is a constant)
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int m) {
+  switch (m) {
+    case 1: return bfly<1>(v);
+    case 2: return bfly<2>(v);
+    case 4: return bfly<4>(v);
+    case 8: return bfly<8>(v);
+    case 16: return bfly<16>(v);
+    default: return bfly<32>(v);
+  }
+}
+__device__ __forceinline__ int32_t xor_lane(int32_t v, int m) { return int32_t(xor_lane(uint32_t(v), m)); }
 template <class Op>
 __device__ __forceinline__ int32_t group_reduce(int32_t v, int F, Op op) {
-  if (F >= 2) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-  if (F >= 4) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-  if (F >= 8) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-  if (F >= 16) v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));  // row_mirror
-  if (F >= 32) v = op(v, __builtin_amdgcn_ds_swizzle(v, 0x401F));  // bit mode: lane ^ 16
-  if (F >= 64) v = op(v, __shfl_xor(v, 32, 64));
+  butterfly(F, [&](auto m) { v = op(v, bfly_i<decltype(m)::value>(v)); });
   return v;
 }
 struct OpWAdd {
@@ -99,12 +146,6 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
-  lo = __shfl_xor(lo, m, 64);
-  hi = __shfl_xor(hi, m, 64);
-  return (uint64_t(hi) << 32) | lo;
-}
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
   uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
   lo = __shfl(lo, src, 64);
@@ -116,48 +157,47 @@ __device__ __forceinline__ bool key_lt(const Key& a, const Key& b) { return a.hi
 __device__ __forceinline__ bool key_le(const Key& a, const Key& b) { return !key_lt(b, a); }
 __device__ __forceinline__ Key key_max() { return Key{~0ull, ~0ull}; }
 __device__ __forceinline__ Key wave_min_key(Key k) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    Key o{shfl_xor_u64(k.hi, m), shfl_xor_u64(k.lo, m)};
+  butterfly(64, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    const Key o{bfly64<M>(k.hi), bfly64<M>(k.lo)};
     if (key_lt(o, k)) k = o;
-  }
+  });
   return k;
 }
 // Wave arg-min / arg-max over (value, index) pairs: ties keep the smaller
-// (arg-min) or larger (arg-max) index.
+// (arg-min) or larger (arg-max) index (lexicographic, so the butterfly's
+// order does not matter).
 __device__ __forceinline__ void wave_argmin(uint64_t& v, int32_t& i) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    const uint64_t ov = shfl_xor_u64(v, m);
-    const int32_t oi = __shfl_xor(i, m, 64);
+  butterfly(64, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    const uint64_t ov = bfly64<M>(v);
+    const int32_t oi = bfly_i<M>(i);
     if (ov < v || (ov == v && oi < i)) {
       v = ov;
       i = oi;
     }
-  }
+  });
 }
 __device__ __forceinline__ void wave_argmax(uint64_t& v, int32_t& i) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    const uint64_t ov = shfl_xor_u64(v, m);
-    const int32_t oi = __shfl_xor(i, m, 64);
+  butterfly(64, [&](auto m) {
+    constexpr int M = decltype(m)::value;
+    const uint64_t ov = bfly64<M>(v);
+    const int32_t oi = bfly_i<M>(i);
     if (ov > v || (ov == v && oi > i)) {
       v = ov;
       i = oi;
     }
-  }
+  });
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    uint64_t o = shfl_xor_u64(v, m);
+  butterfly(64, [&](auto m) {
+    const uint64_t o = bfly64<decltype(m)::value>(v);
     v = o < v ? o : v;
-  }
+  });
   return v;
 }
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += int64_t(shfl_xor_u64(uint64_t(v), m));
+  butterfly(64, [&](auto m) { v += int64_t(bfly64<decltype(m)::value>(uint64_t(v))); });
   return v;
 }
 __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
@@ -172,11 +212,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
   return x - v;
 }
 
-__device__ __forceinline__ int32_t wave_sum_wrap32(int32_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = w_add(v, __shfl_xor(v, m, 64));
-  return v;
-}
+__device__ __forceinline__ int32_t wave_sum_wrap32(int32_t v) { return group_reduce(v, 64, OpWAdd()); }
 
 __device__ __forceinline__ uint32_t s_asc(int32_t x) { return uint32_t(x) ^ 0x80000000u; }
 __device__ __forceinline__ uint32_t s_desc(int32_t x) { return ~(uint32_t(x) ^ 0x80000000u); }
@@ -505,15 +541,20 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 // Semantics identical to fill_leaves_kernel.
 // Per-eval parameters of a fill chunk, staged in LDS once per block so the
 // per-eval loop has no dependent global loads (eval record -> taint row).
-struct FillEvalParams {
-  int32_t eid, taint_off, nsel, slice_size, slice_level, inner;  // inner: ssal of the leaf level
-  int32_t sel_far;  // a nodeSelector column beyond the kStagedLabels held in registers
-  int32_t run, sig_new;  // signature run (DevBatch::fill_run); 1: first position of its run in the chunk
-  int32_t rmask, lmask;  // the run's worker / leader column masks
-  int32_t aff_begin, aff_end;  // required node affinity requirements; aff_begin < 0: none
-  int32_t dom_begin, dom_end;  // required replacement domain leaf range; dom_begin < 0: none
+// The fields the per-eval loop reads come first, in 16-byte groups: the loop
+// fetches them with three ds_read_b128 and one wait (not one LDS round trip
+// per field), the selector pairs with four more when the eval has selectors.
+struct alignas(16) FillEvalParams {
+  int32_t eid, nsel, slice_size, slice_level;
+  int32_t inner, sel_far, aff_begin, aff_end;  // inner: ssal of the leaf level; sel_far: a nodeSelector
+                                               // column beyond the kStagedLabels held in registers;
+                                               // aff_begin < 0: no required node affinity
+  int32_t dom_begin, dom_end, taint_off, sig_new;  // replacement domain leaf range (dom_begin < 0: none);
+                                                   // sig_new 1: first position of its signature run
+  int32_t run, rmask, lmask, pad;  // signature run (DevBatch::fill_run); the run's worker / leader column masks
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
+static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
@@ -732,13 +773,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // waits (vmcnt) for every store of the earlier evals
   const bool dead = valid && !live;
   for (int e = 0; e < ne; e++) {
-    const FillEvalParams& P = sh_p[e];
+    const int4* pq = reinterpret_cast<const int4*>(&sh_p[e]);
+    const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
     if constexpr (MR) {
-      if (uni(P.sig_new)) count_run(e);  // a new signature run: CountIn once per leaf for the run
+      if (uni(q2.w)) count_run(e);  // sig_new: a new signature run, CountIn once per leaf for the run
     }
-    const int eid = uni(P.eid);
-    const int nsel = uni(P.nsel);
-    const int32_t slice_size = uni(P.slice_size), slice_level = uni(P.slice_level);
+    const int eid = uni(q0.x);
+    const int nsel = uni(q0.y);
+    const int32_t slice_size = uni(q0.z), slice_level = uni(q0.w);
+    const int32_t p_inner = uni(q1.x), sel_far = uni(q1.y), aff_begin = uni(q1.z), aff_end = uni(q1.w);
+    const int32_t dom_begin = uni(q2.x), dom_end = uni(q2.y);
     int32_t state = 0, swl = 0, ls = 0;
     int kind = dead ? EX_DEAD : EX_NONE, id = -1;
     if (valid && kind == EX_NONE) {
@@ -746,7 +790,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         if (s.taint_profile) {
           int t;
           if constexpr (TS) t = sh_taint[e][prof];
-          else t = b.taint_table[uni(P.taint_off) + prof];
+          else t = b.taint_table[uni(q2.z) + prof];
           if (t >= 0) {
             kind = EX_TAINT;
             id = t;
@@ -755,30 +799,29 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         if (kind == EX_NONE && nsel > 0) {
           // two loops: with every column in registers the loop holds no global
           // load, so no vmcnt wait (which would also drain the earlier stores)
-          if (!uni(P.sel_far)) {
-            for (int k = 0; k < nsel; k++) {
-              const int col = uni(P.sel_col[k]);
-              int32_t v = lab[0];
+          const int4 c0 = pq[4], c1 = pq[5], v0 = pq[6], v1 = pq[7];  // sel_col[8], sel_val[8]
+          const int32_t scol[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          const int32_t sval[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          if (!sel_far) {
 #pragma unroll
-              for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
-              if (v != uni(P.sel_val[k])) {
-                kind = EX_SELECTOR;
-                break;
+            for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+              if (k < nsel && kind == EX_NONE) {
+                const int col = uni(scol[k]);
+                int32_t v = lab[0];
+#pragma unroll
+                for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+                if (v != uni(sval[k])) kind = EX_SELECTOR;
               }
             }
           } else {
-            for (int k = 0; k < nsel; k++) {
-              if (label_at(uni(P.sel_col[k])) != uni(P.sel_val[k])) {
-                kind = EX_SELECTOR;
-                break;
-              }
-            }
+#pragma unroll
+            for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++)
+              if (k < nsel && kind == EX_NONE && label_at(uni(scol[k])) != uni(sval[k])) kind = EX_SELECTOR;
           }
         }
-        const int ab = uni(P.aff_begin);
-        if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(P.aff_end), leaf, label_at)) kind = EX_AFFINITY;
+        if (kind == EX_NONE && aff_begin >= 0 && !affinity_match(b, aff_begin, aff_end, leaf, label_at)) kind = EX_AFFINITY;
       }
-      if (kind == EX_NONE && outside_domain(uni(P.dom_begin), uni(P.dom_end), leaf)) kind = EX_TOPOLOGY;
+      if (kind == EX_NONE && outside_domain(dom_begin, dom_end, leaf)) kind = EX_TOPOLOGY;
       if (kind == EX_NONE) {
         state = state0;
         swl = swl0;
@@ -815,7 +858,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       // power-of-two fan-out F <= 64, parent p owns leaves [p*F, (p+1)*F), so
       // a parent's children are F aligned lanes of one wave (xor reductions).
       const int F = b.rack_fanout;
-      const int32_t inner = uni(P.inner);
+      const int32_t inner = p_inner;
       int32_t cs = state, csw = swl;
       if (inner != 0 && inner != 1) {  // wave-uniform; x / 1 * 1 == x
         cs = w_mul(go_div32(cs, inner), inner);
@@ -1171,13 +1214,13 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
       lead = max(cls, lead);
     }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      cap = w_add(cap, __shfl_xor(cap, m, 64));
-      slc = w_add(slc, __shfl_xor(slc, m, 64));
-      minD = min(minD, __shfl_xor(minD, m, 64));
-      minSD = min(minSD, __shfl_xor(minSD, m, 64));
-      lead = max(lead, __shfl_xor(lead, m, 64));
-      has |= __shfl_xor(has, m, 64);
+    for (int m = 1; m <= 32; m <<= 1) {
+      cap = w_add(cap, xor_lane(cap, m));
+      slc = w_add(slc, xor_lane(slc, m));
+      minD = min(minD, xor_lane(minD, m));
+      minSD = min(minSD, xor_lane(minSD, m));
+      lead = max(lead, xor_lane(lead, m));
+      has |= xor_lane(has, m);
     }
     if (lane == 0) {
       int32_t state = cap;
@@ -1866,8 +1909,8 @@ __device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* 
     uint32_t r = m == 1 ? ~0u : 0u;
     for (int i = lane; i < cnt; i += kWave) r = m == 1 ? min(r, v[i]) : max(r, v[i]);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      const uint32_t o = __shfl_xor(r, d, 64);
+    for (int d = 1; d <= 32; d <<= 1) {
+      const uint32_t o = xor_lane(r, d);
       r = m == 1 ? min(r, o) : max(r, o);
     }
     return r;
@@ -2010,10 +2053,10 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   }
   wsum = wave_sum_i64(wsum);
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    vmin = min(vmin, __shfl_xor(vmin, m, 64));
-    vmax = max(vmax, __shfl_xor(vmax, m, 64));
-    wmin = min(wmin, __shfl_xor(wmin, m, 64));
+  for (int m = 1; m <= 32; m <<= 1) {
+    vmin = min(vmin, xor_lane(vmin, m));
+    vmax = max(vmax, xor_lane(vmax, m));
+    wmin = min(wmin, xor_lane(wmin, m));
   }
   const bool all_eq = ballot(neq) == 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
@@ -2061,9 +2104,9 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
       }
     });
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      umin = min(umin, __shfl_xor(umin, m, 64));
-      umax = max(umax, __shfl_xor(umax, m, 64));
+    for (int m = 1; m <= 32; m <<= 1) {
+      umin = min(umin, xor_lane(umin, m));
+      umax = max(umax, xor_lane(umax, m));
     }
     if (int64_t(umax) - int64_t(umin) >= kThrBins) return -1;
     // pass D: weight per state value inside class t
@@ -2475,7 +2518,7 @@ __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
     uint32_t rank = s.id_rank ? uint32_t(s.id_rank[loff + i]) : uint32_t(i);
     if (rank == brank) bidx = i;
   }
-  for (int m = 32; m >= 1; m >>= 1) bidx = max(bidx, __shfl_xor(bidx, m, 64));
+  for (int m = 1; m <= 32; m <<= 1) bidx = max(bidx, xor_lane(bidx, m));
   for (int c = 0; c < w.ev->num_layers && c < KUEUE_TAS_MAX_LAYERS; c++) {
     int t = w.ev->layer_level[c];
     int32_t size = w.ev->layer_size[c];
@@ -2524,9 +2567,9 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
       mx = max(mx, g - loff);
     });
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      mn = min(mn, __shfl_xor(mn, m, 64));
-      mx = max(mx, __shfl_xor(mx, m, 64));
+    for (int m = 1; m <= 32; m <<= 1) {
+      mn = min(mn, xor_lane(mn, m));
+      mx = max(mx, xor_lane(mx, m));
     }
     const int64_t words = (int64_t(mx) - mn + 32) / 32;
     if (words * 4 <= int64_t(w.cap) * int64_t(sizeof(Key))) {
@@ -2838,7 +2881,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
       if (x >= lo && x < vmin) vmin = x;
     }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) vmin = min(vmin, __shfl_xor(vmin, m, 64));
+    for (int m = 1; m <= 32; m <<= 1) vmin = min(vmin, xor_lane(vmin, m));
     if (vmin == 0x7fffffff) break;
     lo = vmin;
     for (int i = lane_id(); i < kW; i += kWave) hist[i] = 0;
@@ -3169,7 +3212,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       inv = wave_min_key(inv);
       last = Key{~inv.hi, ~inv.lo};
     }
-    for (int m = 32; m >= 1; m >>= 1) minss = min(minss, __shfl_xor(minss, m, 64));
+    for (int m = 1; m <= 32; m <<= 1) minss = min(minss, xor_lane(minss, m));
     int topg = loff + int(uint32_t(top.lo));
     if (w.bf && w.get(F_SSWL, topg) >= sliceCount && w.get(F_LS, topg) >= leaderCount) {
       // findBestFitDomainForSlices(sorted, sliceCount, leaderCount)
@@ -3726,12 +3769,12 @@ __global__ __launch_bounds__(256) void encode_v1beta2_kernel(EncodeArgs a) {
     S = min(S, q);
     if (k == 0) same &= (a.ids ? a.counts[j] : a.pairs[2 * j + 1]) == c0;
   }
-  for (int d = 32; d >= 1; d >>= 1) {
-    P = min(P, __shfl_xor(P, d, 64));
-    S = min(S, __shfl_xor(S, d, 64));
-    mn = min(mn, __shfl_xor(mn, d, 64));
-    mx = max(mx, __shfl_xor(mx, d, 64));
-    same &= __shfl_xor(same, d, 64);
+  for (int d = 1; d <= 32; d <<= 1) {
+    P = min(P, xor_lane(P, d));
+    S = min(S, xor_lane(S, d));
+    mn = min(mn, xor_lane(mn, d));
+    mx = max(mx, xor_lane(mx, d));
+    same &= xor_lane(same, d);
   }
   if (lane == 0) {
     red[wave][0] = P;

@@ -118,6 +118,26 @@ inline int __builtin_amdgcn_ds_swizzle(int v, int pattern) {
   const int src = (l & ~31) | ((((l & 31) & and_m) | or_m) ^ xor_m);
   return int(emu::wave_exchange(uint64_t(uint32_t(v)), src));
 }
+// gfx950 v_permlane16_swap / v_permlane32_swap with vdst = old, vsrc = src:
+// the odd 16-lane rows (upper 32-lane half) of vdst trade places with the
+// even rows (lower half) of vsrc; returns {vdst', vsrc'}
+struct emu_u32x2 {
+  uint32_t v[2];
+  uint32_t operator[](int i) const { return v[i]; }
+};
+inline emu_u32x2 emu_permlane_swap(uint32_t old, uint32_t src, int span) {
+  const int l = __lane_of_cur();
+  const uint32_t o = uint32_t(emu::wave_exchange(uint64_t(old), l ^ span));
+  const uint32_t s = uint32_t(emu::wave_exchange(uint64_t(src), l ^ span));
+  if (l & span) return {{s, src}};  // vdst' = src of the partner row, vsrc' keeps its own
+  return {{old, o}};                // vdst' keeps its own, vsrc' = old of the partner row
+}
+inline emu_u32x2 __builtin_amdgcn_permlane16_swap(uint32_t old, uint32_t src, bool, bool) {
+  return emu_permlane_swap(old, src, 16);
+}
+inline emu_u32x2 __builtin_amdgcn_permlane32_swap(uint32_t old, uint32_t src, bool, bool) {
+  return emu_permlane_swap(old, src, 32);
+}
 template <typename T>
 inline T __shfl_xor(T v, int mask, int width = 64) {
   (void)width;
