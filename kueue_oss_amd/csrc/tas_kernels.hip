@@ -200,15 +200,18 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
   butterfly(64, [&](auto m) { v += int64_t(bfly64<decltype(m)::value>(uint64_t(v))); });
   return v;
 }
+// Exclusive wave scan (int add) with DPP, no LDS: row_shr 1/2/4/8 scan each
+// row of 16, row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the
+// row totals; the total is lane 63's inclusive sum (v_readlane).
 __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
-  const int lane = lane_id();
   int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl(x, max(lane - d, 0), 64);
-    if (lane >= d) x += y;
-  }
-  *total = __shfl(x, 63, 64);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  *total = __builtin_amdgcn_readlane(x, 63);
   return x - v;
 }
 

@@ -102,15 +102,32 @@ inline T __shfl(T v, int src, int width = 64) {
   return out;
 }
 // DPP / swizzle lane permutations (the controls the kernels use)
-inline int __builtin_amdgcn_update_dpp(int, int v, int ctrl, int, int, bool) {
+inline int __builtin_amdgcn_update_dpp(int old, int v, int ctrl, int row_mask, int, bool bound_ctrl) {
   const int l = __lane_of_cur();
-  int src;
+  const int row = l >> 4;
+  int src = l;
+  bool ok = true;
   if (ctrl < 0x100) src = (l & ~3) | ((ctrl >> (2 * (l & 3))) & 3);  // quad_perm
   else if (ctrl == 0x140) src = (l & ~15) | (15 - (l & 15));          // row_mirror
   else if (ctrl == 0x141) src = (l & ~7) | (7 - (l & 7));             // row_half_mirror
-  else abort();
-  return int(emu::wave_exchange(uint64_t(uint32_t(v)), src));
+  else if (ctrl > 0x110 && ctrl <= 0x11F) {                           // row_shr:n
+    src = l - (ctrl - 0x110);
+    ok = src >= 0 && (src >> 4) == row;
+  } else if (ctrl == 0x142) {  // row_bcast:15: lane 15 of the previous row
+    src = row * 16 - 1;
+    ok = row > 0;
+  } else if (ctrl == 0x143) {  // row_bcast:31: lane 31 to rows 2 and 3
+    src = 31;
+    ok = row >= 2;
+  } else {
+    abort();
+  }
+  const int r = int(emu::wave_exchange(uint64_t(uint32_t(v)), ok ? src : l));  // collective: every lane calls
+  if (!((row_mask >> row) & 1)) return old;  // disabled row: not written
+  if (!ok) return bound_ctrl ? 0 : old;
+  return r;
 }
+inline int __builtin_amdgcn_readlane(int v, int lane) { return int(emu::wave_exchange(uint64_t(uint32_t(v)), lane & 63)); }
 inline int __builtin_amdgcn_ds_swizzle(int v, int pattern) {
   if (pattern & 0x8000) abort();  // bit mode only
   const int l = __lane_of_cur();
