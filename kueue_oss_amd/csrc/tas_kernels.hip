@@ -146,11 +146,15 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// value of lane `src` (wave-uniform: a ballot's first set bit, 0, 63) by
+// v_readlane into an SGPR, no LDS round trip
+template <class T>
+__device__ __forceinline__ T bcast(T v, int src) {
+  static_assert(sizeof(T) == 4, "32-bit lane values");
+  return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
-  lo = __shfl(lo, src, 64);
-  hi = __shfl(hi, src, 64);
-  return (uint64_t(hi) << 32) | lo;
+  return (uint64_t(bcast(uint32_t(v >> 32), src)) << 32) | bcast(uint32_t(v), src);
 }
 
 __device__ __forceinline__ bool key_lt(const Key& a, const Key& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
@@ -203,14 +207,17 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 // Exclusive wave scan (int add) with DPP, no LDS: row_shr 1/2/4/8 scan each
 // row of 16, row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the
 // row totals; the total is lane 63's inclusive sum (v_readlane).
-__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
-  int x = v;
+__device__ __forceinline__ int wave_incl_scan(int x) {  // wrapping int add
   x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
   x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
   x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int x = wave_incl_scan(v);
   *total = __builtin_amdgcn_readlane(x, 63);
   return x - v;
 }
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
-      int tid = __shfl(id, src, 64);
+      int tid = bcast(id, src);
       uint64_t mm = ballot(kind == EX_TAINT && id == tid);
       if (lane == 0) atomicAdd(&b.taint_counts[int64_t(eid) * b.num_taints + tid], __popcll(mm));
       tm &= ~mm;
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
     uint64_t rm = ballot(kind == EX_RESOURCE);
     while (rm) {
       int src = __ffsll((unsigned long long)rm) - 1;
-      int rid = __shfl(id, src, 64);
+      int rid = bcast(id, src);
       uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
       if (lane == 0) atomicAdd(&b.res_counts[int64_t(eid) * s.R + rid], __popcll(mm));
       rm &= ~mm;
@@ -927,7 +934,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
       int src = __ffsll((unsigned long long)tm) - 1;
-      int tid = __shfl(id, src, 64);
+      int tid = bcast(id, src);
       uint64_t mm = ballot(kind == EX_TAINT && id == tid);
       if (lane == 0) {
         if (lds_stats) atomicAdd(&sh_stats[e][kStatFixed + tid], __popcll(mm));
@@ -938,7 +945,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     uint64_t rm = ballot(kind == EX_RESOURCE);
     while (rm) {
       int src = __ffsll((unsigned long long)rm) - 1;
-      int rid = __shfl(id, src, 64);
+      int rid = bcast(id, src);
       uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
       if (lane == 0) {
         if (lds_stats) atomicAdd(&sh_stats[e][kStatFixed + b.num_taints + rid], __popcll(mm));
@@ -1063,14 +1070,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     if (lane == 0 && domm) atomicAdd(&sh_stats[e][2], __popcll(domm));
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
-      const int tid = __shfl(id, __ffsll((unsigned long long)tm) - 1, 64);
+      const int tid = bcast(id, __ffsll((unsigned long long)tm) - 1);
       const uint64_t mm = ballot(kind == EX_TAINT && id == tid);
       if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + tid], __popcll(mm));
       tm &= ~mm;
     }
     uint64_t rm = ballot(kind == EX_RESOURCE);
     while (rm) {
-      const int rid = __shfl(id, __ffsll((unsigned long long)rm) - 1, 64);
+      const int rid = bcast(id, __ffsll((unsigned long long)rm) - 1);
       const uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
       if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + b.num_taints + rid], __popcll(mm));
       rm &= ~mm;
@@ -1362,7 +1369,7 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
     uint64_t pending = ballot(act);
     while (pending) {
       const int src = __ffsll((unsigned long long)pending) - 1;
-      const int b0 = __shfl(bin, src, 64);
+      const int b0 = bcast(bin, src);
       const uint64_t m = ballot(act && bin == b0);
       if (lane == src) atomicAdd(&h[b0], uint32_t(__popcll(m)));
       pending &= ~m;
@@ -1938,11 +1945,7 @@ __device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* 
       c[k] = k < PER ? hist[PER * lane + k] : 0u;
       lsum += c[k];
     }
-    uint32_t x = lsum;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl(x, max(lane - d, 0), 64);
-      if (lane >= d) x += y;
-    }
+    const uint32_t x = uint32_t(wave_incl_scan(int(lsum)));
     const uint64_t hit = ballot(x >= uint32_t(m));
     const int src = __ffsll((unsigned long long)hit) - 1;  // exists: m <= matching count
     int digit = 0;
@@ -1952,8 +1955,8 @@ __device__ uint32_t lds_select_kth(const uint32_t* v, int cnt, int m, uint32_t* 
       while (k < PER - 1 && before + c[k] < uint32_t(m)) before += c[k++];
       digit = PER * lane + k;
     }
-    digit = __shfl(digit, src, 64);
-    before = __shfl(before, src, 64);
+    digit = bcast(digit, src);
+    before = bcast(before, src);
     m -= int(before);
     prefix |= uint32_t(digit) << shift;
     pmask |= uint32_t(NB - 1) << shift;
@@ -2000,7 +2003,7 @@ __device__ int bins_threshold(const uint64_t* hist, bool desc, int64_t need, int
       }
     }
   }
-  pp = __shfl(pp, src, 64);
+  pp = bcast(pp, src);
   *before = int64_t(shfl_u64(uint64_t(bb), src));
   return desc ? kThrBins - 1 - pp : pp;
 }
@@ -2456,7 +2459,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
     wave_sync();
     const int nparents = min(kWave, n - i0);
     // uniform power-of-two fan-out in this step: element e belongs to parent e >> sh
-    const int f0 = __shfl(cnt, 0, 64);
+    const int f0 = bcast(cnt, 0);
     const bool uniform = f0 > 0 && (f0 & (f0 - 1)) == 0 && ballot(i < n && cnt != f0) == 0;
     const int sh = uniform ? __builtin_ctz(f0) : 0;
     for (int b0 = 0; b0 < tot; b0 += kU * kWave) {
@@ -2734,7 +2737,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
           }
         }
       }
-      t = __shfl(tt, src, 64);
+      t = bcast(tt, src);
       before = int64_t(shfl_u64(uint64_t(bb), src));
     } else {
       before = int64_t(shfl_u64(uint64_t(x), 63));
@@ -2955,7 +2958,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
   LfcJob job{0, 0, 0, 0};
   static_assert(kLfcBins == 128, "two bins per lane");
   const uint32_t h0 = tot[lane], h1 = tot[lane + 64];
-  const uint32_t nover = __shfl(h1, 63, 64);
+  const uint32_t nover = bcast(h1, 63);
   // LFC first fit (:1260-1265)
   int fit_leaf = -1;
   if (need <= kLfcBins - 2) {
@@ -3014,7 +3017,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
       before = ex + l0;
       below = ey + c0;
     }
-    t = __shfl(t, src, 64);
+    t = bcast(t, src);
     before = int64_t(shfl_u64(uint64_t(before), src));
     below = int64_t(shfl_u64(uint64_t(below), src));
     const int64_t mt = (int64_t(need) - before + t - 1) / t;
@@ -3048,7 +3051,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
       if (has) {
         int first = 0;
         if (lane == 0) first = atomicAdd(b.lfc_nitems, __popcll(has));
-        first = __shfl(first, 0, 64);
+        first = bcast(first, 0);
         if (nkeep > 0) {
           LfcItem it;
           it.eid = w.eid;
