@@ -153,8 +153,15 @@ __device__ __forceinline__ T bcast(T v, int src) {
   static_assert(sizeof(T) == 4, "32-bit lane values");
   return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
 }
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+__device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
   return (uint64_t(bcast(uint32_t(v >> 32), src)) << 32) | bcast(uint32_t(v), src);
+}
+// per-lane source (scans, gathers): ds_bpermute
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  lo = __shfl(lo, src, 64);
+  hi = __shfl(hi, src, 64);
+  return (uint64_t(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ bool key_lt(const Key& a, const Key& b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
@@ -1988,7 +1995,7 @@ __device__ int bins_threshold(const uint64_t* hist, bool desc, int64_t need, int
   const int64_t excl = x - lsum;
   const uint64_t m = ballot(x >= need);
   if (!m) {
-    *before = int64_t(shfl_u64(uint64_t(x), 63));
+    *before = int64_t(bcast64(uint64_t(x), 63));
     return -1;
   }
   const int src = __ffsll((unsigned long long)m) - 1;
@@ -2004,7 +2011,7 @@ __device__ int bins_threshold(const uint64_t* hist, bool desc, int64_t need, int
     }
   }
   pp = bcast(pp, src);
-  *before = int64_t(shfl_u64(uint64_t(bb), src));
+  *before = int64_t(bcast64(uint64_t(bb), src));
   return desc ? kThrBins - 1 - pp : pp;
 }
 
@@ -2248,10 +2255,10 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
     if (m) {
       const int src = __ffsll((unsigned long long)m) - 1;
       cross = i0 + src;
-      before = run + int64_t(shfl_u64(uint64_t(x - wt), src));
+      before = run + int64_t(bcast64(uint64_t(x - wt), src));
       break;
     }
-    run += int64_t(shfl_u64(uint64_t(x), 63));
+    run += int64_t(bcast64(uint64_t(x), 63));
   }
   if (cross < 0) return 0;
   const int32_t remc = int32_t(rem - before);
@@ -2725,7 +2732,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
     uint64_t m = ballot(x >= need);
     if (m) {
       int src = __ffsll((unsigned long long)m) - 1;
-      int64_t e = int64_t(shfl_u64(uint64_t(excl), src));
+      int64_t e = int64_t(bcast64(uint64_t(excl), src));
       int tt = -1;
       int64_t bb = e;
       if (lane_id() == src) {
@@ -2738,9 +2745,9 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
         }
       }
       t = bcast(tt, src);
-      before = int64_t(shfl_u64(uint64_t(bb), src));
+      before = int64_t(bcast64(uint64_t(bb), src));
     } else {
-      before = int64_t(shfl_u64(uint64_t(x), 63));
+      before = int64_t(bcast64(uint64_t(x), 63));
     }
   }
   if (t < 0) {
@@ -3018,8 +3025,8 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
       below = ey + c0;
     }
     t = bcast(t, src);
-    before = int64_t(shfl_u64(uint64_t(before), src));
-    below = int64_t(shfl_u64(uint64_t(below), src));
+    before = int64_t(bcast64(uint64_t(before), src));
+    below = int64_t(bcast64(uint64_t(below), src));
     const int64_t mt = (int64_t(need) - before + t - 1) / t;
     job.t = t;
     job.m = int32_t(mt);
@@ -3064,8 +3071,8 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
     }
     return job;
   }
-  const int64_t bins_mass = int64_t(shfl_u64(uint64_t(x), 63));
-  const int64_t bins_cnt = int64_t(shfl_u64(uint64_t(y), 63));
+  const int64_t bins_mass = int64_t(bcast64(uint64_t(x), 63));
+  const int64_t bins_cnt = int64_t(bcast64(uint64_t(y), 63));
   const int64_t total = bins_mass + int64_t(b.lfc_ovtot[slot]);
   if (total < need) {  // not enough capacity: remaining = need - total (:1315-1316)
     not_fit(w, L1, int32_t(total), need, o);

@@ -127,7 +127,16 @@ inline int __builtin_amdgcn_update_dpp(int old, int v, int ctrl, int row_mask, i
   if (!ok) return bound_ctrl ? 0 : old;
   return r;
 }
-inline int __builtin_amdgcn_readlane(int v, int lane) { return int(emu::wave_exchange(uint64_t(uint32_t(v)), lane & 63)); }
+// v_readlane takes its lane from an SGPR: a lane index that differs across
+// the wave is a kernel bug (hardware would use one lane's index for all)
+inline int __builtin_amdgcn_readlane(int v, int lane) {
+  const int lane0 = int(emu::wave_exchange(uint64_t(uint32_t(lane)), 0));
+  if (emu::wave_ballot(lane != lane0) != 0) {
+    fprintf(stderr, "emu: __builtin_amdgcn_readlane with a non-uniform lane index\n");
+    abort();
+  }
+  return int(emu::wave_exchange(uint64_t(uint32_t(v)), lane & 63));
+}
 inline int __builtin_amdgcn_ds_swizzle(int v, int pattern) {
   if (pattern & 0x8000) abort();  // bit mode only
   const int l = __lane_of_cur();
