@@ -1401,11 +1401,22 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.rack_pos = c->d_rack_pos.p;
     }
     const bool ts = b.num_profiles <= kStagedProfiles;
+    // global lookups in the eval loop: a nodeSelector column beyond the
+    // staged label columns, or required node affinity
+    bool gl = false;
+    for (size_t i = 0; i < n && !gl; i++) {
+      gl = (reqs[i].flags & KUEUE_TAS_F_AFFINITY) != 0;
+      for (int k = 0; k < reqs[i].num_selectors; k++) gl = gl || reqs[i].sel_col[k] >= kStagedLabels;
+    }
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
     auto staged = [&](auto ns, auto tsv, auto mr, int first, int count) {
       if (count <= 0) return;
-      hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value>),
-                         dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+      if (gl)
+        hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, true>),
+                           dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+      else
+        hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, false>),
+                           dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
     };
     auto staged2 = [&](auto ns, auto tsv) {
       staged(ns, tsv, std::false_type(), 0, nsingle);

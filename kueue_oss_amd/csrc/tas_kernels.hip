@@ -588,7 +588,12 @@ constexpr int kMaxFillStats = 64;  // kStatFixed + taints + resource columns; mo
 // MR: the launch's chunks hold several signature runs (CountIn per run inside
 // the eval loop); otherwise one run per chunk, counted before the loop (fewer
 // live registers: higher occupancy).  chunk_base: first chunk of the launch.
-template <int NS, bool TS, bool MR>
+// GL: some eval of the launch needs global lookups in the eval loop (a
+// nodeSelector column beyond the staged ones, required node affinity).
+// Without it the loop holds no global load at all: on gfx9 vmcnt counts
+// stores too, so a load's wait inside the loop would drain every store of
+// the earlier evals.
+template <int NS, bool TS, bool MR, bool GL>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                           int chunk_base) {
   __shared__ FillEvalParams sh_p[kEvalsPerBlock];
@@ -789,6 +794,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // loads the per-eval loop needs, hoisted: a global load inside the loop
   // waits (vmcnt) for every store of the earlier evals
   const bool dead = valid && !live;
+  const int rack_f = b.rack_fanout;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_p[e]);
     const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
@@ -819,7 +825,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
           const int4 c0 = pq[4], c1 = pq[5], v0 = pq[6], v1 = pq[7];  // sel_col[8], sel_val[8]
           const int32_t scol[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
           const int32_t sval[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          if (!sel_far) {
+          if (!GL || !sel_far) {
 #pragma unroll
             for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
               if (k < nsel && kind == EX_NONE) {
@@ -836,7 +842,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
               if (k < nsel && kind == EX_NONE && label_at(uni(scol[k])) != uni(sval[k])) kind = EX_SELECTOR;
           }
         }
-        if (kind == EX_NONE && aff_begin >= 0 && !affinity_match(b, aff_begin, aff_end, leaf, label_at)) kind = EX_AFFINITY;
+        if constexpr (GL) {
+          if (kind == EX_NONE && aff_begin >= 0 && !affinity_match(b, aff_begin, aff_end, leaf, label_at)) kind = EX_AFFINITY;
+        }
       }
       if (kind == EX_NONE && outside_domain(dom_begin, dom_end, leaf)) kind = EX_TOPOLOGY;
       if (kind == EX_NONE) {
@@ -870,11 +878,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         base[4 * SD + gleaf] = ls;
       }
     }
-    if (b.rack_fanout) {
-      // fused fillInCountsHelper (:1658-1719) of the leaves' parents: uniform
-      // power-of-two fan-out F <= 64, parent p owns leaves [p*F, (p+1)*F), so
-      // a parent's children are F aligned lanes of one wave (xor reductions).
-      const int F = b.rack_fanout;
+    // fused fillInCountsHelper (:1658-1719) of the leaves' parents: uniform
+    // power-of-two fan-out F <= 64, parent p owns leaves [p*F, (p+1)*F), so
+    // a parent's children are F aligned lanes of one wave (butterfly
+    // reductions).  F = 32 / 64 compile-time: no per-step fan-out tests.
+    auto rack_rollup = [&](auto FC) {
+      const int F = decltype(FC)::value > 0 ? int(decltype(FC)::value) : b.rack_fanout;
       const int32_t inner = p_inner;
       int32_t cs = state, csw = swl;
       if (inner != 0 && inner != 1) {  // wave-uniform; x / 1 * 1 == x
@@ -921,7 +930,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
           base[4 * SD + g] = lead;
         }
       }
-    }
+    };
+    if (rack_f == 32) rack_rollup(std::integral_constant<int, 32>());
+    else if (rack_f == 64) rack_rollup(std::integral_constant<int, 64>());
+    else if (rack_f) rack_rollup(std::integral_constant<int, 0>());
     if (split) continue;
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) {

@@ -19,11 +19,14 @@ EXP = os.path.join(ROOT, "_exp")
 K = "tas_kernels.hip"
 VARIANTS = {
     "base": [],
-    "no_loop": [("  for (int e = 0; e < ne; e++) {\n    const FillEvalParams& P = sh_p[e];",
-                 "  for (int e = 0; e < (state0 == -7 ? ne : 0); e++) {\n    const FillEvalParams& P = sh_p[e];")],
+    "no_loop": [("  for (int e = 0; e < ne; e++) {\n    const int4* pq",
+                 "  for (int e = 0; e < (state0 == -7 ? ne : 0); e++) {\n    const int4* pq")],
     "no_excl": [("    if (valid && kind == EX_NONE) {\n      if (s.lowest_is_hostname) {\n        if (s.taint_profile) {\n          int t;",
                  "    if (valid && kind == EX_NONE) {\n      if (false) {\n        if (s.taint_profile) {\n          int t;")],
     "no_rack": [("    if (b.rack_fanout) {\n      // fused", "    if (false) {\n      // fused")],
+    "no_leaf_store": [("    if (valid) {\n      base[gleaf] = state;", "    if (valid && state == -7) {\n      base[gleaf] = state;")],
+    "no_store_no_rack": [("    if (valid) {\n      base[gleaf] = state;", "    if (valid && state == -7) {\n      base[gleaf] = state;"),
+                         ("    if (b.rack_fanout) {\n      // fused", "    if (false) {\n      // fused")],
 }
 
 
