@@ -1379,13 +1379,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->last_stats[0] += nfill;
   if (s.N > 0 && nfchunks > 0) {
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
+    // the staged kernels take kFillTilesPerBlock leaf tiles per block
+    const bool staged_fill = ucols <= 8;
+    const unsigned sgx = (grid.x + kFillTilesPerBlock - 1) / kFillTilesPerBlock;
+    const unsigned nblk_fill = staged_fill ? sgx : grid.x;  // blocks per fill position (stats partials)
     c->last_stats[2] += 1;
     c->last_stats[3] = ucols;
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
     if (b.nstat) {
-      HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * grid.x * size_t(nstat)));
+      // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
+      HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * std::max(grid.x, nblk_fill) * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
     }
     if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
@@ -1413,10 +1418,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (count <= 0) return;
       if (gl)
         hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, true>),
-                           dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+                           dim3(sgx, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
       else
         hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, false>),
-                           dim3(grid.x, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+                           dim3(sgx, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
     };
     auto staged2 = [&](auto ns, auto tsv) {
       staged(ns, tsv, std::false_type(), 0, nsingle);
@@ -1434,7 +1439,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
     if (b.nstat && !b.stats_split) {  // ExclusionStats counted inside the fill
-      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(grid.x));
+      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(nblk_fill));
       HIPCHK(c, hipGetLastError());
     }
   }

@@ -572,6 +572,7 @@ struct alignas(16) FillEvalParams {
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
+constexpr int kFillTilesPerBlock = 2;  // leaf tiles of one staged-fill block
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
@@ -609,12 +610,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // and land on the same XCD back to back, where the tile's snapshot columns
   // are still in that XCD's L2 (each chunk re-reads them).  A bijection of
   // the 2-D grid; identity when the tile count is not a multiple of 8.
-  int tile = blockIdx.x, chunk = blockIdx.y;
+  int tgroup = blockIdx.x, chunk = blockIdx.y;
   if ((gridDim.x & 7u) == 0 && gridDim.y > 1) {
     const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
     const uint32_t g = lin >> 3;
     chunk = int(g % gridDim.y);
-    tile = int((g / gridDim.y) * 8u + (lin & 7u));
+    tgroup = int((g / gridDim.y) * 8u + (lin & 7u));
   }
   chunk += chunk_base;
   const int e0 = b.fill_chunks[2 * chunk];
@@ -661,6 +662,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     if (j >= NS && j - NS < ev.nlead) sh_term[e][j] = b.terms[ev.lead_begin + (j - NS)];
   }
   __syncthreads();
+  // kFillTilesPerBlock consecutive leaf tiles per block: the setup above
+  // (chunk parameters, terms, taint rows: dependent global loads) is paid
+  // once per block, and the grid fits one residency round
+  const int ntiles = (s.N + kFillThreads - 1) / kFillThreads;
+  for (int tile = tgroup * kFillTilesPerBlock; tile < min(ntiles, (tgroup + 1) * kFillTilesPerBlock); tile++) {
   const int leaf = tile * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
   const int N = s.N;
@@ -973,11 +979,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       rm &= ~mm;
     }
   }
+  }  // tiles
   if (lds_stats) {  // per-block partials [fill position][block][stat]
     __syncthreads();
     for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
       const int e = i / b.nstat, k = i % b.nstat;
-      b.fill_stats[(int64_t(e0 + e) * gridDim.x + tile) * b.nstat + k] = sh_stats[e][k];
+      b.fill_stats[(int64_t(e0 + e) * gridDim.x + tgroup) * b.nstat + k] = sh_stats[e][k];
     }
   }
 }

@@ -23,10 +23,14 @@ VARIANTS = {
                  "  for (int e = 0; e < (state0 == -7 ? ne : 0); e++) {\n    const int4* pq")],
     "no_excl": [("    if (valid && kind == EX_NONE) {\n      if (s.lowest_is_hostname) {\n        if (s.taint_profile) {\n          int t;",
                  "    if (valid && kind == EX_NONE) {\n      if (false) {\n        if (s.taint_profile) {\n          int t;")],
-    "no_rack": [("    if (b.rack_fanout) {\n      // fused", "    if (false) {\n      // fused")],
+    "no_rack": [("  const int rack_f = b.rack_fanout;", "  const int rack_f = 0;")],
     "no_leaf_store": [("    if (valid) {\n      base[gleaf] = state;", "    if (valid && state == -7) {\n      base[gleaf] = state;")],
+    "no_loop_no_count": [("  for (int e = 0; e < ne; e++) {\n    const int4* pq",
+                          "  for (int e = 0; e < (state0 == -7 ? ne : 0); e++) {\n    const int4* pq"),
+                         ("  if constexpr (!MR) count_run(0);", "  if constexpr (!MR) { if (ne < 0) count_run(0); }")],
+    "no_count": [("  if constexpr (!MR) count_run(0);", "  if constexpr (!MR) { if (ne < 0) count_run(0); }")],
     "no_store_no_rack": [("    if (valid) {\n      base[gleaf] = state;", "    if (valid && state == -7) {\n      base[gleaf] = state;"),
-                         ("    if (b.rack_fanout) {\n      // fused", "    if (false) {\n      // fused")],
+                         ("  const int rack_f = b.rack_fanout;", "  const int rack_f = 0;")],
 }
 
 
