@@ -1414,29 +1414,43 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       for (int k = 0; k < reqs[i].num_selectors; k++) gl = gl || reqs[i].sel_col[k] >= kStagedLabels;
     }
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
-    auto staged = [&](auto ns, auto tsv, auto mr, int first, int count) {
+    auto staged = [&](auto ns, auto tsv, auto mr, int first, int count, hipStream_t st) {
       if (count <= 0) return;
       if (gl)
         hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, true>),
-                           dim3(sgx, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+                           dim3(sgx, unsigned(count)), dim3(256), 0, st, s, b, umask, first);
       else
         hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, false>),
-                           dim3(sgx, unsigned(count)), dim3(256), 0, c->stream, s, b, umask, first);
+                           dim3(sgx, unsigned(count)), dim3(256), 0, st, s, b, umask, first);
     };
-    auto staged2 = [&](auto ns, auto tsv) {
-      staged(ns, tsv, std::false_type(), 0, nsingle);
-      staged(ns, tsv, std::true_type(), nsingle, nfchunks - nsingle);
+    // the multi-run chunks (a few small signatures) run beside the single-run
+    // chunks on stream2 (idle until the fill is done): their launch's ramp and
+    // tail overlap the big launch instead of following it
+    auto staged2 = [&](auto ns, auto tsv) -> int {
+      const bool side = nsingle > 0 && nfchunks > nsingle;
+      if (side) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[1], 0));
+        staged(ns, tsv, std::true_type(), nsingle, nfchunks - nsingle, c->stream2);
+        HIPCHK(c, hipEventRecord(c->evl[2], c->stream2));
+      } else {
+        staged(ns, tsv, std::true_type(), nsingle, nfchunks - nsingle, c->stream);
+      }
+      staged(ns, tsv, std::false_type(), 0, nsingle, c->stream);
+      if (side) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[2], 0));
+      return 0;
     };
     using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
-    if (ucols <= 4 && ts) staged2(I4(), std::true_type());
-    else if (ucols <= 4) staged2(I4(), std::false_type());
-    else if (ucols <= 8 && ts) staged2(I8(), std::true_type());
-    else if (ucols <= 8) staged2(I8(), std::false_type());
+    int src = 0;
+    if (ucols <= 4 && ts) src = staged2(I4(), std::true_type());
+    else if (ucols <= 4) src = staged2(I4(), std::false_type());
+    else if (ucols <= 8 && ts) src = staged2(I8(), std::true_type());
+    else if (ucols <= 8) src = staged2(I8(), std::false_type());
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 8) hipLaunchKernelGGL(fill_leaves_kernel<8>, grid, dim3(256), 0, c->stream, s, b);
     else if (maxt <= 16) hipLaunchKernelGGL(fill_leaves_kernel<16>, grid, dim3(256), 0, c->stream, s, b);
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
+    if (src) return src;
     HIPCHK(c, hipGetLastError());
     if (b.nstat && !b.stats_split) {  // ExclusionStats counted inside the fill
       hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(nblk_fill));

@@ -572,7 +572,7 @@ struct alignas(16) FillEvalParams {
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
 };
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
-constexpr int kFillTilesPerBlock = 2;  // leaf tiles of one staged-fill block
+constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
