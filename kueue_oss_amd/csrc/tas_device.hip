@@ -249,9 +249,15 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     delete c;
     return nullptr;
   }
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+  // priorities: the main stream (fill -> roll-up -> BestFit select, the
+  // critical path) and the fast-LFC branch high, the ExclusionStats branch
+  // (off the critical path, a full-grid kernel beside select) low, so the
+  // dispatcher hands CUs to select's workgroups first
+  int prio_lo = 0, prio_hi = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess) {
     delete c;
     return nullptr;
   }

@@ -254,6 +254,14 @@ inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) {
   emu::streams().push_back(*s);
   return hipSuccess;
 }
+inline hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned flags, int) {
+  return hipStreamCreateWithFlags(s, flags);  // priorities only order the hardware dispatcher
+}
+inline hipError_t hipDeviceGetStreamPriorityRange(int* lo, int* hi) {
+  *lo = 0;
+  *hi = -1;
+  return hipSuccess;
+}
 inline hipError_t hipStreamSynchronize(hipStream_t s) {
   s->drain();
   return hipSuccess;
