@@ -1145,12 +1145,11 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
 // ----------------------------------------------------------------------------
 // K2: fillInCountsHelper, one level (parents at `level`)
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b, int level) {
-  if (int(blockIdx.y) >= b.nfill) return;
-  const int eid = b.fill_ids[blockIdx.y];
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= s.level_size[level]) return;
-  const DevEval& ev = b.evals[eid];
+// fillInCountsHelper (:1658-1719) of one parent domain p of `level` for
+// class eid, one thread over the CSR children (wrapping int32 sums, min/max:
+// the order of the children does not matter).
+__device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& b, int eid, const DevEval& ev, int level,
+                                              int p) {
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   const int cl = level + 1;
   const int32_t inner = ev.ssal[cl];
@@ -1162,16 +1161,32 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
   const int coff = s.level_off[cl];
   int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0;
   bool has = false;
-  for (int c = cb; c < ce; c++) {
-    const int g = coff + c;
-    int32_t cs = base[g];
-    int32_t css = base[SD + g];
-    int32_t csw = cs, csswl = css, cls = 0;
-    if (leaderReq) {
-      csw = base[2 * SD + g];
-      csswl = base[3 * SD + g];
-      cls = base[4 * SD + g];
+  // children in batches of kRU: the batch's loads are issued together (one
+  // memory latency per batch, not per child)
+  constexpr int kRU = 8;
+  for (int c0 = cb; c0 < ce; c0 += kRU) {
+    int32_t vs[kRU], vss[kRU], vsw[kRU], vsswl[kRU], vls[kRU];
+#pragma unroll
+    for (int u = 0; u < kRU; u++) {
+      const int g = coff + min(c0 + u, ce - 1);
+      vs[u] = base[g];
+      vss[u] = base[SD + g];
+      vsw[u] = vs[u];
+      vsswl[u] = vss[u];
+      vls[u] = 0;
+      if (leaderReq) {
+        vsw[u] = base[2 * SD + g];
+        vsswl[u] = base[3 * SD + g];
+        vls[u] = base[4 * SD + g];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < kRU; u++) {
+    if (c0 + u >= ce) break;
+    int32_t cs = vs[u];
+    const int32_t css = vss[u];
+    int32_t csw = vsw[u];
+    const int32_t csswl = vsswl[u], cls = vls[u];
     if (hasInner) {
       cs = w_mul(go_div32(cs, inner), inner);
       csw = w_mul(go_div32(csw, inner), inner);
@@ -1184,6 +1199,7 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
       minSD = min(w_sub(css, csswl), minSD);
     }
     lead = max(cls, lead);
+    }
   }
   int32_t state = cap;
   int32_t swl = has ? w_sub(cap, minD) : 0;
@@ -1199,6 +1215,31 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
     base[2 * SD + g] = swl;
     base[3 * SD + g] = sswl;
     base[4 * SD + g] = lead;
+  }
+}
+
+__global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b, int level) {
+  if (int(blockIdx.y) >= b.nfill) return;
+  const int eid = b.fill_ids[blockIdx.y];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= s.level_size[level]) return;
+  rollup_parent(s, b, eid, b.evals[eid], level, p);
+}
+
+// The small top of the tree in ONE launch: one block per class rolls up
+// levels top..0, a thread per parent, a barrier between levels (the parents
+// a level writes are the children the next one reads; none was read before
+// in this kernel, so no stale L1 line).  Replaces one launch per level.
+constexpr int kUpperParents = 1024;  // parents of `top` at most (<= 4 per thread)
+constexpr int kUpperFanout = 64;     // mean fan-out into `top` at most (serial child loop)
+__global__ __launch_bounds__(256) void rollup_upper_kernel(DevSnap s, DevBatch b, int top) {
+  if (int(blockIdx.x) >= b.nfill) return;
+  const int eid = b.fill_ids[blockIdx.x];
+  const DevEval& ev = b.evals[eid];
+  for (int level = top; level >= 0; level--) {
+    for (int p = threadIdx.x; p < s.level_size[level]; p += blockDim.x) rollup_parent(s, b, eid, ev, level, p);
+    __threadfence_block();
+    __syncthreads();
   }
 }
 

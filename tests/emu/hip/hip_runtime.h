@@ -187,6 +187,7 @@ inline int atomicOr(int* p, int v) { int o = *p; *p = o | v; return o; }
 inline int atomicAnd(int* p, int v) { int o = *p; *p = o & v; return o; }
 inline unsigned atomicAnd(unsigned* p, unsigned v) { unsigned o = *p; *p = o & v; return o; }
 inline void __threadfence() {}
+inline void __threadfence_block() {}
 // device-scope loads that bypass L1 on hardware; plain loads here
 #define __HIP_MEMORY_SCOPE_AGENT 3
 template <class T>
