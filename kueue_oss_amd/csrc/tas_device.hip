@@ -1476,17 +1476,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipEventRecord(c->evs[1], c->stream3));
   }
   // K2
-  int upper = s.L - 2 - (b.rack_fanout ? 1 : 0);  // levels [0, upper] left to roll up
-  // the small top of the tree (few parents, moderate fan-out at every level
-  // from `fused_top` down) in one launch, the levels below it one launch each
-  int fused_top = -1;
-  for (int l = 0; l <= upper; l++) {
-    if (s.level_size[l] <= 0 || s.level_size[l] > kUpperParents ||
-        s.level_size[l + 1] > int64_t(kUpperFanout) * s.level_size[l])
-      break;
-    fused_top = l;
-  }
-  for (int l = upper; l > fused_top; l--) {
+  const int upper = s.L - 2 - (b.rack_fanout ? 1 : 0);  // levels [0, upper] left to roll up
+  for (int l = upper; l >= 0; l--) {
     if (s.level_size[l] <= 0) continue;
     const int fanout = s.level_size[l + 1] / s.level_size[l];
     if (fanout >= 8) {  // wave per parent: coalesced child reads
@@ -1497,10 +1488,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       dim3 grid((s.level_size[l] + 255) / 256, unsigned(nfill));
       hipLaunchKernelGGL(rollup_level_kernel, grid, dim3(256), 0, c->stream, s, b, l);
     }
-    HIPCHK(c, hipGetLastError());
-  }
-  if (fused_top >= 0 && nfill > 0) {
-    hipLaunchKernelGGL(rollup_upper_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, s, b, fused_top);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));

@@ -1226,23 +1226,6 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
   rollup_parent(s, b, eid, b.evals[eid], level, p);
 }
 
-// The small top of the tree in ONE launch: one block per class rolls up
-// levels top..0, a thread per parent, a barrier between levels (the parents
-// a level writes are the children the next one reads; none was read before
-// in this kernel, so no stale L1 line).  Replaces one launch per level.
-constexpr int kUpperParents = 1024;  // parents of `top` at most (<= 4 per thread)
-constexpr int kUpperFanout = 64;     // mean fan-out into `top` at most (serial child loop)
-__global__ __launch_bounds__(256) void rollup_upper_kernel(DevSnap s, DevBatch b, int top) {
-  if (int(blockIdx.x) >= b.nfill) return;
-  const int eid = b.fill_ids[blockIdx.x];
-  const DevEval& ev = b.evals[eid];
-  for (int level = top; level >= 0; level--) {
-    for (int p = threadIdx.x; p < s.level_size[level]; p += blockDim.x) rollup_parent(s, b, eid, ev, level, p);
-    __threadfence_block();
-    __syncthreads();
-  }
-}
-
 // Same reduction with one wave per parent: lanes stride over the CSR children
 // (coalesced reads), then a wave reduction.  Used when the mean fan-out is
 // large (e.g. leaves -> racks).  kParentsPerWave parents per wave.
