@@ -110,8 +110,24 @@ def roofline_of(snap, doc, wls, steps, stage_sum):
     return st, fill_bytes, per_launch_fill_ms, achieved, R_used
 
 
+def heartbeat(period=30.0):
+    """A progress line on stderr every `period` s (long setup / oracle phases
+    of the 1M-node config print nothing else for minutes)."""
+    import threading
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench] alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     a = parse()
+    heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
