@@ -1909,6 +1909,30 @@ class HostPool {
   bool stop_ = false;
 };
 
+// A workload's assumedUsage overlay across its PodSet groups (addAssumedUsage
+// :658-666): records appended per assigned domain, sorted by (leaf, column)
+// and merged (wrapping add: order-free) before the next pass reads them.
+struct AssumedUsage {
+  std::vector<kueue_tas_assumed> v;
+  size_t merged = 0;  // v is sorted with distinct keys when merged == v.size()
+  void add(int32_t leaf, int32_t col, int64_t x) { v.push_back({leaf, col, x}); }
+  const std::vector<kueue_tas_assumed>& records() {
+    if (merged != v.size()) {
+      std::stable_sort(v.begin(), v.end(), [](const kueue_tas_assumed& a, const kueue_tas_assumed& b) {
+        return a.leaf < b.leaf || (a.leaf == b.leaf && a.col < b.col);
+      });
+      size_t o = 0;
+      for (size_t i = 0; i < v.size(); i++) {
+        if (o > 0 && v[o - 1].leaf == v[i].leaf && v[o - 1].col == v[i].col) v[o - 1].value = add64(v[o - 1].value, v[i].value);
+        else v[o++] = v[i];
+      }
+      v.resize(o);
+      merged = o;
+    }
+    return v;
+  }
+};
+
 struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
@@ -1961,7 +1985,7 @@ struct Evaluator {
 
   // requests of one pass: taint rows shared through rowOff, assumed usage per workload
   void build_pass(std::vector<Workload>& wls, size_t pass, const std::vector<char>& done,
-                  const std::vector<std::map<int32_t, std::map<int32_t, int64_t>>>& assumedBy,
+                  std::vector<AssumedUsage>& assumedBy,
                   std::vector<kueue_tas_eval_req>& rq, std::vector<int32_t>& tt, std::vector<kueue_tas_assumed>& as,
                   std::vector<kueue_tas_affinity_req>& af, std::vector<int32_t>& afv,
                   std::vector<std::pair<size_t, GroupEval*>>& bt, std::vector<std::pair<size_t, GroupEval*>>& early) {
@@ -2005,22 +2029,20 @@ struct Evaluator {
       }
       q.affinity_end = int32_t(af.size());
       q.assumed_begin = int32_t(as.size());
+      const std::vector<kueue_tas_assumed>& mine = assumedBy[w].records();
       if (base && !(*base)[w].empty()) {  // merge the base overlay with the group's assumed usage
         const Overlay& b = (*base)[w];
         size_t k = 0;
-        for (auto& lv : assumedBy[w])
-          for (auto& cv : lv.second) {
-            while (k < b.size() && (b[k].leaf < lv.first || (b[k].leaf == lv.first && b[k].col < cv.first)))
-              as.push_back(b[k++]);
-            if (k < b.size() && b[k].leaf == lv.first && b[k].col == cv.first)
-              as.push_back({lv.first, cv.first, add64(b[k++].value, cv.second)});
-            else
-              as.push_back({lv.first, cv.first, cv.second});
-          }
+        for (const kueue_tas_assumed& r : mine) {
+          while (k < b.size() && (b[k].leaf < r.leaf || (b[k].leaf == r.leaf && b[k].col < r.col))) as.push_back(b[k++]);
+          if (k < b.size() && b[k].leaf == r.leaf && b[k].col == r.col)
+            as.push_back({r.leaf, r.col, add64(b[k++].value, r.value)});
+          else
+            as.push_back(r);
+        }
         as.insert(as.end(), b.begin() + int64_t(k), b.end());
       } else {
-        for (auto& lv : assumedBy[w])
-          for (auto& cv : lv.second) as.push_back({lv.first, cv.first, cv.second});
+        as.insert(as.end(), mine.begin(), mine.end());
       }
       q.assumed_end = int32_t(as.size());
       bt.emplace_back(w, &g);
@@ -2043,6 +2065,7 @@ struct Evaluator {
     stats[0] = stats[1] = stats[2] = stats[3] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
     const double t_start = now_ms();
+    double t_prep = t_start;  // start of the current pass's preparation
     results->resize(wls.size());
     used.assign(wls.size(), 0);
     if (!precompiled) {
@@ -2060,7 +2083,7 @@ struct Evaluator {
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
     std::vector<char> done(wls.size(), 0);
-    std::vector<std::map<int32_t, std::map<int32_t, int64_t>>> assumedBy(wls.size());
+    std::vector<AssumedUsage> assumedBy(wls.size());
     size_t maxGroups = 0;
     for (auto& wl : wls) maxGroups = std::max(maxGroups, wl.groups.size());
     const size_t T = snap->taintStrings.size();
@@ -2099,7 +2122,7 @@ struct Evaluator {
         for (size_t w = 0; w < wls.size(); w++)
           for (size_t k = 0; k < used[w]; k++) (*results)[w][k].materialize();
       const double t_call = now_ms();
-      host_ms[0] += t_call - t_start;
+      host_ms[0] += t_call - t_prep;  // this pass's preparation only
       const size_t n = bt->size();
       outs.resize(n);
       offsets.resize(n + 1);
@@ -2155,10 +2178,8 @@ struct Evaluator {
         if (pass + 1 < wls[w].groups.size()) {
           auto add = [&](const TASPodSetRequests* tr, const DomainAssignment* ds, int32_t nd) {
             for (int32_t k = 0; k < nd; k++)
-              for (auto& kv : tr->requestIds) {
-                int64_t& slot = assumedBy[w][ds[k].leaf][snap->col_of(kv.first)];
-                slot = add64(slot, mul64(kv.second, ds[k].count));
-              }
+              for (auto& kv : tr->requestIds)
+                assumedBy[w].add(ds[k].leaf, snap->col_of(kv.first), mul64(kv.second, ds[k].count));
           };
           add(g.workers, e, o.num_workers);
           if (g.leader) add(g.leader, ld, o.num_leaders);
@@ -2170,7 +2191,8 @@ struct Evaluator {
           else set_result((*results)[w], used[w], m->name, false, nullptr, 0, kEmpty);
         }
       }
-      host_ms[2] += now_ms() - t_decode;
+      t_prep = now_ms();
+      host_ms[2] += t_prep - t_decode;
     }
     for (size_t w = 0; w < wls.size(); w++) (*results)[w].resize(used[w]);
     host_ms[3] = now_ms() - t_start;
