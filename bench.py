@@ -133,15 +133,25 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = None
+    gpu = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist_mod
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # rehearsal knobs for a one-GPU box: every rank on device 0, gloo
+        # collectives over host tensors (RCCL needs one GPU per rank)
+        backend = os.environ.get("KTAS_BENCH_BACKEND", "nccl")
+        if os.environ.get("KTAS_BENCH_SAME_DEVICE"):
+            gpu = 0
+        if backend == "nccl":
+            torch.cuda.set_device(gpu)
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            device = f"cuda:{gpu}"
+        else:
+            dist_mod.init_process_group(backend)
+            device = "cpu"
         dist = dist_mod
-        device = f"cuda:{local_rank}"
 
     import numpy as np
     import torch
@@ -157,7 +167,7 @@ def main():
     gen_s = time.time() - t0
 
     t0 = time.time()
-    snap = TASFlavorSnapshot(snap_doc, device=local_rank if world > 1 else 0)
+    snap = TASFlavorSnapshot(snap_doc, device=gpu if world > 1 else 0)
     snap.compile(all_wls)  # identical resource columns on every replica
     if world > 1:
         snap.set_shard(ids)
