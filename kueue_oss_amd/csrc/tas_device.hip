@@ -136,9 +136,9 @@ struct kueue_tas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // fast-LFC branch (tables, select, emit) beside the BestFit select
+  hipStream_t stream3 = nullptr;  // ExclusionStats branch (staged fill): counts + reduce beside the roll-up/select
   hipEvent_t evs[2] = {};         // ExclusionStats branch: start, end (also the join)
   DevBuf<int8_t> d_fill_lim;
-  DevBuf<int32_t> d_stats_need;
   std::vector<int32_t> cls_pos, cls_cur;
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
@@ -249,12 +249,15 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     delete c;
     return nullptr;
   }
-  // both streams at the high priority: the batch's kernels go ahead of
-  // other work on the device
+  // priorities: the main stream (fill -> roll-up -> BestFit select, the
+  // critical path) and the fast-LFC branch high, the ExclusionStats branch
+  // (off the critical path, a full-grid kernel beside select) low, so the
+  // dispatcher hands CUs to select's workgroups first
   int prio_lo = 0, prio_hi = 0;
   if (hipSetDevice(c->device) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_lo) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -269,6 +272,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  if (c->stream3) (void)hipStreamSynchronize(c->stream3);
   c->d_child_off.release();
   c->d_id_rank.release();
   c->d_taint_profile.release();
@@ -285,7 +289,6 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_setfree.release();
   c->d_fits.release();
   c->d_fill_lim.release();
-  c->d_stats_need.release();
   c->d_parent.release();
   c->d_names.release();
   c->d_name_off.release();
@@ -320,6 +323,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evs)
     if (e) (void)hipEventDestroy(e);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1326,7 +1330,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.fill_stats = nullptr;
   b.stats_split = 0;
   b.fill_lim = nullptr;
-  b.stats_need = nullptr;
   b.cls_member_off = nullptr;
   b.cls_members = nullptr;
   b.rack_fanout = 0;
@@ -1396,7 +1399,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * std::max(grid.x, nblk_fill) * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
     }
-    if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel after select
+    if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
       HIPCHK(c, c->d_fill_lim.ensure(size_t(nruns) * size_t(s.N)));
       b.stats_split = 1;
       b.fill_lim = c->d_fill_lim.p;
@@ -1461,6 +1464,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  if (b.stats_split) {  // counts, reduce and member stores beside the roll-up / select
+    HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
+    HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
+    dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
+    if (b.num_profiles <= kStagedProfiles) hipLaunchKernelGGL(fill_exclusion_kernel<true>, grid, dim3(256), 0, c->stream3, s, b);
+    else hipLaunchKernelGGL(fill_exclusion_kernel<false>, grid, dim3(256), 0, c->stream3, s, b);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(grid.x));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->evs[1], c->stream3));
+  }
   // K2
   const int upper = s.L - 2 - (b.rack_fanout ? 1 : 0);  // levels [0, upper] left to roll up
   for (int l = upper; l >= 0; l--) {
@@ -1520,22 +1534,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
-  if (b.stats_split) {
-    // ExclusionStats after select, only for classes with a failed member
-    // (they only feed the failure messages): no full-grid kernel competing
-    // with select for the CUs, and most classes skip it
-    HIPCHK(c, c->d_stats_need.ensure(size_t(std::max(nfill, 1))));
-    b.stats_need = c->d_stats_need.p;
-    HIPCHK(c, hipEventRecord(c->evs[0], c->stream));
-    hipLaunchKernelGGL(stats_need_kernel, dim3(unsigned((nfill + 255) / 256)), dim3(256), 0, c->stream, b);
-    dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
-    if (b.num_profiles <= kStagedProfiles) hipLaunchKernelGGL(fill_exclusion_kernel<true>, grid, dim3(256), 0, c->stream, s, b);
-    else hipLaunchKernelGGL(fill_exclusion_kernel<false>, grid, dim3(256), 0, c->stream, s, b);
-    HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(grid.x));
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->evs[1], c->stream));
-  }
+  if (b.stats_split) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
@@ -1552,7 +1551,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->ent_stride = entry_cap;
   lap(4);
   memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
-  {  // nodeSelector / affinity exclusions: counted after select, read from the stats region
+  {  // nodeSelector / affinity exclusions: counted beside select (stream3), read from the stats region after the join
     const int32_t* sel = c->res_stats_h + n * nt + n * size_t(s.R);
     for (size_t i = 0; i < n; i++) {
       out[i].excl_selector = sel[i];

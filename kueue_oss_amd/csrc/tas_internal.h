@@ -132,7 +132,6 @@ struct DevBatch {
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_lim)
   int8_t* fill_lim;        // [signature runs][N] limiting resource where the run's signature gives state 0, else -1
-  int32_t* stats_need;     // [fill positions] 1: a member of the class failed (its ExclusionStats are needed)
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)
   const int32_t* cls_members;     // eval ids
   int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)

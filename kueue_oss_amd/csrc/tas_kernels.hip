@@ -995,21 +995,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 // third stream beside the roll-up and select.  Same grid and masks as the
 // fill; the resource case reads the limiting resource the fill recorded per
 // (chunk, leaf) where the chunk's signature gives state 0.
-// ExclusionStats only feed the failure messages (notFitMessage :1721-1741,
-// multiLayerNotFitMessage): after select, mark the fill positions (classes)
-// with a failed member; the exclusion pass counts only those.
-__global__ __launch_bounds__(256) void stats_need_kernel(DevBatch b) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= b.nfill) return;
-  int need = b.out[b.fill_ids[f]].status != KUEUE_TAS_ST_OK;
-  for (int m = b.cls_member_off[f]; m < b.cls_member_off[f + 1] && !need; m++)
-    need = b.out[b.cls_members[m]].status != KUEUE_TAS_ST_OK;
-  b.stats_need[f] = need;
-}
-
 template <bool TS>  // as fill_leaves_staged_kernel
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
-  __shared__ int32_t sh_need[kEvalsPerBlock];
   __shared__ int32_t sh_toff[kEvalsPerBlock];
   __shared__ int32_t sh_nsel[kEvalsPerBlock];
   __shared__ int32_t sh_run[kEvalsPerBlock];
@@ -1017,16 +1004,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   const int e0 = b.fill_chunks[2 * blockIdx.y];
   const int ne = b.fill_chunks[2 * blockIdx.y + 1];
-  // positions without a failed member: no partials (the reduce skips them)
-  bool any = false;
-  for (int e = 0; e < ne; e++) any |= b.stats_need[e0 + e] != 0;
-  if (!any) return;  // block-uniform
-  for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   constexpr bool stage_taints = TS;
   if (int(threadIdx.x) < ne) {
-    sh_need[threadIdx.x] = b.stats_need[e0 + threadIdx.x];
     const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
     sh_toff[threadIdx.x] = ev.taint_table;
     sh_nsel[threadIdx.x] = ev.nsel;
@@ -1064,14 +1046,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
     return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
   };
   const bool dead = valid && leaf_out(s, leaf);
-  int lim_run = -1;
   for (int e = 0; e < ne; e++) {
-    if (!uni(sh_need[e])) continue;
     const int run = uni(sh_run[e]);
-    if (run != lim_run) {
-      lim = valid ? int(b.fill_lim[int64_t(run) * N + leaf]) : -1;
-      lim_run = run;
-    }
+    if (e == 0 || run != uni(sh_run[e - 1])) lim = valid ? int(b.fill_lim[int64_t(run) * N + leaf]) : -1;
     int kind = EX_NONE, id = -1;
     if (valid && !dead) {
       if (s.lowest_is_hostname) {
@@ -1146,14 +1123,11 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
   const int f = blockIdx.x;
   const int eid = b.fill_ids[f];
   const int wv = threadIdx.x >> 6, lane = lane_id();
-  const bool need = b.stats_need == nullptr || b.stats_need[f] != 0;  // else: no partials, the stats are 0
   for (int k = wv; k < b.nstat; k += 4) {  // one wave per statistic, lanes over the fill blocks
     const int32_t* p = b.fill_stats + int64_t(f) * nblk * b.nstat + k;
     int32_t acc = 0;
-    if (need) {
 #pragma unroll 8
-      for (int j = lane; j < nblk; j += kWave) acc += p[int64_t(j) * b.nstat];
-    }
+    for (int j = lane; j < nblk; j += kWave) acc += p[int64_t(j) * b.nstat];
     acc = wave_sum_wrap32(acc);
     const int m0 = b.cls_member_off ? b.cls_member_off[f] : 0;
     const int m1 = b.cls_member_off ? b.cls_member_off[f + 1] : 0;
@@ -3576,7 +3550,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   o.num_workers = o.num_leaders = 0;
   o.assignment_nil = 0;
   o.total_nodes = s.n_live;
-  o.excl_selector = 0;  // set by the host from the stats region (counted after select)
+  o.excl_selector = 0;  // set by the host from the stats region (counted concurrently, stream3)
   o.excl_affinity = 0;
   o.excl_topology = 0;
   for (int c = 0; c < KUEUE_TAS_MAX_LAYERS; c++) o.ml_fit[c] = o.ml_need[c] = 0;
