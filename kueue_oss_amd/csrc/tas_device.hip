@@ -138,7 +138,7 @@ struct kueue_tas_ctx {
   hipStream_t stream2 = nullptr;  // fast-LFC branch (tables, select, emit) beside the BestFit select
   hipStream_t stream3 = nullptr;  // ExclusionStats branch (staged fill): counts + reduce beside the roll-up/select
   hipEvent_t evs[2] = {};         // ExclusionStats branch: start, end (also the join)
-  DevBuf<uint32_t> d_fill_code;
+  DevBuf<uint8_t> d_fill_code;
   std::vector<int32_t> cls_pos, cls_cur;
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
@@ -1400,7 +1400,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.fill_stats = c->d_fill_stats.p;
     }
     if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
-      HIPCHK(c, c->d_fill_code.ensure(size_t(nfchunks) * 4 * size_t(s.N)));
+      HIPCHK(c, c->d_fill_code.ensure(size_t(nfill) * size_t(s.N)));
       b.stats_split = 1;
       b.fill_code = c->d_fill_code.p;
       b.cls_member_off = reinterpret_cast<const int32_t*>(ds + o_moff);

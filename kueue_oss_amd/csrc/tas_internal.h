@@ -131,7 +131,7 @@ struct DevBatch {
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
   int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_code)
-  uint32_t* fill_code;     // [fill chunk][4][N] per leaf 4 positions' codes a word: 0, or 1 + the ExclusionStats slot
+  uint8_t* fill_code;      // [fill positions][N] 0, or 1 + the ExclusionStats slot the leaf counts in
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)
   const int32_t* cls_members;     // eval ids
   int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)

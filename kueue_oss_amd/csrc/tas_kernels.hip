@@ -798,7 +798,6 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // waits (vmcnt) for every store of the earlier evals
   const bool dead = valid && !live;
   const int rack_f = b.rack_fanout;
-  uint32_t code_word = 0;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_p[e]);
     const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
@@ -939,16 +938,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     else if (rack_f == 64) rack_rollup(std::integral_constant<int, 64>());
     else if (rack_f) rack_rollup(std::integral_constant<int, 0>());
     if (split) {  // the leaf's ExclusionStats slot, counted by fill_exclusion_kernel off the critical path
-      int slot = -1;
-      if (kind == EX_SELECTOR) slot = 0;
-      else if (kind == EX_AFFINITY) slot = 1;
-      else if (kind == EX_TOPOLOGY) slot = 2;
-      else if (kind == EX_TAINT) slot = kStatFixed + id;
-      else if (kind == EX_RESOURCE) slot = kStatFixed + b.num_taints + id;
-      code_word |= uint32_t(slot + 1) << (8 * (e & 3));
-      if ((e & 3) == 3 || e == ne - 1) {  // four positions per dword store
-        if (valid) b.fill_code[(int64_t(chunk) * 4 + (e >> 2)) * N + leaf] = code_word;
-        code_word = 0;
+      if (valid) {
+        int slot = -1;
+        if (kind == EX_SELECTOR) slot = 0;
+        else if (kind == EX_AFFINITY) slot = 1;
+        else if (kind == EX_TOPOLOGY) slot = 2;
+        else if (kind == EX_TAINT) slot = kStatFixed + id;
+        else if (kind == EX_RESOURCE) slot = kStatFixed + b.num_taints + id;
+        b.fill_code[int64_t(e0 + e) * N + leaf] = uint8_t(slot + 1);
       }
       continue;
     }
@@ -1015,15 +1012,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
   const int lane = lane_id();
-  static_assert(kEvalsPerBlock == 16, "four code words per leaf");
-  uint32_t words[4];  // the chunk's codes of this leaf, loads in flight together
+  int code[kEvalsPerBlock];  // the chunk's codes of this leaf, loads in flight together
 #pragma unroll
-  for (int q = 0; q < 4; q++)
-    words[q] = (valid && 4 * q < ne) ? b.fill_code[(int64_t(blockIdx.y) * 4 + q) * s.N + leaf] : 0u;
+  for (int e = 0; e < kEvalsPerBlock; e++)
+    code[e] = (valid && e < ne) ? int(b.fill_code[int64_t(e0 + e) * s.N + leaf]) : 0;
 #pragma unroll
   for (int e = 0; e < kEvalsPerBlock; e++) {
     if (e >= ne) break;
-    const int c = int((words[e >> 2] >> (8 * (e & 3))) & 0xffu);
+    int c = code[e];
     uint64_t m = ballot(c != 0);
     while (m) {
       const int v = bcast(c, __ffsll((unsigned long long)m) - 1);
