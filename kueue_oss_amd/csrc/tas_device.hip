@@ -138,7 +138,7 @@ struct kueue_tas_ctx {
   hipStream_t stream2 = nullptr;  // fast-LFC branch (tables, select, emit) beside the BestFit select
   hipStream_t stream3 = nullptr;  // ExclusionStats branch (staged fill): counts + reduce beside the roll-up/select
   hipEvent_t evs[2] = {};         // ExclusionStats branch: start, end (also the join)
-  DevBuf<uint8_t> d_fill_code;
+  DevBuf<int8_t> d_fill_lim;
   std::vector<int32_t> cls_pos, cls_cur;
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
@@ -288,7 +288,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_deltas.release();
   c->d_setfree.release();
   c->d_fits.release();
-  c->d_fill_code.release();
+  c->d_fill_lim.release();
   c->d_parent.release();
   c->d_names.release();
   c->d_name_off.release();
@@ -1329,7 +1329,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.nstat_R = s.R;
   b.fill_stats = nullptr;
   b.stats_split = 0;
-  b.fill_code = nullptr;
+  b.fill_lim = nullptr;
   b.cls_member_off = nullptr;
   b.cls_members = nullptr;
   b.rack_fanout = 0;
@@ -1400,9 +1400,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       b.fill_stats = c->d_fill_stats.p;
     }
     if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
-      HIPCHK(c, c->d_fill_code.ensure(size_t(nfill) * size_t(s.N)));
+      HIPCHK(c, c->d_fill_lim.ensure(size_t(nruns) * size_t(s.N)));
       b.stats_split = 1;
-      b.fill_code = c->d_fill_code.p;
+      b.fill_lim = c->d_fill_lim.p;
       b.cls_member_off = reinterpret_cast<const int32_t*>(ds + o_moff);
       b.cls_members = reinterpret_cast<const int32_t*>(ds + o_mem);
     }
@@ -1468,7 +1468,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
     HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
-    hipLaunchKernelGGL(fill_exclusion_kernel, grid, dim3(256), 0, c->stream3, s, b);
+    if (b.num_profiles <= kStagedProfiles) hipLaunchKernelGGL(fill_exclusion_kernel<true>, grid, dim3(256), 0, c->stream3, s, b);
+    else hipLaunchKernelGGL(fill_exclusion_kernel<false>, grid, dim3(256), 0, c->stream3, s, b);
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(grid.x));
     HIPCHK(c, hipGetLastError());

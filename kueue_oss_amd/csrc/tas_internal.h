@@ -130,8 +130,8 @@ struct DevBatch {
   int32_t nstat;           // kStatFixed + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
   int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
-  int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_code)
-  uint8_t* fill_code;      // [fill positions][N] 0, or 1 + the ExclusionStats slot the leaf counts in
+  int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_lim)
+  int8_t* fill_lim;        // [signature runs][N] limiting resource where the run's signature gives state 0, else -1
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)
   const int32_t* cls_members;     // eval ids
   int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)

@@ -781,6 +781,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       const DevTerm* wt = sh_term[e];
       const DevTerm* lt = sh_term[e] + NS;
       state0 = count_slots(wt, rmask, lt, lmask, pres, false, &lim0);
+      if (split) b.fill_lim[int64_t(uni(P.run)) * N + leaf] = int8_t(state0 == 0 ? lim0 : -1);
       swl0 = state0;
       if (leader) {
         int dummy;
@@ -790,6 +791,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
           swl0 = count_slots(wt, rmask, lt, lmask, pres | lmask, true, &dummy);
         }
       }
+    } else if (split && valid) {
+      b.fill_lim[int64_t(uni(P.run)) * N + leaf] = int8_t(-1);
     }
   };
   if constexpr (!MR) count_run(0);
@@ -937,18 +940,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     if (rack_f == 32) rack_rollup(std::integral_constant<int, 32>());
     else if (rack_f == 64) rack_rollup(std::integral_constant<int, 64>());
     else if (rack_f) rack_rollup(std::integral_constant<int, 0>());
-    if (split) {  // the leaf's ExclusionStats slot, counted by fill_exclusion_kernel off the critical path
-      if (valid) {
-        int slot = -1;
-        if (kind == EX_SELECTOR) slot = 0;
-        else if (kind == EX_AFFINITY) slot = 1;
-        else if (kind == EX_TOPOLOGY) slot = 2;
-        else if (kind == EX_TAINT) slot = kStatFixed + id;
-        else if (kind == EX_RESOURCE) slot = kStatFixed + b.num_taints + id;
-        b.fill_code[int64_t(e0 + e) * N + leaf] = uint8_t(slot + 1);
-      }
-      continue;
-    }
+    if (split) continue;
     uint64_t selm = ballot(kind == EX_SELECTOR);
     if (lane == 0 && selm) {
       if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
@@ -998,34 +990,123 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 }
 
 // ExclusionStats of the staged fill's classes (fillInCounts :1578-1634:
-// first untolerated taint, then nodeSelector, affinity, required domain,
-// then a resource giving state 0) counted from the per-(position, leaf) slot
-// codes the fill wrote: a byte load per leaf and class and a ballot per
-// distinct slot, in a kernel of its own beside the roll-up and select (only
-// the failure messages need them).  Same grid as the fill, per-block partials.
+// first untolerated taint, then nodeSelector, then a resource giving state 0)
+// in a kernel of their own, off the fill's critical path: it runs on a
+// third stream beside the roll-up and select.  Same grid and masks as the
+// fill; the resource case reads the limiting resource the fill recorded per
+// (chunk, leaf) where the chunk's signature gives state 0.
+template <bool TS>  // as fill_leaves_staged_kernel
 __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s, DevBatch b) {
+  __shared__ int32_t sh_toff[kEvalsPerBlock];
+  __shared__ int32_t sh_nsel[kEvalsPerBlock];
+  __shared__ int32_t sh_run[kEvalsPerBlock];
+  __shared__ int32_t sh_aff[kEvalsPerBlock][4];  // affinity range, required-domain leaf range
+  __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
+  __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
   for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   const int e0 = b.fill_chunks[2 * blockIdx.y];
   const int ne = b.fill_chunks[2 * blockIdx.y + 1];
+  constexpr bool stage_taints = TS;
+  if (int(threadIdx.x) < ne) {
+    const DevEval& ev = b.evals[b.fill_ids[e0 + threadIdx.x]];
+    sh_toff[threadIdx.x] = ev.taint_table;
+    sh_nsel[threadIdx.x] = ev.nsel;
+    sh_run[threadIdx.x] = b.fill_run[e0 + threadIdx.x];
+    const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
+    sh_aff[threadIdx.x][0] = aff ? ev.aff_begin : -1;
+    sh_aff[threadIdx.x][1] = aff ? ev.aff_end : -1;
+    sh_aff[threadIdx.x][2] = ev.dom_begin;
+    sh_aff[threadIdx.x][3] = ev.dom_end;
+    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+      sh_sel[threadIdx.x][2 * k] = ev.sel_col[k];
+      sh_sel[threadIdx.x][2 * k + 1] = ev.sel_val[k];
+    }
+  }
+  __syncthreads();
+  if (s.taint_profile && stage_taints) {
+    for (int i = threadIdx.x; i < ne * kStagedProfiles; i += kFillThreads) {
+      const int e = i / kStagedProfiles, p = i % kStagedProfiles;
+      sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_toff[e] + p] : -1;
+    }
+  }
   __syncthreads();
   const int leaf = blockIdx.x * kFillThreads + threadIdx.x;
   const bool valid = leaf < s.N;
+  const int N = s.N;
   const int lane = lane_id();
-  int code[kEvalsPerBlock];  // the chunk's codes of this leaf, loads in flight together
+  const int prof = (valid && s.taint_profile) ? s.taint_profile[leaf] : 0;
+  int lim = -1;  // limiting resource of the position's signature run (the fill recorded it)
+  int32_t lab[kStagedLabels];
 #pragma unroll
-  for (int e = 0; e < kEvalsPerBlock; e++)
-    code[e] = (valid && e < ne) ? int(b.fill_code[int64_t(e0 + e) * s.N + leaf]) : 0;
+  for (int k = 0; k < kStagedLabels; k++) lab[k] = (valid && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
+  static_assert(kStagedLabels == 4, "staged_label takes four staged columns");
+  const int32_t lab0 = lab[0], lab1 = lab[1], lab2 = lab[2], lab3 = lab[3];
+  auto label_at = [s, leaf, lab0, lab1, lab2, lab3](int col) {  // by value: nothing escapes to scratch
+    return staged_label(s, leaf, col, lab0, lab1, lab2, lab3);
+  };
+  const bool dead = valid && leaf_out(s, leaf);
+  for (int e = 0; e < ne; e++) {
+    const int run = uni(sh_run[e]);
+    if (e == 0 || run != uni(sh_run[e - 1])) lim = valid ? int(b.fill_lim[int64_t(run) * N + leaf]) : -1;
+    int kind = EX_NONE, id = -1;
+    if (valid && !dead) {
+      if (s.lowest_is_hostname) {
+        if (s.taint_profile) {
+          int t;
+          if constexpr (TS) t = sh_taint[e][prof];
+          else t = b.taint_table[uni(sh_toff[e]) + prof];
+          if (t >= 0) {
+            kind = EX_TAINT;
+            id = t;
+          }
+        }
+        if (kind == EX_NONE) {
+          const int nsel = uni(sh_nsel[e]);
+          for (int k = 0; k < nsel; k++) {
+            const int col = uni(sh_sel[e][2 * k]);
+            int32_t v;
+            if (col < kStagedLabels) {
+              v = lab[0];
 #pragma unroll
-  for (int e = 0; e < kEvalsPerBlock; e++) {
-    if (e >= ne) break;
-    int c = code[e];
-    uint64_t m = ballot(c != 0);
-    while (m) {
-      const int v = bcast(c, __ffsll((unsigned long long)m) - 1);
-      const uint64_t mm = ballot(c == v);
-      if (lane == 0) atomicAdd(&sh_stats[e][v - 1], __popcll(mm));
-      m &= ~mm;
+              for (int q = 1; q < kStagedLabels; q++) v = col == q ? lab[q] : v;
+            } else {
+              v = s.label_values[int64_t(col) * N + leaf];
+            }
+            if (v != uni(sh_sel[e][2 * k + 1])) {
+              kind = EX_SELECTOR;
+              break;
+            }
+          }
+        }
+        const int ab = uni(sh_aff[e][0]);
+        if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(sh_aff[e][1]), leaf, label_at)) kind = EX_AFFINITY;
+      }
+      if (kind == EX_NONE && outside_domain(uni(sh_aff[e][2]), uni(sh_aff[e][3]), leaf)) kind = EX_TOPOLOGY;
+      if (kind == EX_NONE && lim >= 0) {
+        kind = EX_RESOURCE;
+        id = lim;
+      }
+    }
+    const uint64_t selm = ballot(kind == EX_SELECTOR);
+    if (lane == 0 && selm) atomicAdd(&sh_stats[e][0], __popcll(selm));
+    const uint64_t affm = ballot(kind == EX_AFFINITY);
+    if (lane == 0 && affm) atomicAdd(&sh_stats[e][1], __popcll(affm));
+    const uint64_t domm = ballot(kind == EX_TOPOLOGY);
+    if (lane == 0 && domm) atomicAdd(&sh_stats[e][2], __popcll(domm));
+    uint64_t tm = ballot(kind == EX_TAINT);
+    while (tm) {
+      const int tid = bcast(id, __ffsll((unsigned long long)tm) - 1);
+      const uint64_t mm = ballot(kind == EX_TAINT && id == tid);
+      if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + tid], __popcll(mm));
+      tm &= ~mm;
+    }
+    uint64_t rm = ballot(kind == EX_RESOURCE);
+    while (rm) {
+      const int rid = bcast(id, __ffsll((unsigned long long)rm) - 1);
+      const uint64_t mm = ballot(kind == EX_RESOURCE && id == rid);
+      if (lane == 0) atomicAdd(&sh_stats[e][kStatFixed + b.num_taints + rid], __popcll(mm));
+      rm &= ~mm;
     }
   }
   __syncthreads();
