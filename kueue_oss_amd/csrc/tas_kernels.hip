@@ -941,20 +941,29 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     else if (rack_f == 64) rack_rollup(std::integral_constant<int, 64>());
     else if (rack_f) rack_rollup(std::integral_constant<int, 0>());
     if (split) continue;
-    uint64_t selm = ballot(kind == EX_SELECTOR);
-    if (lane == 0 && selm) {
-      if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
-      else atomicAdd(&b.sel_counts[eid], __popcll(selm));
+    // wave-uniform skips: a wave with every leaf counted nowhere, and the
+    // kinds this eval cannot produce (no selector / affinity / domain)
+    if (ballot(valid && kind != EX_NONE && kind != EX_DEAD) == 0) continue;
+    if (nsel > 0) {
+      const uint64_t selm = ballot(kind == EX_SELECTOR);
+      if (lane == 0 && selm) {
+        if (lds_stats) atomicAdd(&sh_stats[e][0], __popcll(selm));
+        else atomicAdd(&b.sel_counts[eid], __popcll(selm));
+      }
     }
-    const uint64_t affm = ballot(kind == EX_AFFINITY);
-    if (lane == 0 && affm) {
-      if (lds_stats) atomicAdd(&sh_stats[e][1], __popcll(affm));
-      else atomicAdd(&b.aff_counts[eid], __popcll(affm));
+    if (aff_begin >= 0) {
+      const uint64_t affm = ballot(kind == EX_AFFINITY);
+      if (lane == 0 && affm) {
+        if (lds_stats) atomicAdd(&sh_stats[e][1], __popcll(affm));
+        else atomicAdd(&b.aff_counts[eid], __popcll(affm));
+      }
     }
-    const uint64_t domm = ballot(kind == EX_TOPOLOGY);
-    if (lane == 0 && domm) {
-      if (lds_stats) atomicAdd(&sh_stats[e][2], __popcll(domm));
-      else atomicAdd(&b.dom_counts[eid], __popcll(domm));
+    if (dom_begin >= 0) {
+      const uint64_t domm = ballot(kind == EX_TOPOLOGY);
+      if (lane == 0 && domm) {
+        if (lds_stats) atomicAdd(&sh_stats[e][2], __popcll(domm));
+        else atomicAdd(&b.dom_counts[eid], __popcll(domm));
+      }
     }
     uint64_t tm = ballot(kind == EX_TAINT);
     while (tm) {
