@@ -29,6 +29,8 @@ VARIANTS = {
                           "  for (int e = 0; e < (state0 == -7 ? ne : 0); e++) {\n    const int4* pq"),
                          ("  if constexpr (!MR) count_run(0);", "  if constexpr (!MR) { if (ne < 0) count_run(0); }")],
     "no_count": [("  if constexpr (!MR) count_run(0);", "  if constexpr (!MR) { if (ne < 0) count_run(0); }")],
+    "evals_per_block_8": [("constexpr int kEvalsPerBlock = 16;", "constexpr int kEvalsPerBlock = 8;")],
+    "evals_per_block_32": [("constexpr int kEvalsPerBlock = 16;", "constexpr int kEvalsPerBlock = 32;")],
     "no_store_no_rack": [("    if (valid) {\n      base[gleaf] = state;", "    if (valid && state == -7) {\n      base[gleaf] = state;"),
                          ("  const int rack_f = b.rack_fanout;", "  const int rack_f = 0;")],
 }
