@@ -42,10 +42,10 @@
 extern "C" {
 #endif
 
-#define KUEUE_TAS_ABI_VERSION 3
+#define KUEUE_TAS_ABI_VERSION 4
 #define KUEUE_TAS_MAX_LEVELS 16    /* topology_types.go:114 (<=16 levels) */
 #define KUEUE_TAS_MAX_COLS 32      /* resource columns per snapshot */
-#define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs per request */
+#define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs held inline per request (more: KUEUE_TAS_F_SELECTOR_EXT) */
 #define KUEUE_TAS_MAX_LAYERS 4     /* podsetSliceRequiredTopologyConstraints */
 
 /* error codes */
@@ -97,6 +97,7 @@ typedef struct {
 #define KUEUE_TAS_F_MULTILAYER 32u    /* len(multiLayerConstraints) > 0 :873-875 */
 #define KUEUE_TAS_F_AFFINITY 64u      /* requirements.affinitySelector != nil :889-897 (hostname leaves) */
 #define KUEUE_TAS_F_DOMAIN 128u       /* requiredReplacementDomain != "" (node replacement, :614-678) */
+#define KUEUE_TAS_F_SELECTOR_EXT 256u /* nodeSelector pairs beyond the inline sel_col/sel_val (selector_begin/end) */
 
 typedef struct {
   uint32_t flags;
@@ -125,6 +126,15 @@ typedef struct {
   int32_t domain_begin;           /* with KUEUE_TAS_F_DOMAIN: only leaves [begin, end) take part */
   int32_t domain_end;             /*   (belongsToRequiredDomain :1649-1656); the others count as
                                      ExclusionStats.TopologyDomain (:1613-1617) */
+  int32_t selector_begin;         /* with KUEUE_TAS_F_SELECTOR_EXT: the nodeSelector pairs beyond the
+                                     num_selectors inline ones, as requirements [begin, end) of the
+                                     batch affinity table (col = label column, the required value id in
+                                     the values table, negate 0; `term` ignored).  A leaf passes the
+                                     nodeSelector when every inline pair and every such requirement
+                                     matches (labels.ValidatedSelectorFromSet, selector.go:954-968: one
+                                     Equals requirement per key, any number of keys); otherwise it counts
+                                     as ExclusionStats.NodeSelector (:1599-1603) */
+  int32_t selector_end;
 } kueue_tas_eval_req;
 
 /* One compiled requirement of required node affinity

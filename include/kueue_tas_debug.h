@@ -53,6 +53,20 @@ int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
  * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
  * fill staged (0: generic kernel). */
 int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
+/* Phase-1 kernel variants the last kueue_tas_eval_batch ran (OR of the bits
+ * below; tests pin that their inputs reach every variant). */
+#define KUEUE_TAS_PATH_STAGED 1u                /* fill_leaves_staged_kernel, taint rows in LDS */
+#define KUEUE_TAS_PATH_STAGED_GLOBAL_TAINTS 2u  /* staged fill, > 32 taint profiles: rows from global */
+#define KUEUE_TAS_PATH_GENERIC4 4u              /* fill_leaves_kernel<4> (> 8 request columns) */
+#define KUEUE_TAS_PATH_GENERIC8 8u
+#define KUEUE_TAS_PATH_GENERIC16 16u
+#define KUEUE_TAS_PATH_GENERIC32 32u
+#define KUEUE_TAS_PATH_STAGED_GL 64u            /* staged fill with global lookups (far selector columns, affinity) */
+#define KUEUE_TAS_PATH_GLOBAL_STATS 128u        /* ExclusionStats by global atomics (> 64 stat slots or generic fill) */
+#define KUEUE_TAS_PATH_EXCL 256u                /* fill_exclusion_kernel<true> (split stats) */
+#define KUEUE_TAS_PATH_EXCL_GLOBAL_TAINTS 512u  /* fill_exclusion_kernel<false> */
+#define KUEUE_TAS_PATH_SELECTOR_EXT 1024u       /* nodeSelector pairs beyond the inline ones */
+uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 
 /* ---- host layer ---------------------------------------------------------- */
 /* Device stage times of the last run (summed over its batches, ms):
@@ -71,7 +85,8 @@ int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
  * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
 /* Work counters of the last find/run: [0] device batches, [1] evals,
- * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] 0. */
+ * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] OR of
+ * kueue_tas_last_fill_paths. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
 /* Host wall time of the last kueue_tas_host_admit (ms): [0] record
  * preparation, [1] kueue_tas_admit (uploads, admit_kernel, result copy),

@@ -1,4 +1,4 @@
-"""ctypes mirror of the plain-C structs of include/kueue_tas.h (ABI version 3).
+"""ctypes mirror of the plain-C structs of include/kueue_tas.h (ABI version 4).
 
 For bindings that call the device layer directly (kueue_tas_snapshot_load,
 kueue_tas_eval_batch) instead of going through the JSON host layer; the
@@ -19,6 +19,7 @@ F_LEADER = 16
 F_MULTILAYER = 32
 F_AFFINITY = 64
 F_DOMAIN = 128
+F_SELECTOR_EXT = 256
 
 ST_OK = 0
 ST_NO_DOMAINS = 1
@@ -76,6 +77,8 @@ class EvalReq(c.Structure):  # kueue_tas_eval_req
         ("affinity_end", c.c_int32),
         ("domain_begin", c.c_int32),
         ("domain_end", c.c_int32),
+        ("selector_begin", c.c_int32),
+        ("selector_end", c.c_int32),
     ]
 
 

@@ -214,7 +214,16 @@ struct kueue_tas_ctx {
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
+  uint32_t fill_paths = 0;               // KUEUE_TAS_PATH_* bits of the last kueue_tas_eval_batch
 };
+
+// The leaf-row scatter kernels write repeated entries in no fixed order:
+// the calls that take a leaf list require distinct leaves.
+static bool distinct_leaves(const int32_t* leaves, size_t n) {
+  std::vector<int32_t> sorted(leaves, leaves + n);
+  std::sort(sorted.begin(), sorted.end());
+  return std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+}
 
 static int fail(kueue_tas_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -586,6 +595,7 @@ int kueue_tas_snapshot_set_free(kueue_tas_ctx* c, const int32_t* leaves, size_t 
   if (!leaves || !rows || !free_present) return fail(c, KUEUE_TAS_EINVAL, "null argument");
   for (size_t i = 0; i < n; i++)
     if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "set_free leaf out of range");
+  if (!distinct_leaves(leaves, n)) return fail(c, KUEUE_TAS_EINVAL, "repeated leaf in set_free");
   HIPCHK(c, hipSetDevice(c->device));
   const size_t R = size_t(c->snap.R);
   const size_t rows_off = (n * 4 + 7) / 8 * 8;
@@ -611,6 +621,7 @@ int kueue_tas_snapshot_set_leaf_live(kueue_tas_ctx* c, const int32_t* leaves, si
   if (!leaves || !live) return fail(c, KUEUE_TAS_EINVAL, "null argument");
   for (size_t i = 0; i < n; i++)
     if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "leaf out of range");
+  if (!distinct_leaves(leaves, n)) return fail(c, KUEUE_TAS_EINVAL, "repeated leaf in set_leaf_live");
   for (size_t i = 0; i < n; i++) {
     const uint8_t d = live[i] ? 0 : 1;
     c->n_dead += int64_t(d) - int64_t(c->h_dead[size_t(leaves[i])]);
@@ -654,6 +665,7 @@ int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* c, const int32_t* leaves, s
     if (leaves[i] < 0 || leaves[i] >= c->snap.N) return fail(c, KUEUE_TAS_EINVAL, "leaf out of range");
     if (profiles[i] < 0) return fail(c, KUEUE_TAS_EINVAL, "negative taint profile");
   }
+  if (!distinct_leaves(leaves, n)) return fail(c, KUEUE_TAS_EINVAL, "repeated leaf in set_leaf_attrs");
   HIPCHK(c, hipSetDevice(c->device));
   for (size_t i = 0; i < n; i++) c->num_profiles = std::max(c->num_profiles, profiles[i] + 1);
   const size_t prof_off = n * 4, lab_off = 2 * n * 4;
@@ -821,19 +833,27 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       return fail(c, KUEUE_TAS_EINVAL, "level out of range");
     if (r.num_selectors < 0 || r.num_selectors > KUEUE_TAS_MAX_SELECTORS) return fail(c, KUEUE_TAS_EINVAL, "num_selectors");
     if (r.num_selectors > 0 && s.K == 0) return fail(c, KUEUE_TAS_EINVAL, "selectors without label columns");
-    if (r.flags & KUEUE_TAS_F_AFFINITY) {  // host-side shape check of everything the fill will read
-      if (r.affinity_begin < 0 || r.affinity_end < r.affinity_begin || size_t(r.affinity_end) > num_aff ||
-          (r.affinity_end > r.affinity_begin && (!aff || !aff_vals)))
-        return fail(c, KUEUE_TAS_EINVAL, "affinity range");
-      for (int32_t k = r.affinity_begin; k < r.affinity_end; k++) {
+    // host-side shape check of every requirement the fill will read
+    auto check_reqs = [&](int32_t rb, int32_t re, bool terms, const char* what) -> int {
+      if (rb < 0 || re < rb || size_t(re) > num_aff || (re > rb && (!aff || !aff_vals)))
+        return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " range");
+      for (int32_t k = rb; k < re; k++) {
         const kueue_tas_affinity_req& q = aff[k];
         if (q.col < KUEUE_TAS_AFFINITY_LEAF || q.col >= s.K || q.begin < 0 || q.len < 0 ||
-            size_t(q.begin) + size_t(q.len) > num_aff_vals || (k > r.affinity_begin && q.term < aff[k - 1].term))
-          return fail(c, KUEUE_TAS_EINVAL, "affinity requirement");
+            size_t(q.begin) + size_t(q.len) > num_aff_vals || (terms && k > rb && q.term < aff[k - 1].term))
+          return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " requirement");
         for (int32_t j = 1; j < q.len; j++)
           if (aff_vals[q.begin + j] <= aff_vals[q.begin + j - 1])
-            return fail(c, KUEUE_TAS_EINVAL, "affinity values not sorted");
+            return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " values not sorted");
       }
+      return 0;
+    };
+    if (r.flags & KUEUE_TAS_F_AFFINITY)
+      if (int rc = check_reqs(r.affinity_begin, r.affinity_end, true, "affinity")) return rc;
+    if (r.flags & KUEUE_TAS_F_SELECTOR_EXT) {
+      if (r.num_selectors != KUEUE_TAS_MAX_SELECTORS)
+        return fail(c, KUEUE_TAS_EINVAL, "KUEUE_TAS_F_SELECTOR_EXT needs the inline selector pairs filled");
+      if (int rc = check_reqs(r.selector_begin, r.selector_end, false, "nodeSelector")) return rc;
     }
     if (r.assumed_begin < 0 || r.assumed_end < r.assumed_begin || size_t(r.assumed_end) > num_assumed ||
         (r.assumed_end > r.assumed_begin && !assumed))
@@ -888,6 +908,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     e.aff_end = r.affinity_end;
     e.dom_begin = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_begin : -1;
     e.dom_end = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_end : -1;
+    const bool sx = (r.flags & KUEUE_TAS_F_SELECTOR_EXT) != 0 && r.selector_end > r.selector_begin;
+    e.sx_begin = sx ? r.selector_begin : -1;
+    e.sx_end = sx ? r.selector_end : -1;
     e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
     for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
       e.layer_level[k] = r.layer_level[k];
@@ -999,14 +1022,21 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     for (int k = 0; k < e.nsel; k++) add(uint64_t(uint32_t(e.sel_col[k])) | (uint64_t(uint32_t(e.sel_val[k])) << 32));
     if (const int32_t* row = taint_row(e))
       for (int p = 0; p < P; p++) add(uint64_t(uint32_t(row[p])));
-    if (e.flags & KUEUE_TAS_F_AFFINITY) {
-      add(0xaff1u);
-      for (int k = e.aff_begin; k < e.aff_end; k++) {
+    auto add_reqs = [&](int32_t rb, int32_t re) {
+      for (int k = rb; k < re; k++) {
         const kueue_tas_affinity_req& q = aff[k];
         add(uint64_t(uint32_t(q.term)) | (uint64_t(uint32_t(q.col)) << 32));
         add(uint64_t(uint32_t(q.negate)) | (uint64_t(uint32_t(q.len)) << 32));
         for (int j = 0; j < q.len; j++) add(uint64_t(uint32_t(aff_vals[q.begin + j])));
       }
+    };
+    if (e.flags & KUEUE_TAS_F_AFFINITY) {
+      add(0xaff1u);
+      add_reqs(e.aff_begin, e.aff_end);
+    }
+    if (e.sx_begin >= 0) {
+      add(0x5e1eu);
+      add_reqs(e.sx_begin, e.sx_end);
     }
     return h;
   };
@@ -1020,17 +1050,22 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int32_t *rx = taint_row(x), *ry = taint_row(y);
     if ((rx == nullptr) != (ry == nullptr)) return false;
     if (!(rx == nullptr || rx == ry || memcmp(rx, ry, size_t(P) * 4) == 0)) return false;
+    auto same_reqs = [&](int32_t xb, int32_t xe, int32_t yb, int32_t ye) {
+      if (xe - xb != ye - yb) return false;
+      for (int k = 0; k < xe - xb; k++) {
+        const kueue_tas_affinity_req& p = aff[xb + k];
+        const kueue_tas_affinity_req& q = aff[yb + k];
+        if (p.term != q.term || p.col != q.col || p.negate != q.negate || p.len != q.len) return false;
+        if (p.begin != q.begin && memcmp(aff_vals + p.begin, aff_vals + q.begin, size_t(p.len) * 4) != 0) return false;
+      }
+      return true;
+    };
+    if ((x.sx_begin >= 0) != (y.sx_begin >= 0)) return false;
+    if (x.sx_begin >= 0 && !same_reqs(x.sx_begin, x.sx_end, y.sx_begin, y.sx_end)) return false;
     const bool ax = (x.flags & KUEUE_TAS_F_AFFINITY) != 0, ay = (y.flags & KUEUE_TAS_F_AFFINITY) != 0;
     if (ax != ay) return false;
     if (!ax) return true;
-    if (x.aff_end - x.aff_begin != y.aff_end - y.aff_begin) return false;
-    for (int k = 0; k < x.aff_end - x.aff_begin; k++) {
-      const kueue_tas_affinity_req& p = aff[x.aff_begin + k];
-      const kueue_tas_affinity_req& q = aff[y.aff_begin + k];
-      if (p.term != q.term || p.col != q.col || p.negate != q.negate || p.len != q.len) return false;
-      if (p.begin != q.begin && memcmp(aff_vals + p.begin, aff_vals + q.begin, size_t(p.len) * 4) != 0) return false;
-    }
-    return true;
+    return same_reqs(x.aff_begin, x.aff_end, y.aff_begin, y.aff_end);
   };
   auto fast_lfc = [&](const DevEval& e) {
     return (e.flags & KUEUE_TAS_F_LFC) != 0 &&
@@ -1416,7 +1451,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     // staged label columns, or required node affinity
     bool gl = false;
     for (size_t i = 0; i < n && !gl; i++) {
-      gl = (reqs[i].flags & KUEUE_TAS_F_AFFINITY) != 0;
+      gl = (reqs[i].flags & (KUEUE_TAS_F_AFFINITY | KUEUE_TAS_F_SELECTOR_EXT)) != 0;
       for (int k = 0; k < reqs[i].num_selectors; k++) gl = gl || reqs[i].sel_col[k] >= kStagedLabels;
     }
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
@@ -1448,6 +1483,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
     int src = 0;
+    c->fill_paths |= ucols <= 8 ? (ts ? KUEUE_TAS_PATH_STAGED : KUEUE_TAS_PATH_STAGED_GLOBAL_TAINTS)
+                                : maxt <= 4 ? KUEUE_TAS_PATH_GENERIC4 : maxt <= 8 ? KUEUE_TAS_PATH_GENERIC8
+                                : maxt <= 16 ? KUEUE_TAS_PATH_GENERIC16 : KUEUE_TAS_PATH_GENERIC32;
+    if (ucols <= 8 && gl) c->fill_paths |= KUEUE_TAS_PATH_STAGED_GL;
+    if (!lds_stats) c->fill_paths |= KUEUE_TAS_PATH_GLOBAL_STATS;
+    if (b.stats_split) c->fill_paths |= b.num_profiles <= kStagedProfiles ? KUEUE_TAS_PATH_EXCL : KUEUE_TAS_PATH_EXCL_GLOBAL_TAINTS;
+    for (size_t i = 0; i < n; i++)
+      if (hev[i].sx_begin >= 0) c->fill_paths |= KUEUE_TAS_PATH_SELECTOR_EXT;
     if (ucols <= 4 && ts) src = staged2(I4(), std::true_type());
     else if (ucols <= 4) src = staged2(I4(), std::false_type());
     else if (ucols <= 8 && ts) src = staged2(I8(), std::true_type());
@@ -1606,6 +1649,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
   for (auto& v : c->host_ms) v = 0;
+  c->fill_paths = 0;
   const size_t chunk = size_t(c->max_batch);
   std::vector<int64_t> off;
   entry_offsets[0] = 0;
@@ -1699,6 +1743,8 @@ int kueue_tas_last_host_times(kueue_tas_ctx* c, double* ms, int n) {
   for (int k = 0; k < n && k < 6; k++) ms[k] = c->host_ms[k];
   return KUEUE_TAS_OK;
 }
+
+uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* c) { return c ? c->fill_paths : 0u; }
 
 int kueue_tas_last_stats(kueue_tas_ctx* c, int64_t* stats4) {
   if (!c || !stats4) return KUEUE_TAS_EINVAL;

@@ -332,6 +332,10 @@ struct GroupEval {
   // relative to aff_vals; build_pass rebases them into the batch tables
   std::vector<kueue_tas_affinity_req> aff;
   std::vector<int32_t> aff_vals;
+  // nodeSelector pairs beyond the inline ones (KUEUE_TAS_F_SELECTOR_EXT), as
+  // requirements relative to sel_vals, rebased the same way
+  std::vector<kueue_tas_affinity_req> sel_ext;
+  std::vector<int32_t> sel_vals;
 };
 
 struct Workload {
@@ -395,6 +399,11 @@ class FlavorSnapshot {
   // columns / profiles / labels
   std::vector<std::string> cols;
   std::map<std::string, int32_t> colByName;
+  // resources some request, usage record or Fits term has named: the only
+  // ones CountInWithLimitingResource / Fits ever read (requests.go:174-217
+  // iterate the request's keys), kept as columns even when the snapshot has
+  // more resource names than KUEUE_TAS_MAX_COLS (see wanted_columns)
+  std::set<std::string> reqNames;
   std::vector<std::vector<Taint>> profiles;
   std::vector<std::vector<int32_t>> profileTaintIds;  // taintIdByString[taint_string(t)] per profile taint
   std::vector<int32_t> leafProfile;
@@ -673,13 +682,9 @@ class FlavorSnapshot {
       if (it != nodeToLeaf.end()) req_sub(freeCap[leafById[it->second]], kv.second);
     }
     // resource columns
-    std::set<std::string> names;
-    for (int i = 0; i < N; i++) {
-      for (auto& kv : freeCap[i]) names.insert(kv.first);
-      for (auto& kv : tasUsage[i]) names.insert(kv.first);
-    }
-    names.insert("pods");
-    set_columns(names);
+    for (int i = 0; i < N; i++)
+      for (auto& kv : tasUsage[i]) reqNames.insert(kv.first);  // usage of admitted workloads: requested names
+    recolumn();
     // taint profiles + label dictionaries (filters apply only with hostname leaves)
     leafProfile.assign(N, 0);
     if (lowestIsHostname) {
@@ -929,13 +934,7 @@ class FlavorSnapshot {
       for (auto& kv : f) new_col |= !colByName.count(kv.first);
       freeCap[size_t(l)] = std::move(f);
     }
-    if (new_col) {
-      std::set<std::string> names(cols.begin(), cols.end());
-      for (int32_t l : leaves)
-        for (auto& kv : freeCap[size_t(l)]) names.insert(kv.first);
-      set_columns(names);
-      return 0;
-    }
+    if (new_col && recolumn()) return 0;  // dirty: the next upload() takes the host mirror
     if (dirty || !ctx || leaves.empty()) return 0;
     const size_t R = cols.size();
     std::vector<int32_t> ls(leaves.begin(), leaves.end());
@@ -943,9 +942,10 @@ class FlavorSnapshot {
     std::vector<uint32_t> pres(ls.size(), 0);
     for (size_t i = 0; i < ls.size(); i++)
       for (auto& kv : freeCap[size_t(ls[i])]) {
-        const int c = colByName[kv.first];
-        rows[i * R + size_t(c)] = kv.second;
-        pres[i] |= 1u << c;
+        const auto c = colByName.find(kv.first);
+        if (c == colByName.end()) continue;  // a resource no request reads (wanted_columns)
+        rows[i * R + size_t(c->second)] = kv.second;
+        pres[i] |= 1u << c->second;
       }
     int rc = kueue_tas_snapshot_set_free(ctx, ls.data(), ls.size(), rows.data(), pres.data());
     if (rc) {
@@ -982,9 +982,38 @@ class FlavorSnapshot {
     }
     auto pc = colByName.find("pods");
     podsCol = pc == colByName.end() ? -1 : pc->second;
-    if (cols.size() > KUEUE_TAS_MAX_COLS) throw std::runtime_error("too many resource columns");
     dirty = true;
     compile_gen++;
+  }
+  // The device columns: every resource name of the snapshot (free capacity,
+  // TAS usage, requests) when they fit KUEUE_TAS_MAX_COLS; otherwise only
+  // "pods" and the names requests / usage records / Fits terms have used —
+  // a resource no request names never changes a count (CountIn and Fits
+  // iterate the request's keys, requests.go:174-217), and the host mirror
+  // keeps every resource for SerializeFreeCapacityPerDomain.  More than
+  // KUEUE_TAS_MAX_COLS requested names in one flavor is the only limit.
+  std::set<std::string> wanted_columns() const {
+    std::set<std::string> all(reqNames);
+    all.insert("pods");
+    for (const Requests& f : freeCap) {
+      for (auto& kv : f) all.insert(kv.first);
+      if (all.size() > KUEUE_TAS_MAX_COLS) break;
+    }
+    if (all.size() <= KUEUE_TAS_MAX_COLS) return all;
+    std::set<std::string> req(reqNames);
+    req.insert("pods");
+    if (req.size() > KUEUE_TAS_MAX_COLS)
+      throw std::runtime_error("more than " + std::to_string(KUEUE_TAS_MAX_COLS) +
+                               " distinct requested resources in one TAS flavor");
+    return req;
+  }
+  // Re-derives the column set; returns true when it changed (compiled
+  // requests are stale, the next upload() reloads).
+  bool recolumn() {
+    const std::set<std::string> want = wanted_columns();
+    if (want.size() == cols.size() && std::equal(want.begin(), want.end(), cols.begin())) return false;
+    set_columns(want);
+    return true;
   }
   // Requests may name resources no node has: they become all-absent columns.
   // Returns true when the column set changed (compiled requests are stale).
@@ -996,13 +1025,9 @@ class FlavorSnapshot {
     for (auto& p : podsets)
       for (auto& kv : p.requestIds) known = known && col_of(kv.first) >= 0;
     if (known) return false;
-    std::set<std::string> names(cols.begin(), cols.end());
-    size_t before = names.size();
     for (auto& p : podsets)
-      for (auto& kv : p.singlePodRequests) names.insert(kv.first);
-    if (names.size() == before) return false;
-    set_columns(names);
-    return true;
+      for (auto& kv : p.singlePodRequests) reqNames.insert(kv.first);
+    return recolumn();
   }
 
   int upload() {
@@ -1021,16 +1046,18 @@ class FlavorSnapshot {
     for (int l = 0; l + 1 < L; l++) co.insert(co.end(), childOff[l].begin(), childOff[l].end());
     std::vector<int64_t> fr(size_t(R) * N, 0), us(size_t(R) * N, 0);
     std::vector<uint32_t> fp(N, 0), up(N, 0);
-    for (int i = 0; i < N; i++) {
+    for (int i = 0; i < N; i++) {  // resources without a column are read by no request (wanted_columns)
       for (auto& kv : freeCap[i]) {
-        int c = colByName[kv.first];
-        fr[size_t(c) * N + i] = kv.second;
-        fp[i] |= 1u << c;
+        const auto c = colByName.find(kv.first);
+        if (c == colByName.end()) continue;
+        fr[size_t(c->second) * N + i] = kv.second;
+        fp[i] |= 1u << c->second;
       }
       for (auto& kv : tasUsage[i]) {
-        int c = colByName[kv.first];
-        us[size_t(c) * N + i] = kv.second;
-        up[i] |= 1u << c;
+        const auto c = colByName.find(kv.first);
+        if (c == colByName.end()) continue;
+        us[size_t(c->second) * N + i] = kv.second;
+        up[i] |= 1u << c->second;
       }
     }
     std::vector<int32_t> ranks;
@@ -1132,11 +1159,9 @@ class FlavorSnapshot {
       }
     }
     if (new_col) {
-      std::set<std::string> names(cols.begin(), cols.end());
       for (auto& u : us)
-        for (auto& kv : u.single) names.insert(kv.first);
-      set_columns(names);  // dirty: the next upload() takes the host mirror
-      return 0;
+        for (auto& kv : u.single) reqNames.insert(kv.first);
+      if (recolumn()) return 0;  // dirty: the next upload() takes the host mirror
     }
     if (!device || dirty || !ctx || deltas.empty()) return 0;
     int rc = kueue_tas_snapshot_apply_deltas(ctx, deltas.data(), deltas.size(), nullptr);
@@ -1145,14 +1170,13 @@ class FlavorSnapshot {
   }
   // Columns for every resource of a usage list (a removal overlay needs one).
   bool ensure_columns_for_usage(const std::vector<DomainUsage>& us) {
-    std::set<std::string> names(cols.begin(), cols.end());
-    const size_t before = names.size();
-    names.insert("pods");
+    bool known = true;
     for (auto& u : us)
-      for (auto& kv : u.single) names.insert(kv.first);
-    if (names.size() == before) return false;
-    set_columns(names);
-    return true;
+      for (auto& kv : u.single) known = known && colByName.count(kv.first);
+    if (known) return false;
+    for (auto& u : us)
+      for (auto& kv : u.single) reqNames.insert(kv.first);
+    return recolumn();
   }
   // RemoveUsage(us) as an evaluation overlay: the leaf's tasUsage loses
   // SinglePodRequests x count + pods:count (updateTASUsage :257-293), so the
@@ -1179,6 +1203,7 @@ class FlavorSnapshot {
   }
   // TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415), on the device.
   int fits(const std::vector<DomainUsage>& us, bool* out) {
+    ensure_columns_for_usage(us);  // a term's resource must be a column to be read
     int rc = upload();
     if (rc) return rc;
     std::vector<kueue_tas_fits_req> reqs;
@@ -1261,6 +1286,8 @@ class FlavorSnapshot {
     g.compiled = true;
     g.early_reason.clear();
     g.layer_names.clear();
+    g.sel_ext.clear();
+    g.sel_vals.clear();
     const auto& tr = w.topologyRequest;
     // getSliceSizeWithSinglePodAsDefault (:1162-1180)
     int32_t sliceSize = 1;
@@ -1389,10 +1416,9 @@ class FlavorSnapshot {
         }
       }
       if (w.nodeSelector && !w.nodeSelector->empty() && !labelKeys.empty()) {
-        if (w.nodeSelector->size() > KUEUE_TAS_MAX_SELECTORS) {
-          g.early_reason = "unsupported: more than 8 nodeSelector terms";
-          return;
-        }
+        // any number of pairs (one Equals requirement per key): the first
+        // KUEUE_TAS_MAX_SELECTORS inline, the rest as requirements of the
+        // batch affinity table (a key or value no leaf has: id -1, no match)
         for (auto& kv : *w.nodeSelector) {
           auto it = labelCol.find(kv.first);
           int col = it == labelCol.end() ? 0 : it->second;
@@ -1401,10 +1427,16 @@ class FlavorSnapshot {
             auto d = labelDict[col].find(kv.second);
             if (d != labelDict[col].end()) val = d->second;
           }
-          q.sel_col[q.num_selectors] = col;
-          q.sel_val[q.num_selectors] = val;
-          q.num_selectors++;
+          if (q.num_selectors < KUEUE_TAS_MAX_SELECTORS) {
+            q.sel_col[q.num_selectors] = col;
+            q.sel_val[q.num_selectors] = val;
+            q.num_selectors++;
+          } else {
+            g.sel_ext.push_back({0, col, 0, int32_t(g.sel_vals.size()), 1});
+            g.sel_vals.push_back(val);
+          }
         }
+        if (!g.sel_ext.empty()) q.flags |= KUEUE_TAS_F_SELECTOR_EXT;
       }
     }
     // required node affinity: validated always, filters only hostname leaves (:889-897, :1605-1610)
@@ -1940,7 +1972,7 @@ struct Evaluator {
   double dev_host_ms[6] = {};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   int64_t counts[3] = {0, 0, 0};
-  int64_t stats[4] = {0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches
+  int64_t stats[5] = {0, 0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches, [4] fill paths
   std::vector<kueue_tas_eval_req> reqs;
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
@@ -2028,6 +2060,16 @@ struct Evaluator {
         afv.insert(afv.end(), g.aff_vals.begin(), g.aff_vals.end());
       }
       q.affinity_end = int32_t(af.size());
+      q.selector_begin = q.selector_end = int32_t(af.size());
+      if (q.flags & KUEUE_TAS_F_SELECTOR_EXT) {  // nodeSelector pairs beyond the inline ones, same tables
+        const int32_t vb = int32_t(afv.size());
+        for (auto r : g.sel_ext) {
+          r.begin += vb;
+          af.push_back(r);
+        }
+        afv.insert(afv.end(), g.sel_vals.begin(), g.sel_vals.end());
+        q.selector_end = int32_t(af.size());
+      }
       q.assumed_begin = int32_t(as.size());
       const std::vector<kueue_tas_assumed>& mine = assumedBy[w].records();
       if (base && !(*base)[w].empty()) {  // merge the base overlay with the group's assumed usage
@@ -2062,7 +2104,7 @@ struct Evaluator {
     for (auto& v : stage_ms) v = 0;
     for (auto& v : dev_host_ms) v = 0;
     counts[0] = counts[1] = counts[2] = 0;
-    stats[0] = stats[1] = stats[2] = stats[3] = 0;
+    stats[0] = stats[1] = stats[2] = stats[3] = stats[4] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
     const double t_start = now_ms();
     double t_prep = t_start;  // start of the current pass's preparation
@@ -2158,6 +2200,7 @@ struct Evaluator {
       kueue_tas_last_stats(snap->ctx, st4);
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
       stats[3] = std::max(stats[3], st4[3]);
+      stats[4] |= int64_t(kueue_tas_last_fill_paths(snap->ctx));
       counts[0]++;
       counts[1] += int64_t(n);
       for (auto& q : *rq) counts[2] += (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
@@ -2531,7 +2574,7 @@ struct kueue_tas_host {
   std::vector<std::vector<PodSetResult>> last;
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
-  int64_t stats[4] = {0, 0, 0, 0};
+  int64_t stats[5] = {0, 0, 0, 0, 0};
   uint64_t compiled_cols = 0;  // FlavorSnapshot::col_gen the compiled workloads were compiled against
   // this rank's shard of the compiled workloads (indices into `compiled`)
   // and its own compiled copies; empty: run_compiled evaluates them all
@@ -3576,8 +3619,7 @@ int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8) {
   stats8[0] = h->counts[0];
   stats8[1] = h->counts[1];
   stats8[2] = h->counts[2];
-  for (int k = 0; k < 4; k++) stats8[3 + k] = h->stats[k];
-  stats8[7] = 0;
+  for (int k = 0; k < 5; k++) stats8[3 + k] = h->stats[k];
   return 0;
 }
 
@@ -3790,7 +3832,11 @@ int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* d, siz
       if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
         throw std::runtime_error("delta out of range");
     s.defer_mirror(d, n);
-    if (s.dirty || !s.ctx) return s.upload();
+    if (s.dirty || !s.ctx) {
+      const int rc = s.upload();
+      if (rc) h->err = s.err;  // sticky, as on the admit path
+      return rc;
+    }
     int rc = n ? kueue_tas_snapshot_apply_deltas(s.ctx, d, n, nullptr) : 0;
     if (rc) h->err = std::string("apply deltas: ") + kueue_tas_last_error(s.ctx);
     return rc;
@@ -3902,8 +3948,8 @@ int kueue_tas_host_compile_workload(kueue_tas_host* h, const char* podsets_json,
     }
     size_t na = 0, nv = 0;
     for (auto& g : wl.groups) {
-      na += g.aff.size();
-      nv += g.aff_vals.size();
+      na += g.aff.size() + g.sel_ext.size();
+      nv += g.aff_vals.size() + g.sel_vals.size();
     }
     const size_t P = s.profiles.size();
     *n_groups = wl.groups.size();
@@ -3930,6 +3976,14 @@ int kueue_tas_host_compile_workload(kueue_tas_host* h, const char* podsets_json,
       q.affinity_end = int32_t(ka);
       std::copy(g.aff_vals.begin(), g.aff_vals.end(), affinity_values + kv);
       kv += g.aff_vals.size();
+      q.selector_begin = int32_t(ka);
+      for (auto r : g.sel_ext) {
+        r.begin += int32_t(kv);
+        affinity[ka++] = r;
+      }
+      q.selector_end = int32_t(ka);
+      std::copy(g.sel_vals.begin(), g.sel_vals.end(), affinity_values + kv);
+      kv += g.sel_vals.size();
       reqs[i] = q;
       if (i) reasons += ",";
       kjson::write_string(reasons, g.early_reason);

@@ -45,6 +45,8 @@ struct DevEval {
   int32_t aff_end;
   int32_t dom_begin;      // required replacement domain: leaves [dom_begin, dom_end); dom_begin < 0: none
   int32_t dom_end;
+  int32_t sx_begin;       // nodeSelector pairs beyond the inline ones: requirements [sx_begin, sx_end) of aff
+  int32_t sx_end;         //   (KUEUE_TAS_F_SELECTOR_EXT; sx_begin < 0: none)
   int32_t num_layers;
   int32_t layer_level[KUEUE_TAS_MAX_LAYERS];
   int32_t layer_size[KUEUE_TAS_MAX_LAYERS];

@@ -332,6 +332,21 @@ __device__ __forceinline__ bool affinity_match(const DevBatch& b, int rb, int re
   return any || cur;
 }
 
+// nodeSelector pairs beyond the inline ones (KUEUE_TAS_F_SELECTOR_EXT): one
+// Equals requirement per key (labels.ValidatedSelectorFromSet, selector.go:
+// 954-968), each compiled to "the leaf's value id is in a sorted set" XOR
+// negate like an affinity requirement; every one must match (:1599-1603).
+template <class LabelAt>
+__device__ __forceinline__ bool selector_ext_match(const DevBatch& b, int rb, int re, int leaf, LabelAt label_at) {
+  for (int r = rb; r < re; r++) {
+    const int col = uni(b.aff[r].col);
+    const int32_t v = col < 0 ? int32_t(leaf) : label_at(col);
+    if (sorted_contains(b.aff_vals + uni(b.aff[r].begin), uni(b.aff[r].len), v) == (uni(b.aff[r].negate) != 0))
+      return false;
+  }
+  return true;
+}
+
 // Requests.CountIn / CountInWithLimitingResource over up to MAXT terms held in
 // registers (fully unrolled: no runtime-indexed private arrays).  Terms are in
 // ascending column (= resource name) order, so the first missing key and the
@@ -435,6 +450,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
             }
           }
         }
+        if (kind == EX_NONE && uni(ev.sx_begin) >= 0 &&
+            !selector_ext_match(b, uni(ev.sx_begin), uni(ev.sx_end), leaf,
+                                [&](int col) { return s.label_values[int64_t(col) * N + leaf]; }))
+          kind = EX_SELECTOR;
         if (kind == EX_NONE && (flags & KUEUE_TAS_F_AFFINITY) &&
             !affinity_match(b, uni(ev.aff_begin), uni(ev.aff_end), leaf,
                             [&](int col) { return s.label_values[int64_t(col) * N + leaf]; }))
@@ -568,8 +587,10 @@ struct alignas(16) FillEvalParams {
                                                // aff_begin < 0: no required node affinity
   int32_t dom_begin, dom_end, taint_off, sig_new;  // replacement domain leaf range (dom_begin < 0: none);
                                                    // sig_new 1: first position of its signature run
-  int32_t run, rmask, lmask, pad;  // signature run (DevBatch::fill_run); the run's worker / leader column masks
+  int32_t run, rmask, lmask, sx_begin;  // signature run (DevBatch::fill_run); the run's worker / leader column
+                                        // masks; nodeSelector requirements beyond the inline pairs (-1: none)
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
+  int32_t sx_end, pad[3];
 };
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
 constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
@@ -642,6 +663,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       P.sel_val[k] = ev.sel_val[k];
       if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
     }
+    P.sx_begin = ev.sx_begin;
+    P.sx_end = ev.sx_end;
+    if (ev.sx_begin >= 0) P.sel_far = 1;  // the requirements are read from global memory (GL launch)
     P.run = b.fill_run[e0 + threadIdx.x];
     P.sig_new = threadIdx.x == 0 || b.fill_run[e0 + threadIdx.x - 1] != P.run;
     P.rmask = int32_t(ev.req_mask);
@@ -846,6 +870,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
 #pragma unroll
             for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++)
               if (k < nsel && kind == EX_NONE && label_at(uni(scol[k])) != uni(sval[k])) kind = EX_SELECTOR;
+            if constexpr (GL) {
+              const int32_t sxb = uni(pq[3].w);  // (the host fills the inline pairs first: nsel == 8)
+              if (kind == EX_NONE && sxb >= 0 && !selector_ext_match(b, sxb, uni(pq[8].x), leaf, label_at))
+                kind = EX_SELECTOR;
+            }
           }
         }
         if constexpr (GL) {
@@ -1011,6 +1040,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   __shared__ int32_t sh_run[kEvalsPerBlock];
   __shared__ int32_t sh_aff[kEvalsPerBlock][4];  // affinity range, required-domain leaf range
   __shared__ int32_t sh_sel[kEvalsPerBlock][2 * KUEUE_TAS_MAX_SELECTORS];
+  __shared__ int32_t sh_sx[kEvalsPerBlock][2];  // nodeSelector requirements beyond the inline pairs
   __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
   for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
@@ -1031,6 +1061,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
       sh_sel[threadIdx.x][2 * k] = ev.sel_col[k];
       sh_sel[threadIdx.x][2 * k + 1] = ev.sel_val[k];
     }
+    sh_sx[threadIdx.x][0] = ev.sx_begin;
+    sh_sx[threadIdx.x][1] = ev.sx_end;
   }
   __syncthreads();
   if (s.taint_profile && stage_taints) {
@@ -1087,6 +1119,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
               break;
             }
           }
+          const int sxb = uni(sh_sx[e][0]);
+          if (kind == EX_NONE && sxb >= 0 && !selector_ext_match(b, sxb, uni(sh_sx[e][1]), leaf, label_at))
+            kind = EX_SELECTOR;
         }
         const int ab = uni(sh_aff[e][0]);
         if (kind == EX_NONE && ab >= 0 && !affinity_match(b, ab, uni(sh_aff[e][1]), leaf, label_at)) kind = EX_AFFINITY;

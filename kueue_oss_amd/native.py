@@ -47,7 +47,7 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_entries", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_entries", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_last_fill_paths", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
@@ -354,11 +354,13 @@ class TASFlavorSnapshot:
 
     def last_stats(self):
         """Work counters of the last run: dict(batches, evals, leader_evals,
-        fill_evals, leaf_partial_evals, fill_launches, staged_cols)."""
+        fill_evals, leaf_partial_evals, fill_launches, staged_cols, fill_paths:
+        OR of the KUEUE_TAS_PATH_* bits of include/kueue_tas_debug.h)."""
         st = (ctypes.c_int64 * 8)()
         self._lib.kueue_tas_host_last_stats(self._h, st)
-        keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols")
-        return dict(zip(keys, list(st)[:7]))
+        keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols",
+                "fill_paths")
+        return dict(zip(keys, list(st)))
 
     STAGES = ("fill", "rollup", "replicate", "lfc_branch", "select", "join_wait", "device_total")
 

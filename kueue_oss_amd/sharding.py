@@ -87,6 +87,8 @@ def broadcast_deltas(deltas, dist, src: int = 0, device=None):
     n = torch.tensor([len(deltas) if is_src and deltas is not None else 0], dtype=torch.int64, device=device)
     dist.broadcast(n, src)
     k = int(n.item())
+    if k < 0:  # the source's admission failed (admit_round): every rank fails with it
+        raise RuntimeError(f"admission failed on rank {src}")
     if k == 0:
         return np.zeros(0, dtype=DELTA_DTYPE)
     if is_src:  # 16-byte records as two int64 words
@@ -103,11 +105,19 @@ def admit_round(snap, world: int, rank: int, dist, device=None, src: int = 0):
     assignments, rank ``src`` admits in workload order (Fits + AddUsage on its
     replica) and broadcasts the applied deltas, the other replicas apply them.
     Returns (gathered quads, admitted (id, 0/1) pairs or None off-src, deltas)."""
+    import torch
+
     quads = gather_assignments(snap.last_assignments(), world, dist, device)
     admitted = None
     deltas = None
     if rank == src:
-        admitted, deltas = snap.admit(quads)
+        try:
+            admitted, deltas = snap.admit(quads)
+        except Exception:
+            # a failed admission must not leave the other ranks waiting in the
+            # broadcast: send the failure count (-1) so every rank raises
+            dist.broadcast(torch.tensor([-1], dtype=torch.int64, device=device), src)
+            raise
     deltas = broadcast_deltas(deltas, dist, src, device)
     if rank != src:
         snap.apply_deltas(deltas)

@@ -689,6 +689,118 @@ def affinity_case(rng: random.Random, max_nodes: int = 60, invalid_p: float = 0.
     return case
 
 
+_WIDE_EFFECTS = ["NoSchedule", "NoExecute", "PreferNoSchedule"]
+
+
+def wide_case(rng: random.Random, variant: str, n_nodes: int = 400, n_workloads: int = 48):
+    """Batches that reach the fill-kernel variants the bench configs never
+    touch (tas_device.hip eval_chunk dispatch):
+
+    * ``"cols"``: the batch's requests span 9..27 resource columns (up to 21
+      terms in one request: ``fill_leaves_kernel<16>`` / ``<32>``), with many
+      taint strings, so ``3 + taints + R > 64`` ExclusionStats slots take the
+      global-atomic path;
+    * ``"profiles"``: at most 5 request columns (the staged fill) and more
+      than 32 distinct taint profiles: taint rows read from global memory and
+      ``fill_exclusion_kernel<false>``;
+    * ``"slots"``: at most 5 request columns and more than 61 taint strings:
+      the staged fill counting ExclusionStats with global atomics;
+    * ``"manyres"``: nodes with 47 resource names (more than
+      KUEUE_TAS_MAX_COLS device columns), requests naming a few of them.
+
+    Every variant has twelve label columns (selector columns beyond the four
+    held in registers), nodeSelectors of up to 12 pairs (beyond the 8 inline
+    pairs of kueue_tas_eval_req), required node affinity, tolerations
+    (Equal / Exists / Gt / Lt) over the taint pool, leader / worker groups,
+    slices and ragged racks.  Returns (snapshot document, workloads)."""
+    levels = ["block", "rack", HOST]
+    n_ext = {"cols": 24, "profiles": 2, "slots": 2, "manyres": 44}[variant]
+    ext = [f"example.com/r{k:02d}" for k in range(n_ext)]
+    n_tkeys = {"cols": 30, "profiles": 12, "slots": 40, "manyres": 3}[variant]
+    pool = []
+    for k in range(n_tkeys):
+        for v in (["", "a"] if variant != "slots" else ["", "a", "7"]):
+            pool.append({"key": f"t{k}", "value": v, "effect": _WIDE_EFFECTS[k % 3]})
+    if variant == "slots":
+        pool += [{"key": "lvl", "value": str(j), "effect": "NoSchedule"} for j in (1, 4, 9, 16, 25)]
+    label_vals = {f"l{k}": [f"v{j}" for j in range(2 + k % 3)] for k in range(12)}
+    nodes = []
+    i = 0
+    while i < n_nodes:
+        b = rng.randrange(3)
+        r = rng.randrange(6)
+        for _ in range(rng.randint(1, 40)):
+            if i >= n_nodes:
+                break
+            labels = {"block": f"b{b}", "rack": f"b{b}-r{r}", HOST: f"n{i}"}
+            for key, vals in label_vals.items():
+                if rng.random() < 0.85:
+                    labels[key] = rng.choice(vals)
+            alloc = {"cpu": rng.choice([0, 4000, 16000, 64000]), "memory": rng.choice([4 * GI, 64 * GI]), "pods": 110}
+            for e in ext:
+                if rng.random() < (0.97 if variant in ("cols", "manyres") else 0.8):
+                    alloc[e] = rng.choice([0, 2, 4, 8, 16] if variant == "cols" else [0, 1, 2, 4, 8, 16])
+            nt = rng.choice([0, 0, 0, 1, 2]) if variant == "cols" else rng.choice([0, 0, 1, 1, 2, 3])
+            taints = [dict(t) for t in rng.sample(pool, nt)]
+            nodes.append(_node(f"node{i}", labels, alloc, taints, ready=rng.random() < 0.97))
+            i += 1
+    tols_pool = [{"key": f"t{k}", "operator": rng.choice(["Exists", "Equal"]), "value": "a" if k % 2 else "",
+                  "effect": rng.choice(["", _WIDE_EFFECTS[k % 3]])} for k in range(n_tkeys)]
+    tols_pool += [{"key": "lvl", "operator": "Gt", "value": "5", "effect": ""},
+                  {"key": "lvl", "operator": "Lt", "value": "10", "effect": ""}]
+    names = [n["name"] for n in nodes]
+    kmax = rng.choice([14, 21])  # longest request (+ pods): fill_leaves_kernel<16> or <32>
+    wls = []
+    for w in range(n_workloads):
+        def podset(name, count, group=None):
+            req = {"cpu": rng.choice([0, 500, 2000])} if rng.random() < 0.8 else {}
+            if rng.random() < 0.5:
+                req["memory"] = rng.choice([GI, 4 * GI])
+            if variant == "cols":
+                k = rng.choice([2, 6, 10, 13]) if w % 3 or kmax < 16 else rng.choice([18, 20, kmax])
+                for e in rng.sample(ext, min(k, len(ext))):
+                    req[e] = rng.choice([0, 1, 1, 1, 2])
+            elif variant == "manyres":  # a few of the 44 node resources per request
+                for e in rng.sample(ext[:12], rng.randint(0, 4)):
+                    req[e] = rng.choice([0, 1, 2])
+            else:
+                for e in ext:
+                    if rng.random() < 0.4:
+                        req[e] = rng.choice([0, 1, 2])
+            kind = rng.random()
+            kw = {}
+            if kind < 0.35:
+                kw["required"] = rng.choice(levels[:2])
+            elif kind < 0.6:
+                kw["preferred"] = rng.choice(levels[:2])
+            elif kind < 0.85:
+                kw["unconstrained"] = True
+            if kw and rng.random() < 0.25:
+                kw["slice_topo"] = rng.choice(levels[1:])
+                kw["slice_size"] = rng.choice([1, 2, 4])
+                count = kw["slice_size"] * max(1, count // kw["slice_size"])
+            sel = None
+            if rng.random() < 0.6:  # mostly copied from a node's labels, so some nodes match
+                keys = rng.sample(sorted(label_vals), rng.choice([1, 3, 8, 9, 10, 12]))
+                like = rng.choice(nodes)["labels"]
+                sel = {k: like[k] if k in like and rng.random() < 0.9 else rng.choice(label_vals[k]) for k in keys}
+                if rng.random() < 0.05:
+                    sel["absent-key"] = "x"
+            tols = [dict(t) for t in rng.sample(tols_pool, rng.randint(0, min(6, len(tols_pool))))] if rng.random() < 0.7 else []
+            ps = _ps(name, count, req, tolerations=tols, selector=sel, group=group, implied=not kw, **kw)
+            if rng.random() < 0.2:
+                ps["affinity"] = random_affinity(rng, names, invalid_p=0.0)
+            return ps
+
+        if rng.random() < 0.2:
+            wls.append([podset("leader", 1, "g"), podset("workers", rng.choice([2, 4, 8]), "g")])
+        else:
+            wls.append([podset("main", rng.choice([1, 2, 3, 5, 8, 16, 40]))])
+    snap = {"name": f"wide-{variant}", "levels": levels, "nodes": nodes, "pods": [], "tasUsage": [],
+            "nodeLabels": {}, "featureGates": {}}
+    return snap, wls
+
+
 def replacement_case(rng: random.Random, oracle_run) -> dict:
     """A node-replacement case (FindTopologyAssignmentsForFlavor with a
     workload whose Status.UnhealthyNodes names a node of its admitted

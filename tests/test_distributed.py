@@ -110,6 +110,52 @@ def test_gloo_shard_gather_admit_broadcast(world, emu_lib):
     assert b2 == res[n + len(admit_idx):]
 
 
+def _failing_worker(rank, world, port, q, lib_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kueue_oss_amd import TASFlavorSnapshot, native
+
+        lib = native.load_library(lib_path)
+        snap_doc, wls = _workload(8)
+        snap = TASFlavorSnapshot(snap_doc, lib=lib)
+        snap.compile(wls)
+        snap.set_shard(sharding.shard_ids(wls, world, rank))
+        snap.run_compiled()
+        if rank == 0:
+            def broken_admit(quads):
+                raise RuntimeError("forced admission failure")
+
+            snap.admit = broken_admit
+        try:
+            sharding.admit_round(snap, world, rank, dist)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+        snap.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_admit_failure_fails_every_rank(emu_lib):
+    """A host error in rank 0's admission: every rank raises
+    instead of the others waiting forever in the delta broadcast."""
+    lib_path = os.path.join(HERE, "emu", "_build", "libkueue_tas_emu.so")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q, lib_path)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert outs[0] == "forced admission failure"
+    assert outs[1] == "admission failed on rank 0"
+
+
 def test_shard_is_cost_balanced():
     _, wls = synth.config_c2(n_workloads=400)
     shards = [sharding.shard_workloads(wls, 4, r) for r in range(4)]

@@ -188,6 +188,14 @@ def _raw(lib, seed):
             want = _want(doc2, _podset(doc["levels"], *s))
             assert (None if st != abi.ST_OK else [[leaves[l][-1], c] for l, c in w]) == want, s
 
+        # the leaf-row scatter calls take distinct leaves: a repeated one is EINVAL
+        lib.kueue_tas_snapshot_set_leaf_live.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                         ctypes.c_void_p]
+        twice = np.array([picks[0], picks[0]], dtype=np.int32)
+        live = np.array([0, 1], dtype=np.int32)
+        assert lib.kueue_tas_snapshot_set_leaf_live(ctx, twice.ctypes.data, 2, live.ctypes.data) == -1
+        assert b"repeated leaf" in lib.kueue_tas_last_error(ctx)
+
         # kueue_tas_snapshot_apply_deltas == the same usage in the document
         ds = (abi.Delta * len(picks))(*[abi.Delta(l, cols.index("cpu"), 1000) for l in picks])
         assert lib.kueue_tas_snapshot_apply_deltas(ctx, ds, len(picks), None) == 0
@@ -216,12 +224,22 @@ def _first_group(podsets):
     return w["name"], l["name"]
 
 
-def _compiled(make, lib, seed, n=40):
+def _wide_cases(rng):
+    """Cases of synth.wide_case (nodeSelectors beyond the 8 inline pairs:
+    kueue_tas_host_compile_workload emits KUEUE_TAS_F_SELECTOR_EXT records)."""
+    while True:
+        doc, wls = synth.wide_case(rng, "profiles", n_nodes=120, n_workloads=8)
+        for w in wls:
+            yield dict(doc, podSets=w)
+
+
+def _compiled(make, lib, seed, n=40, gen=None):
     abi.bind_device_layer(lib)
     rng = random.Random(seed)
+    cases = gen(rng) if gen else None
     checked = 0
     for _ in range(n):
-        case = synth.random_case(rng)
+        case = next(cases) if cases else synth.random_case(rng)
         snap = make(case)
         try:
             reqs, ng, taints, nt, aff, na, vals, early = snap.compile_workload(case["podSets"])
@@ -255,6 +273,10 @@ def test_emulated_compiled_requests(emu_lib):
     _compiled(lambda d: TASFlavorSnapshot(d, lib=emu_lib), emu_lib, 11)
 
 
+def test_emulated_compiled_wide_selectors(emu_lib):
+    _compiled(lambda d: TASFlavorSnapshot(d, lib=emu_lib), emu_lib, 12, n=24, gen=_wide_cases)
+
+
 def emu_lib_path():
     import os
     return os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu", "_build", "libkueue_tas_emu.so")
@@ -269,3 +291,8 @@ def test_raw_descriptor_on_gpu(seed):
 @pytest.mark.gpu
 def test_compiled_requests_on_gpu():
     _compiled(lambda d: TASFlavorSnapshot(d), native.load_library(), 11, n=120)
+
+
+@pytest.mark.gpu
+def test_compiled_wide_selectors_on_gpu():
+    _compiled(lambda d: TASFlavorSnapshot(d), native.load_library(), 12, n=48, gen=_wide_cases)
