@@ -263,6 +263,15 @@ int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, siz
                          const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
                          int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
                          int32_t* res_counts);
+/* Phase-1 counters of request i of the last kueue_tas_eval_batch (its
+ * fillInCounts + fillInCountsHelper result, tas_flavor_snapshot.go:1568-1719):
+ * out[f * S + g] for field f = state, sliceState, stateWithLeader,
+ * sliceStateWithLeader, leaderState (:71-84) and domain g in level order
+ * (level 0 first, domain index order inside a level), S = sum D_l; cap >= 5 S.
+ * Valid for the requests of the batch's last device chunk (all of them when
+ * n <= max_batch) until the next call on ctx.  The host layer runs
+ * TASBalancedPlacement (tas_balanced_placement.go) over them. */
+int kueue_tas_last_counters(kueue_tas_ctx* ctx, size_t i, int32_t* out, size_t cap);
 /* Copy the packed entries of the last kueue_tas_eval_batch (after EOVERFLOW). */
 int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries_capacity);
 /* Zero-copy view of the packed entries of the last kueue_tas_eval_batch

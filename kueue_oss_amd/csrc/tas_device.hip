@@ -215,6 +215,11 @@ struct kueue_tas_ctx {
   double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
   uint32_t fill_paths = 0;               // KUEUE_TAS_PATH_* bits of the last kueue_tas_eval_batch
+  // phase-1 counters of the last device chunk (kueue_tas_last_counters):
+  // requests [chunk_base, chunk_base + chunk_rep.size()), their class reps
+  size_t chunk_base = 0;
+  std::vector<int32_t> chunk_rep;
+  std::vector<uint8_t> chunk_leader;
 };
 
 // The leaf-row scatter kernels write repeated entries in no fixed order:
@@ -1269,6 +1274,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
   }
   lap(1);
+  c->chunk_rep.assign(h_rep, h_rep + n);
+  c->chunk_leader.resize(n);
+  for (size_t i = 0; i < n; i++) c->chunk_leader[i] = (hev[i].flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
   // ---- device buffers ----
   const int64_t SD = s.SD;
   const int64_t ctr_stride = 5 * SD;
@@ -1656,6 +1664,7 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t m = std::min(chunk, n - i0);
     off.assign(m + 1, 0);
+    c->chunk_base = i0;
     for (;;) {
       size_t keep = c->ent_used;
       int rc = eval_chunk(c, reqs + i0, m, taint_table, taint_table_len, num_taints, assumed, num_assumed, affinity,
@@ -1692,6 +1701,38 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
   entry_offsets[n] = total;
   if (size_t(total) > entries_capacity) return fail(c, KUEUE_TAS_EOVERFLOW, "entries buffer too small");
   return kueue_tas_fetch_entries(c, entries, entries_capacity);
+}
+
+int kueue_tas_last_counters(kueue_tas_ctx* c, size_t i, int32_t* out, size_t cap) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (!out) return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  if (i < c->chunk_base || i >= c->chunk_base + c->chunk_rep.size())
+    return fail(c, KUEUE_TAS_EINVAL, "request not in the last device chunk (max_batch)");
+  const DevSnap& s = c->snap;
+  size_t total = 0;
+  for (int l = 0; l < s.L; l++) total += size_t(s.level_size[l]);
+  if (cap < 5 * total) return fail(c, KUEUE_TAS_EOVERFLOW, "counters buffer too small");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t k = i - c->chunk_base;
+  const int32_t* rep = c->d_counters.p + int64_t(c->chunk_rep[k]) * 5 * s.SD;
+  const bool leader = c->chunk_leader[k] != 0;
+  for (int f = 0; f < 5; f++) {
+    // phase 1 writes the leader fields only for leader requests; otherwise
+    // they equal state / sliceState and leaderState is 0 (select's Wave::get)
+    const int src = leader ? f : (f == 2 ? 0 : f == 3 ? 1 : f);
+    size_t pos = size_t(f) * total;
+    for (int l = 0; l < s.L; l++) {
+      const size_t nl = size_t(s.level_size[l]);
+      if (!leader && f == 4) std::memset(out + pos, 0, nl * 4);
+      else if (nl)
+        HIPCHK(c, hipMemcpyAsync(out + pos, rep + int64_t(src) * s.SD + s.level_off[l], nl * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+      pos += nl;
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KUEUE_TAS_OK;
 }
 
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* c, size_t* num_pairs) {

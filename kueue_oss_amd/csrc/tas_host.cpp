@@ -39,6 +39,7 @@
 #include "../../include/kueue_tas_debug.h"
 #include "json_reader.h"
 #include "label_selectors.h"
+#include "tas_balanced.h"
 
 namespace kueue_tas {
 
@@ -336,6 +337,9 @@ struct GroupEval {
   // requirements relative to sel_vals, rebased the same way
   std::vector<kueue_tas_affinity_req> sel_ext;
   std::vector<int32_t> sel_vals;
+  // TASBalancedPlacement applies (:907: gate on, not required, not
+  // unconstrained): the host runs it over the device's phase-1 counters
+  bool balanced = false;
 };
 
 struct Workload {
@@ -1288,6 +1292,7 @@ class FlavorSnapshot {
     g.layer_names.clear();
     g.sel_ext.clear();
     g.sel_vals.clear();
+    g.balanced = false;
     const auto& tr = w.topologyRequest;
     // getSliceSizeWithSinglePodAsDefault (:1162-1180)
     int32_t sliceSize = 1;
@@ -1450,11 +1455,9 @@ class FlavorSnapshot {
       }
       if (lowestIsHostname) compile_affinity(*w.affinity, g);
     }
-    // TASBalancedPlacement branches after fillInCounts (:907-917): not supported
-    if (gates.balanced && !required && !unconstrained) {
-      g.early_reason = "unsupported: TASBalancedPlacement";
-      return;
-    }
+    // TASBalancedPlacement branches after fillInCounts (:907-917): the
+    // device computes phase 1, the host layer the balanced placement
+    g.balanced = gates.balanced && !required && !unconstrained;
   }
 
   // Required node affinity compiled against the snapshot's label
@@ -2091,6 +2094,99 @@ struct Evaluator {
     }
   }
 
+  // ---- TASBalancedPlacement (tas_flavor_snapshot.go:906-917) ----
+  // For the batch's balanced groups: their phase-1 counters from a second
+  // device batch of just those requests (kueue_tas_last_counters), then the
+  // host algorithm (tas_balanced.h).  balOut[i].used: useBalancedPlacement;
+  // otherwise the first batch's findLevelWithFitDomains result stands.  The
+  // first batch's entries are copied first (the second batch reuses the
+  // view buffer), and *ent_view / offsets then index the copy.
+  struct BalancedOut {
+    bool used = false;
+    std::string reason;
+    std::vector<DomainAssignment> workers, leaders;
+  };
+  std::vector<BalancedOut> balOut;
+  std::vector<int32_t> balEnt, balCtr;
+  std::vector<kueue_tas_eval_req> balReq;
+  std::vector<kueue_tas_eval_out> balOuts;
+  std::vector<int64_t> balOffs;
+  int balanced_pass(const std::vector<kueue_tas_eval_req>& rq, const std::vector<int32_t>& tt,
+                    const std::vector<kueue_tas_affinity_req>* af, const std::vector<int32_t>* afv,
+                    const std::vector<std::pair<size_t, GroupEval*>>& bt, const int32_t** ent_view) {
+    const size_t n = bt.size();
+    balOut.assign(n, BalancedOut{});
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < n; i++)
+      if (bt[i].second->balanced) idx.push_back(i);
+    if (idx.empty()) return 0;
+    balEnt.clear();
+    int64_t pos = 0;
+    for (size_t i = 0; i < n; i++) {
+      const int64_t cnt = outs[i].status == KUEUE_TAS_ST_OK ? int64_t(outs[i].num_workers + outs[i].num_leaders) : 0;
+      balEnt.insert(balEnt.end(), *ent_view + offsets[i] * 2, *ent_view + (offsets[i] + cnt) * 2);
+      offsets[i] = pos;
+      pos += cnt;
+    }
+    offsets[n] = pos;
+    *ent_view = balEnt.data();
+    const FlavorSnapshot& s = *snap;
+    const int L = s.L();
+    size_t total = 0;
+    for (int l = 0; l < L; l++) total += s.values[size_t(l)].size();
+    const size_t chunk = size_t(s.cfg.max_batch > 0 ? s.cfg.max_batch : 1024);
+    for (size_t c0 = 0; c0 < idx.size(); c0 += chunk) {  // every request of a call in one device chunk
+      const size_t m = std::min(chunk, idx.size() - c0);
+      balReq.clear();
+      for (size_t k = 0; k < m; k++) balReq.push_back(rq[idx[c0 + k]]);
+      balOuts.resize(m);
+      balOffs.resize(m + 1);
+      int rc = kueue_tas_eval_batch(s.ctx, balReq.data(), m, tt.data(), tt.size(), int32_t(s.taintStrings.size()),
+                                    assumed.data(), assumed.size(), af->data(), af->size(), afv->data(), afv->size(),
+                                    balOuts.data(), balOffs.data(), nullptr, 0, nullptr, nullptr);
+      balCtr.resize(std::max<size_t>(5 * total, 1));
+      for (size_t k = 0; k < m && rc == 0; k++) {
+        rc = kueue_tas_last_counters(s.ctx, k, balCtr.data(), balCtr.size());
+        if (rc) break;
+        ktas_balanced::Tree t;
+        t.L = L;
+        t.ctr.resize(size_t(L));
+        size_t g0 = 0;
+        for (int l = 0; l < L; l++) {
+          const size_t D = s.values[size_t(l)].size();
+          t.size.push_back(int32_t(D));
+          if (l + 1 < L) t.co.push_back(&s.childOff[size_t(l)]);
+          auto& cl = t.ctr[size_t(l)];
+          cl.resize(D);
+          for (size_t d = 0; d < D; d++) {
+            const size_t g = g0 + d;
+            cl[d] = {balCtr[g], balCtr[total + g], balCtr[2 * total + g], balCtr[3 * total + g], balCtr[4 * total + g]};
+          }
+          g0 += D;
+        }
+        const kueue_tas_eval_req& q = balReq[k];
+        ktas_balanced::Params p;
+        p.count = q.count;
+        p.sliceSize = q.slice_size;
+        p.leaderCount = (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
+        p.requestedLevelIdx = q.requested_level;
+        p.sliceLevelIdx = q.slice_level;
+        p.sliceSizeAtLevel = q.slice_size_at_level;
+        const ktas_balanced::Result r = ktas_balanced::Placement(t, p).run();
+        BalancedOut& o = balOut[idx[c0 + k]];
+        o.used = r.used;
+        o.reason = r.reason;
+        for (auto& x : r.workers) o.workers.push_back({x.first, x.second});
+        for (auto& x : r.leaders) o.leaders.push_back({x.first, x.second});
+      }
+      if (rc) {
+        snap->err = std::string("balanced placement: ") + kueue_tas_last_error(s.ctx);
+        return rc;
+      }
+    }
+    return 0;
+  }
+
   // base: optional per-workload starting overlay, records sorted by (leaf,
   // column) with distinct keys, subtracted from the remaining capacity: the
   // negated usage of the workloads a preemption candidate set removes
@@ -2185,6 +2281,8 @@ struct Evaluator {
       }
       // zero-copy view (pinned, strided regions) or the packed copy
       const int32_t* ent_view = packed ? entries.data() : kueue_tas_last_entries(snap->ctx, nullptr);
+      rc = balanced_pass(*rq, *tt, af, afv, *bt, &ent_view);
+      if (rc) return rc;
       const double t_decode = now_ms();
       host_ms[1] += t_decode - t_call;
       float t4[4];
@@ -2208,14 +2306,23 @@ struct Evaluator {
         const size_t w = (*bt)[i].first;
         GroupEval& g = *(*bt)[i].second;
         const kueue_tas_eval_out& o = outs[i];
-        if (o.status != KUEUE_TAS_ST_OK) {
+        const BalancedOut* bo = g.balanced && balOut[i].used ? &balOut[i] : nullptr;
+        if (bo && !bo->reason.empty()) {  // TAS Balanced Placement failure (tas_balanced_placement.go:149-184, :295-314)
+          for (auto* m : g.members) set_result((*results)[w], used[w], m->name, false, nullptr, 0, bo->reason);
+          done[w] = 1;
+          continue;
+        }
+        if (!bo && o.status != KUEUE_TAS_ST_OK) {
           snap->failure_reason(reasonBuf, g, o, taint_counts.data() + i * std::max<size_t>(T, 1), res_counts.data() + i * R);
           for (auto* m : g.members) set_result((*results)[w], used[w], m->name, false, nullptr, 0, reasonBuf);
           done[w] = 1;
           continue;
         }
-        const DomainAssignment* e = reinterpret_cast<const DomainAssignment*>(ent_view + size_t(offsets[i]) * 2);
-        const DomainAssignment* ld = e + o.num_workers;
+        const DomainAssignment* e = bo ? bo->workers.data()
+                                       : reinterpret_cast<const DomainAssignment*>(ent_view + size_t(offsets[i]) * 2);
+        const int32_t nw = bo ? int32_t(bo->workers.size()) : o.num_workers;
+        const int32_t nl = bo ? int32_t(bo->leaders.size()) : o.num_leaders;
+        const DomainAssignment* ld = bo ? bo->leaders.data() : e + o.num_workers;
         // addAssumedUsage (:658-666) only matters for the workload's later groups:
         // SinglePodRequests x count (no pods term)
         if (pass + 1 < wls[w].groups.size()) {
@@ -2224,15 +2331,17 @@ struct Evaluator {
               for (auto& kv : tr->requestIds)
                 assumedBy[w].add(ds[k].leaf, snap->col_of(kv.first), mul64(kv.second, ds[k].count));
           };
-          add(g.workers, e, o.num_workers);
-          if (g.leader) add(g.leader, ld, o.num_leaders);
+          add(g.workers, e, nw);
+          if (g.leader) add(g.leader, ld, nl);
         }
         static const std::string kEmpty;
         for (auto* m : g.members) {
-          if (m == g.workers) set_result((*results)[w], used[w], m->name, true, e, size_t(o.num_workers), kEmpty);
-          else if (m == g.leader) set_result((*results)[w], used[w], m->name, true, ld, size_t(o.num_leaders), kEmpty);
+          if (m == g.workers) set_result((*results)[w], used[w], m->name, true, e, size_t(nw), kEmpty);
+          else if (m == g.leader) set_result((*results)[w], used[w], m->name, true, ld, size_t(nl), kEmpty);
           else set_result((*results)[w], used[w], m->name, false, nullptr, 0, kEmpty);
         }
+        if (bo)  // the balanced result lives in balOut until the next batch
+          for (size_t k = 0; k < used[w]; k++) (*results)[w][k].materialize();
       }
       t_prep = now_ms();
       host_ms[2] += t_prep - t_decode;

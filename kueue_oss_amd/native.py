@@ -47,7 +47,7 @@ class KueueTasConfig(ctypes.Structure):
 EXPORTED_SYMBOLS = [
     "kueue_tas_abi_version", "kueue_tas_ctx_create", "kueue_tas_ctx_destroy", "kueue_tas_last_error",
     "kueue_tas_snapshot_load", "kueue_tas_snapshot_apply_deltas", "kueue_tas_eval_batch", "kueue_tas_fetch_entries",
-    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_entries", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_last_fill_paths", "kueue_tas_host_create", "kueue_tas_host_destroy",
+    "kueue_tas_last_timings", "kueue_tas_last_stage_times", "kueue_tas_last_eval_ticks", "kueue_tas_last_host_times", "kueue_tas_last_entries", "kueue_tas_last_eval_profile", "kueue_tas_last_stats", "kueue_tas_last_fill_paths", "kueue_tas_last_counters", "kueue_tas_host_create", "kueue_tas_host_destroy",
     "kueue_tas_host_last_error", "kueue_tas_host_find", "kueue_tas_host_find_batch",
     "kueue_tas_host_compile", "kueue_tas_host_run_compiled", "kueue_tas_host_last_timings",
     "kueue_tas_host_last_stage_times", "kueue_tas_host_last_eval_ticks", "kueue_tas_host_last_device_host_times", "kueue_tas_host_last_eval_profile", "kueue_tas_host_last_profile", "kueue_tas_host_last_stats", "kueue_tas_free",
@@ -66,7 +66,7 @@ EXPORTED_SYMBOLS = [
 
 # the Makefile's SRC_HASH inputs, in order
 _HASHED_SOURCES = ("tas_device.hip", "tas_host.cpp", "tas_internal.h", "tas_kernels.hip", "json_reader.h",
-                   "label_selectors.h", os.path.join("..", "..", "include", "kueue_tas.h"),
+                   "label_selectors.h", "tas_balanced.h", os.path.join("..", "..", "include", "kueue_tas.h"),
                    os.path.join("..", "..", "include", "kueue_tas_debug.h"))
 
 

@@ -801,6 +801,26 @@ def wide_case(rng: random.Random, variant: str, n_nodes: int = 400, n_workloads:
     return snap, wls
 
 
+def balanced_case(rng: random.Random, max_nodes: int = 60) -> dict:
+    """random_case under the TASBalancedPlacement gate (tas_flavor_snapshot.go:
+    906-917) with mostly preferred requests (the gated branch), slices,
+    leader groups and multi-layer constraints."""
+    case = random_case(rng, max_nodes=max_nodes)
+    case["featureGates"]["TASBalancedPlacement"] = True
+    levels = case["levels"]
+    for ps in case["podSets"]:
+        tr = ps.get("topologyRequest")
+        if tr is not None and tr.get("required") and rng.random() < 0.7:
+            tr["preferred"], tr["required"] = tr["required"], None
+        elif tr is None and rng.random() < 0.6:
+            ps["topologyRequest"] = {"required": None, "preferred": rng.choice(levels), "unconstrained": None,
+                                     "podSetSliceRequiredTopology": None, "podSetSliceSize": None,
+                                     "podsetSliceRequiredTopologyConstraints": []}
+            ps.pop("implied", None)
+    case["name"] = "balanced"
+    return case
+
+
 def replacement_case(rng: random.Random, oracle_run) -> dict:
     """A node-replacement case (FindTopologyAssignmentsForFlavor with a
     workload whose Status.UnhealthyNodes names a node of its admitted

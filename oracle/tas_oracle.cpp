@@ -31,11 +31,14 @@
 //     Go map order (random); we report the smallest key's (k8s_selectors.h).
 //   * findIncompleteSliceDomain with >=2 qualifying domains returns the
 //     first in Go map order (random); we return the first in assignment order.
-// Out of scope (returns an error reason "unsupported: ..."):
-//   TASBalancedPlacement.
+//   * TASBalancedPlacement iterates domainsPerLevel and domain.children in
+//     Go map order (random); we iterate in lexicographic levelValues order,
+//     and sortDomainsByCapacityAndEntropy's ties keep that order.
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cmath>
+#include <limits>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -881,6 +884,274 @@ class Snapshot {
     return out;
   }
 
+  // ---- TASBalancedPlacement (pkg/cache/scheduler/tas_balanced_placement.go) ----
+  // Where Go iterates a map — domainsPerLevel (:243-246) and every
+  // domain.children slice, which initialize (:210-241) fills in the random
+  // order of the s.leaves map — this restatement iterates in lexicographic
+  // levelValues order (slices.Compare), the order of the other comparators'
+  // final tie-break; sortDomainsByCapacityAndEntropy (:211-231, pdqsort with
+  // a comparator that ties on equal entropy) is a stable insertion sort.  The
+  // product (tas_balanced.h) uses the same rules.  Only inputs with such ties
+  // can differ from a given Go run, and those differ between Go runs too.
+  std::deque<Domain> clones;  // cloneDomain storage of one find_topology_assignment call
+  static std::vector<Domain*> lex_sorted(std::vector<Domain*> v) {
+    std::stable_sort(v.begin(), v.end(), [](Domain* a, Domain* b) { return compare_values(a->levelValues, b->levelValues) < 0; });
+    return v;
+  }
+  static std::vector<Domain*> level_domains_lex(const std::map<std::string, Domain*>& m) {
+    std::vector<Domain*> v;
+    for (auto& kv : m) v.push_back(kv.second);
+    return lex_sorted(v);
+  }
+  Domain* clone_domain(const Domain* d, Domain* parent) {  // :351-359
+    clones.push_back(*d);
+    Domain* c = &clones.back();
+    c->parent = parent;
+    c->children.clear();
+    for (Domain* k : lex_sorted(d->children)) c->children.push_back(clone_domain(k, c));
+    return c;
+  }
+  std::vector<Domain*> clone_domains(const std::vector<Domain*>& ds) {  // :343-349
+    std::vector<Domain*> out;
+    for (Domain* d : ds) out.push_back(clone_domain(d, nullptr));
+    return out;
+  }
+  static void clear_state(Domain* d) {  // :323-332
+    d->state = d->sliceState = d->stateWithLeader = d->sliceStateWithLeader = d->leaderState = 0;
+    for (Domain* c : d->children) clear_state(c);
+  }
+  static void clear_leader_capacity(Domain* d) {  // :334-341
+    d->stateWithLeader = d->sliceStateWithLeader = d->leaderState = 0;
+    for (Domain* c : d->children) clear_leader_capacity(c);
+  }
+  static void prune_node(Domain* d, int32_t threshold, bool leaderRequired) {  // :361-370
+    if (d->sliceState < threshold) {
+      clear_state(d);
+      return;
+    }
+    if (leaderRequired && d->leaderState > 0 && d->sliceStateWithLeader < threshold) clear_leader_capacity(d);
+  }
+  void prune_domains(const std::vector<Domain*>& ds, int32_t threshold, int32_t sliceSize, int sliceLevelIdx, int level,
+                     bool leaderRequired) {  // :372-382
+    for (Domain* d : ds)
+      for (Domain* c : d->children) prune_node(c, threshold, leaderRequired);
+    for (Domain* d : ds) {
+      fill_in_counts_helper(d, sliceSize, sliceLevelIdx, level, std::map<int, int32_t>{}, leaderRequired);
+      prune_node(d, threshold, leaderRequired);
+    }
+  }
+  struct Greedy {
+    bool fit = false;
+    int32_t count = 0;
+    Domain* lastWithLeader = nullptr;
+    Domain* last = nullptr;
+  };
+  Greedy evaluate_greedy(const std::vector<Domain*>& ds, int32_t sliceCount, int32_t leaderCount) const {  // :30-63
+    Greedy g;
+    int32_t remS = sliceCount, remL = leaderCount;
+    std::vector<Domain*> withoutLeader;
+    size_t idx = 0;
+    if (leaderCount > 0) {
+      std::vector<Domain*> wl = sorted_domains_with_leader(ds, false);
+      for (; remL > 0 && idx < wl.size() && wl[idx]->leaderState > 0; idx++) {
+        g.count = w_add(g.count, 1);
+        g.lastWithLeader = wl[idx];
+        remL = w_sub(remL, wl[idx]->leaderState);
+        remS = w_sub(remS, wl[idx]->sliceStateWithLeader);
+      }
+      withoutLeader = sorted_domains(std::vector<Domain*>(wl.begin() + int64_t(idx), wl.end()), false);
+    } else {
+      withoutLeader = sorted_domains(ds, false);
+    }
+    if (remL > 0) return Greedy{};
+    for (idx = 0; remS > 0 && idx < withoutLeader.size() && withoutLeader[idx]->sliceState > 0; idx++) {
+      g.count = w_add(g.count, 1);
+      g.last = withoutLeader[idx];
+      remS = w_sub(remS, withoutLeader[idx]->sliceState);
+    }
+    if (remS > 0) return Greedy{};
+    g.fit = true;
+    return g;
+  }
+  // Go's math.Log / math.Log2 (src/math/log.go, log10.go: FreeBSD e_log.c),
+  // so entropies and their comparisons round as in the reference.
+  static double go_log(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+    const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+                 L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                 L7 = 1.479819860511658591e-01;
+    if (std::isnan(x) || std::isinf(x)) return x;
+    if (x < 0) return std::nan("");
+    if (x == 0) return -std::numeric_limits<double>::infinity();
+    int ki;
+    double f1 = std::frexp(x, &ki);
+    if (f1 < M_SQRT2 / 2) {
+      f1 *= 2;
+      ki--;
+    }
+    const double f = f1 - 1, k = double(ki);
+    const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+    const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    const double R = t1 + t2, hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+  }
+  static double go_log2(double x) {
+    int e;
+    const double frac = std::frexp(x, &e);
+    if (frac == 0.5) return double(e - 1);  // exact powers of two
+    return go_log(frac) * (1 / 0.693147180559945309417232121458176568) + double(e);
+  }
+  static double entropy(const Domain* d) {  // calculateEntropy (:186-209) of the children's states
+    if (d->children.empty()) return 0.0;
+    int32_t total = 0;
+    for (Domain* c : d->children) total = w_add(total, c->state);
+    if (total == 0) return 0.0;
+    double e = 0, tf = double(total);
+    for (Domain* c : d->children)
+      if (c->state > 0) {
+        const double p = double(c->state) / tf;
+        e += -p * go_log2(p);
+      }
+    return e;
+  }
+  static void sort_by_capacity_and_entropy(std::vector<Domain*>& ds) {  // :211-231
+    auto cmp = [](Domain* a, Domain* b) -> int {  // Go's int(b - a) on int32 fields
+      if (int32_t r = w_sub(b->leaderState, a->leaderState)) return r;
+      if (int32_t r = w_sub(b->sliceStateWithLeader, a->sliceStateWithLeader)) return r;
+      const double ea = entropy(a), eb = entropy(b);
+      return eb > ea ? 1 : (eb < ea ? -1 : 0);
+    };
+    for (size_t i = 1; i < ds.size(); i++)  // stable insertion sort
+      for (size_t j = i; j > 0 && cmp(ds[j - 1], ds[j]) > 0; j--) std::swap(ds[j - 1], ds[j]);
+  }
+  // selectOptimalDomainSetToFit (:81-147); nullopt = Go's nil
+  std::optional<std::vector<Domain*>> select_optimal_domain_set(std::vector<Domain*>& ds, int32_t sliceCount,
+                                                                int32_t leaderCount, int32_t sliceSize, bool byEntropy) {
+    const Greedy g = evaluate_greedy(ds, sliceCount, leaderCount);
+    if (!g.fit) return std::nullopt;
+    if (byEntropy) sort_by_capacity_and_entropy(ds);
+    const int32_t opt = g.count;
+    // placements[i][leadersLeft][stateLeft]: the first domain list found using i domains
+    std::vector<std::map<int32_t, std::map<int32_t, std::vector<Domain*>>>> pl(size_t(std::max(opt, 0)) + 1);
+    pl[0][leaderCount][w_mul(sliceCount, sliceSize)] = {};
+    for (Domain* d : ds)
+      for (int32_t i = opt; i > 0; i--)
+        for (auto& lk : pl[size_t(i - 1)])
+          for (auto& sk : lk.second) {
+            const int32_t beforeLeader = lk.first, beforeState = sk.first;
+            if (beforeLeader <= 0 && beforeState <= 0) continue;
+            std::vector<Domain*> np = sk.second;
+            np.push_back(d);
+            if (beforeLeader > 0 && d->leaderState > 0)  // with the leader
+              pl[size_t(i)][w_sub(beforeLeader, d->leaderState)].emplace(w_sub(beforeState, d->stateWithLeader), np);
+            if (d->sliceState > 0)  // without
+              pl[size_t(i)][beforeLeader].emplace(w_sub(beforeState, d->state), np);
+          }
+    auto it = pl[size_t(std::max(opt, 0))].find(0);
+    if (it == pl[size_t(std::max(opt, 0))].end()) return std::nullopt;
+    int32_t bestSlice = INT32_MIN;
+    const std::vector<Domain*>* best = nullptr;
+    for (auto& kv : it->second)
+      if (kv.first > bestSlice && kv.first <= 0) {
+        bestSlice = kv.first;
+        best = &kv.second;
+      }
+    if (!best) return std::nullopt;
+    return *best;
+  }
+  std::string place_slices_balanced(std::vector<Domain*> ds, int32_t sliceCount, int32_t leaderCount, int32_t sliceSize,
+                                    int32_t threshold, std::vector<Domain*>* out) {  // :149-184
+    auto res = select_optimal_domain_set(ds, sliceCount, leaderCount, sliceSize, false);
+    if (!res) return "TAS Balanced Placement: Cannot find optimal domain set to fit the request";
+    if (sliceCount < w_mul(int32_t(res->size()), threshold)) return "TAS Balanced Placement: Not enough slices to meet the threshold";
+    std::vector<Domain*> rd = sorted_domains_with_leader(*res, false);
+    int32_t extra = w_sub(sliceCount, w_mul(int32_t(rd.size()), threshold));
+    int32_t leadersLeft = leaderCount, take = 0;
+    for (Domain* d : rd) {
+      if (leadersLeft > 0) {
+        take = std::min(w_sub(d->sliceStateWithLeader, threshold), extra);
+        d->leaderState = 1;
+        leadersLeft = w_sub(leadersLeft, 1);
+      } else if (extra > 0) {
+        take = std::min(w_sub(d->sliceState, threshold), extra);
+        d->leaderState = 0;
+      } else {
+        d->leaderState = 0;
+        take = 0;
+      }
+      d->state = w_mul(w_add(threshold, take), sliceSize);
+      d->sliceState = w_add(threshold, take);
+      d->sliceStateWithLeader = d->sliceState;
+      d->stateWithLeader = w_sub(d->state, d->leaderState);
+      extra = w_sub(extra, take);
+    }
+    if (extra > 0 || leadersLeft > 0) return "TAS Balanced Placement: Not all slices or leaders could be placed";
+    *out = rd;
+    return "";
+  }
+  // findBestDomainsForBalancedPlacement (:236-290); returns the threshold, or
+  // sets *panic when Go divides by zero (balanceThresholdValue :67 with no
+  // domain selected: sliceCount <= 0)
+  int32_t find_best_domains_balanced(const Params& st, std::vector<Domain*>* best, bool* panic) {
+    const int32_t sliceCount = go_div32(st.count, st.sliceSize);
+    std::vector<std::vector<Domain*>> groups;
+    if (st.requestedLevelIdx == 0) {
+      groups.push_back(level_domains_lex(domainsPerLevel[0]));
+    } else {
+      for (Domain* h : level_domains_lex(domainsPerLevel[size_t(st.requestedLevelIdx - 1)]))
+        groups.push_back(lex_sorted(h->children));
+    }
+    int32_t bestThreshold = 0, bestCount = 0;
+    const bool leaderReq = st.leaderCount > 0;
+    for (auto& sib : groups) {
+      std::vector<Domain*> cand = clone_domains(sib);
+      const std::vector<Domain*> lower = st.requestedLevelIdx < st.sliceLevelIdx ? lower_level_domains(cand) : cand;
+      const Greedy g = evaluate_greedy(lower, sliceCount, st.leaderCount);
+      if (!g.fit) continue;
+      if (g.count == 0) {
+        *panic = true;
+        return 0;
+      }
+      int32_t threshold = go_div32(sliceCount, g.count);  // balanceThresholdValue (:66-75)
+      if (g.lastWithLeader) threshold = std::min(threshold, g.lastWithLeader->sliceStateWithLeader);
+      if (g.last) threshold = std::min(threshold, g.last->sliceState);
+      int32_t thrWL = threshold;
+      if (st.leaderCount > 0 && g.last) thrWL = std::min(threshold, g.last->sliceStateWithLeader);
+      if (threshold < bestThreshold) continue;
+      prune_domains(cand, threshold, st.sliceSize, st.sliceLevelIdx, st.requestedLevelIdx, leaderReq);
+      Greedy g2 = evaluate_greedy(cand, sliceCount, st.leaderCount);
+      if (!g2.fit && thrWL < threshold) {  // retry with a threshold that reserves leader capacity
+        if (thrWL <= 0 || thrWL < bestThreshold) continue;
+        threshold = thrWL;
+        cand = clone_domains(sib);
+        prune_domains(cand, threshold, st.sliceSize, st.sliceLevelIdx, st.requestedLevelIdx, leaderReq);
+        g2 = evaluate_greedy(cand, sliceCount, st.leaderCount);
+      }
+      if (!g2.fit) continue;
+      if (threshold > bestThreshold || (threshold == bestThreshold && g2.count < bestCount)) {
+        bestThreshold = threshold;
+        bestCount = g2.count;
+        *best = cand;
+      }
+    }
+    return bestThreshold;
+  }
+  // applyBalancedPlacementAlgorithm (:295-314)
+  std::string apply_balanced(const Params& st, int32_t bestThreshold, std::vector<Domain*> cur, std::vector<Domain*>* out,
+                             int* fitLevelIdx) {
+    const int32_t sliceCount = go_div32(st.count, st.sliceSize);
+    if (st.requestedLevelIdx < st.sliceLevelIdx) {
+      auto res = select_optimal_domain_set(cur, sliceCount, st.leaderCount, st.sliceSize, true);
+      if (!res) return "TAS Balanced Placement: Cannot find optimal domain set to fit the request";
+      cur = lower_level_domains(*res);
+      *fitLevelIdx = st.requestedLevelIdx + 1;
+    } else {
+      *fitLevelIdx = st.requestedLevelIdx;
+    }
+    return place_slices_balanced(cur, sliceCount, st.leaderCount, st.sliceSize, bestThreshold, out);
+  }
+
   // findTopologyAssignment (:804-999)
   std::string find_topology_assignment(const PodSetRequest& workers, const PodSetRequest* leader,
                                        std::map<std::string, Requests>& assumed, bool simulateEmpty,
@@ -937,17 +1208,31 @@ class Snapshot {
 
     fill_in_counts(rq, st);
 
-    if (gates.balanced && !st.required && !st.unconstrained) return "unsupported: TASBalancedPlacement";
     int fitLevelIdx = 0;
     std::vector<Domain*> cur;
-    r = find_level_with_fit_domains(st.requestedLevelIdx, st, &fitLevelIdx, &cur);
-    if (!r.empty()) return r;
+    bool useBalanced = false;  // :906-917
+    clones.clear();
+    if (gates.balanced && !st.required && !st.unconstrained) {
+      bool panic = false;
+      std::vector<Domain*> best;
+      const int32_t thr = find_best_domains_balanced(st, &best, &panic);
+      if (panic) return "panic: runtime error: integer divide by zero";
+      useBalanced = thr > 0;
+      if (useBalanced) {
+        r = apply_balanced(st, thr, best, &cur, &fitLevelIdx);
+        if (!r.empty()) return r;
+      }
+    }
+    if (!useBalanced) {
+      r = find_level_with_fit_domains(st.requestedLevelIdx, st, &fitLevelIdx, &cur);
+      if (!r.empty()) return r;
+    }
     std::vector<Domain*> next;
     if (!update_counts_to_minimum(cur, st.count, st.leaderCount, st.sliceSize, st.unconstrained, true, &next)) next.clear();
     cur = next;
     int level = fitLevelIdx;
     int L = int(domainsPerLevel.size());
-    for (; level < std::min(L - 1, st.sliceLevelIdx); level++) {
+    for (; level < std::min(L - 1, st.sliceLevelIdx) && !useBalanced; level++) {
       auto lower = sorted_domains(lower_level_domains(cur), st.unconstrained);
       if (!update_counts_to_minimum(lower, st.count, st.leaderCount, st.sliceSize, st.unconstrained, true, &next)) next.clear();
       cur = next;

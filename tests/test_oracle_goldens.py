@@ -12,9 +12,10 @@ def test_fixture_inventory():
     from golden_util import load_cases as lc
     allc = lc(scope_in=False)
     assert len(allc) == 104  # 104 named cases in the reference table (:383-6266)
-    assert len(CASES) == 86  # + the 4 elastic workload-slice cases (:5524-5733)
-    out = [c for c in allc if c["scope"] != "in"]
-    assert all(c["scope"].startswith("out:") for c in out)
+    # every case in scope: incl. the 4 elastic workload-slice cases (:5524-5733)
+    # and the 18 TASBalancedPlacement cases (:2437-3884)
+    assert len(CASES) == 104
+    assert sum(1 for c in CASES if c.get("featureGates", {}).get("TASBalancedPlacement")) == 18
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"L{c['line']}" for c in CASES])

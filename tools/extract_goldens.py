@@ -616,8 +616,6 @@ def normalise_case(name, line, raw):
             **({"previousAssignment": pa} if pa is not None else {}),
         })
     out["podSets"] = pss
-    if fg.get("TASBalancedPlacement"):
-        out["scope"] = "out:balanced placement (alpha gate TASBalancedPlacement; SURVEY §2 row 6)"
     return out
 
 
