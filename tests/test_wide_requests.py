@@ -36,7 +36,7 @@ WANT = {
 }
 
 
-def _run(make, variant, seeds, n_nodes, n_workloads):
+def _run(make, variant, seeds, n_nodes, n_workloads, want_paths=None):
     paths = 0
     fits = fails = 0
     for seed in seeds:
@@ -52,7 +52,7 @@ def _run(make, variant, seeds, n_nodes, n_workloads):
         assert mism == [], (variant, seed, mism[:5], got[mism[0]], want[mism[0]])
         fits += sum(1 for w in want for r in w if r["assignment"])
         fails += sum(1 for w in want for r in w if r["reason"])
-    every, some = WANT[variant]
+    every, some = want_paths or WANT[variant]
     assert paths & every == every, (variant, hex(paths))
     assert some == 0 or paths & some, (variant, hex(paths))
     assert fits > 0 and fails > 0, (fits, fails)  # both outcomes (placements and ExclusionStats strings)
@@ -72,4 +72,4 @@ def test_wide_variants_on_gpu(variant):
 @pytest.mark.gpu
 def test_wide_variants_small_lds_on_gpu():
     # list_cap 64: the same batches through the lazy / global-sort / histogram walks
-    _run(lambda d: TASFlavorSnapshot(d, list_cap=64), "cols", [5], 2500, 64)
+    _run(lambda d: TASFlavorSnapshot(d, list_cap=64), "cols", [5], 2500, 64, (GLOBAL_STATS | SEL_EXT, G16 | G32))
