@@ -197,6 +197,7 @@ struct kueue_tas_ctx {
   DevBuf<LfcJob> d_lfc_jobs;
   DevBuf<LfcItem> d_lfc_items;  // [0]: item count, then the items
   DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
+  DevBuf<int32_t> d_level_max;        // [n][kMaxLevels] level_max_kernel
   std::vector<int32_t> last_prof;
   int num_profiles = 1;
   int64_t stat_fills = 0, stat_evals = 0;  // phase-1 dedup counters (lifetime)
@@ -275,6 +276,14 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     delete c;
     return nullptr;
   }
+  // the BestFit select launch declares more than 64 KiB of dynamic LDS
+  // (kSelectWaves x kFinalWalkLds; a workgroup may use all 160 KiB of a CU)
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&select_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kSelectWaves * std::max(kFinalWalkLds, c->list_cap * 16)) != hipSuccess) {
+    c->err = "select_kernel dynamic LDS attribute";
+    delete c;
+    return nullptr;
+  }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->evl) (void)hipEventCreate(&e);
   for (auto& e : c->evs) (void)hipEventCreate(&e);
@@ -329,6 +338,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_jobs.release();
   c->d_lfc_items.release();
   c->d_prof.release();
+  c->d_level_max.release();
   if (c->ent_host) (void)hipHostFree(c->ent_host);
   c->ent_host = c->ent_dev = nullptr;
   for (auto& e : c->ev)
@@ -1541,6 +1551,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
     HIPCHK(c, hipGetLastError());
   }
+  if (nfill > 0 && s.L >= 2 && nbf > 0) {  // level maxima for the BestFit-side find_level
+    HIPCHK(c, c->d_level_max.ensure(n * size_t(kMaxLevels)));
+    b.level_max = c->d_level_max.p;
+    hipLaunchKernelGGL(level_max_kernel, dim3(unsigned(nfill), unsigned(s.L - 1)), dim3(256), 0, c->stream, s, b);
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   if (npairs && !b.stats_split) {  // exclusion stats of the class rep to the other members
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
@@ -1550,7 +1566,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
   const int32_t* d_bf = reinterpret_cast<const int32_t*>(ds + o_bf);
   const int waves = kSelectWaves;  // the kernel's per-wave LDS state is sized for this
-  const size_t sel_lds = size_t(waves) * size_t(c->list_cap) * 16;
+  // per-wave LDS: the sort capacity (list_cap keys); the BestFit side also
+  // holds final_leaf_walk's candidates (kFinalWalkLds per wave)
+  const int lfc_wave_lds = c->list_cap * 16, bf_wave_lds = std::max(lfc_wave_lds, kFinalWalkLds);
   // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
   // (after the stats replication); the main stream runs the BestFit side
   if (nfast) {
@@ -1561,8 +1579,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[4], 0));  // stats replicated
-    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves), sel_lds,
-                       c->stream2, s, b, d_fast, nfast);
+    b.wave_lds = lfc_wave_lds;
+    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves),
+                       size_t(waves) * size_t(lfc_wave_lds), c->stream2, s, b, d_fast, nfast);
     HIPCHK(c, hipGetLastError());
     const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
     hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
@@ -1579,8 +1598,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   // K3 (BestFit side and every other non-fast eval)
   if (nbf) {
-    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nbf + waves - 1) / waves)), dim3(64 * waves), sel_lds, c->stream,
-                       s, b, d_bf, nbf);
+    b.wave_lds = bf_wave_lds;
+    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nbf + waves - 1) / waves)), dim3(64 * waves),
+                       size_t(waves) * size_t(bf_wave_lds), c->stream, s, b, d_bf, nbf);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));

@@ -151,6 +151,7 @@ struct DevBatch {
   int64_t scratch_stride;  // uint64 elements of scratch per eval
   uint64_t* scratch;       // [n][scratch_stride]
   int32_t list_cap;        // LDS sort capacity per wave
+  int32_t wave_lds;        // select_kernel's LDS bytes per wave (>= list_cap keys; the launch's dynamic LDS / waves)
   LeafPartial* partials;   // [leaf-level evals][nblk]
   const int32_t* partial_idx; // [n] row of the eval's partials, -1 if none
   int32_t nblk;            // fill blocks per eval (partials per eval)
@@ -177,6 +178,8 @@ struct DevBatch {
   int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
   int32_t tag_epoch;
   int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
+  int32_t* level_max;      // [n][kMaxLevels] max sliceState per level < L-1 of the class rep's counters
+                           // (level_max_kernel; rows of class reps only), null: not computed
 };
 
 }  // namespace ktas

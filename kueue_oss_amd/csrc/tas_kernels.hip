@@ -1346,6 +1346,43 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
   }
 }
 
+// Per phase-1 class and level above the leaves: the maximum sliceState, the
+// sliceState of the first domain of sortedDomainsWithLeader (:1511-1535) for
+// a leaderless eval.  find_level skips a level whose maximum cannot hold
+// the eval's slices without scanning it (required: notFitMessage's count,
+// :1271-1274; preferred: the recursion to the level above, :1275-1277).
+// One block per (class, level): the level's sliceState read as int4 (levels
+// start 16-byte aligned), every load of a thread issued before the reduction.
+__global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
+  __shared__ int32_t red[4];
+  const int eid = b.fill_ids[blockIdx.x];
+  const int l = blockIdx.y;
+  const int D = s.level_size[l];
+  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(eid) * b.ctr_stride + s.SD + s.level_off[l]);
+  const int nq = (D + 3) / 4;
+  int32_t m = INT32_MIN;
+  constexpr int U = 8;
+  for (int q0 = 0; q0 < nq; q0 += U * 256) {
+    int4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = ss4[min(q0 + u * 256 + int(threadIdx.x), nq - 1)];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int q = q0 + u * 256 + int(threadIdx.x);
+      if (q < nq) {
+        const int32_t e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (4 * q + k < D) m = max(m, e[k]);
+      }
+    }
+  }
+  m = group_reduce(m, 64, OpMax());
+  if (lane_id() == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) b.level_max[int64_t(eid) * kMaxLevels + l] = max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
 // Leaf-level selection partials for evals whose requested level is the leaf
 // level: per 64-leaf wave, the reductions findLevelWithFitDomains needs
 // (:1244-1270): first/last sortedDomainsWithLeader key, LFC first fit,
@@ -1515,7 +1552,7 @@ enum Field : int { F_STATE = 0, F_SLICE = 1, F_SWL = 2, F_SSWL = 3, F_LS = 4 };
 #endif
 enum ProfCat : int {
   P_LDS_SORT = 0, P_THRESHOLD, P_GATHER, P_EMIT, P_WALK, P_GLOBAL_SORT, P_UPDATE, P_FIND,
-  P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_NCAT
+  P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_FINAL, P_NCAT
 };
 
 // The select path's snapshot descriptor, in the constant address space: the
@@ -1538,8 +1575,9 @@ struct Wave {
   int32_t my_tag;
   bool dirty;
   int64_t SD;
-  Key* lds;        // per-wave LDS buffer (list_cap keys)
+  Key* lds;        // per-wave LDS buffer (list_cap keys; lds_bytes in all)
   int cap;
+  int lds_bytes;
   int32_t* listA;  // global scratch lists (lcap entries each)
   int32_t* listB;
   int32_t* listC;
@@ -1550,6 +1588,7 @@ struct Wave {
   bool overflow;
   const LeafPartial* partials;  // leaf-level partial reductions of this eval (or null)
   int nblk;
+  const int32_t* level_max;     // level_max_kernel row of this eval's class (or null)
 #if KTAS_PROFILE
   uint64_t prof[P_NCAT];
 #endif
@@ -2597,6 +2636,277 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
   return np;
 }
 
+// ---- the last descent step in LDS: leaves of the chosen parents ----
+// The leaderless BestFit descent's last step when the slice level is the
+// leaf level (:930-935 with currentLevelIdx = L-2): walk the positive
+// children of the <= 64 chosen parents (the threshold walk above: take whole
+// elements in sortedDomains order until their sliceState reaches sliceCount,
+// the crossing replaced by findBestFitDomainBy's best fit) and write the
+// (leaf, count) entries of buildAssignment (:1472-1501) directly.  The
+// parents are sorted first, so their children arrive in leaf order and the
+// output needs no sort; the candidates' (index, sliceState, state) live in
+// LDS (SoA), so every pass is an LDS sweep.  Nothing is mutated: the
+// counters of the last level are read by nobody after the walk (the counts
+// a taken leaf ends with are sliceState * sliceSize, the best fit's
+// remainder * sliceSize, exactly what the generic walk's updates + emit
+// produce).  Returns 1 (entries written, *nout), 0 (Go's nil: the leaves
+// cannot hold sliceCount) or -1 (too many parents / candidates or a
+// threshold precondition unmet: nothing written, the caller runs the
+// generic path).
+__device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t count, int32_t sliceSize,
+                               int32_t* ent, int ecap, int* nout) {
+  ProfScope prof_scope_(w, P_FINAL);
+  const DevSnap& s = g_select_snap;
+  const int lane = lane_id();
+  const int level = s.L - 2;
+  const int32_t rem = go_div32(count, sliceSize);
+  constexpr int kHist = kThrBins;  // weight per sliceState value (u32: the weight sum stays < 2^31)
+  constexpr int kMaxPar = 1024;    // parents (sorted list) and parent-bitmap words
+  if (np > kMaxPar || np <= 0 || rem <= 0) return -1;
+  const int cmax = (w.lds_bytes - (kHist + 2 * kMaxPar) * 4) / 12;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);
+  int32_t* SP = reinterpret_cast<int32_t*>(hist + kHist);  // parents in index order
+  uint32_t* BM = reinterpret_cast<uint32_t*>(SP + kMaxPar); // parent bitmap over [pmin, pmax]
+  int32_t* CI = reinterpret_cast<int32_t*>(BM + kMaxPar);   // candidates: leaf index, sliceState, state
+  int32_t* CS = CI + max(cmax, 0);
+  int32_t* CT = CS + max(cmax, 0);
+  const int poff = s.level_off[level], coff = s.level_off[level + 1];
+  const int32_t* co = s.child_off + s.child_base[level];
+  // parents in index order through an LDS bitmap (the walk above listed
+  // them in its sort order)
+  int32_t pmin = INT32_MAX, pmax = INT32_MIN;
+  for (int i = lane; i < np; i += kWave) {
+    pmin = min(pmin, parents[i]);
+    pmax = max(pmax, parents[i]);
+  }
+  pmin = group_reduce(pmin, 64, OpMin());
+  pmax = group_reduce(pmax, 64, OpMax());
+  const int words = (pmax - pmin) / 32 + 1;
+  if (cmax <= 0 || words > kMaxPar) return -1;
+  for (int i = lane; i < words; i += kWave) BM[i] = 0;
+  wave_sync();
+  for (int i = lane; i < np; i += kWave) atomicOr(&BM[(parents[i] - pmin) >> 5], 1u << ((parents[i] - pmin) & 31));
+  wave_sync();
+  int nsp = 0;
+  for (int j0 = 0; j0 < words; j0 += kWave) {
+    const int j = j0 + lane;
+    const uint32_t word = j < words ? BM[j] : 0u;
+    int tot;
+    int pos = nsp + wave_excl_scan(__popc(word), &tot);
+    for (uint32_t x = word; x; x &= x - 1) SP[pos++] = pmin + 32 * j + __builtin_ctz(x) - poff;
+    nsp += tot;
+  }
+  wave_sync();
+  // their children (leaf indices), in leaf order: 64 parents per step
+  int total = 0;
+  for (int p0 = 0; p0 < nsp; p0 += kWave) {
+    const bool act = p0 + lane < nsp;
+    const int p = act ? SP[p0 + lane] : 0;
+    const int cb = act ? co[p] : 0;
+    uint64_t mask = 0;  // positive children of this lane's parent (bit j: child cb + j)
+    int nc = 0;
+    if (w.rack_pos) {  // the fill's per-parent masks: no counter loads
+      mask = act ? w.rack_pos[p] : 0ull;
+      nc = __popcll(mask);
+    } else {
+      nc = act ? co[p + 1] - cb : 0;
+    }
+    int tot;
+    int off = total + wave_excl_scan(nc, &tot);
+    if (total + tot > cmax) return -1;
+    if (w.rack_pos) {
+      for (uint64_t m = mask; m; m &= m - 1) CI[off++] = cb + __builtin_ctzll(m);
+    } else {
+      for (int j = 0; j < nc; j++) CI[off + j] = cb + j;
+    }
+    total += tot;
+  }
+  wave_sync();
+  // the candidates' counters (clean reads: nothing of this level was walked
+  // before), kU loads in flight; without masks the non-positive ones drop
+  int n = 0;
+  for (int base = 0; base < total; base += kU * kWave) {
+    int32_t ix[kU], ss[kU], st[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) ix[u] = CI[min(base + u * kWave + lane, total - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      ss[u] = w.get_clean(F_SLICE, coff + ix[u]);
+      st[u] = w.get_clean(F_STATE, coff + ix[u]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const bool keep = base + u * kWave + lane < total && ss[u] > 0;
+      const uint64_t km = ballot(keep);
+      if (keep) {
+        const int pos = n + __popcll(km & ((1ull << lane) - 1ull));
+        CI[pos] = ix[u];
+        CS[pos] = ss[u];
+        CT[pos] = st[u];
+      }
+      n += __popcll(km);
+    }
+    wave_sync();
+  }
+  // pass A: weight (sliceState) per value, range, sum, sliceState == state everywhere
+  for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
+  wave_sync();
+  int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+  int64_t wsum = 0;
+  bool neq = false;
+  for (int i = lane; i < n; i += kWave) {
+    const int32_t v = CS[i];
+    vmin = min(vmin, v);
+    vmax = max(vmax, v);
+    wsum += v;
+    neq |= v != CT[i];
+  }
+  vmin = group_reduce(vmin, 64, OpMin());
+  vmax = group_reduce(vmax, 64, OpMax());
+  wsum = wave_sum_i64(wsum);
+  const bool all_eq = ballot(neq) == 0;
+  if (n == 0 || wsum >= (int64_t(1) << 31) || int64_t(vmax) - vmin >= kHist) return -1;
+  if (wsum < rem) return 0;  // the list cannot hold rem (:1469)
+  for (int i = lane; i < n; i += kWave) atomicAdd(&hist[CS[i] - vmin], uint32_t(CS[i]));
+  wave_sync();
+  // the crossing class t: first value (descending) whose inclusive weight reaches rem
+  int32_t t;
+  int64_t before1;
+  {
+    int64_t local[4], lsum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int b = kHist - 1 - (4 * lane + k);
+      local[k] = hist[b];
+      lsum += local[k];
+    }
+    int64_t x = lsum;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = int64_t(shfl_u64(uint64_t(x), max(lane - d, 0)));
+      if (lane >= d) x += y;
+    }
+    const uint64_t hit = ballot(x >= rem);  // exists: wsum >= rem
+    const int src = __ffsll((unsigned long long)hit) - 1;
+    int pp = -1;
+    int64_t bb = x - lsum;
+    if (lane == src) {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (pp < 0) {
+          if (bb + local[k] >= rem) pp = 4 * lane + k;
+          else bb += local[k];
+        }
+    }
+    t = vmin + (kHist - 1 - bcast(pp, src));
+    before1 = int64_t(bcast64(uint64_t(bb), src));
+  }
+  const int64_t rem1 = rem - before1;
+  // inside class t the order is state ascending: the crossing state u
+  int32_t u = t;
+  int64_t rem2 = rem1;
+  if (!all_eq) {
+    int32_t umin = INT32_MAX, umax = INT32_MIN;
+    for (int i = lane; i < n; i += kWave)
+      if (CS[i] == t) {
+        umin = min(umin, CT[i]);
+        umax = max(umax, CT[i]);
+      }
+    umin = group_reduce(umin, 64, OpMin());
+    umax = group_reduce(umax, 64, OpMax());
+    if (int64_t(umax) - umin >= kHist) return -1;
+    wave_sync();
+    for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = lane; i < n; i += kWave)
+      if (CS[i] == t) atomicAdd(&hist[CT[i] - umin], uint32_t(t));
+    wave_sync();
+    int64_t acc = 0;
+    int j = 0;
+    for (; j < kHist; j++) {  // wave-uniform walk over the class's state values
+      const uint32_t h = hist[j];
+      if (acc + h >= rem1) break;
+      acc += h;
+    }
+    u = umin + j;
+    rem2 = rem1 - acc;
+  }
+  const int64_t m = (rem2 + t - 1) / t;  // elements of class (t, u) taken; the m-th is the crossing
+  const int32_t remc = int32_t(rem2 - (m - 1) * t);
+  // the crossing: the m-th element of class (t, u) in index order (candidate order)
+  int32_t kth = -1;
+  {
+    int64_t seen = 0;
+    for (int i0 = 0; i0 < n && kth < 0; i0 += kWave) {
+      const int i = i0 + lane;
+      const bool in = i < n && CS[i] == t && CT[i] == u;
+      const uint64_t bm = ballot(in);
+      const int c = __popcll(bm);
+      if (seen + c >= m) {
+        const int r = int(m - seen);  // r-th set bit of bm (1-based)
+        const bool mine = in && __popcll(bm & ((1ull << lane) - 1ull)) == r - 1;
+        kth = CI[i0 + __ffsll((unsigned long long)ballot(mine)) - 1];
+      }
+      seen += c;
+    }
+  }
+  // key order (sortedDomains, BestFit: sliceState desc, state asc, index asc)
+  auto before_cross = [&](int32_t v, int32_t st, int32_t ix) {
+    return v > t || (v == t && (st < u || (st == u && ix < kth)));
+  };
+  // findBestFitDomainBy over the crossing and everything after it (:1216-1231):
+  // minimal sliceState >= remc, first in sorted order
+  uint64_t bv = ~0ull;  // (s_asc(weight), key rank: state then index)
+  int32_t bst = 0, bix = 0;
+  for (int i = lane; i < n; i += kWave) {
+    const int32_t v = CS[i], st = CT[i], ix = CI[i];
+    if (!before_cross(v, st, ix) && v >= remc) {
+      const uint64_t k = (uint64_t(s_asc(v)) << 32) | s_asc(st);
+      if (k < bv || (k == bv && ix < bix)) {
+        bv = k;
+        bst = st;
+        bix = ix;
+      }
+    }
+  }
+  butterfly(64, [&](auto mm) {
+    constexpr int M = decltype(mm)::value;
+    const uint64_t ov = bfly64<M>(bv);
+    const int32_t oi = bfly_i<M>(bix);
+    if (ov < bv || (ov == bv && oi < bix)) {
+      bv = ov;
+      bix = oi;
+    }
+  });
+  const int32_t chosen = bix;
+  // emission in leaf order: taken leaves with sliceState * sliceSize, the
+  // best fit with the remainder; zero counts dropped (buildAssignment :1478)
+  int cnt = 0;
+  for (int i0 = 0; i0 < n; i0 += kWave) {
+    const int i = i0 + lane;
+    int32_t ix = 0, c = 0;
+    if (i < n) {
+      ix = CI[i];
+      if (before_cross(CS[i], CT[i], ix)) c = w_mul(CS[i], sliceSize);
+      else if (ix == chosen) c = w_mul(remc, sliceSize);
+    }
+    const bool keep = c != 0;
+    const uint64_t km = ballot(keep);
+    if (keep) {
+      const int pos = cnt + __popcll(km & ((1ull << lane) - 1ull));
+      if (pos < ecap) {
+        ent[2 * pos] = ix;
+        ent[2 * pos + 1] = c;
+      }
+    }
+    cnt += __popcll(km);
+  }
+  (void)bst;
+  wave_sync();
+  *nout = cnt;
+  return 1;
+}
+
 // multiLayerNotFitMessage numbers (:1754-1793)
 __device__ void multilayer_message(Wave& w, int level, kueue_tas_eval_out& o) {
   const DevSnap& s = g_select_snap;
@@ -3188,6 +3498,22 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       o.a = level;
       return 1;
     }
+    // leaderless BestFit, no multi-layer message: when no domain of the level
+    // holds sliceCount the top of the sorted level (max sliceState) does not
+    // fit, so the level's outcome needs no scan
+    if (w.level_max && !w.leader && w.bf && level < s.L - 1 && !(ev.flags & KUEUE_TAS_F_MULTILAYER)) {
+      const int32_t mx = w.level_max[level];
+      if (mx < sliceCount) {
+        if (required) {
+          not_fit(w, level, mx, sliceCount, o);  // notFitMessage(top.sliceState, sliceCount) (:1272-1274)
+          return 1;
+        }
+        if (level > 0 && !w.unconstrained) {  // preferred: one level up (:1275-1277)
+          level--;
+          continue;
+        }
+      }
+    }
     // sortedDomainsWithLeader: first (top), last, LFC first fit, BF best fit
     Key top = key_max(), lfcfit = key_max(), last = Key{0, 0};
     int32_t minss = 0x7fffffff;
@@ -3536,6 +3862,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
 // One wave per eval of `ids` (the BestFit-side and the fast-LFC evals are
 // launched separately, on two streams).
 constexpr int kSelectWaves = 4;  // select_kernel's block = 4 waves (launch: 256 threads)
+constexpr int kFinalWalkLds = 32768;  // BestFit-side LDS bytes per wave (final_leaf_walk: ~1,960 candidates)
 __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, const int32_t* ids, int nids) {
   extern __shared__ Key lds_all[];
   const int wave = threadIdx.x >> 6;
@@ -3566,8 +3893,9 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.my_tag = b.tag_epoch;
   w.dirty = false;
   w.SD = s.SD;
-  w.lds = lds_all + int64_t(wave) * b.list_cap;
+  w.lds = lds_all + int64_t(wave) * (b.wave_lds / int(sizeof(Key)));
   w.cap = b.list_cap;
+  w.lds_bytes = b.wave_lds;
   int64_t lcap = b.scratch_stride / 6;  // 4 int32 lists (2 per u64) + 2 key arrays (2 u64 per key)
   uint64_t* sc = b.scratch + int64_t(eid) * b.scratch_stride;
   w.lcap = int(lcap);
@@ -3584,6 +3912,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.partials = (ev.requested_level == s.L - 1 && b.partial_idx[eid] >= 0)
                    ? b.partials + int64_t(b.partial_idx[eid]) * b.nblk : nullptr;
   w.nblk = b.nblk;
+  w.level_max = b.level_max ? b.level_max + int64_t(b.rep_of[eid]) * kMaxLevels : nullptr;
   int32_t* ent = b.entries + int64_t(eid) * b.entry_cap * 2;
   const int ecap = b.entry_cap;
 
@@ -3629,9 +3958,21 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
     if (!ok) o.assignment_nil = 1;
     int level = fitLevel;
     int32_t* spare = w.listA;
+    bool emitted = false;  // the last step wrote the entries itself (final_leaf_walk)
     for (; level < min(L - 1, ev.slice_level); level++) {  // above the slice level (:930-935)
       // leaderless BestFit slice walk with rem > 0: only positive children can be taken
       const bool positive = !w.leader && w.bf && go_div32(ev.count, ev.slice_size) > 0;
+      if (positive && level == L - 2 && ev.slice_level == L - 1 && !w.overflow) {
+        int nw = 0;
+        const int r = final_leaf_walk(w, cur, ncur, ev.count, ev.slice_size, ent, ecap, &nw);
+        if (r >= 0) {
+          if (r == 0) o.assignment_nil = 1;
+          o.num_workers = nw;
+          emitted = true;
+          level = L - 1;
+          break;
+        }
+      }
       int32_t* kids = positive ? w.listD : w.listC;
       int nch = positive ? gather_children_positive(w, cur, ncur, level, kids) : gather_children(w, cur, ncur, level, kids);
       int& nn = sh_ints[wave][2];
@@ -3674,7 +4015,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
       ncur = nn;
     }
     o.fit_level = fitLevel;
-    if (w.leader) {
+    if (emitted) {
+    } else if (w.leader) {
       // leaders: copies with state = leaderState (:975-994)
       int nl = 0, nw = 0;
       for (int i = 0; i < ncur; i++) {

@@ -378,7 +378,7 @@ class TASFlavorSnapshot:
         return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
     PROF = ("lds_sort", "threshold_walk", "gather", "emit", "walk_sorted", "global_sort", "update_counts", "find_level",
-            "tw_keys", "tw_select", "tw_emit", "setup")
+            "tw_keys", "tw_select", "tw_emit", "setup", "final_leaf_walk")
 
     def last_eval_profile(self, n: int):
         """Profiling build only: inclusive select-phase ticks per eval, dicts keyed by PROF."""

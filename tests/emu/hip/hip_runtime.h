@@ -290,6 +290,8 @@ inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+enum hipFuncAttribute { hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
+inline hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int) { return hipSuccess; }  // LDS is host memory here
 inline hipError_t hipEventDestroy(hipEvent_t e) { delete e; return hipSuccess; }
 
 // kernel arguments are captured by value: the launch may run after the caller's locals are gone
