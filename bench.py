@@ -427,10 +427,26 @@ def widened_rows(a, snap, snap_doc, mine, synth):
         snap.find_topology_assignments_for_flavor(w)
         lat.append((time.perf_counter() - t0) * 1e3)
     lat.sort()
+    # nodes joining (new hosts under existing racks): spliced into the tree in place
+    host = "kubernetes.io/hostname"
+    joins = []
+    for k in range(65):
+        nd = copy.deepcopy(snap_doc["nodes"][k * 983 % N])
+        nd["name"] = f"{nd['name']}-join{k}"
+        nd["labels"][host] = f"{nd['labels'][host]}-join{k}"
+        joins.append(nd)
+    t0 = time.perf_counter()
+    add1_rebuilt = snap.update_nodes(joins[:1])
+    add1_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    add_rebuilt = snap.update_nodes(joins[1:])
+    add_ms = (time.perf_counter() - t0) * 1e3
     return {"single_call_ms": {"median": round(lat[len(lat) // 2], 3), "p90": round(lat[int(len(lat) * 0.9)], 3),
                                "calls": len(lat), "path": "kueue_tas_host_find (JSON) on the C3 snapshot"},
             "node_leave_ms_per_64": round(leave_ms, 3), "node_return_ms_per_64": round(return_ms, 3),
             "node_leave_return_rebuilt": bool(left_rebuilt or back_rebuilt),
+            "node_add_ms": round(add1_ms, 3), "node_add_ms_per_64": round(add_ms, 3),
+            "node_add_rebuilt": bool(add1_rebuilt or add_rebuilt),
             "node_replacement_ms": None if rep_ms is None else round(rep_ms, 3), "node_replacement_ok": rep_ok,
             "pod_events_ms_per_64": round(pod_ms, 3),
             "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,

@@ -28,12 +28,15 @@
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <deque>
 #include <set>
 #include <stdexcept>
 #include <string>
 #include <string_view>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/kueue_tas_debug.h"
@@ -44,6 +47,89 @@
 namespace kueue_tas {
 
 using Requests = std::map<std::string, int64_t>;
+
+// fn(a, b) over [0, n) cut into contiguous ranges of at least `grain`
+// items, on up to 8 threads (the host mirror's O(N) passes).
+template <class F>
+static void parallel_ranges(size_t n, size_t grain, F fn) {
+  const size_t t = std::min<size_t>({8, std::max<unsigned>(1, std::thread::hardware_concurrency()), n / grain + 1});
+  if (t <= 1) {
+    fn(size_t(0), n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (size_t k = 1; k < t; k++) pool.emplace_back(fn, n * k / t, n * (k + 1) / t);
+  fn(size_t(0), n / t);
+  for (auto& th : pool) th.join();
+}
+
+// A leaf index by string key (DomainID, node name) through a stable slot per
+// key: reordering the leaves (FlavorSnapshot::flush_joins) rewrites one
+// contiguous int array, never the hash table.
+struct LeafIndex {
+  std::unordered_map<std::string, int32_t> slot;
+  std::vector<int32_t> leaf;
+  int32_t find(const std::string& k) const {
+    auto it = slot.find(k);
+    return it == slot.end() ? -1 : leaf[size_t(it->second)];
+  }
+  bool count(const std::string& k) const { return slot.count(k) != 0; }
+  int32_t at(const std::string& k) const { return leaf[size_t(slot.at(k))]; }
+  void add(const std::string& k, int32_t l) {  // the first leaf of a key stays
+    if (slot.emplace(k, int32_t(leaf.size())).second) leaf.push_back(l);
+  }
+  void set(const std::string& k, int32_t l) {
+    auto r = slot.emplace(k, int32_t(leaf.size()));
+    if (r.second) leaf.push_back(l);
+    else leaf[size_t(r.first->second)] = l;
+  }
+  void clear() {
+    slot.clear();
+    leaf.clear();
+  }
+  void remap(const std::vector<int32_t>& rm) {
+    for (auto& l : leaf) l = rm[size_t(l)];
+  }
+};
+
+// Per-leaf values held by pointer: reordering the leaves moves pointers, not
+// the std::map headers (whose tree root points back at its header — a cache
+// miss per moved map).
+template <class T>
+struct LeafVec {
+  std::vector<std::unique_ptr<T>> v;
+  LeafVec() = default;
+  LeafVec(const LeafVec& o) { *this = o; }
+  LeafVec(LeafVec&&) noexcept = default;
+  LeafVec& operator=(LeafVec&&) noexcept = default;
+  LeafVec& operator=(const LeafVec& o) {
+    if (this != &o) {
+      v.clear();
+      v.reserve(o.v.size());
+      for (auto& p : o.v) v.push_back(std::make_unique<T>(*p));
+    }
+    return *this;
+  }
+  T& operator[](size_t i) { return *v[i]; }
+  const T& operator[](size_t i) const { return *v[i]; }
+  size_t size() const { return v.size(); }
+  void resize(size_t n) {
+    const size_t o = v.size();
+    v.resize(n);
+    for (size_t i = o; i < n; i++) v[i] = std::make_unique<T>();
+  }
+  struct const_iterator {
+    typename std::vector<std::unique_ptr<T>>::const_iterator it;
+    const T& operator*() const { return **it; }
+    const_iterator& operator++() {
+      ++it;
+      return *this;
+    }
+    bool operator!=(const const_iterator& o) const { return it != o.it; }
+  };
+  const_iterator begin() const { return {v.begin()}; }
+  const_iterator end() const { return {v.end()}; }
+};
 static const char* kHostname = "kubernetes.io/hostname";
 
 static int64_t add64(int64_t a, int64_t b) { return int64_t(uint64_t(a) + uint64_t(b)); }
@@ -378,7 +464,7 @@ class FlavorSnapshot {
   }
   std::vector<std::vector<int32_t>> childOff;                 // [l][D_l + 1]
   std::vector<std::string> leafId;
-  std::unordered_map<std::string, int32_t> leafById;
+  LeafIndex leafById;  // DomainID -> leaf
   std::vector<const NodeInfo*> leafNode;
   // Leaves whose last node left in place (kueue_tas_snapshot_set_leaf_live):
   // out of the snapshot until that node returns; every domain above keeps a
@@ -388,13 +474,13 @@ class FlavorSnapshot {
   std::vector<int32_t> leafParent, liveUnder;
   std::unordered_map<std::string, std::pair<int32_t, size_t>> leftNodes;  // node name -> (leaf, nodes[] slot)
   int32_t live_leaf(const std::string& id) const {
-    auto it = leafById.find(id);
-    return (it == leafById.end() || leafDead[size_t(it->second)]) ? -1 : it->second;
+    const int32_t l = leafById.find(id);
+    return (l < 0 || leafDead[size_t(l)]) ? -1 : l;
   }
-  std::vector<Requests> freeCap, tasUsage;
+  LeafVec<Requests> freeCap, tasUsage;
   // non-TAS pod cache mirror (tas_non_tas_pod_cache.go:30-120), kept so pod
   // events update leaves in place: allocatable sum and member nodes per leaf
-  std::vector<Requests> leafAlloc;
+  LeafVec<Requests> leafAlloc;
   std::vector<std::vector<std::string>> leafNodeNames;
   std::unordered_map<std::string, std::string> nodeToLeaf;
   std::map<std::string, std::pair<std::string, Requests>> podUsage;
@@ -417,12 +503,12 @@ class FlavorSnapshot {
   std::map<std::string, int32_t> labelCol;
   std::vector<std::map<std::string, int32_t>> labelDict;
   std::vector<int32_t> labelValues;  // [K][N]
-  std::vector<NodeInfo> nodes;
+  std::deque<NodeInfo> nodes;  // stable addresses: leafNode points into it, nodes join in place
   std::map<std::string, std::string> flavorLabels;
   std::unordered_map<std::string, size_t> nodeIdx;  // node name -> nodes[]
   // hostname leaves by their node's name (matchFields metadata.name) and the
   // leaves whose node has no name (nodeaffinity ignores matchFields there)
-  std::unordered_map<std::string, int32_t> leafByNodeName;
+  LeafIndex leafByNodeName;
   std::vector<int32_t> unnamedLeaves;
 
   kueue_tas_ctx* ctx = nullptr;
@@ -445,7 +531,12 @@ class FlavorSnapshot {
   // (TASFlavorCache.updateUsage, tas_flavor.go:154-171, plus the
   // AddUsage/RemoveUsage updates since).  A rebuild re-assembles from that
   // state: nothing is re-parsed and no event log is kept.
+  // first-seen order of the cache's nodes (the tie rule where two nodes share
+  // a hostname leaf); leaving nodes are tombstoned in O(1) and compacted lazily
   std::vector<std::string> nodeCacheOrder;
+  std::vector<char> nodeOrderLive;
+  std::unordered_map<std::string, size_t> nodeOrderPos;
+  size_t nodeOrderDead = 0;
   std::unordered_map<std::string, NodeInfo> nodeCache;
   std::map<std::string, Requests> usageByDomain;
 
@@ -500,12 +591,31 @@ class FlavorSnapshot {
     NodeInfo ni = parse_node(n, &ready, &unsched);
     auto it = nodeCache.find(ni.name);
     if (ready && !unsched) {
-      if (it == nodeCache.end()) nodeCacheOrder.push_back(ni.name);
+      if (it == nodeCache.end()) {
+        nodeOrderPos[ni.name] = nodeCacheOrder.size();
+        nodeCacheOrder.push_back(ni.name);
+        nodeOrderLive.push_back(1);
+      }
       nodeCache[ni.name] = std::move(ni);
     } else if (it != nodeCache.end()) {
-      nodeCacheOrder.erase(std::find(nodeCacheOrder.begin(), nodeCacheOrder.end(), ni.name));
+      auto p = nodeOrderPos.find(ni.name);
+      nodeOrderLive[p->second] = 0;
+      nodeOrderPos.erase(p);
       nodeCache.erase(it);
+      if (++nodeOrderDead > 64 && 2 * nodeOrderDead > nodeCacheOrder.size()) compact_node_order();
     }
+  }
+  void compact_node_order() {
+    size_t k = 0;
+    for (size_t i = 0; i < nodeCacheOrder.size(); i++)
+      if (nodeOrderLive[i]) {
+        nodeOrderPos[nodeCacheOrder[i]] = k;
+        if (k != i) nodeCacheOrder[k] = std::move(nodeCacheOrder[i]);
+        k++;
+      }
+    nodeCacheOrder.resize(k);
+    nodeOrderLive.assign(k, 1);
+    nodeOrderDead = 0;
   }
   // A new snapshot with this one's settings and cache state (for a rebuild).
   // Usage deltas already applied on the device whose host-mirror update
@@ -539,7 +649,11 @@ class FlavorSnapshot {
     ns->gates = gates;
     ns->flavorLabels = flavorLabels;
     ns->cfg = cfg;
+    compact_node_order();
     ns->nodeCacheOrder = nodeCacheOrder;
+    ns->nodeOrderLive = nodeOrderLive;
+    ns->nodeOrderPos = nodeOrderPos;
+    ns->reqNames = reqNames;
     ns->nodeCache = nodeCache;
     ns->usageByDomain = usageByDomain;
     ns->podUsage = podUsage;
@@ -550,9 +664,9 @@ class FlavorSnapshot {
   // TASFlavorCache.snapshot (tas_flavor.go:118-138) over the cache state.
   void assemble() {
     nodes.clear();
-    nodes.reserve(nodeCacheOrder.size());
-    for (auto& name : nodeCacheOrder) {  // nodesCache.find: NodeMatchesFlavor (util/tas/node.go:21-33)
-      const NodeInfo& ni = nodeCache.at(name);
+    for (size_t o = 0; o < nodeCacheOrder.size(); o++) {  // nodesCache.find: NodeMatchesFlavor (util/tas/node.go:21-33)
+      if (!nodeOrderLive[o]) continue;
+      const NodeInfo& ni = nodeCache.at(nodeCacheOrder[o]);
       bool match = true;
       for (auto& kv : flavorLabels) {
         auto it = ni.labels.find(kv.first);
@@ -637,7 +751,7 @@ class FlavorSnapshot {
         for (size_t k = 0; k < t.lv.size(); k++) id += (k ? "," : "") + t.lv[k];
       }
       leafId[i] = id;
-      leafById[id] = i;
+      leafById.set(id, i);
       leafNode[i] = t.node;
       freeCap[i] = t.cap;
     }
@@ -645,7 +759,7 @@ class FlavorSnapshot {
     nodeIdx.clear();
     for (size_t i = 0; i < nodes.size(); i++) nodeIdx[nodes[i].name] = i;
     leafNodeNames.assign(N, {});
-    for (auto& kv : nodeToLeaf) leafNodeNames[leafById[kv.second]].push_back(kv.first);
+    for (auto& kv : nodeToLeaf) leafNodeNames[size_t(leafById.at(kv.second))].push_back(kv.first);
     leafDead.assign(size_t(N), 0);
     leftNodes.clear();
     leafParent.assign(size_t(N), 0);
@@ -677,13 +791,13 @@ class FlavorSnapshot {
     }
     // TAS usage per domain (TASFlavorCache.updateUsage, tas_flavor.go:154-171): leaves only
     for (auto& kv : usageByDomain) {
-      auto it = leafById.find(kv.first);
-      if (it != leafById.end()) req_add(tasUsage[it->second], kv.second);
+      const int32_t l = leafById.find(kv.first);
+      if (l >= 0) req_add(tasUsage[size_t(l)], kv.second);
     }
     // non-TAS pods (tas_non_tas_pod_cache.go:46-120)
     for (auto& kv : nodeUsage) {
       auto it = nodeToLeaf.find(kv.first);
-      if (it != nodeToLeaf.end()) req_sub(freeCap[leafById[it->second]], kv.second);
+      if (it != nodeToLeaf.end()) req_sub(freeCap[size_t(leafById.at(it->second))], kv.second);
     }
     // resource columns
     for (int i = 0; i < N; i++)
@@ -740,7 +854,7 @@ class FlavorSnapshot {
     if (lowestIsHostname)
       for (int i = 0; i < N; i++) {
         if (leafNode[i]->name.empty()) unnamedLeaves.push_back(i);
-        else leafByNodeName.emplace(leafNode[i]->name, i);
+        else leafByNodeName.add(leafNode[i]->name, i);
       }
   }
 
@@ -785,27 +899,29 @@ class FlavorSnapshot {
     std::set<int32_t> leaves;
     for (auto& n : touched) {
       auto it = nodeToLeaf.find(n);
-      if (it != nodeToLeaf.end()) leaves.insert(leafById[it->second]);
+      if (it != nodeToLeaf.end()) leaves.insert(leafById.at(it->second));
     }
     return push_leaves(leaves, false);
   }
 
   // ---- node events (nodesCache.sync, tas_nodes_cache.go:38-72) ----
-  // Applied in place when the tree does not change:
+  // Applied in place:
   //  * an update of a node in the snapshot that keeps it a member (Ready,
   //    schedulable, matching the flavor, every level label) at the same
-  //    topology position, whose taint list is an existing profile and whose
-  //    labels use existing label keys and values: leaf attributes only —
-  //    allocatable (freeCapacity, addCapacity :243-248), taint profile,
+  //    topology position: leaf attributes only — allocatable (freeCapacity, addCapacity :243-248), taint profile,
   //    selector label columns;
   //  * a node leaving the snapshot (NotReady, cordoned, no longer matching):
   //    its leaf loses its capacity, or, as its last node, leaves the snapshot
   //    (kueue_tas_snapshot_set_leaf_live) while its parent keeps a live leaf;
   //  * such a node returning to the same position (the leaf comes back);
-  //  * an event for a node that is not and stays not in the snapshot.
-  // Anything else (a new node, a move, a new taint profile or label value, a
-  // domain losing its last leaf) returns false: the caller rebuilds the
-  // snapshot, as the reference does every cycle.
+  //  * an event for a node that is not and stays not in the snapshot;
+  //  * a new node, or a member moving to another position: it joins in place
+  //    (add_node splices its leaf into the tree);
+  //  * a new taint profile or label value: registered, the compiled
+  //    requests recompile.
+  // A domain losing its last leaf, a node under a hostname another node
+  // shares, or a second node joining an existing hostname returns false: the
+  // caller rebuilds the snapshot, as the reference does every cycle.
   bool member_of(const NodeInfo& ni, bool ready, bool unsched) const {  // nodesCache.find (util/tas/node.go:21-33)
     if (!ready || unsched) return false;
     for (auto& kv : flavorLabels) {
@@ -816,20 +932,60 @@ class FlavorSnapshot {
       if (!ni.labels.count(l)) return false;
     return true;
   }
-  // taint profile and label ids of `ni` when they already exist (-1: rebuild)
-  int32_t known_attrs(const NodeInfo& ni) const {
+  // The taint profile of `ni`, its taint strings and its label keys / values
+  // registered (appended) when new.  *changed: compiled requests are stale
+  // (taint rows hold one entry per profile, selectors and affinity hold label
+  // value ids); *relayout: a new label column (the device arrays reload).
+  int32_t register_attrs(const NodeInfo& ni, bool* changed, bool* relayout) {
     if (!lowestIsHostname) return 0;
     std::vector<Taint> ts;
     for (auto& t : ni.taints)
       if (t.effect == "NoSchedule" || t.effect == "NoExecute") ts.push_back(t);
+    int32_t prof;
     auto pit = std::find(profiles.begin(), profiles.end(), ts);
-    if (pit == profiles.end()) return -1;
+    if (pit == profiles.end()) {
+      prof = int32_t(profiles.size());
+      profiles.push_back(ts);
+      std::vector<int32_t> ids;
+      for (auto& t : ts) {
+        const std::string s = taint_string(t);
+        auto it = taintIdByString.find(s);
+        if (it == taintIdByString.end()) {
+          it = taintIdByString.emplace(s, int32_t(taintStrings.size())).first;
+          taintStrings.push_back(s);
+        }
+        ids.push_back(it->second);
+      }
+      profileTaintIds.push_back(std::move(ids));
+      *changed = true;
+    } else {
+      prof = int32_t(pit - profiles.begin());
+    }
+    const size_t N = size_t(this->N());
     for (auto& kv : ni.labels) {
       auto c = labelCol.find(kv.first);
-      if (c == labelCol.end() || !labelDict[size_t(c->second)].count(kv.second)) return -1;
+      if (c == labelCol.end()) {  // a new label column, absent on every other leaf
+        c = labelCol.emplace(kv.first, int32_t(labelKeys.size())).first;
+        labelKeys.push_back(kv.first);
+        labelDict.emplace_back();
+        labelValues.resize(labelKeys.size() * N, 0);
+        *changed = *relayout = true;
+      }
+      auto& dict = labelDict[size_t(c->second)];
+      if (!dict.count(kv.second)) {
+        dict.emplace(kv.second, int32_t(dict.size()) + 1);
+        *changed = true;
+      }
     }
-    return int32_t(pit - profiles.begin());
+    return prof;
   }
+  // Compiled requests and host results refer to this layout (leaf indices,
+  // profiles, label ids): a new generation makes the host recompile.
+  void new_layout() {
+    col_gen = next_gen();
+    compile_gen++;
+  }
+  bool spliced = false;  // a node joined at a new topology position since the host last looked
   void set_attrs(NodeInfo& cur, NodeInfo&& ni, int32_t leaf, int32_t prof) {
     nodeCache[ni.name] = ni;
     cur.labels = std::move(ni.labels);
@@ -855,21 +1011,38 @@ class FlavorSnapshot {
     const bool member = member_of(ni, ready, unsched);
     const int L = this->L();
     auto ix = nodeIdx.find(ni.name);
+    if (!joins.empty() && (ix != nodeIdx.end() || member)) {  // reads the tree: pending joins merge first
+      bool join = ix == nodeIdx.end() && !leftNodes.count(ni.name);
+      if (join) {
+        const std::string id = lowestIsHostname ? ni.labels.at(kHostname) : [&] {
+          std::string s;
+          for (size_t k = 0; k < levelKeys.size(); k++) s += (k ? "," : "") + ni.labels.at(levelKeys[k]);
+          return s;
+        }();
+        join = !joinIds.count(id) && !leafById.count(id);
+      }
+      if (!join) flush_joins(touched, liveChanged);
+    }
     if (ix == nodeIdx.end()) {
       if (!member) {  // not in the snapshot before or after
         sync_node(n);
         return true;
       }
       auto left = leftNodes.find(ni.name);
-      if (left == leftNodes.end()) return false;  // a new node: the tree changes
+      if (left == leftNodes.end()) return add_node(n, std::move(ni), touched, liveChanged);  // a new node
       const int32_t leaf = left->second.first;
       const size_t slot = left->second.second;
       std::vector<std::string> lv;
       for (auto& k : levelKeys) lv.push_back(ni.labels.at(k));
-      if (lv != values[size_t(L - 1)][size_t(leaf)]) return false;  // moved
-      if (lowestIsHostname && ni.labels.at(kHostname) != leafId[size_t(leaf)]) return false;
-      const int32_t prof = known_attrs(ni);
-      if (prof < 0) return false;
+      if (lv != values[size_t(L - 1)][size_t(leaf)] ||
+          (lowestIsHostname && ni.labels.at(kHostname) != leafId[size_t(leaf)])) {  // back at another position
+        leftNodes.erase(left);
+        return add_node(n, std::move(ni), touched, liveChanged);
+      }
+      bool changed = false, relayout = false;
+      const int32_t prof = register_attrs(ni, &changed, &relayout);
+      if (changed) new_layout();
+      if (relayout) dirty = true;
       // back in: the node's slot, its leaf (alive again when it was its last node)
       sync_node(n);
       nodeIdx[ni.name] = slot;
@@ -888,7 +1061,15 @@ class FlavorSnapshot {
     }
     NodeInfo& cur = nodes[ix->second];
     const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
-    if (!member) {  // leaves the snapshot
+    // a hostname shared by two nodes: the leaf's taints and labels are the
+    // first node's in cache order (tas_flavor.go:165-191) — rebuilt
+    if (lowestIsHostname && leafNodeNames[size_t(leaf)].size() > 1) return false;
+    bool moved = false;  // a member at another topology position: leaves, then joins there
+    for (auto& l : levelKeys) {
+      auto a = ni.labels.find(l), b = cur.labels.find(l);
+      moved = moved || a == ni.labels.end() || b == cur.labels.end() || a->second != b->second;
+    }
+    if (!member || moved) {  // leaves the snapshot
       auto& names = leafNodeNames[size_t(leaf)];
       if (names.size() == 1) {
         if (liveUnder[size_t(leafParent[size_t(leaf)])] <= 1) return false;  // its domain would vanish
@@ -903,19 +1084,264 @@ class FlavorSnapshot {
       sync_node(n);
       realloc_leaf(leaf);
       touched->insert(leaf);
-      return true;
+      if (!moved) return true;
+      leftNodes.erase(ni.name);
+      return add_node(n, std::move(ni), touched, liveChanged);
     }
-    for (auto& l : levelKeys) {
-      auto a = ni.labels.find(l), b = cur.labels.find(l);
-      if (a == ni.labels.end() || b == cur.labels.end() || a->second != b->second) return false;
-    }
-    const int32_t prof = known_attrs(ni);
-    if (prof < 0) return false;
+    bool changed = false, relayout = false;
+    const int32_t prof = register_attrs(ni, &changed, &relayout);
+    if (changed) new_layout();
+    if (relayout) dirty = true;
     sync_node(n);
     set_attrs(cur, std::move(ni), leaf, prof);
     realloc_leaf(leaf);
     touched->insert(leaf);
     return true;
+  }
+  // A member node that is not in the snapshot joins it (nodesCache.sync,
+  // tas_nodes_cache.go:38-50, then addNode / initialize, :160-241).  Into an
+  // existing aggregated leaf (the lowest level is not hostname: addCapacity
+  // :243-248) it only adds capacity; otherwise its leaf — and any missing
+  // ancestor — joins the tree at its lexicographic position (queued, merged
+  // by flush_joins): the new leaf's capacity is allocatable - its non-TAS
+  // usage and its TAS usage the cache's for its DomainID (tas_flavor.go:
+  // 118-171), exactly what a rebuild from the cache state would assemble.
+  // The device arrays reload (one upload); compiled requests recompile
+  // (new_layout).  false (rebuild) only for a second node under an existing
+  // hostname (leafDomain.node is the first one, :165-191).
+  bool add_node(const kjson::Node& n, NodeInfo&& ni, std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
+    const int L = this->L();
+    std::vector<std::string> lv;
+    for (auto& k : levelKeys) lv.push_back(ni.labels.at(k));
+    std::string id;
+    if (lowestIsHostname) id = ni.labels.at(kHostname);
+    else
+      for (size_t k = 0; k < lv.size(); k++) id += (k ? "," : "") + lv[k];
+    if (const int32_t leaf = leafById.find(id); leaf >= 0) {
+      if (lowestIsHostname || values[size_t(L - 1)][size_t(leaf)] != lv) return false;
+      sync_node(n);  // another node of an aggregated leaf
+      nodes.push_back(std::move(ni));
+      const NodeInfo& nd = nodes.back();
+      nodeIdx[nd.name] = nodes.size() - 1;
+      nodeToLeaf[nd.name] = id;
+      leafNodeNames[size_t(leaf)].push_back(nd.name);
+      if (leafDead[size_t(leaf)]) {
+        leafDead[size_t(leaf)] = 0;
+        liveUnder[size_t(leafParent[size_t(leaf)])]++;
+        liveChanged->insert(leaf);
+      }
+      realloc_leaf(leaf);
+      touched->insert(leaf);
+      return true;
+    }
+    bool changed = false, relayout = false;
+    const int32_t prof = register_attrs(ni, &changed, &relayout);
+    sync_node(n);
+    nodes.push_back(std::move(ni));
+    const NodeInfo& nd = nodes.back();
+    nodeIdx[nd.name] = nodes.size() - 1;
+    nodeToLeaf[nd.name] = id;
+    joinIds.insert(id);
+    joins.push_back({&nd, std::move(id), std::move(lv), prof});
+    (void)touched;
+    (void)liveChanged;
+    return true;
+  }
+  // Nodes joining at new topology positions, merged into the tree together
+  // (flush_joins) — before the next event that reads the tree, and at the
+  // end of the batch.
+  struct Join {
+    const NodeInfo* node;
+    std::string id;
+    std::vector<std::string> lv;
+    int32_t prof;
+  };
+  std::vector<Join> joins;
+  std::unordered_set<std::string> joinIds;
+  std::string domain_id(int l, size_t i) const {  // utiltas.DomainID (util/tas/tas.go:29-31)
+    if (l == L() - 1) return leafId[i];
+    std::string s;
+    for (size_t k = 0; k < values[size_t(l)][i].size(); k++) s += (k ? "," : "") + values[size_t(l)][i][k];
+    return s;
+  }
+  // One merge of the pending joins: every level gains its missing prefixes at
+  // their lexicographic positions (binary searches, O(K log D) comparisons),
+  // and the level arrays, CSR offsets, DomainID ranks and every leaf-indexed
+  // array move to the new indices in one O(D) pass — what a rebuild from the
+  // cache state would assemble (tas_flavor.go:118-171), without re-sorting
+  // or re-reading a node.  Leaf sets the batch's earlier events recorded move
+  // with the leaves.
+  void flush_joins(std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
+    if (joins.empty()) return;
+    flush_mirror();  // tasUsage rows move
+    const int L = this->L();
+    std::sort(joins.begin(), joins.end(), [](const Join& a, const Join& b) { return a.lv < b.lv; });
+    std::vector<std::vector<int32_t>> remap(static_cast<size_t>(L)), fresh(static_cast<size_t>(L));  // [l][old] -> new; [l] inserted
+    for (int l = 0; l < L; l++) {
+      auto& lvl = values[size_t(l)];
+      std::vector<std::vector<std::string>> add;
+      std::vector<size_t> at;
+      for (auto& j : joins) {
+        std::vector<std::string> pre(j.lv.begin(), j.lv.begin() + l + 1);
+        if (!add.empty() && add.back() == pre) continue;
+        auto it = std::lower_bound(lvl.begin(), lvl.end(), pre);
+        if (it != lvl.end() && *it == pre) continue;
+        at.push_back(size_t(it - lvl.begin()));
+        add.push_back(std::move(pre));
+      }
+      const size_t D0 = lvl.size();
+      std::vector<std::vector<std::string>> merged;
+      merged.reserve(D0 + add.size());
+      auto& rm = remap[size_t(l)];
+      rm.resize(D0);
+      size_t a = 0;
+      for (size_t i = 0; i < D0; i++) {
+        for (; a < add.size() && at[a] == i; a++) {
+          fresh[size_t(l)].push_back(int32_t(merged.size()));
+          merged.push_back(std::move(add[a]));
+        }
+        rm[i] = int32_t(merged.size());
+        merged.push_back(std::move(lvl[i]));
+      }
+      for (; a < add.size(); a++) {
+        fresh[size_t(l)].push_back(int32_t(merged.size()));
+        merged.push_back(std::move(add[a]));
+      }
+      lvl = std::move(merged);
+    }
+    // CSR offsets: children per (new) parent, then a prefix sum
+    for (int l = 0; l + 1 < L; l++) {
+      auto& off = childOff[size_t(l)];
+      const auto& up = values[size_t(l)];
+      std::vector<int32_t> cnt(up.size(), 0);
+      for (size_t p = 0; p + 1 < off.size(); p++) cnt[size_t(remap[size_t(l)][p])] = off[p + 1] - off[p];
+      for (int32_t c : fresh[size_t(l + 1)]) {
+        const auto& v = values[size_t(l + 1)][size_t(c)];
+        const std::vector<std::string> pre(v.begin(), v.begin() + l + 1);
+        cnt[size_t(std::lower_bound(up.begin(), up.end(), pre) - up.begin())]++;
+      }
+      off.assign(up.size() + 1, 0);
+      for (size_t p = 0; p < up.size(); p++) off[p + 1] = off[p] + cnt[p];
+    }
+    // leaf-indexed arrays (joins are in leaf order: fresh[L-1][k] is joins[k]'s leaf)
+    const auto& rm = remap[size_t(L - 1)];
+    const auto& fr = fresh[size_t(L - 1)];
+    const size_t N0 = rm.size(), N = N0 + fr.size();
+    auto move_leaves = [&](auto& vec, auto make) {
+      std::remove_reference_t<decltype(vec)> out(N);
+      for (size_t i = 0; i < N0; i++) out[size_t(rm[i])] = std::move(vec[i]);
+      for (size_t k = 0; k < fr.size(); k++) out[size_t(fr[k])] = make(joins[k]);
+      vec = std::move(out);
+    };
+    auto move_boxed = [&](LeafVec<Requests>& vec, auto make) {
+      std::vector<std::unique_ptr<Requests>> out(N);
+      for (size_t i = 0; i < N0; i++) out[size_t(rm[i])] = std::move(vec.v[i]);
+      for (size_t k = 0; k < fr.size(); k++) out[size_t(fr[k])] = std::make_unique<Requests>(make(joins[k]));
+      vec.v = std::move(out);
+    };
+    move_leaves(leafId, [](const Join& j) { return j.id; });
+    move_leaves(leafNode, [](const Join& j) { return j.node; });
+    move_boxed(leafAlloc, [](const Join& j) { return j.node->allocatable; });
+    move_boxed(freeCap, [&](const Join& j) {
+      Requests f = j.node->allocatable;
+      if (auto u = nodeUsage.find(j.node->name); u != nodeUsage.end()) req_sub(f, u->second);
+      return f;
+    });
+    move_boxed(tasUsage, [&](const Join& j) {
+      auto u = usageByDomain.find(j.id);
+      return u == usageByDomain.end() ? Requests() : u->second;
+    });
+    move_leaves(leafNodeNames, [](const Join& j) { return std::vector<std::string>{j.node->name}; });
+    move_leaves(leafDead, [](const Join&) { return uint8_t(0); });
+    move_leaves(leafProfile, [](const Join& j) { return j.prof; });
+    if (!labelKeys.empty()) {
+      const size_t K = labelKeys.size();
+      std::vector<int32_t> lab(K * N, 0);
+      for (size_t k = 0; k < K; k++) {
+        const int32_t* src = labelValues.data() + k * N0;
+        int32_t* dst = lab.data() + k * N;
+        for (size_t i = 0; i < N0; i++) dst[rm[i]] = src[i];
+        for (size_t j = 0; j < fr.size(); j++) {
+          auto it = joins[j].node->labels.find(labelKeys[k]);
+          dst[fr[j]] = it == joins[j].node->labels.end() ? 0 : labelDict[k].at(it->second);
+        }
+      }
+      labelValues = std::move(lab);
+    }
+    // leaf indices held in maps: remapped in place (no re-hashing), then the joins added
+    leafById.remap(rm);
+    for (size_t k = 0; k < fr.size(); k++) leafById.set(joins[k].id, fr[k]);
+    for (auto& kv : leftNodes) kv.second.first = rm[size_t(kv.second.first)];
+    if (lowestIsHostname) {
+      leafByNodeName.remap(rm);
+      for (auto& u : unnamedLeaves) u = rm[size_t(u)];
+      for (size_t k = 0; k < fr.size(); k++) {
+        if (joins[k].node->name.empty()) unnamedLeaves.push_back(fr[k]);
+        else leafByNodeName.add(joins[k].node->name, fr[k]);
+      }
+      std::sort(unnamedLeaves.begin(), unnamedLeaves.end());
+    }
+    // leaf parents and live leaves per parent
+    leafParent.assign(N, 0);
+    liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
+    if (L >= 2) {
+      const auto& co = childOff[size_t(L - 2)];
+      for (size_t p = 0; p + 1 < co.size(); p++)
+        for (int32_t i = co[p]; i < co[p + 1]; i++) leafParent[size_t(i)] = int32_t(p);
+    }
+    for (size_t i = 0; i < N; i++)
+      if (!leafDead[i]) liveUnder[size_t(leafParent[i])]++;
+    // DomainID ranks (multiLayerNotFitMessage tie-break): each new id's
+    // position among the old ones by a binary search over the old rank order;
+    // an old domain's rank grows by the new ids placed before it
+    for (int l = 0; l < L; l++) {
+      const auto& f = fresh[size_t(l)];
+      if (f.empty()) continue;
+      auto& rk = idRank[size_t(l)];
+      const auto& rml = remap[size_t(l)];
+      const size_t D0 = rk.size();
+      std::vector<int32_t> byRank(D0);
+      for (size_t i = 0; i < D0; i++) byRank[size_t(rk[i])] = rml[i];  // new indices in old rank order
+      std::vector<std::pair<std::string, int32_t>> ids;
+      for (int32_t c : f) ids.emplace_back(domain_id(l, size_t(c)), c);
+      std::sort(ids.begin(), ids.end());
+      std::vector<int32_t> q(ids.size());
+      for (size_t k = 0; k < ids.size(); k++) {
+        size_t lo = 0, hi = D0;
+        while (lo < hi) {
+          const size_t mid = (lo + hi) / 2;
+          if (domain_id(l, size_t(byRank[mid])) < ids[k].first) lo = mid + 1;
+          else hi = mid;
+        }
+        q[k] = int32_t(lo);
+      }
+      std::vector<int32_t> out(D0 + ids.size());
+      size_t k = 0;
+      for (size_t r = 0; r < D0; r++) {
+        while (k < q.size() && size_t(q[k]) <= r) k++;
+        out[size_t(byRank[r])] = int32_t(r + k);
+      }
+      for (size_t j = 0; j < ids.size(); j++) out[size_t(ids[j].second)] = q[j] + int32_t(j);
+      rk = std::move(out);
+    }
+    leafVals.clear();
+    for (auto& j : joins)
+      for (auto& kv : j.node->allocatable)
+        if (!colByName.count(kv.first)) {
+          recolumn();
+          break;
+        }
+    for (std::set<int32_t>* set : {touched, liveChanged}) {
+      std::set<int32_t> moved;
+      for (int32_t l : *set) moved.insert(rm[size_t(l)]);
+      *set = std::move(moved);
+    }
+    touched->insert(fr.begin(), fr.end());
+    joins.clear();
+    joinIds.clear();
+    new_layout();
+    dirty = true;
+    spliced = true;
   }
   int push_liveness(const std::set<int32_t>& leaves) {
     if (dirty || !ctx || leaves.empty()) return 0;  // a reload applies leafDead itself
@@ -971,10 +1397,13 @@ class FlavorSnapshot {
   // Column sets are numbered process-wide: compiled requests hold column
   // indices, so a request compiled against an older set must be recompiled.
   uint64_t col_gen = 0;
+  static uint64_t next_gen() {  // process-wide: a generation is never reused by another snapshot
+    static std::atomic<uint64_t> gen_counter{0};
+    return ++gen_counter;
+  }
   void set_columns(const std::set<std::string>& names) {
     flush_mirror();  // pending records name columns of the old set
-    static std::atomic<uint64_t> gen_counter{0};
-    col_gen = ++gen_counter;
+    col_gen = next_gen();
     cols.assign(names.begin(), names.end());
     colByName.clear();
     colOfId.clear();
@@ -1050,20 +1479,22 @@ class FlavorSnapshot {
     for (int l = 0; l + 1 < L; l++) co.insert(co.end(), childOff[l].begin(), childOff[l].end());
     std::vector<int64_t> fr(size_t(R) * N, 0), us(size_t(R) * N, 0);
     std::vector<uint32_t> fp(N, 0), up(N, 0);
-    for (int i = 0; i < N; i++) {  // resources without a column are read by no request (wanted_columns)
-      for (auto& kv : freeCap[i]) {
-        const auto c = colByName.find(kv.first);
-        if (c == colByName.end()) continue;
-        fr[size_t(c->second) * N + i] = kv.second;
-        fp[i] |= 1u << c->second;
+    parallel_ranges(size_t(N), 8192, [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) {  // resources without a column are read by no request (wanted_columns)
+        for (auto& kv : freeCap[i]) {
+          const auto c = colByName.find(kv.first);
+          if (c == colByName.end()) continue;
+          fr[size_t(c->second) * size_t(N) + i] = kv.second;
+          fp[i] |= 1u << c->second;
+        }
+        for (auto& kv : tasUsage[i]) {
+          const auto c = colByName.find(kv.first);
+          if (c == colByName.end()) continue;
+          us[size_t(c->second) * size_t(N) + i] = kv.second;
+          up[i] |= 1u << c->second;
+        }
       }
-      for (auto& kv : tasUsage[i]) {
-        const auto c = colByName.find(kv.first);
-        if (c == colByName.end()) continue;
-        us[size_t(c->second) * N + i] = kv.second;
-        up[i] |= 1u << c->second;
-      }
-    }
+    });
     std::vector<int32_t> ranks;
     for (int l = 0; l < L; l++) ranks.insert(ranks.end(), idRank[l].begin(), idRank[l].end());
     kueue_tas_snapshot_desc d{};
@@ -1148,9 +1579,8 @@ class FlavorSnapshot {
         Requests& d = usageByDomain[u.id];
         for (auto& kv : tot) d[kv.first] = add ? add64(d[kv.first], kv.second) : sub64(d[kv.first], kv.second);
       }
-      auto it = leafById.find(u.id);
-      if (it == leafById.end()) continue;
-      const int32_t leaf = it->second;
+      const int32_t leaf = leafById.find(u.id);
+      if (leaf < 0) continue;
       for (auto& kv : tot) {
         Requests& mine = tasUsage[leaf];
         mine[kv.first] = add ? add64(mine[kv.first], kv.second) : sub64(mine[kv.first], kv.second);
@@ -1191,13 +1621,13 @@ class FlavorSnapshot {
   std::vector<kueue_tas_assumed> removal(const std::vector<DomainUsage>& us) const {
     std::map<std::pair<int32_t, int32_t>, int64_t> o;
     for (auto& u : us) {
-      auto it = leafById.find(u.id);
-      if (it == leafById.end() || leafDead[size_t(it->second)]) continue;
+      const int32_t leaf = leafById.find(u.id);
+      if (leaf < 0 || leafDead[size_t(leaf)]) continue;
       for (auto& kv : u.single) {
-        int64_t& slot = o[{it->second, colByName.at(kv.first)}];
+        int64_t& slot = o[{leaf, colByName.at(kv.first)}];
         slot = sub64(slot, mul64(kv.second, u.count));
       }
-      int64_t& pods = o[{it->second, colByName.at("pods")}];
+      int64_t& pods = o[{leaf, colByName.at("pods")}];
       pods = sub64(pods, u.count);
     }
     std::vector<kueue_tas_assumed> r;
@@ -1519,14 +1949,14 @@ class FlavorSnapshot {
         const bool in = e.op == "In";
         std::vector<int32_t> ids;
         if (e.key == "metadata.name") {
-          auto it = leafByNodeName.find(v);
+          const int32_t named = leafByNodeName.find(v);
           if (in) {
-            if (it != leafByNodeName.end()) ids.push_back(it->second);
+            if (named >= 0) ids.push_back(named);
             ids.insert(ids.end(), unnamedLeaves.begin(), unnamedLeaves.end());
             if (ids.empty()) never = true;
             else add(KUEUE_TAS_AFFINITY_LEAF, std::move(ids), false);
-          } else if (it != leafByNodeName.end()) {
-            add(KUEUE_TAS_AFFINITY_LEAF, {it->second}, true);
+          } else if (named >= 0) {
+            add(KUEUE_TAS_AFFINITY_LEAF, {named}, true);
           }
         } else if (in != v.empty()) {  // In "x" / NotIn "": only unnamed leaves pass
           if (unnamedLeaves.empty()) never = true;
@@ -3413,6 +3843,12 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
     for (; k < arr.items.size(); k++)
       if (!h->snap->node_event_in_place(arr.items[k], &touched, &liveChanged)) break;
     const bool structural = k < arr.items.size();
+    if (structural) {  // rebuilt from the cache state, which holds the pending joins
+      h->snap->joins.clear();
+      h->snap->joinIds.clear();
+    } else {
+      h->snap->flush_joins(&touched, &liveChanged);
+    }
     if (rebuilt) *rebuilt = structural ? 1 : 0;
     int rc;
     if (structural) {  // the events applied so far are in the cache state; the rest replay on it
@@ -3421,8 +3857,14 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
       rest.items.assign(arr.items.begin() + int64_t(k), arr.items.end());
       rc = rebuild(h, rest);
     } else {
+      if (h->snap->spliced) {  // leaf indices moved: results and the evaluator's caches refer to the old tree
+        h->snap->spliced = false;
+        h->ev.reset();
+        h->last.clear();
+      }
       rc = h->snap->push_liveness(liveChanged);
       if (!rc) rc = h->snap->push_leaves(touched, true);
+      if (!rc && h->snap->dirty && h->snap->ctx) rc = h->snap->upload();  // joined leaves: the reload is this event's
     }
     if (rc) h->err = h->snap->err;
     return rc;

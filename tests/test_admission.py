@@ -59,10 +59,12 @@ def test_admission_session_arith_on_gpu():
     _sessions(63, 150, gen=synth.arith_stress_case)
 
 
-def _admit_then_rebuild(make_snap):
+def _admit_then_rebuild(make_snap, splice):
     """kueue_tas_host_admit applies usage on the device and defers the host
-    mirror; a node event that forces a rebuild must see every admitted
-    record (the oracle rebuilt from a document holding that usage)."""
+    mirror; a node event that re-assembles the snapshot — a splice of a new
+    leaf (splice=True) or a rebuild (a second node under an existing
+    hostname) — must see every admitted record (the oracle rebuilt from a
+    document holding that usage)."""
     import copy
 
     snap_doc, wls = synth.config_c2(n_workloads=24, shape=(2, 2, 4, 8))
@@ -76,28 +78,32 @@ def _admit_then_rebuild(make_snap):
     for i, ok in admitted.tolist():
         if ok:
             want_doc.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
-    # a node with a new rack: not an in-place update, the snapshot is rebuilt
     extra = copy.deepcopy(snap_doc["nodes"][0])
     extra["name"] = "added-node"
-    for k in list(extra["labels"]):
-        if k != "kubernetes.io/hostname":
-            extra["labels"][k] = extra["labels"][k] + "-x"
-    extra["labels"]["kubernetes.io/hostname"] = "added-node"
+    if splice:  # a node with a new rack: spliced into the tree in place
+        for k in list(extra["labels"]):
+            if k != "kubernetes.io/hostname":
+                extra["labels"][k] = extra["labels"][k] + "-x"
+        extra["labels"]["kubernetes.io/hostname"] = "added-node"
+    # else: the first node's hostname — leafDomain.node stays the first node,
+    # the snapshot is rebuilt
     want_doc["nodes"].append(extra)
-    assert snap.update_nodes([extra]) is True  # rebuilt
+    assert snap.update_nodes([extra]) is (not splice)
     got = snap.find_topology_assignments_for_workloads(wls)
     snap.close()
     want, _ = oracle_lib.eval_workloads(want_doc, wls, threads=4)
     assert got == want
 
 
-def test_emulated_admit_then_rebuild(emu_lib):  # noqa: F811
-    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+@pytest.mark.parametrize("splice", [True, False])
+def test_emulated_admit_then_rebuild(emu_lib, splice):  # noqa: F811
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d, lib=emu_lib), splice)
 
 
 @pytest.mark.gpu
-def test_admit_then_rebuild_on_gpu():
-    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d))
+@pytest.mark.parametrize("splice", [True, False])
+def test_admit_then_rebuild_on_gpu(splice):
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d), splice)
 
 
 def _admit_batch(make, n=64, shape=(2, 2, 4, 8), huge_memory=False):

@@ -282,3 +282,85 @@ def test_emulated_leave_return_in_place(emu_lib):  # noqa: F811
 @pytest.mark.gpu
 def test_leave_return_in_place_on_gpu():
     _check_leave_return(32, 200)
+
+
+def _check_grow(seed, n, lib=None):
+    """Nodes joining the snapshot — new hosts under existing racks, under a
+    new rack or block, and members moving to another position — are spliced
+    into the tree in place, never a rebuild; every evaluation equals the
+    oracle rebuilt from the document with the events, with admitted usage
+    (also on the joined leaves) added meanwhile."""
+    rng = random.Random(seed)
+    steps_total = 0
+    for i in range(n):
+        case = synth.random_case(rng)
+        levels = case["levels"]
+        if levels[-1] != "kubernetes.io/hostname" or not case["nodes"]:
+            continue
+        snap = TASFlavorSnapshot(case, lib=lib) if lib else TASFlavorSnapshot(case)
+        ref = copy.deepcopy(case)
+        adds = []
+        for step in range(6):
+            latest = {nd["name"]: nd for nd in ref["nodes"]}
+            hosts = [nd["labels"].get("kubernetes.io/hostname") for nd in latest.values()]
+            members = [nd for nd in latest.values()
+                       if nd["conditions"] == [{"type": "Ready", "status": "True"}] and not nd["unschedulable"]
+                       and all(k in nd["labels"] for k in levels)
+                       and all(nd["labels"].get(k, "") == v for k, v in case.get("nodeLabels", {}).items())]
+            r = rng.random()
+            ev = None
+            if members and r < 0.7:
+                src = rng.choice(members)
+                ev = copy.deepcopy(src)
+                ev["labels"]["kubernetes.io/hostname"] = f"g{i}-{step}"
+                ev["name"] = f"grow-{i}-{step}"
+                k = rng.randrange(len(levels))  # levels above k keep src's values
+                for lv in levels[k:-1]:
+                    ev["labels"][lv] = f"{ev['labels'][lv]}-n{step}"
+                if rng.random() < 0.3 and hosts.count(src["labels"]["kubernetes.io/hostname"]) == 1:
+                    # a member moves: same node name at the new position (its old leaf
+                    # leaves, which needs a live sibling; otherwise a rebuild — skip)
+                    ev["name"] = src["name"]
+                    parent = [src["labels"].get(x) for x in levels[:-1]]
+                    # (a hostname shared by two nodes makes one leaf, placed by one of them)
+                    sib = [x for x in members if [x["labels"].get(y) for y in levels[:-1]] == parent
+                           and hosts.count(x["labels"].get("kubernetes.io/hostname")) == 1]
+                    if len(sib) < 2:
+                        ev["name"] = f"grow-{i}-{step}"
+            if ev is not None:
+                evs = [ev]
+                if rng.random() < 0.4:  # one batch: more joins (merged together), then an
+                    for x in range(rng.randint(1, 3)):  # update of a joined node (merged first)
+                        e2 = copy.deepcopy(ev)
+                        e2["name"] = f"grow-{i}-{step}-{x}"
+                        e2["labels"]["kubernetes.io/hostname"] = f"g{i}-{step}-{x}"
+                        if rng.random() < 0.5:
+                            e2["labels"][levels[0]] = f"{e2['labels'][levels[0]]}-m{x}"
+                        evs.append(e2)
+                    if rng.random() < 0.5:
+                        e3 = copy.deepcopy(evs[-1])
+                        e3["allocatable"]["cpu"] = e3["allocatable"].get("cpu", 0) + 500
+                        evs.append(e3)
+                assert snap.update_nodes(evs) is False, (i, step, [e["name"] for e in evs])
+                ref["nodes"] = ref["nodes"] + evs
+            else:
+                res = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+                u = synth.usage_records(case["podSets"], res)
+                if u:
+                    snap.add_usage(u)
+                    adds.append({"op": "add", "usage": u})
+            got = snap.find_topology_assignments_for_flavor(case["podSets"])
+            want = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
+            assert got == want, (i, step, got, want)
+            steps_total += 1
+        snap.close()
+    assert steps_total > 50
+
+
+def test_emulated_grow_in_place(emu_lib):  # noqa: F811
+    _check_grow(41, 60, lib=emu_lib)
+
+
+@pytest.mark.gpu
+def test_grow_in_place_on_gpu():
+    _check_grow(42, 200)
