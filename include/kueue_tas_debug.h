@@ -66,6 +66,8 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_EXCL 256u                /* fill_exclusion_kernel<true> (split stats) */
 #define KUEUE_TAS_PATH_EXCL_GLOBAL_TAINTS 512u  /* fill_exclusion_kernel<false> */
 #define KUEUE_TAS_PATH_SELECTOR_EXT 1024u       /* nodeSelector pairs beyond the inline ones */
+#define KUEUE_TAS_PATH_RAGGED_ROLLUP 2048u      /* staged fill rolls up ragged leaf parents (packed wave slots) */
+#define KUEUE_TAS_PATH_UNIFORM_ROLLUP 4096u     /* staged fill rolls up uniform power-of-two leaf parents */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 
 /* ---- host layer ---------------------------------------------------------- */

@@ -172,6 +172,8 @@ struct kueue_tas_ctx {
   DevBuf<uint8_t> d_fits;  // kueue_tas_fits: requests | terms | results
   // v1beta2 encoder: parent map (leaf mode), resident names, per-call buffers
   DevBuf<int32_t> d_parent;
+  DevBuf<int2> d_wave_tab;       // ragged parents: packed leaf waves (DevSnap::wave_tab)
+  DevBuf<int32_t> d_leaf_parent;
   DevBuf<char> d_names;
   DevBuf<int64_t> d_name_off;
   bool names_loaded = false;
@@ -313,6 +315,8 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_fits.release();
   c->d_fill_lim.release();
   c->d_parent.release();
+  c->d_wave_tab.release();
+  c->d_leaf_parent.release();
   c->d_names.release();
   c->d_name_off.release();
   c->d_enc_bytes.release();
@@ -442,6 +446,44 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
       bool ok = true;
       for (int p = 0; p <= P && ok; p++) ok = co[p] == p * F;
       if (ok) c->rack_fanout = F;
+    }
+  }
+  // otherwise, parents of at most 64 leaves: pack whole parents into waves
+  // (first fit in leaf order) so the fill still rolls them up in the wave
+  s.wave_tab = nullptr;
+  s.n_wave_slots = 0;
+  s.leaf_parent = nullptr;
+  if (c->rack_fanout == 0 && s.L >= 2 && d->level_sizes[s.L - 2] > 0 && d->child_offsets && s.N > 0) {
+    const int P = d->level_sizes[s.L - 2];
+    const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
+    bool ok = co[0] == 0 && co[P] == s.N;
+    std::vector<int2> tab;
+    std::vector<int32_t> lp(N, 0);
+    int cb = 0, cn = 0;
+    for (int p = 0; p < P && ok; p++) {
+      const int f = co[p + 1] - co[p];
+      if (f < 1 || f > kWave) {
+        ok = false;
+        break;
+      }
+      if (cn + f > kWave) {
+        tab.push_back(make_int2(cb, cn));
+        cb = co[p];
+        cn = 0;
+      }
+      cn += f;
+      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
+    }
+    if (ok) {
+      tab.push_back(make_int2(cb, cn));
+      HIPCHK(c, c->d_wave_tab.ensure(tab.size()));
+      HIPCHK(c, hipMemcpy(c->d_wave_tab.p, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+      HIPCHK(c, c->d_leaf_parent.ensure(N));
+      HIPCHK(c, hipMemcpy(c->d_leaf_parent.p, lp.data(), N * 4, hipMemcpyHostToDevice));
+      s.wave_tab = c->d_wave_tab.p;
+      s.n_wave_slots = int32_t(tab.size());
+      s.leaf_parent = c->d_leaf_parent.p;
+      c->rack_fanout = -1;
     }
   }
   // parent global domain id of every domain (v1beta2 leaf-mode encoder)
@@ -1438,9 +1480,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   c->last_stats[0] += nfill;
   if (s.N > 0 && nfchunks > 0) {
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
-    // the staged kernels take kFillTilesPerBlock leaf tiles per block
+    // the staged kernels take kFillTilesPerBlock leaf tiles per block (with
+    // ragged parents a tile is 4 packed wave slots)
     const bool staged_fill = ucols <= 8;
-    const unsigned sgx = (grid.x + kFillTilesPerBlock - 1) / kFillTilesPerBlock;
+    const unsigned stiles = ucols <= 8 && c->rack_fanout < 0 ? unsigned((s.n_wave_slots + 3) / 4) : grid.x;
+    const unsigned sgx = (stiles + kFillTilesPerBlock - 1) / kFillTilesPerBlock;
     const unsigned nblk_fill = staged_fill ? sgx : grid.x;  // blocks per fill position (stats partials)
     c->last_stats[2] += 1;
     c->last_stats[3] = ucols;
@@ -1461,6 +1505,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
     b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (b.rack_fanout) {
+      c->fill_paths |= b.rack_fanout < 0 ? KUEUE_TAS_PATH_RAGGED_ROLLUP : KUEUE_TAS_PATH_UNIFORM_ROLLUP;
       HIPCHK(c, c->d_rack_pos.ensure(n * size_t(s.level_size[s.L - 2])));
       b.rack_pos = c->d_rack_pos.p;
     }

@@ -76,6 +76,12 @@ struct DevSnap {
   const int32_t* label_values;         // [K][N] or null
   const uint8_t* leaf_dead;            // [N] 1: the leaf left the snapshot (kueue_tas_snapshot_set_leaf_live); null: none
   int32_t n_live;                      // leaves in the snapshot (ExclusionStats.TotalNodes)
+  // Ragged leaf parents (fan-out <= 64, not uniform): the staged fill's waves
+  // each take whole parents — wave slot w covers leaves [x, x + y) of
+  // wave_tab[w] — so it rolls the parents up inside the wave (null: none).
+  const int2* wave_tab;                // [n_wave_slots]
+  int32_t n_wave_slots;
+  const int32_t* leaf_parent;          // [N] parent index in level L-2 (with wave_tab)
 };
 
 // 128-bit lexicographic sort key; lo's low 32 bits hold the domain index in its level.
@@ -136,7 +142,8 @@ struct DevBatch {
   int8_t* fill_lim;        // [signature runs][N] limiting resource where the run's signature gives state 0, else -1
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)
   const int32_t* cls_members;     // eval ids
-  int32_t rack_fanout;     // > 0: the staged fill also rolls up the leaves' parents (uniform power-of-two fan-out)
+  int32_t rack_fanout;     // the staged fill also rolls up the leaves' parents: > 0 uniform power-of-two
+                           // fan-out, -1 ragged (DevSnap::wave_tab), 0 no
   uint64_t* rack_pos;      // [n][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rep rows)
   int64_t ctr_stride;      // int32 elements per eval (5 * SD)
   int32_t* counters;       // [n][5][SD]

@@ -223,6 +223,28 @@ __device__ __forceinline__ int wave_incl_scan(int x) {  // wrapping int add
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return x;
 }
+// Segmented inclusive wave scan: lane gets op over lanes [max(seg0, ...), lane]
+// of its segment (seg0: the lane's segment start; segments are contiguous).
+// The same DPP steps as wave_incl_scan, each applied only where its source
+// lane lies in the lane's segment.
+template <class Op>
+__device__ __forceinline__ int32_t seg_incl_scan(int32_t x, int lane, int seg0, Op op) {
+  const int r = lane & 15;
+  int32_t t;
+  t = __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  if (r >= 1 && lane - 1 >= seg0) x = op(x, t);
+  t = __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  if (r >= 2 && lane - 2 >= seg0) x = op(x, t);
+  t = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  if (r >= 4 && lane - 4 >= seg0) x = op(x, t);
+  t = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  if (r >= 8 && lane - 8 >= seg0) x = op(x, t);
+  t = __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 (rows 1, 3)
+  if (((lane >> 4) & 1) && seg0 <= (lane & ~15) - 1) x = op(x, t);
+  t = __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 (rows 2, 3)
+  if (lane >= 32 && seg0 <= 31) x = op(x, t);
+  return x;
+}
 __device__ __forceinline__ int wave_excl_scan(int v, int* total) {
   const int x = wave_incl_scan(v);
   *total = __builtin_amdgcn_readlane(x, 63);
@@ -689,13 +711,37 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // kFillTilesPerBlock consecutive leaf tiles per block: the setup above
   // (chunk parameters, terms, taint rows: dependent global loads) is paid
   // once per block, and the grid fits one residency round
-  const int ntiles = (s.N + kFillThreads - 1) / kFillThreads;
+  // ragged parents (rack_fanout < 0): a tile is 4 wave slots of whole parents
+  const bool packed = b.rack_fanout < 0;
+  const int ntiles = packed ? (s.n_wave_slots + 3) / 4 : (s.N + kFillThreads - 1) / kFillThreads;
   for (int tile = tgroup * kFillTilesPerBlock; tile < min(ntiles, (tgroup + 1) * kFillTilesPerBlock); tile++) {
-  const int leaf = tile * kFillThreads + threadIdx.x;
-  const bool valid = leaf < s.N;
+  const int lane = lane_id();
+  int leaf;
+  bool valid;
+  if (packed) {
+    const int slot = tile * 4 + int(threadIdx.x >> 6);
+    const int2 wt = slot < s.n_wave_slots ? s.wave_tab[slot] : make_int2(0, 0);
+    leaf = wt.x + lane;
+    valid = lane < wt.y;
+  } else {
+    leaf = tile * kFillThreads + int(threadIdx.x);
+    valid = leaf < s.N;
+  }
   const int N = s.N;
   const int gleaf = s.level_off[s.L - 1] + leaf;
-  const int lane = lane_id();
+  // ragged parents: this lane's parent, its segment's first lane, and
+  // whether it is the segment's last lane (which writes the parent)
+  int rparent = -1, seg0 = 0;
+  bool seg_tail = false;
+  if (packed) {
+    rparent = valid ? s.leaf_parent[leaf] : -1;
+    const int prevp = __shfl(rparent, lane > 0 ? lane - 1 : 0);
+    const uint64_t H = ballot(valid && (lane == 0 || prevp != rparent));
+    const uint64_t V = ballot(valid);
+    const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
+    seg0 = 63 - __builtin_clzll((H & upto) | 1ull);
+    seg_tail = valid && (lane == kWave - 1 || ((H >> (lane + 1)) & 1ull) || !((V >> (lane + 1)) & 1ull));
+  }
   int scol[NS];
   int64_t fr[NS], us[NS];
   {
@@ -966,7 +1012,57 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         }
       }
     };
-    if (rack_f == 32) rack_rollup(std::integral_constant<int, 32>());
+    // the same over ragged parents: segmented scans, the segment's last lane writes
+    auto ragged_rollup = [&]() {
+      const int32_t inner = p_inner;
+      int32_t cs = state, csw = swl;
+      if (inner != 0 && inner != 1) {
+        cs = w_mul(go_div32(cs, inner), inner);
+        csw = w_mul(go_div32(csw, inner), inner);
+      }
+      int32_t cap = cs, slc = ss, lead = ls, minD = 0x7fffffff, minSD = 0x7fffffff;
+      int has = 0;
+      if (!leader || ls > 0) {
+        has = 1;
+        minD = w_sub(cs, csw);
+        minSD = w_sub(ss, sswl);
+      }
+      cap = seg_incl_scan(cap, lane, seg0, OpWAdd());
+      if (s.L - 1 != slice_level) {
+      } else if (inner == 1 && slice_size == 1) {
+        slc = cap;
+      } else {
+        slc = seg_incl_scan(slc, lane, seg0, OpWAdd());
+      }
+      if (leader) {
+        minD = seg_incl_scan(minD, lane, seg0, OpMin());
+        minSD = seg_incl_scan(minSD, lane, seg0, OpMin());
+        lead = seg_incl_scan(lead, lane, seg0, OpMax());
+        has = seg_incl_scan(has, lane, seg0, OpMax());
+      }
+      const uint64_t posm = ballot(valid && ss > 0);
+      if (seg_tail) {
+        const int len = lane - seg0 + 1;
+        const uint64_t seg = len == kWave ? posm : (posm >> seg0) & ((1ull << len) - 1ull);
+        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + rparent] = seg;
+        const int32_t pswl = has ? w_sub(cap, minD) : 0;
+        int32_t psswl = has ? w_sub(slc, minSD) : 0;
+        if (s.L - 2 == slice_level) {
+          slc = go_div32(cap, slice_size);
+          psswl = go_div32(pswl, slice_size);
+        }
+        const int g = s.level_off[s.L - 2] + rparent;
+        base[g] = cap;
+        base[SD + g] = slc;
+        if (leader) {
+          base[2 * SD + g] = pswl;
+          base[3 * SD + g] = psswl;
+          base[4 * SD + g] = lead;
+        }
+      }
+    };
+    if (rack_f < 0) ragged_rollup();
+    else if (rack_f == 32) rack_rollup(std::integral_constant<int, 32>());
     else if (rack_f == 64) rack_rollup(std::integral_constant<int, 64>());
     else if (rack_f) rack_rollup(std::integral_constant<int, 0>());
     if (split) continue;

@@ -246,6 +246,10 @@ inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
 struct int4 {
   int x, y, z, w;
 };
+struct int2 {
+  int x, y;
+};
+inline int2 make_int2(int x, int y) { return int2{x, y}; }
 inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t st) {
   st->ops.push_back([=]() { memset(d, v, n); });
   return hipSuccess;
