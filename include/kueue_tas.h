@@ -198,6 +198,9 @@ typedef struct {
 /* count ExclusionStats inside the fill instead of the concurrent
  * fill_exclusion_kernel branch (test knob: both paths must agree) */
 #define KUEUE_TAS_CFG_INLINE_STATS 2
+/* keep single-run fill chunks on the one-leaf-per-thread staged kernel
+ * instead of fill_pair_kernel (test knob: both paths must agree) */
+#define KUEUE_TAS_CFG_NO_PAIR_FILL 4
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

@@ -145,6 +145,7 @@ struct kueue_tas_ctx {
   std::string err;
   int list_cap = 1024;
   bool inline_stats = false;  // KUEUE_TAS_CFG_INLINE_STATS
+  bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
@@ -253,6 +254,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
   if (cfg) {
     c->device = cfg->device;
     c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0;
+    c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -1491,18 +1493,26 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
+    // single-run chunks on fill_pair_kernel (two leaves per thread): staged
+    // columns, uniform fan-out >= 2 or no fused parents; it counts the
+    // ExclusionStats itself, so the batch takes the inline-stats path
+    const bool pair = c->pair_fill && staged_fill && (c->rack_fanout == 0 || c->rack_fanout >= 2);
+    const unsigned pgx = unsigned((s.N + kPairTile - 1) / kPairTile);
     if (b.nstat) {
       // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * std::max(grid.x, nblk_fill) * size_t(nstat)));
       b.fill_stats = c->d_fill_stats.p;
-    }
-    if (b.nstat && !c->inline_stats) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
-      HIPCHK(c, c->d_fill_lim.ensure(size_t(nruns) * size_t(s.N)));
-      b.stats_split = 1;
-      b.fill_lim = c->d_fill_lim.p;
+      // the reduce sums every member's stats and stores them for the class's other members
       b.cls_member_off = reinterpret_cast<const int32_t*>(ds + o_moff);
       b.cls_members = reinterpret_cast<const int32_t*>(ds + o_mem);
     }
+    if (b.nstat && !c->inline_stats && !pair) {  // staged fill: ExclusionStats by fill_exclusion_kernel on stream3
+      HIPCHK(c, c->d_fill_lim.ensure(size_t(nruns) * size_t(s.N)));
+      b.stats_split = 1;
+      b.fill_lim = c->d_fill_lim.p;
+    }
+    // partial slots per fill position: the exclusion grid (split), else the widest fill grid
+    b.nstat_blocks = int32_t(b.stats_split ? grid.x : pair ? pgx : nblk_fill);
     b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (b.rack_fanout) {
       c->fill_paths |= b.rack_fanout < 0 ? KUEUE_TAS_PATH_RAGGED_ROLLUP : KUEUE_TAS_PATH_UNIFORM_ROLLUP;
@@ -1520,12 +1530,27 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
     auto staged = [&](auto ns, auto tsv, auto mr, int first, int count, hipStream_t st) {
       if (count <= 0) return;
+      constexpr int NSv = decltype(ns)::value;
+      constexpr bool TSv = decltype(tsv)::value, MRv = decltype(mr)::value;
+      if (pair) {  // two leaves per thread
+        c->fill_paths |= KUEUE_TAS_PATH_PAIR;
+        const dim3 pg(pgx, unsigned(count));
+        if (gl && b.rack_fanout == 32)
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, 32>), pg, dim3(256), 0, st, s, b, umask, first);
+        else if (gl)
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, 0>), pg, dim3(256), 0, st, s, b, umask, first);
+        else if (b.rack_fanout == 32)
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, false, 32>), pg, dim3(256), 0, st, s, b, umask, first);
+        else
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, false, 0>), pg, dim3(256), 0, st, s, b, umask, first);
+        return;
+      }
       if (gl)
-        hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, true>),
-                           dim3(sgx, unsigned(count)), dim3(256), 0, st, s, b, umask, first);
+        hipLaunchKernelGGL((fill_leaves_staged_kernel<NSv, TSv, MRv, true>), dim3(sgx, unsigned(count)), dim3(256), 0,
+                           st, s, b, umask, first);
       else
-        hipLaunchKernelGGL((fill_leaves_staged_kernel<decltype(ns)::value, decltype(tsv)::value, decltype(mr)::value, false>),
-                           dim3(sgx, unsigned(count)), dim3(256), 0, st, s, b, umask, first);
+        hipLaunchKernelGGL((fill_leaves_staged_kernel<NSv, TSv, MRv, false>), dim3(sgx, unsigned(count)), dim3(256), 0,
+                           st, s, b, umask, first);
     };
     // the multi-run chunks (a few small signatures) run beside the single-run
     // chunks on stream2 (idle until the fill is done): their launch's ramp and
@@ -1565,7 +1590,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     if (src) return src;
     HIPCHK(c, hipGetLastError());
     if (b.nstat && !b.stats_split) {  // ExclusionStats counted inside the fill
-      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(nblk_fill));
+      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(b.nstat_blocks));
       HIPCHK(c, hipGetLastError());
     }
   }
@@ -1603,7 +1628,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  if (npairs && !b.stats_split) {  // exclusion stats of the class rep to the other members
+  if (npairs && !b.nstat) {  // exclusion stats of the class rep to the other members (global-atomic stats)
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
     HIPCHK(c, hipGetLastError());
   }

@@ -137,7 +137,8 @@ struct DevBatch {
   int32_t num_profiles;    // taint-profile rows per eval in taint_table
   int32_t nstat;           // kStatFixed + num_taints + R when the staged fill counts ExclusionStats in LDS, else 0
   int32_t nstat_R;         // R (resource columns) for fill_stats_reduce_kernel
-  int32_t* fill_stats;     // [nfill][fill blocks][nstat] per-block ExclusionStats partials
+  int32_t* fill_stats;     // [nfill][nstat_blocks][nstat] per-block ExclusionStats partials
+  int32_t nstat_blocks;    // partial slots per fill position (the widest fill grid of the batch)
   int32_t stats_split;     // 1: the staged fill leaves ExclusionStats to fill_exclusion_kernel (fill_lim)
   int8_t* fill_lim;        // [signature runs][N] limiting resource where the run's signature gives state 0, else -1
   const int32_t* cls_member_off;  // [nfill + 1] class members other than the rep, in fill order (CSR)

@@ -1118,7 +1118,441 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
     __syncthreads();
     for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
       const int e = i / b.nstat, k = i % b.nstat;
-      b.fill_stats[(int64_t(e0 + e) * gridDim.x + tgroup) * b.nstat + k] = sh_stats[e][k];
+      b.fill_stats[(int64_t(e0 + e) * b.nstat_blocks + tgroup) * b.nstat + k] = sh_stats[e][k];
+    }
+  }
+}
+
+// ---- the staged fill with two adjacent leaves per thread ----
+// Same semantics as fill_leaves_staged_kernel<NS, TS, false, GL> for chunks
+// of one signature run (CountIn before the class loop) on a snapshot whose
+// leaf parents are uniform power-of-two fan-out F >= 2 (or not rolled up,
+// F = 0), with the ExclusionStats counted in the loop.  A thread holds
+// leaves 2t and 2t+1 of a 512-leaf tile, so every per-class cost that does
+// not depend on the leaf — the parameter reads, the wave-uniform branches,
+// the counter row addresses, a ballot, a butterfly step — is paid once per
+// 128 leaves instead of 64: the parent sums start with the in-lane pair and
+// take one butterfly step fewer, the two counter words go out as one 8-byte
+// store, the ExclusionStats ballots cover two leaves each.
+constexpr int kPairTile = 2 * kFillThreads;  // leaves per pair-kernel block
+
+// Or-fold: the positive-children masks
+struct OpOr {
+  __device__ int32_t operator()(int32_t a, int32_t b) const { return a | b; }
+};
+
+// MR: chunks of several signature runs (CountIn again at each run's first
+// position, the leaves' remaining capacity kept in registers), as the
+// staged kernel's MR.
+template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none)
+__global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
+                                                                 int chunk_base) {
+  __shared__ FillEvalParams sh_p[kEvalsPerBlock];
+  __shared__ DevTerm sh_term[MR ? kEvalsPerBlock : 1][2 * NS];  // a run's worker | leader terms (at its first position)
+  __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
+  __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  const bool lds_stats = b.nstat > 0;
+  if (lds_stats)
+    for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
+  int tile = blockIdx.x, chunk = blockIdx.y;  // XCD-aware (tile, chunk) order as in the staged kernel
+  if ((gridDim.x & 7u) == 0 && gridDim.y > 1) {
+    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t g = lin >> 3;
+    chunk = int(g % gridDim.y);
+    tile = int((g / gridDim.y) * 8u + (lin & 7u));
+  }
+  chunk += chunk_base;
+  const int e0 = b.fill_chunks[2 * chunk];
+  const int ne = b.fill_chunks[2 * chunk + 1];
+  if (int(threadIdx.x) < ne) {
+    const int eid = b.fill_ids[e0 + threadIdx.x];
+    const DevEval& ev = b.evals[eid];
+    FillEvalParams& P = sh_p[threadIdx.x];
+    P.eid = eid;
+    P.taint_off = ev.taint_table;
+    P.nsel = ev.nsel;
+    P.slice_size = ev.slice_size;
+    P.slice_level = ev.slice_level;
+    P.inner = ev.ssal[s.L - 1];
+    const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
+    P.aff_begin = aff ? ev.aff_begin : -1;
+    P.aff_end = aff ? ev.aff_end : -1;
+    P.dom_begin = ev.dom_begin;
+    P.dom_end = ev.dom_end;
+    P.sel_far = 0;
+    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+      P.sel_col[k] = ev.sel_col[k];
+      P.sel_val[k] = ev.sel_val[k];
+      if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
+    }
+    P.sx_begin = ev.sx_begin;
+    P.sx_end = ev.sx_end;
+    if (ev.sx_begin >= 0) P.sel_far = 1;
+    P.run = b.fill_run[e0 + threadIdx.x];
+    P.sig_new = threadIdx.x == 0 || b.fill_run[e0 + threadIdx.x - 1] != P.run;
+    P.rmask = int32_t(ev.req_mask);
+    P.lmask = int32_t(ev.lead_mask);
+    if (MR ? P.sig_new : threadIdx.x == 0) {  // the run's terms, at its first position
+      DevTerm* t = sh_term[MR ? threadIdx.x : 0];
+      for (int j = 0; j < NS; j++) {
+        if (j < ev.nreq) t[j] = b.terms[ev.term_begin + j];
+        if (j < ev.nlead) t[NS + j] = b.terms[ev.lead_begin + j];
+      }
+    }
+  }
+  __syncthreads();
+  if (s.taint_profile && TS) {
+    for (int i = threadIdx.x; i < ne * kStagedProfiles; i += kFillThreads) {
+      const int e = i / kStagedProfiles, p = i % kStagedProfiles;
+      sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_p[e].taint_off + p] : -1;
+    }
+  }
+  __syncthreads();
+  const int lane = lane_id();
+  const int N = s.N;
+  const int leaf0 = tile * kPairTile + 2 * int(threadIdx.x);
+  const int gleaf0 = s.level_off[s.L - 1] + leaf0;
+  bool valid[2];
+  int scol[NS];
+  int64_t cap[2][NS], used[2][NS];
+  uint32_t fp[2], up[2];
+  int prof[2];
+  int32_t lab[2][kStagedLabels];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int leaf = leaf0 + j;
+    valid[j] = leaf < N;
+    fp[j] = valid[j] ? s.free_present[leaf] : 0u;
+    up[j] = valid[j] ? s.usage_present[leaf] : 0u;
+    prof[j] = (valid[j] && s.taint_profile) ? s.taint_profile[leaf] : 0;
+#pragma unroll
+    for (int k = 0; k < kStagedLabels; k++)
+      lab[j][k] = (valid[j] && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
+  }
+  {
+    uint32_t m = stage_mask;
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      scol[k] = m ? __builtin_ctz(m) : -1;
+      if (m) m &= m - 1;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        cap[j][k] = used[j][k] = 0;
+        if (valid[j] && scol[k] >= 0) {
+          cap[j][k] = s.free_cap[int64_t(scol[k]) * N + leaf0 + j];
+          used[j][k] = s.tas_usage[int64_t(scol[k]) * N + leaf0 + j];
+        }
+      }
+    }
+  }
+  // ---- base signature: remaining capacity per leaf ----
+  bool leader, live[2];
+  uint32_t pres[2];
+  {
+    const DevEval& ev = b.evals[uni(b.fill_ids[e0])];
+    const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
+    const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
+    leader = (flags & KUEUE_TAS_F_LEADER) != 0;
+    const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int leaf = leaf0 + j;
+      live[j] = valid[j] && !leaf_out(s, leaf);
+      pres[j] = fp[j] | (sim ? 0u : up[j]);
+      int a_lo = 0, a_hi = 0;
+      if (live[j] && aend > abeg) {
+        int lo = abeg, hi = aend;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (b.assumed[mid].leaf < leaf) lo = mid + 1;
+          else hi = mid;
+        }
+        a_lo = lo;
+        a_hi = lo;
+        while (a_hi < aend && b.assumed[a_hi].leaf == leaf) {
+          pres[j] |= 1u << b.assumed[a_hi].col;
+          a_hi++;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        int64_t c = sim ? cap[j][k] : int64_t(uint64_t(cap[j][k]) - uint64_t(used[j][k]));
+        for (int a = a_lo; a < a_hi; a++)
+          if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
+        cap[j][k] = c;
+      }
+    }
+  }
+  // CountInWithLimitingResource over the run's terms (LDS), ascending column order
+  auto count_slots = [&](const int64_t (&cp)[NS], const DevTerm* terms, uint32_t mask, const DevTerm* lterms,
+                         uint32_t lmask, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
+    int32_t result = 0;
+    bool any = false, done = false;
+    int lim = -1;
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      const int col = scol[k];
+      if (col >= 0 && ((mask >> col) & 1u) && !done) {
+        const DevTerm t = uni_term(terms[__popc(mask & ((1u << col) - 1u))]);
+        if (!((presm >> col) & 1u) && t.val != 0) {
+          lim = col;
+          result = 0;
+          any = true;
+          done = true;
+        } else {
+          int64_t c = cp[k];
+          if (sub_leader && ((lmask >> col) & 1u)) {
+            const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
+            c = int64_t(uint64_t(c) - uint64_t(lt.val));
+          }
+          const int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
+          if (!any || cnt < result) {
+            result = cnt;
+            lim = col;
+            any = true;
+          }
+        }
+      }
+    }
+    *lim_out = lim;
+    return any ? result : 0;
+  };
+  int32_t state0[2] = {0, 0}, swl0[2] = {0, 0}, ls0[2] = {0, 0};
+  int lim0[2] = {-1, -1};
+  auto count_run = [&](int e) {  // CountIn of the run starting at chunk position e, both leaves
+    const uint32_t rmask = uint32_t(uni(sh_p[e].rmask)), lmask = uint32_t(uni(sh_p[e].lmask));
+    const DevTerm* wt = sh_term[MR ? e : 0];
+    const DevTerm* lt = wt + NS;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      state0[j] = swl0[j] = ls0[j] = 0;
+      lim0[j] = -1;
+      if (!live[j]) continue;
+      state0[j] = count_slots(cap[j], wt, rmask, lt, lmask, pres[j], false, &lim0[j]);
+      swl0[j] = state0[j];
+      if (leader) {
+        int dummy;
+        const int32_t lc = count_slots(cap[j], lt, lmask, lt, lmask, pres[j], false, &dummy);
+        if (lc > 0) {
+          ls0[j] = 1;
+          swl0[j] = count_slots(cap[j], wt, rmask, lt, lmask, pres[j] | lmask, true, &dummy);
+        }
+      }
+    }
+  };
+  if constexpr (!MR) count_run(0);
+  const int rack_f = FC > 0 ? FC : b.rack_fanout;  // fan-out of the fused parents (0: none)
+  const int half = rack_f >> 1;                    // lanes per parent
+  const int parent = rack_f > 0 ? leaf0 / rack_f : 0;
+  const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's pair within its parent
+  const bool pair_store = (gleaf0 & 1) == 0;              // 8-byte aligned counter pairs (wave-uniform)
+  const int64_t SD = s.SD;
+  for (int e = 0; e < ne; e++) {
+    const int4* pq = reinterpret_cast<const int4*>(&sh_p[e]);
+    const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
+    if constexpr (MR) {
+      if (uni(q2.w)) count_run(e);  // sig_new
+    }
+    const int eid = uni(q0.x);
+    const int nsel = uni(q0.y);
+    const int32_t slice_size = uni(q0.z), slice_level = uni(q0.w);
+    const int32_t p_inner = uni(q1.x), sel_far = uni(q1.y), aff_begin = uni(q1.z), aff_end = uni(q1.w);
+    const int32_t dom_begin = uni(q2.x), dom_end = uni(q2.y);
+    int32_t state[2], swl[2], ls[2], ss[2], sswl[2];
+    int kind[2], id[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int leaf = leaf0 + j;
+      state[j] = swl[j] = ls[j] = 0;
+      kind[j] = (valid[j] && !live[j]) ? EX_DEAD : EX_NONE;
+      id[j] = -1;
+      if (valid[j] && kind[j] == EX_NONE) {
+        if (s.lowest_is_hostname) {
+          if (s.taint_profile) {
+            int t;
+            if constexpr (TS) t = sh_taint[e][prof[j]];
+            else t = b.taint_table[uni(q2.z) + prof[j]];
+            if (t >= 0) {
+              kind[j] = EX_TAINT;
+              id[j] = t;
+            }
+          }
+          if (kind[j] == EX_NONE && nsel > 0) {
+            const int4 c0 = pq[4], c1 = pq[5], v0 = pq[6], v1 = pq[7];
+            const int32_t sc[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            const int32_t sv[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
+            if (!GL || !sel_far) {
+#pragma unroll
+              for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+                if (k < nsel && kind[j] == EX_NONE) {
+                  const int col = uni(sc[k]);
+                  int32_t v = l0;
+                  v = col == 1 ? l1 : v;
+                  v = col == 2 ? l2 : v;
+                  v = col == 3 ? l3 : v;
+                  if (v != uni(sv[k])) kind[j] = EX_SELECTOR;
+                }
+              }
+            } else {
+              auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
+#pragma unroll
+              for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++)
+                if (k < nsel && kind[j] == EX_NONE && label_at(uni(sc[k])) != uni(sv[k])) kind[j] = EX_SELECTOR;
+              if constexpr (GL) {
+                const int32_t sxb = uni(pq[3].w);
+                if (kind[j] == EX_NONE && sxb >= 0 && !selector_ext_match(b, sxb, uni(pq[8].x), leaf, label_at))
+                  kind[j] = EX_SELECTOR;
+              }
+            }
+          }
+          if constexpr (GL) {
+            if (kind[j] == EX_NONE && aff_begin >= 0) {
+              const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
+              auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
+              if (!affinity_match(b, aff_begin, aff_end, leaf, label_at)) kind[j] = EX_AFFINITY;
+            }
+          }
+        }
+        if (kind[j] == EX_NONE && outside_domain(dom_begin, dom_end, leaf)) kind[j] = EX_TOPOLOGY;
+        if (kind[j] == EX_NONE) {
+          state[j] = state0[j];
+          swl[j] = swl0[j];
+          ls[j] = ls0[j];
+          if (state[j] == 0 && lim0[j] >= 0) {
+            kind[j] = EX_RESOURCE;
+            id[j] = lim0[j];
+          }
+        }
+      }
+      ss[j] = sswl[j] = 0;
+      if (s.L - 1 == slice_level) {
+        if (slice_size == 1) {
+          ss[j] = state[j];
+          sswl[j] = swl[j];
+        } else {
+          ss[j] = go_div32(state[j], slice_size);
+          sswl[j] = leader ? go_div32(swl[j], slice_size) : ss[j];
+        }
+      }
+    }
+    int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    auto store2 = [&](int64_t off, int32_t a, int32_t c) {  // counter words of leaves leaf0, leaf0 + 1
+      if (pair_store && valid[1]) {
+        *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(a, c);
+      } else {
+        if (valid[0]) base[off + gleaf0] = a;
+        if (valid[1]) base[off + gleaf0 + 1] = c;
+      }
+    };
+    store2(0, state[0], state[1]);
+    store2(SD, ss[0], ss[1]);
+    if (leader) {
+      store2(2 * SD, swl[0], swl[1]);
+      store2(3 * SD, sswl[0], sswl[1]);
+      store2(4 * SD, ls[0], ls[1]);
+    }
+    // fused fillInCountsHelper (:1658-1719) of the leaves' parents
+    if (rack_f > 0) {
+      const int32_t inner = p_inner;
+      int32_t cap2 = 0, slc = 0, lead = 0, minD = 0x7fffffff, minSD = 0x7fffffff, has = 0;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        int32_t cs = state[j], csw = swl[j];
+        if (inner != 0 && inner != 1) {
+          cs = w_mul(go_div32(cs, inner), inner);
+          csw = w_mul(go_div32(csw, inner), inner);
+        }
+        cap2 = w_add(cap2, cs);
+        slc = w_add(slc, ss[j]);
+        lead = max(lead, ls[j]);
+        if (!leader || ls[j] > 0) {
+          has = 1;
+          minD = min(minD, w_sub(cs, csw));
+          minSD = min(minSD, w_sub(ss[j], sswl[j]));
+        }
+      }
+      const bool same = s.L - 1 == slice_level && inner == 1 && slice_size == 1;  // wave-uniform: slc == cap2
+      cap2 = group_reduce(cap2, half, OpWAdd());
+      if (s.L - 1 != slice_level) slc = 0;
+      else if (same) slc = cap2;
+      else slc = group_reduce(slc, half, OpWAdd());
+      if (leader) {
+        minD = group_reduce(minD, half, OpMin());
+        minSD = group_reduce(minSD, half, OpMin());
+        lead = group_reduce(lead, half, OpMax());
+        has = group_reduce(has, half, OpMax());
+      }
+      // positive children: bits 2*gpos, 2*gpos + 1 of the parent's mask
+      const uint32_t pb = uint32_t(valid[0] && ss[0] > 0) | (uint32_t(valid[1] && ss[1] > 0) << 1);
+      uint64_t posm;
+      if (rack_f <= 32) {
+        posm = uint32_t(group_reduce(int32_t(pb << (2 * gpos)), half, OpOr()));
+      } else {
+        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < 16 ? pb << (2 * gpos) : 0u), half, OpOr()));
+        const uint32_t hi = uint32_t(group_reduce(int32_t(gpos >= 16 ? pb << (2 * gpos - 32) : 0u), half, OpOr()));
+        posm = (uint64_t(hi) << 32) | lo;
+      }
+      if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
+        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + parent] = posm;
+        const int32_t pswl = has ? w_sub(cap2, minD) : 0;
+        int32_t psswl = has ? w_sub(slc, minSD) : 0;
+        if (s.L - 2 == slice_level) {
+          slc = go_div32(cap2, slice_size);
+          psswl = go_div32(pswl, slice_size);
+        }
+        const int g = s.level_off[s.L - 2] + parent;
+        base[g] = cap2;
+        base[SD + g] = slc;
+        if (leader) {
+          base[2 * SD + g] = pswl;
+          base[3 * SD + g] = psswl;
+          base[4 * SD + g] = lead;
+        }
+      }
+    }
+    // ExclusionStats (:1579-1634): wave-uniform skip when no leaf of the
+    // wave's 128 is excluded; each ballot covers both leaves of a lane
+    const uint64_t any0 = ballot(valid[0] && kind[0] != EX_NONE && kind[0] != EX_DEAD);
+    const uint64_t any1 = ballot(valid[1] && kind[1] != EX_NONE && kind[1] != EX_DEAD);
+    if ((any0 | any1) == 0) continue;
+    auto count_kind = [&](int k, int slot, int32_t* gl) {
+      const int c = __popcll(ballot(kind[0] == k)) + __popcll(ballot(kind[1] == k));
+      if (lane == 0 && c) {
+        if (lds_stats) atomicAdd(&sh_stats[e][slot], c);
+        else atomicAdd(gl, c);
+      }
+    };
+    if (nsel > 0) count_kind(EX_SELECTOR, 0, &b.sel_counts[eid]);
+    if (aff_begin >= 0) count_kind(EX_AFFINITY, 1, &b.aff_counts[eid]);
+    if (dom_begin >= 0) count_kind(EX_TOPOLOGY, 2, &b.dom_counts[eid]);
+    // per taint / resource id: the first remaining lane's id, both halves counted together
+    auto count_ids = [&](int k, int slot0, int32_t* gl) {
+      uint64_t m0 = ballot(kind[0] == k), m1 = ballot(kind[1] == k);
+      while (m0 | m1) {
+        const int x = m0 ? bcast(id[0], __ffsll((unsigned long long)m0) - 1)
+                         : bcast(id[1], __ffsll((unsigned long long)m1) - 1);
+        const uint64_t h0 = ballot(kind[0] == k && id[0] == x), h1 = ballot(kind[1] == k && id[1] == x);
+        const int c = __popcll(h0) + __popcll(h1);
+        if (lane == 0) {
+          if (lds_stats) atomicAdd(&sh_stats[e][slot0 + x], c);
+          else atomicAdd(gl + x, c);
+        }
+        m0 &= ~h0;
+        m1 &= ~h1;
+      }
+    };
+    count_ids(EX_TAINT, kStatFixed, b.taint_counts + int64_t(eid) * b.num_taints);
+    count_ids(EX_RESOURCE, kStatFixed + b.num_taints, b.res_counts + int64_t(eid) * s.R);
+  }
+  if (lds_stats) {  // per-block partials [fill position][tile][stat]; slots past this grid's tiles zeroed
+    __syncthreads();
+    const int nb = b.nstat_blocks;
+    for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
+      const int e = i / b.nstat, k = i % b.nstat;
+      b.fill_stats[(int64_t(e0 + e) * nb + tile) * b.nstat + k] = sh_stats[e][k];
+      for (int t = tile + int(gridDim.x); t < nb; t += int(gridDim.x))
+        b.fill_stats[(int64_t(e0 + e) * nb + t) * b.nstat + k] = 0;
     }
   }
 }
@@ -1252,7 +1686,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_exclusion_kernel(DevSnap s,
   __syncthreads();
   for (int i = threadIdx.x; i < ne * b.nstat; i += kFillThreads) {
     const int e = i / b.nstat, k = i % b.nstat;
-    b.fill_stats[(int64_t(e0 + e) * gridDim.x + blockIdx.x) * b.nstat + k] = sh_stats[e][k];
+    b.fill_stats[(int64_t(e0 + e) * b.nstat_blocks + blockIdx.x) * b.nstat + k] = sh_stats[e][k];
   }
 }
 
@@ -3957,7 +4391,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
 
 // One wave per eval of `ids` (the BestFit-side and the fast-LFC evals are
 // launched separately, on two streams).
-constexpr int kSelectWaves = 4;  // select_kernel's block = 4 waves (launch: 256 threads)
+constexpr int kSelectWaves = 1;  // select_kernel: one wave per block (a small LDS footprint lets blocks start beside other kernels)
 constexpr int kFinalWalkLds = 32768;  // BestFit-side LDS bytes per wave (final_leaf_walk: ~1,960 candidates)
 __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, const int32_t* ids, int nids) {
   extern __shared__ Key lds_all[];

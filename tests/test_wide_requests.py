@@ -27,12 +27,19 @@ from kueue_oss_amd import TASFlavorSnapshot, synth
 
 STAGED, STAGED_GT, G4, G8, G16, G32 = 1, 2, 4, 8, 16, 32
 STAGED_GL, GLOBAL_STATS, EXCL, EXCL_GT, SEL_EXT = 64, 128, 256, 512, 1024
+PAIR = 8192
 
 WANT = {
     "cols": (G16 | G32 | GLOBAL_STATS | SEL_EXT, 0),
     "profiles": (STAGED_GT | EXCL_GT | STAGED_GL | SEL_EXT, 0),
     "slots": (GLOBAL_STATS | SEL_EXT, STAGED | STAGED_GT),
     "manyres": (SEL_EXT, 0),  # (47 names: only the requested ones become columns, no refusal)
+}
+# the same batches through fill_pair_kernel (two leaves per thread, stats in
+# its loop: no fill_exclusion_kernel)
+WANT_PAIR = {
+    "profiles": (STAGED_GT | STAGED_GL | SEL_EXT | PAIR, 0),
+    "slots": (GLOBAL_STATS | SEL_EXT | PAIR, STAGED | STAGED_GT),
 }
 
 
@@ -60,13 +67,24 @@ def _run(make, variant, seeds, n_nodes, n_workloads, want_paths=None):
 
 @pytest.mark.parametrize("variant", ["cols", "profiles", "slots", "manyres"])
 def test_emulated_wide_variants(emu_lib, variant):
-    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), variant, [0, 1], 300, 24)
+    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False), variant, [0, 1], 300, 24)
+
+
+@pytest.mark.parametrize("variant", ["profiles", "slots"])
+def test_emulated_wide_variants_pair(emu_lib, variant):
+    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), variant, [0, 1], 1600, 24, WANT_PAIR[variant])  # racks > 64 leaves
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["cols", "profiles", "slots", "manyres"])
 def test_wide_variants_on_gpu(variant):
-    _run(lambda d: TASFlavorSnapshot(d), variant, [0, 1, 2, 3], 2500, 96)
+    _run(lambda d: TASFlavorSnapshot(d, pair_fill=False), variant, [0, 1, 2, 3], 2500, 96)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["profiles", "slots"])
+def test_wide_variants_pair_on_gpu(variant):
+    _run(lambda d: TASFlavorSnapshot(d), variant, [0, 1, 2, 3], 2560, 96, WANT_PAIR[variant])
 
 
 @pytest.mark.gpu
