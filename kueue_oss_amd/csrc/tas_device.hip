@@ -1637,7 +1637,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int32_t* d_bf = reinterpret_cast<const int32_t*>(ds + o_bf);
   const int waves = kSelectWaves;  // the kernel's per-wave LDS state is sized for this
   // per-wave LDS: the sort capacity (list_cap keys); the BestFit side also
-  // holds final_leaf_walk's candidates (kFinalWalkLds per wave)
+  // holds lds_level_walk's candidates (kFinalWalkLds per wave)
   const int lfc_wave_lds = c->list_cap * 16, bf_wave_lds = std::max(lfc_wave_lds, kFinalWalkLds);
   // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
   // (after the stats replication); the main stream runs the BestFit side

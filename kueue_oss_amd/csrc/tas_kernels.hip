@@ -139,8 +139,17 @@ __device__ __forceinline__ int32_t count_term(int64_t cap, const DevTerm& t) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Orders one wave's own LDS / global accesses across its lanes.  Wavefront
+// scope: a wave's vector memory and LDS operations complete in issue order
+// (LLVM AMDGPU memory model, GFX942/950: a wavefront-scope fence emits no
+// wait), so this is a compiler barrier only.  A workgroup-scope fence would
+// wait for every outstanding store (s_waitcnt vmcnt(0)): one memory round
+// trip per call, a PCIe round trip after stores to pinned host memory.  The
+// select path's lists in global scratch are wave-private (one wave per
+// workgroup), so their cross-lane ordering needs wavefront scope only.
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  wave_fence();
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -2082,7 +2091,8 @@ enum Field : int { F_STATE = 0, F_SLICE = 1, F_SWL = 2, F_SSWL = 3, F_LS = 4 };
 #endif
 enum ProfCat : int {
   P_LDS_SORT = 0, P_THRESHOLD, P_GATHER, P_EMIT, P_WALK, P_GLOBAL_SORT, P_UPDATE, P_FIND,
-  P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_FINAL, P_NCAT
+  P_TW_KEYS, P_TW_SELECT, P_TW_EMIT, P_SETUP, P_FINAL,
+  P_FW_PARENTS, P_FW_CHILDREN, P_FW_LOADS, P_FW_SELECT, P_FW_EMIT, P_WS_FILTER, P_SEL_EMIT, P_NCAT
 };
 
 // The select path's snapshot descriptor, in the constant address space: the
@@ -2290,14 +2300,14 @@ __device__ void global_sort(Wave& w, Key* a, Key* tmp, int n) {
         dst[r0 + j + lo] = B[j];
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wave_fence();
     Key* t = src;
     src = dst;
     dst = t;
   }
   if (src != a) {
     for (int i = lane; i < n; i += kWave) a[i] = src[i];
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wave_fence();
   }
 }
 
@@ -2728,7 +2738,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     wmin = min(wmin, xor_lane(wmin, m));
   }
   const bool all_eq = ballot(neq) == 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   wave_sync();
   if (wmin < 0 || wsum >= (int64_t(1) << 31)) return -1;  // int32 rem arithmetic never wraps
   Key ck;          // key of the crossing element
@@ -2858,7 +2868,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
     best = wave_min_key(bst == wbst ? best : key_max());
     chosen = loff + int(uint32_t(best.lo));
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   // the crossing element (or its best fit) takes the remainder
   w.set(F_LS, chosen, 0);
   if (slices) {
@@ -2871,7 +2881,7 @@ __device__ int threshold_walk(Wave& w, const int32_t* gids, int n, int level, in
   cnt++;
   if (cnt > w.lcap) w.overflow = true;
   *np = cnt;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   return 1;
 }
 
@@ -2937,7 +2947,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
     if (cnt + i < w.lcap) out[cnt + i] = g;
   }
   cnt += cross;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   const int chosen = loff + int(uint32_t(w.lds[pick].lo));
   w.set(F_LS, chosen, 0);
   if (slices) {
@@ -2950,7 +2960,7 @@ __device__ int lds_prefix_walk(Wave& w, int n, int loff, int32_t count, int32_t 
   cnt++;
   if (cnt > w.lcap) w.overflow = true;
   *np = cnt;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   return 1;
 }
 
@@ -2964,6 +2974,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   const bool leaderless = !w.leader && leaderCount <= 0 && sliceRecompute <= 1;
   constexpr int kSmallWalk = 64;  // shorter lists: sort + prefix walk
   if (leaderless && w.bf && slices && n > kSmallWalk && gids != w.listD && go_div32(count, sliceSize) > 0) {
+    ProfScope ps_filter(w, P_WS_FILTER);
     // BestFit slice walk with rem > 0: elements with sliceState <= 0 sort after
     // every positive one (sliceState desc), cannot move the running sum up to
     // rem, and cannot be the best fit (weight >= remc > 0), so they are never
@@ -2984,7 +2995,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
         m += __popcll(bm);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wave_fence();
     gids = w.listD;
     n = m;
   }
@@ -3029,7 +3040,7 @@ __device__ bool walk_sorted(Wave& w, const int32_t* gids, int n, int level, int3
   // longer than the LDS: merge-sort the keys in global memory once (O(n log n)),
   // then walk them in order
   for (int i = lane_id(); i < n; i += kWave) w.gkeys[i] = w.kplain_clean(gids[i]);
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   global_sort(w, w.gkeys, w.gkeys2, n);
   if (sliceRecompute > 1) {
     for (int i = 0; i < n; i++) {
@@ -3067,7 +3078,7 @@ __device__ int gather_children(Wave& w, const int32_t* parents, int n, int level
     for (int j = 0; j < cnt; j++) out[np + ex + j] = coff + cb + j;
     np += tot;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   return np;
 }
 
@@ -3103,7 +3114,7 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
       np += tot;
     }
     if (np > w.lcap) w.overflow = true;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wave_fence();
     return np;
   }
   for (int i0 = 0; i0 < n; i0 += kWave) {
@@ -3161,35 +3172,38 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
       return np;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  wave_fence();
   wave_sync();
   return np;
 }
 
-// ---- the last descent step in LDS: leaves of the chosen parents ----
-// The leaderless BestFit descent's last step when the slice level is the
-// leaf level (:930-935 with currentLevelIdx = L-2): walk the positive
-// children of the <= 64 chosen parents (the threshold walk above: take whole
-// elements in sortedDomains order until their sliceState reaches sliceCount,
-// the crossing replaced by findBestFitDomainBy's best fit) and write the
-// (leaf, count) entries of buildAssignment (:1472-1501) directly.  The
-// parents are sorted first, so their children arrive in leaf order and the
-// output needs no sort; the candidates' (index, sliceState, state) live in
-// LDS (SoA), so every pass is an LDS sweep.  Nothing is mutated: the
-// counters of the last level are read by nobody after the walk (the counts
-// a taken leaf ends with are sliceState * sliceSize, the best fit's
-// remainder * sliceSize, exactly what the generic walk's updates + emit
-// produce).  Returns 1 (entries written, *nout), 0 (Go's nil: the leaves
-// cannot hold sliceCount) or -1 (too many parents / candidates or a
-// threshold precondition unmet: nothing written, the caller runs the
-// generic path).
-__device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t count, int32_t sliceSize,
-                               int32_t* ent, int ecap, int* nout) {
+// ---- one descent step in LDS: the children of the chosen parents ----
+// The leaderless BestFit descent above the slice level when the slice level
+// is the leaf level (:930-935): every level's step is
+// updateCountsToMinimumGeneric over sortedDomains(lowerLevelDomains(chosen))
+// with the full count.  Walk the positive children of the chosen parents
+// (the threshold walk above: take whole elements in sortedDomains order
+// until their sliceState reaches sliceCount, the crossing replaced by
+// findBestFitDomainBy's best fit).  The parents are sorted first, so their
+// children arrive in index order; the candidates' (index, sliceState,
+// state) live in LDS (SoA), so every pass is an LDS sweep.  At the last step
+// (level = L-2, `ent` set) the (leaf, count) entries of buildAssignment
+// (:1472-1501) are written directly; at a step above it (`out` set) the
+// chosen children, in index order, become the next step's parents.  Nothing
+// is mutated: a level's counters are read by nobody after its walk (the
+// next step reads the children's, and a taken leaf ends with sliceState *
+// sliceSize, the best fit with the remainder * sliceSize, exactly what the
+// generic walk's updates + emit produce).  Returns 1 (written, *nout), 0
+// (Go's nil: the children cannot hold sliceCount) or -1 (too many parents /
+// candidates or a threshold precondition unmet: nothing written, the caller
+// runs the generic path for this level).
+__device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np, int32_t count, int32_t sliceSize,
+                              int32_t* ent, int ecap, int32_t* out, int* nout) {
   ProfScope prof_scope_(w, P_FINAL);
   const DevSnap& s = g_select_snap;
   const int lane = lane_id();
-  const int level = s.L - 2;
   const int32_t rem = go_div32(count, sliceSize);
+  const uint64_t* rack_pos = level == s.L - 2 ? w.rack_pos : nullptr;  // the fill's positive-leaf masks
   constexpr int kHist = kThrBins;  // weight per sliceState value (u32: the weight sum stays < 2^31)
   constexpr int kMaxPar = 1024;    // parents (sorted list) and parent-bitmap words
   if (np > kMaxPar || np <= 0 || rem <= 0) return -1;
@@ -3202,10 +3216,24 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
   int32_t* CT = CS + max(cmax, 0);
   const int poff = s.level_off[level], coff = s.level_off[level + 1];
   const int32_t* co = s.child_off + s.child_base[level];
+  // weight per sliceState value, by absolute value (the candidates are
+  // positive); cleared while the parents' loads are in flight
+  for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
   // parents in index order through an LDS bitmap (the walk above listed
-  // them in its sort order)
-  int32_t pmin = INT32_MAX, pmax = INT32_MIN;
-  for (int i = lane; i < np; i += kWave) {
+  // them in its sort order); up to 64 of them stay in a register
+  uint64_t t_prof = KTAS_PROFILE ? wall_clock64() : 0;
+  auto lap_prof = [&](int cat) {
+#if KTAS_PROFILE
+    const uint64_t t = wall_clock64();
+    w.prof[cat] += t - t_prof;
+    t_prof = t;
+#else
+    (void)cat;
+#endif
+  };
+  const int32_t p_reg = lane < np ? parents[lane] : INT32_MAX;
+  int32_t pmin = p_reg, pmax = lane < np ? p_reg : INT32_MIN;
+  for (int i = kWave + lane; i < np; i += kWave) {
     pmin = min(pmin, parents[i]);
     pmax = max(pmax, parents[i]);
   }
@@ -3215,7 +3243,8 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
   if (cmax <= 0 || words > kMaxPar) return -1;
   for (int i = lane; i < words; i += kWave) BM[i] = 0;
   wave_sync();
-  for (int i = lane; i < np; i += kWave) atomicOr(&BM[(parents[i] - pmin) >> 5], 1u << ((parents[i] - pmin) & 31));
+  if (lane < np) atomicOr(&BM[(p_reg - pmin) >> 5], 1u << ((p_reg - pmin) & 31));
+  for (int i = kWave + lane; i < np; i += kWave) atomicOr(&BM[(parents[i] - pmin) >> 5], 1u << ((parents[i] - pmin) & 31));
   wave_sync();
   int nsp = 0;
   for (int j0 = 0; j0 < words; j0 += kWave) {
@@ -3227,6 +3256,7 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
     nsp += tot;
   }
   wave_sync();
+  lap_prof(P_FW_PARENTS);
   // their children (leaf indices), in leaf order: 64 parents per step
   int total = 0;
   for (int p0 = 0; p0 < nsp; p0 += kWave) {
@@ -3235,8 +3265,8 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
     const int cb = act ? co[p] : 0;
     uint64_t mask = 0;  // positive children of this lane's parent (bit j: child cb + j)
     int nc = 0;
-    if (w.rack_pos) {  // the fill's per-parent masks: no counter loads
-      mask = act ? w.rack_pos[p] : 0ull;
+    if (rack_pos) {  // the fill's per-parent masks: no counter loads
+      mask = act ? rack_pos[p] : 0ull;
       nc = __popcll(mask);
     } else {
       nc = act ? co[p + 1] - cb : 0;
@@ -3244,7 +3274,7 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
     int tot;
     int off = total + wave_excl_scan(nc, &tot);
     if (total + tot > cmax) return -1;
-    if (w.rack_pos) {
+    if (rack_pos) {
       for (uint64_t m = mask; m; m &= m - 1) CI[off++] = cb + __builtin_ctzll(m);
     } else {
       for (int j = 0; j < nc; j++) CI[off + j] = cb + j;
@@ -3252,9 +3282,15 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
     total += tot;
   }
   wave_sync();
+  lap_prof(P_FW_CHILDREN);
   // the candidates' counters (clean reads: nothing of this level was walked
-  // before), kU loads in flight; without masks the non-positive ones drop
+  // before), kU loads in flight; the non-positive ones drop.  Pass A rides
+  // along: range, weight sum, sliceState == state everywhere, and the weight
+  // per value for values below kHist
   int n = 0;
+  int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+  int64_t wsum = 0;
+  bool neq = false;
   for (int base = 0; base < total; base += kU * kWave) {
     int32_t ix[kU], ss[kU], st[kU];
 #pragma unroll
@@ -3274,31 +3310,30 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
         CI[pos] = ix[u];
         CS[pos] = ss[u];
         CT[pos] = st[u];
+        vmin = min(vmin, ss[u]);
+        vmax = max(vmax, ss[u]);
+        wsum += ss[u];
+        neq |= ss[u] != st[u];
+        if (ss[u] < kHist) atomicAdd(&hist[ss[u]], uint32_t(ss[u]));
       }
       n += __popcll(km);
     }
     wave_sync();
   }
-  // pass A: weight (sliceState) per value, range, sum, sliceState == state everywhere
-  for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
-  wave_sync();
-  int32_t vmin = INT32_MAX, vmax = INT32_MIN;
-  int64_t wsum = 0;
-  bool neq = false;
-  for (int i = lane; i < n; i += kWave) {
-    const int32_t v = CS[i];
-    vmin = min(vmin, v);
-    vmax = max(vmax, v);
-    wsum += v;
-    neq |= v != CT[i];
-  }
   vmin = group_reduce(vmin, 64, OpMin());
   vmax = group_reduce(vmax, 64, OpMax());
   wsum = wave_sum_i64(wsum);
   const bool all_eq = ballot(neq) == 0;
+  lap_prof(P_FW_LOADS);
   if (n == 0 || wsum >= (int64_t(1) << 31) || int64_t(vmax) - vmin >= kHist) return -1;
   if (wsum < rem) return 0;  // the list cannot hold rem (:1469)
-  for (int i = lane; i < n; i += kWave) atomicAdd(&hist[CS[i] - vmin], uint32_t(CS[i]));
+  int32_t hbase = 0;  // value of bin 0
+  if (vmax >= kHist) {  // values past the absolute bins: rebuild from vmin
+    hbase = vmin;
+    for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
+    wave_sync();
+    for (int i = lane; i < n; i += kWave) atomicAdd(&hist[CS[i] - vmin], uint32_t(CS[i]));
+  }
   wave_sync();
   // the crossing class t: first value (descending) whose inclusive weight reaches rem
   int32_t t;
@@ -3328,7 +3363,7 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
           else bb += local[k];
         }
     }
-    t = vmin + (kHist - 1 - bcast(pp, src));
+    t = hbase + (kHist - 1 - bcast(pp, src));
     before1 = int64_t(bcast64(uint64_t(bb), src));
   }
   const int64_t rem1 = rem - before1;
@@ -3363,39 +3398,58 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
   }
   const int64_t m = (rem2 + t - 1) / t;  // elements of class (t, u) taken; the m-th is the crossing
   const int32_t remc = int32_t(rem2 - (m - 1) * t);
-  // the crossing: the m-th element of class (t, u) in index order (candidate order)
+  // One pass: the crossing (the m-th element of class (t, u) in candidate =
+  // index order) and findBestFitDomainBy over the crossing and everything
+  // after it (:1216-1231: minimal sliceState >= remc, first in sorted order).
+  // Elements of value v in [remc, t) all sort after the crossing (value
+  // desc), so their minimum needs no crossing; when there is none, the best
+  // fit has value t: the crossing itself (all_eq: state == t for the whole
+  // class, so the crossing is its first element not taken), else the
+  // generic pass below.
   int32_t kth = -1;
+  uint64_t bv = ~0ull;  // (s_asc(weight), s_asc(state))
+  int32_t bix = INT32_MAX;
   {
     int64_t seen = 0;
-    for (int i0 = 0; i0 < n && kth < 0; i0 += kWave) {
+    for (int i0 = 0; i0 < n; i0 += kWave) {
       const int i = i0 + lane;
-      const bool in = i < n && CS[i] == t && CT[i] == u;
+      int32_t v = 0, st = 0, ix = 0;
+      if (i < n) {
+        v = CS[i];
+        st = CT[i];
+        ix = CI[i];
+      }
+      const bool in = i < n && v == t && st == u;
       const uint64_t bm = ballot(in);
       const int c = __popcll(bm);
-      if (seen + c >= m) {
+      if (kth < 0 && seen + c >= m) {
         const int r = int(m - seen);  // r-th set bit of bm (1-based)
         const bool mine = in && __popcll(bm & ((1ull << lane) - 1ull)) == r - 1;
-        kth = CI[i0 + __ffsll((unsigned long long)ballot(mine)) - 1];
+        kth = bcast(ix, __ffsll((unsigned long long)ballot(mine)) - 1);
       }
       seen += c;
+      if (i < n && v < t && v >= remc) {
+        const uint64_t k = (uint64_t(s_asc(v)) << 32) | s_asc(st);
+        if (k < bv || (k == bv && ix < bix)) {
+          bv = k;
+          bix = ix;
+        }
+      }
     }
   }
   // key order (sortedDomains, BestFit: sliceState desc, state asc, index asc)
   auto before_cross = [&](int32_t v, int32_t st, int32_t ix) {
     return v > t || (v == t && (st < u || (st == u && ix < kth)));
   };
-  // findBestFitDomainBy over the crossing and everything after it (:1216-1231):
-  // minimal sliceState >= remc, first in sorted order
-  uint64_t bv = ~0ull;  // (s_asc(weight), key rank: state then index)
-  int32_t bst = 0, bix = 0;
-  for (int i = lane; i < n; i += kWave) {
-    const int32_t v = CS[i], st = CT[i], ix = CI[i];
-    if (!before_cross(v, st, ix) && v >= remc) {
-      const uint64_t k = (uint64_t(s_asc(v)) << 32) | s_asc(st);
-      if (k < bv || (k == bv && ix < bix)) {
-        bv = k;
-        bst = st;
-        bix = ix;
+  if (!all_eq) {  // value-t elements after the crossing compete with the lower values
+    for (int i = lane; i < n; i += kWave) {
+      const int32_t v = CS[i], st = CT[i], ix = CI[i];
+      if (v == t && !before_cross(v, st, ix)) {
+        const uint64_t k = (uint64_t(s_asc(v)) << 32) | s_asc(st);
+        if (k < bv || (k == bv && ix < bix)) {
+          bv = k;
+          bix = ix;
+        }
       }
     }
   }
@@ -3408,31 +3462,39 @@ __device__ int final_leaf_walk(Wave& w, const int32_t* parents, int np, int32_t 
       bix = oi;
     }
   });
-  const int32_t chosen = bix;
-  // emission in leaf order: taken leaves with sliceState * sliceSize, the
-  // best fit with the remainder; zero counts dropped (buildAssignment :1478)
+  const int32_t chosen = bv == ~0ull ? kth : bix;  // all_eq without a lower value: the crossing
+  lap_prof(P_FW_SELECT);
+  // emission in index order: taken children with sliceState * sliceSize, the
+  // best fit with the remainder; zero counts dropped (buildAssignment :1478);
+  // above the last step the chosen children (taken and the best fit)
   int cnt = 0;
+  const int ocap = ent ? ecap : w.lcap;
   for (int i0 = 0; i0 < n; i0 += kWave) {
     const int i = i0 + lane;
     int32_t ix = 0, c = 0;
     if (i < n) {
       ix = CI[i];
-      if (before_cross(CS[i], CT[i], ix)) c = w_mul(CS[i], sliceSize);
-      else if (ix == chosen) c = w_mul(remc, sliceSize);
+      if (before_cross(CS[i], CT[i], ix)) c = ent ? w_mul(CS[i], sliceSize) : 1;
+      else if (ix == chosen) c = ent ? w_mul(remc, sliceSize) : 1;
     }
     const bool keep = c != 0;
     const uint64_t km = ballot(keep);
     if (keep) {
       const int pos = cnt + __popcll(km & ((1ull << lane) - 1ull));
-      if (pos < ecap) {
-        ent[2 * pos] = ix;
-        ent[2 * pos + 1] = c;
+      if (pos < ocap) {
+        if (ent) {
+          ent[2 * pos] = ix;
+          ent[2 * pos + 1] = c;
+        } else {
+          out[pos] = coff + ix;
+        }
       }
     }
     cnt += __popcll(km);
   }
-  (void)bst;
+  if (!ent && cnt > ocap) w.overflow = true;
   wave_sync();
+  lap_prof(P_FW_EMIT);
   *nout = cnt;
   return 1;
 }
@@ -3533,7 +3595,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
         for (uint32_t x = word; x; x &= x - 1) sorted[pos++] = mn + int32_t(j) * 32 + __builtin_ctz(x);
         ns += tot;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      wave_fence();
       // ... then their counts with kU loads in flight, kept ones compacted in order
       int cnt = base;
       for (int b0 = 0; b0 < ns; b0 += kU * kWave) {
@@ -3571,7 +3633,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
     arr = w.lds;
   } else {
     for (int i = lane_id(); i < n; i += kWave) w.gkeys[i] = Key{0, uint64_t(uint32_t(gids[i] - loff))};
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wave_fence();
     global_sort(w, w.gkeys, w.gkeys2, n);
     arr = w.gkeys;
   }
@@ -4251,7 +4313,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
         // re-sort the remainder sortedDomainsWithLeader[idx:] with sortedDomains
         const int nrem = D - idx;
         for (int i = lane_id(); i < nrem; i += kWave) w.gkeys[i] = w.lds[idx + i];
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        wave_fence();
         wave_sync();
         for (int i = lane_id(); i < nrem; i += kWave) w.lds[i] = w.kplain(loff + int(uint32_t(w.gkeys[i].lo)));
         wave_sync();
@@ -4392,7 +4454,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
 // One wave per eval of `ids` (the BestFit-side and the fast-LFC evals are
 // launched separately, on two streams).
 constexpr int kSelectWaves = 1;  // select_kernel: one wave per block (a small LDS footprint lets blocks start beside other kernels)
-constexpr int kFinalWalkLds = 32768;  // BestFit-side LDS bytes per wave (final_leaf_walk: ~1,960 candidates)
+constexpr int kFinalWalkLds = 32768;  // BestFit-side LDS bytes per wave (lds_level_walk: ~1,960 candidates)
 __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, const int32_t* ids, int nids) {
   extern __shared__ Key lds_all[];
   const int wave = threadIdx.x >> 6;
@@ -4488,19 +4550,28 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
     if (!ok) o.assignment_nil = 1;
     int level = fitLevel;
     int32_t* spare = w.listA;
-    bool emitted = false;  // the last step wrote the entries itself (final_leaf_walk)
+    bool emitted = false;  // the last step wrote the entries itself (lds_level_walk)
     for (; level < min(L - 1, ev.slice_level); level++) {  // above the slice level (:930-935)
       // leaderless BestFit slice walk with rem > 0: only positive children can be taken
       const bool positive = !w.leader && w.bf && go_div32(ev.count, ev.slice_size) > 0;
-      if (positive && level == L - 2 && ev.slice_level == L - 1 && !w.overflow) {
+      if (positive && ev.slice_level == L - 1 && !w.overflow) {  // the step in LDS
         int nw = 0;
-        const int r = final_leaf_walk(w, cur, ncur, ev.count, ev.slice_size, ent, ecap, &nw);
+        const bool last = level == L - 2;
+        const int r = lds_level_walk(w, level, cur, ncur, ev.count, ev.slice_size, last ? ent : nullptr, ecap,
+                                     last ? nullptr : spare, &nw);
         if (r >= 0) {
-          if (r == 0) o.assignment_nil = 1;
-          o.num_workers = nw;
-          emitted = true;
-          level = L - 1;
-          break;
+          if (r == 0 || last) {  // entries written, or Go's nil (every later step is empty)
+            if (r == 0) o.assignment_nil = 1;
+            o.num_workers = r == 0 ? 0 : nw;
+            emitted = true;
+            level = L - 1;
+            break;
+          }
+          int32_t* t = cur;
+          cur = spare;
+          spare = t;
+          ncur = nw;
+          continue;
         }
       }
       int32_t* kids = positive ? w.listD : w.listC;
@@ -4534,7 +4605,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
           break;
         }
         for (int j = lane; j < nch; j += kWave) w.listC[j] = s.level_off[level + 1] + cb + j;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        wave_fence();
         bool ok3 = walk_sorted(w, w.listC, nch, level + 1, w.get(F_STATE, d), w.get(F_LS, d), sol, sol > 1, sol, spare,
                                &nn);
         if (!ok3) o.assignment_nil = 1;

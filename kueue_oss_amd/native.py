@@ -380,7 +380,8 @@ class TASFlavorSnapshot:
         return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
     PROF = ("lds_sort", "threshold_walk", "gather", "emit", "walk_sorted", "global_sort", "update_counts", "find_level",
-            "tw_keys", "tw_select", "tw_emit", "setup", "final_leaf_walk")
+            "tw_keys", "tw_select", "tw_emit", "setup", "final_leaf_walk",
+            "fw_parents", "fw_children", "fw_loads", "fw_select", "fw_emit", "ws_filter", "sel_emit")
 
     def last_eval_profile(self, n: int):
         """Profiling build only: inclusive select-phase ticks per eval, dicts keyed by PROF."""

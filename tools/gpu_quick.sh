@@ -8,7 +8,7 @@ tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 300 python bench.py --no-cpu --no-extras > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { echo BENCH_FAILED; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench_quick.json')); print(d['value'], d['step_ms'], d['stages'], d['roofline']['frac'])"
 if [ "$1" = "probe" ]; then
-  make -s -C kueue_oss_amd/csrc prof || { echo PROF_BUILD_FAILED; exit 1; }
+  :
   timeout -k 10 200 python tools/probe_select.py --prof > gpurun_out/probe_select.log 2>&1 || { echo PROBE_FAILED; exit 1; }
   tail -12 gpurun_out/probe_select.log
 fi
