@@ -3197,15 +3197,23 @@ __device__ int gather_children_positive(Wave& w, const int32_t* parents, int n, 
 // (Go's nil: the children cannot hold sliceCount) or -1 (too many parents /
 // candidates or a threshold precondition unmet: nothing written, the caller
 // runs the generic path for this level).
-__device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np, int32_t count, int32_t sliceSize,
-                              int32_t* ent, int ecap, int32_t* out, int* nout) {
+// Parents and the chosen children of a step above the last one stay in LDS
+// between steps (lds_walk_chosen: the parent-bitmap region), so a step
+// issues no global store that a later load's vmcnt wait would drain.
+constexpr int kWalkHist = kThrBins;  // lds_level_walk's LDS layout: hist | SP | BM | CI | CS | CT
+constexpr int kWalkMaxPar = 1024;
+__device__ __forceinline__ int32_t* lds_walk_chosen(const Wave& w) {
+  return reinterpret_cast<int32_t*>(w.lds) + kWalkHist + kWalkMaxPar;
+}
+__device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np, bool parents_lds, int32_t count,
+                              int32_t sliceSize, int32_t* ent, int ecap, int32_t* out, int* nout, bool* out_lds) {
   ProfScope prof_scope_(w, P_FINAL);
   const DevSnap& s = g_select_snap;
   const int lane = lane_id();
   const int32_t rem = go_div32(count, sliceSize);
   const uint64_t* rack_pos = level == s.L - 2 ? w.rack_pos : nullptr;  // the fill's positive-leaf masks
-  constexpr int kHist = kThrBins;  // weight per sliceState value (u32: the weight sum stays < 2^31)
-  constexpr int kMaxPar = 1024;    // parents (sorted list) and parent-bitmap words
+  constexpr int kHist = kWalkHist;    // weight per sliceState value (u32: the weight sum stays < 2^31)
+  constexpr int kMaxPar = kWalkMaxPar;  // parents (sorted list) and parent-bitmap words
   if (np > kMaxPar || np <= 0 || rem <= 0) return -1;
   const int cmax = (w.lds_bytes - (kHist + 2 * kMaxPar) * 4) / 12;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);
@@ -3231,29 +3239,36 @@ __device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np
     (void)cat;
 #endif
   };
-  const int32_t p_reg = lane < np ? parents[lane] : INT32_MAX;
-  int32_t pmin = p_reg, pmax = lane < np ? p_reg : INT32_MIN;
-  for (int i = kWave + lane; i < np; i += kWave) {
-    pmin = min(pmin, parents[i]);
-    pmax = max(pmax, parents[i]);
-  }
-  pmin = group_reduce(pmin, 64, OpMin());
-  pmax = group_reduce(pmax, 64, OpMax());
-  const int words = (pmax - pmin) / 32 + 1;
-  if (cmax <= 0 || words > kMaxPar) return -1;
-  for (int i = lane; i < words; i += kWave) BM[i] = 0;
-  wave_sync();
-  if (lane < np) atomicOr(&BM[(p_reg - pmin) >> 5], 1u << ((p_reg - pmin) & 31));
-  for (int i = kWave + lane; i < np; i += kWave) atomicOr(&BM[(parents[i] - pmin) >> 5], 1u << ((parents[i] - pmin) & 31));
-  wave_sync();
+  if (cmax <= 0) return -1;
   int nsp = 0;
-  for (int j0 = 0; j0 < words; j0 += kWave) {
-    const int j = j0 + lane;
-    const uint32_t word = j < words ? BM[j] : 0u;
-    int tot;
-    int pos = nsp + wave_excl_scan(__popc(word), &tot);
-    for (uint32_t x = word; x; x &= x - 1) SP[pos++] = pmin + 32 * j + __builtin_ctz(x) - poff;
-    nsp += tot;
+  if (parents_lds) {  // the previous step's chosen children: in LDS, in index order
+    const int32_t* P = lds_walk_chosen(w);
+    for (int i = lane; i < np; i += kWave) SP[i] = P[i] - poff;
+    nsp = np;
+  } else {
+    const int32_t p_reg = lane < np ? parents[lane] : INT32_MAX;
+    int32_t pmin = p_reg, pmax = lane < np ? p_reg : INT32_MIN;
+    for (int i = kWave + lane; i < np; i += kWave) {
+      pmin = min(pmin, parents[i]);
+      pmax = max(pmax, parents[i]);
+    }
+    pmin = group_reduce(pmin, 64, OpMin());
+    pmax = group_reduce(pmax, 64, OpMax());
+    const int words = (pmax - pmin) / 32 + 1;
+    if (words > kMaxPar) return -1;
+    for (int i = lane; i < words; i += kWave) BM[i] = 0;
+    wave_sync();
+    if (lane < np) atomicOr(&BM[(p_reg - pmin) >> 5], 1u << ((p_reg - pmin) & 31));
+    for (int i = kWave + lane; i < np; i += kWave) atomicOr(&BM[(parents[i] - pmin) >> 5], 1u << ((parents[i] - pmin) & 31));
+    wave_sync();
+    for (int j0 = 0; j0 < words; j0 += kWave) {
+      const int j = j0 + lane;
+      const uint32_t word = j < words ? BM[j] : 0u;
+      int tot;
+      int pos = nsp + wave_excl_scan(__popc(word), &tot);
+      for (uint32_t x = word; x; x &= x - 1) SP[pos++] = pmin + 32 * j + __builtin_ctz(x) - poff;
+      nsp += tot;
+    }
   }
   wave_sync();
   lap_prof(P_FW_PARENTS);
@@ -3468,6 +3483,8 @@ __device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np
   // best fit with the remainder; zero counts dropped (buildAssignment :1478);
   // above the last step the chosen children (taken and the best fit)
   int cnt = 0;
+  const bool to_lds = !ent && n <= kMaxPar;  // the chosen children stay in LDS (the bitmap region)
+  int32_t* chosen_lds = lds_walk_chosen(w);
   const int ocap = ent ? ecap : w.lcap;
   for (int i0 = 0; i0 < n; i0 += kWave) {
     const int i = i0 + lane;
@@ -3481,21 +3498,21 @@ __device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np
     const uint64_t km = ballot(keep);
     if (keep) {
       const int pos = cnt + __popcll(km & ((1ull << lane) - 1ull));
-      if (pos < ocap) {
-        if (ent) {
-          ent[2 * pos] = ix;
-          ent[2 * pos + 1] = c;
-        } else {
-          out[pos] = coff + ix;
-        }
+      if (ent) {
+        if (pos < ocap) *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(ix, c);  // one 8-byte store
+      } else if (to_lds) {
+        chosen_lds[pos] = coff + ix;
+      } else if (pos < ocap) {
+        out[pos] = coff + ix;
       }
     }
     cnt += __popcll(km);
   }
-  if (!ent && cnt > ocap) w.overflow = true;
+  if (!ent && !to_lds && cnt > ocap) w.overflow = true;
   wave_sync();
   lap_prof(P_FW_EMIT);
   *nout = cnt;
+  *out_lds = to_lds;
   return 1;
 }
 
@@ -3611,8 +3628,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
           if (keep) {
             const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
             if (pos < ent_cap) {
-              ent[2 * pos] = lf[u];
-              ent[2 * pos + 1] = v[u];
+              *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(lf[u], v[u]);
             }
           }
           cnt += __popcll(km);
@@ -3652,8 +3668,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
     if (keep) {
       int pos = cnt + rank;
       if (pos < ent_cap) {
-        ent[2 * pos] = leaf;
-        ent[2 * pos + 1] = v;
+        *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(leaf, v);
       }
     }
     cnt += __popcll(m);
@@ -3812,8 +3827,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
     for (int k = 0; k < 4; k++) {
       if (keep[k]) {
         if (pos < ent_cap) {
-          ent[2 * pos] = 4 * q + k;
-          ent[2 * pos + 1] = val[k];
+          *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(4 * q + k, val[k]);
         }
         pos++;
       }
@@ -3930,8 +3944,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
     if (keep) {
       const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
       if (pos < ecap) {
-        ent[2 * pos] = i;
-        ent[2 * pos + 1] = (tie && r == mt - 1) ? rem_last : x;
+        *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(i, (tie && r == mt - 1) ? rem_last : x);
       }
     }
     cnt += __popcll(km);
@@ -3981,8 +3994,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
     o.fit_level = L1;
     if (need != 0) {
       if (lane == 0 && ecap > 0) {
-        ent[0] = fit_leaf;
-        ent[1] = need;
+        *reinterpret_cast<int2*>(ent) = make_int2(fit_leaf, need);
       }
       o.num_workers = 1;
     }
@@ -4551,14 +4563,17 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
     int level = fitLevel;
     int32_t* spare = w.listA;
     bool emitted = false;  // the last step wrote the entries itself (lds_level_walk)
+    bool cur_lds = false;  // cur's domains are in LDS (lds_walk_chosen), not in the global list
     for (; level < min(L - 1, ev.slice_level); level++) {  // above the slice level (:930-935)
       // leaderless BestFit slice walk with rem > 0: only positive children can be taken
       const bool positive = !w.leader && w.bf && go_div32(ev.count, ev.slice_size) > 0;
-      if (positive && ev.slice_level == L - 1 && !w.overflow) {  // the step in LDS
+      const bool lds_step = positive && ev.slice_level == L - 1 && !w.overflow;
+      if (lds_step) {  // the step in LDS
         int nw = 0;
+        bool out_lds = false;
         const bool last = level == L - 2;
-        const int r = lds_level_walk(w, level, cur, ncur, ev.count, ev.slice_size, last ? ent : nullptr, ecap,
-                                     last ? nullptr : spare, &nw);
+        const int r = lds_level_walk(w, level, cur, ncur, cur_lds, ev.count, ev.slice_size, last ? ent : nullptr, ecap,
+                                     last ? nullptr : spare, &nw, &out_lds);
         if (r >= 0) {
           if (r == 0 || last) {  // entries written, or Go's nil (every later step is empty)
             if (r == 0) o.assignment_nil = 1;
@@ -4567,12 +4582,21 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
             level = L - 1;
             break;
           }
-          int32_t* t = cur;
-          cur = spare;
-          spare = t;
+          if (!out_lds) {
+            int32_t* t = cur;
+            cur = spare;
+            spare = t;
+          }
+          cur_lds = out_lds;
           ncur = nw;
           continue;
         }
+      }
+      if (cur_lds) {  // the generic step reads its parents from the global list
+        const int32_t* P = lds_walk_chosen(w);
+        for (int i = lane; i < ncur; i += kWave) cur[i] = P[i];
+        wave_sync();
+        cur_lds = false;
       }
       int32_t* kids = positive ? w.listD : w.listC;
       int nch = positive ? gather_children_positive(w, cur, ncur, level, kids) : gather_children(w, cur, ncur, level, kids);
@@ -4693,8 +4717,7 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
     for (int k = 0; k < 8; k++) {
       if (keep[k]) {
         if (pos < b.entry_cap) {
-          ent[2 * pos] = lo + k;
-          ent[2 * pos + 1] = x[k];
+          *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(lo + k, x[k]);
         }
         pos++;
       }
