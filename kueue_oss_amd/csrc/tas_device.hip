@@ -1589,12 +1589,19 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     if (src) return src;
     HIPCHK(c, hipGetLastError());
-    if (b.nstat && !b.stats_split) {  // ExclusionStats counted inside the fill
-      hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, b, int(b.nstat_blocks));
-      HIPCHK(c, hipGetLastError());
-    }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  // ExclusionStats on stream3 beside the roll-up / select, joined before the
+  // D2H: the reduce of the fill's per-block partials (counted inside the
+  // fill), or the split path's counting kernel + reduce
+  const bool stats_branch = b.nstat > 0;
+  if (stats_branch && !b.stats_split) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
+    HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
+    hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(b.nstat_blocks));
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->evs[1], c->stream3));
+  }
   if (b.stats_split) {  // counts, reduce and member stores beside the roll-up / select
     HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
     HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
@@ -1675,7 +1682,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
-  if (b.stats_split) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
+  if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
@@ -1716,7 +1723,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const float partials = st[3];  // ev4 -> ev5: leaf partials; stage [3] reports the concurrent fast-LFC branch
   st[3] = 0.f;
   if (nfast) (void)hipEventElapsedTime(&st[3], c->evl[0], c->evl[1]);
-  if (b.stats_split) (void)hipEventElapsedTime(&st[2], c->evs[0], c->evs[1]);  // the concurrent stats branch
+  if (b.nstat > 0) (void)hipEventElapsedTime(&st[2], c->evs[0], c->evs[1]);  // the concurrent stats branch
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
   for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
   ms[0] += st[0];                    // fill (+ exclusion stats reduce)

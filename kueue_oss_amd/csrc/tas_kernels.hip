@@ -1367,73 +1367,87 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const int32_t slice_size = uni(q0.z), slice_level = uni(q0.w);
     const int32_t p_inner = uni(q1.x), sel_far = uni(q1.y), aff_begin = uni(q1.z), aff_end = uni(q1.w);
     const int32_t dom_begin = uni(q2.x), dom_end = uni(q2.y);
+    // per-leaf classification as selects (fillInCounts :1578-1643, first
+    // exclusion wins: taint, nodeSelector, affinity, required domain, then
+    // a resource giving state 0): every condition below is either
+    // wave-uniform (a scalar branch) or a v_cndmask, no divergent branch
     int32_t state[2], swl[2], ls[2], ss[2], sswl[2];
     int kind[2], id[2];
+    const bool hn = s.lowest_is_hostname != 0;
+    int4 c0 = make_int4(0, 0, 0, 0), c1 = c0, v0 = c0, v1 = c0;
+    if (hn && nsel > 0) {
+      c0 = pq[4];
+      c1 = pq[5];
+      v0 = pq[6];
+      v1 = pq[7];
+    }
+    const int32_t sc[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const int32_t sv[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const int leaf = leaf0 + j;
-      state[j] = swl[j] = ls[j] = 0;
-      kind[j] = (valid[j] && !live[j]) ? EX_DEAD : EX_NONE;
-      id[j] = -1;
-      if (valid[j] && kind[j] == EX_NONE) {
-        if (s.lowest_is_hostname) {
-          if (s.taint_profile) {
-            int t;
-            if constexpr (TS) t = sh_taint[e][prof[j]];
-            else t = b.taint_table[uni(q2.z) + prof[j]];
-            if (t >= 0) {
-              kind[j] = EX_TAINT;
-              id[j] = t;
+      bool ok = live[j];
+      int k = (valid[j] && !live[j]) ? EX_DEAD : EX_NONE;
+      int idv = -1;
+      if (hn && s.taint_profile) {
+        int t;
+        if constexpr (TS) t = sh_taint[e][prof[j]];
+        else t = b.taint_table[uni(q2.z) + prof[j]];
+        const bool x = ok & (t >= 0);
+        k = x ? EX_TAINT : k;
+        idv = x ? t : idv;
+        ok = ok & !x;
+      }
+      if (hn && nsel > 0) {
+        const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
+        bool mis = false;
+        if (!GL || !sel_far) {
+#pragma unroll
+          for (int q = 0; q < KUEUE_TAS_MAX_SELECTORS; q++) {
+            if (q < nsel) {  // wave-uniform
+              const int col = uni(sc[q]);
+              int32_t v = l0;
+              v = col == 1 ? l1 : v;
+              v = col == 2 ? l2 : v;
+              v = col == 3 ? l3 : v;
+              mis = mis | (v != uni(sv[q]));
             }
           }
-          if (kind[j] == EX_NONE && nsel > 0) {
-            const int4 c0 = pq[4], c1 = pq[5], v0 = pq[6], v1 = pq[7];
-            const int32_t sc[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-            const int32_t sv[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-            const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
-            if (!GL || !sel_far) {
+        } else if (ok) {
+          auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
 #pragma unroll
-              for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
-                if (k < nsel && kind[j] == EX_NONE) {
-                  const int col = uni(sc[k]);
-                  int32_t v = l0;
-                  v = col == 1 ? l1 : v;
-                  v = col == 2 ? l2 : v;
-                  v = col == 3 ? l3 : v;
-                  if (v != uni(sv[k])) kind[j] = EX_SELECTOR;
-                }
-              }
-            } else {
-              auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
-#pragma unroll
-              for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++)
-                if (k < nsel && kind[j] == EX_NONE && label_at(uni(sc[k])) != uni(sv[k])) kind[j] = EX_SELECTOR;
-              if constexpr (GL) {
-                const int32_t sxb = uni(pq[3].w);
-                if (kind[j] == EX_NONE && sxb >= 0 && !selector_ext_match(b, sxb, uni(pq[8].x), leaf, label_at))
-                  kind[j] = EX_SELECTOR;
-              }
-            }
-          }
+          for (int q = 0; q < KUEUE_TAS_MAX_SELECTORS; q++)
+            if (q < nsel && !mis && label_at(uni(sc[q])) != uni(sv[q])) mis = true;
           if constexpr (GL) {
-            if (kind[j] == EX_NONE && aff_begin >= 0) {
-              const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
-              auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
-              if (!affinity_match(b, aff_begin, aff_end, leaf, label_at)) kind[j] = EX_AFFINITY;
-            }
+            const int32_t sxb = uni(pq[3].w);
+            if (!mis && sxb >= 0 && !selector_ext_match(b, sxb, uni(pq[8].x), leaf, label_at)) mis = true;
           }
         }
-        if (kind[j] == EX_NONE && outside_domain(dom_begin, dom_end, leaf)) kind[j] = EX_TOPOLOGY;
-        if (kind[j] == EX_NONE) {
-          state[j] = state0[j];
-          swl[j] = swl0[j];
-          ls[j] = ls0[j];
-          if (state[j] == 0 && lim0[j] >= 0) {
-            kind[j] = EX_RESOURCE;
-            id[j] = lim0[j];
+        const bool x = ok & mis;
+        k = x ? EX_SELECTOR : k;
+        ok = ok & !mis;
+      }
+      if constexpr (GL) {
+        if (hn && aff_begin >= 0 && ok) {
+          const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
+          auto label_at = [s, leaf, l0, l1, l2, l3](int col) { return staged_label(s, leaf, col, l0, l1, l2, l3); };
+          if (!affinity_match(b, aff_begin, aff_end, leaf, label_at)) {
+            k = EX_AFFINITY;
+            ok = false;
           }
         }
       }
+      if (dom_begin >= 0) {
+        const bool x = ok & outside_domain(dom_begin, dom_end, leaf);
+        k = x ? EX_TOPOLOGY : k;
+        ok = ok & !x;
+      }
+      state[j] = ok ? state0[j] : 0;
+      swl[j] = ok ? swl0[j] : 0;
+      ls[j] = ok ? ls0[j] : 0;
+      const bool rx = ok & (state0[j] == 0) & (lim0[j] >= 0);
+      kind[j] = rx ? EX_RESOURCE : k;
+      id[j] = rx ? lim0[j] : idv;
       ss[j] = sswl[j] = 0;
       if (s.L - 1 == slice_level) {
         if (slice_size == 1) {

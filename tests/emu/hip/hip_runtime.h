@@ -250,6 +250,7 @@ struct int2 {
   int x, y;
 };
 inline int2 make_int2(int x, int y) { return int2{x, y}; }
+inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
 inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t st) {
   st->ops.push_back([=]() { memset(d, v, n); });
   return hipSuccess;

@@ -68,7 +68,7 @@ def main():
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "pmc_summary.json"), "w") as fh:
         json.dump(table, fh, indent=1)
-    fills = [k for k in table if k.startswith("ktas::fill_leaves")]
+    fills = [k for k in table if k.startswith("ktas::fill_leaves") or k.startswith("ktas::fill_pair")]
     if fills:
         k = max(fills, key=lambda x: table[x]["dispatches"])
         doc = {"config": config, "kernel": k, "fill_bytes_per_launch": table[k]["hbm_bytes"],
