@@ -201,6 +201,9 @@ typedef struct {
 /* keep single-run fill chunks on the one-leaf-per-thread staged kernel
  * instead of fill_pair_kernel (test knob: both paths must agree) */
 #define KUEUE_TAS_CFG_NO_PAIR_FILL 4
+/* admit with the one-wave in-order chain (admit_kernel) instead of the
+ * windowed admit_window_kernel (test knob: both must agree) */
+#define KUEUE_TAS_CFG_SERIAL_ADMIT 8
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

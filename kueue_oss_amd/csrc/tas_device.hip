@@ -146,6 +146,7 @@ struct kueue_tas_ctx {
   int list_cap = 1024;
   bool inline_stats = false;  // KUEUE_TAS_CFG_INLINE_STATS
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
+  bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
@@ -255,6 +256,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->device = cfg->device;
     c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0;
     c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
+    c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -852,11 +854,19 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<int32_t*>(d + o_exact));
     HIPCHK(c, hipGetLastError());
   }
-  hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
-                     c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
-                     reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
-                     pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
-                     reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
+  if (c->admit_window)  // windowed optimistic admission (one 1024-thread workgroup)
+    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow), lds_bits ? nwords * 4 : 0, c->stream,
+                       c->snap, c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
+                       reinterpret_cast<const AdmitRec*>(d + o_recs), reinterpret_cast<const int64_t*>(d + o_off),
+                       int(n_wl), pods_col, reinterpret_cast<const int32_t*>(d + o_fit0),
+                       reinterpret_cast<const int32_t*>(d + o_exact), reinterpret_cast<uint32_t*>(d + o_bits),
+                       lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
+  else  // one wave down the chain
+    hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
+                       c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
+                       reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
+                       pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
+                       reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(admitted, d + o_out, n_wl * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

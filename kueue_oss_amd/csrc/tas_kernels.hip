@@ -5196,4 +5196,101 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
   if (lane == 0) admitted[n_wl] = int32_t(uint32_t(sink));
 }
 
+// Windowed optimistic admission (the same decisions as admit_kernel: the
+// TAS half of Scheduler.processEntry, scheduler.go:371-435, per workload in
+// order, Fits tas_flavor_snapshot.go:401-415 then AddUsage :257-265).  Usage
+// only grows during a call, so a candidate checked against the usage of the
+// workloads admitted so far keeps that verdict until the next admission.
+// One 1024-thread workgroup: each of its kAdmitWindow waves checks one of the
+// next kAdmitWindow candidates in parallel; the window's rejections before
+// its first fitting candidate are final, that candidate is admitted (every
+// thread adds a share of its usage with returning atomics, consumed before
+// the barrier, so the next window's L2 loads see it) and the next window
+// starts right after it.  Rounds = admissions + rejections / kAdmitWindow
+// instead of one dependent chain step per workload.  A record whose leaf no
+// admitted workload of this call touched (LDS bitmap) keeps its phase-1
+// verdict without a load.
+constexpr int kAdmitWindow = 16;
+__global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
+    DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
+    const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
+    const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
+    int32_t* admitted) {
+  extern __shared__ uint32_t touched_lds[];
+  __shared__ int32_t sh_fit[kAdmitWindow];
+  const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
+  const bool in_lds = touched_in_lds != 0;
+  if (in_lds)  // (the global bitmap is cleared by the host)
+    for (int k = threadIdx.x; k < (s.N + 31) / 32; k += blockDim.x) touched_lds[k] = 0;
+  const bool exact = *exact_flag != 0;
+  unsigned long long sink = 0;
+  __syncthreads();
+  int w0 = 0;
+  while (w0 < n_wl) {  // block-uniform
+    const int w = w0 + wave;
+    bool fit = false;
+    if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
+      fit = true;
+      const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
+      for (int64_t base = r0; base < r1 && fit; base += kWave) {
+        const int64_t i = base + lane;
+        bool ok = true;
+        if (i < r1) {
+          const AdmitRec a = recs[i];
+          if (exact || a.status == kAdmitWide) {
+            ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+          } else if (a.status == kAdmitNever) {
+            ok = false;
+          } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
+            int64_t us[kAdmitTerms];
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++)
+              us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
+          }
+        }
+        fit = ballot(!ok) == 0;
+      }
+    }
+    if (lane == 0) sh_fit[wave] = fit ? 1 : 0;
+    __syncthreads();
+    int first = kAdmitWindow;  // first fitting candidate of the window (every thread alike)
+    for (int k = kAdmitWindow - 1; k >= 0; k--)
+      if (sh_fit[k]) first = k;
+    const int nrej = min(first, n_wl - w0);
+    if (int(threadIdx.x) < nrej) admitted[w0 + threadIdx.x] = 0;
+    if (first < kAdmitWindow) {  // admit it: AddUsage over its records, every thread a share
+      const int wa = w0 + first;
+      const int64_t r0 = wl_off[wa], r1 = wl_off[wa + 1];
+      for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+        const kueue_tas_fits_req r = reqs[i];
+        uint32_t bits = 0;
+        for (int k = 0; k < r.num_terms; k++) {
+          const kueue_tas_fits_term t = terms[r.term_begin + k];
+          if (t.col >= 0) {  // the host gives every usage resource a column first
+            sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
+                              (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
+            bits |= 1u << t.col;
+          }
+        }
+        if (pods_col >= 0) {
+          sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                            (unsigned long long)int64_t(r.count));
+          bits |= 1u << pods_col;
+        }
+        sink += atomicOr(usage_present + r.leaf, bits);
+        if (in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+        else sink += atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+      }
+      if (threadIdx.x == 0) admitted[wa] = 1;
+      w0 = wa + 1;
+    } else {
+      w0 += kAdmitWindow;
+    }
+    __syncthreads();  // the admission's atomics returned (consumed into sink) before the next window loads
+  }
+  if (threadIdx.x == 0) admitted[n_wl] = int32_t(uint32_t(sink));
+}
+
 }  // namespace ktas

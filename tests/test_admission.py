@@ -137,12 +137,36 @@ def _admit_batch(make, n=64, shape=(2, 2, 4, 8), huge_memory=False):
     assert b2 == res[n + len(admit_idx):]
 
 
+# serial: the one-wave in-order chain (admit_kernel, KUEUE_TAS_CFG_SERIAL_ADMIT);
+# default: the windowed admit_window_kernel — the same decisions either way
+@pytest.mark.parametrize("serial", [False, True])
 @pytest.mark.parametrize("tiny", [False, True])
-def test_emulated_admit_batch(emu_lib, tiny):  # noqa: F811
-    _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib), huge_memory=tiny)
+def test_emulated_admit_batch(emu_lib, tiny, serial):  # noqa: F811
+    _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib, serial_admit=serial), huge_memory=tiny)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("serial", [False, True])
 @pytest.mark.parametrize("tiny", [False, True])
-def test_admit_batch_on_gpu(tiny):
-    _admit_batch(lambda d: TASFlavorSnapshot(d), n=256, shape=(2, 4, 8, 16), huge_memory=tiny)
+def test_admit_batch_on_gpu(tiny, serial):
+    _admit_batch(lambda d: TASFlavorSnapshot(d, serial_admit=serial), n=256, shape=(2, 4, 8, 16), huge_memory=tiny)
+
+
+@pytest.mark.gpu
+def test_admit_window_matches_serial_c3_on_gpu():
+    # the C3 bench batch (1,024 workloads, heavy leaf overlap: most are
+    # rejected after an earlier admission): window and chain agree bit for bit
+    import numpy as np
+
+    doc, wls = synth.config_c3(n_workloads=1024)
+    out = []
+    for serial in (False, True):
+        snap = TASFlavorSnapshot(doc, serial_admit=serial)
+        snap.compile(wls)
+        snap.run_compiled()
+        admitted, deltas = snap.admit(snap.last_assignments())
+        out.append((admitted.copy(), np.sort(deltas, order=["leaf", "col"])))
+        snap.close()
+    assert (out[0][0] == out[1][0]).all()
+    assert (out[0][1] == out[1][1]).all()
+    assert 0 < int(out[0][0][:, 1].sum()) < len(wls)
