@@ -221,7 +221,7 @@ struct kueue_tas_ctx {
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
   uint32_t fill_paths = 0;               // KUEUE_TAS_PATH_* bits of the last kueue_tas_eval_batch
   // phase-1 counters of the last device chunk (kueue_tas_last_counters):
-  // requests [chunk_base, chunk_base + chunk_rep.size()), their class reps
+  // requests [chunk_base, chunk_base + chunk_rep.size()), their class counter rows
   size_t chunk_base = 0;
   std::vector<int32_t> chunk_rep;
   std::vector<uint8_t> chunk_leader;
@@ -1296,6 +1296,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       for (size_t i = 0; i < n; i++)
         if (int32_t(i) != rep[size_t(cls_of[i])]) h_mem[cur[size_t(pos[size_t(cls_of[i])])]++] = int32_t(i);
     }
+    {  // counters are stored per class, row = fill position: evals and LFC tables refer to their class's row
+      const std::vector<int32_t>& pos = c->cls_pos;
+      for (size_t i = 0; i < n; i++) h_rep[i] = pos[size_t(cls_of[i])];
+      for (int k = 0; k < ncls; k++)
+        if (slot_of[size_t(k)] >= 0) h_lrep[slot_of[size_t(k)]] = pos[size_t(k)];
+    }
     int32_t* h_frun = reinterpret_cast<int32_t*>(hs + o_frun);
     // a signature with at least half a chunk of classes gets chunks of its
     // own (one run: CountIn before the eval loop); the smaller ones of a base
@@ -1347,10 +1353,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   int64_t lcap = int64_t(c->maxD) * 2 + 64;
   const int64_t scratch_stride = 6 * lcap;
   const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
-  HIPCHK(c, c->d_counters.ensure(size_t(n) * size_t(ctr_stride)));
-  HIPCHK(c, c->d_overlay.ensure(size_t(n) * size_t(ctr_stride)));
-  if (c->d_tags.n < size_t(n) * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
-    HIPCHK(c, c->d_tags.ensure(size_t(n) * size_t(SD)));
+  HIPCHK(c, c->d_counters.ensure(size_t(std::max(nfill, 1)) * size_t(ctr_stride)));  // one row per class
+  // overlay, tags and scratch lists per BestFit-side select slot (fast-LFC
+  // evals never mutate or walk lists): sized by nbf, not n
+  const size_t nph2 = size_t(std::max(nbf, 1));
+  HIPCHK(c, c->d_overlay.ensure(nph2 * size_t(ctr_stride)));
+  if (c->d_tags.n < nph2 * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
+    HIPCHK(c, c->d_tags.ensure(nph2 * size_t(SD)));
     HIPCHK(c, hipMemsetAsync(c->d_tags.p, 0, c->d_tags.n * 4, c->stream));
     c->tag_epoch = 0;
   }
@@ -1389,7 +1398,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
     }
   }
-  HIPCHK(c, c->d_scratch.ensure(n * size_t(scratch_stride)));
+  HIPCHK(c, c->d_scratch.ensure(nph2 * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
   HIPCHK(c, c->d_lfc_items.ensure(size_t(std::max(nfast, 1)) * size_t(std::max(nchunks, 1)) + 1));
   HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
@@ -1526,7 +1535,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (b.rack_fanout) {
       c->fill_paths |= b.rack_fanout < 0 ? KUEUE_TAS_PATH_RAGGED_ROLLUP : KUEUE_TAS_PATH_UNIFORM_ROLLUP;
-      HIPCHK(c, c->d_rack_pos.ensure(n * size_t(s.level_size[s.L - 2])));
+      HIPCHK(c, c->d_rack_pos.ensure(size_t(nfill) * size_t(s.level_size[s.L - 2])));
       b.rack_pos = c->d_rack_pos.p;
     }
     const bool ts = b.num_profiles <= kStagedProfiles;
@@ -1639,7 +1648,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     HIPCHK(c, hipGetLastError());
   }
   if (nfill > 0 && s.L >= 2 && nbf > 0) {  // level maxima for the BestFit-side find_level
-    HIPCHK(c, c->d_level_max.ensure(n * size_t(kMaxLevels)));
+    HIPCHK(c, c->d_level_max.ensure(size_t(nfill) * size_t(kMaxLevels)));
     b.level_max = c->d_level_max.p;
     hipLaunchKernelGGL(level_max_kernel, dim3(unsigned(nfill), unsigned(s.L - 1)), dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());

@@ -145,9 +145,9 @@ struct DevBatch {
   const int32_t* cls_members;     // eval ids
   int32_t rack_fanout;     // the staged fill also rolls up the leaves' parents: > 0 uniform power-of-two
                            // fan-out, -1 ragged (DevSnap::wave_tab), 0 no
-  uint64_t* rack_pos;      // [n][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rep rows)
-  int64_t ctr_stride;      // int32 elements per eval (5 * SD)
-  int32_t* counters;       // [n][5][SD]
+  uint64_t* rack_pos;      // [nfill][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rows)
+  int64_t ctr_stride;      // int32 elements per class row (5 * SD)
+  int32_t* counters;       // [nfill][5][SD]: one row per phase-1 class, in fill order (row = fill position)
   int32_t* taint_counts;   // [n][num_taints]
   int32_t* res_counts;     // [n][R]
   int32_t* sel_counts;     // [n]
@@ -169,9 +169,9 @@ struct DevBatch {
                               // signature (leader / simulateEmpty flags, assumed usage), request terms may differ
   const int32_t* fill_run;    // [nfill] signature run of each fill position: consecutive positions of a chunk
                               // with the same request terms share a run (one CountIn per leaf)
-  const int32_t* rep_of;   // [n] class rep whose phase-1 counters the eval reads
+  const int32_t* rep_of;   // [n] counter row (class fill position) whose phase-1 counters the eval reads
   const int32_t* lfc_slot; // [n] fast-LFC table slot, -1 if the eval is not fast LFC
-  const int32_t* lfc_rep;  // [lfc_nslots] eval whose leaf counters the table summarizes
+  const int32_t* lfc_rep;  // [lfc_nslots] counter row whose leaf counters the table summarizes
   int32_t lfc_nslots;
   int32_t lfc_nchunks;
   uint32_t* lfc_ch;        // [nslots][nchunks][kLfcBins] per-chunk value counts
@@ -186,7 +186,7 @@ struct DevBatch {
   int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
   int32_t tag_epoch;
   int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
-  int32_t* level_max;      // [n][kMaxLevels] max sliceState per level < L-1 of the class rep's counters
+  int32_t* level_max;      // [nfill][kMaxLevels] max sliceState per level < L-1 of the class row's counters
                            // (level_max_kernel; rows of class reps only), null: not computed
 };
 

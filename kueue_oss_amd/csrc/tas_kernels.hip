@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
       }
     }
     if (valid) {
-      int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+      int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
       const int64_t SD = s.SD;
       int32_t ss = 0, sswl = 0;
       if (s.L - 1 == ev.slice_level) {
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
         sswl = leader ? go_div32(swl, slice_size) : ss;
       }
     }
-    int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
     const int64_t SD = s.SD;
     if (valid) {
       base[gleaf] = state;
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       const uint64_t posm = ballot(valid && ss > 0);  // positive children, for the BestFit descent
       if ((lane & (F - 1)) == 0 && parent < s.level_size[s.L - 2]) {
         const uint64_t seg = F == kWave ? posm : (posm >> lane) & ((1ull << F) - 1ull);
-        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + parent] = seg;
+        b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = seg;
         const int32_t pswl = has ? w_sub(cap, minD) : 0;
         int32_t psswl = has ? w_sub(slc, minSD) : 0;
         if (s.L - 2 == slice_level) {
@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       if (seg_tail) {
         const int len = lane - seg0 + 1;
         const uint64_t seg = len == kWave ? posm : (posm >> seg0) & ((1ull << len) - 1ull);
-        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + rparent] = seg;
+        b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + rparent] = seg;
         const int32_t pswl = has ? w_sub(cap, minD) : 0;
         int32_t psswl = has ? w_sub(slc, minSD) : 0;
         if (s.L - 2 == slice_level) {
@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         }
       }
     }
-    int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+    int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
     auto store2 = [&](int64_t off, int32_t a, int32_t c) {  // counter words of leaves leaf0, leaf0 + 1
       if (pair_store && valid[1]) {
         *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(a, c);
@@ -1517,7 +1517,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         posm = (uint64_t(hi) << 32) | lo;
       }
       if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
-        b.rack_pos[int64_t(eid) * s.level_size[s.L - 2] + parent] = posm;
+        b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = posm;
         const int32_t pswl = has ? w_sub(cap2, minD) : 0;
         int32_t psswl = has ? w_sub(slc, minSD) : 0;
         if (s.L - 2 == slice_level) {
@@ -1745,7 +1745,7 @@ __global__ __launch_bounds__(256) void fill_stats_reduce_kernel(DevBatch b, int 
 // fillInCountsHelper (:1658-1719) of one parent domain p of `level` for
 // class eid, one thread over the CSR children (wrapping int32 sums, min/max:
 // the order of the children does not matter).
-__device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& b, int eid, const DevEval& ev, int level,
+__device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& b, int row, const DevEval& ev, int level,
                                               int p) {
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   const int cl = level + 1;
@@ -1753,7 +1753,7 @@ __device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& 
   const bool hasInner = inner != 0;
   const int cb = s.child_off[s.child_base[level] + p];
   const int ce = s.child_off[s.child_base[level] + p + 1];
-  int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
   const int64_t SD = s.SD;
   const int coff = s.level_off[cl];
   int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0;
@@ -1820,7 +1820,7 @@ __global__ __launch_bounds__(256) void rollup_level_kernel(DevSnap s, DevBatch b
   const int eid = b.fill_ids[blockIdx.y];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= s.level_size[level]) return;
-  rollup_parent(s, b, eid, b.evals[eid], level, p);
+  rollup_parent(s, b, int(blockIdx.y), b.evals[eid], level, p);
 }
 
 // Same reduction with one wave per parent: lanes stride over the CSR children
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
   const int cl = level + 1;
   const int32_t inner = ev.ssal[cl];
   const bool hasInner = inner != 0;
-  int32_t* base = b.counters + int64_t(eid) * b.ctr_stride;
+  int32_t* base = b.counters + int64_t(blockIdx.y) * b.ctr_stride;  // the class's row: its fill position
   const int64_t SD = s.SD;
   const int coff = s.level_off[cl];
   const int lane = lane_id();
@@ -1908,10 +1908,10 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
 // start 16-byte aligned), every load of a thread issued before the reduction.
 __global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
   __shared__ int32_t red[4];
-  const int eid = b.fill_ids[blockIdx.x];
+  const int row = blockIdx.x;  // the class's fill position
   const int l = blockIdx.y;
   const int D = s.level_size[l];
-  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(eid) * b.ctr_stride + s.SD + s.level_off[l]);
+  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(row) * b.ctr_stride + s.SD + s.level_off[l]);
   const int nq = (D + 3) / 4;
   int32_t m = INT32_MIN;
   constexpr int U = 8;
@@ -1933,7 +1933,7 @@ __global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
   m = group_reduce(m, 64, OpMax());
   if (lane_id() == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) b.level_max[int64_t(eid) * kMaxLevels + l] = max(max(red[0], red[1]), max(red[2], red[3]));
+  if (threadIdx.x == 0) b.level_max[int64_t(row) * kMaxLevels + l] = max(max(red[0], red[1]), max(red[2], red[3]));
 }
 
 // Leaf-level selection partials for evals whose requested level is the leaf
@@ -1997,20 +1997,13 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
   }
 }
 
-// Replicate phase-1 results (counters, exclusion stats) from a
-// representative eval to an eval with identical phase-1 inputs.
+// Replicate the exclusion stats of a class representative to another member
+// of its class (global-atomic stats path; the counters are shared: every
+// member reads its class's row, DevBatch::rep_of).  pairs: (rep, ~member).
 __global__ __launch_bounds__(256) void replicate_kernel(DevSnap s, DevBatch b, const int32_t* pairs, int npairs) {
   const int pi = blockIdx.y;
   if (pi >= npairs) return;
-  const int src = pairs[2 * pi], dst_raw = pairs[2 * pi + 1];
-  const bool stats_only = dst_raw < 0;  // fast-LFC duplicates read the rep's counters in place
-  const int dst = stats_only ? ~dst_raw : dst_raw;
-  const bool leader = (b.evals[dst].flags & KUEUE_TAS_F_LEADER) != 0;
-  const int64_t words = stats_only ? 0 : int64_t(leader ? 5 : 2) * s.SD;  // SD is a multiple of 4
-  const int4* a = reinterpret_cast<const int4*>(b.counters + int64_t(src) * b.ctr_stride);
-  int4* d = reinterpret_cast<int4*>(b.counters + int64_t(dst) * b.ctr_stride);
-  const int64_t q = words / 4;
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < q; i += int64_t(gridDim.x) * blockDim.x) d[i] = a[i];
+  const int src = pairs[2 * pi], dst = ~pairs[2 * pi + 1];
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < b.num_taints; i += blockDim.x)
       b.taint_counts[int64_t(dst) * b.num_taints + i] = b.taint_counts[int64_t(src) * b.num_taints + i];
@@ -4506,8 +4499,10 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
   w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
   w.rack_pos = b.rack_fanout ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
-  w.ov = b.overlay + int64_t(eid) * b.ctr_stride;
-  w.tag = b.tags + int64_t(eid) * s.SD;
+  // per-launch-slot phase-2 buffers: the BestFit-side launch numbers its
+  // evals 0..nbf-1; fast-LFC evals (the other launch) never touch them
+  w.ov = b.overlay + int64_t(slot) * b.ctr_stride;
+  w.tag = b.tags + int64_t(slot) * s.SD;
   w.my_tag = b.tag_epoch;
   w.dirty = false;
   w.SD = s.SD;
@@ -4515,7 +4510,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.cap = b.list_cap;
   w.lds_bytes = b.wave_lds;
   int64_t lcap = b.scratch_stride / 6;  // 4 int32 lists (2 per u64) + 2 key arrays (2 u64 per key)
-  uint64_t* sc = b.scratch + int64_t(eid) * b.scratch_stride;
+  uint64_t* sc = b.scratch + int64_t(slot) * b.scratch_stride;
   w.lcap = int(lcap);
   w.listA = reinterpret_cast<int32_t*>(sc);
   w.listB = w.listA + lcap;
