@@ -953,6 +953,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
   const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
   const size_t o_moff = seg((n + 1) * 4), o_mem = seg(n * 4);  // class members in fill order (CSR)
+  // last: the per-position fill records, uploaded up to the batch's nfill
+  const size_t o_fpos = seg(n * sizeof(FillPos));
   HIPCHK(c, c->h_stage.ensure(stage_bytes));
   HIPCHK(c, c->d_stage.ensure(stage_bytes));
   uint8_t* hs = c->h_stage.p;
@@ -1409,8 +1411,57 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
   HIPCHK(c, c->d_partials.ensure(size_t(std::max(nleafsel, 1)) * size_t(std::max(nblk, 1))));
 
+  // fill_pair_kernel's per-position records in fill order (FillPos)
+  {
+    FillPos* fp = reinterpret_cast<FillPos*>(hs + o_fpos);
+    const int32_t* h_fill = reinterpret_cast<const int32_t*>(hs + o_fill);
+    const int32_t* h_fch = reinterpret_cast<const int32_t*>(hs + o_fchunks);
+    const int32_t* h_frun = reinterpret_cast<const int32_t*>(hs + o_frun);
+    const int nsw = ucols <= 4 ? 4 : 8;  // the launch's NS: worker terms [0, NS), leader terms [NS, 2 NS)
+    for (int ch = 0; ch < nfchunks; ch++) {
+      const int e0 = h_fch[2 * ch], ne = h_fch[2 * ch + 1];
+      const DevEval& base = hev[h_fill[e0]];
+      for (int t = 0; t < ne; t++) {
+        const int pos = e0 + t;
+        const DevEval& ev = hev[h_fill[pos]];
+        FillPos& r = fp[pos];
+        memset(&r, 0, sizeof r);
+        FillEvalParams& P = r.p;
+        P.eid = h_fill[pos];
+        P.taint_off = ev.taint_table;
+        P.nsel = ev.nsel;
+        P.slice_size = ev.slice_size;
+        P.slice_level = ev.slice_level;
+        P.inner = ev.ssal[s.L - 1];
+        const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
+        P.aff_begin = aff ? ev.aff_begin : -1;
+        P.aff_end = aff ? ev.aff_end : -1;
+        P.dom_begin = ev.dom_begin;
+        P.dom_end = ev.dom_end;
+        for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+          P.sel_col[k] = ev.sel_col[k];
+          P.sel_val[k] = ev.sel_val[k];
+          if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
+        }
+        P.sx_begin = ev.sx_begin;
+        P.sx_end = ev.sx_end;
+        if (ev.sx_begin >= 0) P.sel_far = 1;
+        P.run = h_frun[pos];
+        P.sig_new = t == 0 || h_frun[pos - 1] != P.run;
+        P.rmask = int32_t(ev.req_mask);
+        P.lmask = int32_t(ev.lead_mask);
+        P.pad[0] = int32_t(base.flags);  // the chunk's base signature
+        P.pad[1] = base.assumed_begin;
+        P.pad[2] = base.assumed_end;
+        for (int q = 0; q < kStagedProfiles; q++)
+          r.taint[q] = q < c->num_profiles && size_t(ev.taint_table + q) < taint_table_len ? taint_table[ev.taint_table + q] : -1;
+        for (int j = 0; j < ev.nreq && j < nsw; j++) r.term[j] = hterms[ev.term_begin + j];
+        for (int j = 0; j < ev.nlead && j < nsw; j++) r.term[nsw + j] = hterms[ev.lead_begin + j];
+      }
+    }
+  }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, stage_bytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, o_fpos + size_t(nfill) * sizeof(FillPos), hipMemcpyHostToDevice, c->stream));
   // the select path's descriptor (g_select_snap), ordered before both select
   // launches: stream2 joins after events recorded later on this stream.
   // Uploaded only when it differs from what the device already holds (the
@@ -1496,6 +1547,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   b.nfill = nfill;
   b.fill_chunks = reinterpret_cast<const int32_t*>(ds + o_fchunks);
   b.fill_run = reinterpret_cast<const int32_t*>(ds + o_frun);
+  b.fill_pos = reinterpret_cast<const FillPos*>(ds + o_fpos);
   // K1
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   c->last_stats[0] += nfill;

@@ -167,6 +167,7 @@ struct DevBatch {
   int32_t nfill;
   const int32_t* fill_chunks; // [nchunks][2] (start, len) into fill_ids: <= kEvalsPerBlock classes with one base
                               // signature (leader / simulateEmpty flags, assumed usage), request terms may differ
+  const struct FillPos* fill_pos;  // [nfill] host-built per-position records (fill_pair_kernel)
   const int32_t* fill_run;    // [nfill] signature run of each fill position: consecutive positions of a chunk
                               // with the same request terms share a run (one CountIn per leaf)
   const int32_t* rep_of;   // [n] counter row (class fill position) whose phase-1 counters the eval reads

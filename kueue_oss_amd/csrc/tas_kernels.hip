@@ -626,6 +626,20 @@ struct alignas(16) FillEvalParams {
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
 constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
 constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
+
+// Everything fill_pair_kernel needs about one fill position, built by the
+// host in fill order (DevBatch::fill_pos): the parameters (pad[0] = the
+// chunk's base flags, pad[1..2] = its assumed-usage range), the eval's
+// taint-profile row and its run's worker | leader terms.  A block copies its
+// chunk's records into LDS with one coalesced pass: one memory round trip
+// instead of the chain chunk -> eval ids -> eval records -> rows / terms.
+constexpr int kPosTerms = 16;  // 2 * the largest staged column count
+struct alignas(16) FillPos {
+  FillEvalParams p;
+  int32_t taint[kStagedProfiles];
+  DevTerm term[kPosTerms];
+};
+static_assert(sizeof(FillPos) % 16 == 0, "FillPos is copied as int4");
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
 // ExclusionStats of a fill block are counted in LDS and written as per-block
@@ -1156,10 +1170,9 @@ struct OpOr {
 template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none)
 __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
-  __shared__ FillEvalParams sh_p[kEvalsPerBlock];
-  __shared__ DevTerm sh_term[MR ? kEvalsPerBlock : 1][2 * NS];  // a run's worker | leader terms (at its first position)
-  __shared__ int32_t sh_taint[kEvalsPerBlock][kStagedProfiles];
+  __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   if (lds_stats)
     for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
@@ -1170,53 +1183,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     chunk = int(g % gridDim.y);
     tile = int((g / gridDim.y) * 8u + (lin & 7u));
   }
-  chunk += chunk_base;
-  const int e0 = b.fill_chunks[2 * chunk];
-  const int ne = b.fill_chunks[2 * chunk + 1];
-  if (int(threadIdx.x) < ne) {
-    const int eid = b.fill_ids[e0 + threadIdx.x];
-    const DevEval& ev = b.evals[eid];
-    FillEvalParams& P = sh_p[threadIdx.x];
-    P.eid = eid;
-    P.taint_off = ev.taint_table;
-    P.nsel = ev.nsel;
-    P.slice_size = ev.slice_size;
-    P.slice_level = ev.slice_level;
-    P.inner = ev.ssal[s.L - 1];
-    const bool aff = (ev.flags & KUEUE_TAS_F_AFFINITY) != 0;
-    P.aff_begin = aff ? ev.aff_begin : -1;
-    P.aff_end = aff ? ev.aff_end : -1;
-    P.dom_begin = ev.dom_begin;
-    P.dom_end = ev.dom_end;
-    P.sel_far = 0;
-    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
-      P.sel_col[k] = ev.sel_col[k];
-      P.sel_val[k] = ev.sel_val[k];
-      if (k < ev.nsel && ev.sel_col[k] >= kStagedLabels) P.sel_far = 1;
-    }
-    P.sx_begin = ev.sx_begin;
-    P.sx_end = ev.sx_end;
-    if (ev.sx_begin >= 0) P.sel_far = 1;
-    P.run = b.fill_run[e0 + threadIdx.x];
-    P.sig_new = threadIdx.x == 0 || b.fill_run[e0 + threadIdx.x - 1] != P.run;
-    P.rmask = int32_t(ev.req_mask);
-    P.lmask = int32_t(ev.lead_mask);
-    if (MR ? P.sig_new : threadIdx.x == 0) {  // the run's terms, at its first position
-      DevTerm* t = sh_term[MR ? threadIdx.x : 0];
-      for (int j = 0; j < NS; j++) {
-        if (j < ev.nreq) t[j] = b.terms[ev.term_begin + j];
-        if (j < ev.nlead) t[NS + j] = b.terms[ev.lead_begin + j];
-      }
-    }
-  }
-  __syncthreads();
-  if (s.taint_profile && TS) {
-    for (int i = threadIdx.x; i < ne * kStagedProfiles; i += kFillThreads) {
-      const int e = i / kStagedProfiles, p = i % kStagedProfiles;
-      sh_taint[e][p] = p < b.num_profiles ? b.taint_table[sh_p[e].taint_off + p] : -1;
-    }
-  }
-  __syncthreads();
+  // the leaves' snapshot columns first (they do not depend on the chunk),
+  // then the chunk's records: both sets of loads in flight together
   const int lane = lane_id();
   const int N = s.N;
   const int leaf0 = tile * kPairTile + 2 * int(threadIdx.x);
@@ -1254,13 +1222,22 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       }
     }
   }
+  chunk += chunk_base;
+  const int e0 = b.fill_chunks[2 * chunk];
+  const int ne = b.fill_chunks[2 * chunk + 1];
+  {
+    const int4* src = reinterpret_cast<const int4*>(b.fill_pos + e0);
+    int4* dst = reinterpret_cast<int4*>(sh_pos);
+    const int words = ne * int(sizeof(FillPos) / 16);
+    for (int i = threadIdx.x; i < words; i += kFillThreads) dst[i] = src[i];
+  }
+  __syncthreads();
   // ---- base signature: remaining capacity per leaf ----
   bool leader, live[2];
   uint32_t pres[2];
   {
-    const DevEval& ev = b.evals[uni(b.fill_ids[e0])];
-    const uint32_t flags = uint32_t(uni(int32_t(ev.flags)));
-    const int abeg = uni(ev.assumed_begin), aend = uni(ev.assumed_end);
+    const uint32_t flags = uint32_t(uni(sh_pos[0].p.pad[0]));
+    const int abeg = uni(sh_pos[0].p.pad[1]), aend = uni(sh_pos[0].p.pad[2]);
     leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
 #pragma unroll
@@ -1329,8 +1306,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   int32_t state0[2] = {0, 0}, swl0[2] = {0, 0}, ls0[2] = {0, 0};
   int lim0[2] = {-1, -1};
   auto count_run = [&](int e) {  // CountIn of the run starting at chunk position e, both leaves
-    const uint32_t rmask = uint32_t(uni(sh_p[e].rmask)), lmask = uint32_t(uni(sh_p[e].lmask));
-    const DevTerm* wt = sh_term[MR ? e : 0];
+    const uint32_t rmask = uint32_t(uni(sh_pos[e].p.rmask)), lmask = uint32_t(uni(sh_pos[e].p.lmask));
+    const DevTerm* wt = sh_pos[e].term;
     const DevTerm* lt = wt + NS;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
@@ -1357,7 +1334,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   const bool pair_store = (gleaf0 & 1) == 0;              // 8-byte aligned counter pairs (wave-uniform)
   const int64_t SD = s.SD;
   for (int e = 0; e < ne; e++) {
-    const int4* pq = reinterpret_cast<const int4*>(&sh_p[e]);
+    const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
     const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
     if constexpr (MR) {
       if (uni(q2.w)) count_run(e);  // sig_new
@@ -1391,7 +1368,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       int idv = -1;
       if (hn && s.taint_profile) {
         int t;
-        if constexpr (TS) t = sh_taint[e][prof[j]];
+        if constexpr (TS) t = sh_pos[e].taint[prof[j]];
         else t = b.taint_table[uni(q2.z) + prof[j]];
         const bool x = ok & (t >= 0);
         k = x ? EX_TAINT : k;
