@@ -953,6 +953,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const size_t o_slot = seg(n * 4), o_lrep = seg(n * 4), o_fast = seg(n * 4), o_leafsel = seg(n * 4);
   const size_t o_pidx = seg(n * 4), o_bf = seg(n * 4);
   const size_t o_moff = seg((n + 1) * 4), o_mem = seg(n * 4);  // class members in fill order (CSR)
+  // rollup_top_kernel's level maxima (INT32_MIN) and per-class arrival counters (0)
+  const size_t o_top = seg(n * (kMaxLevels + 1) * 4);
   // last: the per-position fill records, uploaded up to the batch's nfill
   const size_t o_fpos = seg(n * sizeof(FillPos));
   HIPCHK(c, c->h_stage.ensure(stage_bytes));
@@ -1411,6 +1413,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
   HIPCHK(c, c->d_partials.ensure(size_t(std::max(nleafsel, 1)) * size_t(std::max(nblk, 1))));
 
+  {  // rollup_top_kernel's initial level maxima and arrival counters
+    int32_t* t = reinterpret_cast<int32_t*>(hs + o_top);
+    for (size_t i = 0; i < size_t(nfill) * kMaxLevels; i++) t[i] = INT32_MIN;
+    for (size_t i = 0; i < size_t(nfill); i++) t[n * kMaxLevels + i] = 0;
+  }
   // fill_pair_kernel's per-position records in fill order (FillPos)
   {
     FillPos* fp = reinterpret_cast<FillPos*>(hs + o_fpos);
@@ -1686,7 +1693,19 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   }
   // K2
   const int upper = s.L - 2 - (b.rack_fanout ? 1 : 0);  // levels [0, upper] left to roll up
-  for (int l = upper; l >= 0; l--) {
+  int top_parents = 0;  // parents above level `upper`: the fused launch's last block rolls them up
+  for (int l = 0; l < upper; l++) top_parents += s.level_size[l];
+  const bool fused_top = nfill > 0 && upper >= 0 && s.level_size[upper] > 0 && top_parents <= 4096 &&
+                         s.level_size[upper + 1] / s.level_size[upper] >= 8;
+  if (fused_top) {  // every upper level and the level maxima in one launch
+    b.level_max = nbf > 0 ? reinterpret_cast<int32_t*>(ds + o_top) : nullptr;
+    const int per_block = 4 * kParentsPerWave;
+    dim3 grid((s.level_size[upper] + per_block - 1) / per_block, unsigned(nfill));
+    hipLaunchKernelGGL(rollup_top_kernel, grid, dim3(256), 0, c->stream, s, b, upper,
+                       reinterpret_cast<int32_t*>(ds + o_top) + n * kMaxLevels);
+    HIPCHK(c, hipGetLastError());
+  }
+  for (int l = fused_top ? -1 : upper; l >= 0; l--) {
     if (s.level_size[l] <= 0) continue;
     const int fanout = s.level_size[l + 1] / s.level_size[l];
     if (fanout >= 8) {  // wave per parent: coalesced child reads
@@ -1699,7 +1718,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     }
     HIPCHK(c, hipGetLastError());
   }
-  if (nfill > 0 && s.L >= 2 && nbf > 0) {  // level maxima for the BestFit-side find_level
+  if (!fused_top && nfill > 0 && s.L >= 2 && nbf > 0) {  // level maxima for the BestFit-side find_level
     HIPCHK(c, c->d_level_max.ensure(size_t(nfill) * size_t(kMaxLevels)));
     b.level_max = c->d_level_max.p;
     hipLaunchKernelGGL(level_max_kernel, dim3(unsigned(nfill), unsigned(s.L - 1)), dim3(256), 0, c->stream, s, b);

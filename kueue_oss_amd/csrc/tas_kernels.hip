@@ -1913,6 +1913,133 @@ __global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
   if (threadIdx.x == 0) b.level_max[int64_t(row) * kMaxLevels + l] = max(max(red[0], red[1]), max(red[2], red[3]));
 }
 
+// The top of the tree in one launch (fillInCountsHelper :1658-1719 for
+// levels `level` .. 0, plus the level maxima findLevelWithFitDomains' skip
+// reads): the grid rolls level `level` up, one wave per parent as
+// rollup_level_wave_kernel, and records the maximum sliceState of the
+// children it reads (level + 1, when that is not the leaf level) with one
+// atomicMax per block; the last block of each class to finish (a release
+// fence and a per-class arrival counter) then rolls up levels level-1 .. 0
+// itself — a few hundred parents — reading its siblings' parents through
+// L2, and writes those levels' maxima.  One launch instead of one per level
+// plus level_max_kernel.  b.level_max rows start at INT32_MIN and the
+// counters at 0 (host staging upload).
+__device__ __forceinline__ int32_t load_l2_i32(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool L2>
+__device__ __forceinline__ void rollup_parent_wave(const DevSnap& s, int32_t* base, const DevEval& ev, bool leaderReq,
+                                                   int level, int p, int32_t* cmax) {
+  const int cl = level + 1;
+  const int32_t inner = ev.ssal[cl];
+  const bool hasInner = inner != 0;
+  const int64_t SD = s.SD;
+  const int coff = s.level_off[cl];
+  const int lane = lane_id();
+  const int cb = s.child_off[s.child_base[level] + p];
+  const int ce = s.child_off[s.child_base[level] + p + 1];
+  auto ld = [&](int64_t o) { return L2 ? load_l2_i32(base + o) : base[o]; };
+  int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0, mx = INT32_MIN;
+  int has = 0;
+  for (int c = cb + lane; c < ce; c += kWave) {
+    const int g = coff + c;
+    int32_t cs = ld(g);
+    const int32_t css = ld(SD + g);
+    int32_t csw = cs, csswl = css, cls = 0;
+    if (leaderReq) {
+      csw = ld(2 * SD + g);
+      csswl = ld(3 * SD + g);
+      cls = ld(4 * SD + g);
+    }
+    mx = max(mx, css);
+    if (hasInner) {
+      cs = w_mul(go_div32(cs, inner), inner);
+      csw = w_mul(go_div32(csw, inner), inner);
+    }
+    cap = w_add(cap, cs);
+    slc = w_add(slc, css);
+    if (!leaderReq || cls > 0) {
+      has = 1;
+      minD = min(w_sub(cs, csw), minD);
+      minSD = min(w_sub(css, csswl), minSD);
+    }
+    lead = max(cls, lead);
+  }
+#pragma unroll
+  for (int m = 1; m <= 32; m <<= 1) {
+    cap = w_add(cap, xor_lane(cap, m));
+    slc = w_add(slc, xor_lane(slc, m));
+    minD = min(minD, xor_lane(minD, m));
+    minSD = min(minSD, xor_lane(minSD, m));
+    lead = max(lead, xor_lane(lead, m));
+    has |= xor_lane(has, m);
+    mx = max(mx, xor_lane(mx, m));
+  }
+  *cmax = max(*cmax, mx);
+  if (lane == 0) {
+    const int32_t state = cap;
+    const int32_t swl = has ? w_sub(cap, minD) : 0;
+    int32_t sswl = has ? w_sub(slc, minSD) : 0;
+    if (level == ev.slice_level) {
+      slc = go_div32(state, ev.slice_size);
+      sswl = go_div32(swl, ev.slice_size);
+    }
+    const int g = s.level_off[level] + p;
+    base[g] = state;
+    base[SD + g] = slc;
+    if (leaderReq) {
+      base[2 * SD + g] = swl;
+      base[3 * SD + g] = sswl;
+      base[4 * SD + g] = lead;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void rollup_top_kernel(DevSnap s, DevBatch b, int level, int32_t* arrivals) {
+  __shared__ int32_t red[4];
+  __shared__ int32_t last;
+  const int row = blockIdx.y;  // the class's fill position
+  const int eid = b.fill_ids[row];
+  const DevEval& ev = b.evals[eid];
+  const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int wv = threadIdx.x >> 6;
+  int32_t cmax = INT32_MIN;
+  const int p0 = (blockIdx.x * 4 + wv) * kParentsPerWave;
+  for (int j = 0; j < kParentsPerWave; j++) {
+    const int p = p0 + j;
+    if (p < s.level_size[level]) rollup_parent_wave<false>(s, base, ev, leaderReq, level, p, &cmax);
+  }
+  if (lane_id() == 0) red[wv] = cmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t m = max(max(red[0], red[1]), max(red[2], red[3]));
+    if (level + 1 < s.L - 1 && b.level_max) atomicMax(&b.level_max[int64_t(row) * kMaxLevels + level + 1], m);
+    __threadfence();  // this block's parents reach L2 before its arrival counts
+    last = atomicAdd(&arrivals[row], 1) == int(gridDim.x) - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int l = level - 1; l >= -1; l--) {
+    // l >= 0: roll level l up from level l + 1; the maximum of level l + 1 comes with the reads
+    int32_t lm = INT32_MIN;
+    if (l >= 0) {
+      for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, ev, leaderReq, l, p, &lm);
+    } else {  // level 0's own maximum
+      const int32_t* ss = base + s.SD + s.level_off[0];
+      for (int i = threadIdx.x; i < s.level_size[0]; i += 256) lm = max(lm, load_l2_i32(ss + i));
+      lm = group_reduce(lm, 64, OpMax());
+    }
+    if (lane_id() == 0) red[wv] = lm;
+    __syncthreads();
+    if (threadIdx.x == 0 && b.level_max && l + 1 < s.L - 1)
+      b.level_max[int64_t(row) * kMaxLevels + l + 1] = max(max(red[0], red[1]), max(red[2], red[3]));
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 // Leaf-level selection partials for evals whose requested level is the leaf
 // level: per 64-leaf wave, the reductions findLevelWithFitDomains needs
 // (:1244-1270): first/last sortedDomainsWithLeader key, LFC first fit,

@@ -184,6 +184,7 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 }
 inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v; return o; }
 inline int atomicOr(int* p, int v) { int o = *p; *p = o | v; return o; }
+inline int atomicMax(int* p, int v) { int o = *p; if (v > o) *p = v; return o; }
 inline int atomicAnd(int* p, int v) { int o = *p; *p = o & v; return o; }
 inline unsigned atomicAnd(unsigned* p, unsigned v) { unsigned o = *p; *p = o & v; return o; }
 inline void __threadfence() {}
