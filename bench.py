@@ -318,7 +318,8 @@ def main():
                                    "values in the step; 50% BestFit required/preferred, 50% LeastFreeCapacity "
                                    "unconstrained; taints + nodeSelector)",
                        "nodes": N, "batch_per_gpu": a.batch, "parallelism": f"dp{world} (replicated snapshot)"},
-            "roofline": {"kernel": "fill_leaves_staged_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+            "roofline": {"kernel": "fill_pair_kernel" if st.get("fill_paths", 0) & 8192 else "fill_leaves_staged_kernel",
+                         "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "bytes_per_launch": int(fill_bytes),
                          "avg_launch_ms": round(per_launch_fill_ms, 4),

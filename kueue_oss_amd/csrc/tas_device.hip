@@ -855,10 +855,11 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
     HIPCHK(c, hipGetLastError());
   }
   if (c->admit_window)  // windowed optimistic admission (one 1024-thread workgroup)
-    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow), lds_bits ? nwords * 4 : 0, c->stream,
+    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(kAdmitThreads), lds_bits ? nwords * 4 : 0, c->stream,
                        c->snap, c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
                        reinterpret_cast<const AdmitRec*>(d + o_recs), reinterpret_cast<const int64_t*>(d + o_off),
-                       int(n_wl), pods_col, reinterpret_cast<const int32_t*>(d + o_fit0),
+                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n_wl), pods_col,
+                       reinterpret_cast<const int32_t*>(d + o_fit0),
                        reinterpret_cast<const int32_t*>(d + o_exact), reinterpret_cast<uint32_t*>(d + o_bits),
                        lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   else  // one wave down the chain

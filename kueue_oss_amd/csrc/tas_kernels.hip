@@ -3340,7 +3340,7 @@ __device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np
   for (int i = lane; i < kHist; i += kWave) hist[i] = 0;
   // parents in index order through an LDS bitmap (the walk above listed
   // them in its sort order); up to 64 of them stay in a register
-  uint64_t t_prof = KTAS_PROFILE ? wall_clock64() : 0;
+  [[maybe_unused]] uint64_t t_prof = KTAS_PROFILE ? wall_clock64() : 0;
   auto lap_prof = [&](int cat) {
 #if KTAS_PROFILE
     const uint64_t t = wall_clock64();
@@ -5300,8 +5300,9 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
 // order, Fits tas_flavor_snapshot.go:401-415 then AddUsage :257-265).  Usage
 // only grows during a call, so a candidate checked against the usage of the
 // workloads admitted so far keeps that verdict until the next admission.
-// One 1024-thread workgroup: each of its kAdmitWindow waves checks one of the
-// next kAdmitWindow candidates in parallel; the window's rejections before
+// One 1024-thread workgroup checks the next kAdmitWindow candidates in
+// parallel (their records are one contiguous range: every thread takes
+// records of it, kAdmitU in flight); the window's rejections before
 // its first fitting candidate are final, that candidate is admitted (every
 // thread adds a share of its usage with returning atomics, consumed before
 // the barrier, so the next window's L2 loads see it) and the next window
@@ -5310,14 +5311,14 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
 // admitted workload of this call touched (LDS bitmap) keeps its phase-1
 // verdict without a load.
 constexpr int kAdmitWindow = 16;
-__global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
+constexpr int kAdmitThreads = 1024;
+__global__ __launch_bounds__(kAdmitThreads) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
-    const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
-    const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
+    const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, const int32_t* rec_wl, int n_wl,
+    int pods_col, const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
     int32_t* admitted) {
   extern __shared__ uint32_t touched_lds[];
   __shared__ int32_t sh_fit[kAdmitWindow];
-  const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
   const bool in_lds = touched_in_lds != 0;
   if (in_lds)  // (the global bitmap is cleared by the host)
     for (int k = threadIdx.x; k < (s.N + 31) / 32; k += blockDim.x) touched_lds[k] = 0;
@@ -5326,34 +5327,51 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
   __syncthreads();
   int w0 = 0;
   while (w0 < n_wl) {  // block-uniform
-    const int w = w0 + wave;
-    bool fit = false;
-    if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
-      fit = true;
-      const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
-      for (int64_t base = r0; base < r1 && fit; base += kWave) {
-        const int64_t i = base + lane;
-        bool ok = true;
+    // the window's candidates (consecutive workloads: their records are one
+    // contiguous range) checked with every thread of the block, one record
+    // per thread per step, kAdmitU records in flight
+    const int wend = min(w0 + kAdmitWindow, n_wl);
+    if (int(threadIdx.x) < kAdmitWindow) {
+      const int w = w0 + int(threadIdx.x);
+      sh_fit[threadIdx.x] = (w < wend && (wl_fit0[w] != 0 || exact)) ? 1 : 0;
+    }
+    __syncthreads();
+    const int64_t r0 = wl_off[w0], r1 = wl_off[wend];
+    constexpr int kAdmitU = 4;
+    for (int64_t base = r0; base < r1; base += int64_t(kAdmitThreads) * kAdmitU) {
+      AdmitRec a[kAdmitU];
+      int slot[kAdmitU];
+#pragma unroll
+      for (int u = 0; u < kAdmitU; u++) {
+        const int64_t i = base + int64_t(u) * kAdmitThreads + threadIdx.x;
+        slot[u] = -1;
         if (i < r1) {
-          const AdmitRec a = recs[i];
-          if (exact || a.status == kAdmitWide) {
-            ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
-          } else if (a.status == kAdmitNever) {
-            ok = false;
-          } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
-            int64_t us[kAdmitTerms];
-#pragma unroll
-            for (int u = 0; u < kAdmitTerms; u++)
-              us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
-#pragma unroll
-            for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
-          }
+          slot[u] = rec_wl[i] - w0;
+          a[u] = recs[i];
         }
-        fit = ballot(!ok) == 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kAdmitU; u++) {
+        const int64_t i = base + int64_t(u) * kAdmitThreads + threadIdx.x;
+        if (slot[u] < 0 || !sh_fit[slot[u]]) continue;  // not a candidate, or already failed
+        bool ok = true;
+        if (exact || a[u].status == kAdmitWide) {
+          ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+        } else if (a[u].status == kAdmitNever) {
+          ok = false;
+        } else if (a[u].status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a[u].leaf)) {
+          int64_t us[kAdmitTerms];
+#pragma unroll
+          for (int t = 0; t < kAdmitTerms; t++)
+            us[t] = (a[u].col[t] >= 0 && a[u].val[t] > 0) ? load_l2(tas_usage + int64_t(a[u].col[t]) * s.N + a[u].leaf) : 0;
+#pragma unroll
+          for (int t = 0; t < kAdmitTerms; t++) ok &= !(a[u].col[t] >= 0 && a[u].val[t] > 0) || us[t] <= a[u].lim[t];
+        }
+        if (!ok) sh_fit[slot[u]] = 0;  // benign race: every writer stores 0
       }
     }
-    if (lane == 0) sh_fit[wave] = fit ? 1 : 0;
     __syncthreads();
+
     int first = kAdmitWindow;  // first fitting candidate of the window (every thread alike)
     for (int k = kAdmitWindow - 1; k >= 0; k--)
       if (sh_fit[k]) first = k;
