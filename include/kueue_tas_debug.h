@@ -68,7 +68,7 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_SELECTOR_EXT 1024u       /* nodeSelector pairs beyond the inline ones */
 #define KUEUE_TAS_PATH_RAGGED_ROLLUP 2048u      /* staged fill rolls up ragged leaf parents (packed wave slots) */
 #define KUEUE_TAS_PATH_UNIFORM_ROLLUP 4096u     /* staged fill rolls up uniform power-of-two leaf parents */
-#define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: single-run chunks, two leaves per thread */
+#define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: four adjacent leaves per thread */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 
 /* ---- host layer ---------------------------------------------------------- */

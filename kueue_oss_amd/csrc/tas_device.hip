@@ -1572,10 +1572,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
-    // single-run chunks on fill_pair_kernel (two leaves per thread): staged
+    // single-run chunks on fill_pair_kernel (four leaves per thread): staged
     // columns, uniform fan-out >= 2 or no fused parents; it counts the
     // ExclusionStats itself, so the batch takes the inline-stats path
-    const bool pair = c->pair_fill && staged_fill && (c->rack_fanout == 0 || c->rack_fanout >= 2);
+    const bool pair = c->pair_fill && staged_fill && (c->rack_fanout == 0 || c->rack_fanout >= kPairLP);
     const unsigned pgx = unsigned((s.N + kPairTile - 1) / kPairTile);
     if (b.nstat) {
       // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
@@ -1611,7 +1611,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (count <= 0) return;
       constexpr int NSv = decltype(ns)::value;
       constexpr bool TSv = decltype(tsv)::value, MRv = decltype(mr)::value;
-      if (pair) {  // two leaves per thread
+      if (pair) {  // four leaves per thread
         c->fill_paths |= KUEUE_TAS_PATH_PAIR;
         const dim3 pg(pgx, unsigned(count));
         if (gl && b.rack_fanout == 32)

@@ -1146,18 +1146,20 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   }
 }
 
-// ---- the staged fill with two adjacent leaves per thread ----
-// Same semantics as fill_leaves_staged_kernel<NS, TS, false, GL> for chunks
-// of one signature run (CountIn before the class loop) on a snapshot whose
-// leaf parents are uniform power-of-two fan-out F >= 2 (or not rolled up,
-// F = 0), with the ExclusionStats counted in the loop.  A thread holds
-// leaves 2t and 2t+1 of a 512-leaf tile, so every per-class cost that does
-// not depend on the leaf — the parameter reads, the wave-uniform branches,
-// the counter row addresses, a ballot, a butterfly step — is paid once per
-// 128 leaves instead of 64: the parent sums start with the in-lane pair and
-// take one butterfly step fewer, the two counter words go out as one 8-byte
-// store, the ExclusionStats ballots cover two leaves each.
-constexpr int kPairTile = 2 * kFillThreads;  // leaves per pair-kernel block
+// ---- the staged fill with four adjacent leaves per thread ----
+// Same semantics as fill_leaves_staged_kernel<NS, TS, MR, GL> on a snapshot
+// whose leaf parents are uniform power-of-two fan-out F >= kPairLP (or not
+// rolled up, F = 0), with the ExclusionStats counted in the loop.  A thread
+// holds leaves 4t .. 4t+3 of a 1024-leaf tile, so every per-class cost that
+// does not depend on the leaf — the parameter reads, the wave-uniform
+// branches (scalar instructions: the CU's one scalar unit is this kernel's
+// tightest issue port), the counter row addresses, a ballot, a butterfly
+// step — is paid once per 256 leaves instead of 64: the parent sums start
+// with the in-lane group and take two butterfly steps fewer, the four
+// counter words go out as one 16-byte store, the ExclusionStats ballots
+// cover four leaves each.
+constexpr int kPairLP = 4;                     // leaves per thread (adjacent)
+constexpr int kPairTile = kPairLP * kFillThreads;  // leaves per block
 
 // Or-fold: the positive-children masks
 struct OpOr {
@@ -1187,16 +1189,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // then the chunk's records: both sets of loads in flight together
   const int lane = lane_id();
   const int N = s.N;
-  const int leaf0 = tile * kPairTile + 2 * int(threadIdx.x);
+  const int leaf0 = tile * kPairTile + kPairLP * int(threadIdx.x);
   const int gleaf0 = s.level_off[s.L - 1] + leaf0;
-  bool valid[2];
+  bool valid[kPairLP];
   int scol[NS];
-  int64_t cap[2][NS], used[2][NS];
-  uint32_t fp[2], up[2];
-  int prof[2];
-  int32_t lab[2][kStagedLabels];
+  int64_t cap[kPairLP][NS], used[kPairLP][NS];
+  uint32_t fp[kPairLP], up[kPairLP];
+  int prof[kPairLP];
+  int32_t lab[kPairLP][kStagedLabels];
 #pragma unroll
-  for (int j = 0; j < 2; j++) {
+  for (int j = 0; j < kPairLP; j++) {
     const int leaf = leaf0 + j;
     valid[j] = leaf < N;
     fp[j] = valid[j] ? s.free_present[leaf] : 0u;
@@ -1213,7 +1215,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       scol[k] = m ? __builtin_ctz(m) : -1;
       if (m) m &= m - 1;
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         cap[j][k] = used[j][k] = 0;
         if (valid[j] && scol[k] >= 0) {
           cap[j][k] = s.free_cap[int64_t(scol[k]) * N + leaf0 + j];
@@ -1233,15 +1235,15 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   }
   __syncthreads();
   // ---- base signature: remaining capacity per leaf ----
-  bool leader, live[2];
-  uint32_t pres[2];
+  bool leader, live[kPairLP];
+  uint32_t pres[kPairLP];
   {
     const uint32_t flags = uint32_t(uni(sh_pos[0].p.pad[0]));
     const int abeg = uni(sh_pos[0].p.pad[1]), aend = uni(sh_pos[0].p.pad[2]);
     leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
       live[j] = valid[j] && !leaf_out(s, leaf);
       pres[j] = fp[j] | (sim ? 0u : up[j]);
@@ -1303,14 +1305,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     *lim_out = lim;
     return any ? result : 0;
   };
-  int32_t state0[2] = {0, 0}, swl0[2] = {0, 0}, ls0[2] = {0, 0};
-  int lim0[2] = {-1, -1};
+  int32_t state0[kPairLP] = {}, swl0[kPairLP] = {}, ls0[kPairLP] = {};
+  int lim0[kPairLP];
+#pragma unroll
+  for (int j = 0; j < kPairLP; j++) lim0[j] = -1;
   auto count_run = [&](int e) {  // CountIn of the run starting at chunk position e, both leaves
     const uint32_t rmask = uint32_t(uni(sh_pos[e].p.rmask)), lmask = uint32_t(uni(sh_pos[e].p.lmask));
     const DevTerm* wt = sh_pos[e].term;
     const DevTerm* lt = wt + NS;
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       state0[j] = swl0[j] = ls0[j] = 0;
       lim0[j] = -1;
       if (!live[j]) continue;
@@ -1328,10 +1332,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   };
   if constexpr (!MR) count_run(0);
   const int rack_f = FC > 0 ? FC : b.rack_fanout;  // fan-out of the fused parents (0: none)
-  const int half = rack_f >> 1;                    // lanes per parent
+  const int half = rack_f / kPairLP;                    // lanes per parent
   const int parent = rack_f > 0 ? leaf0 / rack_f : 0;
-  const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's pair within its parent
-  const bool pair_store = (gleaf0 & 1) == 0;              // 8-byte aligned counter pairs (wave-uniform)
+  const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's group within its parent
+  const bool vec_store = (gleaf0 & (kPairLP - 1)) == 0;        // kPairLP-word aligned counter groups (wave-uniform)
   const int64_t SD = s.SD;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
@@ -1348,8 +1352,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // exclusion wins: taint, nodeSelector, affinity, required domain, then
     // a resource giving state 0): every condition below is either
     // wave-uniform (a scalar branch) or a v_cndmask, no divergent branch
-    int32_t state[2], swl[2], ls[2], ss[2], sswl[2];
-    int kind[2], id[2];
+    int32_t state[kPairLP], swl[kPairLP], ls[kPairLP], ss[kPairLP], sswl[kPairLP];
+    int kind[kPairLP], id[kPairLP];
     const bool hn = s.lowest_is_hostname != 0;
     int4 c0 = make_int4(0, 0, 0, 0), c1 = c0, v0 = c0, v1 = c0;
     if (hn && nsel > 0) {
@@ -1361,7 +1365,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const int32_t sc[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const int32_t sv[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
       bool ok = live[j];
       int k = (valid[j] && !live[j]) ? EX_DEAD : EX_NONE;
@@ -1437,27 +1441,29 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       }
     }
     int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
-    auto store2 = [&](int64_t off, int32_t a, int32_t c) {  // counter words of leaves leaf0, leaf0 + 1
-      if (pair_store && valid[1]) {
-        *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(a, c);
+    auto storev = [&](int64_t off, const int32_t (&v)[kPairLP]) {  // counter words of leaves leaf0 .. leaf0 + kPairLP - 1
+      if (vec_store && valid[kPairLP - 1]) {
+        if constexpr (kPairLP == 4) *reinterpret_cast<int4*>(base + off + gleaf0) = make_int4(v[0], v[1], v[2], v[3]);
+        else *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(v[0], v[1]);
       } else {
-        if (valid[0]) base[off + gleaf0] = a;
-        if (valid[1]) base[off + gleaf0 + 1] = c;
+#pragma unroll
+        for (int j = 0; j < kPairLP; j++)
+          if (valid[j]) base[off + gleaf0 + j] = v[j];
       }
     };
-    store2(0, state[0], state[1]);
-    store2(SD, ss[0], ss[1]);
+    storev(0, state);
+    storev(SD, ss);
     if (leader) {
-      store2(2 * SD, swl[0], swl[1]);
-      store2(3 * SD, sswl[0], sswl[1]);
-      store2(4 * SD, ls[0], ls[1]);
+      storev(2 * SD, swl);
+      storev(3 * SD, sswl);
+      storev(4 * SD, ls);
     }
     // fused fillInCountsHelper (:1658-1719) of the leaves' parents
     if (rack_f > 0) {
       const int32_t inner = p_inner;
       int32_t cap2 = 0, slc = 0, lead = 0, minD = 0x7fffffff, minSD = 0x7fffffff, has = 0;
 #pragma unroll
-      for (int j = 0; j < 2; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         int32_t cs = state[j], csw = swl[j];
         if (inner != 0 && inner != 1) {
           cs = w_mul(go_div32(cs, inner), inner);
@@ -1483,14 +1489,18 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         lead = group_reduce(lead, half, OpMax());
         has = group_reduce(has, half, OpMax());
       }
-      // positive children: bits 2*gpos, 2*gpos + 1 of the parent's mask
-      const uint32_t pb = uint32_t(valid[0] && ss[0] > 0) | (uint32_t(valid[1] && ss[1] > 0) << 1);
+      // positive children: bits kPairLP*gpos .. kPairLP*gpos + kPairLP - 1 of the parent's mask
+      uint32_t pb = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) pb |= uint32_t(valid[j] && ss[j] > 0) << j;
       uint64_t posm;
       if (rack_f <= 32) {
-        posm = uint32_t(group_reduce(int32_t(pb << (2 * gpos)), half, OpOr()));
+        posm = uint32_t(group_reduce(int32_t(pb << (kPairLP * gpos)), half, OpOr()));
       } else {
-        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < 16 ? pb << (2 * gpos) : 0u), half, OpOr()));
-        const uint32_t hi = uint32_t(group_reduce(int32_t(gpos >= 16 ? pb << (2 * gpos - 32) : 0u), half, OpOr()));
+        const int lo_groups = 32 / kPairLP;
+        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < lo_groups ? pb << (kPairLP * gpos) : 0u), half, OpOr()));
+        const uint32_t hi =
+            uint32_t(group_reduce(int32_t(gpos >= lo_groups ? pb << (kPairLP * gpos - 32) : 0u), half, OpOr()));
         posm = (uint64_t(hi) << 32) | lo;
       }
       if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
@@ -1513,11 +1523,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
     // ExclusionStats (:1579-1634): wave-uniform skip when no leaf of the
     // wave's 128 is excluded; each ballot covers both leaves of a lane
-    const uint64_t any0 = ballot(valid[0] && kind[0] != EX_NONE && kind[0] != EX_DEAD);
-    const uint64_t any1 = ballot(valid[1] && kind[1] != EX_NONE && kind[1] != EX_DEAD);
-    if ((any0 | any1) == 0) continue;
+    uint64_t anyx = 0;
+#pragma unroll
+    for (int j = 0; j < kPairLP; j++) anyx |= ballot(valid[j] && kind[j] != EX_NONE && kind[j] != EX_DEAD);
+    if (anyx == 0) continue;
     auto count_kind = [&](int k, int slot, int32_t* gl) {
-      const int c = __popcll(ballot(kind[0] == k)) + __popcll(ballot(kind[1] == k));
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) c += __popcll(ballot(kind[j] == k));
       if (lane == 0 && c) {
         if (lds_stats) atomicAdd(&sh_stats[e][slot], c);
         else atomicAdd(gl, c);
@@ -1528,18 +1541,31 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     if (dom_begin >= 0) count_kind(EX_TOPOLOGY, 2, &b.dom_counts[eid]);
     // per taint / resource id: the first remaining lane's id, both halves counted together
     auto count_ids = [&](int k, int slot0, int32_t* gl) {
-      uint64_t m0 = ballot(kind[0] == k), m1 = ballot(kind[1] == k);
-      while (m0 | m1) {
-        const int x = m0 ? bcast(id[0], __ffsll((unsigned long long)m0) - 1)
-                         : bcast(id[1], __ffsll((unsigned long long)m1) - 1);
-        const uint64_t h0 = ballot(kind[0] == k && id[0] == x), h1 = ballot(kind[1] == k && id[1] == x);
-        const int c = __popcll(h0) + __popcll(h1);
+      uint64_t m[kPairLP];
+      uint64_t any = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        m[j] = ballot(kind[j] == k);
+        any |= m[j];
+      }
+      while (any) {
+        int x = 0;  // the id of the first lane / leaf still to count
+#pragma unroll
+        for (int j = kPairLP - 1; j >= 0; j--)
+          if (m[j]) x = bcast(id[j], __ffsll((unsigned long long)m[j]) - 1);
+        int c = 0;
+        any = 0;
+#pragma unroll
+        for (int j = 0; j < kPairLP; j++) {
+          const uint64_t h = ballot(kind[j] == k && id[j] == x);
+          c += __popcll(h);
+          m[j] &= ~h;
+          any |= m[j];
+        }
         if (lane == 0) {
           if (lds_stats) atomicAdd(&sh_stats[e][slot0 + x], c);
           else atomicAdd(gl + x, c);
         }
-        m0 &= ~h0;
-        m1 &= ~h1;
       }
     };
     count_ids(EX_TAINT, kStatFixed, b.taint_counts + int64_t(eid) * b.num_taints);

@@ -1,9 +1,9 @@
-"""fill_pair_kernel: the staged fill with two adjacent leaves per thread
+"""fill_pair_kernel: the staged fill with four adjacent leaves per thread
 (fillInCounts tas_flavor_snapshot.go:1568-1647 + the fused first level of
 fillInCountsHelper :1658-1719), ExclusionStats counted in its class loop.
 Checked bit-exactly against the oracle for single-run and multi-run chunks,
-fused fan-outs 2 / 16 / 32 / 64, no fused parents (fan-out > 64, odd leaf
-counts: the unpaired last leaf), leader groups, taints, selectors and
+fused fan-outs 4 / 8 / 16 / 32 / 64, no fused parents (fan-out > 64, leaf
+counts not a multiple of four: the partial last group), leader groups, taints, selectors and
 affinity; the one-leaf staged kernel (KUEUE_TAS_CFG_NO_PAIR_FILL) must give
 the same results.  kueue_tas_last_fill_paths pins which kernel ran."""
 import random
@@ -35,7 +35,8 @@ def _configs(scale):
     yield "c3 fan-out 32", *synth.config_c3(seed=3, n_workloads=3 * n, shape=(2, 2, 4 * scale, 32))
     yield "c3 fan-out 64", *synth.config_c3(seed=4, n_workloads=n, shape=(2, 2, 2 * scale, 64))
     yield "c3 fan-out 16", *synth.config_c3(seed=5, n_workloads=n, shape=(2, 2, 4 * scale, 16))
-    yield "c3 fan-out 2", *synth.config_c3(seed=6, n_workloads=n, shape=(2, 4, 16 * scale, 2))
+    yield "c3 fan-out 4", *synth.config_c3(seed=6, n_workloads=n, shape=(2, 4, 8 * scale, 4))
+    yield "c3 fan-out 8", *synth.config_c3(seed=10, n_workloads=n, shape=(2, 4, 4 * scale, 8))
     yield "c3 fan-out 101 (no fused parents, odd N)", *synth.config_c3(seed=7, n_workloads=n, shape=(1, 1, 3, 101))
     yield "c2 mixed", *synth.config_c2(seed=8, n_workloads=n, shape=(2, 2, 4 * scale, 32))
     yield "c4 leaders", *synth.config_c4(seed=9, n_workloads=8 * scale, shape=(2, 2, 4 * scale, 16))
@@ -46,6 +47,9 @@ def _run(make_pair, make_staged, scale):
         paths = _batch(make_pair, doc, wls)
         assert paths & PAIR, name
         assert _batch(make_staged, doc, wls) & PAIR == 0, name
+    # fan-out 2 (below the kernel's four leaves per thread): the one-leaf staged kernel
+    doc, wls = synth.config_c3(seed=11, n_workloads=64 * scale, shape=(2, 4, 16 * scale, 2))
+    assert _batch(make_pair, doc, wls) & PAIR == 0
 
 
 def _random(make, seed, n):
