@@ -195,8 +195,8 @@ typedef struct {
 /* host layer: copy the entries through kueue_tas_eval_batch's packed buffer
  * instead of reading the zero-copy view (exercises both ABI paths) */
 #define KUEUE_TAS_CFG_PACKED_ENTRIES 1
-/* count ExclusionStats inside the fill instead of the concurrent
- * fill_exclusion_kernel branch (test knob: both paths must agree) */
+/* count ExclusionStats inside the fill (the default since round 3; kept
+ * for callers that set it) */
 #define KUEUE_TAS_CFG_INLINE_STATS 2
 /* keep single-run fill chunks on the one-leaf-per-thread staged kernel
  * instead of fill_pair_kernel (test knob: both paths must agree) */
@@ -204,6 +204,10 @@ typedef struct {
 /* admit with the one-wave in-order chain (admit_kernel) instead of the
  * windowed admit_window_kernel (test knob: both must agree) */
 #define KUEUE_TAS_CFG_SERIAL_ADMIT 8
+/* one-leaf staged fill: ExclusionStats by the concurrent
+ * fill_exclusion_kernel branch instead of inside the fill (test knob: both
+ * paths must agree) */
+#define KUEUE_TAS_CFG_SPLIT_STATS 16
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

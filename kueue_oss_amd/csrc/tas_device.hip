@@ -144,7 +144,7 @@ struct kueue_tas_ctx {
   hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
   std::string err;
   int list_cap = 1024;
-  bool inline_stats = false;  // KUEUE_TAS_CFG_INLINE_STATS
+  bool inline_stats = true;   // ExclusionStats counted in the fill (KUEUE_TAS_CFG_SPLIT_STATS: fill_exclusion_kernel)
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   int max_batch = 1024;
@@ -254,7 +254,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
   auto* c = new kueue_tas_ctx();
   if (cfg) {
     c->device = cfg->device;
-    c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0;
+    c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0 || (cfg->flags & KUEUE_TAS_CFG_SPLIT_STATS) == 0;
     c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
     c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
     if (cfg->list_cap > 0) {

@@ -135,9 +135,10 @@ def _random_affinity_parity(seed, n, make_snap, max_nodes=60):
     return bad
 
 
-@pytest.mark.parametrize("seed,inline,max_nodes,n", [(61, False, 60, 200), (62, True, 60, 120), (63, False, 500, 40)])
-def test_emulated_random_affinity_matches_oracle(emu_lib, seed, inline, max_nodes, n):
-    bad = _random_affinity_parity(seed, n, lambda c: TASFlavorSnapshot(c, lib=emu_lib, inline_stats=inline),
+# split: the one-leaf staged fill with the ExclusionStats counted by fill_exclusion_kernel
+@pytest.mark.parametrize("seed,split,max_nodes,n", [(61, False, 60, 200), (62, True, 60, 120), (63, False, 500, 40)])
+def test_emulated_random_affinity_matches_oracle(emu_lib, seed, split, max_nodes, n):
+    bad = _random_affinity_parity(seed, n, lambda c: TASFlavorSnapshot(c, lib=emu_lib, split_stats=split, pair_fill=not split),
                                   max_nodes=max_nodes)
     assert not bad, bad[0]
 
@@ -157,7 +158,8 @@ def test_validation_reasons_on_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,inline,max_nodes,n", [(71, False, 60, 400), (72, True, 60, 200), (73, False, 600, 60)])
-def test_random_affinity_on_gpu(seed, inline, max_nodes, n):
-    bad = _random_affinity_parity(seed, n, lambda c: TASFlavorSnapshot(c, inline_stats=inline), max_nodes=max_nodes)
+@pytest.mark.parametrize("seed,split,max_nodes,n", [(71, False, 60, 400), (72, True, 60, 200), (73, False, 600, 60)])
+def test_random_affinity_on_gpu(seed, split, max_nodes, n):
+    bad = _random_affinity_parity(seed, n, lambda c: TASFlavorSnapshot(c, split_stats=split, pair_fill=not split),
+                                  max_nodes=max_nodes)
     assert not bad, bad[0]

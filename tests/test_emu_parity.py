@@ -87,13 +87,14 @@ def test_emulated_int64_arithmetic_stress(emu_lib, seed):
         assert got == want, (i, got, want)
 
 
-def test_emulated_inline_stats_path_matches_oracle(emu_lib):
-    # KUEUE_TAS_CFG_INLINE_STATS: ExclusionStats counted inside the fill (no third-stream branch)
+def test_emulated_split_stats_path_matches_oracle(emu_lib):
+    # KUEUE_TAS_CFG_SPLIT_STATS: the one-leaf staged fill with the ExclusionStats
+    # counted by the concurrent fill_exclusion_kernel branch (the default counts them in the fill)
     rng = random.Random(14)
     for i in range(120):
         case = synth.random_case(rng)
         want = oracle_lib.run_case(case)["results"]
-        snap = TASFlavorSnapshot(case, lib=emu_lib, inline_stats=True)
+        snap = TASFlavorSnapshot(case, lib=emu_lib, split_stats=True, pair_fill=False)
         got = snap.find_topology_assignments_for_flavor(case["podSets"])
         snap.close()
         assert got == want, (i, got, want)

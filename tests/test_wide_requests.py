@@ -67,7 +67,7 @@ def _run(make, variant, seeds, n_nodes, n_workloads, want_paths=None):
 
 @pytest.mark.parametrize("variant", ["cols", "profiles", "slots", "manyres"])
 def test_emulated_wide_variants(emu_lib, variant):
-    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False), variant, [0, 1], 300, 24)
+    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, split_stats=True), variant, [0, 1], 300, 24)
 
 
 @pytest.mark.parametrize("variant", ["profiles", "slots"])
@@ -78,7 +78,7 @@ def test_emulated_wide_variants_pair(emu_lib, variant):
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["cols", "profiles", "slots", "manyres"])
 def test_wide_variants_on_gpu(variant):
-    _run(lambda d: TASFlavorSnapshot(d, pair_fill=False), variant, [0, 1, 2, 3], 2500, 96)
+    _run(lambda d: TASFlavorSnapshot(d, pair_fill=False, split_stats=True), variant, [0, 1, 2, 3], 2500, 96)
 
 
 @pytest.mark.gpu
