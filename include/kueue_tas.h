@@ -208,6 +208,12 @@ typedef struct {
  * fill_exclusion_kernel branch instead of inside the fill (test knob: both
  * paths must agree) */
 #define KUEUE_TAS_CFG_SPLIT_STATS 16
+/* roll the upper levels up and take the level maxima in one launch
+ * (rollup_top_kernel: the last block of each class does the top levels)
+ * instead of per-level launches and level_max_kernel.  Off by default: its
+ * per-block device-scope release costs more than the launches it saves on
+ * MI355X (C3 0.039 vs 0.028 ms, C3J 0.505 vs 0.087 ms; profiles/r03_lp4) */
+#define KUEUE_TAS_CFG_FUSED_TOP 32
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

@@ -147,6 +147,7 @@ struct kueue_tas_ctx {
   bool inline_stats = true;   // ExclusionStats counted in the fill (KUEUE_TAS_CFG_SPLIT_STATS: fill_exclusion_kernel)
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
+  bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
@@ -257,6 +258,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0 || (cfg->flags & KUEUE_TAS_CFG_SPLIT_STATS) == 0;
     c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
     c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
+    c->fused_top = (cfg->flags & KUEUE_TAS_CFG_FUSED_TOP) != 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -855,11 +857,10 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
     HIPCHK(c, hipGetLastError());
   }
   if (c->admit_window)  // windowed optimistic admission (one 1024-thread workgroup)
-    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(kAdmitThreads), lds_bits ? nwords * 4 : 0, c->stream,
+    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow), lds_bits ? nwords * 4 : 0, c->stream,
                        c->snap, c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
                        reinterpret_cast<const AdmitRec*>(d + o_recs), reinterpret_cast<const int64_t*>(d + o_off),
-                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n_wl), pods_col,
-                       reinterpret_cast<const int32_t*>(d + o_fit0),
+                       int(n_wl), pods_col, reinterpret_cast<const int32_t*>(d + o_fit0),
                        reinterpret_cast<const int32_t*>(d + o_exact), reinterpret_cast<uint32_t*>(d + o_bits),
                        lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   else  // one wave down the chain
@@ -1005,6 +1006,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
         t.col = cols[k];
         t.val = vals[k];
         t.neg = vals[k] < 0;
+        t.inv = vals[k] > 0 ? 1.0 / double(vals[k]) : 0.0;
         uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
         if (mag) compute_magic(mag, &t);
         *mask |= 1u << cols[k];
@@ -1414,7 +1416,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
   HIPCHK(c, c->d_partials.ensure(size_t(std::max(nleafsel, 1)) * size_t(std::max(nblk, 1))));
 
-  {  // rollup_top_kernel's initial level maxima and arrival counters
+  if (c->fused_top) {  // rollup_top_kernel's initial level maxima and arrival counters
     int32_t* t = reinterpret_cast<int32_t*>(hs + o_top);
     for (size_t i = 0; i < size_t(nfill) * kMaxLevels; i++) t[i] = INT32_MIN;
     for (size_t i = 0; i < size_t(nfill); i++) t[n * kMaxLevels + i] = 0;
@@ -1572,7 +1574,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int nstat = nstat_all;
     b.nstat = lds_stats ? nstat : 0;
     b.nstat_R = s.R;
-    // single-run chunks on fill_pair_kernel (four leaves per thread): staged
+    // single-run chunks on fill_pair_kernel (kPairLP leaves per thread): staged
     // columns, uniform fan-out >= 2 or no fused parents; it counts the
     // ExclusionStats itself, so the batch takes the inline-stats path
     const bool pair = c->pair_fill && staged_fill && (c->rack_fanout == 0 || c->rack_fanout >= kPairLP);
@@ -1611,7 +1613,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (count <= 0) return;
       constexpr int NSv = decltype(ns)::value;
       constexpr bool TSv = decltype(tsv)::value, MRv = decltype(mr)::value;
-      if (pair) {  // four leaves per thread
+      if (pair) {  // kPairLP leaves per thread
         c->fill_paths |= KUEUE_TAS_PATH_PAIR;
         const dim3 pg(pgx, unsigned(count));
         if (gl && b.rack_fanout == 32)
@@ -1696,7 +1698,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const int upper = s.L - 2 - (b.rack_fanout ? 1 : 0);  // levels [0, upper] left to roll up
   int top_parents = 0;  // parents above level `upper`: the fused launch's last block rolls them up
   for (int l = 0; l < upper; l++) top_parents += s.level_size[l];
-  const bool fused_top = nfill > 0 && upper >= 0 && s.level_size[upper] > 0 && top_parents <= 4096 &&
+  const bool fused_top = c->fused_top && nfill > 0 && upper >= 0 && s.level_size[upper] > 0 && top_parents <= 4096 &&
                          s.level_size[upper + 1] / s.level_size[upper] >= 8;
   if (fused_top) {  // every upper level and the level maxima in one launch
     b.level_max = nbf > 0 ? reinterpret_cast<int32_t*>(ds + o_top) : nullptr;

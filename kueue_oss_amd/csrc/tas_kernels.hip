@@ -311,7 +311,24 @@ __device__ __forceinline__ DevTerm uni_term(const DevTerm& t) {
   u.add = uint8_t(uni(t.add));
   u.pow2 = uint8_t(uni(t.pow2));
   u.neg = uint8_t(uni(t.neg));
+  u.inv = __builtin_bit_cast(double, uni64(__builtin_bit_cast(int64_t, t.inv)));
   return u;
+}
+
+// CountInWithLimitingResource's `count < result` for a term after the first
+// (requests.go:206-214), with the int64 division only when it can matter:
+// for c >= 0 and val > 0 an fp64 estimate c * (1 / val) has an absolute
+// error below 1e-6 while the quotient is below 2^31 (relative error of the
+// product <= 3 * 2^-53), so an estimate >= r + 0.5 proves floor(c / val) >= r
+// without the int32 wrap of a larger quotient — the term cannot lower the
+// minimum.  Otherwise *cnt gets the exact count (count_term).
+__device__ __forceinline__ bool term_lowers(int64_t c, const DevTerm& t, int32_t r, int32_t* cnt) {
+  if (c >= 0 && t.val > 0) {
+    const double q = double(c) * t.inv;
+    if (q >= double(r) + 0.5 && q < 2147483000.0) return false;
+  }
+  *cnt = count_term(c, t);
+  return *cnt < r;
 }
 
 // Sorted-set membership of a per-lane id in a wave-uniform id list.
@@ -851,11 +868,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
             const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
             c = int64_t(uint64_t(c) - uint64_t(lt.val));
           }
-          int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
-          if (!any || cnt < result) {
-            result = cnt;
+          if (!any) {
+            result = t.val == 0 ? 0x7fffffff : count_term(c, t);
             lim = col;
             any = true;
+          } else if (t.val != 0) {  // a zero request (count MaxInt32) never lowers the minimum
+            int32_t cnt;
+            if (term_lowers(c, t, result, &cnt)) {
+              result = cnt;
+              lim = col;
+            }
           }
         }
       }
@@ -1017,7 +1039,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
       const int parent = leaf / F;
       const uint64_t posm = ballot(valid && ss > 0);  // positive children, for the BestFit descent
       if ((lane & (F - 1)) == 0 && parent < s.level_size[s.L - 2]) {
-        const uint64_t seg = F == kWave ? posm : (posm >> lane) & ((1ull << F) - 1ull);
+        const uint64_t seg = F == kWave ? posm : (posm >> lane) & ((1ull << (F & 63)) - 1ull);
         b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = seg;
         const int32_t pswl = has ? w_sub(cap, minD) : 0;
         int32_t psswl = has ? w_sub(slc, minSD) : 0;
@@ -1146,19 +1168,22 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   }
 }
 
-// ---- the staged fill with four adjacent leaves per thread ----
+// ---- the staged fill with kPairLP adjacent leaves per thread ----
 // Same semantics as fill_leaves_staged_kernel<NS, TS, MR, GL> on a snapshot
 // whose leaf parents are uniform power-of-two fan-out F >= kPairLP (or not
 // rolled up, F = 0), with the ExclusionStats counted in the loop.  A thread
-// holds leaves 4t .. 4t+3 of a 1024-leaf tile, so every per-class cost that
-// does not depend on the leaf — the parameter reads, the wave-uniform
-// branches (scalar instructions: the CU's one scalar unit is this kernel's
-// tightest issue port), the counter row addresses, a ballot, a butterfly
-// step — is paid once per 256 leaves instead of 64: the parent sums start
-// with the in-lane group and take two butterfly steps fewer, the four
-// counter words go out as one 16-byte store, the ExclusionStats ballots
-// cover four leaves each.
-constexpr int kPairLP = 4;                     // leaves per thread (adjacent)
+// holds leaves kPairLP*t .. kPairLP*t + kPairLP - 1 of a kPairTile-leaf tile,
+// so every per-class cost that does not depend on the leaf — the parameter
+// reads, the wave-uniform branches (scalar instructions: the CU's one scalar
+// unit is this kernel's tightest issue port), the counter row addresses, a
+// ballot, a butterfly step — is paid once per 64 * kPairLP leaves instead of
+// 64: the parent sums start with the in-lane group and take log2(kPairLP)
+// butterfly steps fewer, the counter words go out as one wide store, the
+// ExclusionStats ballots cover kPairLP leaves each.  Two leaves measured
+// faster than four on C3 (84 us vs 117 us per launch, profiles/r03_lp4): at
+// four the register footprint halves the waves per SIMD and the grid (128
+// tiles x classes / 8) leaves too few waves to hide the column loads.
+constexpr int kPairLP = 2;                     // leaves per thread (adjacent)
 constexpr int kPairTile = kPairLP * kFillThreads;  // leaves per block
 
 // Or-fold: the positive-children masks
@@ -1293,11 +1318,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
             const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
             c = int64_t(uint64_t(c) - uint64_t(lt.val));
           }
-          const int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
-          if (!any || cnt < result) {
-            result = cnt;
+          if (!any) {
+            result = t.val == 0 ? 0x7fffffff : count_term(c, t);
             lim = col;
             any = true;
+          } else if (t.val != 0) {  // a zero request (count MaxInt32) never lowers the minimum
+            int32_t cnt;
+            if (term_lowers(c, t, result, &cnt)) {
+              result = cnt;
+              lim = col;
+            }
           }
         }
       }
@@ -5326,9 +5356,8 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
 // order, Fits tas_flavor_snapshot.go:401-415 then AddUsage :257-265).  Usage
 // only grows during a call, so a candidate checked against the usage of the
 // workloads admitted so far keeps that verdict until the next admission.
-// One 1024-thread workgroup checks the next kAdmitWindow candidates in
-// parallel (their records are one contiguous range: every thread takes
-// records of it, kAdmitU in flight); the window's rejections before
+// One 1024-thread workgroup: each of its kAdmitWindow waves checks one of the
+// next kAdmitWindow candidates in parallel; the window's rejections before
 // its first fitting candidate are final, that candidate is admitted (every
 // thread adds a share of its usage with returning atomics, consumed before
 // the barrier, so the next window's L2 loads see it) and the next window
@@ -5336,15 +5365,18 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
 // instead of one dependent chain step per workload.  A record whose leaf no
 // admitted workload of this call touched (LDS bitmap) keeps its phase-1
 // verdict without a load.
+// (A variant that spread the window's records over all 1024 threads measured
+// admit_device 4.1 ms vs 1.8 ms on C3 (profiles/r03_lp4, r03): a wave per candidate
+// stops at the candidate's first failing record, the spread one checks all.)
 constexpr int kAdmitWindow = 16;
-constexpr int kAdmitThreads = 1024;
-__global__ __launch_bounds__(kAdmitThreads) void admit_window_kernel(
+__global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
-    const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, const int32_t* rec_wl, int n_wl,
-    int pods_col, const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
+    const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
+    const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
     int32_t* admitted) {
   extern __shared__ uint32_t touched_lds[];
   __shared__ int32_t sh_fit[kAdmitWindow];
+  const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
   const bool in_lds = touched_in_lds != 0;
   if (in_lds)  // (the global bitmap is cleared by the host)
     for (int k = threadIdx.x; k < (s.N + 31) / 32; k += blockDim.x) touched_lds[k] = 0;
@@ -5353,51 +5385,34 @@ __global__ __launch_bounds__(kAdmitThreads) void admit_window_kernel(
   __syncthreads();
   int w0 = 0;
   while (w0 < n_wl) {  // block-uniform
-    // the window's candidates (consecutive workloads: their records are one
-    // contiguous range) checked with every thread of the block, one record
-    // per thread per step, kAdmitU records in flight
-    const int wend = min(w0 + kAdmitWindow, n_wl);
-    if (int(threadIdx.x) < kAdmitWindow) {
-      const int w = w0 + int(threadIdx.x);
-      sh_fit[threadIdx.x] = (w < wend && (wl_fit0[w] != 0 || exact)) ? 1 : 0;
-    }
-    __syncthreads();
-    const int64_t r0 = wl_off[w0], r1 = wl_off[wend];
-    constexpr int kAdmitU = 4;
-    for (int64_t base = r0; base < r1; base += int64_t(kAdmitThreads) * kAdmitU) {
-      AdmitRec a[kAdmitU];
-      int slot[kAdmitU];
-#pragma unroll
-      for (int u = 0; u < kAdmitU; u++) {
-        const int64_t i = base + int64_t(u) * kAdmitThreads + threadIdx.x;
-        slot[u] = -1;
-        if (i < r1) {
-          slot[u] = rec_wl[i] - w0;
-          a[u] = recs[i];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kAdmitU; u++) {
-        const int64_t i = base + int64_t(u) * kAdmitThreads + threadIdx.x;
-        if (slot[u] < 0 || !sh_fit[slot[u]]) continue;  // not a candidate, or already failed
+    const int w = w0 + wave;
+    bool fit = false;
+    if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
+      fit = true;
+      const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
+      for (int64_t base = r0; base < r1 && fit; base += kWave) {
+        const int64_t i = base + lane;
         bool ok = true;
-        if (exact || a[u].status == kAdmitWide) {
-          ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
-        } else if (a[u].status == kAdmitNever) {
-          ok = false;
-        } else if (a[u].status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a[u].leaf)) {
-          int64_t us[kAdmitTerms];
+        if (i < r1) {
+          const AdmitRec a = recs[i];
+          if (exact || a.status == kAdmitWide) {
+            ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+          } else if (a.status == kAdmitNever) {
+            ok = false;
+          } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
+            int64_t us[kAdmitTerms];
 #pragma unroll
-          for (int t = 0; t < kAdmitTerms; t++)
-            us[t] = (a[u].col[t] >= 0 && a[u].val[t] > 0) ? load_l2(tas_usage + int64_t(a[u].col[t]) * s.N + a[u].leaf) : 0;
+            for (int u = 0; u < kAdmitTerms; u++)
+              us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
 #pragma unroll
-          for (int t = 0; t < kAdmitTerms; t++) ok &= !(a[u].col[t] >= 0 && a[u].val[t] > 0) || us[t] <= a[u].lim[t];
+            for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
+          }
         }
-        if (!ok) sh_fit[slot[u]] = 0;  // benign race: every writer stores 0
+        fit = ballot(!ok) == 0;
       }
     }
+    if (lane == 0) sh_fit[wave] = fit ? 1 : 0;
     __syncthreads();
-
     int first = kAdmitWindow;  // first fitting candidate of the window (every thread alike)
     for (int k = kAdmitWindow - 1; k >= 0; k--)
       if (sh_fit[k]) first = k;

@@ -1,11 +1,12 @@
-"""fill_pair_kernel: the staged fill with four adjacent leaves per thread
+"""fill_pair_kernel: the staged fill with two adjacent leaves per thread
 (fillInCounts tas_flavor_snapshot.go:1568-1647 + the fused first level of
 fillInCountsHelper :1658-1719), ExclusionStats counted in its class loop.
 Checked bit-exactly against the oracle for single-run and multi-run chunks,
-fused fan-outs 4 / 8 / 16 / 32 / 64, no fused parents (fan-out > 64, leaf
-counts not a multiple of four: the partial last group), leader groups, taints, selectors and
+fused fan-outs 2 / 4 / 8 / 16 / 32 / 64, no fused parents (fan-out > 64, odd
+leaf counts: the partial last group), leader groups, taints, selectors and
 affinity; the one-leaf staged kernel (KUEUE_TAS_CFG_NO_PAIR_FILL) must give
-the same results.  kueue_tas_last_fill_paths pins which kernel ran."""
+the same results (that run also takes the KUEUE_TAS_CFG_FUSED_TOP roll-up:
+rollup_top_kernel).  kueue_tas_last_fill_paths pins which kernel ran."""
 import random
 
 import pytest
@@ -47,9 +48,9 @@ def _run(make_pair, make_staged, scale):
         paths = _batch(make_pair, doc, wls)
         assert paths & PAIR, name
         assert _batch(make_staged, doc, wls) & PAIR == 0, name
-    # fan-out 2 (below the kernel's four leaves per thread): the one-leaf staged kernel
+    # fan-out 2: one parent per lane (the smallest fused fan-out the kernel takes)
     doc, wls = synth.config_c3(seed=11, n_workloads=64 * scale, shape=(2, 4, 16 * scale, 2))
-    assert _batch(make_pair, doc, wls) & PAIR == 0
+    assert _batch(make_pair, doc, wls) & PAIR
 
 
 def _random(make, seed, n):
@@ -68,11 +69,11 @@ def _random(make, seed, n):
 
 
 def test_emulated_pair_fill(emu_lib):  # noqa: F811
-    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False), 1)
+    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, fused_top=True), 1)
     assert _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 31, 40) & PAIR
 
 
 @pytest.mark.gpu
 def test_pair_fill_on_gpu():
-    _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False), 4)
+    _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False, fused_top=True), 4)
     assert _random(lambda d: TASFlavorSnapshot(d), 32, 150) & PAIR
