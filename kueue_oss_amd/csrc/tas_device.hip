@@ -1427,7 +1427,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     const int32_t* h_fill = reinterpret_cast<const int32_t*>(hs + o_fill);
     const int32_t* h_fch = reinterpret_cast<const int32_t*>(hs + o_fchunks);
     const int32_t* h_frun = reinterpret_cast<const int32_t*>(hs + o_frun);
-    const int nsw = ucols <= 4 ? 4 : 8;  // the launch's NS: worker terms [0, NS), leader terms [NS, 2 NS)
+    const int nsw = ucols <= 4 ? 4 : ucols <= 5 ? 5 : 8;  // the launch's NS: worker terms [0, NS), leader terms [NS, 2 NS)
     for (int ch = 0; ch < nfchunks; ch++) {
       const int e0 = h_fch[2 * ch], ne = h_fch[2 * ch + 1];
       const DevEval& base = hev[h_fill[e0]];
@@ -1650,6 +1650,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       return 0;
     };
     using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
     using I8 = std::integral_constant<int, 8>;
     int src = 0;
     c->fill_paths |= ucols <= 8 ? (ts ? KUEUE_TAS_PATH_STAGED : KUEUE_TAS_PATH_STAGED_GLOBAL_TAINTS)
@@ -1662,6 +1663,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       if (hev[i].sx_begin >= 0) c->fill_paths |= KUEUE_TAS_PATH_SELECTOR_EXT;
     if (ucols <= 4 && ts) src = staged2(I4(), std::true_type());
     else if (ucols <= 4) src = staged2(I4(), std::false_type());
+    else if (ucols <= 5 && ts) src = staged2(I5(), std::true_type());
+    else if (ucols <= 5) src = staged2(I5(), std::false_type());
     else if (ucols <= 8 && ts) src = staged2(I8(), std::true_type());
     else if (ucols <= 8) src = staged2(I8(), std::false_type());
     else if (maxt <= 4) hipLaunchKernelGGL(fill_leaves_kernel<4>, grid, dim3(256), 0, c->stream, s, b);
