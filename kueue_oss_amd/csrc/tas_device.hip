@@ -1006,7 +1006,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
         t.col = cols[k];
         t.val = vals[k];
         t.neg = vals[k] < 0;
-        t.inv = vals[k] > 0 ? 1.0 / double(vals[k]) : 0.0;
         uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
         if (mag) compute_magic(mag, &t);
         *mask |= 1u << cols[k];

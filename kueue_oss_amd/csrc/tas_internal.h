@@ -17,7 +17,6 @@ constexpr int kMaxCols = KUEUE_TAS_MAX_COLS;
 struct DevTerm {
   int64_t val;       // request value (Go int64)
   uint64_t magic;    // multiplier (0 when power of two)
-  double inv;        // 1.0 / val for val > 0 (the fill's bound test), else 0
   int32_t col;       // resource column
   uint8_t shift;     // post shift
   uint8_t add;       // 1: "add" variant of the decode

@@ -311,24 +311,45 @@ __device__ __forceinline__ DevTerm uni_term(const DevTerm& t) {
   u.add = uint8_t(uni(t.add));
   u.pow2 = uint8_t(uni(t.pow2));
   u.neg = uint8_t(uni(t.neg));
-  u.inv = __builtin_bit_cast(double, uni64(__builtin_bit_cast(int64_t, t.inv)));
   return u;
 }
 
-// CountInWithLimitingResource's `count < result` for a term after the first
-// (requests.go:206-214), with the int64 division only when it can matter:
-// for c >= 0 and val > 0 an fp64 estimate c * (1 / val) has an absolute
-// error below 1e-6 while the quotient is below 2^31 (relative error of the
-// product <= 3 * 2^-53), so an estimate >= r + 0.5 proves floor(c / val) >= r
-// without the int32 wrap of a larger quotient — the term cannot lower the
-// minimum.  Otherwise *cnt gets the exact count (count_term).
-__device__ __forceinline__ bool term_lowers(int64_t c, const DevTerm& t, int32_t r, int32_t* cnt) {
-  if (c >= 0 && t.val > 0) {
-    const double q = double(c) * t.inv;
-    if (q >= double(r) + 0.5 && q < 2147483000.0) return false;
+// CountInWithLimitingResource (requests.go:190-215) over the staged columns
+// in ascending column order, as selects: the column tests, the term fields
+// and the division variant are wave-uniform (scalar branches), the per-leaf
+// parts — a missing resource, the running minimum, the limiting column —
+// are v_cndmask, so no divergent branch (no exec-mask bookkeeping on the
+// CU's one scalar unit per term).  Counts are >= 0 (count_term), a zero
+// request counts MaxInt32 and never lowers the minimum; the first missing
+// resource (capacity absent, request non-zero) returns 0 with that column.
+template <int NS>
+__device__ __forceinline__ int32_t count_slots_sel(const int (&scol)[NS], const int64_t (&cap)[NS], const DevTerm* terms,
+                                                   uint32_t mask, const DevTerm* lterms, uint32_t lmask, uint32_t presm,
+                                                   bool sub_leader, int* lim_out) {
+  int32_t result = 0;
+  bool any = false, done = false;
+  int lim = -1;
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    const int col = scol[k];
+    if (col >= 0 && ((mask >> col) & 1u)) {  // wave-uniform
+      const DevTerm t = uni_term(terms[__popc(mask & ((1u << col) - 1u))]);
+      int64_t c = cap[k];
+      if (sub_leader && ((lmask >> col) & 1u)) {
+        const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
+        c = int64_t(uint64_t(c) - uint64_t(lt.val));
+      }
+      const int32_t cnt = t.val == 0 ? 0x7fffffff : count_term(c, t);
+      const bool miss = t.val != 0 && !((presm >> col) & 1u);
+      const bool upd = !done && (miss || !any || cnt < result);
+      result = upd ? (miss ? 0 : cnt) : result;
+      lim = upd ? col : lim;
+      done = done || miss;
+      any = true;
+    }
   }
-  *cnt = count_term(c, t);
-  return *cnt < r;
+  *lim_out = lim;
+  return any ? result : 0;
 }
 
 // Sorted-set membership of a per-lane id in a wave-uniform id list.
@@ -849,41 +870,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSna
   // CountInWithLimitingResource over a run's terms (LDS), ascending column order
   auto count_slots = [&](const DevTerm* terms, uint32_t mask, const DevTerm* lterms, uint32_t lmask, uint32_t presm,
                          bool sub_leader, int* lim_out) -> int32_t {
-    int32_t result = 0;
-    bool any = false, done = false;
-    int lim = -1;
-#pragma unroll
-    for (int k = 0; k < NS; k++) {
-      const int col = scol[k];
-      if (col >= 0 && ((mask >> col) & 1u) && !done) {
-        const DevTerm t = uni_term(terms[__popc(mask & ((1u << col) - 1u))]);
-        if (!((presm >> col) & 1u) && t.val != 0) {
-          lim = col;
-          result = 0;
-          any = true;
-          done = true;
-        } else {
-          int64_t c = cap[k];
-          if (sub_leader && ((lmask >> col) & 1u)) {
-            const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
-            c = int64_t(uint64_t(c) - uint64_t(lt.val));
-          }
-          if (!any) {
-            result = t.val == 0 ? 0x7fffffff : count_term(c, t);
-            lim = col;
-            any = true;
-          } else if (t.val != 0) {  // a zero request (count MaxInt32) never lowers the minimum
-            int32_t cnt;
-            if (term_lowers(c, t, result, &cnt)) {
-              result = cnt;
-              lim = col;
-            }
-          }
-        }
-      }
-    }
-    *lim_out = lim;
-    return any ? result : 0;
+    return count_slots_sel<NS>(scol, cap, terms, mask, lterms, lmask, presm, sub_leader, lim_out);
   };
   int32_t state0 = 0, swl0 = 0, ls0 = 0;
   int lim0 = -1;
@@ -1299,41 +1286,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // CountInWithLimitingResource over the run's terms (LDS), ascending column order
   auto count_slots = [&](const int64_t (&cp)[NS], const DevTerm* terms, uint32_t mask, const DevTerm* lterms,
                          uint32_t lmask, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
-    int32_t result = 0;
-    bool any = false, done = false;
-    int lim = -1;
-#pragma unroll
-    for (int k = 0; k < NS; k++) {
-      const int col = scol[k];
-      if (col >= 0 && ((mask >> col) & 1u) && !done) {
-        const DevTerm t = uni_term(terms[__popc(mask & ((1u << col) - 1u))]);
-        if (!((presm >> col) & 1u) && t.val != 0) {
-          lim = col;
-          result = 0;
-          any = true;
-          done = true;
-        } else {
-          int64_t c = cp[k];
-          if (sub_leader && ((lmask >> col) & 1u)) {
-            const DevTerm lt = uni_term(lterms[__popc(lmask & ((1u << col) - 1u))]);
-            c = int64_t(uint64_t(c) - uint64_t(lt.val));
-          }
-          if (!any) {
-            result = t.val == 0 ? 0x7fffffff : count_term(c, t);
-            lim = col;
-            any = true;
-          } else if (t.val != 0) {  // a zero request (count MaxInt32) never lowers the minimum
-            int32_t cnt;
-            if (term_lowers(c, t, result, &cnt)) {
-              result = cnt;
-              lim = col;
-            }
-          }
-        }
-      }
-    }
-    *lim_out = lim;
-    return any ? result : 0;
+    return count_slots_sel<NS>(scol, cp, terms, mask, lterms, lmask, presm, sub_leader, lim_out);
   };
   int32_t state0[kPairLP] = {}, swl0[kPairLP] = {}, ls0[kPairLP] = {};
   int lim0[kPairLP];
@@ -2195,10 +2148,20 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
   const int lo = chunk * kLfcChunk, hi = min(s.N, lo + kLfcChunk);
   uint64_t mysum = 0;
   const int lane = lane_id();
-  for (int base = lo; base < hi; base += blockDim.x) {  // wave-uniform trip count
-    const int i = base + int(threadIdx.x);
+  // every load of the chunk issued before the first bin loop (the loop's LDS
+  // atomics would otherwise order each load after the previous group's work)
+  constexpr int kPer = kLfcChunk / 256;  // launched with 256 threads
+  int32_t xs[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {
+    const int i = lo + u * 256 + int(threadIdx.x);
+    xs[u] = i < hi ? v[i] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; u++) {  // wave-uniform trip count
+    const int i = lo + u * 256 + int(threadIdx.x);
     const bool act = i < hi;
-    const int32_t x = act ? v[i] : 0;
+    const int32_t x = xs[u];
     const bool over = x >= kLfcBins - 1 || x < 0;  // x < 0 cannot occur at a leaf (CountIn clamps at 0)
     if (act && over) mysum += uint64_t(int64_t(x));
     const int bin = over ? kLfcBins - 1 : x;

@@ -9,7 +9,7 @@ for c in ${@:-C1 C2 C4 C5}; do
     C1) args="--batch 1" ;;
     C2) args="--batch 1000" ;;
     C4) args="--batch 256" ;;
-    C5) args="--batch 256 --steps 20 --warmup 3 --cpu-sample 4" ;;
+    C5) args="--batch 1024 --steps 20 --warmup 3 --cpu-sample 4" ;;
     *) echo "unknown config $c"; exit 2 ;;
   esac
   timeout -k 10 900 python bench.py --config $c $args --no-extras > gpurun_out/configs/$c.json 2> gpurun_out/configs/$c.err || exit 1
