@@ -698,8 +698,13 @@ constexpr int kMaxFillStats = 64;  // kStatFixed + taints + resource columns; mo
 // Without it the loop holds no global load at all: on gfx9 vmcnt counts
 // stores too, so a load's wait inside the loop would drain every store of
 // the earlier evals.
+// The five-column variants without global lookups fit 96 VGPRs without
+// spilling when asked to: 5 waves per SIMD instead of 4 (C3J's multi-run fill).
+#ifndef KTAS_WAVES_PER_EU  // (tests/emu's CPU build defines it empty)
+#define KTAS_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
 template <int NS, bool TS, bool MR, bool GL>
-__global__ __launch_bounds__(kFillThreads) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
+__global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(NS == 5 && !GL ? 5 : 1) void fill_leaves_staged_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                           int chunk_base) {
   __shared__ FillEvalParams sh_p[kEvalsPerBlock];
   __shared__ DevTerm sh_term[kEvalsPerBlock][2 * NS];  // a run's worker | leader terms (at its first position)

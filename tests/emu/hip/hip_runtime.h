@@ -19,6 +19,7 @@
 #include <tuple>
 #include <vector>
 
+#define KTAS_WAVES_PER_EU(n)  // occupancy hint: meaningless on the CPU
 #define __global__
 #define __device__
 #define __host__
