@@ -86,10 +86,13 @@ def load_traffic(path, config):
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
     if d.get("config") != config:
-        return None
-    return d.get("fill_bytes_per_launch")
+        return None, None
+    return d.get("fill_bytes_per_launch"), {"file": "profiles/fill_traffic.json", "kernel": d.get("kernel"),
+                                            "pmc": d.get("source"), "correction": d.get("correction"),
+                                            "note": "committed PMC pass of the same command (tools/pmc.sh), "
+                                                    "not measured in this run"}
 
 
 def pct(xs, q):
@@ -193,20 +196,41 @@ def main():
     gc.freeze()
     for _ in range(a.warmup):
         step()
+    # the admission deltas of one whole batch (the timed region
+    # includes delta application): admitted once untimed, then every timed
+    # step applies them alternately negated and again after its evaluation,
+    # so steps evaluate on S + D and S in turn (updateTASUsage on the
+    # resident snapshot, kueue_tas_host_apply_deltas)
+    snap.run_compiled(flags=FULL)
+    if dist is not None:
+        _, _, step_deltas = admit_round(snap, world, rank, dist, device)
+    else:
+        _, step_deltas = snap.admit(snap.last_assignments())
+    neg_deltas = step_deltas.copy()
+    neg_deltas["delta"] = -neg_deltas["delta"]
+    plus = [True]  # the snapshot holds S + D
+
+    def timed_step():
+        step()
+        snap.apply_deltas(neg_deltas if plus[0] else step_deltas)
+        plus[0] = not plus[0]
+
     barrier()
     per_step = [0.0] * a.steps
     clock = time.perf_counter
     t0 = clock()
     for i in range(a.steps):
         ts = clock()
-        step()
+        timed_step()
         per_step[i] = clock() - ts
     barrier()
     dt = time.perf_counter() - t0
+    if plus[0]:
+        snap.apply_deltas(neg_deltas)  # back to S for everything below
     per_step = [x * 1e3 for x in per_step]
     # stage / host breakdown from the same step, in untimed repeats (their
     # ctypes getters stay out of the timed loop)
-    stage_sum, dev_host_sum = {}, {}
+    stage_sum, dev_host_sum, detail_sum = {}, {}, {}
     host_sum = [0.0] * 4
     for _ in range(a.steps):
         step()
@@ -215,6 +239,8 @@ def main():
         host_sum = [x + y for x, y in zip(host_sum, snap.last_profile())]
         for k, v in snap.last_device_host_times().items():
             dev_host_sum[k] = dev_host_sum.get(k, 0.0) + v
+        for k, v in snap.last_host_detail().items():
+            detail_sum[k] = detail_sum.get(k, 0.0) + v
     barrier()
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device=device)
@@ -223,6 +249,8 @@ def main():
     placements = len(all_wls) * a.steps  # every rank's shard, all steps
     value = placements / dt
     st, fill_bytes, per_launch_fill_ms, achieved, R_used = roofline_of(snap, snap_doc, mine, a.steps, stage_sum)
+    # the step's results on S (the timed steps alternate S + D and S)
+    step()
     timed_results = snap.last_results() if rank == 0 and not a.no_cpu else None
 
     # ---- precompiled-request rate (round-1 definition of the step) ----
@@ -296,7 +324,8 @@ def main():
     stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}
     host = dict(zip(("staging_ms", "eval_calls_ms", "decode_ms", "total_ms"), (round(x / a.steps, 3) for x in host_sum)))
     host["eval_call_detail_ms"] = {k: round(v / a.steps, 3) for k, v in dev_host_sum.items()}
-    traffic = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config)
+    host["staging_detail_ms"] = {k: round(v / a.steps, 3) for k, v in detail_sum.items()}
+    traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles", "fill_traffic.json"), a.config)
     if rank == 0:
         line = {
             "metric": "TAS placements/sec at 128k nodes (1/2/4/8 GPU); % HBM roofline",
@@ -321,13 +350,15 @@ def main():
             "roofline": {"kernel": "fill_pair_kernel" if st.get("fill_paths", 0) & 8192 else "fill_leaves_staged_kernel",
                          "bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_launch": int(fill_bytes),
+                         "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": int(fill_bytes),
                          "avg_launch_ms": round(per_launch_fill_ms, 4),
                          "per_launch": f"{N} leaves x {st['fill_evals'] // max(st['fill_launches'], 1)} phase-1 evals "
                                        f"({st['evals'] // max(st['batches'], 1)} evals, deduplicated), {R_used} columns"},
             "precompiled_rate": {"value": round(pre_rate * world, 1), "unit": "placements/s",
                                  "note": "requests compiled once before timing, no TopologyAssignment values "
                                          "(round-1 step definition), no gather"},
+            "deltas_in_step": {"records": int(len(step_deltas)), "note": "every timed step applies one whole-batch "
+                               "admission's deltas (alternately negated and again) after its evaluation"},
             "admission": {"round_ms_median": round(pct(adm_ms, 0.5), 3), "rounds": rounds,
                           "admitted": admitted_n, "deltas": deltas_n,
                           "parts_ms_median": dict(zip(["evaluate", "gather_admit_broadcast", "admit_host_prep",

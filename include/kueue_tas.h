@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KUEUE_TAS_ABI_VERSION 4
+#define KUEUE_TAS_ABI_VERSION 5
 #define KUEUE_TAS_MAX_LEVELS 16    /* topology_types.go:114 (<=16 levels) */
 #define KUEUE_TAS_MAX_COLS 32      /* resource columns per snapshot */
 #define KUEUE_TAS_MAX_SELECTORS 8  /* nodeSelector key=value pairs held inline per request (more: KUEUE_TAS_F_SELECTOR_EXT) */
@@ -214,6 +214,10 @@ typedef struct {
  * per-block device-scope release costs more than the launches it saves on
  * MI355X (C3 0.039 vs 0.028 ms, C3J 0.505 vs 0.087 ms; profiles/r03_lp4) */
 #define KUEUE_TAS_CFG_FUSED_TOP 32
+/* host layer: build TopologyAssignment Values on the host instead of taking
+ * the device's entry tags (kueue_tas_snapshot_set_leaf_tags; test knob: both
+ * must agree) */
+#define KUEUE_TAS_CFG_HOST_VALUES 64
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);
@@ -294,6 +298,21 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries
  * (pinned host memory the device wrote; valid until the next call on ctx).
  * Pass entries = NULL to kueue_tas_eval_batch to skip its copy. */
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
+
+/* Per-leaf opaque 64-bit tags that the device copies next to every entry it
+ * emits (select_kernel, lfc_emit_kernel).  The host layer passes, per leaf,
+ * the address of the leaf's TopologyAssignment Values (its levelValues from
+ * the assignment's first level, buildAssignment tas_flavor_snapshot.go:1472-1501),
+ * so an assignment's Values come back with its (leaf, count) entries instead
+ * of a host pass over every domain; the Go shim can pass
+ * leaf indices into its own []string table the same way.  n must be the
+ * snapshot's leaf count; tags == NULL turns the copy off.  Kept across
+ * batches; kueue_tas_snapshot_load clears it. */
+int kueue_tas_snapshot_set_leaf_tags(kueue_tas_ctx* ctx, const uint64_t* tags, size_t n);
+/* The tags of the last kueue_tas_eval_batch's entries: element k belongs to
+ * entry pair k of kueue_tas_last_entries() (same strided layout, same
+ * lifetime); NULL when no leaf tags are set. */
+const uint64_t* kueue_tas_last_entry_tags(kueue_tas_ctx* ctx);
 
 
 /* ---- admission re-check: TASFlavorSnapshot.Fits (tas_flavor_snapshot.go:401-415) ----

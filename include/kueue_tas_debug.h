@@ -68,7 +68,8 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_SELECTOR_EXT 1024u       /* nodeSelector pairs beyond the inline ones */
 #define KUEUE_TAS_PATH_RAGGED_ROLLUP 2048u      /* staged fill rolls up ragged leaf parents (packed wave slots) */
 #define KUEUE_TAS_PATH_UNIFORM_ROLLUP 4096u     /* staged fill rolls up uniform power-of-two leaf parents */
-#define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: four adjacent leaves per thread */
+#define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: two adjacent leaves per thread (kPairLP) */
+#define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 
 /* ---- host layer ---------------------------------------------------------- */
@@ -87,6 +88,10 @@ int kueue_tas_host_last_eval_ticks(kueue_tas_host* h, int32_t* ticks, size_t n);
 /* Host wall time of the last run_compiled (ms): [0] request staging,
  * [1] kueue_tas_eval_batch calls (device + transfers), [2] result decode, [3] total. */
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
+/* Finer host wall time of the last run (ms): [0] grouping + column check,
+ * [1] request compile (findTopologyAssignment prelude), [2] per-pass request
+ * staging (build_pass), [3] TopologyAssignment Values.  Copies min(n, 4). */
+int kueue_tas_host_last_host_detail(kueue_tas_host* h, double* ms, int n);
 /* Work counters of the last find/run: [0] device batches, [1] evals,
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] OR of
  * kueue_tas_last_fill_paths. */

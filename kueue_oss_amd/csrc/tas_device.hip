@@ -213,6 +213,13 @@ struct kueue_tas_ctx {
   int32_t* ent_dev = nullptr;
   size_t ent_cap = 0;   // int32 capacity
   size_t ent_used = 0;  // int32 used by the last batch
+  // entry tags (kueue_tas_snapshot_set_leaf_tags): per-leaf table in HBM, the
+  // per-entry copies in pinned device-mapped host memory beside the entries
+  DevBuf<uint64_t> d_leaf_tags;
+  bool leaf_tags_on = false;
+  uint64_t* tag_host = nullptr;
+  uint64_t* tag_dev = nullptr;
+  size_t tag_cap = 0;   // uint64 capacity (entry pairs)
   int32_t ent_stride = 0;              // pairs per eval region of the last chunk
   std::vector<int32_t> ent_count;      // pairs written per eval of the last batch (request order)
   std::vector<int64_t> ent_strided_off;  // their region offsets (pairs) in ent_host
@@ -351,6 +358,9 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_level_max.release();
   if (c->ent_host) (void)hipHostFree(c->ent_host);
   c->ent_host = c->ent_dev = nullptr;
+  if (c->tag_host) (void)hipHostFree(c->tag_host);
+  c->tag_host = c->tag_dev = nullptr;
+  c->d_leaf_tags.release();
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evl)
@@ -389,6 +399,10 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   s.N = d->level_sizes[s.L - 1];
   const size_t N = size_t(s.N);
   s.leaf_dead = nullptr;  // a load describes live leaves only
+  s.leaf_tag = nullptr;   // leaf tags describe the previous leaves
+  s.tag_out = nullptr;
+  s.ent_base = nullptr;
+  c->leaf_tags_on = false;
   s.n_live = s.N;
   c->h_dead.assign(N, 0);
   c->n_dead = 0;
@@ -1403,6 +1417,21 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       c->ent_cap = cap;
       HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ent_dev), p, 0));
     }
+    if (c->leaf_tags_on && c->tag_cap < c->ent_cap / 2) {  // one tag per entry pair, same layout
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      const size_t cap = c->ent_cap / 2;
+      uint64_t* p = nullptr;
+      HIPCHK(c, hipHostMalloc(&p, cap * 8, hipHostMallocMapped | hipHostMallocCoherent));
+      if (c->ent_used && c->tag_host) memcpy(p, c->tag_host, c->ent_used / 2 * 8);
+      if (c->tag_host) (void)hipHostFree(c->tag_host);
+      c->tag_host = p;
+      c->tag_cap = cap;
+      HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->tag_dev), p, 0));
+    }
+    if (c->leaf_tags_on) c->fill_paths |= KUEUE_TAS_PATH_ENTRY_TAGS;
+    c->snap.leaf_tag = c->leaf_tags_on ? c->d_leaf_tags.p : nullptr;
+    c->snap.tag_out = c->leaf_tags_on ? c->tag_dev : nullptr;
+    c->snap.ent_base = c->ent_dev;
   }
   HIPCHK(c, c->d_scratch.ensure(nph2 * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
@@ -1931,6 +1960,26 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* c, size_t* num_pairs) {
   if (!c) return nullptr;
   if (num_pairs) *num_pairs = c->ent_used / 2;
   return c->ent_host;
+}
+
+int kueue_tas_snapshot_set_leaf_tags(kueue_tas_ctx* c, const uint64_t* tags, size_t n) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (!tags) {
+    c->leaf_tags_on = false;
+    return KUEUE_TAS_OK;
+  }
+  if (n != size_t(c->snap.N)) return fail(c, KUEUE_TAS_EINVAL, "leaf tags: n must be the snapshot's leaf count");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, c->d_leaf_tags.ensure(std::max<size_t>(n, 1)));
+  if (n) HIPCHK(c, hipMemcpyAsync(c->d_leaf_tags.p, tags, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->leaf_tags_on = true;
+  return KUEUE_TAS_OK;
+}
+
+const uint64_t* kueue_tas_last_entry_tags(kueue_tas_ctx* c) {
+  return (c && c->leaf_tags_on && c->snap.tag_out) ? c->tag_host : nullptr;
 }
 
 int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_capacity) {

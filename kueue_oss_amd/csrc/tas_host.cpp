@@ -390,12 +390,22 @@ struct PodSetResult {
   bool has_assignment = false;
   DomainSpan domains;                  // leaf indices (lexicographic order)
   std::vector<DomainAssignment> own;   // storage once the view is materialized
-  std::vector<DomainValues> values;    // with KUEUE_TAS_RUN_VALUES: the TopologyAssignment domains
+  // with KUEUE_TAS_RUN_VALUES, the TopologyAssignment domains: domain k has
+  // Values = values[k][0 .. levels) (the leaf's levelValues[levelIdx:]) and
+  // Count = domains[k].count.  A view of the entry tags the device wrote
+  // beside the entries (kueue_tas_last_entry_tags), or own_values.
+  const std::string* const* values = nullptr;
+  std::vector<const std::string*> own_values;
+  DomainValues value(size_t k, int32_t levels) const { return {values[k], levels, domains[k].count}; }
   std::string reason;
   void materialize() {
     if (domains.n && domains.p != own.data()) {
       own.assign(domains.p, domains.p + domains.n);
       domains.p = own.data();
+    }
+    if (values && values != own_values.data()) {
+      own_values.assign(values, values + domains.n);
+      values = own_values.data();
     }
   }
 };
@@ -1529,6 +1539,17 @@ class FlavorSnapshot {
       err = std::string("snapshot names: ") + kueue_tas_last_error(ctx);
       return rc;
     }
+    if (!(cfg.flags & KUEUE_TAS_CFG_HOST_VALUES)) {  // entry tags: each leaf's Values address (Values come back with the entries)
+      const int32_t lvl = lowestIsHostname ? L - 1 : 0;
+      const std::string* const* lv = leaf_values();
+      std::vector<uint64_t> tags(size_t(N), 0);
+      for (int i = 0; i < N; i++) tags[size_t(i)] = uint64_t(reinterpret_cast<uintptr_t>(lv[i] + lvl));
+      rc = kueue_tas_snapshot_set_leaf_tags(ctx, tags.data(), tags.size());
+      if (rc) {
+        err = std::string("leaf tags: ") + kueue_tas_last_error(ctx);
+        return rc;
+      }
+    }
     {  // a load puts every leaf in: take the dead ones out again
       std::vector<int32_t> dl, live;
       for (int i = 0; i < N; i++)
@@ -1714,6 +1735,20 @@ class FlavorSnapshot {
   uint64_t compile_gen = 1;  // bumped whenever compiled requests may change
   void compile_group(GroupEval& g, bool simulateEmpty) {
     compile_gen++;
+    compile_group_only(g, simulateEmpty);
+  }
+  // The columns every request of the PodSets names exist (ensure_columns_for
+  // would not change anything); safe to call from several threads.
+  bool columns_known(const std::vector<TASPodSetRequests>& podsets) const {
+    for (auto& p : podsets)
+      for (auto& kv : p.requestIds)
+        if (col_of(kv.first) < 0) return false;
+    return true;
+  }
+  // compile_group without the generation bump: reads the snapshot and writes
+  // only g, so different groups compile concurrently (the caller bumps
+  // compile_gen once for the batch)
+  void compile_group_only(GroupEval& g, bool simulateEmpty) const {
     const TASPodSetRequests& w = *g.workers;
     kueue_tas_eval_req& q = g.req;
     memset(&q, 0, sizeof q);
@@ -1898,7 +1933,7 @@ class FlavorSnapshot {
   // requirements with the same outcome on every leaf fold away.  Sets
   // KUEUE_TAS_F_AFFINITY unless every leaf matches; no remaining term means
   // no leaf matches.  Matching runs in the fill kernels (affinity_match).
-  void compile_affinity(const labelsel::RequiredAffinity& terms, GroupEval& g) {
+  void compile_affinity(const labelsel::RequiredAffinity& terms, GroupEval& g) const {
     int32_t term_id = 0;
     auto add = [&](int32_t col, std::vector<int32_t> ids, bool negate) {
       std::sort(ids.begin(), ids.end());
@@ -2404,6 +2439,7 @@ struct Evaluator {
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   double dev_host_ms[6] = {};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
+  double detail_ms[4] = {0, 0, 0, 0};  // grouping + column check, request compile, build_pass, Values
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[5] = {0, 0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches, [4] fill paths
   std::vector<kueue_tas_eval_req> reqs;
@@ -2435,7 +2471,7 @@ struct Evaluator {
       if (rs[k].name == name) {
         rs[k].has_assignment = has;
         rs[k].domains = DomainSpan{d, nd};
-        rs[k].values.clear();
+        rs[k].values = nullptr;
         rs[k].reason = reason;
         return;
       }
@@ -2444,7 +2480,7 @@ struct Evaluator {
     r.name = name;
     r.has_assignment = has;
     r.domains = DomainSpan{d, nd};  // zero-copy view of the batch's entries
-    r.values.clear();
+    r.values = nullptr;
     r.reason = reason;
   }
 
@@ -2632,21 +2668,46 @@ struct Evaluator {
     counts[0] = counts[1] = counts[2] = 0;
     stats[0] = stats[1] = stats[2] = stats[3] = stats[4] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
+    detail_ms[0] = detail_ms[1] = detail_ms[2] = detail_ms[3] = 0;
     const double t_start = now_ms();
     double t_prep = t_start;  // start of the current pass's preparation
     results->resize(wls.size());
     used.assign(wls.size(), 0);
     if (!precompiled) {
-      // serial: split over the host pool this got slower on the GPU box (the
-      // compiled records then sit in other cores' caches when build_pass reads them)
+      // grouping (FindTopologyAssignmentsForFlavor :528-541) and the
+      // findTopologyAssignment prelude (:804-897) per workload, over the host
+      // pool: every workload writes only its own groups; new resource
+      // columns (rare: they reload the snapshot) are added serially between
+      HostPool& pool = HostPool::get();
+      std::atomic<bool> unknown{false};
+      pool.run(wls.size(), 64, [&](size_t b, size_t e) {
+        bool u = false;
+        for (size_t w = b; w < e; w++) {
+          if (wls[w].groups.empty() || regroup) make_groups(wls[w]);
+          u = u || !snap->columns_known(wls[w].podsets);
+        }
+        if (u) unknown.store(true, std::memory_order_relaxed);
+      });
       bool changed = false;
-      for (auto& wl : wls) {
-        if (wl.groups.empty() || regroup) make_groups(wl);
-        changed |= snap->ensure_columns_for(wl.podsets);
-      }
-      for (auto& wl : wls)
-        for (auto& g : wl.groups)
-          if (!g.compiled || changed) snap->compile_group(g, simulateEmpty);
+      if (unknown.load())
+        for (auto& wl : wls) changed |= snap->ensure_columns_for(wl.podsets);
+      const double t_c = now_ms();
+      detail_ms[0] += t_c - t_start;
+      snap->compile_gen++;
+      std::string perr;
+      std::mutex perr_mu;
+      pool.run(wls.size(), 64, [&](size_t b, size_t e) {
+        try {
+          for (size_t w = b; w < e; w++)
+            for (auto& g : wls[w].groups)
+              if (!g.compiled || changed) snap->compile_group_only(g, simulateEmpty);
+        } catch (const std::exception& x) {
+          std::lock_guard<std::mutex> lk(perr_mu);
+          if (perr.empty()) perr = x.what();
+        }
+      });
+      if (!perr.empty()) throw std::runtime_error(perr);
+      detail_ms[1] += now_ms() - t_c;
     }
     int rc = snap->upload();  // (re)load when columns were added
     if (rc) return rc;
@@ -2664,6 +2725,7 @@ struct Evaluator {
       const std::vector<int32_t>* afv = &affv;
       const std::vector<std::pair<size_t, GroupEval*>>* bt = &batch;
       const std::vector<std::pair<size_t, GroupEval*>>* ea = &early;
+      const double t_bp = now_ms();
       if (pass == 0 && precompiled && !base) {  // no assumed usage yet: reuse the compiled first pass
         if (p0_for != &wls || p0_gen != snap->compile_gen) {
           build_pass(wls, 0, done, assumedBy, p0_reqs, p0_taint, assumed, p0_aff, p0_affv, p0_batch, p0_early);
@@ -2680,6 +2742,7 @@ struct Evaluator {
       } else {
         build_pass(wls, pass, done, assumedBy, reqs, taint_table, assumed, aff, affv, batch, early);
       }
+      detail_ms[2] += now_ms() - t_bp;
       for (auto& we : *ea) {
         for (auto* m : we.second->members)
           set_result((*results)[we.first], used[we.first], m->name, false, nullptr, 0, we.second->early_reason);
@@ -3128,6 +3191,7 @@ struct kueue_tas_host {
   std::vector<std::array<int32_t, 3>> admit_doms;
   std::vector<kueue_tas_fits_req> admit_fr;
   std::vector<kueue_tas_fits_term> admit_terms;
+  std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
     for (auto* v : {&compiled, &shard})
@@ -4082,24 +4146,45 @@ int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash)
     h->err = h->snap->err;
     return rc;
   }
+  const FlavorSnapshot& snap = *h->snap;
+  const int32_t nlev = snap.lowestIsHostname ? 1 : snap.L();  // Values per domain
   if (flags & KUEUE_TAS_RUN_VALUES) {
+    // Values of the domains still viewing the last batch's entries: the tags
+    // the device wrote beside them (the leaf's Values address, uploaded per
+    // snapshot by FlavorSnapshot::upload); the rest (earlier passes'
+    // materialized results, balanced placements) on the host
     const double t0 = now_ms();
-    const FlavorSnapshot& s = *h->snap;
-    const int L = s.L();
-    const int32_t lvl = s.lowestIsHostname ? L - 1 : 0;
-    const std::string* const* lv = s.leaf_values();
-    HostPool::get().run(results.size(), 64, [&](size_t b, size_t e) {
-      for (size_t w = b; w < e; w++)
-        for (auto& r : results[w]) {
+    size_t npairs = 0;
+    const DomainAssignment* e0 =
+        reinterpret_cast<const DomainAssignment*>(kueue_tas_last_entries(snap.ctx, &npairs));
+    const uint64_t* tags = kueue_tas_last_entry_tags(snap.ctx);
+    std::vector<PodSetResult*>& rest = h->values_rest;
+    rest.clear();
+    for (auto& rs : results)
+      for (auto& r : rs) {
+        const size_t nd = r.domains.size();
+        if (!nd) continue;
+        if (tags && r.domains.p >= e0 && r.domains.p + nd <= e0 + npairs)
+          r.values = reinterpret_cast<const std::string* const*>(tags + (r.domains.p - e0));
+        else
+          rest.push_back(&r);
+      }
+    if (!rest.empty()) {
+      const int32_t lvl = snap.L() - nlev;
+      const std::string* const* lv = snap.leaf_values();
+      HostPool::get().run(rest.size(), 16, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+          PodSetResult& r = *rest[i];
           const size_t nd = r.domains.size();
-          r.values.resize(nd);
-          const DomainAssignment* d = r.domains.begin();
-          DomainValues* out = r.values.data();
-          for (size_t k = 0; k < nd; k++) out[k] = {lv[d[k].leaf] + lvl, int32_t(L - lvl), d[k].count};
+          r.own_values.resize(nd);
+          for (size_t k = 0; k < nd; k++) r.own_values[k] = lv[r.domains[k].leaf] + lvl;
+          r.values = r.own_values.data();
         }
-    });
+      });
+    }
     ev.host_ms[2] += now_ms() - t0;
     ev.host_ms[3] += now_ms() - t0;
+    ev.detail_ms[3] += now_ms() - t0;
   }
   memcpy(h->ms, ev.ms, sizeof h->ms);
   memcpy(h->counts, ev.counts, sizeof h->counts);
@@ -4119,8 +4204,9 @@ int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash)
           mix(uint64_t(uint32_t(d.leaf)));
           mix(uint64_t(uint32_t(d.count)));
         }
-        for (auto& v : r.values)
-          for (int32_t k = 0; k < v.n; k++) mix(std::hash<std::string>()(v.values[k]));
+        if (r.values)
+          for (size_t d = 0; d < r.domains.size(); d++)
+            for (int32_t k = 0; k < nlev; k++) mix(std::hash<std::string>()(r.value(d, nlev).values[k]));
         mix(std::hash<std::string>()(r.reason));
       }
     *result_hash = x;
@@ -4155,6 +4241,12 @@ int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4) {
   if (!h || !h->ev) return KUEUE_TAS_EINVAL;
   memcpy(ms4, h->ev->host_ms, sizeof h->ev->host_ms);
+  return 0;
+}
+
+int kueue_tas_host_last_host_detail(kueue_tas_host* h, double* ms, int n) {
+  if (!h || !h->ev || !ms || n < 0) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < 4; k++) ms[k] = h->ev->detail_ms[k];
   return 0;
 }
 

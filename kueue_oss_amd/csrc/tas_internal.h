@@ -82,6 +82,12 @@ struct DevSnap {
   const int2* wave_tab;                // [n_wave_slots]
   int32_t n_wave_slots;
   const int32_t* leaf_parent;          // [N] parent index in level L-2 (with wave_tab)
+  // Entry tags (kueue_tas_snapshot_set_leaf_tags): every emitted entry pair k
+  // of the entries region starting at ent_base also stores leaf_tag[leaf] at
+  // tag_out[k] (null leaf_tag: off).  Set per batch before the descriptor upload.
+  const uint64_t* leaf_tag;            // [N]
+  uint64_t* tag_out;                   // [entry pairs] device view of the pinned tag region
+  const int32_t* ent_base;             // device view of the pinned entries region
 };
 
 // 128-bit lexicographic sort key; lo's low 32 bits hold the domain index in its level.

@@ -2239,6 +2239,16 @@ enum ProfCat : int {
 // process-wide lock, so contexts do not interleave their descriptors).
 __constant__ DevSnap g_select_snap;
 
+// One (leaf, count) entry of an assignment (buildAssignment :1490-1501) as
+// one 8-byte store into the eval's region of pinned host memory, plus the
+// leaf's tag (kueue_tas_snapshot_set_leaf_tags: the host's Values address)
+// at the same pair index of the tag region when tags are on.
+__device__ __forceinline__ void put_entry(int32_t* ent, int pos, int32_t leaf, int32_t count) {
+  *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(leaf, count);
+  const uint64_t* lt = g_select_snap.leaf_tag;
+  if (lt) g_select_snap.tag_out[((ent - g_select_snap.ent_base) >> 1) + pos] = lt[leaf];
+}
+
 struct Wave {
   const DevEval* ev;
   int eid;
@@ -3634,7 +3644,7 @@ __device__ int lds_level_walk(Wave& w, int level, const int32_t* parents, int np
     if (keep) {
       const int pos = cnt + __popcll(km & ((1ull << lane) - 1ull));
       if (ent) {
-        if (pos < ocap) *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(ix, c);  // one 8-byte store
+        if (pos < ocap) put_entry(ent, pos, ix, c);  // one 8-byte store
       } else if (to_lds) {
         chosen_lds[pos] = coff + ix;
       } else if (pos < ocap) {
@@ -3763,7 +3773,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
           if (keep) {
             const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
             if (pos < ent_cap) {
-              *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(lf[u], v[u]);
+              put_entry(ent, pos, lf[u], v[u]);
             }
           }
           cnt += __popcll(km);
@@ -3803,7 +3813,7 @@ __device__ int emit_sorted(Wave& w, const int32_t* gids, int n, bool use_ls, boo
     if (keep) {
       int pos = cnt + rank;
       if (pos < ent_cap) {
-        *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(leaf, v);
+        put_entry(ent, pos, leaf, v);
       }
     }
     cnt += __popcll(m);
@@ -3962,7 +3972,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
     for (int k = 0; k < 4; k++) {
       if (keep[k]) {
         if (pos < ent_cap) {
-          *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(4 * q + k, val[k]);
+          put_entry(ent, pos, 4 * q + k, val[k]);
         }
         pos++;
       }
@@ -4079,7 +4089,7 @@ __device__ void lfc_wide(Wave& w, int32_t need, const int32_t* V, int64_t before
     if (keep) {
       const int pos = cnt + __popcll(km & ((1ull << lane_id()) - 1ull));
       if (pos < ecap) {
-        *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(i, (tie && r == mt - 1) ? rem_last : x);
+        put_entry(ent, pos, i, (tie && r == mt - 1) ? rem_last : x);
       }
     }
     cnt += __popcll(km);
@@ -4129,7 +4139,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
     o.fit_level = L1;
     if (need != 0) {
       if (lane == 0 && ecap > 0) {
-        *reinterpret_cast<int2*>(ent) = make_int2(fit_leaf, need);
+        put_entry(ent, 0, fit_leaf, need);
       }
       o.num_workers = 1;
     }
@@ -4854,7 +4864,7 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
     for (int k = 0; k < 8; k++) {
       if (keep[k]) {
         if (pos < b.entry_cap) {
-          *reinterpret_cast<int2*>(ent + 2 * pos) = make_int2(lo + k, x[k]);
+          put_entry(ent, pos, lo + k, x[k]);
         }
         pos++;
       }

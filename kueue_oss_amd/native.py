@@ -61,7 +61,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
     "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
-    "kueue_tas_snapshot_set_leaf_live",
+    "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
+    "kueue_tas_host_last_host_detail",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -139,6 +140,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_device_host_times.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    lib.kueue_tas_host_last_host_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_find_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_find_workload.restype = c.c_int
@@ -220,11 +222,11 @@ class TASFlavorSnapshot:
     def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
                  packed_entries: bool = False, inline_stats: bool = False,
                  pair_fill: bool = True, serial_admit: bool = False, split_stats: bool = False,
-                 fused_top: bool = False):
+                 fused_top: bool = False, host_values: bool = False):
         self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0)
                               | (0 if pair_fill else 4) | (8 if serial_admit else 0) | (16 if split_stats else 0)
-                              | (32 if fused_top else 0))
+                              | (32 if fused_top else 0) | (64 if host_values else 0))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:
@@ -405,6 +407,14 @@ class TASFlavorSnapshot:
         ms = (ctypes.c_double * 4)()
         self._lib.kueue_tas_host_last_profile(self._h, ms)
         return tuple(ms)
+
+    HOST_DETAIL = ("groups", "compile", "build_pass", "values")
+
+    def last_host_detail(self):
+        """Finer host wall ms of the last run_compiled, dict keyed by HOST_DETAIL."""
+        ms = (ctypes.c_double * 4)()
+        self._lib.kueue_tas_host_last_host_detail(self._h, ms, 4)
+        return dict(zip(self.HOST_DETAIL, list(ms)))
 
     def last_results(self) -> list:
         """Results of the last run_compiled, one result list per compiled workload."""

@@ -44,60 +44,79 @@ def shard_workloads(workloads: list, world: int, rank: int) -> list:
     return [workloads[i] for i in shard_ids(workloads, world, rank)]
 
 
-def _gather_var(arr, world: int, dist, device=None):
-    """All-gather a variable-length 1-D tensor: sizes first, then the buffers
-    padded to the largest (RCCL / gloo all_gather need equal shapes)."""
-    import torch
+# Fixed-capacity exchange buffers (in int32 / int64 words), remembered across
+# rounds and grown to the next power of two when a round overflows them: in
+# the steady state one collective and one device-to-host copy per exchange,
+# no size round trip and no per-rank .item() syncs.
+_CAP = {"gather": 1 << 16, "deltas": 1 << 12}
 
-    n = torch.tensor([arr.numel()], dtype=torch.int64, device=device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    m = max(int(x.item()) for x in sizes)
-    pad = torch.zeros((max(m, 1),), dtype=arr.dtype, device=device)
-    pad[: arr.numel()] = arr
-    out = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(out, pad)
-    return [o[: int(sizes[i].item())] for i, o in enumerate(out)]
+
+def _grow(key, need):
+    c = _CAP[key]
+    while c < need:
+        c *= 2
+    _CAP[key] = c
+    return c
 
 
 def gather_assignments(quads, world: int, dist, device=None):
     """All-gather every rank's full assignments (kueue_tas_host_last_assignments
     int32 quads: per workload a header and one (id, podset, leaf, count) per
-    assigned domain) over RCCL (xGMI) or gloo.  Returns the concatenated int32
-    numpy array, ranks in order; every rank receives all of it."""
+    assigned domain) over RCCL (xGMI) or gloo.  Each rank sends one padded
+    record buffer [length, quads..., padding] of the shared capacity; a round
+    in which some rank's quads exceed it is repeated once with a larger
+    capacity (every rank sees every length, so all agree).  Returns the
+    concatenated int32 numpy array, ranks in order; every rank receives all of it."""
     import numpy as np
     import torch
 
-    t = torch.from_numpy(np.ascontiguousarray(quads, dtype=np.int32)).to(device)
-    parts = _gather_var(t, world, dist, device)
-    return torch.cat(parts).cpu().numpy() if parts else np.zeros(0, dtype=np.int32)
+    q = np.ascontiguousarray(quads, dtype=np.int32).reshape(-1)
+    n = q.size
+    while True:
+        cap = _CAP["gather"]
+        host = np.zeros(cap + 1, dtype=np.int32)
+        host[0] = n
+        host[1:1 + min(n, cap)] = q[:cap]
+        buf = torch.from_numpy(host).to(device)
+        out = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        parts = torch.stack(out).cpu().numpy()  # the exchange's one device-to-host copy
+        lens = parts[:, 0]
+        if int(lens.max()) <= cap:
+            return np.concatenate([parts[r, 1:1 + int(lens[r])] for r in range(world)])
+        _grow("gather", int(lens.max()))
 
 
 def broadcast_deltas(deltas, dist, src: int = 0, device=None):
     """Broadcast the post-admission snapshot deltas (numpy
     native.DELTA_DTYPE records: leaf, column, int64 delta — updateTASUsage,
     tas_flavor_snapshot.go:257-293) from rank ``src``; every replica gets the
-    identical list to apply with kueue_tas_host_apply_deltas."""
+    identical list to apply with kueue_tas_host_apply_deltas.  One padded
+    buffer [count, records as two int64 words each...] of the shared
+    capacity; a count of -1 is the source's failure sentinel (admit_round)."""
     import numpy as np
     import torch
 
     from .native import DELTA_DTYPE
 
     is_src = dist.get_rank() == src
-    n = torch.tensor([len(deltas) if is_src and deltas is not None else 0], dtype=torch.int64, device=device)
-    dist.broadcast(n, src)
-    k = int(n.item())
-    if k < 0:  # the source's admission failed (admit_round): every rank fails with it
-        raise RuntimeError(f"admission failed on rank {src}")
-    if k == 0:
-        return np.zeros(0, dtype=DELTA_DTYPE)
-    if is_src:  # 16-byte records as two int64 words
-        words = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE).view(np.int64).reshape(k, 2)
-        buf = torch.from_numpy(words.copy()).to(device)
-    else:
-        buf = torch.zeros((k, 2), dtype=torch.int64, device=device)
-    dist.broadcast(buf, src)
-    return buf.cpu().numpy().reshape(-1).view(DELTA_DTYPE).copy()
+    k = -1 if is_src and deltas is None else (len(deltas) if is_src else 0)
+    while True:
+        cap = _CAP["deltas"]
+        host = np.zeros(1 + 2 * cap, dtype=np.int64)
+        if is_src:
+            host[0] = k
+            if 0 < k <= cap:
+                host[1:1 + 2 * k] = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE).view(np.int64)
+        buf = torch.from_numpy(host).to(device)
+        dist.broadcast(buf, src)
+        got = buf.cpu().numpy()
+        k = int(got[0])
+        if k < 0:  # the source's admission failed: every rank fails with it
+            raise RuntimeError(f"admission failed on rank {src}")
+        if k <= cap:
+            return got[1:1 + 2 * k].copy().view(DELTA_DTYPE)
+        _grow("deltas", k)
 
 
 def admit_round(snap, world: int, rank: int, dist, device=None, src: int = 0):
@@ -105,8 +124,6 @@ def admit_round(snap, world: int, rank: int, dist, device=None, src: int = 0):
     assignments, rank ``src`` admits in workload order (Fits + AddUsage on its
     replica) and broadcasts the applied deltas, the other replicas apply them.
     Returns (gathered quads, admitted (id, 0/1) pairs or None off-src, deltas)."""
-    import torch
-
     quads = gather_assignments(snap.last_assignments(), world, dist, device)
     admitted = None
     deltas = None
@@ -116,7 +133,10 @@ def admit_round(snap, world: int, rank: int, dist, device=None, src: int = 0):
         except Exception:
             # a failed admission must not leave the other ranks waiting in the
             # broadcast: send the failure count (-1) so every rank raises
-            dist.broadcast(torch.tensor([-1], dtype=torch.int64, device=device), src)
+            try:
+                broadcast_deltas(None, dist, src, device)
+            except RuntimeError:
+                pass  # the sentinel's own echo; the original error propagates
             raise
     deltas = broadcast_deltas(deltas, dist, src, device)
     if rank != src:

@@ -22,6 +22,36 @@ def _modes(make_snap, snap_doc, wls):
     assert hashes[0] == hashes[1] == hashes[3]  # VALUES adds the value strings to the hash
 
 
+def _values_paths(make_snap, snap_doc, wls):
+    """TopologyAssignment Values from the device's entry tags equal the
+    host-built ones (the hash covers every Value string of every domain)."""
+    flags = TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES
+    hashes = []
+    for host_values in (False, True):
+        snap = make_snap(snap_doc, host_values)
+        snap.compile(wls)
+        hashes.append([snap.run_compiled(want_hash=True, flags=flags) for _ in range(2)])
+        assert bool(snap.last_stats()["fill_paths"] & 16384) == (not host_values)  # KUEUE_TAS_PATH_ENTRY_TAGS
+        snap.close()
+    assert hashes[0] == hashes[1] and hashes[0][0] == hashes[0][1]
+
+
+def test_emulated_values_from_entry_tags(emu_lib):
+    snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 2, 8, 16))
+    _values_paths(lambda d, hv: TASFlavorSnapshot(d, lib=emu_lib, host_values=hv), snap_doc, wls)
+    snap_doc, wls = synth.config_c4(n_workloads=8, shape=(2, 2, 4, 16))  # two passes: materialized results
+    _values_paths(lambda d, hv: TASFlavorSnapshot(d, lib=emu_lib, host_values=hv), snap_doc, wls)
+
+
+@pytest.mark.gpu
+def test_values_from_entry_tags_on_gpu():
+    for gen in (synth.config_c3, synth.config_c3j):
+        snap_doc, wls = gen(n_workloads=256)
+        _values_paths(lambda d, hv: TASFlavorSnapshot(d, host_values=hv), snap_doc, wls)
+    snap_doc, wls = synth.config_c4(n_workloads=32, shape=(2, 4, 16, 32))
+    _values_paths(lambda d, hv: TASFlavorSnapshot(d, host_values=hv), snap_doc, wls)
+
+
 def test_emulated_run_modes_c3_small(emu_lib):
     snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 2, 8, 16))
     _modes(lambda d: TASFlavorSnapshot(d, lib=emu_lib), snap_doc, wls)

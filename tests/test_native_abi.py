@@ -28,7 +28,7 @@ def test_library_exports_all_header_symbols():
     lib = kueue_oss_amd.load_library()
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.kueue_tas_abi_version() == 4
+    assert lib.kueue_tas_abi_version() == 5
 
 
 def test_struct_sizes_match_header_layout():
