@@ -283,6 +283,16 @@ int kueue_tas_eval_batch(kueue_tas_ctx* ctx, const kueue_tas_eval_req* reqs, siz
                          const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
                          int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
                          int32_t* res_counts);
+/* kueue_tas_eval_batch with the requests given by address: reqs[i] points at
+ * request i wherever the caller keeps it (the host layer's compiled PodSet
+ * groups), so a batch is assembled without copying the records. */
+int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* ctx, const kueue_tas_eval_req* const* reqs, size_t n,
+                              const int32_t* taint_table, size_t taint_table_len, int32_t num_taints,
+                              const kueue_tas_assumed* assumed, size_t num_assumed,
+                              const kueue_tas_affinity_req* affinity, size_t num_affinity,
+                              const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
+                              int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
+                              int32_t* res_counts);
 /* Phase-1 counters of request i of the last kueue_tas_eval_batch (its
  * fillInCounts + fillInCountsHelper result, tas_flavor_snapshot.go:1568-1719):
  * out[f * S + g] for field f = state, sliceState, stateWithLeader,

@@ -71,6 +71,10 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: two adjacent leaves per thread (kPairLP) */
 #define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
+/* Stage events: on (default), every stage of kueue_tas_last_stage_times is
+ * timed; off, only the fill bracket is (the other events are pure
+ * instrumentation; the ones that order the streams are always recorded). */
+int kueue_tas_set_stage_timing(kueue_tas_ctx* ctx, int32_t on);
 
 /* ---- host layer ---------------------------------------------------------- */
 /* Device stage times of the last run (summed over its batches, ms):
@@ -92,6 +96,13 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
  * [1] request compile (findTopologyAssignment prelude), [2] per-pass request
  * staging (build_pass), [3] TopologyAssignment Values.  Copies min(n, 4). */
 int kueue_tas_host_last_host_detail(kueue_tas_host* h, double* ms, int n);
+/* kueue_tas_set_stage_timing for the host's snapshot (kept across reloads). */
+int kueue_tas_host_set_stage_timing(kueue_tas_host* h, int32_t on);
+/* Device stage ms (as kueue_tas_last_stage_times) summed over every
+ * kueue_tas_host_run since the last reset, with the number of runs and of
+ * fill launches; reset != 0 clears the sums after copying them. */
+int kueue_tas_host_stage_accum(kueue_tas_host* h, float* ms, int n, int64_t* runs, int64_t* fill_launches,
+                               int32_t reset);
 /* Work counters of the last find/run: [0] device batches, [1] evals,
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] OR of
  * kueue_tas_last_fill_paths. */

@@ -148,6 +148,8 @@ struct kueue_tas_ctx {
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
+  bool labels16 = false;      // every staged label column's value ids < 2^16 (packed nodeSelector compare)
+  bool stage_timing = true;   // record every stage event (else only the fill bracket; kueue_tas_set_stage_timing)
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
   // snapshot
@@ -233,6 +235,7 @@ struct kueue_tas_ctx {
   size_t chunk_base = 0;
   std::vector<int32_t> chunk_rep;
   std::vector<uint8_t> chunk_leader;
+  std::vector<const kueue_tas_eval_req*> req_ptrs;  // kueue_tas_eval_batch's requests as kueue_tas_eval_batch_ptrs takes them
 };
 
 // The leaf-row scatter kernels write repeated entries in no fixed order:
@@ -440,6 +443,9 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
     s.taint_profile = c->d_taint_profile.p;
   }
   s.label_values = nullptr;
+  c->labels16 = true;
+  for (int k = 0; k < std::min(s.K, kStagedLabels) && d->label_values; k++)
+    for (size_t i = 0; i < N && c->labels16; i++) c->labels16 = uint32_t(d->label_values[size_t(k) * N + i]) <= 0xffffu;
   if (s.K > 0 && d->label_values && N) {
     HIPCHK(c, c->d_labels.ensure(size_t(s.K) * N));
     HIPCHK(c, hipMemcpyAsync(c->d_labels.p, d->label_values, size_t(s.K) * N * 4, hipMemcpyHostToDevice, c->stream));
@@ -745,6 +751,9 @@ int kueue_tas_snapshot_set_leaf_attrs(kueue_tas_ctx* c, const int32_t* leaves, s
   if (!distinct_leaves(leaves, n)) return fail(c, KUEUE_TAS_EINVAL, "repeated leaf in set_leaf_attrs");
   HIPCHK(c, hipSetDevice(c->device));
   for (size_t i = 0; i < n; i++) c->num_profiles = std::max(c->num_profiles, profiles[i] + 1);
+  for (size_t i = 0; i < n && K; i++)  // the packed nodeSelector compare needs 16-bit staged ids
+    for (size_t k = 0; k < std::min<size_t>(K, size_t(kStagedLabels)); k++)
+      if (uint32_t(labels[i * K + k]) > 0xffffu) c->labels16 = false;
   const size_t prof_off = n * 4, lab_off = 2 * n * 4;
   HIPCHK(c, c->d_setfree.ensure(lab_off + n * K * 4));
   uint8_t* d = c->d_setfree.p;
@@ -893,7 +902,7 @@ static double wall_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n, const int32_t* taint_table,
+static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
                       const kueue_tas_affinity_req* aff, size_t num_aff, const int32_t* aff_vals, size_t num_aff_vals,
                       kueue_tas_eval_out* out, int64_t* offsets, int32_t* taint_counts, int32_t* res_counts,
@@ -910,7 +919,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   size_t nterms = 0;
   int maxt = 1;
   for (size_t i = 0; i < n; i++) {
-    const auto& r = reqs[i];
+    const auto& r = *reqs[i];
     if (r.num_req < 0 || r.num_req > KUEUE_TAS_MAX_COLS || r.num_leader_req < 0 || r.num_leader_req > KUEUE_TAS_MAX_COLS)
       return fail(c, KUEUE_TAS_EINVAL, "num_req");
     if (r.slice_size == 0) return fail(c, KUEUE_TAS_EINVAL, "slice_size == 0 (integer divide by zero)");
@@ -981,7 +990,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   // ---- compile requests to device form (magic numbers) ----
   size_t tp = 0;
   for (size_t i = 0; i < n; i++) {
-    const auto& r = reqs[i];
+    const auto& r = *reqs[i];
     DevEval& e = hev[i];
     memset(&e, 0, sizeof e);
     e.flags = r.flags;
@@ -1484,6 +1493,39 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
         P.sx_begin = ev.sx_begin;
         P.sx_end = ev.sx_end;
         if (ev.sx_begin >= 0) P.sel_far = 1;
+        {  // the packed nodeSelector compare (FillEvalParams::sel_fast)
+          uint32_t m[2] = {0u, 0u}, w[2] = {0u, 0u};
+          bool fast = c->labels16 && !P.sel_far, never = false;
+          for (int k = 0; k < ev.nsel && fast; k++) {
+            const int col = ev.sel_col[k];
+            const uint32_t sh = uint32_t(col & 1) * 16u;
+            const uint32_t fm = 0xffffu << sh;
+            if (col < 0 || col >= kStagedLabels) {
+              fast = false;
+              break;
+            }
+            const int32_t val = ev.sel_val[k];
+            if (val < 0 || val > 0xffff) {  // a value no leaf has
+              never = true;
+              continue;
+            }
+            const uint32_t fw = uint32_t(val) << sh;
+            uint32_t& mm = m[col >> 1];
+            uint32_t& ww = w[col >> 1];
+            if ((mm & fm) && (ww & fm) != fw) never = true;  // one column, two values
+            mm |= fm;
+            ww = (ww & ~fm) | fw;
+          }
+          if (fast && never) {  // want bits outside the mask: no leaf matches
+            m[0] = 0u;
+            w[0] = 1u;
+          }
+          P.sel_fast = fast ? 1 : 0;
+          P.sel_mlo = m[0];
+          P.sel_mhi = m[1];
+          P.sel_wlo = w[0];
+          P.sel_whi = w[1];
+        }
         P.run = h_frun[pos];
         P.sig_new = t == 0 || h_frun[pos - 1] != P.run;
         P.rmask = int32_t(ev.req_mask);
@@ -1498,7 +1540,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
       }
     }
   }
-  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, o_fpos + size_t(nfill) * sizeof(FillPos), hipMemcpyHostToDevice, c->stream));
   // the select path's descriptor (g_select_snap), ordered before both select
   // launches: stream2 joins after events recorded later on this stream.
@@ -1633,8 +1675,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     // staged label columns, or required node affinity
     bool gl = false;
     for (size_t i = 0; i < n && !gl; i++) {
-      gl = (reqs[i].flags & (KUEUE_TAS_F_AFFINITY | KUEUE_TAS_F_SELECTOR_EXT)) != 0;
-      for (int k = 0; k < reqs[i].num_selectors; k++) gl = gl || reqs[i].sel_col[k] >= kStagedLabels;
+      gl = (hev[i].flags & (KUEUE_TAS_F_AFFINITY | KUEUE_TAS_F_SELECTOR_EXT)) != 0;
+      for (int k = 0; k < hev[i].nsel; k++) gl = gl || hev[i].sel_col[k] >= kStagedLabels;
     }
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
     auto staged = [&](auto ns, auto tsv, auto mr, int first, int count, hipStream_t st) {
@@ -1709,14 +1751,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   const bool stats_branch = b.nstat > 0;
   if (stats_branch && !b.stats_split) {
     HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
-    HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
+    if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
     hipLaunchKernelGGL(fill_stats_reduce_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream3, b, int(b.nstat_blocks));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->evs[1], c->stream3));
   }
   if (b.stats_split) {  // counts, reduce and member stores beside the roll-up / select
     HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev[2], 0));
-    HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
+    if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evs[0], c->stream3));
     dim3 grid((s.N + 255) / 256, unsigned(nfchunks));
     if (b.num_profiles <= kStagedProfiles) hipLaunchKernelGGL(fill_exclusion_kernel<true>, grid, dim3(256), 0, c->stream3, s, b);
     else hipLaunchKernelGGL(fill_exclusion_kernel<false>, grid, dim3(256), 0, c->stream3, s, b);
@@ -1758,7 +1800,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(level_max_kernel, dim3(unsigned(nfill), unsigned(s.L - 1)), dim3(256), 0, c->stream, s, b);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   if (npairs && !b.nstat) {  // exclusion stats of the class rep to the other members (global-atomic stats)
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
     HIPCHK(c, hipGetLastError());
@@ -1774,7 +1816,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   // (after the stats replication); the main stream runs the BestFit side
   if (nfast) {
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[2], 0));  // fill done
-    HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
+    if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
     hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
@@ -1796,7 +1838,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
     hipLaunchKernelGGL(leaf_partials_kernel, grid, dim3(256), 0, c->stream, s, b, d_leafsel, nleafsel);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
   // K3 (BestFit side and every other non-fast eval)
   if (nbf) {
     b.wave_lds = bf_wave_lds;
@@ -1804,10 +1846,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
                        size_t(waves) * size_t(bf_wave_lds), c->stream, s, b, d_bf, nbf);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
   if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
-  HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1843,6 +1885,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_t n
   if (taint_counts && nt) memcpy(taint_counts, c->res_stats_h, n * nt * 4);
   if (res_counts && s.R) memcpy(res_counts, c->res_stats_h + n * nt, n * size_t(s.R) * 4);
   float st[KUEUE_TAS_NUM_STAGES] = {};
+  if (!c->stage_timing) {  // only the fill bracket (ev1 -> ev2) was recorded
+    (void)hipEventElapsedTime(&st[0], c->ev[1], c->ev[2]);
+    for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
+    ms[0] += st[0];
+    lap(5);
+    return KUEUE_TAS_OK;
+  }
   for (int k = 0; k < 6; k++) (void)hipEventElapsedTime(&st[k], c->ev[k + 1], c->ev[k + 2]);
   const float partials = st[3];  // ev4 -> ev5: leaf partials; stage [3] reports the concurrent fast-LFC branch
   st[3] = 0.f;
@@ -1864,6 +1913,23 @@ int kueue_tas_eval_batch(kueue_tas_ctx* c, const kueue_tas_eval_req* reqs, size_
                          const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
                          int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
                          int32_t* res_counts) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (n && !reqs) return fail(c, KUEUE_TAS_EINVAL, "null requests");
+  std::vector<const kueue_tas_eval_req*>& ptrs = c->req_ptrs;
+  ptrs.resize(n);
+  for (size_t i = 0; i < n; i++) ptrs[i] = reqs + i;
+  return kueue_tas_eval_batch_ptrs(c, ptrs.data(), n, taint_table, taint_table_len, num_taints, assumed, num_assumed,
+                                   affinity, num_affinity, affinity_values, num_affinity_values, out, entry_offsets,
+                                   entries, entries_capacity, taint_counts, res_counts);
+}
+
+int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, size_t n,
+                              const int32_t* taint_table, size_t taint_table_len, int32_t num_taints,
+                              const kueue_tas_assumed* assumed, size_t num_assumed,
+                              const kueue_tas_affinity_req* affinity, size_t num_affinity,
+                              const int32_t* affinity_values, size_t num_affinity_values, kueue_tas_eval_out* out,
+                              int64_t* entry_offsets, int32_t* entries, size_t entries_capacity, int32_t* taint_counts,
+                              int32_t* res_counts) {
   // g_select_snap is one per device: batches of different contexts must not interleave
   static std::mutex select_snap_mu;
   std::lock_guard<std::mutex> select_snap_lock(select_snap_mu);
@@ -1993,6 +2059,12 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* c, int32_t* entries, size_t entries_c
     if (k) memcpy(entries + 2 * pos, c->ent_host + 2 * size_t(c->ent_strided_off[i]), k * 8);
     pos += k;
   }
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_set_stage_timing(kueue_tas_ctx* c, int32_t on) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  c->stage_timing = on != 0;
   return KUEUE_TAS_OK;
 }
 

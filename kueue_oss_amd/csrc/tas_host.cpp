@@ -522,6 +522,7 @@ class FlavorSnapshot {
   std::vector<int32_t> unnamedLeaves;
 
   kueue_tas_ctx* ctx = nullptr;
+  bool stageTiming = true;  // kueue_tas_set_stage_timing of ctx
   bool dirty = true;
   std::string err;
   kueue_tas_config cfg{};
@@ -1482,6 +1483,7 @@ class FlavorSnapshot {
         err = "kueue_tas_ctx_create failed: no usable HIP device (the TAS path has no CPU fallback)";
         return KUEUE_TAS_EDEVICE;
       }
+      kueue_tas_set_stage_timing(ctx, stageTiming ? 1 : 0);
     }
     const int L = this->L(), N = this->N(), R = int(cols.size());
     std::vector<int32_t> sizes(L), co;
@@ -2442,7 +2444,7 @@ struct Evaluator {
   double detail_ms[4] = {0, 0, 0, 0};  // grouping + column check, request compile, build_pass, Values
   int64_t counts[3] = {0, 0, 0};
   int64_t stats[5] = {0, 0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches, [4] fill paths
-  std::vector<kueue_tas_eval_req> reqs;
+  std::vector<const kueue_tas_eval_req*> reqs;  // the batch's requests: the groups' own records, by address
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
   std::vector<kueue_tas_affinity_req> aff;
@@ -2455,7 +2457,7 @@ struct Evaluator {
   // repeated runs over the same compiled workloads (run_compiled)
   const std::vector<Workload>* p0_for = nullptr;
   uint64_t p0_gen = 0;
-  std::vector<kueue_tas_eval_req> p0_reqs;
+  std::vector<const kueue_tas_eval_req*> p0_reqs;
   std::vector<int32_t> p0_taint;
   std::vector<kueue_tas_affinity_req> p0_aff;
   std::vector<int32_t> p0_affv;
@@ -2487,7 +2489,7 @@ struct Evaluator {
   // requests of one pass: taint rows shared through rowOff, assumed usage per workload
   void build_pass(std::vector<Workload>& wls, size_t pass, const std::vector<char>& done,
                   std::vector<AssumedUsage>& assumedBy,
-                  std::vector<kueue_tas_eval_req>& rq, std::vector<int32_t>& tt, std::vector<kueue_tas_assumed>& as,
+                  std::vector<const kueue_tas_eval_req*>& rq, std::vector<int32_t>& tt, std::vector<kueue_tas_assumed>& as,
                   std::vector<kueue_tas_affinity_req>& af, std::vector<int32_t>& afv,
                   std::vector<std::pair<size_t, GroupEval*>>& bt, std::vector<std::pair<size_t, GroupEval*>>& early) {
     rq.clear();
@@ -2507,8 +2509,10 @@ struct Evaluator {
         early.emplace_back(w, &g);
         continue;
       }
-      rq.push_back(g.req);
-      kueue_tas_eval_req& q = rq.back();
+      // the batch tables' offsets go into the group's own record, which the
+      // batch references in place (kueue_tas_eval_batch_ptrs: no copy)
+      kueue_tas_eval_req& q = g.req;
+      rq.push_back(&q);
       if (!lastRow || *lastRow != g.taint_row) {  // consecutive requests mostly share a row
         auto it = rowOff.find(g.taint_row);
         if (it == rowOff.end()) {
@@ -2577,7 +2581,7 @@ struct Evaluator {
   std::vector<kueue_tas_eval_req> balReq;
   std::vector<kueue_tas_eval_out> balOuts;
   std::vector<int64_t> balOffs;
-  int balanced_pass(const std::vector<kueue_tas_eval_req>& rq, const std::vector<int32_t>& tt,
+  int balanced_pass(const std::vector<const kueue_tas_eval_req*>& rq, const std::vector<int32_t>& tt,
                     const std::vector<kueue_tas_affinity_req>* af, const std::vector<int32_t>* afv,
                     const std::vector<std::pair<size_t, GroupEval*>>& bt, const int32_t** ent_view) {
     const size_t n = bt.size();
@@ -2604,7 +2608,7 @@ struct Evaluator {
     for (size_t c0 = 0; c0 < idx.size(); c0 += chunk) {  // every request of a call in one device chunk
       const size_t m = std::min(chunk, idx.size() - c0);
       balReq.clear();
-      for (size_t k = 0; k < m; k++) balReq.push_back(rq[idx[c0 + k]]);
+      for (size_t k = 0; k < m; k++) balReq.push_back(*rq[idx[c0 + k]]);
       balOuts.resize(m);
       balOffs.resize(m + 1);
       int rc = kueue_tas_eval_batch(s.ctx, balReq.data(), m, tt.data(), tt.size(), int32_t(s.taintStrings.size()),
@@ -2719,7 +2723,7 @@ struct Evaluator {
     const size_t R = snap->cols.size();
     std::vector<std::pair<size_t, GroupEval*>> early;
     for (size_t pass = 0; pass < maxGroups; pass++) {
-      const std::vector<kueue_tas_eval_req>* rq = &reqs;
+      const std::vector<const kueue_tas_eval_req*>* rq = &reqs;
       const std::vector<int32_t>* tt = &taint_table;
       const std::vector<kueue_tas_affinity_req>* af = &aff;
       const std::vector<int32_t>* afv = &affv;
@@ -2741,6 +2745,7 @@ struct Evaluator {
         assumed.clear();
       } else {
         build_pass(wls, pass, done, assumedBy, reqs, taint_table, assumed, aff, affv, batch, early);
+        if (pass == 0) p0_for = nullptr;  // the groups' records now hold this batch's table offsets
       }
       detail_ms[2] += now_ms() - t_bp;
       for (auto& we : *ea) {
@@ -2761,7 +2766,7 @@ struct Evaluator {
       res_counts.resize(n * R);
       const bool packed = (snap->cfg.flags & KUEUE_TAS_CFG_PACKED_ENTRIES) != 0;
       if (packed && entries.size() < 2 * 64 * n) entries.resize(2 * 64 * n);
-      rc = kueue_tas_eval_batch(snap->ctx, rq->data(), n, tt->data(), tt->size(), int32_t(T), assumed.data(),
+      rc = kueue_tas_eval_batch_ptrs(snap->ctx, rq->data(), n, tt->data(), tt->size(), int32_t(T), assumed.data(),
                                 assumed.size(), af->data(), af->size(), afv->data(), afv->size(), outs.data(), offsets.data(), packed ? entries.data() : nullptr,
                                 packed ? entries.size() / 2 : 0, taint_counts.data(), res_counts.data());
       if (rc == KUEUE_TAS_EOVERFLOW && packed) {
@@ -2794,11 +2799,20 @@ struct Evaluator {
       stats[4] |= int64_t(kueue_tas_last_fill_paths(snap->ctx));
       counts[0]++;
       counts[1] += int64_t(n);
-      for (auto& q : *rq) counts[2] += (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
-      for (size_t i = 0; i < n; i++) {
+      // decode: every eval of the pass writes only its own workload's
+      // results, assumed usage and done flag, so the evals decode in parallel
+      // (the failure-text caches are filled first: they are shared)
+      snap->reason_order();
+      (void)snap->topology_quoted();
+      std::atomic<int64_t> leaders{0};
+      HostPool::get().run(n, 64, [&](size_t i0, size_t i1) {
+      std::string reasonBuf;
+      int64_t nlead = 0;
+      for (size_t i = i0; i < i1; i++) {
         const size_t w = (*bt)[i].first;
         GroupEval& g = *(*bt)[i].second;
         const kueue_tas_eval_out& o = outs[i];
+        nlead += (g.req.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
         const BalancedOut* bo = g.balanced && balOut[i].used ? &balOut[i] : nullptr;
         if (bo && !bo->reason.empty()) {  // TAS Balanced Placement failure (tas_balanced_placement.go:149-184, :295-314)
           for (auto* m : g.members) set_result((*results)[w], used[w], m->name, false, nullptr, 0, bo->reason);
@@ -2836,6 +2850,9 @@ struct Evaluator {
         if (bo)  // the balanced result lives in balOut until the next batch
           for (size_t k = 0; k < used[w]; k++) (*results)[w][k].materialize();
       }
+      leaders.fetch_add(nlead, std::memory_order_relaxed);
+      });
+      counts[2] += leaders.load();
       t_prep = now_ms();
       host_ms[2] += t_prep - t_decode;
     }
@@ -3192,6 +3209,8 @@ struct kueue_tas_host {
   std::vector<kueue_tas_fits_req> admit_fr;
   std::vector<kueue_tas_fits_term> admit_terms;
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
+  float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
+  int64_t accum_runs = 0, accum_fills = 0;
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
     for (auto* v : {&compiled, &shard})
@@ -4186,6 +4205,9 @@ int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash)
     ev.host_ms[3] += now_ms() - t0;
     ev.detail_ms[3] += now_ms() - t0;
   }
+  for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) h->stage_accum[k] += ev.stage_ms[k];
+  h->accum_runs++;
+  h->accum_fills += ev.stats[2];
   memcpy(h->ms, ev.ms, sizeof h->ms);
   memcpy(h->counts, ev.counts, sizeof h->counts);
   memcpy(h->stats, ev.stats, sizeof h->stats);
@@ -4241,6 +4263,25 @@ int kueue_tas_host_last_eval_profile(kueue_tas_host* h, int32_t* ticks, size_t n
 int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4) {
   if (!h || !h->ev) return KUEUE_TAS_EINVAL;
   memcpy(ms4, h->ev->host_ms, sizeof h->ev->host_ms);
+  return 0;
+}
+
+int kueue_tas_host_set_stage_timing(kueue_tas_host* h, int32_t on) {
+  if (!h || !h->snap) return KUEUE_TAS_EINVAL;
+  h->snap->stageTiming = on != 0;
+  return h->snap->ctx ? kueue_tas_set_stage_timing(h->snap->ctx, on) : 0;
+}
+
+int kueue_tas_host_stage_accum(kueue_tas_host* h, float* ms, int n, int64_t* runs, int64_t* fill_launches,
+                               int32_t reset) {
+  if (!h || n < 0 || (n && !ms)) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < KUEUE_TAS_NUM_STAGES; k++) ms[k] = h->stage_accum[k];
+  if (runs) *runs = h->accum_runs;
+  if (fill_launches) *fill_launches = h->accum_fills;
+  if (reset) {
+    for (auto& v : h->stage_accum) v = 0;
+    h->accum_runs = h->accum_fills = 0;
+  }
   return 0;
 }
 

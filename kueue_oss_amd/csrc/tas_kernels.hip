@@ -660,6 +660,15 @@ struct alignas(16) FillEvalParams {
                                         // masks; nodeSelector requirements beyond the inline pairs (-1: none)
   int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
   int32_t sx_end, pad[3];
+  // the nodeSelector as one masked compare of the leaf's packed staged label
+  // ids (fill_pair_kernel): column c < kStagedLabels is the 16-bit field c of
+  // the 64-bit key; sel_fast 1 when every pair is a staged column and every
+  // staged column's ids fit 16 bits (kueue_tas_ctx::labels16), else the loop
+  // over sel_col / sel_val.  A pair whose value id no leaf has, or two pairs
+  // on one column with different values, set a want bit outside the mask
+  // (never equal: every leaf mismatches, as labels.SelectorFromSet does).
+  uint32_t sel_mlo, sel_mhi, sel_wlo, sel_whi;
+  int32_t sel_fast, pad2[3];
 };
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
 constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
@@ -1225,6 +1234,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     for (int k = 0; k < kStagedLabels; k++)
       lab[j][k] = (valid[j] && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
   }
+  uint32_t pk_lo[kPairLP], pk_hi[kPairLP];  // the staged label ids as one 64-bit key (FillEvalParams::sel_fast)
+#pragma unroll
+  for (int j = 0; j < kPairLP; j++) {
+    pk_lo[j] = (uint32_t(lab[j][0]) & 0xffffu) | (uint32_t(lab[j][1]) << 16);
+    pk_hi[j] = (uint32_t(lab[j][2]) & 0xffffu) | (uint32_t(lab[j][3]) << 16);
+  }
   {
     uint32_t m = stage_mask;
 #pragma unroll
@@ -1323,7 +1338,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   const int half = rack_f / kPairLP;                    // lanes per parent
   const int parent = rack_f > 0 ? leaf0 / rack_f : 0;
   const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's group within its parent
-  const bool vec_store = (gleaf0 & (kPairLP - 1)) == 0;        // kPairLP-word aligned counter groups (wave-uniform)
+  // every leaf of the block's tile exists and its counter words are
+  // kPairLP-aligned (level offsets are multiples of 4): block-uniform, so the
+  // stores below take a scalar branch, not a per-lane exec mask
+  const bool full_tile = (tile + 1) * kPairTile <= N && (s.level_off[s.L - 1] & (kPairLP - 1)) == 0;
   const int64_t SD = s.SD;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
@@ -1352,6 +1370,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
     const int32_t sc[KUEUE_TAS_MAX_SELECTORS] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const int32_t sv[KUEUE_TAS_MAX_SELECTORS] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    bool sel_fast = false;
+    uint32_t sel_mlo = 0u, sel_mhi = 0u, sel_wlo = 0u, sel_whi = 0u;
+    if (hn && nsel > 0) {
+      const int4 m = pq[9];
+      sel_fast = uni(pq[10].x) != 0;
+      sel_mlo = uint32_t(uni(m.x));
+      sel_mhi = uint32_t(uni(m.y));
+      sel_wlo = uint32_t(uni(m.z));
+      sel_whi = uint32_t(uni(m.w));
+    }
 #pragma unroll
     for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
@@ -1370,7 +1398,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       if (hn && nsel > 0) {
         const int32_t l0 = lab[j][0], l1 = lab[j][1], l2 = lab[j][2], l3 = lab[j][3];
         bool mis = false;
-        if (!GL || !sel_far) {
+        if (sel_fast) {  // wave-uniform: one masked compare of the packed key
+          mis = ((pk_lo[j] & sel_mlo) != sel_wlo) | ((pk_hi[j] & sel_mhi) != sel_whi);
+        } else if (!GL || !sel_far) {
 #pragma unroll
           for (int q = 0; q < KUEUE_TAS_MAX_SELECTORS; q++) {
             if (q < nsel) {  // wave-uniform
@@ -1430,7 +1460,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
     int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
     auto storev = [&](int64_t off, const int32_t (&v)[kPairLP]) {  // counter words of leaves leaf0 .. leaf0 + kPairLP - 1
-      if (vec_store && valid[kPairLP - 1]) {
+      if (full_tile) {
         if constexpr (kPairLP == 4) *reinterpret_cast<int4*>(base + off + gleaf0) = make_int4(v[0], v[1], v[2], v[3]);
         else *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(v[0], v[1]);
       } else {

@@ -62,7 +62,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
     "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
-    "kueue_tas_host_last_host_detail",
+    "kueue_tas_host_last_host_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
+    "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -141,6 +142,9 @@ def _bind(lib):
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_host_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
+    lib.kueue_tas_host_set_stage_timing.argtypes = [c.c_void_p, c.c_int32]
+    lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
+                                               c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_find_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_find_workload.restype = c.c_int
@@ -415,6 +419,20 @@ class TASFlavorSnapshot:
         ms = (ctypes.c_double * 4)()
         self._lib.kueue_tas_host_last_host_detail(self._h, ms, 4)
         return dict(zip(self.HOST_DETAIL, list(ms)))
+
+    def set_stage_timing(self, on: bool):
+        """Record every device stage event (True, default) or only the fill bracket."""
+        if self._lib.kueue_tas_host_set_stage_timing(self._h, 1 if on else 0):
+            raise RuntimeError(self._err())
+
+    def stage_accum(self, reset: bool = False):
+        """Device stage ms summed over every run_compiled since the last reset:
+        (dict keyed by STAGES, runs, fill launches)."""
+        ms = (ctypes.c_float * len(self.STAGES))()
+        runs, fills = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.kueue_tas_host_stage_accum(self._h, ms, len(self.STAGES), ctypes.byref(runs), ctypes.byref(fills),
+                                             1 if reset else 0)
+        return dict(zip(self.STAGES, list(ms))), runs.value, fills.value
 
     def last_results(self) -> list:
         """Results of the last run_compiled, one result list per compiled workload."""
