@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "tas_internal.h"
+#include "tas_pool.h"
 #include "tas_kernels.hip"
 
 using namespace ktas;
@@ -100,6 +101,13 @@ struct FlatMap {
       }
     }
   }
+};
+
+// One static part's phase-1 classes (eval_chunk): chains of local classes
+// per 64-bit class hash, each local class's first member.
+struct PartClasses {
+  FlatMap head;
+  std::vector<int32_t> rep, next;
 };
 
 // libdivide-style u64 magic for exact division by an invariant divisor d >= 1.
@@ -236,6 +244,15 @@ struct kueue_tas_ctx {
   std::vector<int32_t> chunk_rep;
   std::vector<uint8_t> chunk_leader;
   std::vector<const kueue_tas_eval_req*> req_ptrs;  // kueue_tas_eval_batch's requests as kueue_tas_eval_batch_ptrs takes them
+  // eval_chunk's per-request host work (kept between batches)
+  std::vector<int64_t> req_term_off;
+  std::vector<int32_t> req_chunk_maxt;
+  std::vector<std::pair<size_t, std::string>> req_errs;
+  std::vector<uint64_t> req_sig_hash, req_cls_hash;
+  std::vector<uint8_t> req_fast, req_leaf;
+  std::vector<int32_t> req_local_cls, part_map;
+  std::vector<size_t> part_base;
+  std::vector<PartClasses> part_cls;
 };
 
 // The leaf-row scatter kernels write repeated entries in no fixed order:
@@ -915,55 +932,86 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     c->host_ms[k] += t - tm;
     tm = t;
   };
-  // ---- layout of the single pinned upload (evals, terms, tables, index lists) ----
-  size_t nterms = 0;
-  int maxt = 1;
-  for (size_t i = 0; i < n; i++) {
+  // ---- per-request host work over the worker pool: validation and term
+  // counts (pass A), then the device records, division magic and the class
+  // hashes (pass B); errors are reported for the lowest request index ----
+  ktas_pool::HostPool& pool = ktas_pool::HostPool::get();
+  // static parts: the same thread handles the same requests in both passes
+  // (and the host layer's compile and decode of the same workloads before
+  // and after), so their records stay in that core's cache
+  const size_t nparts = pool.parts();
+  const size_t nchunk = nparts;
+  auto part_of = [&](size_t i0) -> size_t {  // the static part starting at request i0
+    size_t t = 0;
+    while (t + 1 < nparts && ktas_pool::HostPool::part_begin(n, t + 1, nparts) <= i0) t++;
+    return t;
+  };
+  std::vector<int64_t>& toff = c->req_term_off;  // first term slot of each request
+  toff.assign(n + 1, 0);
+  std::vector<int32_t>& chunk_maxt = c->req_chunk_maxt;
+  chunk_maxt.assign(std::max<size_t>(nchunk, 1), 1);
+  std::vector<std::pair<size_t, std::string>>& errs = c->req_errs;  // per chunk: (first bad request, message)
+  errs.assign(std::max<size_t>(nchunk, 1), {SIZE_MAX, std::string()});
+  auto validate = [&](size_t i, std::string* msg) -> bool {
     const auto& r = *reqs[i];
     if (r.num_req < 0 || r.num_req > KUEUE_TAS_MAX_COLS || r.num_leader_req < 0 || r.num_leader_req > KUEUE_TAS_MAX_COLS)
-      return fail(c, KUEUE_TAS_EINVAL, "num_req");
-    if (r.slice_size == 0) return fail(c, KUEUE_TAS_EINVAL, "slice_size == 0 (integer divide by zero)");
+      return *msg = "num_req", false;
+    if (r.slice_size == 0) return *msg = "slice_size == 0 (integer divide by zero)", false;
     if (r.requested_level < 0 || r.requested_level >= s.L || r.slice_level < 0 || r.slice_level >= s.L)
-      return fail(c, KUEUE_TAS_EINVAL, "level out of range");
-    if (r.num_selectors < 0 || r.num_selectors > KUEUE_TAS_MAX_SELECTORS) return fail(c, KUEUE_TAS_EINVAL, "num_selectors");
-    if (r.num_selectors > 0 && s.K == 0) return fail(c, KUEUE_TAS_EINVAL, "selectors without label columns");
+      return *msg = "level out of range", false;
+    if (r.num_selectors < 0 || r.num_selectors > KUEUE_TAS_MAX_SELECTORS) return *msg = "num_selectors", false;
+    if (r.num_selectors > 0 && s.K == 0) return *msg = "selectors without label columns", false;
     // host-side shape check of every requirement the fill will read
-    auto check_reqs = [&](int32_t rb, int32_t re, bool terms, const char* what) -> int {
+    auto check_reqs = [&](int32_t rb, int32_t re, bool terms, const char* what) -> bool {
       if (rb < 0 || re < rb || size_t(re) > num_aff || (re > rb && (!aff || !aff_vals)))
-        return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " range");
+        return *msg = std::string(what) + " range", false;
       for (int32_t k = rb; k < re; k++) {
         const kueue_tas_affinity_req& q = aff[k];
         if (q.col < KUEUE_TAS_AFFINITY_LEAF || q.col >= s.K || q.begin < 0 || q.len < 0 ||
             size_t(q.begin) + size_t(q.len) > num_aff_vals || (terms && k > rb && q.term < aff[k - 1].term))
-          return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " requirement");
+          return *msg = std::string(what) + " requirement", false;
         for (int32_t j = 1; j < q.len; j++)
           if (aff_vals[q.begin + j] <= aff_vals[q.begin + j - 1])
-            return fail(c, KUEUE_TAS_EINVAL, std::string(what) + " values not sorted");
+            return *msg = std::string(what) + " values not sorted", false;
       }
-      return 0;
+      return true;
     };
-    if (r.flags & KUEUE_TAS_F_AFFINITY)
-      if (int rc = check_reqs(r.affinity_begin, r.affinity_end, true, "affinity")) return rc;
+    if ((r.flags & KUEUE_TAS_F_AFFINITY) && !check_reqs(r.affinity_begin, r.affinity_end, true, "affinity")) return false;
     if (r.flags & KUEUE_TAS_F_SELECTOR_EXT) {
       if (r.num_selectors != KUEUE_TAS_MAX_SELECTORS)
-        return fail(c, KUEUE_TAS_EINVAL, "KUEUE_TAS_F_SELECTOR_EXT needs the inline selector pairs filled");
-      if (int rc = check_reqs(r.selector_begin, r.selector_end, false, "nodeSelector")) return rc;
+        return *msg = "KUEUE_TAS_F_SELECTOR_EXT needs the inline selector pairs filled", false;
+      if (!check_reqs(r.selector_begin, r.selector_end, false, "nodeSelector")) return false;
     }
     if (r.assumed_begin < 0 || r.assumed_end < r.assumed_begin || size_t(r.assumed_end) > num_assumed ||
         (r.assumed_end > r.assumed_begin && !assumed))
-      return fail(c, KUEUE_TAS_EINVAL, "assumed range");
+      return *msg = "assumed range", false;
     for (int32_t a = r.assumed_begin; a < r.assumed_end; a++) {  // sorted by leaf (the fill's binary search)
       const kueue_tas_assumed& x = assumed[a];
       if (x.leaf < 0 || x.leaf >= s.N || x.col < 0 || x.col >= s.R || x.col >= KUEUE_TAS_MAX_COLS ||
           (a > r.assumed_begin && x.leaf < assumed[a - 1].leaf))
-        return fail(c, KUEUE_TAS_EINVAL, "assumed record out of range or not sorted by leaf");
+        return *msg = "assumed record out of range or not sorted by leaf", false;
     }
     if ((r.flags & KUEUE_TAS_F_DOMAIN) &&
         (r.domain_begin < 0 || r.domain_end < r.domain_begin || r.domain_end > s.N))
-      return fail(c, KUEUE_TAS_EINVAL, "required domain leaf range");
-    nterms += size_t(r.num_req + r.num_leader_req);
-    maxt = std::max(maxt, std::max(r.num_req, r.num_leader_req));
-  }
+      return *msg = "required domain leaf range", false;
+    return true;
+  };
+  pool.run_static(n, [&](size_t i0, size_t i1) {
+    const size_t ch = part_of(i0);
+    std::string msg;
+    for (size_t i = i0; i < i1; i++) {
+      const auto& r = *reqs[i];
+      if (errs[ch].first == SIZE_MAX && !validate(i, &msg)) errs[ch] = {i, msg};
+      toff[i + 1] = int64_t(std::max(r.num_req, 0)) + int64_t(std::max(r.num_leader_req, 0));
+      chunk_maxt[ch] = std::max(chunk_maxt[ch], std::max(r.num_req, r.num_leader_req));
+    }
+  });
+  for (auto& e : errs)
+    if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
+  for (size_t i = 0; i < n; i++) toff[i + 1] += toff[i];
+  const size_t nterms = size_t(toff[n]);
+  int maxt = 1;
+  for (int32_t m : chunk_maxt) maxt = std::max(maxt, m);
   size_t stage_bytes = 0;
   auto seg = [&](size_t bytes) {
     const size_t o = stage_bytes;
@@ -987,73 +1035,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   uint8_t* hs = c->h_stage.p;
   DevEval* hev = reinterpret_cast<DevEval*>(hs + o_evals);
   DevTerm* hterms = reinterpret_cast<DevTerm*>(hs + o_terms);
-  // ---- compile requests to device form (magic numbers) ----
-  size_t tp = 0;
-  for (size_t i = 0; i < n; i++) {
-    const auto& r = *reqs[i];
-    DevEval& e = hev[i];
-    memset(&e, 0, sizeof e);
-    e.flags = r.flags;
-    e.count = r.count;
-    e.slice_size = r.slice_size;
-    e.requested_level = r.requested_level;
-    e.slice_level = r.slice_level;
-    e.nsel = r.num_selectors;
-    e.taint_table = r.taint_table;
-    e.assumed_begin = r.assumed_begin;
-    e.assumed_end = r.assumed_end;
-    e.aff_begin = r.affinity_begin;
-    e.aff_end = r.affinity_end;
-    e.dom_begin = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_begin : -1;
-    e.dom_end = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_end : -1;
-    const bool sx = (r.flags & KUEUE_TAS_F_SELECTOR_EXT) != 0 && r.selector_end > r.selector_begin;
-    e.sx_begin = sx ? r.selector_begin : -1;
-    e.sx_end = sx ? r.selector_end : -1;
-    e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
-    for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
-      e.layer_level[k] = r.layer_level[k];
-      e.layer_size[k] = r.layer_size[k] == 0 ? 1 : r.layer_size[k];
-    }
-    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) e.ssal[l] = r.slice_size_at_level[l];
-    for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
-      e.sel_col[k] = r.sel_col[k];
-      e.sel_val[k] = r.sel_val[k];
-    }
-    auto add_terms = [&](const int32_t* cols, const int64_t* vals, int cnt, uint32_t* mask) -> int {
-      int prev = -1;
-      for (int k = 0; k < cnt; k++) {
-        if (cols[k] < 0 || cols[k] >= s.R || cols[k] <= prev) return -1;
-        prev = cols[k];
-        DevTerm& t = hterms[tp++];
-        memset(&t, 0, sizeof t);
-        t.col = cols[k];
-        t.val = vals[k];
-        t.neg = vals[k] < 0;
-        uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
-        if (mag) compute_magic(mag, &t);
-        *mask |= 1u << cols[k];
-      }
-      return 0;
-    };
-    e.term_begin = int32_t(tp);
-    e.nreq = r.num_req;
-    if (add_terms(r.req_col, r.req_val, r.num_req, &e.req_mask)) return fail(c, KUEUE_TAS_EINVAL, "req columns");
-    e.lead_begin = int32_t(tp);
-    e.nlead = (r.flags & KUEUE_TAS_F_LEADER) ? r.num_leader_req : 0;
-    if (add_terms(r.leader_col, r.leader_val, e.nlead, &e.lead_mask)) return fail(c, KUEUE_TAS_EINVAL, "leader columns");
-  }
-  if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
-  if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
-  if (num_aff) memcpy(hs + o_aff, aff, num_aff * sizeof(kueue_tas_affinity_req));
-  if (num_aff_vals) memcpy(hs + o_affv, aff_vals, num_aff_vals * 4);
-  lap(0);
-
-  // Phase-1 classes: evals with identical phase-1 inputs (request terms,
-  // masks, overlay, slice parameters) get identical counters; phase 1 runs
-  // once per class (its representative).  Every member's select reads the
-  // class counters and keeps its mutations in a private overlay; duplicates
-  // only get the rep's exclusion stats.  A class's request signature (terms,
-  // overlay, simulateEmpty, leader) decides which classes share a fill chunk.
+  // ---- class hashes (phase-1 classes below) ----
   const int32_t P = c->num_profiles;
   auto taint_row = [&](const DevEval& e) -> const int32_t* {
     return (taint_table && size_t(e.taint_table) + size_t(P) <= taint_table_len) ? taint_table + e.taint_table
@@ -1078,33 +1060,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       add(uint64_t(assumed[a].value));
     }
     return h;
-  };
-  auto same_sig = [&](const DevEval& x, const DevEval& y) {
-    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
-    if (x.nreq != y.nreq || x.nlead != y.nlead) return false;
-    for (int k = 0; k < x.nreq + x.nlead; k++) {
-      const DevTerm& a = hterms[k < x.nreq ? x.term_begin + k : x.lead_begin + (k - x.nreq)];
-      const DevTerm& b2 = hterms[k < y.nreq ? y.term_begin + k : y.lead_begin + (k - y.nreq)];
-      if (a.col != b2.col || a.val != b2.val) return false;
-    }
-    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
-    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
-      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
-      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
-      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
-    }
-    return true;
-  };
-  // base signature: what the leaf's remaining capacity depends on (a fill chunk shares it)
-  auto same_base = [&](const DevEval& x, const DevEval& y) {
-    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
-    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
-    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
-      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
-      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
-      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
-    }
-    return true;
   };
   auto mask_hash = [&](const DevEval& e) {
     uint64_t h = 0x9e3779b97f4a7c15ull;
@@ -1138,6 +1093,33 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
     return h;
   };
+  auto same_sig = [&](const DevEval& x, const DevEval& y) {
+    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
+    if (x.nreq != y.nreq || x.nlead != y.nlead) return false;
+    for (int k = 0; k < x.nreq + x.nlead; k++) {
+      const DevTerm& a = hterms[k < x.nreq ? x.term_begin + k : x.lead_begin + (k - x.nreq)];
+      const DevTerm& b2 = hterms[k < y.nreq ? y.term_begin + k : y.lead_begin + (k - y.nreq)];
+      if (a.col != b2.col || a.val != b2.val) return false;
+    }
+    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
+    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
+      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
+      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
+      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
+    }
+    return true;
+  };
+  // base signature: what the leaf's remaining capacity depends on (a fill chunk shares it)
+  auto same_base = [&](const DevEval& x, const DevEval& y) {
+    if ((x.flags ^ y.flags) & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_SIMULATE_EMPTY)) return false;
+    if (x.assumed_end - x.assumed_begin != y.assumed_end - y.assumed_begin) return false;
+    for (int a = 0; a < x.assumed_end - x.assumed_begin; a++) {
+      const kueue_tas_assumed& p = assumed[x.assumed_begin + a];
+      const kueue_tas_assumed& q = assumed[y.assumed_begin + a];
+      if (p.leaf != q.leaf || p.col != q.col || p.value != q.value) return false;
+    }
+    return true;
+  };
   auto same_mask = [&](const DevEval& x, const DevEval& y) {
     if (x.slice_size != y.slice_size || x.slice_level != y.slice_level || x.nsel != y.nsel) return false;
     if (x.dom_begin != y.dom_begin || x.dom_end != y.dom_end) return false;
@@ -1170,6 +1152,123 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
            (e.flags & (KUEUE_TAS_F_LEADER | KUEUE_TAS_F_REQUIRED | KUEUE_TAS_F_MULTILAYER)) == 0 &&
            e.requested_level == s.L - 1 && e.slice_level == s.L - 1 && e.slice_size == 1 && e.count >= 0 && s.N > 0;
   };
+  std::vector<uint64_t>& h_sig = c->req_sig_hash;   // signature hash per request
+  std::vector<uint64_t>& h_cls = c->req_cls_hash;   // signature x mask hash per request
+  h_sig.resize(n);
+  h_cls.resize(n);
+  std::vector<uint8_t>& req_fast = c->req_fast;     // fast-LFC eligible (fast_lfc)
+  std::vector<uint8_t>& req_leaf = c->req_leaf;     // requested level == the leaf level
+  std::vector<int32_t>& req_local_cls = c->req_local_cls;  // class within the request's static part
+  req_fast.resize(n);
+  req_leaf.resize(n);
+  req_local_cls.resize(n);
+  c->part_cls.resize(nparts);
+  for (size_t t = 0; t < nparts; t++) {
+    PartClasses& pc = c->part_cls[t];
+    pc.head.reset(ktas_pool::HostPool::part_begin(n, t + 1, nparts) - ktas_pool::HostPool::part_begin(n, t, nparts));
+    pc.rep.clear();
+    pc.next.clear();
+  }
+  // ---- compile requests to device form (magic numbers) ----
+  pool.run_static(n, [&](size_t i0, size_t i1) {
+    const size_t ch = part_of(i0);
+    for (size_t i = i0; i < i1; i++) {
+      const auto& r = *reqs[i];
+      DevEval& e = hev[i];
+      memset(&e, 0, sizeof e);
+      e.flags = r.flags;
+      e.count = r.count;
+      e.slice_size = r.slice_size;
+      e.requested_level = r.requested_level;
+      e.slice_level = r.slice_level;
+      e.nsel = r.num_selectors;
+      e.taint_table = r.taint_table;
+      e.assumed_begin = r.assumed_begin;
+      e.assumed_end = r.assumed_end;
+      e.aff_begin = r.affinity_begin;
+      e.aff_end = r.affinity_end;
+      e.dom_begin = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_begin : -1;
+      e.dom_end = (r.flags & KUEUE_TAS_F_DOMAIN) ? r.domain_end : -1;
+      const bool sx = (r.flags & KUEUE_TAS_F_SELECTOR_EXT) != 0 && r.selector_end > r.selector_begin;
+      e.sx_begin = sx ? r.selector_begin : -1;
+      e.sx_end = sx ? r.selector_end : -1;
+      e.num_layers = std::min(r.num_layers, KUEUE_TAS_MAX_LAYERS);
+      for (int k = 0; k < KUEUE_TAS_MAX_LAYERS; k++) {
+        e.layer_level[k] = r.layer_level[k];
+        e.layer_size[k] = r.layer_size[k] == 0 ? 1 : r.layer_size[k];
+      }
+      for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) e.ssal[l] = r.slice_size_at_level[l];
+      for (int k = 0; k < KUEUE_TAS_MAX_SELECTORS; k++) {
+        e.sel_col[k] = r.sel_col[k];
+        e.sel_val[k] = r.sel_val[k];
+      }
+      int64_t tp = toff[i];
+      auto add_terms = [&](const int32_t* cols, const int64_t* vals, int cnt, uint32_t* mask) -> int {
+        int prev = -1;
+        for (int k = 0; k < cnt; k++) {
+          if (cols[k] < 0 || cols[k] >= s.R || cols[k] <= prev) return -1;
+          prev = cols[k];
+          DevTerm& t = hterms[tp++];
+          memset(&t, 0, sizeof t);
+          t.col = cols[k];
+          t.val = vals[k];
+          t.neg = vals[k] < 0;
+          uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
+          if (mag) compute_magic(mag, &t);
+          *mask |= 1u << cols[k];
+        }
+        return 0;
+      };
+      e.term_begin = int32_t(tp);
+      e.nreq = r.num_req;
+      if (add_terms(r.req_col, r.req_val, r.num_req, &e.req_mask)) {
+        if (errs[ch].first == SIZE_MAX) errs[ch] = {i, "req columns"};
+        continue;
+      }
+      e.lead_begin = int32_t(tp);
+      e.nlead = (r.flags & KUEUE_TAS_F_LEADER) ? r.num_leader_req : 0;
+      if (add_terms(r.leader_col, r.leader_val, e.nlead, &e.lead_mask)) {
+        if (errs[ch].first == SIZE_MAX) errs[ch] = {i, "leader columns"};
+        continue;
+      }
+      h_sig[i] = sig_hash(e);
+      h_cls[i] = h_sig[i] ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
+      req_fast[i] = fast_lfc(e) ? 1 : 0;
+      req_leaf[i] = e.requested_level == s.L - 1 ? 1 : 0;
+      // this part's classes (first member in request order), exact compare on a hash hit
+      PartClasses& pc = c->part_cls[ch];
+      int32_t k = -1;
+      int32_t* head = pc.head.find(h_cls[i]);
+      for (int32_t q = *head; q >= 0; q = pc.next[size_t(q)]) {
+        const DevEval& r = hev[pc.rep[size_t(q)]];
+        if (same_sig(e, r) && same_mask(e, r)) {
+          k = q;
+          break;
+        }
+      }
+      if (k < 0) {
+        k = int32_t(pc.rep.size());
+        pc.rep.push_back(int32_t(i));
+        pc.next.push_back(*head);
+        *head = k;
+      }
+      req_local_cls[i] = k;
+    }
+  });
+  for (auto& e : errs)
+    if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
+  if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
+  if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
+  if (num_aff) memcpy(hs + o_aff, aff, num_aff * sizeof(kueue_tas_affinity_req));
+  if (num_aff_vals) memcpy(hs + o_affv, aff_vals, num_aff_vals * 4);
+  lap(0);
+
+  // Phase-1 classes: evals with identical phase-1 inputs (request terms,
+  // masks, overlay, slice parameters) get identical counters; phase 1 runs
+  // once per class (its representative).  Every member's select reads the
+  // class counters and keeps its mutations in a private overlay; duplicates
+  // only get the rep's exclusion stats.  A class's request signature (terms,
+  // overlay, simulateEmpty, leader) decides which classes share a fill chunk.
   int32_t* h_fill = reinterpret_cast<int32_t*>(hs + o_fill);
   int32_t* h_fchunks = reinterpret_cast<int32_t*>(hs + o_fchunks);
   int32_t* h_pairs = reinterpret_cast<int32_t*>(hs + o_pairs);
@@ -1200,10 +1299,19 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     std::vector<int32_t>& sig_next = c->sig_next;
     cls_next.clear();
     sig_next.clear();
-    for (size_t i = 0; i < n; i++) {
+    // the parts' classes merged in part order: a global class is numbered by
+    // its first member, as a serial pass over the requests would number it
+    std::vector<int32_t>& part_map = c->part_map;  // (part, local class) -> global class
+    std::vector<size_t>& part_base = c->part_base;
+    part_base.assign(nparts + 1, 0);
+    for (size_t t = 0; t < nparts; t++) part_base[t + 1] = part_base[t] + c->part_cls[t].rep.size();
+    part_map.assign(part_base[nparts], -1);
+    for (size_t t = 0; t < nparts; t++)
+    for (size_t j = 0; j < c->part_cls[t].rep.size(); j++) {
+      const size_t i = size_t(c->part_cls[t].rep[j]);
       const DevEval& e = hev[i];
-      const uint64_t hs1 = sig_hash(e);
-      const uint64_t hc = hs1 ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
+      const uint64_t hs1 = h_sig[i];
+      const uint64_t hc = h_cls[i];
       int32_t k = -1;
       int32_t* head = cls_head.find(hc);
       for (int32_t q = *head; q >= 0; q = cls_next[size_t(q)]) {
@@ -1233,15 +1341,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         }
         cls_sig.push_back(sg);
       }
-      cls_of[i] = k;
+      part_map[part_base[t] + j] = k;
     }
+    for (size_t t = 0; t < nparts; t++)
+      for (size_t i = ktas_pool::HostPool::part_begin(n, t, nparts); i < ktas_pool::HostPool::part_begin(n, t + 1, nparts); i++)
+        cls_of[i] = part_map[part_base[t] + size_t(req_local_cls[i])];
     const int ncls = int(cls_rep.size());
     // representative: the first fast-LFC member if any (its class gets an LFC table slot)
     std::vector<int32_t>& rep = c->cls_fastrep;
     rep.assign(size_t(ncls), -1);
     for (size_t i = 0; i < n; i++) {
       const int32_t k = cls_of[i];
-      if (rep[size_t(k)] < 0 && fast_lfc(hev[i])) rep[size_t(k)] = int32_t(i);
+      if (rep[size_t(k)] < 0 && req_fast[i]) rep[size_t(k)] = int32_t(i);
     }
     std::vector<int32_t>& slot_of = c->cls_slot;
     slot_of.assign(size_t(ncls), -1);
@@ -1255,7 +1366,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
     for (size_t i = 0; i < n; i++) {
       const int32_t k = cls_of[i], r = rep[size_t(k)];
-      const bool fast = slot_of[size_t(k)] >= 0 && fast_lfc(hev[i]);
+      const bool fast = slot_of[size_t(k)] >= 0 && req_fast[i];
       h_rep[i] = r;
       h_slot[i] = fast ? slot_of[size_t(k)] : -1;
       if (fast) h_fast[nfast++] = int32_t(i);
@@ -1266,7 +1377,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         npairs++;
       }
       h_pidx[i] = -1;
-      if (hev[i].requested_level == s.L - 1 && !fast) {
+      if (req_leaf[i] && !fast) {
         h_pidx[i] = nleafsel;
         h_leafsel[nleafsel++] = int32_t(i);
       }
@@ -1647,7 +1758,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     // single-run chunks on fill_pair_kernel (kPairLP leaves per thread): staged
     // columns, uniform fan-out >= 2 or no fused parents; it counts the
     // ExclusionStats itself, so the batch takes the inline-stats path
-    const bool pair = c->pair_fill && staged_fill && (c->rack_fanout == 0 || c->rack_fanout >= kPairLP);
+    // experiment: ragged parents on the pair kernel without the fused roll-up
+    static const bool ragged_pair_exp = getenv("KTAS_RAGGED_PAIR") != nullptr;
+    const bool ragged_unfused = ragged_pair_exp && c->rack_fanout < 0;
+    const bool pair = c->pair_fill && staged_fill &&
+                      (c->rack_fanout == 0 || c->rack_fanout >= kPairLP || ragged_unfused);
     const unsigned pgx = unsigned((s.N + kPairTile - 1) / kPairTile);
     if (b.nstat) {
       // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
@@ -1664,7 +1779,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
     // partial slots per fill position: the exclusion grid (split), else the widest fill grid
     b.nstat_blocks = int32_t(b.stats_split ? grid.x : pair ? pgx : nblk_fill);
-    b.rack_fanout = ucols <= 8 ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
+    b.rack_fanout = ucols <= 8 && !ragged_unfused ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
     if (b.rack_fanout) {
       c->fill_paths |= b.rack_fanout < 0 ? KUEUE_TAS_PATH_RAGGED_ROLLUP : KUEUE_TAS_PATH_UNIFORM_ROLLUP;
       HIPCHK(c, c->d_rack_pos.ensure(size_t(nfill) * size_t(s.level_size[s.L - 2])));

@@ -43,6 +43,7 @@
 #include "json_reader.h"
 #include "label_selectors.h"
 #include "tas_balanced.h"
+#include "tas_pool.h"
 
 namespace kueue_tas {
 
@@ -2314,102 +2315,11 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
 
 // Batched driver: pass p evaluates group p of every workload still running
 // (groups of one workload are sequential through assumedUsage, :543-591).
+using ktas_pool::HostPool;
+
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-// Persistent host workers for per-batch loops that are independent per
-// workload (TopologyAssignment values of a step's results).  The
-// calling thread takes chunks too and only waits for chunks already taken,
-// so a worker still asleep never delays a call; idle workers spin briefly
-// for the next job (steps follow each other within a millisecond), then
-// sleep after 2 ms.  KUEUE_TAS_HOST_THREADS sets the worker count (0: inline).
-class HostPool {
- public:
-  static HostPool& get() {
-    static HostPool pool;
-    return pool;
-  }
-  size_t workers() const { return threads_.size(); }
-  // fn(begin, end) over [0, n) in chunks of `grain`; one job at a time
-  template <class F>
-  void run(size_t n, size_t grain, F&& fn) {
-    if (threads_.empty() || n <= grain) {
-      if (n) fn(size_t(0), n);
-      return;
-    }
-    std::lock_guard<std::mutex> one(callMu_);
-    std::function<void(size_t, size_t)> f(std::ref(fn));
-    auto job = std::make_shared<Job>();
-    job->fn = &f;
-    job->n = n;
-    job->grain = grain;
-    job->chunks = (n + grain - 1) / grain;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = job;
-      epoch_.fetch_add(1, std::memory_order_release);
-    }
-    cv_.notify_all();
-    work(*job);
-    while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
-    std::lock_guard<std::mutex> lk(mu_);
-    job_.reset();  // late workers keep their reference; its chunks are exhausted
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-      epoch_.fetch_add(1);
-    }
-    cv_.notify_all();
-    for (auto& t : threads_) t.join();
-  }
-
- private:
-  struct Job {
-    std::function<void(size_t, size_t)>* fn = nullptr;
-    size_t n = 0, grain = 1, chunks = 0;
-    std::atomic<size_t> next{0}, done{0};
-  };
-  HostPool() {
-    size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
-    if (const char* e = getenv("KUEUE_TAS_HOST_THREADS")) n = size_t(std::max(0, atoi(e)));
-    for (size_t i = 0; i < n; i++) threads_.emplace_back([this] { loop(); });
-  }
-  static void work(Job& j) {
-    for (;;) {
-      const size_t c = j.next.fetch_add(1, std::memory_order_relaxed);
-      if (c >= j.chunks) return;
-      const size_t b = c * j.grain;
-      (*j.fn)(b, std::min(j.n, b + j.grain));
-      j.done.fetch_add(1, std::memory_order_release);
-    }
-  }
-  void loop() {
-    uint64_t seen = epoch_.load();
-    for (;;) {
-      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(2000);
-      while (epoch_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < spin_until)
-        std::this_thread::yield();
-      std::shared_ptr<Job> job;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || epoch_.load() != seen; });
-        if (stop_) return;
-        seen = epoch_.load();
-        job = job_;
-      }
-      if (job) work(*job);
-    }
-  }
-  std::vector<std::thread> threads_;
-  std::mutex mu_, callMu_;
-  std::condition_variable cv_;
-  std::atomic<uint64_t> epoch_{0};
-  std::shared_ptr<Job> job_;
-  bool stop_ = false;
-};
 
 // A workload's assumedUsage overlay across its PodSet groups (addAssumedUsage
 // :658-666): records appended per assigned domain, sorted by (leaf, column)
@@ -2564,6 +2474,133 @@ struct Evaluator {
     }
   }
 
+  // build_pass for the first pass without a base overlay (the batch of
+  // every timed step), assembled by the pool's static parts: part t holds
+  // the workloads whose groups thread t compiled, so it reads them from its
+  // own cache.  Each part first lays out its share in local tables, then —
+  // once the parts' sizes give their offsets — writes it into the batch
+  // tables and rebases its records' offsets.  Same batch as build_pass
+  // (taint rows are deduplicated within a part only: equal rows compare
+  // equal by value wherever they are).
+  struct PartBatch {
+    std::vector<const kueue_tas_eval_req*> rq;
+    std::vector<std::pair<size_t, GroupEval*>> bt, early;
+    std::vector<int32_t> tt;
+    std::vector<std::pair<const std::vector<int32_t>*, int32_t>> rows;  // distinct rows of the part, local offsets
+    std::vector<kueue_tas_affinity_req> af;
+    std::vector<int32_t> afv;
+    size_t rqb = 0, ttb = 0, afb = 0, afvb = 0;
+  };
+  std::vector<PartBatch> partBatch;
+  void build_pass0_static(std::vector<Workload>& wls, const std::vector<char>& done,
+                          std::vector<const kueue_tas_eval_req*>& rq, std::vector<int32_t>& tt,
+                          std::vector<kueue_tas_assumed>& as, std::vector<kueue_tas_affinity_req>& af,
+                          std::vector<int32_t>& afv, std::vector<std::pair<size_t, GroupEval*>>& bt,
+                          std::vector<std::pair<size_t, GroupEval*>>& early) {
+    HostPool& pool = HostPool::get();
+    const size_t T = pool.parts(), W = wls.size();
+    partBatch.resize(T);
+    auto part_of = [&](size_t b) {
+      size_t t = 0;
+      while (t + 1 < T && HostPool::part_begin(W, t + 1, T) <= b) t++;
+      return t;
+    };
+    pool.run_static(W, [&](size_t b, size_t e) {
+      PartBatch& pb = partBatch[part_of(b)];
+      pb.rq.clear();
+      pb.bt.clear();
+      pb.early.clear();
+      pb.tt.clear();
+      pb.rows.clear();
+      pb.af.clear();
+      pb.afv.clear();
+      for (size_t w = b; w < e; w++) {
+        if (done[w] || wls[w].groups.empty()) continue;
+        GroupEval& g = wls[w].groups[0];
+        if (!g.early_reason.empty()) {
+          pb.early.emplace_back(w, &g);
+          continue;
+        }
+        kueue_tas_eval_req& q = g.req;
+        pb.rq.push_back(&q);
+        int32_t off = -1;
+        for (auto& r : pb.rows)  // a handful of distinct rows per batch
+          if (r.first == &g.taint_row || *r.first == g.taint_row) {
+            off = r.second;
+            break;
+          }
+        if (off < 0) {
+          off = int32_t(pb.tt.size());
+          pb.rows.emplace_back(&g.taint_row, off);
+          pb.tt.insert(pb.tt.end(), g.taint_row.begin(), g.taint_row.end());
+        }
+        q.taint_table = off;  // part-local offsets: rebased below
+        q.affinity_begin = int32_t(pb.af.size());
+        if (q.flags & KUEUE_TAS_F_AFFINITY) {
+          const int32_t vb = int32_t(pb.afv.size());
+          for (auto r : g.aff) {
+            r.begin += vb;
+            pb.af.push_back(r);
+          }
+          pb.afv.insert(pb.afv.end(), g.aff_vals.begin(), g.aff_vals.end());
+        }
+        q.affinity_end = int32_t(pb.af.size());
+        q.selector_begin = q.selector_end = int32_t(pb.af.size());
+        if (q.flags & KUEUE_TAS_F_SELECTOR_EXT) {
+          const int32_t vb = int32_t(pb.afv.size());
+          for (auto r : g.sel_ext) {
+            r.begin += vb;
+            pb.af.push_back(r);
+          }
+          pb.afv.insert(pb.afv.end(), g.sel_vals.begin(), g.sel_vals.end());
+          q.selector_end = int32_t(pb.af.size());
+        }
+        q.assumed_begin = q.assumed_end = 0;  // no assumed usage before the first pass
+        pb.bt.emplace_back(w, &g);
+      }
+    });
+    size_t nrq = 0, ntt = 0, naf = 0, nafv = 0;
+    early.clear();
+    for (auto& pb : partBatch) {
+      pb.rqb = nrq;
+      pb.ttb = ntt;
+      pb.afb = naf;
+      pb.afvb = nafv;
+      nrq += pb.rq.size();
+      ntt += pb.tt.size();
+      naf += pb.af.size();
+      nafv += pb.afv.size();
+      early.insert(early.end(), pb.early.begin(), pb.early.end());
+    }
+    rq.resize(nrq);
+    bt.resize(nrq);
+    tt.resize(ntt);
+    af.resize(naf);
+    afv.resize(nafv);
+    as.clear();
+    pool.run_static(W, [&](size_t b, size_t) {
+      PartBatch& pb = partBatch[part_of(b)];
+      const int32_t ttb = int32_t(pb.ttb), afb = int32_t(pb.afb), afvb = int32_t(pb.afvb);
+      for (size_t k = 0; k < pb.rq.size(); k++) {
+        kueue_tas_eval_req& q = pb.bt[k].second->req;
+        q.taint_table += ttb;
+        q.affinity_begin += afb;
+        q.affinity_end += afb;
+        q.selector_begin += afb;
+        q.selector_end += afb;
+        rq[pb.rqb + k] = pb.rq[k];
+        bt[pb.rqb + k] = pb.bt[k];
+      }
+      std::copy(pb.tt.begin(), pb.tt.end(), tt.begin() + int64_t(pb.ttb));
+      for (size_t k = 0; k < pb.af.size(); k++) {
+        kueue_tas_affinity_req r = pb.af[k];
+        r.begin += afvb;
+        af[pb.afb + k] = r;
+      }
+      std::copy(pb.afv.begin(), pb.afv.end(), afv.begin() + int64_t(pb.afvb));
+    });
+  }
+
   // ---- TASBalancedPlacement (tas_flavor_snapshot.go:906-917) ----
   // For the batch's balanced groups: their phase-1 counters from a second
   // device batch of just those requests (kueue_tas_last_counters), then the
@@ -2684,7 +2721,7 @@ struct Evaluator {
       // columns (rare: they reload the snapshot) are added serially between
       HostPool& pool = HostPool::get();
       std::atomic<bool> unknown{false};
-      pool.run(wls.size(), 64, [&](size_t b, size_t e) {
+      pool.run_static(wls.size(), [&](size_t b, size_t e) {
         bool u = false;
         for (size_t w = b; w < e; w++) {
           if (wls[w].groups.empty() || regroup) make_groups(wls[w]);
@@ -2700,7 +2737,7 @@ struct Evaluator {
       snap->compile_gen++;
       std::string perr;
       std::mutex perr_mu;
-      pool.run(wls.size(), 64, [&](size_t b, size_t e) {
+      pool.run_static(wls.size(), [&](size_t b, size_t e) {
         try {
           for (size_t w = b; w < e; w++)
             for (auto& g : wls[w].groups)
@@ -2743,9 +2780,12 @@ struct Evaluator {
         bt = &p0_batch;
         ea = &p0_early;
         assumed.clear();
+      } else if (pass == 0 && !base) {
+        build_pass0_static(wls, done, reqs, taint_table, assumed, aff, affv, batch, early);
+        p0_for = nullptr;  // the groups' records now hold this batch's table offsets
       } else {
         build_pass(wls, pass, done, assumedBy, reqs, taint_table, assumed, aff, affv, batch, early);
-        if (pass == 0) p0_for = nullptr;  // the groups' records now hold this batch's table offsets
+        if (pass == 0) p0_for = nullptr;
       }
       detail_ms[2] += now_ms() - t_bp;
       for (auto& we : *ea) {
@@ -2805,7 +2845,7 @@ struct Evaluator {
       snap->reason_order();
       (void)snap->topology_quoted();
       std::atomic<int64_t> leaders{0};
-      HostPool::get().run(n, 64, [&](size_t i0, size_t i1) {
+      HostPool::get().run_static(n, [&](size_t i0, size_t i1) {
       std::string reasonBuf;
       int64_t nlead = 0;
       for (size_t i = i0; i < i1; i++) {

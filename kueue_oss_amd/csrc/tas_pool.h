@@ -1,0 +1,154 @@
+// tas_pool.h — the persistent host worker pool shared by the host layer
+// (tas_host.cpp) and the device layer's per-batch host work (tas_device.hip).
+// One pool per process (HostPool::get is an inline function: one instance
+// across translation units).  Not part of the public ABI.
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <pthread.h>
+#include <thread>
+#include <vector>
+
+namespace ktas_pool {
+
+// Persistent host workers for per-batch loops that are independent per
+// workload.  Two modes:
+//  * run(n, grain, fn): chunks of `grain` items taken by whoever is free; the
+//    calling thread takes chunks too and only waits for chunks already taken,
+//    so a worker still asleep never delays a call;
+//  * run_static(n, fn): the same contiguous part [t*n/T, (t+1)*n/T) always
+//    goes to the same thread t (t = 0: the caller), so the phases of one
+//    batch that touch the same workloads (compile, batch assembly, device
+//    records, decode) find them in that core's cache instead of pulling them
+//    across cores.
+// Idle workers spin briefly for the next job (steps follow each other within
+// a millisecond), then sleep after 2 ms.  KUEUE_TAS_HOST_THREADS sets the
+// worker count (0: inline).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool pool;
+    return pool;
+  }
+  size_t workers() const { return threads_.size(); }
+  size_t parts() const { return threads_.size() + 1; }
+  // fn(begin, end) over [0, n) in chunks of `grain`; one job at a time
+  template <class F>
+  void run(size_t n, size_t grain, F&& fn) {
+    if (inline_only() || n <= grain) {
+      if (n) fn(size_t(0), n);
+      return;
+    }
+    std::function<void(size_t, size_t)> f(std::ref(fn));
+    submit(n, grain, &f, false);
+  }
+  // fn(begin, end) over the parts() static parts of [0, n)
+  template <class F>
+  void run_static(size_t n, F&& fn) {
+    if (inline_only() || n < 2 * parts()) {  // the same parts, one after the other
+      for (size_t t = 0; t < parts(); t++)
+        if (part_begin(n, t, parts()) < part_begin(n, t + 1, parts())) fn(part_begin(n, t, parts()), part_begin(n, t + 1, parts()));
+      return;
+    }
+    std::function<void(size_t, size_t)> f(std::ref(fn));
+    submit(n, 0, &f, true);
+  }
+  // the static part of [0, n) that thread t runs
+  static size_t part_begin(size_t n, size_t t, size_t T) { return n * t / T; }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      epoch_.fetch_add(1);
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+
+ private:
+  struct Job {
+    std::function<void(size_t, size_t)>* fn = nullptr;
+    size_t n = 0, grain = 1, chunks = 0;
+    bool fixed = false;  // run_static: chunk t is thread t's part
+    std::atomic<size_t> next{0}, done{0};
+  };
+  void submit(size_t n, size_t grain, std::function<void(size_t, size_t)>* f, bool fixed) {
+    std::lock_guard<std::mutex> one(callMu_);
+    auto job = std::make_shared<Job>();
+    job->fn = f;
+    job->n = n;
+    job->grain = grain;
+    job->fixed = fixed;
+    job->chunks = fixed ? parts() : (n + grain - 1) / grain;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = job;
+      epoch_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    work(*job, 0);
+    while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
+    std::lock_guard<std::mutex> lk(mu_);
+    job_.reset();  // late workers keep their reference; its chunks are exhausted
+  }
+  HostPool() {
+    size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
+    if (const char* e = getenv("KUEUE_TAS_HOST_THREADS")) n = size_t(std::max(0, atoi(e)));
+    // every worker starts from the epoch before any job: a static job posted
+    // before a worker first runs is still seen by it (it owns a part)
+    const uint64_t e0 = epoch_.load();
+    for (size_t i = 0; i < n; i++) threads_.emplace_back([this, i, e0] { loop(i + 1, e0); });
+    // a child forked without exec has none of the workers: it runs inline
+    pthread_atfork(nullptr, nullptr, [] { forked_child() = true; });
+  }
+  static bool& forked_child() {
+    static bool f = false;
+    return f;
+  }
+  bool inline_only() const { return threads_.empty() || forked_child(); }
+  void work(Job& j, size_t self) {
+    if (j.fixed) {  // this thread's own part only
+      const size_t T = j.chunks;
+      (*j.fn)(part_begin(j.n, self, T), part_begin(j.n, self + 1, T));
+      j.done.fetch_add(1, std::memory_order_release);
+      return;
+    }
+    for (;;) {
+      const size_t c = j.next.fetch_add(1, std::memory_order_relaxed);
+      if (c >= j.chunks) return;
+      const size_t b = c * j.grain;
+      (*j.fn)(b, std::min(j.n, b + j.grain));
+      j.done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void loop(size_t self, uint64_t seen) {
+    for (;;) {
+      const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(2000);
+      while (epoch_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < spin_until)
+        std::this_thread::yield();
+      std::shared_ptr<Job> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || epoch_.load() != seen; });
+        if (stop_) return;
+        seen = epoch_.load();
+        job = job_;
+      }
+      if (job) work(*job, self);
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_, callMu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> epoch_{0};
+  std::shared_ptr<Job> job_;
+  bool stop_ = false;
+};
+
+}  // namespace ktas_pool

@@ -68,7 +68,7 @@ EXPORTED_SYMBOLS = [
 
 # the Makefile's SRC_HASH inputs, in order
 _HASHED_SOURCES = ("tas_device.hip", "tas_host.cpp", "tas_internal.h", "tas_kernels.hip", "json_reader.h",
-                   "label_selectors.h", "tas_balanced.h", os.path.join("..", "..", "include", "kueue_tas.h"),
+                   "label_selectors.h", "tas_balanced.h", "tas_pool.h", os.path.join("..", "..", "include", "kueue_tas.h"),
                    os.path.join("..", "..", "include", "kueue_tas_debug.h"))
 
 

@@ -14,7 +14,7 @@ def pytest_configure(config):
 import pytest  # noqa: E402
 
 _EMU_SRCS = ("tas_kernels.hip", "tas_device.hip", "tas_host.cpp", "tas_internal.h", "json_reader.h",
-             "label_selectors.h", "tas_balanced.h")
+             "label_selectors.h", "tas_balanced.h", "tas_pool.h")
 
 
 @pytest.fixture(scope="session")

@@ -26,7 +26,8 @@ grep -q 'emu::wave_barrier(); own(g);' "$OUT/src/tas_kernels.hip" || { echo "loc
 grep -q '= v; emu::wave_barrier();' "$OUT/src/tas_kernels.hip" || { echo "lockstep patch failed"; exit 1; }
 grep -q '^  Wave sh_wave\[' "$OUT/src/tas_kernels.hip" || { echo "per-wave state patch failed"; exit 1; }
 grep -q '^  __shared__ \(Wave\|kueue_tas_eval_out\|int sh_ints\)' "$OUT/src/tas_kernels.hip" && { echo "per-wave state patch incomplete"; exit 1; }
-cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$CSRC/label_selectors.h" "$CSRC/tas_balanced.h" "$OUT/src/"
+cp "$CSRC/tas_internal.h" "$CSRC/json_reader.h" "$CSRC/label_selectors.h" "$CSRC/tas_balanced.h" \
+   "$CSRC/tas_pool.h" "$OUT/src/"
 sed "s#\"../../include/#\"#" "$CSRC/tas_internal.h" > "$OUT/src/tas_internal.h"
 cp "$ROOT/include/kueue_tas.h" "$ROOT/include/kueue_tas_debug.h" "$OUT/src/"
 cp "$CSRC/tas_device.hip" "$OUT/src/tas_device.cpp"
