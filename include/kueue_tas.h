@@ -309,6 +309,32 @@ int kueue_tas_fetch_entries(kueue_tas_ctx* ctx, int32_t* entries, size_t entries
  * Pass entries = NULL to kueue_tas_eval_batch to skip its copy. */
 const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
 
+/* Nodes joining the snapshot (nodesCache.sync tas_nodes_cache.go:38-50 ->
+ * addNode / initialize tas_flavor_snapshot.go:160-241) without a reload: the
+ * leaves keep their bytewise-lexicographic numbering, so the joined leaves
+ * move every later leaf; the device gathers its resident leaf columns into
+ * the new numbering and takes the joined leaves' rows from the caller.
+ *  topo:      the new tree (levels, CSR, DomainID ranks as in
+ *             kueue_tas_snapshot_load; its leaf arrays are ignored and may
+ *             be NULL); same num_cols, num_label_cols, lowest_is_hostname
+ *  leaf_src:  [N_new] the leaf's index before the splice, or -1 for a joined
+ *             leaf (whose row is the next of the new_* rows, in leaf order)
+ *  new_*:     the joined leaves' rows, [R][num_new] / [num_new] / [K][num_new]
+ * Leaves that had left (kueue_tas_snapshot_set_leaf_live) stay out; leaf tags
+ * are cleared; names must be loaded again before a v1beta2 encode. */
+typedef struct {
+  const kueue_tas_snapshot_desc* topo;
+  const int32_t* leaf_src;
+  int32_t num_new;
+  const int64_t* new_free_capacity;
+  const int64_t* new_tas_usage;
+  const uint32_t* new_free_present;
+  const uint32_t* new_usage_present;
+  const int32_t* new_taint_profile;  /* NULL when the snapshot has no taint profiles */
+  const int32_t* new_label_values;   /* NULL when K == 0 */
+} kueue_tas_splice_desc;
+int kueue_tas_snapshot_splice(kueue_tas_ctx* ctx, const kueue_tas_splice_desc* d);
+
 /* Per-leaf opaque 64-bit tags that the device copies next to every entry it
  * emits (select_kernel, lfc_emit_kernel).  The host layer passes, per leaf,
  * the address of the leaf's TopologyAssignment Values (its levelValues from

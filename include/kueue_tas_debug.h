@@ -45,7 +45,8 @@ int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
 
 /* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request
  * compile, [1] phase-1 classes, [2] uploads + launches, [3] wait for the
- * select results, [4] entry packing + D2H, [5] copy-out.  Copies min(n, 6). */
+ * select results, [4] entry packing + D2H, [5] copy-out; within [0]: [6] the
+ * validation pass, [7] the records + class-hash pass.  Copies min(n, 8). */
 int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
 
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
@@ -70,11 +71,15 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_UNIFORM_ROLLUP 4096u     /* staged fill rolls up uniform power-of-two leaf parents */
 #define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: two adjacent leaves per thread (kPairLP) */
 #define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
+#define KUEUE_TAS_PATH_RAGGED_PAIR 32768u       /* fill_pair_kernel on ragged leaf parents (128-leaf slots, segmented scans) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 /* Stage events: on (default), every stage of kueue_tas_last_stage_times is
  * timed; off, only the fill bracket is (the other events are pure
  * instrumentation; the ones that order the streams are always recorded). */
 int kueue_tas_set_stage_timing(kueue_tas_ctx* ctx, int32_t on);
+/* Lifetime counts of successful kueue_tas_snapshot_load and
+ * kueue_tas_snapshot_splice calls on ctx (tests pin which one an event took). */
+int kueue_tas_snapshot_counters(kueue_tas_ctx* ctx, int64_t* loads, int64_t* splices);
 
 /* ---- host layer ---------------------------------------------------------- */
 /* Device stage times of the last run (summed over its batches, ms):

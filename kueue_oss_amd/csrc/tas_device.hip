@@ -48,6 +48,10 @@ struct DevBuf {
     p = nullptr;
     n = 0;
   }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+  }
 };
 
 template <typename T>
@@ -157,6 +161,7 @@ struct kueue_tas_ctx {
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
   bool labels16 = false;      // every staged label column's value ids < 2^16 (packed nodeSelector compare)
+  int64_t n_loads = 0, n_splices = 0;  // kueue_tas_snapshot_load / _splice calls that succeeded (lifetime)
   bool stage_timing = true;   // record every stage event (else only the fill bracket; kueue_tas_set_stage_timing)
   int max_batch = 1024;
   int entry_cap = 512;  // per-eval device entry capacity (grows on demand)
@@ -204,6 +209,7 @@ struct kueue_tas_ctx {
   std::vector<int32_t> sig_base, base_rep, cls_packed, sig_ncls;
   FlatMap cls_head, sig_head;
   DevBuf<int32_t> d_overlay, d_tags;
+  DevBuf<int2> d_wave_tab2;     // 128-leaf slots of whole ragged parents (fill_pair_kernel, FC = -1)
   DevBuf<uint64_t> d_rack_pos;  // positive-child masks of the leaves' parents (fused fill)  // select's copy-on-write counters and ownership tags
   int32_t tag_epoch = 0;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
@@ -235,7 +241,8 @@ struct kueue_tas_ctx {
   std::vector<int64_t> ent_strided_off;  // their region offsets (pairs) in ent_host
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
-  double host_ms[6] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out
+  double host_ms[8] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out, [6] of compile:
+                           // validation pass, [7] of compile: records + hashes pass
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
   uint32_t fill_paths = 0;               // KUEUE_TAS_PATH_* bits of the last kueue_tas_eval_batch
   // phase-1 counters of the last device chunk (kueue_tas_last_counters):
@@ -395,7 +402,33 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
 
 const char* kueue_tas_last_error(kueue_tas_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
 
-int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) {
+static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const kueue_tas_splice_desc* sp);
+
+int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) { return load_impl(c, d, nullptr); }
+
+int kueue_tas_snapshot_splice(kueue_tas_ctx* c, const kueue_tas_splice_desc* sp) {
+  if (!c || !sp || !sp->topo || !sp->leaf_src) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  const kueue_tas_snapshot_desc* d = sp->topo;
+  if (d->num_levels != c->snap.L || d->num_cols != c->snap.R || d->num_label_cols != c->snap.K ||
+      d->lowest_is_hostname != c->snap.lowest_is_hostname)
+    return fail(c, KUEUE_TAS_EINVAL, "splice: the tree's levels, columns and label columns stay");
+  if (d->num_levels < 1 || d->num_levels > KUEUE_TAS_MAX_LEVELS) return fail(c, KUEUE_TAS_EINVAL, "num_levels");
+  const int n_new = d->level_sizes[d->num_levels - 1];
+  int fresh = 0;
+  for (int j = 0; j < n_new; j++) {
+    const int32_t x = sp->leaf_src[j];
+    if (x >= c->snap.N || x < -1) return fail(c, KUEUE_TAS_EINVAL, "splice: leaf source out of range");
+    fresh += x < 0 ? 1 : 0;
+  }
+  if (fresh != sp->num_new) return fail(c, KUEUE_TAS_EINVAL, "splice: num_new is not the count of joined leaves");
+  if (sp->num_new > 0 && (!sp->new_free_capacity || !sp->new_tas_usage || !sp->new_free_present ||
+                          !sp->new_usage_present || (c->snap.K > 0 && !sp->new_label_values)))
+    return fail(c, KUEUE_TAS_EINVAL, "splice: joined rows missing");
+  return load_impl(c, d, sp);
+}
+
+static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const kueue_tas_splice_desc* sp) {
   if (!c || !d) return KUEUE_TAS_EINVAL;
   if (d->num_levels < 1 || d->num_levels > KUEUE_TAS_MAX_LEVELS) return fail(c, KUEUE_TAS_EINVAL, "num_levels");
   if (d->num_cols < 0 || d->num_cols > KUEUE_TAS_MAX_COLS) return fail(c, KUEUE_TAS_EINVAL, "num_cols");
@@ -424,8 +457,25 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   s.ent_base = nullptr;
   c->leaf_tags_on = false;
   s.n_live = s.N;
+  // a splice keeps the leaves that had left out: their flags move with them
+  std::vector<uint8_t> old_dead;
+  const int old_N = c->snap.N;
+  if (sp) old_dead.swap(c->h_dead);
   c->h_dead.assign(N, 0);
   c->n_dead = 0;
+  std::vector<int32_t> gsrc;
+  if (sp) {
+    gsrc.resize(N);
+    int32_t k = 0;
+    for (size_t j = 0; j < N; j++) {
+      const int32_t x = sp->leaf_src[j];
+      gsrc[j] = x >= 0 ? x : -(++k);
+      if (x >= 0 && size_t(x) < old_dead.size() && old_dead[size_t(x)]) {
+        c->h_dead[j] = 1;
+        c->n_dead++;
+      }
+    }
+  }
   // CSR offsets
   size_t nco = 0;
   for (int l = 0; l + 1 < s.L; l++) {
@@ -435,6 +485,83 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   HIPCHK(c, c->d_child_off.ensure(nco));
   if (nco) HIPCHK(c, hipMemcpyAsync(c->d_child_off.p, d->child_offsets, nco * 4, hipMemcpyHostToDevice, c->stream));
   s.child_off = c->d_child_off.p;
+  if (sp) {  // the resident leaf columns gathered into the new numbering, the joined rows from the caller
+    const int nn = std::max(sp->num_new, 1);
+    const bool prof = c->snap.taint_profile != nullptr;
+    const bool lab = s.K > 0 && c->snap.label_values != nullptr;
+    DevBuf<int64_t> f, u;
+    DevBuf<uint32_t> fp, up;
+    DevBuf<int32_t> pr, lb, src;
+    DevBuf<uint8_t> rows;
+    HIPCHK(c, f.ensure(size_t(s.R) * N));
+    HIPCHK(c, u.ensure(size_t(s.R) * N));
+    HIPCHK(c, fp.ensure(N));
+    HIPCHK(c, up.ensure(N));
+    if (prof) HIPCHK(c, pr.ensure(N));
+    if (lab) HIPCHK(c, lb.ensure(size_t(s.K) * N));
+    HIPCHK(c, src.ensure(N));
+    // the joined rows: free | usage | free_present | usage_present | profile | labels
+    const size_t o_u = size_t(s.R) * nn * 8, o_fp = 2 * o_u, o_up = o_fp + size_t(nn) * 4, o_pr = o_up + size_t(nn) * 4,
+                 o_lb = o_pr + size_t(nn) * 4, rbytes = o_lb + size_t(std::max(s.K, 1)) * nn * 4;
+    HIPCHK(c, rows.ensure(rbytes));
+    HIPCHK(c, hipMemcpyAsync(src.p, gsrc.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+    if (sp->num_new > 0) {
+      const size_t k = size_t(sp->num_new);
+      if (s.R) {
+        HIPCHK(c, hipMemcpyAsync(rows.p, sp->new_free_capacity, size_t(s.R) * k * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(rows.p + o_u, sp->new_tas_usage, size_t(s.R) * k * 8, hipMemcpyHostToDevice, c->stream));
+      }
+      HIPCHK(c, hipMemcpyAsync(rows.p + o_fp, sp->new_free_present, k * 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(rows.p + o_up, sp->new_usage_present, k * 4, hipMemcpyHostToDevice, c->stream));
+      if (prof && sp->new_taint_profile)
+        HIPCHK(c, hipMemcpyAsync(rows.p + o_pr, sp->new_taint_profile, k * 4, hipMemcpyHostToDevice, c->stream));
+      if (lab) HIPCHK(c, hipMemcpyAsync(rows.p + o_lb, sp->new_label_values, size_t(s.K) * k * 4, hipMemcpyHostToDevice, c->stream));
+      for (size_t i = 0; i < k; i++) {
+        if (sp->new_taint_profile) c->num_profiles = std::max(c->num_profiles, sp->new_taint_profile[i] + 1);
+        for (int q = 0; q < std::min(s.K, kStagedLabels) && sp->new_label_values; q++)
+          if (uint32_t(sp->new_label_values[size_t(q) * k + i]) > 0xffffu) c->labels16 = false;
+      }
+    }
+    if (N) {
+      hipLaunchKernelGGL(splice_leaves_kernel, dim3(unsigned((N + 255) / 256)), dim3(256), 0, c->stream, src.p, int(N),
+                         old_N, s.R, lab ? s.K : 0, nn, c->d_free.p, c->d_usage.p, c->d_free_present.p,
+                         c->d_usage_present.p, prof ? c->d_taint_profile.p : nullptr, lab ? c->d_labels.p : nullptr,
+                         reinterpret_cast<const int64_t*>(rows.p), reinterpret_cast<const int64_t*>(rows.p + o_u),
+                         reinterpret_cast<const uint32_t*>(rows.p + o_fp), reinterpret_cast<const uint32_t*>(rows.p + o_up),
+                         (prof && sp->new_taint_profile) ? reinterpret_cast<const int32_t*>(rows.p + o_pr) : nullptr,
+                         reinterpret_cast<const int32_t*>(rows.p + o_lb), f.p, u.p, fp.p, up.p, prof ? pr.p : nullptr,
+                         lab ? lb.p : nullptr);
+      HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->d_free.swap(f);
+    c->d_usage.swap(u);
+    c->d_free_present.swap(fp);
+    c->d_usage_present.swap(up);
+    if (prof) c->d_taint_profile.swap(pr);
+    if (lab) c->d_labels.swap(lb);
+    // f, u, ... now hold the old columns and are freed here
+    s.free_cap = c->d_free.p;
+    s.tas_usage = c->d_usage.p;
+    s.free_present = c->d_free_present.p;
+    s.usage_present = c->d_usage_present.p;
+    s.taint_profile = prof ? c->d_taint_profile.p : nullptr;
+    s.label_values = lab ? c->d_labels.p : nullptr;
+    if (c->n_dead > 0) {  // the leaves that had left, at their new indices
+      HIPCHK(c, c->d_dead.ensure(N));
+      HIPCHK(c, hipMemcpy(c->d_dead.p, c->h_dead.data(), N, hipMemcpyHostToDevice));
+      s.leaf_dead = c->d_dead.p;
+      s.n_live = int32_t(int64_t(N) - c->n_dead);
+    }
+    f.release();
+    u.release();
+    fp.release();
+    up.release();
+    pr.release();
+    lb.release();
+    src.release();
+    rows.release();
+  } else {
   HIPCHK(c, c->d_free.ensure(size_t(s.R) * N));
   HIPCHK(c, c->d_usage.ensure(size_t(s.R) * N));
   if (s.R && N) {
@@ -468,6 +595,7 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
     HIPCHK(c, hipMemcpyAsync(c->d_labels.p, d->label_values, size_t(s.K) * N * 4, hipMemcpyHostToDevice, c->stream));
     s.label_values = c->d_labels.p;
   }
+  }
   s.id_rank = nullptr;
   if (d->domain_id_rank && off) {  // re-laid out on the padded level offsets
     std::vector<int32_t> ranks(size_t(off), 0);
@@ -496,6 +624,45 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   s.wave_tab = nullptr;
   s.n_wave_slots = 0;
   s.leaf_parent = nullptr;
+  s.wave_tab2 = nullptr;
+  s.n_wave_slots2 = 0;
+  s.ragged_max_fan = 0;
+  // and the same packing into 128-leaf slots for fill_pair_kernel's two
+  // leaves per lane (parents of at most 128 leaves)
+  if (c->rack_fanout == 0 && s.L >= 2 && d->level_sizes[s.L - 2] > 0 && d->child_offsets && s.N > 0) {
+    const int P = d->level_sizes[s.L - 2];
+    const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
+    bool ok = co[0] == 0 && co[P] == s.N;
+    std::vector<int2> tab;
+    std::vector<int32_t> lp(N, 0);
+    int cb = 0, cn = 0, fmax = 0;
+    for (int p = 0; p < P && ok; p++) {
+      const int f = co[p + 1] - co[p];
+      if (f < 1 || f > 2 * kWave) {
+        ok = false;
+        break;
+      }
+      fmax = std::max(fmax, f);
+      if (cn + f > 2 * kWave) {
+        tab.push_back(make_int2(cb, cn));
+        cb = co[p];
+        cn = 0;
+      }
+      cn += f;
+      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
+    }
+    if (ok) {
+      tab.push_back(make_int2(cb, cn));
+      HIPCHK(c, c->d_wave_tab2.ensure(tab.size()));
+      HIPCHK(c, hipMemcpy(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+      HIPCHK(c, c->d_leaf_parent.ensure(N));
+      HIPCHK(c, hipMemcpy(c->d_leaf_parent.p, lp.data(), N * 4, hipMemcpyHostToDevice));
+      s.wave_tab2 = c->d_wave_tab2.p;
+      s.n_wave_slots2 = int32_t(tab.size());
+      s.leaf_parent = c->d_leaf_parent.p;
+      s.ragged_max_fan = fmax;
+    }
+  }
   if (c->rack_fanout == 0 && s.L >= 2 && d->level_sizes[s.L - 2] > 0 && d->child_offsets && s.N > 0) {
     const int P = d->level_sizes[s.L - 2];
     const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
@@ -545,6 +712,14 @@ int kueue_tas_snapshot_load(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d) 
   c->snap = s;
   c->maxD = maxD;
   c->loaded = true;
+  (sp ? c->n_splices : c->n_loads)++;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_counters(kueue_tas_ctx* c, int64_t* loads, int64_t* splices) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (loads) *loads = c->n_loads;
+  if (splices) *splices = c->n_splices;
   return KUEUE_TAS_OK;
 }
 
@@ -1008,6 +1183,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   });
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
+  c->host_ms[6] += wall_ms() - tm;
   for (size_t i = 0; i < n; i++) toff[i + 1] += toff[i];
   const size_t nterms = size_t(toff[n]);
   int maxt = 1;
@@ -1170,6 +1346,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     pc.next.clear();
   }
   // ---- compile requests to device form (magic numbers) ----
+  const double t_b = wall_ms();
   pool.run_static(n, [&](size_t i0, size_t i1) {
     const size_t ch = part_of(i0);
     for (size_t i = i0; i < i1; i++) {
@@ -1257,6 +1434,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   });
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
+  c->host_ms[7] += wall_ms() - t_b;
   if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
   if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
   if (num_aff) memcpy(hs + o_aff, aff, num_aff * sizeof(kueue_tas_affinity_req));
@@ -1758,12 +1936,15 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     // single-run chunks on fill_pair_kernel (kPairLP leaves per thread): staged
     // columns, uniform fan-out >= 2 or no fused parents; it counts the
     // ExclusionStats itself, so the batch takes the inline-stats path
-    // experiment: ragged parents on the pair kernel without the fused roll-up
-    static const bool ragged_pair_exp = getenv("KTAS_RAGGED_PAIR") != nullptr;
-    const bool ragged_unfused = ragged_pair_exp && c->rack_fanout < 0;
+    // ragged leaf parents of <= 128 leaves on fill_pair_kernel (two leaves per
+    // lane, segmented scans over the lanes' pairs): every class without a
+    // leader (leader classes keep the one-leaf staged kernel)
+    bool any_leader = false;
+    for (size_t i = 0; i < n && !any_leader; i++) any_leader = (hev[i].flags & KUEUE_TAS_F_LEADER) != 0;
+    const bool ragged_pair = c->pair_fill && staged_fill && s.wave_tab2 != nullptr && !any_leader;
     const bool pair = c->pair_fill && staged_fill &&
-                      (c->rack_fanout == 0 || c->rack_fanout >= kPairLP || ragged_unfused);
-    const unsigned pgx = unsigned((s.N + kPairTile - 1) / kPairTile);
+                      (ragged_pair || (c->rack_fanout >= 0 && (c->rack_fanout == 0 || c->rack_fanout >= kPairLP)));
+    const unsigned pgx = ragged_pair ? unsigned((s.n_wave_slots2 + 3) / 4) : unsigned((s.N + kPairTile - 1) / kPairTile);
     if (b.nstat) {
       // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * std::max(grid.x, nblk_fill) * size_t(nstat)));
@@ -1779,11 +1960,15 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
     // partial slots per fill position: the exclusion grid (split), else the widest fill grid
     b.nstat_blocks = int32_t(b.stats_split ? grid.x : pair ? pgx : nblk_fill);
-    b.rack_fanout = ucols <= 8 && !ragged_unfused ? c->rack_fanout : 0;  // staged kernels fuse the first roll-up level
+    b.rack_fanout = ragged_pair ? -1 : ucols <= 8 ? c->rack_fanout : 0;  // the fill fuses the first roll-up level
     if (b.rack_fanout) {
       c->fill_paths |= b.rack_fanout < 0 ? KUEUE_TAS_PATH_RAGGED_ROLLUP : KUEUE_TAS_PATH_UNIFORM_ROLLUP;
-      HIPCHK(c, c->d_rack_pos.ensure(size_t(nfill) * size_t(s.level_size[s.L - 2])));
-      b.rack_pos = c->d_rack_pos.p;
+      if (ragged_pair) c->fill_paths |= KUEUE_TAS_PATH_RAGGED_PAIR;
+      // positive-children masks are 64-bit: none when a ragged parent is wider
+      if (!ragged_pair || s.ragged_max_fan <= kWave) {
+        HIPCHK(c, c->d_rack_pos.ensure(size_t(nfill) * size_t(s.level_size[s.L - 2])));
+        b.rack_pos = c->d_rack_pos.p;
+      }
     }
     const bool ts = b.num_profiles <= kStagedProfiles;
     // global lookups in the eval loop: a nodeSelector column beyond the
@@ -1801,7 +1986,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       if (pair) {  // kPairLP leaves per thread
         c->fill_paths |= KUEUE_TAS_PATH_PAIR;
         const dim3 pg(pgx, unsigned(count));
-        if (gl && b.rack_fanout == 32)
+        if (ragged_pair && gl)
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, -1>), pg, dim3(256), 0, st, s, b, umask, first);
+        else if (ragged_pair)
+          hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, false, -1>), pg, dim3(256), 0, st, s, b, umask, first);
+        else if (gl && b.rack_fanout == 32)
           hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, 32>), pg, dim3(256), 0, st, s, b, umask, first);
         else if (gl)
           hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, 0>), pg, dim3(256), 0, st, s, b, umask, first);
@@ -2207,9 +2396,9 @@ int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   return KUEUE_TAS_OK;
 }
 
-int kueue_tas_last_host_times(kueue_tas_ctx* c, double* ms, int n) {
+int kueue_tas_last_host_times(kueue_tas_ctx* c, double* ms, int n) {  // copies min(n, 8)
   if (!c || !ms || n < 0) return KUEUE_TAS_EINVAL;
-  for (int k = 0; k < n && k < 6; k++) ms[k] = c->host_ms[k];
+  for (int k = 0; k < n && k < 8; k++) ms[k] = c->host_ms[k];
   return KUEUE_TAS_OK;
 }
 

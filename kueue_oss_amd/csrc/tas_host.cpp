@@ -1349,11 +1349,111 @@ class FlavorSnapshot {
       *set = std::move(moved);
     }
     touched->insert(fr.begin(), fr.end());
+    // the device follows by a splice (its leaf columns gathered into the new
+    // numbering, the joined rows uploaded) unless a reload is due anyway
+    if (!dirty && ctx) {
+      if (!splicePending) {
+        spliceSrc.resize(N0);
+        for (size_t i = 0; i < N0; i++) spliceSrc[i] = int32_t(i);
+      }
+      std::vector<int32_t> src(N, -1);
+      for (size_t i = 0; i < N0; i++) src[size_t(rm[i])] = spliceSrc[i];
+      spliceSrc = std::move(src);
+      splicePending = true;
+    } else {
+      dirty = true;
+    }
     joins.clear();
     joinIds.clear();
     new_layout();
-    dirty = true;
     spliced = true;
+  }
+  // kueue_tas_snapshot_splice of the pending joins: the tree and the joined
+  // leaves' rows from the host mirror; every other leaf's row stays on the device
+  bool splicePending = false;
+  std::vector<int32_t> spliceSrc;  // per current leaf: its index on the device, -1 joined since
+  bool namesStale = false;         // domain names to reload before a v1beta2 encode
+  int upload_splice() {
+    splicePending = false;
+    const int L = this->L(), N = this->N(), R = int(cols.size());
+    std::vector<int32_t> sizes(L), co, ranks;
+    for (int l = 0; l < L; l++) sizes[l] = int32_t(values[l].size());
+    for (int l = 0; l + 1 < L; l++) co.insert(co.end(), childOff[l].begin(), childOff[l].end());
+    for (int l = 0; l < L; l++) ranks.insert(ranks.end(), idRank[l].begin(), idRank[l].end());
+    std::vector<int32_t> fresh;
+    for (int j = 0; j < N; j++)
+      if (spliceSrc[size_t(j)] < 0) fresh.push_back(j);
+    const size_t k = fresh.size(), K = labelKeys.size();
+    std::vector<int64_t> fr(size_t(R) * k, 0), us(size_t(R) * k, 0);
+    std::vector<uint32_t> fp(k, 0), up(k, 0);
+    std::vector<int32_t> prof(k, 0), lab(K * k, 0);
+    for (size_t q = 0; q < k; q++) {
+      const size_t j = size_t(fresh[q]);
+      for (auto& kv : freeCap[j]) {
+        const auto c = colByName.find(kv.first);
+        if (c == colByName.end()) continue;
+        fr[size_t(c->second) * k + q] = kv.second;
+        fp[q] |= 1u << c->second;
+      }
+      for (auto& kv : tasUsage[j]) {
+        const auto c = colByName.find(kv.first);
+        if (c == colByName.end()) continue;
+        us[size_t(c->second) * k + q] = kv.second;
+        up[q] |= 1u << c->second;
+      }
+      prof[q] = leafProfile[j];
+      for (size_t c = 0; c < K; c++) lab[c * k + q] = labelValues[c * size_t(N) + j];
+    }
+    kueue_tas_snapshot_desc d{};
+    d.num_levels = L;
+    d.level_sizes = sizes.data();
+    d.child_offsets = co.data();
+    d.num_cols = R;
+    d.lowest_is_hostname = lowestIsHostname ? 1 : 0;
+    d.num_label_cols = int32_t(K);
+    d.domain_id_rank = ranks.data();
+    kueue_tas_splice_desc sd{};
+    sd.topo = &d;
+    sd.leaf_src = spliceSrc.data();
+    sd.num_new = int32_t(k);
+    sd.new_free_capacity = fr.data();
+    sd.new_tas_usage = us.data();
+    sd.new_free_present = fp.data();
+    sd.new_usage_present = up.data();
+    sd.new_taint_profile = lowestIsHostname ? prof.data() : nullptr;
+    sd.new_label_values = K ? lab.data() : nullptr;
+    int rc = kueue_tas_snapshot_splice(ctx, &sd);
+    spliceSrc.clear();
+    if (rc) {
+      err = std::string("snapshot splice: ") + kueue_tas_last_error(ctx);
+      return rc;
+    }
+    namesStale = true;
+    return set_tags();
+  }
+  int set_tags() {  // entry tags: each leaf's Values address (Values come back with the entries)
+    if (cfg.flags & KUEUE_TAS_CFG_HOST_VALUES) return 0;
+    const int L = this->L(), N = this->N();
+    const int32_t lvl = lowestIsHostname ? L - 1 : 0;
+    const std::string* const* lv = leaf_values();
+    std::vector<uint64_t> tags(size_t(N), 0);
+    for (int i = 0; i < N; i++) tags[size_t(i)] = uint64_t(reinterpret_cast<uintptr_t>(lv[i] + lvl));
+    const int rc = kueue_tas_snapshot_set_leaf_tags(ctx, tags.data(), tags.size());
+    if (rc) err = std::string("leaf tags: ") + kueue_tas_last_error(ctx);
+    return rc;
+  }
+  int load_names() {  // own label value of every domain, for the v1beta2 encoder's leaf mode
+    std::string names;
+    std::vector<int64_t> name_off(1, 0);
+    for (int l = 0; l < L(); l++)
+      for (auto& v : values[size_t(l)]) {
+        names += v.back();
+        name_off.push_back(int64_t(names.size()));
+      }
+    const int rc = kueue_tas_snapshot_load_names(ctx, names.data(), names.size(), name_off.data());
+    if (rc) err = std::string("snapshot names: ") + kueue_tas_last_error(ctx);
+    namesStale = rc != 0;
+    return rc;
   }
   int push_liveness(const std::set<int32_t>& leaves) {
     if (dirty || !ctx || leaves.empty()) return 0;  // a reload applies leafDead itself
@@ -1476,7 +1576,9 @@ class FlavorSnapshot {
   }
 
   int upload() {
-    if (!dirty) return 0;
+    if (!dirty) return splicePending && ctx ? upload_splice() : 0;
+    splicePending = false;
+    spliceSrc.clear();
     flush_mirror();
     if (!ctx) {
       ctx = kueue_tas_ctx_create(&cfg);
@@ -1529,30 +1631,8 @@ class FlavorSnapshot {
       err = std::string("snapshot load: ") + kueue_tas_last_error(ctx);
       return rc;
     }
-    // own label value of every domain, for the v1beta2 encoder's leaf mode
-    std::string names;
-    std::vector<int64_t> name_off(1, 0);
-    for (int l = 0; l < L; l++)
-      for (auto& v : values[l]) {
-        names += v.back();
-        name_off.push_back(int64_t(names.size()));
-      }
-    rc = kueue_tas_snapshot_load_names(ctx, names.data(), names.size(), name_off.data());
-    if (rc) {
-      err = std::string("snapshot names: ") + kueue_tas_last_error(ctx);
-      return rc;
-    }
-    if (!(cfg.flags & KUEUE_TAS_CFG_HOST_VALUES)) {  // entry tags: each leaf's Values address (Values come back with the entries)
-      const int32_t lvl = lowestIsHostname ? L - 1 : 0;
-      const std::string* const* lv = leaf_values();
-      std::vector<uint64_t> tags(size_t(N), 0);
-      for (int i = 0; i < N; i++) tags[size_t(i)] = uint64_t(reinterpret_cast<uintptr_t>(lv[i] + lvl));
-      rc = kueue_tas_snapshot_set_leaf_tags(ctx, tags.data(), tags.size());
-      if (rc) {
-        err = std::string("leaf tags: ") + kueue_tas_last_error(ctx);
-        return rc;
-      }
-    }
+    if ((rc = load_names())) return rc;
+    if ((rc = set_tags())) return rc;
     {  // a load puts every leaf in: take the dead ones out again
       std::vector<int32_t> dl, live;
       for (int i = 0; i < N; i++)
@@ -2349,7 +2429,7 @@ struct Evaluator {
   FlavorSnapshot* snap;
   float ms[4] = {0, 0, 0, 0};
   float stage_ms[KUEUE_TAS_NUM_STAGES] = {};
-  double dev_host_ms[6] = {};
+  double dev_host_ms[8] = {};
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   double detail_ms[4] = {0, 0, 0, 0};  // grouping + column check, request compile, build_pass, Values
   int64_t counts[3] = {0, 0, 0};
@@ -2829,9 +2909,9 @@ struct Evaluator {
       float st[KUEUE_TAS_NUM_STAGES];
       kueue_tas_last_stage_times(snap->ctx, st, KUEUE_TAS_NUM_STAGES);
       for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
-      double ht[6];
-      kueue_tas_last_host_times(snap->ctx, ht, 6);
-      for (int k = 0; k < 6; k++) dev_host_ms[k] += ht[k];
+      double ht[8];
+      kueue_tas_last_host_times(snap->ctx, ht, 8);
+      for (int k = 0; k < 8; k++) dev_host_ms[k] += ht[k];
       int64_t st4[4];
       kueue_tas_last_stats(snap->ctx, st4);
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
@@ -3017,6 +3097,8 @@ static int encode_results(FlavorSnapshot& s, const std::vector<const PodSetResul
   std::vector<kueue_tas_level_enc> enc(which.size() * size_t(nl));
   std::vector<int32_t> same(which.size());
   if (!which.empty()) {
+    if (s.namesStale)
+      if (int rc = s.load_names()) return rc;
     int rc = kueue_tas_encode_v1beta2_leaves(s.ctx, pairs.data(), off.data(), which.size(), first, enc.data(),
                                              same.data());
     if (rc) {
@@ -3248,6 +3330,7 @@ struct kueue_tas_host {
   std::vector<std::array<int32_t, 3>> admit_doms;
   std::vector<kueue_tas_fits_req> admit_fr;
   std::vector<kueue_tas_fits_term> admit_terms;
+  std::vector<std::pair<int32_t, int32_t>> admit_ps_terms;  // per PodSet of the workload: (term_begin, num_terms)
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
   float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
   int64_t accum_runs = 0, accum_fills = 0;
@@ -3972,6 +4055,12 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
     } else {
       h->snap->flush_joins(&touched, &liveChanged);
     }
+    int rc0 = 0;
+    if (!structural && h->snap->splicePending) rc0 = h->snap->upload();  // the pushes below use the new numbering
+    if (rc0) {
+      h->err = h->snap->err;
+      return rc0;
+    }
     if (rebuilt) *rebuilt = structural ? 1 : 0;
     int rc;
     if (structural) {  // the events applied so far are in the cache state; the rest replay on it
@@ -4280,7 +4369,7 @@ int kueue_tas_host_run_compiled(kueue_tas_host* h, uint64_t* result_hash) { retu
 
 int kueue_tas_host_last_device_host_times(kueue_tas_host* h, double* ms, int n) {
   if (!h || !h->ev || !ms || n < 0) return KUEUE_TAS_EINVAL;
-  for (int k = 0; k < n && k < 6; k++) ms[k] = h->ev->dev_host_ms[k];
+  for (int k = 0; k < n && k < 8; k++) ms[k] = h->ev->dev_host_ms[k];
   return 0;
 }
 
@@ -4477,17 +4566,22 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       ids.push_back(int32_t(g));
       if (seen[g] == 1) {
         const Workload& wl = h->compiled[g];
+        // the PodSet's single-pod request terms once per workload, shared by its domains' records
+        std::vector<std::pair<int32_t, int32_t>>& psTerms = h->admit_ps_terms;
+        psTerms.assign(wl.podsets.size(), {-1, 0});
         for (int64_t k = start[g]; k < start[g + 1]; k++) {
           const auto& d = doms[size_t(k)];
-          const TASPodSetRequests& ps = wl.podsets[size_t(d[0])];
-          kueue_tas_fits_req r{d[1], d[2], int32_t(terms.size()), 0};
-          for (auto& t : ps.requestIds) {
-            const int32_t c = s.col_of(t.first);
-            if (c < 0) throw std::runtime_error("admit: request resource without a column");
-            terms.push_back({t.second, c, 0});
-            r.num_terms++;
+          auto& pt = psTerms[size_t(d[0])];
+          if (pt.first < 0) {
+            pt.first = int32_t(terms.size());
+            for (auto& t : wl.podsets[size_t(d[0])].requestIds) {
+              const int32_t c = s.col_of(t.first);
+              if (c < 0) throw std::runtime_error("admit: request resource without a column");
+              terms.push_back({t.second, c, 0});
+              pt.second++;
+            }
           }
-          fr.push_back(r);
+          fr.push_back({d[1], d[2], pt.first, pt.second});
         }
       } else {  // a failed evaluation is never admitted: one record that cannot fit
         fr.push_back({-1, 0, int32_t(terms.size()), 0});

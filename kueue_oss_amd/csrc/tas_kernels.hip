@@ -1195,7 +1195,8 @@ struct OpOr {
 // MR: chunks of several signature runs (CountIn again at each run's first
 // position, the leaves' remaining capacity kept in registers), as the
 // staged kernel's MR.
-template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none)
+template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none),
+                                                      // -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
 __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
   __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records
@@ -1215,7 +1216,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // then the chunk's records: both sets of loads in flight together
   const int lane = lane_id();
   const int N = s.N;
-  const int leaf0 = tile * kPairTile + kPairLP * int(threadIdx.x);
+  int leaf0 = tile * kPairTile + kPairLP * int(threadIdx.x);
+  int slot_len = N - tile * kPairTile;  // leaves of this lane's window from the window's first
+  if constexpr (FC < 0) {  // this wave's 128-leaf slot of whole parents
+    const int slot = tile * 4 + int(threadIdx.x >> 6);
+    const int2 wt = slot < s.n_wave_slots2 ? s.wave_tab2[slot] : make_int2(0, 0);
+    leaf0 = wt.x + kPairLP * lane;
+    slot_len = wt.y;
+  }
   const int gleaf0 = s.level_off[s.L - 1] + leaf0;
   bool valid[kPairLP];
   int scol[NS];
@@ -1226,7 +1234,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
 #pragma unroll
   for (int j = 0; j < kPairLP; j++) {
     const int leaf = leaf0 + j;
-    valid[j] = leaf < N;
+    if constexpr (FC < 0) valid[j] = kPairLP * lane + j < slot_len;
+    else valid[j] = leaf < N;
     fp[j] = valid[j] ? s.free_present[leaf] : 0u;
     up[j] = valid[j] ? s.usage_present[leaf] : 0u;
     prof[j] = (valid[j] && s.taint_profile) ? s.taint_profile[leaf] : 0;
@@ -1334,14 +1343,37 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
   };
   if constexpr (!MR) count_run(0);
-  const int rack_f = FC > 0 ? FC : b.rack_fanout;  // fan-out of the fused parents (0: none)
+  // ragged slots: the parents of the lane's two leaves, which of them start
+  // (head) or end (tail) a parent, and the lane holding the start of its
+  // second leaf's parent (the segmented scans' bound)
+  int rp[kPairLP] = {}, seg0 = 0, st0 = 0, st1 = 0;
+  bool head0 = false, head1 = false, tail0 = false, tail1 = false;
+  if constexpr (FC < 0) {
+    rp[0] = valid[0] ? s.leaf_parent[leaf0] : -1;
+    rp[1] = valid[1] ? s.leaf_parent[leaf0 + 1] : -2;
+    const int pprev = __shfl(rp[1], lane > 0 ? lane - 1 : 0);
+    const int pnext = __shfl(rp[0], lane < kWave - 1 ? lane + 1 : lane);
+    head0 = valid[0] && (lane == 0 || pprev != rp[0]);
+    head1 = valid[1] && rp[1] != rp[0];
+    tail0 = valid[0] && (!valid[1] || rp[1] != rp[0]);
+    tail1 = valid[1] && (lane == kWave - 1 || pnext != rp[1]);
+    const uint64_t H = ballot(head0 || head1);
+    const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
+    seg0 = 63 - __builtin_clzll((H & upto) | 1ull);
+    // slot positions (2 * lane + j) where the leaves' parents start
+    const int hpos = head1 ? kPairLP * lane + 1 : kPairLP * lane;
+    st1 = __shfl(hpos, seg0);
+    const int st1_prev = __shfl(st1, lane > 0 ? lane - 1 : 0);
+    st0 = head0 ? kPairLP * lane : st1_prev;
+  }
+  const int rack_f = FC > 0 ? FC : FC < 0 ? -1 : b.rack_fanout;  // fan-out of the fused parents (0: none, -1: ragged)
   const int half = rack_f / kPairLP;                    // lanes per parent
   const int parent = rack_f > 0 ? leaf0 / rack_f : 0;
   const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's group within its parent
   // every leaf of the block's tile exists and its counter words are
   // kPairLP-aligned (level offsets are multiples of 4): block-uniform, so the
   // stores below take a scalar branch, not a per-lane exec mask
-  const bool full_tile = (tile + 1) * kPairTile <= N && (s.level_off[s.L - 1] & (kPairLP - 1)) == 0;
+  const bool full_tile = FC >= 0 && (tile + 1) * kPairTile <= N && (s.level_off[s.L - 1] & (kPairLP - 1)) == 0;
   const int64_t SD = s.SD;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
@@ -1538,6 +1570,55 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
           base[4 * SD + g] = lead;
         }
       }
+    }
+    // the same over ragged parents (no leader classes here): per lane the
+    // summary of its second leaf's parent segment (just that leaf when it
+    // starts a parent, else both leaves), segmented inclusive scans bounded
+    // by the segment's first lane; a parent ending at the lane's first leaf
+    // takes the previous lane's scan plus that leaf
+    if constexpr (FC < 0) {
+      const int32_t inner = p_inner;
+      int32_t v[kPairLP];
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        v[j] = state[j];
+        if (inner != 0 && inner != 1) v[j] = w_mul(go_div32(v[j], inner), inner);
+      }
+      auto seg_sum = [&](int32_t a0, int32_t a1, int32_t* t0, int32_t* t1) {
+        const int32_t S = seg_incl_scan(head1 ? a1 : w_add(a0, a1), lane, seg0, OpWAdd());
+        const int32_t Sp = __shfl(S, lane > 0 ? lane - 1 : 0);
+        *t1 = S;
+        *t0 = w_add(head0 ? 0 : Sp, a0);
+      };
+      int32_t cap0, cap1, slc0 = 0, slc1 = 0;
+      seg_sum(v[0], v[1], &cap0, &cap1);
+      if (s.L - 1 != slice_level) {  // wave-uniform: the leaves' sliceState is 0
+      } else if (inner == 1 && slice_size == 1) {  // wave-uniform: sliceState == state
+        slc0 = cap0;
+        slc1 = cap1;
+      } else {
+        seg_sum(ss[0], ss[1], &slc0, &slc1);
+      }
+      const bool masks = b.rack_pos != nullptr;  // every parent <= 64 leaves
+      uint64_t pm0 = 0, pm1 = 0;
+      if (masks) {  // positive children: disjoint bits per parent, so the segment sums are its ORs
+        const uint64_t m0 = (valid[0] && ss[0] > 0) ? 1ull << ((kPairLP * lane - st0) & 63) : 0ull;
+        const uint64_t m1 = (valid[1] && ss[1] > 0) ? 1ull << ((kPairLP * lane + 1 - st1) & 63) : 0ull;
+        int32_t lo0, lo1, hi0, hi1;
+        seg_sum(int32_t(uint32_t(m0)), int32_t(uint32_t(m1)), &lo0, &lo1);
+        seg_sum(int32_t(uint32_t(m0 >> 32)), int32_t(uint32_t(m1 >> 32)), &hi0, &hi1);
+        pm0 = (uint64_t(uint32_t(hi0)) << 32) | uint32_t(lo0);
+        pm1 = (uint64_t(uint32_t(hi1)) << 32) | uint32_t(lo1);
+      }
+      auto put_parent = [&](int par, int32_t cp, int32_t sl, uint64_t pm) {
+        if (masks) b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + par] = pm;
+        if (s.L - 2 == slice_level) sl = go_div32(cp, slice_size);
+        const int g = s.level_off[s.L - 2] + par;
+        base[g] = cp;
+        base[SD + g] = sl;
+      };
+      if (tail0) put_parent(rp[0], cap0, slc0, pm0);
+      if (tail1) put_parent(rp[1], cap1, slc1, pm1);
     }
     // ExclusionStats (:1579-1634): wave-uniform skip when no leaf of the
     // wave's 128 is excluded; each ballot covers both leaves of a lane
@@ -4666,7 +4747,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.bf = !w.lfc;
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
   w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
-  w.rack_pos = b.rack_fanout ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
+  w.rack_pos = (b.rack_fanout && b.rack_pos) ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
   // per-launch-slot phase-2 buffers: the BestFit-side launch numbers its
   // evals 0..nbf-1; fast-LFC evals (the other launch) never touch them
   w.ov = b.overlay + int64_t(slot) * b.ctr_stride;
@@ -4937,6 +5018,38 @@ __global__ void set_leaf_attrs_kernel(int32_t* taint_profile, int32_t* label_val
   if (taint_profile) taint_profile[leaf] = profiles[i];
   if (label_values)
     for (int k = 0; k < K; k++) label_values[int64_t(k) * N + leaf] = labels[int64_t(i) * K + k];
+}
+
+// kueue_tas_snapshot_splice: every leaf of the new numbering takes its
+// columns from its old index (src >= 0) or from joined row -src-1.
+__global__ void splice_leaves_kernel(const int32_t* gsrc, int n_new, int n_old, int R, int K, int num_new,
+                                     const int64_t* of, const int64_t* ou, const uint32_t* ofp, const uint32_t* oup,
+                                     const int32_t* oprof, const int32_t* olab, const int64_t* nf, const int64_t* nu,
+                                     const uint32_t* nfp, const uint32_t* nup, const int32_t* nprof, const int32_t* nlab,
+                                     int64_t* f, int64_t* u, uint32_t* fp, uint32_t* up, int32_t* prof, int32_t* lab) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_new) return;
+  const int src = gsrc[j];
+  if (src >= 0) {
+    for (int c = 0; c < R; c++) {
+      f[int64_t(c) * n_new + j] = of[int64_t(c) * n_old + src];
+      u[int64_t(c) * n_new + j] = ou[int64_t(c) * n_old + src];
+    }
+    fp[j] = ofp[src];
+    up[j] = oup[src];
+    if (prof) prof[j] = oprof ? oprof[src] : 0;
+    for (int k = 0; k < K; k++) lab[int64_t(k) * n_new + j] = olab[int64_t(k) * n_old + src];
+  } else {
+    const int k0 = -src - 1;
+    for (int c = 0; c < R; c++) {
+      f[int64_t(c) * n_new + j] = nf[int64_t(c) * num_new + k0];
+      u[int64_t(c) * n_new + j] = nu[int64_t(c) * num_new + k0];
+    }
+    fp[j] = nfp[k0];
+    up[j] = nup[k0];
+    if (prof) prof[j] = nprof ? nprof[k0] : 0;
+    for (int k = 0; k < K; k++) lab[int64_t(k) * n_new + j] = nlab[int64_t(k) * num_new + k0];
+  }
 }
 
 __global__ void set_leaf_dead_kernel(uint8_t* dead, const int32_t* leaves_live, int n) {

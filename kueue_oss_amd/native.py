@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
     "kueue_tas_host_last_host_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
-    "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum",
+    "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -143,6 +143,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_host_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_set_stage_timing.argtypes = [c.c_void_p, c.c_int32]
+    lib.kueue_tas_snapshot_counters.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
                                                c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
@@ -398,12 +399,13 @@ class TASFlavorSnapshot:
         self._lib.kueue_tas_host_last_eval_profile(self._h, buf, n)
         return [dict(zip(self.PROF, buf[k * i: k * i + k])) for i in range(n)]
 
-    DEVICE_HOST = ("compile", "classes", "enqueue", "wait", "pack_d2h", "copy_out")
+    DEVICE_HOST = ("compile", "classes", "enqueue", "wait", "pack_d2h", "copy_out", "compile_validate",
+                   "compile_records")
 
     def last_device_host_times(self):
         """Host ms inside the device layer over the last run, dict keyed by DEVICE_HOST."""
-        ms = (ctypes.c_double * 6)()
-        self._lib.kueue_tas_host_last_device_host_times(self._h, ms, 6)
+        ms = (ctypes.c_double * 8)()
+        self._lib.kueue_tas_host_last_device_host_times(self._h, ms, 8)
         return dict(zip(self.DEVICE_HOST, list(ms)))
 
     def last_profile(self):
@@ -433,6 +435,12 @@ class TASFlavorSnapshot:
         self._lib.kueue_tas_host_stage_accum(self._h, ms, len(self.STAGES), ctypes.byref(runs), ctypes.byref(fills),
                                              1 if reset else 0)
         return dict(zip(self.STAGES, list(ms))), runs.value, fills.value
+
+    def snapshot_counters(self):
+        """(snapshot loads, snapshot splices) of the device context so far."""
+        lo, sp = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.kueue_tas_snapshot_counters(self.device_ctx(), ctypes.byref(lo), ctypes.byref(sp))
+        return lo.value, sp.value
 
     def last_results(self) -> list:
         """Results of the last run_compiled, one result list per compiled workload."""

@@ -275,6 +275,47 @@ def _check_leave_return(seed, n, lib=None):
     assert steps_total > 50
 
 
+def _check_join_64(lib=None, shape=(2, 4, 16, 32)):
+    """64 hosts joining existing racks of a C3-shaped snapshot (131,072 nodes at
+    full size), admitted usage on the snapshot first: one splice, no reload,
+    every result of a C3 batch equal to the oracle's on the grown document."""
+    doc, wls = synth.config_c3(n_workloads=48, shape=shape)
+    snap = TASFlavorSnapshot(doc, lib=lib) if lib else TASFlavorSnapshot(doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    admitted, deltas = snap.admit(snap.last_assignments())
+    res = snap.last_results()
+    ref = copy.deepcopy(doc)
+    for i, ok in admitted.tolist():
+        if ok:
+            ref.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
+    N = len(doc["nodes"])
+    joins = []
+    for k in range(64):
+        nd = copy.deepcopy(doc["nodes"][k * 983 % N])
+        nd["name"] = f"{nd['name']}-join{k}"
+        nd["labels"]["kubernetes.io/hostname"] = f"{nd['labels']['kubernetes.io/hostname']}-join{k}"
+        joins.append(nd)
+    loads0, splices0 = snap.snapshot_counters()
+    assert snap.update_nodes(joins) is False
+    assert snap.snapshot_counters() == (loads0, splices0 + 1)
+    ref["nodes"] = ref["nodes"] + joins
+    got = snap.find_topology_assignments_for_workloads(wls)
+    assert snap.snapshot_counters() == (loads0, splices0 + 1)  # the evaluation did not reload either
+    snap.close()
+    want, _ = oracle_lib.eval_workloads(ref, wls, threads=8)
+    assert got == want
+
+
+def test_emulated_join_64_spliced(emu_lib):  # noqa: F811
+    _check_join_64(emu_lib, shape=(1, 2, 8, 16))
+
+
+@pytest.mark.gpu
+def test_join_64_spliced_on_gpu():
+    _check_join_64(shape=(4, 16, 64, 32))
+
+
 def test_emulated_leave_return_in_place(emu_lib):  # noqa: F811
     _check_leave_return(31, 60, lib=emu_lib)
 
@@ -292,6 +333,7 @@ def _check_grow(seed, n, lib=None):
     (also on the joined leaves) added meanwhile."""
     rng = random.Random(seed)
     steps_total = 0
+    spliced = reloaded = 0  # joins the device took by kueue_tas_snapshot_splice / by a reload
     for i in range(n):
         case = synth.random_case(rng)
         levels = case["levels"]
@@ -341,7 +383,11 @@ def _check_grow(seed, n, lib=None):
                         e3 = copy.deepcopy(evs[-1])
                         e3["allocatable"]["cpu"] = e3["allocatable"].get("cpu", 0) + 500
                         evs.append(e3)
+                loads0, splices0 = snap.snapshot_counters()
                 assert snap.update_nodes(evs) is False, (i, step, [e["name"] for e in evs])
+                loads1, splices1 = snap.snapshot_counters()
+                spliced += splices1 - splices0
+                reloaded += loads1 - loads0
                 ref["nodes"] = ref["nodes"] + evs
             else:
                 res = oracle_lib.session(ref, adds + [{"op": "find", "podSets": case["podSets"]}])[-1]
@@ -355,6 +401,51 @@ def _check_grow(seed, n, lib=None):
             steps_total += 1
         snap.close()
     assert steps_total > 50
+    # joins splice the device snapshot; a reload only for a new resource or label column
+    assert spliced > 20 and reloaded < spliced / 4, (spliced, reloaded)
+    # joins splice the device snapshot; a reload only for a new resource or label column
+    assert spliced > 20 and reloaded < spliced / 4, (spliced, reloaded)
+
+
+def _check_join_64(lib=None, shape=(2, 4, 16, 32)):
+    """64 hosts joining existing racks of a C3-shaped snapshot (131,072 nodes at
+    full size), admitted usage on the snapshot first: one splice, no reload,
+    every result of a C3 batch equal to the oracle's on the grown document."""
+    doc, wls = synth.config_c3(n_workloads=48, shape=shape)
+    snap = TASFlavorSnapshot(doc, lib=lib) if lib else TASFlavorSnapshot(doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    admitted, deltas = snap.admit(snap.last_assignments())
+    res = snap.last_results()
+    ref = copy.deepcopy(doc)
+    for i, ok in admitted.tolist():
+        if ok:
+            ref.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
+    N = len(doc["nodes"])
+    joins = []
+    for k in range(64):
+        nd = copy.deepcopy(doc["nodes"][k * 983 % N])
+        nd["name"] = f"{nd['name']}-join{k}"
+        nd["labels"]["kubernetes.io/hostname"] = f"{nd['labels']['kubernetes.io/hostname']}-join{k}"
+        joins.append(nd)
+    loads0, splices0 = snap.snapshot_counters()
+    assert snap.update_nodes(joins) is False
+    assert snap.snapshot_counters() == (loads0, splices0 + 1)
+    ref["nodes"] = ref["nodes"] + joins
+    got = snap.find_topology_assignments_for_workloads(wls)
+    assert snap.snapshot_counters() == (loads0, splices0 + 1)  # the evaluation did not reload either
+    snap.close()
+    want, _ = oracle_lib.eval_workloads(ref, wls, threads=8)
+    assert got == want
+
+
+def test_emulated_join_64_spliced(emu_lib):  # noqa: F811
+    _check_join_64(emu_lib, shape=(1, 2, 8, 16))
+
+
+@pytest.mark.gpu
+def test_join_64_spliced_on_gpu():
+    _check_join_64(shape=(4, 16, 64, 32))
 
 
 def test_emulated_grow_in_place(emu_lib):  # noqa: F811

@@ -23,7 +23,7 @@ for name, fl in (("precompiled", 0), ("compile", C), ("values", V), ("full", C |
     med = [sorted(c)[len(c) // 2] for c in zip(*rows)]
     print(name, " ".join(f"{k}={v:.3f}" for k, v in zip(
         ["wall", "staging", "eval_call", "decode", "total", "d_compile", "d_classes", "d_enqueue", "d_wait", "d_pack",
-         "d_copy", "h_groups", "h_compile", "h_build_pass", "h_values"], med)))
+         "d_copy", "d_validate", "d_records", "h_groups", "h_compile", "h_build_pass", "h_values"], med)))
 res = snap.last_results()
 print("failures", sum(1 for r in res for p in r if p["reason"]), "domains",
       sum(len(p["assignment"]["domains"]) for r in res for p in r if p.get("assignment")))
