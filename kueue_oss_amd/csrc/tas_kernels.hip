@@ -1620,8 +1620,51 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       if (tail0) put_parent(rp[0], cap0, slc0, pm0);
       if (tail1) put_parent(rp[1], cap1, slc1, pm1);
     }
-    // ExclusionStats (:1579-1634): wave-uniform skip when no leaf of the
-    // wave's 128 is excluded; each ballot covers both leaves of a lane
+    // ExclusionStats (:1579-1634): every excluded leaf maps to its stats slot
+    // (nodeSelector, affinity, topologyDomain, taint id, resource id); one
+    // loop over the distinct slots present in the wave's 128 leaves, each a
+    // ballot per leaf of the lane, the counts gathered in the lane that owns
+    // the slot (kMaxFillStats == 64 slots, one per lane) and added to LDS
+    // with one conflict-free ds_add per lane: no per-kind sections, no
+    // single-lane atomics (exec-mask bookkeeping on the scalar unit)
+    if (lds_stats) {
+      static_assert(kMaxFillStats == kWave, "one stats slot per lane");
+      int sl[kPairLP];
+      uint64_t m[kPairLP];
+      uint64_t any = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        int x = -1;
+        x = kind[j] == EX_SELECTOR ? 0 : x;
+        x = kind[j] == EX_AFFINITY ? 1 : x;
+        x = kind[j] == EX_TOPOLOGY ? 2 : x;
+        x = kind[j] == EX_TAINT ? kStatFixed + id[j] : x;
+        x = kind[j] == EX_RESOURCE ? kStatFixed + b.num_taints + id[j] : x;
+        sl[j] = valid[j] ? x : -1;
+        m[j] = ballot(sl[j] >= 0);
+        any |= m[j];
+      }
+      if (any == 0) continue;
+      int32_t acc = 0;
+      while (any) {  // wave-uniform: one trip per distinct slot
+        int x = 0;
+#pragma unroll
+        for (int j = kPairLP - 1; j >= 0; j--)
+          if (m[j]) x = bcast(sl[j], __ffsll((unsigned long long)m[j]) - 1);
+        int c = 0;
+        any = 0;
+#pragma unroll
+        for (int j = 0; j < kPairLP; j++) {
+          const uint64_t h = ballot(sl[j] == x);
+          c += __popcll(h);
+          m[j] &= ~h;
+          any |= m[j];
+        }
+        acc += lane == x ? c : 0;
+      }
+      atomicAdd(&sh_stats[e][lane], acc);
+      continue;
+    }
     uint64_t anyx = 0;
 #pragma unroll
     for (int j = 0; j < kPairLP; j++) anyx |= ballot(valid[j] && kind[j] != EX_NONE && kind[j] != EX_DEAD);
