@@ -1201,25 +1201,23 @@ class FlavorSnapshot {
         at.push_back(size_t(it - lvl.begin()));
         add.push_back(std::move(pre));
       }
+      // in place: the level grows by the new prefixes and every old domain
+      // moves right by the number inserted before it (from the back, so no
+      // slot is overwritten before it moved; a moved vector keeps its
+      // buffer, so the leaves' Values addresses survive the move)
       const size_t D0 = lvl.size();
-      std::vector<std::vector<std::string>> merged;
-      merged.reserve(D0 + add.size());
       auto& rm = remap[size_t(l)];
       rm.resize(D0);
-      size_t a = 0;
-      for (size_t i = 0; i < D0; i++) {
-        for (; a < add.size() && at[a] == i; a++) {
-          fresh[size_t(l)].push_back(int32_t(merged.size()));
-          merged.push_back(std::move(add[a]));
-        }
-        rm[i] = int32_t(merged.size());
-        merged.push_back(std::move(lvl[i]));
+      auto& fr = fresh[size_t(l)];
+      for (size_t a = 0, i = 0; i < D0; i++) {
+        while (a < add.size() && at[a] == i) a++;
+        rm[i] = int32_t(i + a);
       }
-      for (; a < add.size(); a++) {
-        fresh[size_t(l)].push_back(int32_t(merged.size()));
-        merged.push_back(std::move(add[a]));
-      }
-      lvl = std::move(merged);
+      for (size_t a = 0; a < add.size(); a++) fr.push_back(int32_t(at[a] + a));
+      lvl.resize(D0 + add.size());
+      for (size_t i = D0; i-- > 0;)
+        if (size_t(rm[i]) != i) lvl[size_t(rm[i])] = std::move(lvl[i]);
+      for (size_t a = 0; a < add.size(); a++) lvl[size_t(fr[a])] = std::move(add[a]);
     }
     // CSR offsets: children per (new) parent, then a prefix sum
     for (int l = 0; l + 1 < L; l++) {
@@ -1239,47 +1237,55 @@ class FlavorSnapshot {
     const auto& rm = remap[size_t(L - 1)];
     const auto& fr = fresh[size_t(L - 1)];
     const size_t N0 = rm.size(), N = N0 + fr.size();
+    // every leaf-indexed array grows in place the same way (from the back),
+    // the arrays on the host pool's workers at once
     auto move_leaves = [&](auto& vec, auto make) {
-      std::remove_reference_t<decltype(vec)> out(N);
-      for (size_t i = 0; i < N0; i++) out[size_t(rm[i])] = std::move(vec[i]);
-      for (size_t k = 0; k < fr.size(); k++) out[size_t(fr[k])] = make(joins[k]);
-      vec = std::move(out);
+      vec.resize(N);
+      for (size_t i = N0; i-- > 0;)
+        if (size_t(rm[i]) != i) vec[size_t(rm[i])] = std::move(vec[i]);
+      for (size_t k = 0; k < fr.size(); k++) vec[size_t(fr[k])] = make(joins[k]);
     };
     auto move_boxed = [&](LeafVec<Requests>& vec, auto make) {
-      std::vector<std::unique_ptr<Requests>> out(N);
-      for (size_t i = 0; i < N0; i++) out[size_t(rm[i])] = std::move(vec.v[i]);
-      for (size_t k = 0; k < fr.size(); k++) out[size_t(fr[k])] = std::make_unique<Requests>(make(joins[k]));
-      vec.v = std::move(out);
+      move_leaves(vec.v, [&](const Join& j) { return std::make_unique<Requests>(make(j)); });
     };
-    move_leaves(leafId, [](const Join& j) { return j.id; });
-    move_leaves(leafNode, [](const Join& j) { return j.node; });
-    move_boxed(leafAlloc, [](const Join& j) { return j.node->allocatable; });
-    move_boxed(freeCap, [&](const Join& j) {
-      Requests f = j.node->allocatable;
-      if (auto u = nodeUsage.find(j.node->name); u != nodeUsage.end()) req_sub(f, u->second);
-      return f;
+    std::vector<std::function<void()>> tasks;
+    tasks.emplace_back([&] { move_leaves(leafId, [](const Join& j) { return j.id; }); });
+    tasks.emplace_back([&] { move_leaves(leafNode, [](const Join& j) { return j.node; }); });
+    tasks.emplace_back([&] { move_boxed(leafAlloc, [](const Join& j) { return j.node->allocatable; }); });
+    tasks.emplace_back([&] {
+      move_boxed(freeCap, [&](const Join& j) {
+        Requests f = j.node->allocatable;
+        if (auto u = nodeUsage.find(j.node->name); u != nodeUsage.end()) req_sub(f, u->second);
+        return f;
+      });
     });
-    move_boxed(tasUsage, [&](const Join& j) {
-      auto u = usageByDomain.find(j.id);
-      return u == usageByDomain.end() ? Requests() : u->second;
+    tasks.emplace_back([&] {
+      move_boxed(tasUsage, [&](const Join& j) {
+        auto u = usageByDomain.find(j.id);
+        return u == usageByDomain.end() ? Requests() : u->second;
+      });
     });
-    move_leaves(leafNodeNames, [](const Join& j) { return std::vector<std::string>{j.node->name}; });
-    move_leaves(leafDead, [](const Join&) { return uint8_t(0); });
-    move_leaves(leafProfile, [](const Join& j) { return j.prof; });
-    if (!labelKeys.empty()) {
+    tasks.emplace_back([&] { move_leaves(leafNodeNames, [](const Join& j) { return std::vector<std::string>{j.node->name}; }); });
+    tasks.emplace_back([&] {
+      move_leaves(leafDead, [](const Join&) { return uint8_t(0); });
+      move_leaves(leafProfile, [](const Join& j) { return j.prof; });
+    });
+    tasks.emplace_back([&] {
+      if (labelKeys.empty()) return;
       const size_t K = labelKeys.size();
-      std::vector<int32_t> lab(K * N, 0);
-      for (size_t k = 0; k < K; k++) {
-        const int32_t* src = labelValues.data() + k * N0;
-        int32_t* dst = lab.data() + k * N;
-        for (size_t i = 0; i < N0; i++) dst[rm[i]] = src[i];
+      labelValues.resize(K * N, 0);  // [K][N0] -> [K][N] in place: later columns and entries first
+      for (size_t k = K; k-- > 0;) {
+        int32_t* col = labelValues.data();
+        for (size_t i = N0; i-- > 0;) col[k * N + size_t(rm[i])] = col[k * N0 + i];
         for (size_t j = 0; j < fr.size(); j++) {
           auto it = joins[j].node->labels.find(labelKeys[k]);
-          dst[fr[j]] = it == joins[j].node->labels.end() ? 0 : labelDict[k].at(it->second);
+          col[k * N + size_t(fr[j])] = it == joins[j].node->labels.end() ? 0 : labelDict[k].at(it->second);
         }
       }
-      labelValues = std::move(lab);
-    }
+    });
+    ktas_pool::HostPool::get().run(tasks.size(), 1, [&](size_t b, size_t e) {
+      for (size_t t = b; t < e; t++) tasks[t]();
+    });
     // leaf indices held in maps: remapped in place (no re-hashing), then the joins added
     leafById.remap(rm);
     for (size_t k = 0; k < fr.size(); k++) leafById.set(joins[k].id, fr[k]);
@@ -2722,50 +2728,63 @@ struct Evaluator {
     size_t total = 0;
     for (int l = 0; l < L; l++) total += s.values[size_t(l)].size();
     const size_t chunk = size_t(s.cfg.max_batch > 0 ? s.cfg.max_batch : 1024);
-    for (size_t c0 = 0; c0 < idx.size(); c0 += chunk) {  // every request of a call in one device chunk
-      const size_t m = std::min(chunk, idx.size() - c0);
+    // the first batch's last device chunk still holds its requests' phase-1
+    // counters (kueue_tas_last_counters): those are read in place; only the
+    // balanced requests of earlier chunks are evaluated again
+    const size_t last0 = n > 0 ? (n - 1) / chunk * chunk : 0;
+    std::vector<size_t> again, here;
+    for (size_t i : idx) (i >= last0 ? here : again).push_back(i);
+    auto place = [&](size_t i, size_t slot) -> int {  // the counters of request `slot` of the last batch -> balOut[i]
+      balCtr.resize(std::max<size_t>(5 * total, 1));
+      int rc = kueue_tas_last_counters(s.ctx, slot, balCtr.data(), balCtr.size());
+      if (rc) return rc;
+      ktas_balanced::Tree t;
+      t.L = L;
+      t.ctr.resize(size_t(L));
+      size_t g0 = 0;
+      for (int l = 0; l < L; l++) {
+        const size_t D = s.values[size_t(l)].size();
+        t.size.push_back(int32_t(D));
+        if (l + 1 < L) t.co.push_back(&s.childOff[size_t(l)]);
+        auto& cl = t.ctr[size_t(l)];
+        cl.resize(D);
+        for (size_t d = 0; d < D; d++) {
+          const size_t g = g0 + d;
+          cl[d] = {balCtr[g], balCtr[total + g], balCtr[2 * total + g], balCtr[3 * total + g], balCtr[4 * total + g]};
+        }
+        g0 += D;
+      }
+      const kueue_tas_eval_req& q = *rq[i];
+      ktas_balanced::Params p;
+      p.count = q.count;
+      p.sliceSize = q.slice_size;
+      p.leaderCount = (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
+      p.requestedLevelIdx = q.requested_level;
+      p.sliceLevelIdx = q.slice_level;
+      p.sliceSizeAtLevel = q.slice_size_at_level;
+      const ktas_balanced::Result r = ktas_balanced::Placement(t, p).run();
+      BalancedOut& o = balOut[i];
+      o.used = r.used;
+      o.reason = r.reason;
+      for (auto& x : r.workers) o.workers.push_back({x.first, x.second});
+      for (auto& x : r.leaders) o.leaders.push_back({x.first, x.second});
+      return 0;
+    };
+    for (size_t i : here)
+      if (int rc = place(i, i)) {  // the batch index: the last chunk's requests keep theirs
+        snap->err = std::string("balanced placement: ") + kueue_tas_last_error(s.ctx);
+        return rc;
+      }
+    for (size_t c0 = 0; c0 < again.size(); c0 += chunk) {  // every request of a call in one device chunk
+      const size_t m = std::min(chunk, again.size() - c0);
       balReq.clear();
-      for (size_t k = 0; k < m; k++) balReq.push_back(*rq[idx[c0 + k]]);
+      for (size_t k = 0; k < m; k++) balReq.push_back(*rq[again[c0 + k]]);
       balOuts.resize(m);
       balOffs.resize(m + 1);
       int rc = kueue_tas_eval_batch(s.ctx, balReq.data(), m, tt.data(), tt.size(), int32_t(s.taintStrings.size()),
                                     assumed.data(), assumed.size(), af->data(), af->size(), afv->data(), afv->size(),
                                     balOuts.data(), balOffs.data(), nullptr, 0, nullptr, nullptr);
-      balCtr.resize(std::max<size_t>(5 * total, 1));
-      for (size_t k = 0; k < m && rc == 0; k++) {
-        rc = kueue_tas_last_counters(s.ctx, k, balCtr.data(), balCtr.size());
-        if (rc) break;
-        ktas_balanced::Tree t;
-        t.L = L;
-        t.ctr.resize(size_t(L));
-        size_t g0 = 0;
-        for (int l = 0; l < L; l++) {
-          const size_t D = s.values[size_t(l)].size();
-          t.size.push_back(int32_t(D));
-          if (l + 1 < L) t.co.push_back(&s.childOff[size_t(l)]);
-          auto& cl = t.ctr[size_t(l)];
-          cl.resize(D);
-          for (size_t d = 0; d < D; d++) {
-            const size_t g = g0 + d;
-            cl[d] = {balCtr[g], balCtr[total + g], balCtr[2 * total + g], balCtr[3 * total + g], balCtr[4 * total + g]};
-          }
-          g0 += D;
-        }
-        const kueue_tas_eval_req& q = balReq[k];
-        ktas_balanced::Params p;
-        p.count = q.count;
-        p.sliceSize = q.slice_size;
-        p.leaderCount = (q.flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
-        p.requestedLevelIdx = q.requested_level;
-        p.sliceLevelIdx = q.slice_level;
-        p.sliceSizeAtLevel = q.slice_size_at_level;
-        const ktas_balanced::Result r = ktas_balanced::Placement(t, p).run();
-        BalancedOut& o = balOut[idx[c0 + k]];
-        o.used = r.used;
-        o.reason = r.reason;
-        for (auto& x : r.workers) o.workers.push_back({x.first, x.second});
-        for (auto& x : r.leaders) o.leaders.push_back({x.first, x.second});
-      }
+      for (size_t k = 0; k < m && rc == 0; k++) rc = place(again[c0 + k], k);
       if (rc) {
         snap->err = std::string("balanced placement: ") + kueue_tas_last_error(s.ctx);
         return rc;
@@ -2899,10 +2918,6 @@ struct Evaluator {
       }
       // zero-copy view (pinned, strided regions) or the packed copy
       const int32_t* ent_view = packed ? entries.data() : kueue_tas_last_entries(snap->ctx, nullptr);
-      rc = balanced_pass(*rq, *tt, af, afv, *bt, &ent_view);
-      if (rc) return rc;
-      const double t_decode = now_ms();
-      host_ms[1] += t_decode - t_call;
       float t4[4];
       kueue_tas_last_timings(snap->ctx, t4);
       for (int k = 0; k < 4; k++) ms[k] += t4[k];
@@ -2917,6 +2932,10 @@ struct Evaluator {
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
       stats[3] = std::max(stats[3], st4[3]);
       stats[4] |= int64_t(kueue_tas_last_fill_paths(snap->ctx));
+      rc = balanced_pass(*rq, *tt, af, afv, *bt, &ent_view);  // after the diagnostics: it may run a batch
+      if (rc) return rc;
+      const double t_decode = now_ms();
+      host_ms[1] += t_decode - t_call;
       counts[0]++;
       counts[1] += int64_t(n);
       // decode: every eval of the pass writes only its own workload's
