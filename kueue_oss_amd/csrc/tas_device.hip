@@ -2085,7 +2085,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
                        reinterpret_cast<int32_t*>(ds + o_top) + n * kMaxLevels);
     HIPCHK(c, hipGetLastError());
   }
-  for (int l = fused_top ? -1 : upper; l >= 0; l--) {
+  // the small top levels (<= kTailParents domains) go to rollup_tail_kernel with the level maxima
+  int tail_top = -1;
+  if (!fused_top && nfill > 0)
+    for (int l = upper; l >= 0 && tail_top < 0; l--)
+      if (s.level_size[l] <= kTailParents) tail_top = l;
+  for (int l = fused_top ? -1 : upper; l > tail_top; l--) {
     if (s.level_size[l] <= 0) continue;
     const int fanout = s.level_size[l + 1] / s.level_size[l];
     if (fanout >= 8) {  // wave per parent: coalesced child reads
@@ -2098,10 +2103,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
     HIPCHK(c, hipGetLastError());
   }
-  if (!fused_top && nfill > 0 && s.L >= 2 && nbf > 0) {  // level maxima for the BestFit-side find_level
-    HIPCHK(c, c->d_level_max.ensure(size_t(nfill) * size_t(kMaxLevels)));
-    b.level_max = c->d_level_max.p;
-    hipLaunchKernelGGL(level_max_kernel, dim3(unsigned(nfill), unsigned(s.L - 1)), dim3(256), 0, c->stream, s, b);
+  if (!fused_top && nfill > 0 && s.L >= 2 && (nbf > 0 || tail_top >= 0)) {
+    // the small top levels and the level maxima for the BestFit-side find_level
+    b.level_max = nullptr;
+    if (nbf > 0) {
+      HIPCHK(c, c->d_level_max.ensure(size_t(nfill) * size_t(kMaxLevels)));
+      b.level_max = c->d_level_max.p;
+    }
+    hipLaunchKernelGGL(rollup_tail_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, s, b, tail_top);
     HIPCHK(c, hipGetLastError());
   }
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));

@@ -2208,6 +2208,39 @@ __global__ __launch_bounds__(256) void rollup_top_kernel(DevSnap s, DevBatch b, 
   }
 }
 
+// The roll-up's small top levels and every level's maximum sliceState in one
+// launch: one block per class rolls up levels top .. 0 (a few parents each,
+// one wave per parent, levels in order with a block barrier between), then
+// streams each level l < L-1's sliceState row for its maximum (findLevel's
+// level scans: b.level_max).  Replaces the per-level launches of those
+// levels and level_max_kernel.
+constexpr int kTailParents = 16;  // levels of at most this many domains go to rollup_tail_kernel
+__global__ __launch_bounds__(256) void rollup_tail_kernel(DevSnap s, DevBatch b, int top) {
+  __shared__ int32_t red[4];
+  const int row = blockIdx.x;  // the class's fill position
+  const DevEval& ev = b.evals[b.fill_ids[row]];
+  const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
+  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int wv = threadIdx.x >> 6;
+  for (int l = top; l >= 0; l--) {
+    int32_t unused = INT32_MIN;
+    for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, ev, leaderReq, l, p, &unused);
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (!b.level_max) return;
+  for (int l = 0; l + 1 < s.L; l++) {
+    const int32_t* ss = base + s.SD + s.level_off[l];
+    int32_t m = INT32_MIN;
+    for (int i = threadIdx.x; i < s.level_size[l]; i += 256) m = max(m, l <= top ? load_l2_i32(ss + i) : ss[i]);
+    m = group_reduce(m, 64, OpMax());
+    if (lane_id() == 0) red[wv] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) b.level_max[int64_t(row) * kMaxLevels + l] = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+  }
+}
+
 // Leaf-level selection partials for evals whose requested level is the leaf
 // level: per 64-leaf wave, the reductions findLevelWithFitDomains needs
 // (:1244-1270): first/last sortedDomainsWithLeader key, LFC first fit,
@@ -5607,10 +5640,14 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
       }
       if (threadIdx.x == 0) admitted[wa] = 1;
       w0 = wa + 1;
+      // the admission's usage atomics complete (agent scope) before any wave
+      // of the next window reads usage through L2 (the barrier
+      // alone does not order them)
+      __threadfence();
     } else {
       w0 += kAdmitWindow;
     }
-    __syncthreads();  // the admission's atomics returned (consumed into sink) before the next window loads
+    __syncthreads();
   }
   if (threadIdx.x == 0) admitted[n_wl] = int32_t(uint32_t(sink));
 }
