@@ -115,7 +115,17 @@ struct PartClasses {
 };
 
 // libdivide-style u64 magic for exact division by an invariant divisor d >= 1.
-void compute_magic(uint64_t d, DevTerm* t) {
+// 2^(64 + fl) / d and its remainder for 2^fl < d < 2^(fl + 1): the quotient
+// fits 64 bits, so one 128-by-64 divq gives both (two __int128 divisions
+// through the runtime library cost ~10x that per term)
+static inline uint64_t div_pow2_by(int fl, uint64_t d, uint64_t* rem) {
+  uint64_t q, r;
+  __asm__("divq %4" : "=a"(q), "=d"(r) : "a"(uint64_t(0)), "d"(uint64_t(1) << fl), "rm"(d));
+  *rem = r;
+  return q;
+}
+
+void compute_magic_uncached(uint64_t d, DevTerm* t) {
   t->magic = 0;
   t->shift = 0;
   t->add = 0;
@@ -126,9 +136,8 @@ void compute_magic(uint64_t d, DevTerm* t) {
     t->shift = uint8_t(fl);
     return;
   }
-  unsigned __int128 num = (unsigned __int128)1 << (64 + fl);
-  uint64_t proposed = uint64_t(num / d);
-  uint64_t rem = uint64_t(num % d);
+  uint64_t rem;
+  uint64_t proposed = div_pow2_by(fl, d, &rem);
   uint64_t e = d - rem;
   if (e < (uint64_t(1) << fl)) {
     t->shift = uint8_t(fl);
@@ -140,6 +149,30 @@ void compute_magic(uint64_t d, DevTerm* t) {
     t->add = 1;
   }
   t->magic = proposed + 1;
+}
+
+// the divisors of a batch repeat (a request shape per workload type): a
+// per-thread direct-mapped cache of the magic numbers
+void compute_magic(uint64_t d, DevTerm* t) {
+  struct Slot {
+    uint64_t d = 0, magic = 0;
+    uint8_t shift = 0, add = 0, pow2 = 0;
+  };
+  static thread_local Slot cache[256];
+  Slot& c = cache[(d * 0x9e3779b97f4a7c15ull) >> 56];
+  if (c.d != d) {
+    compute_magic_uncached(d, t);
+    c.d = d;
+    c.magic = t->magic;
+    c.shift = t->shift;
+    c.add = t->add;
+    c.pow2 = t->pow2;
+    return;
+  }
+  t->magic = c.magic;
+  t->shift = c.shift;
+  t->add = c.add;
+  t->pow2 = c.pow2;
 }
 
 }  // namespace

@@ -45,6 +45,10 @@
 #include "tas_balanced.h"
 #include "tas_pool.h"
 
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 namespace kueue_tas {
 
 using Requests = std::map<std::string, int64_t>;
@@ -1379,8 +1383,10 @@ class FlavorSnapshot {
   bool splicePending = false;
   std::vector<int32_t> spliceSrc;  // per current leaf: its index on the device, -1 joined since
   bool namesStale = false;         // domain names to reload before a v1beta2 encode
+  double splice_ms[3] = {0, 0, 0};  // last splice: host rows, kueue_tas_snapshot_splice, leaf tags
   int upload_splice() {
     splicePending = false;
+    const double t0 = now_ms();
     const int L = this->L(), N = this->N(), R = int(cols.size());
     std::vector<int32_t> sizes(L), co, ranks;
     for (int l = 0; l < L; l++) sizes[l] = int32_t(values[l].size());
@@ -1428,6 +1434,7 @@ class FlavorSnapshot {
     sd.new_usage_present = up.data();
     sd.new_taint_profile = lowestIsHostname ? prof.data() : nullptr;
     sd.new_label_values = K ? lab.data() : nullptr;
+    const double t1 = now_ms();
     int rc = kueue_tas_snapshot_splice(ctx, &sd);
     spliceSrc.clear();
     if (rc) {
@@ -1435,7 +1442,12 @@ class FlavorSnapshot {
       return rc;
     }
     namesStale = true;
-    return set_tags();
+    const double t2 = now_ms();
+    rc = set_tags();
+    splice_ms[0] = t1 - t0;
+    splice_ms[1] = t2 - t1;
+    splice_ms[2] = now_ms() - t2;
+    return rc;
   }
   int set_tags() {  // entry tags: each leaf's Values address (Values come back with the entries)
     if (cfg.flags & KUEUE_TAS_CFG_HOST_VALUES) return 0;
@@ -2403,9 +2415,6 @@ static std::vector<TASPodSetRequests> parse_podsets(const kjson::Node& arr) {
 // (groups of one workload are sequential through assumedUsage, :543-591).
 using ktas_pool::HostPool;
 
-static double now_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // A workload's assumedUsage overlay across its PodSet groups (addAssumedUsage
 // :658-666): records appended per assigned domain, sorted by (leaf, column)
@@ -3352,6 +3361,9 @@ struct kueue_tas_host {
   std::vector<std::pair<int32_t, int32_t>> admit_ps_terms;  // per PodSet of the workload: (term_begin, num_terms)
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
   float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
+  // last kueue_tas_host_update_nodes: parse, node events, flush_joins, splice
+  // (host rows, device call, leaf tags), evaluator reset, pushes, total
+  double upd_ms[9] = {};
   int64_t accum_runs = 0, accum_fills = 0;
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
@@ -4062,24 +4074,37 @@ static int rebuild(kueue_tas_host* h, const kjson::Node& node_events) {
 int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32_t* rebuilt) {
   if (!h || !h->snap || !h->err.empty()) return KUEUE_TAS_EINVAL;
   try {
+    double* um = h->upd_ms;
+    for (double& x : h->upd_ms) x = 0;
+    const double t0 = now_ms();
     kjson::Node arr = kjson::parse(nodes_json);
+    const double t1 = now_ms();
     std::set<int32_t> touched, liveChanged;
     size_t k = 0;
     for (; k < arr.items.size(); k++)
       if (!h->snap->node_event_in_place(arr.items[k], &touched, &liveChanged)) break;
     const bool structural = k < arr.items.size();
+    const double t2 = now_ms();
     if (structural) {  // rebuilt from the cache state, which holds the pending joins
       h->snap->joins.clear();
       h->snap->joinIds.clear();
     } else {
       h->snap->flush_joins(&touched, &liveChanged);
     }
+    const double t3 = now_ms();
     int rc0 = 0;
-    if (!structural && h->snap->splicePending) rc0 = h->snap->upload();  // the pushes below use the new numbering
+    const bool splice = !structural && h->snap->splicePending;
+    if (splice) rc0 = h->snap->upload();  // the pushes below use the new numbering
     if (rc0) {
       h->err = h->snap->err;
       return rc0;
     }
+    const double t4 = now_ms();
+    um[0] = t1 - t0;
+    um[1] = t2 - t1;
+    um[2] = t3 - t2;
+    if (splice)
+      for (int q = 0; q < 3; q++) um[3 + q] = h->snap->splice_ms[q];
     if (rebuilt) *rebuilt = structural ? 1 : 0;
     int rc;
     if (structural) {  // the events applied so far are in the cache state; the rest replay on it
@@ -4093,10 +4118,14 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
         h->ev.reset();
         h->last.clear();
       }
+      um[6] = now_ms() - t4;
       rc = h->snap->push_liveness(liveChanged);
       if (!rc) rc = h->snap->push_leaves(touched, true);
       if (!rc && h->snap->dirty && h->snap->ctx) rc = h->snap->upload();  // joined leaves: the reload is this event's
     }
+    const double t5 = now_ms();
+    um[7] = t5 - t4 - um[6];
+    um[8] = t5 - t0;
     if (rc) h->err = h->snap->err;
     return rc;
   } catch (const std::exception& e) {
@@ -4431,6 +4460,12 @@ int kueue_tas_host_stage_accum(kueue_tas_host* h, float* ms, int n, int64_t* run
     h->accum_runs = h->accum_fills = 0;
   }
   return 0;
+}
+
+int kueue_tas_host_last_update_detail(kueue_tas_host* h, double* ms, int n) {
+  if (!h || !ms) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < 9; k++) ms[k] = h->upd_ms[k];
+  return KUEUE_TAS_OK;
 }
 
 int kueue_tas_host_last_host_detail(kueue_tas_host* h, double* ms, int n) {

@@ -62,7 +62,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
     "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
-    "kueue_tas_host_last_host_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
+    "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
 ]
 
@@ -142,6 +142,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_eval_ticks.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
     lib.kueue_tas_host_last_profile.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     lib.kueue_tas_host_last_host_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
+    lib.kueue_tas_host_last_update_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_set_stage_timing.argtypes = [c.c_void_p, c.c_int32]
     lib.kueue_tas_snapshot_counters.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
@@ -421,6 +422,15 @@ class TASFlavorSnapshot:
         ms = (ctypes.c_double * 4)()
         self._lib.kueue_tas_host_last_host_detail(self._h, ms, 4)
         return dict(zip(self.HOST_DETAIL, list(ms)))
+
+    UPDATE_DETAIL = ("parse", "events", "flush_joins", "splice_rows", "splice_device", "leaf_tags",
+                     "evaluator_reset", "pushes", "total")
+
+    def last_update_detail(self):
+        """Host wall ms of the last update_nodes, dict keyed by UPDATE_DETAIL."""
+        ms = (ctypes.c_double * 9)()
+        self._lib.kueue_tas_host_last_update_detail(self._h, ms, 9)
+        return {k: round(v, 3) for k, v in zip(self.UPDATE_DETAIL, list(ms))}
 
     def set_stage_timing(self, on: bool):
         """Record every device stage event (True, default) or only the fill bracket."""

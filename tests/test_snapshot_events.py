@@ -275,47 +275,6 @@ def _check_leave_return(seed, n, lib=None):
     assert steps_total > 50
 
 
-def _check_join_64(lib=None, shape=(2, 4, 16, 32)):
-    """64 hosts joining existing racks of a C3-shaped snapshot (131,072 nodes at
-    full size), admitted usage on the snapshot first: one splice, no reload,
-    every result of a C3 batch equal to the oracle's on the grown document."""
-    doc, wls = synth.config_c3(n_workloads=48, shape=shape)
-    snap = TASFlavorSnapshot(doc, lib=lib) if lib else TASFlavorSnapshot(doc)
-    snap.compile(wls)
-    snap.run_compiled()
-    admitted, deltas = snap.admit(snap.last_assignments())
-    res = snap.last_results()
-    ref = copy.deepcopy(doc)
-    for i, ok in admitted.tolist():
-        if ok:
-            ref.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
-    N = len(doc["nodes"])
-    joins = []
-    for k in range(64):
-        nd = copy.deepcopy(doc["nodes"][k * 983 % N])
-        nd["name"] = f"{nd['name']}-join{k}"
-        nd["labels"]["kubernetes.io/hostname"] = f"{nd['labels']['kubernetes.io/hostname']}-join{k}"
-        joins.append(nd)
-    loads0, splices0 = snap.snapshot_counters()
-    assert snap.update_nodes(joins) is False
-    assert snap.snapshot_counters() == (loads0, splices0 + 1)
-    ref["nodes"] = ref["nodes"] + joins
-    got = snap.find_topology_assignments_for_workloads(wls)
-    assert snap.snapshot_counters() == (loads0, splices0 + 1)  # the evaluation did not reload either
-    snap.close()
-    want, _ = oracle_lib.eval_workloads(ref, wls, threads=8)
-    assert got == want
-
-
-def test_emulated_join_64_spliced(emu_lib):  # noqa: F811
-    _check_join_64(emu_lib, shape=(1, 2, 8, 16))
-
-
-@pytest.mark.gpu
-def test_join_64_spliced_on_gpu():
-    _check_join_64(shape=(4, 16, 64, 32))
-
-
 def test_emulated_leave_return_in_place(emu_lib):  # noqa: F811
     _check_leave_return(31, 60, lib=emu_lib)
 
