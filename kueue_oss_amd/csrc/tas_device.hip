@@ -1075,6 +1075,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_out = al(up_bytes);
   const size_t nwords = (size_t(c->snap.N) + 31) / 32;
   const bool lds_bits = nwords * 4 <= 64 * 1024;
+  // the windowed kernel's round bitmap beside the touched one: admission chains within a window
+  const bool lds_chain = c->admit_window && 2 * nwords * 4 <= 64 * 1024;
   const size_t o_recs = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
   const size_t o_bits = o_recs + al(n * sizeof(AdmitRec));
   HIPCHK(c, c->d_fits.ensure(o_bits + (lds_bits ? 0 : nwords * 4)));
@@ -1105,12 +1107,13 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
     HIPCHK(c, hipGetLastError());
   }
   if (c->admit_window)  // windowed optimistic admission (one 1024-thread workgroup)
-    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow), lds_bits ? nwords * 4 : 0, c->stream,
-                       c->snap, c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
-                       reinterpret_cast<const AdmitRec*>(d + o_recs), reinterpret_cast<const int64_t*>(d + o_off),
-                       int(n_wl), pods_col, reinterpret_cast<const int32_t*>(d + o_fit0),
-                       reinterpret_cast<const int32_t*>(d + o_exact), reinterpret_cast<uint32_t*>(d + o_bits),
-                       lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
+    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
+                       lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
+                       c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
+                       reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
+                       reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
+                       reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
+                       reinterpret_cast<int32_t*>(d + o_out));
   else  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),

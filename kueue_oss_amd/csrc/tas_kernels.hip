@@ -5552,41 +5552,62 @@ __global__ __launch_bounds__(64) void admit_kernel(DevSnap s, int64_t* tas_usage
 // TAS half of Scheduler.processEntry, scheduler.go:371-435, per workload in
 // order, Fits tas_flavor_snapshot.go:401-415 then AddUsage :257-265).  Usage
 // only grows during a call, so a candidate checked against the usage of the
-// workloads admitted so far keeps that verdict until the next admission.
-// One 1024-thread workgroup: each of its kAdmitWindow waves checks one of the
-// next kAdmitWindow candidates in parallel; the window's rejections before
-// its first fitting candidate are final, that candidate is admitted (every
-// thread adds a share of its usage with returning atomics, consumed before
-// the barrier, so the next window's L2 loads see it) and the next window
-// starts right after it.  Rounds = admissions + rejections / kAdmitWindow
-// instead of one dependent chain step per workload.  A record whose leaf no
-// admitted workload of this call touched (LDS bitmap) keeps its phase-1
-// verdict without a load.
+// workloads admitted so far keeps a failed verdict for good, and a fitting
+// verdict until an admission adds usage on one of its leaves.
+// One 1024-thread workgroup, one round per window of kAdmitWindow candidates:
+//  1. each wave checks one candidate against the current usage (a record
+//     whose leaf no admission of this call touched keeps its phase-1 verdict
+//     without a load: the `touched` bitmap);
+//  2. the window is decided in order: rejections are final; the first fitting
+//     candidate is admitted; a later fitting one is admitted as well when none
+//     of its leaves was admitted onto earlier in this round (the `round`
+//     bitmap, LDS) — its check still holds — and the round stops at the first
+//     fitting candidate that shares a leaf with this round's admissions (it
+//     is checked again, first of the next window);
+//  3. an admitted candidate's wave adds its usage with non-returning atomics;
+//     the round ends with every wave's memory counters drained (s_waitcnt 0:
+//     the atomics performed at L2, where the next round's loads read) and a
+//     barrier.
+// Rounds ~ conflicts + candidates / kAdmitWindow instead of admissions +
+// rejections / kAdmitWindow.  Without room for both bitmaps in LDS the round
+// admits only its first fitting candidate (the round-3 windowed kernel).
 // (A variant that spread the window's records over all 1024 threads measured
 // admit_device 4.1 ms vs 1.8 ms on C3 (profiles/r03_lp4, r03): a wave per candidate
-// stops at the candidate's first failing record, the spread one checks all.)
+// stops at the candidate's first failing record, the spread one checks all.
+// An agent-scope __threadfence per admission writes the XCD's L2 back
+// (buffer_wbl2): the drained counters order the atomics without it.)
 constexpr int kAdmitWindow = 16;
+__device__ __forceinline__ void admit_drain() {  // every outstanding memory operation of the wave completed
+  __builtin_amdgcn_s_waitcnt(0);
+}
 __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
     const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
     const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
     int32_t* admitted) {
-  extern __shared__ uint32_t touched_lds[];
+  extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
   __shared__ int32_t sh_fit[kAdmitWindow];
+  __shared__ int32_t sh_conf;
   const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
+  const int nwords = (s.N + 31) / 32;
   const bool in_lds = touched_in_lds != 0;
+  const bool chain = touched_in_lds == 2;
+  uint32_t* round_lds = touched_lds + nwords;
   if (in_lds)  // (the global bitmap is cleared by the host)
-    for (int k = threadIdx.x; k < (s.N + 31) / 32; k += blockDim.x) touched_lds[k] = 0;
+    for (int k = threadIdx.x; k < (chain ? 2 : 1) * nwords; k += blockDim.x) touched_lds[k] = 0;
   const bool exact = *exact_flag != 0;
-  unsigned long long sink = 0;
   __syncthreads();
   int w0 = 0;
   while (w0 < n_wl) {  // block-uniform
     const int w = w0 + wave;
+    int64_t r0 = 0, r1 = 0;
+    if (w < n_wl) {
+      r0 = wl_off[w];
+      r1 = wl_off[w + 1];
+    }
     bool fit = false;
     if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
       fit = true;
-      const int64_t r0 = wl_off[w], r1 = wl_off[w + 1];
       for (int64_t base = r0; base < r1 && fit; base += kWave) {
         const int64_t i = base + lane;
         bool ok = true;
@@ -5610,46 +5631,62 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     }
     if (lane == 0) sh_fit[wave] = fit ? 1 : 0;
     __syncthreads();
-    int first = kAdmitWindow;  // first fitting candidate of the window (every thread alike)
-    for (int k = kAdmitWindow - 1; k >= 0; k--)
-      if (sh_fit[k]) first = k;
-    const int nrej = min(first, n_wl - w0);
-    if (int(threadIdx.x) < nrej) admitted[w0 + threadIdx.x] = 0;
-    if (first < kAdmitWindow) {  // admit it: AddUsage over its records, every thread a share
-      const int wa = w0 + first;
-      const int64_t r0 = wl_off[wa], r1 = wl_off[wa + 1];
-      for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
-        const kueue_tas_fits_req r = reqs[i];
-        uint32_t bits = 0;
-        for (int k = 0; k < r.num_terms; k++) {
-          const kueue_tas_fits_term t = terms[r.term_begin + k];
-          if (t.col >= 0) {  // the host gives every usage resource a column first
-            sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
-                              (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
-            bits |= 1u << t.col;
-          }
-        }
-        if (pods_col >= 0) {
-          sink += atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
-                            (unsigned long long)int64_t(r.count));
-          bits |= 1u << pods_col;
-        }
-        sink += atomicOr(usage_present + r.leaf, bits);
-        if (in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
-        else sink += atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+    // the window in order (block-uniform control flow)
+    const int wend = min(kAdmitWindow, n_wl - w0);
+    int k = 0, nadm = 0;
+    for (; k < wend; k++) {
+      if (!sh_fit[k]) {  // final rejection
+        if (wave == k && lane == 0) admitted[w0 + k] = 0;
+        continue;
       }
-      if (threadIdx.x == 0) admitted[wa] = 1;
-      w0 = wa + 1;
-      // the admission's usage atomics complete (agent scope) before any wave
-      // of the next window reads usage through L2 (the barrier
-      // alone does not order them)
-      __threadfence();
-    } else {
-      w0 += kAdmitWindow;
+      if (nadm > 0) {  // a later fitting candidate: its check holds unless it shares a leaf with this round's admissions
+        if (!chain) break;
+        if (wave == k) {
+          bool hit = false;
+          for (int64_t base = r0; base < r1 && !hit; base += kWave) {
+            const int64_t i = base + lane;
+            const int32_t leaf = i < r1 ? recs[i].leaf : -1;
+            hit = ballot(leaf >= 0 && ((round_lds[leaf >> 5] >> (leaf & 31)) & 1u)) != 0;
+          }
+          if (lane == 0) sh_conf = hit ? 1 : 0;
+        }
+        __syncthreads();
+        if (sh_conf) break;
+      }
+      if (wave == k) {  // admit: AddUsage over its records, the wave's lanes a share each
+        for (int64_t i = r0 + lane; i < r1; i += kWave) {
+          const kueue_tas_fits_req r = reqs[i];
+          uint32_t bits = 0;
+          for (int q = 0; q < r.num_terms; q++) {
+            const kueue_tas_fits_term t = terms[r.term_begin + q];
+            if (t.col >= 0) {  // the host gives every usage resource a column first
+              atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
+                        (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
+              bits |= 1u << t.col;
+            }
+          }
+          if (pods_col >= 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+                      (unsigned long long)int64_t(r.count));
+            bits |= 1u << pods_col;
+          }
+          atomicOr(usage_present + r.leaf, bits);
+          if (in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+          else atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
+          if (chain) atomicOr(round_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+        }
+        if (lane == 0) admitted[w0 + k] = 1;
+      }
+      nadm++;
+      if (chain) __syncthreads();  // the round's leaves visible to the next candidate's overlap check
     }
+    // candidates w0 .. w0 + k - 1 are decided; w0 + k (if any) is checked again
+    admit_drain();  // this wave's atomics performed at L2 before any wave's next loads
+    if (chain && nadm > 0)
+      for (int q = threadIdx.x; q < nwords; q += blockDim.x) round_lds[q] = 0;
     __syncthreads();
+    w0 += k;
   }
-  if (threadIdx.x == 0) admitted[n_wl] = int32_t(uint32_t(sink));
 }
 
 }  // namespace ktas

@@ -90,6 +90,7 @@ inline void drain_all() {
 inline void __syncthreads() { emu::block_barrier(); }
 #define __builtin_amdgcn_fence(order, scope) emu::wave_barrier()
 #define __builtin_amdgcn_wave_barrier() emu::wave_barrier()
+#define __builtin_amdgcn_s_waitcnt(x) ((void)(x))  // the emulator's memory is sequentially consistent
 
 inline int __lane_of_cur() { return int(emu::cur()->tid.x & 63u); }
 template <typename T>
