@@ -480,18 +480,24 @@ def widened_rows(a, snap, snap_doc, mine, synth):
         nd["name"] = f"{nd['name']}-join{k}"
         nd["labels"][host] = f"{nd['labels'][host]}-join{k}"
         joins.append(nd)
+    c0 = snap.snapshot_counters()
     t0 = time.perf_counter()
     add1_rebuilt = snap.update_nodes(joins[:1])
     add1_ms = (time.perf_counter() - t0) * 1e3
+    add1_detail = snap.last_update_detail()
     t0 = time.perf_counter()
     add_rebuilt = snap.update_nodes(joins[1:])
     add_ms = (time.perf_counter() - t0) * 1e3
+    add_detail = snap.last_update_detail()
+    c1 = snap.snapshot_counters()
     return {"single_call_ms": {"median": round(lat[len(lat) // 2], 3), "p90": round(lat[int(len(lat) * 0.9)], 3),
                                "calls": len(lat), "path": "kueue_tas_host_find (JSON) on the C3 snapshot"},
             "node_leave_ms_per_64": round(leave_ms, 3), "node_return_ms_per_64": round(return_ms, 3),
             "node_leave_return_rebuilt": bool(left_rebuilt or back_rebuilt),
             "node_add_ms": round(add1_ms, 3), "node_add_ms_per_64": round(add_ms, 3),
             "node_add_rebuilt": bool(add1_rebuilt or add_rebuilt),
+            "node_add_device": {"loads": c1[0] - c0[0], "splices": c1[1] - c0[1]},
+            "node_add_detail_ms": {"first": add1_detail, "per_64": add_detail},
             "node_replacement_ms": None if rep_ms is None else round(rep_ms, 3), "node_replacement_ok": rep_ok,
             "pod_events_ms_per_64": round(pod_ms, 3),
             "node_updates_ms_per_64": round(node_ms, 3), "node_updates_rebuilt": rebuilt,
