@@ -218,9 +218,6 @@ typedef struct {
  * the device's entry tags (kueue_tas_snapshot_set_leaf_tags; test knob: both
  * must agree) */
 #define KUEUE_TAS_CFG_HOST_VALUES 64
-/* keep single-run fill chunks with uniform leaf parents at two leaves per
- * thread instead of four (test knob: both paths must agree) */
-#define KUEUE_TAS_CFG_NO_QUAD_FILL 128
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

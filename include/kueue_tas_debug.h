@@ -72,7 +72,6 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: two adjacent leaves per thread (kPairLP) */
 #define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
 #define KUEUE_TAS_PATH_RAGGED_PAIR 32768u       /* fill_pair_kernel on ragged leaf parents (128-leaf slots, segmented scans) */
-#define KUEUE_TAS_PATH_QUAD 65536u              /* fill_pair_kernel with four leaves per thread (single-run chunks) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 /* Stage events: on (default), every stage of kueue_tas_last_stage_times is
  * timed; off, only the fill bracket is (the other events are pure

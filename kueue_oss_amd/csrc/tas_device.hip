@@ -191,7 +191,6 @@ struct kueue_tas_ctx {
   int list_cap = 1024;
   bool inline_stats = true;   // ExclusionStats counted in the fill (KUEUE_TAS_CFG_SPLIT_STATS: fill_exclusion_kernel)
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
-  bool quad_fill = true;      // four leaves per thread on single-run chunks (KUEUE_TAS_CFG_NO_QUAD_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
   bool labels16 = false;      // every staged label column's value ids < 2^16 (packed nodeSelector compare)
@@ -327,7 +326,6 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
     c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
     c->fused_top = (cfg->flags & KUEUE_TAS_CFG_FUSED_TOP) != 0;
-    c->quad_fill = (cfg->flags & KUEUE_TAS_CFG_NO_QUAD_FILL) == 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -1983,9 +1981,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     const bool pair = c->pair_fill && staged_fill &&
                       (ragged_pair || (c->rack_fanout >= 0 && (c->rack_fanout == 0 || c->rack_fanout >= kPairLP)));
     const unsigned pgx = ragged_pair ? unsigned((s.n_wave_slots2 + 3) / 4) : unsigned((s.N + kPairTile - 1) / kPairTile);
-    // single-run chunks with uniform fan-out >= 4 (or none): four leaves per thread
-    const bool quad = pair && !ragged_pair && c->quad_fill && (c->rack_fanout == 0 || c->rack_fanout >= 4);
-    const unsigned pgx4 = unsigned((s.N + 4 * kFillThreads - 1) / (4 * kFillThreads));
     if (b.nstat) {
       // sized for the tile grid: fill_exclusion_kernel (split stats) writes one partial per tile
       HIPCHK(c, c->d_fill_stats.ensure(size_t(nfill) * std::max(grid.x, nblk_fill) * size_t(nstat)));
@@ -2024,21 +2019,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       if (count <= 0) return;
       constexpr int NSv = decltype(ns)::value;
       constexpr bool TSv = decltype(tsv)::value, MRv = decltype(mr)::value;
-      if constexpr (!MRv) {
-        if (quad) {  // four leaves per thread (the stats partials past its tiles zeroed by the kernel)
-          c->fill_paths |= KUEUE_TAS_PATH_PAIR | KUEUE_TAS_PATH_QUAD;
-          const dim3 pg(pgx4, unsigned(count));
-          if (gl && b.rack_fanout == 32)
-            hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, false, true, 32, 4>), pg, dim3(256), 0, st, s, b, umask, first);
-          else if (gl)
-            hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, false, true, 0, 4>), pg, dim3(256), 0, st, s, b, umask, first);
-          else if (b.rack_fanout == 32)
-            hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, false, false, 32, 4>), pg, dim3(256), 0, st, s, b, umask, first);
-          else
-            hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, false, false, 0, 4>), pg, dim3(256), 0, st, s, b, umask, first);
-          return;
-        }
-      }
       if (pair) {  // kPairLP leaves per thread
         c->fill_paths |= KUEUE_TAS_PATH_PAIR;
         const dim3 pg(pgx, unsigned(count));

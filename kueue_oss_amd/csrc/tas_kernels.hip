@@ -1195,17 +1195,10 @@ struct OpOr {
 // MR: chunks of several signature runs (CountIn again at each run's first
 // position, the leaves' remaining capacity kept in registers), as the
 // staged kernel's MR.
-// LP: leaves per thread, kPairLP or 4 (single-run chunks with uniform or no
-// fused parents: the per-class scalar work paid once per 256 leaves; the
-// leaves' capacity columns die after the chunk's one CountIn, so four leaves
-// fit the register budget of two)
-template <int NS, bool TS, bool MR, bool GL, int FC, int LP = kPairLP>  // FC: 32 compile-time fan-out, 0: b.rack_fanout
-                                                                       // (or none), -1: ragged parents in 128-leaf
-                                                                       // slots (DevSnap::wave_tab2)
+template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none),
+                                                      // -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
 __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
-  static_assert(LP == kPairLP || (LP == 4 && FC >= 0 && !MR), "four leaves per thread: single-run, uniform parents");
-  constexpr int kTile = LP * kFillThreads;  // leaves per block
   __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
@@ -1223,25 +1216,25 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // then the chunk's records: both sets of loads in flight together
   const int lane = lane_id();
   const int N = s.N;
-  int leaf0 = tile * kTile + LP * int(threadIdx.x);
-  int slot_len = N - tile * kTile;  // leaves of this lane's window from the window's first
+  int leaf0 = tile * kPairTile + kPairLP * int(threadIdx.x);
+  int slot_len = N - tile * kPairTile;  // leaves of this lane's window from the window's first
   if constexpr (FC < 0) {  // this wave's 128-leaf slot of whole parents
     const int slot = tile * 4 + int(threadIdx.x >> 6);
     const int2 wt = slot < s.n_wave_slots2 ? s.wave_tab2[slot] : make_int2(0, 0);
-    leaf0 = wt.x + LP * lane;
+    leaf0 = wt.x + kPairLP * lane;
     slot_len = wt.y;
   }
   const int gleaf0 = s.level_off[s.L - 1] + leaf0;
-  bool valid[LP];
+  bool valid[kPairLP];
   int scol[NS];
-  int64_t cap[LP][NS], used[LP][NS];
-  uint32_t fp[LP], up[LP];
-  int prof[LP];
-  int32_t lab[LP][kStagedLabels];
+  int64_t cap[kPairLP][NS], used[kPairLP][NS];
+  uint32_t fp[kPairLP], up[kPairLP];
+  int prof[kPairLP];
+  int32_t lab[kPairLP][kStagedLabels];
 #pragma unroll
-  for (int j = 0; j < LP; j++) {
+  for (int j = 0; j < kPairLP; j++) {
     const int leaf = leaf0 + j;
-    if constexpr (FC < 0) valid[j] = LP * lane + j < slot_len;
+    if constexpr (FC < 0) valid[j] = kPairLP * lane + j < slot_len;
     else valid[j] = leaf < N;
     fp[j] = valid[j] ? s.free_present[leaf] : 0u;
     up[j] = valid[j] ? s.usage_present[leaf] : 0u;
@@ -1250,9 +1243,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     for (int k = 0; k < kStagedLabels; k++)
       lab[j][k] = (valid[j] && s.label_values && k < s.K) ? s.label_values[int64_t(k) * N + leaf] : 0;
   }
-  uint32_t pk_lo[LP], pk_hi[LP];  // the staged label ids as one 64-bit key (FillEvalParams::sel_fast)
+  uint32_t pk_lo[kPairLP], pk_hi[kPairLP];  // the staged label ids as one 64-bit key (FillEvalParams::sel_fast)
 #pragma unroll
-  for (int j = 0; j < LP; j++) {
+  for (int j = 0; j < kPairLP; j++) {
     pk_lo[j] = (uint32_t(lab[j][0]) & 0xffffu) | (uint32_t(lab[j][1]) << 16);
     pk_hi[j] = (uint32_t(lab[j][2]) & 0xffffu) | (uint32_t(lab[j][3]) << 16);
   }
@@ -1263,7 +1256,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       scol[k] = m ? __builtin_ctz(m) : -1;
       if (m) m &= m - 1;
 #pragma unroll
-      for (int j = 0; j < LP; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         cap[j][k] = used[j][k] = 0;
         if (valid[j] && scol[k] >= 0) {
           cap[j][k] = s.free_cap[int64_t(scol[k]) * N + leaf0 + j];
@@ -1283,15 +1276,15 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   }
   __syncthreads();
   // ---- base signature: remaining capacity per leaf ----
-  bool leader, live[LP];
-  uint32_t pres[LP];
+  bool leader, live[kPairLP];
+  uint32_t pres[kPairLP];
   {
     const uint32_t flags = uint32_t(uni(sh_pos[0].p.pad[0]));
     const int abeg = uni(sh_pos[0].p.pad[1]), aend = uni(sh_pos[0].p.pad[2]);
     leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool sim = (flags & KUEUE_TAS_F_SIMULATE_EMPTY) != 0;
 #pragma unroll
-    for (int j = 0; j < LP; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
       live[j] = valid[j] && !leaf_out(s, leaf);
       pres[j] = fp[j] | (sim ? 0u : up[j]);
@@ -1324,16 +1317,16 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
                          uint32_t lmask, uint32_t presm, bool sub_leader, int* lim_out) -> int32_t {
     return count_slots_sel<NS>(scol, cp, terms, mask, lterms, lmask, presm, sub_leader, lim_out);
   };
-  int32_t state0[LP] = {}, swl0[LP] = {}, ls0[LP] = {};
-  int lim0[LP];
+  int32_t state0[kPairLP] = {}, swl0[kPairLP] = {}, ls0[kPairLP] = {};
+  int lim0[kPairLP];
 #pragma unroll
-  for (int j = 0; j < LP; j++) lim0[j] = -1;
+  for (int j = 0; j < kPairLP; j++) lim0[j] = -1;
   auto count_run = [&](int e) {  // CountIn of the run starting at chunk position e, both leaves
     const uint32_t rmask = uint32_t(uni(sh_pos[e].p.rmask)), lmask = uint32_t(uni(sh_pos[e].p.lmask));
     const DevTerm* wt = sh_pos[e].term;
     const DevTerm* lt = wt + NS;
 #pragma unroll
-    for (int j = 0; j < LP; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       state0[j] = swl0[j] = ls0[j] = 0;
       lim0[j] = -1;
       if (!live[j]) continue;
@@ -1353,7 +1346,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // ragged slots: the parents of the lane's two leaves, which of them start
   // (head) or end (tail) a parent, and the lane holding the start of its
   // second leaf's parent (the segmented scans' bound)
-  int rp[LP] = {}, seg0 = 0, st0 = 0, st1 = 0;
+  int rp[kPairLP] = {}, seg0 = 0, st0 = 0, st1 = 0;
   bool head0 = false, head1 = false, tail0 = false, tail1 = false;
   if constexpr (FC < 0) {
     rp[0] = valid[0] ? s.leaf_parent[leaf0] : -1;
@@ -1368,19 +1361,19 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
     seg0 = 63 - __builtin_clzll((H & upto) | 1ull);
     // slot positions (2 * lane + j) where the leaves' parents start
-    const int hpos = head1 ? LP * lane + 1 : LP * lane;
+    const int hpos = head1 ? kPairLP * lane + 1 : kPairLP * lane;
     st1 = __shfl(hpos, seg0);
     const int st1_prev = __shfl(st1, lane > 0 ? lane - 1 : 0);
-    st0 = head0 ? LP * lane : st1_prev;
+    st0 = head0 ? kPairLP * lane : st1_prev;
   }
   const int rack_f = FC > 0 ? FC : FC < 0 ? -1 : b.rack_fanout;  // fan-out of the fused parents (0: none, -1: ragged)
-  const int half = rack_f / LP;                    // lanes per parent
+  const int half = rack_f / kPairLP;                    // lanes per parent
   const int parent = rack_f > 0 ? leaf0 / rack_f : 0;
   const int gpos = rack_f > 0 ? (lane & (half - 1)) : 0;  // this lane's group within its parent
   // every leaf of the block's tile exists and its counter words are
-  // LP-aligned (level offsets are multiples of 4): block-uniform, so the
+  // kPairLP-aligned (level offsets are multiples of 4): block-uniform, so the
   // stores below take a scalar branch, not a per-lane exec mask
-  const bool full_tile = FC >= 0 && (tile + 1) * kTile <= N && (s.level_off[s.L - 1] & (LP - 1)) == 0;
+  const bool full_tile = FC >= 0 && (tile + 1) * kPairTile <= N && (s.level_off[s.L - 1] & (kPairLP - 1)) == 0;
   const int64_t SD = s.SD;
   for (int e = 0; e < ne; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
@@ -1397,8 +1390,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // exclusion wins: taint, nodeSelector, affinity, required domain, then
     // a resource giving state 0): every condition below is either
     // wave-uniform (a scalar branch) or a v_cndmask, no divergent branch
-    int32_t state[LP], swl[LP], ls[LP], ss[LP], sswl[LP];
-    int kind[LP], id[LP];
+    int32_t state[kPairLP], swl[kPairLP], ls[kPairLP], ss[kPairLP], sswl[kPairLP];
+    int kind[kPairLP], id[kPairLP];
     const bool hn = s.lowest_is_hostname != 0;
     int4 c0 = make_int4(0, 0, 0, 0), c1 = c0, v0 = c0, v1 = c0;
     if (hn && nsel > 0) {
@@ -1420,7 +1413,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       sel_whi = uint32_t(uni(m.w));
     }
 #pragma unroll
-    for (int j = 0; j < LP; j++) {
+    for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
       bool ok = live[j];
       int k = (valid[j] && !live[j]) ? EX_DEAD : EX_NONE;
@@ -1498,13 +1491,13 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       }
     }
     int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
-    auto storev = [&](int64_t off, const int32_t (&v)[LP]) {  // counter words of leaves leaf0 .. leaf0 + LP - 1
+    auto storev = [&](int64_t off, const int32_t (&v)[kPairLP]) {  // counter words of leaves leaf0 .. leaf0 + kPairLP - 1
       if (full_tile) {
-        if constexpr (LP == 4) *reinterpret_cast<int4*>(base + off + gleaf0) = make_int4(v[0], v[1], v[2], v[3]);
+        if constexpr (kPairLP == 4) *reinterpret_cast<int4*>(base + off + gleaf0) = make_int4(v[0], v[1], v[2], v[3]);
         else *reinterpret_cast<int2*>(base + off + gleaf0) = make_int2(v[0], v[1]);
       } else {
 #pragma unroll
-        for (int j = 0; j < LP; j++)
+        for (int j = 0; j < kPairLP; j++)
           if (valid[j]) base[off + gleaf0 + j] = v[j];
       }
     };
@@ -1520,7 +1513,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       const int32_t inner = p_inner;
       int32_t cap2 = 0, slc = 0, lead = 0, minD = 0x7fffffff, minSD = 0x7fffffff, has = 0;
 #pragma unroll
-      for (int j = 0; j < LP; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         int32_t cs = state[j], csw = swl[j];
         if (inner != 0 && inner != 1) {
           cs = w_mul(go_div32(cs, inner), inner);
@@ -1546,18 +1539,18 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         lead = group_reduce(lead, half, OpMax());
         has = group_reduce(has, half, OpMax());
       }
-      // positive children: bits LP*gpos .. LP*gpos + LP - 1 of the parent's mask
+      // positive children: bits kPairLP*gpos .. kPairLP*gpos + kPairLP - 1 of the parent's mask
       uint32_t pb = 0;
 #pragma unroll
-      for (int j = 0; j < LP; j++) pb |= uint32_t(valid[j] && ss[j] > 0) << j;
+      for (int j = 0; j < kPairLP; j++) pb |= uint32_t(valid[j] && ss[j] > 0) << j;
       uint64_t posm;
       if (rack_f <= 32) {
-        posm = uint32_t(group_reduce(int32_t(pb << (LP * gpos)), half, OpOr()));
+        posm = uint32_t(group_reduce(int32_t(pb << (kPairLP * gpos)), half, OpOr()));
       } else {
-        const int lo_groups = 32 / LP;
-        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < lo_groups ? pb << (LP * gpos) : 0u), half, OpOr()));
+        const int lo_groups = 32 / kPairLP;
+        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < lo_groups ? pb << (kPairLP * gpos) : 0u), half, OpOr()));
         const uint32_t hi =
-            uint32_t(group_reduce(int32_t(gpos >= lo_groups ? pb << (LP * gpos - 32) : 0u), half, OpOr()));
+            uint32_t(group_reduce(int32_t(gpos >= lo_groups ? pb << (kPairLP * gpos - 32) : 0u), half, OpOr()));
         posm = (uint64_t(hi) << 32) | lo;
       }
       if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
@@ -1585,9 +1578,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // takes the previous lane's scan plus that leaf
     if constexpr (FC < 0) {
       const int32_t inner = p_inner;
-      int32_t v[LP];
+      int32_t v[kPairLP];
 #pragma unroll
-      for (int j = 0; j < LP; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         v[j] = state[j];
         if (inner != 0 && inner != 1) v[j] = w_mul(go_div32(v[j], inner), inner);
       }
@@ -1609,8 +1602,8 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       const bool masks = b.rack_pos != nullptr;  // every parent <= 64 leaves
       uint64_t pm0 = 0, pm1 = 0;
       if (masks) {  // positive children: disjoint bits per parent, so the segment sums are its ORs
-        const uint64_t m0 = (valid[0] && ss[0] > 0) ? 1ull << ((LP * lane - st0) & 63) : 0ull;
-        const uint64_t m1 = (valid[1] && ss[1] > 0) ? 1ull << ((LP * lane + 1 - st1) & 63) : 0ull;
+        const uint64_t m0 = (valid[0] && ss[0] > 0) ? 1ull << ((kPairLP * lane - st0) & 63) : 0ull;
+        const uint64_t m1 = (valid[1] && ss[1] > 0) ? 1ull << ((kPairLP * lane + 1 - st1) & 63) : 0ull;
         int32_t lo0, lo1, hi0, hi1;
         seg_sum(int32_t(uint32_t(m0)), int32_t(uint32_t(m1)), &lo0, &lo1);
         seg_sum(int32_t(uint32_t(m0 >> 32)), int32_t(uint32_t(m1 >> 32)), &hi0, &hi1);
@@ -1636,11 +1629,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // single-lane atomics (exec-mask bookkeeping on the scalar unit)
     if (lds_stats) {
       static_assert(kMaxFillStats == kWave, "one stats slot per lane");
-      int sl[LP];
-      uint64_t m[LP];
+      int sl[kPairLP];
+      uint64_t m[kPairLP];
       uint64_t any = 0;
 #pragma unroll
-      for (int j = 0; j < LP; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         int x = -1;
         x = kind[j] == EX_SELECTOR ? 0 : x;
         x = kind[j] == EX_AFFINITY ? 1 : x;
@@ -1656,12 +1649,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       while (any) {  // wave-uniform: one trip per distinct slot
         int x = 0;
 #pragma unroll
-        for (int j = LP - 1; j >= 0; j--)
+        for (int j = kPairLP - 1; j >= 0; j--)
           if (m[j]) x = bcast(sl[j], __ffsll((unsigned long long)m[j]) - 1);
         int c = 0;
         any = 0;
 #pragma unroll
-        for (int j = 0; j < LP; j++) {
+        for (int j = 0; j < kPairLP; j++) {
           const uint64_t h = ballot(sl[j] == x);
           c += __popcll(h);
           m[j] &= ~h;
@@ -1674,12 +1667,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
     uint64_t anyx = 0;
 #pragma unroll
-    for (int j = 0; j < LP; j++) anyx |= ballot(valid[j] && kind[j] != EX_NONE && kind[j] != EX_DEAD);
+    for (int j = 0; j < kPairLP; j++) anyx |= ballot(valid[j] && kind[j] != EX_NONE && kind[j] != EX_DEAD);
     if (anyx == 0) continue;
     auto count_kind = [&](int k, int slot, int32_t* gl) {
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < LP; j++) c += __popcll(ballot(kind[j] == k));
+      for (int j = 0; j < kPairLP; j++) c += __popcll(ballot(kind[j] == k));
       if (lane == 0 && c) {
         if (lds_stats) atomicAdd(&sh_stats[e][slot], c);
         else atomicAdd(gl, c);
@@ -1690,22 +1683,22 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     if (dom_begin >= 0) count_kind(EX_TOPOLOGY, 2, &b.dom_counts[eid]);
     // per taint / resource id: the first remaining lane's id, both halves counted together
     auto count_ids = [&](int k, int slot0, int32_t* gl) {
-      uint64_t m[LP];
+      uint64_t m[kPairLP];
       uint64_t any = 0;
 #pragma unroll
-      for (int j = 0; j < LP; j++) {
+      for (int j = 0; j < kPairLP; j++) {
         m[j] = ballot(kind[j] == k);
         any |= m[j];
       }
       while (any) {
         int x = 0;  // the id of the first lane / leaf still to count
 #pragma unroll
-        for (int j = LP - 1; j >= 0; j--)
+        for (int j = kPairLP - 1; j >= 0; j--)
           if (m[j]) x = bcast(id[j], __ffsll((unsigned long long)m[j]) - 1);
         int c = 0;
         any = 0;
 #pragma unroll
-        for (int j = 0; j < LP; j++) {
+        for (int j = 0; j < kPairLP; j++) {
           const uint64_t h = ballot(kind[j] == k && id[j] == x);
           c += __popcll(h);
           m[j] &= ~h;

@@ -228,12 +228,11 @@ class TASFlavorSnapshot:
     def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
                  packed_entries: bool = False, inline_stats: bool = False,
                  pair_fill: bool = True, serial_admit: bool = False, split_stats: bool = False,
-                 fused_top: bool = False, host_values: bool = False, quad_fill: bool = True):
+                 fused_top: bool = False, host_values: bool = False):
         self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0)
                               | (0 if pair_fill else 4) | (8 if serial_admit else 0) | (16 if split_stats else 0)
-                              | (32 if fused_top else 0) | (64 if host_values else 0)
-                              | (0 if quad_fill else 128))
+                              | (32 if fused_top else 0) | (64 if host_values else 0))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:

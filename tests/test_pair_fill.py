@@ -6,10 +6,7 @@ fused fan-outs 2 / 4 / 8 / 16 / 32 / 64, no fused parents (fan-out > 64, odd
 leaf counts: the partial last group), leader groups, taints, selectors and
 affinity; the one-leaf staged kernel (KUEUE_TAS_CFG_NO_PAIR_FILL) must give
 the same results (that run also takes the KUEUE_TAS_CFG_FUSED_TOP roll-up:
-rollup_top_kernel), and so must two leaves per thread where the default
-takes four (single-run chunks with uniform fan-out >= 4 or no fused parents:
-KUEUE_TAS_PATH_QUAD; KUEUE_TAS_CFG_NO_QUAD_FILL keeps two).
-kueue_tas_last_fill_paths pins which kernel ran."""
+rollup_top_kernel).  kueue_tas_last_fill_paths pins which kernel ran."""
 import random
 
 import pytest
@@ -18,7 +15,6 @@ import oracle_lib
 from kueue_oss_amd import TASFlavorSnapshot, synth
 
 PAIR = 8192
-QUAD = 65536
 
 
 def _batch(make, doc, wls):
@@ -37,8 +33,7 @@ def _batch(make, doc, wls):
 def _configs(scale):
     """(name, doc, workloads) covering the pair kernel's variants."""
     n = 64 * scale
-    # 400+ workloads: signatures with >= 8 classes, so single-run chunks (four leaves per thread)
-    yield "c3 fan-out 32", *synth.config_c3(seed=3, n_workloads=max(400, 3 * n), shape=(2, 2, 4 * scale, 32))
+    yield "c3 fan-out 32", *synth.config_c3(seed=3, n_workloads=3 * n, shape=(2, 2, 4 * scale, 32))
     yield "c3 fan-out 64", *synth.config_c3(seed=4, n_workloads=n, shape=(2, 2, 2 * scale, 64))
     yield "c3 fan-out 16", *synth.config_c3(seed=5, n_workloads=n, shape=(2, 2, 4 * scale, 16))
     yield "c3 fan-out 4", *synth.config_c3(seed=6, n_workloads=n, shape=(2, 4, 8 * scale, 4))
@@ -48,18 +43,14 @@ def _configs(scale):
     yield "c4 leaders", *synth.config_c4(seed=9, n_workloads=8 * scale, shape=(2, 2, 4 * scale, 16))
 
 
-def _run(make_pair, make_staged, make_two, scale):
+def _run(make_pair, make_staged, scale):
     for name, doc, wls in _configs(scale):
         paths = _batch(make_pair, doc, wls)
         assert paths & PAIR, name
-        if name == "c3 fan-out 32":  # single-run chunks with fan-out >= 4
-            assert paths & QUAD, name
-        assert _batch(make_two, doc, wls) & QUAD == 0, name
         assert _batch(make_staged, doc, wls) & PAIR == 0, name
-    # fan-out 2: one parent per lane (the smallest fused fan-out the kernel takes): two leaves per thread
+    # fan-out 2: one parent per lane (the smallest fused fan-out the kernel takes)
     doc, wls = synth.config_c3(seed=11, n_workloads=64 * scale, shape=(2, 4, 16 * scale, 2))
-    paths = _batch(make_pair, doc, wls)
-    assert paths & PAIR and not paths & QUAD
+    assert _batch(make_pair, doc, wls) & PAIR
 
 
 def _random(make, seed, n):
@@ -78,14 +69,11 @@ def _random(make, seed, n):
 
 
 def test_emulated_pair_fill(emu_lib):  # noqa: F811
-    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib),
-         lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, fused_top=True),
-         lambda d: TASFlavorSnapshot(d, lib=emu_lib, quad_fill=False), 1)
+    _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, fused_top=True), 1)
     assert _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 31, 40) & PAIR
 
 
 @pytest.mark.gpu
 def test_pair_fill_on_gpu():
-    _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False, fused_top=True),
-         lambda d: TASFlavorSnapshot(d, quad_fill=False), 4)
+    _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False, fused_top=True), 4)
     assert _random(lambda d: TASFlavorSnapshot(d), 32, 150) & PAIR
