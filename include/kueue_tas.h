@@ -320,8 +320,11 @@ const int32_t* kueue_tas_last_entries(kueue_tas_ctx* ctx, size_t* num_pairs);
  *  leaf_src:  [N_new] the leaf's index before the splice, or -1 for a joined
  *             leaf (whose row is the next of the new_* rows, in leaf order)
  *  new_*:     the joined leaves' rows, [R][num_new] / [num_new] / [K][num_new]
- * Leaves that had left (kueue_tas_snapshot_set_leaf_live) stay out; leaf tags
- * are cleared; names must be loaded again before a v1beta2 encode. */
+ *  new_leaf_tags: [num_new] the joined leaves' tags when leaf tags are set
+ *             (kueue_tas_snapshot_set_leaf_tags): every resident leaf's tag
+ *             moves with it; NULL clears the tags
+ * Leaves that had left (kueue_tas_snapshot_set_leaf_live) stay out; names
+ * must be loaded again before a v1beta2 encode. */
 typedef struct {
   const kueue_tas_snapshot_desc* topo;
   const int32_t* leaf_src;
@@ -332,6 +335,7 @@ typedef struct {
   const uint32_t* new_usage_present;
   const int32_t* new_taint_profile;  /* NULL when the snapshot has no taint profiles */
   const int32_t* new_label_values;   /* NULL when K == 0 */
+  const uint64_t* new_leaf_tags;     /* NULL: leaf tags cleared */
 } kueue_tas_splice_desc;
 int kueue_tas_snapshot_splice(kueue_tas_ctx* ctx, const kueue_tas_splice_desc* d);
 

@@ -52,6 +52,8 @@ struct DevBuf {
     std::swap(p, o.p);
     std::swap(n, o.n);
   }
+  // ensure with 1/8 headroom when it grows (buffers that grow by a few rows at a time)
+  hipError_t reserve(size_t count) { return count <= n && p ? hipSuccess : ensure(count + count / 8); }
 };
 
 template <typename T>
@@ -265,6 +267,16 @@ struct kueue_tas_ctx {
   // entry tags (kueue_tas_snapshot_set_leaf_tags): per-leaf table in HBM, the
   // per-entry copies in pinned device-mapped host memory beside the entries
   DevBuf<uint64_t> d_leaf_tags;
+  // kueue_tas_snapshot_splice: the gather's targets (the resident columns'
+  // previous buffers after the swap, reused by the next splice) and its
+  // pinned staging (leaf sources and joined rows)
+  DevBuf<int64_t> sp_free, sp_usage;
+  DevBuf<uint32_t> sp_fp, sp_up;
+  DevBuf<int32_t> sp_prof, sp_lab, sp_src;
+  DevBuf<uint64_t> sp_tags;
+  DevBuf<uint8_t> sp_rows;
+  HostBuf<uint8_t> h_load;
+  HostBuf<uint8_t> h_tab;  // load_impl's re-derived tables (pinned arena, async copies)
   bool leaf_tags_on = false;
   uint64_t* tag_host = nullptr;
   uint64_t* tag_dev = nullptr;
@@ -488,6 +500,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   s.leaf_tag = nullptr;   // leaf tags describe the previous leaves
   s.tag_out = nullptr;
   s.ent_base = nullptr;
+  const bool tags_were_on = c->leaf_tags_on;
   c->leaf_tags_on = false;
   s.n_live = s.N;
   // a splice keeps the leaves that had left out: their flags move with them
@@ -509,6 +522,18 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
       }
     }
   }
+  // the re-derived tables go up through one pinned arena (async copies, one
+  // stream synchronization at the end) instead of a synchronous copy each
+  HIPCHK(c, c->h_tab.ensure(size_t(off) * 8 + N * 9 + (N + 2) * 16 + 4096));
+  size_t arena_pos = 0;
+  auto stage = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    if (!bytes) return hipSuccess;
+    if (arena_pos + bytes > c->h_tab.n) return hipErrorInvalidValue;  // (the bound above covers every table)
+    memcpy(c->h_tab.p + arena_pos, src, bytes);
+    const hipError_t e = hipMemcpyAsync(dst, c->h_tab.p + arena_pos, bytes, hipMemcpyHostToDevice, c->stream);
+    arena_pos += (bytes + 255) / 256 * 256;
+    return e;
+  };
   // CSR offsets
   size_t nco = 0;
   for (int l = 0; l + 1 < s.L; l++) {
@@ -522,58 +547,69 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     const int nn = std::max(sp->num_new, 1);
     const bool prof = c->snap.taint_profile != nullptr;
     const bool lab = s.K > 0 && c->snap.label_values != nullptr;
-    DevBuf<int64_t> f, u;
-    DevBuf<uint32_t> fp, up;
-    DevBuf<int32_t> pr, lb, src;
-    DevBuf<uint8_t> rows;
-    HIPCHK(c, f.ensure(size_t(s.R) * N));
-    HIPCHK(c, u.ensure(size_t(s.R) * N));
-    HIPCHK(c, fp.ensure(N));
-    HIPCHK(c, up.ensure(N));
-    if (prof) HIPCHK(c, pr.ensure(N));
-    if (lab) HIPCHK(c, lb.ensure(size_t(s.K) * N));
-    HIPCHK(c, src.ensure(N));
-    // the joined rows: free | usage | free_present | usage_present | profile | labels
+    const bool tags = tags_were_on && sp->new_leaf_tags != nullptr;
+    HIPCHK(c, c->sp_free.reserve(size_t(s.R) * N));
+    HIPCHK(c, c->sp_usage.reserve(size_t(s.R) * N));
+    HIPCHK(c, c->sp_fp.reserve(N));
+    HIPCHK(c, c->sp_up.reserve(N));
+    if (prof) HIPCHK(c, c->sp_prof.reserve(N));
+    if (lab) HIPCHK(c, c->sp_lab.reserve(size_t(s.K) * N));
+    if (tags) HIPCHK(c, c->sp_tags.reserve(N));
+    HIPCHK(c, c->sp_src.reserve(N));
+    // the joined rows: free | usage | free_present | usage_present | profile | labels | tags
     const size_t o_u = size_t(s.R) * nn * 8, o_fp = 2 * o_u, o_up = o_fp + size_t(nn) * 4, o_pr = o_up + size_t(nn) * 4,
-                 o_lb = o_pr + size_t(nn) * 4, rbytes = o_lb + size_t(std::max(s.K, 1)) * nn * 4;
-    HIPCHK(c, rows.ensure(rbytes));
-    HIPCHK(c, hipMemcpyAsync(src.p, gsrc.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+                 o_lb = o_pr + size_t(nn) * 4, o_tg = (o_lb + size_t(std::max(s.K, 1)) * nn * 4 + 7) / 8 * 8,
+                 rbytes = o_tg + size_t(nn) * 8;
+    HIPCHK(c, c->sp_rows.reserve(rbytes));
+    // one pinned staging area: leaf sources, then the joined rows
+    const size_t o_rows = (N * 4 + 255) / 256 * 256;
+    HIPCHK(c, c->h_load.ensure(o_rows + rbytes));
+    uint8_t* hl = c->h_load.p;
+    if (N) memcpy(hl, gsrc.data(), N * 4);
+    uint8_t* hr = hl + o_rows;
     if (sp->num_new > 0) {
       const size_t k = size_t(sp->num_new);
       if (s.R) {
-        HIPCHK(c, hipMemcpyAsync(rows.p, sp->new_free_capacity, size_t(s.R) * k * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(rows.p + o_u, sp->new_tas_usage, size_t(s.R) * k * 8, hipMemcpyHostToDevice, c->stream));
+        memcpy(hr, sp->new_free_capacity, size_t(s.R) * k * 8);
+        memcpy(hr + o_u, sp->new_tas_usage, size_t(s.R) * k * 8);
       }
-      HIPCHK(c, hipMemcpyAsync(rows.p + o_fp, sp->new_free_present, k * 4, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(rows.p + o_up, sp->new_usage_present, k * 4, hipMemcpyHostToDevice, c->stream));
-      if (prof && sp->new_taint_profile)
-        HIPCHK(c, hipMemcpyAsync(rows.p + o_pr, sp->new_taint_profile, k * 4, hipMemcpyHostToDevice, c->stream));
-      if (lab) HIPCHK(c, hipMemcpyAsync(rows.p + o_lb, sp->new_label_values, size_t(s.K) * k * 4, hipMemcpyHostToDevice, c->stream));
+      memcpy(hr + o_fp, sp->new_free_present, k * 4);
+      memcpy(hr + o_up, sp->new_usage_present, k * 4);
+      if (prof && sp->new_taint_profile) memcpy(hr + o_pr, sp->new_taint_profile, k * 4);
+      if (lab) memcpy(hr + o_lb, sp->new_label_values, size_t(s.K) * k * 4);
+      if (tags) memcpy(hr + o_tg, sp->new_leaf_tags, k * 8);
       for (size_t i = 0; i < k; i++) {
         if (sp->new_taint_profile) c->num_profiles = std::max(c->num_profiles, sp->new_taint_profile[i] + 1);
         for (int q = 0; q < std::min(s.K, kStagedLabels) && sp->new_label_values; q++)
           if (uint32_t(sp->new_label_values[size_t(q) * k + i]) > 0xffffu) c->labels16 = false;
       }
     }
+    if (N) HIPCHK(c, hipMemcpyAsync(c->sp_src.p, hl, N * 4, hipMemcpyHostToDevice, c->stream));
+    if (sp->num_new > 0) HIPCHK(c, hipMemcpyAsync(c->sp_rows.p, hr, rbytes, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* rows = c->sp_rows.p;
     if (N) {
-      hipLaunchKernelGGL(splice_leaves_kernel, dim3(unsigned((N + 255) / 256)), dim3(256), 0, c->stream, src.p, int(N),
-                         old_N, s.R, lab ? s.K : 0, nn, c->d_free.p, c->d_usage.p, c->d_free_present.p,
+      hipLaunchKernelGGL(splice_leaves_kernel, dim3(unsigned((N + 255) / 256)), dim3(256), 0, c->stream, c->sp_src.p,
+                         int(N), old_N, s.R, lab ? s.K : 0, nn, c->d_free.p, c->d_usage.p, c->d_free_present.p,
                          c->d_usage_present.p, prof ? c->d_taint_profile.p : nullptr, lab ? c->d_labels.p : nullptr,
-                         reinterpret_cast<const int64_t*>(rows.p), reinterpret_cast<const int64_t*>(rows.p + o_u),
-                         reinterpret_cast<const uint32_t*>(rows.p + o_fp), reinterpret_cast<const uint32_t*>(rows.p + o_up),
-                         (prof && sp->new_taint_profile) ? reinterpret_cast<const int32_t*>(rows.p + o_pr) : nullptr,
-                         reinterpret_cast<const int32_t*>(rows.p + o_lb), f.p, u.p, fp.p, up.p, prof ? pr.p : nullptr,
-                         lab ? lb.p : nullptr);
+                         reinterpret_cast<const int64_t*>(rows), reinterpret_cast<const int64_t*>(rows + o_u),
+                         reinterpret_cast<const uint32_t*>(rows + o_fp), reinterpret_cast<const uint32_t*>(rows + o_up),
+                         (prof && sp->new_taint_profile) ? reinterpret_cast<const int32_t*>(rows + o_pr) : nullptr,
+                         reinterpret_cast<const int32_t*>(rows + o_lb), c->sp_free.p, c->sp_usage.p, c->sp_fp.p,
+                         c->sp_up.p, prof ? c->sp_prof.p : nullptr, lab ? c->sp_lab.p : nullptr,
+                         tags ? c->d_leaf_tags.p : nullptr, reinterpret_cast<const uint64_t*>(rows + o_tg),
+                         tags ? c->sp_tags.p : nullptr);
       HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->d_free.swap(f);
-    c->d_usage.swap(u);
-    c->d_free_present.swap(fp);
-    c->d_usage_present.swap(up);
-    if (prof) c->d_taint_profile.swap(pr);
-    if (lab) c->d_labels.swap(lb);
-    // f, u, ... now hold the old columns and are freed here
+    // the gathered columns go live; the previous ones become the next
+    // splice's targets (stream order puts every later kernel after the gather)
+    c->d_free.swap(c->sp_free);
+    c->d_usage.swap(c->sp_usage);
+    c->d_free_present.swap(c->sp_fp);
+    c->d_usage_present.swap(c->sp_up);
+    if (prof) c->d_taint_profile.swap(c->sp_prof);
+    if (lab) c->d_labels.swap(c->sp_lab);
+    if (tags) c->d_leaf_tags.swap(c->sp_tags);
+    c->leaf_tags_on = tags;
     s.free_cap = c->d_free.p;
     s.tas_usage = c->d_usage.p;
     s.free_present = c->d_free_present.p;
@@ -582,18 +618,10 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     s.label_values = lab ? c->d_labels.p : nullptr;
     if (c->n_dead > 0) {  // the leaves that had left, at their new indices
       HIPCHK(c, c->d_dead.ensure(N));
-      HIPCHK(c, hipMemcpy(c->d_dead.p, c->h_dead.data(), N, hipMemcpyHostToDevice));
+      HIPCHK(c, stage(c->d_dead.p, c->h_dead.data(), N));
       s.leaf_dead = c->d_dead.p;
       s.n_live = int32_t(int64_t(N) - c->n_dead);
     }
-    f.release();
-    u.release();
-    fp.release();
-    up.release();
-    pr.release();
-    lb.release();
-    src.release();
-    rows.release();
   } else {
   HIPCHK(c, c->d_free.ensure(size_t(s.R) * N));
   HIPCHK(c, c->d_usage.ensure(size_t(s.R) * N));
@@ -636,7 +664,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     for (int l = 0; l < s.L; l++)
       for (int i = 0; i < d->level_sizes[l]; i++) ranks[size_t(s.level_off[l] + i)] = d->domain_id_rank[src++];
     HIPCHK(c, c->d_id_rank.ensure(size_t(off)));
-    HIPCHK(c, hipMemcpy(c->d_id_rank.p, ranks.data(), size_t(off) * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, stage(c->d_id_rank.p, ranks.data(), size_t(off) * 4));
     s.id_rank = c->d_id_rank.p;
   }
   // leaves' parents with a uniform power-of-two fan-out F <= 64 in leaf order:
@@ -687,9 +715,9 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     if (ok) {
       tab.push_back(make_int2(cb, cn));
       HIPCHK(c, c->d_wave_tab2.ensure(tab.size()));
-      HIPCHK(c, hipMemcpy(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+      HIPCHK(c, stage(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2)));
       HIPCHK(c, c->d_leaf_parent.ensure(N));
-      HIPCHK(c, hipMemcpy(c->d_leaf_parent.p, lp.data(), N * 4, hipMemcpyHostToDevice));
+      HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
       s.wave_tab2 = c->d_wave_tab2.p;
       s.n_wave_slots2 = int32_t(tab.size());
       s.leaf_parent = c->d_leaf_parent.p;
@@ -720,9 +748,9 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     if (ok) {
       tab.push_back(make_int2(cb, cn));
       HIPCHK(c, c->d_wave_tab.ensure(tab.size()));
-      HIPCHK(c, hipMemcpy(c->d_wave_tab.p, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+      HIPCHK(c, stage(c->d_wave_tab.p, tab.data(), tab.size() * sizeof(int2)));
       HIPCHK(c, c->d_leaf_parent.ensure(N));
-      HIPCHK(c, hipMemcpy(c->d_leaf_parent.p, lp.data(), N * 4, hipMemcpyHostToDevice));
+      HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
       s.wave_tab = c->d_wave_tab.p;
       s.n_wave_slots = int32_t(tab.size());
       s.leaf_parent = c->d_leaf_parent.p;
@@ -738,7 +766,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
         for (int j = co[p]; j < co[p + 1]; j++) parent[size_t(s.level_off[l + 1] + j)] = s.level_off[l] + p;
     }
     HIPCHK(c, c->d_parent.ensure(parent.size()));
-    HIPCHK(c, hipMemcpy(c->d_parent.p, parent.data(), parent.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, stage(c->d_parent.p, parent.data(), parent.size() * 4));
   }
   c->names_loaded = false;
   HIPCHK(c, hipStreamSynchronize(c->stream));

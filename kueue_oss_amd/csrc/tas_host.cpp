@@ -645,13 +645,41 @@ class FlavorSnapshot {
     mirrorPending.insert(mirrorPending.end(), d, d + n);
     if (mirrorPending.size() > (size_t(1) << 22)) flush_mirror();
   }
+  // a long backlog (rounds of admissions since the mirror was last read) is
+  // folded per (column, leaf) first, so each distinct key costs its two map
+  // updates once (a key whose deltas cancel still gets its entry: a present
+  // zero differs from an absent key, requests.go:189-192)
+  std::vector<int64_t> mirrorAcc;  // [R][N] folded deltas (zero outside a flush)
+  std::vector<uint32_t> mirrorKeys;
+  std::vector<uint8_t> mirrorSeen;
   void flush_mirror() {
-    for (auto& d : mirrorPending) {
-      const std::string& res = cols[size_t(d.col)];
-      int64_t& v = tasUsage[size_t(d.leaf)][res];
-      v = add64(v, d.delta);
-      int64_t& u = usageByDomain[leafId[size_t(d.leaf)]][res];
-      u = add64(u, d.delta);
+    auto apply = [&](int32_t leaf, int32_t col, int64_t delta) {
+      const std::string& res = cols[size_t(col)];
+      int64_t& v = tasUsage[size_t(leaf)][res];
+      v = add64(v, delta);
+      int64_t& u = usageByDomain[leafId[size_t(leaf)]][res];
+      u = add64(u, delta);
+    };
+    const size_t N = size_t(this->N()), R = cols.size();
+    if (mirrorPending.size() < 4096 || N * R >= (size_t(1) << 32)) {
+      for (auto& d : mirrorPending) apply(d.leaf, d.col, d.delta);
+    } else {
+      mirrorAcc.resize(N * R, 0);
+      mirrorSeen.resize(N * R, 0);
+      mirrorKeys.clear();
+      for (auto& d : mirrorPending) {
+        const uint32_t key = uint32_t(size_t(d.col) * N + size_t(d.leaf));
+        if (!mirrorSeen[key]) {
+          mirrorSeen[key] = 1;
+          mirrorKeys.push_back(key);
+        }
+        mirrorAcc[key] = add64(mirrorAcc[key], d.delta);
+      }
+      for (uint32_t key : mirrorKeys) {
+        apply(int32_t(key % N), int32_t(key / N), mirrorAcc[key]);
+        mirrorAcc[key] = 0;
+        mirrorSeen[key] = 0;
+      }
     }
     mirrorPending.clear();
   }
@@ -1290,62 +1318,73 @@ class FlavorSnapshot {
     ktas_pool::HostPool::get().run(tasks.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks[t]();
     });
-    // leaf indices held in maps: remapped in place (no re-hashing), then the joins added
-    leafById.remap(rm);
-    for (size_t k = 0; k < fr.size(); k++) leafById.set(joins[k].id, fr[k]);
-    for (auto& kv : leftNodes) kv.second.first = rm[size_t(kv.second.first)];
-    if (lowestIsHostname) {
-      leafByNodeName.remap(rm);
-      for (auto& u : unnamedLeaves) u = rm[size_t(u)];
-      for (size_t k = 0; k < fr.size(); k++) {
-        if (joins[k].node->name.empty()) unnamedLeaves.push_back(fr[k]);
-        else leafByNodeName.add(joins[k].node->name, fr[k]);
+    // then, on the pool again: the leaf-index maps, the leaves' parents and
+    // live counts, and each level's DomainID ranks
+    std::vector<std::function<void()>> tasks2;
+    tasks2.emplace_back([&] {  // leaf indices held in maps: remapped in place (no re-hashing), then the joins added
+      leafById.remap(rm);
+      for (size_t k = 0; k < fr.size(); k++) leafById.set(joins[k].id, fr[k]);
+      for (auto& kv : leftNodes) kv.second.first = rm[size_t(kv.second.first)];
+    });
+    if (lowestIsHostname)
+      tasks2.emplace_back([&] {
+        leafByNodeName.remap(rm);
+        for (auto& u : unnamedLeaves) u = rm[size_t(u)];
+        for (size_t k = 0; k < fr.size(); k++) {
+          if (joins[k].node->name.empty()) unnamedLeaves.push_back(fr[k]);
+          else leafByNodeName.add(joins[k].node->name, fr[k]);
+        }
+        std::sort(unnamedLeaves.begin(), unnamedLeaves.end());
+      });
+    tasks2.emplace_back([&] {  // leaf parents and live leaves per parent
+      leafParent.assign(N, 0);
+      liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
+      if (L >= 2) {
+        const auto& co = childOff[size_t(L - 2)];
+        for (size_t p = 0; p + 1 < co.size(); p++)
+          for (int32_t i = co[p]; i < co[p + 1]; i++) leafParent[size_t(i)] = int32_t(p);
       }
-      std::sort(unnamedLeaves.begin(), unnamedLeaves.end());
-    }
-    // leaf parents and live leaves per parent
-    leafParent.assign(N, 0);
-    liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
-    if (L >= 2) {
-      const auto& co = childOff[size_t(L - 2)];
-      for (size_t p = 0; p + 1 < co.size(); p++)
-        for (int32_t i = co[p]; i < co[p + 1]; i++) leafParent[size_t(i)] = int32_t(p);
-    }
-    for (size_t i = 0; i < N; i++)
-      if (!leafDead[i]) liveUnder[size_t(leafParent[i])]++;
+      for (size_t i = 0; i < N; i++)
+        if (!leafDead[i]) liveUnder[size_t(leafParent[i])]++;
+    });
     // DomainID ranks (multiLayerNotFitMessage tie-break): each new id's
     // position among the old ones by a binary search over the old rank order;
     // an old domain's rank grows by the new ids placed before it
     for (int l = 0; l < L; l++) {
-      const auto& f = fresh[size_t(l)];
-      if (f.empty()) continue;
-      auto& rk = idRank[size_t(l)];
-      const auto& rml = remap[size_t(l)];
-      const size_t D0 = rk.size();
-      std::vector<int32_t> byRank(D0);
-      for (size_t i = 0; i < D0; i++) byRank[size_t(rk[i])] = rml[i];  // new indices in old rank order
-      std::vector<std::pair<std::string, int32_t>> ids;
-      for (int32_t c : f) ids.emplace_back(domain_id(l, size_t(c)), c);
-      std::sort(ids.begin(), ids.end());
-      std::vector<int32_t> q(ids.size());
-      for (size_t k = 0; k < ids.size(); k++) {
-        size_t lo = 0, hi = D0;
-        while (lo < hi) {
-          const size_t mid = (lo + hi) / 2;
-          if (domain_id(l, size_t(byRank[mid])) < ids[k].first) lo = mid + 1;
-          else hi = mid;
+      if (fresh[size_t(l)].empty()) continue;
+      tasks2.emplace_back([&, l] {
+        const auto& f = fresh[size_t(l)];
+        auto& rk = idRank[size_t(l)];
+        const auto& rml = remap[size_t(l)];
+        const size_t D0 = rk.size();
+        std::vector<int32_t> byRank(D0);
+        for (size_t i = 0; i < D0; i++) byRank[size_t(rk[i])] = rml[i];  // new indices in old rank order
+        std::vector<std::pair<std::string, int32_t>> ids;
+        for (int32_t c : f) ids.emplace_back(domain_id(l, size_t(c)), c);
+        std::sort(ids.begin(), ids.end());
+        std::vector<int32_t> q(ids.size());
+        for (size_t k = 0; k < ids.size(); k++) {
+          size_t lo = 0, hi = D0;
+          while (lo < hi) {
+            const size_t mid = (lo + hi) / 2;
+            if (domain_id(l, size_t(byRank[mid])) < ids[k].first) lo = mid + 1;
+            else hi = mid;
+          }
+          q[k] = int32_t(lo);
         }
-        q[k] = int32_t(lo);
-      }
-      std::vector<int32_t> out(D0 + ids.size());
-      size_t k = 0;
-      for (size_t r = 0; r < D0; r++) {
-        while (k < q.size() && size_t(q[k]) <= r) k++;
-        out[size_t(byRank[r])] = int32_t(r + k);
-      }
-      for (size_t j = 0; j < ids.size(); j++) out[size_t(ids[j].second)] = q[j] + int32_t(j);
-      rk = std::move(out);
+        std::vector<int32_t> out(D0 + ids.size());
+        size_t k = 0;
+        for (size_t r = 0; r < D0; r++) {
+          while (k < q.size() && size_t(q[k]) <= r) k++;
+          out[size_t(byRank[r])] = int32_t(r + k);
+        }
+        for (size_t j = 0; j < ids.size(); j++) out[size_t(ids[j].second)] = q[j] + int32_t(j);
+        rk = std::move(out);
+      });
     }
+    ktas_pool::HostPool::get().run(tasks2.size(), 1, [&](size_t b, size_t e) {
+      for (size_t t = b; t < e; t++) tasks2[t]();
+    });
     leafVals.clear();
     for (auto& j : joins)
       for (auto& kv : j.node->allocatable)
@@ -1358,9 +1397,8 @@ class FlavorSnapshot {
       for (int32_t l : *set) moved.insert(rm[size_t(l)]);
       *set = std::move(moved);
     }
-    touched->insert(fr.begin(), fr.end());
     // the device follows by a splice (its leaf columns gathered into the new
-    // numbering, the joined rows uploaded) unless a reload is due anyway
+    // numbering, the joined rows uploaded with it) unless a reload is due anyway
     if (!dirty && ctx) {
       if (!splicePending) {
         spliceSrc.resize(N0);
@@ -1372,6 +1410,7 @@ class FlavorSnapshot {
       splicePending = true;
     } else {
       dirty = true;
+      touched->insert(fr.begin(), fr.end());
     }
     joins.clear();
     joinIds.clear();
@@ -1434,6 +1473,15 @@ class FlavorSnapshot {
     sd.new_usage_present = up.data();
     sd.new_taint_profile = lowestIsHostname ? prof.data() : nullptr;
     sd.new_label_values = K ? lab.data() : nullptr;
+    // with leaf tags on the device, the resident leaves' tags move with them
+    // (a moved Values vector keeps its buffer): only the joined leaves' go up
+    std::vector<uint64_t> ntags;
+    if (tagsSet && !(cfg.flags & KUEUE_TAS_CFG_HOST_VALUES)) {
+      const int32_t lvl = lowestIsHostname ? L - 1 : 0;
+      const std::string* const* lv = leaf_values();
+      for (size_t q = 0; q < k; q++) ntags.push_back(uint64_t(reinterpret_cast<uintptr_t>(lv[size_t(fresh[q])] + lvl)));
+      sd.new_leaf_tags = ntags.data();
+    }
     const double t1 = now_ms();
     int rc = kueue_tas_snapshot_splice(ctx, &sd);
     spliceSrc.clear();
@@ -1443,13 +1491,15 @@ class FlavorSnapshot {
     }
     namesStale = true;
     const double t2 = now_ms();
-    rc = set_tags();
+    if (!sd.new_leaf_tags) rc = set_tags();
     splice_ms[0] = t1 - t0;
     splice_ms[1] = t2 - t1;
     splice_ms[2] = now_ms() - t2;
     return rc;
   }
+  bool tagsSet = false;  // the device holds every leaf's tag (set_tags since the last load)
   int set_tags() {  // entry tags: each leaf's Values address (Values come back with the entries)
+    tagsSet = false;
     if (cfg.flags & KUEUE_TAS_CFG_HOST_VALUES) return 0;
     const int L = this->L(), N = this->N();
     const int32_t lvl = lowestIsHostname ? L - 1 : 0;
@@ -1458,6 +1508,7 @@ class FlavorSnapshot {
     for (int i = 0; i < N; i++) tags[size_t(i)] = uint64_t(reinterpret_cast<uintptr_t>(lv[i] + lvl));
     const int rc = kueue_tas_snapshot_set_leaf_tags(ctx, tags.data(), tags.size());
     if (rc) err = std::string("leaf tags: ") + kueue_tas_last_error(ctx);
+    tagsSet = rc == 0;
     return rc;
   }
   int load_names() {  // own label value of every domain, for the v1beta2 encoder's leaf mode

@@ -5102,10 +5102,12 @@ __global__ void splice_leaves_kernel(const int32_t* gsrc, int n_new, int n_old, 
                                      const int64_t* of, const int64_t* ou, const uint32_t* ofp, const uint32_t* oup,
                                      const int32_t* oprof, const int32_t* olab, const int64_t* nf, const int64_t* nu,
                                      const uint32_t* nfp, const uint32_t* nup, const int32_t* nprof, const int32_t* nlab,
-                                     int64_t* f, int64_t* u, uint32_t* fp, uint32_t* up, int32_t* prof, int32_t* lab) {
+                                     int64_t* f, int64_t* u, uint32_t* fp, uint32_t* up, int32_t* prof, int32_t* lab,
+                                     const uint64_t* otag, const uint64_t* ntag, uint64_t* tag) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_new) return;
   const int src = gsrc[j];
+  if (tag) tag[j] = src >= 0 ? otag[src] : ntag[-src - 1];
   if (src >= 0) {
     for (int c = 0; c < R; c++) {
       f[int64_t(c) * n_new + j] = of[int64_t(c) * n_old + src];

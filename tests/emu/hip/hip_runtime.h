@@ -201,6 +201,7 @@ using std::min;
 // ---- runtime API subset ----
 typedef int hipError_t;
 constexpr hipError_t hipSuccess = 0;
+constexpr hipError_t hipErrorInvalidValue = 1;
 typedef emu::Stream* hipStream_t;
 typedef emu::Event* hipEvent_t;
 enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
