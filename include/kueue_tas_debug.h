@@ -101,9 +101,10 @@ int kueue_tas_host_last_profile(kueue_tas_host* h, double* ms4);
  * [1] request compile (findTopologyAssignment prelude), [2] per-pass request
  * staging (build_pass), [3] TopologyAssignment Values.  Copies min(n, 4). */
 int kueue_tas_host_last_host_detail(kueue_tas_host* h, double* ms, int n);
-// The last kueue_tas_host_update_nodes call's host time (ms) in n <= 9 slots:
+// The last kueue_tas_host_update_nodes call's host time (ms) in n <= 13 slots:
 // JSON parse, node events, flush_joins (host mirror merge), splice host rows,
-// kueue_tas_snapshot_splice, leaf tags, evaluator reset, pushes, total.
+// kueue_tas_snapshot_splice, leaf tags, evaluator reset, pushes, total, then
+// flush_joins' parts: host-mirror fold, levels + CSR, leaf arrays, maps + ranks.
 int kueue_tas_host_last_update_detail(kueue_tas_host* h, double* ms, int n);
 /* kueue_tas_set_stage_timing for the host's snapshot (kept across reloads). */
 int kueue_tas_host_set_stage_timing(kueue_tas_host* h, int32_t on);

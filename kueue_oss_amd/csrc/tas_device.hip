@@ -69,6 +69,8 @@ struct HostBuf {  // pinned host staging
     if (e == hipSuccess) n = std::max<size_t>(count, 1);
     return e;
   }
+  // ensure with 1/8 headroom when it grows (a pinned allocation costs a millisecond)
+  hipError_t reserve(size_t count) { return count <= n && p ? hipSuccess : ensure(count + count / 8); }
   void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
@@ -524,7 +526,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   }
   // the re-derived tables go up through one pinned arena (async copies, one
   // stream synchronization at the end) instead of a synchronous copy each
-  HIPCHK(c, c->h_tab.ensure(size_t(off) * 8 + N * 9 + (N + 2) * 16 + 4096));
+  HIPCHK(c, c->h_tab.reserve(size_t(off) * 8 + N * 9 + (N + 2) * 16 + 4096));
   size_t arena_pos = 0;
   auto stage = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     if (!bytes) return hipSuccess;
@@ -540,7 +542,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     s.child_base[l] = int32_t(nco);
     nco += size_t(d->level_sizes[l]) + 1;
   }
-  HIPCHK(c, c->d_child_off.ensure(nco));
+  HIPCHK(c, c->d_child_off.reserve(nco));
   if (nco) HIPCHK(c, hipMemcpyAsync(c->d_child_off.p, d->child_offsets, nco * 4, hipMemcpyHostToDevice, c->stream));
   s.child_off = c->d_child_off.p;
   if (sp) {  // the resident leaf columns gathered into the new numbering, the joined rows from the caller
@@ -563,7 +565,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     HIPCHK(c, c->sp_rows.reserve(rbytes));
     // one pinned staging area: leaf sources, then the joined rows
     const size_t o_rows = (N * 4 + 255) / 256 * 256;
-    HIPCHK(c, c->h_load.ensure(o_rows + rbytes));
+    HIPCHK(c, c->h_load.reserve(o_rows + rbytes));
     uint8_t* hl = c->h_load.p;
     if (N) memcpy(hl, gsrc.data(), N * 4);
     uint8_t* hr = hl + o_rows;
@@ -617,7 +619,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     s.taint_profile = prof ? c->d_taint_profile.p : nullptr;
     s.label_values = lab ? c->d_labels.p : nullptr;
     if (c->n_dead > 0) {  // the leaves that had left, at their new indices
-      HIPCHK(c, c->d_dead.ensure(N));
+      HIPCHK(c, c->d_dead.reserve(N));
       HIPCHK(c, stage(c->d_dead.p, c->h_dead.data(), N));
       s.leaf_dead = c->d_dead.p;
       s.n_live = int32_t(int64_t(N) - c->n_dead);
@@ -663,7 +665,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     int64_t src = 0;
     for (int l = 0; l < s.L; l++)
       for (int i = 0; i < d->level_sizes[l]; i++) ranks[size_t(s.level_off[l] + i)] = d->domain_id_rank[src++];
-    HIPCHK(c, c->d_id_rank.ensure(size_t(off)));
+    HIPCHK(c, c->d_id_rank.reserve(size_t(off)));
     HIPCHK(c, stage(c->d_id_rank.p, ranks.data(), size_t(off) * 4));
     s.id_rank = c->d_id_rank.p;
   }
@@ -714,9 +716,9 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     }
     if (ok) {
       tab.push_back(make_int2(cb, cn));
-      HIPCHK(c, c->d_wave_tab2.ensure(tab.size()));
+      HIPCHK(c, c->d_wave_tab2.reserve(tab.size()));
       HIPCHK(c, stage(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2)));
-      HIPCHK(c, c->d_leaf_parent.ensure(N));
+      HIPCHK(c, c->d_leaf_parent.reserve(N));
       HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
       s.wave_tab2 = c->d_wave_tab2.p;
       s.n_wave_slots2 = int32_t(tab.size());
@@ -747,9 +749,9 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     }
     if (ok) {
       tab.push_back(make_int2(cb, cn));
-      HIPCHK(c, c->d_wave_tab.ensure(tab.size()));
+      HIPCHK(c, c->d_wave_tab.reserve(tab.size()));
       HIPCHK(c, stage(c->d_wave_tab.p, tab.data(), tab.size() * sizeof(int2)));
-      HIPCHK(c, c->d_leaf_parent.ensure(N));
+      HIPCHK(c, c->d_leaf_parent.reserve(N));
       HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
       s.wave_tab = c->d_wave_tab.p;
       s.n_wave_slots = int32_t(tab.size());
@@ -765,7 +767,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
       for (int p = 0; p < d->level_sizes[l]; p++)
         for (int j = co[p]; j < co[p + 1]; j++) parent[size_t(s.level_off[l + 1] + j)] = s.level_off[l] + p;
     }
-    HIPCHK(c, c->d_parent.ensure(parent.size()));
+    HIPCHK(c, c->d_parent.reserve(parent.size()));
     HIPCHK(c, stage(c->d_parent.p, parent.data(), parent.size() * 4));
   }
   c->names_loaded = false;

@@ -1215,9 +1215,18 @@ class FlavorSnapshot {
   // cache state would assemble (tas_flavor.go:118-171), without re-sorting
   // or re-reading a node.  Leaf sets the batch's earlier events recorded move
   // with the leaves.
+  double flush_ms[4] = {0, 0, 0, 0};  // last flush_joins: host-mirror fold, levels + CSR, leaf arrays, maps + ranks
   void flush_joins(std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
+    for (double& x : flush_ms) x = 0;
     if (joins.empty()) return;
+    double tf = now_ms();
+    auto lap = [&](int k) {
+      const double t = now_ms();
+      flush_ms[k] = t - tf;
+      tf = t;
+    };
     flush_mirror();  // tasUsage rows move
+    lap(0);
     const int L = this->L();
     std::sort(joins.begin(), joins.end(), [](const Join& a, const Join& b) { return a.lv < b.lv; });
     std::vector<std::vector<int32_t>> remap(static_cast<size_t>(L)), fresh(static_cast<size_t>(L));  // [l][old] -> new; [l] inserted
@@ -1265,6 +1274,7 @@ class FlavorSnapshot {
       off.assign(up.size() + 1, 0);
       for (size_t p = 0; p < up.size(); p++) off[p + 1] = off[p] + cnt[p];
     }
+    lap(1);
     // leaf-indexed arrays (joins are in leaf order: fresh[L-1][k] is joins[k]'s leaf)
     const auto& rm = remap[size_t(L - 1)];
     const auto& fr = fresh[size_t(L - 1)];
@@ -1318,6 +1328,7 @@ class FlavorSnapshot {
     ktas_pool::HostPool::get().run(tasks.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks[t]();
     });
+    lap(2);
     // then, on the pool again: the leaf-index maps, the leaves' parents and
     // live counts, and each level's DomainID ranks
     std::vector<std::function<void()>> tasks2;
@@ -1385,6 +1396,7 @@ class FlavorSnapshot {
     ktas_pool::HostPool::get().run(tasks2.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks2[t]();
     });
+    lap(3);
     leafVals.clear();
     for (auto& j : joins)
       for (auto& kv : j.node->allocatable)
@@ -3413,8 +3425,9 @@ struct kueue_tas_host {
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
   float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
   // last kueue_tas_host_update_nodes: parse, node events, flush_joins, splice
-  // (host rows, device call, leaf tags), evaluator reset, pushes, total
-  double upd_ms[9] = {};
+  // (host rows, device call, leaf tags), evaluator reset, pushes, total, and
+  // flush_joins' parts (host-mirror fold, levels + CSR, leaf arrays, maps + ranks)
+  double upd_ms[13] = {};
   int64_t accum_runs = 0, accum_fills = 0;
   void recompile_all() {
     for (auto& wl : compiled) snap->ensure_columns_for(wl.podsets);
@@ -4156,6 +4169,7 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
     um[2] = t3 - t2;
     if (splice)
       for (int q = 0; q < 3; q++) um[3 + q] = h->snap->splice_ms[q];
+    for (int q = 0; q < 4; q++) um[9 + q] = h->snap->flush_ms[q];
     if (rebuilt) *rebuilt = structural ? 1 : 0;
     int rc;
     if (structural) {  // the events applied so far are in the cache state; the rest replay on it
@@ -4515,7 +4529,7 @@ int kueue_tas_host_stage_accum(kueue_tas_host* h, float* ms, int n, int64_t* run
 
 int kueue_tas_host_last_update_detail(kueue_tas_host* h, double* ms, int n) {
   if (!h || !ms) return KUEUE_TAS_EINVAL;
-  for (int k = 0; k < n && k < 9; k++) ms[k] = h->upd_ms[k];
+  for (int k = 0; k < n && k < 13; k++) ms[k] = h->upd_ms[k];
   return KUEUE_TAS_OK;
 }
 

@@ -424,12 +424,13 @@ class TASFlavorSnapshot:
         return dict(zip(self.HOST_DETAIL, list(ms)))
 
     UPDATE_DETAIL = ("parse", "events", "flush_joins", "splice_rows", "splice_device", "leaf_tags",
-                     "evaluator_reset", "pushes", "total")
+                     "evaluator_reset", "pushes", "total", "flush_mirror_fold", "flush_levels", "flush_leaf_arrays",
+                     "flush_maps_ranks")
 
     def last_update_detail(self):
         """Host wall ms of the last update_nodes, dict keyed by UPDATE_DETAIL."""
-        ms = (ctypes.c_double * 9)()
-        self._lib.kueue_tas_host_last_update_detail(self._h, ms, 9)
+        ms = (ctypes.c_double * 13)()
+        self._lib.kueue_tas_host_last_update_detail(self._h, ms, 13)
         return {k: round(v, 3) for k, v in zip(self.UPDATE_DETAIL, list(ms))}
 
     def set_stage_timing(self, on: bool):

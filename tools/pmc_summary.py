@@ -13,6 +13,8 @@ quad-cycles (MI355X_MICROARCH.md PMC table).  Writes the table to
 profiles/fill_traffic.json, which bench.py reports as roofline.traffic.
 
     python tools/pmc_summary.py gpurun_out profiles/r01 C3
+    python tools/pmc_summary.py gpurun_out profiles/r04 C3J _c3j   (tools/pmc.sh _c3j passes;
+        writes pmc_summary_c3j.json, fill_traffic.json only for C3)
 """
 import csv
 import json
@@ -36,8 +38,9 @@ def read(path, counter):
 
 def main():
     src, out, config = sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "C3"
-    fetch = read(os.path.join(src, "pmc1", "p_counter_collection.csv"), "FETCH_SIZE")
-    write = read(os.path.join(src, "pmc2", "p_counter_collection.csv"), "WRITE_SIZE")
+    tag = sys.argv[4] if len(sys.argv) > 4 else ""
+    fetch = read(os.path.join(src, "pmc1" + tag, "p_counter_collection.csv"), "FETCH_SIZE")
+    write = read(os.path.join(src, "pmc2" + tag, "p_counter_collection.csv"), "WRITE_SIZE")
     table = {}
     for k in sorted(set(fetch) | set(write)):
         f = sum(fetch[k]) / len(fetch[k]) if fetch[k] else 0.0
@@ -49,7 +52,7 @@ def main():
                                   "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"]),
                        ("pmc4", ["SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"])):
         for cn in names:
-            for k, v in read(os.path.join(src, sub, "p_counter_collection.csv"), cn).items():
+            for k, v in read(os.path.join(src, sub + tag, "p_counter_collection.csv"), cn).items():
                 sq.setdefault(k, {})[cn] = sum(v) / len(v)
     for k, d in sq.items():
         row = table.setdefault(k, {})
@@ -66,10 +69,10 @@ def main():
                                       "wait_inst_any": round(d.get("SQ_WAIT_INST_ANY", 0) / tot, 3),
                                       "active_inst_any": round(d.get("SQ_ACTIVE_INST_ANY", 0) / tot, 3)}
     os.makedirs(out, exist_ok=True)
-    with open(os.path.join(out, "pmc_summary.json"), "w") as fh:
+    with open(os.path.join(out, "pmc_summary%s.json" % tag), "w") as fh:
         json.dump(table, fh, indent=1)
     fills = [k for k in table if k.startswith("ktas::fill_leaves") or k.startswith("ktas::fill_pair")]
-    if fills:
+    if fills and config == "C3":
         k = max(fills, key=lambda x: table[x]["dispatches"])
         doc = {"config": config, "kernel": k, "fill_bytes_per_launch": table[k]["hbm_bytes"],
                "fetch_kb": table[k]["fetch_kb"], "write_kb": table[k]["write_kb"],
