@@ -1108,8 +1108,11 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   // the windowed kernel's round bitmap beside the touched one: admission chains within a window
   const bool lds_chain = c->admit_window && 2 * nwords * 4 <= 64 * 1024;
   const size_t o_recs = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
-  const size_t o_bits = o_recs + al(n * sizeof(AdmitRec));
-  HIPCHK(c, c->d_fits.ensure(o_bits + (lds_bits ? 0 : nwords * 4)));
+  const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
+  const size_t o_todo = o_dep + al(n_wl * 4);
+  const size_t o_minc = o_todo + al((n_wl + 1) * 4);
+  const size_t o_bits = o_minc + al(size_t(c->snap.N) * 4);
+  HIPCHK(c, c->d_fits.ensure(o_bits + nwords * 4));
   HIPCHK(c, c->h_stage.ensure(up_bytes));
   uint8_t* h = c->h_stage.p;
   if (n) memcpy(h, reqs, n * sizeof(kueue_tas_fits_req));
@@ -1125,7 +1128,13 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
     reinterpret_cast<int64_t*>(h + o_total)[k] = exact ? 0 : int64_t(total[k]);
   uint8_t* d = c->d_fits.p;
   HIPCHK(c, hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, c->stream));
-  if (!lds_bits) HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
+  // order-free candidates decided in parallel (admit_minc / dep / indep), unless exact
+  const bool indep = c->admit_window && !exact && n > 0;
+  if (indep) {
+    HIPCHK(c, hipMemsetAsync(d + o_minc, 0x7f, size_t(c->snap.N) * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(d + o_dep, 0, n_wl * 4, c->stream));
+  }
   const auto* d_reqs = reinterpret_cast<const kueue_tas_fits_req*>(d);
   const auto* d_terms = reinterpret_cast<const kueue_tas_fits_term*>(d + o_terms);
   if (n) {
@@ -1136,20 +1145,37 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<int32_t*>(d + o_exact));
     HIPCHK(c, hipGetLastError());
   }
-  if (c->admit_window)  // windowed optimistic admission (one 1024-thread workgroup)
+  if (c->admit_window) {  // independent candidates in parallel, the rest windowed (one 1024-thread workgroup)
+    const auto* recwl = reinterpret_cast<const int32_t*>(d + o_recwl);
+    const auto* fit0d = reinterpret_cast<const int32_t*>(d + o_fit0);
+    auto* depd = reinterpret_cast<int32_t*>(d + o_dep);
+    if (indep) {
+      const dim3 g(unsigned((n + 255) / 256));
+      hipLaunchKernelGGL(admit_minc_kernel, g, dim3(256), 0, c->stream, d_reqs, recwl, int(n), fit0d, c->snap.N,
+                         reinterpret_cast<int32_t*>(d + o_minc));
+      hipLaunchKernelGGL(admit_dep_kernel, g, dim3(256), 0, c->stream, d_reqs, recwl, int(n), fit0d, c->snap.N,
+                         reinterpret_cast<const int32_t*>(d + o_minc), depd);
+      hipLaunchKernelGGL(admit_indep_kernel, g, dim3(256), 0, c->stream, c->snap, c->d_usage.p, c->d_usage_present.p,
+                         d_reqs, d_terms, recwl, int(n), fit0d, depd, pods_col, reinterpret_cast<uint32_t*>(d + o_bits));
+      HIPCHK(c, hipGetLastError());
+    }
+    hipLaunchKernelGGL(admit_todo_kernel, dim3(1), dim3(1024), 0, c->stream, int(n_wl), fit0d, depd, indep ? 0 : 1,
+                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo));
+    HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
                        lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
                        reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
                        reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
-                       reinterpret_cast<int32_t*>(d + o_out));
-  else  // one wave down the chain
+                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<const int32_t*>(d + o_todo));
+  } else {  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
                        reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
                        pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
+  }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(admitted, d + o_out, n_wl * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

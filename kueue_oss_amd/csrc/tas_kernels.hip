@@ -5416,6 +5416,90 @@ __global__ __launch_bounds__(256) void admit_fit0_kernel(DevSnap s, const int64_
   if (bad) atomicOr(exact, 1);
 }
 
+// Phase 1b (parallel): the order of admission only matters between
+// candidates that share a leaf.  minc[leaf] is the first phase-1 fitting
+// candidate with a record on the leaf; a fitting candidate that is minc of
+// every one of its leaves shares no leaf with an earlier fitting candidate,
+// so no earlier admission can change its verdict (only a fitting candidate
+// is ever admitted): it is admitted here — its usage added in parallel, its
+// leaves marked touched for the re-checks of later candidates that share
+// them — and only the other ("dependent") candidates go through the in-order
+// window kernel, compacted (admit_todo_kernel).  Adding a later independent
+// candidate's usage before an earlier dependent one is decided changes
+// nothing for the earlier one: by construction they share no leaf.
+__global__ __launch_bounds__(256) void admit_minc_kernel(const kueue_tas_fits_req* reqs, const int32_t* rec_wl, int n,
+                                                         const int32_t* wl_fit0, int N, int32_t* minc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t leaf = reqs[i].leaf, w = rec_wl[i];
+  if (leaf >= 0 && leaf < N && wl_fit0[w] != 0) atomicMin(minc + leaf, w);
+}
+__global__ __launch_bounds__(256) void admit_dep_kernel(const kueue_tas_fits_req* reqs, const int32_t* rec_wl, int n,
+                                                        const int32_t* wl_fit0, int N, const int32_t* minc,
+                                                        int32_t* dep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t leaf = reqs[i].leaf, w = rec_wl[i];
+  if (leaf >= 0 && leaf < N && wl_fit0[w] != 0 && minc[leaf] != w) dep[w] = 1;  // (same value from every writer)
+}
+__global__ __launch_bounds__(256) void admit_indep_kernel(DevSnap s, int64_t* tas_usage, uint32_t* usage_present,
+                                                          const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms,
+                                                          const int32_t* rec_wl, int n, const int32_t* wl_fit0,
+                                                          const int32_t* dep, int pods_col, uint32_t* touched) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int w = rec_wl[i];
+  if (wl_fit0[w] == 0 || dep[w] != 0) return;
+  const kueue_tas_fits_req r = reqs[i];
+  if (r.leaf < 0 || r.leaf >= s.N) return;  // (a fitting candidate's leaves are valid)
+  uint32_t bits = 0;
+  for (int q = 0; q < r.num_terms; q++) {
+    const kueue_tas_fits_term t = terms[r.term_begin + q];
+    if (t.col >= 0) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
+                (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
+      bits |= 1u << t.col;
+    }
+  }
+  if (pods_col >= 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
+              (unsigned long long)int64_t(r.count));
+    bits |= 1u << pods_col;
+  }
+  atomicOr(usage_present + r.leaf, bits);
+  atomicOr(touched + (r.leaf >> 5), 1u << (r.leaf & 31));
+}
+// One workgroup: the verdicts decided so far (phase-1 failures 0,
+// independent candidates 1) and the rest — every candidate in exact mode —
+// compacted in order into todo[1 ..], todo[0] = their count.
+__global__ __launch_bounds__(1024) void admit_todo_kernel(int n_wl, const int32_t* wl_fit0, const int32_t* dep,
+                                                          int exact, int32_t* admitted, int32_t* todo) {
+  __shared__ int32_t sh_wave[16];
+  const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
+  int32_t base = 0;
+  for (int c0 = 0; c0 < n_wl; c0 += int(blockDim.x)) {  // block-uniform
+    const int w = c0 + int(threadIdx.x);
+    bool flag = false;
+    if (w < n_wl) {
+      flag = exact != 0 || (wl_fit0[w] != 0 && dep[w] != 0);
+      if (!flag) admitted[w] = wl_fit0[w] != 0 ? 1 : 0;
+    }
+    const uint64_t m = ballot(flag);
+    const int32_t below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) sh_wave[wave] = __popcll(m);
+    __syncthreads();
+    int32_t off = base, total = 0;
+    for (int k = 0; k < int(blockDim.x) >> 6; k++) {
+      if (k < wave) off += sh_wave[k];
+      total += sh_wave[k];
+    }
+    if (flag) todo[1 + off + below] = w;
+    base += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) todo[0] = base;
+}
+
 // Phase 2: one wave walks the workloads in order (the dependency chain), its
 // lanes splitting a workload's records.  A workload whose phase-1 fit failed
 // is rejected at once; one that fitted is re-checked (usage <= lim, with
@@ -5586,7 +5670,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
     const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
     const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
-    int32_t* admitted) {
+    int32_t* admitted, const int32_t* todo) {
   extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
   __shared__ int32_t sh_fit[kAdmitWindow];
   __shared__ int32_t sh_conf;
@@ -5595,13 +5679,15 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
   const bool in_lds = touched_in_lds != 0;
   const bool chain = touched_in_lds == 2;
   uint32_t* round_lds = touched_lds + nwords;
-  if (in_lds)  // (the global bitmap is cleared by the host)
-    for (int k = threadIdx.x; k < (chain ? 2 : 1) * nwords; k += blockDim.x) touched_lds[k] = 0;
+  if (in_lds)  // the leaves admit_indep_kernel admitted onto (the global bitmap, cleared by the host)
+    for (int k = threadIdx.x; k < (chain ? 2 : 1) * nwords; k += blockDim.x)
+      touched_lds[k] = k < nwords ? touched_global[k] : 0u;
   const bool exact = *exact_flag != 0;
+  const int ntodo = todo[0];
   __syncthreads();
-  int w0 = 0;
-  while (w0 < n_wl) {  // block-uniform
-    const int w = w0 + wave;
+  int w0 = 0;  // position in the todo list
+  while (w0 < ntodo) {  // block-uniform
+    const int w = w0 + wave < ntodo ? todo[1 + w0 + wave] : n_wl;
     int64_t r0 = 0, r1 = 0;
     if (w < n_wl) {
       r0 = wl_off[w];
@@ -5634,11 +5720,11 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     if (lane == 0) sh_fit[wave] = fit ? 1 : 0;
     __syncthreads();
     // the window in order (block-uniform control flow)
-    const int wend = min(kAdmitWindow, n_wl - w0);
+    const int wend = min(kAdmitWindow, ntodo - w0);
     int k = 0, nadm = 0;
     for (; k < wend; k++) {
       if (!sh_fit[k]) {  // final rejection
-        if (wave == k && lane == 0) admitted[w0 + k] = 0;
+        if (wave == k && lane == 0) admitted[w] = 0;
         continue;
       }
       if (nadm > 0) {  // a later fitting candidate: its check holds unless it shares a leaf with this round's admissions
@@ -5677,12 +5763,12 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
           else atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
           if (chain) atomicOr(round_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
         }
-        if (lane == 0) admitted[w0 + k] = 1;
+        if (lane == 0) admitted[w] = 1;
       }
       nadm++;
       if (chain) __syncthreads();  // the round's leaves visible to the next candidate's overlap check
     }
-    // candidates w0 .. w0 + k - 1 are decided; w0 + k (if any) is checked again
+    // todo[1 + w0 .. w0 + k - 1] are decided; w0 + k (if any) is checked again
     admit_drain();  // this wave's atomics performed at L2 before any wave's next loads
     if (chain && nadm > 0)
       for (int q = threadIdx.x; q < nwords; q += blockDim.x) round_lds[q] = 0;

@@ -188,6 +188,7 @@ inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v;
 inline int atomicOr(int* p, int v) { int o = *p; *p = o | v; return o; }
 inline int atomicMax(int* p, int v) { int o = *p; if (v > o) *p = v; return o; }
 inline int atomicAnd(int* p, int v) { int o = *p; *p = o & v; return o; }
+inline int atomicMin(int* p, int v) { int o = *p; *p = v < o ? v : o; return o; }
 inline unsigned atomicAnd(unsigned* p, unsigned v) { unsigned o = *p; *p = o & v; return o; }
 inline void __threadfence() {}
 inline void __threadfence_block() {}
