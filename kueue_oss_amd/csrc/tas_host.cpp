@@ -1230,17 +1230,31 @@ class FlavorSnapshot {
     const int L = this->L();
     std::sort(joins.begin(), joins.end(), [](const Join& a, const Join& b) { return a.lv < b.lv; });
     std::vector<std::vector<int32_t>> remap(static_cast<size_t>(L)), fresh(static_cast<size_t>(L));  // [l][old] -> new; [l] inserted
+    std::vector<size_t> pos(joins.size());
+    std::vector<uint8_t> found(joins.size());
     for (int l = 0; l < L; l++) {
       auto& lvl = values[size_t(l)];
+      // each join's prefix searched in the (unchanged) level on the pool,
+      // then the new prefixes collected in order, repeats dropped
+      auto prefix_less = [l](const std::vector<std::string>& v, const std::vector<std::string>& jl) {
+        return std::lexicographical_compare(v.begin(), v.end(), jl.begin(), jl.begin() + l + 1);
+      };
+      ktas_pool::HostPool::get().run(joins.size(), 8, [&](size_t b, size_t e) {
+        for (size_t k = b; k < e; k++) {
+          const auto& jl = joins[k].lv;
+          auto it = std::lower_bound(lvl.begin(), lvl.end(), jl, prefix_less);
+          pos[k] = size_t(it - lvl.begin());
+          found[k] = it != lvl.end() && std::equal(it->begin(), it->end(), jl.begin(), jl.begin() + l + 1);
+        }
+      });
       std::vector<std::vector<std::string>> add;
       std::vector<size_t> at;
-      for (auto& j : joins) {
-        std::vector<std::string> pre(j.lv.begin(), j.lv.begin() + l + 1);
-        if (!add.empty() && add.back() == pre) continue;
-        auto it = std::lower_bound(lvl.begin(), lvl.end(), pre);
-        if (it != lvl.end() && *it == pre) continue;
-        at.push_back(size_t(it - lvl.begin()));
-        add.push_back(std::move(pre));
+      for (size_t k = 0; k < joins.size(); k++) {
+        const auto& jl = joins[k].lv;
+        if (found[k]) continue;
+        if (!add.empty() && std::equal(add.back().begin(), add.back().end(), jl.begin(), jl.begin() + l + 1)) continue;
+        at.push_back(pos[k]);
+        add.emplace_back(jl.begin(), jl.begin() + l + 1);
       }
       // in place: the level grows by the new prefixes and every old domain
       // moves right by the number inserted before it (from the back, so no

@@ -1391,6 +1391,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // a resource giving state 0): every condition below is either
     // wave-uniform (a scalar branch) or a v_cndmask, no divergent branch
     int32_t state[kPairLP], swl[kPairLP], ls[kPairLP], ss[kPairLP], sswl[kPairLP];
+    bool okm[kPairLP];
     int kind[kPairLP], id[kPairLP];
     const bool hn = s.lowest_is_hostname != 0;
     int4 c0 = make_int4(0, 0, 0, 0), c1 = c0, v0 = c0, v1 = c0;
@@ -1474,19 +1475,32 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         ok = ok & !x;
       }
       state[j] = ok ? state0[j] : 0;
-      swl[j] = ok ? swl0[j] : 0;
-      ls[j] = ok ? ls0[j] : 0;
+      okm[j] = ok;
       const bool rx = ok & (state0[j] == 0) & (lim0[j] >= 0);
       kind[j] = rx ? EX_RESOURCE : k;
       id[j] = rx ? lim0[j] : idv;
-      ss[j] = sswl[j] = 0;
-      if (s.L - 1 == slice_level) {
-        if (slice_size == 1) {
-          ss[j] = state[j];
-          sswl[j] = swl[j];
-        } else {
-          ss[j] = go_div32(state[j], slice_size);
-          sswl[j] = leader ? go_div32(swl[j], slice_size) : ss[j];
+    }
+    // a simple class (no leader, one-pod slices at the leaf level, no inner
+    // slice rounding — every class of C3): sliceState is state and no
+    // leader field exists, one wave-uniform branch instead of one per field
+    const bool simple = !leader && s.L - 1 == slice_level && slice_size == 1 && (p_inner == 0 || p_inner == 1);
+    if (simple) {
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) ss[j] = state[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        swl[j] = okm[j] ? swl0[j] : 0;
+        ls[j] = okm[j] ? ls0[j] : 0;
+        ss[j] = sswl[j] = 0;
+        if (s.L - 1 == slice_level) {
+          if (slice_size == 1) {
+            ss[j] = state[j];
+            sswl[j] = swl[j];
+          } else {
+            ss[j] = go_div32(state[j], slice_size);
+            sswl[j] = leader ? go_div32(swl[j], slice_size) : ss[j];
+          }
         }
       }
     }
@@ -1508,8 +1522,32 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       storev(3 * SD, sswl);
       storev(4 * SD, ls);
     }
+    // positive children of the lane's parent group: bits kPairLP*gpos ..
+    // kPairLP*gpos + kPairLP - 1 of the parent's mask
+    auto pos_mask = [&]() -> uint64_t {
+      uint32_t pb = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) pb |= uint32_t(valid[j] && ss[j] > 0) << j;
+      if (rack_f <= 32) return uint32_t(group_reduce(int32_t(pb << (kPairLP * gpos)), half, OpOr()));
+      const int lo_groups = 32 / kPairLP;
+      const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < lo_groups ? pb << (kPairLP * gpos) : 0u), half, OpOr()));
+      const uint32_t hi = uint32_t(group_reduce(int32_t(gpos >= lo_groups ? pb << (kPairLP * gpos - 32) : 0u), half, OpOr()));
+      return (uint64_t(hi) << 32) | lo;
+    };
     // fused fillInCountsHelper (:1658-1719) of the leaves' parents
-    if (rack_f > 0) {
+    if (rack_f > 0 && simple) {  // sliceState == state at the parent too
+      int32_t cap2 = 0;
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) cap2 = w_add(cap2, state[j]);
+      cap2 = group_reduce(cap2, half, OpWAdd());
+      const uint64_t posm = pos_mask();
+      if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
+        b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = posm;
+        const int g = s.level_off[s.L - 2] + parent;
+        base[g] = cap2;
+        base[SD + g] = cap2;
+      }
+    } else if (rack_f > 0) {
       const int32_t inner = p_inner;
       int32_t cap2 = 0, slc = 0, lead = 0, minD = 0x7fffffff, minSD = 0x7fffffff, has = 0;
 #pragma unroll
@@ -1539,20 +1577,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         lead = group_reduce(lead, half, OpMax());
         has = group_reduce(has, half, OpMax());
       }
-      // positive children: bits kPairLP*gpos .. kPairLP*gpos + kPairLP - 1 of the parent's mask
-      uint32_t pb = 0;
-#pragma unroll
-      for (int j = 0; j < kPairLP; j++) pb |= uint32_t(valid[j] && ss[j] > 0) << j;
-      uint64_t posm;
-      if (rack_f <= 32) {
-        posm = uint32_t(group_reduce(int32_t(pb << (kPairLP * gpos)), half, OpOr()));
-      } else {
-        const int lo_groups = 32 / kPairLP;
-        const uint32_t lo = uint32_t(group_reduce(int32_t(gpos < lo_groups ? pb << (kPairLP * gpos) : 0u), half, OpOr()));
-        const uint32_t hi =
-            uint32_t(group_reduce(int32_t(gpos >= lo_groups ? pb << (kPairLP * gpos - 32) : 0u), half, OpOr()));
-        posm = (uint64_t(hi) << 32) | lo;
-      }
+      const uint64_t posm = pos_mask();
       if (gpos == 0 && valid[0] && parent < s.level_size[s.L - 2]) {
         b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = posm;
         const int32_t pswl = has ? w_sub(cap2, minD) : 0;
