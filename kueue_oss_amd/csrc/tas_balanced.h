@@ -18,6 +18,11 @@
 // lexicographic levelValues order; sortDomainsByCapacityAndEntropy (:211-231,
 // pdqsort, comparator 0 on equal entropy) is a stable insertion sort.  The
 // oracle (oracle/tas_oracle.cpp) restates the same rules.
+// Parity unpinned: Go's slices.SortFunc is an insertion sort
+// only up to 12 elements (pdqsort, not stable, above), so more than 12
+// siblings whose keys tie may order differently; go_log restates Go's pure-Go
+// math.Log, while Go on amd64 calls its assembly archLog.  No reference
+// golden reaches either case.
 #pragma once
 #include <stdint.h>
 
