@@ -1201,6 +1201,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
                                                                  int chunk_base) {
   __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
+  // multi-run chunks: each leaf's remaining capacity waits in LDS for the
+  // next run's CountIn ([column][leaf of the lane][thread]), not in 4 * NS
+  // VGPRs live across the whole class loop
+  __shared__ int64_t sh_cap[MR ? NS * kPairLP * kFillThreads : 1];
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   if (lds_stats)
@@ -1309,6 +1313,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         for (int a = a_lo; a < a_hi; a++)
           if (b.assumed[a].col == scol[k]) c = int64_t(uint64_t(c) - uint64_t(b.assumed[a].value));
         cap[j][k] = c;
+        if constexpr (MR) sh_cap[(k * kPairLP + j) * kFillThreads + threadIdx.x] = c;
       }
     }
   }
@@ -1330,14 +1335,20 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       state0[j] = swl0[j] = ls0[j] = 0;
       lim0[j] = -1;
       if (!live[j]) continue;
-      state0[j] = count_slots(cap[j], wt, rmask, lt, lmask, pres[j], false, &lim0[j]);
+      int64_t cj[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        if constexpr (MR) cj[k] = sh_cap[(k * kPairLP + j) * kFillThreads + threadIdx.x];
+        else cj[k] = cap[j][k];
+      }
+      state0[j] = count_slots(cj, wt, rmask, lt, lmask, pres[j], false, &lim0[j]);
       swl0[j] = state0[j];
       if (leader) {
         int dummy;
-        const int32_t lc = count_slots(cap[j], lt, lmask, lt, lmask, pres[j], false, &dummy);
+        const int32_t lc = count_slots(cj, lt, lmask, lt, lmask, pres[j], false, &dummy);
         if (lc > 0) {
           ls0[j] = 1;
-          swl0[j] = count_slots(cap[j], wt, rmask, lt, lmask, pres[j] | lmask, true, &dummy);
+          swl0[j] = count_slots(cj, wt, rmask, lt, lmask, pres[j] | lmask, true, &dummy);
         }
       }
     }
