@@ -278,6 +278,7 @@ def main():
     rounds = 5
     adm_ms, admitted_n, deltas_n = [], 0, 0
     adm_parts = []
+    adm_stats = (-1, -1, -1)
     for _ in range(rounds):
         barrier()
         ta = time.perf_counter()
@@ -290,6 +291,8 @@ def main():
         barrier()
         adm_ms.append((time.perf_counter() - ta) * 1e3)
         adm_parts.append([(tb - ta) * 1e3, (time.perf_counter() - tb) * 1e3] + list(snap.last_admit_times()))
+        if rank == 0:
+            adm_stats = snap.last_admit_stats()
         if admitted is not None:
             admitted_n = int(admitted[:, 1].sum())
         deltas_n = len(deltas)
@@ -374,12 +377,15 @@ def main():
                                "admission's deltas (alternately negated and again) after its evaluation"},
             "admission": {"round_ms_median": round(pct(adm_ms, 0.5), 3), "rounds": rounds,
                           "admitted": admitted_n, "deltas": deltas_n,
+                          "device_pass": dict(zip(["window_rounds", "in_order_candidates", "candidates"],
+                                                  [int(x) for x in adm_stats])),
                           "parts_ms_median": dict(zip(["evaluate", "gather_admit_broadcast", "admit_host_prep",
                                                        "admit_device", "admit_delta_list"],
                                                       [round(pct([p[k] for p in adm_parts], 0.5), 3)
                                                        for k in range(5)])),
                           "round": "evaluate + all-gather assignments + rank-0 Fits/AddUsage in workload order "
-                                   "(admit_kernel) + delta broadcast + replicas apply"},
+                                   "(order-free candidates in parallel, the rest admit_window_kernel) + delta "
+                                   "broadcast + replicas apply"},
             "stages": stages,
             "host": host,
             "work": st,

@@ -121,6 +121,11 @@ int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
  * preparation, [1] kueue_tas_admit (uploads, admit_kernel, result copy),
  * [2] delta list. */
 int kueue_tas_host_last_admit_times(kueue_tas_host* h, double* ms3);
+// The last kueue_tas_admit: rounds of admit_window_kernel, candidates it
+// walked in order (the rest were decided in parallel: phase-1 failures and
+// order-free admissions), candidates in total; -1 for the serial chain.
+int kueue_tas_last_admit_stats(kueue_tas_ctx* ctx, int64_t* out3);
+int kueue_tas_host_last_admit_stats(kueue_tas_host* h, int64_t* out3);
 
 #ifdef __cplusplus
 }

@@ -269,6 +269,8 @@ struct kueue_tas_ctx {
   // entry tags (kueue_tas_snapshot_set_leaf_tags): per-leaf table in HBM, the
   // per-entry copies in pinned device-mapped host memory beside the entries
   DevBuf<uint64_t> d_leaf_tags;
+  HostBuf<int32_t> h_admit;          // kueue_tas_admit's verdicts + its two diagnostics words (pinned D2H)
+  int64_t admit_stats[3] = {-1, -1, -1};  // last kueue_tas_admit: window rounds, in-order candidates, candidates
   // kueue_tas_snapshot_splice: the gather's targets (the resident columns'
   // previous buffers after the swap, reused by the next splice) and its
   // pinned staging (leaf sources and joined rows)
@@ -1107,7 +1109,7 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const bool lds_bits = nwords * 4 <= 64 * 1024;
   // the windowed kernel's round bitmap beside the touched one: admission chains within a window
   const bool lds_chain = c->admit_window && 2 * nwords * 4 <= 64 * 1024;
-  const size_t o_recs = o_out + al((n_wl + 1) * 4);  // + the kernel's sink word
+  const size_t o_recs = o_out + al((n_wl + 2) * 4);  // + two diagnostics words (admit_window_kernel)
   const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
   const size_t o_todo = o_dep + al(n_wl * 4);
   const size_t o_minc = o_todo + al((n_wl + 1) * 4);
@@ -1177,8 +1179,19 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   }
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(admitted, d + o_out, n_wl * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, c->h_admit.reserve(n_wl + 2));
+  HIPCHK(c, hipMemcpyAsync(c->h_admit.p, d + o_out, (n_wl + 2) * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(admitted, c->h_admit.p, n_wl * 4);
+  c->admit_stats[0] = c->admit_window ? c->h_admit.p[n_wl] : -1;
+  c->admit_stats[1] = c->admit_window ? c->h_admit.p[n_wl + 1] : -1;
+  c->admit_stats[2] = int64_t(n_wl);
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_admit_stats(kueue_tas_ctx* c, int64_t* out3) {
+  if (!c || !out3) return KUEUE_TAS_EINVAL;
+  memcpy(out3, c->admit_stats, sizeof c->admit_stats);
   return KUEUE_TAS_OK;
 }
 

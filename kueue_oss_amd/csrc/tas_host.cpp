@@ -4760,6 +4760,11 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
   }
 }
 
+int kueue_tas_host_last_admit_stats(kueue_tas_host* h, int64_t* out3) {
+  if (!h || !h->snap || !h->snap->ctx || !out3) return KUEUE_TAS_EINVAL;
+  return kueue_tas_last_admit_stats(h->snap->ctx, out3);
+}
+
 int kueue_tas_host_last_admit_times(kueue_tas_host* h, double* ms3) {
   if (!h || !ms3) return KUEUE_TAS_EINVAL;
   memcpy(ms3, h->admit_ms, sizeof h->admit_ms);

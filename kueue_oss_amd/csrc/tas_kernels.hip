@@ -5722,7 +5722,9 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
   const int ntodo = todo[0];
   __syncthreads();
   int w0 = 0;  // position in the todo list
+  int rounds = 0;
   while (w0 < ntodo) {  // block-uniform
+    rounds++;
     const int w = w0 + wave < ntodo ? todo[1 + w0 + wave] : n_wl;
     int64_t r0 = 0, r1 = 0;
     if (w < n_wl) {
@@ -5810,6 +5812,10 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
       for (int q = threadIdx.x; q < nwords; q += blockDim.x) round_lds[q] = 0;
     __syncthreads();
     w0 += k;
+  }
+  if (threadIdx.x == 0) {  // diagnostics after the verdicts: rounds, candidates in the in-order pass
+    admitted[n_wl] = rounds;
+    admitted[n_wl + 1] = ntodo;
   }
 }
 

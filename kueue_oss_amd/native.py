@@ -60,7 +60,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_deltas", "kueue_tas_host_run", "kueue_tas_build_id",
     "kueue_tas_host_has_level", "kueue_tas_host_assignment_stale", "kueue_tas_host_free_capacity_json",
     "kueue_tas_resource_quantity_string", "kueue_tas_host_ctx", "kueue_tas_host_leaf_ids",
-    "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_host_find_workload",
+    "kueue_tas_host_compile_workload", "kueue_tas_host_last_admit_times", "kueue_tas_last_admit_stats",
+    "kueue_tas_host_last_admit_stats", "kueue_tas_host_find_workload",
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
     "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
@@ -148,6 +149,8 @@ def _bind(lib):
     lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
                                                c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    lib.kueue_tas_last_admit_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
+    lib.kueue_tas_host_last_admit_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
     lib.kueue_tas_host_find_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_find_workload.restype = c.c_int
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
@@ -497,6 +500,13 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_last_deltas(self._h, deltas.ctypes.data, deltas.size):
             raise RuntimeError(self._err())
         return adm[: nw.value], deltas
+
+    def last_admit_stats(self):
+        """The last admit: (window rounds, candidates walked in order, candidates); -1 for the serial chain."""
+        out = (ctypes.c_int64 * 3)()
+        if self._lib.kueue_tas_host_last_admit_stats(self._h, out):
+            raise RuntimeError(self._err())
+        return tuple(out)
 
     def last_admit_times(self):
         """Host ms of the last admit: (record prep, kueue_tas_admit, delta list)."""
