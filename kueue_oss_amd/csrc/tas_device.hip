@@ -1068,29 +1068,54 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   if (wl_off[0] != 0 || size_t(wl_off[n_wl]) != n) return fail(c, KUEUE_TAS_EINVAL, "workload offsets");
   for (size_t w = 0; w < n_wl; w++)
     if (wl_off[w + 1] < wl_off[w]) return fail(c, KUEUE_TAS_EINVAL, "workload offsets not monotone");
-  for (size_t i = 0; i < n; i++) {
-    const kueue_tas_fits_req& r = reqs[i];
-    if (r.leaf >= c->snap.N || r.num_terms < 0 || r.term_begin < 0 || size_t(r.term_begin) + size_t(r.num_terms) > num_terms)
-      return fail(c, KUEUE_TAS_EINVAL, "admit record out of range");
-    for (int k = 0; k < r.num_terms; k++)
-      if (terms[r.term_begin + k].col < 0 || terms[r.term_begin + k].col >= c->snap.R)
-        return fail(c, KUEUE_TAS_EINVAL, "admit term column out of range");
-  }
-  // monotone shortcut (admit_fit0_kernel) only for non-negative values and
-  // counts whose total usage this call could add stays below 2^61 (with
-  // every capacity and usage value below 2^61, checked on the device, no
-  // int64 arithmetic of the call wraps)
+  // per record on the host pool: the range checks, and for the monotone
+  // shortcut (admit_fit0_kernel) the most usage this call can add per column
+  // — the shortcut holds only for non-negative values and counts whose totals
+  // stay below 2^61 (with every capacity and usage value below 2^61, checked
+  // on the device, no int64 arithmetic of the call wraps)
+  ktas_pool::HostPool& pool = ktas_pool::HostPool::get();
+  const size_t nparts = pool.parts();
+  struct AdmitPart {
+    __int128 total[KUEUE_TAS_MAX_COLS];
+    bool exact;
+    int err;  // 0, 1: record out of range, 2: term column out of range
+  };
+  std::vector<AdmitPart> parts(nparts);
+  pool.run_static(n, [&](size_t i0, size_t i1) {
+    size_t t = 0;
+    while (t + 1 < nparts && ktas_pool::HostPool::part_begin(n, t + 1, nparts) <= i0) t++;
+    AdmitPart& ap = parts[t];
+    memset(ap.total, 0, sizeof ap.total);
+    ap.exact = false;
+    ap.err = 0;
+    for (size_t i = i0; i < i1 && !ap.err; i++) {
+      const kueue_tas_fits_req& r = reqs[i];
+      if (r.leaf >= c->snap.N || r.num_terms < 0 || r.term_begin < 0 || size_t(r.term_begin) + size_t(r.num_terms) > num_terms) {
+        ap.err = 1;
+        break;
+      }
+      ap.exact = ap.exact || r.count < 0;
+      for (int k = 0; k < r.num_terms; k++) {
+        const kueue_tas_fits_term& tm = terms[r.term_begin + k];
+        if (tm.col < 0 || tm.col >= c->snap.R) {
+          ap.err = 2;
+          break;
+        }
+        ap.exact = ap.exact || tm.value < 0;
+        if (tm.col < KUEUE_TAS_MAX_COLS) ap.total[tm.col] += __int128(tm.value) * r.count;
+      }
+      if (pods_col >= 0) ap.total[pods_col] += r.count;
+    }
+  });
   bool exact = false;
   __int128 total[KUEUE_TAS_MAX_COLS] = {};  // per column: the most usage this call can add
-  for (size_t i = 0; i < n && !exact; i++) {
-    const kueue_tas_fits_req& r = reqs[i];
-    exact = r.count < 0;
-    for (int k = 0; k < r.num_terms && !exact; k++) {
-      const kueue_tas_fits_term& t = terms[r.term_begin + k];
-      exact = t.value < 0;
-      if (t.col >= 0 && t.col < KUEUE_TAS_MAX_COLS) total[t.col] += __int128(t.value) * r.count;
-    }
-    if (pods_col >= 0) total[pods_col] += r.count;
+  for (size_t t = 0; t < nparts && n > 0; t++) {
+    if (parts[t].err == 1) return fail(c, KUEUE_TAS_EINVAL, "admit record out of range");
+    if (parts[t].err == 2) return fail(c, KUEUE_TAS_EINVAL, "admit term column out of range");
+  }
+  for (size_t t = 0; t < nparts && n > 0; t++) {
+    exact = exact || parts[t].exact;
+    for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++) total[k] += parts[t].total[k];
   }
   for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++) exact = exact || total[k] >= (__int128(1) << 61);
   HIPCHK(c, hipSetDevice(c->device));
@@ -1117,12 +1142,16 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   HIPCHK(c, c->d_fits.ensure(o_bits + nwords * 4));
   HIPCHK(c, c->h_stage.ensure(up_bytes));
   uint8_t* h = c->h_stage.p;
-  if (n) memcpy(h, reqs, n * sizeof(kueue_tas_fits_req));
   if (num_terms) memcpy(h + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term));
   memcpy(h + o_off, wl_off, (n_wl + 1) * 8);
   int32_t* rec_wl = reinterpret_cast<int32_t*>(h + o_recwl);
-  for (size_t w = 0; w < n_wl; w++)
-    for (int64_t i = wl_off[w]; i < wl_off[w + 1]; i++) rec_wl[i] = int32_t(w);
+  pool.run_static(n_wl, [&](size_t w0, size_t w1) {  // the records and their workload, per workload range
+    if (w1 > w0 && wl_off[w1] > wl_off[w0])
+      memcpy(h + size_t(wl_off[w0]) * sizeof(kueue_tas_fits_req), reqs + wl_off[w0],
+             size_t(wl_off[w1] - wl_off[w0]) * sizeof(kueue_tas_fits_req));
+    for (size_t w = w0; w < w1; w++)
+      for (int64_t i = wl_off[w]; i < wl_off[w + 1]; i++) rec_wl[i] = int32_t(w);
+  });
   int32_t* fit0 = reinterpret_cast<int32_t*>(h + o_fit0);
   for (size_t w = 0; w < n_wl; w++) fit0[w] = 1;
   *reinterpret_cast<int32_t*>(h + o_exact) = exact ? 1 : 0;

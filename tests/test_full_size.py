@@ -62,12 +62,21 @@ C5_PER_RANK = 1024
 WORLD = 2
 
 
+_CAPFD = None  # the running test's capfd: progress goes to the terminal past pytest's capture
+
+
 def _progress(msg):
-    print(f"[c5] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+    line = f"[c5] {time.strftime('%H:%M:%S')} {msg}"
+    if _CAPFD is not None:
+        with _CAPFD.disabled():
+            print(line, file=sys.stderr, flush=True)
+    else:
+        print(line, file=sys.stderr, flush=True)
 
 
 def _heartbeat(stop, period=20.0):
-    """Progress lines while the 1M-node phases run (setup and the oracle print nothing)."""
+    """Progress lines while the 1M-node phases run (setup and the oracle print
+    nothing), so a runner that takes a silent minute for a hang sees it alive."""
     t0 = time.time()
     while not stop.wait(period):
         _progress(f"alive {time.time() - t0:.0f}s")
@@ -109,7 +118,7 @@ def _rank_worker(rank, world, port, q):
         snap.run_compiled(flags=FULL)
         res = snap.last_results()
         pos = {g: k for k, g in enumerate(ids)}
-        out["sample1"] = {i: res[pos[i]] for i in _sample_ids(wls, ids)}
+        out["sample1"] = {i: res[pos[i]] for i in _sample_ids(wls, ids, 4)}
         out["gathered1"] = sharding.gather_assignments(snap.last_assignments(), world, dist)
         quads, admitted, deltas = sharding.admit_round(snap, world, rank, dist)
         out["admit_quads"] = quads
@@ -141,13 +150,16 @@ def _by_workload(quads):
 
 
 @pytest.mark.timeout(1200)
-def test_c5_sharded_two_ranks_on_one_gpu():
+def test_c5_sharded_two_ranks_on_one_gpu(capfd):
+    global _CAPFD
+    _CAPFD = capfd
     stop = threading.Event()
     threading.Thread(target=_heartbeat, args=(stop,), daemon=True).start()
     try:
         _c5_sharded()
     finally:
         stop.set()
+        _CAPFD = None
 
 
 def _c5_sharded():
