@@ -6,6 +6,7 @@
 # the first failure.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAILED; tail -5 gpurun_out/smoke.log; exit 1; }
 timeout -k 10 420 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -5 gpurun_out/bench.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench.json')); print(d['value'], d['stages'], d['roofline']['frac'], d['parity_full_batch']['ok'], d['extras']['c3j']['value'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --no-extras > gpurun_out/prof_bench.json 2> gpurun_out/prof.log || { echo PROF_FAILED; exit 1; }
