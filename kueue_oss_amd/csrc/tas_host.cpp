@@ -1232,6 +1232,7 @@ class FlavorSnapshot {
     std::vector<std::vector<int32_t>> remap(static_cast<size_t>(L)), fresh(static_cast<size_t>(L));  // [l][old] -> new; [l] inserted
     std::vector<size_t> pos(joins.size());
     std::vector<uint8_t> found(joins.size());
+    std::vector<std::vector<std::vector<std::string>>> adds(static_cast<size_t>(L));  // [l] the level's new prefixes
     for (int l = 0; l < L; l++) {
       auto& lvl = values[size_t(l)];
       // each join's prefix searched in the (unchanged) level on the pool,
@@ -1247,7 +1248,7 @@ class FlavorSnapshot {
           found[k] = it != lvl.end() && std::equal(it->begin(), it->end(), jl.begin(), jl.begin() + l + 1);
         }
       });
-      std::vector<std::vector<std::string>> add;
+      auto& add = adds[size_t(l)];
       std::vector<size_t> at;
       for (size_t k = 0; k < joins.size(); k++) {
         const auto& jl = joins[k].lv;
@@ -1256,10 +1257,8 @@ class FlavorSnapshot {
         at.push_back(pos[k]);
         add.emplace_back(jl.begin(), jl.begin() + l + 1);
       }
-      // in place: the level grows by the new prefixes and every old domain
-      // moves right by the number inserted before it (from the back, so no
-      // slot is overwritten before it moved; a moved vector keeps its
-      // buffer, so the leaves' Values addresses survive the move)
+      // every old domain moves right by the number of prefixes inserted
+      // before it (the moves themselves run on the pool, move_level below)
       const size_t D0 = lvl.size();
       auto& rm = remap[size_t(l)];
       rm.resize(D0);
@@ -1269,25 +1268,22 @@ class FlavorSnapshot {
         rm[i] = int32_t(i + a);
       }
       for (size_t a = 0; a < add.size(); a++) fr.push_back(int32_t(at[a] + a));
+    }
+    // a level grows in place (from the back, so no slot is overwritten before
+    // it moved; a moved vector keeps its buffer, so the leaves' Values
+    // addresses survive the move)
+    auto move_level = [&](int l) {
+      auto& lvl = values[size_t(l)];
+      const auto& lrm = remap[size_t(l)];
+      const auto& lfr = fresh[size_t(l)];
+      auto& add = adds[size_t(l)];
+      if (add.empty()) return;
+      const size_t D0 = lvl.size();
       lvl.resize(D0 + add.size());
       for (size_t i = D0; i-- > 0;)
-        if (size_t(rm[i]) != i) lvl[size_t(rm[i])] = std::move(lvl[i]);
-      for (size_t a = 0; a < add.size(); a++) lvl[size_t(fr[a])] = std::move(add[a]);
-    }
-    // CSR offsets: children per (new) parent, then a prefix sum
-    for (int l = 0; l + 1 < L; l++) {
-      auto& off = childOff[size_t(l)];
-      const auto& up = values[size_t(l)];
-      std::vector<int32_t> cnt(up.size(), 0);
-      for (size_t p = 0; p + 1 < off.size(); p++) cnt[size_t(remap[size_t(l)][p])] = off[p + 1] - off[p];
-      for (int32_t c : fresh[size_t(l + 1)]) {
-        const auto& v = values[size_t(l + 1)][size_t(c)];
-        const std::vector<std::string> pre(v.begin(), v.begin() + l + 1);
-        cnt[size_t(std::lower_bound(up.begin(), up.end(), pre) - up.begin())]++;
-      }
-      off.assign(up.size() + 1, 0);
-      for (size_t p = 0; p < up.size(); p++) off[p + 1] = off[p] + cnt[p];
-    }
+        if (size_t(lrm[i]) != i) lvl[size_t(lrm[i])] = std::move(lvl[i]);
+      for (size_t a = 0; a < add.size(); a++) lvl[size_t(lfr[a])] = std::move(add[a]);
+    };
     lap(1);
     // leaf-indexed arrays (joins are in leaf order: fresh[L-1][k] is joins[k]'s leaf)
     const auto& rm = remap[size_t(L - 1)];
@@ -1305,6 +1301,7 @@ class FlavorSnapshot {
       move_leaves(vec.v, [&](const Join& j) { return std::make_unique<Requests>(make(j)); });
     };
     std::vector<std::function<void()>> tasks;
+    for (int l = L; l-- > 0;) tasks.emplace_back([&, l] { move_level(l); });  // the leaf level first: the longest
     tasks.emplace_back([&] { move_leaves(leafId, [](const Join& j) { return j.id; }); });
     tasks.emplace_back([&] { move_leaves(leafNode, [](const Join& j) { return j.node; }); });
     tasks.emplace_back([&] { move_boxed(leafAlloc, [](const Join& j) { return j.node->allocatable; }); });
@@ -1342,6 +1339,20 @@ class FlavorSnapshot {
     ktas_pool::HostPool::get().run(tasks.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks[t]();
     });
+    // CSR offsets: children per (new) parent, then a prefix sum
+    for (int l = 0; l + 1 < L; l++) {
+      auto& off = childOff[size_t(l)];
+      const auto& up = values[size_t(l)];
+      std::vector<int32_t> cnt(up.size(), 0);
+      for (size_t p = 0; p + 1 < off.size(); p++) cnt[size_t(remap[size_t(l)][p])] = off[p + 1] - off[p];
+      for (int32_t c : fresh[size_t(l + 1)]) {
+        const auto& v = values[size_t(l + 1)][size_t(c)];
+        const std::vector<std::string> pre(v.begin(), v.begin() + l + 1);
+        cnt[size_t(std::lower_bound(up.begin(), up.end(), pre) - up.begin())]++;
+      }
+      off.assign(up.size() + 1, 0);
+      for (size_t p = 0; p < up.size(); p++) off[p + 1] = off[p] + cnt[p];
+    }
     lap(2);
     // then, on the pool again: the leaf-index maps, the leaves' parents and
     // live counts, and each level's DomainID ranks
