@@ -1,5 +1,7 @@
 """Diagnostic: per-eval select-kernel time on the C3 bench batch (which evals
-form the kernel's critical path)."""
+form the kernel's critical path).  --prof loads the profiling build
+(`make -C kueue_oss_amd/csrc prof` first: it is not part of build() and does
+not ship with the tree unless built)."""
 import collections
 import json
 import os
