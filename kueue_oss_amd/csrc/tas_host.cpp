@@ -3446,7 +3446,7 @@ struct kueue_tas_host {
   std::vector<std::array<int32_t, 3>> admit_doms;
   std::vector<kueue_tas_fits_req> admit_fr;
   std::vector<kueue_tas_fits_term> admit_terms;
-  std::vector<std::pair<int32_t, int32_t>> admit_ps_terms;  // per PodSet of the workload: (term_begin, num_terms)
+  std::vector<int64_t> admit_toff;  // per admitted-round workload: first term
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
   float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
   // last kueue_tas_host_update_nodes: parse, node events, flush_joins, splice
@@ -4701,37 +4701,75 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     std::vector<kueue_tas_fits_term>& terms = h->admit_terms;
     std::vector<int64_t>& off = h->admit_off;
     std::vector<int32_t>& ids = h->admit_ids;
-    fr.clear();
-    terms.clear();
-    off.assign(1, 0);
     ids.clear();
-    for (size_t g = 0; g < W; g++) {
-      if (!seen[g]) continue;
-      ids.push_back(int32_t(g));
-      if (seen[g] == 1) {
+    for (size_t g = 0; g < W; g++)
+      if (seen[g]) ids.push_back(int32_t(g));
+    // per workload in id order: its records (one per domain; a failed
+    // evaluation one record that cannot fit) and its PodSets' single-pod
+    // request terms (once per PodSet, shared by the PodSet's domains):
+    // counted, offset, then written in place — both passes on the host pool
+    const size_t nw = ids.size();
+    std::vector<int64_t>& toff = h->admit_toff;
+    off.assign(nw + 1, 0);
+    toff.assign(nw + 1, 0);
+    std::atomic<bool> bad_col{false};
+    auto& pool = ktas_pool::HostPool::get();
+    pool.run(nw, 64, [&](size_t k0, size_t k1) {
+      std::vector<uint8_t> used;
+      for (size_t k = k0; k < k1; k++) {
+        const size_t g = size_t(ids[k]);
+        if (seen[g] != 1) {
+          off[k + 1] = 1;
+          continue;
+        }
         const Workload& wl = h->compiled[g];
-        // the PodSet's single-pod request terms once per workload, shared by its domains' records
-        std::vector<std::pair<int32_t, int32_t>>& psTerms = h->admit_ps_terms;
+        used.assign(wl.podsets.size(), 0);
+        int64_t nt = 0;
+        for (int64_t i = start[g]; i < start[g + 1]; i++) {
+          const size_t ps = size_t(doms[size_t(i)][0]);
+          if (!used[ps]) {
+            used[ps] = 1;
+            nt += int64_t(wl.podsets[ps].requestIds.size());
+          }
+        }
+        off[k + 1] = start[g + 1] - start[g];
+        toff[k + 1] = nt;
+      }
+    });
+    for (size_t k = 0; k < nw; k++) {
+      off[k + 1] += off[k];
+      toff[k + 1] += toff[k];
+    }
+    fr.resize(size_t(off[nw]));
+    terms.resize(size_t(toff[nw]));
+    pool.run(nw, 64, [&](size_t k0, size_t k1) {
+      std::vector<std::pair<int32_t, int32_t>> psTerms;
+      for (size_t k = k0; k < k1; k++) {
+        const size_t g = size_t(ids[k]);
+        int64_t r = off[k], t = toff[k];
+        if (seen[g] != 1) {  // a failed evaluation is never admitted: one record that cannot fit
+          fr[size_t(r)] = {-1, 0, int32_t(t), 0};
+          continue;
+        }
+        const Workload& wl = h->compiled[g];
         psTerms.assign(wl.podsets.size(), {-1, 0});
-        for (int64_t k = start[g]; k < start[g + 1]; k++) {
-          const auto& d = doms[size_t(k)];
+        for (int64_t i = start[g]; i < start[g + 1]; i++) {
+          const auto& d = doms[size_t(i)];
           auto& pt = psTerms[size_t(d[0])];
           if (pt.first < 0) {
-            pt.first = int32_t(terms.size());
-            for (auto& t : wl.podsets[size_t(d[0])].requestIds) {
-              const int32_t c = s.col_of(t.first);
-              if (c < 0) throw std::runtime_error("admit: request resource without a column");
-              terms.push_back({t.second, c, 0});
+            pt.first = int32_t(t);
+            for (auto& rq : wl.podsets[size_t(d[0])].requestIds) {
+              const int32_t c = s.col_of(rq.first);
+              if (c < 0) bad_col = true;
+              terms[size_t(t++)] = {rq.second, c, 0};
               pt.second++;
             }
           }
-          fr.push_back({d[1], d[2], pt.first, pt.second});
+          fr[size_t(r++)] = {d[1], d[2], pt.first, pt.second};
         }
-      } else {  // a failed evaluation is never admitted: one record that cannot fit
-        fr.push_back({-1, 0, int32_t(terms.size()), 0});
       }
-      off.push_back(int64_t(fr.size()));
-    }
+    });
+    if (bad_col) throw std::runtime_error("admit: request resource without a column");
     std::vector<int32_t> adm(ids.size(), 0);
     const auto pods = s.colByName.find("pods");
     const int32_t pods_col = pods == s.colByName.end() ? -1 : pods->second;
