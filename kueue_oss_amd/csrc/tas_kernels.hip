@@ -5709,7 +5709,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     int32_t* admitted, const int32_t* todo) {
   extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
   __shared__ int32_t sh_fit[kAdmitWindow];
-  __shared__ int32_t sh_conf;
+  __shared__ int32_t sh_conf[2];  // per admission attempt, alternating (one barrier per attempt)
   const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
   const int nwords = (s.N + 31) / 32;
   const bool in_lds = touched_in_lds != 0;
@@ -5731,6 +5731,16 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
       r0 = wl_off[w];
       r1 = wl_off[w + 1];
     }
+    // the candidate's first 64 records stay in registers: the overlap check
+    // and AddUsage of an admission then issue no dependent loads
+    int32_t c_leaf = -1, c_count = 0, c_status = kAdmitNever;
+    int32_t c_col[kAdmitTerms];
+    int64_t c_val[kAdmitTerms];
+#pragma unroll
+    for (int u = 0; u < kAdmitTerms; u++) {
+      c_col[u] = -1;
+      c_val[u] = 0;
+    }
     bool fit = false;
     if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
       fit = true;
@@ -5739,6 +5749,16 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
         bool ok = true;
         if (i < r1) {
           const AdmitRec a = recs[i];
+          if (base == r0) {
+            c_leaf = a.leaf;
+            c_count = a.count;
+            c_status = a.status;
+#pragma unroll
+            for (int u = 0; u < kAdmitTerms; u++) {
+              c_col[u] = a.col[u];
+              c_val[u] = a.val[u];
+            }
+          }
           if (exact || a.status == kAdmitWide) {
             ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
           } else if (a.status == kAdmitNever) {
@@ -5765,46 +5785,66 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
         if (wave == k && lane == 0) admitted[w] = 0;
         continue;
       }
-      if (nadm > 0) {  // a later fitting candidate: its check holds unless it shares a leaf with this round's admissions
-        if (!chain) break;
-        if (wave == k) {
-          bool hit = false;
+      if (nadm > 0 && !chain) break;  // without the round bitmap: one admission per round
+      if (wave == k) {
+        // a later fitting candidate's check holds unless it shares a leaf with
+        // this round's admissions; if it does not, it is admitted at once
+        bool hit = false;
+        if (nadm > 0)
           for (int64_t base = r0; base < r1 && !hit; base += kWave) {
             const int64_t i = base + lane;
-            const int32_t leaf = i < r1 ? recs[i].leaf : -1;
+            const int32_t leaf = i >= r1 ? -1 : base == r0 ? c_leaf : recs[i].leaf;
             hit = ballot(leaf >= 0 && ((round_lds[leaf >> 5] >> (leaf & 31)) & 1u)) != 0;
           }
-          if (lane == 0) sh_conf = hit ? 1 : 0;
-        }
-        __syncthreads();
-        if (sh_conf) break;
-      }
-      if (wave == k) {  // admit: AddUsage over its records, the wave's lanes a share each
-        for (int64_t i = r0 + lane; i < r1; i += kWave) {
-          const kueue_tas_fits_req r = reqs[i];
-          uint32_t bits = 0;
-          for (int q = 0; q < r.num_terms; q++) {
-            const kueue_tas_fits_term t = terms[r.term_begin + q];
-            if (t.col >= 0) {  // the host gives every usage resource a column first
-              atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + r.leaf),
-                        (unsigned long long)(uint64_t(t.value) * uint64_t(int64_t(r.count))));
-              bits |= 1u << t.col;
+        if (!hit) {  // admit: AddUsage over its records, the wave's lanes a share each
+          for (int64_t base = r0; base < r1; base += kWave) {
+            const int64_t i = base + lane;
+            if (i >= r1) continue;
+            int32_t leaf;
+            uint32_t bits = 0;
+            int64_t count;
+            if (base == r0 && !exact && c_status != kAdmitWide) {  // the record's terms are in registers
+              leaf = c_leaf;
+              count = c_count;
+#pragma unroll
+              for (int u = 0; u < kAdmitTerms; u++)
+                if (c_col[u] >= 0) {  // the host gives every usage resource a column first
+                  atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(c_col[u]) * s.N + leaf),
+                            (unsigned long long)(uint64_t(c_val[u]) * uint64_t(count)));
+                  bits |= 1u << c_col[u];
+                }
+            } else {
+              const kueue_tas_fits_req r = reqs[i];
+              leaf = r.leaf;
+              count = r.count;
+              for (int q = 0; q < r.num_terms; q++) {
+                const kueue_tas_fits_term t = terms[r.term_begin + q];
+                if (t.col >= 0) {
+                  atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(t.col) * s.N + leaf),
+                            (unsigned long long)(uint64_t(t.value) * uint64_t(count)));
+                  bits |= 1u << t.col;
+                }
+              }
             }
+            if (pods_col >= 0) {
+              atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + leaf),
+                        (unsigned long long)count);
+              bits |= 1u << pods_col;
+            }
+            atomicOr(usage_present + leaf, bits);
+            if (in_lds) atomicOr(touched_lds + (leaf >> 5), 1u << (leaf & 31));
+            else atomicOr(touched_global + (leaf >> 5), 1u << (leaf & 31));
+            if (chain) atomicOr(round_lds + (leaf >> 5), 1u << (leaf & 31));
           }
-          if (pods_col >= 0) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(pods_col) * s.N + r.leaf),
-                      (unsigned long long)int64_t(r.count));
-            bits |= 1u << pods_col;
-          }
-          atomicOr(usage_present + r.leaf, bits);
-          if (in_lds) atomicOr(touched_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
-          else atomicOr(touched_global + (r.leaf >> 5), 1u << (r.leaf & 31));
-          if (chain) atomicOr(round_lds + (r.leaf >> 5), 1u << (r.leaf & 31));
+          if (lane == 0) admitted[w] = 1;
         }
-        if (lane == 0) admitted[w] = 1;
+        if (lane == 0) sh_conf[nadm & 1] = hit ? 1 : 0;
+      }
+      if (chain) {  // the verdict, and the round's leaves for the next candidate's overlap check
+        __syncthreads();
+        if (sh_conf[nadm & 1]) break;
       }
       nadm++;
-      if (chain) __syncthreads();  // the round's leaves visible to the next candidate's overlap check
     }
     // todo[1 + w0 .. w0 + k - 1] are decided; w0 + k (if any) is checked again
     admit_drain();  // this wave's atomics performed at L2 before any wave's next loads
