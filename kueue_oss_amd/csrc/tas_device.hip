@@ -1137,7 +1137,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_recs = o_out + al((n_wl + 2) * 4);  // + two diagnostics words (admit_window_kernel)
   const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
   const size_t o_todo = o_dep + al(n_wl * 4);
-  const size_t o_minc = o_todo + al((n_wl + 1) * 4);
+  const size_t o_todor = o_todo + al((n_wl + 1) * 4);
+  const size_t o_minc = o_todor + al(n_wl * 16);
   const size_t o_bits = o_minc + al(size_t(c->snap.N) * 4);
   HIPCHK(c, c->d_fits.ensure(o_bits + nwords * 4));
   HIPCHK(c, c->h_stage.ensure(up_bytes));
@@ -1191,7 +1192,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
       HIPCHK(c, hipGetLastError());
     }
     hipLaunchKernelGGL(admit_todo_kernel, dim3(1), dim3(1024), 0, c->stream, int(n_wl), fit0d, depd, indep ? 0 : 1,
-                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo));
+                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo),
+                       reinterpret_cast<const int64_t*>(d + o_off), reinterpret_cast<int64_t*>(d + o_todor));
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
                        lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
@@ -1199,7 +1201,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
                        reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
-                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<const int32_t*>(d + o_todo));
+                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<const int32_t*>(d + o_todo),
+                       reinterpret_cast<const int64_t*>(d + o_todor));
   } else {  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),

@@ -5507,9 +5507,11 @@ __global__ __launch_bounds__(256) void admit_indep_kernel(DevSnap s, int64_t* ta
 }
 // One workgroup: the verdicts decided so far (phase-1 failures 0,
 // independent candidates 1) and the rest — every candidate in exact mode —
-// compacted in order into todo[1 ..], todo[0] = their count.
+// compacted in order into todo[1 ..], todo[0] = their count, and their
+// record ranges into todo_r[2 j], todo_r[2 j + 1].
 __global__ __launch_bounds__(1024) void admit_todo_kernel(int n_wl, const int32_t* wl_fit0, const int32_t* dep,
-                                                          int exact, int32_t* admitted, int32_t* todo) {
+                                                          int exact, int32_t* admitted, int32_t* todo,
+                                                          const int64_t* wl_off, int64_t* todo_r) {
   __shared__ int32_t sh_wave[16];
   const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
   int32_t base = 0;
@@ -5529,7 +5531,12 @@ __global__ __launch_bounds__(1024) void admit_todo_kernel(int n_wl, const int32_
       if (k < wave) off += sh_wave[k];
       total += sh_wave[k];
     }
-    if (flag) todo[1 + off + below] = w;
+    if (flag) {
+      const int j = off + below;
+      todo[1 + j] = w;
+      todo_r[2 * j] = wl_off[w];  // its record range: one load level less in the window kernel
+      todo_r[2 * j + 1] = wl_off[w + 1];
+    }
     base += total;
     __syncthreads();
   }
@@ -5706,7 +5713,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
     const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
     const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
-    int32_t* admitted, const int32_t* todo) {
+    int32_t* admitted, const int32_t* todo, const int64_t* todo_r) {
   extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
   __shared__ int32_t sh_fit[kAdmitWindow];
   __shared__ int32_t sh_conf[2];  // per admission attempt, alternating (one barrier per attempt)
@@ -5723,24 +5730,37 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
   __syncthreads();
   int w0 = 0;  // position in the todo list
   int rounds = 0;
+  int pf_pos = -1, pf_w = n_wl;  // the next window's candidate, fetched during this round
+  int64_t pf_r0 = 0, pf_r1 = 0;
   while (w0 < ntodo) {  // block-uniform
     rounds++;
-    const int w = w0 + wave < ntodo ? todo[1 + w0 + wave] : n_wl;
+    const int pos = w0 + wave;
+    int w = n_wl;
     int64_t r0 = 0, r1 = 0;
-    if (w < n_wl) {
-      r0 = wl_off[w];
-      r1 = wl_off[w + 1];
+    if (pos < ntodo) {
+      if (pf_pos == pos) {  // the previous window was decided whole
+        w = pf_w;
+        r0 = pf_r0;
+        r1 = pf_r1;
+      } else {
+        w = todo[1 + pos];
+        r0 = todo_r[2 * pos];
+        r1 = todo_r[2 * pos + 1];
+      }
+    }
+    pf_pos = pos + kAdmitWindow;
+    if (pf_pos < ntodo) {
+      pf_w = todo[1 + pf_pos];
+      pf_r0 = todo_r[2 * pf_pos];
+      pf_r1 = todo_r[2 * pf_pos + 1];
     }
     // the candidate's first 64 records stay in registers: the overlap check
     // and AddUsage of an admission then issue no dependent loads
     int32_t c_leaf = -1, c_count = 0, c_status = kAdmitNever;
-    int32_t c_col[kAdmitTerms];
+    uint32_t c_col[kAdmitTerms / 4] = {};  // column + 1 per byte (0: none; columns < KUEUE_TAS_MAX_COLS)
     int64_t c_val[kAdmitTerms];
 #pragma unroll
-    for (int u = 0; u < kAdmitTerms; u++) {
-      c_col[u] = -1;
-      c_val[u] = 0;
-    }
+    for (int u = 0; u < kAdmitTerms; u++) c_val[u] = 0;
     bool fit = false;
     if (w < n_wl && (wl_fit0[w] != 0 || exact)) {
       fit = true;
@@ -5755,7 +5775,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
             c_status = a.status;
 #pragma unroll
             for (int u = 0; u < kAdmitTerms; u++) {
-              c_col[u] = a.col[u];
+              c_col[u >> 2] |= uint32_t(a.col[u] + 1) << (8 * (u & 3));
               c_val[u] = a.val[u];
             }
           }
@@ -5807,12 +5827,14 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
               leaf = c_leaf;
               count = c_count;
 #pragma unroll
-              for (int u = 0; u < kAdmitTerms; u++)
-                if (c_col[u] >= 0) {  // the host gives every usage resource a column first
-                  atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(c_col[u]) * s.N + leaf),
+              for (int u = 0; u < kAdmitTerms; u++) {
+                const int col = int((c_col[u >> 2] >> (8 * (u & 3))) & 0xffu) - 1;
+                if (col >= 0) {  // the host gives every usage resource a column first
+                  atomicAdd(reinterpret_cast<unsigned long long*>(tas_usage + int64_t(col) * s.N + leaf),
                             (unsigned long long)(uint64_t(c_val[u]) * uint64_t(count)));
-                  bits |= 1u << c_col[u];
+                  bits |= 1u << col;
                 }
+              }
             } else {
               const kueue_tas_fits_req r = reqs[i];
               leaf = r.leaf;
