@@ -605,14 +605,21 @@ class FlavorSnapshot {
   void sync_node(const kjson::Node& n) {
     bool ready, unsched;
     NodeInfo ni = parse_node(n, &ready, &unsched);
+    sync_node(std::move(ni), ready, unsched);
+  }
+  // the cache state's copy of an event's node (nodesCache.sync,
+  // tas_nodes_cache.go:38-50), from the event's parsed form
+  void sync_node(NodeInfo ni, bool ready, bool unsched) {
     auto it = nodeCache.find(ni.name);
     if (ready && !unsched) {
       if (it == nodeCache.end()) {
         nodeOrderPos[ni.name] = nodeCacheOrder.size();
         nodeCacheOrder.push_back(ni.name);
         nodeOrderLive.push_back(1);
+        nodeCache.emplace(ni.name, std::move(ni));
+      } else {
+        it->second = std::move(ni);
       }
-      nodeCache[ni.name] = std::move(ni);
     } else if (it != nodeCache.end()) {
       auto p = nodeOrderPos.find(ni.name);
       nodeOrderLive[p->second] = 0;
@@ -1049,9 +1056,10 @@ class FlavorSnapshot {
     for (auto& nm : leafNodeNames[size_t(leaf)]) req_add(alloc, nodes[nodeIdx.at(nm)].allocatable);
     leafAlloc[size_t(leaf)] = std::move(alloc);
   }
-  bool node_event_in_place(const kjson::Node& n, std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
-    bool ready, unsched;
-    NodeInfo ni = parse_node(n, &ready, &unsched);
+  // `ni`, `ready`, `unsched`: the event's node as parse_node reads it (the
+  // batch's events are parsed on the host pool first)
+  bool node_event_in_place(NodeInfo&& ni, bool ready, bool unsched, std::set<int32_t>* touched,
+                           std::set<int32_t>* liveChanged) {
     const bool member = member_of(ni, ready, unsched);
     const int L = this->L();
     auto ix = nodeIdx.find(ni.name);
@@ -1069,11 +1077,11 @@ class FlavorSnapshot {
     }
     if (ix == nodeIdx.end()) {
       if (!member) {  // not in the snapshot before or after
-        sync_node(n);
+        sync_node(std::move(ni), ready, unsched);
         return true;
       }
       auto left = leftNodes.find(ni.name);
-      if (left == leftNodes.end()) return add_node(n, std::move(ni), touched, liveChanged);  // a new node
+      if (left == leftNodes.end()) return add_node(std::move(ni), touched, liveChanged);  // a new node
       const int32_t leaf = left->second.first;
       const size_t slot = left->second.second;
       std::vector<std::string> lv;
@@ -1081,14 +1089,14 @@ class FlavorSnapshot {
       if (lv != values[size_t(L - 1)][size_t(leaf)] ||
           (lowestIsHostname && ni.labels.at(kHostname) != leafId[size_t(leaf)])) {  // back at another position
         leftNodes.erase(left);
-        return add_node(n, std::move(ni), touched, liveChanged);
+        return add_node(std::move(ni), touched, liveChanged);
       }
       bool changed = false, relayout = false;
       const int32_t prof = register_attrs(ni, &changed, &relayout);
       if (changed) new_layout();
       if (relayout) dirty = true;
       // back in: the node's slot, its leaf (alive again when it was its last node)
-      sync_node(n);
+      sync_node(ni, true, false);
       nodeIdx[ni.name] = slot;
       nodeToLeaf[ni.name] = leafId[size_t(leaf)];
       leafNodeNames[size_t(leaf)].push_back(ni.name);
@@ -1125,18 +1133,23 @@ class FlavorSnapshot {
       leftNodes[ni.name] = {leaf, ix->second};
       nodeToLeaf.erase(ni.name);
       nodeIdx.erase(ix);
-      sync_node(n);
+      if (!moved) {
+        sync_node(std::move(ni), ready, unsched);
+        realloc_leaf(leaf);
+        touched->insert(leaf);
+        return true;
+      }
+      sync_node(ni, ready, unsched);
       realloc_leaf(leaf);
       touched->insert(leaf);
-      if (!moved) return true;
       leftNodes.erase(ni.name);
-      return add_node(n, std::move(ni), touched, liveChanged);
+      return add_node(std::move(ni), touched, liveChanged);
     }
     bool changed = false, relayout = false;
     const int32_t prof = register_attrs(ni, &changed, &relayout);
     if (changed) new_layout();
     if (relayout) dirty = true;
-    sync_node(n);
+    sync_node(ni, true, false);
     set_attrs(cur, std::move(ni), leaf, prof);
     realloc_leaf(leaf);
     touched->insert(leaf);
@@ -1153,7 +1166,7 @@ class FlavorSnapshot {
   // The device arrays reload (one upload); compiled requests recompile
   // (new_layout).  false (rebuild) only for a second node under an existing
   // hostname (leafDomain.node is the first one, :165-191).
-  bool add_node(const kjson::Node& n, NodeInfo&& ni, std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {
+  bool add_node(NodeInfo&& ni, std::set<int32_t>* touched, std::set<int32_t>* liveChanged) {  // a member: ready, schedulable
     const int L = this->L();
     std::vector<std::string> lv;
     for (auto& k : levelKeys) lv.push_back(ni.labels.at(k));
@@ -1163,7 +1176,7 @@ class FlavorSnapshot {
       for (size_t k = 0; k < lv.size(); k++) id += (k ? "," : "") + lv[k];
     if (const int32_t leaf = leafById.find(id); leaf >= 0) {
       if (lowestIsHostname || values[size_t(L - 1)][size_t(leaf)] != lv) return false;
-      sync_node(n);  // another node of an aggregated leaf
+      sync_node(ni, true, false);  // another node of an aggregated leaf
       nodes.push_back(std::move(ni));
       const NodeInfo& nd = nodes.back();
       nodeIdx[nd.name] = nodes.size() - 1;
@@ -1180,7 +1193,7 @@ class FlavorSnapshot {
     }
     bool changed = false, relayout = false;
     const int32_t prof = register_attrs(ni, &changed, &relayout);
-    sync_node(n);
+    sync_node(ni, true, false);
     nodes.push_back(std::move(ni));
     const NodeInfo& nd = nodes.back();
     nodeIdx[nd.name] = nodes.size() - 1;
@@ -4168,10 +4181,25 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
     const double t0 = now_ms();
     kjson::Node arr = kjson::parse(nodes_json);
     const double t1 = now_ms();
+    // every event's node parsed on the host pool, then applied in order
+    const size_t ne = arr.items.size();
+    std::vector<NodeInfo> parsed(ne);
+    std::vector<char> ready(ne), unsched(ne);
+    auto parse_range = [&](size_t b, size_t e) {
+      for (size_t q = b; q < e; q++) {
+        bool r, u;
+        parsed[q] = FlavorSnapshot::parse_node(arr.items[q], &r, &u);
+        ready[q] = r;
+        unsched[q] = u;
+      }
+    };
+    if (ne >= 16) ktas_pool::HostPool::get().run(ne, 4, parse_range);
+    else parse_range(0, ne);
     std::set<int32_t> touched, liveChanged;
     size_t k = 0;
-    for (; k < arr.items.size(); k++)
-      if (!h->snap->node_event_in_place(arr.items[k], &touched, &liveChanged)) break;
+    for (; k < ne; k++)
+      if (!h->snap->node_event_in_place(std::move(parsed[k]), ready[k] != 0, unsched[k] != 0, &touched, &liveChanged))
+        break;
     const bool structural = k < arr.items.size();
     const double t2 = now_ms();
     if (structural) {  // rebuilt from the cache state, which holds the pending joins
