@@ -3455,6 +3455,8 @@ struct kueue_tas_host {
   double admit_ms[3] = {0, 0, 0};            // last admit: host prep, kueue_tas_admit, delta list
   // admit's working storage (kept between rounds)
   std::vector<int32_t> admit_seen, admit_ids;
+  std::vector<int32_t> admit_pseen;  // [part][workload] of the record passes on the host pool
+  std::vector<int64_t> admit_pcnt;
   std::vector<int64_t> admit_start, admit_off;
   std::vector<std::array<int32_t, 3>> admit_doms;
   std::vector<kueue_tas_fits_req> admit_fr;
@@ -4684,16 +4686,50 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     // nothing is admitted when the caller's buffer is short
     const size_t W = h->compiled.size();
     std::vector<int32_t>& seen = h->admit_seen;  // per id: 0 absent, 1 present, 2 failed evaluation
+    // the records in the host pool's static parts: per part and workload, the
+    // presence mark and the record count (pass 1), then each part scatters its
+    // records behind the earlier parts' (pass 2) — the order of one serial pass
+    const size_t R = len / 4;
+    auto& pool = ktas_pool::HostPool::get();
+    const size_t T = pool.parts();
+    auto part_of = [&](size_t b) {
+      size_t t = 0;
+      while (t + 1 < T && ktas_pool::HostPool::part_begin(R, t + 1, T) <= b) t++;
+      return t;
+    };
+    const int64_t Nleaf = h->snap->N();
+    std::vector<int32_t>& pseen = h->admit_pseen;
+    std::vector<int64_t>& pcnt = h->admit_pcnt;
+    pseen.assign(T * W, 0);
+    pcnt.assign(T * W, 0);
+    std::atomic<bool> bad_g{false}, bad_r{false};
+    pool.run_static(R, [&](size_t b, size_t e) {
+      if (b >= e) return;
+      const size_t t = part_of(b);
+      int32_t* sn = pseen.data() + t * W;
+      int64_t* cnt = pcnt.data() + t * W;
+      for (size_t q = b; q < e; q++) {
+        const int32_t* r = recs + 4 * q;
+        const int32_t g = r[0];
+        if (g < 0 || size_t(g) >= W) {
+          bad_g = true;
+          return;
+        }
+        if (r[1] < 0) {
+          sn[g] = r[2] != 0 ? 2 : std::max(sn[g], 1);
+        } else {
+          sn[g] = std::max(sn[g], 1);
+          if (size_t(r[1]) >= h->compiled[size_t(g)].podsets.size() || r[2] < 0 || r[2] >= Nleaf) bad_r = true;
+          else cnt[g]++;
+        }
+      }
+    });
+    if (bad_g) throw std::runtime_error("admit: workload id out of range");
     seen.assign(W, 0);
     size_t nwl = 0;
-    for (size_t o = 0; o < len; o += 4) {
-      const int32_t g = recs[o];
-      if (g < 0 || size_t(g) >= W) throw std::runtime_error("admit: workload id out of range");
-      if (!seen[size_t(g)]) {
-        seen[size_t(g)] = 1;
-        nwl++;
-      }
-    }
+    for (size_t t = 0; t < T; t++)
+      for (size_t g = 0; g < W; g++) seen[g] = std::max(seen[g], pseen[t * W + g]);
+    for (size_t g = 0; g < W; g++) nwl += seen[g] != 0;
     *n_workloads = nwl;
     if (!admitted || admitted_cap < 2 * nwl) return KUEUE_TAS_EOVERFLOW;
     h->last_deltas.clear();
@@ -4704,27 +4740,29 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       h->err = s.err;
       return rc;
     }
-    // records of each workload, grouped by id with a counting sort
+    if (bad_r) throw std::runtime_error("admit: record out of range");
+    // records of each workload, grouped by id (a counting sort over the parts)
     std::vector<int64_t>& start = h->admit_start;
     start.assign(W + 1, 0);
-    for (size_t o = 0; o < len; o += 4) {
-      const int32_t g = recs[o];
-      if (recs[o + 1] < 0) {
-        if (recs[o + 2] != 0) seen[size_t(g)] = 2;
-      } else {
-        if (size_t(recs[o + 1]) >= h->compiled[size_t(g)].podsets.size() || recs[o + 2] < 0 || recs[o + 2] >= s.N())
-          throw std::runtime_error("admit: record out of range");
-        start[size_t(g) + 1]++;
+    for (size_t g = 0; g < W; g++) {
+      int64_t c = start[g];
+      for (size_t t = 0; t < T; t++) {  // part t's first slot for workload g
+        const int64_t k = pcnt[t * W + g];
+        pcnt[t * W + g] = c;
+        c += k;
       }
+      start[g + 1] = c;
     }
-    for (size_t g = 0; g < W; g++) start[g + 1] += start[g];
     std::vector<std::array<int32_t, 3>>& doms = h->admit_doms;  // podset, leaf, count
     doms.resize(size_t(start[W]));
-    {
-      std::vector<int64_t> pos(start.begin(), start.end() - 1);
-      for (size_t o = 0; o < len; o += 4)
-        if (recs[o + 1] >= 0) doms[size_t(pos[size_t(recs[o])]++)] = {recs[o + 1], recs[o + 2], recs[o + 3]};
-    }
+    pool.run_static(R, [&](size_t b, size_t e) {
+      if (b >= e) return;
+      int64_t* pos = pcnt.data() + part_of(b) * W;
+      for (size_t q = b; q < e; q++) {
+        const int32_t* r = recs + 4 * q;
+        if (r[1] >= 0) doms[size_t(pos[size_t(r[0])]++)] = {r[1], r[2], r[3]};
+      }
+    });
     std::vector<kueue_tas_fits_req>& fr = h->admit_fr;
     std::vector<kueue_tas_fits_term>& terms = h->admit_terms;
     std::vector<int64_t>& off = h->admit_off;
@@ -4741,7 +4779,6 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
     off.assign(nw + 1, 0);
     toff.assign(nw + 1, 0);
     std::atomic<bool> bad_col{false};
-    auto& pool = ktas_pool::HostPool::get();
     pool.run(nw, 64, [&](size_t k0, size_t k1) {
       std::vector<uint8_t> used;
       for (size_t k = k0; k < k1; k++) {
