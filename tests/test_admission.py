@@ -170,3 +170,36 @@ def test_admit_window_matches_serial_c3_on_gpu():
     assert (out[0][0] == out[1][0]).all()
     assert (out[0][1] == out[1][1]).all()
     assert 0 < int(out[0][0][:, 1].sum()) < len(wls)
+
+
+def test_emulated_admit_record_order_and_errors(emu_lib):  # noqa: F811
+    """kueue_tas_host_admit groups the quads per workload in the host pool's
+    static parts: any quad order gives the same decisions and deltas as the
+    gathered order; a workload id or record out of range is an error."""
+    import numpy as np
+
+    snap_doc, wls = synth.config_c2(n_workloads=64, shape=(2, 2, 4, 8))
+
+    def fresh():
+        s = TASFlavorSnapshot(snap_doc, lib=emu_lib)
+        s.compile(wls)
+        s.run_compiled()
+        return s
+
+    s = fresh()
+    q = np.asarray(s.last_assignments(), dtype=np.int32).reshape(-1, 4)
+    a1, d1 = s.admit(q.ravel())
+    s.close()
+    assert len(q) > 64 and a1[:, 1].any() and not a1[:, 1].all()
+    s = fresh()
+    a2, d2 = s.admit(np.ascontiguousarray(q[::-1]).ravel())
+    s.close()
+    assert a1.tolist() == a2.tolist()
+    assert np.array_equal(np.sort(d1, order=["leaf", "col"]), np.sort(d2, order=["leaf", "col"]))
+    for field, value, msg in ((0, 10**6, "workload id out of range"), (2, 10**7, "record out of range")):
+        bad = q.copy()
+        bad[np.nonzero(bad[:, 1] >= 0)[0][len(q) // 3], field] = value
+        s = fresh()
+        with pytest.raises(RuntimeError, match=msg):
+            s.admit(bad.ravel())
+        s.close()
