@@ -1075,37 +1075,41 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   // on the device, no int64 arithmetic of the call wraps)
   ktas_pool::HostPool& pool = ktas_pool::HostPool::get();
   const size_t nparts = pool.parts();
-  struct AdmitPart {
+  struct alignas(64) AdmitPart {  // one per worker, on cache lines of its own
     __int128 total[KUEUE_TAS_MAX_COLS];
     bool exact;
     int err;  // 0, 1: record out of range, 2: term column out of range
   };
   std::vector<AdmitPart> parts(nparts);
+  const int32_t snapN = c->snap.N, snapR = c->snap.R;
   pool.run_static(n, [&](size_t i0, size_t i1) {
     size_t t = 0;
     while (t + 1 < nparts && ktas_pool::HostPool::part_begin(n, t + 1, nparts) <= i0) t++;
-    AdmitPart& ap = parts[t];
-    memset(ap.total, 0, sizeof ap.total);
-    ap.exact = false;
-    ap.err = 0;
-    for (size_t i = i0; i < i1 && !ap.err; i++) {
+    __int128 tot[KUEUE_TAS_MAX_COLS] = {};  // accumulated on the worker's stack, stored once
+    bool ex = false;
+    int err = 0;
+    for (size_t i = i0; i < i1 && !err; i++) {
       const kueue_tas_fits_req& r = reqs[i];
-      if (r.leaf >= c->snap.N || r.num_terms < 0 || r.term_begin < 0 || size_t(r.term_begin) + size_t(r.num_terms) > num_terms) {
-        ap.err = 1;
+      if (r.leaf >= snapN || r.num_terms < 0 || r.term_begin < 0 || size_t(r.term_begin) + size_t(r.num_terms) > num_terms) {
+        err = 1;
         break;
       }
-      ap.exact = ap.exact || r.count < 0;
+      ex = ex || r.count < 0;
       for (int k = 0; k < r.num_terms; k++) {
         const kueue_tas_fits_term& tm = terms[r.term_begin + k];
-        if (tm.col < 0 || tm.col >= c->snap.R) {
-          ap.err = 2;
+        if (tm.col < 0 || tm.col >= snapR) {
+          err = 2;
           break;
         }
-        ap.exact = ap.exact || tm.value < 0;
-        if (tm.col < KUEUE_TAS_MAX_COLS) ap.total[tm.col] += __int128(tm.value) * r.count;
+        ex = ex || tm.value < 0;
+        if (tm.col < KUEUE_TAS_MAX_COLS) tot[tm.col] += __int128(tm.value) * r.count;
       }
-      if (pods_col >= 0) ap.total[pods_col] += r.count;
+      if (pods_col >= 0) tot[pods_col] += r.count;
     }
+    AdmitPart& ap = parts[t];
+    memcpy(ap.total, tot, sizeof tot);
+    ap.exact = ex;
+    ap.err = err;
   });
   bool exact = false;
   __int128 total[KUEUE_TAS_MAX_COLS] = {};  // per column: the most usage this call can add
