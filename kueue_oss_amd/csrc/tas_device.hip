@@ -113,7 +113,7 @@ struct FlatMap {
 
 // One static part's phase-1 classes (eval_chunk): chains of local classes
 // per 64-bit class hash, each local class's first member.
-struct PartClasses {
+struct alignas(64) PartClasses {  // one per host part, on cache lines of its own
   FlatMap head;
   std::vector<int32_t> rep, next;
 };
@@ -1315,12 +1315,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   pool.run_static(n, [&](size_t i0, size_t i1) {
     const size_t ch = part_of(i0);
     std::string msg;
+    int32_t mt = 1;  // this part's widest request, stored once (the parts' slots share a cache line)
     for (size_t i = i0; i < i1; i++) {
       const auto& r = *reqs[i];
       if (errs[ch].first == SIZE_MAX && !validate(i, &msg)) errs[ch] = {i, msg};
       toff[i + 1] = int64_t(std::max(r.num_req, 0)) + int64_t(std::max(r.num_leader_req, 0));
-      chunk_maxt[ch] = std::max(chunk_maxt[ch], std::max(r.num_req, r.num_leader_req));
+      mt = std::max(mt, std::max(r.num_req, r.num_leader_req));
     }
+    chunk_maxt[ch] = mt;
   });
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);

@@ -2678,7 +2678,7 @@ struct Evaluator {
   // tables and rebases its records' offsets.  Same batch as build_pass
   // (taint rows are deduplicated within a part only: equal rows compare
   // equal by value wherever they are).
-  struct PartBatch {
+  struct alignas(64) PartBatch {  // one per host part, on cache lines of its own
     std::vector<const kueue_tas_eval_req*> rq;
     std::vector<std::pair<size_t, GroupEval*>> bt, early;
     std::vector<int32_t> tt;
