@@ -505,6 +505,10 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   s.tag_out = nullptr;
   s.ent_base = nullptr;
   const bool tags_were_on = c->leaf_tags_on;
+  // from here on the context's tables describe the new tree: a failure below
+  // leaves it unloaded (every call then reports ENOSNAPSHOT) rather than
+  // holding the old snapshot beside the new dead-leaf map
+  c->loaded = false;
   c->leaf_tags_on = false;
   s.n_live = s.N;
   // a splice keeps the leaves that had left out: their flags move with them

@@ -2696,13 +2696,10 @@ struct Evaluator {
     HostPool& pool = HostPool::get();
     const size_t T = pool.parts(), W = wls.size();
     partBatch.resize(T);
-    auto part_of = [&](size_t b) {
-      size_t t = 0;
-      while (t + 1 < T && HostPool::part_begin(W, t + 1, T) <= b) t++;
-      return t;
-    };
-    pool.run_static(W, [&](size_t b, size_t e) {
-      PartBatch& pb = partBatch[part_of(b)];
+    // every part is cleared here, not in its task: run_static skips empty
+    // parts (W < parts()), and a part left from a larger batch would still
+    // be merged below with pointers into that batch's workloads
+    for (auto& pb : partBatch) {
       pb.rq.clear();
       pb.bt.clear();
       pb.early.clear();
@@ -2710,6 +2707,14 @@ struct Evaluator {
       pb.rows.clear();
       pb.af.clear();
       pb.afv.clear();
+    }
+    auto part_of = [&](size_t b) {
+      size_t t = 0;
+      while (t + 1 < T && HostPool::part_begin(W, t + 1, T) <= b) t++;
+      return t;
+    };
+    pool.run_static(W, [&](size_t b, size_t e) {
+      PartBatch& pb = partBatch[part_of(b)];
       for (size_t w = b; w < e; w++) {
         if (done[w] || wls[w].groups.empty()) continue;
         GroupEval& g = wls[w].groups[0];

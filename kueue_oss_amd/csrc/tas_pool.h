@@ -8,6 +8,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -77,6 +78,8 @@ class HostPool {
     size_t n = 0, grain = 1, chunks = 0;
     bool fixed = false;  // run_static: chunk t is thread t's part
     std::atomic<size_t> next{0}, done{0};
+    std::mutex errMu;
+    std::exception_ptr err;  // the first exception a chunk threw, rethrown on the caller
   };
   void submit(size_t n, size_t grain, std::function<void(size_t, size_t)>* f, bool fixed) {
     std::lock_guard<std::mutex> one(callMu_);
@@ -93,9 +96,22 @@ class HostPool {
     }
     cv_.notify_all();
     work(*job, 0);
+    // every chunk has finished (thrown or not) before `f` — on the caller's
+    // stack — goes out of scope
     while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
-    std::lock_guard<std::mutex> lk(mu_);
-    job_.reset();  // late workers keep their reference; its chunks are exhausted
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_.reset();  // late workers keep their reference; its chunks are exhausted
+    }
+    if (job->err) std::rethrow_exception(job->err);
+  }
+  static void call(Job& j, size_t b, size_t e) {
+    try {
+      (*j.fn)(b, e);
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(j.errMu);
+      if (!j.err) j.err = std::current_exception();
+    }
   }
   HostPool() {
     size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
@@ -115,7 +131,7 @@ class HostPool {
   void work(Job& j, size_t self) {
     if (j.fixed) {  // this thread's own part only
       const size_t T = j.chunks;
-      (*j.fn)(part_begin(j.n, self, T), part_begin(j.n, self + 1, T));
+      call(j, part_begin(j.n, self, T), part_begin(j.n, self + 1, T));
       j.done.fetch_add(1, std::memory_order_release);
       return;
     }
@@ -123,7 +139,7 @@ class HostPool {
       const size_t c = j.next.fetch_add(1, std::memory_order_relaxed);
       if (c >= j.chunks) return;
       const size_t b = c * j.grain;
-      (*j.fn)(b, std::min(j.n, b + j.grain));
+      call(j, b, std::min(j.n, b + j.grain));
       j.done.fetch_add(1, std::memory_order_release);
     }
   }

@@ -74,3 +74,28 @@ def test_run_modes_c3j_on_gpu():
     # ragged racks (no fused roll-up) and one phase-1 class per workload
     snap_doc, wls = synth.config_c3j(n_workloads=96, shape=(2, 8, 16))
     _modes(lambda d: TASFlavorSnapshot(d), snap_doc, wls)
+
+
+def _shrinking_batches(make_snap, snap_doc, wls):
+    """A compiled batch smaller than the host pool's part count after a larger
+    one on the same handle (parts the smaller batch leaves empty
+    must not keep the larger batch's entries)."""
+    snap = make_snap(snap_doc)
+    for sub in (wls, wls[:1], wls[:3], wls):
+        want, _ = oracle_lib.eval_workloads(snap_doc, sub, threads=4)
+        snap.compile(sub)
+        for flags in (TASFlavorSnapshot.RUN_COMPILE, TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES):
+            snap.run_compiled(flags=flags)
+            assert snap.last_results() == want, (len(sub), flags)
+    snap.close()
+
+
+def test_emulated_shrinking_batches(emu_lib):
+    snap_doc, wls = synth.config_c3(n_workloads=24, shape=(2, 2, 8, 16))
+    _shrinking_batches(lambda d: TASFlavorSnapshot(d, lib=emu_lib), snap_doc, wls)
+
+
+@pytest.mark.gpu
+def test_shrinking_batches_on_gpu():
+    snap_doc, wls = synth.config_c3(n_workloads=64, shape=(2, 4, 16, 32))
+    _shrinking_batches(lambda d: TASFlavorSnapshot(d), snap_doc, wls)

@@ -362,8 +362,6 @@ def _check_grow(seed, n, lib=None):
     assert steps_total > 50
     # joins splice the device snapshot; a reload only for a new resource or label column
     assert spliced > 20 and reloaded < spliced / 4, (spliced, reloaded)
-    # joins splice the device snapshot; a reload only for a new resource or label column
-    assert spliced > 20 and reloaded < spliced / 4, (spliced, reloaded)
 
 
 def _check_join_64(lib=None, shape=(2, 4, 16, 32)):
