@@ -48,18 +48,20 @@ def parse():
     return ap.parse_args()
 
 
-def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols, parents=0):
+def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols, parents=0, n_alias=0):
     """Minimum HBM bytes of one fill launch: the SoA snapshot columns the
     batch requests (free + used int64 per requested column, the two presence
     words, taint profile, label ids) once per launch, plus the leaf counters
     written for every eval whose phase 1 runs (one per distinct phase-1 input:
-    state + sliceState int32; stateWithLeader, sliceStateWithLeader,
-    leaderState for leader evals).  With the fused parent roll-up (`parents`
-    leaf parents of uniform power-of-two fan-out) each phase-1 eval also
-    writes the parents' state + sliceState and a 64-bit positive-children
-    mask (+ the three leader fields)."""
+    state int32, sliceState int32 unless the class is simple — `n_alias` of
+    them: its sliceState is its state, the row aliases it; stateWithLeader,
+    sliceStateWithLeader, leaderState for leader evals).  With the fused
+    parent roll-up (`parents` leaf parents of uniform power-of-two fan-out)
+    each phase-1 eval also writes the parents' state (+ sliceState) and a
+    64-bit positive-children mask (+ the three leader fields)."""
     snap = N * (16 * R_used + 8 + 4 + 4 * label_cols)
-    writes = N * (8 * n_fill + 12 * n_leader) + parents * (16 * n_fill + 12 * n_leader)
+    ss_rows = n_fill - n_alias
+    writes = N * (4 * n_fill + 4 * ss_rows + 12 * n_leader) + parents * (12 * n_fill + 4 * ss_rows + 12 * n_leader)
     return snap + writes
 
 
@@ -108,7 +110,7 @@ def roofline_of(snap, doc, wls, steps, stage_sum):
     R_used = st["staged_cols"] or len({r for w in wls for p in w for r in p["requests"]} | {"pods"})
     label_cols = 1 if any(p.get("nodeSelector") for w in wls for p in w) else 0
     fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(st["leader_evals"], st["fill_evals"]) / launches,
-                                        R_used, label_cols, fused_parents(doc))
+                                        R_used, label_cols, fused_parents(doc), st.get("alias_fills", 0) / launches)
     achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
     return st, fill_bytes, per_launch_fill_ms, achieved, R_used
 

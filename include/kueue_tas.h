@@ -218,6 +218,10 @@ typedef struct {
  * the device's entry tags (kueue_tas_snapshot_set_leaf_tags; test knob: both
  * must agree) */
 #define KUEUE_TAS_CFG_HOST_VALUES 64
+/* classify every leaf of fill_pair_kernel's single-run chunks per class (the
+ * round-4 path) instead of once per leaf category and wave (test knob: both
+ * paths must agree) */
+#define KUEUE_TAS_CFG_NO_CATEGORY_FILL 128
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

@@ -54,6 +54,9 @@ int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
  * leaf-level selection partials, [2] fill launches, [3] snapshot columns the
  * fill staged (0: generic kernel). */
 int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
+/* Fill rows of the last eval_batch whose sliceState field aliases their state
+ * (simple classes: the row's sliceState is neither stored nor read). */
+int64_t kueue_tas_last_alias_fills(kueue_tas_ctx* ctx);
 /* Phase-1 kernel variants the last kueue_tas_eval_batch ran (OR of the bits
  * below; tests pin that their inputs reach every variant). */
 #define KUEUE_TAS_PATH_STAGED 1u                /* fill_leaves_staged_kernel, taint rows in LDS */
@@ -72,6 +75,7 @@ int kueue_tas_last_stats(kueue_tas_ctx* ctx, int64_t* stats4);
 #define KUEUE_TAS_PATH_PAIR 8192u               /* fill_pair_kernel: two adjacent leaves per thread (kPairLP) */
 #define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
 #define KUEUE_TAS_PATH_RAGGED_PAIR 32768u       /* fill_pair_kernel on ragged leaf parents (128-leaf slots, segmented scans) */
+#define KUEUE_TAS_PATH_CATEGORY 65536u          /* fill_pair_kernel's single-run chunks classify leaf categories (CAT) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 /* Stage events: on (default), every stage of kueue_tas_last_stage_times is
  * timed; off, only the fill bracket is (the other events are pure
@@ -117,6 +121,9 @@ int kueue_tas_host_stage_accum(kueue_tas_host* h, float* ms, int n, int64_t* run
  * [2] leader evals, [3..6] kueue_tas_last_stats summed ([6]: max), [7] OR of
  * kueue_tas_last_fill_paths. */
 int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8);
+/* kueue_tas_host_last_stats followed by [8] the fill rows whose sliceState
+ * aliases state (kueue_tas_last_alias_fills summed); copies min(n, 9). */
+int kueue_tas_host_last_stats_ext(kueue_tas_host* h, int64_t* out, int32_t n);
 /* Host wall time of the last kueue_tas_host_admit (ms): [0] record
  * preparation, [1] kueue_tas_admit (uploads, admit_kernel, result copy),
  * [2] delta list. */

@@ -197,6 +197,7 @@ struct kueue_tas_ctx {
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
   bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
+  bool cat_fill = true;       // fill_pair_kernel's leaf categories (KUEUE_TAS_CFG_NO_CATEGORY_FILL clears it)
   bool labels16 = false;      // every staged label column's value ids < 2^16 (packed nodeSelector compare)
   int64_t n_loads = 0, n_splices = 0;  // kueue_tas_snapshot_load / _splice calls that succeeded (lifetime)
   bool stage_timing = true;   // record every stage event (else only the fill bracket; kueue_tas_set_stage_timing)
@@ -293,12 +294,14 @@ struct kueue_tas_ctx {
   double host_ms[8] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out, [6] of compile:
                            // validation pass, [7] of compile: records + hashes pass
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
+  int64_t last_alias_fills = 0;          // fill rows whose sliceState aliases state (FillEvalParams::ss_alias)
   uint32_t fill_paths = 0;               // KUEUE_TAS_PATH_* bits of the last kueue_tas_eval_batch
   // phase-1 counters of the last device chunk (kueue_tas_last_counters):
   // requests [chunk_base, chunk_base + chunk_rep.size()), their class counter rows
   size_t chunk_base = 0;
   std::vector<int32_t> chunk_rep;
   std::vector<uint8_t> chunk_leader;
+  std::vector<uint8_t> chunk_alias;  // the class row's sliceState aliases state (FillEvalParams::ss_alias)
   std::vector<const kueue_tas_eval_req*> req_ptrs;  // kueue_tas_eval_batch's requests as kueue_tas_eval_batch_ptrs takes them
   // eval_chunk's per-request host work (kept between batches)
   std::vector<int64_t> req_term_off;
@@ -342,6 +345,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->pair_fill = (cfg->flags & KUEUE_TAS_CFG_NO_PAIR_FILL) == 0;
     c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
     c->fused_top = (cfg->flags & KUEUE_TAS_CFG_FUSED_TOP) != 0;
+    c->cat_fill = (cfg->flags & KUEUE_TAS_CFG_NO_CATEGORY_FILL) == 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -1812,6 +1816,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   c->chunk_rep.assign(h_rep, h_rep + n);
   c->chunk_leader.resize(n);
   for (size_t i = 0; i < n; i++) c->chunk_leader[i] = (hev[i].flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
+  c->chunk_alias.assign(n, 0);  // filled with the fill records below
   // ---- device buffers ----
   const int64_t SD = s.SD;
   const int64_t ctr_stride = 5 * SD;
@@ -1928,6 +1933,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         }
         P.sx_begin = ev.sx_begin;
         P.sx_end = ev.sx_end;
+        {  // a simple class: sliceState == state at every level, its row's sliceState field aliases state
+          bool simple = (ev.flags & KUEUE_TAS_F_LEADER) == 0 && ev.slice_level == s.L - 1 && ev.slice_size == 1;
+          for (int l = 0; l < s.L && simple; l++) simple = ev.ssal[l] == 0 || ev.ssal[l] == 1;
+          P.ss_alias = simple ? 1 : 0;
+        }
         if (ev.sx_begin >= 0) P.sel_far = 1;
         {  // the packed nodeSelector compare (FillEvalParams::sel_fast)
           uint32_t m[2] = {0u, 0u}, w[2] = {0u, 0u};
@@ -1975,6 +1985,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         for (int j = 0; j < ev.nlead && j < nsw; j++) r.term[nsw + j] = hterms[ev.lead_begin + j];
       }
     }
+    for (size_t i = 0; i < n; i++) c->chunk_alias[i] = uint8_t(fp[c->chunk_rep[i]].p.ss_alias);
+    for (int k = 0; k < nfill; k++) c->last_alias_fills += fp[k].p.ss_alias;
   }
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, o_fpos + size_t(nfill) * sizeof(FillPos), hipMemcpyHostToDevice, c->stream));
@@ -2125,6 +2137,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       gl = (hev[i].flags & (KUEUE_TAS_F_AFFINITY | KUEUE_TAS_F_SELECTOR_EXT)) != 0;
       for (int k = 0; k < hev[i].nsel; k++) gl = gl || hev[i].sel_col[k] >= kStagedLabels;
     }
+    // leaf categories in the single-run pair fill: every filter on staged
+    // data (no affinity, no far selector column: !gl), taint rows and the
+    // ExclusionStats in LDS, label ids packed in 16 bits
+    const bool cat = c->cat_fill && pair && !gl && ts && b.nstat > 0 && c->labels16;
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
     auto staged = [&](auto ns, auto tsv, auto mr, int first, int count, hipStream_t st) {
       if (count <= 0) return;
@@ -2133,6 +2149,18 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       if (pair) {  // kPairLP leaves per thread
         c->fill_paths |= KUEUE_TAS_PATH_PAIR;
         const dim3 pg(pgx, unsigned(count));
+        if constexpr (TSv && !MRv) {  // single-run chunks: leaf categories
+          if (cat) {
+            c->fill_paths |= KUEUE_TAS_PATH_CATEGORY;
+            if (ragged_pair)
+              hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, -1, true>), pg, dim3(256), 0, st, s, b, umask, first);
+            else if (b.rack_fanout == 32)
+              hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 32, true>), pg, dim3(256), 0, st, s, b, umask, first);
+            else
+              hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 0, true>), pg, dim3(256), 0, st, s, b, umask, first);
+            return;
+          }
+        }
         if (ragged_pair && gl)
           hipLaunchKernelGGL((fill_pair_kernel<NSv, TSv, MRv, true, -1>), pg, dim3(256), 0, st, s, b, umask, first);
         else if (ragged_pair)
@@ -2403,6 +2431,7 @@ int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* c, const kueue_tas_eval_req* const*
   c->last_ticks.clear();
   c->last_prof.clear();
   for (auto& v : c->last_stats) v = 0;
+  c->last_alias_fills = 0;
   for (auto& v : c->host_ms) v = 0;
   c->fill_paths = 0;
   const size_t chunk = size_t(c->max_batch);
@@ -2467,7 +2496,8 @@ int kueue_tas_last_counters(kueue_tas_ctx* c, size_t i, int32_t* out, size_t cap
   for (int f = 0; f < 5; f++) {
     // phase 1 writes the leader fields only for leader requests; otherwise
     // they equal state / sliceState and leaderState is 0 (select's Wave::get)
-    const int src = leader ? f : (f == 2 ? 0 : f == 3 ? 1 : f);
+    int src = leader ? f : (f == 2 ? 0 : f == 3 ? 1 : f);
+    if (c->chunk_alias[k] && src == 1) src = 0;  // a simple class's sliceState row aliases state
     size_t pos = size_t(f) * total;
     for (int l = 0; l < s.L; l++) {
       const size_t nl = size_t(s.level_size[l]);
@@ -2559,6 +2589,8 @@ int kueue_tas_last_host_times(kueue_tas_ctx* c, double* ms, int n) {  // copies 
 }
 
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* c) { return c ? c->fill_paths : 0u; }
+
+int64_t kueue_tas_last_alias_fills(kueue_tas_ctx* c) { return c ? c->last_alias_fills : 0; }
 
 int kueue_tas_last_stats(kueue_tas_ctx* c, int64_t* stats4) {
   if (!c || !stats4) return KUEUE_TAS_EINVAL;

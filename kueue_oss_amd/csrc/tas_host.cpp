@@ -2549,7 +2549,8 @@ struct Evaluator {
   double host_ms[4] = {0, 0, 0, 0};  // prepare, eval call (incl. device), decode, total
   double detail_ms[4] = {0, 0, 0, 0};  // grouping + column check, request compile, build_pass, Values
   int64_t counts[3] = {0, 0, 0};
-  int64_t stats[5] = {0, 0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches, [4] fill paths
+  int64_t stats[6] = {0, 0, 0, 0, 0, 0};  // kueue_tas_last_stats summed over the run's batches, [4] fill paths,
+                                          // [5] alias fill rows
   std::vector<const kueue_tas_eval_req*> reqs;  // the batch's requests: the groups' own records, by address
   std::vector<int32_t> taint_table;
   std::vector<kueue_tas_assumed> assumed;
@@ -2921,7 +2922,7 @@ struct Evaluator {
     for (auto& v : stage_ms) v = 0;
     for (auto& v : dev_host_ms) v = 0;
     counts[0] = counts[1] = counts[2] = 0;
-    stats[0] = stats[1] = stats[2] = stats[3] = stats[4] = 0;
+    stats[0] = stats[1] = stats[2] = stats[3] = stats[4] = stats[5] = 0;
     host_ms[0] = host_ms[1] = host_ms[2] = host_ms[3] = 0;
     detail_ms[0] = detail_ms[1] = detail_ms[2] = detail_ms[3] = 0;
     const double t_start = now_ms();
@@ -3047,6 +3048,7 @@ struct Evaluator {
       for (int k = 0; k < 3; k++) stats[k] += st4[k];
       stats[3] = std::max(stats[3], st4[3]);
       stats[4] |= int64_t(kueue_tas_last_fill_paths(snap->ctx));
+      stats[5] += kueue_tas_last_alias_fills(snap->ctx);
       rc = balanced_pass(*rq, *tt, af, afv, *bt, &ent_view);  // after the diagnostics: it may run a batch
       if (rc) return rc;
       const double t_decode = now_ms();
@@ -3449,7 +3451,7 @@ struct kueue_tas_host {
   std::vector<std::vector<PodSetResult>> last;
   float ms[4] = {0, 0, 0, 0};
   int64_t counts[3] = {0, 0, 0};
-  int64_t stats[5] = {0, 0, 0, 0, 0};
+  int64_t stats[6] = {0, 0, 0, 0, 0, 0};
   uint64_t compiled_cols = 0;  // FlavorSnapshot::col_gen the compiled workloads were compiled against
   // this rank's shard of the compiled workloads (indices into `compiled`)
   // and its own compiled copies; empty: run_compiled evaluates them all
@@ -4612,6 +4614,15 @@ int kueue_tas_host_last_stats(kueue_tas_host* h, int64_t* stats8) {
   stats8[1] = h->counts[1];
   stats8[2] = h->counts[2];
   for (int k = 0; k < 5; k++) stats8[3 + k] = h->stats[k];
+  return 0;
+}
+
+int kueue_tas_host_last_stats_ext(kueue_tas_host* h, int64_t* out, int32_t n) {
+  if (!h || !out || n < 0) return KUEUE_TAS_EINVAL;
+  int64_t all[9];
+  kueue_tas_host_last_stats(h, all);
+  all[8] = h->stats[5];
+  for (int k = 0; k < n && k < 9; k++) out[k] = all[k];
   return 0;
 }
 

@@ -668,7 +668,12 @@ struct alignas(16) FillEvalParams {
   // on one column with different values, set a want bit outside the mask
   // (never equal: every leaf mismatches, as labels.SelectorFromSet does).
   uint32_t sel_mlo, sel_mhi, sel_wlo, sel_whi;
-  int32_t sel_fast, pad2[3];
+  int32_t sel_fast;
+  // 1: the class is simple (no leader, one-pod slices at the leaf level, no
+  // inner slice rounding), so its sliceState equals its state at every level
+  // and the class row's sliceState field is not stored: every reader takes
+  // the state field instead (ss_off)
+  int32_t ss_alias, pad2[2];
 };
 static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
 constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
@@ -687,6 +692,11 @@ struct alignas(16) FillPos {
   DevTerm term[kPosTerms];
 };
 static_assert(sizeof(FillPos) % 16 == 0, "FillPos is copied as int4");
+// Offset of the sliceState field in a class row (counters[row]): SD, or 0
+// for a simple class whose sliceState is its state (FillEvalParams::ss_alias).
+__device__ __forceinline__ int64_t ss_off(const DevBatch& b, int row, int64_t SD) {
+  return b.fill_pos[row].p.ss_alias ? 0 : SD;
+}
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
 // ExclusionStats of a fill block are counted in LDS and written as per-block
@@ -1185,6 +1195,7 @@ __global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(NS == 5 && !GL ? 5 
 // four the register footprint halves the waves per SIMD and the grid (128
 // tiles x classes / 8) leaves too few waves to hide the column loads.
 constexpr int kPairLP = 2;                     // leaves per thread (adjacent)
+constexpr int kCatSlots = 2 * 64;              // leaf-category table of a fill_pair_kernel block (CAT)
 constexpr int kPairTile = kPairLP * kFillThreads;  // leaves per block
 
 // Or-fold: the positive-children masks
@@ -1195,20 +1206,38 @@ struct OpOr {
 // MR: chunks of several signature runs (CountIn again at each run's first
 // position, the leaves' remaining capacity kept in registers), as the
 // staged kernel's MR.
-template <int NS, bool TS, bool MR, bool GL, int FC>  // FC: 32 compile-time fan-out, 0: b.rack_fanout (or none),
-                                                      // -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
+// CAT: leaf categories (below); single-run chunks only (!MR), every filter on
+// staged data (!GL), taint rows in LDS (TS), ExclusionStats in LDS.
+template <int NS, bool TS, bool MR, bool GL, int FC, bool CAT = false>  // FC: 32 compile-time fan-out, 0: b.rack_fanout
+                                                      // (or none), -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
 __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
+  static_assert(!CAT || (!MR && !GL && TS), "leaf categories: single-run chunks, staged filters, LDS taint rows");
   __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records
   __shared__ int32_t sh_stats[kEvalsPerBlock][kMaxFillStats];
   // multi-run chunks: each leaf's remaining capacity waits in LDS for the
   // next run's CountIn ([column][leaf of the lane][thread]), not in 4 * NS
   // VGPRs live across the whole class loop
   __shared__ int64_t sh_cap[MR ? NS * kPairLP * kFillThreads : 1];
+  // CAT: the block's leaf-category table (key | 1 << 63, 0: empty), leaf
+  // counts per category, the overflow flag, each class's pass mask
+  __shared__ unsigned long long sh_ckey[CAT ? kCatSlots : 1];
+  __shared__ int32_t sh_ccnt[CAT ? kCatSlots : 1];
+  __shared__ int32_t sh_cflag;
+  __shared__ uint64_t sh_pass[CAT ? 2 * kEvalsPerBlock : 1];
+  __shared__ uint64_t sh_passd[CAT ? kEvalsPerBlock : 1];  // over dense category ids (<= 64 categories)
+  __shared__ uint8_t sh_okb[CAT ? kFillThreads / kWave : 1][CAT ? kCatSlots : 1];  // a wave's verdicts by dense id
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   if (lds_stats)
     for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
+  if constexpr (CAT) {
+    for (int i = threadIdx.x; i < kCatSlots; i += kFillThreads) {
+      sh_ckey[i] = 0ull;
+      sh_ccnt[i] = 0;
+    }
+    if (threadIdx.x == 0) sh_cflag = 0;
+  }
   int tile = blockIdx.x, chunk = blockIdx.y;  // XCD-aware (tile, chunk) order as in the staged kernel
   if ((gridDim.x & 7u) == 0 && gridDim.y > 1) {
     const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1354,6 +1383,145 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     }
   };
   if constexpr (!MR) count_run(0);
+  // ---- CAT: leaf categories.  In a single-run chunk every filter of
+  // fillInCounts (:1578-1634) sees a leaf only through its category: out of
+  // the snapshot or not, taint profile, the label ids the chunk's
+  // nodeSelectors test, and the run's limiting column when CountIn gives 0
+  // (the resource exclusion).  The block's 512 leaves fall into few
+  // categories (C3: 3 profiles x 4 gpu-type ids x a few limiting columns),
+  // numbered by an LDS hash table (64-bit keys, compare-and-swap, linear
+  // probing) that also counts each category's leaves.  Every class then
+  // decides its verdict once per category (a lane per category, the classes
+  // spread over the block's waves) and adds its ExclusionStats as one LDS
+  // add per excluded category; the wave's pass mask goes to LDS.  In the
+  // class loop a leaf takes its category's bit: no per-leaf classification,
+  // no per-class stats ballots (the SALU / VALU issue that bounded the
+  // round-4 fill).  A block whose categories overflow the table, or one of
+  // whose classes filters on something else (a required domain, a selector
+  // outside the packed compare), keeps the per-leaf path.
+  int cslot[kPairLP], did[kPairLP];  // the leaves' table slots and dense category ids
+  int ncat = 0;
+  bool cat_ok = false;
+  if constexpr (CAT) {
+    // the chunk's selected label fields (16-bit fields of the packed key)
+    uint32_t kmlo = 0u, kmhi = 0u;
+    bool catable = lds_stats;  // (the host launches CAT with LDS stats only)
+    for (int e = 0; e < ne; e++) {
+      const FillEvalParams& P = sh_pos[e].p;
+      kmlo |= uint32_t(P.sel_mlo);
+      kmhi |= uint32_t(P.sel_mhi);
+      catable = catable && P.dom_begin < 0 && (P.nsel == 0 || P.sel_fast != 0 || !s.lowest_is_hostname);
+    }
+    int fld[3] = {0, 0, 0}, nf = 0;
+#pragma unroll
+    for (int f = 0; f < kStagedLabels; f++) {
+      const uint32_t m = ((f < 2 ? kmlo : kmhi) >> (16 * (f & 1))) & 0xffffu;
+      if (m) {
+        if (nf < 3) fld[nf] = f;
+        nf++;
+      }
+    }
+    cat_ok = catable && nf <= 3;  // block-uniform
+    if (cat_ok) {
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        cslot[j] = -1;
+        if (!valid[j]) continue;
+        const int zl = (live[j] && state0[j] == 0) ? lim0[j] : -1;
+        uint64_t key = (1ull << 63) | (uint64_t(uint32_t(!live[j]) | (uint32_t(prof[j]) << 1) | (uint32_t(zl + 1) << 6)) << 48);
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          if (q < nf) {
+            const int f = fld[q];
+            const uint32_t v = ((f < 2 ? pk_lo[j] : pk_hi[j]) >> (16 * (f & 1))) & 0xffffu;
+            key |= uint64_t(v) << (16 * q);
+          }
+        }
+        uint32_t h = uint32_t(key ^ (key >> 29) ^ (key >> 48)) * 0x9e3779b1u;
+        h >>= 25;  // 7 bits: kCatSlots
+        for (int probe = 0; probe < kCatSlots; probe++) {
+          const unsigned long long old = atomicCAS(&sh_ckey[h], 0ull, (unsigned long long)key);
+          if (old == 0ull || old == key) {
+            cslot[j] = int(h);
+            break;
+          }
+          h = (h + 1) & (kCatSlots - 1);
+        }
+        if (cslot[j] < 0) atomicOr(&sh_cflag, 1);
+        else atomicAdd(&sh_ccnt[cslot[j]], 1);
+      }
+      __syncthreads();
+      cat_ok = sh_cflag == 0;  // block-uniform
+    }
+    uint64_t U0 = 0, U1 = 0;  // the table's used slots: dense id = rank among them
+    if (cat_ok) {
+      U0 = ballot(sh_ckey[lane] != 0ull);
+      U1 = ballot(sh_ckey[kWave + lane] != 0ull);
+      ncat = __popcll(U0) + __popcll(U1);
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        const int sl = cslot[j];
+        did[j] = sl < 0 ? 0
+                 : sl < kWave ? __popcll(U0 & ((1ull << sl) - 1ull))
+                              : __popcll(U0) + __popcll(U1 & ((1ull << (sl - kWave)) - 1ull));
+      }
+    }
+    if (cat_ok) {
+      // the classes' verdicts per category: wave w takes classes w, w + 4, ...;
+      // a lane per table slot (two halves of 64)
+      const int wave = int(threadIdx.x >> 6);
+      const bool hn = s.lowest_is_hostname != 0;
+      for (int e = wave; e < ne; e += kFillThreads / kWave) {
+        const FillEvalParams& P = sh_pos[e].p;
+        const int nsel = P.nsel;
+        const uint32_t mlo = uint32_t(P.sel_mlo), mhi = uint32_t(P.sel_mhi), wlo = uint32_t(P.sel_wlo),
+                       whi = uint32_t(P.sel_whi);
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          const int slot = half * kWave + lane;
+          const uint64_t key = sh_ckey[slot];
+          const uint32_t small = uint32_t(key >> 48);
+          const bool used = (key >> 63) != 0;
+          const bool dead = (small & 1u) != 0;
+          const int pf = int((small >> 1) & 31u);
+          const int zl = int((small >> 6) & 63u) - 1;
+          uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            if (q < nf) {
+              const int f = fld[q];
+              const uint32_t v = uint32_t(key >> (16 * q)) & 0xffffu;
+              if (f < 2) lo |= v << (16 * (f & 1));
+              else hi |= v << (16 * (f & 1));
+            }
+          }
+          bool ok = used && !dead;
+          int x = -1;
+          if (hn && s.taint_profile) {
+            const int t = sh_pos[e].taint[pf];
+            x = (ok && t >= 0) ? kStatFixed + t : x;
+            ok = ok && t < 0;
+          }
+          if (hn && nsel > 0) {
+            const bool mis = ((lo & mlo) != wlo) | ((hi & mhi) != whi);
+            x = (ok && mis) ? 0 : x;
+            ok = ok && !mis;
+          }
+          x = (ok && zl >= 0) ? kStatFixed + b.num_taints + zl : x;
+          if (x >= 0) atomicAdd(&sh_stats[e][x], sh_ccnt[slot]);
+          const uint64_t pass = ballot(ok);
+          if (lane == 0) sh_pass[2 * e + half] = pass;
+          const uint64_t Uh = half ? U1 : U0;
+          if (used) sh_okb[wave][(half ? __popcll(U0) : 0) + __popcll(Uh & ((1ull << lane) - 1ull))] = ok ? 1 : 0;
+        }
+        wave_sync();
+        const uint64_t passd = ballot(lane < ncat && sh_okb[wave][lane] != 0);
+        if (lane == 0) sh_passd[e] = passd;
+        wave_sync();
+      }
+      __syncthreads();
+    }
+  }
   // ragged slots: the parents of the lane's two leaves, which of them start
   // (head) or end (tail) a parent, and the lane holding the start of its
   // second leaf's parent (the segmented scans' bound)
@@ -1386,7 +1554,53 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // stores below take a scalar branch, not a per-lane exec mask
   const bool full_tile = FC >= 0 && (tile + 1) * kPairTile <= N && (s.level_off[s.L - 1] & (kPairLP - 1)) == 0;
   const int64_t SD = s.SD;
-  for (int e = 0; e < ne; e++) {
+  // CAT, every class of the chunk simple (no leader, one-pod slices at the
+  // leaf level, no inner rounding: sliceState is state at the leaves and the
+  // parents) and uniform parents: the lean loop — per class a pass-mask
+  // lookup per leaf, the counter stores and the fused parents, nothing else
+  bool lean = false;
+  if constexpr (CAT && FC >= 0) {
+    lean = cat_ok && !leader && ncat <= kWave;
+    for (int e = 0; e < ne && lean; e++) lean = sh_pos[e].p.ss_alias != 0;  // simple (the host's mark)
+  }
+  if (lean) {
+    // per class: a leaf's state is state0 under its category's pass bit (a
+    // 0 / -1 mask); the leaf-pair store; the parent's state and positive-
+    // children mask from the same masks (pA / pB: the lane's leaves that have
+    // room, at their bits of the parent's mask); rows and parents by pointer
+    const int lsz = rack_f > 0 ? s.level_size[s.L - 2] : 0;
+    const int poff = rack_f > 0 ? s.level_off[s.L - 2] : 0;
+    const bool has_par = rack_f > 0 && valid[0] && parent < lsz && b.rack_pos != nullptr;
+    const uint64_t pA = (valid[0] && state0[0] > 0) ? 1ull << (kPairLP * gpos) : 0ull;
+    const uint64_t pB = (valid[1] && state0[1] > 0) ? 2ull << (kPairLP * gpos) : 0ull;
+    const int64_t cst = b.ctr_stride;
+    int32_t* rowp = b.counters + int64_t(e0) * cst;
+    uint64_t* rpp = b.rack_pos ? b.rack_pos + int64_t(e0) * lsz + parent : nullptr;
+    for (int e = 0; e < ne; e++, rowp += cst, rpp += lsz) {
+      const uint64_t pm = sh_passd[e];
+      const int32_t m0 = int32_t(uint32_t(pm >> did[0]) << 31) >> 31;
+      const int32_t m1 = int32_t(uint32_t(pm >> did[1]) << 31) >> 31;
+      const int32_t st0 = state0[0] & m0, st1 = state0[1] & m1;
+      // (the sliceState row is not stored: FillEvalParams::ss_alias)
+      if (full_tile) {
+        *reinterpret_cast<int2*>(rowp + gleaf0) = make_int2(st0, st1);
+      } else {
+        if (valid[0]) rowp[gleaf0] = st0;
+        if (valid[1]) rowp[gleaf0 + 1] = st1;
+      }
+      if (rack_f > 0) {  // fused fillInCountsHelper (:1658-1719) of the leaves' parents
+        const int32_t cap2 = group_reduce(w_add(st0, st1), half, OpWAdd());
+        const uint64_t bits = (uint64_t(int64_t(m0)) & pA) | (uint64_t(int64_t(m1)) & pB);
+        uint64_t posm = uint32_t(group_reduce(int32_t(uint32_t(bits)), half, OpOr()));
+        if (rack_f > 32) posm |= uint64_t(uint32_t(group_reduce(int32_t(uint32_t(bits >> 32)), half, OpOr()))) << 32;
+        if (gpos == 0 && has_par) {
+          *rpp = posm;
+          rowp[poff + parent] = cap2;
+        }
+      }
+    }
+  }
+  for (int e = 0; e < ne && !lean; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
     const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
     if constexpr (MR) {
@@ -1424,6 +1638,19 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       sel_wlo = uint32_t(uni(m.z));
       sel_whi = uint32_t(uni(m.w));
     }
+    // CAT: the class's pass mask over the block's categories (the verdicts
+    // and the ExclusionStats were settled before the loop)
+    const bool cat_cls = CAT && cat_ok;  // block-uniform
+    if (cat_cls) {
+      const uint64_t p0 = sh_pass[2 * e], p1 = sh_pass[2 * e + 1];
+#pragma unroll
+      for (int j = 0; j < kPairLP; j++) {
+        const uint64_t w = cslot[j] >= kWave ? p1 : p0;
+        okm[j] = cslot[j] >= 0 && ((w >> (cslot[j] & 63)) & 1ull);
+        state[j] = okm[j] ? state0[j] : 0;
+      }
+    }
+    if (!cat_cls) {
 #pragma unroll
     for (int j = 0; j < kPairLP; j++) {
       const int leaf = leaf0 + j;
@@ -1491,6 +1718,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       kind[j] = rx ? EX_RESOURCE : k;
       id[j] = rx ? lim0[j] : idv;
     }
+    }  // !cat_cls
     // a simple class (no leader, one-pod slices at the leaf level, no inner
     // slice rounding — every class of C3): sliceState is state and no
     // leader field exists, one wave-uniform branch instead of one per field
@@ -1526,8 +1754,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
           if (valid[j]) base[off + gleaf0 + j] = v[j];
       }
     };
+    // a simple class's sliceState is its state: the host marks it (ss_alias)
+    // and every reader takes the state row
+    const bool alias = uni(sh_pos[e].p.ss_alias) != 0;
     storev(0, state);
-    storev(SD, ss);
+    if (!alias) storev(SD, ss);
     if (leader) {
       storev(2 * SD, swl);
       storev(3 * SD, sswl);
@@ -1556,7 +1787,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + parent] = posm;
         const int g = s.level_off[s.L - 2] + parent;
         base[g] = cap2;
-        base[SD + g] = cap2;
+        if (!alias) base[SD + g] = cap2;
       }
     } else if (rack_f > 0) {
       const int32_t inner = p_inner;
@@ -1663,6 +1894,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // the slot (kMaxFillStats == 64 slots, one per lane) and added to LDS
     // with one conflict-free ds_add per lane: no per-kind sections, no
     // single-lane atomics (exec-mask bookkeeping on the scalar unit)
+    if (cat_cls) continue;  // counted per category above
     if (lds_stats) {
       static_assert(kMaxFillStats == kWave, "one stats slot per lane");
       int sl[kPairLP];
@@ -1936,6 +2168,7 @@ __device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& 
   const int ce = s.child_off[s.child_base[level] + p + 1];
   int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
   const int64_t SD = s.SD;
+  const int64_t SSO = ss_off(b, row, SD);
   const int coff = s.level_off[cl];
   int32_t cap = 0, slc = 0, minD = 0x7fffffff, minSD = 0x7fffffff, lead = 0;
   bool has = false;
@@ -1948,7 +2181,7 @@ __device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& 
     for (int u = 0; u < kRU; u++) {
       const int g = coff + min(c0 + u, ce - 1);
       vs[u] = base[g];
-      vss[u] = base[SD + g];
+      vss[u] = base[SSO + g];
       vsw[u] = vs[u];
       vsswl[u] = vss[u];
       vls[u] = 0;
@@ -1988,7 +2221,7 @@ __device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& 
   }
   const int g = s.level_off[level] + p;
   base[g] = state;
-  base[SD + g] = slc;
+  if (SSO) base[SD + g] = slc;
   if (leaderReq) {
     base[2 * SD + g] = swl;
     base[3 * SD + g] = sswl;
@@ -2018,6 +2251,7 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
   const bool hasInner = inner != 0;
   int32_t* base = b.counters + int64_t(blockIdx.y) * b.ctr_stride;  // the class's row: its fill position
   const int64_t SD = s.SD;
+  const int64_t SSO = ss_off(b, int(blockIdx.y), SD);
   const int coff = s.level_off[cl];
   const int lane = lane_id();
   const int p0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kParentsPerWave;
@@ -2031,7 +2265,7 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
     for (int c = cb + lane; c < ce; c += kWave) {
       const int g = coff + c;
       int32_t cs = base[g];
-      int32_t css = base[SD + g];
+      int32_t css = base[SSO + g];
       int32_t csw = cs, csswl = css, cls = 0;
       if (leaderReq) {
         csw = base[2 * SD + g];
@@ -2070,7 +2304,7 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
       }
       const int g = s.level_off[level] + p;
       base[g] = state;
-      base[SD + g] = slc;
+      if (SSO) base[SD + g] = slc;
       if (leaderReq) {
         base[2 * SD + g] = swl;
         base[3 * SD + g] = sswl;
@@ -2092,7 +2326,7 @@ __global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
   const int row = blockIdx.x;  // the class's fill position
   const int l = blockIdx.y;
   const int D = s.level_size[l];
-  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(row) * b.ctr_stride + s.SD + s.level_off[l]);
+  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(row) * b.ctr_stride + ss_off(b, row, s.SD) + s.level_off[l]);
   const int nq = (D + 3) / 4;
   int32_t m = INT32_MIN;
   constexpr int U = 8;
@@ -2132,8 +2366,8 @@ __device__ __forceinline__ int32_t load_l2_i32(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <bool L2>
-__device__ __forceinline__ void rollup_parent_wave(const DevSnap& s, int32_t* base, const DevEval& ev, bool leaderReq,
-                                                   int level, int p, int32_t* cmax) {
+__device__ __forceinline__ void rollup_parent_wave(const DevSnap& s, int32_t* base, int64_t SSO, const DevEval& ev,
+                                                   bool leaderReq, int level, int p, int32_t* cmax) {
   const int cl = level + 1;
   const int32_t inner = ev.ssal[cl];
   const bool hasInner = inner != 0;
@@ -2148,7 +2382,7 @@ __device__ __forceinline__ void rollup_parent_wave(const DevSnap& s, int32_t* ba
   for (int c = cb + lane; c < ce; c += kWave) {
     const int g = coff + c;
     int32_t cs = ld(g);
-    const int32_t css = ld(SD + g);
+    const int32_t css = ld(SSO + g);
     int32_t csw = cs, csswl = css, cls = 0;
     if (leaderReq) {
       csw = ld(2 * SD + g);
@@ -2190,7 +2424,7 @@ __device__ __forceinline__ void rollup_parent_wave(const DevSnap& s, int32_t* ba
     }
     const int g = s.level_off[level] + p;
     base[g] = state;
-    base[SD + g] = slc;
+    if (SSO) base[SD + g] = slc;
     if (leaderReq) {
       base[2 * SD + g] = swl;
       base[3 * SD + g] = sswl;
@@ -2207,12 +2441,13 @@ __global__ __launch_bounds__(256) void rollup_top_kernel(DevSnap s, DevBatch b, 
   const DevEval& ev = b.evals[eid];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int64_t SSO = ss_off(b, row, s.SD);
   const int wv = threadIdx.x >> 6;
   int32_t cmax = INT32_MIN;
   const int p0 = (blockIdx.x * 4 + wv) * kParentsPerWave;
   for (int j = 0; j < kParentsPerWave; j++) {
     const int p = p0 + j;
-    if (p < s.level_size[level]) rollup_parent_wave<false>(s, base, ev, leaderReq, level, p, &cmax);
+    if (p < s.level_size[level]) rollup_parent_wave<false>(s, base, SSO, ev, leaderReq, level, p, &cmax);
   }
   if (lane_id() == 0) red[wv] = cmax;
   __syncthreads();
@@ -2229,9 +2464,9 @@ __global__ __launch_bounds__(256) void rollup_top_kernel(DevSnap s, DevBatch b, 
     // l >= 0: roll level l up from level l + 1; the maximum of level l + 1 comes with the reads
     int32_t lm = INT32_MIN;
     if (l >= 0) {
-      for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, ev, leaderReq, l, p, &lm);
+      for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, SSO, ev, leaderReq, l, p, &lm);
     } else {  // level 0's own maximum
-      const int32_t* ss = base + s.SD + s.level_off[0];
+      const int32_t* ss = base + SSO + s.level_off[0];
       for (int i = threadIdx.x; i < s.level_size[0]; i += 256) lm = max(lm, load_l2_i32(ss + i));
       lm = group_reduce(lm, 64, OpMax());
     }
@@ -2257,16 +2492,17 @@ __global__ __launch_bounds__(256) void rollup_tail_kernel(DevSnap s, DevBatch b,
   const DevEval& ev = b.evals[b.fill_ids[row]];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
   int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int64_t SSO = ss_off(b, row, s.SD);
   const int wv = threadIdx.x >> 6;
   for (int l = top; l >= 0; l--) {
     int32_t unused = INT32_MIN;
-    for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, ev, leaderReq, l, p, &unused);
+    for (int p = wv; p < s.level_size[l]; p += 4) rollup_parent_wave<true>(s, base, SSO, ev, leaderReq, l, p, &unused);
     __threadfence_block();
     __syncthreads();
   }
   if (!b.level_max) return;
   for (int l = 0; l + 1 < s.L; l++) {
-    const int32_t* ss = base + s.SD + s.level_off[l];
+    const int32_t* ss = base + SSO + s.level_off[l];
     int32_t m = INT32_MIN;
     for (int i = threadIdx.x; i < s.level_size[l]; i += 256) m = max(m, l <= top ? load_l2_i32(ss + i) : ss[i]);
     m = group_reduce(m, 64, OpMax());
@@ -2298,10 +2534,11 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
     const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
     const int32_t sliceCount = go_div32(uni(ev.count), uni(ev.slice_size));
     const int32_t* base = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
+    const int64_t SSO = ss_off(b, b.rep_of[eid], SD);
     int32_t state = 0, ss = 0, swl = 0, sswl = 0, ls = 0;
     if (valid) {
       state = base[gleaf];
-      ss = base[SD + gleaf];
+      ss = base[SSO + gleaf];
       swl = state;
       sswl = ss;
       if (leader) {
@@ -2372,7 +2609,8 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
   for (int i = threadIdx.x; i < kLfcBins; i += blockDim.x) h[i] = 0;
   if (threadIdx.x == 0) ovs = 0;
   __syncthreads();
-  const int32_t* v = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
+  const int32_t* v = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + ss_off(b, b.lfc_rep[slot], s.SD) +
+                     s.level_off[s.L - 1];
   const int lo = chunk * kLfcChunk, hi = min(s.N, lo + kLfcChunk);
   uint64_t mysum = 0;
   const int lane = lane_id();
@@ -2483,6 +2721,7 @@ struct Wave {
   int32_t my_tag;
   bool dirty;
   int64_t SD;
+  int64_t ssoff;  // the sliceState field's offset in ctr: SD, or 0 for a simple class (ss_off)
   Key* lds;        // per-wave LDS buffer (list_cap keys; lds_bytes in all)
   int cap;
   int lds_bytes;
@@ -2513,15 +2752,16 @@ struct Wave {
       if (f == F_SSWL) f = F_SLICE;
     }
     const int64_t o = int64_t(f) * SD + g;
-    if (!dirty) return ctr[o];
-    const int32_t shared = ctr[o], own = ov[o];
+    const int64_t co = (f == F_SLICE ? ssoff : int64_t(f) * SD) + g;
+    if (!dirty) return ctr[co];
+    const int32_t shared = ctr[co], own = ov[o];
     return tag[g] == my_tag ? own : shared;
   }
   // first write of a domain: copy its counters into the overlay
   __device__ void own(int g) {
     if (tag[g] != my_tag) {
       const int nf = leader ? 5 : 2;
-      for (int f = 0; f < nf; f++) ov[int64_t(f) * SD + g] = ctr[int64_t(f) * SD + g];
+      for (int f = 0; f < nf; f++) ov[int64_t(f) * SD + g] = ctr[(f == F_SLICE ? ssoff : int64_t(f) * SD) + g];
       tag[g] = my_tag;
     }
   }
@@ -2556,7 +2796,7 @@ struct Wave {
       if (f == F_SWL) f = F_STATE;
       if (f == F_SSWL) f = F_SLICE;
     }
-    return ctr[int64_t(f) * SD + g];
+    return ctr[(f == F_SLICE ? ssoff : int64_t(f) * SD) + g];
   }
   __device__ Key kplain_clean(int g) const {
     int idx = g - g_select_snap.level_off[level_of(g)];
@@ -4059,7 +4299,7 @@ __device__ int lfc_leaf_greedy(Wave& w, int32_t sliceCount, kueue_tas_eval_out& 
   const int loff = s.level_off[s.L - 1];
   const int32_t ss = w.ev->slice_size;
   const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
-  const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
+  const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.ssoff + loff);
   const int nq = (D + 3) / 4;
   constexpr int kBins = 256;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w.lds);  // 1 KiB <= list_cap * 16 B (host: list_cap >= 64)
@@ -4329,7 +4569,7 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
   const DevSnap& s = g_select_snap;
   const int L1 = s.L - 1;
   const int lane = lane_id();
-  const int32_t* V = w.ctr + w.SD + s.level_off[L1];
+  const int32_t* V = w.ctr + w.ssoff + s.level_off[L1];
   const int32_t need = w.ev->count;  // sliceCount = count / 1 (host: count >= 0)
   const uint32_t* tot = b.lfc_tot + int64_t(slot) * kLfcBins;
   LfcJob job{0, 0, 0, 0};
@@ -4521,7 +4761,7 @@ __device__ int find_level(Wave& w, int32_t* results, int* nres, int* fitLevel, k
       // candidate (:1216-1231: min sliceState >= sliceCount, ties by key) in
       // the same pass; LFC evals the first fit, the last key and the minimum.
       const int4* S4 = reinterpret_cast<const int4*>(w.ctr + loff);
-      const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.SD + loff);
+      const int4* SS4 = reinterpret_cast<const int4*>(w.ctr + w.ssoff + loff);
       const int nq = (D + 3) / 4;
       const bool lfc = w.lfc, bf = w.bf;
       uint64_t tv = ~0ull, fv = ~0ull, lv = 0, bv = ~0ull;
@@ -4867,6 +5107,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.my_tag = b.tag_epoch;
   w.dirty = false;
   w.SD = s.SD;
+  w.ssoff = ss_off(b, b.rep_of[eid], s.SD);
   w.lds = lds_all + int64_t(wave) * (b.wave_lds / int(sizeof(Key)));
   w.cap = b.list_cap;
   w.lds_bytes = b.wave_lds;
@@ -5050,7 +5291,8 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
     const int slot = b.lfc_slot[eid];
     const int t = job.t;
     const int64_t mt = job.m;
-    const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + s.SD + s.level_off[s.L - 1];
+    const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + ss_off(b, b.lfc_rep[slot], s.SD) +
+                       s.level_off[s.L - 1];
     const int lo = item.chunk * kLfcChunk + int(threadIdx.x) * 8;
     int32_t x[8];
 #pragma unroll

@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
     "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
+    "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -154,6 +155,9 @@ def _bind(lib):
     lib.kueue_tas_host_find_workload.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_find_workload.restype = c.c_int
     lib.kueue_tas_host_last_stats.argtypes = [c.c_void_p, c.POINTER(c.c_int64)]
+    lib.kueue_tas_host_last_stats_ext.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.c_int32]
+    lib.kueue_tas_last_alias_fills.argtypes = [c.c_void_p]
+    lib.kueue_tas_last_alias_fills.restype = c.c_int64
     lib.kueue_tas_host_update_usage.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
     lib.kueue_tas_host_update_usage.restype = c.c_int
     lib.kueue_tas_host_fits.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
@@ -231,11 +235,12 @@ class TASFlavorSnapshot:
     def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
                  packed_entries: bool = False, inline_stats: bool = False,
                  pair_fill: bool = True, serial_admit: bool = False, split_stats: bool = False,
-                 fused_top: bool = False, host_values: bool = False):
+                 fused_top: bool = False, host_values: bool = False, category_fill: bool = True):
         self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0)
                               | (0 if pair_fill else 4) | (8 if serial_admit else 0) | (16 if split_stats else 0)
-                              | (32 if fused_top else 0) | (64 if host_values else 0))
+                              | (32 if fused_top else 0) | (64 if host_values else 0)
+                              | (0 if category_fill else 128))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:
@@ -370,11 +375,12 @@ class TASFlavorSnapshot:
     def last_stats(self):
         """Work counters of the last run: dict(batches, evals, leader_evals,
         fill_evals, leaf_partial_evals, fill_launches, staged_cols, fill_paths:
-        OR of the KUEUE_TAS_PATH_* bits of include/kueue_tas_debug.h)."""
-        st = (ctypes.c_int64 * 8)()
-        self._lib.kueue_tas_host_last_stats(self._h, st)
+        OR of the KUEUE_TAS_PATH_* bits of include/kueue_tas_debug.h,
+        alias_fills: fill rows whose sliceState aliases state)."""
+        st = (ctypes.c_int64 * 9)()
+        self._lib.kueue_tas_host_last_stats_ext(self._h, st, 9)
         keys = ("batches", "evals", "leader_evals", "fill_evals", "leaf_partial_evals", "fill_launches", "staged_cols",
-                "fill_paths")
+                "fill_paths", "alias_fills")
         return dict(zip(keys, list(st)))
 
     STAGES = ("fill", "rollup", "replicate", "lfc_branch", "select", "join_wait", "device_total")

@@ -184,6 +184,11 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
   *p = o + v;
   return o;
 }
+inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cmp, unsigned long long v) {
+  unsigned long long o = *p;
+  if (o == cmp) *p = v;
+  return o;
+}
 inline unsigned atomicOr(unsigned* p, unsigned v) { unsigned o = *p; *p = o | v; return o; }
 inline int atomicOr(int* p, int v) { int o = *p; *p = o | v; return o; }
 inline int atomicMax(int* p, int v) { int o = *p; if (v > o) *p = v; return o; }

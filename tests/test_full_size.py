@@ -5,17 +5,26 @@ multi-rank path with two ranks on the one GPU of the box.
   one of the 1,024 workloads of the bench step (the same flags: compile +
   evaluation + TopologyAssignment values, ``RUN_COMPILE | RUN_VALUES``)
   against a 16-thread oracle run.
-* C5 (1,048,576 nodes): two ranks, each evaluating its cost-balanced shard of
-  a 2,048-workload batch (1,024 per rank, ``max_batch=1024``) through
-  ``shard_ids`` + ``run_compiled`` + ``gather_assignments`` + ``admit_round``
-  (gloo collectives over host tensors: RCCL needs one GPU per rank), then a
-  second batch on the updated replicas.  Checked against (a) one unsharded
-  replica on the same GPU running the same sequence (every assignment, every
-  admission decision, every delta, the whole second batch), (b) the oracle:
-  a stratified sample of both batches, and every admission decision replayed
-  as Fits + AddUsage in workload order on the oracle snapshot
-  (scheduler.go:371-435, tas_flavor_snapshot.go:401-415, :257-293).
+* C2 (16,384 nodes, 1,000 workloads) and C4 (65,536 nodes, 256 JobSet-like
+  workloads): the whole batch of the config against the 16-thread oracle.
+* C5 at its stated size (1,048,576 nodes, 100,000 pending workloads): two
+  ranks on the one GPU (gloo collectives over host tensors: RCCL needs one
+  GPU per rank), each walking its cost-balanced shard (``shard_ids``) in
+  1,024-workload device batches; per round every rank evaluates its next
+  batch (``set_shard`` + ``run_compiled``), then ``admit_round``: all-gather
+  of the assignments, rank 0 admits in workload order, delta broadcast, the
+  other replica applies.  Checked against (a) one unsharded replica on the
+  same GPU running the same rounds (every gathered assignment, every
+  admission decision, every delta of every round), (b) the oracle: every
+  admission decision of every round replayed as Fits + AddUsage in workload
+  order on the oracle snapshot, and a stratified BestFit / LFC sample of
+  three rounds evaluated at that point of the sequence (scheduler.go:371-435,
+  :583-619, tas_flavor_snapshot.go:401-415, :257-293).  The test also times
+  one 8,192-candidate admission round on a fresh replica (the rank-0 load of
+  an 8-GPU node: 8 x 1,024 evaluations gathered) and writes it to
+  ``gpurun_out/c5_admit8192.json``.
 """
+import json
 import os
 import socket
 import sys
@@ -57,9 +66,24 @@ def test_c3j_whole_batch_on_gpu():
     assert sum(1 for r in got if all(not p["reason"] for p in r)) > 500
 
 
-# ---- C5 sharded over two ranks on one GPU ----
-C5_PER_RANK = 1024
+@pytest.mark.timeout(600)
+def test_c2_whole_batch_on_gpu():
+    got = _whole_batch(synth.config_c2, n=1000)
+    assert sum(1 for r in got if all(not p["reason"] for p in r)) > 500
+
+
+@pytest.mark.timeout(600)
+def test_c4_whole_batch_on_gpu():
+    got = _whole_batch(synth.config_c4, n=256)
+    assert sum(1 for r in got if all(not p["reason"] for p in r)) > 100
+
+
+# ---- C5 at its stated size: 100,000 workloads sharded over two ranks on one GPU ----
+C5_WORKLOADS = 100_000
+C5_BATCH = 1024  # device batch per rank per round
 WORLD = 2
+SAMPLE_ROUNDS = 3  # rounds whose BestFit / LFC sample the oracle evaluates
+ADMIT_CANDIDATES = 8 * C5_BATCH  # rank 0's admission round at 8 GPUs
 
 
 _CAPFD = None  # the running test's capfd: progress goes to the terminal past pytest's capture
@@ -90,15 +114,36 @@ def _free_port():
     return p
 
 
-def _sample_ids(wls, ids, k=8):
-    """k BestFit (required / preferred) and k unconstrained workloads of a shard."""
+def _c5():
+    return synth.config_c5(n_workloads=C5_WORKLOADS)
+
+
+def _rounds(wls):
+    """[[rank 0's batch, rank 1's batch] per round]: every rank walks its shard
+    in C5_BATCH slices, round k evaluating slice k of every shard."""
+    shards = [sharding.shard_ids(wls, WORLD, r) for r in range(WORLD)]
+    n = max((len(s) + C5_BATCH - 1) // C5_BATCH for s in shards)
+    return [[s[k * C5_BATCH:(k + 1) * C5_BATCH] for s in shards] for k in range(n)]
+
+
+def _sample_rounds(n_rounds):
+    return sorted({0, n_rounds // 2, n_rounds - 1})[:SAMPLE_ROUNDS]
+
+
+def _sample_ids(wls, ids, k=2):
+    """k BestFit (required / preferred) and k unconstrained workloads of a batch."""
     bf = [i for i in ids if wls[i][0]["topologyRequest"] and not wls[i][0]["topologyRequest"].get("unconstrained")]
     lfc = [i for i in ids if i not in set(bf)]
     return bf[:k] + lfc[:k]
 
 
-def _c5():
-    return synth.config_c5(n_workloads=C5_PER_RANK * WORLD)
+def _digest(*arrays):
+    import hashlib
+
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
 
 
 def _rank_worker(rank, world, port, q):
@@ -109,25 +154,29 @@ def _rank_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         doc, wls = _c5()
-        ids = sharding.shard_ids(wls, world, rank)
-        snap = TASFlavorSnapshot(doc, device=0, max_batch=C5_PER_RANK)
+        rounds = _rounds(wls)
+        samples = set(_sample_rounds(len(rounds)))
+        snap = TASFlavorSnapshot(doc, device=0, max_batch=C5_BATCH)
         del doc
         snap.compile(wls)
-        snap.set_shard(ids)
-        out = {"ids": ids}
-        snap.run_compiled(flags=FULL)
-        res = snap.last_results()
-        pos = {g: k for k, g in enumerate(ids)}
-        out["sample1"] = {i: res[pos[i]] for i in _sample_ids(wls, ids, 4)}
-        out["gathered1"] = sharding.gather_assignments(snap.last_assignments(), world, dist)
-        quads, admitted, deltas = sharding.admit_round(snap, world, rank, dist)
-        out["admit_quads"] = quads
-        out["admitted"] = admitted
-        out["deltas"] = deltas
-        snap.run_compiled(flags=FULL)
-        res = snap.last_results()
-        out["sample2"] = {i: res[pos[i]] for i in _sample_ids(wls, ids, 4)}
-        out["gathered2"] = sharding.gather_assignments(snap.last_assignments(), world, dist)
+        out = {"rounds": [], "samples": {}}
+        t0 = time.time()
+        for k, batches in enumerate(rounds):
+            mine = batches[rank]
+            snap.set_shard(mine)
+            snap.run_compiled(flags=FULL)
+            if k in samples:
+                res = snap.last_results()
+                pos = {g: j for j, g in enumerate(mine)}
+                out["samples"].update({i: res[pos[i]] for i in _sample_ids(wls, mine)})
+            quads, admitted, deltas = sharding.admit_round(snap, world, rank, dist)
+            if rank == 0:
+                out["rounds"].append((quads, admitted, deltas))
+            else:
+                out["rounds"].append(_digest(quads, deltas))
+            if rank == 0 and k % 10 == 0:
+                _progress(f"round {k}/{len(rounds)} {time.time() - t0:.1f}s")
+        out["seconds"] = time.time() - t0
         snap.close()
         q.put((rank, out))
     except Exception as e:  # noqa: BLE001 - reported to the parent
@@ -149,8 +198,46 @@ def _by_workload(quads):
     return {g: (f, sorted(r)) for g, (f, r) in out.items()}
 
 
-@pytest.mark.timeout(1200)
-def test_c5_sharded_two_ranks_on_one_gpu(capfd):
+def _negated(deltas):
+    neg = deltas.copy()
+    neg["delta"] = -neg["delta"]
+    return neg
+
+
+def _admit_8192(snap):
+    """One rank-0 admission round of ADMIT_CANDIDATES gathered candidates (the
+    8-GPU load: 8 x 1,024 evaluations) on a fresh replica, timed three times;
+    each repetition's deltas are negated afterwards (the snapshot returns to
+    its state).  Returns the timing record."""
+    ids = list(range(ADMIT_CANDIDATES))
+    snap.set_shard(ids)
+    snap.run_compiled(flags=FULL)
+    quads = snap.last_assignments()
+    times, parts, first = [], [], None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        admitted, deltas = snap.admit(quads)
+        times.append((time.perf_counter() - t0) * 1e3)
+        parts.append(snap.last_admit_times())
+        stats = snap.last_admit_stats()
+        snap.apply_deltas(_negated(deltas))
+        if first is None:
+            first = (admitted.tolist(), _digest(np.sort(deltas, order=["leaf", "col"])))
+        assert (admitted.tolist(), _digest(np.sort(deltas, order=["leaf", "col"]))) == first
+    rec = {"candidates": len(ids), "nodes": 1 << 20, "quads": int(quads.size // 4),
+           "admitted": int(np.asarray(first[0])[:, 1].sum()),
+           "round_ms": [round(t, 3) for t in times], "round_ms_min": round(min(times), 3),
+           "parts_ms_last": dict(zip(["admit_host_prep", "admit_device", "admit_delta_list"],
+                                     [round(x, 3) for x in parts[-1]])),
+           "device_pass": dict(zip(["window_rounds", "in_order_candidates", "candidates"], [int(x) for x in stats]))}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "c5_admit8192.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    return rec
+
+
+@pytest.mark.timeout(1100)
+def test_c5_sharded_100k_two_ranks_on_one_gpu(capfd):
     global _CAPFD
     _CAPFD = capfd
     stop = threading.Event()
@@ -171,62 +258,74 @@ def _c5_sharded():
     procs = [ctx.Process(target=_rank_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=900) for _ in range(WORLD))
-    for p in procs:
-        p.join(timeout=120)
+    try:
+        # meanwhile: one unsharded replica on the same GPU, the same rounds
+        doc, wls = _c5()
+        n = len(wls)
+        rounds = _rounds(wls)
+        assert sorted(i for b in rounds for r in b for i in r) == list(range(n))
+        snap = TASFlavorSnapshot(doc, max_batch=C5_BATCH)
+        snap.compile(wls)
+        adm8 = _admit_8192(snap)
+        _progress(f"8,192-candidate admission round: {adm8['round_ms']} ms")
+        replica = []
+        t0 = time.time()
+        for k, batches in enumerate(rounds):
+            snap.set_shard(sorted(i for b in batches for i in b))
+            snap.run_compiled(flags=FULL)
+            u = _by_workload(snap.last_assignments())
+            admitted, deltas = snap.admit(snap.last_assignments())
+            replica.append((u, admitted, deltas))
+        _progress(f"unsharded replica: {len(rounds)} rounds in {time.time() - t0:.1f}s")
+        leaf_names = snap.leaf_ids()
+        snap.close()
+        outs = dict(q.get(timeout=900) for _ in range(WORLD))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
     for r in range(WORLD):
         assert "error" not in outs[r], outs[r].get("error")
         assert procs[r].exitcode == 0
-    _progress("ranks done")
-    doc, wls = _c5()
-    n = len(wls)
-    assert sorted(i for r in range(WORLD) for i in outs[r]["ids"]) == list(range(n))
-    assert all(len(outs[r]["ids"]) <= C5_PER_RANK + 64 for r in range(WORLD))
-    for key in ("gathered1", "gathered2", "admit_quads"):
-        assert np.array_equal(outs[0][key], outs[1][key]), key
-    assert outs[0]["deltas"].tolist() == outs[1]["deltas"].tolist()
-    g1, g2 = _by_workload(outs[0]["gathered1"]), _by_workload(outs[0]["gathered2"])
-    assert sorted(g1) == list(range(n)) and sorted(g2) == list(range(n))
-
-    # (a) one unsharded replica on the same GPU, same sequence
-    snap = TASFlavorSnapshot(doc, max_batch=C5_PER_RANK)
-    snap.compile(wls)
-    snap.run_compiled(flags=FULL)
-    u1 = _by_workload(snap.last_assignments())
-    admitted, deltas = snap.admit(snap.last_assignments())
-    snap.run_compiled(flags=FULL)
-    u2 = _by_workload(snap.last_assignments())
-    leaf_names = snap.leaf_ids()
-    snap.close()
-    assert [w for w in range(n) if g1[w] != u1[w]] == []
-    assert outs[0]["admitted"].tolist() == admitted.tolist()
-    assert np.array_equal(np.sort(outs[0]["deltas"], order=["leaf", "col"]), np.sort(deltas, order=["leaf", "col"]))
-    assert [w for w in range(n) if g2[w] != u2[w]] == []
-    n_adm = int(admitted[:, 1].sum())
+    _progress(f"ranks done in {outs[0]['seconds']:.1f}s; comparing")
+    # (a) every round: both ranks saw the same exchange, and it equals the replica's round
+    assert len(outs[0]["rounds"]) == len(outs[1]["rounds"]) == len(rounds)
+    cand_rounds = []
+    n_adm = 0
+    for k, ((quads, admitted, deltas), dig1, (u, r_adm, r_del)) in enumerate(
+            zip(outs[0]["rounds"], outs[1]["rounds"], replica)):
+        assert _digest(quads, deltas) == dig1, k
+        g = _by_workload(quads)
+        ids = sorted(i for b in rounds[k] for i in b)
+        assert sorted(g) == ids and sorted(u) == ids, k
+        assert [w for w in ids if g[w] != u[w]] == [], k
+        assert admitted.tolist() == r_adm.tolist(), k
+        assert np.array_equal(np.sort(deltas, order=["leaf", "col"]), np.sort(r_del, order=["leaf", "col"])), k
+        got_adm = dict(admitted.tolist())
+        assert all(not got_adm[w] for w in ids if g[w][0]), k
+        cand_rounds.append([(w, g[w][1], bool(got_adm[w])) for w in ids if not g[w][0]])
+        n_adm += int(admitted[:, 1].sum())
     assert 0 < n_adm < n
+    _progress(f"unsharded replica agrees on every round ({n_adm} of {n} admitted)")
 
-    _progress("unsharded replica agrees")
-    # (b) the oracle: batch-1 sample, every admission decision, batch-2 sample
-    s1 = {i: r for o in outs.values() for i, r in o["sample1"].items()}
-    ids1 = sorted(s1)
-    want1, _ = oracle_lib.eval_workloads(doc, [wls[i] for i in ids1], threads=16)
-    assert [i for k, i in enumerate(ids1) if s1[i] != want1[k]] == []
+    # (b) the oracle: every admission decision of every round in order, and the
+    # sample rounds' BestFit / LFC workloads evaluated where the rounds put them
+    def usage(w, recs):  # ComputeTASNetUsage records (lowest level: hostname)
+        return [{"values": [leaf_names[leaf]], "singlePodRequests": dict(wls[w][p].get("requests", {})), "count": c}
+                for p, leaf, c in recs]
 
-    def usage(w):  # ComputeTASNetUsage records from the gathered quads (lowest level: hostname)
-        recs = []
-        for p, leaf, c in g1[w][1]:
-            req = wls[w][p].get("requests", {})
-            recs.append({"values": [leaf_names[leaf]], "singlePodRequests": dict(req), "count": c})
-        return recs
-
-    _progress("oracle batch-1 sample agrees")
-    cand = [w for w in range(n) if not g1[w][0]]
-    s2 = {i: r for o in outs.values() for i, r in o["sample2"].items()}
-    ids2 = sorted(s2)
-    ops = [{"op": "admit", "usage": usage(w)} for w in cand]
-    ops += [{"op": "find", "podSets": wls[i]} for i in ids2]
+    samples = outs[0]["samples"]
+    samples.update(outs[1]["samples"])
+    round_of = {i: k for k, b in enumerate(rounds) for r in b for i in r}
+    ops, expect = [], []
+    for k, cands in enumerate(cand_rounds):
+        for i in sorted(i for i in samples if round_of[i] == k):  # evaluated before round k's admissions
+            ops.append({"op": "find", "podSets": wls[i]})
+            expect.append(("find", i, samples[i]))
+        for w, recs, ok in cands:
+            ops.append({"op": "admit", "usage": usage(w, recs)})
+            expect.append(("admit", w, ok))
+    assert sum(1 for e in expect if e[0] == "find") == 4 * WORLD * len(_sample_rounds(len(rounds)))
     res = oracle_lib.session(doc, ops)
-    got_adm = dict(admitted.tolist())
-    assert {w: bool(got_adm[w]) for w in cand} == dict(zip(cand, res[:len(cand)]))
-    assert all(not got_adm[w] for w in range(n) if g1[w][0])
-    assert [i for k, i in enumerate(ids2) if s2[i] != res[len(cand) + k]] == []
+    bad = [(kind, w) for (kind, w, want), got in zip(expect, res) if got != want]
+    assert bad == [], bad[:8]
+    _progress(f"oracle agrees: {len(cand_rounds)} rounds of admissions, {len(samples)} sampled evaluations")
