@@ -248,6 +248,7 @@ struct kueue_tas_ctx {
   FlatMap cls_head, sig_head;
   DevBuf<int32_t> d_overlay, d_tags;
   DevBuf<int2> d_wave_tab2;     // 128-leaf slots of whole ragged parents (fill_pair_kernel, FC = -1)
+  DevBuf<int32_t> d_wide;       // leaf parents wider than a slot (DevSnap::wide_parents)
   DevBuf<uint64_t> d_rack_pos;  // positive-child masks of the leaves' parents (fused fill)  // select's copy-on-write counters and ownership tags
   int32_t tag_epoch = 0;
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
@@ -700,32 +701,50 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   s.wave_tab2 = nullptr;
   s.n_wave_slots2 = 0;
   s.ragged_max_fan = 0;
+  s.wide_parents = nullptr;
+  s.n_wide = 0;
   // and the same packing into 128-leaf slots for fill_pair_kernel's two
-  // leaves per lane (parents of at most 128 leaves)
+  // leaves per lane (parents of at most 128 leaves; a wider parent takes
+  // slots of its own, one per 128-leaf piece, flagged wide)
   if (c->rack_fanout == 0 && s.L >= 2 && d->level_sizes[s.L - 2] > 0 && d->child_offsets && s.N > 0) {
     const int P = d->level_sizes[s.L - 2];
     const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
     bool ok = co[0] == 0 && co[P] == s.N;
     std::vector<int2> tab;
-    std::vector<int32_t> lp(N, 0);
+    std::vector<int32_t> lp(N, 0), wide;
     int cb = 0, cn = 0, fmax = 0;
     for (int p = 0; p < P && ok; p++) {
       const int f = co[p + 1] - co[p];
-      if (f < 1 || f > 2 * kWave) {
+      if (f < 1) {
         ok = false;
         break;
       }
       fmax = std::max(fmax, f);
+      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
+      if (f > 2 * kWave) {  // pieces of their own
+        if (cn) tab.push_back(make_int2(cb, cn));
+        for (int k = co[p]; k < co[p + 1]; k += 2 * kWave)
+          tab.push_back(make_int2(k, std::min(2 * kWave, co[p + 1] - k) | (1 << 16)));
+        wide.push_back(p);
+        cb = co[p + 1];
+        cn = 0;
+        continue;
+      }
       if (cn + f > 2 * kWave) {
         tab.push_back(make_int2(cb, cn));
         cb = co[p];
         cn = 0;
       }
       cn += f;
-      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
     }
     if (ok) {
-      tab.push_back(make_int2(cb, cn));
+      if (cn) tab.push_back(make_int2(cb, cn));
+      if (!wide.empty()) {
+        HIPCHK(c, c->d_wide.reserve(wide.size()));
+        HIPCHK(c, stage(c->d_wide.p, wide.data(), wide.size() * 4));
+        s.wide_parents = c->d_wide.p;
+        s.n_wide = int32_t(wide.size());
+      }
       HIPCHK(c, c->d_wave_tab2.reserve(tab.size()));
       HIPCHK(c, stage(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2)));
       HIPCHK(c, c->d_leaf_parent.reserve(N));
@@ -2137,6 +2156,15 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       gl = (hev[i].flags & (KUEUE_TAS_F_AFFINITY | KUEUE_TAS_F_SELECTOR_EXT)) != 0;
       for (int k = 0; k < hev[i].nsel; k++) gl = gl || hev[i].sel_col[k] >= kStagedLabels;
     }
+    // leaf parents wider than a slot: zeroed before the ragged pair fill adds
+    // its pieces' sums (the fill bracket and stream2's chunks start after it)
+    const bool wide = ragged_pair && s.n_wide > 0;
+    if (wide) {
+      hipLaunchKernelGGL(wide_parents_zero_kernel, dim3(unsigned((s.n_wide + 255) / 256), unsigned(nfill)), dim3(256), 0,
+                         c->stream, s, b);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    }
     // leaf categories in the single-run pair fill: every filter on staged
     // data (no affinity, no far selector column: !gl), taint rows and the
     // ExclusionStats in LDS, label ids packed in 16 bits
@@ -2222,6 +2250,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     else hipLaunchKernelGGL(fill_leaves_kernel<32>, grid, dim3(256), 0, c->stream, s, b);
     if (src) return src;
     HIPCHK(c, hipGetLastError());
+    if (wide) {
+      hipLaunchKernelGGL(wide_parents_finish_kernel, dim3(unsigned((s.n_wide + 255) / 256), unsigned(nfill)), dim3(256),
+                         0, c->stream, s, b);
+      HIPCHK(c, hipGetLastError());
+    }
   }
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   // ExclusionStats on stream3 beside the roll-up / select, joined before the

@@ -82,12 +82,17 @@ struct DevSnap {
   const int2* wave_tab;                // [n_wave_slots]
   int32_t n_wave_slots;
   const int32_t* leaf_parent;          // [N] parent index in level L-2 (with wave_tab or wave_tab2)
-  // Ragged leaf parents of <= 128 leaves for fill_pair_kernel (two leaves per
-  // lane): slot w covers leaves [x, x + y) of wave_tab2[w], whole parents only
-  // (null: some parent is wider).  ragged_max_fan: the widest leaf parent.
+  // Ragged leaf parents for fill_pair_kernel (two leaves per lane): slot w
+  // covers leaves [x, x + (y & 0xffff)) of wave_tab2[w] — whole parents of at
+  // most 128 leaves, or (y >> 16 == 1) one 128-leaf piece of a wider parent,
+  // whose parent sums the slots add atomically (wide_parents: those parents'
+  // indices in level L-2, zeroed before the fill).  ragged_max_fan: the
+  // widest leaf parent.
   const int2* wave_tab2;
   int32_t n_wave_slots2;
   int32_t ragged_max_fan;
+  const int32_t* wide_parents;         // [n_wide]
+  int32_t n_wide;
   // Entry tags (kueue_tas_snapshot_set_leaf_tags): every emitted entry pair k
   // of the entries region starting at ent_base also stores leaf_tag[leaf] at
   // tag_out[k] (null leaf_tag: off).  Set per batch before the descriptor upload.

@@ -1251,11 +1251,13 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   const int N = s.N;
   int leaf0 = tile * kPairTile + kPairLP * int(threadIdx.x);
   int slot_len = N - tile * kPairTile;  // leaves of this lane's window from the window's first
+  bool wide_slot = false;               // FC < 0: the slot is a 128-leaf piece of a wider parent
   if constexpr (FC < 0) {  // this wave's 128-leaf slot of whole parents
     const int slot = tile * 4 + int(threadIdx.x >> 6);
     const int2 wt = slot < s.n_wave_slots2 ? s.wave_tab2[slot] : make_int2(0, 0);
     leaf0 = wt.x + kPairLP * lane;
-    slot_len = wt.y;
+    slot_len = wt.y & 0xffff;
+    wide_slot = (wt.y >> 16) != 0;
   }
   const int gleaf0 = s.level_off[s.L - 1] + leaf0;
   bool valid[kPairLP];
@@ -1878,11 +1880,18 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         pm1 = (uint64_t(uint32_t(hi1)) << 32) | uint32_t(lo1);
       }
       auto put_parent = [&](int par, int32_t cp, int32_t sl, uint64_t pm) {
+        const int g = s.level_off[s.L - 2] + par;
+        if (wide_slot) {  // (wave-uniform) one piece of a wider parent: the pieces' sums add up
+          // (int32 wrap: in any order) into the zeroed parent; a sliceState at
+          // the slice level is the whole sum's quotient (wide_parents_finish_kernel)
+          atomicAdd(&base[g], cp);
+          if (!alias && s.L - 2 != slice_level) atomicAdd(&base[SD + g], sl);
+          return;
+        }
         if (masks) b.rack_pos[int64_t(e0 + e) * s.level_size[s.L - 2] + par] = pm;
         if (s.L - 2 == slice_level) sl = go_div32(cp, slice_size);
-        const int g = s.level_off[s.L - 2] + par;
         base[g] = cp;
-        base[SD + g] = sl;
+        if (!alias) base[SD + g] = sl;
       };
       if (tail0) put_parent(rp[0], cap0, slc0, pm0);
       if (tail1) put_parent(rp[1], cap1, slc1, pm1);
@@ -1991,6 +2000,28 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         b.fill_stats[(int64_t(e0 + e) * nb + t) * b.nstat + k] = 0;
     }
   }
+}
+
+// Leaf parents wider than a fill slot (DevSnap::wide_parents): zeroed in every
+// class row before fill_pair_kernel's ragged mode adds its pieces' sums, and
+// afterwards, for classes whose slice level is the parents' level, their
+// sliceState = state / sliceSize (fillInCountsHelper :1712-1716).
+__global__ __launch_bounds__(256) void wide_parents_zero_kernel(DevSnap s, DevBatch b) {
+  const int row = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= b.nfill || i >= s.n_wide) return;
+  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int g = s.level_off[s.L - 2] + s.wide_parents[i];
+  base[g] = 0;
+  if (!b.fill_pos[row].p.ss_alias) base[s.SD + g] = 0;
+}
+__global__ __launch_bounds__(256) void wide_parents_finish_kernel(DevSnap s, DevBatch b) {
+  const int row = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= b.nfill || i >= s.n_wide) return;
+  const FillEvalParams& P = b.fill_pos[row].p;
+  if (P.slice_level != s.L - 2 || P.ss_alias) return;
+  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  const int g = s.level_off[s.L - 2] + s.wide_parents[i];
+  base[s.SD + g] = go_div32(base[g], P.slice_size);
 }
 
 // ExclusionStats of the staged fill's classes (fillInCounts :1578-1634:

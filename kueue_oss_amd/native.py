@@ -495,12 +495,19 @@ class TASFlavorSnapshot:
         replica; returns (admitted (id, 0/1) pairs [n, 2], deltas numpy DELTA_DTYPE)."""
         import numpy as np
         q = np.ascontiguousarray(quads, dtype=np.int32)
-        heads = int(np.unique(q[0::4]).size) if q.size else 0
+        # one header quad (id, -1, failed, n) per workload: the admitted
+        # capacity without a sort (np.unique cost ~0.5 ms per 20k quads)
+        heads = int(np.count_nonzero(q[1::4] < 0)) if q.size else 0
         adm = np.zeros((heads, 2), dtype=np.int32)
         nw = ctypes.c_size_t()
         nd = ctypes.c_size_t()
-        if self._lib.kueue_tas_host_admit(self._h, q.ctypes.data, q.size, adm.ctypes.data, adm.size,
-                                          ctypes.byref(nw), ctypes.byref(nd)):
+        rc = self._lib.kueue_tas_host_admit(self._h, q.ctypes.data, q.size, adm.ctypes.data, adm.size,
+                                            ctypes.byref(nw), ctypes.byref(nd))
+        if rc == -5 and nw.value > heads:  # workloads without a header quad: size by the library's count
+            adm = np.zeros((nw.value, 2), dtype=np.int32)
+            rc = self._lib.kueue_tas_host_admit(self._h, q.ctypes.data, q.size, adm.ctypes.data, adm.size,
+                                                ctypes.byref(nw), ctypes.byref(nd))
+        if rc:
             raise RuntimeError(self._err())
         deltas = np.zeros(nd.value, dtype=DELTA_DTYPE)
         if self._lib.kueue_tas_host_last_deltas(self._h, deltas.ctypes.data, deltas.size):
