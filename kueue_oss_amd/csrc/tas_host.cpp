@@ -650,8 +650,17 @@ class FlavorSnapshot {
   std::vector<kueue_tas_delta> mirrorPending;
   void defer_mirror(const kueue_tas_delta* d, size_t n) {
     mirrorPending.insert(mirrorPending.end(), d, d + n);
-    if (mirrorPending.size() > (size_t(1) << 22)) flush_mirror();
+    // a bounded backlog: whoever reads the mirror next (a node join, an
+    // upload) folds at most this many records (~1 ms with the entry cache)
+    if (mirrorPending.size() > (size_t(1) << 18)) flush_mirror();
   }
+  // The two map entries a (column, leaf) delta updates — tasUsage[leaf][res]
+  // and usageByDomain[leaf id][res] — cached by key after their first fold:
+  // std::map nodes never move and keys are never erased here, so a fold is
+  // two pointer adds per key instead of two string-keyed map walks.  Cleared
+  // when leaves are renumbered (flush_joins) or the columns change (recolumn).
+  std::vector<std::pair<int64_t*, int64_t*>> mirrorPtr;  // [R][N]
+  void clear_mirror_cache() { mirrorPtr.clear(); }
   // a long backlog (rounds of admissions since the mirror was last read) is
   // folded per (column, leaf) first, so each distinct key costs its two map
   // updates once (a key whose deltas cancel still gets its entry: a present
@@ -660,14 +669,26 @@ class FlavorSnapshot {
   std::vector<uint32_t> mirrorKeys;
   std::vector<uint8_t> mirrorSeen;
   void flush_mirror() {
-    auto apply = [&](int32_t leaf, int32_t col, int64_t delta) {
-      const std::string& res = cols[size_t(col)];
-      int64_t& v = tasUsage[size_t(leaf)][res];
-      v = add64(v, delta);
-      int64_t& u = usageByDomain[leafId[size_t(leaf)]][res];
-      u = add64(u, delta);
-    };
+    if (mirrorPending.empty()) return;
     const size_t N = size_t(this->N()), R = cols.size();
+    const bool cached = N * R < (size_t(1) << 28);
+    if (cached && mirrorPtr.size() != N * R) mirrorPtr.assign(N * R, {nullptr, nullptr});
+    auto apply = [&](int32_t leaf, int32_t col, int64_t delta) {
+      std::pair<int64_t*, int64_t*>* e = cached ? &mirrorPtr[size_t(col) * N + size_t(leaf)] : nullptr;
+      if (!e || !e->first) {
+        const std::string& res = cols[size_t(col)];
+        int64_t* v = &tasUsage[size_t(leaf)][res];
+        int64_t* u = &usageByDomain[leafId[size_t(leaf)]][res];
+        if (!e) {
+          *v = add64(*v, delta);
+          *u = add64(*u, delta);
+          return;
+        }
+        *e = {v, u};
+      }
+      *e->first = add64(*e->first, delta);
+      *e->second = add64(*e->second, delta);
+    };
     if (mirrorPending.size() < 4096 || N * R >= (size_t(1) << 32)) {
       for (auto& d : mirrorPending) apply(d.leaf, d.col, d.delta);
     } else {
@@ -1239,6 +1260,7 @@ class FlavorSnapshot {
       tf = t;
     };
     flush_mirror();  // tasUsage rows move
+    clear_mirror_cache();
     lap(0);
     const int L = this->L();
     std::sort(joins.begin(), joins.end(), [](const Join& a, const Join& b) { return a.lv < b.lv; });
@@ -1674,6 +1696,8 @@ class FlavorSnapshot {
   // Re-derives the column set; returns true when it changed (compiled
   // requests are stale, the next upload() reloads).
   bool recolumn() {
+    flush_mirror();
+    clear_mirror_cache();
     const std::set<std::string> want = wanted_columns();
     if (want.size() == cols.size() && std::equal(want.begin(), want.end(), cols.begin())) return false;
     set_columns(want);
