@@ -1165,7 +1165,7 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const bool lds_bits = nwords * 4 <= 64 * 1024;
   // the windowed kernel's round bitmap beside the touched one: admission chains within a window
   const bool lds_chain = c->admit_window && 2 * nwords * 4 <= 64 * 1024;
-  const size_t o_recs = o_out + al((n_wl + 2) * 4);  // + two diagnostics words (admit_window_kernel)
+  const size_t o_recs = o_out + al((n_wl + 3) * 4);  // + three diagnostics words (admit_window_kernel)
   const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
   const size_t o_todo = o_dep + al(n_wl * 4);
   const size_t o_todor = o_todo + al((n_wl + 1) * 4);
@@ -1232,8 +1232,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
                        reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
-                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<const int32_t*>(d + o_todo),
-                       reinterpret_cast<const int64_t*>(d + o_todor));
+                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo),
+                       reinterpret_cast<int64_t*>(d + o_todor));
   } else {  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
@@ -1846,7 +1846,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   // overlay, tags and scratch lists per BestFit-side select slot (fast-LFC
   // evals never mutate or walk lists): sized by nbf, not n
   const size_t nph2 = size_t(std::max(nbf, 1));
-  HIPCHK(c, c->d_overlay.ensure(nph2 * size_t(ctr_stride)));
+  bool batch_leader = false;
+  for (size_t i = 0; i < n && !batch_leader; i++) batch_leader = (hev[i].flags & KUEUE_TAS_F_LEADER) != 0;
+  const int64_t ov_stride = batch_leader ? ctr_stride : 2 * SD;  // leaderless overlays hold two fields
+  HIPCHK(c, c->d_overlay.ensure(nph2 * size_t(ov_stride)));
   if (c->d_tags.n < nph2 * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
     HIPCHK(c, c->d_tags.ensure(nph2 * size_t(SD)));
     HIPCHK(c, hipMemsetAsync(c->d_tags.p, 0, c->d_tags.n * 4, c->stream));
@@ -2049,6 +2052,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.rack_fanout = 0;
   b.rack_pos = nullptr;
   b.ctr_stride = ctr_stride;
+  b.ov_stride = ov_stride;
   b.counters = c->d_counters.p;
   b.overlay = c->d_overlay.p;
   b.tags = c->d_tags.p;

@@ -5133,7 +5133,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.rack_pos = (b.rack_fanout && b.rack_pos) ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
   // per-launch-slot phase-2 buffers: the BestFit-side launch numbers its
   // evals 0..nbf-1; fast-LFC evals (the other launch) never touch them
-  w.ov = b.overlay + int64_t(slot) * b.ctr_stride;
+  w.ov = b.overlay + int64_t(slot) * b.ov_stride;
   w.tag = b.tags + int64_t(slot) * s.SD;
   w.my_tag = b.tag_epoch;
   w.dirty = false;
@@ -5986,10 +5986,11 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
     const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
     const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
-    int32_t* admitted, const int32_t* todo, const int64_t* todo_r) {
+    int32_t* admitted, int32_t* todo, int64_t* todo_r) {
   extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
   __shared__ int32_t sh_fit[kAdmitWindow];
   __shared__ int32_t sh_conf[2];  // per admission attempt, alternating (one barrier per attempt)
+  __shared__ int32_t sh_scan[64 * kAdmitWindow];  // the sweep's compaction (a count per thread)
   const int lane = lane_id(), wave = int(threadIdx.x) >> 6;
   const int nwords = (s.N + 31) / 32;
   const bool in_lds = touched_in_lds != 0;
@@ -5999,10 +6000,10 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     for (int k = threadIdx.x; k < (chain ? 2 : 1) * nwords; k += blockDim.x)
       touched_lds[k] = k < nwords ? touched_global[k] : 0u;
   const bool exact = *exact_flag != 0;
-  const int ntodo = todo[0];
+  int ntodo = todo[0];
   __syncthreads();
   int w0 = 0;  // position in the todo list
-  int rounds = 0;
+  int rounds = 0, sweeps = 0, nrej_since = 0;
   int pf_pos = -1, pf_w = n_wl;  // the next window's candidate, fetched during this round
   int64_t pf_r0 = 0, pf_r1 = 0;
   while (w0 < ntodo) {  // block-uniform
@@ -6147,10 +6148,98 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
       for (int q = threadIdx.x; q < nwords; q += blockDim.x) round_lds[q] = 0;
     __syncthreads();
     w0 += k;
+    // Rejection sweep: usage only grows during the pass (AddUsage), so a
+    // candidate that does not fit the current usage cannot fit at its turn
+    // (scheduler.go:426-435 runs Fits on usage that includes every earlier
+    // admission): after a round that rejected several candidates, every
+    // remaining candidate is checked against the current usage in parallel
+    // (a wave per candidate), the failures rejected at once, and the todo
+    // list compacted in place — nominated workloads that all target the same
+    // best-fit domains (an idle, uniform cluster) leave the pass in a few
+    // sweeps instead of a window round per 16 of them.
+    for (int q = 0; q < k; q++) nrej_since += sh_fit[q] ? 0 : 1;
+    if (nrej_since >= kAdmitWindow / 4 && ntodo - w0 > 2 * kAdmitWindow && !exact) {  // block-uniform
+      nrej_since = 0;
+      sweeps++;
+      for (int pos = w0 + wave; pos < ntodo; pos += kAdmitWindow) {
+        const int w = todo[1 + pos];
+        const int64_t r0 = todo_r[2 * pos], r1 = todo_r[2 * pos + 1];
+        bool fit = wl_fit0[w] != 0;
+        for (int64_t base = r0; base < r1 && fit; base += kWave) {
+          const int64_t i = base + lane;
+          bool ok = true;
+          if (i < r1) {
+            const AdmitRec a = recs[i];
+            if (a.status == kAdmitWide) {
+              ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+            } else if (a.status == kAdmitNever) {
+              ok = false;
+            } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
+              int64_t us[kAdmitTerms];
+#pragma unroll
+              for (int u = 0; u < kAdmitTerms; u++)
+                us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
+#pragma unroll
+              for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
+            }
+          }
+          fit = ballot(!ok) == 0;
+        }
+        if (!fit && lane == 0) {
+          admitted[w] = 0;
+          todo[1 + pos] = -1;  // rejected: dropped by the compaction
+        }
+      }
+      __syncthreads();
+      // in-place stable compaction of todo[w0 .. ntodo): every thread reads its
+      // contiguous share into registers, a block scan of the kept counts, then
+      // the writes (to lower or equal positions, after every read)
+      constexpr int kPer = 16;  // positions per thread per pass (1,024 threads: 16,384 a pass)
+      int out_base = w0;
+      for (int seg = w0; seg < ntodo; seg += kPer * int(blockDim.x)) {
+        const int p0 = seg + int(threadIdx.x) * kPer;
+        int ww[kPer];
+        int64_t rr0[kPer], rr1[kPer];
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+          const int p = p0 + u;
+          ww[u] = p < ntodo ? todo[1 + p] : -1;
+          rr0[u] = ww[u] >= 0 ? todo_r[2 * p] : 0;
+          rr1[u] = ww[u] >= 0 ? todo_r[2 * p + 1] : 0;
+          cnt += ww[u] >= 0 ? 1 : 0;
+        }
+        sh_scan[threadIdx.x] = cnt;
+        __syncthreads();
+        for (int off = 1; off < int(blockDim.x); off <<= 1) {  // Hillis-Steele inclusive scan
+          const int v = threadIdx.x >= unsigned(off) ? sh_scan[threadIdx.x - off] : 0;
+          __syncthreads();
+          sh_scan[threadIdx.x] += v;
+          __syncthreads();
+        }
+        int o = out_base + sh_scan[threadIdx.x] - cnt;
+        const int seg_total = sh_scan[blockDim.x - 1];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+          if (ww[u] >= 0) {
+            todo[1 + o] = ww[u];
+            todo_r[2 * o] = rr0[u];
+            todo_r[2 * o + 1] = rr1[u];
+            o++;
+          }
+        out_base += seg_total;
+        __threadfence_block();
+        __syncthreads();
+      }
+      ntodo = out_base;
+      pf_pos = -1;  // the prefetched candidate's position moved
+    }
   }
-  if (threadIdx.x == 0) {  // diagnostics after the verdicts: rounds, candidates in the in-order pass
+  if (threadIdx.x == 0) {  // diagnostics after the verdicts: rounds, candidates in the in-order pass, sweeps
     admitted[n_wl] = rounds;
-    admitted[n_wl + 1] = ntodo;
+    admitted[n_wl + 1] = todo[0];
+    admitted[n_wl + 2] = sweeps;
   }
 }
 

@@ -259,26 +259,13 @@ def _c5_sharded():
     for p in procs:
         p.start()
     try:
-        # meanwhile: one unsharded replica on the same GPU, the same rounds
+        # meanwhile the same workloads here (host only: the replica below
+        # starts when the ranks have freed their device memory — three
+        # 1M-node contexts with 1,024-eval phase-2 buffers exceed one GPU)
         doc, wls = _c5()
         n = len(wls)
         rounds = _rounds(wls)
         assert sorted(i for b in rounds for r in b for i in r) == list(range(n))
-        snap = TASFlavorSnapshot(doc, max_batch=C5_BATCH)
-        snap.compile(wls)
-        adm8 = _admit_8192(snap)
-        _progress(f"8,192-candidate admission round: {adm8['round_ms']} ms")
-        replica = []
-        t0 = time.time()
-        for k, batches in enumerate(rounds):
-            snap.set_shard(sorted(i for b in batches for i in b))
-            snap.run_compiled(flags=FULL)
-            u = _by_workload(snap.last_assignments())
-            admitted, deltas = snap.admit(snap.last_assignments())
-            replica.append((u, admitted, deltas))
-        _progress(f"unsharded replica: {len(rounds)} rounds in {time.time() - t0:.1f}s")
-        leaf_names = snap.leaf_ids()
-        snap.close()
         outs = dict(q.get(timeout=900) for _ in range(WORLD))
     finally:
         for p in procs:
@@ -286,7 +273,23 @@ def _c5_sharded():
     for r in range(WORLD):
         assert "error" not in outs[r], outs[r].get("error")
         assert procs[r].exitcode == 0
-    _progress(f"ranks done in {outs[0]['seconds']:.1f}s; comparing")
+    _progress(f"ranks done in {outs[0]['seconds']:.1f}s")
+    # one unsharded replica on the same GPU, the same rounds
+    snap = TASFlavorSnapshot(doc, max_batch=C5_BATCH)
+    snap.compile(wls)
+    adm8 = _admit_8192(snap)
+    _progress(f"8,192-candidate admission round: {adm8['round_ms']} ms")
+    replica = []
+    t0 = time.time()
+    for k, batches in enumerate(rounds):
+        snap.set_shard(sorted(i for b in batches for i in b))
+        snap.run_compiled(flags=FULL)
+        u = _by_workload(snap.last_assignments())
+        admitted, deltas = snap.admit(snap.last_assignments())
+        replica.append((u, admitted, deltas))
+    _progress(f"unsharded replica: {len(rounds)} rounds in {time.time() - t0:.1f}s; comparing")
+    leaf_names = snap.leaf_ids()
+    snap.close()
     # (a) every round: both ranks saw the same exchange, and it equals the replica's round
     assert len(outs[0]["rounds"]) == len(outs[1]["rounds"]) == len(rounds)
     cand_rounds = []
