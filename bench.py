@@ -335,6 +335,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_extras:
         extras = widened_rows(a, snap, snap_doc, mine, synth)
         extras["c3j"] = c3j_variant(a, synth, TASFlavorSnapshot, FULL)
+        if a.config == "C3":
+            extras["admission_8192"] = admission_8192(snap, synth, FULL)
 
     stages = {k + "_ms": round(v / a.steps, 3) for k, v in stage_sum.items()}
     host = dict(zip(("staging_ms", "eval_calls_ms", "decode_ms", "total_ms"), (round(x / a.steps, 3) for x in host_sum)))
@@ -515,6 +517,36 @@ def widened_rows(a, snap, snap_doc, mine, synth):
             "v1beta2_encode_ms_per_batch": round(enc_ms, 3),
             "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
             "usage_update_ms_per_call": round(upd_ms, 3)}
+
+
+def admission_8192(snap, synth, flags, n=8 * 1024, reps=4):
+    """Rank 0's admission round at 8 GPUs (8 x 1,024 gathered candidates) on
+    this snapshot: the C3 generator's first n workloads evaluated in device
+    batches of 1,024, then Fits + AddUsage in workload order (kueue_tas_host_admit),
+    each repetition's deltas negated afterwards.  Run last: it recompiles the
+    snapshot's workload set."""
+    import numpy as np
+
+    _, wls = synth.config_c3(n_workloads=n)
+    snap.compile(wls)
+    snap.set_shard(list(range(n)))
+    snap.run_compiled(flags=flags)
+    quads = snap.last_assignments()
+    times, parts = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        admitted, deltas = snap.admit(quads)
+        times.append((time.perf_counter() - t0) * 1e3)
+        parts.append(snap.last_admit_times())
+        stats = snap.last_admit_stats()
+        neg = deltas.copy()
+        neg["delta"] = -neg["delta"]
+        snap.apply_deltas(neg)
+    return {"candidates": n, "round_ms_median": round(float(np.median(times)), 3),
+            "parts_ms_median": dict(zip(["admit_host_prep", "admit_device", "admit_delta_list"],
+                                        [round(float(np.median([p[k] for p in parts])), 3) for k in range(3)])),
+            "admitted": int(admitted[:, 1].sum()), "deltas": int(len(deltas)),
+            "device_pass": dict(zip(["window_rounds", "in_order_candidates", "candidates"], [int(x) for x in stats]))}
 
 
 def c3j_variant(a, synth, TASFlavorSnapshot, flags, steps=20, sample=32):

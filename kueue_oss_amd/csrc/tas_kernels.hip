@@ -1224,9 +1224,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   __shared__ unsigned long long sh_ckey[CAT ? kCatSlots : 1];
   __shared__ int32_t sh_ccnt[CAT ? kCatSlots : 1];
   __shared__ int32_t sh_cflag;
-  __shared__ uint64_t sh_pass[CAT ? 2 * kEvalsPerBlock : 1];
-  __shared__ uint64_t sh_passd[CAT ? kEvalsPerBlock : 1];  // over dense category ids (<= 64 categories)
-  __shared__ uint8_t sh_okb[CAT ? kFillThreads / kWave : 1][CAT ? kCatSlots : 1];  // a wave's verdicts by dense id
+  __shared__ uint64_t sh_passd[CAT ? 2 * kEvalsPerBlock : 1];  // pass masks over dense category ids (two words)
+  __shared__ unsigned long long sh_dkey[CAT ? kCatSlots : 1];  // the categories' keys by dense id
+  __shared__ int32_t sh_dcnt[CAT ? kCatSlots : 1];             // and their leaf counts
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   if (lds_stats)
@@ -1467,23 +1467,34 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
                  : sl < kWave ? __popcll(U0 & ((1ull << sl) - 1ull))
                               : __popcll(U0) + __popcll(U1 & ((1ull << (sl - kWave)) - 1ull));
       }
+      if (threadIdx.x < kCatSlots) {  // the dense table (threads of waves 0 and 1: a slot each)
+        const int sl = int(threadIdx.x);
+        const uint64_t Uh = sl < kWave ? U0 : U1;
+        if ((Uh >> (sl & 63)) & 1ull) {
+          const int d = (sl < kWave ? 0 : __popcll(U0)) + __popcll(Uh & ((1ull << (sl & 63)) - 1ull));
+          sh_dkey[d] = sh_ckey[sl];
+          sh_dcnt[d] = sh_ccnt[sl];
+        }
+      }
+      __syncthreads();
     }
     if (cat_ok) {
       // the classes' verdicts per category: wave w takes classes w, w + 4, ...;
-      // a lane per table slot (two halves of 64)
+      // a lane per dense category id (a second half past 64 categories)
       const int wave = int(threadIdx.x >> 6);
       const bool hn = s.lowest_is_hostname != 0;
+      const int halves = ncat > kWave ? 2 : 1;
       for (int e = wave; e < ne; e += kFillThreads / kWave) {
         const FillEvalParams& P = sh_pos[e].p;
         const int nsel = P.nsel;
         const uint32_t mlo = uint32_t(P.sel_mlo), mhi = uint32_t(P.sel_mhi), wlo = uint32_t(P.sel_wlo),
                        whi = uint32_t(P.sel_whi);
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-          const int slot = half * kWave + lane;
-          const uint64_t key = sh_ckey[slot];
+        if (halves == 1 && lane == 0) sh_passd[2 * e + 1] = 0ull;
+        for (int half = 0; half < halves; half++) {
+          const int dd = half * kWave + lane;
+          const bool used = dd < ncat;
+          const uint64_t key = used ? sh_dkey[dd] : 0ull;
           const uint32_t small = uint32_t(key >> 48);
-          const bool used = (key >> 63) != 0;
           const bool dead = (small & 1u) != 0;
           const int pf = int((small >> 1) & 31u);
           const int zl = int((small >> 6) & 63u) - 1;
@@ -1510,16 +1521,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
             ok = ok && !mis;
           }
           x = (ok && zl >= 0) ? kStatFixed + b.num_taints + zl : x;
-          if (x >= 0) atomicAdd(&sh_stats[e][x], sh_ccnt[slot]);
+          if (x >= 0) atomicAdd(&sh_stats[e][x], sh_dcnt[dd]);
           const uint64_t pass = ballot(ok);
-          if (lane == 0) sh_pass[2 * e + half] = pass;
-          const uint64_t Uh = half ? U1 : U0;
-          if (used) sh_okb[wave][(half ? __popcll(U0) : 0) + __popcll(Uh & ((1ull << lane) - 1ull))] = ok ? 1 : 0;
+          if (lane == 0) sh_passd[2 * e + half] = pass;
         }
-        wave_sync();
-        const uint64_t passd = ballot(lane < ncat && sh_okb[wave][lane] != 0);
-        if (lane == 0) sh_passd[e] = passd;
-        wave_sync();
       }
       __syncthreads();
     }
@@ -1579,7 +1584,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     int32_t* rowp = b.counters + int64_t(e0) * cst;
     uint64_t* rpp = b.rack_pos ? b.rack_pos + int64_t(e0) * lsz + parent : nullptr;
     for (int e = 0; e < ne; e++, rowp += cst, rpp += lsz) {
-      const uint64_t pm = sh_passd[e];
+      const uint64_t pm = sh_passd[2 * e];
       const int32_t m0 = int32_t(uint32_t(pm >> did[0]) << 31) >> 31;
       const int32_t m1 = int32_t(uint32_t(pm >> did[1]) << 31) >> 31;
       const int32_t st0 = state0[0] & m0, st1 = state0[1] & m1;
@@ -1644,11 +1649,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     // and the ExclusionStats were settled before the loop)
     const bool cat_cls = CAT && cat_ok;  // block-uniform
     if (cat_cls) {
-      const uint64_t p0 = sh_pass[2 * e], p1 = sh_pass[2 * e + 1];
+      const uint64_t p0 = sh_passd[2 * e], p1 = sh_passd[2 * e + 1];
 #pragma unroll
       for (int j = 0; j < kPairLP; j++) {
-        const uint64_t w = cslot[j] >= kWave ? p1 : p0;
-        okm[j] = cslot[j] >= 0 && ((w >> (cslot[j] & 63)) & 1ull);
+        const uint64_t w = did[j] >= kWave ? p1 : p0;
+        okm[j] = cslot[j] >= 0 && ((w >> (did[j] & 63)) & 1ull);
         state[j] = okm[j] ? state0[j] : 0;
       }
     }
