@@ -42,6 +42,11 @@ int kueue_tas_last_eval_ticks(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
  * update, findLevelWithFitDomains, threshold-walk keys / k-th select / emit,
  * setup).  ticks holds 12n values. */
 int kueue_tas_last_eval_profile(kueue_tas_ctx* ctx, int32_t* ticks, size_t n);
+/* Profiling build: fill_pair_kernel's per-block phase stamps of the last
+ * device batch (100 MHz clock, 8 per block: start, records staged, CountIn,
+ * categories, verdicts, class loop done); copies min(n, available) ints and
+ * returns that count (0 in the product build). */
+int64_t kueue_tas_last_fill_profile(kueue_tas_ctx* ctx, int32_t* out, size_t n);
 
 /* Host wall time inside the last kueue_tas_eval_batch (ms): [0] request
  * compile, [1] phase-1 classes, [2] uploads + launches, [3] wait for the
@@ -84,6 +89,14 @@ int kueue_tas_set_stage_timing(kueue_tas_ctx* ctx, int32_t on);
 /* Lifetime counts of successful kueue_tas_snapshot_load and
  * kueue_tas_snapshot_splice calls on ctx (tests pin which one an event took). */
 int kueue_tas_snapshot_counters(kueue_tas_ctx* ctx, int64_t* loads, int64_t* splices);
+/* Host-mirror support (the host layer's copy of tasUsage follows the device
+ * lazily): _usage_mark records the resident usage columns and presence bits
+ * as the mirror's state (a device-side shadow copy); _usage_changes lists
+ * every (leaf, column) whose usage or presence moved since the mark, with
+ * its current value (absolute), then marks again.  The list is owned by the
+ * context, valid until its next call. */
+int kueue_tas_snapshot_usage_mark(kueue_tas_ctx* ctx);
+int kueue_tas_snapshot_usage_changes(kueue_tas_ctx* ctx, const kueue_tas_delta** changes, size_t* n);
 
 /* ---- host layer ---------------------------------------------------------- */
 /* Device stage times of the last run (summed over its batches, ms):

@@ -33,6 +33,10 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -60,6 +64,10 @@ template <typename T>
 struct HostBuf {  // pinned host staging
   T* p = nullptr;
   size_t n = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipHostFree(p);
@@ -257,6 +265,8 @@ struct kueue_tas_ctx {
   DevBuf<LfcJob> d_lfc_jobs;
   DevBuf<LfcItem> d_lfc_items;  // [0]: item count, then the items
   DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
+  DevBuf<int32_t> d_fprof;            // profiling build: fill phase stamps [blocks][8]
+  std::vector<int32_t> last_fprof;
   DevBuf<int32_t> d_level_max;        // [n][kMaxLevels] level_max_kernel
   std::vector<int32_t> last_prof;
   int num_profiles = 1;
@@ -283,6 +293,18 @@ struct kueue_tas_ctx {
   DevBuf<uint8_t> sp_rows;
   HostBuf<uint8_t> h_load;
   HostBuf<uint8_t> h_tab;  // load_impl's re-derived tables (pinned arena, async copies)
+  // host-mirror shadow of the usage columns and presence bits (usage_mark / usage_changes)
+  DevBuf<int64_t> d_ushadow;
+  DevBuf<uint32_t> d_pshadow;
+  DevBuf<kueue_tas_delta> d_uchg;
+  DevBuf<int32_t> d_uchg_n;
+  HostBuf<int32_t> h_uchg_n;
+  std::vector<kueue_tas_delta> uchg;
+  bool shadow_ok = false;
+  // apply_deltas stages the records in pinned memory (async copy, no sync);
+  // the event guards the staging buffer's reuse
+  HostBuf<kueue_tas_delta> h_deltas;
+  hipEvent_t ev_deltas = nullptr;
   bool leaf_tags_on = false;
   uint64_t* tag_host = nullptr;
   uint64_t* tag_dev = nullptr;
@@ -448,6 +470,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->evs)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_deltas) (void)hipEventDestroy(c->ev_deltas);
   if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -940,18 +963,64 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
     if (deltas[i].leaf < 0 || deltas[i].leaf >= c->snap.N || deltas[i].col < 0 || deltas[i].col >= c->snap.R)
       return fail(c, KUEUE_TAS_EINVAL, "delta out of range");
   if (n) {
+    // the records through pinned staging: an async copy, no stream sync (the
+    // launches that read the usage follow on the same stream); the previous
+    // call's copy must be done before its buffer is rewritten
+    if (c->ev_deltas) HIPCHK(c, hipEventSynchronize(c->ev_deltas));
+    else HIPCHK(c, hipEventCreateWithFlags(&c->ev_deltas, hipEventDisableTiming));
+    HIPCHK(c, c->h_deltas.reserve(n));
+    memcpy(c->h_deltas.p, deltas, n * sizeof(kueue_tas_delta));
     HIPCHK(c, c->d_deltas.ensure(n));
-    HIPCHK(c, hipMemcpyAsync(c->d_deltas.p, deltas, n * sizeof(kueue_tas_delta), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_deltas.p, c->h_deltas.p, n * sizeof(kueue_tas_delta), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_deltas, c->stream));
     int blocks = int((n + 255) / 256);
     hipLaunchKernelGGL(apply_deltas_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_usage.p, c->d_usage_present.p,
                        c->snap.N, c->d_deltas.p, int(n));
     HIPCHK(c, hipGetLastError());
   }
-  if (usage_present_or_null)
+  if (usage_present_or_null) {
     HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, usage_present_or_null, size_t(c->snap.N) * 4, hipMemcpyHostToDevice,
                              c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (the caller's array)
+  }
   return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_usage_mark(kueue_tas_ctx* c) {
+  if (!c || !c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t N = size_t(c->snap.N), R = size_t(c->snap.R);
+  HIPCHK(c, c->d_ushadow.ensure(N * R));
+  HIPCHK(c, c->d_pshadow.ensure(N));
+  if (N * R) HIPCHK(c, hipMemcpyAsync(c->d_ushadow.p, c->d_usage.p, N * R * 8, hipMemcpyDeviceToDevice, c->stream));
+  if (N) HIPCHK(c, hipMemcpyAsync(c->d_pshadow.p, c->d_usage_present.p, N * 4, hipMemcpyDeviceToDevice, c->stream));
+  c->shadow_ok = true;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_snapshot_usage_changes(kueue_tas_ctx* c, const kueue_tas_delta** changes, size_t* n) {
+  if (!c || !changes || !n) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
+  if (!c->shadow_ok) return fail(c, KUEUE_TAS_EINVAL, "usage_changes before usage_mark");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t N = size_t(c->snap.N), R = size_t(c->snap.R);
+  HIPCHK(c, c->d_uchg.ensure(std::max<size_t>(N * R, 1)));
+  HIPCHK(c, c->d_uchg_n.ensure(1));
+  HIPCHK(c, c->h_uchg_n.ensure(1));
+  HIPCHK(c, hipMemsetAsync(c->d_uchg_n.p, 0, 4, c->stream));
+  if (N * R) {
+    hipLaunchKernelGGL(usage_diff_kernel, dim3(unsigned((N * R + 255) / 256)), dim3(256), 0, c->stream, c->d_usage.p,
+                       c->d_usage_present.p, c->d_ushadow.p, c->d_pshadow.p, int(N), int(R), c->d_uchg.p, c->d_uchg_n.p);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipMemcpyAsync(c->h_uchg_n.p, c->d_uchg_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t k = size_t(c->h_uchg_n.p[0]);
+  c->uchg.resize(k);
+  if (k) HIPCHK(c, hipMemcpy(c->uchg.data(), c->d_uchg.p, k * sizeof(kueue_tas_delta), hipMemcpyDeviceToHost));
+  *changes = c->uchg.data();
+  *n = k;
+  return kueue_tas_snapshot_usage_mark(c);
 }
 
 int kueue_tas_snapshot_set_free(kueue_tas_ctx* c, const int32_t* leaves, size_t n, const int64_t* rows,
@@ -2089,6 +2158,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     HIPCHK(c, c->d_prof.ensure(n * P_NCAT));
     HIPCHK(c, hipMemsetAsync(c->d_prof.p, 0, n * P_NCAT * 4, c->stream));
     b.prof = c->d_prof.p;
+    HIPCHK(c, c->d_fprof.ensure(size_t(1) << 18));
+    HIPCHK(c, hipMemsetAsync(c->d_fprof.p, 0, (size_t(1) << 18) * 4, c->stream));
+    b.fill_prof = c->d_fprof.p;
   }
   c->stat_fills += nfill;
   c->stat_evals += int64_t(n);
@@ -2402,6 +2474,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     const size_t base = c->last_prof.size();
     c->last_prof.resize(base + n * P_NCAT);
     HIPCHK(c, hipMemcpy(c->last_prof.data() + base, c->d_prof.p, n * P_NCAT * 4, hipMemcpyDeviceToHost));
+    c->last_fprof.resize(size_t(1) << 18);
+    HIPCHK(c, hipMemcpy(c->last_fprof.data(), c->d_fprof.p, (size_t(1) << 18) * 4, hipMemcpyDeviceToHost));
   }
   for (size_t i = 0; i < n; i++) {
     c->last_ticks.push_back(c->res_out_h[i].reserved[0]);
@@ -2611,6 +2685,13 @@ int kueue_tas_last_eval_ticks(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   if (!c || !ticks) return KUEUE_TAS_EINVAL;
   for (size_t i = 0; i < 2 * n; i++) ticks[i] = i < c->last_ticks.size() ? c->last_ticks[i] : 0;
   return KUEUE_TAS_OK;
+}
+
+int64_t kueue_tas_last_fill_profile(kueue_tas_ctx* c, int32_t* out, size_t n) {
+  if (!c || !out) return 0;
+  const size_t k = std::min(n, c->last_fprof.size());
+  if (k) memcpy(out, c->last_fprof.data(), k * 4);
+  return int64_t(k);
 }
 
 int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {

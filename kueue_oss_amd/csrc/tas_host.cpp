@@ -641,75 +641,58 @@ class FlavorSnapshot {
     nodeOrderDead = 0;
   }
   // A new snapshot with this one's settings and cache state (for a rebuild).
-  // Usage deltas already applied on the device whose host-mirror update
-  // (tasUsage, usageByDomain: updateTASUsage, tas_flavor_snapshot.go:257-293)
-  // waits until a reader needs the mirror (upload, a column change, a
-  // rebuild): an admission round touches thousands of (leaf, column) pairs and
-  // the device copy is the one evaluations read.  Wrapping adds commute, so
-  // the deferred records may be folded in any order.
-  std::vector<kueue_tas_delta> mirrorPending;
-  void defer_mirror(const kueue_tas_delta* d, size_t n) {
-    mirrorPending.insert(mirrorPending.end(), d, d + n);
-    // a bounded backlog: whoever reads the mirror next (a node join, an
-    // upload) folds at most this many records (~1 ms with the entry cache)
-    if (mirrorPending.size() > (size_t(1) << 18)) flush_mirror();
-  }
-  // The two map entries a (column, leaf) delta updates — tasUsage[leaf][res]
-  // and usageByDomain[leaf id][res] — cached by key after their first fold:
-  // std::map nodes never move and keys are never erased here, so a fold is
-  // two pointer adds per key instead of two string-keyed map walks.  Cleared
+  // Usage deltas applied on the device — admissions (kueue_tas_host_admit)
+  // and other ranks' delta lists (kueue_tas_host_apply_deltas) — reach the
+  // host mirror (tasUsage, usageByDomain: updateTASUsage,
+  // tas_flavor_snapshot.go:257-293) only when a reader needs it (an upload, a
+  // column change, a node join, a rebuild): the device copy is the one
+  // evaluations read.  The device keeps a shadow of the usage columns as of
+  // the mirror's last sync (kueue_tas_snapshot_usage_mark); a flush asks it
+  // for the (leaf, column) entries that moved since (usage_changes: one diff
+  // kernel, absolute values) and sets those mirror entries.  Admission rounds
+  // cost the mirror nothing, and a reader pays for the entries that changed,
+  // however many rounds went by.
+  bool deviceAhead = false;
+  void device_applied() { deviceAhead = true; }
+  // The two map entries a (column, leaf) value lives in — tasUsage[leaf][res]
+  // and usageByDomain[leaf id][res] — cached by key after their first use:
+  // std::map nodes never move and keys are never erased here, so an update
+  // is two pointer stores instead of two string-keyed map walks.  Cleared
   // when leaves are renumbered (flush_joins) or the columns change (recolumn).
   std::vector<std::pair<int64_t*, int64_t*>> mirrorPtr;  // [R][N]
   void clear_mirror_cache() { mirrorPtr.clear(); }
-  // a long backlog (rounds of admissions since the mirror was last read) is
-  // folded per (column, leaf) first, so each distinct key costs its two map
-  // updates once (a key whose deltas cancel still gets its entry: a present
-  // zero differs from an absent key, requests.go:189-192)
-  std::vector<int64_t> mirrorAcc;  // [R][N] folded deltas (zero outside a flush)
-  std::vector<uint32_t> mirrorKeys;
-  std::vector<uint8_t> mirrorSeen;
-  void flush_mirror() {
-    if (mirrorPending.empty()) return;
+  std::pair<int64_t*, int64_t*> mirror_entries(int32_t leaf, int32_t col) {
     const size_t N = size_t(this->N()), R = cols.size();
     const bool cached = N * R < (size_t(1) << 28);
     if (cached && mirrorPtr.size() != N * R) mirrorPtr.assign(N * R, {nullptr, nullptr});
-    auto apply = [&](int32_t leaf, int32_t col, int64_t delta) {
-      std::pair<int64_t*, int64_t*>* e = cached ? &mirrorPtr[size_t(col) * N + size_t(leaf)] : nullptr;
-      if (!e || !e->first) {
-        const std::string& res = cols[size_t(col)];
-        int64_t* v = &tasUsage[size_t(leaf)][res];
-        int64_t* u = &usageByDomain[leafId[size_t(leaf)]][res];
-        if (!e) {
-          *v = add64(*v, delta);
-          *u = add64(*u, delta);
-          return;
-        }
-        *e = {v, u};
-      }
-      *e->first = add64(*e->first, delta);
-      *e->second = add64(*e->second, delta);
-    };
-    if (mirrorPending.size() < 4096 || N * R >= (size_t(1) << 32)) {
-      for (auto& d : mirrorPending) apply(d.leaf, d.col, d.delta);
-    } else {
-      mirrorAcc.resize(N * R, 0);
-      mirrorSeen.resize(N * R, 0);
-      mirrorKeys.clear();
-      for (auto& d : mirrorPending) {
-        const uint32_t key = uint32_t(size_t(d.col) * N + size_t(d.leaf));
-        if (!mirrorSeen[key]) {
-          mirrorSeen[key] = 1;
-          mirrorKeys.push_back(key);
-        }
-        mirrorAcc[key] = add64(mirrorAcc[key], d.delta);
-      }
-      for (uint32_t key : mirrorKeys) {
-        apply(int32_t(key % N), int32_t(key / N), mirrorAcc[key]);
-        mirrorAcc[key] = 0;
-        mirrorSeen[key] = 0;
-      }
+    std::pair<int64_t*, int64_t*>* e = cached ? &mirrorPtr[size_t(col) * N + size_t(leaf)] : nullptr;
+    if (e && e->first) return *e;
+    const std::string& res = cols[size_t(col)];
+    const std::pair<int64_t*, int64_t*> p{&tasUsage[size_t(leaf)][res], &usageByDomain[leafId[size_t(leaf)]][res]};
+    if (e) *e = p;
+    return p;
+  }
+  // deltas the device did not take (a stale device snapshot reloads from the mirror)
+  void apply_to_mirror(const kueue_tas_delta* d, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+      auto e = mirror_entries(d[i].leaf, d[i].col);
+      *e.first = add64(*e.first, d[i].delta);
+      *e.second = add64(*e.second, d[i].delta);
     }
-    mirrorPending.clear();
+  }
+  void flush_mirror() {
+    if (!deviceAhead) return;
+    deviceAhead = false;
+    if (!ctx) return;
+    const kueue_tas_delta* ch = nullptr;
+    size_t k = 0;
+    if (kueue_tas_snapshot_usage_changes(ctx, &ch, &k))
+      throw std::runtime_error(std::string("host mirror sync: ") + kueue_tas_last_error(ctx));
+    for (size_t i = 0; i < k; i++) {  // absolute values: the device's usage as of now
+      auto e = mirror_entries(ch[i].leaf, ch[i].col);
+      *e.first = ch[i].delta;
+      *e.second = ch[i].delta;
+    }
   }
   std::unique_ptr<FlavorSnapshot> fork_state() {
     flush_mirror();
@@ -1557,6 +1540,7 @@ class FlavorSnapshot {
     const double t1 = now_ms();
     int rc = kueue_tas_snapshot_splice(ctx, &sd);
     spliceSrc.clear();
+    if (!rc) rc = kueue_tas_snapshot_usage_mark(ctx);  // device usage == host mirror
     if (rc) {
       err = std::string("snapshot splice: ") + kueue_tas_last_error(ctx);
       return rc;
@@ -1770,6 +1754,7 @@ class FlavorSnapshot {
     d.label_values = labelValues.empty() ? nullptr : labelValues.data();
     d.domain_id_rank = ranks.data();
     int rc = kueue_tas_snapshot_load(ctx, &d);
+    if (!rc) rc = kueue_tas_snapshot_usage_mark(ctx);  // device usage == host mirror
     if (rc) {
       err = std::string("snapshot load: ") + kueue_tas_last_error(ctx);
       return rc;
@@ -1816,6 +1801,7 @@ class FlavorSnapshot {
   // is updated in place by a delta launch; a resource no column holds yet
   // changes the column set, and then the next evaluation reloads the snapshot.
   int update_usage(const std::vector<DomainUsage>& us, bool add, bool device = true) {
+    flush_mirror();  // the mirror and the device's shadow in step before both change
     std::vector<kueue_tas_delta> deltas;
     bool new_col = false;
     for (auto& u : us) {
@@ -1846,6 +1832,7 @@ class FlavorSnapshot {
     }
     if (!device || dirty || !ctx || deltas.empty()) return 0;
     int rc = kueue_tas_snapshot_apply_deltas(ctx, deltas.data(), deltas.size(), nullptr);
+    if (!rc) rc = kueue_tas_snapshot_usage_mark(ctx);  // the mirror already has these deltas
     if (rc) err = std::string("apply deltas: ") + kueue_tas_last_error(ctx);
     return rc;
   }
@@ -4903,7 +4890,7 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       }
     }
     if (n_deltas) *n_deltas = deltas.size();
-    s.defer_mirror(deltas.data(), deltas.size());
+    s.device_applied();
     h->admit_ms[0] = t1 - t0;
     h->admit_ms[1] = t2 - t1;
     h->admit_ms[2] = now_ms() - t2;
@@ -4941,14 +4928,15 @@ int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* d, siz
     for (size_t i = 0; i < n; i++)
       if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
         throw std::runtime_error("delta out of range");
-    s.defer_mirror(d, n);
-    if (s.dirty || !s.ctx) {
+    if (s.dirty || !s.ctx) {  // no device copy to follow: the mirror takes the deltas, the upload the mirror
+      s.apply_to_mirror(d, n);
       const int rc = s.upload();
       if (rc) h->err = s.err;  // sticky, as on the admit path
       return rc;
     }
     int rc = n ? kueue_tas_snapshot_apply_deltas(s.ctx, d, n, nullptr) : 0;
     if (rc) h->err = std::string("apply deltas: ") + kueue_tas_last_error(s.ctx);
+    else if (n) s.device_applied();  // the host mirror follows at its next read
     return rc;
   } catch (const std::exception& e) {
     h->err = e.what();

@@ -206,6 +206,7 @@ struct DevBatch {
   int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
   int32_t tag_epoch;
   int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
+  int32_t* fill_prof;      // [blocks][8] fill_pair_kernel phase stamps (profiling build only, else null)
   int32_t* level_max;      // [nfill][kMaxLevels] max sliceState per level < L-1 of the class row's counters
                            // (level_max_kernel; rows of class reps only), null: not computed
 };

@@ -1198,6 +1198,18 @@ constexpr int kPairLP = 2;                     // leaves per thread (adjacent)
 constexpr int kCatSlots = 2 * 64;              // leaf-category table of a fill_pair_kernel block (CAT)
 constexpr int kPairTile = kPairLP * kFillThreads;  // leaves per block
 
+// Profiling build: fill_pair_kernel's block phase stamps (DevBatch::fill_prof)
+#ifndef KTAS_PROFILE
+#define KTAS_PROFILE 0
+#endif
+#define KTAS_FILL_STAMP(k)                                                                       \
+  do {                                                                                          \
+    if (KTAS_PROFILE && b.fill_prof && threadIdx.x == 0) {                                      \
+      const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;                                 \
+      if (blk < (1u << 15)) b.fill_prof[blk * 8 + (k)] = int32_t(uint32_t(wall_clock64()));       \
+    }                                                                                           \
+  } while (0)
+
 // Or-fold: the positive-children masks
 struct OpOr {
   __device__ int32_t operator()(int32_t a, int32_t b) const { return a | b; }
@@ -1229,6 +1241,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   __shared__ int32_t sh_dcnt[CAT ? kCatSlots : 1];             // and their leaf counts
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
+  KTAS_FILL_STAMP(0);
   if (lds_stats)
     for (int i = threadIdx.x; i < kEvalsPerBlock * kMaxFillStats; i += kFillThreads) (&sh_stats[0][0])[i] = 0;
   if constexpr (CAT) {
@@ -1384,7 +1397,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       }
     }
   };
+  KTAS_FILL_STAMP(1);
   if constexpr (!MR) count_run(0);
+  KTAS_FILL_STAMP(2);
   // ---- CAT: leaf categories.  In a single-run chunk every filter of
   // fillInCounts (:1578-1634) sees a leaf only through its category: out of
   // the snapshot or not, taint profile, the label ids the chunk's
@@ -1455,6 +1470,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       __syncthreads();
       cat_ok = sh_cflag == 0;  // block-uniform
     }
+    KTAS_FILL_STAMP(3);
     uint64_t U0 = 0, U1 = 0;  // the table's used slots: dense id = rank among them
     if (cat_ok) {
       U0 = ballot(sh_ckey[lane] != 0ull);
@@ -1527,6 +1543,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         }
       }
       __syncthreads();
+      KTAS_FILL_STAMP(4);
     }
   }
   // ragged slots: the parents of the lane's two leaves, which of them start
@@ -1607,6 +1624,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       }
     }
   }
+  KTAS_FILL_STAMP(5);
   for (int e = 0; e < ne && !lean; e++) {
     const int4* pq = reinterpret_cast<const int4*>(&sh_pos[e].p);
     const int4 q0 = pq[0], q1 = pq[1], q2 = pq[2];
@@ -5389,6 +5407,21 @@ __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present,
 // (nonTasUsageCache.update/delete, tas_non_tas_pod_cache.go:46-87, folded in by
 // TASFlavorCache.snapshot, tas_flavor.go:133-137): one thread per (leaf, column),
 // column-major stores so a wave writes one column of 64 leaves.
+// Host-mirror diff (kueue_tas_snapshot_usage_changes): every (column, leaf)
+// whose usage or presence bit differs from the shadow, with its value.
+__global__ void usage_diff_kernel(const int64_t* usage, const uint32_t* present, const int64_t* shadow,
+                                  const uint32_t* pshadow, int N, int R, kueue_tas_delta* out, int32_t* count) {
+  const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= int64_t(N) * R) return;
+  const int col = int(idx / N), leaf = int(idx % N);
+  const int64_t v = usage[idx];
+  const bool p = (present[leaf] >> col) & 1u, ps = (pshadow[leaf] >> col) & 1u;
+  if (v != shadow[idx] || p != ps) {
+    const int k = atomicAdd(count, 1);
+    out[k] = kueue_tas_delta{leaf, col, v};
+  }
+}
+
 __global__ void set_free_kernel(int64_t* free_cap, uint32_t* free_present, int N, int R, const int32_t* leaves,
                                 const int64_t* rows, const uint32_t* present, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

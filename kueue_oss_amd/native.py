@@ -65,7 +65,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
     "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
-    "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext",
+    "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
+    "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -158,6 +159,8 @@ def _bind(lib):
     lib.kueue_tas_host_last_stats_ext.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_last_alias_fills.argtypes = [c.c_void_p]
     lib.kueue_tas_last_alias_fills.restype = c.c_int64
+    lib.kueue_tas_last_fill_profile.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_size_t]
+    lib.kueue_tas_last_fill_profile.restype = c.c_int64
     lib.kueue_tas_host_update_usage.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
     lib.kueue_tas_host_update_usage.restype = c.c_int
     lib.kueue_tas_host_fits.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]

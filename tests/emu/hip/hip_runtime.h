@@ -305,6 +305,12 @@ inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
+constexpr unsigned hipEventDisableTiming = 2;
+inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
+inline hipError_t hipEventSynchronize(hipEvent_t e) {  // the recording stream up to the event
+  if (e->stream) e->stream->run_until(e->pos);
+  return hipSuccess;
+}
 enum hipFuncAttribute { hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
 inline hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int) { return hipSuccess; }  // LDS is host memory here
 inline hipError_t hipEventDestroy(hipEvent_t e) { delete e; return hipSuccess; }
