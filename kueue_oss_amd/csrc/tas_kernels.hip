@@ -6041,7 +6041,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
   int ntodo = todo[0];
   __syncthreads();
   int w0 = 0;  // position in the todo list
-  int rounds = 0, sweeps = 0, nrej_since = 0;
+  int rounds = 0, sweeps = 0, nrej_since = 0, sweep_gate = kAdmitWindow / 4;
   int pf_pos = -1, pf_w = n_wl;  // the next window's candidate, fetched during this round
   int64_t pf_r0 = 0, pf_r1 = 0;
   while (w0 < ntodo) {  // block-uniform
@@ -6195,10 +6195,13 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     // list compacted in place — nominated workloads that all target the same
     // best-fit domains (an idle, uniform cluster) leave the pass in a few
     // sweeps instead of a window round per 16 of them.
+    // A sweep costs a pass over every remaining candidate's records: after one
+    // that rejected under a quarter of them the next needs 4x the rejections.
     for (int q = 0; q < k; q++) nrej_since += sh_fit[q] ? 0 : 1;
-    if (nrej_since >= kAdmitWindow / 4 && ntodo - w0 > 2 * kAdmitWindow && !exact) {  // block-uniform
+    if (nrej_since >= sweep_gate && ntodo - w0 > 2 * kAdmitWindow && !exact) {  // block-uniform
       nrej_since = 0;
       sweeps++;
+      const int swept_from = ntodo - w0;
       for (int pos = w0 + wave; pos < ntodo; pos += kAdmitWindow) {
         const int w = todo[1 + pos];
         const int64_t r0 = todo_r[2 * pos], r1 = todo_r[2 * pos + 1];
@@ -6270,6 +6273,7 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
         __threadfence_block();
         __syncthreads();
       }
+      if (4 * (swept_from - (out_base - w0)) < swept_from) sweep_gate *= 4;
       ntodo = out_base;
       pf_pos = -1;  // the prefetched candidate's position moved
     }
