@@ -1,7 +1,8 @@
 """fill_pair_kernel: the staged fill with two adjacent leaves per thread
 (fillInCounts tas_flavor_snapshot.go:1568-1647 + the fused first level of
 fillInCountsHelper :1658-1719), ExclusionStats counted in its class loop.
-Checked bit-exactly against the oracle for single-run and multi-run chunks,
+Checked bit-exactly against the oracle for single-run and multi-run chunks
+(C3J-like: a request signature per workload over ragged racks),
 fused fan-outs 2 / 4 / 8 / 16 / 32 / 64, no fused parents (fan-out > 64, odd
 leaf counts: the partial last group), leader groups, taints, selectors and
 affinity; the one-leaf staged kernel (KUEUE_TAS_CFG_NO_PAIR_FILL) must give
@@ -47,6 +48,9 @@ def _configs(scale):
     yield "c3 fan-out 101 (no fused parents, odd N)", *synth.config_c3(seed=7, n_workloads=n, shape=(1, 1, 3, 101))
     yield "c2 mixed", *synth.config_c2(seed=8, n_workloads=n, shape=(2, 2, 4 * scale, 32))
     yield "c4 leaders", *synth.config_c4(seed=9, n_workloads=8 * scale, shape=(2, 2, 4 * scale, 16))
+    # every workload its own request signature (multi-run chunks) over ragged
+    # racks, full GPU leaves excluded by resource
+    yield "c3j multi-run", *synth.config_c3j(seed=13, n_workloads=2 * n, shape=(2, 2, 4 * scale))
 
 
 def _run(make_pair, make_staged, scale, make_percls=None):

@@ -17,7 +17,7 @@ ap.add_argument("--check", type=int, default=0)
 ap.add_argument("--config", default="C3J")
 a = ap.parse_args()
 doc, wls = synth.CONFIGS[a.config](n_workloads=1024)
-snap = TASFlavorSnapshot(doc)
+snap = TASFlavorSnapshot(doc, category_fill=not os.environ.get("NO_CAT"))
 snap.compile(wls)
 FULL = TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES
 for _ in range(3):
