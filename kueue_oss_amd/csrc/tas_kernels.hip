@@ -1226,7 +1226,10 @@ template <int NS, bool TS, bool MR, bool GL, int FC, bool CAT = false>  // FC: 3
 // tiles x 8 chunks — resident at once instead of 6 blocks per CU and a second
 // dispatch round): ~20 prologue values spill to scratch, 37.8 -> 36.4 us
 // (profiles/r05/waves8)
-__global__ __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_eu(CAT ? 8 : 1)))
+#ifndef KTAS_WAVES_PER_EU  // (the CPU emulator build of tests/emu defines it empty)
+#define KTAS_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
+__global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(CAT ? 8 : 1)
 void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
   static_assert(!CAT || (!MR && !GL && TS), "leaf categories: single-run chunks, staged filters, LDS taint rows");
