@@ -4539,11 +4539,22 @@ __device__ int lfc_first_leaf(const Wave& w, const DevBatch& b, int slot, const 
     if (m) chunk = c0 + __ffsll((unsigned long long)m) - 1;
   }
   if (chunk < 0) return -1;
+  // the chunk in rounds of 8 x 64 leaves, every load of a round issued
+  // before its ballots (one memory round trip per 512 leaves, not per 64)
   const int lo = chunk * kLfcChunk, hi = min(g_select_snap.N, lo + kLfcChunk);
-  for (int i0 = lo; i0 < hi; i0 += kWave) {
-    const int i = i0 + lane_id();
-    const uint64_t m = ballot(i < hi && V[i] == v);
-    if (m) return i0 + __ffsll((unsigned long long)m) - 1;
+  constexpr int kU = 8;
+  for (int i0 = lo; i0 < hi; i0 += kU * kWave) {
+    int32_t x[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const int i = i0 + k * kWave + lane_id();
+      x[k] = i < hi ? V[i] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t m = ballot(x[k] == v);
+      if (m) return i0 + k * kWave + __ffsll((unsigned long long)m) - 1;
+    }
   }
   return -1;
 }
@@ -4714,9 +4725,19 @@ __device__ LfcJob lfc_fast(Wave& w, const DevBatch& b, int slot, kueue_tas_eval_
       if (ci < b.lfc_nchunks) {
         const int64_t off = (int64_t(slot) * b.lfc_nchunks + ci) * kLfcBins;
         int64_t a = 0, cc = 0;
-        for (int v = 1; v < t; v++) {
-          a += b.lfc_cp[off + v];
-          cc += b.lfc_ch[off + v];
+        for (int v0 = 1; v0 < t; v0 += 8) {  // 8 bins' loads in flight per round trip
+          uint32_t pv[8], hv[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const bool in = v0 + k < t;
+            pv[k] = in ? b.lfc_cp[off + v0 + k] : 0u;
+            hv[k] = in ? b.lfc_ch[off + v0 + k] : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            a += pv[k];
+            cc += hv[k];
+          }
         }
         tb = b.lfc_cp[off + t];
         const int64_t tin = b.lfc_ch[off + t];
