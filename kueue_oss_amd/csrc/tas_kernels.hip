@@ -1222,15 +1222,10 @@ struct OpOr {
 // staged data (!GL), taint rows in LDS (TS), ExclusionStats in LDS.
 template <int NS, bool TS, bool MR, bool GL, int FC, bool CAT = false>  // FC: 32 compile-time fan-out, 0: b.rack_fanout
                                                       // (or none), -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
-// CAT: at most 64 VGPRs (8 waves per SIMD, every block of the C3 grid — 256
-// tiles x 8 chunks — resident at once instead of 6 blocks per CU and a second
-// dispatch round): ~20 prologue values spill to scratch, 37.8 -> 36.4 us
-// (profiles/r05/waves8)
-#ifndef KTAS_WAVES_PER_EU  // (the CPU emulator build of tests/emu defines it empty)
-#define KTAS_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
-#endif
-__global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(CAT ? 8 : 1)
-void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
+// (75-79 VGPRs: 6 waves per SIMD.  Forcing 8 — the whole C3 grid resident —
+// spilled ~20 prologue values: 37.8 -> 36.4 us but 61 -> 113 MB of HBM
+// traffic per launch, profiles/r05/waves8 and final2/pmc_summary.json)
+__global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevBatch b, uint32_t stage_mask,
                                                                  int chunk_base) {
   static_assert(!CAT || (!MR && !GL && TS), "leaf categories: single-run chunks, staged filters, LDS taint rows");
   __shared__ FillPos sh_pos[kEvalsPerBlock];  // the chunk's host-built position records

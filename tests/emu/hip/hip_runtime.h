@@ -25,7 +25,6 @@
 #define __host__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
-#define KTAS_WAVES_PER_EU(...)
 #define __shared__ static thread_local
 #define __constant__
 #define HIP_SYMBOL(x) (&(x))
