@@ -190,7 +190,8 @@ def main():
         snap.run_compiled(flags=flags)
         if dist is not None and gather:
             # RCCL all-gather of every rank's full assignments (quads) over xGMI
-            gather_assignments(snap.last_assignments(), world, dist, device)
+            # (the block stays on the device: only an admitting rank copies it out)
+            gather_assignments(snap.last_assignments(), world, dist, device, to_host=False)
 
     # the snapshot document and generated workloads are long-lived: keep them
     # out of the collector's scans during the timed loop

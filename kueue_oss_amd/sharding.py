@@ -59,14 +59,41 @@ def _grow(key, need):
     return c
 
 
-def gather_assignments(quads, world: int, dist, device=None):
+_BUFS: dict = {}
+
+
+def _exchange_buffers(key, words: int, world: int, dtype, device):
+    """Reused exchange buffers for one (capacity, world, device): a pinned host
+    staging row (async host-to-device copy), the device send row and the
+    [world, words] receive block (RCCL all_gather_into_tensor).  Host
+    collectives (gloo, device None / "cpu") send the host row itself."""
+    import torch
+
+    k = (key, words, world, str(device), dtype)
+    b = _BUFS.get(k)
+    if b is None:
+        cuda = device is not None and str(device).startswith("cuda")
+        host = torch.zeros(words, dtype=dtype, pin_memory=cuda)
+        send = torch.empty(words, dtype=dtype, device=device) if cuda else host
+        recv = torch.empty((world, words), dtype=dtype, device=device if cuda else None)
+        for old in [x for x in _BUFS if x[0] == key]:  # one live capacity per exchange
+            del _BUFS[old]
+        b = _BUFS[k] = (host, send, recv, cuda)
+    return b
+
+
+def gather_assignments(quads, world: int, dist, device=None, to_host: bool = True):
     """All-gather every rank's full assignments (kueue_tas_host_last_assignments
     int32 quads: per workload a header and one (id, podset, leaf, count) per
     assigned domain) over RCCL (xGMI) or gloo.  Each rank sends one padded
-    record buffer [length, quads..., padding] of the shared capacity; a round
-    in which some rank's quads exceed it is repeated once with a larger
-    capacity (every rank sees every length, so all agree).  Returns the
-    concatenated int32 numpy array, ranks in order; every rank receives all of it."""
+    record row [length, quads..., padding] of the shared capacity from reused
+    buffers (pinned staging, one async host-to-device copy; RCCL:
+    all_gather_into_tensor into one [world, capacity] block); a round in which
+    some rank's quads exceed the capacity is repeated once with a larger one
+    (every rank sees every length, so all agree).  Returns the concatenated
+    int32 numpy array, ranks in order (every rank receives all of it), or with
+    ``to_host=False`` the device block and the per-rank lengths (no
+    device-to-host copy of the block: a rank that does not admit)."""
     import numpy as np
     import torch
 
@@ -74,15 +101,20 @@ def gather_assignments(quads, world: int, dist, device=None):
     n = q.size
     while True:
         cap = _CAP["gather"]
-        host = np.zeros(cap + 1, dtype=np.int32)
-        host[0] = n
-        host[1:1 + min(n, cap)] = q[:cap]
-        buf = torch.from_numpy(host).to(device)
-        out = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(out, buf)
-        parts = torch.stack(out).cpu().numpy()  # the exchange's one device-to-host copy
-        lens = parts[:, 0]
+        host, send, recv, cuda = _exchange_buffers("gather", cap + 1, world, torch.int32, device)
+        hv = host.numpy()
+        hv[0] = n
+        hv[1:1 + min(n, cap)] = q[:cap]  # words past the length are never read
+        if cuda:
+            send.copy_(host, non_blocking=True)  # ordered before the collective on the current stream
+            dist.all_gather_into_tensor(recv, send)
+        else:
+            dist.all_gather(list(recv.unbind(0)), send)
+        lens = recv[:, 0].cpu().numpy()  # (synchronizes: the staging row is free again)
         if int(lens.max()) <= cap:
+            if not to_host:
+                return recv, lens
+            parts = recv.cpu().numpy()  # the exchange's one device-to-host copy
             return np.concatenate([parts[r, 1:1 + int(lens[r])] for r in range(world)])
         _grow("gather", int(lens.max()))
 
@@ -93,7 +125,8 @@ def broadcast_deltas(deltas, dist, src: int = 0, device=None):
     tas_flavor_snapshot.go:257-293) from rank ``src``; every replica gets the
     identical list to apply with kueue_tas_host_apply_deltas.  One padded
     buffer [count, records as two int64 words each...] of the shared
-    capacity; a count of -1 is the source's failure sentinel (admit_round)."""
+    capacity (reused pinned staging and device row); a count of -1 is the
+    source's failure sentinel (admit_round)."""
     import numpy as np
     import torch
 
@@ -103,14 +136,18 @@ def broadcast_deltas(deltas, dist, src: int = 0, device=None):
     k = -1 if is_src and deltas is None else (len(deltas) if is_src else 0)
     while True:
         cap = _CAP["deltas"]
-        host = np.zeros(1 + 2 * cap, dtype=np.int64)
+        host, buf, _, cuda = _exchange_buffers("deltas", 1 + 2 * cap, 1, torch.int64, device)
+        hv = host.numpy()
         if is_src:
-            host[0] = k
+            hv[0] = k
             if 0 < k <= cap:
-                host[1:1 + 2 * k] = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE).view(np.int64)
-        buf = torch.from_numpy(host).to(device)
+                hv[1:1 + 2 * k] = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE).view(np.int64)
+            if cuda:
+                buf.copy_(host, non_blocking=True)
         dist.broadcast(buf, src)
-        got = buf.cpu().numpy()
+        if cuda:
+            host.copy_(buf)  # (synchronous: the records are read right away)
+        got = hv
         k = int(got[0])
         if k < 0:  # the source's admission failed: every rank fails with it
             raise RuntimeError(f"admission failed on rank {src}")

@@ -176,3 +176,48 @@ def test_delta_records_roundtrip():
     d["delta"] = [-5, 1 << 40, 7]
     words = d.view(np.int64).reshape(3, 2)
     assert words.reshape(-1).view(DELTA_DTYPE).tolist() == d.tolist()
+
+
+_NCCL_EXCHANGE = r"""
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from kueue_oss_amd import sharding
+from kueue_oss_amd.native import DELTA_DTYPE
+
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+rng = np.random.default_rng(5)
+for n in (12, 4 * 70000):  # the second overflows the initial capacity: the grow-and-repeat round
+    q = rng.integers(-5, 1 << 20, size=n, dtype=np.int32)
+    got = sharding.gather_assignments(q, 1, dist, "cuda:0")
+    assert np.array_equal(got, q), n
+    block, lens = sharding.gather_assignments(q, 1, dist, "cuda:0", to_host=False)
+    assert block.is_cuda and int(lens[0]) == n
+    assert np.array_equal(block[0, 1:1 + n].cpu().numpy(), q)
+d = np.zeros(5000, dtype=DELTA_DTYPE)  # overflows the initial delta capacity
+d["leaf"] = np.arange(5000)
+d["col"] = 1
+d["delta"] = -(np.arange(5000, dtype=np.int64) << 33)
+got = sharding.broadcast_deltas(d, dist, 0, "cuda:0")
+assert np.array_equal(got, d)
+dist.destroy_process_group()
+print("exchange ok")
+"""
+
+
+@pytest.mark.gpu
+def test_exchange_buffers_on_rccl():
+    """The RCCL side of the exchange (pinned staging, all_gather_into_tensor,
+    device-resident block, capacity growth, delta broadcast) in a one-rank
+    nccl group on the box's GPU (a child process: its own process group)."""
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, "-c", _NCCL_EXCHANGE, os.path.dirname(HERE), str(_free_port())],
+                       capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0 and "exchange ok" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
