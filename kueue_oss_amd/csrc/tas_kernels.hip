@@ -2561,7 +2561,27 @@ __global__ __launch_bounds__(256) void rollup_tail_kernel(DevSnap s, DevBatch b,
   for (int l = 0; l + 1 < s.L; l++) {
     const int32_t* ss = base + SSO + s.level_off[l];
     int32_t m = INT32_MIN;
-    for (int i = threadIdx.x; i < s.level_size[l]; i += 256) m = max(m, l <= top ? load_l2_i32(ss + i) : ss[i]);
+    if (l <= top) {  // this block's own parents: through L2
+      for (int i = threadIdx.x; i < s.level_size[l]; i += 256) m = max(m, load_l2_i32(ss + i));
+    } else {  // written by earlier launches: int4 loads (levels start 16-byte aligned), all issued first
+      const int D = s.level_size[l];
+      const int nq = (D + 3) / 4;
+      const int4* ss4 = reinterpret_cast<const int4*>(ss);
+      constexpr int U = 4;
+      for (int q0 = 0; q0 < nq; q0 += U * 256) {
+        int4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ss4[min(q0 + u * 256 + int(threadIdx.x), nq - 1)];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int q = q0 + u * 256 + int(threadIdx.x);
+          const int32_t e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (q < nq && 4 * q + k < D) m = max(m, e[k]);
+        }
+      }
+    }
     m = group_reduce(m, 64, OpMax());
     if (lane_id() == 0) red[wv] = m;
     __syncthreads();
