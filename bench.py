@@ -189,9 +189,10 @@ def main():
     def step(flags=FULL, gather=True):
         snap.run_compiled(flags=flags)
         if dist is not None and gather:
-            # RCCL all-gather of every rank's full assignments (quads) over xGMI
-            # (the block stays on the device: only an admitting rank copies it out)
-            gather_assignments(snap.last_assignments(), world, dist, device, to_host=False)
+            # RCCL all-gather of every rank's full assignments (quads) over xGMI;
+            # rank 0, the admitting rank, copies the gathered block to its host
+            # (admit_round's exchange), the other ranks leave it on the device
+            gather_assignments(snap.last_assignments(), world, dist, device, to_host=rank == 0)
 
     # the snapshot document and generated workloads are long-lived: keep them
     # out of the collector's scans during the timed loop
@@ -439,6 +440,19 @@ def widened_rows(a, snap, snap_doc, mine, synth):
     pre_ms = (time.perf_counter() - t0) * 1e3
     for c in cands:
         snap.remove_usage(c)
+    # batched partial-admission search (podset_reducer.go:37-86): the first
+    # workload whose full counts x 64 do not fit, every PodSet down to 1 pod
+    pa = None
+    for w in mine[:64]:
+        big = [dict(p, count=p.get("count", 1) * 64, minCount=1) for p in w]
+        if any(r["reason"] for r in snap.find_topology_assignments_for_flavor(big)):
+            snap.partial_admission_search(big)
+            t0 = time.perf_counter()
+            r = snap.partial_admission_search(big)
+            pa = {"ms": round((time.perf_counter() - t0) * 1e3, 3), "found": r["found"], "probes": r["probes"],
+                  "evaluations": r["evaluations"], "device_batches": r["batches"],
+                  "full_counts": [p["count"] for p in big], "counts": r["counts"]}
+            break
     evs = [{"namespace": "bench", "name": f"np{k}", "nodeName": snap_doc["nodes"][k * 977 % N]["name"],
             "phase": "Running", "requests": {"cpu": 1000, "memory": 1 << 30}} for k in range(64)]
     t0 = time.perf_counter()
@@ -515,6 +529,7 @@ def widened_rows(a, snap, snap_doc, mine, synth):
             "preemption_search_profile_ms": pr["profileMs"],
             "preemption_search_ms": round(pre_ms, 3), "preemption_candidates": len(cands),
             "preemption_first_fit": pr["firstFit"], "preemption_fill_back_evals": pr["fillBackEvals"],
+            "partial_admission_search": pa,
             "v1beta2_encode_ms_per_batch": round(enc_ms, 3),
             "fits_ms_per_call": round(fits_ms, 3), "fits_records_per_call": min(8, len(recs)),
             "usage_update_ms_per_call": round(upd_ms, 3)}

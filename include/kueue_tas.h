@@ -557,6 +557,23 @@ int kueue_tas_host_update_nodes(kueue_tas_host* h, const char* nodes_json, int32
 int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json, const char* candidates_json,
                                      char** out_json);
 
+/* Batched partial-admission search: PodSetReducer.Search
+ * (pkg/scheduler/flavorassigner/podset_reducer.go:37-86, called from
+ * Scheduler.getInitialAssignments, pkg/scheduler/scheduler.go:720-739) over
+ * the TAS fit of the workload: podsets_json as for kueue_tas_host_find, each
+ * PodSet with its "count" and optional "minCount" (absent = count) and
+ * "tas": false for a PodSet that only takes part in the count arithmetic
+ * (no TAS request).  A probe's counts fit when FindTopologyAssignmentsForWorkload
+ * with those counts (count-0 PodSets skipped, tas_flavorassigner.go:52-55)
+ * reports no failure; quota and preemption targets are the caller's.
+ * sort.Search's decision tree is evaluated `max_batch` probes (<= 0: 1023)
+ * per device batch, speculatively, so the probes and the answer are the
+ * reference's.  *out_json = {"found": bool, "counts": [per PodSet] or null,
+ * "results": [PodSet results of the found counts] or null, "probes": the
+ * reference's fits() calls, "evaluations", "batches", "profileMs"}. */
+int kueue_tas_host_partial_admission_search(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty,
+                                            int32_t max_batch, char** out_json);
+
 /* ---- the snapshot queries of the scheduler's other callers ---------------
  *  has_level: TASFlavorSnapshot.HasLevel (tas_flavor_snapshot.go:1065-1088;
  *    caller tas_flavorassigner.go:195) for a kueue.PodSetTopologyRequest in

@@ -97,6 +97,11 @@ int kueue_tas_snapshot_counters(kueue_tas_ctx* ctx, int64_t* loads, int64_t* spl
  * context, valid until its next call. */
 int kueue_tas_snapshot_usage_mark(kueue_tas_ctx* ctx);
 int kueue_tas_snapshot_usage_changes(kueue_tas_ctx* ctx, const kueue_tas_delta** changes, size_t* n);
+/* kueue_tas_snapshot_apply_deltas for deltas the host mirror already took
+ * (AddUsage / RemoveUsage through the host layer): the shadow takes them as
+ * well, so the mirror needs no diff for them and earlier device-only changes
+ * stay pending for the next _usage_changes. */
+int kueue_tas_snapshot_apply_deltas_mirrored(kueue_tas_ctx* ctx, const kueue_tas_delta* deltas, size_t n);
 
 /* ---- host layer ---------------------------------------------------------- */
 /* Device stage times of the last run (summed over its batches, ms):

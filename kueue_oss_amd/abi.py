@@ -1,4 +1,4 @@
-"""ctypes mirror of the plain-C structs of include/kueue_tas.h (ABI version 4).
+"""ctypes mirror of the plain-C structs of include/kueue_tas.h (ABI version 5).
 
 For bindings that call the device layer directly (kueue_tas_snapshot_load,
 kueue_tas_eval_batch) instead of going through the JSON host layer; the

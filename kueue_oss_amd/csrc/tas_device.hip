@@ -955,8 +955,17 @@ int kueue_tas_encode_v1beta2_leaves(kueue_tas_ctx* c, const int32_t* pairs, cons
   return run_encode(c, a, n_assign, out, same_counts);
 }
 
+static int apply_deltas_impl(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n,
+                             const uint32_t* usage_present_or_null, bool mirrored);
 int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n,
                                     const uint32_t* usage_present_or_null) {
+  return apply_deltas_impl(c, deltas, n, usage_present_or_null, false);
+}
+int kueue_tas_snapshot_apply_deltas_mirrored(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n) {
+  return apply_deltas_impl(c, deltas, n, nullptr, true);
+}
+static int apply_deltas_impl(kueue_tas_ctx* c, const kueue_tas_delta* deltas, size_t n,
+                             const uint32_t* usage_present_or_null, bool mirrored) {
   if (!c || !c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
   HIPCHK(c, hipSetDevice(c->device));
   for (size_t i = 0; i < n; i++)
@@ -974,8 +983,10 @@ int kueue_tas_snapshot_apply_deltas(kueue_tas_ctx* c, const kueue_tas_delta* del
     HIPCHK(c, hipMemcpyAsync(c->d_deltas.p, c->h_deltas.p, n * sizeof(kueue_tas_delta), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_deltas, c->stream));
     int blocks = int((n + 255) / 256);
+    const bool sh = mirrored && c->shadow_ok;  // no shadow yet: the next mark copies the usage whole
     hipLaunchKernelGGL(apply_deltas_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_usage.p, c->d_usage_present.p,
-                       c->snap.N, c->d_deltas.p, int(n));
+                       c->snap.N, c->d_deltas.p, int(n), sh ? c->d_ushadow.p : nullptr,
+                       sh ? c->d_pshadow.p : nullptr);
     HIPCHK(c, hipGetLastError());
   }
   if (usage_present_or_null) {
@@ -1231,9 +1242,24 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t up_bytes = o_total + KUEUE_TAS_MAX_COLS * 8;
   const size_t o_out = al(up_bytes);
   const size_t nwords = (size_t(c->snap.N) + 31) / 32;
-  const bool lds_bits = nwords * 4 <= 64 * 1024;
+  // the dynamic bitmaps share the workgroup's 64 KB of LDS with the kernel's
+  // static arrays (the window kernel's fit / conflict flags and sweep scan)
+  static const size_t static_lds[2] = {
+      [] {
+        hipFuncAttributes a{};
+        return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(admit_kernel)) == hipSuccess ? size_t(a.sharedSizeBytes)
+                                                                                                  : size_t(16 * 1024);
+      }(),
+      [] {
+        hipFuncAttributes a{};
+        return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(admit_window_kernel)) == hipSuccess
+                   ? size_t(a.sharedSizeBytes)
+                   : size_t(16 * 1024);
+      }()};
+  const size_t lds_budget = 64 * 1024 - static_lds[c->admit_window ? 1 : 0];
+  const bool lds_bits = nwords * 4 <= lds_budget;
   // the windowed kernel's round bitmap beside the touched one: admission chains within a window
-  const bool lds_chain = c->admit_window && 2 * nwords * 4 <= 64 * 1024;
+  const bool lds_chain = c->admit_window && 2 * nwords * 4 <= lds_budget;
   const size_t o_recs = o_out + al((n_wl + 3) * 4);  // + three diagnostics words (admit_window_kernel)
   const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
   const size_t o_todo = o_dep + al(n_wl * 4);

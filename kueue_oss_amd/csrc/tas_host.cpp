@@ -672,8 +672,12 @@ class FlavorSnapshot {
     if (e) *e = p;
     return p;
   }
-  // deltas the device did not take (a stale device snapshot reloads from the mirror)
+  // deltas the device did not take (a stale device snapshot reloads from the
+  // mirror).  The mirror first takes what the device applied since the last
+  // mark: the upload's own flush would otherwise overwrite these deltas with
+  // the device's absolute values, which do not hold them.
   void apply_to_mirror(const kueue_tas_delta* d, size_t n) {
+    flush_mirror();
     for (size_t i = 0; i < n; i++) {
       auto e = mirror_entries(d[i].leaf, d[i].col);
       *e.first = add64(*e.first, d[i].delta);
@@ -1800,8 +1804,16 @@ class FlavorSnapshot {
   // pods:count; domains that are not leaves are skipped.  The device replica
   // is updated in place by a delta launch; a resource no column holds yet
   // changes the column set, and then the next evaluation reloads the snapshot.
+  // The device's own pending changes (admissions) stay pending: the mirror,
+  // the device usage and the device's shadow of the mirror all take the same
+  // deltas, so O(#records) work and no diff (updateTASUsage is O(#domains)).
   int update_usage(const std::vector<DomainUsage>& us, bool add, bool device = true) {
-    flush_mirror();  // the mirror and the device's shadow in step before both change
+    {  // the mirror alone takes these deltas (stale device, or a new column reloads it): in step first
+      bool known = !dirty && device;
+      for (auto& u : us)
+        for (auto& kv : u.single) known = known && colByName.count(kv.first);
+      if (!known) flush_mirror();
+    }
     std::vector<kueue_tas_delta> deltas;
     bool new_col = false;
     for (auto& u : us) {
@@ -1831,8 +1843,7 @@ class FlavorSnapshot {
       if (recolumn()) return 0;  // dirty: the next upload() takes the host mirror
     }
     if (!device || dirty || !ctx || deltas.empty()) return 0;
-    int rc = kueue_tas_snapshot_apply_deltas(ctx, deltas.data(), deltas.size(), nullptr);
-    if (!rc) rc = kueue_tas_snapshot_usage_mark(ctx);  // the mirror already has these deltas
+    int rc = kueue_tas_snapshot_apply_deltas_mirrored(ctx, deltas.data(), deltas.size());  // the mirror has them
     if (rc) err = std::string("apply deltas: ") + kueue_tas_last_error(ctx);
     return rc;
   }
@@ -4421,6 +4432,149 @@ int kueue_tas_host_preemption_search(kueue_tas_host* h, const char* podsets_json
   try {
     std::string out;
     int rc = preemption_search(h, kjson::parse(podsets_json), kjson::parse(candidates_json), &out);
+    if (rc) {
+      h->err = h->snap->err;
+      return rc;
+    }
+    *out_json = dup(out);
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+// Batched partial-admission search: PodSetReducer.Search
+// (pkg/scheduler/flavorassigner/podset_reducer.go:37-86, driven by
+// Scheduler.getInitialAssignments, scheduler.go:720-739) with the fits closure
+// reduced to its TAS part — Assign(nextCounts) scales each PodSet to its
+// count (flavorassigner.go:599-609), a count-0 PodSet sends no TAS request
+// (tas_flavorassigner.go:52-55), and the counts fit when
+// FindTopologyAssignmentsForWorkload reports no failure (:734-747).
+// sort.Search's decision tree is evaluated speculatively: from the current
+// interval [i, j) every probe of its next `depth` levels (at most `cap`
+// distinct counts vectors, each a workload evaluation against the same
+// snapshot) goes into ONE device batch, then the search walks those levels
+// on the results — the probes and the answer are exactly sort.Search's, for
+// any fits predicate, in ceil(log2(totalDelta + 1) / depth) batches.
+static int partial_admission_search(kueue_tas_host* h, const kjson::Node& podsets_doc, bool simulate_empty,
+                                    int32_t cap, std::string* out) {
+  FlavorSnapshot& s = *h->snap;
+  const std::vector<TASPodSetRequests> podsets = parse_podsets(podsets_doc);
+  const size_t n = podsets.size();
+  std::vector<int32_t> full(n), delta(n);
+  std::vector<char> tas(n, 1);
+  int32_t total = 0;
+  for (size_t i = 0; i < n; i++) {  // NewPodSetReducer (:37-53)
+    const kjson::Node& p = podsets_doc.items[i];
+    full[i] = podsets[i].count;
+    const kjson::Node* m = p.find("minCount");
+    delta[i] = full[i] - (m && !m->null() ? int32_t(m->i64()) : full[i]);
+    total += delta[i];
+    if (const kjson::Node* t = p.find("tas")) tas[i] = t->null() || t->b();
+  }
+  auto fill = [&](int64_t up) {  // fillPodSetSizesForSearchIndex (:55-62)
+    std::vector<int32_t> c(n);
+    for (size_t i = 0; i < n; i++) c[i] = full[i] - int32_t(int64_t(delta[i]) * up / int64_t(total));
+    return c;
+  };
+  int depth = 1;
+  while (depth < 20 && (int64_t(1) << (depth + 1)) - 1 <= int64_t(std::max(cap, 1))) depth++;
+  // index -> (fits, results); a batch's results view the device's entry
+  // regions, valid until the next batch: the walk after each batch emits them
+  std::unordered_map<int64_t, std::pair<bool, std::vector<PodSetResult>>> probed;
+  int64_t evals = 0, batches = 0, probes = 0;
+  double eval_ms = 0;
+  const double t0 = now_ms();
+  int64_t i = 0, j = int64_t(total) + 1, lastGood = 0;
+  std::string lastR;  // the last fitting probe's results, emitted
+  bool any = total != 0;  // totalDelta == 0: (nil, false) without a probe (:71-73)
+  while (any && i < j) {
+    // the next `depth` levels of sort.Search's decision tree from [i, j)
+    std::vector<int64_t> want;
+    std::vector<std::pair<int64_t, int64_t>> lvl{{i, j}};
+    for (int d = 0; d < depth && !lvl.empty(); d++) {
+      std::vector<std::pair<int64_t, int64_t>> next;
+      for (auto [a, b] : lvl) {
+        if (a >= b) continue;
+        const int64_t hh = int64_t(uint64_t(a + b) >> 1);
+        if (!probed.count(hh)) want.push_back(hh);
+        next.push_back({hh + 1, b});  // !f(h)
+        next.push_back({a, hh});      // f(h)
+      }
+      lvl = std::move(next);
+    }
+    std::vector<Workload> wls;
+    std::vector<int64_t> of;
+    for (int64_t hh : want) {
+      const std::vector<int32_t> cur = fill(hh);
+      Workload w;
+      for (size_t k = 0; k < n; k++)
+        if (tas[k] && cur[k] != 0) {
+          w.podsets.push_back(podsets[k]);
+          w.podsets.back().count = cur[k];
+        }
+      if (w.podsets.empty()) {  // nothing for TAS to place: the TAS part fits
+        probed[hh] = {true, {}};
+        continue;
+      }
+      wls.push_back(std::move(w));
+      of.push_back(hh);
+    }
+    if (!wls.empty()) {
+      Evaluator ev{&s};
+      std::vector<std::vector<PodSetResult>> results;
+      const double te = now_ms();
+      int rc = ev.run(wls, simulate_empty, &results);
+      if (rc) return rc;
+      eval_ms += now_ms() - te;
+      batches++;
+      evals += int64_t(wls.size());
+      for (size_t q = 0; q < wls.size(); q++) {
+        bool f = true;
+        for (auto& r : results[q]) f = f && r.reason.empty();  // TASAssignmentsResult.Failure() (:384-391)
+        probed[of[q]] = {f, std::move(results[q])};
+      }
+    }
+    // sort.Search over the probed levels (:76-84)
+    while (i < j) {
+      const int64_t hh = int64_t(uint64_t(i + j) >> 1);
+      auto it = probed.find(hh);
+      if (it == probed.end()) break;  // beyond this batch's levels
+      probes++;
+      if (it->second.first) {
+        lastGood = hh;
+        lastR.clear();
+        emit_results(lastR, s, it->second.second);
+        j = hh;
+      } else {
+        i = hh + 1;
+      }
+    }
+  }
+  const bool found = any && i == lastGood;  // (:85)
+  *out = std::string("{\"found\":") + (found ? "true" : "false") + ",\"counts\":";
+  if (!found) {
+    *out += "null,\"results\":null";
+  } else {
+    const std::vector<int32_t> c = fill(lastGood);
+    *out += "[";
+    for (size_t k = 0; k < n; k++) *out += (k ? "," : "") + std::to_string(c[k]);
+    *out += "],\"results\":" + lastR;
+  }
+  *out += ",\"probes\":" + std::to_string(probes) + ",\"evaluations\":" + std::to_string(evals) +
+          ",\"batches\":" + std::to_string(batches) + ",\"profileMs\":{\"evaluate\":" + std::to_string(eval_ms) +
+          ",\"search\":" + std::to_string(now_ms() - t0) + "}}";
+  return 0;
+}
+
+int kueue_tas_host_partial_admission_search(kueue_tas_host* h, const char* podsets_json, int32_t simulate_empty,
+                                            int32_t max_batch, char** out_json) {
+  if (!h || !h->snap || !h->err.empty() || !out_json || !podsets_json) return KUEUE_TAS_EINVAL;
+  try {
+    std::string out;
+    int rc = partial_admission_search(h, kjson::parse(podsets_json), simulate_empty != 0,
+                                      max_batch > 0 ? max_batch : 1023, &out);
     if (rc) {
       h->err = h->snap->err;
       return rc;

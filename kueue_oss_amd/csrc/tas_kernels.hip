@@ -5437,14 +5437,21 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
 }
 
 // Snapshot delta: tas_usage[col][leaf] += delta (updateTASUsage :257-293)
+// With `shadow` set the host mirror already holds these deltas (a host-layer
+// AddUsage / RemoveUsage): the mirror's shadow takes them too, so the next
+// diff (usage_diff_kernel) reports only what the device applied on its own.
 __global__ void apply_deltas_kernel(int64_t* tas_usage, uint32_t* usage_present, int N, const kueue_tas_delta* d,
-                                    int n) {
+                                    int n, int64_t* shadow, uint32_t* pshadow) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   kueue_tas_delta x = d[i];
-  atomicAdd(reinterpret_cast<unsigned long long*>(&tas_usage[int64_t(x.col) * N + x.leaf]),
-            (unsigned long long)(uint64_t(x.delta)));
+  const int64_t at = int64_t(x.col) * N + x.leaf;
+  atomicAdd(reinterpret_cast<unsigned long long*>(&tas_usage[at]), (unsigned long long)(uint64_t(x.delta)));
   atomicOr(&usage_present[x.leaf], 1u << x.col);
+  if (shadow) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&shadow[at]), (unsigned long long)(uint64_t(x.delta)));
+    atomicOr(&pshadow[x.leaf], 1u << x.col);
+  }
 }
 
 // Leaf free-capacity rows replaced after non-TAS pod events

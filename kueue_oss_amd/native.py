@@ -66,7 +66,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
-    "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes",
+    "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
+    "kueue_tas_host_partial_admission_search",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -187,6 +188,9 @@ def _bind(lib):
     lib.kueue_tas_host_v1beta2_last.restype = c.c_int
     lib.kueue_tas_host_preemption_search.argtypes = [c.c_void_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.kueue_tas_host_preemption_search.restype = c.c_int
+    lib.kueue_tas_host_partial_admission_search.argtypes = [c.c_void_p, c.c_char_p, c.c_int32, c.c_int32,
+                                                            c.POINTER(c.c_void_p)]
+    lib.kueue_tas_host_partial_admission_search.restype = c.c_int
     lib.kueue_tas_host_update_nodes.argtypes = [c.c_void_p, c.c_char_p, c.POINTER(c.c_int32)]
     lib.kueue_tas_host_update_nodes.restype = c.c_int
     lib.kueue_tas_host_update_pods.argtypes = [c.c_void_p, c.c_char_p]
@@ -320,6 +324,14 @@ class TASFlavorSnapshot:
         that list already JSON-encoded (bytes)."""
         enc = candidates if isinstance(candidates, bytes) else json.dumps(candidates).encode()
         return self._json_call(self._lib.kueue_tas_host_preemption_search, podsets, enc)
+
+    def partial_admission_search(self, podsets: list, simulate_empty: bool = False, max_batch: int = 0) -> dict:
+        """PodSetReducer.Search (pkg/scheduler/flavorassigner/podset_reducer.go:37-86)
+        over the TAS fit: PodSets carry ``count`` and optional ``minCount``
+        (and ``tas: False`` for a PodSet outside TAS); sort.Search's decision
+        tree is evaluated ``max_batch`` probes per device batch (0: 1023)."""
+        return self._json_call(self._lib.kueue_tas_host_partial_admission_search, podsets,
+                               1 if simulate_empty else 0, int(max_batch))
 
     # ---- v1beta2 wire format (pkg/util/tas/tas_assignment.go) ----
     def _json_call(self, fn, payload, *extra):

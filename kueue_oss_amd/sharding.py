@@ -93,7 +93,9 @@ def gather_assignments(quads, world: int, dist, device=None, to_host: bool = Tru
     (every rank sees every length, so all agree).  Returns the concatenated
     int32 numpy array, ranks in order (every rank receives all of it), or with
     ``to_host=False`` the device block and the per-rank lengths (no
-    device-to-host copy of the block: a rank that does not admit)."""
+    device-to-host copy of the block: a rank that does not admit).  That
+    block is the exchange's reused receive buffer: it is valid until the next
+    exchange (clone it to keep it); the lengths are a copy."""
     import numpy as np
     import torch
 
@@ -110,7 +112,8 @@ def gather_assignments(quads, world: int, dist, device=None, to_host: bool = Tru
             dist.all_gather_into_tensor(recv, send)
         else:
             dist.all_gather(list(recv.unbind(0)), send)
-        lens = recv[:, 0].cpu().numpy()  # (synchronizes: the staging row is free again)
+        # (synchronizes: the staging row is free again); a copy, never a view of the reused block
+        lens = np.array(recv[:, 0].cpu().numpy(), copy=True)
         if int(lens.max()) <= cap:
             if not to_host:
                 return recv, lens

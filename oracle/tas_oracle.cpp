@@ -1836,6 +1836,72 @@ static void emit_results(std::string& out, const std::vector<PodSetResult>& rs) 
   out += "]";
 }
 
+// PodSetReducer.Search (pkg/scheduler/flavorassigner/podset_reducer.go:37-86)
+// with the fits closure of Scheduler.getInitialAssignments (scheduler.go:
+// 720-739) reduced to its TAS part: flvAssigner.Assign(nextCounts) scales every
+// PodSet to its count (flavorassigner.go:599-609), WorkloadsTopologyRequests
+// skips a count-0 PodSet (tas_flavorassigner.go:52-55) and the assignment
+// fits when FindTopologyAssignmentsForWorkload has no failure
+// (flavorassigner.go:734-747).  `tas[i]` false: a PodSet outside TAS (its
+// counts take part in the index arithmetic only).  The probes are exactly
+// sort.Search's (sort.go: h = int(uint(i+j) >> 1)).
+struct ReducerResult {
+  bool found = false;
+  std::vector<int32_t> counts;
+  std::vector<PodSetResult> results;
+  int64_t probes = 0;
+};
+static ReducerResult podset_reducer_search(Snapshot& snap, const std::vector<PodSetRequest>& podsets,
+                                           const std::vector<int32_t>& minCounts, const std::vector<bool>& tas,
+                                           bool simulateEmpty) {
+  ReducerResult out;
+  const size_t n = podsets.size();
+  std::vector<int32_t> full(n), deltas(n);
+  int32_t totalDelta = 0;
+  for (size_t i = 0; i < n; i++) {  // NewPodSetReducer (:37-53)
+    full[i] = podsets[i].count;
+    deltas[i] = podsets[i].count - minCounts[i];
+    totalDelta += deltas[i];
+  }
+  if (totalDelta == 0) return out;  // (:71-73)
+  auto fill = [&](int32_t up) {     // fillPodSetSizesForSearchIndex (:55-62)
+    std::vector<int32_t> c(n);
+    for (size_t i = 0; i < n; i++) c[i] = full[i] - int32_t(int64_t(deltas[i]) * int64_t(up) / int64_t(totalDelta));
+    return c;
+  };
+  int lastGoodIdx = 0;
+  std::vector<PodSetResult> lastR;
+  // sort.Search(int(totalDelta)+1, f) (:76-84)
+  int i = 0, j = int(totalDelta) + 1;
+  while (i < j) {
+    const int h = int(unsigned(i + j) >> 1);
+    const std::vector<int32_t> cur = fill(int32_t(h));
+    std::vector<PodSetRequest> reqs;
+    for (size_t k = 0; k < n; k++)
+      if (tas[k] && cur[k] != 0) {
+        reqs.push_back(podsets[k]);
+        reqs.back().count = cur[k];
+      }
+    out.probes++;
+    std::vector<PodSetResult> rs = reqs.empty() ? std::vector<PodSetResult>{}
+                                                : snap.find_topology_assignments_for_flavor(reqs, simulateEmpty);
+    bool f = true;
+    for (auto& r : rs) f = f && r.reason.empty();  // TASAssignmentsResult.Failure() (:384-391)
+    if (f) {
+      lastGoodIdx = h;
+      lastR = std::move(rs);
+    }
+    if (!f) i = h + 1;
+    else j = h;
+  }
+  out.found = i == lastGoodIdx;  // (:85)
+  if (out.found) {
+    out.counts = fill(int32_t(lastGoodIdx));
+    out.results = std::move(lastR);
+  }
+  return out;
+}
+
 static char* dup_out(const std::string& s) {
   char* p = static_cast<char*>(malloc(s.size() + 1));
   memcpy(p, s.data(), s.size() + 1);
@@ -1934,6 +2000,8 @@ int tas_oracle_eval_workloads(const char* snapshot_json, const char* workloads_j
 //   {"op": "fits", "usage": [{values, singlePodRequests, count}...]} -> bool
 //   {"op": "add" | "remove", "usage": [...]}                         -> null
 //   {"op": "admit", "usage": [...]}: fits, then add when it fits     -> bool
+//   {"op": "partialAdmission", "podSets": [... "minCount", "tas"], "simulateEmpty": bool}
+//       -> {"found", "counts", "results", "probes"} (podset_reducer_search)
 // applied in order; returns {"results": [one entry per op]}.
 int tas_oracle_session(const char* snapshot_json, const char* ops_json, char** out_json) {
   using namespace oracle;
@@ -1972,6 +2040,29 @@ int tas_oracle_session(const char* snapshot_json, const char* ops_json, char** o
       } else if (kind == "add" || kind == "remove") {
         snap->update_usage(parse_usage(op.at("usage")), kind == "add");
         out += "null";
+      } else if (kind == "partialAdmission") {  // PodSetReducer.Search over the TAS fit
+        const ojson::Value& ps = op.at("podSets");
+        auto reqs = parse_podsets(ps);
+        std::vector<int32_t> minc;
+        std::vector<bool> tas;
+        for (auto& p : ps.a) {
+          auto m = p.get("minCount");
+          minc.push_back(m && !m->is_null() ? int32_t(m->as_int()) : int32_t(p.at("count").as_int()));
+          auto t = p.get("tas");
+          tas.push_back(!(t && !t->is_null() && !t->as_bool()));
+        }
+        auto sim = op.get("simulateEmpty");
+        ReducerResult r = podset_reducer_search(*snap, reqs, minc, tas, sim && sim->as_bool());
+        out += std::string("{\"found\":") + (r.found ? "true" : "false") + ",\"counts\":";
+        if (!r.found) {
+          out += "null,\"results\":null";
+        } else {
+          out += "[";
+          for (size_t k = 0; k < r.counts.size(); k++) out += (k ? "," : "") + std::to_string(r.counts[k]);
+          out += "],\"results\":";
+          emit_results(out, r.results);
+        }
+        out += ",\"probes\":" + std::to_string(r.probes) + "}";
       } else {
         throw std::runtime_error("unknown op " + kind);
       }

@@ -313,6 +313,14 @@ inline hipError_t hipEventSynchronize(hipEvent_t e) {  // the recording stream u
 }
 enum hipFuncAttribute { hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
 inline hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int) { return hipSuccess; }  // LDS is host memory here
+struct hipFuncAttributes {
+  size_t sharedSizeBytes;
+};
+// static LDS: the hardware's budget is what the kernels' checks reason about (a fixed figure here)
+inline hipError_t hipFuncGetAttributes(hipFuncAttributes* a, const void*) {
+  a->sharedSizeBytes = 8 * 1024;
+  return hipSuccess;
+}
 inline hipError_t hipEventDestroy(hipEvent_t e) { delete e; return hipSuccess; }
 
 // kernel arguments are captured by value: the launch may run after the caller's locals are gone

@@ -106,6 +106,89 @@ def test_admit_then_rebuild_on_gpu(splice):
     _admit_then_rebuild(lambda d: TASFlavorSnapshot(d), splice)
 
 
+def _admit_relayout_apply(make_snap):
+    """Replica deltas after a relayout: an admission leaves the
+    device ahead of the host mirror; a node update with a new label key makes
+    the device layout stale (the next upload reloads from the mirror); the
+    negated admission deltas then arrive as another rank's delta list
+    (kueue_tas_host_apply_deltas) and must survive the reload on every entry
+    the admission touched.  The usage is back to the document's, so the
+    oracle is the document with the node's new label."""
+    import copy
+
+    snap_doc, wls = synth.config_c2(n_workloads=24, shape=(2, 2, 4, 8))
+    snap = make_snap(snap_doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    before = snap.last_results()
+    admitted, deltas = snap.admit(snap.last_assignments())
+    assert len(deltas) and admitted[:, 1].any()
+    want_doc = copy.deepcopy(snap_doc)
+    node = want_doc["nodes"][3]
+    node["labels"]["example.com/brand-new-label"] = "x"
+    assert snap.update_nodes([copy.deepcopy(node)]) is False  # in place, the device layout is stale
+    neg = deltas.copy()
+    neg["delta"] = -neg["delta"]
+    snap.apply_deltas(neg)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    snap.close()
+    want, _ = oracle_lib.eval_workloads(want_doc, wls, threads=4)
+    assert got == want
+    assert got == before  # the label changes no request's fit
+
+
+def test_emulated_admit_relayout_apply(emu_lib):  # noqa: F811
+    _admit_relayout_apply(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+
+
+@pytest.mark.gpu
+def test_admit_relayout_apply_on_gpu():
+    _admit_relayout_apply(lambda d: TASFlavorSnapshot(d))
+
+
+def _usage_updates_after_admission(make_snap):
+    """AddUsage / RemoveUsage (kueue_tas_host_update_usage) right after a
+    device admission: the admission stays pending on the mirror (no diff of
+    the whole usage), the update reaches the device, the mirror and its
+    shadow; a later reader (free capacity) sees both.  Against the oracle
+    session: admit, add a record list, remove another, find."""
+    snap_doc, wls = synth.config_c2(n_workloads=24, shape=(2, 2, 4, 8))
+    snap = make_snap(snap_doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    b1 = snap.last_results()
+    admitted, _ = snap.admit(snap.last_assignments())
+    ok = [i for i, a in admitted.tolist() if a]
+    assert len(ok) >= 3
+    add = synth.usage_records(wls[ok[0]], b1[ok[0]])
+    rem = synth.usage_records(wls[ok[1]], b1[ok[1]])
+    snap.add_usage(add)
+    snap.remove_usage(rem)
+    got = snap.find_topology_assignments_for_workloads(wls)
+    free = snap.serialize_free_capacity_per_domain()
+    lib = snap._lib
+    snap.close()
+    ops = [{"op": "add", "usage": synth.usage_records(wls[i], b1[i])} for i in ok]
+    ops += [{"op": "add", "usage": add}, {"op": "remove", "usage": rem}]
+    ops += [{"op": "find", "podSets": w} for w in wls]
+    assert got == oracle_lib.session(snap_doc, ops)[len(ok) + 2:]
+    # the host mirror equals one that took the same usage through AddUsage only
+    ref = TASFlavorSnapshot(snap_doc, lib=lib)
+    for op in ops[:len(ok) + 2]:
+        (ref.add_usage if op["op"] == "add" else ref.remove_usage)(op["usage"])
+    assert free == ref.serialize_free_capacity_per_domain()
+    ref.close()
+
+
+def test_emulated_usage_updates_after_admission(emu_lib):  # noqa: F811
+    _usage_updates_after_admission(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+
+
+@pytest.mark.gpu
+def test_usage_updates_after_admission_on_gpu():
+    _usage_updates_after_admission(lambda d: TASFlavorSnapshot(d))
+
+
 def _admit_batch(make, n=64, shape=(2, 2, 4, 8), huge_memory=False):
     """kueue_tas_host_admit over one evaluated batch (admit_fit0_kernel +
     admit_kernel: phase-1 rejections, re-checks of workloads whose leaves an
