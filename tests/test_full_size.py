@@ -78,6 +78,36 @@ def test_c4_whole_batch_on_gpu():
     assert sum(1 for r in got if all(not p["reason"] for p in r)) > 100
 
 
+@pytest.mark.timeout(900)
+def test_c5_whole_batch_on_gpu(capfd):
+    """A whole 1,024-workload C5 device batch at 1,048,576 nodes (the C2 mix:
+    required / preferred BestFit and unconstrained LeastFreeCapacity) against
+    the 16-thread oracle, every evaluation (tas_flavor_snapshot.go:519-594)."""
+    global _CAPFD
+    _CAPFD = capfd
+    stop = threading.Event()
+    threading.Thread(target=_heartbeat, args=(stop,), daemon=True).start()
+    try:
+        doc, wls = synth.config_c5(n_workloads=1024)
+        assert len(doc["nodes"]) == 1 << 20
+        bf = sum(1 for w in wls if w[0]["topologyRequest"] and not w[0]["topologyRequest"].get("unconstrained"))
+        assert bf > 300 and len(wls) - bf > 50
+        snap = TASFlavorSnapshot(doc, max_batch=1024)
+        snap.compile(wls)
+        snap.run_compiled(flags=FULL)
+        got = snap.last_results()
+        snap.close()
+        _progress("device batch done; oracle (16 threads)")
+        want, secs = oracle_lib.eval_workloads(doc, wls, threads=16)
+        mism = [i for i in range(len(wls)) if got[i] != want[i]]
+        assert mism == [], (len(mism), mism[:8])
+        _progress(f"oracle agrees on all {len(wls)} evaluations ({secs:.0f}s)")
+        assert sum(1 for r in got if all(not p["reason"] for p in r)) > 500
+    finally:
+        stop.set()
+        _CAPFD = None
+
+
 # ---- C5 at its stated size: 100,000 workloads sharded over two ranks on one GPU ----
 C5_WORKLOADS = 100_000
 C5_BATCH = 1024  # device batch per rank per round
