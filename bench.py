@@ -189,10 +189,11 @@ def main():
     def step(flags=FULL, gather=True):
         snap.run_compiled(flags=flags)
         if dist is not None and gather:
-            # RCCL all-gather of every rank's full assignments (quads) over xGMI;
-            # rank 0, the admitting rank, copies the gathered block to its host
-            # (admit_round's exchange), the other ranks leave it on the device
-            gather_assignments(snap.last_assignments(), world, dist, device, to_host=rank == 0)
+            # RCCL all-gather of every rank's full assignments (quads) over xGMI.
+            # The gathered block stays on the device on every rank: the step
+            #  ends with the exchange; the admission that consumes it
+            # is timed separately (`admission`, which copies it to rank 0's host)
+            gather_assignments(snap.last_assignments(), world, dist, device, to_host=False)
 
     # the snapshot document and generated workloads are long-lived: keep them
     # out of the collector's scans during the timed loop
@@ -441,10 +442,10 @@ def widened_rows(a, snap, snap_doc, mine, synth):
     for c in cands:
         snap.remove_usage(c)
     # batched partial-admission search (podset_reducer.go:37-86): the first
-    # workload whose full counts x 64 do not fit, every PodSet down to 1 pod
+    # workload whose full counts x 8 do not fit, every PodSet down to 1 pod
     pa = None
     for w in mine[:64]:
-        big = [dict(p, count=p.get("count", 1) * 64, minCount=1) for p in w]
+        big = [dict(p, count=p.get("count", 1) * 8, minCount=1) for p in w]
         if any(r["reason"] for r in snap.find_topology_assignments_for_flavor(big)):
             snap.partial_admission_search(big)
             t0 = time.perf_counter()

@@ -53,6 +53,12 @@ int64_t kueue_tas_last_fill_profile(kueue_tas_ctx* ctx, int32_t* out, size_t n);
  * select results, [4] entry packing + D2H, [5] copy-out; within [0]: [6] the
  * validation pass, [7] the records + class-hash pass.  Copies min(n, 8). */
 int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
+/* Host timeline of the last device chunk (ms since its start) at 20 fixed
+ * points: validate, staging layout, records, table copies, class merge, class
+ * members, chunk order, member lists, classes done, buffers, fill records,
+ * upload, fill launches, roll-up launches, LFC branch, select launch, D2H
+ * enqueued, synchronized, offsets (tools/probe_host.py --trace). */
+int kueue_tas_last_host_trace(kueue_tas_ctx* ctx, double* ms, int n);
 
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with

@@ -314,6 +314,7 @@ struct kueue_tas_ctx {
   std::vector<int64_t> ent_strided_off;  // their region offsets (pairs) in ent_host
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
+  double trace[24] = {};  // the last chunk's host timeline (wall ms at fixed points, kueue_tas_last_host_trace)
   double host_ms[8] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out, [6] of compile:
                            // validation pass, [7] of compile: records + hashes pass
   int64_t last_stats[4] = {0, 0, 0, 0};  // fill evals, leaf-partial evals, fill launches, staged columns
@@ -1370,6 +1371,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     c->host_ms[k] += t - tm;
     tm = t;
   };
+  auto trace = [&](int k) { c->trace[k] = wall_ms(); };
+  trace(0);
   // ---- per-request host work over the worker pool: validation and term
   // counts (pass A), then the device records, division magic and the class
   // hashes (pass B); errors are reported for the lowest request index ----
@@ -1449,6 +1452,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
   c->host_ms[6] += wall_ms() - tm;
+  trace(1);
   for (size_t i = 0; i < n; i++) toff[i + 1] += toff[i];
   const size_t nterms = size_t(toff[n]);
   int maxt = 1;
@@ -1610,6 +1614,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     pc.rep.clear();
     pc.next.clear();
   }
+  trace(2);
   // ---- compile requests to device form (magic numbers) ----
   const double t_b = wall_ms();
   pool.run_static(n, [&](size_t i0, size_t i1) {
@@ -1700,11 +1705,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
   c->host_ms[7] += wall_ms() - t_b;
+  trace(3);
   if (taint_table_len) memcpy(hs + o_taint, taint_table, taint_table_len * 4);
   if (num_assumed) memcpy(hs + o_assumed, assumed, num_assumed * sizeof(kueue_tas_assumed));
   if (num_aff) memcpy(hs + o_aff, aff, num_aff * sizeof(kueue_tas_affinity_req));
   if (num_aff_vals) memcpy(hs + o_affv, aff_vals, num_aff_vals * 4);
   lap(0);
+  trace(4);
 
   // Phase-1 classes: evals with identical phase-1 inputs (request terms,
   // masks, overlay, slice parameters) get identical counters; phase 1 runs
@@ -1789,6 +1796,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     for (size_t t = 0; t < nparts; t++)
       for (size_t i = ktas_pool::HostPool::part_begin(n, t, nparts); i < ktas_pool::HostPool::part_begin(n, t + 1, nparts); i++)
         cls_of[i] = part_map[part_base[t] + size_t(req_local_cls[i])];
+    trace(5);
     const int ncls = int(cls_rep.size());
     // representative: the first fast-LFC member if any (its class gets an LFC table slot)
     std::vector<int32_t>& rep = c->cls_fastrep;
@@ -1825,6 +1833,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         h_leafsel[nleafsel++] = int32_t(i);
       }
     }
+    trace(6);
     // fill chunks: classes ordered by (base signature, signature), <= kEvalsPerFillBlock
     // per chunk, one base signature each (the leaf's remaining capacity is
     // shared); a run of one signature inside a chunk shares the CountIn
@@ -1862,6 +1871,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       if (small(sa) != small(sb)) return !small(sa);
       return sa < sb;
     });
+    trace(7);
     for (int k = 0; k < ncls; k++) h_fill[k] = rep[size_t(order[size_t(k)])];
     nfill = ncls;
     {  // members other than the rep, grouped by fill position (stats written by the reduce)
@@ -1885,6 +1895,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       for (int k = 0; k < ncls; k++)
         if (slot_of[size_t(k)] >= 0) h_lrep[slot_of[size_t(k)]] = pos[size_t(k)];
     }
+    trace(8);
     int32_t* h_frun = reinterpret_cast<int32_t*>(hs + o_frun);
     // a signature with at least half a chunk of classes gets chunks of its
     // own (one run: CountIn before the eval loop); the smaller ones of a base
@@ -1927,6 +1938,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     }
   }
   lap(1);
+  trace(9);
   c->chunk_rep.assign(h_rep, h_rep + n);
   c->chunk_leader.resize(n);
   for (size_t i = 0; i < n; i++) c->chunk_leader[i] = (hev[i].flags & KUEUE_TAS_F_LEADER) ? 1 : 0;
@@ -2016,6 +2028,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     for (size_t i = 0; i < size_t(nfill) * kMaxLevels; i++) t[i] = INT32_MIN;
     for (size_t i = 0; i < size_t(nfill); i++) t[n * kMaxLevels + i] = 0;
   }
+  trace(10);
   // fill_pair_kernel's per-position records in fill order (FillPos)
   {
     FillPos* fp = reinterpret_cast<FillPos*>(hs + o_fpos);
@@ -2105,6 +2118,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     for (size_t i = 0; i < n; i++) c->chunk_alias[i] = uint8_t(fp[c->chunk_rep[i]].p.ss_alias);
     for (int k = 0; k < nfill; k++) c->last_alias_fills += fp[k].p.ss_alias;
   }
+  trace(11);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_stage.p, hs, o_fpos + size_t(nfill) * sizeof(FillPos), hipMemcpyHostToDevice, c->stream));
   // the select path's descriptor (g_select_snap), ordered before both select
@@ -2125,6 +2139,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       }
     }
   }
+  trace(12);
   if (!lds_stats) HIPCHK(c, hipMemsetAsync(d_stats, 0, stats_len * 4, c->stream));
   uint8_t* ds = c->d_stage.p;
   DevBatch b{};
@@ -2358,6 +2373,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       HIPCHK(c, hipGetLastError());
     }
   }
+  trace(13);
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   // ExclusionStats on stream3 beside the roll-up / select, joined before the
   // D2H: the reduce of the fill's per-block partials (counted inside the
@@ -2423,6 +2439,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     hipLaunchKernelGGL(rollup_tail_kernel, dim3(unsigned(nfill)), dim3(256), 0, c->stream, s, b, tail_top);
     HIPCHK(c, hipGetLastError());
   }
+  trace(14);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   if (npairs && !b.nstat) {  // exclusion stats of the class rep to the other members (global-atomic stats)
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
@@ -2454,6 +2471,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->evl[1], c->stream2));
   }
+  trace(15);
   // leaf-level selection partials (non-fast evals whose requested level is the leaf level)
   if (nleafsel && s.N > 0) {
     c->last_stats[1] += nleafsel;
@@ -2469,14 +2487,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
                        size_t(waves) * size_t(bf_wave_lds), c->stream, s, b, d_bf, nbf);
     HIPCHK(c, hipGetLastError());
   }
+  trace(16);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
   if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
   if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
+  trace(17);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   lap(3);
+  trace(18);
   int32_t need = 0;
   for (size_t i = 0; i < n; i++) need = std::max(need, c->res_out_h[i].num_workers + c->res_out_h[i].num_leaders);
   if (need > entry_cap) return 1;  // caller grows entry_cap and re-runs this chunk
@@ -2487,6 +2508,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   c->ent_used += size_t(n) * size_t(entry_cap) * 2;
   c->ent_stride = entry_cap;
   lap(4);
+  trace(19);
   memcpy(out, c->res_out_h, n * sizeof(kueue_tas_eval_out));
   {  // nodeSelector / affinity exclusions: counted beside select (stream3), read from the stats region after the join
     const int32_t* sel = c->res_stats_h + n * nt + n * size_t(s.R);
@@ -2723,6 +2745,12 @@ int64_t kueue_tas_last_fill_profile(kueue_tas_ctx* c, int32_t* out, size_t n) {
 int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   if (!c || !ticks) return KUEUE_TAS_EINVAL;
   for (size_t i = 0; i < n * P_NCAT; i++) ticks[i] = i < c->last_prof.size() ? c->last_prof[i] : 0;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_last_host_trace(kueue_tas_ctx* c, double* ms, int n) {  // ms since the chunk's start, [0, 20)
+  if (!c || !ms) return KUEUE_TAS_EINVAL;
+  for (int k = 0; k < n && k < 20; k++) ms[k] = c->trace[k] - c->trace[0];
   return KUEUE_TAS_OK;
 }
 

@@ -67,7 +67,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
     "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
-    "kueue_tas_host_partial_admission_search",
+    "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
