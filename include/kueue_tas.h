@@ -222,6 +222,11 @@ typedef struct {
  * round-4 path) instead of once per leaf category and wave (test knob: both
  * paths must agree) */
 #define KUEUE_TAS_CFG_NO_CATEGORY_FILL 128
+/* test knob: the speculative merge of the host parts' phase-1 classes takes
+ * every class hash as equal, so its exact verification (while the device
+ * runs) fails and the chunk re-runs with the exact merge: the collision path
+ * must give the same results */
+#define KUEUE_TAS_CFG_CLASS_COLLIDE 256
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

@@ -59,6 +59,10 @@ int kueue_tas_last_host_times(kueue_tas_ctx* ctx, double* ms, int n);
  * upload, fill launches, roll-up launches, LFC branch, select launch, D2H
  * enqueued, synchronized, offsets (tools/probe_host.py --trace). */
 int kueue_tas_last_host_trace(kueue_tas_ctx* ctx, double* ms, int n);
+/* Device chunks re-run with the exact class merge after the speculative
+ * merge's verification failed (a 64-bit class hash collision, or
+ * KUEUE_TAS_CFG_CLASS_COLLIDE), over the context's lifetime. */
+int64_t kueue_tas_merge_reruns(kueue_tas_ctx* ctx);
 
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with

@@ -124,6 +124,7 @@ struct FlatMap {
 struct alignas(64) PartClasses {  // one per host part, on cache lines of its own
   FlatMap head;
   std::vector<int32_t> rep, next;
+  std::vector<uint64_t> hcls, hsig;  // each local class's hashes, contiguous for the merge
 };
 
 // libdivide-style u64 magic for exact division by an invariant divisor d >= 1.
@@ -164,14 +165,17 @@ void compute_magic_uncached(uint64_t d, DevTerm* t) {
 }
 
 // the divisors of a batch repeat (a request shape per workload type): a
-// per-thread direct-mapped cache of the magic numbers
-void compute_magic(uint64_t d, DevTerm* t) {
-  struct Slot {
-    uint64_t d = 0, magic = 0;
-    uint8_t shift = 0, add = 0, pow2 = 0;
-  };
-  static thread_local Slot cache[256];
-  Slot& c = cache[(d * 0x9e3779b97f4a7c15ull) >> 56];
+// direct-mapped cache of the magic numbers per host part, kept in the
+// context (a thread_local here cost a __tls_get_addr call per term)
+struct MagicSlot {
+  uint64_t d = 0, magic = 0;
+  uint8_t shift = 0, add = 0, pow2 = 0;
+};
+struct alignas(64) MagicCache {
+  MagicSlot slot[256];
+};
+void compute_magic(uint64_t d, DevTerm* t, MagicCache& cache) {
+  MagicSlot& c = cache.slot[(d * 0x9e3779b97f4a7c15ull) >> 56];
   if (c.d != d) {
     compute_magic_uncached(d, t);
     c.d = d;
@@ -228,6 +232,7 @@ struct kueue_tas_ctx {
   // results of a batch, one D2H: out[n] | stats (taint | res | sel counts)
   DevBuf<uint8_t> d_res;
   HostBuf<uint8_t> h_res;
+  HostBuf<kueue_tas_eval_out> h_res2;  // the fast-LFC branch's own copy of the result headers (its D2H)
   kueue_tas_eval_out* res_out_h = nullptr;
   int32_t* res_stats_h = nullptr;
   DevBuf<uint64_t> d_scratch;
@@ -262,6 +267,7 @@ struct kueue_tas_ctx {
   // fast-LFC leaf tables (LfcJob, tas_internal.h)
   DevBuf<uint32_t> d_lfc_ch, d_lfc_cp, d_lfc_tot;
   DevBuf<uint64_t> d_lfc_ovs, d_lfc_ovtot;
+  DevBuf<uint8_t> d_lfc_u8;
   DevBuf<LfcJob> d_lfc_jobs;
   DevBuf<LfcItem> d_lfc_items;  // [0]: item count, then the items
   DevBuf<int32_t> d_prof;             // profiling build: [n][P_NCAT] select phase ticks
@@ -314,6 +320,10 @@ struct kueue_tas_ctx {
   std::vector<int64_t> ent_strided_off;  // their region offsets (pairs) in ent_host
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
+  std::vector<MagicCache> magic_cache;  // per host part (compute_magic)
+  bool exact_merge = false;  // the next chunk merges the parts' classes with exact compares (after a collision)
+  int64_t merge_reruns = 0;  // chunks re-run after a class hash collision
+  bool collide_test = false; // KUEUE_TAS_CFG_CLASS_COLLIDE
   double trace[24] = {};  // the last chunk's host timeline (wall ms at fixed points, kueue_tas_last_host_trace)
   double host_ms[8] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out, [6] of compile:
                            // validation pass, [7] of compile: records + hashes pass
@@ -370,6 +380,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->admit_window = (cfg->flags & KUEUE_TAS_CFG_SERIAL_ADMIT) == 0;
     c->fused_top = (cfg->flags & KUEUE_TAS_CFG_FUSED_TOP) != 0;
     c->cat_fill = (cfg->flags & KUEUE_TAS_CFG_NO_CATEGORY_FILL) == 0;
+    c->collide_test = (cfg->flags & KUEUE_TAS_CFG_CLASS_COLLIDE) != 0;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -403,9 +414,12 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     delete c;
     return nullptr;
   }
-  for (auto& e : c->ev) (void)hipEventCreate(&e);
-  for (auto& e : c->evl) (void)hipEventCreate(&e);
-  for (auto& e : c->evs) (void)hipEventCreate(&e);
+  // the batch's events order its streams and time its stages; the host never
+  // reads memory through them (it synchronizes the streams), so no system-scope
+  // release: ~1.4 us less device time per record (tools/micro/sync_cost.hip)
+  for (auto& e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  for (auto& e : c->evl) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  for (auto& e : c->evs) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return c;
 }
 
@@ -426,6 +440,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_counters.release();
   c->d_res.release();
   c->h_res.release();
+  c->h_res2.release();
   c->d_scratch.release();
   c->d_deltas.release();
   c->d_setfree.release();
@@ -456,6 +471,7 @@ void kueue_tas_ctx_destroy(kueue_tas_ctx* c) {
   c->d_lfc_tot.release();
   c->d_lfc_ovs.release();
   c->d_lfc_ovtot.release();
+  c->d_lfc_u8.release();
   c->d_lfc_jobs.release();
   c->d_lfc_items.release();
   c->d_prof.release();
@@ -969,9 +985,6 @@ static int apply_deltas_impl(kueue_tas_ctx* c, const kueue_tas_delta* deltas, si
                              const uint32_t* usage_present_or_null, bool mirrored) {
   if (!c || !c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
   HIPCHK(c, hipSetDevice(c->device));
-  for (size_t i = 0; i < n; i++)
-    if (deltas[i].leaf < 0 || deltas[i].leaf >= c->snap.N || deltas[i].col < 0 || deltas[i].col >= c->snap.R)
-      return fail(c, KUEUE_TAS_EINVAL, "delta out of range");
   if (n) {
     // the records through pinned staging: an async copy, no stream sync (the
     // launches that read the usage follow on the same stream); the previous
@@ -979,7 +992,23 @@ static int apply_deltas_impl(kueue_tas_ctx* c, const kueue_tas_delta* deltas, si
     if (c->ev_deltas) HIPCHK(c, hipEventSynchronize(c->ev_deltas));
     else HIPCHK(c, hipEventCreateWithFlags(&c->ev_deltas, hipEventDisableTiming));
     HIPCHK(c, c->h_deltas.reserve(n));
-    memcpy(c->h_deltas.p, deltas, n * sizeof(kueue_tas_delta));
+    // range check and copy in one pass (a whole batch's admission is ~16k
+    // records: over the host pool's static parts when large)
+    const int32_t N = c->snap.N, R = c->snap.R;
+    kueue_tas_delta* dst = c->h_deltas.p;
+    std::atomic<bool> bad{false};
+    auto check_copy = [&](size_t i0, size_t i1) {
+      bool ok = true;
+      for (size_t i = i0; i < i1; i++) {
+        const kueue_tas_delta x = deltas[i];
+        ok &= x.leaf >= 0 && x.leaf < N && x.col >= 0 && x.col < R;
+        dst[i] = x;
+      }
+      if (!ok) bad.store(true, std::memory_order_relaxed);
+    };
+    if (n >= 8192) ktas_pool::HostPool::get().run_static(n, check_copy);
+    else check_copy(0, n);
+    if (bad.load()) return fail(c, KUEUE_TAS_EINVAL, "delta out of range");
     HIPCHK(c, c->d_deltas.ensure(n));
     HIPCHK(c, hipMemcpyAsync(c->d_deltas.p, c->h_deltas.p, n * sizeof(kueue_tas_delta), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_deltas, c->stream));
@@ -1514,7 +1543,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       h ^= h >> 29;
     };
     add(uint64_t(uint32_t(e.slice_size)) | (uint64_t(uint32_t(e.slice_level)) << 32));
-    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++) add(uint64_t(uint32_t(e.ssal[l])));
+    for (int l = 0; l < s.L; l++) add(uint64_t(uint32_t(e.ssal[l])));  // no kernel reads a level >= L
     add(uint64_t(uint32_t(e.nsel)));
     add(uint64_t(uint32_t(e.dom_begin)) | (uint64_t(uint32_t(e.dom_end)) << 32));
     for (int k = 0; k < e.nsel; k++) add(uint64_t(uint32_t(e.sel_col[k])) | (uint64_t(uint32_t(e.sel_val[k])) << 32));
@@ -1568,7 +1597,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   auto same_mask = [&](const DevEval& x, const DevEval& y) {
     if (x.slice_size != y.slice_size || x.slice_level != y.slice_level || x.nsel != y.nsel) return false;
     if (x.dom_begin != y.dom_begin || x.dom_end != y.dom_end) return false;
-    for (int l = 0; l < KUEUE_TAS_MAX_LEVELS; l++)
+    for (int l = 0; l < s.L; l++)
       if (x.ssal[l] != y.ssal[l]) return false;
     for (int k = 0; k < x.nsel; k++)
       if (x.sel_col[k] != y.sel_col[k] || x.sel_val[k] != y.sel_val[k]) return false;
@@ -1613,16 +1642,24 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     pc.head.reset(ktas_pool::HostPool::part_begin(n, t + 1, nparts) - ktas_pool::HostPool::part_begin(n, t, nparts));
     pc.rep.clear();
     pc.next.clear();
+    pc.hcls.clear();
+    pc.hsig.clear();
   }
   trace(2);
   // ---- compile requests to device form (magic numbers) ----
   const double t_b = wall_ms();
+  static uint64_t prof_cyc[8][4];
+  for (auto& a : prof_cyc) for (auto& x : a) x = 0;
+  if (c->magic_cache.size() < nparts) c->magic_cache.resize(nparts);
   pool.run_static(n, [&](size_t i0, size_t i1) {
     const size_t ch = part_of(i0);
+    MagicCache& mc = c->magic_cache[ch];
+    uint64_t* pcy = prof_cyc[ch & 7];
     for (size_t i = i0; i < i1; i++) {
+      uint64_t tq0 = __builtin_ia32_rdtsc();
       const auto& r = *reqs[i];
-      DevEval& e = hev[i];
-      memset(&e, 0, sizeof e);
+      DevEval& e = hev[i];  // every field is assigned below (no memset of the record)
+      e.req_mask = e.lead_mask = 0;
       e.flags = r.flags;
       e.count = r.count;
       e.slice_size = r.slice_size;
@@ -1656,16 +1693,22 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
           if (cols[k] < 0 || cols[k] >= s.R || cols[k] <= prev) return -1;
           prev = cols[k];
           DevTerm& t = hterms[tp++];
-          memset(&t, 0, sizeof t);
           t.col = cols[k];
           t.val = vals[k];
           t.neg = vals[k] < 0;
           uint64_t mag = vals[k] < 0 ? (0ull - uint64_t(vals[k])) : uint64_t(vals[k]);
-          if (mag) compute_magic(mag, &t);
+          if (mag) {
+            compute_magic(mag, &t, mc);
+          } else {
+            t.magic = 0;
+            t.shift = t.add = t.pow2 = 0;
+          }
           *mask |= 1u << cols[k];
         }
         return 0;
       };
+      uint64_t tq1 = __builtin_ia32_rdtsc();
+      pcy[0] += tq1 - tq0;
       e.term_begin = int32_t(tp);
       e.nreq = r.num_req;
       if (add_terms(r.req_col, r.req_val, r.num_req, &e.req_mask)) {
@@ -1678,10 +1721,14 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         if (errs[ch].first == SIZE_MAX) errs[ch] = {i, "leader columns"};
         continue;
       }
+      uint64_t tq2 = __builtin_ia32_rdtsc();
+      pcy[1] += tq2 - tq1;
       h_sig[i] = sig_hash(e);
       h_cls[i] = h_sig[i] ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
       req_fast[i] = fast_lfc(e) ? 1 : 0;
       req_leaf[i] = e.requested_level == s.L - 1 ? 1 : 0;
+      uint64_t tq3 = __builtin_ia32_rdtsc();
+      pcy[2] += tq3 - tq2;
       // this part's classes (first member in request order), exact compare on a hash hit
       PartClasses& pc = c->part_cls[ch];
       int32_t k = -1;
@@ -1697,11 +1744,19 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         k = int32_t(pc.rep.size());
         pc.rep.push_back(int32_t(i));
         pc.next.push_back(*head);
+        pc.hcls.push_back(h_cls[i]);
+        pc.hsig.push_back(h_sig[i]);
         *head = k;
       }
       req_local_cls[i] = k;
+      pcy[3] += __builtin_ia32_rdtsc() - tq3;
     }
   });
+  if (getenv("KTAS_PROF_RECORDS")) {
+    for (size_t t = 0; t < nparts && t < 8; t++)
+      fprintf(stderr, "part %zu: fill %lu terms %lu hash %lu cls %lu (kcycles)\n", t, prof_cyc[t][0] / 1000,
+              prof_cyc[t][1] / 1000, prof_cyc[t][2] / 1000, prof_cyc[t][3] / 1000);
+  }
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
   c->host_ms[7] += wall_ms() - t_b;
@@ -1749,6 +1804,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     std::vector<int32_t>& sig_next = c->sig_next;
     cls_next.clear();
     sig_next.clear();
+    const uint64_t tm0 = __builtin_ia32_rdtsc();
     // the parts' classes merged in part order: a global class is numbered by
     // its first member, as a serial pass over the requests would number it
     std::vector<int32_t>& part_map = c->part_map;  // (part, local class) -> global class
@@ -1756,7 +1812,34 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     part_base.assign(nparts + 1, 0);
     for (size_t t = 0; t < nparts; t++) part_base[t + 1] = part_base[t] + c->part_cls[t].rep.size();
     part_map.assign(part_base[nparts], -1);
-    for (size_t t = 0; t < nparts; t++)
+    // Speculative merge: parts' classes with equal 64-bit hashes are taken
+    // as equal here, and verified exactly while the device runs (the exact
+    // compares read other cores' records: ~0.2 us each on the critical path);
+    // a hash collision re-runs the chunk with this exact merge (exact_merge)
+    if (!c->exact_merge) {
+      for (size_t t = 0; t < nparts; t++) {
+        const PartClasses& pc = c->part_cls[t];
+        for (size_t j = 0; j < pc.rep.size(); j++) {
+          int32_t* head = cls_head.find(c->collide_test ? 0 : pc.hcls[j]);
+          int32_t k = *head;
+          if (k < 0) {
+            k = int32_t(cls_rep.size());
+            cls_rep.push_back(pc.rep[j]);
+            cls_next.push_back(-1);
+            *head = k;
+            int32_t* shead = sig_head.find(c->collide_test ? 0 : pc.hsig[j]);
+            if (*shead < 0) {
+              *shead = int32_t(sig_rep.size());
+              sig_rep.push_back(pc.rep[j]);
+              sig_next.push_back(-1);
+            }
+            cls_sig.push_back(*shead);
+          }
+          part_map[part_base[t] + j] = k;
+        }
+      }
+    }
+    for (size_t t = 0; t < nparts && c->exact_merge; t++)
     for (size_t j = 0; j < c->part_cls[t].rep.size(); j++) {
       const size_t i = size_t(c->part_cls[t].rep[j]);
       const DevEval& e = hev[i];
@@ -1793,9 +1876,13 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       }
       part_map[part_base[t] + j] = k;
     }
+    const uint64_t tm1 = __builtin_ia32_rdtsc();
     for (size_t t = 0; t < nparts; t++)
       for (size_t i = ktas_pool::HostPool::part_begin(n, t, nparts); i < ktas_pool::HostPool::part_begin(n, t + 1, nparts); i++)
         cls_of[i] = part_map[part_base[t] + size_t(req_local_cls[i])];
+    if (getenv("KTAS_PROF_RECORDS"))
+      fprintf(stderr, "merge: part reps %zu, merge %lu kcyc, cls_of %lu kcyc\n", part_base[nparts], (tm1 - tm0) / 1000,
+              (__builtin_ia32_rdtsc() - tm1) / 1000);
     trace(5);
     const int ncls = int(cls_rep.size());
     // representative: the first fast-LFC member if any (its class gets an LFC table slot)
@@ -1969,6 +2056,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   const size_t res_bytes = res_off_stats + stats_len * 4;
   HIPCHK(c, c->d_res.ensure(res_bytes));
   HIPCHK(c, c->h_res.ensure(res_bytes));
+  HIPCHK(c, c->h_res2.ensure(n));
   kueue_tas_eval_out* d_out = reinterpret_cast<kueue_tas_eval_out*>(c->d_res.p);
   int32_t* d_stats = reinterpret_cast<int32_t*>(c->d_res.p + res_off_stats);
   c->res_out_h = reinterpret_cast<kueue_tas_eval_out*>(c->h_res.p);
@@ -2020,6 +2108,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
   HIPCHK(c, c->d_lfc_ovs.ensure(size_t(std::max(nslots * nchunks, 1))));
   HIPCHK(c, c->d_lfc_ovtot.ensure(size_t(std::max(nslots, 1))));
+  HIPCHK(c, c->d_lfc_u8.ensure(size_t(std::max(nslots, 1)) * size_t(std::max(nchunks, 1)) * kLfcChunk));
   const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
   HIPCHK(c, c->d_partials.ensure(size_t(std::max(nleafsel, 1)) * size_t(std::max(nblk, 1))));
 
@@ -2187,6 +2276,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.lfc_nslots = nslots;
   b.lfc_nchunks = nchunks;
   b.lfc_ch = c->d_lfc_ch.p;
+  b.lfc_u8 = c->d_lfc_u8.p;
   b.lfc_cp = c->d_lfc_cp.p;
   b.lfc_tot = c->d_lfc_tot.p;
   b.lfc_ovs = c->d_lfc_ovs.p;
@@ -2441,37 +2531,21 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   }
   trace(14);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  if (npairs && !b.nstat) {  // exclusion stats of the class rep to the other members (global-atomic stats)
+  const bool replicated = npairs && !b.nstat;
+  if (replicated) {  // exclusion stats of the class rep to the other members (global-atomic stats)
     hipLaunchKernelGGL(replicate_kernel, dim3(1, unsigned(npairs)), dim3(256), 0, c->stream, s, b, d_pairs, npairs);
     HIPCHK(c, hipGetLastError());
   }
-  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  // an event on the main stream costs ~8 us of its device time (rocprof
+  // kernel trace): recorded only when the fast-LFC branch waits for the
+  // replication, or for the stage profile
+  if (replicated || c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   const int32_t* d_fast = reinterpret_cast<const int32_t*>(ds + o_fast);
   const int32_t* d_bf = reinterpret_cast<const int32_t*>(ds + o_bf);
   const int waves = kSelectWaves;  // the kernel's per-wave LDS state is sized for this
   // per-wave LDS: the sort capacity (list_cap keys); the BestFit side also
   // holds lds_level_walk's candidates (kFinalWalkLds per wave)
   const int lfc_wave_lds = c->list_cap * 16, bf_wave_lds = std::max(lfc_wave_lds, kFinalWalkLds);
-  // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
-  // (after the stats replication); the main stream runs the BestFit side
-  if (nfast) {
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[2], 0));  // fill done
-    if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
-    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
-    HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[4], 0));  // stats replicated
-    b.wave_lds = lfc_wave_lds;
-    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves),
-                       size_t(waves) * size_t(lfc_wave_lds), c->stream2, s, b, d_fast, nfast);
-    HIPCHK(c, hipGetLastError());
-    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
-    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->evl[1], c->stream2));
-  }
-  trace(15);
   // leaf-level selection partials (non-fast evals whose requested level is the leaf level)
   if (nleafsel && s.N > 0) {
     c->last_stats[1] += nleafsel;
@@ -2489,13 +2563,66 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   }
   trace(16);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
-  if (nfast) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[1], 0));  // join the fast-LFC branch
-  if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // and the ExclusionStats branch
+  // fast-LFC branch on stream2: leaf tables (after the fill), select + emit
+  // (after the stats replication); the main stream runs the BestFit side.
+  // Enqueued after the BestFit select: that launch is on the batch's longest
+  // chain, and the host's calls for this branch would otherwise delay it
+  if (nfast) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[2], 0));  // fill done
+    if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
+    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
+    HIPCHK(c, hipGetLastError());
+    // the fast-LFC select reads the leaf counters and the LFC tables only
+    // (lfc_fast): it waits for the roll-up only when the replication wrote stats
+    if (replicated) HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[4], 0));
+    b.wave_lds = lfc_wave_lds;
+    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves),
+                       size_t(waves) * size_t(lfc_wave_lds), c->stream2, s, b, d_fast, nfast);
+    HIPCHK(c, hipGetLastError());
+    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
+    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->evl[1], c->stream2));
+    // the branch's result headers come back on its own stream: the host
+    // waits for both streams instead of the main stream waiting for this one
+    // (a cross-stream hand-off costs ~17 us of device time, sync_cost.hip)
+    HIPCHK(c, hipMemcpyAsync(c->h_res2.p, d_out, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream2));
+  }
+  trace(15);
+  if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // join the ExclusionStats branch
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_res.p, c->d_res.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
   lap(2);
   trace(17);
+  // the speculative class merge verified exactly while the device runs
+  bool merge_ok = true;
+  if (!c->exact_merge) {
+    const std::vector<int32_t>& cls_rep = c->cls_rep;
+    for (size_t t = 0; t < nparts && merge_ok; t++) {
+      const PartClasses& pc = c->part_cls[t];
+      for (size_t j = 0; j < pc.rep.size() && merge_ok; j++) {
+        const int32_t r = cls_rep[size_t(c->part_map[c->part_base[t] + j])];
+        if (r != pc.rep[j]) merge_ok = same_sig(hev[pc.rep[j]], hev[r]) && same_mask(hev[pc.rep[j]], hev[r]);
+      }
+    }
+    for (size_t k = 0; k < cls_rep.size() && merge_ok; k++) {
+      const int32_t g = c->sig_rep[size_t(c->cls_sig[k])];
+      if (g != cls_rep[k]) merge_ok = same_sig(hev[cls_rep[k]], hev[g]);
+    }
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (nfast) {
+    HIPCHK(c, hipStreamSynchronize(c->stream2));
+    const int32_t* hf = reinterpret_cast<const int32_t*>(hs + o_fast);
+    for (int k = 0; k < nfast; k++) c->res_out_h[hf[k]] = c->h_res2.p[hf[k]];
+  }
+  if (!merge_ok) {  // a 64-bit class hash collision: the caller re-runs the chunk with the exact merge
+    c->exact_merge = true;
+    c->merge_reruns++;
+    return 2;
+  }
   lap(3);
   trace(18);
   int32_t need = 0;
@@ -2545,6 +2672,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   if (nfast) (void)hipEventElapsedTime(&st[3], c->evl[0], c->evl[1]);
   if (b.nstat > 0) (void)hipEventElapsedTime(&st[2], c->evs[0], c->evs[1]);  // the concurrent stats branch
   (void)hipEventElapsedTime(&st[6], c->ev[0], c->ev[7]);
+  if (nfast) {  // the fast-LFC branch may end after the main stream (its results come back on its own stream)
+    float tl = 0.f;
+    (void)hipEventElapsedTime(&tl, c->ev[0], c->evl[1]);
+    st[6] = std::max(st[6], tl);
+  }
   for (int k = 0; k < KUEUE_TAS_NUM_STAGES; k++) stage_ms[k] += st[k];
   ms[0] += st[0];                    // fill (+ exclusion stats reduce)
   ms[1] += st[1] + st[2];            // roll-up + replication
@@ -2606,6 +2738,14 @@ int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* c, const kueue_tas_eval_req* const*
                           num_affinity, affinity_values, num_affinity_values, out + i0,
                           off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
+      if (rc == 2) {  // the speculative class merge met a hash collision: re-run with the exact merge
+        c->ent_used = keep;
+        c->ent_count.resize(i0);
+        c->last_ticks.resize(2 * i0);
+        c->last_prof.resize(KTAS_PROFILE ? i0 * P_NCAT : 0);
+        continue;
+      }
+      c->exact_merge = false;
       if (rc == 1) {  // an assignment exceeded the per-eval device capacity: grow and re-run
         c->ent_used = keep;
         c->ent_count.resize(i0);
@@ -2747,6 +2887,8 @@ int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
   for (size_t i = 0; i < n * P_NCAT; i++) ticks[i] = i < c->last_prof.size() ? c->last_prof[i] : 0;
   return KUEUE_TAS_OK;
 }
+
+int64_t kueue_tas_merge_reruns(kueue_tas_ctx* c) { return c ? c->merge_reruns : -1; }
 
 int kueue_tas_last_host_trace(kueue_tas_ctx* c, double* ms, int n) {  // ms since the chunk's start, [0, 20)
   if (!c || !ms) return KUEUE_TAS_EINVAL;

@@ -5079,16 +5079,22 @@ int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* d, siz
   if (!h || !h->snap || !h->err.empty() || (n && !d)) return KUEUE_TAS_EINVAL;
   try {
     FlavorSnapshot& s = *h->snap;
-    for (size_t i = 0; i < n; i++)
-      if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
-        throw std::runtime_error("delta out of range");
     if (s.dirty || !s.ctx) {  // no device copy to follow: the mirror takes the deltas, the upload the mirror
+      for (size_t i = 0; i < n; i++)
+        if (d[i].leaf < 0 || d[i].leaf >= s.N() || d[i].col < 0 || size_t(d[i].col) >= s.cols.size())
+          throw std::runtime_error("delta out of range");
       s.apply_to_mirror(d, n);
       const int rc = s.upload();
       if (rc) h->err = s.err;  // sticky, as on the admit path
       return rc;
     }
+    // (the device layer checks every record against the resident snapshot,
+    // whose leaves and columns are the mirror's when it is not dirty)
     int rc = n ? kueue_tas_snapshot_apply_deltas(s.ctx, d, n, nullptr) : 0;
+    if (rc == KUEUE_TAS_EINVAL) {
+      h->err = "delta out of range";
+      return KUEUE_TAS_EINVAL;
+    }
     if (rc) h->err = std::string("apply deltas: ") + kueue_tas_last_error(s.ctx);
     else if (n) s.device_applied();  // the host mirror follows at its next read
     return rc;

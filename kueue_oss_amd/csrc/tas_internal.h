@@ -199,6 +199,7 @@ struct DevBatch {
   uint32_t* lfc_tot;       // [nslots][kLfcBins]
   uint64_t* lfc_ovs;       // [nslots][nchunks] sum of the values >= kLfcBins - 1
   uint64_t* lfc_ovtot;     // [nslots]
+  uint8_t* lfc_u8;         // [nslots][nchunks * kLfcChunk] leaf values min(v, 255) (lfc_hist_kernel -> lfc_emit_kernel)
   LfcJob* lfc_jobs;        // [n]
   LfcItem* lfc_items;      // [nfast * nchunks] chunks with greedy output (appended by select)
   int32_t* lfc_nitems;     // [1] number of lfc_items

@@ -2718,6 +2718,16 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
       pending &= ~m;
     }
   }
+  // the chunk's values as bytes, min(v, 255), for lfc_emit_kernel: a greedy
+  // threshold below 255 needs no wider value (a quarter of the emit's reads)
+  {
+    uint8_t* u8 = b.lfc_u8 + int64_t(slot) * b.lfc_nchunks * kLfcChunk + int64_t(lo);
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int32_t x = xs[u];
+      u8[u * 256 + int(threadIdx.x)] = uint8_t(x < 0 ? 0 : x > 255 ? 255 : x);
+    }
+  }
   mysum = uint64_t(wave_sum_i64(int64_t(mysum)));
   if (lane == 0 && mysum) atomicAdd(&ovs, (unsigned long long)mysum);
   __syncthreads();
@@ -5393,8 +5403,15 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
                        s.level_off[s.L - 1];
     const int lo = item.chunk * kLfcChunk + int(threadIdx.x) * 8;
     int32_t x[8];
+    if (t < 255) {  // the byte copy decides every leaf: >= 255 is above the threshold
+      // (the copy holds 0 past the last leaf: a full chunk of bytes per slot)
+      const uint64_t w = *reinterpret_cast<const uint64_t*>(b.lfc_u8 + int64_t(slot) * b.lfc_nchunks * kLfcChunk + lo);
 #pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? V[lo + k] : 0;
+      for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? int32_t((w >> (8 * k)) & 0xffu) : 0;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = (lo + k < s.N) ? V[lo + k] : 0;
+    }
     int nt = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) nt += x[k] == t ? 1 : 0;

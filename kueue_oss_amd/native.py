@@ -67,7 +67,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
     "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
-    "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace",
+    "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace", "kueue_tas_merge_reruns",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -242,12 +242,13 @@ class TASFlavorSnapshot:
     def __init__(self, snapshot: dict, list_cap: int = 0, max_batch: int = 0, device: int = 0, lib=None,
                  packed_entries: bool = False, inline_stats: bool = False,
                  pair_fill: bool = True, serial_admit: bool = False, split_stats: bool = False,
-                 fused_top: bool = False, host_values: bool = False, category_fill: bool = True):
+                 fused_top: bool = False, host_values: bool = False, category_fill: bool = True,
+                 class_collide: bool = False):
         self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0)
                               | (0 if pair_fill else 4) | (8 if serial_admit else 0) | (16 if split_stats else 0)
                               | (32 if fused_top else 0) | (64 if host_values else 0)
-                              | (0 if category_fill else 128))
+                              | (0 if category_fill else 128) | (256 if class_collide else 0))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:
@@ -596,6 +597,12 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_leaf_ids(self._h, ctypes.byref(out)):
             raise RuntimeError(self._err())
         return _take(self._lib, out)
+
+    def merge_reruns(self) -> int:
+        """Device chunks re-run with the exact phase-1 class merge (kueue_tas_merge_reruns)."""
+        self._lib.kueue_tas_merge_reruns.restype = ctypes.c_int64
+        self._lib.kueue_tas_merge_reruns.argtypes = [ctypes.c_void_p]
+        return int(self._lib.kueue_tas_merge_reruns(self.device_ctx()))
 
     def device_ctx(self):
         """The kueue_tas_ctx* under this snapshot (for direct device-layer calls)."""

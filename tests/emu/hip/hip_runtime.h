@@ -306,6 +306,7 @@ inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
 }
 inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 0.f; return hipSuccess; }
 constexpr unsigned hipEventDisableTiming = 2;
+constexpr unsigned hipEventDisableSystemFence = 0x20000000;
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
 inline hipError_t hipEventSynchronize(hipEvent_t e) {  // the recording stream up to the event
   if (e->stream) e->stream->run_until(e->pos);

@@ -114,3 +114,29 @@ def test_emulated_two_resident_flavors_interleaved(emu_lib):
         assert b.find_topology_assignments_for_workloads(wls_b) == want_b
     a.close()
     b.close()
+
+
+def _class_collide(make):
+    """The speculative merge of the host parts' phase-1 classes (equal 64-bit
+    hashes taken as equal, verified exactly while the device runs) with every
+    hash forced equal (KUEUE_TAS_CFG_CLASS_COLLIDE): the verification fails,
+    the chunk re-runs with the exact merge, and every result is the oracle's."""
+    doc, wls = synth.config_c2(n_workloads=96, shape=(2, 2, 4, 8))
+    snap = make(doc)
+    snap.compile(wls)
+    snap.run_compiled(flags=TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES)
+    got = snap.last_results()
+    reruns = snap.merge_reruns()
+    snap.close()
+    want, _ = oracle_lib.eval_workloads(doc, wls, threads=4)
+    assert got == want
+    assert reruns >= 1
+
+
+def test_emulated_class_collide(emu_lib):  # noqa: F811
+    _class_collide(lambda d: TASFlavorSnapshot(d, lib=emu_lib, class_collide=True))
+
+
+@pytest.mark.gpu
+def test_class_collide_on_gpu():
+    _class_collide(lambda d: TASFlavorSnapshot(d, class_collide=True))
