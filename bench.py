@@ -65,6 +65,24 @@ def fill_algorithmic_bytes(N, n_fill, n_leader, R_used, label_cols, parents=0, n
     return snap + writes
 
 
+def survey_8d_bytes(N, R_used, label_cols, W, SD, W_leader=0):
+    """SURVEY.md §8(d) algorithmic bytes of fillInCounts + reduce for W
+    phase-1 evaluations: B = N*(16*R + 2 + 4*K_sel) + W*SD*8 (+ W_leader*SD*12):
+    free + used int64 per requested column, a 2-byte taint-profile id and the
+    selector label ids per leaf once, then state + sliceState int32 for every
+    domain of every evaluation (the leader fields for leader evaluations).
+    W = the launch's phase-1 classes (evaluations with identical phase-1
+    inputs share one fill: the per-unit figure times the units one launch
+    processes)."""
+    return N * (16 * R_used + 2 + 4 * label_cols) + W * SD * 8 + W_leader * SD * 12
+
+
+def total_domains(doc):
+    """Sum of the domains of every level (distinct level-value prefixes)."""
+    levels = doc["levels"]
+    return sum(len({tuple(n["labels"].get(k) for k in levels[:l + 1]) for n in doc["nodes"]}) for l in range(len(levels)))
+
+
 def fused_parents(doc):
     """Number of leaf parents the fill rolls up itself (tas_device.hip
     kueue_tas_snapshot_load: uniform power-of-two fan-out <= 64, contiguous in
@@ -111,8 +129,11 @@ def roofline_of(snap, doc, wls, steps, stage_sum):
     label_cols = 1 if any(p.get("nodeSelector") for w in wls for p in w) else 0
     fill_bytes = fill_algorithmic_bytes(N, st["fill_evals"] / launches, min(st["leader_evals"], st["fill_evals"]) / launches,
                                         R_used, label_cols, fused_parents(doc), st.get("alias_fills", 0) / launches)
-    achieved = fill_bytes / (per_launch_fill_ms * 1e-3) / 1e9
-    return st, fill_bytes, per_launch_fill_ms, achieved, R_used
+    W = st["fill_evals"] / launches
+    bytes_8d = survey_8d_bytes(N, R_used, label_cols, W, total_domains(doc), min(st["leader_evals"], st["fill_evals"]) / launches)
+    achieved = bytes_8d / (per_launch_fill_ms * 1e-3) / 1e9
+    st["written_model_bytes"] = int(fill_bytes)  # the fill's own minimum traffic (aliased rows not written)
+    return st, bytes_8d, per_launch_fill_ms, achieved, R_used
 
 
 def heartbeat(period=30.0):
@@ -264,6 +285,13 @@ def main():
     # the roofline's duration: the fill launches of the timed steps themselves
     timed_fill_ms = timed_stages["fill"] / max(timed_fills, 1)
     achieved_timed = fill_bytes / (timed_fill_ms * 1e-3) / 1e9 if timed_fill_ms > 0 else achieved
+    # the step's delta application alone (untimed repeats; pairs keep S)
+    ta = time.perf_counter()
+    for _ in range(10):
+        snap.apply_deltas(step_deltas)
+        snap.apply_deltas(neg_deltas)
+    barrier()
+    apply_ms = (time.perf_counter() - ta) / 20 * 1e3
     # the step's results on S (the timed steps alternate S + D and S)
     step()
     timed_results = snap.last_results() if rank == 0 and not a.no_cpu else None
@@ -356,7 +384,8 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3),
             "step_ms": {"median": round(pct(per_step, 0.5), 3), "p10": round(pct(per_step, 0.1), 3),
-                        "p90": round(pct(per_step, 0.9), 3)},
+                        "p90": round(pct(per_step, 0.9), 3), "max": round(max(per_step), 3),
+                        "over_1ms": sum(1 for x in per_step if x > 1.0)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -371,6 +400,9 @@ def main():
                          "bound": "hbm", "achieved": round(achieved_timed, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_timed / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src, "bytes_per_launch": int(fill_bytes),
+                         "bytes_definition": "SURVEY.md §8(d): N*(16*R + 2 + 4*K_sel) + W*SD*8 (+ W_leader*SD*12), "
+                                             "W = the launch's phase-1 classes",
+                         "bytes_written_model": st.get("written_model_bytes"),
                          "avg_launch_ms": round(timed_fill_ms, 4),
                          "avg_launch_source": f"HIP events on the fill's stream around each of the {timed_fills} fill "
                                               f"launches of the {timed_runs} timed steps",
@@ -380,8 +412,10 @@ def main():
             "precompiled_rate": {"value": round(pre_rate * world, 1), "unit": "placements/s",
                                  "note": "requests compiled once before timing, no TopologyAssignment values "
                                          "(round-1 step definition), no gather"},
-            "deltas_in_step": {"records": int(len(step_deltas)), "note": "every timed step applies one whole-batch "
+            "deltas_in_step": {"records": int(len(step_deltas)), "apply_ms": round(apply_ms, 4),
+                               "note": "every timed step applies one whole-batch "
                                "admission's deltas (alternately negated and again) after its evaluation"},
+            "class_merge_reruns": snap.merge_reruns(),
             "admission": {"round_ms_median": round(pct(adm_ms, 0.5), 3), "rounds": rounds,
                           "admitted": admitted_n, "deltas": deltas_n,
                           "device_pass": dict(zip(["window_rounds", "in_order_candidates", "candidates"],

@@ -324,6 +324,11 @@ struct kueue_tas_ctx {
   bool exact_merge = false;  // the next chunk merges the parts' classes with exact compares (after a collision)
   int64_t merge_reruns = 0;  // chunks re-run after a class hash collision
   bool collide_test = false; // KUEUE_TAS_CFG_CLASS_COLLIDE
+  int32_t exp_flags = [] {     // diagnostics only (tools/probe_select.py experiments)
+    const char* e = getenv("KTAS_EXP_FLAGS");
+    return e ? int32_t(atoi(e)) : 0;
+  }();
+
   double trace[24] = {};  // the last chunk's host timeline (wall ms at fixed points, kueue_tas_last_host_trace)
   double host_ms[8] = {};  // last batch host time: compile, classes, enqueue, wait, pack+D2H, copy-out, [6] of compile:
                            // validation pass, [7] of compile: records + hashes pass
@@ -2277,6 +2282,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.lfc_nchunks = nchunks;
   b.lfc_ch = c->d_lfc_ch.p;
   b.lfc_u8 = c->d_lfc_u8.p;
+  b.exp_flags = c->exp_flags;
   b.lfc_cp = c->d_lfc_cp.p;
   b.lfc_tot = c->d_lfc_tot.p;
   b.lfc_ovs = c->d_lfc_ovs.p;

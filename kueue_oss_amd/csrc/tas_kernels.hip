@@ -5443,7 +5443,7 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       if (keep[k]) {
-        if (pos < b.entry_cap) {
+        if (pos < b.entry_cap && !(b.exp_flags & 1)) {
           put_entry(ent, pos, lo + k, x[k]);
         }
         pos++;

@@ -1,7 +1,6 @@
-// tas_pool.h — the persistent host worker pool shared by the host layer
-// (tas_host.cpp) and the device layer's per-batch host work (tas_device.hip).
-// One pool per process (HostPool::get is an inline function: one instance
-// across translation units).  Not part of the public ABI.
+// tools/micro/pool_spin.h — experiment: tas_pool.h with pause-spinning workers and caller
+// (no sched_yield) and a condvar notify only when a worker sleeps.
+// Compared with the product pool by pool_bench.cpp on the GPU box host.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -13,13 +12,10 @@
 #include <memory>
 #include <mutex>
 #include <pthread.h>
-#include <sched.h>
-#include <cstdio>
-#include <string>
 #include <thread>
 #include <vector>
 
-namespace ktas_pool {
+namespace ktas_pool3 {
 
 // Persistent host workers for per-batch loops that are independent per
 // workload.  Two modes:
@@ -97,11 +93,11 @@ class HostPool {
       job_ = job;
       epoch_.fetch_add(1, std::memory_order_release);
     }
-    cv_.notify_all();
+    if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
     work(*job, 0);
     // every chunk has finished (thrown or not) before `f` — on the caller's
     // stack — goes out of scope
-    while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
+    while (job->done.load(std::memory_order_acquire) != job->chunks) __builtin_ia32_pause();
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_.reset();  // late workers keep their reference; its chunks are exhausted
@@ -116,68 +112,13 @@ class HostPool {
       if (!j.err) j.err = std::current_exception();
     }
   }
-  // CPUs near the creating thread (the caller of every job: part 0): the
-  // other cores of its last-level cache, one SMT thread each, so a static
-  // part's data moves between cores of one L3 at most (a worker on the other
-  // socket of a two-socket host reads the caller's records across it).
-  // KUEUE_TAS_HOST_PIN=0 leaves placement to the OS.
-  static std::vector<int> near_cpus(size_t want) {
-    std::vector<int> out;
-    const int self = sched_getcpu();
-    if (self < 0) return out;
-    auto read_list = [](const std::string& path) {
-      std::vector<int> v;
-      FILE* f = fopen(path.c_str(), "r");
-      if (!f) return v;
-      char buf[4096] = {};
-      const size_t k = fread(buf, 1, sizeof buf - 1, f);
-      fclose(f);
-      buf[k] = 0;
-      for (char* p = buf; *p;) {  // "a-b,c,d-e"
-        char* q = nullptr;
-        const long a = strtol(p, &q, 10);
-        if (q == p) break;
-        long b = a;
-        if (*q == '-') b = strtol(q + 1, &q, 10);
-        for (long x = a; x <= b; x++) v.push_back(int(x));
-        p = *q == ',' ? q + 1 : q;
-        if (*p == '\n') break;
-      }
-      return v;
-    };
-    const std::string base = "/sys/devices/system/cpu/cpu";
-    const std::vector<int> l3 = read_list(base + std::to_string(self) + "/cache/index3/shared_cpu_list");
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
-    std::vector<int> used = read_list(base + std::to_string(self) + "/topology/thread_siblings_list");
-    for (int c : l3) {
-      if (out.size() >= want) break;
-      if (!CPU_ISSET(c, &allowed) || std::find(used.begin(), used.end(), c) != used.end()) continue;
-      out.push_back(c);
-      for (int sib : read_list(base + std::to_string(c) + "/topology/thread_siblings_list")) used.push_back(sib);
-    }
-    if (out.size() < want) out.clear();  // not enough cores in the L3: leave placement to the OS
-    return out;
-  }
   HostPool() {
     size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
     if (const char* e = getenv("KUEUE_TAS_HOST_THREADS")) n = size_t(std::max(0, atoi(e)));
-    const char* pin_env = getenv("KUEUE_TAS_HOST_PIN");
-    const std::vector<int> cpus = (pin_env && atoi(pin_env) == 0) ? std::vector<int>() : near_cpus(n);
     // every worker starts from the epoch before any job: a static job posted
     // before a worker first runs is still seen by it (it owns a part)
     const uint64_t e0 = epoch_.load();
-    for (size_t i = 0; i < n; i++)
-      threads_.emplace_back([this, i, e0, cpu = cpus.empty() ? -1 : cpus[i]] {
-        if (cpu >= 0) {
-          cpu_set_t set;
-          CPU_ZERO(&set);
-          CPU_SET(cpu, &set);
-          (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
-        }
-        loop(i + 1, e0);
-      });
+    for (size_t i = 0; i < n; i++) threads_.emplace_back([this, i, e0] { loop(i + 1, e0); });
     // a child forked without exec has none of the workers: it runs inline
     pthread_atfork(nullptr, nullptr, [] { forked_child() = true; });
   }
@@ -204,12 +145,16 @@ class HostPool {
   void loop(size_t self, uint64_t seen) {
     for (;;) {
       const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(2000);
-      while (epoch_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < spin_until)
-        std::this_thread::yield();
+      for (unsigned k = 1; epoch_.load(std::memory_order_acquire) == seen; k++) {
+        __builtin_ia32_pause();
+        if ((k & 1023) == 0 && std::chrono::steady_clock::now() >= spin_until) break;
+      }
       std::shared_ptr<Job> job;
       {
         std::unique_lock<std::mutex> lk(mu_);
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
         cv_.wait(lk, [&] { return stop_ || epoch_.load() != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
         if (stop_) return;
         seen = epoch_.load();
         job = job_;
@@ -221,6 +166,7 @@ class HostPool {
   std::mutex mu_, callMu_;
   std::condition_variable cv_;
   std::atomic<uint64_t> epoch_{0};
+  std::atomic<int> sleepers_{0};
   std::shared_ptr<Job> job_;
   bool stop_ = false;
 };

@@ -16,7 +16,8 @@ lib = native.load_library(os.path.join(os.path.dirname(native.library_path()), "
 snap_doc, wls = synth.config_c3(n_workloads=int(os.environ.get("N_WL", "1024")))
 if os.environ.get("BF_ONLY"):  # no unconstrained (fast-LFC) evals: no concurrent LFC branch
     wls = [w for w in wls if w[0]["topologyRequest"] is not None and not w[0]["topologyRequest"].get("unconstrained")]
-snap = TASFlavorSnapshot(snap_doc, lib=lib, packed_entries=bool(os.environ.get("PACKED")))
+snap = TASFlavorSnapshot(snap_doc, lib=lib, packed_entries=bool(os.environ.get("PACKED")),
+                         host_values=bool(os.environ.get("HOST_VALUES")))
 res = snap.find_topology_assignments_for_workloads(wls)
 snap.compile(wls)
 for _ in range(3):
