@@ -136,6 +136,59 @@ def roofline_of(snap, doc, wls, steps, stage_sum):
     return st, bytes_8d, per_launch_fill_ms, achieved, R_used
 
 
+def _cpulist(path):
+    try:
+        with open(path) as f:
+            txt = f.read().strip()
+    except OSError:
+        return []
+    out = []
+    for part in txt.split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def place_host(gpu, local_rank):
+    """Pin this rank's main thread to one last-level-cache domain (CCD) on
+    the GPU's NUMA node, a distinct one per local rank: the library's host
+    pool then pins its workers to the other cores of that L3
+    (tas_pool.h near_cpus), so the step's host passes stay within one L3 and
+    the ranks of an 8-GPU node do not share cores.  Returns the CPU list (or
+    None when the topology is not readable)."""
+    try:
+        allowed = os.sched_getaffinity(0)
+        node = -1
+        try:
+            import torch
+
+            pr = torch.cuda.get_device_properties(gpu)
+            bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+                node = int(f.read().strip())
+        except Exception:  # noqa: BLE001 - no PCI info: any node
+            node = -1
+        cpus = sorted(allowed if node < 0 else set(_cpulist(f"/sys/devices/system/node/node{node}/cpulist")) & allowed)
+        l3s = []
+        seen = set()
+        for c in cpus:
+            if c in seen:
+                continue
+            dom = [x for x in _cpulist(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") if x in allowed]
+            seen.update(dom)
+            if len(dom) >= 6:
+                l3s.append(dom)
+        if not l3s:
+            return None
+        dom = l3s[local_rank % len(l3s)]
+        os.sched_setaffinity(0, dom)
+        return dom
+    except Exception:  # noqa: BLE001 - placement is an optimization only
+        return None
+
+
 def heartbeat(period=30.0):
     """A progress line on stderr every `period` s (long setup / oracle phases
     of the 1M-node config print nothing else for minutes)."""
@@ -182,6 +235,8 @@ def main():
     import numpy as np
     import torch
 
+    cpus_all = os.sched_getaffinity(0)
+    placed = place_host(gpu, local_rank) if torch.cuda.is_available() else None
     from kueue_oss_amd import TASFlavorSnapshot, synth
     from kueue_oss_amd.sharding import admit_round, gather_assignments, shard_ids
 
@@ -193,7 +248,8 @@ def main():
     gen_s = time.time() - t0
 
     t0 = time.time()
-    snap = TASFlavorSnapshot(snap_doc, device=gpu if world > 1 else 0)
+    snap = TASFlavorSnapshot(snap_doc, device=gpu if world > 1 else 0,
+                             host_values=os.environ.get("KTAS_BENCH_HOST_VALUES", "0") == "1")
     snap.compile(all_wls)  # identical resource columns on every replica
     if world > 1:
         snap.set_shard(ids)
@@ -334,6 +390,7 @@ def main():
         snap.apply_deltas(neg)
 
     # ---- whole timed batch vs the CPU oracle; CPU baseline ----
+    os.sched_setaffinity(0, cpus_all)  # the CPU legs run on the process's whole CPU set
     parity = cpu = None
     if rank == 0 and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -434,6 +491,8 @@ def main():
             "parity_full_batch": parity,
             "extras": extras,
             "setup_s": {"generate": round(gen_s, 2), "snapshot_load_and_compile": round(load_s, 2)},
+            "host_placement": {"l3_cpus": placed, "note": "rank's main thread bound to one L3 domain on the "
+                               "GPU's NUMA node; the library pins its host pool to that L3's other cores"},
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -76,11 +76,17 @@ class HostPool {
   }
 
  private:
+  static constexpr size_t kMaxParts = 64;
   struct Job {
     std::function<void(size_t, size_t)>* fn = nullptr;
     size_t n = 0, grain = 1, chunks = 0;
     bool fixed = false;  // run_static: chunk t is thread t's part
     std::atomic<size_t> next{0}, done{0};
+    // run_static: a part is run by whoever claims it first — its own thread,
+    // or the caller once its part is done and the owner has not started (a
+    // worker the OS has not scheduled yet, e.g. after its core ran another
+    // task, does not hold the whole job up)
+    std::atomic<uint8_t> claimed[kMaxParts] = {};
     std::mutex errMu;
     std::exception_ptr err;  // the first exception a chunk threw, rethrown on the caller
   };
@@ -99,6 +105,8 @@ class HostPool {
     }
     cv_.notify_all();
     work(*job, 0);
+    if (fixed)  // parts whose owner has not started yet
+      for (size_t t = 1; t < job->chunks; t++) run_part(*job, t);
     // every chunk has finished (thrown or not) before `f` — on the caller's
     // stack — goes out of scope
     while (job->done.load(std::memory_order_acquire) != job->chunks) std::this_thread::yield();
@@ -163,6 +171,7 @@ class HostPool {
   HostPool() {
     size_t n = std::min<size_t>(4, std::max<unsigned>(2, std::thread::hardware_concurrency()) - 1);
     if (const char* e = getenv("KUEUE_TAS_HOST_THREADS")) n = size_t(std::max(0, atoi(e)));
+    n = std::min(n, kMaxParts - 1);
     const char* pin_env = getenv("KUEUE_TAS_HOST_PIN");
     const std::vector<int> cpus = (pin_env && atoi(pin_env) == 0) ? std::vector<int>() : near_cpus(n);
     // every worker starts from the epoch before any job: a static job posted
@@ -186,11 +195,15 @@ class HostPool {
     return f;
   }
   bool inline_only() const { return threads_.empty() || forked_child(); }
+  static void run_part(Job& j, size_t t) {
+    if (j.claimed[t].exchange(1, std::memory_order_acq_rel)) return;  // its owner (or the caller) has it
+    const size_t T = j.chunks;
+    call(j, part_begin(j.n, t, T), part_begin(j.n, t + 1, T));
+    j.done.fetch_add(1, std::memory_order_release);
+  }
   void work(Job& j, size_t self) {
     if (j.fixed) {  // this thread's own part only
-      const size_t T = j.chunks;
-      call(j, part_begin(j.n, self, T), part_begin(j.n, self + 1, T));
-      j.done.fetch_add(1, std::memory_order_release);
+      run_part(j, self);
       return;
     }
     for (;;) {
