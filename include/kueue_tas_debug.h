@@ -91,6 +91,7 @@ int64_t kueue_tas_last_alias_fills(kueue_tas_ctx* ctx);
 #define KUEUE_TAS_PATH_ENTRY_TAGS 16384u        /* entries emitted with their leaf tags (kueue_tas_snapshot_set_leaf_tags) */
 #define KUEUE_TAS_PATH_RAGGED_PAIR 32768u       /* fill_pair_kernel on ragged leaf parents (128-leaf slots, segmented scans) */
 #define KUEUE_TAS_PATH_CATEGORY 65536u          /* fill_pair_kernel's single-run chunks classify leaf categories (CAT) */
+#define KUEUE_TAS_PATH_LFC_FILL 131072u         /* the fast-LFC chunk tables accumulated by the fill (no lfc_hist_kernel) */
 uint32_t kueue_tas_last_fill_paths(kueue_tas_ctx* ctx);
 /* Stage events: on (default), every stage of kueue_tas_last_stage_times is
  * timed; off, only the fill bracket is (the other events are pure

@@ -323,6 +323,13 @@ struct kueue_tas_ctx {
   std::vector<MagicCache> magic_cache;  // per host part (compute_magic)
   bool exact_merge = false;  // the next chunk merges the parts' classes with exact compares (after a collision)
   int64_t merge_reruns = 0;  // chunks re-run after a class hash collision
+  size_t lfc_half = 0;        // LFC chunk-table entries per half of d_lfc_ch / d_lfc_ovs
+  bool lfc_dirty[2] = {true, true};  // a half not known to be zero
+  int lfc_parity = 0;         // the half the next batch with fast-LFC evals uses
+  bool lfc_in_fill = [] {     // KTAS_LFC_IN_FILL=0: keep lfc_hist_kernel (A/B knob)
+    const char* e = getenv("KTAS_LFC_IN_FILL");
+    return !(e && atoi(e) == 0);
+  }();
   bool collide_test = false; // KUEUE_TAS_CFG_CLASS_COLLIDE
   int32_t exp_flags = [] {     // diagnostics only (tools/probe_select.py experiments)
     const char* e = getenv("KTAS_EXP_FLAGS");
@@ -2108,10 +2115,20 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   HIPCHK(c, c->d_scratch.ensure(nph2 * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
   HIPCHK(c, c->d_lfc_items.ensure(size_t(std::max(nfast, 1)) * size_t(std::max(nchunks, 1)) + 1));
-  HIPCHK(c, c->d_lfc_ch.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
+  // chunk counts and overflow sums in two halves used by alternate batches:
+  // the fill accumulates into zeroed tables (DevBatch::lfc_fill), and a
+  // half's zeroing runs on stream2 during the batch that does not use it
+  const size_t lfc_need = size_t(std::max(nslots * nchunks, 1));
+  if (lfc_need > c->lfc_half) {
+    c->lfc_half = lfc_need + lfc_need / 4;
+    HIPCHK(c, c->d_lfc_ch.ensure(2 * c->lfc_half * kLfcBins));
+    HIPCHK(c, c->d_lfc_ovs.ensure(2 * c->lfc_half));
+    c->lfc_dirty[0] = c->lfc_dirty[1] = true;
+  }
+  const int lfc_cur = c->lfc_parity;
   HIPCHK(c, c->d_lfc_cp.ensure(size_t(std::max(nslots * nchunks, 1)) * kLfcBins));
   HIPCHK(c, c->d_lfc_tot.ensure(size_t(std::max(nslots, 1)) * kLfcBins));
-  HIPCHK(c, c->d_lfc_ovs.ensure(size_t(std::max(nslots * nchunks, 1))));
+
   HIPCHK(c, c->d_lfc_ovtot.ensure(size_t(std::max(nslots, 1))));
   HIPCHK(c, c->d_lfc_u8.ensure(size_t(std::max(nslots, 1)) * size_t(std::max(nchunks, 1)) * kLfcChunk));
   const int nblk = (s.N + 255) / 256 * 4;  // one leaf partial per 64-leaf wave
@@ -2140,6 +2157,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         memset(&r, 0, sizeof r);
         FillEvalParams& P = r.p;
         P.eid = h_fill[pos];
+        P.pad2[0] = c->cls_slot[size_t(c->cls_order[size_t(pos)])];  // fast-LFC table slot, -1: none
+        P.pad2[1] = 0;
         P.taint_off = ev.taint_table;
         P.nsel = ev.nsel;
         P.slice_size = ev.slice_size;
@@ -2280,12 +2299,12 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.lfc_rep = reinterpret_cast<const int32_t*>(ds + o_lrep);
   b.lfc_nslots = nslots;
   b.lfc_nchunks = nchunks;
-  b.lfc_ch = c->d_lfc_ch.p;
+  b.lfc_ch = c->d_lfc_ch.p + size_t(lfc_cur) * c->lfc_half * kLfcBins;
   b.lfc_u8 = c->d_lfc_u8.p;
   b.exp_flags = c->exp_flags;
   b.lfc_cp = c->d_lfc_cp.p;
   b.lfc_tot = c->d_lfc_tot.p;
-  b.lfc_ovs = c->d_lfc_ovs.p;
+  b.lfc_ovs = c->d_lfc_ovs.p + size_t(lfc_cur) * c->lfc_half;
   b.lfc_ovtot = c->d_lfc_ovtot.p;
   b.lfc_jobs = c->d_lfc_jobs.p;
   b.lfc_nitems = reinterpret_cast<int32_t*>(c->d_lfc_items.p);  // item 0's slot holds the count
@@ -2382,6 +2401,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     // data (no affinity, no far selector column: !gl), taint rows and the
     // ExclusionStats in LDS, label ids packed in 16 bits
     const bool cat = c->cat_fill && pair && !gl && ts && b.nstat > 0 && c->labels16;
+    // the fast-LFC chunk tables accumulated by the fill itself (every chunk
+    // runs on fill_pair_kernel: its lean loop from the block's (category,
+    // value) pairs, its per-leaf loop per wave): no lfc_hist_kernel
+    // re-reading the slot classes' leaf rows
+    b.lfc_fill = (nfast > 0 && pair && c->lfc_in_fill) ? 1 : 0;
+    if (b.lfc_fill) c->fill_paths |= KUEUE_TAS_PATH_LFC_FILL;
+    if (b.lfc_fill && c->lfc_dirty[lfc_cur]) {  // (after a reallocation: zeroed before the fill)
+      HIPCHK(c, hipMemsetAsync(b.lfc_ch, 0, c->lfc_half * kLfcBins * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(b.lfc_ovs, 0, c->lfc_half * 8, c->stream));
+      c->lfc_dirty[lfc_cur] = false;
+    }
     // single-run chunks [0, nsingle) and multi-run chunks [nsingle, nfchunks): one launch each
     auto staged = [&](auto ns, auto tsv, auto mr, int first, int count, hipStream_t st) {
       if (count <= 0) return;
@@ -2574,10 +2604,20 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   // Enqueued after the BestFit select: that launch is on the batch's longest
   // chain, and the host's calls for this branch would otherwise delay it
   if (nfast) {
+    if (c->lfc_dirty[lfc_cur ^ 1]) {  // the next batch's half, zeroed while this batch runs
+      HIPCHK(c, hipMemsetAsync(c->d_lfc_ch.p + size_t(lfc_cur ^ 1) * c->lfc_half * kLfcBins, 0,
+                               c->lfc_half * kLfcBins * 4, c->stream2));
+      HIPCHK(c, hipMemsetAsync(c->d_lfc_ovs.p + size_t(lfc_cur ^ 1) * c->lfc_half, 0, c->lfc_half * 8, c->stream2));
+      c->lfc_dirty[lfc_cur ^ 1] = false;
+    }
+    c->lfc_dirty[lfc_cur] = true;  // this batch writes its half
+    c->lfc_parity = lfc_cur ^ 1;
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[2], 0));  // fill done
     if (c->stage_timing) HIPCHK(c, hipEventRecord(c->evl[0], c->stream2));
-    hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
-    HIPCHK(c, hipGetLastError());
+    if (!b.lfc_fill) {
+      hipLaunchKernelGGL(lfc_hist_kernel, dim3(unsigned(nchunks), unsigned(nslots)), dim3(256), 0, c->stream2, s, b);
+      HIPCHK(c, hipGetLastError());
+    }
     hipLaunchKernelGGL(lfc_total_kernel, dim3(unsigned(nslots)), dim3(kLfcBins), 0, c->stream2, b);
     HIPCHK(c, hipGetLastError());
     // the fast-LFC select reads the leaf counters and the LFC tables only

@@ -201,6 +201,7 @@ struct DevBatch {
   uint64_t* lfc_ovtot;     // [nslots]
   uint8_t* lfc_u8;         // [nslots][nchunks * kLfcChunk] leaf values min(v, 255) (lfc_hist_kernel -> lfc_emit_kernel)
   int32_t exp_flags;       // experiment knobs (KTAS_EXP_FLAGS; 0 in the product): 1 = lfc_emit skips its stores
+  int32_t lfc_fill;        // 1: fill_pair_kernel accumulates the LFC chunk tables and byte rows (no lfc_hist_kernel)
   LfcJob* lfc_jobs;        // [n]
   LfcItem* lfc_items;      // [nfast * nchunks] chunks with greedy output (appended by select)
   int32_t* lfc_nitems;     // [1] number of lfc_items

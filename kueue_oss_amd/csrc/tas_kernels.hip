@@ -1210,6 +1210,45 @@ constexpr int kPairTile = kPairLP * kFillThreads;  // leaves per block
     }                                                                                           \
   } while (0)
 
+// The fast-LFC chunk tables from the fill (DevBatch::lfc_fill; what
+// lfc_hist_kernel computes from the written rows): a slot class's leaf values
+// as counts per (slot, 2048-leaf chunk, value bin), the overflow bin's value
+// sum, and the byte copy of the values for lfc_emit_kernel.  Generic per-wave
+// form (any leaf layout, one ballot round per distinct value): the fill's
+// non-lean blocks.  The tables start at zero (lfc_total's stream zeroes them
+// after the batch's emit).
+__device__ void lfc_fill_accum(const DevBatch& b, int slot, const int32_t* vals, const int* leaves, const bool* act,
+                               int n) {
+  const int lane = lane_id();
+  for (int j = 0; j < n; j++) {
+    uint64_t pending = ballot(act[j]);
+    const int32_t x = act[j] ? vals[j] : 0;
+    const int bin = x >= kLfcBins - 1 ? kLfcBins - 1 : (x < 0 ? 0 : x);
+    const int ch = leaves[j] / kLfcChunk;
+    if (act[j]) {
+      b.lfc_u8[int64_t(slot) * b.lfc_nchunks * kLfcChunk + leaves[j]] = uint8_t(x < 0 ? 0 : x > 255 ? 255 : x);
+    }
+    while (pending) {
+      const int src = __ffsll((unsigned long long)pending) - 1;
+      const int key = bcast(ch * kLfcBins + bin, src);
+      const uint64_t m = ballot(act[j] && ch * kLfcBins + bin == key);
+      if (lane == src) atomicAdd(&b.lfc_ch[int64_t(slot) * b.lfc_nchunks * kLfcBins + key], uint32_t(__popcll(m)));
+      pending &= ~m;
+    }
+    // the overflow sums per chunk: a wave's leaves span at most two chunks
+    uint64_t om = ballot(act[j] && x >= kLfcBins - 1);
+    while (om) {
+      const int src = __ffsll((unsigned long long)om) - 1;
+      const int c0 = bcast(ch, src);
+      const uint64_t m = ballot(act[j] && x >= kLfcBins - 1 && ch == c0);
+      unsigned long long v = (act[j] && x >= kLfcBins - 1 && ch == c0) ? (unsigned long long)int64_t(x) : 0ull;
+      v = (unsigned long long)wave_sum_i64(int64_t(v));
+      if (lane == src) atomicAdd(reinterpret_cast<unsigned long long*>(&b.lfc_ovs[int64_t(slot) * b.lfc_nchunks + c0]), v);
+      om &= ~m;
+    }
+  }
+}
+
 // Or-fold: the positive-children masks
 struct OpOr {
   __device__ int32_t operator()(int32_t a, int32_t b) const { return a | b; }
@@ -1242,6 +1281,12 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   __shared__ uint64_t sh_passd[CAT ? 2 * kEvalsPerBlock : 1];  // pass masks over dense category ids (two words)
   __shared__ unsigned long long sh_dkey[CAT ? kCatSlots : 1];  // the categories' keys by dense id
   __shared__ int32_t sh_dcnt[CAT ? kCatSlots : 1];             // and their leaf counts
+  // lean blocks with fast-LFC slot classes (DevBatch::lfc_fill): the distinct
+  // (dense category, state0 > 0) pairs of each wave's leaves and their counts
+  constexpr int kTri = 2 * kWave;  // at most one pair per leaf of the wave
+  __shared__ int32_t sh_tv[CAT ? 4 * kTri : 1];
+  __shared__ int32_t sh_tc[CAT ? 4 * kTri : 1];  // count << 8 | dense category
+  __shared__ int32_t sh_tn[CAT ? 4 : 1];
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   KTAS_FILL_STAMP(0);
@@ -1603,11 +1648,50 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const int64_t cst = b.ctr_stride;
     int32_t* rowp = b.counters + int64_t(e0) * cst;
     uint64_t* rpp = b.rack_pos ? b.rack_pos + int64_t(e0) * lsz + parent : nullptr;
+    // fast-LFC chunk tables from the fill: the wave's (category, value) pairs
+    bool lfc_any = false;
+    if (b.lfc_fill)
+      for (int e = 0; e < ne; e++) lfc_any = lfc_any || sh_pos[e].p.pad2[0] >= 0;
+    if (lfc_any) {
+      const int wv = int(threadIdx.x >> 6);
+      const bool a0 = valid[0] && state0[0] > 0, a1 = valid[1] && state0[1] > 0;
+      const uint64_t k0 = (uint64_t(uint32_t(did[0])) << 32) | uint32_t(state0[0]);
+      const uint64_t k1 = (uint64_t(uint32_t(did[1])) << 32) | uint32_t(state0[1]);
+      uint64_t p0 = ballot(a0), p1 = ballot(a1);
+      int nt = 0;
+      while (p0 | p1) {
+        const bool first = p0 != 0;
+        const int src = __ffsll((unsigned long long)(first ? p0 : p1)) - 1;
+        const uint64_t key = bcast64(first ? k0 : k1, src);
+        const uint64_t m0 = ballot(a0 && k0 == key), m1 = ballot(a1 && k1 == key);
+        if (lane == 0) {
+          sh_tv[wv * kTri + nt] = int32_t(uint32_t(key));
+          sh_tc[wv * kTri + nt] = ((__popcll(m0) + __popcll(m1)) << 8) | int32_t(key >> 32);
+        }
+        nt++;
+        p0 &= ~m0;
+        p1 &= ~m1;
+      }
+      if (lane == 0) sh_tn[wv] = nt;
+    }
+    const int lfc_chunk = (tile * kPairTile) / kLfcChunk;  // the block's leaves lie in one LFC chunk
     for (int e = 0; e < ne; e++, rowp += cst, rpp += lsz) {
       const uint64_t pm = sh_passd[2 * e];
       const int32_t m0 = int32_t(uint32_t(pm >> did[0]) << 31) >> 31;
       const int32_t m1 = int32_t(uint32_t(pm >> did[1]) << 31) >> 31;
       const int32_t st0 = state0[0] & m0, st1 = state0[1] & m1;
+      if (lfc_any) {
+        const int lslot = sh_pos[e].p.pad2[0];  // block-uniform
+        if (lslot >= 0) {  // the byte copy of the class's leaf values (lfc_emit_kernel)
+          uint8_t* u8 = b.lfc_u8 + int64_t(lslot) * b.lfc_nchunks * kLfcChunk + leaf0;
+          const uint32_t c0 = uint32_t(min(st0, 255)), c1 = uint32_t(min(st1, 255));
+          if (full_tile) *reinterpret_cast<uint16_t*>(u8) = uint16_t(c0 | (c1 << 8));
+          else {
+            if (valid[0]) u8[0] = uint8_t(c0);
+            if (valid[1]) u8[1] = uint8_t(c1);
+          }
+        }
+      }
       // (the sliceState row is not stored: FillEvalParams::ss_alias)
       if (full_tile) {
         *reinterpret_cast<int2*>(rowp + gleaf0) = make_int2(st0, st1);
@@ -1623,6 +1707,39 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         if (gpos == 0 && has_par) {
           *rpp = posm;
           rowp[poff + parent] = cap2;
+        }
+      }
+    }
+    if (lfc_any) {  // the slot classes' counts: wave w takes classes w, w + 4, ...
+      __syncthreads();  // every wave's pairs
+      const int wv = int(threadIdx.x >> 6);
+      const int nvalid = min(kPairTile, N - tile * kPairTile);
+      for (int e = wv; e < ne; e += kFillThreads / kWave) {
+        const int lslot = sh_pos[e].p.pad2[0];
+        if (lslot < 0) continue;
+        const uint64_t pm = sh_passd[2 * e];
+        uint32_t* ch = b.lfc_ch + (int64_t(lslot) * b.lfc_nchunks + lfc_chunk) * kLfcBins;
+        int pos_cnt = 0;
+        unsigned long long osum = 0;
+        for (int w2 = 0; w2 < kFillThreads / kWave; w2++) {
+          const int nt = sh_tn[w2];
+          for (int i = lane; i < nt; i += kWave) {
+            const int32_t v = sh_tv[w2 * kTri + i];
+            const int32_t tc = sh_tc[w2 * kTri + i];
+            const int cnt = tc >> 8, d = tc & 0xff;
+            if ((pm >> d) & 1ull) {  // the class takes this category: value v on cnt leaves
+              atomicAdd(&ch[v >= kLfcBins - 1 ? kLfcBins - 1 : v], uint32_t(cnt));
+              pos_cnt += cnt;
+              if (v >= kLfcBins - 1) osum += (unsigned long long)int64_t(v) * (unsigned long long)cnt;
+            }
+          }
+        }
+        pos_cnt = int(wave_sum_i64(pos_cnt));
+        osum = (unsigned long long)wave_sum_i64(int64_t(osum));
+        if (lane == 0) {
+          if (nvalid - pos_cnt > 0) atomicAdd(&ch[0], uint32_t(nvalid - pos_cnt));  // value 0: every other leaf
+          if (osum)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&b.lfc_ovs[int64_t(lslot) * b.lfc_nchunks + lfc_chunk]), osum);
         }
       }
     }
@@ -1787,6 +1904,13 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const bool alias = uni(sh_pos[e].p.ss_alias) != 0;
     storev(0, state);
     if (!alias) storev(SD, ss);
+    if (b.lfc_fill) {  // a fast-LFC slot class (always simple: its values are state)
+      const int lslot = uni(sh_pos[e].p.pad2[0]);
+      if (lslot >= 0) {
+        const int lv[kPairLP] = {leaf0, leaf0 + 1};
+        lfc_fill_accum(b, lslot, state, lv, valid, kPairLP);
+      }
+    }
     if (leader) {
       storev(2 * SD, swl);
       storev(3 * SD, sswl);

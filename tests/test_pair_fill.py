@@ -21,6 +21,7 @@ from kueue_oss_amd import TASFlavorSnapshot, synth
 
 PAIR = 8192
 CATEGORY = 65536
+LFC_FILL = 131072  # the fast-LFC chunk tables accumulated by the fill (no lfc_hist_kernel)
 
 
 def _batch(make, doc, wls):
@@ -58,6 +59,7 @@ def _run(make_pair, make_staged, scale, make_percls=None):
         paths = _batch(make_pair, doc, wls)
         assert paths & PAIR, name
         assert paths & CATEGORY or name != "c3 fan-out 32", name
+        assert paths & LFC_FILL or name != "c3 fan-out 32", name
         assert _batch(make_staged, doc, wls) & (PAIR | CATEGORY) == 0, name
         if make_percls is not None:
             assert _batch(make_percls, doc, wls) & (PAIR | CATEGORY) == PAIR, name
@@ -119,7 +121,8 @@ def test_emulated_pair_fill(emu_lib):  # noqa: F811
     _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, fused_top=True), 1,
          lambda d: TASFlavorSnapshot(d, lib=emu_lib, category_fill=False))
     assert _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 31, 40) & PAIR
-    assert _many_categories(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 1) & CATEGORY
+    # lean and per-leaf blocks of one launch accumulate the LFC tables together
+    assert _many_categories(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 1) & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL
 
 
 @pytest.mark.gpu
@@ -127,4 +130,4 @@ def test_pair_fill_on_gpu():
     _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False, fused_top=True), 4,
          lambda d: TASFlavorSnapshot(d, category_fill=False))
     assert _random(lambda d: TASFlavorSnapshot(d), 32, 150) & PAIR
-    assert _many_categories(lambda d: TASFlavorSnapshot(d), 4) & CATEGORY
+    assert _many_categories(lambda d: TASFlavorSnapshot(d), 4) & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL
