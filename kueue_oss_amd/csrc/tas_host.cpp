@@ -3492,6 +3492,7 @@ struct kueue_tas_host {
   std::vector<kueue_tas_fits_term> admit_terms;
   std::vector<int64_t> admit_toff;  // per admitted-round workload: first term
   std::vector<PodSetResult*> values_rest;  // RUN_VALUES: results whose Values the host builds
+  std::vector<const std::string*> values_flat;  // host-built Values pointers in the entry view's layout
   float stage_accum[KUEUE_TAS_NUM_STAGES] = {};  // kueue_tas_host_stage_accum
   // last kueue_tas_host_update_nodes: parse, node events, flush_joins, splice
   // (host rows, device call, leaf tags), evaluator reset, pushes, total, and
@@ -4648,15 +4649,36 @@ int kueue_tas_host_run(kueue_tas_host* h, uint32_t flags, uint64_t* result_hash)
     const uint64_t* tags = kueue_tas_last_entry_tags(snap.ctx);
     std::vector<PodSetResult*>& rest = h->values_rest;
     rest.clear();
+    // without device tags: the same per-entry Values pointers built by the
+    // host pool in one array laid out like the entry view (no per-result
+    // allocation), each domain the leaf's levelValues from the leaf table
+    std::vector<PodSetResult*> inview;
     for (auto& rs : results)
       for (auto& r : rs) {
         const size_t nd = r.domains.size();
         if (!nd) continue;
-        if (tags && r.domains.p >= e0 && r.domains.p + nd <= e0 + npairs)
+        const bool in = r.domains.p >= e0 && r.domains.p + nd <= e0 + npairs;
+        if (tags && in)
           r.values = reinterpret_cast<const std::string* const*>(tags + (r.domains.p - e0));
+        else if (in)
+          inview.push_back(&r);
         else
           rest.push_back(&r);
       }
+    if (!inview.empty()) {
+      if (h->values_flat.size() < npairs) h->values_flat.resize(npairs);
+      const std::string** vf = h->values_flat.data();
+      const int32_t lvl = snap.L() - nlev;
+      const std::string* const* lv = snap.leaf_values();
+      HostPool::get().run_static(inview.size(), [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+          PodSetResult& r = *inview[i];
+          const size_t o = size_t(r.domains.p - e0), nd = r.domains.size();
+          for (size_t k = 0; k < nd; k++) vf[o + k] = lv[r.domains[k].leaf] + lvl;
+          r.values = vf + o;
+        }
+      });
+    }
     if (!rest.empty()) {
       const int32_t lvl = snap.L() - nlev;
       const std::string* const* lv = snap.leaf_values();
