@@ -227,6 +227,11 @@ typedef struct {
  * runs) fails and the chunk re-runs with the exact merge: the collision path
  * must give the same results */
 #define KUEUE_TAS_CFG_CLASS_COLLIDE 256
+/* fill_pair_kernel accumulates the fast-LFC chunk tables and byte rows
+ * (KUEUE_TAS_PATH_LFC_FILL) instead of lfc_hist_kernel re-reading the slot
+ * classes' rows; off by default (it lengthens the fill on the main chain by
+ * about what it saves the side stream), also KTAS_LFC_IN_FILL=1 */
+#define KUEUE_TAS_CFG_LFC_IN_FILL 512
 
 /* ---- device layer -------------------------------------------------------- */
 int kueue_tas_abi_version(void);

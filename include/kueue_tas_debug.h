@@ -100,6 +100,10 @@ int kueue_tas_set_stage_timing(kueue_tas_ctx* ctx, int32_t on);
 /* Lifetime counts of successful kueue_tas_snapshot_load and
  * kueue_tas_snapshot_splice calls on ctx (tests pin which one an event took). */
 int kueue_tas_snapshot_counters(kueue_tas_ctx* ctx, int64_t* loads, int64_t* splices);
+/* Device memory held by ctx now: *total every buffer of the context,
+ * *phase2 the per-batch evaluation state (class counter rows, BestFit
+ * overlays and their ownership tags), which scales with the batch. */
+int kueue_tas_device_bytes(kueue_tas_ctx* ctx, int64_t* total, int64_t* phase2);
 /* Host-mirror support (the host layer's copy of tasUsage follows the device
  * lazily): _usage_mark records the resident usage columns and presence bits
  * as the mirror's state (a device-side shadow copy); _usage_changes lists

@@ -29,11 +29,33 @@ namespace {
 
 constexpr int kEvalsPerFillBlock = kEvalsPerBlock;
 
+// A simple class: no leader, one-pod slices at the leaf level and no inner
+// slice rounding, so sliceState == state at every level: its class row keeps
+// one field (FillEvalParams::ss_alias, ctr_row).
+bool simple_class(const DevEval& ev, int L) {
+  bool simple = (ev.flags & KUEUE_TAS_F_LEADER) == 0 && ev.slice_level == L - 1 && ev.slice_size == 1;
+  for (int l = 0; l < L && simple; l++) simple = ev.ssal[l] == 0 || ev.ssal[l] == 1;
+  return simple;
+}
+
+// Device bytes per context (kueue_tas_device_bytes): every DevBuf built
+// while a context is constructed links itself into that context's chain.
+struct DevBufLink {
+  size_t bytes = 0;
+  DevBufLink* next = nullptr;
+};
+thread_local DevBufLink** g_devbuf_chain = nullptr;
+
 template <typename T>
-struct DevBuf {
+struct DevBuf : DevBufLink {
   T* p = nullptr;
   size_t n = 0;
-  DevBuf() = default;
+  DevBuf() {
+    if (g_devbuf_chain) {
+      next = *g_devbuf_chain;
+      *g_devbuf_chain = this;
+    }
+  }
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
@@ -42,19 +64,25 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
-    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) n = std::max<size_t>(count, 1);
+    bytes = 0;
+    size_t nb = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc(&p, nb);
+    if (e == hipSuccess) {
+      n = std::max<size_t>(count, 1);
+      bytes = nb;
+    }
     return e;
   }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
+    bytes = 0;
   }
   void swap(DevBuf& o) {
     std::swap(p, o.p);
     std::swap(n, o.n);
+    std::swap(bytes, o.bytes);
   }
   // ensure with 1/8 headroom when it grows (buffers that grow by a few rows at a time)
   hipError_t reserve(size_t count) { return count <= n && p ? hipSuccess : ensure(count + count / 8); }
@@ -321,14 +349,17 @@ struct kueue_tas_ctx {
   float last_ms[4] = {0, 0, 0, 0};
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   std::vector<MagicCache> magic_cache;  // per host part (compute_magic)
+  std::vector<int32_t> h_gsrc;          // a splice's leaf sources (load_impl)
+  std::vector<int32_t> ctr_row_off;     // last batch: each fill position's class row offset (units of SD)
+  DevBufLink* dev_bufs = nullptr;       // every DevBuf member (kueue_tas_device_bytes)
   bool exact_merge = false;  // the next chunk merges the parts' classes with exact compares (after a collision)
   int64_t merge_reruns = 0;  // chunks re-run after a class hash collision
   size_t lfc_half = 0;        // LFC chunk-table entries per half of d_lfc_ch / d_lfc_ovs
   bool lfc_dirty[2] = {true, true};  // a half not known to be zero
   int lfc_parity = 0;         // the half the next batch with fast-LFC evals uses
-  bool lfc_in_fill = [] {     // KTAS_LFC_IN_FILL=0: keep lfc_hist_kernel (A/B knob)
-    const char* e = getenv("KTAS_LFC_IN_FILL");
-    return !(e && atoi(e) == 0);
+  bool lfc_in_fill = [] {     // KTAS_LFC_IN_FILL=1: fast-LFC chunk tables from the pair fill (no lfc_hist_kernel);
+    const char* e = getenv("KTAS_LFC_IN_FILL");  // off by default: it lengthens the fill on the main chain
+    return e && atoi(e) != 0;                     // by more than it saves the side stream
   }();
   bool collide_test = false; // KUEUE_TAS_CFG_CLASS_COLLIDE
   int32_t exp_flags = [] {     // diagnostics only (tools/probe_select.py experiments)
@@ -384,7 +415,11 @@ extern "C" {
 int kueue_tas_abi_version(void) { return KUEUE_TAS_ABI_VERSION; }
 
 kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
+  DevBufLink* chain = nullptr;
+  g_devbuf_chain = &chain;
   auto* c = new kueue_tas_ctx();
+  g_devbuf_chain = nullptr;
+  c->dev_bufs = chain;
   if (cfg) {
     c->device = cfg->device;
     c->inline_stats = (cfg->flags & KUEUE_TAS_CFG_INLINE_STATS) != 0 || (cfg->flags & KUEUE_TAS_CFG_SPLIT_STATS) == 0;
@@ -393,6 +428,7 @@ kueue_tas_ctx* kueue_tas_ctx_create(const kueue_tas_config* cfg) {
     c->fused_top = (cfg->flags & KUEUE_TAS_CFG_FUSED_TOP) != 0;
     c->cat_fill = (cfg->flags & KUEUE_TAS_CFG_NO_CATEGORY_FILL) == 0;
     c->collide_test = (cfg->flags & KUEUE_TAS_CFG_CLASS_COLLIDE) != 0;
+    if (cfg->flags & KUEUE_TAS_CFG_LFC_IN_FILL) c->lfc_in_fill = true;
     if (cfg->list_cap > 0) {
       int lc = 64;
       while (lc < cfg->list_cap && lc < 1024) lc <<= 1;
@@ -574,7 +610,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   if (sp) old_dead.swap(c->h_dead);
   c->h_dead.assign(N, 0);
   c->n_dead = 0;
-  std::vector<int32_t> gsrc;
+  std::vector<int32_t>& gsrc = c->h_gsrc;  // (kept: no fresh pages per splice)
   if (sp) {
     gsrc.resize(N);
     int32_t k = 0;
@@ -687,15 +723,15 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
       s.leaf_dead = c->d_dead.p;
       s.n_live = int32_t(int64_t(N) - c->n_dead);
     }
-  } else {
-  HIPCHK(c, c->d_free.ensure(size_t(s.R) * N));
-  HIPCHK(c, c->d_usage.ensure(size_t(s.R) * N));
+  } else {  // (leaf columns with headroom: a later splice's gather targets then fit without a reallocation)
+  HIPCHK(c, c->d_free.reserve(size_t(s.R) * N));
+  HIPCHK(c, c->d_usage.reserve(size_t(s.R) * N));
   if (s.R && N) {
     HIPCHK(c, hipMemcpyAsync(c->d_free.p, d->free_capacity, size_t(s.R) * N * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_usage.p, d->tas_usage, size_t(s.R) * N * 8, hipMemcpyHostToDevice, c->stream));
   }
-  HIPCHK(c, c->d_free_present.ensure(N));
-  HIPCHK(c, c->d_usage_present.ensure(N));
+  HIPCHK(c, c->d_free_present.reserve(N));
+  HIPCHK(c, c->d_usage_present.reserve(N));
   if (N) {
     HIPCHK(c, hipMemcpyAsync(c->d_free_present.p, d->free_present, N * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_usage_present.p, d->usage_present, N * 4, hipMemcpyHostToDevice, c->stream));
@@ -708,7 +744,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   c->num_profiles = 1;
   if (d->taint_profile && N) {
     for (size_t i = 0; i < N; i++) c->num_profiles = std::max(c->num_profiles, d->taint_profile[i] + 1);
-    HIPCHK(c, c->d_taint_profile.ensure(N));
+    HIPCHK(c, c->d_taint_profile.reserve(N));
     HIPCHK(c, hipMemcpyAsync(c->d_taint_profile.p, d->taint_profile, N * 4, hipMemcpyHostToDevice, c->stream));
     s.taint_profile = c->d_taint_profile.p;
   }
@@ -717,19 +753,26 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   for (int k = 0; k < std::min(s.K, kStagedLabels) && d->label_values; k++)
     for (size_t i = 0; i < N && c->labels16; i++) c->labels16 = uint32_t(d->label_values[size_t(k) * N + i]) <= 0xffffu;
   if (s.K > 0 && d->label_values && N) {
-    HIPCHK(c, c->d_labels.ensure(size_t(s.K) * N));
+    HIPCHK(c, c->d_labels.reserve(size_t(s.K) * N));
     HIPCHK(c, hipMemcpyAsync(c->d_labels.p, d->label_values, size_t(s.K) * N * 4, hipMemcpyHostToDevice, c->stream));
     s.label_values = c->d_labels.p;
   }
   }
   s.id_rank = nullptr;
-  if (d->domain_id_rank && off) {  // re-laid out on the padded level offsets
-    std::vector<int32_t> ranks(size_t(off), 0);
-    int64_t src = 0;
-    for (int l = 0; l < s.L; l++)
-      for (int i = 0; i < d->level_sizes[l]; i++) ranks[size_t(s.level_off[l] + i)] = d->domain_id_rank[src++];
+  if (d->domain_id_rank && off) {  // re-laid out on the padded level offsets, in the pinned arena itself
     HIPCHK(c, c->d_id_rank.reserve(size_t(off)));
-    HIPCHK(c, stage(c->d_id_rank.p, ranks.data(), size_t(off) * 4));
+    const size_t bytes = size_t(off) * 4;
+    if (arena_pos + bytes > c->h_tab.n) return fail(c, KUEUE_TAS_EINVAL, "load: staging arena");
+    int32_t* ranks = reinterpret_cast<int32_t*>(c->h_tab.p + arena_pos);
+    int64_t src = 0;
+    for (int l = 0; l < s.L; l++) {
+      const int32_t b = s.level_off[l], sz = d->level_sizes[l];
+      memcpy(ranks + b, d->domain_id_rank + src, size_t(sz) * 4);
+      for (int32_t i = b + sz; i < s.level_off[l + 1]; i++) ranks[i] = 0;
+      src += sz;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_id_rank.p, ranks, bytes, hipMemcpyHostToDevice, c->stream));
+    arena_pos += (bytes + 255) / 256 * 256;
     s.id_rank = c->d_id_rank.p;
   }
   // leaves' parents with a uniform power-of-two fan-out F <= 64 in leaf order:
@@ -763,7 +806,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
     bool ok = co[0] == 0 && co[P] == s.N;
     std::vector<int2> tab;
-    std::vector<int32_t> lp(N, 0), wide;
+    std::vector<int32_t> wide;
     int cb = 0, cn = 0, fmax = 0;
     for (int p = 0; p < P && ok; p++) {
       const int f = co[p + 1] - co[p];
@@ -772,7 +815,6 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
         break;
       }
       fmax = std::max(fmax, f);
-      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
       if (f > 2 * kWave) {  // pieces of their own
         if (cn) tab.push_back(make_int2(cb, cn));
         for (int k = co[p]; k < co[p + 1]; k += 2 * kWave)
@@ -799,8 +841,7 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
       }
       HIPCHK(c, c->d_wave_tab2.reserve(tab.size()));
       HIPCHK(c, stage(c->d_wave_tab2.p, tab.data(), tab.size() * sizeof(int2)));
-      HIPCHK(c, c->d_leaf_parent.reserve(N));
-      HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
+      HIPCHK(c, c->d_leaf_parent.reserve(N));  // (domain_parents_kernel below)
       s.wave_tab2 = c->d_wave_tab2.p;
       s.n_wave_slots2 = int32_t(tab.size());
       s.leaf_parent = c->d_leaf_parent.p;
@@ -812,7 +853,6 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     const int32_t* co = d->child_offsets + s.child_base[s.L - 2];
     bool ok = co[0] == 0 && co[P] == s.N;
     std::vector<int2> tab;
-    std::vector<int32_t> lp(N, 0);
     int cb = 0, cn = 0;
     for (int p = 0; p < P && ok; p++) {
       const int f = co[p + 1] - co[p];
@@ -826,30 +866,26 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
         cn = 0;
       }
       cn += f;
-      for (int j = co[p]; j < co[p + 1]; j++) lp[size_t(j)] = p;
     }
     if (ok) {
       tab.push_back(make_int2(cb, cn));
       HIPCHK(c, c->d_wave_tab.reserve(tab.size()));
       HIPCHK(c, stage(c->d_wave_tab.p, tab.data(), tab.size() * sizeof(int2)));
       HIPCHK(c, c->d_leaf_parent.reserve(N));
-      HIPCHK(c, stage(c->d_leaf_parent.p, lp.data(), N * 4));
       s.wave_tab = c->d_wave_tab.p;
       s.n_wave_slots = int32_t(tab.size());
       s.leaf_parent = c->d_leaf_parent.p;
       c->rack_fanout = -1;
     }
   }
-  // parent global domain id of every domain (v1beta2 leaf-mode encoder)
-  {
-    std::vector<int32_t> parent(size_t(std::max<int64_t>(off, 1)), -1);
-    for (int l = 0; l + 1 < s.L; l++) {
-      const int32_t* co = d->child_offsets + s.child_base[l];
-      for (int p = 0; p < d->level_sizes[l]; p++)
-        for (int j = co[p]; j < co[p + 1]; j++) parent[size_t(s.level_off[l + 1] + j)] = s.level_off[l] + p;
-    }
-    HIPCHK(c, c->d_parent.reserve(parent.size()));
-    HIPCHK(c, stage(c->d_parent.p, parent.data(), parent.size() * 4));
+  // parent global domain id of every domain (v1beta2 leaf-mode encoder) and
+  // the ragged fills' leaf parents, derived on the device from the offsets
+  // just uploaded (no O(N) host pass or upload per load / splice)
+  HIPCHK(c, c->d_parent.reserve(size_t(std::max<int64_t>(off, 1))));
+  if (off > 0) {
+    hipLaunchKernelGGL(domain_parents_kernel, dim3(unsigned((off + 255) / 256)), dim3(256), 0, c->stream, s,
+                       c->d_parent.p, s.leaf_parent ? c->d_leaf_parent.p : nullptr);
+    HIPCHK(c, hipGetLastError());
   }
   c->names_loaded = false;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -857,6 +893,15 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   c->maxD = maxD;
   c->loaded = true;
   (sp ? c->n_splices : c->n_loads)++;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_device_bytes(kueue_tas_ctx* c, int64_t* total, int64_t* phase2) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  int64_t t = 0;
+  for (const DevBufLink* b = c->dev_bufs; b; b = b->next) t += int64_t(b->bytes);
+  if (total) *total = t;
+  if (phase2) *phase2 = int64_t(c->d_counters.bytes + c->d_overlay.bytes + c->d_tags.bytes);
   return KUEUE_TAS_OK;
 }
 
@@ -1043,8 +1088,8 @@ int kueue_tas_snapshot_usage_mark(kueue_tas_ctx* c) {
   if (!c || !c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot");
   HIPCHK(c, hipSetDevice(c->device));
   const size_t N = size_t(c->snap.N), R = size_t(c->snap.R);
-  HIPCHK(c, c->d_ushadow.ensure(N * R));
-  HIPCHK(c, c->d_pshadow.ensure(N));
+  HIPCHK(c, c->d_ushadow.reserve(N * R));  // (headroom: splices grow N a few leaves at a time)
+  HIPCHK(c, c->d_pshadow.reserve(N));
   if (N * R) HIPCHK(c, hipMemcpyAsync(c->d_ushadow.p, c->d_usage.p, N * R * 8, hipMemcpyDeviceToDevice, c->stream));
   if (N) HIPCHK(c, hipMemcpyAsync(c->d_pshadow.p, c->d_usage_present.p, N * 4, hipMemcpyDeviceToDevice, c->stream));
   c->shadow_ok = true;
@@ -1125,7 +1170,7 @@ int kueue_tas_snapshot_set_leaf_live(kueue_tas_ctx* c, const int32_t* leaves, si
   }
   std::vector<int32_t> lv;  // read by the async copy: lives until the synchronize below
   if (!was_dense) {  // first dead leaf: the whole map (the device copy was dropped while all leaves lived)
-    HIPCHK(c, c->d_dead.ensure(size_t(c->snap.N)));
+    HIPCHK(c, c->d_dead.reserve(size_t(c->snap.N)));
     HIPCHK(c, hipMemcpyAsync(c->d_dead.p, c->h_dead.data(), size_t(c->snap.N), hipMemcpyHostToDevice, c->stream));
   } else {  // scatter the changed leaves
     lv.resize(2 * n);
@@ -1660,15 +1705,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   trace(2);
   // ---- compile requests to device form (magic numbers) ----
   const double t_b = wall_ms();
-  static uint64_t prof_cyc[8][4];
-  for (auto& a : prof_cyc) for (auto& x : a) x = 0;
   if (c->magic_cache.size() < nparts) c->magic_cache.resize(nparts);
   pool.run_static(n, [&](size_t i0, size_t i1) {
     const size_t ch = part_of(i0);
     MagicCache& mc = c->magic_cache[ch];
-    uint64_t* pcy = prof_cyc[ch & 7];
     for (size_t i = i0; i < i1; i++) {
-      uint64_t tq0 = __builtin_ia32_rdtsc();
       const auto& r = *reqs[i];
       DevEval& e = hev[i];  // every field is assigned below (no memset of the record)
       e.req_mask = e.lead_mask = 0;
@@ -1719,8 +1760,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         }
         return 0;
       };
-      uint64_t tq1 = __builtin_ia32_rdtsc();
-      pcy[0] += tq1 - tq0;
       e.term_begin = int32_t(tp);
       e.nreq = r.num_req;
       if (add_terms(r.req_col, r.req_val, r.num_req, &e.req_mask)) {
@@ -1733,14 +1772,10 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         if (errs[ch].first == SIZE_MAX) errs[ch] = {i, "leader columns"};
         continue;
       }
-      uint64_t tq2 = __builtin_ia32_rdtsc();
-      pcy[1] += tq2 - tq1;
       h_sig[i] = sig_hash(e);
       h_cls[i] = h_sig[i] ^ (mask_hash(e) * 0xff51afd7ed558ccdull);
       req_fast[i] = fast_lfc(e) ? 1 : 0;
       req_leaf[i] = e.requested_level == s.L - 1 ? 1 : 0;
-      uint64_t tq3 = __builtin_ia32_rdtsc();
-      pcy[2] += tq3 - tq2;
       // this part's classes (first member in request order), exact compare on a hash hit
       PartClasses& pc = c->part_cls[ch];
       int32_t k = -1;
@@ -1761,14 +1796,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         *head = k;
       }
       req_local_cls[i] = k;
-      pcy[3] += __builtin_ia32_rdtsc() - tq3;
     }
   });
-  if (getenv("KTAS_PROF_RECORDS")) {
-    for (size_t t = 0; t < nparts && t < 8; t++)
-      fprintf(stderr, "part %zu: fill %lu terms %lu hash %lu cls %lu (kcycles)\n", t, prof_cyc[t][0] / 1000,
-              prof_cyc[t][1] / 1000, prof_cyc[t][2] / 1000, prof_cyc[t][3] / 1000);
-  }
   for (auto& e : errs)
     if (e.first != SIZE_MAX) return fail(c, KUEUE_TAS_EINVAL, e.second);
   c->host_ms[7] += wall_ms() - t_b;
@@ -1816,7 +1845,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     std::vector<int32_t>& sig_next = c->sig_next;
     cls_next.clear();
     sig_next.clear();
-    const uint64_t tm0 = __builtin_ia32_rdtsc();
     // the parts' classes merged in part order: a global class is numbered by
     // its first member, as a serial pass over the requests would number it
     std::vector<int32_t>& part_map = c->part_map;  // (part, local class) -> global class
@@ -1888,13 +1916,9 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
       }
       part_map[part_base[t] + j] = k;
     }
-    const uint64_t tm1 = __builtin_ia32_rdtsc();
     for (size_t t = 0; t < nparts; t++)
       for (size_t i = ktas_pool::HostPool::part_begin(n, t, nparts); i < ktas_pool::HostPool::part_begin(n, t + 1, nparts); i++)
         cls_of[i] = part_map[part_base[t] + size_t(req_local_cls[i])];
-    if (getenv("KTAS_PROF_RECORDS"))
-      fprintf(stderr, "merge: part reps %zu, merge %lu kcyc, cls_of %lu kcyc\n", part_base[nparts], (tm1 - tm0) / 1000,
-              (__builtin_ia32_rdtsc() - tm1) / 1000);
     trace(5);
     const int ncls = int(cls_rep.size());
     // representative: the first fast-LFC member if any (its class gets an LFC table slot)
@@ -2044,11 +2068,22 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   c->chunk_alias.assign(n, 0);  // filled with the fill records below
   // ---- device buffers ----
   const int64_t SD = s.SD;
-  const int64_t ctr_stride = 5 * SD;
+  const int64_t ctr_stride = 5 * SD;  // a leader class's row; leaderless rows hold 2 fields, simple ones 1
   int64_t lcap = int64_t(c->maxD) * 2 + 64;
   const int64_t scratch_stride = 6 * lcap;
   const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
-  HIPCHK(c, c->d_counters.ensure(size_t(std::max(nfill, 1)) * size_t(ctr_stride)));  // one row per class
+  {  // one row per class (fill position), sized by its kind (FillEvalParams::ctr_row)
+    c->ctr_row_off.resize(size_t(std::max(nfill, 1)) + 1);
+    int64_t at = 0;
+    for (int pos = 0; pos < nfill; pos++) {
+      const DevEval& ev = hev[h_fill[pos]];
+      c->ctr_row_off[size_t(pos)] = int32_t(at);
+      at += (ev.flags & KUEUE_TAS_F_LEADER) ? 5 : simple_class(ev, s.L) ? 1 : 2;
+    }
+    if (at * SD > (int64_t(1) << 40)) return fail(c, KUEUE_TAS_EINVAL, "class rows exceed the device");
+    c->ctr_row_off[size_t(nfill)] = int32_t(at);
+    HIPCHK(c, c->d_counters.ensure(size_t(std::max<int64_t>(at, 1)) * size_t(SD)));
+  }
   // overlay, tags and scratch lists per BestFit-side select slot (fast-LFC
   // evals never mutate or walk lists): sized by nbf, not n
   const size_t nph2 = size_t(std::max(nbf, 1));
@@ -2157,8 +2192,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         memset(&r, 0, sizeof r);
         FillEvalParams& P = r.p;
         P.eid = h_fill[pos];
-        P.pad2[0] = c->cls_slot[size_t(c->cls_order[size_t(pos)])];  // fast-LFC table slot, -1: none
-        P.pad2[1] = 0;
+        P.lfc_slot = c->cls_slot[size_t(c->cls_order[size_t(pos)])];  // fast-LFC table slot, -1: none
         P.taint_off = ev.taint_table;
         P.nsel = ev.nsel;
         P.slice_size = ev.slice_size;
@@ -2176,11 +2210,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         }
         P.sx_begin = ev.sx_begin;
         P.sx_end = ev.sx_end;
-        {  // a simple class: sliceState == state at every level, its row's sliceState field aliases state
-          bool simple = (ev.flags & KUEUE_TAS_F_LEADER) == 0 && ev.slice_level == s.L - 1 && ev.slice_size == 1;
-          for (int l = 0; l < s.L && simple; l++) simple = ev.ssal[l] == 0 || ev.ssal[l] == 1;
-          P.ss_alias = simple ? 1 : 0;
-        }
+        P.ss_alias = simple_class(ev, s.L) ? 1 : 0;
+        P.ctr_row = c->ctr_row_off[size_t(pos)];
         if (ev.sx_begin >= 0) P.sel_far = 1;
         {  // the packed nodeSelector compare (FillEvalParams::sel_fast)
           uint32_t m[2] = {0u, 0u}, w[2] = {0u, 0u};
@@ -2274,7 +2305,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.cls_members = nullptr;
   b.rack_fanout = 0;
   b.rack_pos = nullptr;
-  b.ctr_stride = ctr_stride;
+  b.ctr_sd = SD;
   b.ov_stride = ov_stride;
   b.counters = c->d_counters.p;
   b.overlay = c->d_overlay.p;
@@ -2836,7 +2867,7 @@ int kueue_tas_last_counters(kueue_tas_ctx* c, size_t i, int32_t* out, size_t cap
   if (cap < 5 * total) return fail(c, KUEUE_TAS_EOVERFLOW, "counters buffer too small");
   HIPCHK(c, hipSetDevice(c->device));
   const size_t k = i - c->chunk_base;
-  const int32_t* rep = c->d_counters.p + int64_t(c->chunk_rep[k]) * 5 * s.SD;
+  const int32_t* rep = c->d_counters.p + int64_t(c->ctr_row_off[size_t(c->chunk_rep[k])]) * s.SD;
   const bool leader = c->chunk_leader[k] != 0;
   for (int f = 0; f < 5; f++) {
     // phase 1 writes the leader fields only for leader requests; otherwise
@@ -2872,7 +2903,7 @@ int kueue_tas_snapshot_set_leaf_tags(kueue_tas_ctx* c, const uint64_t* tags, siz
   }
   if (n != size_t(c->snap.N)) return fail(c, KUEUE_TAS_EINVAL, "leaf tags: n must be the snapshot's leaf count");
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, c->d_leaf_tags.ensure(std::max<size_t>(n, 1)));
+  HIPCHK(c, c->d_leaf_tags.reserve(std::max<size_t>(n, 1)));
   if (n) HIPCHK(c, hipMemcpyAsync(c->d_leaf_tags.p, tags, n * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->leaf_tags_on = true;

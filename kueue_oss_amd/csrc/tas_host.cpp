@@ -1122,8 +1122,13 @@ class FlavorSnapshot {
     NodeInfo& cur = nodes[ix->second];
     const int32_t leaf = leafById.at(nodeToLeaf.at(ni.name));
     // a hostname shared by two nodes: the leaf's taints and labels are the
-    // first node's in cache order (tas_flavor.go:165-191) — rebuilt
-    if (lowestIsHostname && leafNodeNames[size_t(leaf)].size() > 1) return false;
+    // first node's in cache order (leafDomain.node, tas_flavor_snapshot.go:
+    // 160-195); an event on that node is rebuilt, one on any later node
+    // touches the leaf's capacity only
+    if (lowestIsHostname && leafNodeNames[size_t(leaf)].size() > 1) {
+      if (leafNode[size_t(leaf)] == &cur) return false;
+      return later_host_node_event(std::move(ni), member, ix, leaf, ready, unsched, touched, liveChanged);
+    }
     bool moved = false;  // a member at another topology position: leaves, then joins there
     for (auto& l : levelKeys) {
       auto a = ni.labels.find(l), b = cur.labels.find(l);
@@ -1183,8 +1188,19 @@ class FlavorSnapshot {
     else
       for (size_t k = 0; k < lv.size(); k++) id += (k ? "," : "") + lv[k];
     if (const int32_t leaf = leafById.find(id); leaf >= 0) {
-      if (lowestIsHostname || values[size_t(L - 1)][size_t(leaf)] != lv) return false;
-      sync_node(ni, true, false);  // another node of an aggregated leaf
+      if (lowestIsHostname) {
+        // another node under a leaf's hostname: addNode finds the leaf and
+        // only adds capacity (tas_flavor_snapshot.go:160-195) when the leaf's
+        // node stays the first in cache order — the joining node is appended
+        // to the cache unless it was there already (a non-member becoming
+        // one); a dead leaf would take this node's attributes: both rebuilt
+        if (leafDead[size_t(leaf)] || leafNodeNames[size_t(leaf)].empty()) return false;
+        auto mine = nodeOrderPos.find(ni.name);
+        if (mine != nodeOrderPos.end() && mine->second < nodeOrderPos.at(leafNode[size_t(leaf)]->name)) return false;
+      } else if (values[size_t(L - 1)][size_t(leaf)] != lv) {
+        return false;
+      }
+      sync_node(ni, true, false);  // another node of the leaf
       nodes.push_back(std::move(ni));
       const NodeInfo& nd = nodes.back();
       nodeIdx[nd.name] = nodes.size() - 1;
@@ -1211,6 +1227,37 @@ class FlavorSnapshot {
     (void)touched;
     (void)liveChanged;
     return true;
+  }
+  // An event on a node of a hostname leaf that is not the leaf's first node
+  // (a capacity-only member, add_node): it stays (allocatable, labels and
+  // taints of its own, which the leaf does not read), or leaves the leaf —
+  // and joins another hostname's leaf if it is still a member.
+  bool later_host_node_event(NodeInfo&& ni, bool member, std::unordered_map<std::string, size_t>::iterator ix,
+                             int32_t leaf, bool ready, bool unsched, std::set<int32_t>* touched,
+                             std::set<int32_t>* liveChanged) {
+    NodeInfo& cur = nodes[ix->second];
+    const bool renamed = ni.labels.at(kHostname) != leafId[size_t(leaf)];
+    if (member && !renamed) {
+      sync_node(ni, true, false);
+      nodeCache[ni.name] = ni;
+      cur.labels = std::move(ni.labels);
+      cur.taints = std::move(ni.taints);
+      cur.allocatable = std::move(ni.allocatable);
+      realloc_leaf(leaf);
+      touched->insert(leaf);
+      return true;
+    }
+    auto& names = leafNodeNames[size_t(leaf)];
+    names.erase(std::find(names.begin(), names.end(), ni.name));
+    nodeToLeaf.erase(ni.name);
+    nodeIdx.erase(ix);
+    realloc_leaf(leaf);
+    touched->insert(leaf);
+    if (!member) {
+      sync_node(std::move(ni), ready, unsched);
+      return true;
+    }
+    return add_node(std::move(ni), touched, liveChanged);
   }
   // Nodes joining at new topology positions, merged into the tree together
   // (flush_joins) — before the next event that reads the tree, and at the

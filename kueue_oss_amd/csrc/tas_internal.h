@@ -163,7 +163,7 @@ struct DevBatch {
   int32_t rack_fanout;     // the staged fill also rolls up the leaves' parents: > 0 uniform power-of-two
                            // fan-out, -1 ragged (DevSnap::wave_tab), 0 no
   uint64_t* rack_pos;      // [nfill][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rows)
-  int64_t ctr_stride;      // int32 elements per class row (5 * SD)
+  int64_t ctr_sd;          // SD: a class row's field stride (rows at FillEvalParams::ctr_row * SD)
   int64_t ov_stride;       // int32 elements per phase-2 overlay slot: 5 * SD, or 2 * SD when no eval of the
                            // batch has a leader (only state and sliceState are written then)
   int32_t* counters;       // [nfill][5][SD]: one row per phase-1 class, in fill order (row = fill position)

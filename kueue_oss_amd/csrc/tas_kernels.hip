@@ -452,6 +452,67 @@ __device__ __forceinline__ int32_t count_in_regs(const DevTerm* terms, int nt, u
 __device__ __forceinline__ Key key_min2(const Key& a, const Key& b) { return key_lt(b, a) ? b : a; }
 __device__ __forceinline__ Key key_max2(const Key& a, const Key& b) { return key_lt(a, b) ? b : a; }
 
+// Per-eval parameters of a fill chunk, staged in LDS once per block so the
+// per-eval loop has no dependent global loads (eval record -> taint row).
+// The fields the per-eval loop reads come first, in 16-byte groups: the loop
+// fetches them with three ds_read_b128 and one wait (not one LDS round trip
+// per field), the selector pairs with four more when the eval has selectors.
+struct alignas(16) FillEvalParams {
+  int32_t eid, nsel, slice_size, slice_level;
+  int32_t inner, sel_far, aff_begin, aff_end;  // inner: ssal of the leaf level; sel_far: a nodeSelector
+                                               // column beyond the kStagedLabels held in registers;
+                                               // aff_begin < 0: no required node affinity
+  int32_t dom_begin, dom_end, taint_off, sig_new;  // replacement domain leaf range (dom_begin < 0: none);
+                                                   // sig_new 1: first position of its signature run
+  int32_t run, rmask, lmask, sx_begin;  // signature run (DevBatch::fill_run); the run's worker / leader column
+                                        // masks; nodeSelector requirements beyond the inline pairs (-1: none)
+  int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
+  int32_t sx_end, pad[3];
+  // the nodeSelector as one masked compare of the leaf's packed staged label
+  // ids (fill_pair_kernel): column c < kStagedLabels is the 16-bit field c of
+  // the 64-bit key; sel_fast 1 when every pair is a staged column and every
+  // staged column's ids fit 16 bits (kueue_tas_ctx::labels16), else the loop
+  // over sel_col / sel_val.  A pair whose value id no leaf has, or two pairs
+  // on one column with different values, set a want bit outside the mask
+  // (never equal: every leaf mismatches, as labels.SelectorFromSet does).
+  uint32_t sel_mlo, sel_mhi, sel_wlo, sel_whi;
+  int32_t sel_fast;
+  // 1: the class is simple (no leader, one-pod slices at the leaf level, no
+  // inner slice rounding), so its sliceState equals its state at every level
+  // and the class row's sliceState field is not stored: every reader takes
+  // the state field instead (ss_off)
+  int32_t ss_alias;
+  int32_t lfc_slot;  // the class's fast-LFC table slot, -1: none
+  int32_t ctr_row;   // the class row's offset in DevBatch::counters, in units of SD int32s: rows
+                     // hold 1 field (simple), 2 (state, sliceState) or 5 (and the leader fields)
+};
+static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
+constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
+constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
+
+// Everything fill_pair_kernel needs about one fill position, built by the
+// host in fill order (DevBatch::fill_pos): the parameters (pad[0] = the
+// chunk's base flags, pad[1..2] = its assumed-usage range), the eval's
+// taint-profile row and its run's worker | leader terms.  A block copies its
+// chunk's records into LDS with one coalesced pass: one memory round trip
+// instead of the chain chunk -> eval ids -> eval records -> rows / terms.
+constexpr int kPosTerms = 16;  // 2 * the largest staged column count
+struct alignas(16) FillPos {
+  FillEvalParams p;
+  int32_t taint[kStagedProfiles];
+  DevTerm term[kPosTerms];
+};
+static_assert(sizeof(FillPos) % 16 == 0, "FillPos is copied as int4");
+// Offset of the sliceState field in a class row (counters[row]): SD, or 0
+// for a simple class whose sliceState is its state (FillEvalParams::ss_alias).
+__device__ __forceinline__ int64_t ss_off(const DevBatch& b, int row, int64_t SD) {
+  return b.fill_pos[row].p.ss_alias ? 0 : SD;
+}
+// The class row of fill position `row` (FillEvalParams::ctr_row).
+__device__ __forceinline__ int32_t* ctr_base(const DevBatch& b, int row) {
+  return b.counters + int64_t(b.fill_pos[row].p.ctr_row) * b.ctr_sd;
+}
+
 template <int MAXT>
 __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, DevBatch b) {
 
@@ -590,7 +651,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
       }
     }
     if (valid) {
-      int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
+      int32_t* base = ctr_base(b, e0 + e);  // the class's row: its fill position
       const int64_t SD = s.SD;
       int32_t ss = 0, sswl = 0;
       if (s.L - 1 == ev.slice_level) {
@@ -598,7 +659,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
         sswl = go_div32(swl, ev.slice_size);
       }
       base[gleaf] = state;
-      base[SD + gleaf] = ss;
+      if (b.fill_pos[e0 + e].p.ss_alias == 0) base[SD + gleaf] = ss;
       if (leader) {
         base[2 * SD + gleaf] = swl;
         base[3 * SD + gleaf] = sswl;
@@ -644,59 +705,6 @@ __global__ __launch_bounds__(kFillThreads) void fill_leaves_kernel(DevSnap s, De
 // them), so CountInWithLimitingResource runs once per leaf and only the
 // per-eval masks (taints, nodeSelector) and slice parameters differ.
 // Semantics identical to fill_leaves_kernel.
-// Per-eval parameters of a fill chunk, staged in LDS once per block so the
-// per-eval loop has no dependent global loads (eval record -> taint row).
-// The fields the per-eval loop reads come first, in 16-byte groups: the loop
-// fetches them with three ds_read_b128 and one wait (not one LDS round trip
-// per field), the selector pairs with four more when the eval has selectors.
-struct alignas(16) FillEvalParams {
-  int32_t eid, nsel, slice_size, slice_level;
-  int32_t inner, sel_far, aff_begin, aff_end;  // inner: ssal of the leaf level; sel_far: a nodeSelector
-                                               // column beyond the kStagedLabels held in registers;
-                                               // aff_begin < 0: no required node affinity
-  int32_t dom_begin, dom_end, taint_off, sig_new;  // replacement domain leaf range (dom_begin < 0: none);
-                                                   // sig_new 1: first position of its signature run
-  int32_t run, rmask, lmask, sx_begin;  // signature run (DevBatch::fill_run); the run's worker / leader column
-                                        // masks; nodeSelector requirements beyond the inline pairs (-1: none)
-  int32_t sel_col[KUEUE_TAS_MAX_SELECTORS], sel_val[KUEUE_TAS_MAX_SELECTORS];
-  int32_t sx_end, pad[3];
-  // the nodeSelector as one masked compare of the leaf's packed staged label
-  // ids (fill_pair_kernel): column c < kStagedLabels is the 16-bit field c of
-  // the 64-bit key; sel_fast 1 when every pair is a staged column and every
-  // staged column's ids fit 16 bits (kueue_tas_ctx::labels16), else the loop
-  // over sel_col / sel_val.  A pair whose value id no leaf has, or two pairs
-  // on one column with different values, set a want bit outside the mask
-  // (never equal: every leaf mismatches, as labels.SelectorFromSet does).
-  uint32_t sel_mlo, sel_mhi, sel_wlo, sel_whi;
-  int32_t sel_fast;
-  // 1: the class is simple (no leader, one-pod slices at the leaf level, no
-  // inner slice rounding), so its sliceState equals its state at every level
-  // and the class row's sliceState field is not stored: every reader takes
-  // the state field instead (ss_off)
-  int32_t ss_alias, pad2[2];
-};
-static_assert(KUEUE_TAS_MAX_SELECTORS == 8, "selector pairs are fetched as two int4 each");
-constexpr int kFillTilesPerBlock = 1;  // leaf tiles of one staged-fill block
-constexpr int kStagedProfiles = 32;  // taint-profile rows staged in LDS (more: read from global)
-
-// Everything fill_pair_kernel needs about one fill position, built by the
-// host in fill order (DevBatch::fill_pos): the parameters (pad[0] = the
-// chunk's base flags, pad[1..2] = its assumed-usage range), the eval's
-// taint-profile row and its run's worker | leader terms.  A block copies its
-// chunk's records into LDS with one coalesced pass: one memory round trip
-// instead of the chain chunk -> eval ids -> eval records -> rows / terms.
-constexpr int kPosTerms = 16;  // 2 * the largest staged column count
-struct alignas(16) FillPos {
-  FillEvalParams p;
-  int32_t taint[kStagedProfiles];
-  DevTerm term[kPosTerms];
-};
-static_assert(sizeof(FillPos) % 16 == 0, "FillPos is copied as int4");
-// Offset of the sliceState field in a class row (counters[row]): SD, or 0
-// for a simple class whose sliceState is its state (FillEvalParams::ss_alias).
-__device__ __forceinline__ int64_t ss_off(const DevBatch& b, int row, int64_t SD) {
-  return b.fill_pos[row].p.ss_alias ? 0 : SD;
-}
 constexpr int kStagedLabels = 4;     // label columns held in registers (more: read from global)
 
 // ExclusionStats of a fill block are counted in LDS and written as per-block
@@ -1004,11 +1012,11 @@ __global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(NS == 5 && !GL ? 5 
         sswl = leader ? go_div32(swl, slice_size) : ss;
       }
     }
-    int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
+    int32_t* base = ctr_base(b, e0 + e);  // the class's row: its fill position
     const int64_t SD = s.SD;
     if (valid) {
       base[gleaf] = state;
-      base[SD + gleaf] = ss;
+      if (b.fill_pos[e0 + e].p.ss_alias == 0) base[SD + gleaf] = ss;
       if (leader) {
         base[2 * SD + gleaf] = swl;
         base[3 * SD + gleaf] = sswl;
@@ -1060,7 +1068,7 @@ __global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(NS == 5 && !GL ? 5 
         }
         const int g = s.level_off[s.L - 2] + parent;
         base[g] = cap;
-        base[SD + g] = slc;
+        if (b.fill_pos[e0 + e].p.ss_alias == 0) base[SD + g] = slc;
         if (leader) {
           base[2 * SD + g] = pswl;
           base[3 * SD + g] = psswl;
@@ -1109,7 +1117,7 @@ __global__ __launch_bounds__(kFillThreads) KTAS_WAVES_PER_EU(NS == 5 && !GL ? 5 
         }
         const int g = s.level_off[s.L - 2] + rparent;
         base[g] = cap;
-        base[SD + g] = slc;
+        if (b.fill_pos[e0 + e].p.ss_alias == 0) base[SD + g] = slc;
         if (leader) {
           base[2 * SD + g] = pswl;
           base[3 * SD + g] = psswl;
@@ -1645,13 +1653,11 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     const bool has_par = rack_f > 0 && valid[0] && parent < lsz && b.rack_pos != nullptr;
     const uint64_t pA = (valid[0] && state0[0] > 0) ? 1ull << (kPairLP * gpos) : 0ull;
     const uint64_t pB = (valid[1] && state0[1] > 0) ? 2ull << (kPairLP * gpos) : 0ull;
-    const int64_t cst = b.ctr_stride;
-    int32_t* rowp = b.counters + int64_t(e0) * cst;
     uint64_t* rpp = b.rack_pos ? b.rack_pos + int64_t(e0) * lsz + parent : nullptr;
     // fast-LFC chunk tables from the fill: the wave's (category, value) pairs
     bool lfc_any = false;
     if (b.lfc_fill)
-      for (int e = 0; e < ne; e++) lfc_any = lfc_any || sh_pos[e].p.pad2[0] >= 0;
+      for (int e = 0; e < ne; e++) lfc_any = lfc_any || sh_pos[e].p.lfc_slot >= 0;
     if (lfc_any) {
       const int wv = int(threadIdx.x >> 6);
       const bool a0 = valid[0] && state0[0] > 0, a1 = valid[1] && state0[1] > 0;
@@ -1675,13 +1681,14 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       if (lane == 0) sh_tn[wv] = nt;
     }
     const int lfc_chunk = (tile * kPairTile) / kLfcChunk;  // the block's leaves lie in one LFC chunk
-    for (int e = 0; e < ne; e++, rowp += cst, rpp += lsz) {
+    for (int e = 0; e < ne; e++, rpp += lsz) {
+      int32_t* const rowp = b.counters + int64_t(sh_pos[e].p.ctr_row) * b.ctr_sd;
       const uint64_t pm = sh_passd[2 * e];
       const int32_t m0 = int32_t(uint32_t(pm >> did[0]) << 31) >> 31;
       const int32_t m1 = int32_t(uint32_t(pm >> did[1]) << 31) >> 31;
       const int32_t st0 = state0[0] & m0, st1 = state0[1] & m1;
       if (lfc_any) {
-        const int lslot = sh_pos[e].p.pad2[0];  // block-uniform
+        const int lslot = sh_pos[e].p.lfc_slot;  // block-uniform
         if (lslot >= 0) {  // the byte copy of the class's leaf values (lfc_emit_kernel)
           uint8_t* u8 = b.lfc_u8 + int64_t(lslot) * b.lfc_nchunks * kLfcChunk + leaf0;
           const uint32_t c0 = uint32_t(min(st0, 255)), c1 = uint32_t(min(st1, 255));
@@ -1715,7 +1722,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
       const int wv = int(threadIdx.x >> 6);
       const int nvalid = min(kPairTile, N - tile * kPairTile);
       for (int e = wv; e < ne; e += kFillThreads / kWave) {
-        const int lslot = sh_pos[e].p.pad2[0];
+        const int lslot = sh_pos[e].p.lfc_slot;
         if (lslot < 0) continue;
         const uint64_t pm = sh_passd[2 * e];
         uint32_t* ch = b.lfc_ch + (int64_t(lslot) * b.lfc_nchunks + lfc_chunk) * kLfcBins;
@@ -1888,7 +1895,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         }
       }
     }
-    int32_t* base = b.counters + int64_t(e0 + e) * b.ctr_stride;  // the class's row: its fill position
+    int32_t* base = ctr_base(b, e0 + e);  // the class's row: its fill position
     auto storev = [&](int64_t off, const int32_t (&v)[kPairLP]) {  // counter words of leaves leaf0 .. leaf0 + kPairLP - 1
       if (full_tile) {
         if constexpr (kPairLP == 4) *reinterpret_cast<int4*>(base + off + gleaf0) = make_int4(v[0], v[1], v[2], v[3]);
@@ -1905,7 +1912,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     storev(0, state);
     if (!alias) storev(SD, ss);
     if (b.lfc_fill) {  // a fast-LFC slot class (always simple: its values are state)
-      const int lslot = uni(sh_pos[e].p.pad2[0]);
+      const int lslot = uni(sh_pos[e].p.lfc_slot);
       if (lslot >= 0) {
         const int lv[kPairLP] = {leaf0, leaf0 + 1};
         lfc_fill_accum(b, lslot, state, lv, valid, kPairLP);
@@ -1982,7 +1989,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
         }
         const int g = s.level_off[s.L - 2] + parent;
         base[g] = cap2;
-        base[SD + g] = slc;
+        if (!alias) base[SD + g] = slc;
         if (leader) {
           base[2 * SD + g] = pswl;
           base[3 * SD + g] = psswl;
@@ -2159,7 +2166,7 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
 __global__ __launch_bounds__(256) void wide_parents_zero_kernel(DevSnap s, DevBatch b) {
   const int row = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= b.nfill || i >= s.n_wide) return;
-  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  int32_t* base = ctr_base(b, row);
   const int g = s.level_off[s.L - 2] + s.wide_parents[i];
   base[g] = 0;
   if (!b.fill_pos[row].p.ss_alias) base[s.SD + g] = 0;
@@ -2169,7 +2176,7 @@ __global__ __launch_bounds__(256) void wide_parents_finish_kernel(DevSnap s, Dev
   if (row >= b.nfill || i >= s.n_wide) return;
   const FillEvalParams& P = b.fill_pos[row].p;
   if (P.slice_level != s.L - 2 || P.ss_alias) return;
-  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  int32_t* base = ctr_base(b, row);
   const int g = s.level_off[s.L - 2] + s.wide_parents[i];
   base[s.SD + g] = go_div32(base[g], P.slice_size);
 }
@@ -2347,7 +2354,7 @@ __device__ __forceinline__ void rollup_parent(const DevSnap& s, const DevBatch& 
   const bool hasInner = inner != 0;
   const int cb = s.child_off[s.child_base[level] + p];
   const int ce = s.child_off[s.child_base[level] + p + 1];
-  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  int32_t* base = ctr_base(b, row);
   const int64_t SD = s.SD;
   const int64_t SSO = ss_off(b, row, SD);
   const int coff = s.level_off[cl];
@@ -2430,7 +2437,7 @@ __global__ __launch_bounds__(256) void rollup_level_wave_kernel(DevSnap s, DevBa
   const int cl = level + 1;
   const int32_t inner = ev.ssal[cl];
   const bool hasInner = inner != 0;
-  int32_t* base = b.counters + int64_t(blockIdx.y) * b.ctr_stride;  // the class's row: its fill position
+  int32_t* base = ctr_base(b, int(blockIdx.y));  // the class's row: its fill position
   const int64_t SD = s.SD;
   const int64_t SSO = ss_off(b, int(blockIdx.y), SD);
   const int coff = s.level_off[cl];
@@ -2507,7 +2514,7 @@ __global__ __launch_bounds__(256) void level_max_kernel(DevSnap s, DevBatch b) {
   const int row = blockIdx.x;  // the class's fill position
   const int l = blockIdx.y;
   const int D = s.level_size[l];
-  const int4* ss4 = reinterpret_cast<const int4*>(b.counters + int64_t(row) * b.ctr_stride + ss_off(b, row, s.SD) + s.level_off[l]);
+  const int4* ss4 = reinterpret_cast<const int4*>(ctr_base(b, row) + ss_off(b, row, s.SD) + s.level_off[l]);
   const int nq = (D + 3) / 4;
   int32_t m = INT32_MIN;
   constexpr int U = 8;
@@ -2621,7 +2628,7 @@ __global__ __launch_bounds__(256) void rollup_top_kernel(DevSnap s, DevBatch b, 
   const int eid = b.fill_ids[row];
   const DevEval& ev = b.evals[eid];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
-  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  int32_t* base = ctr_base(b, row);
   const int64_t SSO = ss_off(b, row, s.SD);
   const int wv = threadIdx.x >> 6;
   int32_t cmax = INT32_MIN;
@@ -2672,7 +2679,7 @@ __global__ __launch_bounds__(256) void rollup_tail_kernel(DevSnap s, DevBatch b,
   const int row = blockIdx.x;  // the class's fill position
   const DevEval& ev = b.evals[b.fill_ids[row]];
   const bool leaderReq = (ev.flags & KUEUE_TAS_F_LEADER) != 0;
-  int32_t* base = b.counters + int64_t(row) * b.ctr_stride;
+  int32_t* base = ctr_base(b, row);
   const int64_t SSO = ss_off(b, row, s.SD);
   const int wv = threadIdx.x >> 6;
   for (int l = top; l >= 0; l--) {
@@ -2734,7 +2741,7 @@ __global__ __launch_bounds__(kFillThreads) void leaf_partials_kernel(DevSnap s, 
     const bool leader = (flags & KUEUE_TAS_F_LEADER) != 0;
     const bool lfc = (flags & KUEUE_TAS_F_LFC) != 0;
     const int32_t sliceCount = go_div32(uni(ev.count), uni(ev.slice_size));
-    const int32_t* base = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
+    const int32_t* base = ctr_base(b, b.rep_of[eid]);
     const int64_t SSO = ss_off(b, b.rep_of[eid], SD);
     int32_t state = 0, ss = 0, swl = 0, sswl = 0, ls = 0;
     if (valid) {
@@ -2810,7 +2817,7 @@ __global__ __launch_bounds__(256) void lfc_hist_kernel(DevSnap s, DevBatch b) {
   for (int i = threadIdx.x; i < kLfcBins; i += blockDim.x) h[i] = 0;
   if (threadIdx.x == 0) ovs = 0;
   __syncthreads();
-  const int32_t* v = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + ss_off(b, b.lfc_rep[slot], s.SD) +
+  const int32_t* v = ctr_base(b, b.lfc_rep[slot]) + ss_off(b, b.lfc_rep[slot], s.SD) +
                      s.level_off[s.L - 1];
   const int lo = chunk * kLfcChunk, hi = min(s.N, lo + kLfcChunk);
   uint64_t mysum = 0;
@@ -5330,7 +5337,7 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.lfc = (ev.flags & KUEUE_TAS_F_LFC) != 0;
   w.bf = !w.lfc;
   w.unconstrained = (ev.flags & KUEUE_TAS_F_UNCONSTRAINED) != 0;
-  w.ctr = b.counters + int64_t(b.rep_of[eid]) * b.ctr_stride;
+  w.ctr = ctr_base(b, b.rep_of[eid]);
   w.rack_pos = (b.rack_fanout && b.rack_pos) ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
   // per-launch-slot phase-2 buffers: the BestFit-side launch numbers its
   // evals 0..nbf-1; fast-LFC evals (the other launch) never touch them
@@ -5523,7 +5530,7 @@ __global__ __launch_bounds__(256) void lfc_emit_kernel(DevSnap s, DevBatch b) {
     const int slot = b.lfc_slot[eid];
     const int t = job.t;
     const int64_t mt = job.m;
-    const int32_t* V = b.counters + int64_t(b.lfc_rep[slot]) * b.ctr_stride + ss_off(b, b.lfc_rep[slot], s.SD) +
+    const int32_t* V = ctr_base(b, b.lfc_rep[slot]) + ss_off(b, b.lfc_rep[slot], s.SD) +
                        s.level_off[s.L - 1];
     const int lo = item.chunk * kLfcChunk + int(threadIdx.x) * 8;
     int32_t x[8];
@@ -5667,6 +5674,32 @@ __global__ void splice_leaves_kernel(const int32_t* gsrc, int n_new, int n_old, 
     if (prof) prof[j] = nprof ? nprof[k0] : 0;
     for (int k = 0; k < K; k++) lab[int64_t(k) * n_new + j] = nlab[int64_t(k) * num_new + k0];
   }
+}
+
+// A load's parent tables from the CSR child offsets (one thread per padded
+// domain slot, a binary search in its parent level's offsets): the global
+// parent id of every domain (-1 for roots and padding; the v1beta2 leaf-mode
+// encoder) and, when asked, each leaf's parent index within its level (the
+// ragged fills' segmented scans).
+__global__ void domain_parents_kernel(DevSnap s, int32_t* parent, int32_t* leaf_parent) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= s.SD) return;
+  int l = 0;
+  while (l + 1 < s.L && g >= s.level_off[l + 1]) l++;
+  const int i = g - s.level_off[l];
+  int p = -1;
+  if (l > 0 && i < s.level_size[l]) {
+    const int32_t* co = s.child_off + s.child_base[l - 1];
+    int lo = 0, hi = s.level_size[l - 1];  // the last parent q with co[q] <= i
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (co[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    p = lo;
+    if (leaf_parent && l == s.L - 1) leaf_parent[i] = p;
+  }
+  parent[g] = p < 0 ? -1 : s.level_off[l - 1] + p;
 }
 
 __global__ void set_leaf_dead_kernel(uint8_t* dead, const int32_t* leaves_live, int n) {

@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_snapshot_set_leaf_live", "kueue_tas_snapshot_set_leaf_tags", "kueue_tas_last_entry_tags",
     "kueue_tas_host_last_host_detail", "kueue_tas_host_last_update_detail", "kueue_tas_eval_batch_ptrs", "kueue_tas_set_stage_timing",
     "kueue_tas_host_set_stage_timing", "kueue_tas_host_stage_accum", "kueue_tas_snapshot_splice", "kueue_tas_snapshot_counters",
+    "kueue_tas_device_bytes",
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
     "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
     "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace", "kueue_tas_merge_reruns",
@@ -149,6 +150,7 @@ def _bind(lib):
     lib.kueue_tas_host_last_update_detail.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.c_int]
     lib.kueue_tas_host_set_stage_timing.argtypes = [c.c_void_p, c.c_int32]
     lib.kueue_tas_snapshot_counters.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
+    lib.kueue_tas_device_bytes.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
                                                c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
@@ -243,12 +245,13 @@ class TASFlavorSnapshot:
                  packed_entries: bool = False, inline_stats: bool = False,
                  pair_fill: bool = True, serial_admit: bool = False, split_stats: bool = False,
                  fused_top: bool = False, host_values: bool = False, category_fill: bool = True,
-                 class_collide: bool = False):
+                 class_collide: bool = False, lfc_in_fill: bool = False):
         self._lib = lib if lib is not None else load_library()
         cfg = KueueTasConfig(list_cap, max_batch, device, (1 if packed_entries else 0) | (2 if inline_stats else 0)
                               | (0 if pair_fill else 4) | (8 if serial_admit else 0) | (16 if split_stats else 0)
                               | (32 if fused_top else 0) | (64 if host_values else 0)
-                              | (0 if category_fill else 128) | (256 if class_collide else 0))
+                              | (0 if category_fill else 128) | (256 if class_collide else 0)
+                              | (512 if lfc_in_fill else 0))
         doc = {k: v for k, v in snapshot.items() if k != "podSets"}
         h = self._lib.kueue_tas_host_create(json.dumps(doc).encode(), ctypes.byref(cfg))
         if not h:
@@ -477,6 +480,13 @@ class TASFlavorSnapshot:
         lo, sp = ctypes.c_int64(), ctypes.c_int64()
         self._lib.kueue_tas_snapshot_counters(self.device_ctx(), ctypes.byref(lo), ctypes.byref(sp))
         return lo.value, sp.value
+
+    def device_bytes(self):
+        """(every device buffer, the per-batch evaluation state) of the device
+        context, in bytes (kueue_tas_device_bytes)."""
+        t, p2 = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.kueue_tas_device_bytes(self.device_ctx(), ctypes.byref(t), ctypes.byref(p2))
+        return t.value, p2.value
 
     def last_results(self) -> list:
         """Results of the last run_compiled, one result list per compiled workload."""

@@ -59,12 +59,14 @@ def test_admission_session_arith_on_gpu():
     _sessions(63, 150, gen=synth.arith_stress_case)
 
 
-def _admit_then_rebuild(make_snap, splice):
+def _admit_then_rebuild(make_snap, mode):
     """kueue_tas_host_admit applies usage on the device and defers the host
-    mirror; a node event that re-assembles the snapshot — a splice of a new
-    leaf (splice=True) or a rebuild (a second node under an existing
-    hostname) — must see every admitted record (the oracle rebuilt from a
-    document holding that usage)."""
+    mirror; a node event that re-assembles the snapshot must see every
+    admitted record (the oracle rebuilt from a document holding that usage):
+    a splice of a new leaf ("splice"), a second node under an existing
+    hostname (capacity only, in place: "same-host"), and a rebuild (an update
+    of the first node of such a hostname, whose taints and labels are the
+    leaf's: "rebuild")."""
     import copy
 
     snap_doc, wls = synth.config_c2(n_workloads=24, shape=(2, 2, 4, 8))
@@ -80,30 +82,36 @@ def _admit_then_rebuild(make_snap, splice):
             want_doc.setdefault("tasUsage", []).extend(synth.usage_records(wls[i], res[i]))
     extra = copy.deepcopy(snap_doc["nodes"][0])
     extra["name"] = "added-node"
-    if splice:  # a node with a new rack: spliced into the tree in place
+    if mode == "splice":  # a node with a new rack: spliced into the tree in place
         for k in list(extra["labels"]):
             if k != "kubernetes.io/hostname":
                 extra["labels"][k] = extra["labels"][k] + "-x"
         extra["labels"]["kubernetes.io/hostname"] = "added-node"
-    # else: the first node's hostname — leafDomain.node stays the first node,
-    # the snapshot is rebuilt
+    # else: the first node's hostname — leafDomain.node stays the first node
     want_doc["nodes"].append(extra)
-    assert snap.update_nodes([extra]) is (not splice)
+    c0 = snap.snapshot_counters()
+    assert snap.update_nodes([extra]) is False
+    assert snap.snapshot_counters()[0] == c0[0]  # no device reload
+    if mode == "rebuild":
+        first = copy.deepcopy(snap_doc["nodes"][0])
+        first["labels"]["extra-label"] = "x"
+        want_doc["nodes"][0] = first
+        assert snap.update_nodes([first]) is True
     got = snap.find_topology_assignments_for_workloads(wls)
     snap.close()
     want, _ = oracle_lib.eval_workloads(want_doc, wls, threads=4)
     assert got == want
 
 
-@pytest.mark.parametrize("splice", [True, False])
-def test_emulated_admit_then_rebuild(emu_lib, splice):  # noqa: F811
-    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d, lib=emu_lib), splice)
+@pytest.mark.parametrize("mode", ["splice", "same-host", "rebuild"])
+def test_emulated_admit_then_rebuild(emu_lib, mode):  # noqa: F811
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d, lib=emu_lib), mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("splice", [True, False])
-def test_admit_then_rebuild_on_gpu(splice):
-    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d), splice)
+@pytest.mark.parametrize("mode", ["splice", "same-host", "rebuild"])
+def test_admit_then_rebuild_on_gpu(mode):
+    _admit_then_rebuild(lambda d: TASFlavorSnapshot(d), mode)
 
 
 def _admit_relayout_apply(make_snap):

@@ -54,12 +54,14 @@ def _configs(scale):
     yield "c3j multi-run", *synth.config_c3j(seed=13, n_workloads=2 * n, shape=(2, 2, 4 * scale))
 
 
-def _run(make_pair, make_staged, scale, make_percls=None):
+def _run(make_pair, make_staged, scale, make_percls=None, make_lfc=None):
     for name, doc, wls in _configs(scale):
         paths = _batch(make_pair, doc, wls)
         assert paths & PAIR, name
         assert paths & CATEGORY or name != "c3 fan-out 32", name
-        assert paths & LFC_FILL or name != "c3 fan-out 32", name
+        assert paths & LFC_FILL == 0, name  # lfc_hist_kernel by default
+        if make_lfc is not None:
+            assert _batch(make_lfc, doc, wls) & LFC_FILL or name != "c3 fan-out 32", name
         assert _batch(make_staged, doc, wls) & (PAIR | CATEGORY) == 0, name
         if make_percls is not None:
             assert _batch(make_percls, doc, wls) & (PAIR | CATEGORY) == PAIR, name
@@ -119,15 +121,18 @@ def _many_categories(make, scale):
 
 def test_emulated_pair_fill(emu_lib):  # noqa: F811
     _run(lambda d: TASFlavorSnapshot(d, lib=emu_lib), lambda d: TASFlavorSnapshot(d, lib=emu_lib, pair_fill=False, fused_top=True), 1,
-         lambda d: TASFlavorSnapshot(d, lib=emu_lib, category_fill=False))
+         lambda d: TASFlavorSnapshot(d, lib=emu_lib, category_fill=False),
+         lambda d: TASFlavorSnapshot(d, lib=emu_lib, lfc_in_fill=True))
     assert _random(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 31, 40) & PAIR
     # lean and per-leaf blocks of one launch accumulate the LFC tables together
-    assert _many_categories(lambda d: TASFlavorSnapshot(d, lib=emu_lib), 1) & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL
+    assert _many_categories(lambda d: TASFlavorSnapshot(d, lib=emu_lib, lfc_in_fill=True), 1) \
+        & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL
 
 
 @pytest.mark.gpu
 def test_pair_fill_on_gpu():
     _run(lambda d: TASFlavorSnapshot(d), lambda d: TASFlavorSnapshot(d, pair_fill=False, fused_top=True), 4,
-         lambda d: TASFlavorSnapshot(d, category_fill=False))
+         lambda d: TASFlavorSnapshot(d, category_fill=False), lambda d: TASFlavorSnapshot(d, lfc_in_fill=True))
     assert _random(lambda d: TASFlavorSnapshot(d), 32, 150) & PAIR
-    assert _many_categories(lambda d: TASFlavorSnapshot(d), 4) & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL
+    assert _random(lambda d: TASFlavorSnapshot(d, lfc_in_fill=True), 33, 100) & PAIR
+    assert _many_categories(lambda d: TASFlavorSnapshot(d, lfc_in_fill=True), 4) & (CATEGORY | LFC_FILL) == CATEGORY | LFC_FILL

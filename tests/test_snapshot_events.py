@@ -81,7 +81,9 @@ def node_events(rng, ref, n):
                 nd["unschedulable"] = True
         elif r < 0.9:
             nd["name"] = f"new-node-{k}-{rng.randint(0, 1 << 20)}"
-            if "kubernetes.io/hostname" in nd["labels"]:
+            # a third of new nodes join under the copied node's hostname (one
+            # leaf, capacity only: leafDomain.node stays the first node)
+            if "kubernetes.io/hostname" in nd["labels"] and rng.random() < 0.66:
                 nd["labels"]["kubernetes.io/hostname"] = nd["name"]
         else:
             lvl = rng.choice(levels)
