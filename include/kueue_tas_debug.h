@@ -63,6 +63,11 @@ int kueue_tas_last_host_trace(kueue_tas_ctx* ctx, double* ms, int n);
  * merge's verification failed (a 64-bit class hash collision, or
  * KUEUE_TAS_CFG_CLASS_COLLIDE), over the context's lifetime. */
 int64_t kueue_tas_merge_reruns(kueue_tas_ctx* ctx);
+/* The BestFit-side select's slot groups in the last chunk (launches whose
+ * lists, overlays and tags fit the phase-2 budget; 1 within budget) and the
+ * lifetime count of chunks re-run with unbounded select lists after a
+ * bounded list overflowed. */
+int kueue_tas_select_groups(kueue_tas_ctx* ctx, int64_t* last_groups, int64_t* scratch_reruns);
 
 /* Work counters of the last kueue_tas_eval_batch: [0] evals whose phase 1
  * (fill + roll-up) ran (one per distinct phase-1 input), [1] evals with
@@ -102,7 +107,8 @@ int kueue_tas_set_stage_timing(kueue_tas_ctx* ctx, int32_t on);
 int kueue_tas_snapshot_counters(kueue_tas_ctx* ctx, int64_t* loads, int64_t* splices);
 /* Device memory held by ctx now: *total every buffer of the context,
  * *phase2 the per-batch evaluation state (class counter rows, BestFit
- * overlays and their ownership tags), which scales with the batch. */
+ * select lists, overlays and their ownership tags), which scales with the
+ * batch. */
 int kueue_tas_device_bytes(kueue_tas_ctx* ctx, int64_t* total, int64_t* phase2);
 /* Host-mirror support (the host layer's copy of tasUsage follows the device
  * lazily): _usage_mark records the resident usage columns and presence bits

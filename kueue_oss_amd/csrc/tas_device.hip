@@ -351,6 +351,23 @@ struct kueue_tas_ctx {
   std::vector<MagicCache> magic_cache;  // per host part (compute_magic)
   std::vector<int32_t> h_gsrc;          // a splice's leaf sources (load_impl)
   std::vector<int32_t> ctr_row_off;     // last batch: each fill position's class row offset (units of SD)
+  std::vector<int32_t> level_maxfan;    // [L] the widest parent's child count per level (last load)
+  std::vector<int32_t> sel_groups;      // last batch: BestFit-side slot groups (select launches), bounds
+  bool scratch_full = false;            // this chunk re-runs with unbounded select lists (an eval overflowed)
+  int64_t scratch_reruns = 0;           // chunks re-run so
+  int64_t phase2_budget = [] {          // bytes of select lists + overlays + tags per slot group
+    const char* e = getenv("KTAS_PHASE2_BUDGET");  // (tests: a small budget, many groups)
+    return e ? std::max<int64_t>(atoll(e), 1) : int64_t(4096) << 20;
+  }();
+  bool force_scratch_rerun = getenv("KTAS_SCRATCH_TEST_RERUN") != nullptr;  // tests: every chunk re-runs once
+  int64_t lcap_test_cap = [] {          // tests: bounded lists capped lower (overflows re-run unbounded)
+    const char* e = getenv("KTAS_SCRATCH_TEST_CAP");
+    return e ? std::max<int64_t>(atoll(e), 1) : int64_t(0);
+  }();
+  bool scratch_bounded = [] {           // KTAS_SCRATCH_FULL=1: every slot's lists sized for the widest level
+    const char* e = getenv("KTAS_SCRATCH_FULL");
+    return !(e && atoi(e) != 0);
+  }();
   DevBufLink* dev_bufs = nullptr;       // every DevBuf member (kueue_tas_device_bytes)
   bool exact_merge = false;  // the next chunk merges the parts' classes with exact compares (after a collision)
   int64_t merge_reruns = 0;  // chunks re-run after a class hash collision
@@ -641,6 +658,13 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
     s.child_base[l] = int32_t(nco);
     nco += size_t(d->level_sizes[l]) + 1;
   }
+  c->level_maxfan.assign(size_t(s.L), 1);  // widest parent per level (select scratch bounds)
+  for (int l = 0; l + 1 < s.L; l++) {
+    const int32_t* co = d->child_offsets + s.child_base[l];
+    int32_t f = 1;
+    for (int p = 0; p < d->level_sizes[l]; p++) f = std::max(f, co[p + 1] - co[p]);
+    c->level_maxfan[size_t(l)] = f;
+  }
   HIPCHK(c, c->d_child_off.reserve(nco));
   if (nco) HIPCHK(c, hipMemcpyAsync(c->d_child_off.p, d->child_offsets, nco * 4, hipMemcpyHostToDevice, c->stream));
   s.child_off = c->d_child_off.p;
@@ -901,7 +925,7 @@ int kueue_tas_device_bytes(kueue_tas_ctx* c, int64_t* total, int64_t* phase2) {
   int64_t t = 0;
   for (const DevBufLink* b = c->dev_bufs; b; b = b->next) t += int64_t(b->bytes);
   if (total) *total = t;
-  if (phase2) *phase2 = int64_t(c->d_counters.bytes + c->d_overlay.bytes + c->d_tags.bytes);
+  if (phase2) *phase2 = int64_t(c->d_counters.bytes + c->d_overlay.bytes + c->d_tags.bytes + c->d_scratch.bytes);
   return KUEUE_TAS_OK;
 }
 
@@ -1444,6 +1468,33 @@ static double wall_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// The longest candidate list a BestFit-side walk of `ev` can build (its
+// select lists' capacity): every domain of a level at or above its requested
+// level (findLevelWithFitDomains sorts whole levels, tas_flavor_snapshot.go:
+// 1098-1163), and below it the children of the domains chosen one level up,
+// at most one chosen domain per pod (updateCountsToMinimum takes a domain
+// only while pods remain, :1236-1321); twice that, as the unbounded capacity
+// is twice the widest level.  Unconstrained, multi-layer and replacement
+// walks keep the unbounded lists.  An overflow still re-runs the chunk
+// unbounded (eval_chunk returns 2), so the bound costs memory, never results.
+static int64_t scratch_bound(const kueue_tas_ctx* c, const DevSnap& s, const DevEval& ev, int64_t full) {
+  if (ev.flags & (KUEUE_TAS_F_UNCONSTRAINED | KUEUE_TAS_F_MULTILAYER | KUEUE_TAS_F_DOMAIN)) return full;
+  const int r = ev.requested_level;
+  if (r < 0 || r >= s.L || c->level_maxfan.size() < size_t(s.L)) return full;
+  const int64_t pods = int64_t(std::max(ev.count, 0)) + ((ev.flags & KUEUE_TAS_F_LEADER) ? 1 : 0);
+  int64_t top = 0, below = pods;  // whole levels at or above r (find_level's lists are unchecked there)
+  for (int l = 0; l < s.L; l++) {
+    if (l <= r) top = std::max<int64_t>(top, s.level_size[l]);
+    else
+      below = std::max<int64_t>(below, std::min<int64_t>(s.level_size[l], std::min<int64_t>(s.level_size[l - 1], pods) *
+                                                                               c->level_maxfan[size_t(l - 1)]));
+  }
+  int64_t lc = std::min(full, 2 * std::max(top, below) + 64);
+  if (c->lcap_test_cap) lc = std::min(lc, std::max(c->lcap_test_cap, std::min(full, 2 * top + 64)));  // (descent lists only)
+  return lc;
+}
+
+
 static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, size_t n, const int32_t* taint_table,
                       size_t taint_table_len, int32_t num_taints, const kueue_tas_assumed* assumed, size_t num_assumed,
                       const kueue_tas_affinity_req* aff, size_t num_aff, const int32_t* aff_vals, size_t num_aff_vals,
@@ -1559,6 +1610,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   const size_t o_moff = seg((n + 1) * 4), o_mem = seg(n * 4);  // class members in fill order (CSR)
   // rollup_top_kernel's level maxima (INT32_MIN) and per-class arrival counters (0)
   const size_t o_top = seg(n * (kMaxLevels + 1) * 4);
+  const size_t o_sel = seg(n * sizeof(SelSlot));  // BestFit-side select slots' buffers
   // last: the per-position fill records, uploaded up to the batch's nfill
   const size_t o_fpos = seg(n * sizeof(FillPos));
   HIPCHK(c, c->h_stage.ensure(stage_bytes));
@@ -2068,9 +2120,7 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   c->chunk_alias.assign(n, 0);  // filled with the fill records below
   // ---- device buffers ----
   const int64_t SD = s.SD;
-  const int64_t ctr_stride = 5 * SD;  // a leader class's row; leaderless rows hold 2 fields, simple ones 1
-  int64_t lcap = int64_t(c->maxD) * 2 + 64;
-  const int64_t scratch_stride = 6 * lcap;
+  const int64_t full_lcap = int64_t(c->maxD) * 2 + 64;  // a list of any level's domains, twice
   const int nchunks = (s.N + kLfcChunk - 1) / kLfcChunk;
   {  // one row per class (fill position), sized by its kind (FillEvalParams::ctr_row)
     c->ctr_row_off.resize(size_t(std::max(nfill, 1)) + 1);
@@ -2085,16 +2135,43 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     HIPCHK(c, c->d_counters.ensure(size_t(std::max<int64_t>(at, 1)) * size_t(SD)));
   }
   // overlay, tags and scratch lists per BestFit-side select slot (fast-LFC
-  // evals never mutate or walk lists): sized by nbf, not n
-  const size_t nph2 = size_t(std::max(nbf, 1));
-  bool batch_leader = false;
-  for (size_t i = 0; i < n && !batch_leader; i++) batch_leader = (hev[i].flags & KUEUE_TAS_F_LEADER) != 0;
-  const int64_t ov_stride = batch_leader ? ctr_stride : 2 * SD;  // leaderless overlays hold two fields
-  HIPCHK(c, c->d_overlay.ensure(nph2 * size_t(ov_stride)));
-  if (c->d_tags.n < nph2 * size_t(SD) || c->tag_epoch >= 0x7ffffff0) {  // fresh tags: nothing owned
-    HIPCHK(c, c->d_tags.ensure(nph2 * size_t(SD)));
-    HIPCHK(c, hipMemsetAsync(c->d_tags.p, 0, c->d_tags.n * 4, c->stream));
-    c->tag_epoch = 0;
+  // evals never mutate or walk lists): each slot's lists bounded by what its
+  // walk can reach (scratch_bound), its overlay by its kind (2 fields, 5 with
+  // a leader); slots run in groups whose buffers fit phase2_budget, reusing
+  // one group's buffers (a fresh tag epoch per group)
+  SelSlot* hsel = reinterpret_cast<SelSlot*>(hs + o_sel);
+  std::vector<int32_t>& groups = c->sel_groups;
+  groups.assign(1, 0);
+  {
+    int64_t g_scr = 0, g_ov = 0, max_scr = 2, max_ov = 1;
+    int32_t g_tag = 0, max_tag = 1;
+    for (int k = 0; k < nbf; k++) {
+      const DevEval& ev = hev[h_bf[k]];
+      const int64_t lc = (c->scratch_full || !c->scratch_bounded) ? full_lcap : scratch_bound(c, s, ev, full_lcap);
+      const int64_t ovf = (ev.flags & KUEUE_TAS_F_LEADER) ? 5 : 2;
+      const int64_t bytes = lc * 48 + (ovf + 1) * SD * 4;
+      if (g_tag > 0 && g_scr * 8 + g_ov * 4 + int64_t(g_tag) * SD * 4 + bytes > c->phase2_budget) {
+        groups.push_back(k);
+        g_scr = g_ov = 0;
+        g_tag = 0;
+      }
+      hsel[k] = SelSlot{g_scr, g_ov, g_tag, int32_t(lc)};
+      g_scr += 6 * lc;
+      g_ov += ovf * SD;
+      g_tag++;
+      max_scr = std::max(max_scr, g_scr);
+      max_ov = std::max(max_ov, g_ov);
+      max_tag = std::max(max_tag, g_tag);
+    }
+    groups.push_back(nbf);
+    HIPCHK(c, c->d_scratch.ensure(size_t(max_scr)));
+    HIPCHK(c, c->d_overlay.ensure(size_t(max_ov)));
+    const int ngroups = int(groups.size()) - 1;
+    if (c->d_tags.n < size_t(max_tag) * size_t(SD) || c->tag_epoch + ngroups >= 0x7ffffff0) {  // fresh tags: nothing owned
+      HIPCHK(c, c->d_tags.ensure(size_t(max_tag) * size_t(SD)));
+      HIPCHK(c, hipMemsetAsync(c->d_tags.p, 0, c->d_tags.n * 4, c->stream));
+      c->tag_epoch = 0;
+    }
   }
   c->tag_epoch++;
   const size_t nt = size_t(std::max(num_taints, 0));
@@ -2147,7 +2224,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     c->snap.tag_out = c->leaf_tags_on ? c->tag_dev : nullptr;
     c->snap.ent_base = c->ent_dev;
   }
-  HIPCHK(c, c->d_scratch.ensure(nph2 * size_t(scratch_stride)));
   HIPCHK(c, c->d_lfc_jobs.ensure(n));
   HIPCHK(c, c->d_lfc_items.ensure(size_t(std::max(nfast, 1)) * size_t(std::max(nchunks, 1)) + 1));
   // chunk counts and overflow sums in two halves used by alternate batches:
@@ -2306,7 +2382,6 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.rack_fanout = 0;
   b.rack_pos = nullptr;
   b.ctr_sd = SD;
-  b.ov_stride = ov_stride;
   b.counters = c->d_counters.p;
   b.overlay = c->d_overlay.p;
   b.tags = c->d_tags.p;
@@ -2319,7 +2394,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   b.out = d_out;
   b.entries = c->ent_dev + c->ent_used;
   b.entry_cap = entry_cap;
-  b.scratch_stride = scratch_stride;
+  b.sel_slots = reinterpret_cast<const SelSlot*>(ds + o_sel);
+  b.slot_base = 0;
   b.scratch = c->d_scratch.p;
   b.list_cap = c->list_cap;
   b.nblk = nblk;
@@ -2624,9 +2700,17 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
   // K3 (BestFit side and every other non-fast eval)
   if (nbf) {
     b.wave_lds = bf_wave_lds;
-    hipLaunchKernelGGL(select_kernel, dim3(unsigned((nbf + waves - 1) / waves)), dim3(64 * waves),
-                       size_t(waves) * size_t(bf_wave_lds), c->stream, s, b, d_bf, nbf);
-    HIPCHK(c, hipGetLastError());
+    const int32_t epoch0 = c->tag_epoch;
+    for (size_t gi = 0; gi + 1 < c->sel_groups.size(); gi++) {  // one launch per slot group (one, within budget)
+      const int g0 = c->sel_groups[gi], gn = c->sel_groups[gi + 1] - g0;
+      b.slot_base = g0;
+      b.tag_epoch = epoch0 + int32_t(gi);
+      c->tag_epoch = b.tag_epoch;
+      hipLaunchKernelGGL(select_kernel, dim3(unsigned((gn + waves - 1) / waves)), dim3(64 * waves),
+                         size_t(waves) * size_t(bf_wave_lds), c->stream, s, b, d_bf + g0, gn);
+      HIPCHK(c, hipGetLastError());
+    }
+    b.slot_base = 0;
   }
   trace(16);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
@@ -2655,8 +2739,11 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     // (lfc_fast): it waits for the roll-up only when the replication wrote stats
     if (replicated) HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev[4], 0));
     b.wave_lds = lfc_wave_lds;
+    const SelSlot* sel = b.sel_slots;
+    b.sel_slots = nullptr;  // fast-LFC evals keep no lists or overlay
     hipLaunchKernelGGL(select_kernel, dim3(unsigned((nfast + waves - 1) / waves)), dim3(64 * waves),
                        size_t(waves) * size_t(lfc_wave_lds), c->stream2, s, b, d_fast, nfast);
+    b.sel_slots = sel;
     HIPCHK(c, hipGetLastError());
     const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
     hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
@@ -2699,6 +2786,19 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     c->exact_merge = true;
     c->merge_reruns++;
     return 2;
+  }
+  if (!c->scratch_full && c->scratch_bounded) {  // a bounded list overflowed: re-run with unbounded lists
+    const int32_t* hb = reinterpret_cast<const int32_t*>(hs + o_bf);
+    const SelSlot* hq = reinterpret_cast<const SelSlot*>(hs + o_sel);
+    for (int k = 0; k < nbf; k++) {
+      const kueue_tas_eval_out& o = c->res_out_h[hb[k]];
+      if ((o.status == KUEUE_TAS_ST_INTERNAL && o.num_workers + o.num_leaders <= entry_cap && hq[k].lcap < full_lcap) ||
+          c->force_scratch_rerun) {
+        c->scratch_full = true;
+        c->scratch_reruns++;
+        return 2;
+      }
+    }
   }
   lap(3);
   trace(18);
@@ -2815,7 +2915,7 @@ int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* c, const kueue_tas_eval_req* const*
                           num_affinity, affinity_values, num_affinity_values, out + i0,
                           off.data(), taint_counts ? taint_counts + i0 * size_t(std::max(num_taints, 0)) : nullptr,
                           res_counts ? res_counts + i0 * size_t(c->snap.R) : nullptr, ms, stage_ms);
-      if (rc == 2) {  // the speculative class merge met a hash collision: re-run with the exact merge
+      if (rc == 2) {  // a class hash collision (re-run with the exact merge) or a select list overflow (unbounded lists)
         c->ent_used = keep;
         c->ent_count.resize(i0);
         c->last_ticks.resize(2 * i0);
@@ -2835,7 +2935,11 @@ int kueue_tas_eval_batch_ptrs(kueue_tas_ctx* c, const kueue_tas_eval_req* const*
         c->entry_cap = cap;
         continue;
       }
-      if (rc) return rc;
+      if (rc) {
+        c->scratch_full = false;
+        return rc;
+      }
+      c->scratch_full = false;
       break;
     }
     for (size_t i = 0; i <= m; i++) entry_offsets[i0 + i] = off[i];
@@ -2966,6 +3070,13 @@ int kueue_tas_last_eval_profile(kueue_tas_ctx* c, int32_t* ticks, size_t n) {
 }
 
 int64_t kueue_tas_merge_reruns(kueue_tas_ctx* c) { return c ? c->merge_reruns : -1; }
+
+int kueue_tas_select_groups(kueue_tas_ctx* c, int64_t* last_groups, int64_t* scratch_reruns) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (last_groups) *last_groups = c->sel_groups.empty() ? 0 : int64_t(c->sel_groups.size()) - 1;
+  if (scratch_reruns) *scratch_reruns = c->scratch_reruns;
+  return KUEUE_TAS_OK;
+}
 
 int kueue_tas_last_host_trace(kueue_tas_ctx* c, double* ms, int n) {  // ms since the chunk's start, [0, 20)
   if (!c || !ms) return KUEUE_TAS_EINVAL;

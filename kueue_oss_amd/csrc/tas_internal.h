@@ -141,6 +141,18 @@ struct LfcItem {
   int32_t eid, chunk, base, tie0;
 };
 
+// One BestFit-side select slot's phase-2 buffers within its slot group: the
+// list scratch (6 * lcap uint64 at scr_off: four int32 lists, two key
+// arrays), the copy-on-write overlay (2 or 5 fields of SD int32 at ov_off)
+// and the ownership tags (row tag_idx of SD int32).  lcap bounds the eval's
+// candidate lists (kueue_tas_ctx::scratch_bound).
+struct SelSlot {
+  int64_t scr_off;
+  int64_t ov_off;
+  int32_t tag_idx;
+  int32_t lcap;
+};
+
 // Per-batch device buffers.
 struct DevBatch {
   const DevEval* evals;
@@ -164,9 +176,7 @@ struct DevBatch {
                            // fan-out, -1 ragged (DevSnap::wave_tab), 0 no
   uint64_t* rack_pos;      // [nfill][D_{L-2}] with rack_fanout: bit j = child leaf j has sliceState > 0 (class rows)
   int64_t ctr_sd;          // SD: a class row's field stride (rows at FillEvalParams::ctr_row * SD)
-  int64_t ov_stride;       // int32 elements per phase-2 overlay slot: 5 * SD, or 2 * SD when no eval of the
-                           // batch has a leader (only state and sliceState are written then)
-  int32_t* counters;       // [nfill][5][SD]: one row per phase-1 class, in fill order (row = fill position)
+  int32_t* counters;       // one row per phase-1 class in fill order (row = fill position), 1, 2 or 5 fields
   int32_t* taint_counts;   // [n][num_taints]
   int32_t* res_counts;     // [n][R]
   int32_t* sel_counts;     // [n]
@@ -175,8 +185,9 @@ struct DevBatch {
   kueue_tas_eval_out* out; // [n]
   int32_t* entries;        // [n][entry_cap][2]
   int32_t entry_cap;
-  int64_t scratch_stride;  // uint64 elements of scratch per eval
-  uint64_t* scratch;       // [n][scratch_stride]
+  uint64_t* scratch;       // select lists per BestFit-side slot (SelSlot::scr_off, 6 * lcap uint64 each)
+  const struct SelSlot* sel_slots;  // [nbf] each BestFit-side slot's phase-2 buffers (null: the fast-LFC launch)
+  int32_t slot_base;       // the launch's first slot (select runs its slots in groups under a memory budget)
   int32_t list_cap;        // LDS sort capacity per wave
   int32_t wave_lds;        // select_kernel's LDS bytes per wave (>= list_cap keys; the launch's dynamic LDS / waves)
   LeafPartial* partials;   // [leaf-level evals][nblk]
@@ -205,9 +216,9 @@ struct DevBatch {
   LfcJob* lfc_jobs;        // [n]
   LfcItem* lfc_items;      // [nfast * nchunks] chunks with greedy output (appended by select)
   int32_t* lfc_nitems;     // [1] number of lfc_items
-  int32_t* overlay;        // [n][5][SD] phase-2 copy-on-write counters (select)
-  int32_t* tags;           // [n][SD] overlay ownership (== tag_epoch: held)
-  int32_t tag_epoch;
+  int32_t* overlay;        // phase-2 copy-on-write counters per slot (SelSlot::ov_off: 2 or 5 fields of SD)
+  int32_t* tags;           // [slots of a group][SD] overlay ownership (== tag_epoch: held)
+  int32_t tag_epoch;       // the launch's (one per slot group)
   int32_t* prof;           // [n][8] select phase ticks (profiling build only, else null)
   int32_t* fill_prof;      // [blocks][8] fill_pair_kernel phase stamps (profiling build only, else null)
   int32_t* level_max;      // [nfill][kMaxLevels] max sliceState per level < L-1 of the class row's counters

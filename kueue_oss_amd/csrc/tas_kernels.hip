@@ -5341,8 +5341,10 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.rack_pos = (b.rack_fanout && b.rack_pos) ? b.rack_pos + int64_t(b.rep_of[eid]) * s.level_size[s.L - 2] : nullptr;
   // per-launch-slot phase-2 buffers: the BestFit-side launch numbers its
   // evals 0..nbf-1; fast-LFC evals (the other launch) never touch them
-  w.ov = b.overlay + int64_t(slot) * b.ov_stride;
-  w.tag = b.tags + int64_t(slot) * s.SD;
+  SelSlot q{0, 0, 0, 0};  // the fast-LFC launch: no lists, no overlay
+  if (b.sel_slots) q = b.sel_slots[b.slot_base + slot];
+  w.ov = b.overlay + q.ov_off;
+  w.tag = b.tags + int64_t(q.tag_idx) * s.SD;
   w.my_tag = b.tag_epoch;
   w.dirty = false;
   w.SD = s.SD;
@@ -5350,8 +5352,8 @@ __global__ __launch_bounds__(256) void select_kernel(DevSnap s, DevBatch b, cons
   w.lds = lds_all + int64_t(wave) * (b.wave_lds / int(sizeof(Key)));
   w.cap = b.list_cap;
   w.lds_bytes = b.wave_lds;
-  int64_t lcap = b.scratch_stride / 6;  // 4 int32 lists (2 per u64) + 2 key arrays (2 u64 per key)
-  uint64_t* sc = b.scratch + int64_t(slot) * b.scratch_stride;
+  const int64_t lcap = q.lcap;  // 4 int32 lists (2 per u64) + 2 key arrays (2 u64 per key): 6 * lcap u64
+  uint64_t* sc = b.scratch + q.scr_off;
   w.lcap = int(lcap);
   w.listA = reinterpret_cast<int32_t*>(sc);
   w.listB = w.listA + lcap;

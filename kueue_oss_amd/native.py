@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
     "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
     "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace", "kueue_tas_merge_reruns",
+    "kueue_tas_select_groups",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -151,6 +152,7 @@ def _bind(lib):
     lib.kueue_tas_host_set_stage_timing.argtypes = [c.c_void_p, c.c_int32]
     lib.kueue_tas_snapshot_counters.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
     lib.kueue_tas_device_bytes.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
+    lib.kueue_tas_select_groups.argtypes = [c.c_void_p, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]
     lib.kueue_tas_host_stage_accum.argtypes = [c.c_void_p, c.POINTER(c.c_float), c.c_int, c.POINTER(c.c_int64),
                                                c.POINTER(c.c_int64), c.c_int32]
     lib.kueue_tas_host_last_admit_times.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
@@ -607,6 +609,13 @@ class TASFlavorSnapshot:
         if self._lib.kueue_tas_host_leaf_ids(self._h, ctypes.byref(out)):
             raise RuntimeError(self._err())
         return _take(self._lib, out)
+
+    def select_groups(self):
+        """(slot groups of the last chunk's BestFit select, chunks re-run with
+        unbounded select lists so far) — kueue_tas_select_groups."""
+        g, r = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.kueue_tas_select_groups(self.device_ctx(), ctypes.byref(g), ctypes.byref(r))
+        return g.value, r.value
 
     def merge_reruns(self) -> int:
         """Device chunks re-run with the exact phase-1 class merge (kueue_tas_merge_reruns)."""
