@@ -517,7 +517,8 @@ class FlavorSnapshot {
   std::vector<std::string> labelKeys;
   std::map<std::string, int32_t> labelCol;
   std::vector<std::map<std::string, int32_t>> labelDict;
-  std::vector<int32_t> labelValues;  // [K][N]
+  std::vector<int32_t> labelValues;  // [K][labStride]: column k at k * labStride (leaves 0..N-1)
+  size_t labStride = 0;              // >= N, with headroom: joined leaves shift each column in place
   std::deque<NodeInfo> nodes;  // stable addresses: leafNode points into it, nodes join in place
   std::map<std::string, std::string> flavorLabels;
   std::unordered_map<std::string, size_t> nodeIdx;  // node name -> nodes[]
@@ -892,7 +893,8 @@ class FlavorSnapshot {
         labelKeys.push_back(k);
       }
       labelDict.assign(labelKeys.size(), {});
-      labelValues.assign(labelKeys.size() * size_t(N), 0);
+      labStride = size_t(N) + size_t(N) / 8 + 64;
+      labelValues.assign(labelKeys.size() * labStride, 0);
       for (size_t k = 0; k < labelKeys.size(); k++) {
         for (int i = 0; i < N; i++) {
           auto it = leafNode[i]->labels.find(labelKeys[k]);
@@ -900,7 +902,7 @@ class FlavorSnapshot {
           auto& dict = labelDict[k];
           auto d = dict.find(it->second);
           if (d == dict.end()) d = dict.emplace(it->second, int32_t(dict.size()) + 1).first;
-          labelValues[k * size_t(N) + i] = d->second;
+          labelValues[k * labStride + size_t(i)] = d->second;
         }
       }
     }
@@ -1027,7 +1029,7 @@ class FlavorSnapshot {
         c = labelCol.emplace(kv.first, int32_t(labelKeys.size())).first;
         labelKeys.push_back(kv.first);
         labelDict.emplace_back();
-        labelValues.resize(labelKeys.size() * N, 0);
+        labelValues.resize(labelKeys.size() * labStride, 0);
         *changed = *relayout = true;
       }
       auto& dict = labelDict[size_t(c->second)];
@@ -1055,7 +1057,7 @@ class FlavorSnapshot {
       const size_t N = size_t(this->N());
       for (size_t k = 0; k < labelKeys.size(); k++) {
         auto it = cur.labels.find(labelKeys[k]);
-        labelValues[k * N + size_t(leaf)] = it == cur.labels.end() ? 0 : labelDict[k].at(it->second);
+        labelValues[k * labStride + size_t(leaf)] = it == cur.labels.end() ? 0 : labelDict[k].at(it->second);
       }
     }
   }
@@ -1392,19 +1394,26 @@ class FlavorSnapshot {
       move_leaves(leafDead, [](const Join&) { return uint8_t(0); });
       move_leaves(leafProfile, [](const Join& j) { return j.prof; });
     });
-    tasks.emplace_back([&] {
-      if (labelKeys.empty()) return;
+    if (!labelKeys.empty()) {  // each label column shifts in place (its stride has room), one task per column
       const size_t K = labelKeys.size();
-      labelValues.resize(K * N, 0);  // [K][N0] -> [K][N] in place: later columns and entries first
-      for (size_t k = K; k-- > 0;) {
-        int32_t* col = labelValues.data();
-        for (size_t i = N0; i-- > 0;) col[k * N + size_t(rm[i])] = col[k * N0 + i];
-        for (size_t j = 0; j < fr.size(); j++) {
-          auto it = joins[j].node->labels.find(labelKeys[k]);
-          col[k * N + size_t(fr[j])] = it == joins[j].node->labels.end() ? 0 : labelDict[k].at(it->second);
-        }
+      if (N > labStride) {  // out of room: every column moves to a wider stride first
+        const size_t ns = N + N / 8 + 64;
+        std::vector<int32_t> wide(K * ns, 0);
+        for (size_t k = 0; k < K; k++) memcpy(wide.data() + k * ns, labelValues.data() + k * labStride, N0 * 4);
+        labelValues.swap(wide);
+        labStride = ns;
       }
-    });
+      for (size_t k = 0; k < K; k++)
+        tasks.emplace_back([&, k] {
+          int32_t* col = labelValues.data() + k * labStride;
+          for (size_t i = N0; i-- > 0;)
+            if (size_t(rm[i]) != i) col[size_t(rm[i])] = col[i];
+          for (size_t j = 0; j < fr.size(); j++) {
+            auto it = joins[j].node->labels.find(labelKeys[k]);
+            col[size_t(fr[j])] = it == joins[j].node->labels.end() ? 0 : labelDict[k].at(it->second);
+          }
+        });
+    }
     ktas_pool::HostPool::get().run(tasks.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks[t]();
     });
@@ -1441,55 +1450,93 @@ class FlavorSnapshot {
         }
         std::sort(unnamedLeaves.begin(), unnamedLeaves.end());
       });
-    tasks2.emplace_back([&] {  // leaf parents and live leaves per parent
-      leafParent.assign(N, 0);
-      liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
-      if (L >= 2) {
-        const auto& co = childOff[size_t(L - 2)];
-        for (size_t p = 0; p + 1 < co.size(); p++)
-          for (int32_t i = co[p]; i < co[p + 1]; i++) leafParent[size_t(i)] = int32_t(p);
+    // leaf parents and live leaves per parent, in chunks of parents
+    const std::vector<int32_t>* pco = L >= 2 ? &childOff[size_t(L - 2)] : nullptr;
+    leafParent.resize(N);
+    liveUnder.assign(L >= 2 ? values[size_t(L - 2)].size() : 1, 0);
+    if (!pco) {
+      for (size_t i = 0; i < N; i++) {
+        leafParent[i] = 0;
+        if (!leafDead[i]) liveUnder[0]++;
       }
-      for (size_t i = 0; i < N; i++)
-        if (!leafDead[i]) liveUnder[size_t(leafParent[i])]++;
-    });
+    }
+    constexpr size_t kChunk = 8192;
+    const size_t P = pco ? pco->size() - 1 : 0;
+    for (size_t p0 = 0; p0 < P; p0 += kChunk / 16)
+      tasks2.emplace_back([&, p0] {
+        const auto& co = *pco;
+        for (size_t p = p0; p < std::min(P, p0 + kChunk / 16); p++) {
+          int32_t live = 0;
+          for (int32_t i = co[p]; i < co[p + 1]; i++) {
+            leafParent[size_t(i)] = int32_t(p);
+            live += leafDead[size_t(i)] ? 0 : 1;
+          }
+          liveUnder[p] = live;
+        }
+      });
     // DomainID ranks (multiLayerNotFitMessage tie-break): each new id's
     // position among the old ones by a binary search over the old rank order;
-    // an old domain's rank grows by the new ids placed before it
+    // an old domain's rank grows by the new ids placed before it.  The O(D)
+    // passes (old rank order, new ranks) run in chunks.
+    std::vector<std::vector<int32_t>> byRank(static_cast<size_t>(L)), newRank(static_cast<size_t>(L));
     for (int l = 0; l < L; l++) {
       if (fresh[size_t(l)].empty()) continue;
-      tasks2.emplace_back([&, l] {
-        const auto& f = fresh[size_t(l)];
-        auto& rk = idRank[size_t(l)];
-        const auto& rml = remap[size_t(l)];
-        const size_t D0 = rk.size();
-        std::vector<int32_t> byRank(D0);
-        for (size_t i = 0; i < D0; i++) byRank[size_t(rk[i])] = rml[i];  // new indices in old rank order
-        std::vector<std::pair<std::string, int32_t>> ids;
-        for (int32_t c : f) ids.emplace_back(domain_id(l, size_t(c)), c);
-        std::sort(ids.begin(), ids.end());
-        std::vector<int32_t> q(ids.size());
-        for (size_t k = 0; k < ids.size(); k++) {
-          size_t lo = 0, hi = D0;
-          while (lo < hi) {
-            const size_t mid = (lo + hi) / 2;
-            if (domain_id(l, size_t(byRank[mid])) < ids[k].first) lo = mid + 1;
-            else hi = mid;
-          }
-          q[k] = int32_t(lo);
-        }
-        std::vector<int32_t> out(D0 + ids.size());
-        size_t k = 0;
-        for (size_t r = 0; r < D0; r++) {
-          while (k < q.size() && size_t(q[k]) <= r) k++;
-          out[size_t(byRank[r])] = int32_t(r + k);
-        }
-        for (size_t j = 0; j < ids.size(); j++) out[size_t(ids[j].second)] = q[j] + int32_t(j);
-        rk = std::move(out);
-      });
+      const size_t D0 = idRank[size_t(l)].size();
+      byRank[size_t(l)].resize(D0);
+      for (size_t c0 = 0; c0 < D0; c0 += kChunk)
+        tasks2.emplace_back([&, l, c0] {
+          const auto& rk = idRank[size_t(l)];
+          const auto& rml = remap[size_t(l)];
+          auto& br = byRank[size_t(l)];
+          for (size_t i = c0; i < std::min(rk.size(), c0 + kChunk); i++) br[size_t(rk[i])] = rml[i];  // new indices in old rank order
+        });
     }
     ktas_pool::HostPool::get().run(tasks2.size(), 1, [&](size_t b, size_t e) {
       for (size_t t = b; t < e; t++) tasks2[t]();
     });
+    std::vector<std::function<void()>> tasks3;
+    std::vector<std::vector<int32_t>> qpos(static_cast<size_t>(L));
+    std::vector<std::vector<std::pair<std::string, int32_t>>> newIds(static_cast<size_t>(L));
+    for (int l = 0; l < L; l++) {
+      const auto& f = fresh[size_t(l)];
+      if (f.empty()) continue;
+      const auto& br = byRank[size_t(l)];
+      const size_t D0 = br.size();
+      auto& ids = newIds[size_t(l)];
+      for (int32_t c : f) ids.emplace_back(domain_id(l, size_t(c)), c);
+      std::sort(ids.begin(), ids.end());
+      auto& q = qpos[size_t(l)];
+      q.resize(ids.size());
+      for (size_t k = 0; k < ids.size(); k++) {
+        size_t lo = 0, hi = D0;
+        while (lo < hi) {
+          const size_t mid = (lo + hi) / 2;
+          if (domain_id(l, size_t(br[mid])) < ids[k].first) lo = mid + 1;
+          else hi = mid;
+        }
+        q[k] = int32_t(lo);
+      }
+      auto& out = newRank[size_t(l)];
+      out.resize(D0 + ids.size());
+      for (size_t j = 0; j < ids.size(); j++) out[size_t(ids[j].second)] = q[j] + int32_t(j);
+      for (size_t c0 = 0; c0 < D0; c0 += kChunk)
+        tasks3.emplace_back([&, l, c0] {
+          const auto& brl = byRank[size_t(l)];
+          const auto& ql = qpos[size_t(l)];
+          auto& o = newRank[size_t(l)];
+          const size_t e = std::min(brl.size(), c0 + kChunk);
+          size_t k = size_t(std::upper_bound(ql.begin(), ql.end(), int32_t(c0)) - ql.begin());
+          for (size_t r = c0; r < e; r++) {
+            while (k < ql.size() && size_t(ql[k]) <= r) k++;
+            o[size_t(brl[r])] = int32_t(r + k);
+          }
+        });
+    }
+    ktas_pool::HostPool::get().run(tasks3.size(), 1, [&](size_t b, size_t e) {
+      for (size_t t = b; t < e; t++) tasks3[t]();
+    });
+    for (int l = 0; l < L; l++)
+      if (!fresh[size_t(l)].empty()) idRank[size_t(l)] = std::move(newRank[size_t(l)]);
     lap(3);
     leafVals.clear();
     for (auto& j : joins)
@@ -1559,7 +1606,7 @@ class FlavorSnapshot {
         up[q] |= 1u << c->second;
       }
       prof[q] = leafProfile[j];
-      for (size_t c = 0; c < K; c++) lab[c * k + q] = labelValues[c * size_t(N) + j];
+      for (size_t c = 0; c < K; c++) lab[c * k + q] = labelValues[c * labStride + j];
     }
     kueue_tas_snapshot_desc d{};
     d.num_levels = L;
@@ -1675,7 +1722,7 @@ class FlavorSnapshot {
     std::vector<int32_t> prof(ls.size()), lab(ls.size() * K);
     for (size_t i = 0; i < ls.size(); i++) {
       prof[i] = leafProfile[size_t(ls[i])];
-      for (size_t k = 0; k < K; k++) lab[i * K + k] = labelValues[k * N + size_t(ls[i])];
+      for (size_t k = 0; k < K; k++) lab[i * K + k] = labelValues[k * labStride + size_t(ls[i])];
     }
     rc = kueue_tas_snapshot_set_leaf_attrs(ctx, ls.data(), ls.size(), prof.data(), K ? lab.data() : nullptr);
     if (rc) err = std::string("set leaf attrs: ") + kueue_tas_last_error(ctx);
@@ -1802,7 +1849,13 @@ class FlavorSnapshot {
     d.lowest_is_hostname = lowestIsHostname ? 1 : 0;
     d.taint_profile = leafProfile.data();
     d.num_label_cols = int32_t(labelKeys.size());
-    d.label_values = labelValues.empty() ? nullptr : labelValues.data();
+    std::vector<int32_t> labPacked;  // [K][N] for the load
+    if (!labelValues.empty() && labStride != size_t(N)) {
+      labPacked.resize(labelKeys.size() * size_t(N));
+      for (size_t k = 0; k < labelKeys.size(); k++)
+        memcpy(labPacked.data() + k * size_t(N), labelValues.data() + k * labStride, size_t(N) * 4);
+    }
+    d.label_values = labelValues.empty() ? nullptr : labStride != size_t(N) ? labPacked.data() : labelValues.data();
     d.domain_id_rank = ranks.data();
     int rc = kueue_tas_snapshot_load(ctx, &d);
     if (!rc) rc = kueue_tas_snapshot_usage_mark(ctx);  // device usage == host mirror

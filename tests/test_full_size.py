@@ -96,8 +96,11 @@ def test_c5_whole_batch_on_gpu(capfd):
         snap.compile(wls)
         snap.run_compiled(flags=FULL)
         got = snap.last_results()
+        total, phase2 = snap.device_bytes()
         snap.close()
-        _progress("device batch done; oracle (16 threads)")
+        _progress(f"device batch done ({total / 2**30:.2f} GiB on the device, {phase2 / 2**30:.2f} GiB of it "
+                  "phase-2 state); oracle (16 threads)")
+        assert total < 8 * 2**30
         want, secs = oracle_lib.eval_workloads(doc, wls, threads=16)
         mism = [i for i in range(len(wls)) if got[i] != want[i]]
         assert mism == [], (len(mism), mism[:8])
@@ -236,7 +239,7 @@ def _negated(deltas):
 
 def _admit_8192(snap):
     """One rank-0 admission round of ADMIT_CANDIDATES gathered candidates (the
-    8-GPU load: 8 x 1,024 evaluations) on a fresh replica, timed three times;
+    8-GPU load: 8 x 1,024 evaluations) on the replica, timed three times;
     each repetition's deltas are negated afterwards (the snapshot returns to
     its state).  Returns the timing record."""
     ids = list(range(ADMIT_CANDIDATES))
@@ -289,13 +292,28 @@ def _c5_sharded():
     for p in procs:
         p.start()
     try:
-        # meanwhile the same workloads here (host only: the replica below
-        # starts when the ranks have freed their device memory — three
-        # 1M-node contexts with 1,024-eval phase-2 buffers exceed one GPU)
+        # meanwhile one unsharded replica of the same rounds here, on the same
+        # GPU: three 1M-node contexts with 1,024-eval batches at once (each
+        # context's phase-2 state is bounded, kueue_tas_device_bytes)
         doc, wls = _c5()
         n = len(wls)
         rounds = _rounds(wls)
         assert sorted(i for b in rounds for r in b for i in r) == list(range(n))
+        snap = TASFlavorSnapshot(doc, max_batch=C5_BATCH)
+        snap.compile(wls)
+        replica = []
+        t0 = time.time()
+        peak = 0
+        for k, batches in enumerate(rounds):
+            snap.set_shard(sorted(i for b in batches for i in b))
+            snap.run_compiled(flags=FULL)
+            peak = max(peak, snap.device_bytes()[0])
+            u = _by_workload(snap.last_assignments())
+            admitted, deltas = snap.admit(snap.last_assignments())
+            replica.append((u, admitted, deltas))
+        _progress(f"unsharded replica beside the ranks: {len(rounds)} rounds in {time.time() - t0:.1f}s, "
+                  f"device bytes peak {peak / 2**30:.2f} GiB")
+        assert peak < 8 * 2**30
         outs = dict(q.get(timeout=900) for _ in range(WORLD))
     finally:
         for p in procs:
@@ -304,20 +322,8 @@ def _c5_sharded():
         assert "error" not in outs[r], outs[r].get("error")
         assert procs[r].exitcode == 0
     _progress(f"ranks done in {outs[0]['seconds']:.1f}s")
-    # one unsharded replica on the same GPU, the same rounds
-    snap = TASFlavorSnapshot(doc, max_batch=C5_BATCH)
-    snap.compile(wls)
-    adm8 = _admit_8192(snap)
+    adm8 = _admit_8192(snap)  # (after the ranks: a timing of its own)
     _progress(f"8,192-candidate admission round: {adm8['round_ms']} ms")
-    replica = []
-    t0 = time.time()
-    for k, batches in enumerate(rounds):
-        snap.set_shard(sorted(i for b in batches for i in b))
-        snap.run_compiled(flags=FULL)
-        u = _by_workload(snap.last_assignments())
-        admitted, deltas = snap.admit(snap.last_assignments())
-        replica.append((u, admitted, deltas))
-    _progress(f"unsharded replica: {len(rounds)} rounds in {time.time() - t0:.1f}s; comparing")
     leaf_names = snap.leaf_ids()
     snap.close()
     # (a) every round: both ranks saw the same exchange, and it equals the replica's round
