@@ -236,6 +236,10 @@ struct kueue_tas_ctx {
   bool inline_stats = true;   // ExclusionStats counted in the fill (KUEUE_TAS_CFG_SPLIT_STATS: fill_exclusion_kernel)
   bool pair_fill = true;      // fill_pair_kernel for single-run chunks (KUEUE_TAS_CFG_NO_PAIR_FILL clears it)
   bool admit_window = true;   // admit_window_kernel (KUEUE_TAS_CFG_SERIAL_ADMIT: the one-wave chain)
+  int admit_grid_sweeps = [] {  // window-kernel phases (rejection sweeps over the grid between them); 1: in-kernel
+    const char* e = getenv("KTAS_ADMIT_PHASES");
+    return e ? std::max(1, atoi(e)) : 6;
+  }();
   bool fused_top = false;     // rollup_top_kernel (KUEUE_TAS_CFG_FUSED_TOP)
   bool cat_fill = true;       // fill_pair_kernel's leaf categories (KUEUE_TAS_CFG_NO_CATEGORY_FILL clears it)
   bool labels16 = false;      // every staged label column's value ids < 2^16 (packed nodeSelector compare)
@@ -1377,7 +1381,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const size_t o_todor = o_todo + al((n_wl + 1) * 4);
   const size_t o_minc = o_todor + al(n_wl * 16);
   const size_t o_bits = o_minc + al(size_t(c->snap.N) * 4);
-  HIPCHK(c, c->d_fits.ensure(o_bits + nwords * 4));
+  const size_t o_state = o_bits + al(nwords * 4);  // admit_window_kernel's phase state (AdmitState)
+  HIPCHK(c, c->d_fits.ensure(o_state + 256));
   HIPCHK(c, c->h_stage.ensure(up_bytes));
   uint8_t* h = c->h_stage.p;
   if (num_terms) memcpy(h + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term));
@@ -1398,6 +1403,7 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   uint8_t* d = c->d_fits.p;
   HIPCHK(c, hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(d + o_state, 0, 256, c->stream));
   // order-free candidates decided in parallel (admit_minc / dep / indep), unless exact
   const bool indep = c->admit_window && !exact && n > 0;
   if (indep) {
@@ -1432,14 +1438,31 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo),
                        reinterpret_cast<const int64_t*>(d + o_off), reinterpret_cast<int64_t*>(d + o_todor));
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
-                       lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
-                       c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
-                       reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
-                       reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
-                       reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
-                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo),
-                       reinterpret_cast<int64_t*>(d + o_todor));
+    // the window kernel in phases: each stops at a rejection sweep, which the
+    // grid runs (a wave per remaining candidate) before the next phase
+    // resumes; the last phase sweeps inside its workgroup.  A finished pass
+    // leaves the later launches nothing to do.
+    int32_t* st = reinterpret_cast<int32_t*>(d + o_state);
+    int32_t* todo = reinterpret_cast<int32_t*>(d + o_todo);
+    int64_t* todor = reinterpret_cast<int64_t*>(d + o_todor);
+    const int phases = c->admit_grid_sweeps;
+    for (int ph = 0; ph < phases; ph++) {
+      if (ph > 0) {
+        hipLaunchKernelGGL(admit_sweep_kernel, dim3(1024), dim3(256), 0, c->stream, c->snap, c->d_usage.p,
+                           c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs), fit0d,
+                           reinterpret_cast<const uint32_t*>(d + o_bits), reinterpret_cast<int32_t*>(d + o_out), todo,
+                           todor, st);
+        hipLaunchKernelGGL(admit_compact_kernel, dim3(1), dim3(1024), 0, c->stream, todo, todor, st);
+      }
+      hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
+                         lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
+                         c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
+                         reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
+                         reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
+                         reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
+                         reinterpret_cast<int32_t*>(d + o_out), todo, todor, st, ph + 1 < phases ? 1 : 0);
+      HIPCHK(c, hipGetLastError());
+    }
   } else {  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
                        c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
@@ -1448,8 +1471,8 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
                        reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
   }
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, c->h_admit.reserve(n_wl + 2));
-  HIPCHK(c, hipMemcpyAsync(c->h_admit.p, d + o_out, (n_wl + 2) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, c->h_admit.reserve(n_wl + 3));
+  HIPCHK(c, hipMemcpyAsync(c->h_admit.p, d + o_out, (n_wl + 3) * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   memcpy(admitted, c->h_admit.p, n_wl * 4);
   c->admit_stats[0] = c->admit_window ? c->h_admit.p[n_wl] : -1;

@@ -6247,12 +6247,48 @@ constexpr int kAdmitWindow = 16;
 __device__ __forceinline__ void admit_drain() {  // every outstanding memory operation of the wave completed
   __builtin_amdgcn_s_waitcnt(0);
 }
+// A remaining candidate checked against the current usage (the rejection
+// sweep; wave-uniform): every record's Fits, the untouched leaves keeping
+// their phase-1 verdict.
+__device__ bool admit_sweep_fits(const DevSnap& s, const int64_t* tas_usage, const uint32_t* usage_present,
+                                 const kueue_tas_fits_req* reqs, const kueue_tas_fits_term* terms, const AdmitRec* recs,
+                                 const uint32_t* touched_lds, const uint32_t* touched_global, bool in_lds, int64_t r0,
+                                 int64_t r1) {
+  const int lane = lane_id();
+  bool fit = true;
+  for (int64_t base = r0; base < r1 && fit; base += kWave) {
+    const int64_t i = base + lane;
+    bool ok = true;
+    if (i < r1) {
+      const AdmitRec a = recs[i];
+      if (a.status == kAdmitWide) {
+        ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
+      } else if (a.status == kAdmitNever) {
+        ok = false;
+      } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
+        int64_t us[kAdmitTerms];
+#pragma unroll
+        for (int u = 0; u < kAdmitTerms; u++)
+          us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
+#pragma unroll
+        for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
+      }
+    }
+    fit = ballot(!ok) == 0;
+  }
+  return fit;
+}
+// admit_window_kernel's state across its phases (kAdmitState ints): the
+// window kernel hands a rejection sweep to the grid (admit_sweep_kernel,
+// then admit_compact_kernel) and the next phase resumes where it stopped.
+enum AdmitState { AS_STARTED, AS_W0, AS_NTODO, AS_ROUNDS, AS_SWEEPS, AS_GATE, AS_SWEEP, AS_DONE, kAdmitState };
 __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     DevSnap s, int64_t* tas_usage, uint32_t* usage_present, const kueue_tas_fits_req* reqs,
     const kueue_tas_fits_term* terms, const AdmitRec* recs, const int64_t* wl_off, int n_wl, int pods_col,
     const int32_t* wl_fit0, const int32_t* exact_flag, uint32_t* touched_global, int touched_in_lds,
-    int32_t* admitted, int32_t* todo, int64_t* todo_r) {
+    int32_t* admitted, int32_t* todo, int64_t* todo_r, int32_t* st, int grid_sweeps) {
   extern __shared__ uint32_t touched_lds[];  // touched bitmap [nwords] (+ the round's bitmap [nwords] when chained)
+  if (st[AS_DONE]) return;  // an earlier phase finished the pass
   __shared__ int32_t sh_fit[kAdmitWindow];
   __shared__ int32_t sh_conf[2];  // per admission attempt, alternating (one barrier per attempt)
   __shared__ int32_t sh_scan[64 * kAdmitWindow];  // the sweep's compaction (a count per thread)
@@ -6265,10 +6301,12 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     for (int k = threadIdx.x; k < (chain ? 2 : 1) * nwords; k += blockDim.x)
       touched_lds[k] = k < nwords ? touched_global[k] : 0u;
   const bool exact = *exact_flag != 0;
-  int ntodo = todo[0];
+  const bool resumed = st[AS_STARTED] != 0;
+  int ntodo = resumed ? st[AS_NTODO] : todo[0];
   __syncthreads();
-  int w0 = 0;  // position in the todo list
-  int rounds = 0, sweeps = 0, nrej_since = 0, sweep_gate = kAdmitWindow / 4;
+  int w0 = resumed ? st[AS_W0] : 0;  // position in the todo list
+  int rounds = st[AS_ROUNDS], sweeps = st[AS_SWEEPS], nrej_since = 0;
+  int sweep_gate = resumed ? st[AS_GATE] : kAdmitWindow / 4;
   int pf_pos = -1, pf_w = n_wl;  // the next window's candidate, fetched during this round
   int64_t pf_r0 = 0, pf_r1 = 0;
   while (w0 < ntodo) {  // block-uniform
@@ -6427,32 +6465,28 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     for (int q = 0; q < k; q++) nrej_since += sh_fit[q] ? 0 : 1;
     if (nrej_since >= sweep_gate && ntodo - w0 > 2 * kAdmitWindow && !exact) {  // block-uniform
       nrej_since = 0;
+      if (grid_sweeps) {  // the grid sweeps (admit_sweep_kernel): this phase stops here
+        if (in_lds)  // the touched bitmap back to global memory for the sweep and the next phase
+          for (int q = threadIdx.x; q < nwords; q += blockDim.x) touched_global[q] = touched_lds[q];
+        if (threadIdx.x == 0) {
+          st[AS_STARTED] = 1;
+          st[AS_W0] = w0;
+          st[AS_NTODO] = ntodo;
+          st[AS_ROUNDS] = rounds;
+          st[AS_SWEEPS] = sweeps;
+          st[AS_GATE] = sweep_gate;
+          st[AS_SWEEP] = 1;
+        }
+        return;
+      }
       sweeps++;
       const int swept_from = ntodo - w0;
       for (int pos = w0 + wave; pos < ntodo; pos += kAdmitWindow) {
         const int w = todo[1 + pos];
         const int64_t r0 = todo_r[2 * pos], r1 = todo_r[2 * pos + 1];
-        bool fit = wl_fit0[w] != 0;
-        for (int64_t base = r0; base < r1 && fit; base += kWave) {
-          const int64_t i = base + lane;
-          bool ok = true;
-          if (i < r1) {
-            const AdmitRec a = recs[i];
-            if (a.status == kAdmitWide) {
-              ok = admit_record_fits(s, tas_usage, usage_present, reqs[i], terms);
-            } else if (a.status == kAdmitNever) {
-              ok = false;
-            } else if (a.status == kAdmitCheck && admit_touched(touched_lds, touched_global, in_lds, a.leaf)) {
-              int64_t us[kAdmitTerms];
-#pragma unroll
-              for (int u = 0; u < kAdmitTerms; u++)
-                us[u] = (a.col[u] >= 0 && a.val[u] > 0) ? load_l2(tas_usage + int64_t(a.col[u]) * s.N + a.leaf) : 0;
-#pragma unroll
-              for (int u = 0; u < kAdmitTerms; u++) ok &= !(a.col[u] >= 0 && a.val[u] > 0) || us[u] <= a.lim[u];
-            }
-          }
-          fit = ballot(!ok) == 0;
-        }
+        const bool fit = wl_fit0[w] != 0 &&
+                         admit_sweep_fits(s, tas_usage, usage_present, reqs, terms, recs, touched_lds, touched_global,
+                                          in_lds, r0, r1);
         if (!fit && lane == 0) {
           admitted[w] = 0;
           todo[1 + pos] = -1;  // rejected: dropped by the compaction
@@ -6509,6 +6543,85 @@ __global__ __launch_bounds__(64 * kAdmitWindow) void admit_window_kernel(
     admitted[n_wl] = rounds;
     admitted[n_wl + 1] = todo[0];
     admitted[n_wl + 2] = sweeps;
+    st[AS_DONE] = 1;
+  }
+}
+
+// The rejection sweep over the grid (a wave per remaining candidate, grid-
+// stride): admit_window_kernel stopped at a sweep point; every remaining
+// candidate that does not fit the current usage is rejected (final: usage
+// only grows) and marked for the compaction.
+__global__ __launch_bounds__(256) void admit_sweep_kernel(DevSnap s, const int64_t* tas_usage,
+                                                          const uint32_t* usage_present, const kueue_tas_fits_req* reqs,
+                                                          const kueue_tas_fits_term* terms, const AdmitRec* recs,
+                                                          const int32_t* wl_fit0, const uint32_t* touched_global,
+                                                          int32_t* admitted, int32_t* todo, const int64_t* todo_r,
+                                                          const int32_t* st) {
+  if (!st[AS_SWEEP] || st[AS_DONE]) return;
+  const int w0 = st[AS_W0], ntodo = st[AS_NTODO];
+  const int waves = int(gridDim.x * (blockDim.x >> 6));
+  for (int pos = w0 + int(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); pos < ntodo; pos += waves) {
+    const int w = todo[1 + pos];
+    const bool fit = wl_fit0[w] != 0 && admit_sweep_fits(s, tas_usage, usage_present, reqs, terms, recs, nullptr,
+                                                         touched_global, false, todo_r[2 * pos], todo_r[2 * pos + 1]);
+    if (!fit && lane_id() == 0) {
+      admitted[w] = 0;
+      todo[1 + pos] = -1;
+    }
+  }
+}
+
+// The sweep's stable compaction of the todo list (one workgroup, in place:
+// every thread reads its share, a block scan of the kept counts, the writes
+// to lower or equal positions), then the window kernel's next phase.
+__global__ __launch_bounds__(1024) void admit_compact_kernel(int32_t* todo, int64_t* todo_r, int32_t* st) {
+  __shared__ int32_t sh_scan[1024];
+  if (!st[AS_SWEEP] || st[AS_DONE]) return;
+  const int w0 = st[AS_W0], ntodo = st[AS_NTODO];
+  constexpr int kPer = 16;
+  int out_base = w0;
+  for (int seg = w0; seg < ntodo; seg += kPer * int(blockDim.x)) {
+    const int p0 = seg + int(threadIdx.x) * kPer;
+    int ww[kPer];
+    int64_t rr0[kPer], rr1[kPer];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const int p = p0 + u;
+      ww[u] = p < ntodo ? todo[1 + p] : -1;
+      rr0[u] = ww[u] >= 0 ? todo_r[2 * p] : 0;
+      rr1[u] = ww[u] >= 0 ? todo_r[2 * p + 1] : 0;
+      cnt += ww[u] >= 0 ? 1 : 0;
+    }
+    sh_scan[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int off = 1; off < int(blockDim.x); off <<= 1) {
+      const int v = threadIdx.x >= unsigned(off) ? sh_scan[threadIdx.x - off] : 0;
+      __syncthreads();
+      sh_scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    int o = out_base + sh_scan[threadIdx.x] - cnt;
+    const int seg_total = sh_scan[blockDim.x - 1];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; u++)
+      if (ww[u] >= 0) {
+        todo[1 + o] = ww[u];
+        todo_r[2 * o] = rr0[u];
+        todo_r[2 * o + 1] = rr1[u];
+        o++;
+      }
+    out_base += seg_total;
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int swept_from = ntodo - w0;
+    if (4 * (swept_from - (out_base - w0)) < swept_from) st[AS_GATE] *= 4;  // as the in-kernel sweep
+    st[AS_NTODO] = out_base;
+    st[AS_SWEEPS] += 1;
+    st[AS_SWEEP] = 0;
   }
 }
 

@@ -243,6 +243,52 @@ def test_admit_batch_on_gpu(tiny, serial):
     _admit_batch(lambda d: TASFlavorSnapshot(d, serial_admit=serial), n=256, shape=(2, 4, 8, 16), huge_memory=tiny)
 
 
+@pytest.mark.parametrize("phases", ["1", "6"])
+def test_emulated_admit_phases(emu_lib, phases):  # noqa: F811
+    """admit_window_kernel in phases with the rejection sweeps on the grid
+    between them (KTAS_ADMIT_PHASES, default 6) or all in one workgroup (1):
+    the same decisions as the oracle session."""
+    import os
+
+    old = os.environ.get("KTAS_ADMIT_PHASES")
+    os.environ["KTAS_ADMIT_PHASES"] = phases
+    try:
+        _admit_batch(lambda d: TASFlavorSnapshot(d, lib=emu_lib), n=384, shape=(2, 2, 4, 8))
+    finally:
+        if old is None:
+            os.environ.pop("KTAS_ADMIT_PHASES")
+        else:
+            os.environ["KTAS_ADMIT_PHASES"] = old
+
+
+@pytest.mark.gpu
+def test_admit_8192_phases_match_serial_on_gpu():
+    """The 8-GPU admission load (8 x 1,024 gathered C3 candidates): grid
+    sweeps between window phases, one in-kernel phase and the one-wave chain
+    agree bit for bit."""
+    import os
+
+    import numpy as np
+
+    doc, wls = synth.config_c3(n_workloads=8192)
+    out = []
+    for phases, serial in (("6", False), ("1", False), ("6", True)):
+        os.environ["KTAS_ADMIT_PHASES"] = phases
+        try:
+            snap = TASFlavorSnapshot(doc, serial_admit=serial)
+        finally:
+            os.environ.pop("KTAS_ADMIT_PHASES")
+        snap.compile(wls)
+        snap.run_compiled()
+        admitted, deltas = snap.admit(snap.last_assignments())
+        out.append((admitted.copy(), np.sort(deltas, order=["leaf", "col"])))
+        snap.close()
+    for o in out[1:]:
+        assert (out[0][0] == o[0]).all()
+        assert (out[0][1] == o[1]).all()
+    assert 0 < int(out[0][0][:, 1].sum()) < len(wls)
+
+
 @pytest.mark.gpu
 def test_admit_window_matches_serial_c3_on_gpu():
     # the C3 bench batch (1,024 workloads, heavy leaf overlap: most are
