@@ -637,24 +637,53 @@ def admission_8192(snap, synth, flags, n=8 * 1024, reps=4):
     snapshot's workload set."""
     import numpy as np
 
+    import torch
+
     _, wls = synth.config_c3(n_workloads=n)
     snap.compile(wls)
     snap.set_shard(list(range(n)))
     snap.run_compiled(flags=flags)
-    quads = snap.last_assignments()
-    times, parts = [], []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        admitted, deltas = snap.admit(quads)
-        times.append((time.perf_counter() - t0) * 1e3)
-        parts.append(snap.last_admit_times())
-        stats = snap.last_admit_stats()
-        neg = deltas.copy()
-        neg["delta"] = -neg["delta"]
-        snap.apply_deltas(neg)
+    quads = snap.last_assignments().reshape(-1)
+    # the gathered block as RCCL's all-gather leaves it on rank 0's device:
+    # 8 rows [len, quads...], one per rank's 1,024 workloads
+    heads = np.flatnonzero(quads[1::4] < 0) * 4
+    cuts = [int(heads[k]) for k in range(1024, len(heads), 1024)]
+    bounds = [0] + cuts + [quads.size]
+    rows = [quads[bounds[k]:bounds[k + 1]] for k in range(len(bounds) - 1)]
+    cap = max(r.size for r in rows) + 1
+    blk = np.zeros((len(rows), cap), dtype=np.int32)
+    for r, row in enumerate(rows):
+        blk[r, 0] = row.size
+        blk[r, 1:1 + row.size] = row
+    block = torch.from_numpy(blk).to(torch.device("cuda", torch.cuda.current_device()))
+    lens = [r.size for r in rows]
+    torch.cuda.synchronize()
+
+    def rounds(admit):
+        times, parts = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            admitted, deltas = admit()
+            times.append((time.perf_counter() - t0) * 1e3)
+            parts.append(snap.last_admit_times())
+            stats = snap.last_admit_stats()
+            neg = deltas.copy()
+            neg["delta"] = -neg["delta"]
+            snap.apply_deltas(neg)
+        return times, parts, stats, admitted, deltas
+
+    times, parts, stats, admitted, deltas = rounds(lambda: snap.admit_block(block, lens))
+    htimes, hparts, _, hadm, hdel = rounds(lambda: snap.admit(quads))
+    same = bool((hadm == admitted).all() and len(hdel) == len(deltas) and (hdel == deltas).all())
     return {"candidates": n, "round_ms_median": round(float(np.median(times)), 3),
-            "parts_ms_median": dict(zip(["admit_host_prep", "admit_device", "admit_delta_list"],
+            "path": "kueue_tas_host_admit_block on the gathered device block (8 rows)",
+            "parts_ms_median": dict(zip(["admit_table", "admit_device", "admit_out"],
                                         [round(float(np.median([p[k] for p in parts])), 3) for k in range(3)])),
+            "host_path": {"round_ms_median": round(float(np.median(htimes)), 3),
+                          "parts_ms_median": dict(zip(["admit_host_prep", "admit_device", "admit_delta_list"],
+                                                      [round(float(np.median([p[k] for p in hparts])), 3)
+                                                       for k in range(3)])),
+                          "same_verdicts_and_deltas": same},
             "admitted": int(admitted[:, 1].sum()), "deltas": int(len(deltas)),
             "device_pass": dict(zip(["window_rounds", "in_order_candidates", "candidates"], [int(x) for x in stats]))}
 

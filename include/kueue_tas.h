@@ -55,6 +55,7 @@ extern "C" {
 #define KUEUE_TAS_EDEVICE -3
 #define KUEUE_TAS_ENOSNAPSHOT -4
 #define KUEUE_TAS_EOVERFLOW -5
+#define KUEUE_TAS_ELAYOUT -6    /* kueue_tas_admit_block: the block is not in the assignments layout */
 
 typedef struct kueue_tas_ctx kueue_tas_ctx;
 
@@ -399,6 +400,27 @@ int kueue_tas_fits(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n,
  * pods_col; -1: no pods column).  Every term's col must be >= 0. */
 int kueue_tas_admit(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
                     size_t num_terms, const int64_t* wl_off, size_t n_workloads, int32_t pods_col, int32_t* admitted);
+/* The same admission from the gathered block on the device (no host round
+ * trip of the quads: the all-gather's receive block, rank 0's admission at 8
+ * GPUs).  kueue_tas_admit_table first: for each of num_workloads compiled
+ * workloads its PodSets ps_base[w] .. ps_base[w + 1], each PodSet's
+ * single-pod request terms (begin, n) = ps_terms[2 p], ps_terms[2 p + 1]
+ * into terms (ComputeTASNetUsage, flavorassigner.go:94-130).  block: device
+ * pointer, world rows of row_words int32 = [len, quads...] with lens[r] the
+ * row's len (kueue_tas_host_last_assignments' quads: every workload's header
+ * followed by its domain quads, each id once); world <= 16.  Out: the present
+ * workloads in ascending id in ids[0 .. *n_workloads), admitted[] their
+ * verdicts (cap: KUEUE_TAS_EOVERFLOW when short, nothing admitted), and the
+ * applied delta list in kueue_tas_host_admit's order (*deltas valid until the
+ * next call).  KUEUE_TAS_ELAYOUT (nothing admitted) when the block is not in
+ * that layout: the caller admits through the host path. */
+/* bytes from device memory of ctx's device to host memory (synchronous) */
+int kueue_tas_copy_to_host(kueue_tas_ctx* ctx, void* dst, const void* src, size_t bytes);
+int kueue_tas_admit_table(kueue_tas_ctx* ctx, const int32_t* ps_base, int32_t num_workloads, const int32_t* ps_terms,
+                          const kueue_tas_fits_term* terms, size_t num_terms);
+int kueue_tas_admit_block(kueue_tas_ctx* ctx, const int32_t* block, size_t row_words, const int64_t* lens,
+                          int32_t world, int32_t pods_col, int32_t* ids, int32_t* admitted, size_t cap,
+                          size_t* n_workloads, const kueue_tas_delta** deltas, size_t* n_deltas);
 
 /* ---- v1beta2 compact TopologyAssignment encoding -------------------------
  * V1Beta2From / singleCompactSliceEncoding (pkg/util/tas/tas_assignment.go:
@@ -503,6 +525,13 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* quads, size_t len, in
                          size_t* n_workloads, size_t* n_deltas);
 int kueue_tas_host_last_deltas(kueue_tas_host* h, kueue_tas_delta* buf, size_t cap);
 int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* deltas, size_t n);
+/* admit from the all-gather's device block (kueue_tas_admit_block; block and
+ * lens as gather_assignments leaves them): the same verdicts, admitted pairs
+ * and delta list as kueue_tas_host_admit over the block's quads; a block
+ * outside the assignments layout is copied to the host and admitted there. */
+int kueue_tas_host_admit_block(kueue_tas_host* h, const int32_t* block, size_t row_words, const int64_t* lens,
+                               int32_t world, int32_t* admitted, size_t admitted_cap, size_t* n_workloads,
+                               size_t* n_deltas);
 
 /* Every result of the last run_compiled as {"results": [[{"name",
  * "assignment","reason"}...] per compiled workload]} (kueue_tas_free). */

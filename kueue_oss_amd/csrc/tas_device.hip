@@ -354,6 +354,12 @@ struct kueue_tas_ctx {
   float last_stage_ms[KUEUE_TAS_NUM_STAGES] = {};
   std::vector<MagicCache> magic_cache;  // per host part (compute_magic)
   std::vector<int32_t> h_gsrc;          // a splice's leaf sources (load_impl)
+  DevBuf<int32_t> d_adm_ps;             // kueue_tas_admit_table: podset base per workload [W + 1], then (begin, n) per podset
+  DevBuf<kueue_tas_fits_term> d_adm_terms;  // and the podsets' single-pod request terms
+  int32_t adm_W = -1;                   // workloads of the admission table (-1: none)
+  DevBuf<kueue_tas_delta> d_adm_deltas; // kueue_tas_admit_block's delta list
+  HostBuf<kueue_tas_delta> h_adm_deltas;
+  double admit_block_ms = 0;
   std::vector<int32_t> ctr_row_off;     // last batch: each fill position's class row offset (units of SD)
   std::vector<int32_t> level_maxfan;    // [L] the widest parent's child count per level (last load)
   std::vector<int32_t> sel_groups;      // last batch: BestFit-side slot groups (select launches), bounds
@@ -432,6 +438,10 @@ static int fail(kueue_tas_ctx* c, int code, const std::string& msg) {
   } while (0)
 
 extern "C" {
+
+static double wall_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 int kueue_tas_abi_version(void) { return KUEUE_TAS_ABI_VERSION; }
 
@@ -1280,6 +1290,39 @@ int kueue_tas_fits(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, c
   return KUEUE_TAS_OK;
 }
 
+static size_t admit_al(size_t b) { return (b + 255) / 256 * 256; }
+// kueue_tas_admit's device buffer (c->d_fits): the uploaded part [0, up_bytes)
+// (records, terms, workload offsets, record -> workload, phase-1 flags, the
+// exact flag, the per-column totals), then the verdicts (+ diagnostics), the
+// phase-1 records, the window kernel's lists, the per-leaf minima, the touched
+// bitmap and the window phases' state.
+struct AdmitLayout {
+  size_t o_terms, o_off, o_recwl, o_fit0, o_exact, o_total, up_bytes;
+  size_t o_out, o_recs, o_dep, o_todo, o_todor, o_minc, o_bits, o_state, end;
+};
+static AdmitLayout admit_layout(size_t n, size_t num_terms, size_t n_wl, size_t N) {
+  AdmitLayout L{};
+  L.o_terms = admit_al(n * sizeof(kueue_tas_fits_req));
+  L.o_off = L.o_terms + admit_al(num_terms * sizeof(kueue_tas_fits_term));
+  L.o_recwl = L.o_off + admit_al((n_wl + 1) * 8);
+  L.o_fit0 = L.o_recwl + admit_al(n * 4);
+  L.o_exact = L.o_fit0 + admit_al(n_wl * 4);
+  L.o_total = L.o_exact + 256;
+  L.up_bytes = L.o_total + KUEUE_TAS_MAX_COLS * 8;
+  L.o_out = admit_al(L.up_bytes);
+  L.o_recs = L.o_out + admit_al((n_wl + 3) * 4);  // + three diagnostics words (admit_window_kernel)
+  L.o_dep = L.o_recs + admit_al(n * sizeof(AdmitRec));
+  L.o_todo = L.o_dep + admit_al(n_wl * 4);
+  L.o_todor = L.o_todo + admit_al((n_wl + 1) * 4);
+  L.o_minc = L.o_todor + admit_al(n_wl * 16);
+  L.o_bits = L.o_minc + admit_al(N * 4);
+  L.o_state = L.o_bits + admit_al((N + 31) / 32 * 4);  // admit_window_kernel's phase state (AdmitState)
+  L.end = L.o_state + 256;
+  return L;
+}
+static int admit_run(kueue_tas_ctx* c, const AdmitLayout& L, uint8_t* d, const kueue_tas_fits_term* d_terms, size_t n,
+                     size_t n_wl, int32_t pods_col, bool exact);
+
 int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, const kueue_tas_fits_term* terms,
                     size_t num_terms, const int64_t* wl_off, size_t n_wl, int32_t pods_col, int32_t* admitted) {
   if (!c) return KUEUE_TAS_EINVAL;
@@ -1347,15 +1390,200 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   HIPCHK(c, hipSetDevice(c->device));
   // one pinned upload: records, terms, workload offsets, record -> workload,
   // phase-1 flags (1 = fit) and the exact flag
-  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t o_terms = al(n * sizeof(kueue_tas_fits_req));
-  const size_t o_off = o_terms + al(num_terms * sizeof(kueue_tas_fits_term));
-  const size_t o_recwl = o_off + al((n_wl + 1) * 8);
-  const size_t o_fit0 = o_recwl + al(n * 4);
-  const size_t o_exact = o_fit0 + al(n_wl * 4);
-  const size_t o_total = o_exact + 256;
-  const size_t up_bytes = o_total + KUEUE_TAS_MAX_COLS * 8;
-  const size_t o_out = al(up_bytes);
+  const AdmitLayout L = admit_layout(n, num_terms, n_wl, size_t(c->snap.N));
+  HIPCHK(c, c->d_fits.ensure(L.end));
+  HIPCHK(c, c->h_stage.ensure(L.up_bytes));
+  uint8_t* h = c->h_stage.p;
+  if (num_terms) memcpy(h + L.o_terms, terms, num_terms * sizeof(kueue_tas_fits_term));
+  memcpy(h + L.o_off, wl_off, (n_wl + 1) * 8);
+  int32_t* rec_wl = reinterpret_cast<int32_t*>(h + L.o_recwl);
+  pool.run_static(n_wl, [&](size_t w0, size_t w1) {  // the records and their workload, per workload range
+    if (w1 > w0 && wl_off[w1] > wl_off[w0])
+      memcpy(h + size_t(wl_off[w0]) * sizeof(kueue_tas_fits_req), reqs + wl_off[w0],
+             size_t(wl_off[w1] - wl_off[w0]) * sizeof(kueue_tas_fits_req));
+    for (size_t w = w0; w < w1; w++)
+      for (int64_t i = wl_off[w]; i < wl_off[w + 1]; i++) rec_wl[i] = int32_t(w);
+  });
+  int32_t* fit0 = reinterpret_cast<int32_t*>(h + L.o_fit0);
+  for (size_t w = 0; w < n_wl; w++) fit0[w] = 1;
+  *reinterpret_cast<int32_t*>(h + L.o_exact) = exact ? 1 : 0;
+  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++)
+    reinterpret_cast<int64_t*>(h + L.o_total)[k] = exact ? 0 : int64_t(total[k]);
+  uint8_t* d = c->d_fits.p;
+  HIPCHK(c, hipMemcpyAsync(d, h, L.up_bytes, hipMemcpyHostToDevice, c->stream));
+  const int rc = admit_run(c, L, d, reinterpret_cast<const kueue_tas_fits_term*>(d + L.o_terms), n, n_wl, pods_col, exact);
+  if (rc) return rc;
+  HIPCHK(c, c->h_admit.reserve(n_wl + 3));
+  HIPCHK(c, hipMemcpyAsync(c->h_admit.p, d + L.o_out, (n_wl + 3) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(admitted, c->h_admit.p, n_wl * 4);
+  c->admit_stats[0] = c->admit_window ? c->h_admit.p[n_wl] : -1;
+  c->admit_stats[1] = c->admit_window ? c->h_admit.p[n_wl + 1] : -1;
+  c->admit_stats[2] = int64_t(n_wl);
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_copy_to_host(kueue_tas_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!c || (bytes && (!dst || !src))) return KUEUE_TAS_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (bytes) HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_admit_table(kueue_tas_ctx* c, const int32_t* ps_base, int32_t num_workloads, const int32_t* ps_terms,
+                          const kueue_tas_fits_term* terms, size_t num_terms) {
+  if (!c || num_workloads < 0 || !ps_base || (num_terms && !terms)) return KUEUE_TAS_EINVAL;
+  const int32_t P = ps_base[num_workloads];
+  if (P < 0 || (P && !ps_terms)) return fail(c, KUEUE_TAS_EINVAL, "admit table: podsets");
+  for (int32_t w = 0; w < num_workloads; w++)
+    if (ps_base[w + 1] < ps_base[w] || ps_base[0] != 0) return fail(c, KUEUE_TAS_EINVAL, "admit table: podset offsets");
+  for (int32_t p = 0; p < P; p++)
+    if (ps_terms[2 * p] < 0 || ps_terms[2 * p + 1] < 0 || size_t(ps_terms[2 * p]) + size_t(ps_terms[2 * p + 1]) > num_terms)
+      return fail(c, KUEUE_TAS_EINVAL, "admit table: term range");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, c->d_adm_ps.ensure(size_t(num_workloads) + 1 + 2 * size_t(P)));
+  HIPCHK(c, c->d_adm_terms.ensure(std::max<size_t>(num_terms, 1)));
+  HIPCHK(c, hipMemcpy(c->d_adm_ps.p, ps_base, (size_t(num_workloads) + 1) * 4, hipMemcpyHostToDevice));
+  if (P) HIPCHK(c, hipMemcpy(c->d_adm_ps.p + num_workloads + 1, ps_terms, 2 * size_t(P) * 4, hipMemcpyHostToDevice));
+  if (num_terms)
+    HIPCHK(c, hipMemcpy(c->d_adm_terms.p, terms, num_terms * sizeof(kueue_tas_fits_term), hipMemcpyHostToDevice));
+  c->adm_W = num_workloads;
+  return KUEUE_TAS_OK;
+}
+
+int kueue_tas_admit_block(kueue_tas_ctx* c, const int32_t* block, size_t row_words, const int64_t* lens,
+                          int32_t world, int32_t pods_col, int32_t* ids, int32_t* admitted, size_t cap,
+                          size_t* n_workloads, const kueue_tas_delta** deltas, size_t* n_deltas) {
+  if (!c) return KUEUE_TAS_EINVAL;
+  if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
+  if (!block || !lens || !ids || !admitted || !n_workloads || !deltas || !n_deltas || world < 1)
+    return fail(c, KUEUE_TAS_EINVAL, "null argument");
+  if (world > kAdmitMaxRows) return fail(c, KUEUE_TAS_EINVAL, "admit block: more rows than supported");
+  if (c->adm_W < 0) return fail(c, KUEUE_TAS_EINVAL, "admit block: no admission table (kueue_tas_admit_table)");
+  if (pods_col < -1 || pods_col >= c->snap.R) return fail(c, KUEUE_TAS_EINVAL, "pods column out of range");
+  AdmitRows rows{};
+  rows.row_words = int64_t(row_words);
+  rows.world = world;
+  size_t Q = 0;
+  int32_t maxq = 0;
+  for (int r = 0; r < world; r++) {
+    if (lens[r] < 0 || lens[r] % 4 || size_t(lens[r]) + 1 > row_words) return fail(c, KUEUE_TAS_EINVAL, "admit block: row length");
+    rows.nq[r] = int32_t(lens[r] / 4);
+    maxq = std::max(maxq, rows.nq[r]);
+    Q += size_t(rows.nq[r]);
+  }
+  const int W = c->adm_W;
+  HIPCHK(c, hipSetDevice(c->device));
+  // the layout of the host path with the bounds (records <= quads, workloads <= W)
+  const AdmitLayout L = admit_layout(std::max<size_t>(Q, 1), 0, size_t(W), size_t(c->snap.N));
+  // per id: flag, run position, quad count; hdr: workloads, records, deltas; errors; exact; totals (lo, hi)
+  const size_t o_flag = L.end, o_pos = o_flag + admit_al(size_t(W) * 4), o_nd = o_pos + admit_al(size_t(W) * 8),
+               o_ids = o_nd + admit_al(size_t(W) * 4), o_hdr = o_ids + admit_al(size_t(W) * 4),
+               o_tot = o_hdr + 256, o_blk = o_tot + admit_al(KUEUE_TAS_MAX_COLS * 16),
+               nblk = (std::max<size_t>(Q, 1) + 255) / 256, o_dl = o_blk + admit_al(nblk * 4);
+  HIPCHK(c, c->d_fits.ensure(o_dl + 16));
+  uint8_t* d = c->d_fits.p;
+  int32_t* hdr = reinterpret_cast<int32_t*>(d + o_hdr);  // [0] workloads [1] records [2] deltas [3] errors [4] negative
+  HIPCHK(c, hipMemsetAsync(d + o_flag, 0, size_t(W) * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(d + o_hdr, 0, 256 + admit_al(KUEUE_TAS_MAX_COLS * 16), c->stream));
+  const double t0 = wall_ms();
+  if (maxq > 0) {
+    hipLaunchKernelGGL(admit_block_headers_kernel, dim3(unsigned((maxq + 255) / 256), unsigned(world)), dim3(256), 0,
+                       c->stream, block, rows, W, reinterpret_cast<int32_t*>(d + o_flag),
+                       reinterpret_cast<int64_t*>(d + o_pos), reinterpret_cast<int32_t*>(d + o_nd), hdr + 3);
+    HIPCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(admit_block_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, W,
+                     reinterpret_cast<const int32_t*>(d + o_flag), reinterpret_cast<const int32_t*>(d + o_nd),
+                     reinterpret_cast<int32_t*>(d + o_ids), reinterpret_cast<int64_t*>(d + L.o_off),
+                     reinterpret_cast<int32_t*>(d + L.o_fit0), hdr);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, c->h_admit.reserve(size_t(W) + 3 + 64 + KUEUE_TAS_MAX_COLS * 4));
+  int32_t* hh = c->h_admit.p;
+  HIPCHK(c, hipMemcpyAsync(hh, hdr, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int32_t n_wl = hh[0], n = hh[1];
+  if (hh[3] & (ABE_DUP | ABE_LAYOUT | ABE_ID)) return fail(c, KUEUE_TAS_ELAYOUT, "admit block: not the assignments layout");
+  *n_workloads = size_t(n_wl);
+  if (cap < size_t(n_wl)) return KUEUE_TAS_EOVERFLOW;
+  const size_t nwl = size_t(n_wl), nr = size_t(n);
+  if (nwl) {
+    hipLaunchKernelGGL(admit_block_records_kernel, dim3(unsigned((nwl + 3) / 4)), dim3(256), 0, c->stream, block,
+                       c->snap.N, W, reinterpret_cast<const int32_t*>(d + o_ids), reinterpret_cast<const int64_t*>(d + L.o_off),
+                       reinterpret_cast<const int32_t*>(d + o_flag), reinterpret_cast<const int64_t*>(d + o_pos),
+                       reinterpret_cast<const int32_t*>(d + o_nd), c->d_adm_ps.p, c->d_adm_ps.p + W + 1,
+                       c->d_adm_terms.p, n_wl, pods_col, reinterpret_cast<kueue_tas_fits_req*>(d),
+                       reinterpret_cast<int32_t*>(d + L.o_recwl), reinterpret_cast<unsigned long long*>(d + o_tot),
+                       hdr + 4, hdr + 3);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipMemcpyAsync(hh, hdr, 32, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(hh + 8, d + o_tot, KUEUE_TAS_MAX_COLS * 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int32_t errs = hh[3];
+  if (errs & ABE_LAYOUT) return fail(c, KUEUE_TAS_ELAYOUT, "admit block: not the assignments layout");
+  if (errs & ABE_RANGE) return fail(c, KUEUE_TAS_EINVAL, "admit: record out of range");
+  if (errs & ABE_COL) return fail(c, KUEUE_TAS_EINVAL, "admit: request resource without a column");
+  bool exact = hh[4] != 0;
+  const uint64_t* tot = reinterpret_cast<const uint64_t*>(hh + 8);
+  int64_t tot64[KUEUE_TAS_MAX_COLS];
+  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++) {
+    exact = exact || tot[2 * k + 1] != 0 || tot[2 * k] >= (uint64_t(1) << 61);
+    tot64[k] = int64_t(tot[2 * k]);
+  }
+  // the exact flag and the totals, as the host path uploads them
+  HIPCHK(c, c->h_stage.ensure(8 + KUEUE_TAS_MAX_COLS * 8));
+  int32_t* hx = reinterpret_cast<int32_t*>(c->h_stage.p);
+  hx[0] = exact ? 1 : 0;
+  HIPCHK(c, hipMemcpyAsync(d + L.o_exact, hx, 4, hipMemcpyHostToDevice, c->stream));
+  int64_t* ht = reinterpret_cast<int64_t*>(c->h_stage.p + 8);
+  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++) ht[k] = exact ? 0 : tot64[k];
+  HIPCHK(c, hipMemcpyAsync(d + L.o_total, ht, KUEUE_TAS_MAX_COLS * 8, hipMemcpyHostToDevice, c->stream));
+  const int rc = admit_run(c, L, d, c->d_adm_terms.p, nr, nwl, pods_col, exact);
+  if (rc) return rc;
+  // the admitted workloads' deltas on the device, in the host path's order
+  const int32_t* adm_d = reinterpret_cast<const int32_t*>(d + L.o_out);
+  const size_t nb = (std::max<size_t>(nr, 1) + 255) / 256;
+  int32_t* blk = reinterpret_cast<int32_t*>(d + o_blk);
+  if (nr) {
+    hipLaunchKernelGGL(admit_delta_blocks_kernel, dim3(unsigned(nb)), dim3(256), 0, c->stream,
+                       reinterpret_cast<const kueue_tas_fits_req*>(d), reinterpret_cast<const int32_t*>(d + L.o_recwl),
+                       adm_d, n, pods_col, blk);
+    hipLaunchKernelGGL(admit_delta_offsets_kernel, dim3(1), dim3(1024), 0, c->stream, blk, int(nb), hdr);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipMemcpyAsync(hh, d + L.o_out, (nwl + 3) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(hh + nwl + 3, hdr, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ids, d + o_ids, nwl * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(admitted, hh, nwl * 4);
+  c->admit_stats[0] = c->admit_window ? hh[nwl] : -1;
+  c->admit_stats[1] = c->admit_window ? hh[nwl + 1] : -1;
+  c->admit_stats[2] = int64_t(nwl);
+  const size_t ndl = nr ? size_t(hh[nwl + 3 + 2]) : 0;
+  HIPCHK(c, c->d_adm_deltas.ensure(std::max<size_t>(ndl, 1)));
+  HIPCHK(c, c->h_adm_deltas.reserve(std::max<size_t>(ndl, 1)));
+  if (ndl) {
+    hipLaunchKernelGGL(admit_delta_write_kernel, dim3(unsigned(nb)), dim3(256), 0, c->stream,
+                       reinterpret_cast<const kueue_tas_fits_req*>(d), c->d_adm_terms.p,
+                       reinterpret_cast<const int32_t*>(d + L.o_recwl), adm_d, n, pods_col, blk, c->d_adm_deltas.p);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->h_adm_deltas.p, c->d_adm_deltas.p, ndl * sizeof(kueue_tas_delta),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  *deltas = c->h_adm_deltas.p;
+  *n_deltas = ndl;
+  c->admit_block_ms = wall_ms() - t0;
+  return KUEUE_TAS_OK;
+}
+
+// The admission pass over the records in c->d_fits (layout L): phase 1
+// (admit_fit0_kernel), the order-free candidates in parallel unless exact,
+// then the in-order pass (admit_window_kernel in phases with grid sweeps, or
+// the one-wave chain).  Verdicts at L.o_out.
+static int admit_run(kueue_tas_ctx* c, const AdmitLayout& L, uint8_t* d, const kueue_tas_fits_term* d_terms, size_t n,
+                     size_t n_wl, int32_t pods_col, bool exact) {
   const size_t nwords = (size_t(c->snap.N) + 31) / 32;
   // the dynamic bitmaps share the workgroup's 64 KB of LDS with the kernel's
   // static arrays (the window kernel's fit / conflict flags and sweep scan)
@@ -1375,109 +1603,74 @@ int kueue_tas_admit(kueue_tas_ctx* c, const kueue_tas_fits_req* reqs, size_t n, 
   const bool lds_bits = nwords * 4 <= lds_budget;
   // the windowed kernel's round bitmap beside the touched one: admission chains within a window
   const bool lds_chain = c->admit_window && 2 * nwords * 4 <= lds_budget;
-  const size_t o_recs = o_out + al((n_wl + 3) * 4);  // + three diagnostics words (admit_window_kernel)
-  const size_t o_dep = o_recs + al(n * sizeof(AdmitRec));
-  const size_t o_todo = o_dep + al(n_wl * 4);
-  const size_t o_todor = o_todo + al((n_wl + 1) * 4);
-  const size_t o_minc = o_todor + al(n_wl * 16);
-  const size_t o_bits = o_minc + al(size_t(c->snap.N) * 4);
-  const size_t o_state = o_bits + al(nwords * 4);  // admit_window_kernel's phase state (AdmitState)
-  HIPCHK(c, c->d_fits.ensure(o_state + 256));
-  HIPCHK(c, c->h_stage.ensure(up_bytes));
-  uint8_t* h = c->h_stage.p;
-  if (num_terms) memcpy(h + o_terms, terms, num_terms * sizeof(kueue_tas_fits_term));
-  memcpy(h + o_off, wl_off, (n_wl + 1) * 8);
-  int32_t* rec_wl = reinterpret_cast<int32_t*>(h + o_recwl);
-  pool.run_static(n_wl, [&](size_t w0, size_t w1) {  // the records and their workload, per workload range
-    if (w1 > w0 && wl_off[w1] > wl_off[w0])
-      memcpy(h + size_t(wl_off[w0]) * sizeof(kueue_tas_fits_req), reqs + wl_off[w0],
-             size_t(wl_off[w1] - wl_off[w0]) * sizeof(kueue_tas_fits_req));
-    for (size_t w = w0; w < w1; w++)
-      for (int64_t i = wl_off[w]; i < wl_off[w + 1]; i++) rec_wl[i] = int32_t(w);
-  });
-  int32_t* fit0 = reinterpret_cast<int32_t*>(h + o_fit0);
-  for (size_t w = 0; w < n_wl; w++) fit0[w] = 1;
-  *reinterpret_cast<int32_t*>(h + o_exact) = exact ? 1 : 0;
-  for (int k = 0; k < KUEUE_TAS_MAX_COLS; k++)
-    reinterpret_cast<int64_t*>(h + o_total)[k] = exact ? 0 : int64_t(total[k]);
-  uint8_t* d = c->d_fits.p;
-  HIPCHK(c, hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(d + o_bits, 0, nwords * 4, c->stream));
-  HIPCHK(c, hipMemsetAsync(d + o_state, 0, 256, c->stream));
+  HIPCHK(c, hipMemsetAsync(d + L.o_bits, 0, nwords * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(d + L.o_state, 0, 256, c->stream));
   // order-free candidates decided in parallel (admit_minc / dep / indep), unless exact
   const bool indep = c->admit_window && !exact && n > 0;
   if (indep) {
-    HIPCHK(c, hipMemsetAsync(d + o_minc, 0x7f, size_t(c->snap.N) * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(d + o_dep, 0, n_wl * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(d + L.o_minc, 0x7f, size_t(c->snap.N) * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(d + L.o_dep, 0, n_wl * 4, c->stream));
   }
   const auto* d_reqs = reinterpret_cast<const kueue_tas_fits_req*>(d);
-  const auto* d_terms = reinterpret_cast<const kueue_tas_fits_term*>(d + o_terms);
   if (n) {
     hipLaunchKernelGGL(admit_fit0_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, c->stream, c->snap,
                        c->d_usage.p, c->d_usage_present.p, d_reqs, d_terms,
-                       reinterpret_cast<const int32_t*>(d + o_recwl), int(n), reinterpret_cast<const int64_t*>(d + o_total),
-                       reinterpret_cast<int32_t*>(d + o_fit0), reinterpret_cast<AdmitRec*>(d + o_recs),
-                       reinterpret_cast<int32_t*>(d + o_exact));
+                       reinterpret_cast<const int32_t*>(d + L.o_recwl), int(n), reinterpret_cast<const int64_t*>(d + L.o_total),
+                       reinterpret_cast<int32_t*>(d + L.o_fit0), reinterpret_cast<AdmitRec*>(d + L.o_recs),
+                       reinterpret_cast<int32_t*>(d + L.o_exact));
     HIPCHK(c, hipGetLastError());
   }
   if (c->admit_window) {  // independent candidates in parallel, the rest windowed (one 1024-thread workgroup)
-    const auto* recwl = reinterpret_cast<const int32_t*>(d + o_recwl);
-    const auto* fit0d = reinterpret_cast<const int32_t*>(d + o_fit0);
-    auto* depd = reinterpret_cast<int32_t*>(d + o_dep);
+    const auto* recwl = reinterpret_cast<const int32_t*>(d + L.o_recwl);
+    const auto* fit0d = reinterpret_cast<const int32_t*>(d + L.o_fit0);
+    auto* depd = reinterpret_cast<int32_t*>(d + L.o_dep);
     if (indep) {
       const dim3 g(unsigned((n + 255) / 256));
       hipLaunchKernelGGL(admit_minc_kernel, g, dim3(256), 0, c->stream, d_reqs, recwl, int(n), fit0d, c->snap.N,
-                         reinterpret_cast<int32_t*>(d + o_minc));
+                         reinterpret_cast<int32_t*>(d + L.o_minc));
       hipLaunchKernelGGL(admit_dep_kernel, g, dim3(256), 0, c->stream, d_reqs, recwl, int(n), fit0d, c->snap.N,
-                         reinterpret_cast<const int32_t*>(d + o_minc), depd);
+                         reinterpret_cast<const int32_t*>(d + L.o_minc), depd);
       hipLaunchKernelGGL(admit_indep_kernel, g, dim3(256), 0, c->stream, c->snap, c->d_usage.p, c->d_usage_present.p,
-                         d_reqs, d_terms, recwl, int(n), fit0d, depd, pods_col, reinterpret_cast<uint32_t*>(d + o_bits));
+                         d_reqs, d_terms, recwl, int(n), fit0d, depd, pods_col, reinterpret_cast<uint32_t*>(d + L.o_bits));
       HIPCHK(c, hipGetLastError());
     }
     hipLaunchKernelGGL(admit_todo_kernel, dim3(1), dim3(1024), 0, c->stream, int(n_wl), fit0d, depd, indep ? 0 : 1,
-                       reinterpret_cast<int32_t*>(d + o_out), reinterpret_cast<int32_t*>(d + o_todo),
-                       reinterpret_cast<const int64_t*>(d + o_off), reinterpret_cast<int64_t*>(d + o_todor));
+                       reinterpret_cast<int32_t*>(d + L.o_out), reinterpret_cast<int32_t*>(d + L.o_todo),
+                       reinterpret_cast<const int64_t*>(d + L.o_off), reinterpret_cast<int64_t*>(d + L.o_todor));
     HIPCHK(c, hipGetLastError());
     // the window kernel in phases: each stops at a rejection sweep, which the
     // grid runs (a wave per remaining candidate) before the next phase
     // resumes; the last phase sweeps inside its workgroup.  A finished pass
     // leaves the later launches nothing to do.
-    int32_t* st = reinterpret_cast<int32_t*>(d + o_state);
-    int32_t* todo = reinterpret_cast<int32_t*>(d + o_todo);
-    int64_t* todor = reinterpret_cast<int64_t*>(d + o_todor);
+    int32_t* st = reinterpret_cast<int32_t*>(d + L.o_state);
+    int32_t* todo = reinterpret_cast<int32_t*>(d + L.o_todo);
+    int64_t* todor = reinterpret_cast<int64_t*>(d + L.o_todor);
     const int phases = c->admit_grid_sweeps;
     for (int ph = 0; ph < phases; ph++) {
       if (ph > 0) {
         hipLaunchKernelGGL(admit_sweep_kernel, dim3(1024), dim3(256), 0, c->stream, c->snap, c->d_usage.p,
-                           c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs), fit0d,
-                           reinterpret_cast<const uint32_t*>(d + o_bits), reinterpret_cast<int32_t*>(d + o_out), todo,
+                           c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + L.o_recs), fit0d,
+                           reinterpret_cast<const uint32_t*>(d + L.o_bits), reinterpret_cast<int32_t*>(d + L.o_out), todo,
                            todor, st);
         hipLaunchKernelGGL(admit_compact_kernel, dim3(1), dim3(1024), 0, c->stream, todo, todor, st);
       }
       hipLaunchKernelGGL(admit_window_kernel, dim3(1), dim3(64 * kAdmitWindow),
                          lds_chain ? 2 * nwords * 4 : lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
-                         c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
-                         reinterpret_cast<const int64_t*>(d + o_off), int(n_wl), pods_col,
-                         reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
-                         reinterpret_cast<uint32_t*>(d + o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
-                         reinterpret_cast<int32_t*>(d + o_out), todo, todor, st, ph + 1 < phases ? 1 : 0);
+                         c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + L.o_recs),
+                         reinterpret_cast<const int64_t*>(d + L.o_off), int(n_wl), pods_col,
+                         reinterpret_cast<const int32_t*>(d + L.o_fit0), reinterpret_cast<const int32_t*>(d + L.o_exact),
+                         reinterpret_cast<uint32_t*>(d + L.o_bits), lds_chain ? 2 : lds_bits ? 1 : 0,
+                         reinterpret_cast<int32_t*>(d + L.o_out), todo, todor, st, ph + 1 < phases ? 1 : 0);
       HIPCHK(c, hipGetLastError());
     }
   } else {  // one wave down the chain
     hipLaunchKernelGGL(admit_kernel, dim3(1), dim3(64), lds_bits ? nwords * 4 : 0, c->stream, c->snap, c->d_usage.p,
-                       c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + o_recs),
-                       reinterpret_cast<const int64_t*>(d + o_off), int(n_wl),
-                       pods_col, reinterpret_cast<const int32_t*>(d + o_fit0), reinterpret_cast<const int32_t*>(d + o_exact),
-                       reinterpret_cast<uint32_t*>(d + o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + o_out));
+                       c->d_usage_present.p, d_reqs, d_terms, reinterpret_cast<const AdmitRec*>(d + L.o_recs),
+                       reinterpret_cast<const int64_t*>(d + L.o_off), int(n_wl),
+                       pods_col, reinterpret_cast<const int32_t*>(d + L.o_fit0), reinterpret_cast<const int32_t*>(d + L.o_exact),
+                       reinterpret_cast<uint32_t*>(d + L.o_bits), lds_bits ? 1 : 0, reinterpret_cast<int32_t*>(d + L.o_out));
   }
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, c->h_admit.reserve(n_wl + 3));
-  HIPCHK(c, hipMemcpyAsync(c->h_admit.p, d + o_out, (n_wl + 3) * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  memcpy(admitted, c->h_admit.p, n_wl * 4);
-  c->admit_stats[0] = c->admit_window ? c->h_admit.p[n_wl] : -1;
-  c->admit_stats[1] = c->admit_window ? c->h_admit.p[n_wl + 1] : -1;
-  c->admit_stats[2] = int64_t(n_wl);
   return KUEUE_TAS_OK;
 }
 
@@ -1487,9 +1680,6 @@ int kueue_tas_last_admit_stats(kueue_tas_ctx* c, int64_t* out3) {
   return KUEUE_TAS_OK;
 }
 
-static double wall_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // The longest candidate list a BestFit-side walk of `ev` can build (its
 // select lists' capacity): every domain of a level at or above its requested

@@ -3569,6 +3569,7 @@ struct kueue_tas_host {
   std::unique_ptr<FlavorSnapshot> snap;
   std::string err;
   std::vector<Workload> compiled;
+  uint64_t compiled_gen = 0;  // bumped when the compiled workload set is replaced
   std::unique_ptr<Evaluator> ev;
   std::vector<std::vector<PodSetResult>> last;
   float ms[4] = {0, 0, 0, 0};
@@ -3583,7 +3584,8 @@ struct kueue_tas_host {
   std::vector<kueue_tas_delta> last_deltas;  // usage deltas the last kueue_tas_host_admit applied
   double admit_ms[3] = {0, 0, 0};            // last admit: host prep, kueue_tas_admit, delta list
   // admit's working storage (kept between rounds)
-  std::vector<int32_t> admit_seen, admit_ids;
+  std::vector<int32_t> admit_seen, admit_ids, admit_adm;
+  std::array<uint64_t, 3> admit_table_key{0, 0, 0};  // (compiled set, compile_gen, col_gen) of the device admission table
   std::vector<int32_t> admit_pseen;  // [part][workload] of the record passes on the host pool
   std::vector<int64_t> admit_pcnt;
   std::vector<int64_t> admit_start, admit_off;
@@ -4695,6 +4697,7 @@ int kueue_tas_host_compile(kueue_tas_host* h, const char* workloads_json) {
     h->shard_ids.clear();
     h->shard.clear();
     h->compiled.assign(doc["workloads"].items.size(), Workload{});
+    h->compiled_gen++;
     for (size_t i = 0; i < h->compiled.size(); i++) {
       h->compiled[i].podsets = parse_podsets(doc["workloads"].items[i]);
       make_groups(h->compiled[i]);
@@ -5166,6 +5169,85 @@ int kueue_tas_host_admit(kueue_tas_host* h, const int32_t* recs, size_t len, int
       }
     }
     if (n_deltas) *n_deltas = deltas.size();
+    s.device_applied();
+    h->admit_ms[0] = t1 - t0;
+    h->admit_ms[1] = t2 - t1;
+    h->admit_ms[2] = now_ms() - t2;
+    return 0;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return KUEUE_TAS_EINVAL;
+  }
+}
+
+int kueue_tas_host_admit_block(kueue_tas_host* h, const int32_t* block, size_t row_words, const int64_t* lens,
+                               int32_t world, int32_t* admitted, size_t admitted_cap, size_t* n_workloads,
+                               size_t* n_deltas) {
+  if (!h || !h->snap || !h->err.empty() || !block || !lens || world < 1 || !n_workloads) return KUEUE_TAS_EINVAL;
+  try {
+    FlavorSnapshot& s = *h->snap;
+    const double t0 = now_ms();
+    int rc = s.upload();
+    if (rc) {
+      h->err = s.err;
+      return rc;
+    }
+    const size_t W = h->compiled.size();
+    // the compiled workloads' per-PodSet request terms on the device, rebuilt
+    // when the compiled set or the columns change
+    const std::array<uint64_t, 3> key{h->compiled_gen, s.compile_gen, s.col_gen};
+    if (h->admit_table_key != key) {
+      std::vector<int32_t> base(W + 1, 0), pst;
+      std::vector<kueue_tas_fits_term> terms;
+      for (size_t g = 0; g < W; g++) {
+        for (auto& ps : h->compiled[g].podsets) {
+          pst.push_back(int32_t(terms.size()));
+          pst.push_back(int32_t(ps.requestIds.size()));
+          for (auto& rq : ps.requestIds) terms.push_back({rq.second, s.col_of(rq.first), 0});
+        }
+        base[g + 1] = int32_t(pst.size() / 2);
+      }
+      rc = kueue_tas_admit_table(s.ctx, base.data(), int32_t(W), pst.data(), terms.data(), terms.size());
+      if (rc) {
+        h->err = std::string("admit: ") + kueue_tas_last_error(s.ctx);
+        return rc;
+      }
+      h->admit_table_key = key;
+    }
+    const auto pods = s.colByName.find("pods");
+    const int32_t pods_col = pods == s.colByName.end() ? -1 : pods->second;
+    std::vector<int32_t>& ids = h->admit_ids;
+    std::vector<int32_t>& adm = h->admit_adm;
+    ids.resize(std::max<size_t>(W, 1));
+    adm.resize(std::max<size_t>(W, 1));
+    const kueue_tas_delta* dl = nullptr;
+    size_t nw = 0, nd = 0;
+    const double t1 = now_ms();
+    rc = kueue_tas_admit_block(s.ctx, block, row_words, lens, world, pods_col, ids.data(), adm.data(), W, &nw, &dl, &nd);
+    if (rc == KUEUE_TAS_ELAYOUT) {  // not the assignments layout: the quads through the host path
+      std::vector<int32_t> quads;
+      for (int32_t r = 0; r < world; r++) {
+        const size_t at = quads.size();
+        quads.resize(at + size_t(lens[r]));
+        if (lens[r] && kueue_tas_copy_to_host(s.ctx, quads.data() + at, block + size_t(r) * row_words + 1,
+                                              size_t(lens[r]) * 4))
+          throw std::runtime_error("admit: block copy");
+      }
+      return kueue_tas_host_admit(h, quads.data(), quads.size(), admitted, admitted_cap, n_workloads, n_deltas);
+    }
+    if (rc && rc != KUEUE_TAS_EOVERFLOW) {
+      h->err = std::string("admit: ") + kueue_tas_last_error(s.ctx);
+      return rc;
+    }
+    *n_workloads = nw;
+    if (rc == KUEUE_TAS_EOVERFLOW || !admitted || admitted_cap < 2 * nw) return KUEUE_TAS_EOVERFLOW;
+    const double t2 = now_ms();
+    for (size_t k = 0; k < nw; k++) {
+      admitted[2 * k] = ids[k];
+      admitted[2 * k + 1] = adm[k];
+    }
+    h->last_deltas.assign(dl, dl + nd);
+    if (n_deltas) *n_deltas = nd;
     s.device_applied();
     h->admit_ms[0] = t1 - t0;
     h->admit_ms[1] = t2 - t1;

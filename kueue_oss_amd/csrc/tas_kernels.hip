@@ -6625,4 +6625,225 @@ __global__ __launch_bounds__(1024) void admit_compact_kernel(int32_t* todo, int6
   }
 }
 
+
+// ---- admission from the gathered device block (kueue_tas_admit_block) ----
+// The all-gather leaves every rank's assignments in one device block, row r
+// = [words, quads...] (kueue_tas_host_last_assignments' layout: a header
+// (id, -1, failed, n) before each workload's n domain quads (id, podset,
+// leaf, count)).  Rank 0 admits from it without a host round trip: the
+// headers locate each workload's run, one workgroup orders the present
+// workloads by id (processEntry's order, scheduler.go:337-339) and offsets
+// their records, and the records take their PodSet's single-pod request
+// terms from the compiled workloads' per-PodSet table (ComputeTASNetUsage,
+// flavorassigner.go:94-130).  Error bits (AdmitBlockErr) send the host to
+// its own path (a layout it does not assume) or report the record errors
+// its own path reports.
+constexpr int kAdmitMaxRows = 16;
+struct AdmitRows {
+  int64_t row_words;
+  int32_t world;
+  int32_t nq[kAdmitMaxRows];  // quads per row
+};
+enum AdmitBlockErr { ABE_ID = 1, ABE_RANGE = 2, ABE_DUP = 4, ABE_LAYOUT = 8, ABE_COL = 16 };
+
+// One thread per quad slot of every row: a header records its workload's
+// run (the row position of its first domain quad, the quad count, failed).
+__global__ __launch_bounds__(256) void admit_block_headers_kernel(const int32_t* block, AdmitRows rows, int W,
+                                                                  int32_t* wl_flag, int64_t* wl_pos, int32_t* wl_nd,
+                                                                  int32_t* err) {
+  const int r = int(blockIdx.y);
+  const int q = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= rows.world || q >= rows.nq[r]) return;
+  const int32_t* p = block + int64_t(r) * rows.row_words + 1 + 4 * int64_t(q);
+  if (p[1] >= 0) return;
+  const int32_t g = p[0];
+  if (g < 0 || g >= W) {
+    atomicOr(err, ABE_ID);
+    return;
+  }
+  if (atomicAdd(wl_flag + g, p[2] != 0 ? 2 : 1) != 0) atomicOr(err, ABE_DUP);  // one header per workload
+  wl_pos[g] = int64_t(r) * rows.row_words + 1 + 4 * (int64_t(q) + 1);
+  wl_nd[g] = p[3];
+  if (p[3] < 0 || q + 1 + p[3] > rows.nq[r]) atomicOr(err, ABE_LAYOUT);
+}
+
+// One workgroup: the present workloads in id order (ids, fit0 = 1) and their
+// record offsets (a failed evaluation: one record that cannot fit).
+// hdr[0] = workloads, hdr[1] = records.
+__global__ __launch_bounds__(1024) void admit_block_offsets_kernel(int W, const int32_t* wl_flag, const int32_t* wl_nd,
+                                                                   int32_t* ids, int64_t* wl_off, int32_t* fit0,
+                                                                   int32_t* hdr) {
+  __shared__ int32_t sh_c[16], sh_r[16];
+  const int lane = lane_id(), wave = int(threadIdx.x) >> 6, nw = int(blockDim.x) >> 6;
+  int32_t base_w = 0;
+  int64_t base_r = 0;
+  for (int c0 = 0; c0 < W; c0 += int(blockDim.x)) {  // block-uniform
+    const int g = c0 + int(threadIdx.x);
+    const int32_t f = g < W ? wl_flag[g] : 0;
+    const int32_t present = f != 0 ? 1 : 0;
+    const int32_t nrec = f == 0 ? 0 : f >= 2 ? 1 : max(wl_nd[g], 0);
+    int tc, tr;
+    const int ec = wave_excl_scan(present, &tc), er = wave_excl_scan(nrec, &tr);
+    if (lane == 0) {
+      sh_c[wave] = tc;
+      sh_r[wave] = tr;
+    }
+    __syncthreads();
+    int32_t oc = base_w, tot_c = 0;
+    int64_t orr = base_r, tot_r = 0;
+    for (int k = 0; k < nw; k++) {
+      if (k < wave) {
+        oc += sh_c[k];
+        orr += sh_r[k];
+      }
+      tot_c += sh_c[k];
+      tot_r += sh_r[k];
+    }
+    if (present) {
+      const int j = oc + ec;
+      ids[j] = g;
+      wl_off[j] = orr + er;
+      fit0[j] = 1;
+    }
+    base_w += tot_c;
+    base_r += tot_r;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    wl_off[base_w] = base_r;
+    hdr[0] = base_w;
+    hdr[1] = int32_t(base_r);
+  }
+}
+
+// One wave per present workload: its records (leaf, count, its PodSet's
+// terms in the compiled table), record -> workload, and per column the
+// 128-bit total of count x value this call can add (kueue_tas_admit's
+// monotone shortcut precondition; tot[2 col] low, tot[2 col + 1] high words).
+// ex[0] = 1 when a count or a value is negative (no shortcut).
+__global__ __launch_bounds__(256) void admit_block_records_kernel(
+    const int32_t* block, int N, int W, const int32_t* ids, const int64_t* wl_off, const int32_t* wl_flag,
+    const int64_t* wl_pos, const int32_t* wl_nd, const int32_t* ps_base, const int32_t* ps_terms,
+    const kueue_tas_fits_term* terms, int n_wl, int pods_col, kueue_tas_fits_req* reqs, int32_t* rec_wl,
+    unsigned long long* tot, int32_t* ex, int32_t* err) {
+  const int k = int(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int lane = lane_id();
+  if (k >= n_wl) return;
+  const int32_t g = ids[k];
+  const int64_t base = wl_off[k];
+  if (wl_flag[g] >= 2) {  // a failed evaluation is never admitted
+    if (lane == 0) {
+      reqs[base] = kueue_tas_fits_req{-1, 0, 0, 0};
+      rec_wl[base] = k;
+    }
+    return;
+  }
+  const int32_t nd = wl_nd[g];
+  const int64_t pos = wl_pos[g];
+  const int32_t ps0 = ps_base[g], nps = ps_base[g + 1] - ps0;
+  int32_t bad = 0, neg = 0;
+  for (int j = lane; j < nd; j += kWave) {
+    const int32_t* p = block + pos + 4 * int64_t(j);
+    const int32_t pg = p[0], ps = p[1], leaf = p[2], count = p[3];
+    if (pg != g || ps < 0) {
+      bad |= ABE_LAYOUT;
+      continue;
+    }
+    if (ps >= nps || leaf < 0 || leaf >= N) {
+      bad |= ABE_RANGE;
+      continue;
+    }
+    const int32_t tb = ps_terms[2 * (ps0 + ps)], nt = ps_terms[2 * (ps0 + ps) + 1];
+    reqs[base + j] = kueue_tas_fits_req{leaf, count, tb, nt};
+    rec_wl[base + j] = k;
+    if (count < 0) neg = 1;
+    for (int t = 0; t < nt; t++) {
+      const kueue_tas_fits_term tm = terms[tb + t];
+      if (tm.col < 0) {
+        bad |= ABE_COL;
+        continue;
+      }
+      if (tm.value < 0) neg = 1;
+      if (tm.value <= 0 || count <= 0) continue;
+      const uint64_t a = uint64_t(tm.value), c = uint64_t(count);
+      const uint64_t lo = a * c, hi = __umul64hi(a, c);
+      const unsigned long long old = atomicAdd(tot + 2 * tm.col, (unsigned long long)lo);
+      const uint64_t carry = (old + lo < old) ? 1u : 0u;
+      if (hi + carry) atomicAdd(tot + 2 * tm.col + 1, (unsigned long long)(hi + carry));
+    }
+    if (pods_col >= 0 && count > 0) {
+      const unsigned long long old = atomicAdd(tot + 2 * pods_col, (unsigned long long)count);
+      if (old + uint64_t(count) < old) atomicAdd(tot + 2 * pods_col + 1, 1ull);
+    }
+  }
+  if (bad) atomicOr(err, bad);
+  if (neg) atomicOr(ex, 1);
+}
+
+// The admitted workloads' deltas (updateTASUsage per record: its terms, then
+// pods), in record order — the host path's list, element for element.
+// Pass 1: per block of records its delta count; pass 2 (one workgroup): the
+// blocks' offsets; pass 3: each block writes its deltas.
+__device__ __forceinline__ int admit_delta_count(const kueue_tas_fits_req* reqs, const int32_t* rec_wl,
+                                                 const int32_t* admitted, int n, int pods_col, int i) {
+  if (i >= n) return 0;
+  const kueue_tas_fits_req r = reqs[i];
+  if (!admitted[rec_wl[i]] || r.leaf < 0) return 0;
+  return r.num_terms + (pods_col >= 0 ? 1 : 0);
+}
+__global__ __launch_bounds__(256) void admit_delta_blocks_kernel(const kueue_tas_fits_req* reqs, const int32_t* rec_wl,
+                                                                 const int32_t* admitted, int n, int pods_col,
+                                                                 int32_t* blk) {
+  __shared__ int32_t sh[4];
+  const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+  int tot;
+  (void)wave_excl_scan(admit_delta_count(reqs, rec_wl, admitted, n, pods_col, i), &tot);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) blk[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+__global__ __launch_bounds__(1024) void admit_delta_offsets_kernel(int32_t* blk, int nblk, int32_t* hdr) {
+  __shared__ int32_t sh[16];
+  const int lane = lane_id(), wave = int(threadIdx.x) >> 6, nw = int(blockDim.x) >> 6;
+  int32_t base = 0;
+  for (int c0 = 0; c0 < nblk; c0 += int(blockDim.x)) {
+    const int b = c0 + int(threadIdx.x);
+    const int32_t v = b < nblk ? blk[b] : 0;
+    int t;
+    const int e = wave_excl_scan(v, &t);
+    if (lane == 0) sh[wave] = t;
+    __syncthreads();
+    int32_t o = base, tot = 0;
+    for (int k = 0; k < nw; k++) {
+      if (k < wave) o += sh[k];
+      tot += sh[k];
+    }
+    if (b < nblk) blk[b] = o + e;
+    base += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) hdr[2] = base;
+}
+__global__ __launch_bounds__(256) void admit_delta_write_kernel(const kueue_tas_fits_req* reqs,
+                                                                const kueue_tas_fits_term* terms,
+                                                                const int32_t* rec_wl, const int32_t* admitted, int n,
+                                                                int pods_col, const int32_t* blk, kueue_tas_delta* out) {
+  __shared__ int32_t sh[4];
+  const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+  const int c = admit_delta_count(reqs, rec_wl, admitted, n, pods_col, i);
+  int tot;
+  const int e = wave_excl_scan(c, &tot);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  int o = blk[blockIdx.x] + e;
+  for (int k = 0; k < int(threadIdx.x >> 6); k++) o += sh[k];
+  if (!c) return;
+  const kueue_tas_fits_req r = reqs[i];
+  for (int q = 0; q < r.num_terms; q++) {
+    const kueue_tas_fits_term t = terms[r.term_begin + q];
+    out[o++] = kueue_tas_delta{r.leaf, t.col, int64_t(uint64_t(t.value) * uint64_t(int64_t(r.count)))};
+  }
+  if (pods_col >= 0) out[o] = kueue_tas_delta{r.leaf, pods_col, int64_t(r.count)};
+}
+
 }  // namespace ktas

@@ -69,7 +69,8 @@ EXPORTED_SYMBOLS = [
     "kueue_tas_last_alias_fills", "kueue_tas_host_last_stats_ext", "kueue_tas_last_fill_profile",
     "kueue_tas_snapshot_usage_mark", "kueue_tas_snapshot_usage_changes", "kueue_tas_snapshot_apply_deltas_mirrored",
     "kueue_tas_host_partial_admission_search", "kueue_tas_last_host_trace", "kueue_tas_merge_reruns",
-    "kueue_tas_select_groups",
+    "kueue_tas_select_groups", "kueue_tas_admit_table", "kueue_tas_admit_block", "kueue_tas_copy_to_host",
+    "kueue_tas_host_admit_block",
 ]
 
 # the Makefile's SRC_HASH inputs, in order
@@ -184,6 +185,9 @@ def _bind(lib):
     lib.kueue_tas_host_admit.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t,
                                          c.POINTER(c.c_size_t), c.POINTER(c.c_size_t)]
     lib.kueue_tas_host_last_deltas.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.kueue_tas_host_admit_block.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_int32, c.c_void_p,
+                                               c.c_size_t, c.POINTER(c.c_size_t), c.POINTER(c.c_size_t)]
+    lib.kueue_tas_host_admit_block.restype = c.c_int
     lib.kueue_tas_host_last_deltas.restype = c.c_int
     lib.kueue_tas_host_admit.restype = c.c_int
     lib.kueue_tas_host_apply_deltas.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
@@ -385,6 +389,7 @@ class TASFlavorSnapshot:
         rc = self._lib.kueue_tas_host_compile(self._h, json.dumps({"workloads": workloads}).encode())
         if rc != 0:
             raise RuntimeError(f"kueue_tas_host_compile failed ({rc}): {self._err()}")
+        self._n_compiled = len(workloads)
 
     def last_timings(self):
         """(fill_ms, rollup_ms, select_ms, total_ms), (batches, evals, leader_evals) of the last run."""
@@ -535,6 +540,37 @@ class TASFlavorSnapshot:
             adm = np.zeros((nw.value, 2), dtype=np.int32)
             rc = self._lib.kueue_tas_host_admit(self._h, q.ctypes.data, q.size, adm.ctypes.data, adm.size,
                                                 ctypes.byref(nw), ctypes.byref(nd))
+        if rc:
+            raise RuntimeError(self._err())
+        deltas = np.zeros(nd.value, dtype=DELTA_DTYPE)
+        if self._lib.kueue_tas_host_last_deltas(self._h, deltas.ctypes.data, deltas.size):
+            raise RuntimeError(self._err())
+        return adm[: nw.value], deltas
+
+    def admit_block(self, block, lens, row_words=None):
+        """admit() from the all-gather's receive block on the device
+        (kueue_tas_host_admit_block): ``block`` a [world, row_words] int32
+        tensor (rows [len, quads...]) or a raw device pointer with
+        ``row_words``, ``lens`` the rows' lengths.  Same return value."""
+        import numpy as np
+        if hasattr(block, "data_ptr"):
+            ptr, row_words = block.data_ptr(), int(block.shape[1])
+        elif hasattr(block, "ctypes"):  # a host array (the CPU emulator's device memory)
+            ptr, row_words = block.ctypes.data, int(block.shape[1])
+        else:
+            ptr = int(block)
+        ln = np.ascontiguousarray(lens, dtype=np.int64)
+        cap = max(getattr(self, "_n_compiled", 0), 1)  # at most every compiled workload
+        while True:
+            adm = np.zeros((cap, 2), dtype=np.int32)
+            nw = ctypes.c_size_t()
+            nd = ctypes.c_size_t()
+            rc = self._lib.kueue_tas_host_admit_block(self._h, ptr, row_words, ln.ctypes.data, ln.size,
+                                                      adm.ctypes.data, adm.size, ctypes.byref(nw), ctypes.byref(nd))
+            if rc == -5 and nw.value > cap:
+                cap = nw.value
+                continue
+            break
         if rc:
             raise RuntimeError(self._err())
         deltas = np.zeros(nd.value, dtype=DELTA_DTYPE)

@@ -163,13 +163,20 @@ def admit_round(snap, world: int, rank: int, dist, device=None, src: int = 0):
     """One nominate/admit round after every rank's run_compiled: all-gather the
     assignments, rank ``src`` admits in workload order (Fits + AddUsage on its
     replica) and broadcasts the applied deltas, the other replicas apply them.
-    Returns (gathered quads, admitted (id, 0/1) pairs or None off-src, deltas)."""
-    quads = gather_assignments(snap.last_assignments(), world, dist, device)
+    Returns (gathered quads, admitted (id, 0/1) pairs or None off-src, deltas).
+    Over RCCL the gathered block stays on the device: rank ``src`` admits
+    from it (kueue_tas_host_admit_block: records and deltas built on the
+    device, no host round trip of the quads) and the quads returned are None."""
+    quads = block = lens = None
+    if device is not None and str(device).startswith("cuda"):
+        block, lens = gather_assignments(snap.last_assignments(), world, dist, device, to_host=False)
+    else:
+        quads = gather_assignments(snap.last_assignments(), world, dist, device)
     admitted = None
     deltas = None
     if rank == src:
         try:
-            admitted, deltas = snap.admit(quads)
+            admitted, deltas = snap.admit(quads) if block is None else snap.admit_block(block, lens)
         except Exception:
             # a failed admission must not leave the other ranks waiting in the
             # broadcast: send the failure count (-1) so every rank raises

@@ -1,0 +1,147 @@
+"""Admission from the all-gather's device block (kueue_tas_host_admit_block ->
+kueue_tas_admit_block): the records built on the device from the gathered
+quads and the compiled workloads' per-PodSet request table, the deltas
+written on the device.  Everything must equal the host path
+(kueue_tas_host_admit over the same quads: verdicts, and the delta list
+element for element), which tests/test_admission.py pins to the oracle's
+admission session (Scheduler.processEntry, scheduler.go:371-435: Fits
+tas_flavor_snapshot.go:401-415, then AddUsage :257-265).  A block outside
+the assignments layout (shuffled quads) falls back to the host path."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from kueue_oss_amd import TASFlavorSnapshot, synth
+
+
+def _block(quads, world, rng=None, cap_extra=3):
+    """Rows as gather_assignments leaves them: each rank a contiguous run of
+    whole workloads, [len, quads..., padding]."""
+    q = np.asarray(quads, dtype=np.int32).reshape(-1)
+    heads = [i for i in range(0, q.size, 4) if q[i + 1] < 0]
+    cuts = sorted((rng or random.Random(0)).sample(heads, min(world - 1, len(heads)))) if heads else []
+    bounds = [0] + cuts + [q.size]
+    rows = [q[bounds[k]:bounds[k + 1]] for k in range(len(bounds) - 1)]
+    while len(rows) < world:
+        rows.append(q[:0])
+    cap = max(r.size for r in rows) + 1 + cap_extra
+    blk = np.zeros((world, cap), dtype=np.int32)
+    for r, row in enumerate(rows):
+        blk[r, 0] = row.size
+        blk[r, 1:1 + row.size] = row
+    return blk, [r.size for r in rows]
+
+
+def _pair(make, doc, wls, world, seed, shuffle=False, shard=None):
+    out = []
+    for mode in ("host", "block"):
+        snap = make(doc)
+        snap.compile(wls)
+        if shard is not None:
+            snap.set_shard(shard)
+        snap.run_compiled()
+        q = snap.last_assignments().reshape(-1)
+        if mode == "host":
+            adm, d = snap.admit(q)
+        else:
+            if shuffle:  # quads out of the assignments layout
+                quad = q.reshape(-1, 4)
+                perm = list(range(len(quad)))
+                random.Random(seed).shuffle(perm)
+                q = quad[perm].reshape(-1)
+            blk, lens = _block(q, world, random.Random(seed))
+            adm, d = snap.admit_block(blk, lens)
+        after = snap.find_topology_assignments_for_workloads(wls[:16])
+        out.append((adm.copy(), d.copy(), after))
+        snap.close()
+    (a0, d0, f0), (a1, d1, f1) = out
+    assert (a0 == a1).all()
+    if shuffle:  # the host path keeps each workload's quad order: the same deltas, reordered
+        d0, d1 = np.sort(d0, order=["leaf", "col", "delta"]), np.sort(d1, order=["leaf", "col", "delta"])
+    assert len(d0) == len(d1) and (d0 == d1).all()
+    assert f0 == f1
+    return a0, d0
+
+
+def _check(make, n_cfg=4, big=False):
+    rng = random.Random(5)
+    for k in range(n_cfg):
+        doc, wls = synth.config_c2(seed=100 + k, n_workloads=384 if big else 128,
+                                   shape=(2, 4, 8, 16) if big else (2, 2, 4, 16))
+        world = rng.choice([1, 2, 3, 8])
+        adm, d = _pair(make, doc, wls, world, seed=k)
+        assert adm[:, 1].any() and not adm[:, 1].all()
+    # a shard (ids not from 0), huge capacities (the exact pass), shuffled quads (host fallback)
+    doc, wls = synth.config_c2(seed=7, n_workloads=128, shape=(2, 2, 4, 16))
+    _pair(make, doc, wls, 2, seed=1, shard=list(range(40, 128)))
+    huge = {**doc, "nodes": [dict(nd, allocatable={**nd["allocatable"], "memory": 1 << 62}) for nd in doc["nodes"]]}
+    _pair(make, huge, wls, 2, seed=2)
+    _pair(make, doc, wls, 2, seed=3, shuffle=True)
+
+
+def _oracle(make):
+    """The block path against the oracle session directly."""
+    doc, wls = synth.config_c2(seed=9, n_workloads=96, shape=(2, 2, 4, 8))
+    snap = make(doc)
+    snap.compile(wls)
+    snap.run_compiled()
+    b1 = snap.last_results()
+    blk, lens = _block(snap.last_assignments(), 2)
+    admitted, _ = snap.admit_block(blk, lens)
+    snap.close()
+    n = len(wls)
+    ops = [{"op": "find", "podSets": w} for w in wls]
+    admit_idx = [i for i, w in enumerate(wls) if all(not r["reason"] for r in b1[i])]
+    ops += [{"op": "admit", "usage": synth.usage_records(wls[i], b1[i])} for i in admit_idx]
+    res = oracle_lib.session(doc, ops)
+    assert b1 == res[:n]
+    want = dict(zip(admit_idx, res[n:n + len(admit_idx)]))
+    got = {int(i): bool(a) for i, a in admitted.tolist()}
+    assert {i: got[i] for i in want} == want
+    assert all(not got[i] for i in range(n) if i not in want)
+
+
+def test_emulated_admit_block(emu_lib):  # noqa: F811
+    _check(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+    _oracle(lambda d: TASFlavorSnapshot(d, lib=emu_lib))
+
+
+def test_emulated_admit_block_serial(emu_lib):  # noqa: F811
+    _check(lambda d: TASFlavorSnapshot(d, lib=emu_lib, serial_admit=True), n_cfg=2)
+
+
+def _device(blk):
+    import torch
+
+    return torch.from_numpy(blk).to("cuda:0")
+
+
+@pytest.mark.gpu
+def test_admit_block_on_gpu():
+    import torch
+
+    rng = random.Random(6)
+    for k in range(4):
+        doc, wls = synth.config_c3(seed=20 + k, n_workloads=1024, shape=(2, 8, 32, 32))
+        world = rng.choice([1, 2, 8])
+        out = []
+        for mode in ("host", "block"):
+            snap = TASFlavorSnapshot(doc)
+            snap.compile(wls)
+            snap.run_compiled()
+            q = snap.last_assignments()
+            if mode == "host":
+                adm, d = snap.admit(q)
+            else:
+                blk, lens = _block(q, world, random.Random(k))
+                t = _device(blk)
+                adm, d = snap.admit_block(t, lens)
+                torch.cuda.synchronize()
+            out.append((adm.copy(), d.copy()))
+            snap.close()
+        assert (out[0][0] == out[1][0]).all()
+        assert (out[0][1] == out[1][1]).all()
+        assert 0 < int(out[0][0][:, 1].sum()) < len(wls)
+    _oracle(lambda d: TASFlavorSnapshot(d))
