@@ -6726,58 +6726,72 @@ __global__ __launch_bounds__(256) void admit_block_records_kernel(
     const int64_t* wl_pos, const int32_t* wl_nd, const int32_t* ps_base, const int32_t* ps_terms,
     const kueue_tas_fits_term* terms, int n_wl, int pods_col, kueue_tas_fits_req* reqs, int32_t* rec_wl,
     unsigned long long* tot, int32_t* ex, int32_t* err) {
+  // the block's per-column totals in LDS first (one global atomic per column
+  // and block: device-scope atomics on a handful of addresses from every
+  // record serialize at the memory side)
+  __shared__ unsigned long long sh_tot[2 * KUEUE_TAS_MAX_COLS];
+  for (int q = threadIdx.x; q < 2 * KUEUE_TAS_MAX_COLS; q += blockDim.x) sh_tot[q] = 0;
+  __syncthreads();
   const int k = int(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int lane = lane_id();
-  if (k >= n_wl) return;
-  const int32_t g = ids[k];
-  const int64_t base = wl_off[k];
-  if (wl_flag[g] >= 2) {  // a failed evaluation is never admitted
-    if (lane == 0) {
-      reqs[base] = kueue_tas_fits_req{-1, 0, 0, 0};
-      rec_wl[base] = k;
-    }
-    return;
-  }
-  const int32_t nd = wl_nd[g];
-  const int64_t pos = wl_pos[g];
-  const int32_t ps0 = ps_base[g], nps = ps_base[g + 1] - ps0;
   int32_t bad = 0, neg = 0;
-  for (int j = lane; j < nd; j += kWave) {
-    const int32_t* p = block + pos + 4 * int64_t(j);
-    const int32_t pg = p[0], ps = p[1], leaf = p[2], count = p[3];
-    if (pg != g || ps < 0) {
-      bad |= ABE_LAYOUT;
-      continue;
-    }
-    if (ps >= nps || leaf < 0 || leaf >= N) {
-      bad |= ABE_RANGE;
-      continue;
-    }
-    const int32_t tb = ps_terms[2 * (ps0 + ps)], nt = ps_terms[2 * (ps0 + ps) + 1];
-    reqs[base + j] = kueue_tas_fits_req{leaf, count, tb, nt};
-    rec_wl[base + j] = k;
-    if (count < 0) neg = 1;
-    for (int t = 0; t < nt; t++) {
-      const kueue_tas_fits_term tm = terms[tb + t];
-      if (tm.col < 0) {
-        bad |= ABE_COL;
-        continue;
+  auto add128 = [&](int col, uint64_t lo, uint64_t hi) {
+    const unsigned long long old = atomicAdd(sh_tot + 2 * col, (unsigned long long)lo);
+    const uint64_t carry = (old + lo < old) ? 1u : 0u;
+    if (hi + carry) atomicAdd(sh_tot + 2 * col + 1, (unsigned long long)(hi + carry));
+  };
+  if (k < n_wl) {
+    const int32_t g = ids[k];
+    const int64_t base = wl_off[k];
+    if (wl_flag[g] >= 2) {  // a failed evaluation is never admitted
+      if (lane == 0) {
+        reqs[base] = kueue_tas_fits_req{-1, 0, 0, 0};
+        rec_wl[base] = k;
       }
-      if (tm.value < 0) neg = 1;
-      if (tm.value <= 0 || count <= 0) continue;
-      const uint64_t a = uint64_t(tm.value), c = uint64_t(count);
-      const uint64_t lo = a * c, hi = __umul64hi(a, c);
-      const unsigned long long old = atomicAdd(tot + 2 * tm.col, (unsigned long long)lo);
-      const uint64_t carry = (old + lo < old) ? 1u : 0u;
-      if (hi + carry) atomicAdd(tot + 2 * tm.col + 1, (unsigned long long)(hi + carry));
-    }
-    if (pods_col >= 0 && count > 0) {
-      const unsigned long long old = atomicAdd(tot + 2 * pods_col, (unsigned long long)count);
-      if (old + uint64_t(count) < old) atomicAdd(tot + 2 * pods_col + 1, 1ull);
+    } else {
+      const int32_t nd = wl_nd[g];
+      const int64_t pos = wl_pos[g];
+      const int32_t ps0 = ps_base[g], nps = ps_base[g + 1] - ps0;
+      for (int j = lane; j < nd; j += kWave) {
+        const int32_t* p = block + pos + 4 * int64_t(j);
+        const int32_t pg = p[0], ps = p[1], leaf = p[2], count = p[3];
+        if (pg != g || ps < 0) {
+          bad |= ABE_LAYOUT;
+          continue;
+        }
+        if (ps >= nps || leaf < 0 || leaf >= N) {
+          bad |= ABE_RANGE;
+          continue;
+        }
+        const int32_t tb = ps_terms[2 * (ps0 + ps)], nt = ps_terms[2 * (ps0 + ps) + 1];
+        reqs[base + j] = kueue_tas_fits_req{leaf, count, tb, nt};
+        rec_wl[base + j] = k;
+        if (count < 0) neg = 1;
+        for (int t = 0; t < nt; t++) {
+          const kueue_tas_fits_term tm = terms[tb + t];
+          if (tm.col < 0 || tm.col >= KUEUE_TAS_MAX_COLS) {
+            bad |= ABE_COL;
+            continue;
+          }
+          if (tm.value < 0) neg = 1;
+          if (tm.value <= 0 || count <= 0) continue;
+          const uint64_t a = uint64_t(tm.value), c = uint64_t(count);
+          add128(tm.col, a * c, __umul64hi(a, c));
+        }
+        if (pods_col >= 0 && count > 0) add128(pods_col, uint64_t(count), 0);
+      }
     }
   }
   if (bad) atomicOr(err, bad);
   if (neg) atomicOr(ex, 1);
+  __syncthreads();
+  for (int col = threadIdx.x; col < KUEUE_TAS_MAX_COLS; col += blockDim.x) {
+    const uint64_t lo = sh_tot[2 * col], hi = sh_tot[2 * col + 1];
+    if (!lo && !hi) continue;
+    const unsigned long long old = atomicAdd(tot + 2 * col, (unsigned long long)lo);
+    const uint64_t carry = (old + lo < old) ? 1u : 0u;
+    if (hi + carry) atomicAdd(tot + 2 * col + 1, (unsigned long long)(hi + carry));
+  }
 }
 
 // The admitted workloads' deltas (updateTASUsage per record: its terms, then

@@ -137,6 +137,7 @@ def test_admit_block_on_gpu():
             else:
                 blk, lens = _block(q, world, random.Random(k))
                 t = _device(blk)
+                torch.cuda.synchronize()  # the block complete before the library's stream reads it
                 adm, d = snap.admit_block(t, lens)
                 torch.cuda.synchronize()
             out.append((adm.copy(), d.copy()))
