@@ -56,6 +56,7 @@ extern "C" {
 #define KUEUE_TAS_ENOSNAPSHOT -4
 #define KUEUE_TAS_EOVERFLOW -5
 #define KUEUE_TAS_ELAYOUT -6    /* kueue_tas_admit_block: the block is not in the assignments layout */
+#define KUEUE_TAS_EHOSTMEM -7   /* kueue_tas_admit_block: the block is not device memory */
 
 typedef struct kueue_tas_ctx kueue_tas_ctx;
 
@@ -413,7 +414,8 @@ int kueue_tas_admit(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n
  * verdicts (cap: KUEUE_TAS_EOVERFLOW when short, nothing admitted), and the
  * applied delta list in kueue_tas_host_admit's order (*deltas valid until the
  * next call).  KUEUE_TAS_ELAYOUT (nothing admitted) when the block is not in
- * that layout: the caller admits through the host path. */
+ * that layout, KUEUE_TAS_EHOSTMEM when it is not device memory: the caller
+ * admits through the host path. */
 /* bytes from device memory of ctx's device to host memory (synchronous) */
 int kueue_tas_copy_to_host(kueue_tas_ctx* ctx, void* dst, const void* src, size_t bytes);
 int kueue_tas_admit_table(kueue_tas_ctx* ctx, const int32_t* ps_base, int32_t num_workloads, const int32_t* ps_terms,
@@ -528,7 +530,8 @@ int kueue_tas_host_apply_deltas(kueue_tas_host* h, const kueue_tas_delta* deltas
 /* admit from the all-gather's device block (kueue_tas_admit_block; block and
  * lens as gather_assignments leaves them): the same verdicts, admitted pairs
  * and delta list as kueue_tas_host_admit over the block's quads; a block
- * outside the assignments layout is copied to the host and admitted there. */
+ * outside the assignments layout is copied to the host and admitted there,
+ * one in host memory admitted there as it is. */
 int kueue_tas_host_admit_block(kueue_tas_host* h, const int32_t* block, size_t row_words, const int64_t* lens,
                                int32_t world, int32_t* admitted, size_t admitted_cap, size_t* n_workloads,
                                size_t* n_deltas);

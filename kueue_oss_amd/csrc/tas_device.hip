@@ -1474,6 +1474,13 @@ int kueue_tas_admit_block(kueue_tas_ctx* c, const int32_t* block, size_t row_wor
   }
   const int W = c->adm_W;
   HIPCHK(c, hipSetDevice(c->device));
+  {  // device memory only: kernels must not read a pageable host array
+    hipPointerAttribute_t pa{};
+    if (hipPointerGetAttributes(&pa, block) != hipSuccess || pa.type != hipMemoryTypeDevice) {
+      (void)hipGetLastError();
+      return fail(c, KUEUE_TAS_EHOSTMEM, "admit block: not device memory");
+    }
+  }
   // the layout of the host path with the bounds (records <= quads, workloads <= W)
   const AdmitLayout L = admit_layout(std::max<size_t>(Q, 1), 0, size_t(W), size_t(c->snap.N));
   // per id: flag, run position, quad count; hdr: workloads, records, deltas; errors; exact; totals (lo, hi)

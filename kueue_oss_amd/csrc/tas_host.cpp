@@ -5224,14 +5224,17 @@ int kueue_tas_host_admit_block(kueue_tas_host* h, const int32_t* block, size_t r
     size_t nw = 0, nd = 0;
     const double t1 = now_ms();
     rc = kueue_tas_admit_block(s.ctx, block, row_words, lens, world, pods_col, ids.data(), adm.data(), W, &nw, &dl, &nd);
-    if (rc == KUEUE_TAS_ELAYOUT) {  // not the assignments layout: the quads through the host path
+    if (rc == KUEUE_TAS_ELAYOUT || rc == KUEUE_TAS_EHOSTMEM) {  // the quads through the host path
       std::vector<int32_t> quads;
       for (int32_t r = 0; r < world; r++) {
         const size_t at = quads.size();
         quads.resize(at + size_t(lens[r]));
-        if (lens[r] && kueue_tas_copy_to_host(s.ctx, quads.data() + at, block + size_t(r) * row_words + 1,
-                                              size_t(lens[r]) * 4))
+        const int32_t* row = block + size_t(r) * row_words + 1;
+        if (rc == KUEUE_TAS_EHOSTMEM) {
+          if (lens[r]) memcpy(quads.data() + at, row, size_t(lens[r]) * 4);
+        } else if (lens[r] && kueue_tas_copy_to_host(s.ctx, quads.data() + at, row, size_t(lens[r]) * 4)) {
           throw std::runtime_error("admit: block copy");
+        }
       }
       return kueue_tas_host_admit(h, quads.data(), quads.size(), admitted, admitted_cap, n_workloads, n_deltas);
     }

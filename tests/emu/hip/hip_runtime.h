@@ -240,6 +240,17 @@ inline hipError_t hipHostFree(void* p) {
   return hipSuccess;
 }
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
+// every pointer is "device" memory to the emulated kernels (they run on the host)
+enum hipMemoryType { hipMemoryTypeUnregistered = 0, hipMemoryTypeHost = 1, hipMemoryTypeDevice = 2 };
+struct hipPointerAttribute_t {
+  hipMemoryType type;
+  int device;
+};
+inline hipError_t hipPointerGetAttributes(hipPointerAttribute_t* a, const void*) {
+  a->type = hipMemoryTypeDevice;
+  a->device = 0;
+  return hipSuccess;
+}
 inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t st) {
   if (n) st->ops.push_back([=]() { memmove(d, s, n); });
   return hipSuccess;

@@ -81,7 +81,7 @@ def _check(make, n_cfg=4, big=False):
     _pair(make, doc, wls, 2, seed=3, shuffle=True)
 
 
-def _oracle(make):
+def _oracle(make, on_device=lambda blk: blk):
     """The block path against the oracle session directly."""
     doc, wls = synth.config_c2(seed=9, n_workloads=96, shape=(2, 2, 4, 8))
     snap = make(doc)
@@ -89,7 +89,7 @@ def _oracle(make):
     snap.run_compiled()
     b1 = snap.last_results()
     blk, lens = _block(snap.last_assignments(), 2)
-    admitted, _ = snap.admit_block(blk, lens)
+    admitted, _ = snap.admit_block(on_device(blk), lens)
     snap.close()
     n = len(wls)
     ops = [{"op": "find", "podSets": w} for w in wls]
@@ -145,4 +145,14 @@ def test_admit_block_on_gpu():
         assert (out[0][0] == out[1][0]).all()
         assert (out[0][1] == out[1][1]).all()
         assert 0 < int(out[0][0][:, 1].sum()) < len(wls)
+    _oracle(lambda d: TASFlavorSnapshot(d), on_device=_device_synced)
+    # a block in host memory (not the gather's device block): admitted through the host path
     _oracle(lambda d: TASFlavorSnapshot(d))
+
+
+def _device_synced(blk):
+    import torch
+
+    t = _device(blk)
+    torch.cuda.synchronize()
+    return t
