@@ -516,7 +516,8 @@ class FlavorSnapshot {
   std::map<std::string, int32_t> taintIdByString;
   std::vector<std::string> labelKeys;
   std::map<std::string, int32_t> labelCol;
-  std::vector<std::map<std::string, int32_t>> labelDict;
+  std::vector<std::unordered_map<std::string, int32_t>> labelDict;  // value -> id (hashed: the hostname
+                                                                   // column holds a value per leaf)
   std::vector<int32_t> labelValues;  // [K][labStride]: column k at k * labStride (leaves 0..N-1)
   size_t labStride = 0;              // >= N, with headroom: joined leaves shift each column in place
   std::deque<NodeInfo> nodes;  // stable addresses: leafNode points into it, nodes join in place
