@@ -420,6 +420,8 @@ def main():
                "cpu_model": model, "gomaxprocs": "n/a (Go toolchain absent)"}
 
     extras = {}
+    if placed:  # the API rows run where the step ran (the CPU legs had the whole CPU set)
+        os.sched_setaffinity(0, placed)
     if rank == 0 and world == 1 and not a.no_extras:
         extras = widened_rows(a, snap, snap_doc, mine, synth)
         extras["c3j"] = c3j_variant(a, synth, TASFlavorSnapshot, FULL)
