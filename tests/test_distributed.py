@@ -204,6 +204,22 @@ d["col"] = 1
 d["delta"] = -(np.arange(5000, dtype=np.int64) << 33)
 got = sharding.broadcast_deltas(d, dist, 0, "cuda:0")
 assert np.array_equal(got, d)
+# admit_round over RCCL: rank 0 admits from the gathered device block
+# (kueue_tas_host_admit_block); the same verdicts and deltas as the host path
+from kueue_oss_amd import TASFlavorSnapshot, synth
+doc, wls = synth.config_c2(n_workloads=256, shape=(2, 4, 8, 16))
+ref = TASFlavorSnapshot(doc)
+ref.compile(wls)
+ref.run_compiled()
+want_adm, want_d = ref.admit(ref.last_assignments())
+ref.close()
+snap = TASFlavorSnapshot(doc)
+snap.compile(wls)
+snap.run_compiled()
+quads, adm, dl = sharding.admit_round(snap, 1, 0, dist, "cuda:0")
+assert quads is None and np.array_equal(adm, want_adm) and np.array_equal(dl, want_d)
+assert 0 < int(adm[:, 1].sum()) < len(wls)
+snap.close()
 dist.destroy_process_group()
 print("exchange ok")
 """
@@ -212,8 +228,9 @@ print("exchange ok")
 @pytest.mark.gpu
 def test_exchange_buffers_on_rccl():
     """The RCCL side of the exchange (pinned staging, all_gather_into_tensor,
-    device-resident block, capacity growth, delta broadcast) in a one-rank
-    nccl group on the box's GPU (a child process: its own process group)."""
+    device-resident block, capacity growth, delta broadcast, and admit_round
+    admitting from the device block) in a one-rank nccl group on the box's
+    GPU (a child process: its own process group)."""
     import subprocess
     import sys
 
