@@ -230,7 +230,7 @@ struct kueue_tas_ctx {
   DevBuf<int8_t> d_fill_lim;
   std::vector<int32_t> cls_pos, cls_cur;
   hipEvent_t ev[8] = {};  // stage boundaries, see eval_chunk
-  hipEvent_t evl[3] = {};  // fast-LFC branch: start, end (timing), join
+  hipEvent_t evl[4] = {};  // fast-LFC branch: start, end (timing), join, fast select done (emit on the main stream)
   std::string err;
   int list_cap = 1024;
   bool inline_stats = true;   // ExclusionStats counted in the fill (KUEUE_TAS_CFG_SPLIT_STATS: fill_exclusion_kernel)
@@ -389,6 +389,10 @@ struct kueue_tas_ctx {
     return e && atoi(e) != 0;                     // by more than it saves the side stream
   }();
   bool collide_test = false; // KUEUE_TAS_CFG_CLASS_COLLIDE
+  bool emit_after_bf = [] {    // KTAS_EMIT_MAIN=1: lfc_emit on the main stream after the BestFit select
+    const char* e = getenv("KTAS_EMIT_MAIN");
+    return e && atoi(e) != 0;
+  }();
   int32_t exp_flags = [] {     // diagnostics only (tools/probe_select.py experiments)
     const char* e = getenv("KTAS_EXP_FLAGS");
     return e ? int32_t(atoi(e)) : 0;
@@ -2917,6 +2921,8 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
     HIPCHK(c, hipGetLastError());
   }
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+  const bool emit_main = c->emit_after_bf && nbf > 0 && nfast > 0;
+  const int emit_grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
   // K3 (BestFit side and every other non-fast eval)
   if (nbf) {
     b.wave_lds = bf_wave_lds;
@@ -2965,14 +2971,23 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
                        size_t(waves) * size_t(lfc_wave_lds), c->stream2, s, b, d_fast, nfast);
     b.sel_slots = sel;
     HIPCHK(c, hipGetLastError());
-    const int grid = int(std::min<int64_t>(int64_t(nfast) * nchunks, 2048));
-    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(grid)), dim3(256), 0, c->stream2, s, b);
-    HIPCHK(c, hipGetLastError());
+    if (emit_main) {
+      HIPCHK(c, hipEventRecord(c->evl[3], c->stream2));
+    } else {
+      hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(emit_grid)), dim3(256), 0, c->stream2, s, b);
+      HIPCHK(c, hipGetLastError());
+    }
     HIPCHK(c, hipEventRecord(c->evl[1], c->stream2));
     // the branch's result headers come back on its own stream: the host
     // waits for both streams instead of the main stream waiting for this one
     // (a cross-stream hand-off costs ~17 us of device time, sync_cost.hip)
     HIPCHK(c, hipMemcpyAsync(c->h_res2.p, d_out, n * sizeof(kueue_tas_eval_out), hipMemcpyDeviceToHost, c->stream2));
+  }
+  if (nfast && emit_main) {  // the emit after the BestFit select on the main stream (its chunk re-reads
+    // stall the descents beside it); the fast select's items from stream2
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->evl[3], 0));
+    hipLaunchKernelGGL(lfc_emit_kernel, dim3(unsigned(emit_grid)), dim3(256), 0, c->stream, s, b);
+    HIPCHK(c, hipGetLastError());
   }
   trace(15);
   if (stats_branch) HIPCHK(c, hipStreamWaitEvent(c->stream, c->evs[1], 0));  // join the ExclusionStats branch
