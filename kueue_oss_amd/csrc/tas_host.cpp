@@ -1023,7 +1023,6 @@ class FlavorSnapshot {
     } else {
       prof = int32_t(pit - profiles.begin());
     }
-    const size_t N = size_t(this->N());
     for (auto& kv : ni.labels) {
       auto c = labelCol.find(kv.first);
       if (c == labelCol.end()) {  // a new label column, absent on every other leaf
@@ -1055,7 +1054,6 @@ class FlavorSnapshot {
     cur.allocatable = std::move(ni.allocatable);
     leafProfile[size_t(leaf)] = prof;
     if (lowestIsHostname) {
-      const size_t N = size_t(this->N());
       for (size_t k = 0; k < labelKeys.size(); k++) {
         auto it = cur.labels.find(labelKeys[k]);
         labelValues[k * labStride + size_t(leaf)] = it == cur.labels.end() ? 0 : labelDict[k].at(it->second);
@@ -1719,7 +1717,7 @@ class FlavorSnapshot {
       return rc;
     }
     if (!attrs || !lowestIsHostname) return 0;
-    const size_t K = labelKeys.size(), N = size_t(this->N());
+    const size_t K = labelKeys.size();
     std::vector<int32_t> prof(ls.size()), lab(ls.size() * K);
     for (size_t i = 0; i < ls.size(); i++) {
       prof[i] = leafProfile[size_t(ls[i])];
