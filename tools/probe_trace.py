@@ -23,8 +23,6 @@ FULL = TASFlavorSnapshot.RUN_COMPILE | TASFlavorSnapshot.RUN_VALUES
 snap.set_stage_timing(False)
 rows = []
 for i in range(61):
-    if i == 60:  # the last step prints the records / class-merge cycle counters (stderr)
-        os.environ["KTAS_PROF_RECORDS"] = "1"
     t = time.perf_counter()
     snap.run_compiled(flags=FULL)
     wall = (time.perf_counter() - t) * 1e3
