@@ -646,17 +646,38 @@ static int load_impl(kueue_tas_ctx* c, const kueue_tas_snapshot_desc* d, const k
   c->h_dead.assign(N, 0);
   c->n_dead = 0;
   std::vector<int32_t>& gsrc = c->h_gsrc;  // (kept: no fresh pages per splice)
-  if (sp) {
+  if (sp) {  // sources (joined rows numbered in order) and the dead map, in the host pool's static parts
     gsrc.resize(N);
-    int32_t k = 0;
-    for (size_t j = 0; j < N; j++) {
-      const int32_t x = sp->leaf_src[j];
-      gsrc[j] = x >= 0 ? x : -(++k);
-      if (x >= 0 && size_t(x) < old_dead.size() && old_dead[size_t(x)]) {
-        c->h_dead[j] = 1;
-        c->n_dead++;
+    ktas_pool::HostPool& pool = ktas_pool::HostPool::get();
+    const size_t T = pool.parts();
+    std::vector<int32_t> joined(T + 1, 0);
+    std::vector<int64_t> dead(T, 0);
+    auto part_of = [&](size_t b) {
+      size_t t = 0;
+      while (t + 1 < T && ktas_pool::HostPool::part_begin(N, t + 1, T) <= b) t++;
+      return t;
+    };
+    pool.run_static(N, [&](size_t b, size_t e) {  // pass 1: joined rows per part
+      int32_t k = 0;
+      for (size_t j = b; j < e; j++) k += sp->leaf_src[j] < 0 ? 1 : 0;
+      joined[part_of(b) + 1] = k;
+    });
+    for (size_t t = 0; t < T; t++) joined[t + 1] += joined[t];
+    pool.run_static(N, [&](size_t b, size_t e) {  // pass 2: the numbering and the dead leaves
+      const size_t t = part_of(b);
+      int32_t k = joined[t];
+      int64_t nd = 0;
+      for (size_t j = b; j < e; j++) {
+        const int32_t x = sp->leaf_src[j];
+        gsrc[j] = x >= 0 ? x : -(++k);
+        if (x >= 0 && size_t(x) < old_dead.size() && old_dead[size_t(x)]) {
+          c->h_dead[j] = 1;
+          nd++;
+        }
       }
-    }
+      dead[t] = nd;
+    });
+    for (int64_t nd : dead) c->n_dead += nd;
   }
   // the re-derived tables go up through one pinned arena (async copies, one
   // stream synchronization at the end) instead of a synchronous copy each
