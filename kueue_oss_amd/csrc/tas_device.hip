@@ -2775,12 +2775,20 @@ static int eval_chunk(kueue_tas_ctx* c, const kueue_tas_eval_req* const* reqs, s
         if constexpr (TSv && !MRv) {  // single-run chunks: leaf categories
           if (cat) {
             c->fill_paths |= KUEUE_TAS_PATH_CATEGORY;
-            if (ragged_pair)
+            if (b.lfc_fill) {  // (the lean loop's LFC pair lists in LDS)
+              if (ragged_pair)
+                hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, -1, true, true>), pg, dim3(256), 0, st, s, b, umask, first);
+              else if (b.rack_fanout == 32)
+                hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 32, true, true>), pg, dim3(256), 0, st, s, b, umask, first);
+              else
+                hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 0, true, true>), pg, dim3(256), 0, st, s, b, umask, first);
+            } else if (ragged_pair) {
               hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, -1, true>), pg, dim3(256), 0, st, s, b, umask, first);
-            else if (b.rack_fanout == 32)
+            } else if (b.rack_fanout == 32) {
               hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 32, true>), pg, dim3(256), 0, st, s, b, umask, first);
-            else
+            } else {
               hipLaunchKernelGGL((fill_pair_kernel<NSv, true, false, false, 0, true>), pg, dim3(256), 0, st, s, b, umask, first);
+            }
             return;
           }
         }

@@ -1267,7 +1267,10 @@ struct OpOr {
 // staged kernel's MR.
 // CAT: leaf categories (below); single-run chunks only (!MR), every filter on
 // staged data (!GL), taint rows in LDS (TS), ExclusionStats in LDS.
-template <int NS, bool TS, bool MR, bool GL, int FC, bool CAT = false>  // FC: 32 compile-time fan-out, 0: b.rack_fanout
+// FC: 32 compile-time fan-out, 0: b.rack_fanout.  LF: the lean loop may
+// accumulate the fast-LFC tables (DevBatch::lfc_fill); its per-wave pair
+// lists cost 4 KB of LDS, which without LF lets 8 blocks share a CU
+template <int NS, bool TS, bool MR, bool GL, int FC, bool CAT = false, bool LF = false>
                                                       // (or none), -1: ragged parents in 128-leaf slots (DevSnap::wave_tab2)
 // (75-79 VGPRs: 6 waves per SIMD.  Forcing 8 — the whole C3 grid resident —
 // spilled ~20 prologue values: 37.8 -> 36.4 us but 61 -> 113 MB of HBM
@@ -1292,9 +1295,9 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
   // lean blocks with fast-LFC slot classes (DevBatch::lfc_fill): the distinct
   // (dense category, state0 > 0) pairs of each wave's leaves and their counts
   constexpr int kTri = 2 * kWave;  // at most one pair per leaf of the wave
-  __shared__ int32_t sh_tv[CAT ? 4 * kTri : 1];
-  __shared__ int32_t sh_tc[CAT ? 4 * kTri : 1];  // count << 8 | dense category
-  __shared__ int32_t sh_tn[CAT ? 4 : 1];
+  __shared__ int32_t sh_tv[CAT && LF ? 4 * kTri : 1];
+  __shared__ int32_t sh_tc[CAT && LF ? 4 * kTri : 1];  // count << 8 | dense category
+  __shared__ int32_t sh_tn[CAT && LF ? 4 : 1];
   static_assert(2 * NS <= kPosTerms, "a position holds 2 * NS terms");
   const bool lds_stats = b.nstat > 0;
   KTAS_FILL_STAMP(0);
@@ -1656,8 +1659,10 @@ __global__ __launch_bounds__(kFillThreads) void fill_pair_kernel(DevSnap s, DevB
     uint64_t* rpp = b.rack_pos ? b.rack_pos + int64_t(e0) * lsz + parent : nullptr;
     // fast-LFC chunk tables from the fill: the wave's (category, value) pairs
     bool lfc_any = false;
-    if (b.lfc_fill)
-      for (int e = 0; e < ne; e++) lfc_any = lfc_any || sh_pos[e].p.lfc_slot >= 0;
+    if constexpr (LF) {
+      if (b.lfc_fill)
+        for (int e = 0; e < ne; e++) lfc_any = lfc_any || sh_pos[e].p.lfc_slot >= 0;
+    }
     if (lfc_any) {
       const int wv = int(threadIdx.x >> 6);
       const bool a0 = valid[0] && state0[0] > 0, a1 = valid[1] && state0[1] > 0;
