@@ -414,8 +414,8 @@ int kueue_tas_admit(kueue_tas_ctx* ctx, const kueue_tas_fits_req* reqs, size_t n
  * verdicts (cap: KUEUE_TAS_EOVERFLOW when short, nothing admitted), and the
  * applied delta list in kueue_tas_host_admit's order (*deltas valid until the
  * next call).  KUEUE_TAS_ELAYOUT (nothing admitted) when the block is not in
- * that layout, KUEUE_TAS_EHOSTMEM when it is not device memory: the caller
- * admits through the host path. */
+ * that layout or has more than 16 rows, KUEUE_TAS_EHOSTMEM when it is not
+ * device memory: the caller admits through the host path. */
 /* bytes from device memory of ctx's device to host memory (synchronous) */
 int kueue_tas_copy_to_host(kueue_tas_ctx* ctx, void* dst, const void* src, size_t bytes);
 int kueue_tas_admit_table(kueue_tas_ctx* ctx, const int32_t* ps_base, int32_t num_workloads, const int32_t* ps_terms,

@@ -1483,7 +1483,7 @@ int kueue_tas_admit_block(kueue_tas_ctx* c, const int32_t* block, size_t row_wor
   if (!c->loaded) return fail(c, KUEUE_TAS_ENOSNAPSHOT, "no snapshot loaded");
   if (!block || !lens || !ids || !admitted || !n_workloads || !deltas || !n_deltas || world < 1)
     return fail(c, KUEUE_TAS_EINVAL, "null argument");
-  if (world > kAdmitMaxRows) return fail(c, KUEUE_TAS_EINVAL, "admit block: more rows than supported");
+  if (world > kAdmitMaxRows) return fail(c, KUEUE_TAS_ELAYOUT, "admit block: more rows than supported");
   if (c->adm_W < 0) return fail(c, KUEUE_TAS_EINVAL, "admit block: no admission table (kueue_tas_admit_table)");
   if (pods_col < -1 || pods_col >= c->snap.R) return fail(c, KUEUE_TAS_EINVAL, "pods column out of range");
   AdmitRows rows{};

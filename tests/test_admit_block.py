@@ -79,6 +79,7 @@ def _check(make, n_cfg=4, big=False):
     huge = {**doc, "nodes": [dict(nd, allocatable={**nd["allocatable"], "memory": 1 << 62}) for nd in doc["nodes"]]}
     _pair(make, huge, wls, 2, seed=2)
     _pair(make, doc, wls, 2, seed=3, shuffle=True)
+    _pair(make, doc, wls, 20, seed=4)  # more rows than the device path takes: the host path
 
 
 def _oracle(make, on_device=lambda blk: blk):
